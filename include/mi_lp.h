@@ -1,0 +1,237 @@
+/*
+ * mi_lp.h -- C ABI of the MI355X revised-simplex LP engine (drop-in for Glop).
+ *
+ * Plain pointers and sizes only; no C++ or torch types cross this boundary.
+ * Every entry point below replaces one piece of the Glop / MPSolver interface
+ * of OR-Tools 9.7 (paths relative to the reference checkout):
+ *
+ *   mi_lp_create / mi_lp_destroy     glop::RevisedSimplex ctor/dtor
+ *                                    (ortools/glop/revised_simplex.h:125-129)
+ *   mi_lp_set_params                 RevisedSimplex::SetParameters
+ *                                    (revised_simplex.h:132, .cc:3586-3593)
+ *   mi_lp_load                       the LinearProgram handed to Solve()
+ *                                    (revised_simplex.cc:139, lp_data.h:56);
+ *                                    CSC, rows sorted per column, no explicit
+ *                                    zeros (LinearProgram::IsCleanedUp,
+ *                                    lp_solver.cc:185-191)
+ *   mi_lp_load_basis_state           RevisedSimplex::LoadStateForNextSolve
+ *                                    (revised_simplex.h:153, .cc:120-124)
+ *   mi_lp_clear_basis_state          RevisedSimplex::ClearStateForNextSolve (.cc:114)
+ *   mi_lp_notify_matrix_unchanged    NotifyThatMatrixIsUnchangedForNextSolve (.cc:131)
+ *   mi_lp_solve                      RevisedSimplex::Solve (revised_simplex.cc:139-635)
+ *                                    + the ProblemStatus mapping of
+ *                                    LPSolver::RunRevisedSimplexIfNeeded
+ *                                    (lp_solver.cc:591-658)
+ *   mi_lp_get_*                      GetVariableValue / GetReducedCost /
+ *                                    GetDualValue / GetConstraintActivity /
+ *                                    GetVariableStatus / GetConstraintStatus /
+ *                                    GetBasis / GetState / GetPrimalRay /
+ *                                    GetDualRay / GetDualRayRowCombination
+ *                                    (revised_simplex.h:172-239, .cc:637-713)
+ *   mi_lp_begin / mi_lp_run_until /  the PrimalMinimize/DualMinimize loops
+ *   mi_lp_finish                     (revised_simplex.cc:2751-3367) driven in
+ *                                    bounded slices (benchmark harness only)
+ *   mi_lp_batch_solve                CP-SAT's per-worker LP call-out
+ *                                    (sat/linear_programming_constraint.cc:709-760)
+ *                                    for many independent LPs at once
+ *
+ * Error codes mirror glop::Status::ErrorCode (ortools/glop/status.h:29-44).
+ * Threading: one handle = one host thread = one HIP stream (RevisedSimplex is
+ * not thread safe either).
+ */
+#ifndef MI_LP_H_
+#define MI_LP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Opaque solver handle (one glop::RevisedSimplex + its device state). */
+typedef struct mi_lp mi_lp;
+
+/* glop::Status::ErrorCode (status.h:29-44) + ABI-level codes. */
+enum {
+  MI_LP_OK = 0,
+  MI_LP_ERROR_LU = 1,
+  MI_LP_ERROR_BOUND = 2,
+  MI_LP_ERROR_NULL = 3,
+  MI_LP_ERROR_INVALID_PROBLEM = 4,
+  MI_LP_ERROR_DEVICE = 100, /* HIP runtime failure or missing GPU */
+  MI_LP_ERROR_STATE = 101   /* call out of order (e.g. getter before solve) */
+};
+
+/* glop::ProblemStatus (ortools/lp_data/lp_types.h:106-168). */
+enum {
+  MI_LP_OPTIMAL = 0,
+  MI_LP_PRIMAL_INFEASIBLE = 1,
+  MI_LP_DUAL_INFEASIBLE = 2,
+  MI_LP_INFEASIBLE_OR_UNBOUNDED = 3,
+  MI_LP_PRIMAL_UNBOUNDED = 4,
+  MI_LP_DUAL_UNBOUNDED = 5,
+  MI_LP_INIT = 6,
+  MI_LP_PRIMAL_FEASIBLE = 7,
+  MI_LP_DUAL_FEASIBLE = 8,
+  MI_LP_ABNORMAL = 9,
+  MI_LP_INVALID_PROBLEM = 10,
+  MI_LP_IMPRECISE = 11
+};
+
+/* glop::VariableStatus / ConstraintStatus (lp_types.h:188-219). */
+enum {
+  MI_LP_BASIC = 0,
+  MI_LP_FIXED_VALUE = 1,
+  MI_LP_AT_LOWER_BOUND = 2,
+  MI_LP_AT_UPPER_BOUND = 3,
+  MI_LP_FREE = 4
+};
+
+/* GlopParameters enums (ortools/glop/parameters.proto:49-92). */
+enum { MI_LP_DANTZIG = 0, MI_LP_STEEPEST_EDGE = 1, MI_LP_DEVEX = 2 };
+enum { MI_LP_BASIS_NONE = 0, MI_LP_BASIS_BIXBY = 1, MI_LP_BASIS_TRIANGULAR = 2,
+       MI_LP_BASIS_MAROS = 3 };
+
+/* POD mirror of the GlopParameters fields read by RevisedSimplex
+ * (ortools/glop/parameters.proto, field numbers in comments). Fill with
+ * mi_glop_params_default() first; defaults are the proto defaults. */
+typedef struct mi_glop_params {
+  int32_t use_dual_simplex;                          /* 31, false  */
+  int32_t feasibility_rule;                          /* 1, STEEPEST_EDGE */
+  int32_t optimization_rule;                         /* 2, STEEPEST_EDGE */
+  int32_t initial_basis;                             /* 17, TRIANGULAR */
+  int32_t use_transposed_matrix;                     /* 18, true */
+  int32_t basis_refactorization_period;              /* 19, 64 */
+  int32_t dynamically_adjust_refactorization_period; /* 63, true */
+  int32_t change_status_to_imprecise;                /* 58, true */
+  int32_t markowitz_zlatev_parameter;                /* 29, 3 */
+  int32_t allow_simplex_algorithm_change;            /* 32, false */
+  int32_t devex_weights_reset_period;                /* 33, 150 */
+  int32_t use_middle_product_form_update;            /* 35, true (only true supported) */
+  int32_t initialize_devex_with_column_norms;        /* 36, true */
+  int32_t exploit_singleton_column_in_initial_basis; /* 37, true */
+  int32_t random_seed;                               /* 43, 1 */
+  int32_t perturb_costs_in_dual_simplex;             /* 53, false */
+  int32_t use_dedicated_dual_feasibility_algorithm;  /* 62, true */
+  int32_t push_to_vertex;                            /* 65, true */
+  int32_t dual_price_prioritize_norm;                /* 69, false */
+  int32_t use_scaling;                               /* 16, true (Bixby only) */
+  int64_t max_number_of_iterations;                  /* 27, -1 */
+  double refactorization_threshold;                  /* 6, 1e-9 */
+  double recompute_reduced_costs_threshold;          /* 8, 1e-8 */
+  double recompute_edges_norm_threshold;             /* 9, 100 */
+  double primal_feasibility_tolerance;               /* 10, 1e-8 */
+  double dual_feasibility_tolerance;                 /* 11, 1e-8 */
+  double ratio_test_zero_threshold;                  /* 12, 1e-9 */
+  double harris_tolerance_ratio;                     /* 13, 0.5 */
+  double small_pivot_threshold;                      /* 14, 1e-6 */
+  double minimum_acceptable_pivot;                   /* 15, 1e-6 */
+  double drop_tolerance;                             /* 52, 1e-14 */
+  double solution_feasibility_tolerance;             /* 22, 1e-6 */
+  double max_number_of_reoptimizations;              /* 56, 40 */
+  double lu_factorization_pivot_threshold;           /* 25, 0.01 */
+  double max_time_in_seconds;                        /* 26, inf */
+  double max_deterministic_time;                     /* 45, inf */
+  double markowitz_singularity_threshold;            /* 30, 1e-15 */
+  double dual_small_pivot_threshold;                 /* 38, 1e-4 */
+  double objective_lower_limit;                      /* 40, -inf */
+  double objective_upper_limit;                      /* 41, inf */
+  double degenerate_ministep_factor;                 /* 42, 0.01 */
+  double relative_cost_perturbation;                 /* 54, 1e-5 */
+  double relative_max_cost_perturbation;             /* 55, 1e-7 */
+  double initial_condition_number_threshold;         /* 59, 1e50 */
+  double crossover_bound_snapping_distance;          /* 64, inf */
+} mi_glop_params;
+
+typedef struct mi_lp_result {
+  int32_t problem_status; /* MI_LP_OPTIMAL ... */
+  int32_t error_code;     /* MI_LP_OK ... (non-OK => problem_status ABNORMAL) */
+  int64_t iterations;     /* RevisedSimplex::GetNumberOfIterations */
+  double objective;       /* RevisedSimplex::GetObjectiveValue */
+  double deterministic_time;
+  double solve_seconds;   /* wall time of Solve() */
+} mi_lp_result;
+
+/* Per-kernel accounting kept by the engine (roofline bookkeeping). */
+typedef struct mi_lp_kernel_stats {
+  int64_t launches[16];
+  double algorithmic_bytes[16];
+  double device_ms[16]; /* HIP-event time, filled when timing is enabled */
+} mi_lp_kernel_stats;
+
+enum {
+  MI_K_PRICING = 0,     /* ComputeReducedCosts SpMV (reduced_costs.cc:352-423) */
+  MI_K_UPDATE_ROW = 1,  /* UpdateRow column/row-wise (update_row.cc:196-306) */
+  MI_K_PRIMAL_NORMS = 2,/* UpdateEdgeSquaredNorms (primal_edge_norms.cc:208-258) */
+  MI_K_RC_UPDATE = 3,   /* UpdateReducedCosts (reduced_costs.cc:444-488) */
+  MI_K_PRICES = 4,      /* PrimalPrices candidate values (reduced_costs.cc:576-600) */
+  MI_K_COL_NORMS = 5,   /* initial edge norms, identity basis (primal_edge_norms.cc:147-161) */
+  MI_K_SPMV_ROWS = 6,   /* A x row sums: residual / basic values (variable_values.cc:101-133) */
+  MI_K_SINGLE_ROW = 7,  /* ComputeUpdatesForSingleRow (update_row.cc:261-280) */
+  MI_K_DUAL_RATIO = 8,  /* dual ratio-test candidate filter (entering_variable.cc:37-130) */
+  MI_K_COUNT = 9
+};
+
+void mi_glop_params_default(mi_glop_params* p);
+
+/* Returns the number of visible GPUs (0 on a host without one). */
+int mi_lp_device_count(void);
+
+int mi_lp_create(int device, mi_lp** out);
+int mi_lp_destroy(mi_lp* h);
+const char* mi_lp_last_error(const mi_lp* h);
+int mi_lp_set_params(mi_lp* h, const mi_glop_params* p);
+
+/* m constraints, n variables; A in CSC with n+1 col_starts. Bounds may be
+ * +/-INFINITY. maximize != 0 => objective is maximized. */
+int mi_lp_load(mi_lp* h, int32_t m, int32_t n, const int64_t* col_starts,
+               const int32_t* row_idx, const double* vals, const double* col_lb,
+               const double* col_ub, const double* row_lb, const double* row_ub,
+               const double* obj, double obj_offset, double obj_scale,
+               int32_t maximize);
+
+/* statuses: n+m glop::VariableStatus values (structural then slacks). */
+int mi_lp_load_basis_state(mi_lp* h, const int8_t* statuses, int32_t len);
+int mi_lp_clear_basis_state(mi_lp* h);
+int mi_lp_notify_matrix_unchanged(mi_lp* h);
+
+/* interrupt may be NULL; a non-zero value stops the solve like a time limit
+ * (glop_interface.cc:138-140). */
+int mi_lp_solve(mi_lp* h, const volatile int32_t* interrupt, mi_lp_result* out);
+
+int mi_lp_get_primal(const mi_lp* h, double* x);            /* n */
+int mi_lp_get_reduced_costs(const mi_lp* h, double* rc);    /* n */
+int mi_lp_get_duals(const mi_lp* h, double* y);             /* m */
+int mi_lp_get_activities(const mi_lp* h, double* act);      /* m */
+int mi_lp_get_statuses(const mi_lp* h, int8_t* var, int8_t* cons); /* n, m */
+int mi_lp_get_basis(const mi_lp* h, int32_t* basis);        /* m, column ids */
+int mi_lp_get_state(const mi_lp* h, int8_t* statuses);      /* n+m */
+int mi_lp_get_primal_ray(const mi_lp* h, double* ray);      /* n+m */
+int mi_lp_get_dual_ray(const mi_lp* h, double* ray);        /* m */
+int mi_lp_get_dual_ray_row_combination(const mi_lp* h, double* v); /* n+m */
+
+/* Benchmark slicing: mi_lp_begin starts Solve() on a worker thread that
+ * parks when num_iterations reaches pause_at (negative = never).
+ * mi_lp_run_until moves the pause point and blocks until the worker parks
+ * again or finishes (*finished = 1); the device stream is synchronized
+ * before it returns. mi_lp_finish joins and fills the result. */
+int mi_lp_begin(mi_lp* h, int64_t pause_at);
+int mi_lp_run_until(mi_lp* h, int64_t pause_at, int32_t* finished,
+                    int64_t* iterations);
+int mi_lp_finish(mi_lp* h, mi_lp_result* out);
+
+int mi_lp_get_kernel_stats(const mi_lp* h, mi_lp_kernel_stats* s);
+int mi_lp_reset_kernel_stats(mi_lp* h);
+/* enable != 0: bracket every hot kernel with HIP events (adds a sync). */
+int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable);
+
+/* Batch API: solves count independent LPs already loaded in handles (all on
+ * the same device), using worker threads each owning its own stream. */
+int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
+                      mi_lp_result* results);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MI_LP_H_ */

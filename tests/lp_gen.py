@@ -1,0 +1,105 @@
+"""Seeded synthetic LP generators (BASELINE.md section 2 / SURVEY.md 8(d)).
+
+All generators are deterministic functions of (shape, seed).
+"""
+import numpy as np
+
+from mi_glop.lp import LinearProgram
+
+INF = np.inf
+
+
+def random_sparse_lp(m, n, density, seed, eq_frac=0.2, free_frac=0.05,
+                     boxed_frac=0.5, maximize=False):
+    """Feasible LP with mixed row/column bound types (exercises every
+    VariableType of lp_types.h and the triangular crash on equality rows)."""
+    rng = np.random.default_rng(seed)
+    nnz_per_col = max(1, int(round(density * m)))
+    starts = [0]
+    rows, vals = [], []
+    for c in range(n):
+        k = max(1, min(m, rng.binomial(2 * nnz_per_col, 0.5)))
+        r = np.sort(rng.choice(m, size=k, replace=False))
+        v = rng.uniform(0.1, 1.0, size=k) * rng.choice([-1.0, 1.0], size=k)
+        rows.extend(r.tolist())
+        vals.extend(v.tolist())
+        starts.append(len(rows))
+    cs = np.asarray(starts, np.int64)
+    ri = np.asarray(rows, np.int32)
+    va = np.asarray(vals, np.float64)
+    x0 = rng.uniform(0.0, 1.0, size=n)
+    ax = np.zeros(m)
+    for c in range(n):
+        ax[ri[cs[c]:cs[c + 1]]] += va[cs[c]:cs[c + 1]] * x0[c]
+    col_lb = np.zeros(n)
+    col_ub = np.full(n, INF)
+    kinds = rng.uniform(size=n)
+    col_ub[kinds < boxed_frac] = 1.0 + rng.uniform(0, 2, size=(kinds < boxed_frac).sum())
+    free = kinds > 1 - free_frac
+    col_lb[free] = -INF
+    col_ub[free] = INF
+    row_lb = np.full(m, -INF)
+    row_ub = ax + rng.uniform(0.0, 1.0, size=m)
+    rk = rng.uniform(size=m)
+    eq = rk < eq_frac
+    row_lb[eq] = ax[eq]
+    row_ub[eq] = ax[eq]
+    ge = (rk >= eq_frac) & (rk < eq_frac + 0.3)
+    row_lb[ge] = ax[ge] - rng.uniform(0.0, 1.0, size=ge.sum())
+    row_ub[ge] = INF
+    rng_rows = (rk >= eq_frac + 0.3) & (rk < eq_frac + 0.45)
+    row_lb[rng_rows] = ax[rng_rows] - 1.0
+    obj = rng.uniform(-1.0, 1.0, size=n)
+    # Keep the LP bounded: free and unbounded-above columns get a cost that
+    # a dense set of <= rows can bound only sometimes, so cap them by a box.
+    unb = ~np.isfinite(col_ub)
+    col_ub[unb] = 10.0 + rng.uniform(0, 5, size=unb.sum())
+    col_lb[free] = -10.0 - rng.uniform(0, 5, size=free.sum())
+    return LinearProgram(m, n, cs, ri, va, col_lb, col_ub, row_lb, row_ub, obj,
+                         0.0, 1.0, maximize, f"sparse_{m}x{n}_s{seed}")
+
+
+def dense_box_lp(m, n, seed, maximize=True):
+    """Config 2 generator: A_ij ~ U(-1,1) dense,
+    x0 ~ U(0,1), rows A x <= A x0 + U(0,1), 0 <= x <= 10, c ~ U(-1,1)."""
+    rng = np.random.default_rng(seed)
+    A = rng.uniform(-1.0, 1.0, size=(m, n))
+    A[A == 0.0] = 0.5
+    x0 = rng.uniform(0.0, 1.0, size=n)
+    rhs = A @ x0 + rng.uniform(0.0, 1.0, size=m)
+    cs = np.arange(0, (n + 1) * m, m, dtype=np.int64)
+    ri = np.tile(np.arange(m, dtype=np.int32), n)
+    va = np.ascontiguousarray(A.T).reshape(-1)
+    obj = rng.uniform(-1.0, 1.0, size=n)
+    return LinearProgram(m, n, cs, ri, va, np.zeros(n), np.full(n, 10.0),
+                         np.full(m, -INF), rhs, obj, 0.0, 1.0, maximize,
+                         f"dense_{m}x{n}_s{seed}")
+
+
+def to_scipy(lp):
+    """Objective-only cross-check with scipy/HiGHS (test oracle pinning)."""
+    import scipy.sparse as sp
+    from scipy.optimize import linprog
+    A = sp.csc_matrix((lp.vals, lp.row_idx, lp.col_starts), shape=(lp.m, lp.n))
+    c = -lp.obj if lp.maximize else lp.obj
+    A_ub, b_ub, A_eq, b_eq = [], [], [], []
+    Ad = A.tocsr()
+    for r in range(lp.m):
+        lo, hi = lp.row_lb[r], lp.row_ub[r]
+        row = Ad[r]
+        if lo == hi:
+            A_eq.append(row); b_eq.append(hi)
+            continue
+        if np.isfinite(hi):
+            A_ub.append(row); b_ub.append(hi)
+        if np.isfinite(lo):
+            A_ub.append(-row); b_ub.append(-lo)
+    res = linprog(c, A_ub=sp.vstack(A_ub) if A_ub else None, b_ub=b_ub or None,
+                  A_eq=sp.vstack(A_eq) if A_eq else None, b_eq=b_eq or None,
+                  bounds=list(zip(np.where(np.isfinite(lp.col_lb), lp.col_lb, None),
+                                  np.where(np.isfinite(lp.col_ub), lp.col_ub, None))),
+                  method="highs")
+    if res.status != 0:
+        return res.status, None
+    val = res.fun + lp.obj_offset * (1 if not lp.maximize else -1)
+    return 0, (-val if lp.maximize else val)

@@ -1,0 +1,144 @@
+"""ctypes binding of the CPU oracle (oracle/build/liboracle_glop.so).
+
+TEST INFRASTRUCTURE ONLY: the oracle is the checker, never the product.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from mi_glop import abi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "build", "liboracle_glop.so")
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        L = ctypes.CDLL(ORACLE_SO)
+        L.oracle_lp_create.restype = ctypes.c_void_p
+        L.oracle_lp_destroy.argtypes = [ctypes.c_void_p]
+        vp = ctypes.c_void_p
+        L.oracle_lp_set_params.argtypes = [vp, ctypes.POINTER(abi.MiGlopParams)]
+        L.oracle_lp_load.argtypes = [vp, ctypes.c_int32, ctypes.c_int32] + \
+            [ctypes.c_void_p] * 8 + [ctypes.c_double, ctypes.c_double, ctypes.c_int32]
+        L.oracle_lp_solve.argtypes = [vp, ctypes.c_void_p, ctypes.POINTER(abi.MiLpResult)]
+        for name in ["oracle_lp_get_primal", "oracle_lp_get_reduced_costs",
+                     "oracle_lp_get_duals", "oracle_lp_get_activities",
+                     "oracle_lp_get_basis", "oracle_lp_get_state",
+                     "oracle_lp_get_primal_ray", "oracle_lp_get_dual_ray"]:
+            getattr(L, name).argtypes = [vp, ctypes.c_void_p]
+        L.oracle_lp_get_statuses.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_lp_load_basis_state.argtypes = [vp, ctypes.c_void_p, ctypes.c_int32]
+        L.oracle_lp_clear_basis_state.argtypes = [vp]
+        L.oracle_lp_notify_matrix_unchanged.argtypes = [vp]
+        L.oracle_lp_record_iteration_times.argtypes = [vp, ctypes.c_int32]
+        L.oracle_lp_get_iteration_times.argtypes = [vp, ctypes.c_void_p, ctypes.c_int64]
+        L.oracle_lp_get_iteration_times.restype = ctypes.c_int64
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleLp:
+    """Same surface as mi_glop.engine.LpHandle, CPU restatement behind it."""
+
+    def __init__(self, params=None):
+        self._L = lib()
+        self.h = ctypes.c_void_p(self._L.oracle_lp_create())
+        self.params = params or abi.default_params()
+        self.lp = None
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self._L.oracle_lp_destroy(self.h)
+            self.h = None
+
+    def set_params(self, params):
+        self.params = params
+
+    def load(self, lp):
+        self.lp = lp
+        self._keep = [np.ascontiguousarray(x) for x in (
+            lp.col_starts.astype(np.int64), lp.row_idx.astype(np.int32),
+            lp.vals.astype(np.float64), lp.col_lb.astype(np.float64),
+            lp.col_ub.astype(np.float64), lp.row_lb.astype(np.float64),
+            lp.row_ub.astype(np.float64), lp.obj.astype(np.float64))]
+        cs, ri, v, clb, cub, rlb, rub, ob = self._keep
+        self._L.oracle_lp_load(self.h, lp.m, lp.n, _p(cs), _p(ri), _p(v), _p(clb),
+                               _p(cub), _p(rlb), _p(rub), _p(ob), lp.obj_offset,
+                               lp.obj_scale, int(lp.maximize))
+
+    def load_basis_state(self, state):
+        st = np.ascontiguousarray(state, dtype=np.int8)
+        self._L.oracle_lp_load_basis_state(self.h, _p(st), len(st))
+
+    def clear_basis_state(self):
+        self._L.oracle_lp_clear_basis_state(self.h)
+
+    def notify_matrix_unchanged(self):
+        self._L.oracle_lp_notify_matrix_unchanged(self.h)
+
+    def record_iteration_times(self, on=True):
+        self._L.oracle_lp_record_iteration_times(self.h, int(on))
+
+    def iteration_times(self):
+        n = self._L.oracle_lp_get_iteration_times(self.h, None, 0)
+        out = np.zeros(n)
+        self._L.oracle_lp_get_iteration_times(self.h, _p(out), n)
+        return out
+
+    def solve(self):
+        self._L.oracle_lp_set_params(self.h, ctypes.byref(self.params))
+        r = abi.MiLpResult()
+        self._L.oracle_lp_solve(self.h, None, ctypes.byref(r))
+        return r
+
+    def _get(self, fn, n, dtype):
+        out = np.zeros(n, dtype=dtype)
+        getattr(self._L, fn)(self.h, _p(out))
+        return out
+
+    def primal(self):
+        return self._get("oracle_lp_get_primal", self.lp.n, np.float64)
+
+    def reduced_costs(self):
+        return self._get("oracle_lp_get_reduced_costs", self.lp.n, np.float64)
+
+    def duals(self):
+        return self._get("oracle_lp_get_duals", self.lp.m, np.float64)
+
+    def activities(self):
+        return self._get("oracle_lp_get_activities", self.lp.m, np.float64)
+
+    def basis(self):
+        return self._get("oracle_lp_get_basis", self.lp.m, np.int32)
+
+    def state(self):
+        return self._get("oracle_lp_get_state", self.lp.n + self.lp.m, np.int8)
+
+    def statuses(self):
+        var = np.zeros(self.lp.n, np.int8)
+        cons = np.zeros(self.lp.m, np.int8)
+        self._L.oracle_lp_get_statuses(self.h, _p(var), _p(cons))
+        return var, cons
+
+    def primal_ray(self):
+        return self._get("oracle_lp_get_primal_ray", self.lp.n + self.lp.m, np.float64)
+
+    def dual_ray(self):
+        return self._get("oracle_lp_get_dual_ray", self.lp.m, np.float64)
