@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Benchmark: simplex iterations/sec of the MI355X engine on BASELINE.json
+config 2 (dense random LP 10k x 50k, primal simplex, 1 MI355X), with the
+dominant kernel's roofline and the CPU oracle (Glop restatement) timed on the
+host in the same run.
+
+A "step" is one simplex iteration (RevisedSimplex::PrimalMinimize loop body,
+revised_simplex.cc:2772-3039). W warm-up iterations run untimed (they include
+loading, the initial factorization and the first edge norms); then exactly K
+iterations are timed, bracketed by barrier + device synchronize.
+
+Multi-GPU: one process per GPU (torchrun). A single LP does not shard in this
+round, so each rank solves its own replica LP (seed + rank): "replicas only",
+weak scaling, no collective in the data path; value = sum of iterations over
+ranks / max wall time over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "or-tools_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+from mi_glop import abi, engine  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "simplex iterations/sec + batched LPs/sec, 1/2/4/8 MI355X vs Glop CPU"
+
+
+def dense_box_lp(m, n, seed):
+    import lp_gen
+    return lp_gen.dense_box_lp(m, n, seed)
+
+
+def cpu_baseline(lp, warm, iters):
+    """Oracle (CPU restatement of Glop, single thread) on the same LP: time of
+    iterations warm..warm+iters from per-iteration timestamps."""
+    import oracle_lib
+    p = abi.default_params(max_number_of_iterations=warm + iters)
+    o = oracle_lib.OracleLp(p)
+    o.record_iteration_times(True)
+    o.load(lp)
+    t0 = time.perf_counter()
+    r = o.solve()
+    total = time.perf_counter() - t0
+    ts = o.iteration_times()
+    if len(ts) >= warm + iters and iters > 0:
+        dt = ts[warm + iters - 1] - (ts[warm - 1] if warm > 0 else 0.0)
+        rate = iters / dt
+    else:
+        rate = r.iterations / max(total, 1e-9)
+    return rate, dict(iterations=int(r.iterations), wall_s=total,
+                      timed_iterations=iters, warm_iterations=warm)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--m", type=int, default=10000)
+    ap.add_argument("--n", type=int, default=50000)
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--cpu-iters", type=int, default=6)
+    ap.add_argument("--cpu-warmup", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-launch HBM bytes of the dominant kernel from a "
+                         "separate rocprofv3 --pmc pass (profiles/)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = tdist
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+
+    lp = dense_box_lp(args.m, args.n, args.seed + rank)
+    params = abi.default_params()  # Glop defaults: primal simplex, steepest edge
+    h = engine.LpHandle(params, device=local_rank)
+    h.load(lp)
+    t_setup = time.perf_counter()
+    h.begin(args.warmup)  # load to HBM, factorize, first norms, W iterations
+    t_setup = time.perf_counter() - t_setup
+    h.reset_kernel_stats()
+    h.set_kernel_timing(True)
+
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    finished, it = h.run_until(args.warmup + args.steps)
+    sync()
+    barrier()
+    t1 = time.perf_counter()
+    stats = h.kernel_stats()
+    h.set_kernel_timing(False)
+    done = it - args.warmup
+    elapsed = t1 - t0
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([float(done)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        total_done = float(c.item())
+    else:
+        total_done = float(done)
+    h.finish()
+
+    # Dominant kernel in the timed region: roofline vs HBM peak.
+    dom = max(stats, key=lambda k: stats[k]["device_ms"])
+    ds = stats[dom]
+    launches = max(1, ds["launches"])
+    bytes_per_launch = ds["bytes"] / launches
+    ms_per_launch = ds["device_ms"] / launches if ds["device_ms"] > 0 else float("nan")
+    achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ds["device_ms"] > 0 else 0.0
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        traffic = json.load(open(args.traffic_json)).get(dom)
+
+    if rank != 0:
+        return
+    cpu = None
+    if not args.no_cpu and world == 1:
+        rate, info = cpu_baseline(lp, args.cpu_warmup, args.cpu_iters)
+        cpu = {"value": rate, "unit": "iterations/s", "cores": 1, "kind": "port",
+               "sample": (f"oracle (C++ restatement of Glop, -O3, 1 thread) on the same "
+                          f"{args.m}x{args.n} LP: iterations {args.cpu_warmup}.."
+                          f"{args.cpu_warmup + args.cpu_iters} timed "
+                          f"({info['wall_s']:.1f}s wall incl. setup)")}
+    value = total_done / elapsed if elapsed > 0 else 0.0
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * elapsed / max(1, done),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded dense random LP, BASELINE.json config 2 generator)",
+        "config": {
+            "workload": "config 2: dense random LP, primal simplex, Glop defaults",
+            "m": args.m, "n": args.n, "nnz": int(lp.nnz), "seed": args.seed,
+            "timed_iterations": [args.warmup, args.warmup + done],
+            "finished_early": bool(finished),
+            "setup_and_warmup_s": round(t_setup, 3),
+            "parallelism": f"replicas{world}",
+        },
+        "roofline": {
+            "kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "bytes_per_launch": bytes_per_launch, "ms_per_launch": ms_per_launch,
+            "launches": ds["launches"],
+        },
+        "kernels": {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
+                        "GB": round(v["bytes"] / 1e9, 3)} for k, v in stats.items()
+                    if v["launches"]},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,144 @@
+// Device state of one LP on one MI355X: the constraint matrix [A | I] in CSC
+// and CSR (the compact_matrix_ and transposed_matrix_ of RevisedSimplex,
+// revised_simplex.cc:989-1000), scratch vectors and the launchers of the
+// kernels in csrc/kernels/simplex_kernels.hip. All launches go to the
+// handle's own HIP stream. Results come back through pinned host buffers.
+#ifndef MILP_DEVICE_LP_H_
+#define MILP_DEVICE_LP_H_
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/mi_lp.h"
+
+namespace milp {
+
+class CompactSparseMatrix;
+
+struct DeviceError : public std::runtime_error {
+  explicit DeviceError(const std::string& s) : std::runtime_error(s) {}
+};
+
+class DeviceLp {
+ public:
+  DeviceLp() = default;
+  ~DeviceLp();
+  DeviceLp(const DeviceLp&) = delete;
+  DeviceLp& operator=(const DeviceLp&) = delete;
+
+  // Binds the handle to a GPU (hipSetDevice + stream). Throws DeviceError.
+  void Init(int device);
+  bool initialized() const { return stream_ != nullptr; }
+  int device() const { return device_; }
+
+  // Uploads [A | I] in CSC and CSR (transpose) and sizes every scratch buffer.
+  void UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseMatrix& csr);
+
+  // Bit masks over the N columns; uploaded only when the words change.
+  enum Mask { kRelevant = 0, kBasic = 1, kNotBasic = 2, kNumMasks = 3 };
+  void SetMask(Mask which, const uint64_t* words, int num_words);
+
+  // --- update row (update_row.cc:77-306) -------------------------------
+  // Column-wise: coefficient_[j] = a_j . rho for relevant j.
+  void UpdateRowColumnWise(const std::vector<double>& rho, double drop_tolerance,
+                           int64_t relevant_entries);
+  // algorithm 0 single row, 1 row-wise hypersparse, 2 row-wise.
+  void UpdateRowRowWise(const std::vector<int>& filtered_rows,
+                        const std::vector<double>& rho, int algorithm,
+                        double drop_tolerance);
+  // Fetches the listed positions (ascending) and their coefficients of the last
+  // update row.
+  void FetchUpdateRow(std::vector<int>* positions, std::vector<double>* values);
+  // Reads coefficient_[col] of the last update row (non-listed positions).
+  double ReadCoefficient(int col);
+
+  // --- dots over the listed update-row columns ---------------------------
+  // out[k] = a_{list[k]} . v (primal_edge_norms.cc:229-233).
+  void ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<double>* out);
+  // out[k] = a_{cols[k]} . v for an arbitrary host column list.
+  void ListDots(const std::vector<int>& cols, const std::vector<double>& v,
+                std::vector<double>* out);
+
+  // --- pricing (reduced_costs.cc:352-423) ------------------------------
+  void Pricing(const std::vector<double>& c, const std::vector<double>& y,
+               std::vector<double>* rc);
+
+  // --- 1 + ||a_j||^2 for relevant j (identity basis) -------------------
+  void ColumnSquaredNorms(std::vector<double>* out);
+
+  // --- row sums sign * sum_j x_j A[r, j] (increasing j), optionally skipping
+  // basic columns (variable_values.cc:101-131).
+  void RowSums(const std::vector<double>& x, bool skip_basic, double sign,
+               std::vector<double>* out);
+
+  // Accounting (roofline): launches, algorithmic bytes, HIP-event time.
+  void SetTiming(bool on) { timing_ = on; }
+  const mi_lp_kernel_stats& stats() const { return stats_; }
+  void ResetStats();
+  void Synchronize();
+
+ private:
+  template <typename T>
+  T* Alloc(size_t n);
+  void Upload(void* dst, const void* src, size_t bytes);
+  void Download(void* dst, const void* src, size_t bytes);
+  void BeginKernel(int id);
+  void EndKernel(int id, double bytes);
+  void Compact(int n);  // flags_ -> list_ (ascending), count -> list_count_
+  void Check(int err, const char* what);
+
+  int device_ = -1;
+  void* stream_ = nullptr;  // hipStream_t
+  void* ev_start_ = nullptr;
+  void* ev_stop_ = nullptr;
+  bool timing_ = false;
+  mi_lp_kernel_stats stats_{};
+  std::vector<void*> allocations_;
+
+  int m_ = 0;
+  int n_total_ = 0;  // N = n + m
+  int64_t nnz_ = 0;
+  double avg_col_len_ = 0.0;
+  // CSC of [A | I]
+  int64_t* d_starts_ = nullptr;
+  int32_t* d_rows_ = nullptr;
+  double* d_vals_ = nullptr;
+  // CSR of [A | I]
+  int64_t* d_t_starts_ = nullptr;
+  int32_t* d_t_cols_ = nullptr;
+  double* d_t_vals_ = nullptr;
+  std::vector<int64_t> h_starts_;  // host copy for byte accounting
+  std::vector<int64_t> h_t_starts_;
+
+  // masks
+  uint64_t* d_masks_[kNumMasks] = {nullptr, nullptr, nullptr};
+  std::vector<uint64_t> h_masks_[kNumMasks];
+  int mask_words_ = 0;
+
+  // scratch
+  double* d_vec_m_ = nullptr;    // rho / y / dli / ...
+  double* d_vec_m2_ = nullptr;   // row-sum output
+  double* d_vec_n_ = nullptr;    // x / c
+  double* d_coeff_ = nullptr;    // update row coefficients (persistent)
+  uint8_t* d_flags_ = nullptr;
+  int32_t* d_list_ = nullptr;    // compacted listed positions
+  int* d_count_ = nullptr;
+  double* d_out_n_ = nullptr;    // per-column / per-list results
+  int32_t* d_cols_ = nullptr;    // arbitrary column list / filtered rows
+  double* d_rho_vals_ = nullptr; // filtered rho values
+  void* d_cub_temp_ = nullptr;
+  size_t cub_temp_bytes_ = 0;
+  int list_count_ = 0;
+  int64_t list_entries_ = 0;  // sum of column lengths over the listed columns
+
+  // pinned staging
+  int32_t* h_pin_i_ = nullptr;
+  double* h_pin_d_ = nullptr;
+  double* h_pin_d2_ = nullptr;
+};
+
+}  // namespace milp
+
+#endif  // MILP_DEVICE_LP_H_

@@ -1,0 +1,365 @@
+// DeviceLp: device buffers + kernel launch plumbing (see device_lp.h).
+#include "device_lp.h"
+
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstring>
+
+#include "lp_data.h"
+
+#include "../kernels/kernel_args.h"
+
+namespace milp {
+
+namespace {
+inline hipStream_t S(void* p) { return reinterpret_cast<hipStream_t>(p); }
+
+__global__ void gather_kernel(const int32_t* list, const int* count, const double* src,
+                              double* dst) {
+  const int n = *count;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    dst[i] = src[list[i]];
+}
+}  // namespace
+
+void DeviceLp::Check(int err, const char* what) {
+  if (err != hipSuccess) {
+    throw DeviceError(std::string(what) + ": " +
+                      hipGetErrorString(static_cast<hipError_t>(err)));
+  }
+}
+
+DeviceLp::~DeviceLp() {
+  if (device_ >= 0) (void)hipSetDevice(device_);
+  if (stream_ != nullptr) (void)hipStreamSynchronize(S(stream_));
+  for (void* p : allocations_) (void)hipFree(p);
+  if (h_pin_i_) (void)hipHostFree(h_pin_i_);
+  if (h_pin_d_) (void)hipHostFree(h_pin_d_);
+  if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
+  if (ev_start_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_start_));
+  if (ev_stop_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_stop_));
+  if (stream_) (void)hipStreamDestroy(S(stream_));
+}
+
+void DeviceLp::Init(int device) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+    throw DeviceError("no HIP device visible (the MI355X engine has no CPU fallback)");
+  }
+  if (device < 0 || device >= count) throw DeviceError("bad device ordinal");
+  device_ = device;
+  Check(hipSetDevice(device), "hipSetDevice");
+  hipStream_t s;
+  Check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  stream_ = s;
+  hipEvent_t a, b;
+  Check(hipEventCreate(&a), "hipEventCreate");
+  Check(hipEventCreate(&b), "hipEventCreate");
+  ev_start_ = a;
+  ev_stop_ = b;
+}
+
+template <typename T>
+T* DeviceLp::Alloc(size_t n) {
+  void* p = nullptr;
+  Check(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)), "hipMalloc");
+  allocations_.push_back(p);
+  return static_cast<T*>(p);
+}
+
+void DeviceLp::Upload(void* dst, const void* src, size_t bytes) {
+  if (bytes == 0) return;
+  Check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream_)), "H2D");
+}
+
+void DeviceLp::Download(void* dst, const void* src, size_t bytes) {
+  if (bytes == 0) return;
+  Check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, S(stream_)), "D2H");
+  Check(hipStreamSynchronize(S(stream_)), "sync");
+}
+
+void DeviceLp::Synchronize() { Check(hipStreamSynchronize(S(stream_)), "sync"); }
+
+void DeviceLp::ResetStats() { std::memset(&stats_, 0, sizeof(stats_)); }
+
+void DeviceLp::BeginKernel(int /*id*/) {
+  if (timing_) Check(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_start_), S(stream_)), "ev");
+}
+
+void DeviceLp::EndKernel(int id, double bytes) {
+  Check(hipGetLastError(), "kernel launch");
+  stats_.launches[id] += 1;
+  stats_.algorithmic_bytes[id] += bytes;
+  if (timing_) {
+    Check(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_stop_), S(stream_)), "ev");
+    Check(hipEventSynchronize(reinterpret_cast<hipEvent_t>(ev_stop_)), "ev sync");
+    float ms = 0.0f;
+    Check(hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(ev_start_),
+                              reinterpret_cast<hipEvent_t>(ev_stop_)),
+          "ev time");
+    stats_.device_ms[id] += ms;
+  }
+}
+
+void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseMatrix& csr) {
+  Check(hipSetDevice(device_), "hipSetDevice");
+  for (void* p : allocations_) (void)hipFree(p);
+  allocations_.clear();
+  m_ = csc.num_rows();
+  n_total_ = csc.num_cols();
+  nnz_ = csc.num_entries();
+  avg_col_len_ = n_total_ > 0 ? static_cast<double>(nnz_) / n_total_ : 0.0;
+  h_starts_ = csc.starts_;
+  h_t_starts_ = csr.starts_;
+  d_starts_ = Alloc<int64_t>(n_total_ + 1);
+  d_rows_ = Alloc<int32_t>(nnz_);
+  d_vals_ = Alloc<double>(nnz_);
+  d_t_starts_ = Alloc<int64_t>(m_ + 1);
+  d_t_cols_ = Alloc<int32_t>(nnz_);
+  d_t_vals_ = Alloc<double>(nnz_);
+  Upload(d_starts_, csc.starts_.data(), (n_total_ + 1) * sizeof(int64_t));
+  Upload(d_rows_, csc.rows_.data(), nnz_ * sizeof(int32_t));
+  Upload(d_vals_, csc.coefficients_.data(), nnz_ * sizeof(double));
+  Upload(d_t_starts_, csr.starts_.data(), (m_ + 1) * sizeof(int64_t));
+  Upload(d_t_cols_, csr.rows_.data(), nnz_ * sizeof(int32_t));
+  Upload(d_t_vals_, csr.coefficients_.data(), nnz_ * sizeof(double));
+  mask_words_ = (n_total_ + 63) / 64;
+  for (int k = 0; k < kNumMasks; ++k) {
+    d_masks_[k] = Alloc<uint64_t>(mask_words_);
+    h_masks_[k].assign(mask_words_, ~0ull);  // force first upload
+  }
+  d_vec_m_ = Alloc<double>(m_);
+  d_vec_m2_ = Alloc<double>(m_);
+  d_vec_n_ = Alloc<double>(n_total_);
+  d_coeff_ = Alloc<double>(n_total_);
+  d_flags_ = Alloc<uint8_t>(n_total_);
+  d_list_ = Alloc<int32_t>(n_total_);
+  d_count_ = Alloc<int>(1);
+  d_out_n_ = Alloc<double>(n_total_);
+  d_cols_ = Alloc<int32_t>(std::max(n_total_, m_));
+  d_rho_vals_ = Alloc<double>(m_);
+  Check(hipMemsetAsync(d_coeff_, 0, n_total_ * sizeof(double), S(stream_)), "memset");
+  // hipcub temp storage for the flag compaction.
+  cub_temp_bytes_ = 0;
+  Check(hipcub::DeviceSelect::Flagged(nullptr, cub_temp_bytes_,
+                                      hipcub::CountingInputIterator<int32_t>(0), d_flags_,
+                                      d_list_, d_count_, n_total_, S(stream_)),
+        "cub sizing");
+  d_cub_temp_ = Alloc<uint8_t>(cub_temp_bytes_);
+  if (h_pin_i_) (void)hipHostFree(h_pin_i_);
+  if (h_pin_d_) (void)hipHostFree(h_pin_d_);
+  if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
+  const size_t big = std::max(n_total_, m_) + 1;
+  Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_i_), big * sizeof(int32_t)), "pin");
+  Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d_), big * sizeof(double)), "pin");
+  Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d2_), big * sizeof(double)), "pin");
+  list_count_ = 0;
+  Synchronize();
+}
+
+void DeviceLp::SetMask(Mask which, const uint64_t* words, int num_words) {
+  std::vector<uint64_t>& h = h_masks_[which];
+  if (num_words != mask_words_) throw DeviceError("mask size mismatch");
+  if (std::memcmp(h.data(), words, num_words * sizeof(uint64_t)) == 0) return;
+  std::memcpy(h.data(), words, num_words * sizeof(uint64_t));
+  Upload(d_masks_[which], h.data(), num_words * sizeof(uint64_t));
+}
+
+void DeviceLp::Compact(int n) {
+  size_t bytes = cub_temp_bytes_;
+  Check(hipcub::DeviceSelect::Flagged(d_cub_temp_, bytes,
+                                      hipcub::CountingInputIterator<int32_t>(0), d_flags_,
+                                      d_list_, d_count_, n, S(stream_)),
+        "cub flagged");
+  int count = 0;
+  Download(h_pin_i_, d_count_, sizeof(int));
+  count = h_pin_i_[0];
+  list_count_ = count;
+}
+
+void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
+                                   int64_t relevant_entries) {
+  std::memcpy(h_pin_d_, rho.data(), m_ * sizeof(double));
+  Upload(d_vec_m_, h_pin_d_, m_ * sizeof(double));
+  milp_kernels::DotArgs a{};
+  a.starts = d_starts_;
+  a.rows = d_rows_;
+  a.vals = d_vals_;
+  a.y = d_vec_m_;
+  a.ncols = n_total_;
+  a.mask = d_masks_[kRelevant];
+  a.out = d_coeff_;
+  a.flags = d_flags_;
+  a.drop_tolerance = drop;
+  BeginKernel(MI_K_UPDATE_ROW);
+  Check(milp_launch::column_dot(0, avg_col_len_ >= 32.0, a, S(stream_)), "colwise");
+  // Algorithmic bytes: every relevant column is read (12 B/entry), rho is
+  // read once (8 B/row), coefficients + flags written (9 B/column).
+  EndKernel(MI_K_UPDATE_ROW,
+            12.0 * double(relevant_entries) + 8.0 * m_ + 9.0 * n_total_);
+  Compact(n_total_);
+}
+
+void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
+                                const std::vector<double>& rho, int algorithm,
+                                double drop) {
+  const int k = static_cast<int>(filtered_rows.size());
+  std::memcpy(h_pin_i_, filtered_rows.data(), k * sizeof(int32_t));
+  for (int i = 0; i < k; ++i) h_pin_d_[i] = rho[filtered_rows[i]];
+  Upload(d_cols_, h_pin_i_, k * sizeof(int32_t));
+  Upload(d_rho_vals_, h_pin_d_, k * sizeof(double));
+  milp_kernels::RowWiseArgs a{};
+  a.t_starts = d_t_starts_;
+  a.t_cols = d_t_cols_;
+  a.t_vals = d_t_vals_;
+  a.filtered_rows = d_cols_;
+  a.rho = d_rho_vals_;
+  a.num_filtered = k;
+  a.num_cols = n_total_;
+  a.relevant = d_masks_[kRelevant];
+  a.coefficient = d_coeff_;
+  a.flags = d_flags_;
+  a.drop_tolerance = drop;
+  a.algorithm = algorithm;
+  const int id = algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW;
+  BeginKernel(id);
+  Check(milp_launch::row_wise_update(a, S(stream_)), "rowwise");
+  double entries = 0.0;
+  for (int r : filtered_rows) entries += double(h_t_starts_[r + 1] - h_t_starts_[r]);
+  EndKernel(id, 12.0 * entries + 12.0 * k + 9.0 * n_total_);
+  Compact(n_total_);
+}
+
+void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* values) {
+  const int n = list_count_;
+  positions->resize(n);
+  values->resize(n);
+  if (n == 0) return;
+  gather_kernel<<<std::min(1024, (n + 255) / 256), 256, 0, S(stream_)>>>(d_list_, d_count_,
+                                                                         d_coeff_, d_out_n_);
+  Check(hipGetLastError(), "gather");
+  Check(hipMemcpyAsync(h_pin_i_, d_list_, n * sizeof(int32_t), hipMemcpyDeviceToHost,
+                       S(stream_)),
+        "D2H");
+  Download(h_pin_d_, d_out_n_, n * sizeof(double));
+  std::memcpy(positions->data(), h_pin_i_, n * sizeof(int32_t));
+  std::memcpy(values->data(), h_pin_d_, n * sizeof(double));
+  list_entries_ = 0;
+  for (int i = 0; i < n; ++i) {
+    const int c = (*positions)[i];
+    list_entries_ += h_starts_[c + 1] - h_starts_[c];
+  }
+}
+
+double DeviceLp::ReadCoefficient(int col) {
+  double v = 0.0;
+  Download(h_pin_d2_, d_coeff_ + col, sizeof(double));
+  v = h_pin_d2_[0];
+  return v;
+}
+
+void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<double>* out) {
+  const int n = list_count_;
+  out->resize(n);
+  if (n == 0) return;
+  std::memcpy(h_pin_d2_, v.data(), m_ * sizeof(double));
+  Upload(d_vec_m_, h_pin_d2_, m_ * sizeof(double));
+  milp_kernels::DotArgs a{};
+  a.starts = d_starts_;
+  a.rows = d_rows_;
+  a.vals = d_vals_;
+  a.y = d_vec_m_;
+  a.ncols = n;
+  a.col_list = d_list_;
+  a.out = d_out_n_;
+  BeginKernel(MI_K_PRIMAL_NORMS);
+  Check(milp_launch::column_dot(2, avg_col_len_ >= 32.0, a, S(stream_)), "listdots");
+  EndKernel(MI_K_PRIMAL_NORMS,
+            12.0 * double(list_entries_) + 8.0 * m_ + 4.0 * n + 8.0 * n);
+  Download(h_pin_d_, d_out_n_, n * sizeof(double));
+  std::memcpy(out->data(), h_pin_d_, n * sizeof(double));
+}
+
+void DeviceLp::ListDots(const std::vector<int>& cols, const std::vector<double>& v,
+                        std::vector<double>* out) {
+  const int n = static_cast<int>(cols.size());
+  out->resize(n);
+  if (n == 0) return;
+  std::memcpy(h_pin_i_, cols.data(), n * sizeof(int32_t));
+  Upload(d_cols_, h_pin_i_, n * sizeof(int32_t));
+  std::memcpy(h_pin_d2_, v.data(), m_ * sizeof(double));
+  Upload(d_vec_m_, h_pin_d2_, m_ * sizeof(double));
+  milp_kernels::DotArgs a{};
+  a.starts = d_starts_;
+  a.rows = d_rows_;
+  a.vals = d_vals_;
+  a.y = d_vec_m_;
+  a.ncols = n;
+  a.col_list = d_cols_;
+  a.out = d_out_n_;
+  double entries = 0.0;
+  for (int c : cols) entries += double(h_starts_[c + 1] - h_starts_[c]);
+  BeginKernel(MI_K_PRIMAL_NORMS);
+  Check(milp_launch::column_dot(2, avg_col_len_ >= 32.0, a, S(stream_)), "listdots");
+  EndKernel(MI_K_PRIMAL_NORMS, 12.0 * entries + 8.0 * m_ + 12.0 * n);
+  Download(h_pin_d_, d_out_n_, n * sizeof(double));
+  std::memcpy(out->data(), h_pin_d_, n * sizeof(double));
+}
+
+void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& y,
+                       std::vector<double>* rc) {
+  std::memcpy(h_pin_d_, c.data(), n_total_ * sizeof(double));
+  Upload(d_vec_n_, h_pin_d_, n_total_ * sizeof(double));
+  std::memcpy(h_pin_d2_, y.data(), m_ * sizeof(double));
+  Upload(d_vec_m_, h_pin_d2_, m_ * sizeof(double));
+  milp_kernels::DotArgs a{};
+  a.starts = d_starts_;
+  a.rows = d_rows_;
+  a.vals = d_vals_;
+  a.y = d_vec_m_;
+  a.ncols = n_total_;
+  a.c = d_vec_n_;
+  a.out = d_out_n_;
+  BeginKernel(MI_K_PRICING);
+  Check(milp_launch::column_dot(1, avg_col_len_ >= 32.0, a, S(stream_)), "pricing");
+  // 12 B per entry of [A|I] + column starts + y + c in + rc out.
+  EndKernel(MI_K_PRICING, 12.0 * nnz_ + 8.0 * (n_total_ + 1) + 8.0 * m_ + 16.0 * n_total_);
+  rc->resize(n_total_);
+  Download(h_pin_d_, d_out_n_, n_total_ * sizeof(double));
+  std::memcpy(rc->data(), h_pin_d_, n_total_ * sizeof(double));
+}
+
+void DeviceLp::ColumnSquaredNorms(std::vector<double>* out) {
+  BeginKernel(MI_K_COL_NORMS);
+  Check(milp_launch::column_squared_norms(d_starts_, d_vals_, d_masks_[kRelevant], n_total_,
+                                          d_out_n_, S(stream_)),
+        "colnorms");
+  EndKernel(MI_K_COL_NORMS, 8.0 * nnz_ + 8.0 * (n_total_ + 1) + 8.0 * n_total_);
+  out->resize(n_total_);
+  Download(h_pin_d_, d_out_n_, n_total_ * sizeof(double));
+  std::memcpy(out->data(), h_pin_d_, n_total_ * sizeof(double));
+}
+
+void DeviceLp::RowSums(const std::vector<double>& x, bool skip_basic, double sign,
+                       std::vector<double>* out) {
+  std::memcpy(h_pin_d_, x.data(), n_total_ * sizeof(double));
+  Upload(d_vec_n_, h_pin_d_, n_total_ * sizeof(double));
+  milp_kernels::RowSumArgs a{};
+  a.t_starts = d_t_starts_;
+  a.t_cols = d_t_cols_;
+  a.t_vals = d_t_vals_;
+  a.x = d_vec_n_;
+  a.skip = skip_basic ? d_masks_[kBasic] : nullptr;
+  a.sign = sign;
+  a.num_rows = m_;
+  a.out = d_vec_m2_;
+  BeginKernel(MI_K_SPMV_ROWS);
+  Check(milp_launch::row_sums(a, S(stream_)), "rowsums");
+  EndKernel(MI_K_SPMV_ROWS, 12.0 * nnz_ + 8.0 * (m_ + 1) + 8.0 * n_total_ + 8.0 * m_);
+  out->resize(m_);
+  Download(h_pin_d_, d_vec_m2_, m_ * sizeof(double));
+  std::memcpy(out->data(), h_pin_d_, m_ * sizeof(double));
+}
+
+}  // namespace milp

@@ -1,0 +1,936 @@
+// Host basis factorization of the MI355X simplex engine (see lu.h).
+#include "lu.h"
+
+namespace milp {
+
+// ---------------------------------------------------------------------------
+// Markowitz (markowitz.cc:14-494)
+Status Markowitz::ComputeRowAndColumnPermutation(const CompactSparseMatrixView& b,
+                                                 std::vector<int>* row_perm,
+                                                 std::vector<int>* col_perm) {
+  Clear();
+  const int num_rows = b.num_rows();
+  const int num_cols = b.num_cols();
+  col_perm->assign(num_cols, kInvalidCol);
+  row_perm->assign(num_rows, kInvalidRow);
+  if (b.IsEmpty()) return Status::OK();
+  basis_matrix_ = &b;
+  lower_.Reset(num_rows, num_cols);
+  upper_.Reset(num_rows, num_cols);
+  permuted_lower_.Reset(num_cols);
+  permuted_upper_.Reset(num_cols);
+  permuted_lower_column_needs_solve_.assign(num_cols, false);
+  contains_only_singleton_columns_ = true;
+
+  int index = 0;
+  ExtractSingletonColumns(b, row_perm, col_perm, &index);
+  ExtractResidualSingletonColumns(b, row_perm, col_perm, &index);
+  residual_matrix_non_zero_.InitializeFromMatrixSubset(
+      b, *row_perm, *col_perm, &singleton_column_, &singleton_row_);
+
+  const int end_index = std::min(num_rows, num_cols);
+  const Fractional singularity_threshold =
+      parameters_.markowitz_singularity_threshold;
+  while (index < end_index) {
+    Fractional pivot_coefficient = 0.0;
+    int pivot_row = kInvalidRow;
+    int pivot_col = kInvalidCol;
+    const int64_t min_markowitz = FindPivot(*row_perm, *col_perm, &pivot_row,
+                                            &pivot_col, &pivot_coefficient);
+    if (pivot_row == kInvalidRow || pivot_col == kInvalidCol ||
+        std::fabs(pivot_coefficient) <= singularity_threshold) {
+      return Status(Status::ERROR_LU, "The matrix is singular!");
+    }
+    const int pivot_col_degree = residual_matrix_non_zero_.ColDegree(pivot_col);
+    residual_matrix_non_zero_.DeleteRowAndColumn(pivot_row, pivot_col);
+    if (min_markowitz == 0) {
+      if (pivot_col_degree == 1) {
+        RemoveRowFromResidualMatrix(pivot_row, pivot_col);
+      } else {
+        RemoveColumnFromResidualMatrix(pivot_row, pivot_col);
+      }
+    } else {
+      UpdateResidualMatrix(pivot_row, pivot_col);
+    }
+    if (contains_only_singleton_columns_) {
+      lower_.AddDiagonalOnlyColumn(1.0);
+      upper_.AddTriangularColumn(b.column(pivot_col), pivot_row);
+    } else {
+      lower_.AddAndNormalizeTriangularColumn(permuted_lower_.column(pivot_col),
+                                             pivot_row, pivot_coefficient);
+      permuted_lower_.ClearAndReleaseColumn(pivot_col);
+      upper_.AddTriangularColumnWithGivenDiagonalEntry(
+          permuted_upper_.column(pivot_col), pivot_row, pivot_coefficient);
+      permuted_upper_.ClearAndReleaseColumn(pivot_col);
+    }
+    (*col_perm)[pivot_col] = index;
+    (*row_perm)[pivot_row] = index;
+    ++index;
+  }
+  num_fp_operations_ += 10 * lower_.num_entries();
+  num_fp_operations_ += 10 * upper_.num_entries();
+  return Status::OK();
+}
+
+Status Markowitz::ComputeLU(const CompactSparseMatrixView& b,
+                            std::vector<int>* row_perm, std::vector<int>* col_perm,
+                            TriangularMatrix* lower, TriangularMatrix* upper) {
+  lower_.Swap(lower);
+  upper_.Swap(upper);
+  MILP_RETURN_IF_ERROR(ComputeRowAndColumnPermutation(b, row_perm, col_perm));
+  lower_.ApplyRowPermutationToNonDiagonalEntries(*row_perm);
+  upper_.ApplyRowPermutationToNonDiagonalEntries(*row_perm);
+  lower_.Swap(lower);
+  upper_.Swap(upper);
+  return Status::OK();
+}
+
+void Markowitz::Clear() {
+  permuted_lower_.Clear();
+  permuted_upper_.Clear();
+  residual_matrix_non_zero_.Clear();
+  col_by_degree_.Clear();
+  examined_col_.clear();
+  num_fp_operations_ = 0;
+  is_col_by_degree_initialized_ = false;
+}
+
+namespace {
+struct MatrixEntry {
+  int row;
+  int col;
+  Fractional coefficient;
+  bool operator<(const MatrixEntry& o) const {
+    return (row == o.row) ? col < o.col : row < o.row;
+  }
+};
+}  // namespace
+
+void Markowitz::ExtractSingletonColumns(const CompactSparseMatrixView& b,
+                                        std::vector<int>* row_perm,
+                                        std::vector<int>* col_perm, int* index) {
+  std::vector<MatrixEntry> singleton_entries;
+  const int num_cols = b.num_cols();
+  for (int col = 0; col < num_cols; ++col) {
+    const ColumnView c = b.column(col);
+    if (c.n == 1) {
+      singleton_entries.push_back(
+          MatrixEntry{c.GetFirstRow(), col, c.GetFirstCoefficient()});
+    }
+  }
+  std::sort(singleton_entries.begin(), singleton_entries.end());
+  for (const MatrixEntry e : singleton_entries) {
+    if ((*row_perm)[e.row] == kInvalidRow) {
+      (*col_perm)[e.col] = *index;
+      (*row_perm)[e.row] = *index;
+      lower_.AddDiagonalOnlyColumn(1.0);
+      upper_.AddDiagonalOnlyColumn(e.coefficient);
+      ++(*index);
+    }
+  }
+}
+
+namespace {
+bool IsResidualSingletonColumn(const ColumnView& c,
+                               const std::vector<int>& row_perm, int* row) {
+  int residual_degree = 0;
+  for (int64_t i = 0; i < c.n; ++i) {
+    if (row_perm[c.rows[i]] != kInvalidRow) continue;
+    ++residual_degree;
+    if (residual_degree > 1) return false;
+    *row = c.rows[i];
+  }
+  return residual_degree == 1;
+}
+}  // namespace
+
+void Markowitz::ExtractResidualSingletonColumns(const CompactSparseMatrixView& b,
+                                                std::vector<int>* row_perm,
+                                                std::vector<int>* col_perm,
+                                                int* index) {
+  const int num_cols = b.num_cols();
+  int row = kInvalidRow;
+  for (int col = 0; col < num_cols; ++col) {
+    if ((*col_perm)[col] != kInvalidCol) continue;
+    const ColumnView c = b.column(col);
+    if (!IsResidualSingletonColumn(c, *row_perm, &row)) continue;
+    (*col_perm)[col] = *index;
+    (*row_perm)[row] = *index;
+    lower_.AddDiagonalOnlyColumn(1.0);
+    upper_.AddTriangularColumn(c, row);
+    ++(*index);
+  }
+}
+
+const SparseColumn& Markowitz::ComputeColumn(const std::vector<int>& row_perm,
+                                             int col) {
+  const bool first_time = permuted_lower_.column(col).IsEmpty() &&
+                          permuted_upper_.column(col).IsEmpty();
+  SparseColumn* lower_column = permuted_lower_.mutable_column(col);
+  if (permuted_lower_column_needs_solve_[col]) {
+    // Note: when not first_time, the input is a copy of lower_column since the
+    // solve overwrites it (Glop passes ColumnView(*lower_column) and clears
+    // lower_column only after copying its values into the scratchpad).
+    if (first_time) {
+      lower_.PermutedLowerSparseSolve(basis_matrix_->column(col), row_perm,
+                                      lower_column,
+                                      permuted_upper_.mutable_column(col));
+    } else {
+      const SparseColumn input = *lower_column;
+      lower_.PermutedLowerSparseSolve(input.view(), row_perm, lower_column,
+                                      permuted_upper_.mutable_column(col));
+    }
+    permuted_lower_column_needs_solve_[col] = false;
+    num_fp_operations_ += lower_.NumFpOperationsInLastPermutedLowerSparseSolve();
+    return *lower_column;
+  }
+  if (lower_column->num_entries() == residual_matrix_non_zero_.ColDegree(col)) {
+    return *lower_column;
+  }
+  if (first_time) {
+    const ColumnView c = basis_matrix_->column(col);
+    num_fp_operations_ += c.n;
+    lower_column->Reserve(c.n);
+    for (int64_t i = 0; i < c.n; ++i)
+      lower_column->SetCoefficient(c.rows[i], c.coefs[i]);
+  }
+  num_fp_operations_ += lower_column->num_entries();
+  lower_column->MoveTaggedEntriesTo(row_perm, permuted_upper_.mutable_column(col));
+  return *lower_column;
+}
+
+int64_t Markowitz::FindPivot(const std::vector<int>& row_perm,
+                             const std::vector<int>& col_perm, int* pivot_row,
+                             int* pivot_col, Fractional* pivot_coefficient) {
+  while (!singleton_column_.empty()) {
+    const int col = singleton_column_.back();
+    singleton_column_.pop_back();
+    if (residual_matrix_non_zero_.ColDegree(col) != 1) continue;
+    if (contains_only_singleton_columns_) {
+      *pivot_col = col;
+      const ColumnView c = basis_matrix_->column(col);
+      for (int64_t i = 0; i < c.n; ++i) {
+        if (row_perm[c.rows[i]] == kInvalidRow) {
+          *pivot_row = c.rows[i];
+          *pivot_coefficient = c.coefs[i];
+          break;
+        }
+      }
+      return 0;
+    }
+    const SparseColumn& column = ComputeColumn(row_perm, col);
+    if (column.IsEmpty()) continue;
+    *pivot_col = col;
+    *pivot_row = column.GetFirstRow();
+    *pivot_coefficient = column.GetFirstCoefficient();
+    return 0;
+  }
+  contains_only_singleton_columns_ = false;
+
+  while (!singleton_row_.empty()) {
+    const int row = singleton_row_.back();
+    singleton_row_.pop_back();
+    if (row_perm[row] != kInvalidRow) continue;
+    if (residual_matrix_non_zero_.RowDegree(row) != 1) continue;
+    const int col = residual_matrix_non_zero_.GetFirstNonDeletedColumnFromRow(row);
+    if (col == kInvalidCol) continue;
+    const SparseColumn& column = ComputeColumn(row_perm, col);
+    if (column.IsEmpty()) continue;
+    *pivot_col = col;
+    *pivot_row = row;
+    *pivot_coefficient = column.LookUpCoefficient(row);
+    return 0;
+  }
+
+  if (!is_col_by_degree_initialized_) {
+    is_col_by_degree_initialized_ = true;
+    const int num_cols = static_cast<int>(col_perm.size());
+    col_by_degree_.Reset(static_cast<int>(row_perm.size()), num_cols);
+    for (int col = 0; col < num_cols; ++col) {
+      if (col_perm[col] != kInvalidCol) continue;
+      UpdateDegree(col, residual_matrix_non_zero_.ColDegree(col));
+    }
+  }
+
+  int64_t min_markowitz_number = std::numeric_limits<int64_t>::max();
+  examined_col_.clear();
+  const int num_columns_to_examine = parameters_.markowitz_zlatev_parameter;
+  const Fractional threshold = parameters_.lu_factorization_pivot_threshold;
+  while (static_cast<int>(examined_col_.size()) < num_columns_to_examine) {
+    const int col = col_by_degree_.Pop();
+    if (col == kInvalidCol) break;
+    if (col_perm[col] != kInvalidCol) continue;
+    const int col_degree = residual_matrix_non_zero_.ColDegree(col);
+    examined_col_.push_back(col);
+    const int64_t markowitz_lower_bound = col_degree - 1;
+    if (min_markowitz_number < markowitz_lower_bound) break;
+    const SparseColumn& column = ComputeColumn(row_perm, col);
+    Fractional max_magnitude = 0.0;
+    for (int64_t k = 0; k < column.num_entries(); ++k)
+      max_magnitude = std::max(max_magnitude, std::fabs(column.coefs[k]));
+    if (max_magnitude == 0.0) {
+      examined_col_.pop_back();
+      continue;
+    }
+    const Fractional skip_threshold = threshold * max_magnitude;
+    for (int64_t k = 0; k < column.num_entries(); ++k) {
+      const Fractional magnitude = std::fabs(column.coefs[k]);
+      if (magnitude < skip_threshold) continue;
+      const int row_degree = residual_matrix_non_zero_.RowDegree(column.rows[k]);
+      const int64_t markowitz_number =
+          static_cast<int64_t>(col_degree - 1) * (row_degree - 1);
+      if (markowitz_number < min_markowitz_number ||
+          ((markowitz_number == min_markowitz_number) &&
+           magnitude > std::fabs(*pivot_coefficient))) {
+        min_markowitz_number = markowitz_number;
+        *pivot_col = col;
+        *pivot_row = column.rows[k];
+        *pivot_coefficient = column.coefs[k];
+      }
+    }
+  }
+  for (const int col : examined_col_) {
+    if (col != *pivot_col) {
+      col_by_degree_.PushOrAdjust(col, residual_matrix_non_zero_.ColDegree(col));
+    }
+  }
+  return min_markowitz_number;
+}
+
+void Markowitz::UpdateDegree(int col, int degree) {
+  if (degree == 1) {
+    singleton_column_.push_back(col);
+  } else {
+    col_by_degree_.PushOrAdjust(col, degree);
+  }
+}
+
+void Markowitz::RemoveRowFromResidualMatrix(int pivot_row, int /*pivot_col*/) {
+  if (is_col_by_degree_initialized_) {
+    for (const int col : residual_matrix_non_zero_.RowNonZero(pivot_row)) {
+      if (residual_matrix_non_zero_.IsColumnDeleted(col)) continue;
+      UpdateDegree(col, residual_matrix_non_zero_.DecreaseColDegree(col));
+    }
+  } else {
+    for (const int col : residual_matrix_non_zero_.RowNonZero(pivot_row)) {
+      if (residual_matrix_non_zero_.IsColumnDeleted(col)) continue;
+      if (residual_matrix_non_zero_.DecreaseColDegree(col) == 1) {
+        singleton_column_.push_back(col);
+      }
+    }
+  }
+}
+
+void Markowitz::RemoveColumnFromResidualMatrix(int /*pivot_row*/, int pivot_col) {
+  const SparseColumn& c = permuted_lower_.column(pivot_col);
+  for (int64_t k = 0; k < c.num_entries(); ++k) {
+    const int row = c.rows[k];
+    if (residual_matrix_non_zero_.DecreaseRowDegree(row) == 1) {
+      singleton_row_.push_back(row);
+    }
+  }
+}
+
+void Markowitz::UpdateResidualMatrix(int pivot_row, int pivot_col) {
+  const SparseColumn& pivot_column = permuted_lower_.column(pivot_col);
+  residual_matrix_non_zero_.Update(pivot_row, pivot_col, pivot_column);
+  for (const int col : residual_matrix_non_zero_.RowNonZero(pivot_row)) {
+    UpdateDegree(col, residual_matrix_non_zero_.ColDegree(col));
+    permuted_lower_column_needs_solve_[col] = true;
+  }
+  RemoveColumnFromResidualMatrix(pivot_row, pivot_col);
+}
+
+// ---------------------------------------------------------------------------
+// LuFactorization (lu_factorization.cc)
+void LuFactorization::Clear() {
+  lower_.Reset(0, 0);
+  upper_.Reset(0, 0);
+  transpose_upper_.Reset(0, 0);
+  transpose_lower_.Reset(0, 0);
+  is_identity_factorization_ = true;
+  col_perm_.clear();
+  row_perm_.clear();
+  inverse_row_perm_.clear();
+  inverse_col_perm_.clear();
+}
+
+namespace {
+void PopulateFromInverse(const std::vector<int>& inverse, std::vector<int>* out) {
+  out->assign(inverse.size(), 0);
+  for (size_t i = 0; i < inverse.size(); ++i) (*out)[inverse[i]] = static_cast<int>(i);
+}
+}  // namespace
+
+Status LuFactorization::ComputeFactorization(const CompactSparseMatrixView& b) {
+  Clear();
+  if (b.num_rows() != b.num_cols()) {
+    return Status(Status::ERROR_LU, "Not a square matrix!!");
+  }
+  MILP_RETURN_IF_ERROR(
+      markowitz_.ComputeLU(b, &row_perm_, &col_perm_, &lower_, &upper_));
+  PopulateFromInverse(col_perm_, &inverse_col_perm_);
+  PopulateFromInverse(row_perm_, &inverse_row_perm_);
+  ComputeTransposeUpper();
+  ComputeTransposeLower();
+  is_identity_factorization_ = false;
+  return Status::OK();
+}
+
+std::vector<int> LuFactorization::ComputeInitialBasis(
+    const CompactSparseMatrix& matrix, const std::vector<int>& candidates) {
+  CompactSparseMatrixView view{&matrix, &candidates};
+  (void)markowitz_.ComputeRowAndColumnPermutation(view, &row_perm_, &col_perm_);
+  std::vector<int> basis;
+  for (int row = 0; row < matrix.num_rows(); ++row) {
+    if (row_perm_[row] == kInvalidRow) {
+      basis.push_back(matrix.num_cols() + (row - matrix.num_rows()));
+    }
+  }
+  for (size_t i = 0; i < col_perm_.size(); ++i) {
+    if (col_perm_[i] != kInvalidCol) basis.push_back(candidates[i]);
+  }
+  return basis;
+}
+
+namespace {
+Fractional ComputeSquaredNormAndResetToZero(const std::vector<int>& nz,
+                                            std::vector<Fractional>* column) {
+  Fractional sum = 0.0;
+  if (nz.empty()) {
+    sum = SquaredNorm(*column);
+    column->clear();
+  } else {
+    for (const int row : nz) {
+      sum += Square((*column)[row]);
+      (*column)[row] = 0.0;
+    }
+  }
+  return sum;
+}
+}  // namespace
+
+// lu_factorization.cc:128-156
+Fractional LuFactorization::RightSolveSquaredNorm(const ColumnView& a) const {
+  if (is_identity_factorization_) return SquaredNorm(a);
+  non_zero_rows_.clear();
+  dense_zero_scratchpad_.resize(lower_.num_rows(), 0.0);
+  for (int64_t i = 0; i < a.n; ++i) {
+    const int permuted_row = row_perm_[a.rows[i]];
+    dense_zero_scratchpad_[permuted_row] = a.coefs[i];
+    non_zero_rows_.push_back(permuted_row);
+  }
+  lower_.ComputeRowsToConsiderInSortedOrder(&non_zero_rows_);
+  if (non_zero_rows_.empty()) {
+    lower_.LowerSolve(&dense_zero_scratchpad_);
+  } else {
+    lower_.HyperSparseSolve(&dense_zero_scratchpad_, &non_zero_rows_);
+    upper_.ComputeRowsToConsiderInSortedOrder(&non_zero_rows_);
+  }
+  if (non_zero_rows_.empty()) {
+    upper_.UpperSolve(&dense_zero_scratchpad_);
+  } else {
+    upper_.HyperSparseSolveWithReversedNonZeros(&dense_zero_scratchpad_,
+                                                &non_zero_rows_);
+  }
+  return ComputeSquaredNormAndResetToZero(non_zero_rows_, &dense_zero_scratchpad_);
+}
+
+// lu_factorization.cc:158-186
+Fractional LuFactorization::DualEdgeSquaredNorm(int row) const {
+  if (is_identity_factorization_) return 1.0;
+  const int permuted_row = col_perm_.empty() ? row : col_perm_[row];
+  non_zero_rows_.clear();
+  dense_zero_scratchpad_.resize(lower_.num_rows(), 0.0);
+  dense_zero_scratchpad_[permuted_row] = 1.0;
+  non_zero_rows_.push_back(permuted_row);
+  transpose_upper_.ComputeRowsToConsiderInSortedOrder(&non_zero_rows_);
+  if (non_zero_rows_.empty()) {
+    transpose_upper_.LowerSolveStartingAt(permuted_row, &dense_zero_scratchpad_);
+  } else {
+    transpose_upper_.HyperSparseSolve(&dense_zero_scratchpad_, &non_zero_rows_);
+    transpose_lower_.ComputeRowsToConsiderInSortedOrder(&non_zero_rows_);
+  }
+  if (non_zero_rows_.empty()) {
+    transpose_lower_.UpperSolve(&dense_zero_scratchpad_);
+  } else {
+    transpose_lower_.HyperSparseSolveWithReversedNonZeros(&dense_zero_scratchpad_,
+                                                          &non_zero_rows_);
+  }
+  return ComputeSquaredNormAndResetToZero(non_zero_rows_, &dense_zero_scratchpad_);
+}
+
+// lu_factorization.cc:200-212
+void LuFactorization::RightSolveLWithPermutedInput(const std::vector<Fractional>& /*a*/,
+                                                   ScatteredVector* x) const {
+  if (!is_identity_factorization_) {
+    lower_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
+    if (x->non_zeros.empty()) {
+      lower_.LowerSolve(&x->values);
+    } else {
+      lower_.HyperSparseSolve(&x->values, &x->non_zeros);
+    }
+  }
+}
+
+// lu_factorization.cc:214-243
+template <typename Column>
+void LuFactorization::RightSolveLInternal(const Column& b, ScatteredVector* x) const {
+  int first_column_to_consider = x->size();
+  const int limit = lower_.GetFirstNonIdentityColumn();
+  for (size_t k = 0; k < b.rows_size(); ++k) {
+    const int permuted_row = row_perm_[b.row(k)];
+    (*x)[permuted_row] = b.coef(k);
+    x->non_zeros.push_back(permuted_row);
+    const int col = permuted_row;
+    if (col < limit || lower_.ColumnIsDiagonalOnly(col)) continue;
+    first_column_to_consider = std::min(first_column_to_consider, col);
+  }
+  lower_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
+  x->non_zeros_are_sorted = true;
+  if (x->non_zeros.empty()) {
+    lower_.LowerSolveStartingAt(first_column_to_consider, &x->values);
+  } else {
+    lower_.HyperSparseSolve(&x->values, &x->non_zeros);
+  }
+}
+
+namespace {
+struct ColumnViewAdapter {
+  const ColumnView& c;
+  size_t rows_size() const { return static_cast<size_t>(c.n); }
+  int row(size_t k) const { return c.rows[k]; }
+  Fractional coef(size_t k) const { return c.coefs[k]; }
+};
+// Iteration over a ScatteredVector = iteration over its non-zero list.
+struct ScatteredAdapter {
+  const ScatteredVector& v;
+  size_t rows_size() const { return v.non_zeros.size(); }
+  int row(size_t k) const { return v.non_zeros[k]; }
+  Fractional coef(size_t k) const { return v.values[v.non_zeros[k]]; }
+};
+}  // namespace
+
+// lu_factorization.cc:245-258
+void LuFactorization::RightSolveLForColumnView(const ColumnView& b,
+                                               ScatteredVector* x) const {
+  x->non_zeros.clear();
+  if (is_identity_factorization_) {
+    for (int64_t i = 0; i < b.n; ++i) {
+      (*x)[b.rows[i]] = b.coefs[i];
+      x->non_zeros.push_back(b.rows[i]);
+    }
+    return;
+  }
+  RightSolveLInternal(ColumnViewAdapter{b}, x);
+}
+
+// lu_factorization.cc:260-277
+void LuFactorization::RightSolveLWithNonZeros(ScatteredVector* x) const {
+  if (is_identity_factorization_) return;
+  if (x->non_zeros.empty()) {
+    // PermuteWithScratchpad (lp_utils.h:240-257)
+    dense_zero_scratchpad_.assign(x->values.size(), 0.0);
+    dense_zero_scratchpad_.swap(x->values);
+    x->values.assign(dense_zero_scratchpad_.size(), 0.0);
+    for (size_t i = 0; i < dense_zero_scratchpad_.size(); ++i) {
+      const Fractional v = dense_zero_scratchpad_[i];
+      if (v != 0.0) x->values[row_perm_[i]] = v;
+    }
+    dense_zero_scratchpad_.assign(x->values.size(), 0.0);
+    lower_.LowerSolve(&x->values);
+    return;
+  }
+  // PermuteWithKnownNonZeros (lp_utils.h:262-277)
+  dense_zero_scratchpad_.assign(x->values.size(), 0.0);
+  dense_zero_scratchpad_.swap(x->values);
+  x->values.assign(dense_zero_scratchpad_.size(), 0.0);
+  for (int& ref : x->non_zeros) {
+    const Fractional v = dense_zero_scratchpad_[ref];
+    dense_zero_scratchpad_[ref] = 0.0;
+    const int p = row_perm_[ref];
+    x->values[p] = v;
+    ref = p;
+  }
+  lower_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
+  x->non_zeros_are_sorted = true;
+  if (x->non_zeros.empty()) {
+    lower_.LowerSolve(&x->values);
+  } else {
+    lower_.HyperSparseSolve(&x->values, &x->non_zeros);
+  }
+}
+
+// lu_factorization.cc:279-296
+void LuFactorization::RightSolveLForScatteredColumn(const ScatteredVector& b,
+                                                    ScatteredVector* x) const {
+  x->non_zeros.clear();
+  if (is_identity_factorization_) {
+    *x = b;
+    return;
+  }
+  if (b.non_zeros.empty()) {
+    *x = b;
+    RightSolveLWithNonZeros(x);
+    return;
+  }
+  RightSolveLInternal(ScatteredAdapter{b}, x);
+}
+
+// lu_factorization.cc:298-312
+void LuFactorization::LeftSolveUWithNonZeros(ScatteredVector* y) const {
+  if (is_identity_factorization_) return;
+  transpose_upper_.ComputeRowsToConsiderInSortedOrder(&y->non_zeros);
+  y->non_zeros_are_sorted = true;
+  if (y->non_zeros.empty()) {
+    upper_.TransposeUpperSolve(&y->values);
+  } else {
+    upper_.TransposeHyperSparseSolve(&y->values, &y->non_zeros);
+  }
+}
+
+// lu_factorization.cc:314-331
+void LuFactorization::RightSolveUWithNonZeros(ScatteredVector* x) const {
+  if (is_identity_factorization_) return;
+  upper_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
+  x->non_zeros_are_sorted = true;
+  if (x->non_zeros.empty()) {
+    transpose_upper_.TransposeLowerSolve(&x->values);
+  } else {
+    transpose_upper_.TransposeHyperSparseSolveWithReversedNonZeros(
+        &x->values, &x->non_zeros);
+  }
+}
+
+// lu_factorization.cc:333-399
+bool LuFactorization::LeftSolveLWithNonZeros(
+    ScatteredVector* y, ScatteredVector* result_before_permutation) const {
+  if (is_identity_factorization_) return false;
+  std::vector<Fractional>* x = &y->values;
+  std::vector<int>* nz = &y->non_zeros;
+  transpose_lower_.ComputeRowsToConsiderInSortedOrder(nz);
+  y->non_zeros_are_sorted = true;
+  if (nz->empty()) {
+    lower_.TransposeLowerSolve(x);
+  } else {
+    lower_.TransposeHyperSparseSolveWithReversedNonZeros(x, nz);
+  }
+  if (result_before_permutation == nullptr) {
+    if (nz->empty()) {
+      dense_zero_scratchpad_.assign(x->size(), 0.0);
+      dense_zero_scratchpad_.swap(*x);
+      x->assign(dense_zero_scratchpad_.size(), 0.0);
+      for (size_t i = 0; i < dense_zero_scratchpad_.size(); ++i) {
+        const Fractional v = dense_zero_scratchpad_[i];
+        if (v != 0.0) (*x)[inverse_row_perm_[i]] = v;
+      }
+      dense_zero_scratchpad_.assign(x->size(), 0.0);
+    } else {
+      dense_zero_scratchpad_.assign(x->size(), 0.0);
+      dense_zero_scratchpad_.swap(*x);
+      x->assign(dense_zero_scratchpad_.size(), 0.0);
+      for (int& ref : *nz) {
+        const Fractional v = dense_zero_scratchpad_[ref];
+        dense_zero_scratchpad_[ref] = 0.0;
+        const int p = inverse_row_perm_[ref];
+        (*x)[p] = v;
+        ref = p;
+      }
+    }
+    return false;
+  }
+  // ClearAndResizeVectorWithNonZeros(x->size(), result_before_permutation)
+  ClearAndResizeVectorWithNonZeros(static_cast<int>(x->size()),
+                                   result_before_permutation);
+  x->swap(result_before_permutation->values);
+  if (nz->empty()) {
+    for (size_t row = 0; row < inverse_row_perm_.size(); ++row) {
+      const Fractional value = result_before_permutation->values[row];
+      if (value != 0.0) (*x)[inverse_row_perm_[row]] = value;
+    }
+  } else {
+    nz->swap(result_before_permutation->non_zeros);
+    nz->reserve(result_before_permutation->non_zeros.size());
+    for (const int row : result_before_permutation->non_zeros) {
+      const Fractional value = result_before_permutation->values[row];
+      const int permuted_row = inverse_row_perm_[row];
+      (*x)[permuted_row] = value;
+      nz->push_back(permuted_row);
+    }
+    y->non_zeros_are_sorted = false;
+  }
+  return true;
+}
+
+// lu_factorization.cc:405-436
+int LuFactorization::LeftSolveUForUnitRow(int col, ScatteredVector* y) const {
+  if (is_identity_factorization_) {
+    (*y)[col] = 1.0;
+    y->non_zeros.push_back(col);
+    return col;
+  }
+  const int permuted_col = col_perm_.empty() ? col : col_perm_[col];
+  (*y)[permuted_col] = 1.0;
+  y->non_zeros.push_back(permuted_col);
+  if (transpose_upper_.ColumnIsDiagonalOnly(permuted_col)) {
+    (*y)[permuted_col] /= transpose_upper_.GetDiagonalCoefficient(permuted_col);
+  } else {
+    transpose_upper_.ComputeRowsToConsiderInSortedOrder(&y->non_zeros);
+    y->non_zeros_are_sorted = true;
+    if (y->non_zeros.empty()) {
+      transpose_upper_.LowerSolveStartingAt(permuted_col, &y->values);
+    } else {
+      transpose_upper_.HyperSparseSolve(&y->values, &y->non_zeros);
+    }
+  }
+  return permuted_col;
+}
+
+// lu_factorization.cc:438-447
+const SparseColumn& LuFactorization::GetColumnOfU(int col) const {
+  if (is_identity_factorization_) {
+    column_of_upper_.Clear();
+    column_of_upper_.SetCoefficient(col, 1.0);
+    return column_of_upper_;
+  }
+  upper_.CopyColumnToSparseColumn(col_perm_.empty() ? col : col_perm_[col],
+                                  &column_of_upper_);
+  return column_of_upper_;
+}
+
+// ---------------------------------------------------------------------------
+// BasisFactorization (basis_representation.cc:176-627)
+void BasisFactorization::Clear() {
+  num_updates_ = 0;
+  tau_computation_can_be_optimized_ = false;
+  lu_factorization_.Clear();
+  rank_one_factorization_.Clear();
+  storage_.Reset(compact_matrix_.num_rows());
+  right_storage_.Reset(compact_matrix_.num_rows());
+  left_pool_mapping_.clear();
+  right_pool_mapping_.clear();
+}
+
+Status BasisFactorization::Initialize() {
+  Clear();
+  if (IsIdentityBasis()) return Status::OK();
+  return ComputeFactorization();
+}
+
+std::vector<int> BasisFactorization::ComputeInitialBasis(
+    const std::vector<int>& candidates) {
+  std::vector<int> basis =
+      lu_factorization_.ComputeInitialBasis(compact_matrix_, candidates);
+  deterministic_time_ += lu_factorization_.DeterministicTimeOfLastFactorization();
+  return basis;
+}
+
+Status BasisFactorization::Refactorize() {
+  if (IsRefactorized()) return Status::OK();
+  return ForceRefactorization();
+}
+
+Status BasisFactorization::ForceRefactorization() {
+  Clear();
+  return ComputeFactorization();
+}
+
+Status BasisFactorization::ComputeFactorization() {
+  CompactSparseMatrixView basis_matrix{&compact_matrix_, &basis_};
+  const Status status = lu_factorization_.ComputeFactorization(basis_matrix);
+  last_factorization_deterministic_time_ =
+      lu_factorization_.DeterministicTimeOfLastFactorization();
+  deterministic_time_ += last_factorization_deterministic_time_;
+  rank_one_factorization_.ResetDeterministicTime();
+  return status;
+}
+
+// basis_representation.cc:258-302
+Status BasisFactorization::MiddleProductFormUpdate(int entering_col,
+                                                   int leaving_variable_row) {
+  const int right_index = entering_col < static_cast<int>(right_pool_mapping_.size())
+                              ? right_pool_mapping_[entering_col]
+                              : kInvalidCol;
+  const int left_index =
+      leaving_variable_row < static_cast<int>(left_pool_mapping_.size())
+          ? left_pool_mapping_[leaving_variable_row]
+          : kInvalidCol;
+  if (right_index == kInvalidCol || left_index == kInvalidCol) {
+    return ForceRefactorization();
+  }
+  scratchpad_.resize(right_storage_.num_rows(), 0.0);
+  const ColumnView rc = right_storage_.column(right_index);
+  for (int64_t i = 0; i < rc.n; ++i) {
+    scratchpad_[rc.rows[i]] = rc.coefs[i];
+    scratchpad_non_zeros_.push_back(rc.rows[i]);
+  }
+  const SparseColumn& column_of_u =
+      lu_factorization_.GetColumnOfU(leaving_variable_row);
+  for (int64_t k = 0; k < column_of_u.num_entries(); ++k) {
+    scratchpad_[column_of_u.rows[k]] -= column_of_u.coefs[k];
+    scratchpad_non_zeros_.push_back(column_of_u.rows[k]);
+  }
+  const Fractional scalar_product =
+      storage_.ColumnScalarProduct(left_index, scratchpad_.data());
+  const int u_index =
+      storage_.AddAndClearColumnWithNonZeros(&scratchpad_, &scratchpad_non_zeros_);
+  RankOneUpdateElementaryMatrix m(&storage_, u_index, left_index, scalar_product);
+  if (m.IsSingular()) {
+    return Status(Status::ERROR_LU, "Degenerate rank-one update.");
+  }
+  rank_one_factorization_.Update(m);
+  return Status::OK();
+}
+
+// basis_representation.cc:304-340
+Status BasisFactorization::Update(int entering_col, int leaving_variable_row,
+                                  const ScatteredVector& /*direction*/) {
+  if (num_updates_ >= max_num_updates_) {
+    if (!dynamic_period_) return ForceRefactorization();
+    if (last_factorization_deterministic_time_ <
+        rank_one_factorization_.DeterministicTimeSinceLastReset()) {
+      return ForceRefactorization();
+    }
+  }
+  ++num_updates_;
+  MILP_RETURN_IF_ERROR(MiddleProductFormUpdate(entering_col, leaving_variable_row));
+  tau_computation_can_be_optimized_ = false;
+  return Status::OK();
+}
+
+// basis_representation.cc:342-356
+void BasisFactorization::LeftSolve(ScatteredVector* y) const {
+  lu_factorization_.LeftSolveUWithNonZeros(y);
+  rank_one_factorization_.LeftSolveWithNonZeros(y);
+  lu_factorization_.LeftSolveLWithNonZeros(y, nullptr);
+  y->SortNonZerosIfNeeded();
+  BumpDeterministicTimeForSolve(static_cast<int64_t>(y->NumNonZerosEstimate()));
+}
+
+// basis_representation.cc:358-372
+void BasisFactorization::RightSolve(ScatteredVector* d) const {
+  lu_factorization_.RightSolveLWithNonZeros(d);
+  rank_one_factorization_.RightSolveWithNonZeros(d);
+  lu_factorization_.RightSolveUWithNonZeros(d);
+  d->SortNonZerosIfNeeded();
+  BumpDeterministicTimeForSolve(static_cast<int64_t>(d->NumNonZerosEstimate()));
+}
+
+// basis_representation.cc:374-398
+const std::vector<Fractional>& BasisFactorization::RightSolveForTau(
+    const ScatteredVector& a) const {
+  if (tau_computation_can_be_optimized_) {
+    tau_computation_can_be_optimized_ = false;
+    lu_factorization_.RightSolveLWithPermutedInput(a.values, &tau_);
+  } else {
+    ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), &tau_);
+    lu_factorization_.RightSolveLForScatteredColumn(a, &tau_);
+  }
+  rank_one_factorization_.RightSolveWithNonZeros(&tau_);
+  lu_factorization_.RightSolveUWithNonZeros(&tau_);
+  tau_is_computed_ = true;
+  BumpDeterministicTimeForSolve(static_cast<int64_t>(tau_.NumNonZerosEstimate()));
+  return tau_.values;
+}
+
+// basis_representation.cc:400-453
+void BasisFactorization::LeftSolveForUnitRow(int j, ScatteredVector* y) const {
+  ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), y);
+  if (j >= static_cast<int>(left_pool_mapping_.size())) {
+    left_pool_mapping_.resize(j + 1, kInvalidCol);
+  }
+  if (left_pool_mapping_[j] == kInvalidCol) {
+    const int start = lu_factorization_.LeftSolveUForUnitRow(j, y);
+    if (y->non_zeros.empty()) {
+      left_pool_mapping_[j] = storage_.AddDenseColumnPrefix(y->values, start);
+    } else {
+      left_pool_mapping_[j] = storage_.AddDenseColumnWithNonZeros(y->values, y->non_zeros);
+    }
+  } else {
+    storage_.ColumnCopyToClearedDenseColumnWithNonZeros(left_pool_mapping_[j],
+                                                        &y->values, &y->non_zeros);
+  }
+  rank_one_factorization_.LeftSolveWithNonZeros(y);
+  if (tau_is_computed_) {
+    tau_computation_can_be_optimized_ =
+        lu_factorization_.LeftSolveLWithNonZeros(y, &tau_);
+  } else {
+    tau_computation_can_be_optimized_ = false;
+    lu_factorization_.LeftSolveLWithNonZeros(y, nullptr);
+  }
+  tau_is_computed_ = false;
+  y->SortNonZerosIfNeeded();
+  BumpDeterministicTimeForSolve(static_cast<int64_t>(y->NumNonZerosEstimate()));
+}
+
+// basis_representation.cc:455-466
+void BasisFactorization::TemporaryLeftSolveForUnitRow(int j, ScatteredVector* y) const {
+  ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), y);
+  lu_factorization_.LeftSolveUForUnitRow(j, y);
+  lu_factorization_.LeftSolveLWithNonZeros(y, nullptr);
+  y->SortNonZerosIfNeeded();
+  BumpDeterministicTimeForSolve(static_cast<int64_t>(y->NumNonZerosEstimate()));
+}
+
+// basis_representation.cc:468-501
+void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d) const {
+  ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), d);
+  lu_factorization_.RightSolveLForColumnView(compact_matrix_.column(col), d);
+  rank_one_factorization_.RightSolveWithNonZeros(d);
+  if (col >= static_cast<int>(right_pool_mapping_.size())) {
+    right_pool_mapping_.resize(col + 1, kInvalidCol);
+  }
+  if (d->non_zeros.empty()) {
+    right_pool_mapping_[col] = right_storage_.AddDenseColumn(d->values);
+  } else {
+    std::sort(d->non_zeros.begin(), d->non_zeros.end());
+    right_pool_mapping_[col] =
+        right_storage_.AddDenseColumnWithNonZeros(d->values, d->non_zeros);
+  }
+  lu_factorization_.RightSolveUWithNonZeros(d);
+  d->SortNonZerosIfNeeded();
+  BumpDeterministicTimeForSolve(static_cast<int64_t>(d->NumNonZerosEstimate()));
+}
+
+Fractional BasisFactorization::RightSolveSquaredNorm(const ColumnView& a) const {
+  BumpDeterministicTimeForSolve(a.n);
+  return lu_factorization_.RightSolveSquaredNorm(a);
+}
+
+Fractional BasisFactorization::DualEdgeSquaredNorm(int row) const {
+  BumpDeterministicTimeForSolve(1);
+  return lu_factorization_.DualEdgeSquaredNorm(row);
+}
+
+// basis_representation.cc:520-531
+bool BasisFactorization::IsIdentityBasis() const {
+  const int num_rows = compact_matrix_.num_rows();
+  for (int row = 0; row < num_rows; ++row) {
+    const int col = basis_[row];
+    const ColumnView c = compact_matrix_.column(col);
+    if (c.n != 1) return false;
+    if (c.rows[0] != row || c.coefs[0] != 1.0) return false;
+  }
+  return true;
+}
+
+// basis_representation.cc:595-601
+Fractional BasisFactorization::ComputeInfinityNormConditionNumberUpperBound() const {
+  if (IsIdentityBasis()) return 1.0;
+  BumpDeterministicTimeForSolve(compact_matrix_.num_rows());
+  CompactSparseMatrixView basis_matrix{&compact_matrix_, &basis_};
+  return basis_matrix.ComputeInfinityNorm() *
+         lu_factorization_.ComputeInverseInfinityNormUpperBound();
+}
+
+// basis_representation.cc:607-624
+void BasisFactorization::BumpDeterministicTimeForSolve(int64_t num_entries) const {
+  if (compact_matrix_.num_rows() == 0) return;
+  const double density = static_cast<double>(num_entries) /
+                         static_cast<double>(compact_matrix_.num_rows());
+  deterministic_time_ +=
+      density * DeterministicTimeForFpOperations(lu_factorization_.NumberOfEntries()) +
+      DeterministicTimeForFpOperations(rank_one_factorization_.num_entries());
+}
+
+}  // namespace milp

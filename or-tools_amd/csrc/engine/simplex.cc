@@ -1,0 +1,3954 @@
+// MI355X revised-simplex engine: the host-side state machine of
+// glop::RevisedSimplex (OR-Tools 9.7, ortools/glop/revised_simplex.cc and its
+// helper classes), with every O(nnz(A)) pass executed by the HIP kernels of
+// csrc/kernels through DeviceLp:
+//   UpdateRow::ComputeUpdates*          (update_row.cc:196-306)  -> device
+//   PrimalEdgeNorms::UpdateEdgeSquaredNorms dots (primal_edge_norms.cc:208-258)
+//   ReducedCosts::ComputeReducedCosts   (reduced_costs.cc:352-423) -> device
+//   ReducedCosts::ComputeMaximumDualResidual (reduced_costs.cc:96-110)
+//   PrimalEdgeNorms::ComputeEdgeSquaredNorms, identity basis (:147-161)
+//   VariableValues residual / basic-value SpMVs (variable_values.cc:101-131)
+// The kernels reproduce the host loops' floating-point order, so the pivot
+// sequence (basis, statuses, iteration count) is the one Glop's algorithm
+// produces. Basis factorization and FTRAN/BTRAN stay on the host in round 1.
+#include "simplex.h"
+
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <queue>
+#include <string>
+
+#include "../../../include/mi_lp.h"
+#include "device_lp.h"
+
+namespace milp {
+
+// ---------------------------------------------------------------------------
+// DynamicMaximum (pricing.h:152-345)
+int DynamicMaximum::RandomizeIfManyChoices(int best) {
+  if (equivalent_choices_.empty()) return best;
+  equivalent_choices_.push_back(best);
+  return equivalent_choices_[UniformInt(*random_,
+                                        static_cast<int>(equivalent_choices_.size()) - 1)];
+}
+
+int DynamicMaximum::GetMaximum() {
+  Fractional best_value = -kInfinity;
+  int best_position = -1;
+  equivalent_choices_.clear();
+  if (!tops_.empty()) {
+    int new_size = 0;
+    for (size_t k = 0, n = tops_.size(); k < n; ++k) {
+      const HeapElement e = tops_[k];
+      if (!is_candidate_[e.index]) continue;
+      if (values_[e.index] != e.value) continue;
+      tops_[new_size++] = e;
+      if (e.value >= best_value) {
+        if (e.value == best_value) {
+          equivalent_choices_.push_back(e.index);
+          continue;
+        }
+        equivalent_choices_.clear();
+        best_value = e.value;
+        best_position = e.index;
+      }
+    }
+    tops_.resize(new_size);
+    if (new_size != 0) return RandomizeIfManyChoices(best_position);
+  }
+  threshold_ = -kInfinity;
+  is_candidate_.ForEach([&](int position) {
+    const Fractional value = values_[position];
+    if (value < threshold_) return;
+    UpdateTopK(position, value);
+    if (value >= best_value) {
+      if (value == best_value) {
+        equivalent_choices_.push_back(position);
+        return;
+      }
+      equivalent_choices_.clear();
+      best_value = value;
+      best_position = position;
+    }
+  });
+  return RandomizeIfManyChoices(best_position);
+}
+
+void DynamicMaximum::UpdateTopK(int position, Fractional value) {
+  constexpr int k = 31;
+  if (static_cast<int>(tops_.size()) < k) {
+    tops_.push_back(HeapElement{position, value});
+    if (static_cast<int>(tops_.size()) == k) {
+      std::make_heap(tops_.begin(), tops_.end(), HeapLess());
+      threshold_ = tops_[0].value;
+    }
+    return;
+  }
+  if (value == tops_[0].value) {
+    if (AbslBernoulli(*random_, 0.5)) tops_[0].index = position;
+    return;
+  }
+  int i = 0;
+  constexpr int limit = k / 2;
+  for (; i < limit;) {
+    const int left_child = 2 * i + 1;
+    const int right_child = left_child + 1;
+    const Fractional l_value = tops_[left_child].value;
+    const Fractional r_value = tops_[right_child].value;
+    if (l_value > r_value) {
+      if (value <= r_value) break;
+      tops_[i] = tops_[right_child];
+      i = right_child;
+    } else {
+      if (value <= l_value) break;
+      tops_[i] = tops_[left_child];
+      i = left_child;
+    }
+  }
+  tops_[i] = HeapElement{position, value};
+  threshold_ = tops_[0].value;
+}
+
+// ---------------------------------------------------------------------------
+// VariablesInfo (variables_info.cc:14-476)
+bool VariablesInfo::LoadBoundsAndReturnTrueIfUnchanged(
+    const std::vector<double>& vlb, const std::vector<double>& vub,
+    const std::vector<double>& clb, const std::vector<double>& cub) {
+  const int num_cols = matrix_.num_cols();
+  const int num_variables = static_cast<int>(vub.size());
+  const int num_rows = static_cast<int>(clb.size());
+  bool is_unchanged = (num_cols == static_cast<int>(lower_bounds_.size()));
+  lower_bounds_.resize(num_cols, 0.0);
+  upper_bounds_.resize(num_cols, 0.0);
+  variable_type_.resize(num_cols, VariableType::FIXED_VARIABLE);
+  for (int col = 0; col < num_variables; ++col) {
+    if (lower_bounds_[col] != vlb[col] || upper_bounds_[col] != vub[col]) {
+      lower_bounds_[col] = vlb[col];
+      upper_bounds_[col] = vub[col];
+      is_unchanged = false;
+      variable_type_[col] = ComputeVariableType(col);
+    }
+  }
+  for (int row = 0; row < num_rows; ++row) {
+    const int col = num_variables + row;
+    if (lower_bounds_[col] != -cub[row] || upper_bounds_[col] != -clb[row]) {
+      lower_bounds_[col] = -cub[row];
+      upper_bounds_[col] = -clb[row];
+      is_unchanged = false;
+      variable_type_[col] = ComputeVariableType(col);
+    }
+  }
+  return is_unchanged;
+}
+
+void VariablesInfo::ResetStatusInfo() {
+  const int num_cols = matrix_.num_cols();
+  variable_status_.resize(num_cols, VariableStatus::FREE);
+  can_increase_.ClearAndResize(num_cols);
+  can_decrease_.ClearAndResize(num_cols);
+  is_basic_.ClearAndResize(num_cols);
+  not_basic_.ClearAndResize(num_cols);
+  non_basic_boxed_variables_.ClearAndResize(num_cols);
+  boxed_variables_are_relevant_ = true;
+  num_entries_in_relevant_columns_ = 0;
+  relevance_.ClearAndResize(num_cols);
+}
+
+void VariablesInfo::InitializeFromBasisState(int first_slack_col, int num_new_cols,
+                                             const std::vector<VariableStatus>& state) {
+  ResetStatusInfo();
+  const int num_cols = static_cast<int>(lower_bounds_.size());
+  const int first_new_col = first_slack_col - num_new_cols;
+  const int ssize = static_cast<int>(state.size());
+  for (int col = 0; col < num_cols; ++col) {
+    VariableStatus status;
+    if (col < first_new_col && col < ssize) {
+      status = state[col];
+    } else if (col >= first_slack_col && col - num_new_cols < ssize) {
+      status = state[col - num_new_cols];
+    } else {
+      UpdateToNonBasicStatus(col, DefaultVariableStatus(col));
+      continue;
+    }
+    switch (status) {
+      case VariableStatus::BASIC:
+        variable_status_[col] = VariableStatus::BASIC;
+        is_basic_.Set(col, true);
+        break;
+      case VariableStatus::AT_LOWER_BOUND:
+        if (lower_bounds_[col] == upper_bounds_[col]) {
+          UpdateToNonBasicStatus(col, VariableStatus::FIXED_VALUE);
+        } else {
+          UpdateToNonBasicStatus(col, lower_bounds_[col] == -kInfinity
+                                          ? DefaultVariableStatus(col)
+                                          : status);
+        }
+        break;
+      case VariableStatus::AT_UPPER_BOUND:
+        if (lower_bounds_[col] == upper_bounds_[col]) {
+          UpdateToNonBasicStatus(col, VariableStatus::FIXED_VALUE);
+        } else {
+          UpdateToNonBasicStatus(col, upper_bounds_[col] == kInfinity
+                                          ? DefaultVariableStatus(col)
+                                          : status);
+        }
+        break;
+      default:
+        UpdateToNonBasicStatus(col, DefaultVariableStatus(col));
+    }
+  }
+}
+
+int VariablesInfo::ChangeUnusedBasicVariablesToFree(const std::vector<int>& basis) {
+  const int num_cols = static_cast<int>(lower_bounds_.size());
+  is_basic_.ClearAndResize(num_cols);
+  for (const int col : basis) UpdateToBasicStatus(col);
+  int num_no_longer_in_basis = 0;
+  for (int col = 0; col < num_cols; ++col) {
+    if (!is_basic_[col] && variable_status_[col] == VariableStatus::BASIC) {
+      ++num_no_longer_in_basis;
+      if (variable_type_[col] == VariableType::FIXED_VARIABLE) {
+        UpdateToNonBasicStatus(col, VariableStatus::FIXED_VALUE);
+      } else {
+        UpdateToNonBasicStatus(col, VariableStatus::FREE);
+      }
+    }
+  }
+  return num_no_longer_in_basis;
+}
+
+int VariablesInfo::SnapFreeVariablesToBound(Fractional distance,
+                                            const std::vector<Fractional>& sv) {
+  int num_changes = 0;
+  const int num_cols = static_cast<int>(lower_bounds_.size());
+  for (int col = 0; col < num_cols; ++col) {
+    if (variable_status_[col] != VariableStatus::FREE) continue;
+    if (variable_type_[col] == VariableType::UNCONSTRAINED) continue;
+    const Fractional value = col < static_cast<int>(sv.size()) ? sv[col] : 0.0;
+    const Fractional diff_ub = upper_bounds_[col] - value;
+    const Fractional diff_lb = value - lower_bounds_[col];
+    if (diff_lb <= diff_ub) {
+      if (diff_lb <= distance) {
+        ++num_changes;
+        UpdateToNonBasicStatus(col, VariableStatus::AT_LOWER_BOUND);
+      }
+    } else {
+      if (diff_ub <= distance) {
+        ++num_changes;
+        UpdateToNonBasicStatus(col, VariableStatus::AT_UPPER_BOUND);
+      }
+    }
+  }
+  return num_changes;
+}
+
+void VariablesInfo::InitializeToDefaultStatus() {
+  ResetStatusInfo();
+  const int num_cols = static_cast<int>(lower_bounds_.size());
+  for (int col = 0; col < num_cols; ++col)
+    UpdateToNonBasicStatus(col, DefaultVariableStatus(col));
+}
+
+VariableStatus VariablesInfo::DefaultVariableStatus(int col) const {
+  if (lower_bounds_[col] == upper_bounds_[col]) return VariableStatus::FIXED_VALUE;
+  if (lower_bounds_[col] == -kInfinity && upper_bounds_[col] == kInfinity)
+    return VariableStatus::FREE;
+  return std::fabs(lower_bounds_[col]) <= std::fabs(upper_bounds_[col])
+             ? VariableStatus::AT_LOWER_BOUND
+             : VariableStatus::AT_UPPER_BOUND;
+}
+
+void VariablesInfo::MakeBoxedVariableRelevant(bool value) {
+  if (value == boxed_variables_are_relevant_) return;
+  boxed_variables_are_relevant_ = value;
+  const std::vector<int> boxed = non_basic_boxed_variables_.ToVector();
+  if (value) {
+    for (const int col : boxed)
+      SetRelevance(col, variable_type_[col] != VariableType::FIXED_VARIABLE);
+  } else {
+    for (const int col : boxed) SetRelevance(col, false);
+  }
+}
+
+void VariablesInfo::UpdateToBasicStatus(int col) {
+  if (in_dual_phase_one_) {
+    if (lower_bounds_[col] != 0.0) lower_bounds_[col] = -kInfinity;
+    if (upper_bounds_[col] != 0.0) upper_bounds_[col] = +kInfinity;
+    variable_type_[col] = ComputeVariableType(col);
+  }
+  variable_status_[col] = VariableStatus::BASIC;
+  is_basic_.Set(col, true);
+  not_basic_.Set(col, false);
+  can_increase_.Set(col, false);
+  can_decrease_.Set(col, false);
+  non_basic_boxed_variables_.Set(col, false);
+  SetRelevance(col, false);
+}
+
+void VariablesInfo::UpdateToNonBasicStatus(int col, VariableStatus status) {
+  variable_status_[col] = status;
+  is_basic_.Set(col, false);
+  not_basic_.Set(col, true);
+  can_increase_.Set(col, status == VariableStatus::AT_LOWER_BOUND ||
+                             status == VariableStatus::FREE);
+  can_decrease_.Set(col, status == VariableStatus::AT_UPPER_BOUND ||
+                             status == VariableStatus::FREE);
+  const bool boxed = variable_type_[col] == VariableType::UPPER_AND_LOWER_BOUNDED;
+  non_basic_boxed_variables_.Set(col, boxed);
+  const bool relevance = status != VariableStatus::FIXED_VALUE &&
+                         (boxed_variables_are_relevant_ || !boxed);
+  SetRelevance(col, relevance);
+}
+
+VariableType VariablesInfo::ComputeVariableType(int col) const {
+  if (lower_bounds_[col] == -kInfinity) {
+    if (upper_bounds_[col] == kInfinity) return VariableType::UNCONSTRAINED;
+    return VariableType::UPPER_BOUNDED;
+  } else if (upper_bounds_[col] == kInfinity) {
+    return VariableType::LOWER_BOUNDED;
+  } else if (lower_bounds_[col] == upper_bounds_[col]) {
+    return VariableType::FIXED_VARIABLE;
+  }
+  return VariableType::UPPER_AND_LOWER_BOUNDED;
+}
+
+void VariablesInfo::SetRelevance(int col, bool relevance) {
+  if (relevance_.IsSet(col) == relevance) return;
+  if (relevance) {
+    relevance_.Set(col);
+    num_entries_in_relevant_columns_ += matrix_.ColumnNumEntries(col);
+  } else {
+    relevance_.Clear(col);
+    num_entries_in_relevant_columns_ -= matrix_.ColumnNumEntries(col);
+  }
+}
+
+void VariablesInfo::UpdateStatusForNewType(int col) {
+  switch (variable_status_[col]) {
+    case VariableStatus::BASIC:
+      UpdateToBasicStatus(col);
+      break;
+    case VariableStatus::AT_LOWER_BOUND:
+      if (lower_bounds_[col] == upper_bounds_[col]) {
+        UpdateToNonBasicStatus(col, VariableStatus::FIXED_VALUE);
+      } else if (lower_bounds_[col] == -kInfinity) {
+        UpdateToNonBasicStatus(col, DefaultVariableStatus(col));
+      } else {
+        UpdateToNonBasicStatus(col, variable_status_[col]);
+      }
+      break;
+    case VariableStatus::AT_UPPER_BOUND:
+      if (lower_bounds_[col] == upper_bounds_[col]) {
+        UpdateToNonBasicStatus(col, VariableStatus::FIXED_VALUE);
+      } else if (upper_bounds_[col] == kInfinity) {
+        UpdateToNonBasicStatus(col, DefaultVariableStatus(col));
+      } else {
+        UpdateToNonBasicStatus(col, variable_status_[col]);
+      }
+      break;
+    default:
+      UpdateToNonBasicStatus(col, DefaultVariableStatus(col));
+  }
+}
+
+void VariablesInfo::TransformToDualPhaseIProblem(Fractional tol,
+                                                 const std::vector<Fractional>& rc) {
+  in_dual_phase_one_ = true;
+  saved_lower_bounds_ = lower_bounds_;
+  saved_upper_bounds_ = upper_bounds_;
+  const int num_cols = matrix_.num_cols();
+  for (int col = 0; col < num_cols; ++col) {
+    switch (variable_type_[col]) {
+      case VariableType::FIXED_VARIABLE:
+      case VariableType::UPPER_AND_LOWER_BOUNDED:
+        lower_bounds_[col] = 0.0;
+        upper_bounds_[col] = 0.0;
+        variable_type_[col] = VariableType::FIXED_VARIABLE;
+        break;
+      case VariableType::LOWER_BOUNDED:
+        lower_bounds_[col] = 0.0;
+        upper_bounds_[col] = 1.0;
+        variable_type_[col] = VariableType::UPPER_AND_LOWER_BOUNDED;
+        break;
+      case VariableType::UPPER_BOUNDED:
+        lower_bounds_[col] = -1.0;
+        upper_bounds_[col] = 0.0;
+        variable_type_[col] = VariableType::UPPER_AND_LOWER_BOUNDED;
+        break;
+      case VariableType::UNCONSTRAINED:
+        lower_bounds_[col] = -1000.0;
+        upper_bounds_[col] = 1000.0;
+        variable_type_[col] = VariableType::UPPER_AND_LOWER_BOUNDED;
+        break;
+    }
+    if (variable_type_[col] == VariableType::UPPER_AND_LOWER_BOUNDED) {
+      if (rc[col] > tol) {
+        variable_status_[col] = VariableStatus::AT_LOWER_BOUND;
+      } else if (rc[col] < -tol) {
+        variable_status_[col] = VariableStatus::AT_UPPER_BOUND;
+      }
+    }
+    UpdateStatusForNewType(col);
+  }
+}
+
+void VariablesInfo::EndDualPhaseI(Fractional tol, const std::vector<Fractional>& rc) {
+  in_dual_phase_one_ = false;
+  std::swap(saved_lower_bounds_, lower_bounds_);
+  std::swap(saved_upper_bounds_, upper_bounds_);
+  saved_lower_bounds_.clear();
+  saved_upper_bounds_.clear();
+  const int num_cols = matrix_.num_cols();
+  for (int col = 0; col < num_cols; ++col) {
+    variable_type_[col] = ComputeVariableType(col);
+    if (variable_type_[col] == VariableType::UPPER_AND_LOWER_BOUNDED) {
+      if (rc[col] > tol) {
+        variable_status_[col] = VariableStatus::AT_LOWER_BOUND;
+      } else if (rc[col] < -tol) {
+        variable_status_[col] = VariableStatus::AT_UPPER_BOUND;
+      }
+    }
+    UpdateStatusForNewType(col);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// DualEdgeNorms (dual_edge_norms.cc)
+class DualEdgeNorms {
+ public:
+  explicit DualEdgeNorms(const BasisFactorization& bf) : bf_(bf) {}
+  void SetParameters(const GlopParameters& p) { params_ = p; }
+  bool NeedsBasisRefactorization() const { return recompute_; }
+  void Clear() { recompute_ = true; }
+  void ResizeOnNewRows(int n) { norms_.resize(n, 1.0); }
+  const std::vector<Fractional>& GetEdgeSquaredNorms() {
+    if (recompute_) ComputeEdgeSquaredNorms();
+    return norms_;
+  }
+  void UpdateDataOnBasisPermutation(const std::vector<int>& col_perm) {
+    if (recompute_) return;
+    std::vector<Fractional> tmp(norms_.size());
+    for (size_t i = 0; i < col_perm.size(); ++i) tmp[col_perm[i]] = norms_[i];
+    norms_.swap(tmp);
+  }
+  // dual_edge_norms.cc:49-80
+  bool TestPrecision(int leaving_row, const ScatteredVector& rho) {
+    if (recompute_) return true;
+    const Fractional leaving_squared_norm = SquaredNorm(rho);
+    const Fractional old_squared_norm = norms_[leaving_row];
+    const Fractional acc = (std::sqrt(leaving_squared_norm) - std::sqrt(old_squared_norm)) /
+                           std::sqrt(leaving_squared_norm);
+    if (std::fabs(acc) > params_.recompute_edges_norm_threshold) recompute_ = true;
+    norms_[leaving_row] = leaving_squared_norm;
+    return old_squared_norm > 0.25 * leaving_squared_norm;
+  }
+  // dual_edge_norms.cc:82-118
+  void UpdateBeforeBasisPivot(int /*entering_col*/, int leaving_row,
+                              const ScatteredVector& direction,
+                              const ScatteredVector& rho) {
+    if (recompute_) return;
+    const std::vector<Fractional>& tau = bf_.RightSolveForTau(rho);
+    const Fractional pivot = direction[leaving_row];
+    const Fractional new_leaving_squared_norm = norms_[leaving_row] / Square(pivot);
+    for (const int row : direction.non_zeros) {
+      const Fractional c = direction[row];
+      norms_[row] += c * (c * new_leaving_squared_norm - 2.0 / pivot * tau[row]);
+      const Fractional kLowerBound = 1e-4;
+      if (norms_[row] < kLowerBound) {
+        if (row == leaving_row) continue;
+        norms_[row] = kLowerBound;
+      }
+    }
+    norms_[leaving_row] = new_leaving_squared_norm;
+  }
+
+ private:
+  void ComputeEdgeSquaredNorms() {  // dual_edge_norms.cc:120-132
+    const int num_rows = bf_.GetNumberOfRows();
+    norms_.resize(num_rows, 0.0);
+    for (int row = 0; row < num_rows; ++row) norms_[row] = bf_.DualEdgeSquaredNorm(row);
+    recompute_ = false;
+  }
+  const BasisFactorization& bf_;
+  GlopParameters params_;
+  bool recompute_ = true;
+  std::vector<Fractional> norms_;
+};
+
+// ---------------------------------------------------------------------------
+// UpdateRow (update_row.cc)
+class UpdateRow {
+ public:
+  UpdateRow(const CompactSparseMatrix& m, const CompactSparseMatrix& t,
+            const VariablesInfo& vi, const std::vector<int>& basis,
+            const BasisFactorization& bf, DeviceLp* dev)
+      : matrix_(m), transposed_matrix_(t), variables_info_(vi), basis_(basis), bf_(bf),
+        dev_(dev) {}
+  void SetParameters(const GlopParameters& p) { params_ = p; }
+  void Invalidate() {
+    left_inverse_computed_for_ = kInvalidRow;
+    update_row_computed_for_ = kInvalidRow;
+  }
+  const ScatteredVector& GetUnitRowLeftInverse() const { return rho_; }
+  const ScatteredVector& ComputeAndGetUnitRowLeftInverse(int leaving_row) {
+    Invalidate();
+    bf_.TemporaryLeftSolveForUnitRow(leaving_row, &rho_);
+    return rho_;
+  }
+  void ComputeUnitRowLeftInverse(int leaving_row) {
+    if (left_inverse_computed_for_ == leaving_row) return;
+    left_inverse_computed_for_ = leaving_row;
+    bf_.LeftSolveForUnitRow(leaving_row, &rho_);
+  }
+  void ComputeUpdateRow(int leaving_row);
+  bool IsComputedFor(int leaving_row) const {
+    return update_row_computed_for_ == leaving_row;
+  }
+  const std::vector<Fractional>& GetCoefficients() const { return coefficient_; }
+  const std::vector<int>& GetNonZeroPositions() const { return non_zero_position_list_; }
+  // Listed positions are mirrored on the host; any other position holds
+  // whatever the device update-row kernels left there (same write rules as
+  // the host loops), so it is read back from the device.
+  Fractional GetCoefficient(int col) const {
+    if (col < static_cast<int>(listed_.size()) && listed_[col]) return coefficient_[col];
+    return dev_->ReadCoefficient(col);
+  }
+  void ComputeFullUpdateRow(int leaving_row, std::vector<Fractional>* output) const;
+  double DeterministicTime() const {
+    return DeterministicTimeForFpOperations(num_operations_);
+  }
+  // Which algorithm ComputeUpdateRow() used last (exposed for parity tests).
+  int last_algorithm() const { return last_algorithm_; }
+
+ private:
+  void ComputeUpdatesRowWise();
+  void ComputeUpdatesRowWiseHypersparse();
+  void ComputeUpdatesColumnWise();
+  void ComputeUpdatesForSingleRow(int row_as_col);
+  void FetchFromDevice();
+
+  const CompactSparseMatrix& matrix_;
+  const CompactSparseMatrix& transposed_matrix_;
+  const VariablesInfo& variables_info_;
+  const std::vector<int>& basis_;
+  const BasisFactorization& bf_;
+  DeviceLp* dev_;
+  std::vector<char> listed_;
+  std::vector<Fractional> fetched_values_;
+  GlopParameters params_;
+  ScatteredVector rho_;
+  std::vector<int> rho_filtered_non_zeros_;
+  std::vector<int> non_zero_position_list_;
+  Bitset non_zero_position_set_;
+  std::vector<Fractional> coefficient_;
+  int left_inverse_computed_for_ = kInvalidRow;
+  int update_row_computed_for_ = kInvalidRow;
+  int64_t num_operations_ = 0;
+  int last_algorithm_ = -1;
+};
+
+// update_row.cc:77-166
+void UpdateRow::ComputeUpdateRow(int leaving_row) {
+  if (update_row_computed_for_ == leaving_row) return;
+  update_row_computed_for_ = leaving_row;
+  ComputeUnitRowLeftInverse(leaving_row);
+  if (params_.use_transposed_matrix) {
+    int64_t num_row_wise_entries = 0;
+    const Fractional drop_tolerance = params_.drop_tolerance;
+    rho_filtered_non_zeros_.clear();
+    if (rho_.non_zeros.empty()) {
+      const int size = rho_.size();
+      for (int col = 0; col < size; ++col) {
+        if (std::fabs(rho_.values[col]) > drop_tolerance) {
+          rho_filtered_non_zeros_.push_back(col);
+          num_row_wise_entries += transposed_matrix_.ColumnNumEntries(col);
+        }
+      }
+    } else {
+      for (const int col : rho_.non_zeros) {
+        if (std::fabs(rho_.values[col]) > drop_tolerance) {
+          rho_filtered_non_zeros_.push_back(col);
+          num_row_wise_entries += transposed_matrix_.ColumnNumEntries(col);
+        }
+      }
+    }
+    if (rho_filtered_non_zeros_.size() == 1) {
+      ComputeUpdatesForSingleRow(rho_filtered_non_zeros_.front());
+      num_operations_ += num_row_wise_entries;
+      last_algorithm_ = 0;
+      return;
+    }
+    const int64_t num_col_wise_entries = variables_info_.GetNumEntriesInRelevantColumns();
+    const double row_wise = static_cast<double>(num_row_wise_entries);
+    if (row_wise < 0.5 * static_cast<double>(num_col_wise_entries)) {
+      if (row_wise < 1.1 * static_cast<double>(matrix_.num_cols())) {
+        ComputeUpdatesRowWiseHypersparse();
+        num_operations_ += 5 * num_row_wise_entries + matrix_.num_cols() / 64;
+        last_algorithm_ = 1;
+      } else {
+        ComputeUpdatesRowWise();
+        num_operations_ += num_row_wise_entries + matrix_.num_rows();
+        last_algorithm_ = 2;
+      }
+    } else {
+      ComputeUpdatesColumnWise();
+      num_operations_ += num_col_wise_entries + matrix_.num_cols();
+      last_algorithm_ = 3;
+    }
+  } else {
+    ComputeUpdatesColumnWise();
+    num_operations_ +=
+        variables_info_.GetNumEntriesInRelevantColumns() + matrix_.num_cols();
+    last_algorithm_ = 3;
+  }
+}
+
+// The four update-row algorithms (update_row.cc:196-306) run on the GPU;
+// the host keeps Glop's algorithm choice (ComputeUpdateRow above) and mirrors
+// the listed positions.
+void UpdateRow::FetchFromDevice() {
+  for (const int col : non_zero_position_list_) listed_[col] = 0;
+  dev_->FetchUpdateRow(&non_zero_position_list_, &fetched_values_);
+  const int n = static_cast<int>(non_zero_position_list_.size());
+  for (int k = 0; k < n; ++k) {
+    const int col = non_zero_position_list_[k];
+    listed_[col] = 1;
+    coefficient_[col] = fetched_values_[k];
+  }
+}
+
+// update_row.cc:196-216
+void UpdateRow::ComputeUpdatesRowWise() {
+  coefficient_.resize(matrix_.num_cols(), 0.0);
+  listed_.resize(matrix_.num_cols(), 0);
+  dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
+                variables_info_.GetIsRelevantBitRow().NumWords());
+  dev_->UpdateRowRowWise(rho_filtered_non_zeros_, rho_.values, 2, params_.drop_tolerance);
+  FetchFromDevice();
+}
+
+// update_row.cc:220-259
+void UpdateRow::ComputeUpdatesRowWiseHypersparse() {
+  coefficient_.resize(matrix_.num_cols(), 0.0);
+  listed_.resize(matrix_.num_cols(), 0);
+  dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
+                variables_info_.GetIsRelevantBitRow().NumWords());
+  dev_->UpdateRowRowWise(rho_filtered_non_zeros_, rho_.values, 1, params_.drop_tolerance);
+  FetchFromDevice();
+}
+
+// update_row.cc:261-280
+void UpdateRow::ComputeUpdatesForSingleRow(int row_as_col) {
+  coefficient_.resize(matrix_.num_cols(), 0.0);
+  listed_.resize(matrix_.num_cols(), 0);
+  dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
+                variables_info_.GetIsRelevantBitRow().NumWords());
+  const std::vector<int> one(1, row_as_col);
+  dev_->UpdateRowRowWise(one, rho_.values, 0, params_.drop_tolerance);
+  FetchFromDevice();
+}
+
+// update_row.cc:282-306
+void UpdateRow::ComputeUpdatesColumnWise() {
+  coefficient_.resize(matrix_.num_cols(), 0.0);
+  listed_.resize(matrix_.num_cols(), 0);
+  dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
+                variables_info_.GetIsRelevantBitRow().NumWords());
+  dev_->UpdateRowColumnWise(rho_.values, params_.drop_tolerance,
+                            variables_info_.GetNumEntriesInRelevantColumns());
+  FetchFromDevice();
+}
+
+// update_row.cc:311-332
+void UpdateRow::ComputeFullUpdateRow(int leaving_row,
+                                     std::vector<Fractional>* output) const {
+  const int num_cols = matrix_.num_cols();
+  output->assign(num_cols, 0.0);
+  (*output)[basis_[leaving_row]] = 1.0;
+  const Fractional drop_tolerance = params_.drop_tolerance;
+  variables_info_.GetNotBasicBitRow().ForEach([&](int col) {
+    const Fractional coeff = matrix_.ColumnScalarProduct(col, rho_.values.data());
+    if (std::fabs(coeff) > drop_tolerance) (*output)[col] = coeff;
+  });
+}
+
+// ---------------------------------------------------------------------------
+// PrimalEdgeNorms (primal_edge_norms.cc)
+class PrimalEdgeNorms {
+ public:
+  PrimalEdgeNorms(const CompactSparseMatrix& m, const VariablesInfo& vi,
+                  const BasisFactorization& bf, DeviceLp* dev)
+      : matrix_(m), variables_info_(vi), bf_(bf), dev_(dev) {}
+  void SetParameters(const GlopParameters& p) { params_ = p; }
+  void SetPricingRule(int rule) { pricing_rule_ = rule; }
+  void Clear() {
+    matrix_column_norms_.clear();
+    recompute_edge_squared_norms_ = true;
+    reset_devex_weights_ = true;
+    for (bool* w : watchers_) *w = true;
+  }
+  bool NeedsBasisRefactorization() const {
+    if (pricing_rule_ != 1) return false;
+    return recompute_edge_squared_norms_;
+  }
+  const std::vector<Fractional>& GetSquaredNorms() {
+    switch (pricing_rule_) {
+      case 0:
+        return GetMatrixColumnNorms();
+      case 1:
+        return GetEdgeSquaredNorms();
+      default:
+        return GetDevexWeights();
+    }
+  }
+  const std::vector<Fractional>& GetEdgeSquaredNorms() {
+    if (recompute_edge_squared_norms_) ComputeEdgeSquaredNorms();
+    return edge_squared_norms_;
+  }
+  bool TestEnteringEdgeNormPrecision(int entering_col, const ScatteredVector& d);
+  void UpdateBeforeBasisPivot(int entering_col, int leaving_col, int leaving_row,
+                              const ScatteredVector& direction, UpdateRow* update_row);
+  void AddRecomputationWatcher(bool* w) { watchers_.push_back(w); }
+  double DeterministicTime() const {
+    return DeterministicTimeForFpOperations(num_operations_);
+  }
+
+ private:
+  const std::vector<Fractional>& GetDevexWeights() {
+    if (reset_devex_weights_) ResetDevexWeights();
+    return devex_weights_;
+  }
+  const std::vector<Fractional>& GetMatrixColumnNorms() {
+    if (matrix_column_norms_.empty()) ComputeMatrixColumnNorms();
+    return matrix_column_norms_;
+  }
+  void ComputeMatrixColumnNorms() {
+    matrix_column_norms_.resize(matrix_.num_cols(), 0.0);
+    for (int col = 0; col < matrix_.num_cols(); ++col) {
+      matrix_column_norms_[col] = SquaredNorm(matrix_.column(col));
+      num_operations_ += matrix_.column(col).n;
+    }
+  }
+  void ComputeEdgeSquaredNorms() {  // primal_edge_norms.cc:147-161
+    edge_squared_norms_.resize(matrix_.num_cols(), 0.0);
+    if (bf_.lu().IsIdentityFactorization()) {
+      // 1 + ||a_j||^2 (lu_factorization.cc:130) for every relevant column at
+      // once on the GPU; the per-solve deterministic-time bump is replayed.
+      dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
+                    variables_info_.GetIsRelevantBitRow().NumWords());
+      dev_->ColumnSquaredNorms(&device_norms_);
+      variables_info_.GetIsRelevantBitRow().ForEach([&](int col) {
+        bf_.BumpDeterministicTimeForSolve(matrix_.ColumnNumEntries(col));
+        edge_squared_norms_[col] = device_norms_[col];
+      });
+    } else {
+      variables_info_.GetIsRelevantBitRow().ForEach([&](int col) {
+        edge_squared_norms_[col] = 1.0 + bf_.RightSolveSquaredNorm(matrix_.column(col));
+      });
+    }
+    recompute_edge_squared_norms_ = false;
+  }
+  void ComputeDirectionLeftInverse(int entering_col, const ScatteredVector& d);
+  void UpdateEdgeSquaredNorms(int entering_col, int leaving_col, int leaving_row,
+                              const std::vector<Fractional>& direction,
+                              const UpdateRow& update_row);
+  void UpdateDevexWeights(int entering_col, int leaving_col, int leaving_row,
+                          const std::vector<Fractional>& direction,
+                          const UpdateRow& update_row);
+  void ResetDevexWeights() {
+    if (params_.initialize_devex_with_column_norms) {
+      devex_weights_ = GetMatrixColumnNorms();
+    } else {
+      devex_weights_.assign(matrix_.num_cols(), 1.0);
+    }
+    num_devex_updates_since_reset_ = 0;
+    reset_devex_weights_ = false;
+  }
+
+  const CompactSparseMatrix& matrix_;
+  const VariablesInfo& variables_info_;
+  const BasisFactorization& bf_;
+  DeviceLp* dev_;
+  std::vector<Fractional> device_norms_;
+  std::vector<Fractional> dots_;
+  GlopParameters params_;
+  int pricing_rule_ = 1;
+  bool recompute_edge_squared_norms_ = true;
+  bool reset_devex_weights_ = true;
+  std::vector<Fractional> edge_squared_norms_;
+  std::vector<Fractional> matrix_column_norms_;
+  std::vector<Fractional> devex_weights_;
+  int num_devex_updates_since_reset_ = 0;
+  ScatteredVector direction_left_inverse_;
+  int64_t num_operations_ = 0;
+  std::vector<bool*> watchers_;
+};
+
+// primal_edge_norms.cc:79-108
+bool PrimalEdgeNorms::TestEnteringEdgeNormPrecision(int entering_col,
+                                                    const ScatteredVector& d) {
+  if (!recompute_edge_squared_norms_) {
+    const Fractional old_squared_norm = edge_squared_norms_[entering_col];
+    const Fractional precise_squared_norm = 1.0 + SquaredNorm(d);
+    edge_squared_norms_[entering_col] = precise_squared_norm;
+    const Fractional precise_norm = std::sqrt(precise_squared_norm);
+    const Fractional acc = (precise_norm - std::sqrt(old_squared_norm)) / precise_norm;
+    if (std::fabs(acc) > params_.recompute_edges_norm_threshold) {
+      recompute_edge_squared_norms_ = true;
+      for (bool* w : watchers_) *w = true;
+    }
+    if (old_squared_norm < 0.25 * precise_squared_norm) return false;
+  }
+  return true;
+}
+
+// primal_edge_norms.cc:110-136
+void PrimalEdgeNorms::UpdateBeforeBasisPivot(int entering_col, int leaving_col,
+                                             int leaving_row,
+                                             const ScatteredVector& direction,
+                                             UpdateRow* update_row) {
+  if (!recompute_edge_squared_norms_) {
+    update_row->ComputeUpdateRow(leaving_row);
+    ComputeDirectionLeftInverse(entering_col, direction);
+    UpdateEdgeSquaredNorms(entering_col, leaving_col, leaving_row, direction.values,
+                           *update_row);
+  }
+  if (!reset_devex_weights_) {
+    ++num_devex_updates_since_reset_;
+    if (num_devex_updates_since_reset_ > params_.devex_weights_reset_period) {
+      reset_devex_weights_ = true;
+    } else {
+      update_row->ComputeUpdateRow(leaving_row);
+      UpdateDevexWeights(entering_col, leaving_col, leaving_row, direction.values,
+                         *update_row);
+    }
+  }
+}
+
+// primal_edge_norms.cc:166-199
+void PrimalEdgeNorms::ComputeDirectionLeftInverse(int /*entering_col*/,
+                                                  const ScatteredVector& d) {
+  const int size = d.size();
+  const double kThreshold = 0.05 * size;
+  if (!direction_left_inverse_.non_zeros.empty() &&
+      (direction_left_inverse_.non_zeros.size() + d.non_zeros.size() <
+       2 * kThreshold)) {
+    ClearAndResizeVectorWithNonZeros(size, &direction_left_inverse_);
+    for (const int row : d.non_zeros) direction_left_inverse_[row] = d.values[row];
+  } else {
+    direction_left_inverse_.values = d.values;
+    direction_left_inverse_.non_zeros.clear();
+  }
+  if (d.non_zeros.size() < kThreshold) {
+    direction_left_inverse_.non_zeros = d.non_zeros;
+  }
+  bf_.LeftSolve(&direction_left_inverse_);
+}
+
+// primal_edge_norms.cc:208-258
+void PrimalEdgeNorms::UpdateEdgeSquaredNorms(int entering_col, int leaving_col,
+                                             int leaving_row,
+                                             const std::vector<Fractional>& direction,
+                                             const UpdateRow& update_row) {
+  const Fractional pivot = -direction[leaving_row];
+  const Fractional entering_squared_norm = edge_squared_norms_[entering_col];
+  const Fractional leaving_squared_norm =
+      std::max(1.0, entering_squared_norm / Square(pivot));
+  const Fractional factor = 2.0 / pivot;
+  // a_j . (B^-T d) for every listed column in one GPU pass.
+  dev_->ListDotsOverUpdateRow(direction_left_inverse_.values, &dots_);
+  const std::vector<int>& positions = update_row.GetNonZeroPositions();
+  const std::vector<Fractional>& coefficients = update_row.GetCoefficients();
+  for (size_t k = 0; k < positions.size(); ++k) {
+    const int col = positions[k];
+    const Fractional coeff = coefficients[col];
+    const Fractional scalar_product = dots_[k];
+    num_operations_ += matrix_.ColumnNumEntries(col);
+    edge_squared_norms_[col] +=
+        coeff * (coeff * leaving_squared_norm + factor * scalar_product);
+    const Fractional lower_bound = 1.0 + Square(coeff / pivot);
+    if (edge_squared_norms_[col] < lower_bound) edge_squared_norms_[col] = lower_bound;
+  }
+  edge_squared_norms_[leaving_col] = leaving_squared_norm;
+}
+
+// primal_edge_norms.cc:260-281
+void PrimalEdgeNorms::UpdateDevexWeights(int /*entering_col*/, int leaving_col,
+                                         int leaving_row,
+                                         const std::vector<Fractional>& direction,
+                                         const UpdateRow& update_row) {
+  KahanSum s;
+  for (const Fractional v : direction) s.Add(Square(v));
+  const Fractional entering_norm = std::sqrt(s.Value());
+  const Fractional pivot_magnitude = std::fabs(direction[leaving_row]);
+  const Fractional leaving_norm = std::max(1.0, entering_norm / pivot_magnitude);
+  for (const int col : update_row.GetNonZeroPositions()) {
+    const Fractional coeff = update_row.GetCoefficient(col);
+    const Fractional update_vector_norm = std::fabs(coeff) * leaving_norm;
+    devex_weights_[col] = std::max(devex_weights_[col], Square(update_vector_norm));
+  }
+  devex_weights_[leaving_col] = Square(leaving_norm);
+}
+
+// ---------------------------------------------------------------------------
+// ReducedCosts (reduced_costs.cc:24-510)
+class ReducedCosts {
+ public:
+  ReducedCosts(const CompactSparseMatrix& m, const std::vector<Fractional>& obj,
+               const std::vector<int>& basis, const VariablesInfo& vi,
+               const BasisFactorization& bf, Rng* random, DeviceLp* dev)
+      : matrix_(m), objective_(obj), basis_(basis), variables_info_(vi), bf_(bf),
+        random_(random), dev_(dev) {}
+  void SetParameters(const GlopParameters& p) { params_ = p; }
+  bool NeedsBasisRefactorization() const { return must_refactorize_basis_; }
+  Fractional TestEnteringReducedCostPrecision(int entering_col, const ScatteredVector& d);
+  Fractional ComputeMaximumDualResidual();
+  Fractional ComputeMaximumDualInfeasibility();
+  Fractional ComputeMaximumDualInfeasibilityOnNonBoxedVariables();
+  void UpdateBeforeBasisPivot(int entering_col, int leaving_row,
+                              const ScatteredVector& direction, UpdateRow* update_row) {
+    const int leaving_col = basis_[leaving_row];
+    if (!recompute_reduced_costs_) {
+      UpdateReducedCosts(entering_col, leaving_col, leaving_row, direction[leaving_row],
+                         update_row);
+    }
+    UpdateBasicObjective(entering_col, leaving_row);
+  }
+  void SetNonBasicVariableCostToZero(int col, Fractional* current_cost) {
+    reduced_costs_[col] -= objective_[col];
+    *current_cost = 0.0;
+  }
+  bool AreReducedCostsPrecise() const { return are_reduced_costs_precise_; }
+  bool AreReducedCostsRecomputed() const {
+    return recompute_reduced_costs_ || are_reduced_costs_recomputed_;
+  }
+  void MakeReducedCostsPrecise() {
+    if (are_reduced_costs_precise_) return;
+    must_refactorize_basis_ = true;
+    recompute_basic_objective_left_inverse_ = true;
+    SetRecomputeReducedCostsAndNotifyWatchers();
+  }
+  void PerturbCosts();
+  void ShiftCostIfNeeded(bool increasing_rc_is_needed, int col);
+  bool HasCostShift() const { return has_cost_shift_; }
+  void ClearAndRemoveCostShifts() {
+    has_cost_shift_ = false;
+    cost_perturbations_.assign(matrix_.num_cols(), 0.0);
+    recompute_basic_objective_ = true;
+    recompute_basic_objective_left_inverse_ = true;
+    are_reduced_costs_precise_ = false;
+    SetRecomputeReducedCostsAndNotifyWatchers();
+  }
+  void ResetForNewObjective() {
+    recompute_basic_objective_ = true;
+    recompute_basic_objective_left_inverse_ = true;
+    are_reduced_costs_precise_ = false;
+    SetRecomputeReducedCostsAndNotifyWatchers();
+  }
+  void UpdateDataOnBasisPermutation() {
+    recompute_basic_objective_ = true;
+    recompute_basic_objective_left_inverse_ = true;
+  }
+  const std::vector<Fractional>& GetReducedCosts() {
+    if (bf_.IsRefactorized()) must_refactorize_basis_ = false;
+    if (recompute_reduced_costs_) ComputeReducedCosts();
+    return reduced_costs_;
+  }
+  const std::vector<Fractional>& GetFullReducedCosts() {
+    if (!are_reduced_costs_recomputed_) SetRecomputeReducedCostsAndNotifyWatchers();
+    return GetReducedCosts();
+  }
+  const std::vector<Fractional>& GetDualValues() {
+    ComputeBasicObjectiveLeftInverse();
+    return basic_objective_left_inverse_.values;
+  }
+  Fractional GetDualFeasibilityTolerance() const { return dual_feasibility_tolerance_; }
+  bool IsValidPrimalEnteringCandidate(int col) const {
+    const Fractional rc = reduced_costs_[col];
+    const Fractional tol = dual_feasibility_tolerance_;
+    return (variables_info_.GetCanIncreaseBitRow().IsSet(col) && (rc < -tol)) ||
+           (variables_info_.GetCanDecreaseBitRow().IsSet(col) && (rc > tol));
+  }
+  double DeterministicTime() const { return deterministic_time_; }
+  void AddRecomputationWatcher(bool* w) { watchers_.push_back(w); }
+
+ private:
+  void ComputeBasicObjective() {  // reduced_costs.cc:338-350
+    const int n = matrix_.num_rows();
+    cost_perturbations_.resize(matrix_.num_cols(), 0.0);
+    basic_objective_.resize(n, 0.0);
+    for (int col = 0; col < n; ++col) {
+      const int basis_col = basis_[col];
+      basic_objective_[col] = objective_[basis_col] + cost_perturbations_[basis_col];
+    }
+    recompute_basic_objective_ = false;
+    recompute_basic_objective_left_inverse_ = true;
+  }
+  void ComputeReducedCosts();
+  void ComputeBasicObjectiveLeftInverse() {  // reduced_costs.cc:425-439
+    if (recompute_basic_objective_) ComputeBasicObjective();
+    basic_objective_left_inverse_.values = basic_objective_;
+    basic_objective_left_inverse_.non_zeros.clear();
+    bf_.LeftSolve(&basic_objective_left_inverse_);
+    recompute_basic_objective_left_inverse_ = false;
+  }
+  void UpdateReducedCosts(int entering_col, int leaving_col, int leaving_row,
+                          Fractional pivot, UpdateRow* update_row);
+  void UpdateBasicObjective(int entering_col, int leaving_row) {
+    basic_objective_[leaving_row] =
+        objective_[entering_col] + cost_perturbations_[entering_col];
+    recompute_basic_objective_left_inverse_ = true;
+  }
+  void SetRecomputeReducedCostsAndNotifyWatchers() {
+    recompute_reduced_costs_ = true;
+    for (bool* w : watchers_) *w = true;
+  }
+
+  const CompactSparseMatrix& matrix_;
+  const std::vector<Fractional>& objective_;
+  const std::vector<int>& basis_;
+  const VariablesInfo& variables_info_;
+  const BasisFactorization& bf_;
+  Rng* random_;
+  DeviceLp* dev_;
+  std::vector<Fractional> shifted_objective_;
+  std::vector<Fractional> dots_;
+  GlopParameters params_;
+  bool must_refactorize_basis_ = false;
+  bool recompute_basic_objective_left_inverse_ = true;
+  bool recompute_basic_objective_ = true;
+  bool recompute_reduced_costs_ = true;
+  bool are_reduced_costs_precise_ = false;
+  bool are_reduced_costs_recomputed_ = false;
+  bool has_cost_shift_ = false;
+  std::vector<Fractional> basic_objective_;
+  std::vector<Fractional> cost_perturbations_;
+  std::vector<Fractional> reduced_costs_;
+  ScatteredVector basic_objective_left_inverse_;
+  Fractional dual_feasibility_tolerance_ = 0.0;
+  std::vector<bool*> watchers_;
+  double deterministic_time_ = 0.0;
+};
+
+// reduced_costs.cc:53-94
+Fractional ReducedCosts::TestEnteringReducedCostPrecision(int entering_col,
+                                                          const ScatteredVector& d) {
+  if (recompute_basic_objective_) ComputeBasicObjective();
+  const Fractional old_reduced_cost = reduced_costs_[entering_col];
+  const Fractional precise_reduced_cost =
+      objective_[entering_col] + cost_perturbations_[entering_col] -
+      ScalarProduct(basic_objective_, d);
+  reduced_costs_[entering_col] = precise_reduced_cost;
+  if (!recompute_reduced_costs_) {
+    const Fractional acc = old_reduced_cost - precise_reduced_cost;
+    const Fractional scale =
+        (std::fabs(precise_reduced_cost) <= 1.0) ? 1.0 : precise_reduced_cost;
+    if (std::fabs(acc) / scale > params_.recompute_reduced_costs_threshold) {
+      MakeReducedCostsPrecise();
+    }
+  }
+  return precise_reduced_cost;
+}
+
+// reduced_costs.cc:96-110
+Fractional ReducedCosts::ComputeMaximumDualResidual() {
+  Fractional err = 0.0;
+  const int num_rows = matrix_.num_rows();
+  const std::vector<Fractional>& y = GetDualValues();
+  dev_->ListDots(basis_, y, &dots_);  // a_{B(r)} . y on the GPU
+  for (int row = 0; row < num_rows; ++row) {
+    const int basic_col = basis_[row];
+    const Fractional residual =
+        objective_[basic_col] + cost_perturbations_[basic_col] - dots_[row];
+    err = std::max(err, std::fabs(residual));
+  }
+  return err;
+}
+
+// reduced_costs.cc:112-128
+Fractional ReducedCosts::ComputeMaximumDualInfeasibility() {
+  GetReducedCosts();
+  Fractional m = 0.0;
+  const Bitset& dec = variables_info_.GetCanDecreaseBitRow();
+  const Bitset& inc = variables_info_.GetCanIncreaseBitRow();
+  variables_info_.GetIsRelevantBitRow().ForEach([&](int col) {
+    const Fractional rc = reduced_costs_[col];
+    if ((inc.IsSet(col) && rc < 0.0) || (dec.IsSet(col) && rc > 0.0))
+      m = std::max(m, std::fabs(rc));
+  });
+  return m;
+}
+
+// reduced_costs.cc:130-148
+Fractional ReducedCosts::ComputeMaximumDualInfeasibilityOnNonBoxedVariables() {
+  GetReducedCosts();
+  Fractional m = 0.0;
+  const Bitset& dec = variables_info_.GetCanDecreaseBitRow();
+  const Bitset& inc = variables_info_.GetCanIncreaseBitRow();
+  const Bitset& boxed = variables_info_.GetNonBasicBoxedVariables();
+  variables_info_.GetNotBasicBitRow().ForEach([&](int col) {
+    if (boxed[col]) return;
+    const Fractional rc = reduced_costs_[col];
+    if ((inc.IsSet(col) && rc < 0.0) || (dec.IsSet(col) && rc > 0.0))
+      m = std::max(m, std::fabs(rc));
+  });
+  return m;
+}
+
+// reduced_costs.cc:226-275
+void ReducedCosts::PerturbCosts() {
+  Fractional max_cost_magnitude = 0.0;
+  const int structural_size = matrix_.num_cols() - matrix_.num_rows();
+  for (int col = 0; col < structural_size; ++col)
+    max_cost_magnitude = std::max(max_cost_magnitude, std::fabs(objective_[col]));
+  cost_perturbations_.assign(matrix_.num_cols(), 0.0);
+  for (int col = 0; col < structural_size; ++col) {
+    const Fractional objective = objective_[col];
+    const Fractional magnitude =
+        (1.0 + std::uniform_real_distribution<double>()(*random_)) *
+        (params_.relative_cost_perturbation * std::fabs(objective) +
+         params_.relative_max_cost_perturbation * max_cost_magnitude);
+    switch (variables_info_.GetTypeRow()[col]) {
+      case VariableType::UNCONSTRAINED:
+      case VariableType::FIXED_VARIABLE:
+        break;
+      case VariableType::LOWER_BOUNDED:
+        cost_perturbations_[col] = magnitude;
+        break;
+      case VariableType::UPPER_BOUNDED:
+        cost_perturbations_[col] = -magnitude;
+        break;
+      case VariableType::UPPER_AND_LOWER_BOUNDED:
+        if (objective > 0.0) {
+          cost_perturbations_[col] = magnitude;
+        } else if (objective < 0.0) {
+          cost_perturbations_[col] = -magnitude;
+        }
+        break;
+    }
+  }
+}
+
+// reduced_costs.cc:277-294
+void ReducedCosts::ShiftCostIfNeeded(bool increasing_rc_is_needed, int col) {
+  const Fractional minimum_delta =
+      params_.degenerate_ministep_factor * dual_feasibility_tolerance_;
+  if (increasing_rc_is_needed && reduced_costs_[col] <= -minimum_delta) return;
+  if (!increasing_rc_is_needed && reduced_costs_[col] >= minimum_delta) return;
+  const Fractional delta = increasing_rc_is_needed ? minimum_delta : -minimum_delta;
+  cost_perturbations_[col] -= reduced_costs_[col] + delta;
+  reduced_costs_[col] = -delta;
+  has_cost_shift_ = true;
+}
+
+// reduced_costs.cc:352-423 (single-threaded path; the OMP branch does not
+// compile upstream).
+void ReducedCosts::ComputeReducedCosts() {
+  if (recompute_basic_objective_left_inverse_) ComputeBasicObjectiveLeftInverse();
+  Fractional dual_residual_error = 0.0;
+  const int num_cols = matrix_.num_cols();
+  reduced_costs_.resize(num_cols, 0.0);
+  const Bitset& is_basic = variables_info_.GetIsBasicBitRow();
+  cost_perturbations_.resize(num_cols, 0.0);
+  shifted_objective_.resize(num_cols);
+  for (int col = 0; col < num_cols; ++col)
+    shifted_objective_[col] = objective_[col] + cost_perturbations_[col];
+  // rc_j = (c_j + delta_j) - a_j . y for all N columns: the pricing SpMV.
+  dev_->Pricing(shifted_objective_, basic_objective_left_inverse_.values, &reduced_costs_);
+  is_basic.ForEach([&](int col) {
+    dual_residual_error = std::max(dual_residual_error, std::fabs(reduced_costs_[col]));
+  });
+  deterministic_time_ += DeterministicTimeForFpOperations(matrix_.num_entries());
+  recompute_reduced_costs_ = false;
+  are_reduced_costs_recomputed_ = true;
+  are_reduced_costs_precise_ = bf_.IsRefactorized();
+  dual_feasibility_tolerance_ = params_.dual_feasibility_tolerance;
+  if (dual_residual_error > dual_feasibility_tolerance_) {
+    dual_feasibility_tolerance_ = dual_residual_error;
+  }
+}
+
+// reduced_costs.cc:444-488
+void ReducedCosts::UpdateReducedCosts(int entering_col, int leaving_col, int leaving_row,
+                                      Fractional pivot, UpdateRow* update_row) {
+  if (recompute_reduced_costs_) return;
+  const Fractional entering_reduced_cost = reduced_costs_[entering_col];
+  if (entering_reduced_cost == 0.0) {
+    are_reduced_costs_precise_ = false;
+    return;
+  }
+  are_reduced_costs_recomputed_ = false;
+  are_reduced_costs_precise_ = false;
+  update_row->ComputeUpdateRow(leaving_row);
+  const Fractional new_leaving_reduced_cost = entering_reduced_cost / -pivot;
+  for (const int col : update_row->GetNonZeroPositions()) {
+    const Fractional coeff = update_row->GetCoefficient(col);
+    reduced_costs_[col] += new_leaving_reduced_cost * coeff;
+  }
+  reduced_costs_[leaving_col] = new_leaving_reduced_cost;
+  reduced_costs_[entering_col] = 0.0;
+}
+
+// ---------------------------------------------------------------------------
+// PrimalPrices (reduced_costs.cc:512-600)
+class PrimalPrices {
+ public:
+  PrimalPrices(Rng* random, const VariablesInfo& vi, PrimalEdgeNorms* pen,
+               ReducedCosts* rc)
+      : prices_(random), variables_info_(vi), primal_edge_norms_(pen),
+        reduced_costs_(rc) {
+    reduced_costs_->AddRecomputationWatcher(&recompute_);
+    primal_edge_norms_->AddRecomputationWatcher(&recompute_);
+  }
+  int GetBestEnteringColumn() {
+    if (recompute_) {
+      const std::vector<Fractional>& rc = reduced_costs_->GetReducedCosts();
+      prices_.ClearAndResize(static_cast<int>(rc.size()));
+      const std::vector<int> cols = variables_info_.GetIsRelevantBitRow().ToVector();
+      UpdateEnteringCandidates<true>(cols);
+      recompute_ = false;
+    }
+    return prices_.GetMaximum();
+  }
+  void UpdateBeforeBasisPivot(int /*entering_col*/, UpdateRow* update_row) {
+    if (recompute_) return;
+    UpdateEnteringCandidates<false>(update_row->GetNonZeroPositions());
+  }
+  void RecomputePriceAt(int col) {
+    if (recompute_) return;
+    if (reduced_costs_->IsValidPrimalEnteringCandidate(col)) {
+      const std::vector<Fractional>& sn = primal_edge_norms_->GetSquaredNorms();
+      const std::vector<Fractional>& rc = reduced_costs_->GetReducedCosts();
+      prices_.AddOrUpdate(col, Square(rc[col]) / sn[col]);
+    } else {
+      prices_.Remove(col);
+    }
+  }
+  void SetAndDebugCheckThatColumnIsDualFeasible(int col) {
+    if (recompute_) return;
+    prices_.Remove(col);
+  }
+  void ForceRecomputation() { recompute_ = true; }
+
+ private:
+  template <bool from_clean_state>
+  void UpdateEnteringCandidates(const std::vector<int>& cols) {
+    const Fractional tolerance = reduced_costs_->GetDualFeasibilityTolerance();
+    const Bitset& dec = variables_info_.GetCanDecreaseBitRow();
+    const Bitset& inc = variables_info_.GetCanIncreaseBitRow();
+    const std::vector<Fractional>& sn = primal_edge_norms_->GetSquaredNorms();
+    const std::vector<Fractional>& rc = reduced_costs_->GetReducedCosts();
+    for (const int col : cols) {
+      const Fractional reduced_cost = rc[col];
+      const bool is_dual_infeasible =
+          ((reduced_cost > tolerance) && dec.IsSet(col)) !=
+          ((reduced_cost < -tolerance) && inc.IsSet(col));
+      if (is_dual_infeasible) {
+        prices_.AddOrUpdate(col, Square(reduced_cost) / sn[col]);
+      } else {
+        if (!from_clean_state) prices_.Remove(col);
+      }
+    }
+  }
+  bool recompute_ = true;
+  DynamicMaximum prices_;
+  const VariablesInfo& variables_info_;
+  PrimalEdgeNorms* primal_edge_norms_;
+  ReducedCosts* reduced_costs_;
+};
+
+// ---------------------------------------------------------------------------
+// EnteringVariable (entering_variable.cc)
+class EnteringVariable {
+ public:
+  EnteringVariable(const VariablesInfo& vi, Rng* random, ReducedCosts* rc)
+      : variables_info_(vi), random_(random), reduced_costs_(rc) {}
+  void SetParameters(const GlopParameters& p) { params_ = p; }
+  Status DualChooseEnteringColumn(bool nothing_to_recompute, const UpdateRow& update_row,
+                                  Fractional cost_variation,
+                                  std::vector<int>* bound_flip_candidates,
+                                  int* entering_col);
+  Status DualPhaseIChooseEnteringColumn(bool nothing_to_recompute,
+                                        const UpdateRow& update_row,
+                                        Fractional cost_variation, int* entering_col);
+  double DeterministicTime() const {
+    return DeterministicTimeForFpOperations(num_operations_);
+  }
+
+ private:
+  struct ColWithRatio {  // entering_variable.h:118-139
+    int col;
+    Fractional ratio;
+    Fractional coeff_magnitude;
+    ColWithRatio() = default;
+    ColWithRatio(int c, Fractional reduced_cost, Fractional coeff_m)
+        : col(c), ratio(reduced_cost / coeff_m), coeff_magnitude(coeff_m) {}
+    bool operator<(const ColWithRatio& o) const {
+      if (ratio == o.ratio) {
+        if (coeff_magnitude == o.coeff_magnitude) return col > o.col;
+        return coeff_magnitude < o.coeff_magnitude;
+      }
+      return ratio > o.ratio;
+    }
+  };
+  const VariablesInfo& variables_info_;
+  Rng* random_;
+  ReducedCosts* reduced_costs_;
+  GlopParameters params_;
+  std::vector<int> equivalent_entering_choices_;
+  std::vector<ColWithRatio> breakpoints_;
+  int64_t num_operations_ = 0;
+};
+
+// entering_variable.cc:37-239
+Status EnteringVariable::DualChooseEnteringColumn(bool nothing_to_recompute,
+                                                  const UpdateRow& update_row,
+                                                  Fractional cost_variation,
+                                                  std::vector<int>* bound_flip_candidates,
+                                                  int* entering_col) {
+  const std::vector<Fractional>& update_coefficients = update_row.GetCoefficients();
+  const std::vector<Fractional>& reduced_costs = reduced_costs_->GetReducedCosts();
+  breakpoints_.clear();
+  breakpoints_.reserve(update_row.GetNonZeroPositions().size());
+  const Bitset& can_decrease = variables_info_.GetCanDecreaseBitRow();
+  const Bitset& can_increase = variables_info_.GetCanIncreaseBitRow();
+  const Bitset& is_boxed = variables_info_.GetNonBasicBoxedVariables();
+  const Fractional threshold = nothing_to_recompute ? params_.minimum_acceptable_pivot
+                                                    : params_.ratio_test_zero_threshold;
+  Fractional variation_magnitude = std::fabs(cost_variation) - threshold;
+  const Fractional harris_tolerance =
+      params_.harris_tolerance_ratio * reduced_costs_->GetDualFeasibilityTolerance();
+  Fractional harris_ratio = std::numeric_limits<Fractional>::max();
+  const Fractional minimum_delta =
+      params_.degenerate_ministep_factor * reduced_costs_->GetDualFeasibilityTolerance();
+  num_operations_ += 10 * update_row.GetNonZeroPositions().size();
+  for (const int col : update_row.GetNonZeroPositions()) {
+    const Fractional coeff =
+        (cost_variation > 0.0) ? update_coefficients[col] : -update_coefficients[col];
+    ColWithRatio entry;
+    if (can_decrease.IsSet(col) && coeff > threshold) {
+      if (-reduced_costs[col] > harris_ratio * coeff) continue;
+      entry = ColWithRatio(col, -reduced_costs[col], coeff);
+    } else if (can_increase.IsSet(col) && coeff < -threshold) {
+      if (reduced_costs[col] > harris_ratio * -coeff) continue;
+      entry = ColWithRatio(col, reduced_costs[col], -coeff);
+    } else {
+      continue;
+    }
+    const Fractional hr = std::max(minimum_delta / entry.coeff_magnitude,
+                                   entry.ratio + harris_tolerance / entry.coeff_magnitude);
+    if (hr < harris_ratio) {
+      if (is_boxed[col]) {
+        const Fractional delta =
+            variables_info_.GetBoundDifference(col) * entry.coeff_magnitude;
+        if (delta >= variation_magnitude) harris_ratio = hr;
+      } else {
+        harris_ratio = hr;
+      }
+    }
+    breakpoints_.push_back(entry);
+  }
+  std::make_heap(breakpoints_.begin(), breakpoints_.end());
+  harris_ratio = std::numeric_limits<Fractional>::max();
+  *entering_col = kInvalidCol;
+  bound_flip_candidates->clear();
+  Fractional step = 0.0;
+  Fractional best_coeff = -1.0;
+  equivalent_entering_choices_.clear();
+  while (!breakpoints_.empty()) {
+    const ColWithRatio top = breakpoints_.front();
+    if (top.ratio > harris_ratio) break;
+    if (variation_magnitude > 0.0) {
+      if (is_boxed[top.col]) {
+        variation_magnitude -=
+            variables_info_.GetBoundDifference(top.col) * top.coeff_magnitude;
+        if (variation_magnitude > 0.0) {
+          bound_flip_candidates->push_back(top.col);
+          std::pop_heap(breakpoints_.begin(), breakpoints_.end());
+          breakpoints_.pop_back();
+          continue;
+        }
+      }
+    }
+    if (top.coeff_magnitude >= best_coeff) {
+      harris_ratio = std::min(
+          harris_ratio, std::max(minimum_delta / top.coeff_magnitude,
+                                 top.ratio + harris_tolerance / top.coeff_magnitude));
+      if (top.coeff_magnitude == best_coeff && top.ratio == step) {
+        equivalent_entering_choices_.push_back(top.col);
+      } else {
+        equivalent_entering_choices_.clear();
+        best_coeff = top.coeff_magnitude;
+        *entering_col = top.col;
+        step = top.ratio;
+      }
+    }
+    std::pop_heap(breakpoints_.begin(), breakpoints_.end());
+    breakpoints_.pop_back();
+  }
+  if (!equivalent_entering_choices_.empty()) {
+    equivalent_entering_choices_.push_back(*entering_col);
+    *entering_col = equivalent_entering_choices_[UniformInt(
+        *random_, static_cast<int>(equivalent_entering_choices_.size()) - 1)];
+  }
+  if (*entering_col == kInvalidCol) return Status::OK();
+  const Fractional pivot_limit = params_.minimum_acceptable_pivot;
+  if (best_coeff < pivot_limit && !bound_flip_candidates->empty()) {
+    for (int i = static_cast<int>(bound_flip_candidates->size()) - 1; i >= 0; --i) {
+      const int col = (*bound_flip_candidates)[i];
+      if (std::fabs(update_coefficients[col]) < pivot_limit) continue;
+      *entering_col = col;
+      break;
+    }
+  }
+  return Status::OK();
+}
+
+// entering_variable.cc:241-355
+Status EnteringVariable::DualPhaseIChooseEnteringColumn(bool nothing_to_recompute,
+                                                        const UpdateRow& update_row,
+                                                        Fractional cost_variation,
+                                                        int* entering_col) {
+  const std::vector<Fractional>& update_coefficients = update_row.GetCoefficients();
+  const std::vector<Fractional>& reduced_costs = reduced_costs_->GetReducedCosts();
+  breakpoints_.clear();
+  breakpoints_.reserve(update_row.GetNonZeroPositions().size());
+  const Fractional threshold = nothing_to_recompute ? params_.minimum_acceptable_pivot
+                                                    : params_.ratio_test_zero_threshold;
+  const Fractional dual_feasibility_tolerance =
+      reduced_costs_->GetDualFeasibilityTolerance();
+  const Fractional harris_tolerance =
+      params_.harris_tolerance_ratio * dual_feasibility_tolerance;
+  const Fractional minimum_delta =
+      params_.degenerate_ministep_factor * dual_feasibility_tolerance;
+  const Bitset& can_decrease = variables_info_.GetCanDecreaseBitRow();
+  const Bitset& can_increase = variables_info_.GetCanIncreaseBitRow();
+  num_operations_ += 10 * update_row.GetNonZeroPositions().size();
+  for (const int col : update_row.GetNonZeroPositions()) {
+    if (std::fabs(update_coefficients[col]) < threshold) continue;
+    const Fractional coeff =
+        (cost_variation > 0.0) ? update_coefficients[col] : -update_coefficients[col];
+    if (std::fabs(reduced_costs[col]) <= dual_feasibility_tolerance) {
+      if (coeff > 0 && !can_decrease.IsSet(col)) continue;
+      if (coeff < 0 && !can_increase.IsSet(col)) continue;
+      if (coeff * reduced_costs[col] > 0.0) {
+        breakpoints_.push_back(ColWithRatio(
+            col, std::max(minimum_delta, harris_tolerance - std::fabs(reduced_costs[col])),
+            std::fabs(coeff)));
+        continue;
+      }
+    } else {
+      if (coeff * reduced_costs[col] > 0.0) continue;
+    }
+    breakpoints_.push_back(ColWithRatio(
+        col, std::fabs(reduced_costs[col]) + harris_tolerance, std::fabs(coeff)));
+  }
+  std::make_heap(breakpoints_.begin(), breakpoints_.end());
+  Fractional pivot_magnitude = 0.0;
+  *entering_col = kInvalidCol;
+  Fractional step = -1.0;
+  Fractional improvement = std::fabs(cost_variation);
+  while (!breakpoints_.empty()) {
+    const ColWithRatio top = breakpoints_.front();
+    if (top.ratio > step && top.coeff_magnitude >= pivot_magnitude) {
+      *entering_col = top.col;
+      step = top.ratio;
+      pivot_magnitude = top.coeff_magnitude;
+    }
+    improvement -= top.coeff_magnitude;
+    if (can_decrease.IsSet(top.col) && can_increase.IsSet(top.col) &&
+        std::fabs(reduced_costs[top.col]) > threshold) {
+      improvement -= top.coeff_magnitude;
+    }
+    if (improvement <= 0.0) break;
+    std::pop_heap(breakpoints_.begin(), breakpoints_.end());
+    breakpoints_.pop_back();
+  }
+  return Status::OK();
+}
+
+// ---------------------------------------------------------------------------
+// VariableValues (variable_values.cc)
+class VariableValues {
+ public:
+  VariableValues(const GlopParameters& p, const CompactSparseMatrix& m,
+                 const std::vector<int>& basis, const VariablesInfo& vi,
+                 const BasisFactorization& bf, DualEdgeNorms* den, DynamicMaximum* dp,
+                 DeviceLp* dev)
+      : params_(p), matrix_(m), basis_(basis), variables_info_(vi), bf_(bf),
+        dual_edge_norms_(den), dual_prices_(dp), dev_(dev) {}
+  Fractional Get(int col) const { return variable_values_[col]; }
+  void Set(int col, Fractional v) { variable_values_[col] = v; }
+  const std::vector<Fractional>& GetDenseRow() const { return variable_values_; }
+  void SetNonBasicVariableValueFromStatus(int col);
+  void ResetAllNonBasicVariableValues(const std::vector<Fractional>& free_initial);
+  void RecomputeBasicVariableValues();
+  Fractional ComputeMaximumPrimalResidual() const;
+  Fractional ComputeMaximumPrimalInfeasibility() const;
+  void UpdateOnPivoting(const ScatteredVector& direction, int entering_col,
+                        Fractional step) {
+    for (const int row : direction.non_zeros) {
+      const int col = basis_[row];
+      variable_values_[col] -= direction.values[row] * step;
+    }
+    variable_values_[entering_col] += step;
+  }
+  void UpdateGivenNonBasicVariables(const std::vector<int>& cols, bool update_basic);
+  void RecomputeDualPrices(bool put_more_importance_on_norm = false);
+  void UpdateDualPrices(const std::vector<int>& rows);
+  template <typename Rows>
+  bool UpdatePrimalPhaseICosts(const Rows& rows, std::vector<Fractional>* objective) {
+    bool changed = false;
+    const Fractional tolerance = params_.primal_feasibility_tolerance;
+    for (const int row : rows) {
+      const int col = basis_[row];
+      Fractional new_cost = 0.0;
+      if (GetUpperBoundInfeasibility(col) > tolerance) {
+        new_cost = 1.0;
+      } else if (GetLowerBoundInfeasibility(col) > tolerance) {
+        new_cost = -1.0;
+      }
+      if (new_cost != (*objective)[col]) {
+        changed = true;
+        (*objective)[col] = new_cost;
+      }
+    }
+    return changed;
+  }
+
+ private:
+  Fractional GetUpperBoundInfeasibility(int col) const {
+    return variable_values_[col] - variables_info_.GetVariableUpperBounds()[col];
+  }
+  Fractional GetLowerBoundInfeasibility(int col) const {
+    return variables_info_.GetVariableLowerBounds()[col] - variable_values_[col];
+  }
+  const GlopParameters& params_;
+  const CompactSparseMatrix& matrix_;
+  const std::vector<int>& basis_;
+  const VariablesInfo& variables_info_;
+  const BasisFactorization& bf_;
+  bool put_more_importance_on_norm_ = false;
+  DualEdgeNorms* dual_edge_norms_;
+  DynamicMaximum* dual_prices_;
+  DeviceLp* dev_;
+  std::vector<Fractional> variable_values_;
+  mutable ScatteredVector scratchpad_;
+  ScatteredVector initially_all_zero_scratchpad_;
+};
+
+void VariableValues::SetNonBasicVariableValueFromStatus(int col) {
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  variable_values_.resize(matrix_.num_cols(), 0.0);
+  switch (variables_info_.GetStatusRow()[col]) {
+    case VariableStatus::FIXED_VALUE:
+    case VariableStatus::AT_LOWER_BOUND:
+      variable_values_[col] = lb[col];
+      break;
+    case VariableStatus::AT_UPPER_BOUND:
+      variable_values_[col] = ub[col];
+      break;
+    default:
+      break;
+  }
+}
+
+void VariableValues::ResetAllNonBasicVariableValues(const std::vector<Fractional>& fiv) {
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  const std::vector<VariableStatus>& st = variables_info_.GetStatusRow();
+  const int num_cols = matrix_.num_cols();
+  variable_values_.resize(num_cols, 0.0);
+  for (int col = 0; col < num_cols; ++col) {
+    switch (st[col]) {
+      case VariableStatus::FIXED_VALUE:
+      case VariableStatus::AT_LOWER_BOUND:
+        variable_values_[col] = lb[col];
+        break;
+      case VariableStatus::AT_UPPER_BOUND:
+        variable_values_[col] = ub[col];
+        break;
+      case VariableStatus::FREE:
+        variable_values_[col] = col < static_cast<int>(fiv.size()) ? fiv[col] : 0.0;
+        break;
+      case VariableStatus::BASIC:
+        break;
+    }
+  }
+}
+
+// variable_values.cc:101-118
+void VariableValues::RecomputeBasicVariableValues() {
+  const int num_rows = matrix_.num_rows();
+  scratchpad_.non_zeros.clear();
+  // -sum over non-basic columns of x_j a_j, per row in column order (GPU).
+  dev_->SetMask(DeviceLp::kBasic, variables_info_.GetIsBasicBitRow().data(),
+                variables_info_.GetIsBasicBitRow().NumWords());
+  dev_->RowSums(variable_values_, /*skip_basic=*/true, -1.0, &scratchpad_.values);
+  bf_.RightSolve(&scratchpad_);
+  for (int row = 0; row < num_rows; ++row) variable_values_[basis_[row]] = scratchpad_[row];
+  dual_prices_->Clear();
+}
+
+// variable_values.cc:120-131
+Fractional VariableValues::ComputeMaximumPrimalResidual() const {
+  scratchpad_.non_zeros.clear();
+  dev_->RowSums(variable_values_, /*skip_basic=*/false, 1.0, &scratchpad_.values);
+  return InfinityNorm(scratchpad_.values);
+}
+
+// variable_values.cc:133-143
+Fractional VariableValues::ComputeMaximumPrimalInfeasibility() const {
+  Fractional pi = 0.0;
+  for (int col = 0; col < matrix_.num_cols(); ++col) {
+    const Fractional ci =
+        std::max(GetUpperBoundInfeasibility(col), GetLowerBoundInfeasibility(col));
+    pi = std::max(pi, ci);
+  }
+  return pi;
+}
+
+// variable_values.cc:179-227
+void VariableValues::UpdateGivenNonBasicVariables(const std::vector<int>& cols,
+                                                  bool update_basic) {
+  if (!update_basic) {
+    for (const int col : cols) SetNonBasicVariableValueFromStatus(col);
+    return;
+  }
+  const int num_rows = matrix_.num_rows();
+  initially_all_zero_scratchpad_.values.resize(num_rows, 0.0);
+  initially_all_zero_scratchpad_.ClearSparseMask();
+  bool use_dense = false;
+  for (const int col : cols) {
+    const Fractional old_value = variable_values_[col];
+    SetNonBasicVariableValueFromStatus(col);
+    if (use_dense) {
+      matrix_.ColumnAddMultipleToDenseColumn(col, variable_values_[col] - old_value,
+                                             initially_all_zero_scratchpad_.values.data());
+    } else {
+      matrix_.ColumnAddMultipleToSparseScatteredColumn(
+          col, variable_values_[col] - old_value, &initially_all_zero_scratchpad_);
+      use_dense = initially_all_zero_scratchpad_.ShouldUseDenseIteration();
+    }
+  }
+  initially_all_zero_scratchpad_.ClearSparseMask();
+  initially_all_zero_scratchpad_.ClearNonZerosIfTooDense();
+  bf_.RightSolve(&initially_all_zero_scratchpad_);
+  if (initially_all_zero_scratchpad_.non_zeros.empty()) {
+    for (int row = 0; row < num_rows; ++row)
+      variable_values_[basis_[row]] -= initially_all_zero_scratchpad_[row];
+    initially_all_zero_scratchpad_.values.assign(num_rows, 0.0);
+    RecomputeDualPrices();
+    return;
+  }
+  for (const int row : initially_all_zero_scratchpad_.non_zeros) {
+    variable_values_[basis_[row]] -= initially_all_zero_scratchpad_[row];
+    initially_all_zero_scratchpad_[row] = 0.0;
+  }
+  UpdateDualPrices(initially_all_zero_scratchpad_.non_zeros);
+  initially_all_zero_scratchpad_.non_zeros.clear();
+}
+
+// variable_values.cc:229-262
+void VariableValues::RecomputeDualPrices(bool put_more_importance_on_norm) {
+  const int num_rows = matrix_.num_rows();
+  dual_prices_->ClearAndResize(num_rows);
+  dual_prices_->StartDenseUpdates();
+  put_more_importance_on_norm_ = put_more_importance_on_norm;
+  const Fractional tolerance = params_.primal_feasibility_tolerance;
+  const std::vector<Fractional>& sn = dual_edge_norms_->GetEdgeSquaredNorms();
+  for (int row = 0; row < num_rows; ++row) {
+    const int col = basis_[row];
+    const Fractional inf =
+        std::max(GetUpperBoundInfeasibility(col), GetLowerBoundInfeasibility(col));
+    if (inf > tolerance) {
+      dual_prices_->DenseAddOrUpdate(
+          row, put_more_importance_on_norm ? std::fabs(inf) / sn[row] : Square(inf) / sn[row]);
+    }
+  }
+}
+
+// variable_values.cc:264-297
+void VariableValues::UpdateDualPrices(const std::vector<int>& rows) {
+  if (dual_prices_->Size() != matrix_.num_rows()) {
+    RecomputeDualPrices(put_more_importance_on_norm_);
+    return;
+  }
+  const Fractional tolerance = params_.primal_feasibility_tolerance;
+  const std::vector<Fractional>& sn = dual_edge_norms_->GetEdgeSquaredNorms();
+  for (const int row : rows) {
+    const int col = basis_[row];
+    const Fractional inf =
+        std::max(GetUpperBoundInfeasibility(col), GetLowerBoundInfeasibility(col));
+    if (inf > tolerance) {
+      dual_prices_->AddOrUpdate(row, put_more_importance_on_norm_
+                                         ? std::fabs(inf) / sn[row]
+                                         : Square(inf) / sn[row]);
+    } else {
+      dual_prices_->Remove(row);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// InitialBasis::CompleteTriangularBasis (initial_basis.cc:126-206)
+namespace {
+int GetColumnCategory(VariableType t) {
+  switch (t) {
+    case VariableType::UNCONSTRAINED:
+      return 2;
+    case VariableType::LOWER_BOUNDED:
+    case VariableType::UPPER_BOUNDED:
+      return 3;
+    case VariableType::UPPER_AND_LOWER_BOUNDED:
+      return 4;
+    case VariableType::FIXED_VARIABLE:
+      return 5;
+  }
+  return 5;
+}
+
+template <bool only_allow_zero_cost_column>
+void CompleteTriangularBasis(const CompactSparseMatrix& matrix,
+                             const std::vector<Fractional>& objective,
+                             const std::vector<Fractional>& lb,
+                             const std::vector<Fractional>& ub,
+                             const std::vector<VariableType>& type, int num_cols,
+                             std::vector<int>* basis) {
+  const int num_rows = matrix.num_rows();
+  std::vector<char> can_be_replaced(num_rows, false);
+  for (int row = 0; row < num_rows; ++row)
+    if ((*basis)[row] == kInvalidCol) can_be_replaced[row] = true;
+  MatrixNonZeroPattern residual_pattern;
+  residual_pattern.Reset(num_rows, num_cols);
+  for (int col = 0; col < num_cols; ++col) {
+    if (only_allow_zero_cost_column && objective[col] != 0.0) continue;
+    const ColumnView c = matrix.column(col);
+    for (int64_t i = 0; i < c.n; ++i)
+      if (can_be_replaced[c.rows[i]]) residual_pattern.AddEntry(c.rows[i], col);
+  }
+  std::vector<int> residual_singleton_column;
+  Fractional max_scaled_abs_cost = 0.0;
+  for (int col = 0; col < num_cols; ++col) {
+    max_scaled_abs_cost = std::max(max_scaled_abs_cost, std::fabs(objective[col]));
+    if (residual_pattern.ColDegree(col) == 1) residual_singleton_column.push_back(col);
+  }
+  const Fractional kBixbyWeight = 1000.0;
+  max_scaled_abs_cost =
+      (max_scaled_abs_cost == 0.0) ? 1.0 : kBixbyWeight * max_scaled_abs_cost;
+  auto penalty = [&](int col) {  // initial_basis.cc:GetColumnPenalty
+    const VariableType t = type[col];
+    Fractional p = 0.0;
+    if (t == VariableType::LOWER_BOUNDED) p = lb[col];
+    if (t == VariableType::UPPER_BOUNDED) p = -ub[col];
+    if (t == VariableType::UPPER_AND_LOWER_BOUNDED) p = lb[col] - ub[col];
+    return p + std::fabs(objective[col]) / max_scaled_abs_cost;
+  };
+  // initial_basis.cc TriangularColumnComparator.
+  auto cmp = [&](int a, int b) {
+    if (a == b) return false;
+    const int ca = GetColumnCategory(type[a]);
+    const int cb = GetColumnCategory(type[b]);
+    if (ca != cb) return ca > cb;
+    if (matrix.ColumnNumEntries(a) != matrix.ColumnNumEntries(b))
+      return matrix.ColumnNumEntries(a) > matrix.ColumnNumEntries(b);
+    return penalty(a) > penalty(b);
+  };
+  std::priority_queue<int, std::vector<int>, std::function<bool(int, int)>> queue(
+      cmp, std::vector<int>(residual_singleton_column.begin(),
+                            residual_singleton_column.end()));
+  while (!queue.empty()) {
+    const int candidate = queue.top();
+    queue.pop();
+    if (residual_pattern.ColDegree(candidate) != 1) continue;
+    int row = kInvalidRow;
+    Fractional coeff = 0.0;
+    Fractional max_magnitude = 0.0;
+    const ColumnView c = matrix.column(candidate);
+    for (int64_t i = 0; i < c.n; ++i) {
+      max_magnitude = std::max(max_magnitude, std::fabs(c.coefs[i]));
+      if (can_be_replaced[c.rows[i]]) {
+        row = c.rows[i];
+        coeff = c.coefs[i];
+        break;
+      }
+    }
+    const Fractional kStabilityThreshold = 0.01;
+    if (std::fabs(coeff) < kStabilityThreshold * max_magnitude) continue;
+    (*basis)[row] = candidate;
+    can_be_replaced[row] = false;
+    residual_pattern.DeleteRowAndColumn(row, candidate);
+    for (const int col : residual_pattern.RowNonZero(row)) {
+      if (col == candidate) continue;
+      residual_pattern.DecreaseColDegree(col);
+      if (residual_pattern.ColDegree(col) == 1) queue.push(col);
+    }
+  }
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// RevisedSimplex (revised_simplex.cc)
+class RevisedSimplex {
+ public:
+  RevisedSimplex();
+  void SetParameters(const GlopParameters& p) {  // revised_simplex.cc:3586-3593
+    random_.seed(p.random_seed);
+    initial_parameters_ = p;
+    parameters_ = p;
+    PropagateParameters();
+  }
+  Status Solve(const LinearProgram& lp, TimeLimit* time_limit);
+  void ClearStateForNextSolve() {
+    solution_state_.clear();
+    variable_starting_values_.clear();
+  }
+  void LoadStateForNextSolve(const std::vector<VariableStatus>& s) {
+    solution_state_ = s;
+    solution_state_has_been_set_externally_ = true;
+  }
+  void NotifyThatMatrixIsUnchangedForNextSolve() { notify_that_matrix_is_unchanged_ = true; }
+
+  ProblemStatus GetProblemStatus() const { return problem_status_; }
+  Fractional GetObjectiveValue() const { return solution_objective_value_; }
+  int64_t GetNumberOfIterations() const { return num_iterations_; }
+  Fractional GetVariableValue(int col) const { return variable_values_.Get(col); }
+  Fractional GetReducedCost(int col) const { return solution_reduced_costs_[col]; }
+  Fractional GetDualValue(int row) const { return solution_dual_values_[row]; }
+  Fractional GetConstraintActivity(int row) const {
+    return -variable_values_.Get(first_slack_col_ + row);
+  }
+  VariableStatus GetVariableStatus(int col) const {
+    return variables_info_.GetStatusRow()[col];
+  }
+  VariableStatus GetConstraintStatus(int row) const {  // revised_simplex.cc:681-692
+    const VariableStatus s = variables_info_.GetStatusRow()[first_slack_col_ + row];
+    if (s == VariableStatus::AT_LOWER_BOUND) return VariableStatus::AT_UPPER_BOUND;
+    if (s == VariableStatus::AT_UPPER_BOUND) return VariableStatus::AT_LOWER_BOUND;
+    return s;
+  }
+  const std::vector<VariableStatus>& GetState() const { return solution_state_; }
+  int GetBasis(int row) const { return basis_[row]; }
+  const std::vector<Fractional>& GetPrimalRay() const { return solution_primal_ray_; }
+  const std::vector<Fractional>& GetDualRay() const { return solution_dual_ray_; }
+  const std::vector<Fractional>& GetDualRayRowCombination() const {
+    return solution_dual_ray_row_combination_;
+  }
+  double DeterministicTime() const {  // revised_simplex.cc:731-739
+    return DeterministicTimeForFpOperations(num_update_price_operations_) +
+           basis_factorization_.DeterministicTime() + update_row_.DeterministicTime() +
+           entering_variable_.DeterministicTime() + reduced_costs_.DeterministicTime() +
+           primal_edge_norms_.DeterministicTime();
+  }
+  int num_rows() const { return num_rows_; }
+  int num_cols() const { return num_cols_; }
+  // Per-iteration timestamps (seconds since Solve start) for the CPU baseline.
+  std::vector<double> iteration_times;
+  bool record_iteration_times = false;
+  // Called after every completed iteration (benchmark slicing, mi_lp_begin).
+  std::function<void(int64_t)> iteration_hook;
+  DeviceLp& device() { return device_; }
+
+ private:
+  enum class Phase { FEASIBILITY, OPTIMIZATION, PUSH };
+  void PropagateParameters() {
+    basis_factorization_.SetParameters(parameters_.basis_refactorization_period,
+                                       parameters_.dynamically_adjust_refactorization_period,
+                                       parameters_.lu());
+    entering_variable_.SetParameters(parameters_);
+    reduced_costs_.SetParameters(parameters_);
+    dual_edge_norms_.SetParameters(parameters_);
+    primal_edge_norms_.SetParameters(parameters_);
+    update_row_.SetParameters(parameters_);
+  }
+  Status Initialize(const LinearProgram& lp);
+  bool InitializeMatrixAndTestIfUnchanged(const LinearProgram& lp,
+                                          bool* only_change_is_new_rows,
+                                          bool* only_change_is_new_cols,
+                                          int* num_new_cols);
+  bool OldBoundsAreUnchangedAndNewVariablesHaveOneBoundAtZero(const LinearProgram& lp,
+                                                              int num_new_cols);
+  bool InitializeObjectiveAndTestIfUnchanged(const LinearProgram& lp);
+  void InitializeObjectiveLimit();
+  Status CreateInitialBasis();
+  Status InitializeFirstBasis(const std::vector<int>& basis);
+  void SaveState() {
+    solution_state_ = variables_info_.GetStatusRow();
+    solution_state_has_been_set_externally_ = false;
+  }
+  void SetNonBasicVariableStatusAndDeriveValue(int col, VariableStatus status) {
+    variables_info_.UpdateToNonBasicStatus(col, status);
+    variable_values_.SetNonBasicVariableValueFromStatus(col);
+  }
+  void UpdateBasis(int entering_col, int basis_row, VariableStatus leaving_status) {
+    const int leaving_col = basis_[basis_row];
+    variables_info_.UpdateToNonBasicStatus(leaving_col, leaving_status);
+    basis_[basis_row] = entering_col;
+    variables_info_.UpdateToBasicStatus(entering_col);
+    update_row_.Invalidate();
+  }
+  void UseSingletonColumnInInitialBasis(std::vector<int>* basis);
+  void CorrectErrorsOnVariableValues();
+  void ComputeVariableValuesError();
+  void ComputeDirection(int col);
+  template <bool positive>
+  Fractional GetRatio(const std::vector<Fractional>& lb, const std::vector<Fractional>& ub,
+                      int row) const;
+  template <bool positive>
+  Fractional ComputeHarrisRatioAndLeavingCandidates(Fractional bound_flip_ratio,
+                                                    SparseColumn* leaving_candidates) const;
+  Status ChooseLeavingVariableRow(int entering_col, Fractional reduced_cost,
+                                  bool* refactorize, int* leaving_row,
+                                  Fractional* step_length, Fractional* target_bound);
+  void PrimalPhaseIChooseLeavingVariableRow(int entering_col, Fractional reduced_cost,
+                                            bool* refactorize, int* leaving_row,
+                                            Fractional* step_length,
+                                            Fractional* target_bound) const;
+  Status DualChooseLeavingVariableRow(int* leaving_row, Fractional* cost_variation,
+                                      Fractional* target_bound);
+  void DualPhaseIUpdatePrice(int leaving_row, int entering_col);
+  template <bool use_dense_update = false>
+  void OnDualPriceChange(const std::vector<Fractional>& squared_norms, int row,
+                         VariableType type, Fractional threshold);
+  void DualPhaseIUpdatePriceOnReducedCostChange(const std::vector<int>& cols);
+  Status DualPhaseIChooseLeavingVariableRow(int* leaving_row, Fractional* cost_variation,
+                                            Fractional* target_bound);
+  void MakeBoxedVariableDualFeasible(const std::vector<int>& cols, bool update_basic_values);
+  Fractional ComputeStepToMoveBasicVariableToBound(int leaving_row, Fractional target_bound) {
+    const int leaving_col = basis_[leaving_row];
+    const Fractional unscaled_step = variable_values_.Get(leaving_col) - target_bound;
+    return unscaled_step / direction_[leaving_row];
+  }
+  void PermuteBasis();
+  Status UpdateAndPivot(int entering_col, int leaving_row, Fractional target_bound);
+  Status RefactorizeBasisIfNeeded(bool* refactorize) {
+    if (*refactorize && !basis_factorization_.IsRefactorized()) {
+      MILP_RETURN_IF_ERROR(basis_factorization_.Refactorize());
+      update_row_.Invalidate();
+      PermuteBasis();
+    }
+    *refactorize = false;
+    return Status::OK();
+  }
+  Status PrimalMinimize(TimeLimit* time_limit);
+  Status DualMinimize(bool feasibility_phase, TimeLimit* time_limit);
+  Status PrimalPush(TimeLimit* time_limit);
+  Fractional ComputeObjectiveValue() const {
+    return PreciseScalarProduct(objective_, variable_values_.GetDenseRow());
+  }
+  Fractional ComputeInitialProblemObjectiveValue() const {
+    const Fractional sum = PreciseScalarProduct(objective_, variable_values_.GetDenseRow());
+    return objective_scaling_factor_ * (sum + objective_offset_);
+  }
+  int ComputeNumberOfSuperBasicVariables() const {
+    int n = 0;
+    for (int col = 0; col < num_cols_; ++col)
+      if (variables_info_.GetStatusRow()[col] == VariableStatus::FREE &&
+          variable_values_.Get(col) != 0.0)
+        ++n;
+    return n;
+  }
+  void AdvanceDeterministicTime(TimeLimit* tl) {
+    const double cur = DeterministicTime();
+    tl->AdvanceDeterministicTime(cur - last_deterministic_time_update_);
+    last_deterministic_time_update_ = cur;
+  }
+  void OnIterationDone(TimeLimit* tl) {
+    ++num_iterations_;
+    if (record_iteration_times) iteration_times.push_back(tl->GetElapsedTime());
+    if (iteration_hook) iteration_hook(num_iterations_);
+  }
+
+  DeviceLp device_;  // must outlive (be declared before) its users below
+  bool device_matrix_uploaded_ = false;
+  ProblemStatus problem_status_ = ProblemStatus::INIT;
+  int num_rows_ = 0;
+  int num_cols_ = 0;
+  int first_slack_col_ = 0;
+  CompactSparseMatrix compact_matrix_;
+  CompactSparseMatrix transposed_matrix_;
+  Fractional primal_objective_limit_ = kInfinity;
+  Fractional dual_objective_limit_ = kInfinity;
+  std::vector<Fractional> objective_;
+  Fractional objective_offset_ = 0.0;
+  Fractional objective_scaling_factor_ = 1.0;
+  std::vector<Fractional> dual_infeasibility_improvement_direction_;
+  int num_dual_infeasible_positions_ = 0;
+  ScatteredVector initially_all_zero_scratchpad_;
+  std::vector<int> basis_;
+  Fractional solution_objective_value_ = 0.0;
+  std::vector<Fractional> solution_dual_values_;
+  std::vector<Fractional> solution_reduced_costs_;
+  std::vector<Fractional> solution_primal_ray_;
+  std::vector<Fractional> solution_dual_ray_;
+  std::vector<Fractional> solution_dual_ray_row_combination_;
+  std::vector<VariableStatus> solution_state_;
+  bool solution_state_has_been_set_externally_ = true;
+  std::vector<Fractional> variable_starting_values_;
+  bool notify_that_matrix_is_unchanged_ = false;
+  ScatteredVector direction_;
+  Fractional direction_infinity_norm_ = 0.0;
+  std::vector<Fractional> error_;
+  Rng random_;
+  GlopParameters parameters_;
+  GlopParameters initial_parameters_;
+  BasisFactorization basis_factorization_;
+  VariablesInfo variables_info_;
+  PrimalEdgeNorms primal_edge_norms_;
+  DualEdgeNorms dual_edge_norms_;
+  DynamicMaximum dual_prices_;
+  VariableValues variable_values_;
+  UpdateRow update_row_;
+  ReducedCosts reduced_costs_;
+  EnteringVariable entering_variable_;
+  PrimalPrices primal_prices_;
+  std::vector<Fractional> dual_pricing_vector_;
+  std::vector<int> bound_flip_candidates_;
+  int64_t num_iterations_ = 0;
+  int64_t num_update_price_operations_ = 0;
+  double last_deterministic_time_update_ = 0.0;
+  Phase phase_ = Phase::FEASIBILITY;
+  bool objective_limit_reached_ = false;
+  SparseColumn leaving_candidates_;
+  std::vector<int> equivalent_leaving_choices_;
+};
+
+RevisedSimplex::RevisedSimplex()
+    : random_(42),
+      basis_factorization_(&compact_matrix_, &basis_),
+      variables_info_(compact_matrix_),
+      primal_edge_norms_(compact_matrix_, variables_info_, basis_factorization_, &device_),
+      dual_edge_norms_(basis_factorization_),
+      dual_prices_(&random_),
+      variable_values_(parameters_, compact_matrix_, basis_, variables_info_,
+                       basis_factorization_, &dual_edge_norms_, &dual_prices_, &device_),
+      update_row_(compact_matrix_, transposed_matrix_, variables_info_, basis_,
+                  basis_factorization_, &device_),
+      reduced_costs_(compact_matrix_, objective_, basis_, variables_info_,
+                     basis_factorization_, &random_, &device_),
+      entering_variable_(variables_info_, &random_, &reduced_costs_),
+      primal_prices_(&random_, variables_info_, &primal_edge_norms_, &reduced_costs_) {
+  SetParameters(parameters_);
+}
+
+// revised_simplex.cc:139-635
+Status RevisedSimplex::Solve(const LinearProgram& lp, TimeLimit* time_limit) {
+  struct Cleanup {
+    std::function<void()> f;
+    ~Cleanup() { f(); }
+  } cleanup{[this, time_limit]() { AdvanceDeterministicTime(time_limit); }};
+  iteration_times.clear();
+  MILP_RETURN_IF_ERROR(Initialize(lp));
+  dual_infeasibility_improvement_direction_.clear();
+  update_row_.Invalidate();
+  problem_status_ = ProblemStatus::INIT;
+  phase_ = Phase::FEASIBILITY;
+  num_iterations_ = 0;
+  solution_state_has_been_set_externally_ = true;
+
+  const bool use_dual = parameters_.use_dual_simplex;
+  primal_edge_norms_.SetPricingRule(parameters_.feasibility_rule);
+  if (use_dual) {
+    if (parameters_.perturb_costs_in_dual_simplex) reduced_costs_.PerturbCosts();
+    if (parameters_.use_dedicated_dual_feasibility_algorithm) {
+      variables_info_.MakeBoxedVariableRelevant(false);
+      MILP_RETURN_IF_ERROR(DualMinimize(phase_ == Phase::FEASIBILITY, time_limit));
+      if (problem_status_ != ProblemStatus::DUAL_INFEASIBLE) {
+        MILP_RETURN_IF_ERROR(basis_factorization_.Refactorize());
+        PermuteBasis();
+        variables_info_.MakeBoxedVariableRelevant(true);
+        reduced_costs_.MakeReducedCostsPrecise();
+        MakeBoxedVariableDualFeasible(
+            variables_info_.GetNonBasicBoxedVariables().ToVector(), false);
+        variable_values_.RecomputeBasicVariableValues();
+      }
+    } else {
+      reduced_costs_.MakeReducedCostsPrecise();
+      bool refactorize = reduced_costs_.NeedsBasisRefactorization();
+      MILP_RETURN_IF_ERROR(RefactorizeBasisIfNeeded(&refactorize));
+      const Fractional initial_infeasibility =
+          reduced_costs_.ComputeMaximumDualInfeasibilityOnNonBoxedVariables();
+      if (initial_infeasibility < reduced_costs_.GetDualFeasibilityTolerance()) {
+        problem_status_ = ProblemStatus::DUAL_FEASIBLE;
+        MakeBoxedVariableDualFeasible(
+            variables_info_.GetNonBasicBoxedVariables().ToVector(), false);
+        variable_values_.RecomputeBasicVariableValues();
+      } else {
+        variables_info_.TransformToDualPhaseIProblem(
+            reduced_costs_.GetDualFeasibilityTolerance(), reduced_costs_.GetReducedCosts());
+        std::vector<Fractional> zero;
+        variable_values_.ResetAllNonBasicVariableValues(zero);
+        variable_values_.RecomputeBasicVariableValues();
+        MILP_RETURN_IF_ERROR(DualMinimize(false, time_limit));
+        variables_info_.EndDualPhaseI(reduced_costs_.GetDualFeasibilityTolerance(),
+                                      reduced_costs_.GetFullReducedCosts());
+        variable_values_.ResetAllNonBasicVariableValues(variable_starting_values_);
+        variable_values_.RecomputeBasicVariableValues();
+        if (problem_status_ == ProblemStatus::OPTIMAL) {
+          if (reduced_costs_.ComputeMaximumDualInfeasibility() <
+              reduced_costs_.GetDualFeasibilityTolerance() + 1e-6) {
+            problem_status_ = ProblemStatus::DUAL_FEASIBLE;
+          } else {
+            problem_status_ = ProblemStatus::DUAL_INFEASIBLE;
+          }
+        }
+      }
+    }
+  } else {
+    MILP_RETURN_IF_ERROR(PrimalMinimize(time_limit));
+    if (problem_status_ != ProblemStatus::PRIMAL_INFEASIBLE) {
+      InitializeObjectiveAndTestIfUnchanged(lp);
+      reduced_costs_.ResetForNewObjective();
+    }
+  }
+
+  phase_ = Phase::OPTIMIZATION;
+  primal_edge_norms_.SetPricingRule(parameters_.optimization_rule);
+
+  for (int num_optims = 0;
+       num_optims <= parameters_.max_number_of_reoptimizations &&
+       !objective_limit_reached_ &&
+       (num_iterations_ == 0 ||
+        num_iterations_ < parameters_.max_number_of_iterations ||
+        parameters_.max_number_of_iterations < 0) &&
+       !time_limit->LimitReached() &&
+       (problem_status_ == ProblemStatus::PRIMAL_FEASIBLE ||
+        problem_status_ == ProblemStatus::DUAL_FEASIBLE);
+       ++num_optims) {
+    if (problem_status_ == ProblemStatus::PRIMAL_FEASIBLE) {
+      MILP_RETURN_IF_ERROR(PrimalMinimize(time_limit));
+    } else {
+      MILP_RETURN_IF_ERROR(DualMinimize(phase_ == Phase::FEASIBILITY, time_limit));
+    }
+    variable_values_.ResetAllNonBasicVariableValues(variable_starting_values_);
+    MILP_RETURN_IF_ERROR(basis_factorization_.Refactorize());
+    PermuteBasis();
+    variable_values_.RecomputeBasicVariableValues();
+    reduced_costs_.ClearAndRemoveCostShifts();
+
+    if (problem_status_ == ProblemStatus::PRIMAL_UNBOUNDED) {
+      const Fractional tolerance = parameters_.solution_feasibility_tolerance;
+      if (reduced_costs_.ComputeMaximumDualResidual() > tolerance ||
+          variable_values_.ComputeMaximumPrimalResidual() > tolerance ||
+          variable_values_.ComputeMaximumPrimalInfeasibility() > tolerance) {
+        if (parameters_.change_status_to_imprecise) {
+          problem_status_ = ProblemStatus::IMPRECISE;
+        }
+        break;
+      }
+      double max_magnitude = 0.0;
+      double min_distance = kInfinity;
+      const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+      const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+      double cost_delta = 0.0;
+      for (int col = 0; col < num_cols_; ++col) {
+        cost_delta += solution_primal_ray_[col] * objective_[col];
+        if (solution_primal_ray_[col] > 0 && ub[col] != kInfinity) {
+          const Fractional value = variable_values_.Get(col);
+          const Fractional distance =
+              (ub[col] - value + tolerance) / solution_primal_ray_[col];
+          min_distance = std::min(distance, min_distance);
+          max_magnitude = std::max(solution_primal_ray_[col], max_magnitude);
+        }
+        if (solution_primal_ray_[col] < 0 && lb[col] != -kInfinity) {
+          const Fractional value = variable_values_.Get(col);
+          const Fractional distance =
+              (value - lb[col] + tolerance) / -solution_primal_ray_[col];
+          min_distance = std::min(distance, min_distance);
+          max_magnitude = std::max(-solution_primal_ray_[col], max_magnitude);
+        }
+      }
+      if (min_distance * std::fabs(cost_delta) < 1 &&
+          reduced_costs_.ComputeMaximumDualInfeasibility() <= tolerance) {
+        problem_status_ = ProblemStatus::OPTIMAL;
+      }
+      break;
+    }
+    if (problem_status_ == ProblemStatus::DUAL_UNBOUNDED) {
+      const Fractional tolerance = parameters_.solution_feasibility_tolerance;
+      if (reduced_costs_.ComputeMaximumDualResidual() > tolerance ||
+          variable_values_.ComputeMaximumPrimalResidual() > tolerance ||
+          reduced_costs_.ComputeMaximumDualInfeasibility() > tolerance) {
+        if (parameters_.change_status_to_imprecise) {
+          problem_status_ = ProblemStatus::IMPRECISE;
+        }
+      }
+      const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+      const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+      Fractional implied_lb = 0.0;
+      Fractional error = 0.0;
+      for (int col = 0; col < num_cols_; ++col) {
+        const Fractional coeff = solution_dual_ray_row_combination_[col];
+        if (coeff > 0) {
+          if (lb[col] == -kInfinity) {
+            error = std::max(error, coeff);
+          } else {
+            implied_lb += coeff * lb[col];
+          }
+        } else if (coeff < 0) {
+          if (ub[col] == kInfinity) {
+            error = std::max(error, -coeff);
+          } else {
+            implied_lb += coeff * ub[col];
+          }
+        }
+      }
+      if (implied_lb < tolerance || error > tolerance) {
+        if (parameters_.change_status_to_imprecise) {
+          problem_status_ = ProblemStatus::IMPRECISE;
+        }
+      }
+      break;
+    }
+    if (problem_status_ == ProblemStatus::OPTIMAL) {
+      const Fractional solution_tolerance = parameters_.solution_feasibility_tolerance;
+      const Fractional primal_residual = variable_values_.ComputeMaximumPrimalResidual();
+      const Fractional dual_residual = reduced_costs_.ComputeMaximumDualResidual();
+      if (primal_residual > solution_tolerance || dual_residual > solution_tolerance) {
+        if (parameters_.change_status_to_imprecise) {
+          problem_status_ = ProblemStatus::IMPRECISE;
+        }
+      } else {
+        const Fractional primal_tolerance =
+            std::max(primal_residual, parameters_.primal_feasibility_tolerance);
+        const Fractional dual_tolerance =
+            std::max(dual_residual, parameters_.dual_feasibility_tolerance);
+        const Fractional primal_infeasibility =
+            variable_values_.ComputeMaximumPrimalInfeasibility();
+        const Fractional dual_infeasibility =
+            reduced_costs_.ComputeMaximumDualInfeasibility();
+        if (primal_infeasibility > primal_tolerance &&
+            dual_infeasibility > dual_tolerance) {
+          if (parameters_.change_status_to_imprecise) {
+            problem_status_ = ProblemStatus::IMPRECISE;
+          }
+        } else if (primal_infeasibility > primal_tolerance) {
+          if (num_optims == parameters_.max_number_of_reoptimizations) break;
+          problem_status_ = ProblemStatus::DUAL_FEASIBLE;
+        } else if (dual_infeasibility > dual_tolerance) {
+          if (num_optims == parameters_.max_number_of_reoptimizations) break;
+          problem_status_ = ProblemStatus::PRIMAL_FEASIBLE;
+        }
+      }
+    }
+  }
+
+  if (parameters_.change_status_to_imprecise &&
+      problem_status_ != ProblemStatus::DUAL_INFEASIBLE) {
+    const Fractional tolerance = parameters_.solution_feasibility_tolerance;
+    if (variable_values_.ComputeMaximumPrimalResidual() > tolerance ||
+        reduced_costs_.ComputeMaximumDualResidual() > tolerance) {
+      problem_status_ = ProblemStatus::IMPRECISE;
+    } else if (problem_status_ == ProblemStatus::DUAL_FEASIBLE ||
+               problem_status_ == ProblemStatus::DUAL_UNBOUNDED ||
+               problem_status_ == ProblemStatus::PRIMAL_INFEASIBLE) {
+      if (reduced_costs_.ComputeMaximumDualInfeasibility() > tolerance) {
+        problem_status_ = ProblemStatus::IMPRECISE;
+      }
+    } else if (problem_status_ == ProblemStatus::PRIMAL_FEASIBLE ||
+               problem_status_ == ProblemStatus::PRIMAL_UNBOUNDED ||
+               problem_status_ == ProblemStatus::DUAL_INFEASIBLE) {
+      if (variable_values_.ComputeMaximumPrimalInfeasibility() > tolerance) {
+        problem_status_ = ProblemStatus::IMPRECISE;
+      }
+    }
+  }
+
+  if (!variable_starting_values_.empty()) {
+    const int num_super_basic = ComputeNumberOfSuperBasicVariables();
+    if (num_super_basic > 0 && parameters_.push_to_vertex &&
+        problem_status_ == ProblemStatus::OPTIMAL) {
+      phase_ = Phase::PUSH;
+      MILP_RETURN_IF_ERROR(PrimalPush(time_limit));
+    }
+  }
+
+  solution_objective_value_ = ComputeInitialProblemObjectiveValue();
+  solution_dual_values_ = reduced_costs_.GetDualValues();
+  solution_reduced_costs_ = reduced_costs_.GetReducedCosts();
+  SaveState();
+  if (lp.maximize) {
+    for (auto& v : solution_dual_values_) v = -v;
+    for (auto& v : solution_reduced_costs_) v = -v;
+  }
+  if (problem_status_ == ProblemStatus::DUAL_UNBOUNDED ||
+      problem_status_ == ProblemStatus::PRIMAL_UNBOUNDED) {
+    solution_objective_value_ =
+        (problem_status_ == ProblemStatus::DUAL_UNBOUNDED) ? kInfinity : -kInfinity;
+    if (lp.maximize) solution_objective_value_ = -solution_objective_value_;
+  }
+  variable_starting_values_.clear();
+  return Status::OK();
+}
+
+// revised_simplex.cc:836-926
+void RevisedSimplex::UseSingletonColumnInInitialBasis(std::vector<int>* basis) {
+  std::vector<int> singleton_column;
+  std::vector<Fractional> cost_variation(num_cols_, 0.0);
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  for (int col = 0; col < num_cols_; ++col) {
+    if (compact_matrix_.ColumnNumEntries(col) != 1) continue;
+    if (lb[col] == ub[col]) continue;
+    const Fractional slope = compact_matrix_.column(col).GetFirstCoefficient();
+    if (variable_values_.Get(col) == lb[col]) {
+      cost_variation[col] = objective_[col] / std::fabs(slope);
+    } else {
+      cost_variation[col] = -objective_[col] / std::fabs(slope);
+    }
+    singleton_column.push_back(col);
+  }
+  if (singleton_column.empty()) return;
+  std::sort(singleton_column.begin(), singleton_column.end(),
+            [&](int a, int b) { return cost_variation[a] < cost_variation[b]; });
+  const std::vector<Fractional>& values = variable_values_.GetDenseRow();
+  for (const int col : singleton_column) {
+    const int row = compact_matrix_.column(col).GetFirstRow();
+    if ((*basis)[row] == kInvalidCol) (*basis)[row] = col;
+    if (error_[row] == 0.0) continue;
+    const Fractional coeff = compact_matrix_.column(col).GetFirstCoefficient();
+    const Fractional new_value = values[col] + error_[row] / coeff;
+    if (new_value >= lb[col] && new_value <= ub[col]) {
+      error_[row] = 0.0;
+      (*basis)[row] = col;
+      continue;
+    }
+    const Fractional box_width = variables_info_.GetBoundDifference(col);
+    const Fractional error_sign = error_[row] / coeff;
+    if (values[col] == lb[col] && error_sign > 0.0) {
+      error_[row] -= coeff * box_width;
+      SetNonBasicVariableStatusAndDeriveValue(col, VariableStatus::AT_UPPER_BOUND);
+      continue;
+    }
+    if (values[col] == ub[col] && error_sign < 0.0) {
+      error_[row] += coeff * box_width;
+      SetNonBasicVariableStatusAndDeriveValue(col, VariableStatus::AT_LOWER_BOUND);
+      continue;
+    }
+  }
+}
+
+// revised_simplex.cc:928-1002 + lp_data/matrix_utils.cc
+// AreFirstColumnsAndRowsExactlyEquals.
+bool RevisedSimplex::InitializeMatrixAndTestIfUnchanged(const LinearProgram& lp,
+                                                        bool* only_change_is_new_rows,
+                                                        bool* only_change_is_new_cols,
+                                                        int* num_new_cols) {
+  bool old_part_of_matrix_is_unchanged = true;
+  {
+    const int nr = num_rows_;
+    const int nc = first_slack_col_;
+    if (nr > lp.m || nr > compact_matrix_.num_rows() || nc > lp.n ||
+        nc > compact_matrix_.num_cols()) {
+      old_part_of_matrix_is_unchanged = false;
+    } else {
+      for (int col = 0; col < nc && old_part_of_matrix_is_unchanged; ++col) {
+        const int64_t a0 = lp.col_starts[col];
+        const int64_t na = lp.col_starts[col + 1] - a0;
+        const ColumnView b = compact_matrix_.column(col);
+        const int64_t end = std::min(na, b.n);
+        if (end < na && lp.row_idx[a0 + end] < nr) old_part_of_matrix_is_unchanged = false;
+        if (end < b.n && b.rows[end] < nr) old_part_of_matrix_is_unchanged = false;
+        for (int64_t i = 0; i < end && old_part_of_matrix_is_unchanged; ++i) {
+          if (lp.row_idx[a0 + i] != b.rows[i] || lp.vals[a0 + i] != b.coefs[i])
+            old_part_of_matrix_is_unchanged = false;
+        }
+      }
+    }
+  }
+  const int lp_first_slack = lp.n;
+  if (old_part_of_matrix_is_unchanged && lp.m == num_rows_ &&
+      lp_first_slack == first_slack_col_) {
+    if (transposed_matrix_.IsEmpty()) {
+      transposed_matrix_.PopulateFromTranspose(compact_matrix_);
+      device_matrix_uploaded_ = false;
+    }
+    if (!device_matrix_uploaded_) {
+      device_.UploadMatrix(compact_matrix_, transposed_matrix_);
+      device_matrix_uploaded_ = true;
+    }
+    return true;
+  }
+  *only_change_is_new_rows = old_part_of_matrix_is_unchanged && lp.m > num_rows_ &&
+                             lp_first_slack == first_slack_col_;
+  *only_change_is_new_cols = old_part_of_matrix_is_unchanged && lp.m == num_rows_ &&
+                             lp_first_slack > first_slack_col_;
+  *num_new_cols = *only_change_is_new_cols ? lp_first_slack - first_slack_col_ : 0;
+  first_slack_col_ = lp_first_slack;
+  num_rows_ = lp.m;
+  num_cols_ = lp_first_slack + lp.m;
+  compact_matrix_.PopulateFromSparseMatrixAndAddSlacks(lp.m, lp.n, lp.col_starts.data(),
+                                                       lp.row_idx.data(), lp.vals.data());
+  transposed_matrix_.PopulateFromTranspose(compact_matrix_);
+  device_.UploadMatrix(compact_matrix_, transposed_matrix_);
+  device_matrix_uploaded_ = true;
+  return false;
+}
+
+// revised_simplex.cc:1006-1052
+bool RevisedSimplex::OldBoundsAreUnchangedAndNewVariablesHaveOneBoundAtZero(
+    const LinearProgram& lp, int num_new_cols) {
+  const int first_new_col = first_slack_col_ - num_new_cols;
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  for (int col = 0; col < first_new_col; ++col) {
+    if (lb[col] != lp.col_lb[col] || ub[col] != lp.col_ub[col]) return false;
+  }
+  for (int col = first_new_col; col < first_slack_col_; ++col) {
+    if (lp.col_lb[col] != 0.0 && lp.col_ub[col] != 0.0) return false;
+  }
+  for (int row = 0; row < num_rows_; ++row) {
+    const int col = first_slack_col_ + row;
+    if (lb[col - num_new_cols] != -lp.row_ub[row] ||
+        ub[col - num_new_cols] != -lp.row_lb[row])
+      return false;
+  }
+  return true;
+}
+
+// revised_simplex.cc:1054-1095
+bool RevisedSimplex::InitializeObjectiveAndTestIfUnchanged(const LinearProgram& lp) {
+  bool unchanged = true;
+  objective_.resize(num_cols_, 0.0);
+  for (int col = lp.n; col < num_cols_; ++col) {
+    if (objective_[col] != 0.0) {
+      unchanged = false;
+      objective_[col] = 0.0;
+    }
+  }
+  if (lp.maximize) {
+    for (int col = 0; col < lp.n; ++col) {
+      const Fractional coeff = -lp.obj[col];
+      if (objective_[col] != coeff) {
+        unchanged = false;
+        objective_[col] = coeff;
+      }
+    }
+    objective_offset_ = -lp.obj_offset;
+    objective_scaling_factor_ = -lp.obj_scale;
+  } else {
+    for (int col = 0; col < lp.n; ++col) {
+      const Fractional coeff = lp.obj[col];
+      if (objective_[col] != coeff) {
+        unchanged = false;
+        objective_[col] = coeff;
+      }
+    }
+    objective_offset_ = lp.obj_offset;
+    objective_scaling_factor_ = lp.obj_scale;
+  }
+  return unchanged;
+}
+
+// revised_simplex.cc:1097-1127
+void RevisedSimplex::InitializeObjectiveLimit() {
+  objective_limit_reached_ = false;
+  for (const bool set_dual : {true, false}) {
+    const Fractional limit = (objective_scaling_factor_ >= 0.0) != set_dual
+                                 ? parameters_.objective_lower_limit
+                                 : parameters_.objective_upper_limit;
+    const Fractional shifted_limit = limit / objective_scaling_factor_ - objective_offset_;
+    if (set_dual) {
+      dual_objective_limit_ = shifted_limit;
+    } else {
+      primal_objective_limit_ = shifted_limit;
+    }
+  }
+}
+
+// revised_simplex.cc:1134-1278
+Status RevisedSimplex::CreateInitialBasis() {
+  variables_info_.InitializeToDefaultStatus();
+  variable_values_.ResetAllNonBasicVariableValues(variable_starting_values_);
+  std::vector<int> basis(num_rows_, kInvalidCol);
+  for (int row = 0; row < num_rows_; ++row) basis[row] = first_slack_col_ + row;
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  if (!parameters_.use_dual_simplex && parameters_.initial_basis != 3 &&
+      parameters_.exploit_singleton_column_in_initial_basis) {
+    for (int col = 0; col < num_cols_; ++col) {
+      if (compact_matrix_.ColumnNumEntries(col) != 1) continue;
+      const VariableStatus status = variables_info_.GetStatusRow()[col];
+      const Fractional objective = objective_[col];
+      if (objective > 0 && IsFinite(lb[col]) && status == VariableStatus::AT_UPPER_BOUND) {
+        SetNonBasicVariableStatusAndDeriveValue(col, VariableStatus::AT_LOWER_BOUND);
+      } else if (objective < 0 && IsFinite(ub[col]) &&
+                 status == VariableStatus::AT_LOWER_BOUND) {
+        SetNonBasicVariableStatusAndDeriveValue(col, VariableStatus::AT_UPPER_BOUND);
+      }
+    }
+    ComputeVariableValuesError();
+    basis.assign(num_rows_, kInvalidCol);
+    UseSingletonColumnInInitialBasis(&basis);
+    for (int row = 0; row < num_rows_; ++row)
+      if (basis[row] == kInvalidCol) basis[row] = first_slack_col_ + row;
+  }
+  if (parameters_.initial_basis == 0) return InitializeFirstBasis(basis);
+  if (parameters_.initial_basis == 2) {  // TRIANGULAR
+    int num_fixed_variables = 0;
+    for (int row = 0; row < static_cast<int>(basis.size()); ++row) {
+      const int col = basis[row];
+      if (lb[col] == ub[col]) {
+        basis[row] = kInvalidCol;
+        ++num_fixed_variables;
+      }
+    }
+    if (num_fixed_variables != 0) {
+      if (parameters_.use_dual_simplex) {
+        CompleteTriangularBasis<true>(compact_matrix_, objective_, lb, ub,
+                                      variables_info_.GetTypeRow(), num_cols_, &basis);
+      } else {
+        CompleteTriangularBasis<false>(compact_matrix_, objective_, lb, ub,
+                                       variables_info_.GetTypeRow(), num_cols_, &basis);
+      }
+      const Status status = InitializeFirstBasis(basis);
+      if (status.ok()) return status;
+      for (int row = 0; row < num_rows_; ++row) basis[row] = first_slack_col_ + row;
+    }
+  }
+  // MAROS / BIXBY are not restated (non-default): they behave as NONE here.
+  return InitializeFirstBasis(basis);
+}
+
+// revised_simplex.cc:1280-1332
+Status RevisedSimplex::InitializeFirstBasis(const std::vector<int>& basis) {
+  basis_ = basis;
+  basis_.resize(num_rows_, kInvalidCol);
+  for (int row = 0; row < num_rows_; ++row)
+    if (basis_[row] == kInvalidCol) basis_[row] = first_slack_col_ + row;
+  MILP_RETURN_IF_ERROR(basis_factorization_.Initialize());
+  PermuteBasis();
+  const Fractional cond = basis_factorization_.ComputeInfinityNormConditionNumberUpperBound();
+  if (cond > parameters_.initial_condition_number_threshold) {
+    return Status(Status::ERROR_LU, "The matrix condition number upper bound is too high");
+  }
+  for (int row = 0; row < num_rows_; ++row) variables_info_.UpdateToBasicStatus(basis_[row]);
+  variable_values_.ResetAllNonBasicVariableValues(variable_starting_values_);
+  variable_values_.RecomputeBasicVariableValues();
+  return Status::OK();
+}
+
+// revised_simplex.cc:1334-1565
+Status RevisedSimplex::Initialize(const LinearProgram& lp) {
+  parameters_ = initial_parameters_;
+  PropagateParameters();
+  int num_new_cols = 0;
+  bool only_change_is_new_rows = false;
+  bool only_change_is_new_cols = false;
+  bool matrix_is_unchanged = true;
+  bool only_new_bounds = false;
+  if (solution_state_.empty() || !notify_that_matrix_is_unchanged_) {
+    matrix_is_unchanged = InitializeMatrixAndTestIfUnchanged(
+        lp, &only_change_is_new_rows, &only_change_is_new_cols, &num_new_cols);
+    only_new_bounds = only_change_is_new_cols && num_new_cols > 0 &&
+                      OldBoundsAreUnchangedAndNewVariablesHaveOneBoundAtZero(lp, num_new_cols);
+  }
+  notify_that_matrix_is_unchanged_ = false;
+  const bool objective_is_unchanged = InitializeObjectiveAndTestIfUnchanged(lp);
+  const bool bounds_are_unchanged = variables_info_.LoadBoundsAndReturnTrueIfUnchanged(
+      lp.col_lb, lp.col_ub, lp.row_lb, lp.row_ub);
+  if (matrix_is_unchanged && parameters_.allow_simplex_algorithm_change) {
+    if (objective_is_unchanged && !bounds_are_unchanged) {
+      parameters_.use_dual_simplex = true;
+      PropagateParameters();
+    }
+    if (bounds_are_unchanged && !objective_is_unchanged) {
+      parameters_.use_dual_simplex = false;
+      PropagateParameters();
+    }
+  }
+  InitializeObjectiveLimit();
+
+  bool solve_from_scratch = true;
+  if (!solution_state_.empty() && !solution_state_has_been_set_externally_) {
+    if (!parameters_.use_dual_simplex) {
+      dual_edge_norms_.Clear();
+      dual_pricing_vector_.clear();
+      if (matrix_is_unchanged && bounds_are_unchanged) {
+        reduced_costs_.ClearAndRemoveCostShifts();
+        solve_from_scratch = false;
+      } else if (only_change_is_new_cols && only_new_bounds) {
+        variables_info_.InitializeFromBasisState(first_slack_col_, num_new_cols,
+                                                 solution_state_);
+        variable_values_.ResetAllNonBasicVariableValues(variable_starting_values_);
+        const int first_new_col = first_slack_col_ - num_new_cols;
+        for (int& c : basis_)
+          if (c >= first_new_col) c += num_new_cols;
+        primal_edge_norms_.Clear();
+        reduced_costs_.ClearAndRemoveCostShifts();
+        solve_from_scratch = false;
+      }
+    } else {
+      primal_edge_norms_.Clear();
+      if (objective_is_unchanged) {
+        if (matrix_is_unchanged) {
+          if (!bounds_are_unchanged) {
+            variables_info_.InitializeFromBasisState(first_slack_col_, 0, solution_state_);
+            variable_values_.ResetAllNonBasicVariableValues(variable_starting_values_);
+            variable_values_.RecomputeBasicVariableValues();
+          }
+          solve_from_scratch = false;
+        } else if (only_change_is_new_rows) {
+          variables_info_.InitializeFromBasisState(first_slack_col_, 0, solution_state_);
+          dual_edge_norms_.ResizeOnNewRows(num_rows_);
+          reduced_costs_.ClearAndRemoveCostShifts();
+          dual_pricing_vector_.clear();
+          if (InitializeFirstBasis(basis_).ok()) solve_from_scratch = false;
+        }
+      }
+    }
+  }
+
+  if (solve_from_scratch && !solution_state_.empty()) {
+    basis_factorization_.Clear();
+    reduced_costs_.ClearAndRemoveCostShifts();
+    primal_edge_norms_.Clear();
+    dual_edge_norms_.Clear();
+    dual_pricing_vector_.clear();
+    variables_info_.InitializeFromBasisState(first_slack_col_, 0, solution_state_);
+    std::vector<int> candidates = variables_info_.GetIsBasicBitRow().ToVector();
+    if (static_cast<int>(candidates.size()) == num_rows_) {
+      basis_ = candidates;
+      if (InitializeFirstBasis(basis_).ok()) solve_from_scratch = false;
+    }
+    if (solve_from_scratch) {
+      basis_ = basis_factorization_.ComputeInitialBasis(candidates);
+      variables_info_.ChangeUnusedBasicVariablesToFree(basis_);
+      variables_info_.SnapFreeVariablesToBound(parameters_.crossover_bound_snapping_distance,
+                                               variable_starting_values_);
+      if (InitializeFirstBasis(basis_).ok()) solve_from_scratch = false;
+    }
+  }
+
+  if (solve_from_scratch) {
+    basis_factorization_.Clear();
+    reduced_costs_.ClearAndRemoveCostShifts();
+    primal_edge_norms_.Clear();
+    dual_edge_norms_.Clear();
+    dual_pricing_vector_.clear();
+    MILP_RETURN_IF_ERROR(CreateInitialBasis());
+  }
+  return Status::OK();
+}
+
+// revised_simplex.cc:1663-1693
+void RevisedSimplex::CorrectErrorsOnVariableValues() {
+  const Fractional primal_residual = variable_values_.ComputeMaximumPrimalResidual();
+  if (primal_residual >=
+      parameters_.harris_tolerance_ratio * parameters_.primal_feasibility_tolerance) {
+    variable_values_.RecomputeBasicVariableValues();
+  }
+}
+
+void RevisedSimplex::ComputeVariableValuesError() {
+  device_.RowSums(variable_values_.GetDenseRow(), /*skip_basic=*/false, -1.0, &error_);
+}
+
+// revised_simplex.cc:1695-1720
+void RevisedSimplex::ComputeDirection(int col) {
+  basis_factorization_.RightSolveForProblemColumn(col, &direction_);
+  direction_infinity_norm_ = 0.0;
+  if (direction_.non_zeros.empty()) {
+    for (int row = 0; row < num_rows_; ++row) {
+      const Fractional value = direction_[row];
+      if (value != 0.0) {
+        direction_.non_zeros.push_back(row);
+        direction_infinity_norm_ = std::max(direction_infinity_norm_, std::fabs(value));
+      }
+    }
+  } else {
+    for (const int row : direction_.non_zeros) {
+      direction_infinity_norm_ =
+          std::max(direction_infinity_norm_, std::fabs(direction_[row]));
+    }
+  }
+}
+
+// revised_simplex.cc:1732-1754
+template <bool positive>
+Fractional RevisedSimplex::GetRatio(const std::vector<Fractional>& lb,
+                                    const std::vector<Fractional>& ub, int row) const {
+  const int col = basis_[row];
+  const Fractional direction = direction_[row];
+  const Fractional value = variable_values_.Get(col);
+  if (positive) {
+    if (direction > 0.0) return (ub[col] - value) / direction;
+    return (lb[col] - value) / direction;
+  } else {
+    if (direction > 0.0) return (value - lb[col]) / direction;
+    return (value - ub[col]) / direction;
+  }
+}
+
+// revised_simplex.cc:1756-1806
+template <bool positive>
+Fractional RevisedSimplex::ComputeHarrisRatioAndLeavingCandidates(
+    Fractional bound_flip_ratio, SparseColumn* leaving_candidates) const {
+  const Fractional harris_tolerance =
+      parameters_.harris_tolerance_ratio * parameters_.primal_feasibility_tolerance;
+  const Fractional minimum_delta =
+      parameters_.degenerate_ministep_factor * parameters_.primal_feasibility_tolerance;
+  Fractional harris_ratio = bound_flip_ratio;
+  leaving_candidates->Clear();
+  const Fractional threshold = basis_factorization_.IsRefactorized()
+                                   ? parameters_.minimum_acceptable_pivot
+                                   : parameters_.ratio_test_zero_threshold;
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  for (const int row : direction_.non_zeros) {
+    const Fractional magnitude = std::fabs(direction_[row]);
+    if (magnitude <= threshold) continue;
+    const Fractional ratio = GetRatio<positive>(lb, ub, row);
+    if (ratio <= harris_ratio) {
+      leaving_candidates->SetCoefficient(row, ratio);
+      harris_ratio = std::min(harris_ratio, std::max(minimum_delta / magnitude,
+                                                     ratio + harris_tolerance / magnitude));
+    }
+  }
+  return harris_ratio;
+}
+
+namespace {
+bool IsRatioMoreOrEquallyStable(Fractional candidate, Fractional current) {
+  if (current >= 0.0) return candidate >= 0.0 && candidate <= current;
+  return candidate >= current;
+}
+}  // namespace
+
+// revised_simplex.cc:1829-2003
+Status RevisedSimplex::ChooseLeavingVariableRow(int entering_col, Fractional reduced_cost,
+                                                bool* refactorize, int* leaving_row,
+                                                Fractional* step_length,
+                                                Fractional* target_bound) {
+  equivalent_leaving_choices_.clear();
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  while (true) {
+    const Fractional entering_value = variable_values_.Get(entering_col);
+    Fractional current_ratio = (reduced_cost > 0.0) ? entering_value - lb[entering_col]
+                                                    : ub[entering_col] - entering_value;
+    const Fractional harris_ratio =
+        (reduced_cost > 0.0)
+            ? ComputeHarrisRatioAndLeavingCandidates<true>(current_ratio, &leaving_candidates_)
+            : ComputeHarrisRatioAndLeavingCandidates<false>(current_ratio,
+                                                            &leaving_candidates_);
+    if (current_ratio <= harris_ratio) {
+      *leaving_row = kInvalidRow;
+      *step_length = current_ratio;
+      break;
+    }
+    Fractional pivot_magnitude = 0.0;
+    *leaving_row = kInvalidRow;
+    equivalent_leaving_choices_.clear();
+    for (int64_t k = 0; k < leaving_candidates_.num_entries(); ++k) {
+      const Fractional ratio = leaving_candidates_.coefs[k];
+      if (ratio > harris_ratio) continue;
+      const int row = leaving_candidates_.rows[k];
+      const Fractional candidate_magnitude = std::fabs(direction_[row]);
+      if (candidate_magnitude < pivot_magnitude) continue;
+      if (candidate_magnitude == pivot_magnitude) {
+        if (!IsRatioMoreOrEquallyStable(ratio, current_ratio)) continue;
+        if (ratio == current_ratio) {
+          equivalent_leaving_choices_.push_back(row);
+          continue;
+        }
+      }
+      equivalent_leaving_choices_.clear();
+      current_ratio = ratio;
+      pivot_magnitude = candidate_magnitude;
+      *leaving_row = row;
+    }
+    if (!equivalent_leaving_choices_.empty()) {
+      equivalent_leaving_choices_.push_back(*leaving_row);
+      *leaving_row = equivalent_leaving_choices_[UniformInt(
+          random_, static_cast<int>(equivalent_leaving_choices_.size()) - 1)];
+    }
+    if (current_ratio <= 0.0) {
+      const Fractional minimum_delta =
+          parameters_.degenerate_ministep_factor * parameters_.primal_feasibility_tolerance;
+      *step_length = minimum_delta / pivot_magnitude;
+    } else {
+      *step_length = current_ratio;
+    }
+    if (pivot_magnitude < parameters_.small_pivot_threshold * direction_infinity_norm_) {
+      if (!basis_factorization_.IsRefactorized()) {
+        *refactorize = true;
+        return Status::OK();
+      }
+    }
+    break;
+  }
+  if (*leaving_row != kInvalidRow) {
+    const bool is_reduced_cost_positive = (reduced_cost > 0.0);
+    const bool is_leaving_coeff_positive = (direction_[*leaving_row] > 0.0);
+    *target_bound = (is_reduced_cost_positive == is_leaving_coeff_positive)
+                        ? ub[basis_[*leaving_row]]
+                        : lb[basis_[*leaving_row]];
+  }
+  return Status::OK();
+}
+
+namespace {
+// revised_simplex.cc:2010-2035
+struct BreakPoint {
+  int row;
+  Fractional ratio;
+  Fractional coeff_magnitude;
+  Fractional target_bound;
+  bool operator<(const BreakPoint& o) const {
+    if (ratio == o.ratio) {
+      if (coeff_magnitude == o.coeff_magnitude) return row > o.row;
+      return coeff_magnitude < o.coeff_magnitude;
+    }
+    return ratio > o.ratio;
+  }
+};
+}  // namespace
+
+// revised_simplex.cc:2039-2145
+void RevisedSimplex::PrimalPhaseIChooseLeavingVariableRow(
+    int entering_col, Fractional reduced_cost, bool* refactorize, int* leaving_row,
+    Fractional* step_length, Fractional* target_bound) const {
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  const Fractional entering_value = variable_values_.Get(entering_col);
+  Fractional current_ratio = (reduced_cost > 0.0) ? entering_value - lb[entering_col]
+                                                  : ub[entering_col] - entering_value;
+  std::vector<BreakPoint> breakpoints;
+  const Fractional tolerance = parameters_.primal_feasibility_tolerance;
+  for (const int row : direction_.non_zeros) {
+    const Fractional direction = reduced_cost > 0.0 ? direction_[row] : -direction_[row];
+    const Fractional magnitude = std::fabs(direction);
+    if (magnitude < tolerance) continue;
+    const int col = basis_[row];
+    const Fractional value = variable_values_.Get(col);
+    const Fractional lower_bound = lb[col];
+    const Fractional upper_bound = ub[col];
+    const Fractional to_lower = (lower_bound - tolerance - value) / direction;
+    const Fractional to_upper = (upper_bound + tolerance - value) / direction;
+    if (to_lower >= 0.0 && to_lower < current_ratio)
+      breakpoints.push_back(BreakPoint{row, to_lower, magnitude, lower_bound});
+    if (to_upper >= 0.0 && to_upper < current_ratio)
+      breakpoints.push_back(BreakPoint{row, to_upper, magnitude, upper_bound});
+  }
+  std::make_heap(breakpoints.begin(), breakpoints.end());
+  Fractional improvement = std::fabs(reduced_cost);
+  Fractional best_magnitude = 0.0;
+  *leaving_row = kInvalidRow;
+  while (!breakpoints.empty()) {
+    const BreakPoint top = breakpoints.front();
+    if (top.coeff_magnitude > best_magnitude) {
+      *leaving_row = top.row;
+      current_ratio = top.ratio;
+      best_magnitude = top.coeff_magnitude;
+      *target_bound = top.target_bound;
+    }
+    improvement -= top.coeff_magnitude;
+    if (improvement <= 0.0) break;
+    std::pop_heap(breakpoints.begin(), breakpoints.end());
+    breakpoints.pop_back();
+  }
+  if (*leaving_row != kInvalidRow) {
+    const Fractional threshold = parameters_.small_pivot_threshold * direction_infinity_norm_;
+    if (best_magnitude < threshold && !basis_factorization_.IsRefactorized()) {
+      *refactorize = true;
+      return;
+    }
+  }
+  *step_length = current_ratio;
+}
+
+// revised_simplex.cc:2148-2181
+Status RevisedSimplex::DualChooseLeavingVariableRow(int* leaving_row,
+                                                    Fractional* cost_variation,
+                                                    Fractional* target_bound) {
+  if (dual_prices_.Size() == 0) {
+    variable_values_.RecomputeDualPrices(parameters_.dual_price_prioritize_norm);
+  }
+  *leaving_row = dual_prices_.GetMaximum();
+  if (*leaving_row == kInvalidRow) return Status::OK();
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  const int leaving_col = basis_[*leaving_row];
+  const Fractional value = variable_values_.Get(leaving_col);
+  if (value < lb[leaving_col]) {
+    *cost_variation = lb[leaving_col] - value;
+    *target_bound = lb[leaving_col];
+  } else {
+    *cost_variation = ub[leaving_col] - value;
+    *target_bound = ub[leaving_col];
+  }
+  return Status::OK();
+}
+
+namespace {
+bool IsDualPhaseILeavingCandidate(Fractional cost, VariableType type, Fractional threshold) {
+  if (cost == 0.0) return false;
+  return type == VariableType::UPPER_AND_LOWER_BOUNDED ||
+         type == VariableType::FIXED_VARIABLE ||
+         (type == VariableType::UPPER_BOUNDED && cost < -threshold) ||
+         (type == VariableType::LOWER_BOUNDED && cost > threshold);
+}
+}  // namespace
+
+// revised_simplex.cc:2198-2215
+template <bool use_dense_update>
+void RevisedSimplex::OnDualPriceChange(const std::vector<Fractional>& squared_norm, int row,
+                                       VariableType type, Fractional threshold) {
+  const Fractional price = dual_pricing_vector_[row];
+  const bool is_candidate = IsDualPhaseILeavingCandidate(price, type, threshold);
+  if (is_candidate) {
+    if (use_dense_update) {
+      dual_prices_.DenseAddOrUpdate(row, Square(price) / squared_norm[row]);
+    } else {
+      dual_prices_.AddOrUpdate(row, Square(price) / squared_norm[row]);
+    }
+  } else {
+    dual_prices_.Remove(row);
+  }
+}
+
+// revised_simplex.cc:2217-2267
+void RevisedSimplex::DualPhaseIUpdatePrice(int leaving_row, int entering_col) {
+  if (reduced_costs_.AreReducedCostsRecomputed() ||
+      dual_edge_norms_.NeedsBasisRefactorization() || dual_pricing_vector_.empty()) {
+    return;
+  }
+  const std::vector<VariableType>& variable_type = variables_info_.GetTypeRow();
+  const Fractional threshold = parameters_.ratio_test_zero_threshold;
+  const std::vector<Fractional>& squared_norms = dual_edge_norms_.GetEdgeSquaredNorms();
+  const Fractional step = dual_pricing_vector_[leaving_row] / direction_[leaving_row];
+  for (const int row : direction_.non_zeros) {
+    dual_pricing_vector_[row] -= direction_[row] * step;
+    OnDualPriceChange(squared_norms, row, variable_type[basis_[row]], threshold);
+  }
+  dual_pricing_vector_[leaving_row] = step;
+  dual_pricing_vector_[leaving_row] -=
+      dual_infeasibility_improvement_direction_[entering_col];
+  if (dual_infeasibility_improvement_direction_[entering_col] != 0.0) {
+    --num_dual_infeasible_positions_;
+  }
+  dual_infeasibility_improvement_direction_[entering_col] = 0.0;
+  dual_infeasibility_improvement_direction_[basis_[leaving_row]] = 0.0;
+  OnDualPriceChange(squared_norms, leaving_row, variable_type[entering_col], threshold);
+}
+
+// revised_simplex.cc:2269-2333
+void RevisedSimplex::DualPhaseIUpdatePriceOnReducedCostChange(const std::vector<int>& cols) {
+  bool something_to_do = false;
+  const Bitset& can_decrease = variables_info_.GetCanDecreaseBitRow();
+  const Bitset& can_increase = variables_info_.GetCanIncreaseBitRow();
+  const std::vector<Fractional>& reduced_costs = reduced_costs_.GetReducedCosts();
+  const Fractional tolerance = reduced_costs_.GetDualFeasibilityTolerance();
+  for (const int col : cols) {
+    const Fractional reduced_cost = reduced_costs[col];
+    const Fractional sign = (can_increase.IsSet(col) && reduced_cost < -tolerance) ? 1.0
+                            : (can_decrease.IsSet(col) && reduced_cost > tolerance) ? -1.0
+                                                                                    : 0.0;
+    if (sign != dual_infeasibility_improvement_direction_[col]) {
+      if (sign == 0.0) {
+        --num_dual_infeasible_positions_;
+      } else if (dual_infeasibility_improvement_direction_[col] == 0.0) {
+        ++num_dual_infeasible_positions_;
+      }
+      if (!something_to_do) {
+        initially_all_zero_scratchpad_.values.resize(num_rows_, 0.0);
+        initially_all_zero_scratchpad_.ClearSparseMask();
+        initially_all_zero_scratchpad_.non_zeros.clear();
+        something_to_do = true;
+      }
+      num_update_price_operations_ += 10 * compact_matrix_.ColumnNumEntries(col);
+      compact_matrix_.ColumnAddMultipleToSparseScatteredColumn(
+          col, sign - dual_infeasibility_improvement_direction_[col],
+          &initially_all_zero_scratchpad_);
+      dual_infeasibility_improvement_direction_[col] = sign;
+    }
+  }
+  if (something_to_do) {
+    initially_all_zero_scratchpad_.ClearNonZerosIfTooDense();
+    initially_all_zero_scratchpad_.ClearSparseMask();
+    const std::vector<Fractional>& squared_norms = dual_edge_norms_.GetEdgeSquaredNorms();
+    const std::vector<VariableType>& variable_type = variables_info_.GetTypeRow();
+    const Fractional threshold = parameters_.ratio_test_zero_threshold;
+    basis_factorization_.RightSolve(&initially_all_zero_scratchpad_);
+    if (initially_all_zero_scratchpad_.non_zeros.empty()) {
+      dual_prices_.StartDenseUpdates();
+      for (int row = 0; row < num_rows_; ++row) {
+        if (initially_all_zero_scratchpad_[row] == 0.0) continue;
+        dual_pricing_vector_[row] += initially_all_zero_scratchpad_[row];
+        OnDualPriceChange<true>(squared_norms, row, variable_type[basis_[row]], threshold);
+      }
+      initially_all_zero_scratchpad_.values.assign(num_rows_, 0.0);
+    } else {
+      for (const int row : initially_all_zero_scratchpad_.non_zeros) {
+        dual_pricing_vector_[row] += initially_all_zero_scratchpad_[row];
+        OnDualPriceChange(squared_norms, row, variable_type[basis_[row]], threshold);
+        initially_all_zero_scratchpad_[row] = 0.0;
+      }
+    }
+    initially_all_zero_scratchpad_.non_zeros.clear();
+  }
+}
+
+// revised_simplex.cc:2335-2388
+Status RevisedSimplex::DualPhaseIChooseLeavingVariableRow(int* leaving_row,
+                                                          Fractional* cost_variation,
+                                                          Fractional* target_bound) {
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  if (reduced_costs_.AreReducedCostsRecomputed() ||
+      dual_edge_norms_.NeedsBasisRefactorization() || dual_pricing_vector_.empty()) {
+    num_dual_infeasible_positions_ = 0;
+    dual_pricing_vector_.assign(num_rows_, 0.0);
+    dual_prices_.ClearAndResize(num_rows_);
+    dual_infeasibility_improvement_direction_.assign(num_cols_, 0.0);
+    DualPhaseIUpdatePriceOnReducedCostChange(
+        variables_info_.GetIsRelevantBitRow().ToVector());
+  } else {
+    DualPhaseIUpdatePriceOnReducedCostChange(update_row_.GetNonZeroPositions());
+  }
+  *leaving_row = kInvalidRow;
+  if (num_dual_infeasible_positions_ == 0) return Status::OK();
+  *leaving_row = dual_prices_.GetMaximum();
+  if (*leaving_row == kInvalidRow) return Status::OK();
+  *cost_variation = dual_pricing_vector_[*leaving_row];
+  const int leaving_col = basis_[*leaving_row];
+  if (*cost_variation < 0.0) {
+    *target_bound = ub[leaving_col];
+  } else {
+    *target_bound = lb[leaving_col];
+  }
+  return Status::OK();
+}
+
+// revised_simplex.cc:2390-2437
+void RevisedSimplex::MakeBoxedVariableDualFeasible(const std::vector<int>& cols,
+                                                   bool update_basic_values) {
+  std::vector<int> changed_cols;
+  const Fractional threshold = reduced_costs_.GetDualFeasibilityTolerance();
+  const std::vector<Fractional>& reduced_costs = reduced_costs_.GetReducedCosts();
+  const std::vector<VariableStatus>& variable_status = variables_info_.GetStatusRow();
+  for (const int col : cols) {
+    const Fractional reduced_cost = reduced_costs[col];
+    const VariableStatus status = variable_status[col];
+    if (reduced_cost > threshold && status == VariableStatus::AT_UPPER_BOUND) {
+      variables_info_.UpdateToNonBasicStatus(col, VariableStatus::AT_LOWER_BOUND);
+      changed_cols.push_back(col);
+    } else if (reduced_cost < -threshold && status == VariableStatus::AT_LOWER_BOUND) {
+      variables_info_.UpdateToNonBasicStatus(col, VariableStatus::AT_UPPER_BOUND);
+      changed_cols.push_back(col);
+    }
+  }
+  if (!changed_cols.empty()) {
+    variable_values_.UpdateGivenNonBasicVariables(changed_cols, update_basic_values);
+  }
+}
+
+// revised_simplex.cc:2475-2502
+void RevisedSimplex::PermuteBasis() {
+  const std::vector<int> col_perm = basis_factorization_.GetColumnPermutation();
+  if (col_perm.empty()) return;
+  {
+    std::vector<int> tmp(basis_.size());
+    for (size_t i = 0; i < col_perm.size(); ++i) tmp[col_perm[i]] = basis_[i];
+    basis_.swap(tmp);
+  }
+  if (!dual_pricing_vector_.empty()) {
+    std::vector<Fractional> tmp(dual_pricing_vector_.size());
+    for (size_t i = 0; i < col_perm.size(); ++i) tmp[col_perm[i]] = dual_pricing_vector_[i];
+    dual_pricing_vector_.swap(tmp);
+  }
+  reduced_costs_.UpdateDataOnBasisPermutation();
+  dual_edge_norms_.UpdateDataOnBasisPermutation(col_perm);
+  basis_factorization_.SetColumnPermutationToIdentity();
+}
+
+// revised_simplex.cc:2504-2575
+Status RevisedSimplex::UpdateAndPivot(int entering_col, int leaving_row,
+                                      Fractional target_bound) {
+  Fractional pivot_from_update_row;
+  if (update_row_.IsComputedFor(leaving_row)) {
+    pivot_from_update_row = update_row_.GetCoefficient(entering_col);
+  } else {
+    update_row_.ComputeUnitRowLeftInverse(leaving_row);
+    pivot_from_update_row = compact_matrix_.ColumnScalarProduct(
+        entering_col, update_row_.GetUnitRowLeftInverse().values.data());
+  }
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  const int leaving_col = basis_[leaving_row];
+  const VariableStatus leaving_variable_status =
+      lb[leaving_col] == ub[leaving_col] ? VariableStatus::FIXED_VALUE
+      : target_bound == lb[leaving_col]  ? VariableStatus::AT_LOWER_BOUND
+                                         : VariableStatus::AT_UPPER_BOUND;
+  UpdateBasis(entering_col, leaving_row, leaving_variable_status);
+  const Fractional pivot_from_direction = direction_[leaving_row];
+  const Fractional diff = std::fabs(pivot_from_update_row - pivot_from_direction);
+  if (diff > parameters_.refactorization_threshold *
+                 (1.0 + std::min(std::fabs(pivot_from_update_row),
+                                 std::fabs(pivot_from_direction)))) {
+    if (basis_factorization_.NumUpdates() < 10) {
+      Fractional threshold = parameters_.lu_factorization_pivot_threshold;
+      threshold = std::min(threshold * 1.5, 0.9);
+      parameters_.lu_factorization_pivot_threshold = threshold;
+      basis_factorization_.SetLuParameters(parameters_.lu());
+    }
+    MILP_RETURN_IF_ERROR(basis_factorization_.ForceRefactorization());
+  } else {
+    MILP_RETURN_IF_ERROR(basis_factorization_.Update(entering_col, leaving_row, direction_));
+  }
+  if (basis_factorization_.IsRefactorized()) PermuteBasis();
+  return Status::OK();
+}
+
+// revised_simplex.cc:2751-3045
+Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
+  struct Cleanup {
+    std::function<void()> f;
+    ~Cleanup() { f(); }
+  } cleanup{[this, time_limit]() { AdvanceDeterministicTime(time_limit); }};
+  bool refactorize = false;
+  primal_prices_.ForceRecomputation();
+  if (phase_ == Phase::FEASIBILITY) {
+    objective_.assign(num_cols_, 0.0);
+    std::vector<int> all_rows(num_rows_);
+    for (int r = 0; r < num_rows_; ++r) all_rows[r] = r;
+    variable_values_.UpdatePrimalPhaseICosts(all_rows, &objective_);
+    reduced_costs_.ResetForNewObjective();
+  }
+  while (true) {
+    if (!refactorize && reduced_costs_.NeedsBasisRefactorization()) refactorize = true;
+    if (!refactorize && primal_edge_norms_.NeedsBasisRefactorization()) refactorize = true;
+    MILP_RETURN_IF_ERROR(RefactorizeBasisIfNeeded(&refactorize));
+    if (basis_factorization_.IsRefactorized()) {
+      CorrectErrorsOnVariableValues();
+      if (phase_ == Phase::FEASIBILITY) {
+        std::vector<int> all_rows(num_rows_);
+        for (int r = 0; r < num_rows_; ++r) all_rows[r] = r;
+        if (variable_values_.UpdatePrimalPhaseICosts(all_rows, &objective_)) {
+          reduced_costs_.ResetForNewObjective();
+        }
+      }
+      if (phase_ == Phase::OPTIMIZATION &&
+          ComputeObjectiveValue() < primal_objective_limit_) {
+        problem_status_ = ProblemStatus::PRIMAL_FEASIBLE;
+        objective_limit_reached_ = true;
+        return Status::OK();
+      }
+    } else if (phase_ == Phase::FEASIBILITY) {
+      if (variable_values_.UpdatePrimalPhaseICosts(direction_.non_zeros, &objective_)) {
+        reduced_costs_.ResetForNewObjective();
+      }
+    }
+
+    const int entering_col = primal_prices_.GetBestEnteringColumn();
+    if (entering_col == kInvalidCol) {
+      if (reduced_costs_.AreReducedCostsPrecise() && basis_factorization_.IsRefactorized()) {
+        if (phase_ == Phase::FEASIBILITY) {
+          const Fractional primal_infeasibility =
+              variable_values_.ComputeMaximumPrimalInfeasibility();
+          if (primal_infeasibility < parameters_.primal_feasibility_tolerance) {
+            problem_status_ = ProblemStatus::PRIMAL_FEASIBLE;
+          } else {
+            problem_status_ = ProblemStatus::PRIMAL_INFEASIBLE;
+          }
+        } else {
+          problem_status_ = ProblemStatus::OPTIMAL;
+        }
+        break;
+      }
+      reduced_costs_.MakeReducedCostsPrecise();
+      refactorize = true;
+      continue;
+    }
+
+    ComputeDirection(entering_col);
+    if (!primal_edge_norms_.TestEnteringEdgeNormPrecision(entering_col, direction_)) {
+      primal_prices_.RecomputePriceAt(entering_col);
+      continue;
+    }
+    const Fractional reduced_cost =
+        reduced_costs_.TestEnteringReducedCostPrecision(entering_col, direction_);
+    primal_prices_.RecomputePriceAt(entering_col);
+    if (!reduced_costs_.IsValidPrimalEnteringCandidate(entering_col)) {
+      reduced_costs_.MakeReducedCostsPrecise();
+      continue;
+    }
+    AdvanceDeterministicTime(time_limit);
+    if (num_iterations_ == parameters_.max_number_of_iterations ||
+        time_limit->LimitReached()) {
+      break;
+    }
+
+    Fractional step_length;
+    int leaving_row;
+    Fractional target_bound;
+    if (phase_ == Phase::FEASIBILITY) {
+      PrimalPhaseIChooseLeavingVariableRow(entering_col, reduced_cost, &refactorize,
+                                           &leaving_row, &step_length, &target_bound);
+    } else {
+      MILP_RETURN_IF_ERROR(ChooseLeavingVariableRow(entering_col, reduced_cost,
+                                                      &refactorize, &leaving_row,
+                                                      &step_length, &target_bound));
+    }
+    if (refactorize) continue;
+
+    if (step_length == kInfinity || step_length == -kInfinity) {
+      if (!basis_factorization_.IsRefactorized() ||
+          !reduced_costs_.AreReducedCostsPrecise()) {
+        reduced_costs_.MakeReducedCostsPrecise();
+        refactorize = true;
+        continue;
+      }
+      if (phase_ == Phase::FEASIBILITY) {
+        problem_status_ = ProblemStatus::ABNORMAL;
+      } else {
+        problem_status_ = ProblemStatus::PRIMAL_UNBOUNDED;
+        solution_primal_ray_.assign(num_cols_, 0.0);
+        for (int row = 0; row < num_rows_; ++row) {
+          solution_primal_ray_[basis_[row]] = -direction_[row];
+        }
+        solution_primal_ray_[entering_col] = 1.0;
+        if (reduced_cost > 0.0) {
+          for (auto& v : solution_primal_ray_) v = -v;
+        }
+      }
+      break;
+    }
+
+    Fractional step = (reduced_cost > 0.0) ? -step_length : step_length;
+    if (phase_ == Phase::FEASIBILITY && leaving_row != kInvalidRow) {
+      step = ComputeStepToMoveBasicVariableToBound(leaving_row, target_bound);
+    }
+    const int leaving_col = (leaving_row == kInvalidRow) ? kInvalidCol : basis_[leaving_row];
+    bool is_degenerate = false;
+    if (leaving_row != kInvalidRow) {
+      const Fractional dir = -direction_[leaving_row] * step;
+      is_degenerate = (dir == 0.0) ||
+                      (dir > 0.0 && variable_values_.Get(leaving_col) >= target_bound) ||
+                      (dir < 0.0 && variable_values_.Get(leaving_col) <= target_bound);
+    }
+    variable_values_.UpdateOnPivoting(direction_, entering_col, step);
+    if (leaving_row != kInvalidRow) {
+      primal_edge_norms_.UpdateBeforeBasisPivot(entering_col, basis_[leaving_row],
+                                                leaving_row, direction_, &update_row_);
+      reduced_costs_.UpdateBeforeBasisPivot(entering_col, leaving_row, direction_,
+                                            &update_row_);
+      primal_prices_.UpdateBeforeBasisPivot(entering_col, &update_row_);
+      if (!is_degenerate) variable_values_.Set(leaving_col, target_bound);
+      MILP_RETURN_IF_ERROR(UpdateAndPivot(entering_col, leaving_row, target_bound));
+    } else {
+      if (step > 0.0) {
+        SetNonBasicVariableStatusAndDeriveValue(entering_col, VariableStatus::AT_UPPER_BOUND);
+      } else if (step < 0.0) {
+        SetNonBasicVariableStatusAndDeriveValue(entering_col, VariableStatus::AT_LOWER_BOUND);
+      }
+      primal_prices_.SetAndDebugCheckThatColumnIsDualFeasible(entering_col);
+    }
+    if (phase_ == Phase::FEASIBILITY && leaving_row != kInvalidRow) {
+      variable_values_.SetNonBasicVariableValueFromStatus(leaving_col);
+      reduced_costs_.SetNonBasicVariableCostToZero(leaving_col, &objective_[leaving_col]);
+      primal_prices_.RecomputePriceAt(leaving_col);
+    }
+    OnIterationDone(time_limit);
+  }
+  return Status::OK();
+}
+
+// revised_simplex.cc:3058-3367
+Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limit) {
+  struct Cleanup {
+    std::function<void()> f;
+    ~Cleanup() { f(); }
+  } cleanup{[this, time_limit]() { AdvanceDeterministicTime(time_limit); }};
+  bool refactorize = false;
+  bound_flip_candidates_.clear();
+  int leaving_row;
+  Fractional cost_variation;
+  Fractional target_bound;
+  int entering_col;
+  while (true) {
+    const bool old_refactorize_value = refactorize;
+    if (!refactorize && reduced_costs_.NeedsBasisRefactorization()) refactorize = true;
+    if (!refactorize && dual_edge_norms_.NeedsBasisRefactorization()) refactorize = true;
+    MILP_RETURN_IF_ERROR(RefactorizeBasisIfNeeded(&refactorize));
+    if (basis_factorization_.IsRefactorized()) {
+      if (feasibility_phase || old_refactorize_value) {
+        reduced_costs_.MakeReducedCostsPrecise();
+      }
+      if (!feasibility_phase) {
+        MakeBoxedVariableDualFeasible(
+            variables_info_.GetNonBasicBoxedVariables().ToVector(), false);
+        variable_values_.RecomputeBasicVariableValues();
+        variable_values_.RecomputeDualPrices(parameters_.dual_price_prioritize_norm);
+        if (phase_ == Phase::OPTIMIZATION && dual_objective_limit_ != kInfinity &&
+            ComputeObjectiveValue() > dual_objective_limit_) {
+          problem_status_ = ProblemStatus::DUAL_FEASIBLE;
+          objective_limit_reached_ = true;
+          return Status::OK();
+        }
+      }
+    } else {
+      if (!feasibility_phase) {
+        MakeBoxedVariableDualFeasible(bound_flip_candidates_, true);
+        bound_flip_candidates_.clear();
+        variable_values_.UpdateDualPrices(direction_.non_zeros);
+      }
+    }
+
+    if (feasibility_phase) {
+      MILP_RETURN_IF_ERROR(
+          DualPhaseIChooseLeavingVariableRow(&leaving_row, &cost_variation, &target_bound));
+    } else {
+      MILP_RETURN_IF_ERROR(
+          DualChooseLeavingVariableRow(&leaving_row, &cost_variation, &target_bound));
+    }
+    if (leaving_row == kInvalidRow) {
+      if (!basis_factorization_.IsRefactorized() || reduced_costs_.HasCostShift()) {
+        reduced_costs_.ClearAndRemoveCostShifts();
+        refactorize = true;
+        continue;
+      }
+      if (feasibility_phase) {
+        problem_status_ = num_dual_infeasible_positions_ == 0
+                              ? ProblemStatus::DUAL_FEASIBLE
+                              : ProblemStatus::DUAL_INFEASIBLE;
+      } else {
+        problem_status_ = ProblemStatus::OPTIMAL;
+      }
+      return Status::OK();
+    }
+
+    update_row_.ComputeUnitRowLeftInverse(leaving_row);
+    if (!dual_edge_norms_.TestPrecision(leaving_row, update_row_.GetUnitRowLeftInverse())) {
+      if (feasibility_phase) {
+        const Fractional price = dual_pricing_vector_[leaving_row];
+        const std::vector<Fractional>& sn = dual_edge_norms_.GetEdgeSquaredNorms();
+        dual_prices_.AddOrUpdate(leaving_row, Square(price) / sn[leaving_row]);
+      } else {
+        variable_values_.UpdateDualPrices({leaving_row});
+      }
+      continue;
+    }
+    update_row_.ComputeUpdateRow(leaving_row);
+
+    if (feasibility_phase) {
+      MILP_RETURN_IF_ERROR(entering_variable_.DualPhaseIChooseEnteringColumn(
+          reduced_costs_.AreReducedCostsPrecise(), update_row_, cost_variation,
+          &entering_col));
+    } else {
+      MILP_RETURN_IF_ERROR(entering_variable_.DualChooseEnteringColumn(
+          reduced_costs_.AreReducedCostsPrecise(), update_row_, cost_variation,
+          &bound_flip_candidates_, &entering_col));
+    }
+
+    if (entering_col == kInvalidCol) {
+      if (!reduced_costs_.AreReducedCostsPrecise()) {
+        refactorize = true;
+        continue;
+      }
+      if (feasibility_phase) {
+        problem_status_ = ProblemStatus::ABNORMAL;
+      } else {
+        problem_status_ = ProblemStatus::DUAL_UNBOUNDED;
+        solution_dual_ray_ = update_row_.GetUnitRowLeftInverse().values;
+        update_row_.ComputeFullUpdateRow(leaving_row, &solution_dual_ray_row_combination_);
+        if (cost_variation < 0) {
+          for (auto& v : solution_dual_ray_) v = -v;
+          for (auto& v : solution_dual_ray_row_combination_) v = -v;
+        }
+      }
+      return Status::OK();
+    }
+
+    const Fractional entering_coeff = update_row_.GetCoefficient(entering_col);
+    if (std::fabs(entering_coeff) < parameters_.dual_small_pivot_threshold &&
+        !reduced_costs_.AreReducedCostsPrecise()) {
+      refactorize = true;
+      continue;
+    }
+    ComputeDirection(entering_col);
+    if (std::fabs(direction_[leaving_row]) <
+        parameters_.small_pivot_threshold * direction_infinity_norm_) {
+      if (!reduced_costs_.AreReducedCostsPrecise()) {
+        refactorize = true;
+        continue;
+      }
+    }
+    AdvanceDeterministicTime(time_limit);
+    if (num_iterations_ == parameters_.max_number_of_iterations ||
+        time_limit->LimitReached()) {
+      return Status::OK();
+    }
+    const bool increasing_rc_is_needed = (cost_variation > 0.0) == (entering_coeff > 0.0);
+    reduced_costs_.ShiftCostIfNeeded(increasing_rc_is_needed, entering_col);
+    reduced_costs_.UpdateBeforeBasisPivot(entering_col, leaving_row, direction_,
+                                          &update_row_);
+    dual_edge_norms_.UpdateBeforeBasisPivot(entering_col, leaving_row, direction_,
+                                            update_row_.GetUnitRowLeftInverse());
+    Fractional primal_step = 0.0;
+    if (feasibility_phase) {
+      DualPhaseIUpdatePrice(leaving_row, entering_col);
+    } else {
+      primal_step = ComputeStepToMoveBasicVariableToBound(leaving_row, target_bound);
+      variable_values_.UpdateOnPivoting(direction_, entering_col, primal_step);
+    }
+    const int leaving_col = basis_[leaving_row];
+    MILP_RETURN_IF_ERROR(UpdateAndPivot(entering_col, leaving_row, target_bound));
+    variable_values_.SetNonBasicVariableValueFromStatus(leaving_col);
+    OnIterationDone(time_limit);
+  }
+  return Status::OK();
+}
+
+// revised_simplex.cc:3369-3543
+Status RevisedSimplex::PrimalPush(TimeLimit* time_limit) {
+  bool refactorize = false;
+  primal_edge_norms_.Clear();
+  dual_edge_norms_.Clear();
+  update_row_.Invalidate();
+  reduced_costs_.ClearAndRemoveCostShifts();
+  std::vector<int> super_basic_cols;
+  variables_info_.GetNotBasicBitRow().ForEach([&](int col) {
+    if (variables_info_.GetStatusRow()[col] == VariableStatus::FREE &&
+        variable_values_.Get(col) != 0)
+      super_basic_cols.push_back(col);
+  });
+  while (!super_basic_cols.empty()) {
+    AdvanceDeterministicTime(time_limit);
+    if (time_limit->LimitReached()) break;
+    MILP_RETURN_IF_ERROR(RefactorizeBasisIfNeeded(&refactorize));
+    if (basis_factorization_.IsRefactorized()) CorrectErrorsOnVariableValues();
+    const int entering_col = super_basic_cols.back();
+    Fractional fake_rc;
+    const Fractional entering_value = variable_values_.Get(entering_col);
+    if (variables_info_.GetTypeRow()[entering_col] == VariableType::UNCONSTRAINED) {
+      fake_rc = entering_value > 0 ? 1.0 : -1.0;
+    } else {
+      const Fractional diff_ub =
+          variables_info_.GetVariableUpperBounds()[entering_col] - entering_value;
+      const Fractional diff_lb =
+          entering_value - variables_info_.GetVariableLowerBounds()[entering_col];
+      fake_rc = diff_lb <= diff_ub ? 1.0 : -1.0;
+    }
+    ComputeDirection(entering_col);
+    Fractional step_length;
+    int leaving_row;
+    Fractional target_bound;
+    MILP_RETURN_IF_ERROR(ChooseLeavingVariableRow(entering_col, fake_rc, &refactorize,
+                                                    &leaving_row, &step_length,
+                                                    &target_bound));
+    if (refactorize) continue;
+    super_basic_cols.pop_back();
+    if (step_length == kInfinity || step_length == -kInfinity) {
+      if (variables_info_.GetTypeRow()[entering_col] == VariableType::UNCONSTRAINED) {
+        step_length = std::fabs(entering_value);
+      } else {
+        problem_status_ = ProblemStatus::ABNORMAL;
+        break;
+      }
+    }
+    const Fractional step = (fake_rc > 0.0) ? -step_length : step_length;
+    const int leaving_col = (leaving_row == kInvalidRow) ? kInvalidCol : basis_[leaving_row];
+    bool is_degenerate = false;
+    if (leaving_row != kInvalidRow) {
+      const Fractional dir = -direction_[leaving_row] * step;
+      is_degenerate = (dir == 0.0) ||
+                      (dir > 0.0 && variable_values_.Get(leaving_col) >= target_bound) ||
+                      (dir < 0.0 && variable_values_.Get(leaving_col) <= target_bound);
+    }
+    variable_values_.UpdateOnPivoting(direction_, entering_col, step);
+    if (leaving_row != kInvalidRow) {
+      if (!is_degenerate) variable_values_.Set(leaving_col, target_bound);
+      MILP_RETURN_IF_ERROR(UpdateAndPivot(entering_col, leaving_row, target_bound));
+    } else {
+      if (variables_info_.GetTypeRow()[entering_col] == VariableType::UNCONSTRAINED) {
+        variable_values_.Set(entering_col, 0.0);
+      } else if (step > 0.0) {
+        SetNonBasicVariableStatusAndDeriveValue(entering_col, VariableStatus::AT_UPPER_BOUND);
+      } else if (step < 0.0) {
+        SetNonBasicVariableStatusAndDeriveValue(entering_col, VariableStatus::AT_LOWER_BOUND);
+      }
+    }
+    OnIterationDone(time_limit);
+  }
+  return Status::OK();
+}
+
+}  // namespace milp
+
+
+// ===========================================================================
+// C ABI (include/mi_lp.h).
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <mutex>
+#include <thread>
+
+#include <hip/hip_runtime_api.h>
+
+struct mi_lp {
+  milp::RevisedSimplex simplex;
+  milp::GlopParameters params;
+  milp::LinearProgram lp;
+  int device = 0;
+  bool loaded = false;
+  bool solved = false;
+  std::string error;
+  // benchmark slicing (mi_lp_begin / mi_lp_run_until / mi_lp_finish)
+  std::thread worker;
+  std::mutex mu;
+  std::condition_variable cv;
+  int64_t pause_at = -1;
+  int64_t current_iteration = 0;
+  bool paused = false;
+  bool finished = false;
+  bool running = false;
+  mi_lp_result pending{};
+};
+
+namespace {
+
+milp::GlopParameters FromAbi(const mi_glop_params& p) {
+  milp::GlopParameters g;
+  g.use_dual_simplex = p.use_dual_simplex;
+  g.feasibility_rule = p.feasibility_rule;
+  g.optimization_rule = p.optimization_rule;
+  g.initial_basis = p.initial_basis;
+  g.use_transposed_matrix = p.use_transposed_matrix;
+  g.basis_refactorization_period = p.basis_refactorization_period;
+  g.dynamically_adjust_refactorization_period = p.dynamically_adjust_refactorization_period;
+  g.change_status_to_imprecise = p.change_status_to_imprecise;
+  g.markowitz_zlatev_parameter = p.markowitz_zlatev_parameter;
+  g.allow_simplex_algorithm_change = p.allow_simplex_algorithm_change;
+  g.devex_weights_reset_period = p.devex_weights_reset_period;
+  g.use_middle_product_form_update = p.use_middle_product_form_update;
+  g.initialize_devex_with_column_norms = p.initialize_devex_with_column_norms;
+  g.exploit_singleton_column_in_initial_basis = p.exploit_singleton_column_in_initial_basis;
+  g.random_seed = p.random_seed;
+  g.perturb_costs_in_dual_simplex = p.perturb_costs_in_dual_simplex;
+  g.use_dedicated_dual_feasibility_algorithm = p.use_dedicated_dual_feasibility_algorithm;
+  g.push_to_vertex = p.push_to_vertex;
+  g.dual_price_prioritize_norm = p.dual_price_prioritize_norm;
+  g.use_scaling = p.use_scaling;
+  g.max_number_of_iterations = p.max_number_of_iterations;
+  g.refactorization_threshold = p.refactorization_threshold;
+  g.recompute_reduced_costs_threshold = p.recompute_reduced_costs_threshold;
+  g.recompute_edges_norm_threshold = p.recompute_edges_norm_threshold;
+  g.primal_feasibility_tolerance = p.primal_feasibility_tolerance;
+  g.dual_feasibility_tolerance = p.dual_feasibility_tolerance;
+  g.ratio_test_zero_threshold = p.ratio_test_zero_threshold;
+  g.harris_tolerance_ratio = p.harris_tolerance_ratio;
+  g.small_pivot_threshold = p.small_pivot_threshold;
+  g.minimum_acceptable_pivot = p.minimum_acceptable_pivot;
+  g.drop_tolerance = p.drop_tolerance;
+  g.solution_feasibility_tolerance = p.solution_feasibility_tolerance;
+  g.max_number_of_reoptimizations = p.max_number_of_reoptimizations;
+  g.lu_factorization_pivot_threshold = p.lu_factorization_pivot_threshold;
+  g.max_time_in_seconds = p.max_time_in_seconds;
+  g.max_deterministic_time = p.max_deterministic_time;
+  g.markowitz_singularity_threshold = p.markowitz_singularity_threshold;
+  g.dual_small_pivot_threshold = p.dual_small_pivot_threshold;
+  g.objective_lower_limit = p.objective_lower_limit;
+  g.objective_upper_limit = p.objective_upper_limit;
+  g.degenerate_ministep_factor = p.degenerate_ministep_factor;
+  g.relative_cost_perturbation = p.relative_cost_perturbation;
+  g.relative_max_cost_perturbation = p.relative_max_cost_perturbation;
+  g.initial_condition_number_threshold = p.initial_condition_number_threshold;
+  g.crossover_bound_snapping_distance = p.crossover_bound_snapping_distance;
+  return g;
+}
+
+// LPSolver's validity checks (lp_solver.cc:185-202, LinearProgram::IsValid).
+bool ValidLp(const milp::LinearProgram& lp) {
+  if (lp.m < 0 || lp.n < 0 || lp.col_starts.size() != static_cast<size_t>(lp.n) + 1)
+    return false;
+  if (lp.col_starts[0] != 0) return false;
+  for (int c = 0; c < lp.n; ++c) {
+    if (lp.col_starts[c + 1] < lp.col_starts[c]) return false;
+    for (int64_t k = lp.col_starts[c]; k < lp.col_starts[c + 1]; ++k) {
+      const int r = lp.row_idx[k];
+      if (r < 0 || r >= lp.m) return false;
+      if (k > lp.col_starts[c] && r <= lp.row_idx[k - 1]) return false;
+      if (!(lp.vals[k] != 0.0) || !milp::IsFinite(lp.vals[k])) return false;
+    }
+  }
+  auto bad_bounds = [](const std::vector<double>& lo, const std::vector<double>& hi) {
+    for (size_t i = 0; i < lo.size(); ++i) {
+      if (!(lo[i] <= hi[i]) || lo[i] == milp::kInfinity || hi[i] == -milp::kInfinity)
+        return true;
+    }
+    return false;
+  };
+  if (bad_bounds(lp.col_lb, lp.col_ub) || bad_bounds(lp.row_lb, lp.row_ub)) return false;
+  for (const double c : lp.obj)
+    if (!milp::IsFinite(c)) return false;
+  return milp::IsFinite(lp.obj_offset) && milp::IsFinite(lp.obj_scale) && lp.obj_scale != 0.0;
+}
+
+void RunSolve(mi_lp* h, const volatile int32_t* interrupt, mi_lp_result* out) {
+  std::memset(out, 0, sizeof(*out));
+  h->error.clear();
+  if (!h->loaded) {
+    out->error_code = MI_LP_ERROR_STATE;
+    out->problem_status = MI_LP_INIT;
+    h->error = "mi_lp_solve before mi_lp_load";
+    return;
+  }
+  if (!ValidLp(h->lp)) {  // lp_solver.cc:185-202 -> INVALID_PROBLEM
+    out->problem_status = MI_LP_INVALID_PROBLEM;
+    out->error_code = MI_LP_OK;
+    h->solved = false;
+    return;
+  }
+  try {
+    (void)hipSetDevice(h->device);
+    h->simplex.SetParameters(h->params);
+    milp::TimeLimit tl;
+    tl.max_seconds = h->params.max_time_in_seconds;
+    tl.max_deterministic = h->params.max_deterministic_time;
+    tl.interrupt = interrupt;
+    const milp::Status s = h->simplex.Solve(h->lp, &tl);
+    h->simplex.device().Synchronize();
+    out->error_code = static_cast<int32_t>(s.code);
+    out->problem_status = s.ok() ? static_cast<int32_t>(h->simplex.GetProblemStatus())
+                                 : MI_LP_ABNORMAL;  // lp_solver.cc:654-657
+    out->iterations = h->simplex.GetNumberOfIterations();
+    out->objective = h->simplex.GetObjectiveValue();
+    out->deterministic_time = h->simplex.DeterministicTime();
+    out->solve_seconds = tl.GetElapsedTime();
+    if (!s.ok()) h->error = s.msg;
+    h->solved = true;
+  } catch (const milp::DeviceError& e) {
+    h->error = e.what();
+    out->error_code = MI_LP_ERROR_DEVICE;
+    out->problem_status = MI_LP_ABNORMAL;
+    h->solved = false;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void mi_glop_params_default(mi_glop_params* p) {
+  p->use_dual_simplex = 0;
+  p->feasibility_rule = MI_LP_STEEPEST_EDGE;
+  p->optimization_rule = MI_LP_STEEPEST_EDGE;
+  p->initial_basis = MI_LP_BASIS_TRIANGULAR;
+  p->use_transposed_matrix = 1;
+  p->basis_refactorization_period = 64;
+  p->dynamically_adjust_refactorization_period = 1;
+  p->change_status_to_imprecise = 1;
+  p->markowitz_zlatev_parameter = 3;
+  p->allow_simplex_algorithm_change = 0;
+  p->devex_weights_reset_period = 150;
+  p->use_middle_product_form_update = 1;
+  p->initialize_devex_with_column_norms = 1;
+  p->exploit_singleton_column_in_initial_basis = 1;
+  p->random_seed = 1;
+  p->perturb_costs_in_dual_simplex = 0;
+  p->use_dedicated_dual_feasibility_algorithm = 1;
+  p->push_to_vertex = 1;
+  p->dual_price_prioritize_norm = 0;
+  p->use_scaling = 1;
+  p->max_number_of_iterations = -1;
+  p->refactorization_threshold = 1e-9;
+  p->recompute_reduced_costs_threshold = 1e-8;
+  p->recompute_edges_norm_threshold = 100.0;
+  p->primal_feasibility_tolerance = 1e-8;
+  p->dual_feasibility_tolerance = 1e-8;
+  p->ratio_test_zero_threshold = 1e-9;
+  p->harris_tolerance_ratio = 0.5;
+  p->small_pivot_threshold = 1e-6;
+  p->minimum_acceptable_pivot = 1e-6;
+  p->drop_tolerance = 1e-14;
+  p->solution_feasibility_tolerance = 1e-6;
+  p->max_number_of_reoptimizations = 40;
+  p->lu_factorization_pivot_threshold = 0.01;
+  p->max_time_in_seconds = milp::kInfinity;
+  p->max_deterministic_time = milp::kInfinity;
+  p->markowitz_singularity_threshold = 1e-15;
+  p->dual_small_pivot_threshold = 1e-4;
+  p->objective_lower_limit = -milp::kInfinity;
+  p->objective_upper_limit = milp::kInfinity;
+  p->degenerate_ministep_factor = 0.01;
+  p->relative_cost_perturbation = 1e-5;
+  p->relative_max_cost_perturbation = 1e-7;
+  p->initial_condition_number_threshold = 1e50;
+  p->crossover_bound_snapping_distance = milp::kInfinity;
+}
+
+int mi_lp_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int mi_lp_create(int device, mi_lp** out) {
+  if (out == nullptr) return MI_LP_ERROR_NULL;
+  *out = nullptr;
+  mi_lp* h = new mi_lp();
+  try {
+    h->simplex.device().Init(device);
+  } catch (const milp::DeviceError& e) {
+    std::fprintf(stderr, "mi_lp_create: %s\n", e.what());
+    delete h;
+    return MI_LP_ERROR_DEVICE;
+  }
+  h->device = device;
+  mi_glop_params p;
+  mi_glop_params_default(&p);
+  h->params = FromAbi(p);
+  *out = h;
+  return MI_LP_OK;
+}
+
+int mi_lp_destroy(mi_lp* h) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  if (h->worker.joinable()) {
+    {
+      std::lock_guard<std::mutex> l(h->mu);
+      h->pause_at = -1;
+    }
+    h->cv.notify_all();
+    h->worker.join();
+  }
+  delete h;
+  return MI_LP_OK;
+}
+
+const char* mi_lp_last_error(const mi_lp* h) {
+  return h == nullptr ? "null handle" : h->error.c_str();
+}
+
+int mi_lp_set_params(mi_lp* h, const mi_glop_params* p) {
+  if (h == nullptr || p == nullptr) return MI_LP_ERROR_NULL;
+  if (!p->use_middle_product_form_update) {
+    h->error = "only use_middle_product_form_update=true is implemented";
+    return MI_LP_ERROR_INVALID_PROBLEM;
+  }
+  h->params = FromAbi(*p);
+  return MI_LP_OK;
+}
+
+int mi_lp_load(mi_lp* h, int32_t m, int32_t n, const int64_t* cs, const int32_t* ri,
+               const double* vals, const double* clb, const double* cub, const double* rlb,
+               const double* rub, const double* obj, double obj_offset, double obj_scale,
+               int32_t maximize) {
+  if (h == nullptr || cs == nullptr) return MI_LP_ERROR_NULL;
+  if (m < 0 || n < 0) return MI_LP_ERROR_INVALID_PROBLEM;
+  milp::LinearProgram& lp = h->lp;
+  lp.m = m;
+  lp.n = n;
+  lp.col_starts.assign(cs, cs + n + 1);
+  const int64_t nnz = cs[n];
+  if (nnz < 0) return MI_LP_ERROR_INVALID_PROBLEM;
+  lp.row_idx.assign(ri, ri + nnz);
+  lp.vals.assign(vals, vals + nnz);
+  lp.col_lb.assign(clb, clb + n);
+  lp.col_ub.assign(cub, cub + n);
+  lp.row_lb.assign(rlb, rlb + m);
+  lp.row_ub.assign(rub, rub + m);
+  lp.obj.assign(obj, obj + n);
+  lp.obj_offset = obj_offset;
+  lp.obj_scale = obj_scale;
+  lp.maximize = maximize != 0;
+  h->loaded = true;
+  h->solved = false;
+  return MI_LP_OK;
+}
+
+int mi_lp_load_basis_state(mi_lp* h, const int8_t* st, int32_t len) {
+  if (h == nullptr || (st == nullptr && len > 0)) return MI_LP_ERROR_NULL;
+  std::vector<milp::VariableStatus> s(len);
+  for (int i = 0; i < len; ++i) {
+    if (st[i] < 0 || st[i] > 4) return MI_LP_ERROR_INVALID_PROBLEM;
+    s[i] = static_cast<milp::VariableStatus>(st[i]);
+  }
+  h->simplex.LoadStateForNextSolve(s);
+  return MI_LP_OK;
+}
+
+int mi_lp_clear_basis_state(mi_lp* h) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  h->simplex.ClearStateForNextSolve();
+  return MI_LP_OK;
+}
+
+int mi_lp_notify_matrix_unchanged(mi_lp* h) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  h->simplex.NotifyThatMatrixIsUnchangedForNextSolve();
+  return MI_LP_OK;
+}
+
+int mi_lp_solve(mi_lp* h, const volatile int32_t* interrupt, mi_lp_result* out) {
+  if (h == nullptr || out == nullptr) return MI_LP_ERROR_NULL;
+  if (h->running) return MI_LP_ERROR_STATE;
+  RunSolve(h, interrupt, out);
+  return out->error_code;
+}
+
+#define MI_LP_REQUIRE_SOLVED(h)                  \
+  do {                                           \
+    if ((h) == nullptr) return MI_LP_ERROR_NULL; \
+    if (!(h)->solved) return MI_LP_ERROR_STATE;  \
+  } while (0)
+
+int mi_lp_get_primal(const mi_lp* h, double* x) {
+  MI_LP_REQUIRE_SOLVED(h);
+  for (int c = 0; c < h->lp.n; ++c) x[c] = h->simplex.GetVariableValue(c);
+  return MI_LP_OK;
+}
+int mi_lp_get_reduced_costs(const mi_lp* h, double* rc) {
+  MI_LP_REQUIRE_SOLVED(h);
+  for (int c = 0; c < h->lp.n; ++c) rc[c] = h->simplex.GetReducedCost(c);
+  return MI_LP_OK;
+}
+int mi_lp_get_duals(const mi_lp* h, double* y) {
+  MI_LP_REQUIRE_SOLVED(h);
+  for (int r = 0; r < h->lp.m; ++r) y[r] = h->simplex.GetDualValue(r);
+  return MI_LP_OK;
+}
+int mi_lp_get_activities(const mi_lp* h, double* a) {
+  MI_LP_REQUIRE_SOLVED(h);
+  for (int r = 0; r < h->lp.m; ++r) a[r] = h->simplex.GetConstraintActivity(r);
+  return MI_LP_OK;
+}
+int mi_lp_get_statuses(const mi_lp* h, int8_t* var, int8_t* cons) {
+  MI_LP_REQUIRE_SOLVED(h);
+  for (int c = 0; c < h->lp.n; ++c) var[c] = static_cast<int8_t>(h->simplex.GetVariableStatus(c));
+  for (int r = 0; r < h->lp.m; ++r)
+    cons[r] = static_cast<int8_t>(h->simplex.GetConstraintStatus(r));
+  return MI_LP_OK;
+}
+int mi_lp_get_basis(const mi_lp* h, int32_t* b) {
+  MI_LP_REQUIRE_SOLVED(h);
+  for (int r = 0; r < h->lp.m; ++r) b[r] = h->simplex.GetBasis(r);
+  return MI_LP_OK;
+}
+int mi_lp_get_state(const mi_lp* h, int8_t* st) {
+  MI_LP_REQUIRE_SOLVED(h);
+  const auto& s = h->simplex.GetState();
+  for (size_t i = 0; i < s.size(); ++i) st[i] = static_cast<int8_t>(s[i]);
+  return MI_LP_OK;
+}
+int mi_lp_get_primal_ray(const mi_lp* h, double* v) {
+  MI_LP_REQUIRE_SOLVED(h);
+  const auto& r = h->simplex.GetPrimalRay();
+  for (size_t i = 0; i < r.size(); ++i) v[i] = r[i];
+  return MI_LP_OK;
+}
+int mi_lp_get_dual_ray(const mi_lp* h, double* v) {
+  MI_LP_REQUIRE_SOLVED(h);
+  const auto& r = h->simplex.GetDualRay();
+  for (size_t i = 0; i < r.size(); ++i) v[i] = r[i];
+  return MI_LP_OK;
+}
+int mi_lp_get_dual_ray_row_combination(const mi_lp* h, double* v) {
+  MI_LP_REQUIRE_SOLVED(h);
+  const auto& r = h->simplex.GetDualRayRowCombination();
+  for (size_t i = 0; i < r.size(); ++i) v[i] = r[i];
+  return MI_LP_OK;
+}
+
+// --- benchmark slicing -----------------------------------------------------
+int mi_lp_begin(mi_lp* h, int64_t pause_at) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  if (h->running) return MI_LP_ERROR_STATE;
+  h->running = true;
+  h->finished = false;
+  h->paused = false;
+  h->pause_at = pause_at;
+  h->current_iteration = 0;
+  h->simplex.iteration_hook = [h](int64_t it) {
+    std::unique_lock<std::mutex> l(h->mu);
+    h->current_iteration = it;
+    while (h->pause_at >= 0 && it >= h->pause_at) {
+      h->simplex.device().Synchronize();
+      h->paused = true;
+      h->cv.notify_all();
+      h->cv.wait(l);
+    }
+    h->paused = false;
+  };
+  h->worker = std::thread([h]() {
+    RunSolve(h, nullptr, &h->pending);
+    std::lock_guard<std::mutex> l(h->mu);
+    h->finished = true;
+    h->cv.notify_all();
+  });
+  std::unique_lock<std::mutex> l(h->mu);
+  h->cv.wait(l, [h]() { return h->paused || h->finished; });
+  return MI_LP_OK;
+}
+
+int mi_lp_run_until(mi_lp* h, int64_t pause_at, int32_t* finished, int64_t* iterations) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  if (!h->running) return MI_LP_ERROR_STATE;
+  std::unique_lock<std::mutex> l(h->mu);
+  if (!h->finished) {
+    h->pause_at = pause_at;
+    h->paused = false;
+    h->cv.notify_all();
+    h->cv.wait(l, [h]() { return h->paused || h->finished; });
+  }
+  if (finished) *finished = h->finished ? 1 : 0;
+  if (iterations) *iterations = h->current_iteration;
+  return MI_LP_OK;
+}
+
+int mi_lp_finish(mi_lp* h, mi_lp_result* out) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  if (!h->running) return MI_LP_ERROR_STATE;
+  {
+    std::lock_guard<std::mutex> l(h->mu);
+    h->pause_at = -1;
+  }
+  h->cv.notify_all();
+  h->worker.join();
+  h->simplex.iteration_hook = nullptr;
+  h->running = false;
+  if (out) *out = h->pending;
+  return h->pending.error_code;
+}
+
+int mi_lp_get_kernel_stats(const mi_lp* h, mi_lp_kernel_stats* s) {
+  if (h == nullptr || s == nullptr) return MI_LP_ERROR_NULL;
+  *s = const_cast<mi_lp*>(h)->simplex.device().stats();
+  return MI_LP_OK;
+}
+int mi_lp_reset_kernel_stats(mi_lp* h) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  h->simplex.device().ResetStats();
+  return MI_LP_OK;
+}
+int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  h->simplex.device().SetTiming(enable != 0);
+  return MI_LP_OK;
+}
+
+int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
+                      mi_lp_result* results) {
+  if (handles == nullptr || results == nullptr) return MI_LP_ERROR_NULL;
+  if (num_threads < 1) num_threads = 1;
+  std::atomic<int> next(0);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < num_threads; ++t) {
+    pool.emplace_back([&]() {
+      while (true) {
+        const int i = next.fetch_add(1);
+        if (i >= count) break;
+        RunSolve(handles[i], nullptr, &results[i]);
+      }
+    });
+  }
+  for (auto& th : pool) th.join();
+  return MI_LP_OK;
+}
+
+}  // extern "C"

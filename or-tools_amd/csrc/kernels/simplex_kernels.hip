@@ -1,0 +1,307 @@
+// CDNA4 (gfx950) kernels for the O(nnz(A)) inner loops of Glop's revised
+// simplex. Every kernel reproduces the floating-point evaluation order of the
+// Glop loop it replaces, so results are bit-identical to the host code:
+//   * CompactSparseMatrix::ColumnScalarProduct (lp_data/sparse.h:514-542):
+//     four strided accumulators r1..r4 over the column, ((r1+r2)+r3)+r4, then
+//     the <=3 tail terms in order.
+//   * ColumnAddMultipleToDenseColumn scatter (sparse.h:389-399) summed per row
+//     in increasing column order, zero multipliers skipped.
+//   * UpdateRow row-wise algorithms (update_row.cc:196-280): per output column
+//     the filtered rho rows are accumulated in increasing row order.
+// Compiled with -ffp-contract=off: no FMA contraction anywhere.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernel_args.h"
+
+namespace milp_kernels {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ bool bit_set(const uint64_t* words, int i) {
+  return (words[i >> 6] >> (i & 63)) & 1ull;
+}
+
+// ---------------------------------------------------------------------------
+// Column dot product with Glop's 4-accumulator order, one wave per column.
+// The 64 lanes load 64 consecutive entries of the column (coalesced), each
+// computes its product, and lanes 0..3 (accumulator k = lane & 3) fold the 16
+// products of their chain in order by reading them with __shfl. The chain
+// index of entry e (relative to the column start) is e & 3 and entries of one
+// chain are visited in increasing e, exactly as in sparse.h:527-532.
+__device__ __forceinline__ double wave_column_dot(const int64_t s, const int64_t e,
+                                                  const int32_t* __restrict__ rows,
+                                                  const double* __restrict__ vals,
+                                                  const double* __restrict__ y,
+                                                  int lane) {
+  const int64_t len = e - s;
+  const int64_t full = (len >= 4) ? (len / 4) * 4 : 0;  // entries in 4-blocks
+  double acc = 0.0;  // lanes 0..3: r1..r4
+  for (int64_t base = 0; base < full; base += kWave) {
+    const int64_t idx = base + lane;
+    double p = 0.0;
+    if (idx < full) p = vals[s + idx] * y[rows[s + idx]];
+    const int64_t nvalid = (full - base) < kWave ? (full - base) : kWave;
+    // nvalid is a multiple of 4: each chain has nvalid/4 terms in this chunk.
+    const int nt = static_cast<int>(nvalid >> 2);
+#pragma unroll 4
+    for (int t = 0; t < 16; ++t) {
+      const double q = __shfl(p, (t << 2) + (lane & 3), kWave);
+      if (t < nt) acc += q;
+    }
+  }
+  const double r2 = __shfl(acc, 1, kWave);
+  const double r3 = __shfl(acc, 2, kWave);
+  const double r4 = __shfl(acc, 3, kWave);
+  double result = acc + r2 + r3 + r4;
+  // Tail (sparse.h:534-541), same on every lane.
+  for (int64_t i = s + full; i < e; ++i) result += vals[i] * y[rows[i]];
+  return result;
+}
+
+// Quarter-wave variant for short columns: 4 lanes per column, lane k owns
+// chain k and walks it sequentially (16 columns per wave).
+__device__ __forceinline__ double quad_column_dot(const int64_t s, const int64_t e,
+                                                  const int32_t* __restrict__ rows,
+                                                  const double* __restrict__ vals,
+                                                  const double* __restrict__ y,
+                                                  int sub, int lane) {
+  const int64_t len = e - s;
+  const int64_t full = (len >= 4) ? (len / 4) * 4 : 0;
+  double acc = 0.0;
+  for (int64_t i = s + sub; i < s + full; i += 4) acc += vals[i] * y[rows[i]];
+  const int g = lane & ~3;
+  const double r1 = __shfl(acc, g + 0, kWave);
+  const double r2 = __shfl(acc, g + 1, kWave);
+  const double r3 = __shfl(acc, g + 2, kWave);
+  const double r4 = __shfl(acc, g + 3, kWave);
+  double result = r1 + r2 + r3 + r4;
+  for (int64_t i = s + full; i < e; ++i) result += vals[i] * y[rows[i]];
+  return result;
+}
+
+// Modes of the column-dot kernel.
+enum DotMode : int {
+  kUpdateRowColumnWise = 0,  // update_row.cc:282-306 over relevant columns
+  kPricing = 1,              // reduced_costs.cc:372-381: rc = c - a_j.y
+  kListDots = 2,             // primal_edge_norms.cc:229-233 over a column list
+  kFullUpdateRow = 3         // update_row.cc:311-332 over non-basic columns
+};
+
+
+template <int MODE, bool WAVE_PER_COL>
+__global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
+  const int lane = threadIdx.x & 63;
+  int col_slot;
+  int sub = 0;
+  if (WAVE_PER_COL) {
+    col_slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  } else {
+    col_slot = blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2);
+    sub = threadIdx.x & 3;
+  }
+  // All lanes that share a column must stay converged through the shuffles,
+  // so out-of-range slots compute on column 0 and just skip the epilogue.
+  const bool in_range = col_slot < a.ncols;
+  int col = in_range ? col_slot : 0;
+  if (MODE == kListDots) col = in_range ? a.col_list[col_slot] : a.col_list[0];
+  bool active = in_range;
+  if (MODE == kUpdateRowColumnWise || MODE == kFullUpdateRow) {
+    active = active && bit_set(a.mask, col);
+  }
+  const int64_t s = a.starts[col];
+  const int64_t e = active ? a.starts[col + 1] : s;
+  const double dot = WAVE_PER_COL ? wave_column_dot(s, e, a.rows, a.vals, a.y, lane)
+                                  : quad_column_dot(s, e, a.rows, a.vals, a.y, sub, lane);
+  const bool writer = WAVE_PER_COL ? (lane == 0) : (sub == 0);
+  if (!writer || !in_range) return;
+  if (MODE == kUpdateRowColumnWise) {
+    const bool keep = active && fabs(dot) > a.drop_tolerance;
+    a.flags[col] = keep ? 1 : 0;
+    if (keep) a.out[col] = dot;
+  } else if (MODE == kPricing) {
+    a.out[col] = a.c[col] - dot;
+  } else if (MODE == kListDots) {
+    a.out[col_slot] = dot;
+  } else {  // kFullUpdateRow
+    if (active && fabs(dot) > a.drop_tolerance) a.out[col] = dot;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Row-wise update row (update_row.cc:196-280). The filtered non-zeros of rho
+// (ascending rows) are merged column-chunk by column-chunk: a workgroup owns
+// kChunk consecutive columns of the update row, and walks the CSR rows of the
+// transposed matrix in increasing order, binary-searching the first entry in
+// its chunk. Each column therefore receives its contributions in increasing
+// row order, as in the host scatter loops. Accumulators live in LDS.
+constexpr int kChunk = 256;
+
+
+__global__ __launch_bounds__(256) void row_wise_update_kernel(RowWiseArgs a) {
+  __shared__ double acc[kChunk];
+  __shared__ uint8_t touched[kChunk];
+  const int c0 = blockIdx.x * kChunk;
+  const int c1 = min(c0 + kChunk, a.num_cols);
+  for (int i = threadIdx.x; i < kChunk; i += blockDim.x) {
+    acc[i] = 0.0;
+    touched[i] = 0;
+  }
+  __syncthreads();
+  for (int k = 0; k < a.num_filtered; ++k) {
+    const int r = a.filtered_rows[k];
+    const double multiplier = a.rho[r];
+    int64_t lo = a.t_starts[r];
+    int64_t hi = a.t_starts[r + 1];
+    // lower_bound of c0 within the row (all threads compute the same value).
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (a.t_cols[mid] < c0) lo = mid + 1; else hi = mid;
+    }
+    const int64_t row_end = a.t_starts[r + 1];
+    for (int64_t i = lo + threadIdx.x; i < row_end; i += blockDim.x) {
+      const int pos = a.t_cols[i];
+      if (pos >= c1) break;
+      const double v = multiplier * a.t_vals[i];
+      const int l = pos - c0;
+      if (a.algorithm == 0) {
+        acc[l] = v;  // single row: one contribution per position
+      } else if (a.algorithm == 1) {
+        acc[l] = touched[l] ? acc[l] + v : v;  // hypersparse: first is assigned
+      } else {
+        acc[l] = touched[l] ? acc[l] + v : 0.0 + v;  // row-wise: 0.0 += v
+      }
+      touched[l] = 1;
+    }
+    __syncthreads();  // rows are applied in order
+  }
+  for (int l = threadIdx.x; l < c1 - c0; l += blockDim.x) {
+    const int pos = c0 + l;
+    const double v = acc[l];
+    const bool rel = bit_set(a.relevant, pos);
+    bool listed;
+    if (a.algorithm == 0) {
+      listed = touched[l] && rel && fabs(v) > a.drop_tolerance;
+      if (listed) a.coefficient[pos] = v;
+    } else if (a.algorithm == 1) {
+      listed = touched[l] && rel && fabs(v) > a.drop_tolerance;
+      if (touched[l]) a.coefficient[pos] = v;
+    } else {
+      listed = rel && fabs(v) > a.drop_tolerance;
+      a.coefficient[pos] = touched[l] ? v : 0.0;
+    }
+    a.flags[pos] = listed ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Row sums sum_j mult_j * A[r, j] in increasing j (the order the host scatter
+// ColumnAddMultipleToDenseColumn produces), zero multipliers skipped
+// (sparse.h:393). One wave per row: lanes load 64 consecutive CSR entries,
+// lane 0 folds the products in order.
+
+__global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= a.num_rows) return;  // whole wave exits together
+  const int64_t s = a.t_starts[row];
+  const int64_t e = a.t_starts[row + 1];
+  double acc = 0.0;
+  for (int64_t base = s; base < e; base += kWave) {
+    const int64_t i = base + lane;
+    double p = 0.0;
+    bool use = false;
+    if (i < e) {
+      const int col = a.t_cols[i];
+      double m = a.x[col];
+      if (a.skip != nullptr && bit_set(a.skip, col)) m = 0.0;
+      m = a.sign * m;  // exact (sign is +-1)
+      use = (m != 0.0);
+      p = m * a.t_vals[i];
+    }
+    const int nvalid = (e - base) < kWave ? static_cast<int>(e - base) : kWave;
+    for (int t = 0; t < kWave; ++t) {
+      const double q = __shfl(p, t, kWave);
+      const int u = __shfl(static_cast<int>(use), t, kWave);
+      if (t < nvalid && u) acc += q;
+    }
+  }
+  if (lane == 0) a.out[row] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// 1 + SquaredNorm(column) for relevant columns (primal_edge_norms.cc:153-158
+// with an identity basis: lu_factorization.cc:130 returns SquaredNorm(a), a
+// plain in-order sum, lp_utils.cc:22-29).
+__global__ __launch_bounds__(256) void column_squared_norm_kernel(
+    const int64_t* starts, const double* vals, const uint64_t* relevant, int ncols,
+    double* out) {
+  const int lane = threadIdx.x & 63;
+  const int col = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (col >= ncols) return;
+  if (!bit_set(relevant, col)) return;
+  const int64_t s = starts[col];
+  const int64_t e = starts[col + 1];
+  double acc = 0.0;
+  for (int64_t base = s; base < e; base += kWave) {
+    const int64_t i = base + lane;
+    const double v = (i < e) ? vals[i] : 0.0;
+    const double p = v * v;
+    const int nvalid = (e - base) < kWave ? static_cast<int>(e - base) : kWave;
+    for (int t = 0; t < kWave; ++t) {
+      const double q = __shfl(p, t, kWave);
+      if (t < nvalid) acc += q;
+    }
+  }
+  if (lane == 0) out[col] = 1.0 + acc;
+}
+
+}  // namespace milp_kernels
+
+// ---------------------------------------------------------------------------
+// Host-side launchers (extern "C++" inside the engine library).
+namespace milp_launch {
+using namespace milp_kernels;
+
+static inline int div_up(long a, long b) { return static_cast<int>((a + b - 1) / b); }
+
+hipError_t column_dot(int mode, bool wave_per_col, const DotArgs& args, hipStream_t s) {
+  if (args.ncols <= 0) return hipSuccess;
+  const int threads = 256;
+  const int per_block = wave_per_col ? threads / 64 : threads / 4;
+  const int blocks = div_up(args.ncols, per_block);
+  switch (mode * 2 + (wave_per_col ? 1 : 0)) {
+    case 0: column_dot_kernel<0, false><<<blocks, threads, 0, s>>>(args); break;
+    case 1: column_dot_kernel<0, true><<<blocks, threads, 0, s>>>(args); break;
+    case 2: column_dot_kernel<1, false><<<blocks, threads, 0, s>>>(args); break;
+    case 3: column_dot_kernel<1, true><<<blocks, threads, 0, s>>>(args); break;
+    case 4: column_dot_kernel<2, false><<<blocks, threads, 0, s>>>(args); break;
+    case 5: column_dot_kernel<2, true><<<blocks, threads, 0, s>>>(args); break;
+    case 6: column_dot_kernel<3, false><<<blocks, threads, 0, s>>>(args); break;
+    default: column_dot_kernel<3, true><<<blocks, threads, 0, s>>>(args); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t row_wise_update(const RowWiseArgs& args, hipStream_t s) {
+  const int blocks = div_up(args.num_cols, kChunk);
+  row_wise_update_kernel<<<blocks, 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t row_sums(const RowSumArgs& args, hipStream_t s) {
+  if (args.num_rows <= 0) return hipSuccess;
+  row_sum_kernel<<<div_up(args.num_rows, 4), 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t column_squared_norms(const int64_t* starts, const double* vals,
+                                const uint64_t* relevant, int ncols, double* out,
+                                hipStream_t s) {
+  if (ncols <= 0) return hipSuccess;
+  column_squared_norm_kernel<<<div_up(ncols, 4), 256, 0, s>>>(starts, vals, relevant,
+                                                              ncols, out);
+  return hipGetLastError();
+}
+
+}  // namespace milp_launch

@@ -1,0 +1,221 @@
+"""ctypes binding of the MI355X engine (or-tools_amd/lib/libmi_lp.so).
+
+This is the product path: every solve runs the HIP kernels. There is no CPU
+fallback: if the library or a GPU is missing, creating a handle raises.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from . import abi
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libmi_lp.so")
+
+_lib = None
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+def build(jobs=8):
+    """Compiles the engine for gfx950 (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", PKG_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineUnavailable(
+            f"{LIB_PATH} is missing: run `make -C or-tools_amd` (no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    L.mi_glop_params_default.argtypes = [ctypes.POINTER(abi.MiGlopParams)]
+    L.mi_lp_device_count.restype = ctypes.c_int
+    L.mi_lp_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.mi_lp_destroy.argtypes = [vp]
+    L.mi_lp_last_error.argtypes = [vp]
+    L.mi_lp_last_error.restype = ctypes.c_char_p
+    L.mi_lp_set_params.argtypes = [vp, ctypes.POINTER(abi.MiGlopParams)]
+    L.mi_lp_load.argtypes = [vp, ctypes.c_int32, ctypes.c_int32] + [vp] * 8 + \
+        [ctypes.c_double, ctypes.c_double, ctypes.c_int32]
+    L.mi_lp_load_basis_state.argtypes = [vp, vp, ctypes.c_int32]
+    L.mi_lp_clear_basis_state.argtypes = [vp]
+    L.mi_lp_notify_matrix_unchanged.argtypes = [vp]
+    L.mi_lp_solve.argtypes = [vp, vp, ctypes.POINTER(abi.MiLpResult)]
+    for name in ["mi_lp_get_primal", "mi_lp_get_reduced_costs", "mi_lp_get_duals",
+                 "mi_lp_get_activities", "mi_lp_get_basis", "mi_lp_get_state",
+                 "mi_lp_get_primal_ray", "mi_lp_get_dual_ray",
+                 "mi_lp_get_dual_ray_row_combination"]:
+        getattr(L, name).argtypes = [vp, vp]
+    L.mi_lp_get_statuses.argtypes = [vp, vp, vp]
+    L.mi_lp_begin.argtypes = [vp, ctypes.c_int64]
+    L.mi_lp_run_until.argtypes = [vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
+                                  ctypes.POINTER(ctypes.c_int64)]
+    L.mi_lp_finish.argtypes = [vp, ctypes.POINTER(abi.MiLpResult)]
+    L.mi_lp_get_kernel_stats.argtypes = [vp, ctypes.POINTER(abi.MiLpKernelStats)]
+    L.mi_lp_reset_kernel_stats.argtypes = [vp]
+    L.mi_lp_set_kernel_timing.argtypes = [vp, ctypes.c_int32]
+    L.mi_lp_batch_solve.argtypes = [vp, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.POINTER(abi.MiLpResult)]
+    _lib = L
+    return L
+
+
+def device_count():
+    return lib().mi_lp_device_count()
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class LpHandle:
+    """One RevisedSimplex on one GPU (include/mi_lp.h)."""
+
+    def __init__(self, params=None, device=0):
+        self._L = lib()
+        h = ctypes.c_void_p()
+        rc = self._L.mi_lp_create(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise EngineUnavailable(f"mi_lp_create(device={device}) failed with {rc}: "
+                                    "no usable MI355X (there is no CPU fallback)")
+        self.h = h
+        self.params = params or abi.default_params()
+        self.lp = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.mi_lp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self._L.mi_lp_last_error(self.h)
+            raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def set_params(self, params):
+        self.params = params
+
+    def load(self, lp):
+        self.lp = lp
+        self._keep = [np.ascontiguousarray(x, dtype=t) for x, t in (
+            (lp.col_starts, np.int64), (lp.row_idx, np.int32), (lp.vals, np.float64),
+            (lp.col_lb, np.float64), (lp.col_ub, np.float64), (lp.row_lb, np.float64),
+            (lp.row_ub, np.float64), (lp.obj, np.float64))]
+        cs, ri, v, clb, cub, rlb, rub, ob = self._keep
+        self._check(self._L.mi_lp_load(self.h, lp.m, lp.n, _p(cs), _p(ri), _p(v),
+                                       _p(clb), _p(cub), _p(rlb), _p(rub), _p(ob),
+                                       lp.obj_offset, lp.obj_scale, int(lp.maximize)),
+                    "mi_lp_load")
+
+    def load_basis_state(self, state):
+        st = np.ascontiguousarray(state, dtype=np.int8)
+        self._check(self._L.mi_lp_load_basis_state(self.h, _p(st), len(st)),
+                    "mi_lp_load_basis_state")
+
+    def clear_basis_state(self):
+        self._L.mi_lp_clear_basis_state(self.h)
+
+    def notify_matrix_unchanged(self):
+        self._L.mi_lp_notify_matrix_unchanged(self.h)
+
+    def _push_params(self):
+        self._check(self._L.mi_lp_set_params(self.h, ctypes.byref(self.params)),
+                    "mi_lp_set_params")
+
+    def solve(self):
+        self._push_params()
+        r = abi.MiLpResult()
+        self._L.mi_lp_solve(self.h, None, ctypes.byref(r))
+        if r.error_code == 100:
+            raise EngineUnavailable(self._L.mi_lp_last_error(self.h).decode())
+        return r
+
+    # benchmark slicing
+    def begin(self, pause_at):
+        self._push_params()
+        self._check(self._L.mi_lp_begin(self.h, int(pause_at)), "mi_lp_begin")
+
+    def run_until(self, pause_at):
+        fin = ctypes.c_int32()
+        it = ctypes.c_int64()
+        self._check(self._L.mi_lp_run_until(self.h, int(pause_at), ctypes.byref(fin),
+                                            ctypes.byref(it)), "mi_lp_run_until")
+        return bool(fin.value), int(it.value)
+
+    def finish(self):
+        r = abi.MiLpResult()
+        self._L.mi_lp_finish(self.h, ctypes.byref(r))
+        return r
+
+    def kernel_stats(self):
+        s = abi.MiLpKernelStats()
+        self._L.mi_lp_get_kernel_stats(self.h, ctypes.byref(s))
+        return {name: dict(launches=s.launches[i], bytes=s.algorithmic_bytes[i],
+                           device_ms=s.device_ms[i])
+                for i, name in enumerate(abi.KERNEL_NAMES)}
+
+    def reset_kernel_stats(self):
+        self._L.mi_lp_reset_kernel_stats(self.h)
+
+    def set_kernel_timing(self, on=True):
+        self._L.mi_lp_set_kernel_timing(self.h, int(on))
+
+    def _get(self, fn, n, dtype):
+        out = np.zeros(n, dtype=dtype)
+        self._check(getattr(self._L, fn)(self.h, _p(out)), fn)
+        return out
+
+    def primal(self):
+        return self._get("mi_lp_get_primal", self.lp.n, np.float64)
+
+    def reduced_costs(self):
+        return self._get("mi_lp_get_reduced_costs", self.lp.n, np.float64)
+
+    def duals(self):
+        return self._get("mi_lp_get_duals", self.lp.m, np.float64)
+
+    def activities(self):
+        return self._get("mi_lp_get_activities", self.lp.m, np.float64)
+
+    def basis(self):
+        return self._get("mi_lp_get_basis", self.lp.m, np.int32)
+
+    def state(self):
+        return self._get("mi_lp_get_state", self.lp.n + self.lp.m, np.int8)
+
+    def statuses(self):
+        var = np.zeros(self.lp.n, np.int8)
+        cons = np.zeros(self.lp.m, np.int8)
+        self._check(self._L.mi_lp_get_statuses(self.h, _p(var), _p(cons)),
+                    "mi_lp_get_statuses")
+        return var, cons
+
+    def primal_ray(self):
+        return self._get("mi_lp_get_primal_ray", self.lp.n + self.lp.m, np.float64)
+
+    def dual_ray(self):
+        return self._get("mi_lp_get_dual_ray", self.lp.m, np.float64)
+
+
+def batch_solve(handles, num_threads=4):
+    """Solves already-loaded handles concurrently (mi_lp_batch_solve)."""
+    L = lib()
+    for h in handles:
+        h._push_params()
+    arr = (ctypes.c_void_p * len(handles))(*[h.h.value for h in handles])
+    res = (abi.MiLpResult * len(handles))()
+    L.mi_lp_batch_solve(arr, len(handles), num_threads, res)
+    return list(res)

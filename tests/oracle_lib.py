@@ -73,11 +73,10 @@ class OracleLp:
 
     def load(self, lp):
         self.lp = lp
-        self._keep = [np.ascontiguousarray(x) for x in (
-            lp.col_starts.astype(np.int64), lp.row_idx.astype(np.int32),
-            lp.vals.astype(np.float64), lp.col_lb.astype(np.float64),
-            lp.col_ub.astype(np.float64), lp.row_lb.astype(np.float64),
-            lp.row_ub.astype(np.float64), lp.obj.astype(np.float64))]
+        self._keep = [np.ascontiguousarray(x, dtype=t) for x, t in (
+            (lp.col_starts, np.int64), (lp.row_idx, np.int32), (lp.vals, np.float64),
+            (lp.col_lb, np.float64), (lp.col_ub, np.float64), (lp.row_lb, np.float64),
+            (lp.row_ub, np.float64), (lp.obj, np.float64))]
         cs, ri, v, clb, cub, rlb, rub, ob = self._keep
         self._L.oracle_lp_load(self.h, lp.m, lp.n, _p(cs), _p(ri), _p(v), _p(clb),
                                _p(cub), _p(rlb), _p(rub), _p(ob), lp.obj_offset,

@@ -1,0 +1,84 @@
+"""CPU tests of the oracle: pinned by the reference's own known answers
+(tests/kat_lps.py cites the upstream test lines) and by HiGHS objectives on
+seeded synthetic LPs."""
+import numpy as np
+import pytest
+
+from mi_glop import abi
+
+import kat_lps
+import lp_gen
+import oracle_lib
+
+
+@pytest.mark.parametrize("builder", kat_lps.ALL, ids=lambda f: f.__name__)
+@pytest.mark.parametrize("dual", [0, 1])
+def test_known_answers(builder, dual):
+    lp, exp = builder()
+    o = oracle_lib.OracleLp(abi.default_params(use_dual_simplex=dual))
+    o.load(lp)
+    r = o.solve()
+    if "status_in" in exp:
+        assert abi.PROBLEM_STATUS[r.problem_status] in exp["status_in"]
+        return
+    assert r.problem_status == exp["status"]
+    assert r.objective == pytest.approx(exp["objective"], rel=1e-9, abs=1e-9)
+    for key, getter in (("primal", o.primal), ("duals", o.duals),
+                        ("reduced_costs", o.reduced_costs),
+                        ("activities", o.activities)):
+        if key in exp:
+            np.testing.assert_allclose(getter(), exp[key], rtol=1e-7, atol=1e-7)
+
+
+@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("dual", [0, 1])
+def test_against_highs(seed, dual):
+    m = [6, 12, 40, 90][seed % 4]
+    n = [9, 30, 70, 250][seed % 4]
+    lp = lp_gen.random_sparse_lp(m, n, 0.3 if m < 30 else 0.06, seed,
+                                 maximize=bool(seed % 2))
+    st, ref = lp_gen.to_scipy(lp)
+    o = oracle_lib.OracleLp(abi.default_params(use_dual_simplex=dual))
+    o.load(lp)
+    r = o.solve()
+    if st != 0:
+        assert r.problem_status != abi.OPTIMAL
+        return
+    assert r.problem_status == abi.OPTIMAL
+    assert abs(r.objective - ref) <= 1e-6 * max(1.0, abs(ref))
+
+
+def test_dense_box_against_highs():
+    lp = lp_gen.dense_box_lp(60, 240, 7)
+    st, ref = lp_gen.to_scipy(lp)
+    o = oracle_lib.OracleLp()
+    o.load(lp)
+    r = o.solve()
+    assert st == 0 and r.problem_status == abi.OPTIMAL
+    assert abs(r.objective - ref) <= 1e-9 * max(1.0, abs(ref))
+
+
+def test_warm_start_bound_change_dual():
+    """CP-SAT style re-solve: same matrix, one bound tightened, warm-started
+    dual simplex (linear_programming_constraint.cc:443-464, 709-760)."""
+    lp = lp_gen.random_sparse_lp(40, 120, 0.08, 5)
+    p = abi.default_params(use_dual_simplex=1)
+    o = oracle_lib.OracleLp(p)
+    o.load(lp)
+    r0 = o.solve()
+    assert r0.problem_status == abi.OPTIMAL
+    x = o.primal()
+    j = int(np.argmax(np.abs(x - np.round(x))))
+    lp.col_ub = lp.col_ub.copy()
+    lp.col_ub[j] = np.floor(x[j])
+    o.load(lp)
+    r1 = o.solve()
+    st, ref = lp_gen.to_scipy(lp)
+    if st == 0:
+        assert r1.problem_status == abi.OPTIMAL
+        assert abs(r1.objective - ref) <= 1e-6 * max(1, abs(ref))
+    # Warm start is cheaper than a cold solve of the same LP.
+    cold = oracle_lib.OracleLp(p)
+    cold.load(lp)
+    rc = cold.solve()
+    assert r1.iterations <= rc.iterations
