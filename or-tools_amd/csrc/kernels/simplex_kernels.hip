@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void row_wise_update_kernel(RowWiseArgs a) {
   __syncthreads();
   for (int k = 0; k < a.num_filtered; ++k) {
     const int r = a.filtered_rows[k];
-    const double multiplier = a.rho[r];
+    const double multiplier = a.rho[k];  // compacted: rho values of filtered rows
     int64_t lo = a.t_starts[r];
     int64_t hi = a.t_starts[r + 1];
     // lower_bound of c0 within the row (all threads compute the same value).

@@ -100,6 +100,10 @@ class LpHandle:
         except Exception:
             pass
 
+    def last_error(self):
+        msg = self._L.mi_lp_last_error(self.h)
+        return msg.decode() if msg else ""
+
     def _check(self, rc, what):
         if rc != 0:
             msg = self._L.mi_lp_last_error(self.h)

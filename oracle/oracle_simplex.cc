@@ -8,6 +8,8 @@
 // Polish() (needs SetIntegralityScale), logging/stats.
 #include "oracle_simplex.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -712,6 +714,7 @@ class PrimalEdgeNorms {
     if (recompute_edge_squared_norms_) ComputeEdgeSquaredNorms();
     return edge_squared_norms_;
   }
+  const std::vector<Fractional>& RawEdgeNorms() const { return edge_squared_norms_; }
   bool TestEnteringEdgeNormPrecision(int entering_col, const ScatteredVector& d);
   void UpdateBeforeBasisPivot(int entering_col, int leaving_col, int leaving_row,
                               const ScatteredVector& direction, UpdateRow* update_row);
@@ -942,6 +945,7 @@ class ReducedCosts {
     if (recompute_reduced_costs_) ComputeReducedCosts();
     return reduced_costs_;
   }
+  const std::vector<Fractional>& RawReducedCosts() const { return reduced_costs_; }
   const std::vector<Fractional>& GetFullReducedCosts() {
     if (!are_reduced_costs_recomputed_) SetRecomputeReducedCostsAndNotifyWatchers();
     return GetReducedCosts();
@@ -1937,7 +1941,51 @@ class RevisedSimplex {
     tl->AdvanceDeterministicTime(cur - last_deterministic_time_update_);
     last_deterministic_time_update_ = cur;
   }
+  // Debug aid (env MILP_TRACE=<path prefix>): one line per iteration with
+  // bit-hashes of the iterate, to locate the first divergence between the
+  // oracle and the device engine.
+  static uint64_t HashBits(const std::vector<Fractional>& v) {
+    uint64_t h = 1469598103934665603ull;
+    for (const Fractional x : v) {
+      uint64_t b;
+      std::memcpy(&b, &x, sizeof(b));
+      h = (h ^ b) * 1099511628211ull;
+    }
+    return h;
+  }
+  static uint64_t HashInts(const std::vector<int>& v) {
+    uint64_t h = 1469598103934665603ull;
+    for (const int x : v) h = (h ^ static_cast<uint32_t>(x)) * 1099511628211ull;
+    return h;
+  }
+  void TraceIteration() {
+    static const char* prefix = std::getenv("MILP_TRACE");
+    if (prefix == nullptr) return;
+    const std::string path = std::string(prefix) + ".oracle";
+    FILE* f = std::fopen(path.c_str(), "a");
+    if (f == nullptr) return;
+    std::fprintf(f, "it=%lld phase=%d basis=%016llx x=%016llx rc=%016llx se=%016llx obj=%a\n",
+                 static_cast<long long>(num_iterations_), static_cast<int>(phase_),
+                 static_cast<unsigned long long>(HashInts(basis_)),
+                 static_cast<unsigned long long>(HashBits(variable_values_.GetDenseRow())),
+                 static_cast<unsigned long long>(HashBits(reduced_costs_.RawReducedCosts())),
+                 static_cast<unsigned long long>(HashBits(primal_edge_norms_.RawEdgeNorms())),
+                 ComputeObjectiveValue());
+    if (num_cols_ <= 64) {
+      const std::vector<Fractional>* vs[3] = {&variable_values_.GetDenseRow(),
+                                              &reduced_costs_.RawReducedCosts(),
+                                              &primal_edge_norms_.RawEdgeNorms()};
+      const char* names[3] = {"x", "rc", "se"};
+      for (int k = 0; k < 3; ++k) {
+        std::fprintf(f, "  %s:", names[k]);
+        for (const Fractional v : *vs[k]) std::fprintf(f, " %a", v);
+        std::fprintf(f, "\n");
+      }
+    }
+    std::fclose(f);
+  }
   void OnIterationDone(TimeLimit* tl) {
+    TraceIteration();
     ++num_iterations_;
     if (record_iteration_times) iteration_times.push_back(tl->GetElapsedTime());
   }
