@@ -32,6 +32,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "simplex iterations/sec + batched LPs/sec, 1/2/4/8 MI355X vs Glop CPU"
 
 
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    """Progress on stderr (keeps long runs visibly alive)."""
+    print(f"[bench {time.perf_counter() - _T0:8.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def dense_box_lp(m, n, seed):
     import lp_gen
     return lp_gen.dense_box_lp(m, n, seed)
@@ -94,13 +102,17 @@ def main():
             import torch
             torch.cuda.synchronize()
 
+    log(f"generating {args.m}x{args.n} dense LP")
     lp = dense_box_lp(args.m, args.n, args.seed + rank)
     params = abi.default_params()  # Glop defaults: primal simplex, steepest edge
     h = engine.LpHandle(params, device=local_rank)
+    log("loading")
     h.load(lp)
+    log("begin (upload, initial basis, norms, warm-up iterations)")
     t_setup = time.perf_counter()
     h.begin(args.warmup)  # load to HBM, factorize, first norms, W iterations
     t_setup = time.perf_counter() - t_setup
+    log(f"warm-up done in {t_setup:.1f}s; timing {args.steps} iterations")
     h.reset_kernel_stats()
     h.set_kernel_timing(True)
 
@@ -126,6 +138,8 @@ def main():
         total_done = float(c.item())
     else:
         total_done = float(done)
+    log(f"timed window: {done} iterations in {elapsed:.3f}s")
+    h.stop()  # the bench times a window, not the whole solve
     h.finish()
 
     # Dominant kernel in the timed region: roofline vs HBM peak.
@@ -143,6 +157,7 @@ def main():
         return
     cpu = None
     if not args.no_cpu and world == 1:
+        log("cpu baseline (oracle)")
         rate, info = cpu_baseline(lp, args.cpu_warmup, args.cpu_iters)
         cpu = {"value": rate, "unit": "iterations/s", "cores": 1, "kind": "port",
                "sample": (f"oracle (C++ restatement of Glop, -O3, 1 thread) on the same "

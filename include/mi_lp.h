@@ -219,6 +219,9 @@ int mi_lp_begin(mi_lp* h, int64_t pause_at);
 int mi_lp_run_until(mi_lp* h, int64_t pause_at, int32_t* finished,
                     int64_t* iterations);
 int mi_lp_finish(mi_lp* h, mi_lp_result* out);
+/* Interrupts a begun solve at its next time-limit check (the interrupt flag
+ * of glop_interface.cc:186-189); follow with mi_lp_finish. */
+int mi_lp_stop(mi_lp* h);
 
 int mi_lp_get_kernel_stats(const mi_lp* h, mi_lp_kernel_stats* s);
 int mi_lp_reset_kernel_stats(mi_lp* h);

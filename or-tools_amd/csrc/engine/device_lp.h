@@ -78,6 +78,7 @@ class DeviceLp {
   const mi_lp_kernel_stats& stats() const { return stats_; }
   void ResetStats();
   void Synchronize();
+  int dense_columns() const { return nd_; }
 
  private:
   template <typename T>
@@ -87,6 +88,10 @@ class DeviceLp {
   void BeginKernel(int id);
   void EndKernel(int id, double bytes);
   void Compact(int n);  // flags_ -> list_ (ascending), count -> list_count_
+  void BuildDenseBlock();
+  // Launches the CSC kernel over the sparse columns (all columns when there is
+  // no dense block) and the dense-block kernel; mode as in column_dot.
+  void LaunchColumnDots(int mode, const double* d_y, const double* d_c, double* d_out);
   void Check(int err, const char* what);
 
   int device_ = -1;
@@ -94,6 +99,7 @@ class DeviceLp {
   void* ev_start_ = nullptr;
   void* ev_stop_ = nullptr;
   bool timing_ = false;
+  double drop_ = 0.0;  // drop tolerance of the current update row
   mi_lp_kernel_stats stats_{};
   std::vector<void*> allocations_;
 
@@ -110,6 +116,17 @@ class DeviceLp {
   int32_t* d_t_cols_ = nullptr;
   double* d_t_vals_ = nullptr;
   std::vector<int64_t> h_starts_;  // host copy for byte accounting
+  // Dense column block (kernel_args.h DenseArgs): full structural columns.
+  int nd_ = 0;
+  int ns_ = 0;  // remaining (sparse) columns
+  double* d_dense_body_ = nullptr;
+  double* d_dense_tail_ = nullptr;
+  int32_t* d_dense_cols_ = nullptr;
+  int32_t* d_sparse_cols_ = nullptr;
+  uint8_t* d_is_dense_ = nullptr;
+  std::vector<uint8_t> h_is_dense_;
+  std::vector<uint64_t> h_dense_words_;
+  int64_t sparse_entries_ = 0;  // entries of the sparse columns
   std::vector<int64_t> h_t_starts_;
 
   // masks
@@ -125,13 +142,15 @@ class DeviceLp {
   uint8_t* d_flags_ = nullptr;
   int32_t* d_list_ = nullptr;    // compacted listed positions
   int* d_count_ = nullptr;
-  double* d_out_n_ = nullptr;    // per-column / per-list results
+  double* d_out_n_ = nullptr;    // per-column results
+  double* d_out_list_ = nullptr; // per-list-slot results
   int32_t* d_cols_ = nullptr;    // arbitrary column list / filtered rows
   double* d_rho_vals_ = nullptr; // filtered rho values
   void* d_cub_temp_ = nullptr;
   size_t cub_temp_bytes_ = 0;
   int list_count_ = 0;
-  int64_t list_entries_ = 0;  // sum of column lengths over the listed columns
+  int64_t list_entries_ = 0;  // CSC entries over the listed sparse columns
+  int64_t list_dense_ = 0;    // listed dense columns
 
   // pinned staging
   int32_t* h_pin_i_ = nullptr;

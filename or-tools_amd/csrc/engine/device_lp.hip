@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
 #include <cstring>
 
 #include "lp_data.h"
@@ -14,13 +15,6 @@ namespace milp {
 
 namespace {
 inline hipStream_t S(void* p) { return reinterpret_cast<hipStream_t>(p); }
-
-__global__ void gather_kernel(const int32_t* list, const int* count, const double* src,
-                              double* dst) {
-  const int n = *count;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    dst[i] = src[list[i]];
-}
 }  // namespace
 
 void DeviceLp::Check(int err, const char* what) {
@@ -137,6 +131,7 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   d_list_ = Alloc<int32_t>(n_total_);
   d_count_ = Alloc<int>(1);
   d_out_n_ = Alloc<double>(n_total_);
+  d_out_list_ = Alloc<double>(std::max(n_total_, m_));
   d_cols_ = Alloc<int32_t>(std::max(n_total_, m_));
   d_rho_vals_ = Alloc<double>(m_);
   Check(hipMemsetAsync(d_coeff_, 0, n_total_ * sizeof(double), S(stream_)), "memset");
@@ -155,7 +150,91 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d_), big * sizeof(double)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d2_), big * sizeof(double)), "pin");
   list_count_ = 0;
+  BuildDenseBlock();
   Synchronize();
+}
+
+// Full structural columns go to the value-only dense block (8 B per entry
+// instead of 12, unit-stride chains). MILP_DENSE_BLOCK=off|force|auto
+// (auto: at least 256 full columns and 32 rows).
+void DeviceLp::BuildDenseBlock() {
+  nd_ = 0;
+  ns_ = n_total_;
+  h_is_dense_.assign(n_total_, 0);
+  h_dense_words_.assign(mask_words_, 0);
+  sparse_entries_ = nnz_;
+  const char* env = std::getenv("MILP_DENSE_BLOCK");
+  const std::string mode = env ? env : "auto";
+  if (mode == "off" || m_ <= 0) return;
+  std::vector<int32_t> dense, sparse;
+  for (int c = 0; c < n_total_; ++c) {
+    if (h_starts_[c + 1] - h_starts_[c] == m_) dense.push_back(c); else sparse.push_back(c);
+  }
+  const bool use = mode == "force" ? !dense.empty()
+                                   : (dense.size() >= 256 && m_ >= 32);
+  if (!use) return;
+  nd_ = static_cast<int>(dense.size());
+  ns_ = static_cast<int>(sparse.size());
+  for (const int c : dense) {
+    h_is_dense_[c] = 1;
+    h_dense_words_[c >> 6] |= 1ull << (c & 63);
+  }
+  sparse_entries_ = nnz_ - static_cast<int64_t>(nd_) * m_;
+  const int steps = m_ >> 2;
+  d_dense_body_ = Alloc<double>(static_cast<size_t>(steps) * nd_ * 4);
+  d_dense_tail_ = Alloc<double>(static_cast<size_t>(m_ - 4 * steps) * nd_);
+  d_dense_cols_ = Alloc<int32_t>(nd_);
+  d_sparse_cols_ = Alloc<int32_t>(ns_);
+  d_is_dense_ = Alloc<uint8_t>(n_total_);
+  Upload(d_dense_cols_, dense.data(), nd_ * sizeof(int32_t));
+  Upload(d_sparse_cols_, sparse.data(), ns_ * sizeof(int32_t));
+  Upload(d_is_dense_, h_is_dense_.data(), n_total_);
+  Synchronize();  // the host vectors above are pageable and go out of scope
+  Check(milp_launch::dense_pack(d_starts_, d_vals_, d_dense_cols_, nd_, m_, d_dense_body_,
+                                d_dense_tail_, S(stream_)),
+        "dense pack");
+}
+
+void DeviceLp::LaunchColumnDots(int mode, const double* d_y, const double* d_c,
+                                double* d_out) {
+  milp_kernels::DotArgs a{};
+  a.starts = d_starts_;
+  a.rows = d_rows_;
+  a.vals = d_vals_;
+  a.y = d_y;
+  a.c = d_c;
+  a.out = d_out;
+  a.mask = d_masks_[kRelevant];
+  a.flags = d_flags_;
+  a.drop_tolerance = 0.0;
+  if (mode == 2) {  // dots over the update-row list
+    a.ncols = list_count_;
+    a.col_list = d_list_;
+    a.flags = nullptr;  // every listed column is active
+  } else {
+    a.ncols = nd_ > 0 ? ns_ : n_total_;
+    a.col_list = nd_ > 0 ? d_sparse_cols_ : nullptr;
+  }
+  a.skip = nd_ > 0 ? d_is_dense_ : nullptr;
+  const double sparse_avg =
+      (nd_ > 0 ? (ns_ > 0 ? double(sparse_entries_) / ns_ : 0.0) : avg_col_len_);
+  a.drop_tolerance = drop_;
+  Check(milp_launch::column_dot(mode, sparse_avg >= 32.0, a, S(stream_)), "column dots");
+  if (nd_ > 0) {
+    milp_kernels::DenseArgs d{};
+    d.body = d_dense_body_;
+    d.tail = d_dense_tail_;
+    d.dense_cols = d_dense_cols_;
+    d.nd = nd_;
+    d.m = m_;
+    d.y = d_y;
+    d.mask = d_masks_[kRelevant];
+    d.c = d_c;
+    d.out = d_out;
+    d.flags = d_flags_;
+    d.drop_tolerance = drop_;
+    Check(milp_launch::dense_dot(mode, d, S(stream_)), "dense dots");
+  }
 }
 
 void DeviceLp::SetMask(Mask which, const uint64_t* words, int num_words) {
@@ -182,22 +261,21 @@ void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
                                    int64_t relevant_entries) {
   std::memcpy(h_pin_d_, rho.data(), m_ * sizeof(double));
   Upload(d_vec_m_, h_pin_d_, m_ * sizeof(double));
-  milp_kernels::DotArgs a{};
-  a.starts = d_starts_;
-  a.rows = d_rows_;
-  a.vals = d_vals_;
-  a.y = d_vec_m_;
-  a.ncols = n_total_;
-  a.mask = d_masks_[kRelevant];
-  a.out = d_coeff_;
-  a.flags = d_flags_;
-  a.drop_tolerance = drop;
+  drop_ = drop;
+  // Algorithmic bytes: every relevant column is read (12 B per CSC entry,
+  // 8 B per dense-block entry), rho once, coefficients + flags written.
+  int64_t dense_rel = 0;
+  if (nd_ > 0) {
+    const uint64_t* rel = h_masks_[kRelevant].data();
+    for (int w = 0; w < mask_words_; ++w) {
+      dense_rel += __builtin_popcountll(rel[w] & h_dense_words_[w]);
+    }
+  }
+  const double dense_entries = double(dense_rel) * m_;
   BeginKernel(MI_K_UPDATE_ROW);
-  Check(milp_launch::column_dot(0, avg_col_len_ >= 32.0, a, S(stream_)), "colwise");
-  // Algorithmic bytes: every relevant column is read (12 B/entry), rho is
-  // read once (8 B/row), coefficients + flags written (9 B/column).
-  EndKernel(MI_K_UPDATE_ROW,
-            12.0 * double(relevant_entries) + 8.0 * m_ + 9.0 * n_total_);
+  LaunchColumnDots(0, d_vec_m_, nullptr, d_coeff_);
+  EndKernel(MI_K_UPDATE_ROW, 12.0 * (double(relevant_entries) - dense_entries) +
+                                 8.0 * dense_entries + 8.0 * m_ + 9.0 * n_total_);
   Compact(n_total_);
 }
 
@@ -235,20 +313,23 @@ void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* 
   const int n = list_count_;
   positions->resize(n);
   values->resize(n);
+  list_entries_ = 0;
+  list_dense_ = 0;
   if (n == 0) return;
-  gather_kernel<<<std::min(1024, (n + 255) / 256), 256, 0, S(stream_)>>>(d_list_, d_count_,
-                                                                         d_coeff_, d_out_n_);
-  Check(hipGetLastError(), "gather");
+  Check(milp_launch::gather(d_list_, n, d_coeff_, d_out_list_, S(stream_)), "gather");
   Check(hipMemcpyAsync(h_pin_i_, d_list_, n * sizeof(int32_t), hipMemcpyDeviceToHost,
                        S(stream_)),
         "D2H");
-  Download(h_pin_d_, d_out_n_, n * sizeof(double));
+  Download(h_pin_d_, d_out_list_, n * sizeof(double));
   std::memcpy(positions->data(), h_pin_i_, n * sizeof(int32_t));
   std::memcpy(values->data(), h_pin_d_, n * sizeof(double));
-  list_entries_ = 0;
   for (int i = 0; i < n; ++i) {
     const int c = (*positions)[i];
-    list_entries_ += h_starts_[c + 1] - h_starts_[c];
+    if (!h_is_dense_.empty() && h_is_dense_[c]) {
+      ++list_dense_;
+    } else {
+      list_entries_ += h_starts_[c + 1] - h_starts_[c];
+    }
   }
 }
 
@@ -265,19 +346,12 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
   if (n == 0) return;
   std::memcpy(h_pin_d2_, v.data(), m_ * sizeof(double));
   Upload(d_vec_m_, h_pin_d2_, m_ * sizeof(double));
-  milp_kernels::DotArgs a{};
-  a.starts = d_starts_;
-  a.rows = d_rows_;
-  a.vals = d_vals_;
-  a.y = d_vec_m_;
-  a.ncols = n;
-  a.col_list = d_list_;
-  a.out = d_out_n_;
   BeginKernel(MI_K_PRIMAL_NORMS);
-  Check(milp_launch::column_dot(2, avg_col_len_ >= 32.0, a, S(stream_)), "listdots");
-  EndKernel(MI_K_PRIMAL_NORMS,
-            12.0 * double(list_entries_) + 8.0 * m_ + 4.0 * n + 8.0 * n);
-  Download(h_pin_d_, d_out_n_, n * sizeof(double));
+  LaunchColumnDots(2, d_vec_m_, nullptr, d_out_n_);
+  Check(milp_launch::gather(d_list_, n, d_out_n_, d_out_list_, S(stream_)), "gather");
+  EndKernel(MI_K_PRIMAL_NORMS, 12.0 * double(list_entries_) + 8.0 * double(list_dense_) * m_ +
+                                   8.0 * m_ + 4.0 * n + 8.0 * n);
+  Download(h_pin_d_, d_out_list_, n * sizeof(double));
   std::memcpy(out->data(), h_pin_d_, n * sizeof(double));
 }
 
@@ -302,8 +376,9 @@ void DeviceLp::ListDots(const std::vector<int>& cols, const std::vector<double>&
   for (int c : cols) entries += double(h_starts_[c + 1] - h_starts_[c]);
   BeginKernel(MI_K_PRIMAL_NORMS);
   Check(milp_launch::column_dot(2, avg_col_len_ >= 32.0, a, S(stream_)), "listdots");
+  Check(milp_launch::gather(d_cols_, n, d_out_n_, d_out_list_, S(stream_)), "gather");
   EndKernel(MI_K_PRIMAL_NORMS, 12.0 * entries + 8.0 * m_ + 12.0 * n);
-  Download(h_pin_d_, d_out_n_, n * sizeof(double));
+  Download(h_pin_d_, d_out_list_, n * sizeof(double));
   std::memcpy(out->data(), h_pin_d_, n * sizeof(double));
 }
 
@@ -313,18 +388,13 @@ void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& 
   Upload(d_vec_n_, h_pin_d_, n_total_ * sizeof(double));
   std::memcpy(h_pin_d2_, y.data(), m_ * sizeof(double));
   Upload(d_vec_m_, h_pin_d2_, m_ * sizeof(double));
-  milp_kernels::DotArgs a{};
-  a.starts = d_starts_;
-  a.rows = d_rows_;
-  a.vals = d_vals_;
-  a.y = d_vec_m_;
-  a.ncols = n_total_;
-  a.c = d_vec_n_;
-  a.out = d_out_n_;
   BeginKernel(MI_K_PRICING);
-  Check(milp_launch::column_dot(1, avg_col_len_ >= 32.0, a, S(stream_)), "pricing");
-  // 12 B per entry of [A|I] + column starts + y + c in + rc out.
-  EndKernel(MI_K_PRICING, 12.0 * nnz_ + 8.0 * (n_total_ + 1) + 8.0 * m_ + 16.0 * n_total_);
+  LaunchColumnDots(1, d_vec_m_, d_vec_n_, d_out_n_);
+  // 12 B per CSC entry of [A|I] (8 B per dense-block entry) + column starts
+  // + y + c in + rc out.
+  const double dense_entries = double(nd_) * m_;
+  EndKernel(MI_K_PRICING, 12.0 * double(sparse_entries_) + 8.0 * dense_entries +
+                              8.0 * (n_total_ + 1) + 8.0 * m_ + 16.0 * n_total_);
   rc->resize(n_total_);
   Download(h_pin_d_, d_out_n_, n_total_ * sizeof(double));
   std::memcpy(rc->data(), h_pin_d_, n_total_ * sizeof(double));

@@ -3555,6 +3555,7 @@ struct mi_lp {
   bool paused = false;
   bool finished = false;
   bool running = false;
+  volatile int32_t stop = 0;  // mi_lp_stop: interrupts like a time limit
   mi_lp_result pending{};
 };
 
@@ -3910,6 +3911,7 @@ int mi_lp_begin(mi_lp* h, int64_t pause_at) {
   h->running = true;
   h->finished = false;
   h->paused = false;
+  h->stop = 0;
   h->pause_at = pause_at;
   h->current_iteration = 0;
   h->simplex.iteration_hook = [h](int64_t it) {
@@ -3924,7 +3926,7 @@ int mi_lp_begin(mi_lp* h, int64_t pause_at) {
     h->paused = false;
   };
   h->worker = std::thread([h]() {
-    RunSolve(h, nullptr, &h->pending);
+    RunSolve(h, &h->stop, &h->pending);
     std::lock_guard<std::mutex> l(h->mu);
     h->finished = true;
     h->cv.notify_all();
@@ -3946,6 +3948,18 @@ int mi_lp_run_until(mi_lp* h, int64_t pause_at, int32_t* finished, int64_t* iter
   }
   if (finished) *finished = h->finished ? 1 : 0;
   if (iterations) *iterations = h->current_iteration;
+  return MI_LP_OK;
+}
+
+int mi_lp_stop(mi_lp* h) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  if (!h->running) return MI_LP_ERROR_STATE;
+  {
+    std::lock_guard<std::mutex> l(h->mu);
+    h->stop = 1;
+    h->pause_at = -1;
+  }
+  h->cv.notify_all();
   return MI_LP_OK;
 }
 

@@ -18,7 +18,29 @@ struct DotArgs {
   const uint64_t* mask;     // relevance / not-basic bitset (modes 0, 3)
   const double* c;          // kPricing: objective + perturbation
   double* out;              // result per column (or per list entry)
-  uint8_t* flags;           // kUpdateRowColumnWise: |coeff| > drop
+  uint8_t* flags;           // kUpdateRowColumnWise: |coeff| > drop; kListDots: listed
+  double drop_tolerance;
+  const uint8_t* skip;      // optional: columns handled by the dense block
+};
+
+// Dense column block: the structural columns whose CSC column is full (all m
+// rows). Values only, chain-interleaved so that lane (4j + k) streams chain k
+// of column j with unit stride across the wave:
+//   body[(t * nd + j) * 4 + k] = A[4t + k, dense_cols[j]]   for t < m / 4
+//   tail[r * nd + j]           = A[4(m/4) + r, dense_cols[j]] for r < m % 4
+// which is exactly the r1..r4 chain split of ColumnScalarProduct
+// (sparse.h:514-542) for a column whose entry index equals its row index.
+struct DenseArgs {
+  const double* body;
+  const double* tail;
+  const int32_t* dense_cols;  // nd ascending column ids
+  int nd;
+  int m;
+  const double* y;        // dot vector (rho / y / w)
+  const uint64_t* mask;   // kUpdateRowColumnWise: relevant columns
+  const double* c;        // kPricing
+  double* out;            // indexed by column id
+  uint8_t* flags;         // kUpdateRowColumnWise: out; kListDots: in (listed)
   double drop_tolerance;
 };
 
@@ -53,6 +75,10 @@ struct RowSumArgs {
 namespace milp_launch {
 hipError_t column_dot(int mode, bool wave_per_col, const milp_kernels::DotArgs& args,
                       hipStream_t s);
+hipError_t dense_dot(int mode, const milp_kernels::DenseArgs& args, hipStream_t s);
+hipError_t dense_pack(const int64_t* starts, const double* vals, const int32_t* dense_cols,
+                      int nd, int m, double* body, double* tail, hipStream_t s);
+hipError_t gather(const int32_t* list, int n, const double* src, double* dst, hipStream_t s);
 hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s);
 hipError_t row_sums(const milp_kernels::RowSumArgs& args, hipStream_t s);
 hipError_t column_squared_norms(const int64_t* starts, const double* vals,

@@ -103,11 +103,14 @@ __global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
   // All lanes that share a column must stay converged through the shuffles,
   // so out-of-range slots compute on column 0 and just skip the epilogue.
   const bool in_range = col_slot < a.ncols;
-  int col = in_range ? col_slot : 0;
-  if (MODE == kListDots) col = in_range ? a.col_list[col_slot] : a.col_list[0];
+  const int slot = in_range ? col_slot : 0;
+  const int col = a.col_list != nullptr ? a.col_list[slot] : slot;
   bool active = in_range;
+  if (a.skip != nullptr) active = active && !a.skip[col];
   if (MODE == kUpdateRowColumnWise || MODE == kFullUpdateRow) {
     active = active && bit_set(a.mask, col);
+  } else if (MODE == kListDots && a.flags != nullptr) {
+    active = active && a.flags[col];
   }
   const int64_t s = a.starts[col];
   const int64_t e = active ? a.starts[col + 1] : s;
@@ -115,6 +118,7 @@ __global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
                                   : quad_column_dot(s, e, a.rows, a.vals, a.y, sub, lane);
   const bool writer = WAVE_PER_COL ? (lane == 0) : (sub == 0);
   if (!writer || !in_range) return;
+  if (a.skip != nullptr && a.skip[col]) return;  // owned by the dense block
   if (MODE == kUpdateRowColumnWise) {
     const bool keep = active && fabs(dot) > a.drop_tolerance;
     a.flags[col] = keep ? 1 : 0;
@@ -122,10 +126,95 @@ __global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
   } else if (MODE == kPricing) {
     a.out[col] = a.c[col] - dot;
   } else if (MODE == kListDots) {
-    a.out[col_slot] = dot;
+    if (active) a.out[col] = dot;
   } else {  // kFullUpdateRow
     if (active && fabs(dot) > a.drop_tolerance) a.out[col] = dot;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Dense block dots (layout in kernel_args.h). Lane 4j+k owns chain k of dense
+// column j and walks it sequentially (the order Glop's accumulator r_{k+1}
+// sees); each step of a wave is one coalesced 512-B load. Loads are issued
+// kUnroll steps ahead of the dependent adds. Lane 4j then folds
+// ((r1 + r2) + r3) + r4 and adds the <= 3 tail terms in order.
+constexpr int kUnroll = 8;
+
+template <int MODE>
+__global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = tid >> 2;
+  const int k = tid & 3;
+  const bool in_range = j < a.nd;
+  const int col = in_range ? a.dense_cols[j] : 0;
+  bool active = in_range;
+  if (MODE == kUpdateRowColumnWise) active = active && bit_set(a.mask, col);
+  if (MODE == kListDots) active = active && a.flags[col];
+  const int steps = a.m >> 2;
+  double acc = 0.0;
+  if (active) {
+    const double* __restrict__ p = a.body + static_cast<int64_t>(j) * 4 + k;
+    const double* __restrict__ y = a.y + k;
+    const int64_t stride = static_cast<int64_t>(a.nd) * 4;
+    int t = 0;
+    for (; t + kUnroll <= steps; t += kUnroll) {
+      double v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) v[u] = __builtin_nontemporal_load(p + (t + u) * stride);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) acc += v[u] * y[(t + u) * 4];
+    }
+    for (; t < steps; ++t) acc += p[t * stride] * y[t * 4];
+  }
+  const double r2 = __shfl_down(acc, 1, kWave);
+  const double r3 = __shfl_down(acc, 2, kWave);
+  const double r4 = __shfl_down(acc, 3, kWave);
+  if (k != 0 || !in_range) return;
+  double result = acc + r2 + r3 + r4;
+  const int base = steps * 4;
+  for (int r = 0; base + r < a.m; ++r) {
+    result += a.tail[static_cast<int64_t>(r) * a.nd + j] * a.y[base + r];
+  }
+  if (MODE == kUpdateRowColumnWise) {
+    const bool keep = active && fabs(result) > a.drop_tolerance;
+    a.flags[col] = keep ? 1 : 0;
+    if (keep) a.out[col] = result;
+  } else if (MODE == kPricing) {
+    a.out[col] = a.c[col] - result;
+  } else if (MODE == kListDots) {
+    if (active) a.out[col] = result;
+  }
+}
+
+// Builds the dense block from the CSC arrays (one thread per entry).
+__global__ __launch_bounds__(256) void dense_pack_kernel(const int64_t* starts,
+                                                         const double* vals,
+                                                         const int32_t* dense_cols, int nd,
+                                                         int m, double* body, double* tail) {
+  const int64_t total = static_cast<int64_t>(nd) * m;
+  const int steps = m >> 2;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    // e enumerates the destination in body order for coalesced stores.
+    const int64_t body_total = static_cast<int64_t>(steps) * nd * 4;
+    if (e < body_total) {
+      const int k = static_cast<int>(e & 3);
+      const int64_t q = e >> 2;
+      const int j = static_cast<int>(q % nd);
+      const int t = static_cast<int>(q / nd);
+      body[e] = vals[starts[dense_cols[j]] + 4 * t + k];
+    } else {
+      const int64_t f = e - body_total;
+      const int j = static_cast<int>(f % nd);
+      const int r = static_cast<int>(f / nd);
+      tail[f] = vals[starts[dense_cols[j]] + 4 * steps + r];
+    }
+  }
+}
+
+__global__ void gather_kernel(const int32_t* list, int n, const double* src, double* dst) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    dst[i] = src[list[i]];
 }
 
 // ---------------------------------------------------------------------------
@@ -280,6 +369,30 @@ hipError_t column_dot(int mode, bool wave_per_col, const DotArgs& args, hipStrea
     case 6: column_dot_kernel<3, false><<<blocks, threads, 0, s>>>(args); break;
     default: column_dot_kernel<3, true><<<blocks, threads, 0, s>>>(args); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t dense_dot(int mode, const DenseArgs& args, hipStream_t s) {
+  if (args.nd <= 0) return hipSuccess;
+  const int blocks = div_up(static_cast<long>(args.nd) * 4, 256);
+  switch (mode) {
+    case 0: dense_dot_kernel<0><<<blocks, 256, 0, s>>>(args); break;
+    case 1: dense_dot_kernel<1><<<blocks, 256, 0, s>>>(args); break;
+    default: dense_dot_kernel<2><<<blocks, 256, 0, s>>>(args); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t dense_pack(const int64_t* starts, const double* vals, const int32_t* dense_cols,
+                      int nd, int m, double* body, double* tail, hipStream_t s) {
+  if (nd <= 0 || m <= 0) return hipSuccess;
+  dense_pack_kernel<<<4096, 256, 0, s>>>(starts, vals, dense_cols, nd, m, body, tail);
+  return hipGetLastError();
+}
+
+hipError_t gather(const int32_t* list, int n, const double* src, double* dst, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  gather_kernel<<<std::min(2048, div_up(n, 256)), 256, 0, s>>>(list, n, src, dst);
   return hipGetLastError();
 }
 

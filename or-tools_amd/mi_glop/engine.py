@@ -58,6 +58,7 @@ def lib():
     L.mi_lp_run_until.argtypes = [vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                                   ctypes.POINTER(ctypes.c_int64)]
     L.mi_lp_finish.argtypes = [vp, ctypes.POINTER(abi.MiLpResult)]
+    L.mi_lp_stop.argtypes = [vp]
     L.mi_lp_get_kernel_stats.argtypes = [vp, ctypes.POINTER(abi.MiLpKernelStats)]
     L.mi_lp_reset_kernel_stats.argtypes = [vp]
     L.mi_lp_set_kernel_timing.argtypes = [vp, ctypes.c_int32]
@@ -158,6 +159,9 @@ class LpHandle:
         self._check(self._L.mi_lp_run_until(self.h, int(pause_at), ctypes.byref(fin),
                                             ctypes.byref(it)), "mi_lp_run_until")
         return bool(fin.value), int(it.value)
+
+    def stop(self):
+        self._check(self._L.mi_lp_stop(self.h), "mi_lp_stop")
 
     def finish(self):
         r = abi.MiLpResult()

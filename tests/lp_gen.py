@@ -76,6 +76,23 @@ def dense_box_lp(m, n, seed, maximize=True):
                          f"dense_{m}x{n}_s{seed}")
 
 
+def from_dense_box(A, rng, maximize=True):
+    """Box LP over an arbitrary (possibly partly sparse) matrix A: same row
+    and bound construction as dense_box_lp, explicit zeros dropped."""
+    m, n = A.shape
+    x0 = rng.uniform(0.0, 1.0, size=n)
+    rhs = A @ x0 + rng.uniform(0.0, 1.0, size=m)
+    cols = [np.nonzero(A[:, j])[0] for j in range(n)]
+    cs = np.zeros(n + 1, dtype=np.int64)
+    cs[1:] = np.cumsum([len(c) for c in cols])
+    ri = np.concatenate(cols).astype(np.int32) if n else np.zeros(0, np.int32)
+    va = np.concatenate([A[c, j] for j, c in enumerate(cols)]) if n else np.zeros(0)
+    obj = rng.uniform(-1.0, 1.0, size=n)
+    return LinearProgram(m, n, cs, ri, va, np.zeros(n), np.full(n, 10.0),
+                         np.full(m, -INF), rhs, obj, 0.0, 1.0, maximize,
+                         f"mixed_{m}x{n}")
+
+
 def to_scipy(lp):
     """Objective-only cross-check with scipy/HiGHS (test oracle pinning)."""
     import scipy.sparse as sp

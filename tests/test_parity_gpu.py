@@ -41,10 +41,14 @@ def test_random_sparse_parity(seed, dual):
     parity_util.compare(o, ro, g, rg, lp)
 
 
-@pytest.mark.parametrize("shape", [(40, 160), (96, 400), (200, 900)])
-def test_dense_primal_parity(shape):
+@pytest.mark.parametrize("block", ["off", "force"])
+@pytest.mark.parametrize("shape", [(40, 160), (97, 400), (202, 900), (259, 1100)])
+def test_dense_primal_parity(shape, block, monkeypatch):
     """Config-2 family at test size: dense rows make rho dense, so the
-    column-wise update row and the wave-per-column dots are exercised."""
+    column-wise update row and the column dots are exercised, both through
+    the CSC kernels (block=off) and the value-only dense block (force);
+    odd m covers the ColumnScalarProduct tail terms."""
+    monkeypatch.setenv("MILP_DENSE_BLOCK", block)
     lp = lp_gen.dense_box_lp(shape[0], shape[1], 3)
     o, ro, g, rg = parity_util.solve_both(lp, abi.default_params(), _handle)
     parity_util.compare(o, ro, g, rg, lp)
@@ -52,13 +56,37 @@ def test_dense_primal_parity(shape):
     assert st["update_row"]["launches"] > 0
     assert st["primal_norms"]["launches"] > 0
     assert st["pricing"]["launches"] > 0
+    per_launch = st["pricing"]["bytes"] / st["pricing"]["launches"]
+    structural = shape[0] * shape[1]
+    if block == "force":  # dense block streams 8 B per entry, CSC 12 B
+        assert per_launch < 12.0 * structural
+    else:
+        assert per_launch > 12.0 * structural
 
 
-def test_dense_dual_parity():
-    lp = lp_gen.dense_box_lp(80, 300, 11)
+@pytest.mark.parametrize("block", ["off", "force"])
+@pytest.mark.parametrize("seed", [11, 12])
+def test_dense_dual_parity(seed, block, monkeypatch):
+    monkeypatch.setenv("MILP_DENSE_BLOCK", block)
+    lp = lp_gen.dense_box_lp(81 + seed, 300, seed)
     p = abi.default_params(use_dual_simplex=1)
     o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
     parity_util.compare(o, ro, g, rg, lp)
+
+
+def test_mixed_dense_sparse_columns(monkeypatch):
+    """Some full columns next to sparse ones: both kernels share one launch
+    set (dense block + CSC over the remaining columns)."""
+    monkeypatch.setenv("MILP_DENSE_BLOCK", "force")
+    rng = np.random.default_rng(5)
+    m, n = 60, 240
+    dense = rng.uniform(-1, 1, size=(m, n))
+    dense[:, 80:] *= rng.uniform(size=(m, n - 80)) < 0.08
+    lp = lp_gen.from_dense_box(dense, rng)
+    for dual in (0, 1):
+        p = abi.default_params(use_dual_simplex=dual)
+        o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+        parity_util.compare(o, ro, g, rg, lp)
 
 
 def test_warm_start_parity():
