@@ -42,8 +42,11 @@ class DeviceLp {
 
   // --- update row (update_row.cc:77-306) -------------------------------
   // Column-wise: coefficient_[j] = a_j . rho for relevant j.
+  // With w != nullptr the same pass also computes a_j . w for the listed
+  // columns, served by the next ListDotsOverUpdateRow(w) without a 2nd pass.
   void UpdateRowColumnWise(const std::vector<double>& rho, double drop_tolerance,
-                           int64_t relevant_entries);
+                           int64_t relevant_entries,
+                           const std::vector<double>* w = nullptr);
   // algorithm 0 single row, 1 row-wise hypersparse, 2 row-wise.
   void UpdateRowRowWise(const std::vector<int>& filtered_rows,
                         const std::vector<double>& rho, int algorithm,
@@ -91,7 +94,8 @@ class DeviceLp {
   void BuildDenseBlock();
   // Launches the CSC kernel over the sparse columns (all columns when there is
   // no dense block) and the dense-block kernel; mode as in column_dot.
-  void LaunchColumnDots(int mode, const double* d_y, const double* d_c, double* d_out);
+  void LaunchColumnDots(int mode, const double* d_y, const double* d_c, double* d_out,
+                        const double* d_y2 = nullptr, double* d_out2 = nullptr);
   void Check(int err, const char* what);
 
   int device_ = -1;
@@ -137,6 +141,9 @@ class DeviceLp {
   // scratch
   double* d_vec_m_ = nullptr;    // rho / y / dli / ...
   double* d_vec_m2_ = nullptr;   // row-sum output
+  double* d_vec_w_ = nullptr;    // second dot vector of the fused update row
+  bool fused_ready_ = false;     // d_out_n_ holds w . a_j for the listed columns
+  std::vector<double> fused_w_;  // the w those dots were computed with
   double* d_vec_n_ = nullptr;    // x / c
   double* d_coeff_ = nullptr;    // update row coefficients (persistent)
   uint8_t* d_flags_ = nullptr;

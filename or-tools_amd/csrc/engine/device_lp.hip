@@ -125,6 +125,8 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   }
   d_vec_m_ = Alloc<double>(m_);
   d_vec_m2_ = Alloc<double>(m_);
+  d_vec_w_ = Alloc<double>(m_);
+  fused_ready_ = false;
   d_vec_n_ = Alloc<double>(n_total_);
   d_coeff_ = Alloc<double>(n_total_);
   d_flags_ = Alloc<uint8_t>(n_total_);
@@ -196,7 +198,7 @@ void DeviceLp::BuildDenseBlock() {
 }
 
 void DeviceLp::LaunchColumnDots(int mode, const double* d_y, const double* d_c,
-                                double* d_out) {
+                                double* d_out, const double* d_y2, double* d_out2) {
   milp_kernels::DotArgs a{};
   a.starts = d_starts_;
   a.rows = d_rows_;
@@ -204,6 +206,8 @@ void DeviceLp::LaunchColumnDots(int mode, const double* d_y, const double* d_c,
   a.y = d_y;
   a.c = d_c;
   a.out = d_out;
+  a.y2 = d_y2;
+  a.out2 = d_out2;
   a.mask = d_masks_[kRelevant];
   a.flags = d_flags_;
   a.drop_tolerance = 0.0;
@@ -231,6 +235,8 @@ void DeviceLp::LaunchColumnDots(int mode, const double* d_y, const double* d_c,
     d.mask = d_masks_[kRelevant];
     d.c = d_c;
     d.out = d_out;
+    d.y2 = d_y2;
+    d.out2 = d_out2;
     d.flags = d_flags_;
     d.drop_tolerance = drop_;
     Check(milp_launch::dense_dot(mode, d, S(stream_)), "dense dots");
@@ -258,9 +264,15 @@ void DeviceLp::Compact(int n) {
 }
 
 void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
-                                   int64_t relevant_entries) {
+                                   int64_t relevant_entries, const std::vector<double>* w) {
   std::memcpy(h_pin_d_, rho.data(), m_ * sizeof(double));
   Upload(d_vec_m_, h_pin_d_, m_ * sizeof(double));
+  if (w != nullptr) {
+    std::memcpy(h_pin_d2_, w->data(), m_ * sizeof(double));
+    Upload(d_vec_w_, h_pin_d2_, m_ * sizeof(double));
+    fused_w_ = *w;
+  }
+  fused_ready_ = false;
   drop_ = drop;
   // Algorithmic bytes: every relevant column is read (12 B per CSC entry,
   // 8 B per dense-block entry), rho once, coefficients + flags written.
@@ -273,16 +285,25 @@ void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
   }
   const double dense_entries = double(dense_rel) * m_;
   BeginKernel(MI_K_UPDATE_ROW);
-  LaunchColumnDots(0, d_vec_m_, nullptr, d_coeff_);
+  if (w != nullptr) {
+    LaunchColumnDots(4, d_vec_m_, nullptr, d_coeff_, d_vec_w_, d_out_n_);
+  } else {
+    LaunchColumnDots(0, d_vec_m_, nullptr, d_coeff_);
+  }
+  // The fused variant also reads w and writes one more double per listed
+  // column (counted as up to N).
   EndKernel(MI_K_UPDATE_ROW, 12.0 * (double(relevant_entries) - dense_entries) +
-                                 8.0 * dense_entries + 8.0 * m_ + 9.0 * n_total_);
+                                 8.0 * dense_entries + 8.0 * m_ + 9.0 * n_total_ +
+                                 (w != nullptr ? 8.0 * m_ : 0.0));
   Compact(n_total_);
+  fused_ready_ = (w != nullptr);
 }
 
 void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
                                 const std::vector<double>& rho, int algorithm,
                                 double drop) {
   const int k = static_cast<int>(filtered_rows.size());
+  fused_ready_ = false;
   std::memcpy(h_pin_i_, filtered_rows.data(), k * sizeof(int32_t));
   for (int i = 0; i < k; ++i) h_pin_d_[i] = rho[filtered_rows[i]];
   Upload(d_cols_, h_pin_i_, k * sizeof(int32_t));
@@ -344,6 +365,16 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
   const int n = list_count_;
   out->resize(n);
   if (n == 0) return;
+  if (fused_ready_ && v.size() == fused_w_.size() &&
+      std::memcmp(v.data(), fused_w_.data(), v.size() * sizeof(double)) == 0) {
+    // Computed by the fused update-row pass: only the gather remains.
+    fused_ready_ = false;
+    Check(milp_launch::gather(d_list_, n, d_out_n_, d_out_list_, S(stream_)), "gather");
+    Download(h_pin_d_, d_out_list_, n * sizeof(double));
+    std::memcpy(out->data(), h_pin_d_, n * sizeof(double));
+    return;
+  }
+  fused_ready_ = false;
   std::memcpy(h_pin_d2_, v.data(), m_ * sizeof(double));
   Upload(d_vec_m_, h_pin_d2_, m_ * sizeof(double));
   BeginKernel(MI_K_PRIMAL_NORMS);
@@ -357,6 +388,7 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
 
 void DeviceLp::ListDots(const std::vector<int>& cols, const std::vector<double>& v,
                         std::vector<double>* out) {
+  fused_ready_ = false;  // d_out_n_ is reused below
   const int n = static_cast<int>(cols.size());
   out->resize(n);
   if (n == 0) return;
@@ -384,6 +416,7 @@ void DeviceLp::ListDots(const std::vector<int>& cols, const std::vector<double>&
 
 void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& y,
                        std::vector<double>* rc) {
+  fused_ready_ = false;  // d_out_n_ is reused below
   std::memcpy(h_pin_d_, c.data(), n_total_ * sizeof(double));
   Upload(d_vec_n_, h_pin_d_, n_total_ * sizeof(double));
   std::memcpy(h_pin_d2_, y.data(), m_ * sizeof(double));
@@ -401,6 +434,7 @@ void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& 
 }
 
 void DeviceLp::ColumnSquaredNorms(std::vector<double>* out) {
+  fused_ready_ = false;  // d_out_n_ is reused below
   BeginKernel(MI_K_COL_NORMS);
   Check(milp_launch::column_squared_norms(d_starts_, d_vals_, d_masks_[kRelevant], n_total_,
                                           d_out_n_, S(stream_)),

@@ -489,6 +489,7 @@ class UpdateRow {
         dev_(dev) {}
   void SetParameters(const GlopParameters& p) { params_ = p; }
   void Invalidate() {
+    Materialize();
     left_inverse_computed_for_ = kInvalidRow;
     update_row_computed_for_ = kInvalidRow;
   }
@@ -500,6 +501,7 @@ class UpdateRow {
   }
   void ComputeUnitRowLeftInverse(int leaving_row) {
     if (left_inverse_computed_for_ == leaving_row) return;
+    Materialize();  // a deferred pass still needs the current rho
     left_inverse_computed_for_ = leaving_row;
     bf_.LeftSolveForUnitRow(leaving_row, &rho_);
   }
@@ -507,14 +509,33 @@ class UpdateRow {
   bool IsComputedFor(int leaving_row) const {
     return update_row_computed_for_ == leaving_row;
   }
-  const std::vector<Fractional>& GetCoefficients() const { return coefficient_; }
-  const std::vector<int>& GetNonZeroPositions() const { return non_zero_position_list_; }
+  const std::vector<Fractional>& GetCoefficients() const {
+    Materialize();
+    return coefficient_;
+  }
+  const std::vector<int>& GetNonZeroPositions() const {
+    Materialize();
+    return non_zero_position_list_;
+  }
   // Listed positions are mirrored on the host; any other position holds
   // whatever the device update-row kernels left there (same write rules as
   // the host loops), so it is read back from the device.
   Fractional GetCoefficient(int col) const {
+    Materialize();
     if (col < static_cast<int>(listed_.size()) && listed_[col]) return coefficient_[col];
     return dev_->ReadCoefficient(col);
+  }
+  // The column-wise pass is deferred until its result is first read, so the
+  // primal edge-norm update can fuse its a_j . w dots into the same pass over
+  // A. Returns true when that fused pass ran now; the dots are then served by
+  // DeviceLp::ListDotsOverUpdateRow(w).
+  bool MaterializeWithDots(const std::vector<Fractional>& w) {
+    if (!pending_column_wise_) return false;
+    RunColumnWise(&w);
+    return true;
+  }
+  void Materialize() const {
+    if (pending_column_wise_) const_cast<UpdateRow*>(this)->RunColumnWise(nullptr);
   }
   void ComputeFullUpdateRow(int leaving_row, std::vector<Fractional>* output) const;
   double DeterministicTime() const {
@@ -529,6 +550,7 @@ class UpdateRow {
   void ComputeUpdatesColumnWise();
   void ComputeUpdatesForSingleRow(int row_as_col);
   void FetchFromDevice();
+  void RunColumnWise(const std::vector<Fractional>* w);
 
   const CompactSparseMatrix& matrix_;
   const CompactSparseMatrix& transposed_matrix_;
@@ -548,11 +570,17 @@ class UpdateRow {
   int update_row_computed_for_ = kInvalidRow;
   int64_t num_operations_ = 0;
   int last_algorithm_ = -1;
+  // Deferred column-wise pass: the relevance mask and work count it uses are
+  // captured when Glop would have run it (update_row.cc:282-306).
+  bool pending_column_wise_ = false;
+  std::vector<uint64_t> pending_mask_;
+  int64_t pending_relevant_entries_ = 0;
 };
 
 // update_row.cc:77-166
 void UpdateRow::ComputeUpdateRow(int leaving_row) {
   if (update_row_computed_for_ == leaving_row) return;
+  Materialize();
   update_row_computed_for_ = leaving_row;
   ComputeUnitRowLeftInverse(leaving_row);
   if (params_.use_transposed_matrix) {
@@ -655,10 +683,18 @@ void UpdateRow::ComputeUpdatesForSingleRow(int row_as_col) {
 void UpdateRow::ComputeUpdatesColumnWise() {
   coefficient_.resize(matrix_.num_cols(), 0.0);
   listed_.resize(matrix_.num_cols(), 0);
-  dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
-                variables_info_.GetIsRelevantBitRow().NumWords());
-  dev_->UpdateRowColumnWise(rho_.values, params_.drop_tolerance,
-                            variables_info_.GetNumEntriesInRelevantColumns());
+  const Bitset& relevant = variables_info_.GetIsRelevantBitRow();
+  pending_mask_.assign(relevant.data(), relevant.data() + relevant.NumWords());
+  pending_relevant_entries_ = variables_info_.GetNumEntriesInRelevantColumns();
+  pending_column_wise_ = true;
+}
+
+void UpdateRow::RunColumnWise(const std::vector<Fractional>* w) {
+  pending_column_wise_ = false;
+  dev_->SetMask(DeviceLp::kRelevant, pending_mask_.data(),
+                static_cast<int>(pending_mask_.size()));
+  dev_->UpdateRowColumnWise(rho_.values, params_.drop_tolerance, pending_relevant_entries_,
+                            w);
   FetchFromDevice();
 }
 
@@ -814,6 +850,8 @@ void PrimalEdgeNorms::UpdateBeforeBasisPivot(int entering_col, int leaving_col,
   if (!recompute_edge_squared_norms_) {
     update_row->ComputeUpdateRow(leaving_row);
     ComputeDirectionLeftInverse(entering_col, direction);
+    // Column-wise update row and the a_j . w dots share one pass over A.
+    update_row->MaterializeWithDots(direction_left_inverse_.values);
     UpdateEdgeSquaredNorms(entering_col, leaving_col, leaving_row, direction.values,
                            *update_row);
   }

@@ -21,6 +21,8 @@ struct DotArgs {
   uint8_t* flags;           // kUpdateRowColumnWise: |coeff| > drop; kListDots: listed
   double drop_tolerance;
   const uint8_t* skip;      // optional: columns handled by the dense block
+  const double* y2;         // kUpdateRowWithDots: second vector (w = B^-T d)
+  double* out2;             // kUpdateRowWithDots: w . a_j for listed columns
 };
 
 // Dense column block: the structural columns whose CSC column is full (all m
@@ -42,6 +44,8 @@ struct DenseArgs {
   double* out;            // indexed by column id
   uint8_t* flags;         // kUpdateRowColumnWise: out; kListDots: in (listed)
   double drop_tolerance;
+  const double* y2;       // kUpdateRowWithDots
+  double* out2;
 };
 
 struct RowWiseArgs {

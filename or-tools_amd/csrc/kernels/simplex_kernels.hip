@@ -85,7 +85,10 @@ enum DotMode : int {
   kUpdateRowColumnWise = 0,  // update_row.cc:282-306 over relevant columns
   kPricing = 1,              // reduced_costs.cc:372-381: rc = c - a_j.y
   kListDots = 2,             // primal_edge_norms.cc:229-233 over a column list
-  kFullUpdateRow = 3         // update_row.cc:311-332 over non-basic columns
+  kFullUpdateRow = 3,        // update_row.cc:311-332 over non-basic columns
+  // Column-wise update row fused with the primal edge-norm dots
+  // (primal_edge_norms.cc:229-233): one pass over A yields rho.a_j and w.a_j.
+  kUpdateRowWithDots = 4
 };
 
 
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
   const int col = a.col_list != nullptr ? a.col_list[slot] : slot;
   bool active = in_range;
   if (a.skip != nullptr) active = active && !a.skip[col];
-  if (MODE == kUpdateRowColumnWise || MODE == kFullUpdateRow) {
+  if (MODE == kUpdateRowColumnWise || MODE == kFullUpdateRow || MODE == kUpdateRowWithDots) {
     active = active && bit_set(a.mask, col);
   } else if (MODE == kListDots && a.flags != nullptr) {
     active = active && a.flags[col];
@@ -116,10 +119,22 @@ __global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
   const int64_t e = active ? a.starts[col + 1] : s;
   const double dot = WAVE_PER_COL ? wave_column_dot(s, e, a.rows, a.vals, a.y, lane)
                                   : quad_column_dot(s, e, a.rows, a.vals, a.y, sub, lane);
+  double dot2 = 0.0;
+  if (MODE == kUpdateRowWithDots) {  // second sweep of the same column (cache hot)
+    dot2 = WAVE_PER_COL ? wave_column_dot(s, e, a.rows, a.vals, a.y2, lane)
+                        : quad_column_dot(s, e, a.rows, a.vals, a.y2, sub, lane);
+  }
   const bool writer = WAVE_PER_COL ? (lane == 0) : (sub == 0);
   if (!writer || !in_range) return;
   if (a.skip != nullptr && a.skip[col]) return;  // owned by the dense block
-  if (MODE == kUpdateRowColumnWise) {
+  if (MODE == kUpdateRowWithDots) {
+    const bool keep = active && fabs(dot) > a.drop_tolerance;
+    a.flags[col] = keep ? 1 : 0;
+    if (keep) {
+      a.out[col] = dot;
+      a.out2[col] = dot2;
+    }
+  } else if (MODE == kUpdateRowColumnWise) {
     const bool keep = active && fabs(dot) > a.drop_tolerance;
     a.flags[col] = keep ? 1 : 0;
     if (keep) a.out[col] = dot;
@@ -142,19 +157,22 @@ constexpr int kUnroll = 8;
 
 template <int MODE>
 __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
+  constexpr bool kTwo = MODE == kUpdateRowWithDots;
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int j = tid >> 2;
   const int k = tid & 3;
   const bool in_range = j < a.nd;
   const int col = in_range ? a.dense_cols[j] : 0;
   bool active = in_range;
-  if (MODE == kUpdateRowColumnWise) active = active && bit_set(a.mask, col);
+  if (MODE == kUpdateRowColumnWise || kTwo) active = active && bit_set(a.mask, col);
   if (MODE == kListDots) active = active && a.flags[col];
   const int steps = a.m >> 2;
   double acc = 0.0;
+  double acc2 = 0.0;
   if (active) {
     const double* __restrict__ p = a.body + static_cast<int64_t>(j) * 4 + k;
     const double* __restrict__ y = a.y + k;
+    const double* __restrict__ y2 = kTwo ? a.y2 + k : nullptr;
     const int64_t stride = static_cast<int64_t>(a.nd) * 4;
     int t = 0;
     for (; t + kUnroll <= steps; t += kUnroll) {
@@ -162,23 +180,42 @@ __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) v[u] = __builtin_nontemporal_load(p + (t + u) * stride);
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) acc += v[u] * y[(t + u) * 4];
+      for (int u = 0; u < kUnroll; ++u) {
+        acc += v[u] * y[(t + u) * 4];
+        if (kTwo) acc2 += v[u] * y2[(t + u) * 4];
+      }
     }
-    for (; t < steps; ++t) acc += p[t * stride] * y[t * 4];
+    for (; t < steps; ++t) {
+      const double v = p[t * stride];
+      acc += v * y[t * 4];
+      if (kTwo) acc2 += v * y2[t * 4];
+    }
   }
   const double r2 = __shfl_down(acc, 1, kWave);
   const double r3 = __shfl_down(acc, 2, kWave);
   const double r4 = __shfl_down(acc, 3, kWave);
+  double q2 = 0.0, q3 = 0.0, q4 = 0.0;
+  if (kTwo) {
+    q2 = __shfl_down(acc2, 1, kWave);
+    q3 = __shfl_down(acc2, 2, kWave);
+    q4 = __shfl_down(acc2, 3, kWave);
+  }
   if (k != 0 || !in_range) return;
   double result = acc + r2 + r3 + r4;
+  double result2 = acc2 + q2 + q3 + q4;
   const int base = steps * 4;
   for (int r = 0; base + r < a.m; ++r) {
-    result += a.tail[static_cast<int64_t>(r) * a.nd + j] * a.y[base + r];
+    const double v = a.tail[static_cast<int64_t>(r) * a.nd + j];
+    result += v * a.y[base + r];
+    if (kTwo) result2 += v * a.y2[base + r];
   }
-  if (MODE == kUpdateRowColumnWise) {
+  if (MODE == kUpdateRowColumnWise || kTwo) {
     const bool keep = active && fabs(result) > a.drop_tolerance;
     a.flags[col] = keep ? 1 : 0;
-    if (keep) a.out[col] = result;
+    if (keep) {
+      a.out[col] = result;
+      if (kTwo) a.out2[col] = result2;
+    }
   } else if (MODE == kPricing) {
     a.out[col] = a.c[col] - result;
   } else if (MODE == kListDots) {
@@ -367,7 +404,9 @@ hipError_t column_dot(int mode, bool wave_per_col, const DotArgs& args, hipStrea
     case 4: column_dot_kernel<2, false><<<blocks, threads, 0, s>>>(args); break;
     case 5: column_dot_kernel<2, true><<<blocks, threads, 0, s>>>(args); break;
     case 6: column_dot_kernel<3, false><<<blocks, threads, 0, s>>>(args); break;
-    default: column_dot_kernel<3, true><<<blocks, threads, 0, s>>>(args); break;
+    case 7: column_dot_kernel<3, true><<<blocks, threads, 0, s>>>(args); break;
+    case 8: column_dot_kernel<4, false><<<blocks, threads, 0, s>>>(args); break;
+    default: column_dot_kernel<4, true><<<blocks, threads, 0, s>>>(args); break;
   }
   return hipGetLastError();
 }
@@ -378,7 +417,8 @@ hipError_t dense_dot(int mode, const DenseArgs& args, hipStream_t s) {
   switch (mode) {
     case 0: dense_dot_kernel<0><<<blocks, 256, 0, s>>>(args); break;
     case 1: dense_dot_kernel<1><<<blocks, 256, 0, s>>>(args); break;
-    default: dense_dot_kernel<2><<<blocks, 256, 0, s>>>(args); break;
+    case 2: dense_dot_kernel<2><<<blocks, 256, 0, s>>>(args); break;
+    default: dense_dot_kernel<4><<<blocks, 256, 0, s>>>(args); break;
   }
   return hipGetLastError();
 }

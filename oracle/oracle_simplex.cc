@@ -11,6 +11,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
+#include <cmath>
 #include <functional>
 #include <memory>
 #include <queue>
@@ -3631,8 +3633,45 @@ int64_t oracle_lp_get_iteration_times(void* hv, double* out, int64_t cap) {
   return static_cast<int64_t>(t.size());
 }
 
+// LPSolver::SolveWithTimeLimit rejects an LP that is not valid / cleaned up
+// with ProblemStatus::INVALID_PROBLEM (lp_solver.cc:185-202; the checks of
+// LinearProgram::IsValid, lp_data.cc, and IsCleanedUp).
+static bool OracleValidLp(const oracle::LinearProgram& lp) {
+  if (lp.m < 0 || lp.n < 0 || lp.col_starts.size() != static_cast<size_t>(lp.n) + 1) {
+    return false;
+  }
+  if (lp.col_starts[0] != 0) return false;
+  for (int c = 0; c < lp.n; ++c) {
+    if (lp.col_starts[c + 1] < lp.col_starts[c]) return false;
+    for (int64_t k = lp.col_starts[c]; k < lp.col_starts[c + 1]; ++k) {
+      const int r = lp.row_idx[k];
+      if (r < 0 || r >= lp.m) return false;
+      if (k > lp.col_starts[c] && r <= lp.row_idx[k - 1]) return false;
+      if (!(lp.vals[k] != 0.0) || !std::isfinite(lp.vals[k])) return false;
+    }
+  }
+  const double inf = std::numeric_limits<double>::infinity();
+  auto bad = [inf](const std::vector<double>& lo, const std::vector<double>& hi) {
+    for (size_t i = 0; i < lo.size(); ++i) {
+      if (!(lo[i] <= hi[i]) || lo[i] == inf || hi[i] == -inf) return true;
+    }
+    return false;
+  };
+  if (bad(lp.col_lb, lp.col_ub) || bad(lp.row_lb, lp.row_ub)) return false;
+  for (const double c : lp.obj) {
+    if (!std::isfinite(c)) return false;
+  }
+  return std::isfinite(lp.obj_offset) && std::isfinite(lp.obj_scale) && lp.obj_scale != 0.0;
+}
+
 int oracle_lp_solve(void* hv, const volatile int32_t* interrupt, mi_lp_result* out) {
   auto* h = static_cast<OracleHandle*>(hv);
+  if (!OracleValidLp(h->lp)) {
+    std::memset(out, 0, sizeof(*out));
+    out->problem_status = MI_LP_INVALID_PROBLEM;
+    h->solved = false;
+    return 0;
+  }
   h->simplex.SetParameters(h->params);
   oracle::TimeLimit tl;
   tl.max_seconds = h->params.max_time_in_seconds;

@@ -82,3 +82,29 @@ def test_warm_start_bound_change_dual():
     cold.load(lp)
     rc = cold.solve()
     assert r1.iterations <= rc.iterations
+
+
+def _invalid_variants():
+    """LinearProgram::IsValid / IsCleanedUp failures (lp_solver.cc:185-202);
+    pdlp/test_util.cc also ships an invalid / inconsistent-bounds LP."""
+    import copy
+    base, _ = kat_lps.tiny_lp()
+    out = []
+    lp = copy.deepcopy(base); lp.row_lb[0], lp.row_ub[0] = 5.0, 1.0; out.append(("row lb>ub", lp))
+    lp = copy.deepcopy(base); lp.col_lb[1] = np.inf; out.append(("col lb=+inf", lp))
+    lp = copy.deepcopy(base); lp.vals[0] = 0.0; out.append(("explicit zero", lp))
+    lp = copy.deepcopy(base); lp.vals[1] = np.nan; out.append(("nan coefficient", lp))
+    lp = copy.deepcopy(base); lp.obj[2] = np.inf; out.append(("inf objective", lp))
+    lp = copy.deepcopy(base)
+    lp.row_idx[0], lp.row_idx[1] = lp.row_idx[1], lp.row_idx[0]
+    out.append(("unsorted rows", lp))
+    return out
+
+
+@pytest.mark.parametrize("case", _invalid_variants(), ids=lambda c: c[0])
+def test_oracle_invalid_problem(case):
+    _, lp = case
+    o = oracle_lib.OracleLp(abi.default_params())
+    o.load(lp)
+    r = o.solve()
+    assert r.problem_status == abi.INVALID_PROBLEM

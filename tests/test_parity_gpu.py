@@ -139,3 +139,5 @@ def test_invalid_problem_status():
     g.load(lp)
     r = g.solve()
     assert r.problem_status == abi.INVALID_PROBLEM
+    o, ro, g, rg = parity_util.solve_both(lp, abi.default_params(), _handle)
+    parity_util.compare(o, ro, g, rg, lp)
