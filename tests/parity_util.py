@@ -24,7 +24,7 @@ def compare(o, ro, g, rg, lp, rel_tol=1e-6):
     assert rg.problem_status == ro.problem_status, (
         abi.PROBLEM_STATUS[rg.problem_status], abi.PROBLEM_STATUS[ro.problem_status])
     assert rg.iterations == ro.iterations, (rg.iterations, ro.iterations)
-    if ro.error_code != 0:
+    if ro.error_code != 0 or ro.problem_status == abi.INVALID_PROBLEM:
         return
     if np.isfinite(ro.objective):
         assert abs(rg.objective - ro.objective) <= rel_tol * max(1.0, abs(ro.objective)), (
