@@ -77,7 +77,8 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=6)
     ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic-json", default=None,
+    ap.add_argument("--traffic-json",
+                    default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of the dominant kernel from a "
                          "separate rocprofv3 --pmc pass (profiles/)")
     args = ap.parse_args()
@@ -150,8 +151,12 @@ def main():
     ms_per_launch = ds["device_ms"] / launches if ds["device_ms"] > 0 else float("nan")
     achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ds["device_ms"] > 0 else 0.0
     traffic = None
+    traffic_src = None
     if args.traffic_json and os.path.exists(args.traffic_json):
-        traffic = json.load(open(args.traffic_json)).get(dom)
+        tj = json.load(open(args.traffic_json))
+        if dom in tj:
+            traffic = tj[dom]["traffic_bytes_per_launch"]
+            traffic_src = tj.get("_source", args.traffic_json)
 
     if rank != 0:
         return
@@ -189,12 +194,16 @@ def main():
         "roofline": {
             "kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_source": traffic_src,
             "bytes_per_launch": bytes_per_launch, "ms_per_launch": ms_per_launch,
             "launches": ds["launches"],
         },
         "kernels": {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
+                        "call_ms": round(v["call_ms"], 3),
                         "GB": round(v["bytes"] / 1e9, 3)} for k, v in stats.items()
-                    if v["launches"]},
+                    if v["launches"] or v["call_ms"]},
+        "host_ms_per_step": round((1000.0 * elapsed - sum(v["call_ms"] for v in stats.values()))
+                                  / max(1, done), 3),
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

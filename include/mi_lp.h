@@ -157,6 +157,8 @@ typedef struct mi_lp_kernel_stats {
   int64_t launches[16];
   double algorithmic_bytes[16];
   double device_ms[16]; /* HIP-event time, filled when timing is enabled */
+  double call_ms[16];   /* host wall time of the whole device call: uploads,
+                           launches, downloads, synchronization */
 } mi_lp_kernel_stats;
 
 enum {
@@ -169,7 +171,8 @@ enum {
   MI_K_SPMV_ROWS = 6,   /* A x row sums: residual / basic values (variable_values.cc:101-133) */
   MI_K_SINGLE_ROW = 7,  /* ComputeUpdatesForSingleRow (update_row.cc:261-280) */
   MI_K_DUAL_RATIO = 8,  /* dual ratio-test candidate filter (entering_variable.cc:37-130) */
-  MI_K_COUNT = 9
+  MI_K_READBACK = 9,    /* update-row list download / single-coefficient reads */
+  MI_K_COUNT = 10
 };
 
 void mi_glop_params_default(mi_glop_params* p);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 
@@ -15,6 +16,19 @@ namespace milp {
 
 namespace {
 inline hipStream_t S(void* p) { return reinterpret_cast<hipStream_t>(p); }
+
+// Host wall time of one public DeviceLp call, accumulated into call_ms[id].
+struct CallTimer {
+  mi_lp_kernel_stats* stats;
+  int id;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  CallTimer(mi_lp_kernel_stats* s, int i) : stats(s), id(i) {}
+  ~CallTimer() {
+    stats->call_ms[id] += std::chrono::duration<double, std::milli>(
+                              std::chrono::steady_clock::now() - t0)
+                              .count();
+  }
+};
 }  // namespace
 
 void DeviceLp::Check(int err, const char* what) {
@@ -265,6 +279,7 @@ void DeviceLp::Compact(int n) {
 
 void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
                                    int64_t relevant_entries, const std::vector<double>* w) {
+  CallTimer timer(&stats_, MI_K_UPDATE_ROW);
   std::memcpy(h_pin_d_, rho.data(), m_ * sizeof(double));
   Upload(d_vec_m_, h_pin_d_, m_ * sizeof(double));
   if (w != nullptr) {
@@ -302,6 +317,7 @@ void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
 void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
                                 const std::vector<double>& rho, int algorithm,
                                 double drop) {
+  CallTimer timer(&stats_, algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW);
   const int k = static_cast<int>(filtered_rows.size());
   fused_ready_ = false;
   std::memcpy(h_pin_i_, filtered_rows.data(), k * sizeof(int32_t));
@@ -331,6 +347,7 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
 }
 
 void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* values) {
+  CallTimer timer(&stats_, MI_K_READBACK);
   const int n = list_count_;
   positions->resize(n);
   values->resize(n);
@@ -355,6 +372,7 @@ void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* 
 }
 
 double DeviceLp::ReadCoefficient(int col) {
+  CallTimer timer(&stats_, MI_K_READBACK);
   double v = 0.0;
   Download(h_pin_d2_, d_coeff_ + col, sizeof(double));
   v = h_pin_d2_[0];
@@ -362,6 +380,7 @@ double DeviceLp::ReadCoefficient(int col) {
 }
 
 void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<double>* out) {
+  CallTimer timer(&stats_, MI_K_PRIMAL_NORMS);
   const int n = list_count_;
   out->resize(n);
   if (n == 0) return;
@@ -388,6 +407,7 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
 
 void DeviceLp::ListDots(const std::vector<int>& cols, const std::vector<double>& v,
                         std::vector<double>* out) {
+  CallTimer timer(&stats_, MI_K_PRIMAL_NORMS);
   fused_ready_ = false;  // d_out_n_ is reused below
   const int n = static_cast<int>(cols.size());
   out->resize(n);
@@ -416,6 +436,7 @@ void DeviceLp::ListDots(const std::vector<int>& cols, const std::vector<double>&
 
 void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& y,
                        std::vector<double>* rc) {
+  CallTimer timer(&stats_, MI_K_PRICING);
   fused_ready_ = false;  // d_out_n_ is reused below
   std::memcpy(h_pin_d_, c.data(), n_total_ * sizeof(double));
   Upload(d_vec_n_, h_pin_d_, n_total_ * sizeof(double));
@@ -434,6 +455,7 @@ void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& 
 }
 
 void DeviceLp::ColumnSquaredNorms(std::vector<double>* out) {
+  CallTimer timer(&stats_, MI_K_COL_NORMS);
   fused_ready_ = false;  // d_out_n_ is reused below
   BeginKernel(MI_K_COL_NORMS);
   Check(milp_launch::column_squared_norms(d_starts_, d_vals_, d_masks_[kRelevant], n_total_,
@@ -447,6 +469,7 @@ void DeviceLp::ColumnSquaredNorms(std::vector<double>* out) {
 
 void DeviceLp::RowSums(const std::vector<double>& x, bool skip_basic, double sign,
                        std::vector<double>* out) {
+  CallTimer timer(&stats_, MI_K_SPMV_ROWS);
   std::memcpy(h_pin_d_, x.data(), n_total_ * sizeof(double));
   Upload(d_vec_n_, h_pin_d_, n_total_ * sizeof(double));
   milp_kernels::RowSumArgs a{};

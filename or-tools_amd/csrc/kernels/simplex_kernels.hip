@@ -149,11 +149,12 @@ __global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
 
 // ---------------------------------------------------------------------------
 // Dense block dots (layout in kernel_args.h). Lane 4j+k owns chain k of dense
-// column j and walks it sequentially (the order Glop's accumulator r_{k+1}
-// sees); each step of a wave is one coalesced 512-B load. Loads are issued
-// kUnroll steps ahead of the dependent adds. Lane 4j then folds
-// ((r1 + r2) + r3) + r4 and adds the <= 3 tail terms in order.
+// column j and walks it sequentially, two chain elements per 16-byte load, so
+// one wave step is one contiguous 1-KiB load. kUnroll loads are issued ahead
+// of the dependent adds. Lane 4j then folds ((r1 + r2) + r3) + r4 and adds the
+// <= 3 tail terms in order, exactly as ColumnScalarProduct.
 constexpr int kUnroll = 8;
+typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 template <int MODE>
 __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
@@ -167,28 +168,44 @@ __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
   if (MODE == kUpdateRowColumnWise || kTwo) active = active && bit_set(a.mask, col);
   if (MODE == kListDots) active = active && a.flags[col];
   const int steps = a.m >> 2;
+  const int pairs = steps >> 1;
   double acc = 0.0;
   double acc2 = 0.0;
   if (active) {
-    const double* __restrict__ p = a.body + static_cast<int64_t>(j) * 4 + k;
+    const dbl2* __restrict__ p =
+        reinterpret_cast<const dbl2*>(a.body) + static_cast<int64_t>(j) * 4 + k;
     const double* __restrict__ y = a.y + k;
     const double* __restrict__ y2 = kTwo ? a.y2 + k : nullptr;
-    const int64_t stride = static_cast<int64_t>(a.nd) * 4;
+    const int64_t stride = static_cast<int64_t>(a.nd) * 4;  // in double2
     int t = 0;
-    for (; t + kUnroll <= steps; t += kUnroll) {
-      double v[kUnroll];
+    for (; t + kUnroll <= pairs; t += kUnroll) {
+      dbl2 v[kUnroll];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) v[u] = __builtin_nontemporal_load(p + (t + u) * stride);
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
-        acc += v[u] * y[(t + u) * 4];
-        if (kTwo) acc2 += v[u] * y2[(t + u) * 4];
+        const int r = (t + u) * 8;
+        acc += v[u].x * y[r];
+        acc += v[u].y * y[r + 4];
+        if (kTwo) {
+          acc2 += v[u].x * y2[r];
+          acc2 += v[u].y * y2[r + 4];
+        }
       }
     }
-    for (; t < steps; ++t) {
-      const double v = p[t * stride];
-      acc += v * y[t * 4];
-      if (kTwo) acc2 += v * y2[t * 4];
+    for (; t < pairs; ++t) {
+      const dbl2 v = p[t * stride];
+      acc += v.x * y[t * 8];
+      acc += v.y * y[t * 8 + 4];
+      if (kTwo) {
+        acc2 += v.x * y2[t * 8];
+        acc2 += v.y * y2[t * 8 + 4];
+      }
+    }
+    if (steps & 1) {
+      const double v = a.body[static_cast<int64_t>(pairs) * a.nd * 8 + j * 4 + k];
+      acc += v * y[(steps - 1) * 4];
+      if (kTwo) acc2 += v * y2[(steps - 1) * 4];
     }
   }
   const double r2 = __shfl_down(acc, 1, kWave);
@@ -223,25 +240,35 @@ __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
   }
 }
 
-// Builds the dense block from the CSC arrays (one thread per entry).
+// Builds the dense block from the CSC arrays; one thread per destination
+// element so the stores are contiguous.
 __global__ __launch_bounds__(256) void dense_pack_kernel(const int64_t* starts,
                                                          const double* vals,
                                                          const int32_t* dense_cols, int nd,
                                                          int m, double* body, double* tail) {
-  const int64_t total = static_cast<int64_t>(nd) * m;
   const int steps = m >> 2;
+  const int pairs = steps >> 1;
+  const int64_t pair_total = static_cast<int64_t>(pairs) * nd * 8;
+  const int64_t odd_total = (steps & 1) ? static_cast<int64_t>(nd) * 4 : 0;
+  const int64_t tail_total = static_cast<int64_t>(m - 4 * steps) * nd;
+  const int64_t total = pair_total + odd_total + tail_total;
   for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
        e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    // e enumerates the destination in body order for coalesced stores.
-    const int64_t body_total = static_cast<int64_t>(steps) * nd * 4;
-    if (e < body_total) {
-      const int k = static_cast<int>(e & 3);
-      const int64_t q = e >> 2;
-      const int j = static_cast<int>(q % nd);
-      const int t = static_cast<int>(q / nd);
-      body[e] = vals[starts[dense_cols[j]] + 4 * t + k];
+    if (e < pair_total) {
+      const int h = static_cast<int>(e & 1);
+      const int64_t q = e >> 1;
+      const int k = static_cast<int>(q & 3);
+      const int64_t q2 = q >> 2;
+      const int j = static_cast<int>(q2 % nd);
+      const int t2 = static_cast<int>(q2 / nd);
+      body[e] = vals[starts[dense_cols[j]] + 4 * (2 * t2 + h) + k];
+    } else if (e < pair_total + odd_total) {
+      const int64_t f = e - pair_total;
+      const int k = static_cast<int>(f & 3);
+      const int j = static_cast<int>(f >> 2);
+      body[e] = vals[starts[dense_cols[j]] + 4 * (steps - 1) + k];
     } else {
-      const int64_t f = e - body_total;
+      const int64_t f = e - pair_total - odd_total;
       const int j = static_cast<int>(f % nd);
       const int r = static_cast<int>(f / nd);
       tail[f] = vals[starts[dense_cols[j]] + 4 * steps + r];

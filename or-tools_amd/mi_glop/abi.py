@@ -115,6 +115,7 @@ class MiLpKernelStats(ctypes.Structure):
         ("launches", ctypes.c_int64 * 16),
         ("algorithmic_bytes", ctypes.c_double * 16),
         ("device_ms", ctypes.c_double * 16),
+        ("call_ms", ctypes.c_double * 16),
     ]
 
 
@@ -137,7 +138,7 @@ IMPRECISE = 11
 
 # Kernel ids (include/mi_lp.h MI_K_*)
 KERNEL_NAMES = ["pricing", "update_row", "primal_norms", "rc_update", "prices",
-                "col_norms", "spmv_rows", "single_row", "dual_ratio"]
+                "col_norms", "spmv_rows", "single_row", "dual_ratio", "readback"]
 
 # Names of every exported entry point of include/mi_lp.h (checked by tests).
 EXPORTED_SYMBOLS = [

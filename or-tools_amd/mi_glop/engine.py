@@ -172,7 +172,7 @@ class LpHandle:
         s = abi.MiLpKernelStats()
         self._L.mi_lp_get_kernel_stats(self.h, ctypes.byref(s))
         return {name: dict(launches=s.launches[i], bytes=s.algorithmic_bytes[i],
-                           device_ms=s.device_ms[i])
+                           device_ms=s.device_ms[i], call_ms=s.call_ms[i])
                 for i, name in enumerate(abi.KERNEL_NAMES)}
 
     def reset_kernel_stats(self):

@@ -1,0 +1,90 @@
+"""Summarise a rocprofv3 run of bench.py (kernel trace + FETCH_SIZE and
+WRITE_SIZE passes, each its own run) into profiles/<tag>/:
+  kernel_stats.csv   rocprofv3 --stats output, as produced
+  summary.md         per kernel: calls, average duration, HBM bytes/launch
+  traffic.json       per engine kernel id (bench.py names): HBM bytes per
+                     logical launch, for bench.py --traffic-json
+
+FETCH_SIZE / WRITE_SIZE are in KiB. On gfx950 FETCH_SIZE reports half of
+the bytes of a streaming read (MI355X_MICROARCH.md, HBM section); it is
+doubled here. Usage: python scripts/profile_summary.py gpurun_out/prof <tag>
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+GROUPS = {  # HIP kernel name fragment -> engine kernel id (bench.py names)
+    "dense_dot_kernel<1>": "pricing", "column_dot_kernel<1,": "pricing",
+    "dense_dot_kernel<0>": "update_row", "column_dot_kernel<0,": "update_row",
+    "dense_dot_kernel<4>": "update_row", "column_dot_kernel<4,": "update_row",
+    "row_wise_update_kernel": "update_row",
+    "dense_dot_kernel<2>": "primal_norms", "column_dot_kernel<2,": "primal_norms",
+    "row_sum_kernel": "spmv_rows", "column_squared_norm_kernel": "col_norms",
+}
+
+
+def group_of(name):
+    for frag, g in GROUPS.items():
+        if frag in name:
+            return g
+    return None
+
+
+def main(src, tag):
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "profiles", tag)
+    os.makedirs(out, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                os.path.join(out, "kernel_stats.csv"))
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    counters = collections.defaultdict(lambda: collections.defaultdict(float))
+    calls = collections.Counter()
+    for pas, cname in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        path = os.path.join(src, pas, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        for r in csv.DictReader(open(path)):
+            if r["Counter_Name"] != cname:
+                continue
+            kib = float(r["Counter_Value"])
+            counters[r["Kernel_Name"]][cname] += kib * 1024.0 * (2.0 if cname == "FETCH_SIZE" else 1.0)
+            if pas == "fetch":
+                calls[r["Kernel_Name"]] += 1
+    lines = [f"# rocprofv3 summary: {tag}", "",
+             "| kernel | calls | avg us | HBM read MB/launch (FETCH_SIZE x2) | write MB/launch |",
+             "|---|---|---|---|---|"]
+    groups = collections.defaultdict(lambda: [0.0, 0.0, None, 0])  # bytes, ns, anchor, calls
+    for s in stats:
+        name = s["Name"]
+        c = counters.get(name, {})
+        n = max(1, calls.get(name, 0))
+        rd = c.get("FETCH_SIZE", 0.0) / n
+        wr = c.get("WRITE_SIZE", 0.0) / n
+        lines.append(f"| `{name[:90]}` | {s['Calls']} | {float(s['AverageNs']) / 1e3:.1f} | "
+                     f"{rd / 1e6:.2f} | {wr / 1e6:.2f} |")
+        g = group_of(name)
+        if g:
+            total_ns = float(s["TotalDurationNs"])
+            gg = groups[g]
+            gg[0] += (c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0))
+            if gg[2] is None or total_ns > gg[1]:
+                gg[1], gg[2], gg[3] = total_ns, name, calls.get(name, int(s["Calls"]))
+    traffic = {g: {"traffic_bytes_per_launch": v[0] / max(1, v[3]), "anchor_kernel": v[2],
+                   "launches": v[3]} for g, v in groups.items()}
+    json.dump(traffic, open(os.path.join(out, "traffic.json"), "w"), indent=1)
+    latest = dict(traffic, _source=f"profiles/{tag}")
+    json.dump(latest, open(os.path.join(os.path.dirname(out), "traffic_latest.json"), "w"),
+              indent=1)
+    lines += ["", "Per engine kernel id (bytes per logical launch, all HIP kernels of the id):", ""]
+    for g, v in traffic.items():
+        lines.append(f"- {g}: {v['traffic_bytes_per_launch'] / 1e9:.3f} GB/launch "
+                     f"(anchor `{v['anchor_kernel'][:60]}`, {v['launches']} launches)")
+    open(os.path.join(out, "summary.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

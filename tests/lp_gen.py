@@ -76,6 +76,36 @@ def dense_box_lp(m, n, seed, maximize=True):
                          f"dense_{m}x{n}_s{seed}")
 
 
+def sparse_c5_lp(m, n, per_col, seed):
+    """Config 5 generator: about per_col non-zeros per
+    column at distinct random rows, values U([-1,-0.1] u [0.1,1]),
+    x0 ~ U(0,1), rows ranged [A x0 - s, A x0 + s] with s ~ U(0,1),
+    0 <= x <= 10, c = A^T y0 + z with z >= 0 (minimize; dual-feasible-ish
+    start). Vectorised so that m=1e5, n=1e6 builds in seconds."""
+    rng = np.random.default_rng(seed)
+    rows = rng.integers(0, m, size=(n, per_col), dtype=np.int64)
+    rows.sort(axis=1)
+    keep = np.ones_like(rows, dtype=bool)
+    keep[:, 1:] = rows[:, 1:] != rows[:, :-1]
+    lens = keep.sum(axis=1)
+    ri = rows[keep].astype(np.int32)
+    nnz = ri.size
+    mag = rng.uniform(0.1, 1.0, size=nnz)
+    va = np.where(rng.random(nnz) < 0.5, -mag, mag)
+    cs = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=cs[1:])
+    cols = np.repeat(np.arange(n, dtype=np.int64), lens)
+    x0 = rng.uniform(0.0, 1.0, size=n)
+    ax = np.bincount(ri, weights=va * x0[cols], minlength=m)
+    slack = rng.uniform(0.0, 1.0, size=m)
+    y0 = rng.uniform(-1.0, 1.0, size=m)
+    aty = np.bincount(cols, weights=va * y0[ri], minlength=n)
+    obj = aty + rng.uniform(0.0, 1.0, size=n)
+    return LinearProgram(m, n, cs, ri, va, np.zeros(n), np.full(n, 10.0),
+                         ax - slack, ax + slack, obj, 0.0, 1.0, False,
+                         f"c5_{m}x{n}_s{seed}")
+
+
 def from_dense_box(A, rng, maximize=True):
     """Box LP over an arbitrary (possibly partly sparse) matrix A: same row
     and bound construction as dense_box_lp, explicit zeros dropped."""
