@@ -24,6 +24,39 @@
 #include "../../../include/mi_lp.h"
 #include "device_lp.h"
 
+#include <chrono>
+
+namespace milp {
+namespace {
+// Debug aid (env MILP_PHASE_TIMING=1): host wall time per phase of the primal
+// loop, printed to stderr when the solve ends.
+struct PhaseClock {
+  static constexpr int kPhases = 10;
+  const char* names[kPhases] = {"refactor+checks", "entering(pricing)", "direction",
+                                "ratio test",      "values update",     "edge norms",
+                                "rc update",       "prices update",     "pivot",
+                                "other"};
+  double ms[kPhases] = {};
+  bool on = std::getenv("MILP_PHASE_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void Mark(int phase) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    ms[phase] += std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  }
+  void Dump(long long iterations) {
+    if (!on) return;
+    std::fprintf(stderr, "[phase timing] %lld iterations\n", iterations);
+    for (int i = 0; i < kPhases; ++i) {
+      std::fprintf(stderr, "  %-18s %10.3f ms  (%.3f ms/it)\n", names[i], ms[i],
+                   iterations > 0 ? ms[i] / iterations : 0.0);
+    }
+  }
+};
+}  // namespace
+}  // namespace milp
+
 namespace milp {
 
 // ---------------------------------------------------------------------------
@@ -3195,6 +3228,14 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
     std::function<void()> f;
     ~Cleanup() { f(); }
   } cleanup{[this, time_limit]() { AdvanceDeterministicTime(time_limit); }};
+  PhaseClock clock;
+  const int64_t first_iteration = num_iterations_;
+  struct DumpAtExit {
+    PhaseClock* c;
+    const int64_t* it;
+    int64_t first;
+    ~DumpAtExit() { c->Dump(static_cast<long long>(*it - first)); }
+  } dump{&clock, &num_iterations_, first_iteration};
   bool refactorize = false;
   primal_prices_.ForceRecomputation();
   if (phase_ == Phase::FEASIBILITY) {
@@ -3229,7 +3270,9 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
       }
     }
 
+    clock.Mark(0);
     const int entering_col = primal_prices_.GetBestEnteringColumn();
+    clock.Mark(1);
     if (entering_col == kInvalidCol) {
       if (reduced_costs_.AreReducedCostsPrecise() && basis_factorization_.IsRefactorized()) {
         if (phase_ == Phase::FEASIBILITY) {
@@ -3268,6 +3311,7 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
       break;
     }
 
+    clock.Mark(2);
     Fractional step_length;
     int leaving_row;
     Fractional target_bound;
@@ -3279,6 +3323,7 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
                                                       &refactorize, &leaving_row,
                                                       &step_length, &target_bound));
     }
+    clock.Mark(3);
     if (refactorize) continue;
 
     if (step_length == kInfinity || step_length == -kInfinity) {
@@ -3317,14 +3362,19 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
                       (dir < 0.0 && variable_values_.Get(leaving_col) <= target_bound);
     }
     variable_values_.UpdateOnPivoting(direction_, entering_col, step);
+    clock.Mark(4);
     if (leaving_row != kInvalidRow) {
       primal_edge_norms_.UpdateBeforeBasisPivot(entering_col, basis_[leaving_row],
                                                 leaving_row, direction_, &update_row_);
+      clock.Mark(5);
       reduced_costs_.UpdateBeforeBasisPivot(entering_col, leaving_row, direction_,
                                             &update_row_);
+      clock.Mark(6);
       primal_prices_.UpdateBeforeBasisPivot(entering_col, &update_row_);
+      clock.Mark(7);
       if (!is_degenerate) variable_values_.Set(leaving_col, target_bound);
       MILP_RETURN_IF_ERROR(UpdateAndPivot(entering_col, leaving_row, target_bound));
+      clock.Mark(8);
     } else {
       if (step > 0.0) {
         SetNonBasicVariableStatusAndDeriveValue(entering_col, VariableStatus::AT_UPPER_BOUND);
@@ -3339,6 +3389,7 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
       primal_prices_.RecomputePriceAt(leaving_col);
     }
     OnIterationDone(time_limit);
+    clock.Mark(9);
   }
   return Status::OK();
 }
