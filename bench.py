@@ -26,7 +26,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "or-tools_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
-from mi_glop import abi, engine  # noqa: E402
+from mi_glop import abi, distributed, engine  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "simplex iterations/sec + batched LPs/sec, 1/2/4/8 MI355X vs Glop CPU"
@@ -66,6 +66,65 @@ def cpu_baseline(lp, warm, iters):
                       timed_iterations=iters, warm_iterations=warm)
 
 
+def run_batched(args, rank, world, local_rank, dist, barrier, sync):
+    """Config 4: children of one CP-SAT-style search node,
+    sharded across ranks (each rank its own children, weak scaling), solved
+    by `workers` GPU handles per rank with the dual simplex warm-started from
+    the root basis. The only collective: all-reduce(min) of the best child
+    bound (RCCL), the cross-GPU analogue of
+    SharedResponseManager::UpdateInnerObjectiveBounds."""
+    import jobshop
+    jobs = jobshop.random_instance(args.batch_jobs, args.batch_machines, args.seed)
+    lp, ycols = jobshop.relaxation(jobs)
+    root = engine.LpHandle(abi.default_params(use_dual_simplex=1), device=local_rank)
+    root.load(lp)
+    root_res = root.solve()
+    state = root.state()
+    # The node's children, sharded across ranks (each rank: batch_lps of them).
+    all_lbs, all_ubs = jobshop.child_bounds(lp, ycols, args.batch_lps * world, args.seed + 1000)
+    b, e = distributed.shard(args.batch_lps * world, rank, world)
+    lbs, ubs = all_lbs[b:e], all_ubs[b:e]
+    del all_lbs, all_ubs
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
+    workers = [engine.LpHandle(p, device=local_rank) for _ in range(args.batch_workers)]
+    for w in workers:
+        w.load(lp)
+    # Warm-up batch (not timed): first-touch allocations on every worker.
+    engine.batch_solve_bounds(workers, lbs[:args.batch_workers], ubs[:args.batch_workers], state)
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    res = engine.batch_solve_bounds(workers, lbs, ubs, state)
+    best = distributed.share_bound(distributed.best_bound(res, abi.OPTIMAL), dist, "cuda")
+    sync()
+    barrier()
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+    total = args.batch_lps * world
+    out = {
+        "metric": "batched LPs/sec", "value": total / elapsed, "unit": "LPs/s",
+        "lps": total, "seconds": elapsed, "workers_per_gpu": args.batch_workers,
+        "mean_iterations": float(np.mean([r.iterations for r in res])),
+        "best_bound": best, "root_iterations": int(root_res.iterations),
+        "workload": (f"config 4: job-shop {args.batch_jobs}x{args.batch_machines} "
+                     f"(seeded, ta041-shaped family) big-M LP relaxation, m={lp.m} n={lp.n}; "
+                     f"{args.batch_lps} children/GPU with two order variables fixed, dual "
+                     f"simplex warm-started from the root basis, cap 1000 iterations"),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import oracle_lib
+        ows = [oracle_lib.OracleLp(p) for _ in range(args.batch_workers)]
+        for w in ows:
+            w.load(lp)
+        n_cpu = min(len(lbs), args.batch_cpu_lps)
+        t0 = time.perf_counter()
+        oracle_lib.batch_solve_bounds(ows, lbs[:n_cpu], ubs[:n_cpu], state)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {
+            "value": n_cpu / dt, "unit": "LPs/s", "cores": args.batch_workers, "kind": "port",
+            "sample": f"oracle, {args.batch_workers} threads, first {n_cpu} of the same children"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,6 +136,12 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=6)
     ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--batch-lps", type=int, default=512,
+                    help="config-4 children per GPU (0 disables the batched section)")
+    ap.add_argument("--batch-workers", type=int, default=8)
+    ap.add_argument("--batch-jobs", type=int, default=15)
+    ap.add_argument("--batch-machines", type=int, default=10)
+    ap.add_argument("--batch-cpu-lps", type=int, default=512)
     ap.add_argument("--traffic-json",
                     default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of the dominant kernel from a "
@@ -142,6 +207,7 @@ def main():
     log(f"timed window: {done} iterations in {elapsed:.3f}s")
     h.stop()  # the bench times a window, not the whole solve
     h.finish()
+    del h  # release the C2 matrix copies before the batched section
 
     # Dominant kernel in the timed region: roofline vs HBM peak.
     dom = max(stats, key=lambda k: stats[k]["device_ms"])
@@ -158,6 +224,11 @@ def main():
             traffic = tj[dom]["traffic_bytes_per_launch"]
             traffic_src = tj.get("_source", args.traffic_json)
 
+    batched = None
+    if args.batch_lps > 0:
+        log(f"batched section: {args.batch_lps} children per GPU")
+        batched = run_batched(args, rank, world, local_rank, dist, barrier, sync)
+        log(f"batched: {batched['value']:.1f} LPs/s")
     if rank != 0:
         return
     cpu = None
@@ -205,6 +276,7 @@ def main():
         "host_ms_per_step": round((1000.0 * elapsed - sum(v["call_ms"] for v in stats.values()))
                                   / max(1, done), 3),
         "cpu_baseline": cpu,
+        "batched": batched,
     }
     print(json.dumps(line), flush=True)
 

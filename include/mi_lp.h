@@ -196,6 +196,10 @@ int mi_lp_load(mi_lp* h, int32_t m, int32_t n, const int64_t* col_starts,
 /* statuses: n+m glop::VariableStatus values (structural then slacks). */
 int mi_lp_load_basis_state(mi_lp* h, const int8_t* statuses, int32_t len);
 int mi_lp_clear_basis_state(mi_lp* h);
+/* Replaces the variable bounds of the loaded LP (n each); the matrix stays
+ * resident in HBM. LinearProgram::SetVariableBounds as CP-SAT does before
+ * each LP solve (sat/linear_programming_constraint.cc:412, 512, 535, 705). */
+int mi_lp_set_variable_bounds(mi_lp* h, const double* col_lb, const double* col_ub);
 int mi_lp_notify_matrix_unchanged(mi_lp* h);
 
 /* interrupt may be NULL; a non-zero value stops the solve like a time limit
@@ -235,6 +239,13 @@ int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable);
  * the same device), using worker threads each owning its own stream. */
 int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
                       mi_lp_result* results);
+/* Batched children of one search node: count LPs that share
+ * the workers' loaded matrix and differ in variable bounds (lbs/ubs are
+ * count x n, row-major), each warm-started from warm_state (n+m statuses,
+ * may be NULL) like LoadStateForNextSolve. One host thread per worker. */
+int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t count,
+                             const double* lbs, const double* ubs, const int8_t* warm_state,
+                             int32_t warm_len, mi_lp_result* results);
 
 #ifdef __cplusplus
 }

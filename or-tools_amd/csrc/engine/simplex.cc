@@ -3911,6 +3911,14 @@ int mi_lp_load_basis_state(mi_lp* h, const int8_t* st, int32_t len) {
   return MI_LP_OK;
 }
 
+int mi_lp_set_variable_bounds(mi_lp* h, const double* col_lb, const double* col_ub) {
+  if (h == nullptr || col_lb == nullptr || col_ub == nullptr) return MI_LP_ERROR_NULL;
+  if (!h->loaded) return MI_LP_ERROR_STATE;
+  h->lp.col_lb.assign(col_lb, col_lb + h->lp.n);
+  h->lp.col_ub.assign(col_ub, col_ub + h->lp.n);
+  return MI_LP_OK;
+}
+
 int mi_lp_clear_basis_state(mi_lp* h) {
   if (h == nullptr) return MI_LP_ERROR_NULL;
   h->simplex.ClearStateForNextSolve();
@@ -4100,6 +4108,48 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
   }
   for (auto& th : pool) th.join();
   return MI_LP_OK;
+}
+
+// One search node's children: LP i = the workers' common LP with variable
+// bounds lbs/ubs[i * n ...], warm-started from warm_state when given.
+// Workers (handles loaded with the same LP, any devices) pull LPs from a
+// shared counter, one host thread per worker.
+int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t count,
+                             const double* lbs, const double* ubs, const int8_t* warm_state,
+                             int32_t warm_len, mi_lp_result* results) {
+  if (workers == nullptr || lbs == nullptr || ubs == nullptr || results == nullptr) {
+    return MI_LP_ERROR_NULL;
+  }
+  if (num_workers < 1) return MI_LP_ERROR_INVALID_PROBLEM;
+  for (int w = 0; w < num_workers; ++w) {
+    if (workers[w] == nullptr) return MI_LP_ERROR_NULL;
+    if (!workers[w]->loaded || workers[w]->lp.n != workers[0]->lp.n) return MI_LP_ERROR_STATE;
+  }
+  const int64_t n = workers[0]->lp.n;
+  std::atomic<int> next(0);
+  std::atomic<int> first_error(MI_LP_OK);
+  std::vector<std::thread> pool;
+  for (int w = 0; w < num_workers; ++w) {
+    pool.emplace_back([&, w]() {
+      mi_lp* h = workers[w];
+      (void)hipSetDevice(h->device);
+      while (true) {
+        const int i = next.fetch_add(1);
+        if (i >= count) break;
+        mi_lp_set_variable_bounds(h, lbs + i * n, ubs + i * n);
+        if (warm_state != nullptr) {
+          const int rc = mi_lp_load_basis_state(h, warm_state, warm_len);
+          if (rc != MI_LP_OK) {
+            int expected = MI_LP_OK;
+            first_error.compare_exchange_strong(expected, rc);
+          }
+        }
+        RunSolve(h, nullptr, &results[i]);
+      }
+    });
+  }
+  for (auto& th : pool) th.join();
+  return first_error.load();
 }
 
 }  // extern "C"

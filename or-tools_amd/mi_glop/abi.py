@@ -151,5 +151,6 @@ EXPORTED_SYMBOLS = [
     "mi_lp_get_primal_ray", "mi_lp_get_dual_ray",
     "mi_lp_get_dual_ray_row_combination", "mi_lp_begin", "mi_lp_run_until",
     "mi_lp_finish", "mi_lp_stop", "mi_lp_get_kernel_stats", "mi_lp_reset_kernel_stats",
-    "mi_lp_set_kernel_timing", "mi_lp_batch_solve",
+    "mi_lp_set_kernel_timing", "mi_lp_batch_solve", "mi_lp_set_variable_bounds",
+    "mi_lp_batch_solve_bounds",
 ]

@@ -64,6 +64,9 @@ def lib():
     L.mi_lp_set_kernel_timing.argtypes = [vp, ctypes.c_int32]
     L.mi_lp_batch_solve.argtypes = [vp, ctypes.c_int32, ctypes.c_int32,
                                     ctypes.POINTER(abi.MiLpResult)]
+    L.mi_lp_set_variable_bounds.argtypes = [vp, vp, vp]
+    L.mi_lp_batch_solve_bounds.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
+                                           ctypes.c_int32, ctypes.POINTER(abi.MiLpResult)]
     _lib = L
     return L
 
@@ -124,6 +127,12 @@ class LpHandle:
                                        _p(clb), _p(cub), _p(rlb), _p(rub), _p(ob),
                                        lp.obj_offset, lp.obj_scale, int(lp.maximize)),
                     "mi_lp_load")
+
+    def set_variable_bounds(self, col_lb, col_ub):
+        lb = np.ascontiguousarray(col_lb, dtype=np.float64)
+        ub = np.ascontiguousarray(col_ub, dtype=np.float64)
+        self._check(self._L.mi_lp_set_variable_bounds(self.h, _p(lb), _p(ub)),
+                    "mi_lp_set_variable_bounds")
 
     def load_basis_state(self, state):
         st = np.ascontiguousarray(state, dtype=np.int8)
@@ -226,4 +235,25 @@ def batch_solve(handles, num_threads=4):
     arr = (ctypes.c_void_p * len(handles))(*[h.h.value for h in handles])
     res = (abi.MiLpResult * len(handles))()
     L.mi_lp_batch_solve(arr, len(handles), num_threads, res)
+    return list(res)
+
+
+def batch_solve_bounds(workers, lbs, ubs, warm_state=None):
+    """Children of one search node: LP i = the workers' loaded LP with
+    variable bounds lbs[i], ubs[i], warm-started from warm_state
+    (mi_lp_batch_solve_bounds). Returns the list of MiLpResult."""
+    L = lib()
+    for w in workers:
+        w._push_params()
+    lbs = np.ascontiguousarray(lbs, dtype=np.float64)
+    ubs = np.ascontiguousarray(ubs, dtype=np.float64)
+    count = lbs.shape[0]
+    arr = (ctypes.c_void_p * len(workers))(*[w.h.value for w in workers])
+    res = (abi.MiLpResult * count)()
+    ws = None if warm_state is None else np.ascontiguousarray(warm_state, dtype=np.int8)
+    rc = L.mi_lp_batch_solve_bounds(arr, len(workers), count, _p(lbs), _p(ubs),
+                                    None if ws is None else _p(ws),
+                                    0 if ws is None else len(ws), res)
+    if rc != 0:
+        raise RuntimeError(f"mi_lp_batch_solve_bounds failed ({rc})")
     return list(res)

@@ -11,6 +11,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <thread>
 #include <limits>
 #include <cmath>
 #include <functional>
@@ -3741,6 +3743,38 @@ int oracle_lp_get_dual_ray(void* hv, double* v) {
   const auto& r = h->simplex.GetDualRay();
   for (size_t i = 0; i < r.size(); ++i) v[i] = r[i];
   return static_cast<int>(r.size());
+}
+
+int oracle_lp_set_variable_bounds(void* hv, const double* lb, const double* ub) {
+  auto* h = static_cast<OracleHandle*>(hv);
+  h->lp.col_lb.assign(lb, lb + h->lp.n);
+  h->lp.col_ub.assign(ub, ub + h->lp.n);
+  return 0;
+}
+
+// CPU baseline of mi_lp_batch_solve_bounds: same scheduling (shared counter,
+// one thread per worker handle).
+int oracle_lp_batch_solve_bounds(void* const* workers, int32_t num_workers, int32_t count,
+                                 const double* lbs, const double* ubs,
+                                 const int8_t* warm_state, int32_t warm_len,
+                                 mi_lp_result* results) {
+  const int64_t n = static_cast<OracleHandle*>(workers[0])->lp.n;
+  std::atomic<int> next(0);
+  std::vector<std::thread> pool;
+  for (int w = 0; w < num_workers; ++w) {
+    pool.emplace_back([&, w]() {
+      void* h = workers[w];
+      while (true) {
+        const int i = next.fetch_add(1);
+        if (i >= count) break;
+        oracle_lp_set_variable_bounds(h, lbs + i * n, ubs + i * n);
+        if (warm_state != nullptr) oracle_lp_load_basis_state(h, warm_state, warm_len);
+        oracle_lp_solve(h, nullptr, &results[i]);
+      }
+    });
+  }
+  for (auto& t : pool) t.join();
+  return 0;
 }
 
 }  // extern "C"

@@ -45,6 +45,10 @@ def lib():
         L.oracle_lp_notify_matrix_unchanged.argtypes = [vp]
         L.oracle_lp_record_iteration_times.argtypes = [vp, ctypes.c_int32]
         L.oracle_lp_get_iteration_times.argtypes = [vp, ctypes.c_void_p, ctypes.c_int64]
+        L.oracle_lp_set_variable_bounds.argtypes = [vp, vp, vp]
+        L.oracle_lp_batch_solve_bounds.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp,
+                                                   vp, ctypes.c_int32,
+                                                   ctypes.POINTER(abi.MiLpResult)]
         L.oracle_lp_get_iteration_times.restype = ctypes.c_int64
         _lib = L
     return _lib
@@ -81,6 +85,11 @@ class OracleLp:
         self._L.oracle_lp_load(self.h, lp.m, lp.n, _p(cs), _p(ri), _p(v), _p(clb),
                                _p(cub), _p(rlb), _p(rub), _p(ob), lp.obj_offset,
                                lp.obj_scale, int(lp.maximize))
+
+    def set_variable_bounds(self, col_lb, col_ub):
+        self._lbk = np.ascontiguousarray(col_lb, dtype=np.float64)
+        self._ubk = np.ascontiguousarray(col_ub, dtype=np.float64)
+        self._L.oracle_lp_set_variable_bounds(self.h, _p(self._lbk), _p(self._ubk))
 
     def load_basis_state(self, state):
         st = np.ascontiguousarray(state, dtype=np.int8)
@@ -141,3 +150,21 @@ class OracleLp:
 
     def dual_ray(self):
         return self._get("oracle_lp_get_dual_ray", self.lp.m, np.float64)
+
+
+def batch_solve_bounds(workers, lbs, ubs, warm_state=None):
+    """CPU baseline / checker of engine.batch_solve_bounds (one thread per
+    oracle worker, shared LP counter)."""
+    L = lib()
+    for w in workers:
+        L.oracle_lp_set_params(w.h, ctypes.byref(w.params))
+    lbs = np.ascontiguousarray(lbs, dtype=np.float64)
+    ubs = np.ascontiguousarray(ubs, dtype=np.float64)
+    count = lbs.shape[0]
+    arr = (ctypes.c_void_p * len(workers))(*[w.h.value for w in workers])
+    res = (abi.MiLpResult * count)()
+    ws = None if warm_state is None else np.ascontiguousarray(warm_state, dtype=np.int8)
+    L.oracle_lp_batch_solve_bounds(arr, len(workers), count, _p(lbs), _p(ubs),
+                                   None if ws is None else _p(ws),
+                                   0 if ws is None else len(ws), res)
+    return list(res)

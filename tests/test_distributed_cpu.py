@@ -1,0 +1,92 @@
+"""World-size-2 gloo test of the multi-GPU layer (mi_glop.distributed) on
+CPU: the node's children are sharded across ranks, each rank solves its
+shard (the CPU oracle stands in for the GPU engine here), and the RCCL
+all-reduce(min) of the bound -- gloo on CPU -- must equal the single-process
+minimum over all children; the MAX-over-ranks timing helper likewise."""
+import math
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _children():
+    import jobshop
+    from mi_glop import abi
+    import oracle_lib
+    lp, ycols = jobshop.relaxation(jobshop.FT06)
+    root = oracle_lib.OracleLp(abi.default_params(use_dual_simplex=1))
+    root.load(lp)
+    root.solve()
+    lbs, ubs = jobshop.child_bounds(lp, ycols, 10, 3)
+    return lp, root.state(), lbs, ubs
+
+
+def _worker(rank, world, port, out_dir):
+    sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "or-tools_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mi_glop import abi, distributed
+    import oracle_lib
+    lp, state, lbs, ubs = _children()
+    b, e = distributed.shard(len(lbs), rank, world)
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
+    ws = [oracle_lib.OracleLp(p) for _ in range(2)]
+    for w in ws:
+        w.load(lp)
+    res = oracle_lib.batch_solve_bounds(ws, lbs[b:e], ubs[b:e], state)
+    local = distributed.best_bound(res, abi.OPTIMAL)
+    shared = distributed.share_bound(local, dist)
+    slowest = distributed.max_over_ranks(float(rank + 1), dist)
+    with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
+        f.write(f"{b} {e} {local!r} {shared!r} {slowest!r}\n")
+    dist.destroy_process_group()
+
+
+def test_shard_partition():
+    from mi_glop import distributed
+    for count in (0, 1, 7, 16, 1001):
+        for world in (1, 2, 3, 8):
+            blocks = [distributed.shard(count, r, world) for r in range(world)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == count
+            assert all(blocks[i][1] == blocks[i + 1][0] for i in range(world - 1))
+            sizes = [e - b for b, e in blocks]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_bound_share_world2(tmp_path):
+    from mi_glop import abi, distributed
+    import oracle_lib
+    port = _free_port()
+    mp.start_processes(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    rows = [open(tmp_path / f"r{r}.txt").read().split() for r in range(2)]
+    # Single-process reference over all children.
+    lp, state, lbs, ubs = _children()
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
+    o = oracle_lib.OracleLp(p)
+    o.load(lp)
+    best = math.inf
+    for i in range(len(lbs)):
+        o.set_variable_bounds(lbs[i], ubs[i])
+        o.load_basis_state(state)
+        r = o.solve()
+        if r.problem_status == abi.OPTIMAL:
+            best = min(best, r.objective)
+    assert [int(rows[0][0]), int(rows[0][1]), int(rows[1][0]), int(rows[1][1])] == [0, 5, 5, 10]
+    for row in rows:
+        assert float(row[3]) == best  # all-reduce(min) = global best bound
+        assert float(row[4]) == 2.0   # max over ranks
+    assert min(float(rows[0][2]), float(rows[1][2])) == best

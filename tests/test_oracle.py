@@ -108,3 +108,28 @@ def test_oracle_invalid_problem(case):
     o.load(lp)
     r = o.solve()
     assert r.problem_status == abi.INVALID_PROBLEM
+
+
+def test_oracle_batched_children_match_sequential():
+    """The batch scheduler (shared counter, 4 worker handles) gives every
+    child the same result as a fresh sequential solve (C4 workload)."""
+    import jobshop
+    lp, ycols = jobshop.relaxation(jobshop.FT06)
+    root = oracle_lib.OracleLp(abi.default_params(use_dual_simplex=1))
+    root.load(lp)
+    assert root.solve().problem_status == abi.OPTIMAL
+    st = root.state()
+    lbs, ubs = jobshop.child_bounds(lp, ycols, 32, 5)
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
+    ws = [oracle_lib.OracleLp(p) for _ in range(4)]
+    for w in ws:
+        w.load(lp)
+    res = oracle_lib.batch_solve_bounds(ws, lbs, ubs, st)
+    o = oracle_lib.OracleLp(p)
+    o.load(lp)
+    for i in range(32):
+        o.set_variable_bounds(lbs[i], ubs[i])
+        o.load_basis_state(st)
+        r = o.solve()
+        assert (res[i].problem_status, res[i].iterations, res[i].objective) == \
+            (r.problem_status, r.iterations, r.objective)

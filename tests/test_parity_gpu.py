@@ -11,6 +11,7 @@ from mi_glop import abi, engine
 
 import kat_lps
 import lp_gen
+import oracle_lib
 import parity_util
 
 pytestmark = pytest.mark.gpu
@@ -141,3 +142,32 @@ def test_invalid_problem_status():
     assert r.problem_status == abi.INVALID_PROBLEM
     o, ro, g, rg = parity_util.solve_both(lp, abi.default_params(), _handle)
     parity_util.compare(o, ro, g, rg, lp)
+
+
+@pytest.mark.parametrize("shape", [(6, 6), (10, 10)])
+def test_batched_children_parity(shape):
+    """Config-4 batch: children of one search node (bounds of two order
+    variables fixed), warm-started from the root basis, solved by 4 GPU
+    workers; each child must match the oracle solving it alone."""
+    import jobshop
+    jobs = jobshop.FT06 if shape == (6, 6) else jobshop.random_instance(*shape, 3)
+    lp, ycols = jobshop.relaxation(jobs)
+    root = engine.LpHandle(abi.default_params(use_dual_simplex=1))
+    root.load(lp)
+    assert root.solve().problem_status == abi.OPTIMAL
+    state = root.state()
+    lbs, ubs = jobshop.child_bounds(lp, ycols, 24, 11)
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
+    workers = [engine.LpHandle(p) for _ in range(4)]
+    for w in workers:
+        w.load(lp)
+    res = engine.batch_solve_bounds(workers, lbs, ubs, state)
+    o = oracle_lib.OracleLp(p)
+    o.load(lp)
+    for i, r in enumerate(res):
+        o.set_variable_bounds(lbs[i], ubs[i])
+        o.load_basis_state(state)
+        ro = o.solve()
+        assert (r.error_code, r.problem_status, r.iterations) == \
+            (ro.error_code, ro.problem_status, ro.iterations), i
+        assert r.objective == ro.objective, (i, r.objective, ro.objective)
