@@ -65,8 +65,14 @@ class DeviceLp {
                 std::vector<double>* out);
 
   // --- pricing (reduced_costs.cc:352-423) ------------------------------
+  // With w != nullptr the same pass over A also computes a_j . w for the
+  // columns listed by the last update row (the primal edge-norm dots of the
+  // previous pivot, primal_edge_norms.cc:229-233), returned in list order.
   void Pricing(const std::vector<double>& c, const std::vector<double>& y,
-               std::vector<double>* rc);
+               std::vector<double>* rc, const std::vector<double>* w = nullptr,
+               std::vector<double>* list_dots = nullptr);
+  // Changes whenever the device-side update-row list (and its flags) changes.
+  uint64_t list_epoch() const { return list_epoch_; }
 
   // --- 1 + ||a_j||^2 for relevant j (identity basis) -------------------
   void ColumnSquaredNorms(std::vector<double>* out);
@@ -155,14 +161,18 @@ class DeviceLp {
   double* d_rho_vals_ = nullptr; // filtered rho values
   void* d_cub_temp_ = nullptr;
   size_t cub_temp_bytes_ = 0;
+  double* d_out_n2_ = nullptr;   // w . a_j of the fused pricing pass
   int list_count_ = 0;
+  uint64_t list_epoch_ = 0;
   int64_t list_entries_ = 0;  // CSC entries over the listed sparse columns
   int64_t list_dense_ = 0;    // listed dense columns
+  int dense_unroll_ = 16;     // MILP_DENSE_UNROLL: 16-B loads in flight per lane
 
   // pinned staging
   int32_t* h_pin_i_ = nullptr;
   double* h_pin_d_ = nullptr;
   double* h_pin_d2_ = nullptr;
+  double* h_pin_w_ = nullptr;
 };
 
 }  // namespace milp

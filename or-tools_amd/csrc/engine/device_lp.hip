@@ -45,6 +45,7 @@ DeviceLp::~DeviceLp() {
   if (h_pin_i_) (void)hipHostFree(h_pin_i_);
   if (h_pin_d_) (void)hipHostFree(h_pin_d_);
   if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
+  if (h_pin_w_) (void)hipHostFree(h_pin_w_);
   if (ev_start_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_start_));
   if (ev_stop_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_stop_));
   if (stream_) (void)hipStreamDestroy(S(stream_));
@@ -66,6 +67,10 @@ void DeviceLp::Init(int device) {
   Check(hipEventCreate(&b), "hipEventCreate");
   ev_start_ = a;
   ev_stop_ = b;
+  if (const char* u = std::getenv("MILP_DENSE_UNROLL")) {
+    const int v = std::atoi(u);
+    if (v == 8 || v == 16 || v == 32) dense_unroll_ = v;
+  }
 }
 
 template <typename T>
@@ -147,6 +152,7 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   d_list_ = Alloc<int32_t>(n_total_);
   d_count_ = Alloc<int>(1);
   d_out_n_ = Alloc<double>(n_total_);
+  d_out_n2_ = Alloc<double>(n_total_);
   d_out_list_ = Alloc<double>(std::max(n_total_, m_));
   d_cols_ = Alloc<int32_t>(std::max(n_total_, m_));
   d_rho_vals_ = Alloc<double>(m_);
@@ -161,11 +167,14 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   if (h_pin_i_) (void)hipHostFree(h_pin_i_);
   if (h_pin_d_) (void)hipHostFree(h_pin_d_);
   if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
+  if (h_pin_w_) (void)hipHostFree(h_pin_w_);
   const size_t big = std::max(n_total_, m_) + 1;
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_i_), big * sizeof(int32_t)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d_), big * sizeof(double)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d2_), big * sizeof(double)), "pin");
+  Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_w_), (m_ + 1) * sizeof(double)), "pin");
   list_count_ = 0;
+  ++list_epoch_;
   BuildDenseBlock();
   Synchronize();
 }
@@ -253,7 +262,7 @@ void DeviceLp::LaunchColumnDots(int mode, const double* d_y, const double* d_c,
     d.out2 = d_out2;
     d.flags = d_flags_;
     d.drop_tolerance = drop_;
-    Check(milp_launch::dense_dot(mode, d, S(stream_)), "dense dots");
+    Check(milp_launch::dense_dot(mode, dense_unroll_, d, S(stream_)), "dense dots");
   }
 }
 
@@ -275,6 +284,7 @@ void DeviceLp::Compact(int n) {
   Download(h_pin_i_, d_count_, sizeof(int));
   count = h_pin_i_[0];
   list_count_ = count;
+  ++list_epoch_;
 }
 
 void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
@@ -435,23 +445,48 @@ void DeviceLp::ListDots(const std::vector<int>& cols, const std::vector<double>&
 }
 
 void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& y,
-                       std::vector<double>* rc) {
+                       std::vector<double>* rc, const std::vector<double>* w,
+                       std::vector<double>* list_dots) {
   CallTimer timer(&stats_, MI_K_PRICING);
   fused_ready_ = false;  // d_out_n_ is reused below
+  const bool fused = (w != nullptr);
+  if (fused && list_dots == nullptr) throw DeviceError("fused pricing needs list_dots");
   std::memcpy(h_pin_d_, c.data(), n_total_ * sizeof(double));
   Upload(d_vec_n_, h_pin_d_, n_total_ * sizeof(double));
   std::memcpy(h_pin_d2_, y.data(), m_ * sizeof(double));
   Upload(d_vec_m_, h_pin_d2_, m_ * sizeof(double));
+  if (fused) {
+    std::memcpy(h_pin_w_, w->data(), m_ * sizeof(double));
+    Upload(d_vec_w_, h_pin_w_, m_ * sizeof(double));
+  }
+  const int n_list = fused ? list_count_ : 0;
   BeginKernel(MI_K_PRICING);
-  LaunchColumnDots(1, d_vec_m_, d_vec_n_, d_out_n_);
+  if (fused) {
+    LaunchColumnDots(5, d_vec_m_, d_vec_n_, d_out_n_, d_vec_w_, d_out_n2_);
+    Check(milp_launch::gather(d_list_, n_list, d_out_n2_, d_out_list_, S(stream_)), "gather");
+  } else {
+    LaunchColumnDots(1, d_vec_m_, d_vec_n_, d_out_n_);
+  }
   // 12 B per CSC entry of [A|I] (8 B per dense-block entry) + column starts
-  // + y + c in + rc out.
+  // + y + c in + rc out; the fused pass also reads w, the flags,
+  // and writes + gathers one dot per listed column.
   const double dense_entries = double(nd_) * m_;
   EndKernel(MI_K_PRICING, 12.0 * double(sparse_entries_) + 8.0 * dense_entries +
-                              8.0 * (n_total_ + 1) + 8.0 * m_ + 16.0 * n_total_);
+                              8.0 * (n_total_ + 1) + 8.0 * m_ + 16.0 * n_total_ +
+                              (fused ? 8.0 * m_ + 1.0 * n_total_ + 28.0 * n_list : 0.0));
   rc->resize(n_total_);
+  if (fused) {
+    list_dots->resize(n_list);
+    // Same stream: runs after the kernel, before the synchronizing download.
+    if (n_list > 0) {
+      Check(hipMemcpyAsync(h_pin_d2_, d_out_list_, n_list * sizeof(double),
+                           hipMemcpyDeviceToHost, S(stream_)),
+            "D2H");
+    }
+  }
   Download(h_pin_d_, d_out_n_, n_total_ * sizeof(double));
   std::memcpy(rc->data(), h_pin_d_, n_total_ * sizeof(double));
+  if (fused && n_list > 0) std::memcpy(list_dots->data(), h_pin_d2_, n_list * sizeof(double));
 }
 
 void DeviceLp::ColumnSquaredNorms(std::vector<double>* out) {

@@ -29,13 +29,18 @@
 namespace milp {
 namespace {
 // Debug aid (env MILP_PHASE_TIMING=1): host wall time per phase of the primal
-// loop, printed to stderr when the solve ends.
+// or dual loop, printed to stderr when the loop ends.
 struct PhaseClock {
   static constexpr int kPhases = 10;
-  const char* names[kPhases] = {"refactor+checks", "entering(pricing)", "direction",
-                                "ratio test",      "values update",     "edge norms",
-                                "rc update",       "prices update",     "pivot",
-                                "other"};
+  static constexpr const char* kPrimal[kPhases] = {
+      "refactor+checks", "entering(pricing)", "direction", "ratio test", "values update",
+      "edge norms",      "rc update",         "prices update", "pivot",  "other"};
+  static constexpr const char* kDual[kPhases] = {
+      "refactor+recompute", "leaving(pricing)", "btran rho",  "update row",
+      "entering ratio test", "direction ftran", "rc update",  "dual norms (tau)",
+      "values+pivot",        "other"};
+  explicit PhaseClock(bool dual = false) : names(dual ? kDual : kPrimal) {}
+  const char* const* names;
   double ms[kPhases] = {};
   bool on = std::getenv("MILP_PHASE_TIMING") != nullptr;
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
@@ -576,6 +581,8 @@ class UpdateRow {
   }
   // Which algorithm ComputeUpdateRow() used last (exposed for parity tests).
   int last_algorithm() const { return last_algorithm_; }
+  // Changes whenever the listed positions / coefficients are recomputed.
+  uint64_t epoch() const { return epoch_; }
 
  private:
   void ComputeUpdatesRowWise();
@@ -603,6 +610,7 @@ class UpdateRow {
   int update_row_computed_for_ = kInvalidRow;
   int64_t num_operations_ = 0;
   int last_algorithm_ = -1;
+  uint64_t epoch_ = 0;
   // Deferred column-wise pass: the relevance mask and work count it uses are
   // captured when Glop would have run it (update_row.cc:282-306).
   bool pending_column_wise_ = false;
@@ -671,6 +679,7 @@ void UpdateRow::ComputeUpdateRow(int leaving_row) {
 // the host keeps Glop's algorithm choice (ComputeUpdateRow above) and mirrors
 // the listed positions.
 void UpdateRow::FetchFromDevice() {
+  ++epoch_;
   for (const int col : non_zero_position_list_) listed_[col] = 0;
   dev_->FetchUpdateRow(&non_zero_position_list_, &fetched_values_);
   const int n = static_cast<int>(non_zero_position_list_.size());
@@ -751,9 +760,36 @@ class PrimalEdgeNorms {
   PrimalEdgeNorms(const CompactSparseMatrix& m, const VariablesInfo& vi,
                   const BasisFactorization& bf, DeviceLp* dev)
       : matrix_(m), variables_info_(vi), bf_(bf), dev_(dev) {}
-  void SetParameters(const GlopParameters& p) { params_ = p; }
-  void SetPricingRule(int rule) { pricing_rule_ = rule; }
+  void SetParameters(const GlopParameters& p) {
+    FlushPendingUpdate();
+    params_ = p;
+  }
+  void SetPricingRule(int rule) {
+    FlushPendingUpdate();
+    pricing_rule_ = rule;
+  }
+
+  // Parked steepest-edge update (engine-side scheduling, no Glop
+  // counterpart). When the update row was built row-wise, the a_j . w dots of
+  // UpdateEdgeSquaredNorms (primal_edge_norms.cc:229-233) need a pass over A
+  // of their own. The update is parked instead, and completed by the next
+  // pricing pass, which reads A anyway (ReducedCosts::ComputeReducedCosts ->
+  // DeviceLp::Pricing with w), or by a standalone dots pass before anything
+  // else reads the norms. PrimalPrices queues the price updates that read
+  // the norms meanwhile and replays them, in order, on completion. The
+  // arithmetic and its order are unchanged, so results stay bit-identical.
+  void SetDeferral(bool on) { defer_enabled_ = on; }
+  bool HasPendingUpdate() const { return pending_; }
+  const std::vector<Fractional>& PendingDirectionLeftInverse() const {
+    return direction_left_inverse_.values;
+  }
+  uint64_t PendingListEpoch() const { return pending_list_epoch_; }
+  void CompletePendingUpdate(const std::vector<Fractional>& dots);
+  void FlushPendingUpdate();
+  void SetCompletionListener(std::function<void()> f) { on_complete_ = std::move(f); }
+
   void Clear() {
+    FlushPendingUpdate();
     matrix_column_norms_.clear();
     recompute_edge_squared_norms_ = true;
     reset_devex_weights_ = true;
@@ -764,6 +800,7 @@ class PrimalEdgeNorms {
     return recompute_edge_squared_norms_;
   }
   const std::vector<Fractional>& GetSquaredNorms() {
+    FlushPendingUpdate();
     switch (pricing_rule_) {
       case 0:
         return GetMatrixColumnNorms();
@@ -774,6 +811,7 @@ class PrimalEdgeNorms {
     }
   }
   const std::vector<Fractional>& GetEdgeSquaredNorms() {
+    FlushPendingUpdate();
     if (recompute_edge_squared_norms_) ComputeEdgeSquaredNorms();
     return edge_squared_norms_;
   }
@@ -825,6 +863,9 @@ class PrimalEdgeNorms {
   void UpdateEdgeSquaredNorms(int entering_col, int leaving_col, int leaving_row,
                               const std::vector<Fractional>& direction,
                               const UpdateRow& update_row);
+  void DeferEdgeSquaredNormsUpdate(int entering_col, int leaving_col, int leaving_row,
+                                   const std::vector<Fractional>& direction,
+                                   const UpdateRow& update_row);
   void UpdateDevexWeights(int entering_col, int leaving_col, int leaving_row,
                           const std::vector<Fractional>& direction,
                           const UpdateRow& update_row);
@@ -855,11 +896,21 @@ class PrimalEdgeNorms {
   ScatteredVector direction_left_inverse_;
   int64_t num_operations_ = 0;
   std::vector<bool*> watchers_;
+  // Parked update (see SetDeferral).
+  bool defer_enabled_ = true;
+  bool pending_ = false;
+  Fractional pending_pivot_ = 0.0;
+  Fractional pending_leaving_squared_norm_ = 0.0;
+  const UpdateRow* pending_update_row_ = nullptr;
+  uint64_t pending_row_epoch_ = 0;
+  uint64_t pending_list_epoch_ = 0;
+  std::function<void()> on_complete_;
 };
 
 // primal_edge_norms.cc:79-108
 bool PrimalEdgeNorms::TestEnteringEdgeNormPrecision(int entering_col,
                                                     const ScatteredVector& d) {
+  FlushPendingUpdate();
   if (!recompute_edge_squared_norms_) {
     const Fractional old_squared_norm = edge_squared_norms_[entering_col];
     const Fractional precise_squared_norm = 1.0 + SquaredNorm(d);
@@ -880,13 +931,20 @@ void PrimalEdgeNorms::UpdateBeforeBasisPivot(int entering_col, int leaving_col,
                                              int leaving_row,
                                              const ScatteredVector& direction,
                                              UpdateRow* update_row) {
+  FlushPendingUpdate();
   if (!recompute_edge_squared_norms_) {
     update_row->ComputeUpdateRow(leaving_row);
     ComputeDirectionLeftInverse(entering_col, direction);
-    // Column-wise update row and the a_j . w dots share one pass over A.
-    update_row->MaterializeWithDots(direction_left_inverse_.values);
-    UpdateEdgeSquaredNorms(entering_col, leaving_col, leaving_row, direction.values,
-                           *update_row);
+    // Column-wise update row and the a_j . w dots share one pass over A;
+    // after a row-wise update row the dots ride on the next pricing pass.
+    if (update_row->MaterializeWithDots(direction_left_inverse_.values) ||
+        !defer_enabled_ || pricing_rule_ != 1) {
+      UpdateEdgeSquaredNorms(entering_col, leaving_col, leaving_row, direction.values,
+                             *update_row);
+    } else {
+      DeferEdgeSquaredNormsUpdate(entering_col, leaving_col, leaving_row, direction.values,
+                                  *update_row);
+    }
   }
   if (!reset_devex_weights_) {
     ++num_devex_updates_since_reset_;
@@ -947,6 +1005,61 @@ void PrimalEdgeNorms::UpdateEdgeSquaredNorms(int entering_col, int leaving_col,
   edge_squared_norms_[leaving_col] = leaving_squared_norm;
 }
 
+// UpdateEdgeSquaredNorms split in two: the scalars now, the loop over the
+// update row once its dots are known (CompletePendingUpdate).
+void PrimalEdgeNorms::DeferEdgeSquaredNormsUpdate(int entering_col, int leaving_col,
+                                                  int leaving_row,
+                                                  const std::vector<Fractional>& direction,
+                                                  const UpdateRow& update_row) {
+  pending_pivot_ = -direction[leaving_row];
+  const Fractional entering_squared_norm = edge_squared_norms_[entering_col];
+  pending_leaving_squared_norm_ =
+      std::max(1.0, entering_squared_norm / Square(pending_pivot_));
+  for (const int col : update_row.GetNonZeroPositions()) {
+    num_operations_ += matrix_.ColumnNumEntries(col);
+  }
+  // The leaving column is basic, hence not relevant and never one of the
+  // listed positions: its final value can be written now.
+  edge_squared_norms_[leaving_col] = pending_leaving_squared_norm_;
+  pending_update_row_ = &update_row;
+  pending_row_epoch_ = update_row.epoch();
+  pending_list_epoch_ = dev_->list_epoch();
+  pending_ = true;
+}
+
+void PrimalEdgeNorms::CompletePendingUpdate(const std::vector<Fractional>& dots) {
+  if (!pending_) return;
+  pending_ = false;
+  if (pending_update_row_->epoch() != pending_row_epoch_) {
+    throw DeviceError("update row recomputed under a parked edge-norm update");
+  }
+  const Fractional pivot = pending_pivot_;
+  const Fractional leaving_squared_norm = pending_leaving_squared_norm_;
+  const Fractional factor = 2.0 / pivot;
+  const std::vector<int>& positions = pending_update_row_->GetNonZeroPositions();
+  const std::vector<Fractional>& coefficients = pending_update_row_->GetCoefficients();
+  if (dots.size() != positions.size()) throw DeviceError("edge-norm dots size mismatch");
+  for (size_t k = 0; k < positions.size(); ++k) {
+    const int col = positions[k];
+    const Fractional coeff = coefficients[col];
+    edge_squared_norms_[col] += coeff * (coeff * leaving_squared_norm + factor * dots[k]);
+    const Fractional lower_bound = 1.0 + Square(coeff / pivot);
+    if (edge_squared_norms_[col] < lower_bound) edge_squared_norms_[col] = lower_bound;
+  }
+  if (on_complete_) on_complete_();
+}
+
+void PrimalEdgeNorms::FlushPendingUpdate() {
+  if (!pending_) return;
+  if (dev_->list_epoch() == pending_list_epoch_) {
+    dev_->ListDotsOverUpdateRow(direction_left_inverse_.values, &dots_);
+  } else {
+    dev_->ListDots(pending_update_row_->GetNonZeroPositions(), direction_left_inverse_.values,
+                   &dots_);
+  }
+  CompletePendingUpdate(dots_);
+}
+
 // primal_edge_norms.cc:260-281
 void PrimalEdgeNorms::UpdateDevexWeights(int /*entering_col*/, int leaving_col,
                                          int leaving_row,
@@ -975,6 +1088,9 @@ class ReducedCosts {
       : matrix_(m), objective_(obj), basis_(basis), variables_info_(vi), bf_(bf),
         random_(random), dev_(dev) {}
   void SetParameters(const GlopParameters& p) { params_ = p; }
+  // The primal edge norms whose parked update the pricing pass completes.
+  void SetDeferredNorms(PrimalEdgeNorms* norms) { deferred_norms_ = norms; }
+  bool WillRecompute() const { return recompute_reduced_costs_; }
   bool NeedsBasisRefactorization() const { return must_refactorize_basis_; }
   Fractional TestEnteringReducedCostPrecision(int entering_col, const ScatteredVector& d);
   Fractional ComputeMaximumDualResidual();
@@ -1087,6 +1203,9 @@ class ReducedCosts {
   const BasisFactorization& bf_;
   Rng* random_;
   DeviceLp* dev_;
+  PrimalEdgeNorms* deferred_norms_ = nullptr;
+  std::vector<Fractional> fused_rc_;
+  std::vector<Fractional> fused_dots_;
   std::vector<Fractional> shifted_objective_;
   std::vector<Fractional> dots_;
   GlopParameters params_;
@@ -1230,7 +1349,23 @@ void ReducedCosts::ComputeReducedCosts() {
   for (int col = 0; col < num_cols; ++col)
     shifted_objective_[col] = objective_[col] + cost_perturbations_[col];
   // rc_j = (c_j + delta_j) - a_j . y for all N columns: the pricing SpMV.
-  dev_->Pricing(shifted_objective_, basic_objective_left_inverse_.values, &reduced_costs_);
+  const std::vector<Fractional>& y = basic_objective_left_inverse_.values;
+  if (deferred_norms_ != nullptr && deferred_norms_->HasPendingUpdate()) {
+    if (dev_->list_epoch() == deferred_norms_->PendingListEpoch()) {
+      // One pass over A: rc for every column plus the parked edge-norm dots.
+      // The parked update (and the price updates queued behind it) completes
+      // while reduced_costs_ still holds the values they were issued with.
+      dev_->Pricing(shifted_objective_, y, &fused_rc_,
+                    &deferred_norms_->PendingDirectionLeftInverse(), &fused_dots_);
+      deferred_norms_->CompletePendingUpdate(fused_dots_);
+      reduced_costs_.swap(fused_rc_);
+    } else {
+      deferred_norms_->FlushPendingUpdate();
+      dev_->Pricing(shifted_objective_, y, &reduced_costs_);
+    }
+  } else {
+    dev_->Pricing(shifted_objective_, y, &reduced_costs_);
+  }
   is_basic.ForEach([&](int col) {
     dual_residual_error = std::max(dual_residual_error, std::fabs(reduced_costs_[col]));
   });
@@ -1275,10 +1410,17 @@ class PrimalPrices {
         reduced_costs_(rc) {
     reduced_costs_->AddRecomputationWatcher(&recompute_);
     primal_edge_norms_->AddRecomputationWatcher(&recompute_);
+    primal_edge_norms_->SetCompletionListener([this]() { ReplayQueue(); });
   }
   int GetBestEnteringColumn() {
+    // A parked edge-norm update completes inside the pricing pass when the
+    // reduced costs are about to be recomputed, otherwise right here.
+    if (!recompute_ || !reduced_costs_->WillRecompute()) {
+      primal_edge_norms_->FlushPendingUpdate();
+    }
     if (recompute_) {
       const std::vector<Fractional>& rc = reduced_costs_->GetReducedCosts();
+      primal_edge_norms_->FlushPendingUpdate();  // no-op after the fused pass
       prices_.ClearAndResize(static_cast<int>(rc.size()));
       const std::vector<int> cols = variables_info_.GetIsRelevantBitRow().ToVector();
       UpdateEnteringCandidates<true>(cols);
@@ -1288,10 +1430,20 @@ class PrimalPrices {
   }
   void UpdateBeforeBasisPivot(int /*entering_col*/, UpdateRow* update_row) {
     if (recompute_) return;
+    if (primal_edge_norms_->HasPendingUpdate()) {
+      QueueEnteringCandidates(update_row->GetNonZeroPositions());
+      return;
+    }
     UpdateEnteringCandidates<false>(update_row->GetNonZeroPositions());
   }
   void RecomputePriceAt(int col) {
     if (recompute_) return;
+    if (primal_edge_norms_->HasPendingUpdate()) {
+      const bool valid = reduced_costs_->IsValidPrimalEnteringCandidate(col);
+      if (valid) reduced_costs_->GetReducedCosts();  // its side effects happen now
+      queue_.push_back(QueuedOp{col, valid});
+      return;
+    }
     if (reduced_costs_->IsValidPrimalEnteringCandidate(col)) {
       const std::vector<Fractional>& sn = primal_edge_norms_->GetSquaredNorms();
       const std::vector<Fractional>& rc = reduced_costs_->GetReducedCosts();
@@ -1302,11 +1454,48 @@ class PrimalPrices {
   }
   void SetAndDebugCheckThatColumnIsDualFeasible(int col) {
     if (recompute_) return;
+    if (primal_edge_norms_->HasPendingUpdate()) {
+      queue_.push_back(QueuedOp{col, false});
+      return;
+    }
     prices_.Remove(col);
   }
   void ForceRecomputation() { recompute_ = true; }
 
  private:
+  // A price update issued while the edge-norm update is parked: the
+  // candidate test is done at issue time (it does not read the norms); the
+  // price rc^2 / norm is computed at replay, before any reduced cost changes.
+  struct QueuedOp {
+    int col;
+    bool add;  // AddOrUpdate(col, price) if true, Remove(col) otherwise
+  };
+  void QueueEnteringCandidates(const std::vector<int>& cols) {
+    const Fractional tolerance = reduced_costs_->GetDualFeasibilityTolerance();
+    const Bitset& dec = variables_info_.GetCanDecreaseBitRow();
+    const Bitset& inc = variables_info_.GetCanIncreaseBitRow();
+    const std::vector<Fractional>& rc = reduced_costs_->GetReducedCosts();
+    for (const int col : cols) {
+      const Fractional reduced_cost = rc[col];
+      const bool is_dual_infeasible =
+          ((reduced_cost > tolerance) && dec.IsSet(col)) !=
+          ((reduced_cost < -tolerance) && inc.IsSet(col));
+      queue_.push_back(QueuedOp{col, is_dual_infeasible});
+    }
+  }
+  void ReplayQueue() {
+    const std::vector<Fractional>& sn = primal_edge_norms_->RawEdgeNorms();
+    const std::vector<Fractional>& rc = reduced_costs_->RawReducedCosts();
+    for (const QueuedOp& op : queue_) {
+      if (op.add) {
+        prices_.AddOrUpdate(op.col, Square(rc[op.col]) / sn[op.col]);
+      } else {
+        prices_.Remove(op.col);
+      }
+    }
+    queue_.clear();
+  }
+  std::vector<QueuedOp> queue_;
   template <bool from_clean_state>
   void UpdateEnteringCandidates(const std::vector<int>& cols) {
     const Fractional tolerance = reduced_costs_->GetDualFeasibilityTolerance();
@@ -2050,6 +2239,7 @@ class RevisedSimplex {
   void TraceIteration() {
     static const char* prefix = std::getenv("MILP_TRACE");
     if (prefix == nullptr) return;
+    primal_edge_norms_.FlushPendingUpdate();  // hash the norms Glop has here
     const std::string path = std::string(prefix) + ".device";
     FILE* f = std::fopen(path.c_str(), "a");
     if (f == nullptr) return;
@@ -2149,6 +2339,7 @@ RevisedSimplex::RevisedSimplex()
                      basis_factorization_, &random_, &device_),
       entering_variable_(variables_info_, &random_, &reduced_costs_),
       primal_prices_(&random_, variables_info_, &primal_edge_norms_, &reduced_costs_) {
+  reduced_costs_.SetDeferredNorms(&primal_edge_norms_);
   SetParameters(parameters_);
 }
 
@@ -3227,7 +3418,18 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
   struct Cleanup {
     std::function<void()> f;
     ~Cleanup() { f(); }
-  } cleanup{[this, time_limit]() { AdvanceDeterministicTime(time_limit); }};
+  } cleanup{[this, time_limit]() {
+    try {
+      primal_edge_norms_.FlushPendingUpdate();  // nothing parked leaves the loop
+    } catch (const DeviceError&) {
+      // The device failed; the next device call reports it.
+    }
+    AdvanceDeterministicTime(time_limit);
+  }};
+  {
+    const char* defer = std::getenv("MILP_DEFER_NORMS");
+    primal_edge_norms_.SetDeferral(defer == nullptr || std::strcmp(defer, "0") != 0);
+  }
   PhaseClock clock;
   const int64_t first_iteration = num_iterations_;
   struct DumpAtExit {
@@ -3400,6 +3602,14 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     std::function<void()> f;
     ~Cleanup() { f(); }
   } cleanup{[this, time_limit]() { AdvanceDeterministicTime(time_limit); }};
+  PhaseClock clock(/*dual=*/true);
+  const int64_t first_iteration = num_iterations_;
+  struct DumpAtExit {
+    PhaseClock* c;
+    const int64_t* it;
+    int64_t first;
+    ~DumpAtExit() { c->Dump(static_cast<long long>(*it - first)); }
+  } dump{&clock, &num_iterations_, first_iteration};
   bool refactorize = false;
   bound_flip_candidates_.clear();
   int leaving_row;
@@ -3434,6 +3644,7 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
         variable_values_.UpdateDualPrices(direction_.non_zeros);
       }
     }
+    clock.Mark(0);
 
     if (feasibility_phase) {
       MILP_RETURN_IF_ERROR(
@@ -3442,6 +3653,7 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
       MILP_RETURN_IF_ERROR(
           DualChooseLeavingVariableRow(&leaving_row, &cost_variation, &target_bound));
     }
+    clock.Mark(1);
     if (leaving_row == kInvalidRow) {
       if (!basis_factorization_.IsRefactorized() || reduced_costs_.HasCostShift()) {
         reduced_costs_.ClearAndRemoveCostShifts();
@@ -3459,6 +3671,7 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     }
 
     update_row_.ComputeUnitRowLeftInverse(leaving_row);
+    clock.Mark(2);
     if (!dual_edge_norms_.TestPrecision(leaving_row, update_row_.GetUnitRowLeftInverse())) {
       if (feasibility_phase) {
         const Fractional price = dual_pricing_vector_[leaving_row];
@@ -3470,6 +3683,8 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
       continue;
     }
     update_row_.ComputeUpdateRow(leaving_row);
+    update_row_.GetNonZeroPositions();  // materialize (timed as the update row)
+    clock.Mark(3);
 
     if (feasibility_phase) {
       MILP_RETURN_IF_ERROR(entering_variable_.DualPhaseIChooseEnteringColumn(
@@ -3480,6 +3695,7 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
           reduced_costs_.AreReducedCostsPrecise(), update_row_, cost_variation,
           &bound_flip_candidates_, &entering_col));
     }
+    clock.Mark(4);
 
     if (entering_col == kInvalidCol) {
       if (!reduced_costs_.AreReducedCostsPrecise()) {
@@ -3507,6 +3723,7 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
       continue;
     }
     ComputeDirection(entering_col);
+    clock.Mark(5);
     if (std::fabs(direction_[leaving_row]) <
         parameters_.small_pivot_threshold * direction_infinity_norm_) {
       if (!reduced_costs_.AreReducedCostsPrecise()) {
@@ -3523,8 +3740,10 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     reduced_costs_.ShiftCostIfNeeded(increasing_rc_is_needed, entering_col);
     reduced_costs_.UpdateBeforeBasisPivot(entering_col, leaving_row, direction_,
                                           &update_row_);
+    clock.Mark(6);
     dual_edge_norms_.UpdateBeforeBasisPivot(entering_col, leaving_row, direction_,
                                             update_row_.GetUnitRowLeftInverse());
+    clock.Mark(7);
     Fractional primal_step = 0.0;
     if (feasibility_phase) {
       DualPhaseIUpdatePrice(leaving_row, entering_col);
@@ -3535,7 +3754,9 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     const int leaving_col = basis_[leaving_row];
     MILP_RETURN_IF_ERROR(UpdateAndPivot(entering_col, leaving_row, target_bound));
     variable_values_.SetNonBasicVariableValueFromStatus(leaving_col);
+    clock.Mark(8);
     OnIterationDone(time_limit);
+    clock.Mark(9);
   }
   return Status::OK();
 }

@@ -21,8 +21,8 @@ struct DotArgs {
   uint8_t* flags;           // kUpdateRowColumnWise: |coeff| > drop; kListDots: listed
   double drop_tolerance;
   const uint8_t* skip;      // optional: columns handled by the dense block
-  const double* y2;         // kUpdateRowWithDots: second vector (w = B^-T d)
-  double* out2;             // kUpdateRowWithDots: w . a_j for listed columns
+  const double* y2;         // kUpdateRowWithDots / kPricingWithDots: w = B^-T d
+  double* out2;             // w . a_j for listed columns
 };
 
 // Dense column block: the structural columns whose CSC column is full (all m
@@ -46,7 +46,7 @@ struct DenseArgs {
   double* out;            // indexed by column id
   uint8_t* flags;         // kUpdateRowColumnWise: out; kListDots: in (listed)
   double drop_tolerance;
-  const double* y2;       // kUpdateRowWithDots
+  const double* y2;       // kUpdateRowWithDots / kPricingWithDots
   double* out2;
 };
 
@@ -81,7 +81,8 @@ struct RowSumArgs {
 namespace milp_launch {
 hipError_t column_dot(int mode, bool wave_per_col, const milp_kernels::DotArgs& args,
                       hipStream_t s);
-hipError_t dense_dot(int mode, const milp_kernels::DenseArgs& args, hipStream_t s);
+// unroll: 16-byte loads in flight per lane (8, 16 or 32).
+hipError_t dense_dot(int mode, int unroll, const milp_kernels::DenseArgs& args, hipStream_t s);
 hipError_t dense_pack(const int64_t* starts, const double* vals, const int32_t* dense_cols,
                       int nd, int m, double* body, double* tail, hipStream_t s);
 hipError_t gather(const int32_t* list, int n, const double* src, double* dst, hipStream_t s);

@@ -88,7 +88,11 @@ enum DotMode : int {
   kFullUpdateRow = 3,        // update_row.cc:311-332 over non-basic columns
   // Column-wise update row fused with the primal edge-norm dots
   // (primal_edge_norms.cc:229-233): one pass over A yields rho.a_j and w.a_j.
-  kUpdateRowWithDots = 4
+  kUpdateRowWithDots = 4,
+  // Pricing fused with the edge-norm dots deferred from the previous pivot:
+  // rc_j = c_j - a_j.y for every column and w.a_j for the columns flagged as
+  // listed in that pivot's update row. One pass over A instead of two.
+  kPricingWithDots = 5
 };
 
 
@@ -120,9 +124,17 @@ __global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
   const double dot = WAVE_PER_COL ? wave_column_dot(s, e, a.rows, a.vals, a.y, lane)
                                   : quad_column_dot(s, e, a.rows, a.vals, a.y, sub, lane);
   double dot2 = 0.0;
+  bool listed = false;
   if (MODE == kUpdateRowWithDots) {  // second sweep of the same column (cache hot)
     dot2 = WAVE_PER_COL ? wave_column_dot(s, e, a.rows, a.vals, a.y2, lane)
                         : quad_column_dot(s, e, a.rows, a.vals, a.y2, sub, lane);
+  } else if (MODE == kPricingWithDots) {
+    // Only listed columns sweep again; the others walk an empty range so the
+    // lanes of a column stay converged through the shuffles.
+    listed = active && a.flags[col] != 0;
+    const int64_t e2 = listed ? e : s;
+    dot2 = WAVE_PER_COL ? wave_column_dot(s, e2, a.rows, a.vals, a.y2, lane)
+                        : quad_column_dot(s, e2, a.rows, a.vals, a.y2, sub, lane);
   }
   const bool writer = WAVE_PER_COL ? (lane == 0) : (sub == 0);
   if (!writer || !in_range) return;
@@ -140,6 +152,9 @@ __global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
     if (keep) a.out[col] = dot;
   } else if (MODE == kPricing) {
     a.out[col] = a.c[col] - dot;
+  } else if (MODE == kPricingWithDots) {
+    a.out[col] = a.c[col] - dot;
+    if (listed) a.out2[col] = dot2;
   } else if (MODE == kListDots) {
     if (active) a.out[col] = dot;
   } else {  // kFullUpdateRow
@@ -150,22 +165,23 @@ __global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
 // ---------------------------------------------------------------------------
 // Dense block dots (layout in kernel_args.h). Lane 4j+k owns chain k of dense
 // column j and walks it sequentially, two chain elements per 16-byte load, so
-// one wave step is one contiguous 1-KiB load. kUnroll loads are issued ahead
+// one wave step is one contiguous 1-KiB load. UNROLL loads are issued ahead
 // of the dependent adds. Lane 4j then folds ((r1 + r2) + r3) + r4 and adds the
 // <= 3 tail terms in order, exactly as ColumnScalarProduct.
-constexpr int kUnroll = 8;
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
-template <int MODE>
+template <int MODE, int UNROLL>
 __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
-  constexpr bool kTwo = MODE == kUpdateRowWithDots;
+  constexpr int kUnroll = UNROLL;
+  constexpr bool kTwo = MODE == kUpdateRowWithDots || MODE == kPricingWithDots;
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int j = tid >> 2;
   const int k = tid & 3;
   const bool in_range = j < a.nd;
   const int col = in_range ? a.dense_cols[j] : 0;
   bool active = in_range;
-  if (MODE == kUpdateRowColumnWise || kTwo) active = active && bit_set(a.mask, col);
+  if (MODE == kUpdateRowColumnWise || MODE == kUpdateRowWithDots)
+    active = active && bit_set(a.mask, col);
   if (MODE == kListDots) active = active && a.flags[col];
   const int steps = a.m >> 2;
   const int pairs = steps >> 1;
@@ -226,7 +242,7 @@ __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
     result += v * a.y[base + r];
     if (kTwo) result2 += v * a.y2[base + r];
   }
-  if (MODE == kUpdateRowColumnWise || kTwo) {
+  if (MODE == kUpdateRowColumnWise || MODE == kUpdateRowWithDots) {
     const bool keep = active && fabs(result) > a.drop_tolerance;
     a.flags[col] = keep ? 1 : 0;
     if (keep) {
@@ -235,6 +251,9 @@ __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
     }
   } else if (MODE == kPricing) {
     a.out[col] = a.c[col] - result;
+  } else if (MODE == kPricingWithDots) {
+    a.out[col] = a.c[col] - result;
+    if (a.flags[col]) a.out2[col] = result2;  // listed in the deferred update row
   } else if (MODE == kListDots) {
     if (active) a.out[col] = result;
   }
@@ -433,21 +452,33 @@ hipError_t column_dot(int mode, bool wave_per_col, const DotArgs& args, hipStrea
     case 6: column_dot_kernel<3, false><<<blocks, threads, 0, s>>>(args); break;
     case 7: column_dot_kernel<3, true><<<blocks, threads, 0, s>>>(args); break;
     case 8: column_dot_kernel<4, false><<<blocks, threads, 0, s>>>(args); break;
-    default: column_dot_kernel<4, true><<<blocks, threads, 0, s>>>(args); break;
+    case 9: column_dot_kernel<4, true><<<blocks, threads, 0, s>>>(args); break;
+    case 10: column_dot_kernel<5, false><<<blocks, threads, 0, s>>>(args); break;
+    case 11: column_dot_kernel<5, true><<<blocks, threads, 0, s>>>(args); break;
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t dense_dot(int mode, const DenseArgs& args, hipStream_t s) {
-  if (args.nd <= 0) return hipSuccess;
-  const int blocks = div_up(static_cast<long>(args.nd) * 4, 256);
+template <int UNROLL>
+static hipError_t launch_dense_dot(int mode, int blocks, const DenseArgs& args, hipStream_t s) {
   switch (mode) {
-    case 0: dense_dot_kernel<0><<<blocks, 256, 0, s>>>(args); break;
-    case 1: dense_dot_kernel<1><<<blocks, 256, 0, s>>>(args); break;
-    case 2: dense_dot_kernel<2><<<blocks, 256, 0, s>>>(args); break;
-    default: dense_dot_kernel<4><<<blocks, 256, 0, s>>>(args); break;
+    case 0: dense_dot_kernel<0, UNROLL><<<blocks, 256, 0, s>>>(args); break;
+    case 1: dense_dot_kernel<1, UNROLL><<<blocks, 256, 0, s>>>(args); break;
+    case 2: dense_dot_kernel<2, UNROLL><<<blocks, 256, 0, s>>>(args); break;
+    case 4: dense_dot_kernel<4, UNROLL><<<blocks, 256, 0, s>>>(args); break;
+    case 5: dense_dot_kernel<5, UNROLL><<<blocks, 256, 0, s>>>(args); break;
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+hipError_t dense_dot(int mode, int unroll, const DenseArgs& args, hipStream_t s) {
+  if (args.nd <= 0) return hipSuccess;
+  const int blocks = div_up(static_cast<long>(args.nd) * 4, 256);
+  if (unroll >= 32) return launch_dense_dot<32>(mode, blocks, args, s);
+  if (unroll >= 16) return launch_dense_dot<16>(mode, blocks, args, s);
+  return launch_dense_dot<8>(mode, blocks, args, s);
 }
 
 hipError_t dense_pack(const int64_t* starts, const double* vals, const int32_t* dense_cols,

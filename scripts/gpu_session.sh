@@ -1,0 +1,27 @@
+#!/bin/bash
+# One GPU session: parity tests, then engine probes (C2 variants, C5).
+# Every GPU step has its own time limit; the first failure ends the session.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+echo "start $(date +%T)"
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest $R/tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/gpu_tests.log; exit 1; }
+  tail -2 $OUT/gpu_tests.log
+fi
+if [ -z "$SKIP_C2" ]; then
+  MILP_PHASE_TIMING=1 timeout -k 10 600 python -u $R/scripts/probe.py --config c2 --steps 20 \
+    --variants "MILP_DENSE_UNROLL=8,MILP_DEFER_NORMS=0" "MILP_DENSE_UNROLL=8" \
+               "MILP_DENSE_UNROLL=16" "MILP_DENSE_UNROLL=32" \
+    > $OUT/probe_c2.json 2> $OUT/probe_c2.err || { echo "c2 probe failed"; tail -30 $OUT/probe_c2.err; exit 1; }
+  cat $OUT/probe_c2.json
+fi
+if [ -z "$SKIP_C5" ]; then
+  MILP_PHASE_TIMING=1 timeout -k 10 600 python -u $R/scripts/probe.py --config c5 --m 100000 --n 1000000 \
+    --warmup ${C5_WARMUP:-2000} --steps ${C5_STEPS:-500} \
+    > $OUT/probe_c5.json 2> $OUT/probe_c5.err || { echo "c5 probe failed"; tail -30 $OUT/probe_c5.err; exit 1; }
+  cat $OUT/probe_c5.json
+fi
+echo "done $(date +%T)"

@@ -66,6 +66,34 @@ def test_dense_primal_parity(shape, block, monkeypatch):
 
 
 @pytest.mark.parametrize("block", ["off", "force"])
+@pytest.mark.parametrize("shape", [(97, 400), (259, 1100)])
+def test_parked_edge_norm_update_parity(shape, block, monkeypatch):
+    """The edge-norm dots parked after a row-wise update row ride on the next
+    pricing pass (phase I resets the costs every iteration). With and without
+    parking, every result must equal the oracle's, and parking must remove
+    standalone dots passes."""
+    monkeypatch.setenv("MILP_DENSE_BLOCK", block)
+    lp = lp_gen.dense_box_lp(shape[0], shape[1], 7)
+    launches = {}
+    for defer in ("0", "1"):
+        monkeypatch.setenv("MILP_DEFER_NORMS", defer)
+        o, ro, g, rg = parity_util.solve_both(lp, abi.default_params(), _handle)
+        parity_util.compare(o, ro, g, rg, lp)
+        launches[defer] = g.kernel_stats()["primal_norms"]["launches"]
+    assert launches["1"] < launches["0"], launches
+
+
+@pytest.mark.parametrize("unroll", ["8", "32"])
+def test_dense_block_unroll_parity(unroll, monkeypatch):
+    """The dense-block kernel's load depth does not change any result."""
+    monkeypatch.setenv("MILP_DENSE_BLOCK", "force")
+    monkeypatch.setenv("MILP_DENSE_UNROLL", unroll)
+    lp = lp_gen.dense_box_lp(131, 700, 4)
+    o, ro, g, rg = parity_util.solve_both(lp, abi.default_params(), _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+
+
+@pytest.mark.parametrize("block", ["off", "force"])
 @pytest.mark.parametrize("seed", [11, 12])
 def test_dense_dual_parity(seed, block, monkeypatch):
     monkeypatch.setenv("MILP_DENSE_BLOCK", block)
