@@ -66,6 +66,103 @@ def cpu_baseline(lp, warm, iters):
                       timed_iterations=iters, warm_iterations=warm)
 
 
+def kernel_roofline(stats, traffic_json=None):
+    """Roofline of the dominant kernel id of a timed window: algorithmic bytes
+    per launch / HIP-event time per launch, against the HBM peak."""
+    dom = max(stats, key=lambda k: stats[k]["device_ms"])
+    ds = stats[dom]
+    launches = max(1, ds["launches"])
+    bytes_per_launch = ds["bytes"] / launches
+    ms_per_launch = ds["device_ms"] / launches if ds["device_ms"] > 0 else float("nan")
+    achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ds["device_ms"] > 0 else 0.0
+    traffic = None
+    traffic_src = None
+    if traffic_json and os.path.exists(traffic_json):
+        tj = json.load(open(traffic_json))
+        if dom in tj:
+            traffic = tj[dom]["traffic_bytes_per_launch"]
+            traffic_src = tj.get("_source", traffic_json)
+    return {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_source": traffic_src, "bytes_per_launch": bytes_per_launch,
+            "ms_per_launch": ms_per_launch, "launches": ds["launches"]}
+
+
+def kernel_table(stats):
+    return {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
+                "call_ms": round(v["call_ms"], 3), "GB": round(v["bytes"] / 1e9, 4)}
+            for k, v in stats.items() if v["launches"] or v["call_ms"]}
+
+
+def run_c5(args, rank, world, local_rank, dist, barrier, sync):
+    """Config 5: synthetic sparse LP 100k x 1M, 0.01% nnz,
+    dual simplex with dual steepest edge. One LP per rank (replicas, seed +
+    rank). The window [c5_warmup, c5_warmup + c5_steps) is timed: early
+    iterations are hypersparse, and the window sits where the update row
+    has become the dominant pass. The rate is measured with kernel timing
+    off; a second window of the same length, with HIP-event timing on,
+    gives the kernel split and the roofline."""
+    import lp_gen
+    lp = lp_gen.sparse_c5_lp(args.c5_m, args.c5_n, 10, args.seed + rank)
+    p = abi.default_params(use_dual_simplex=1)
+    h = engine.LpHandle(p, device=local_rank)
+    h.load(lp)
+    t = time.perf_counter()
+    h.begin(args.c5_warmup)
+    setup = time.perf_counter() - t
+    log(f"c5: warm-up to iteration {args.c5_warmup} in {setup:.1f}s")
+    h.reset_kernel_stats()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    fin, it = h.run_until(args.c5_warmup + args.c5_steps)
+    sync()
+    barrier()
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+    done = it - args.c5_warmup
+    total_done = done * world  # replicas: every rank runs the same window length
+    h.reset_kernel_stats()
+    h.set_kernel_timing(True)
+    h.run_until(it + args.c5_steps)
+    stats = h.kernel_stats()
+    h.stop()
+    h.finish()
+    del h
+    out = {
+        "metric": "simplex iterations/sec", "unit": "iterations/s",
+        "value": total_done / elapsed if elapsed > 0 else 0.0,
+        "ms_per_iteration": 1000.0 * elapsed / max(1, done),
+        "timed_iterations": [args.c5_warmup, args.c5_warmup + done],
+        "finished_early": bool(fin), "setup_and_warmup_s": round(setup, 2),
+        "workload": (f"config 5: sparse {args.c5_m}x{args.c5_n}, 10 nnz/column "
+                     f"(nnz={int(lp.nnz)}), dual simplex, dual steepest edge, Glop defaults"),
+        "roofline": kernel_roofline(stats),
+        "kernels": kernel_table(stats),
+        "kernel_window": [args.c5_warmup + done, args.c5_warmup + 2 * done],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu and args.c5_cpu_steps > 0:
+        import oracle_lib
+        log("c5: cpu baseline (oracle)")
+        po = abi.default_params(use_dual_simplex=1,
+                                max_number_of_iterations=args.c5_warmup + args.c5_cpu_steps)
+        o = oracle_lib.OracleLp(po)
+        o.record_iteration_times(True)
+        o.load(lp)
+        t = time.perf_counter()
+        o.solve()
+        wall = time.perf_counter() - t
+        ts = o.iteration_times()
+        k = args.c5_cpu_steps
+        if len(ts) >= args.c5_warmup + k:
+            dt = ts[args.c5_warmup + k - 1] - ts[args.c5_warmup - 1]
+            out["cpu_baseline"] = {
+                "value": k / dt, "unit": "iterations/s", "cores": 1, "kind": "port",
+                "sample": (f"oracle (C++ restatement of Glop, -O3, 1 thread) on the same LP: "
+                           f"iterations {args.c5_warmup}..{args.c5_warmup + k} "
+                           f"({wall:.1f}s wall incl. the warm-up)")}
+    return out
+
+
 def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     """Config 4: children of one CP-SAT-style search node,
     sharded across ranks (each rank its own children, weak scaling), solved
@@ -142,6 +239,12 @@ def main():
     ap.add_argument("--batch-jobs", type=int, default=15)
     ap.add_argument("--batch-machines", type=int, default=10)
     ap.add_argument("--batch-cpu-lps", type=int, default=512)
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 section")
+    ap.add_argument("--c5-m", type=int, default=100000)
+    ap.add_argument("--c5-n", type=int, default=1000000)
+    ap.add_argument("--c5-warmup", type=int, default=20000)
+    ap.add_argument("--c5-steps", type=int, default=1000)
+    ap.add_argument("--c5-cpu-steps", type=int, default=300)
     ap.add_argument("--traffic-json",
                     default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of the dominant kernel from a "
@@ -210,20 +313,13 @@ def main():
     del h  # release the C2 matrix copies before the batched section
 
     # Dominant kernel in the timed region: roofline vs HBM peak.
-    dom = max(stats, key=lambda k: stats[k]["device_ms"])
-    ds = stats[dom]
-    launches = max(1, ds["launches"])
-    bytes_per_launch = ds["bytes"] / launches
-    ms_per_launch = ds["device_ms"] / launches if ds["device_ms"] > 0 else float("nan")
-    achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ds["device_ms"] > 0 else 0.0
-    traffic = None
-    traffic_src = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        tj = json.load(open(args.traffic_json))
-        if dom in tj:
-            traffic = tj[dom]["traffic_bytes_per_launch"]
-            traffic_src = tj.get("_source", args.traffic_json)
+    roofline = kernel_roofline(stats, args.traffic_json)
 
+    c5 = None
+    if not args.no_c5:
+        log(f"config-5 section: {args.c5_m}x{args.c5_n}")
+        c5 = run_c5(args, rank, world, local_rank, dist, barrier, sync)
+        log(f"c5: {c5['value']:.1f} iterations/s")
     batched = None
     if args.batch_lps > 0:
         log(f"batched section: {args.batch_lps} children per GPU")
@@ -262,20 +358,12 @@ def main():
             "setup_and_warmup_s": round(t_setup, 3),
             "parallelism": f"replicas{world}",
         },
-        "roofline": {
-            "kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "traffic_source": traffic_src,
-            "bytes_per_launch": bytes_per_launch, "ms_per_launch": ms_per_launch,
-            "launches": ds["launches"],
-        },
-        "kernels": {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
-                        "call_ms": round(v["call_ms"], 3),
-                        "GB": round(v["bytes"] / 1e9, 3)} for k, v in stats.items()
-                    if v["launches"] or v["call_ms"]},
+        "roofline": roofline,
+        "kernels": kernel_table(stats),
         "host_ms_per_step": round((1000.0 * elapsed - sum(v["call_ms"] for v in stats.values()))
                                   / max(1, done), 3),
         "cpu_baseline": cpu,
+        "c5": c5,
         "batched": batched,
     }
     print(json.dumps(line), flush=True)

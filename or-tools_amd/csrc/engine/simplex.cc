@@ -39,7 +39,7 @@ struct PhaseClock {
       "refactor+recompute", "leaving(pricing)", "btran rho",  "update row",
       "entering ratio test", "direction ftran", "rc update",  "dual norms (tau)",
       "values+pivot",        "other"};
-  explicit PhaseClock(bool dual = false) : names(dual ? kDual : kPrimal) {}
+  explicit PhaseClock(bool dual = false);
   const char* const* names;
   double ms[kPhases] = {};
   bool on = std::getenv("MILP_PHASE_TIMING") != nullptr;
@@ -50,15 +50,51 @@ struct PhaseClock {
     ms[phase] += std::chrono::duration<double, std::milli>(now - t).count();
     t = now;
   }
-  void Dump(long long iterations) {
-    if (!on) return;
-    std::fprintf(stderr, "[phase timing] %lld iterations\n", iterations);
-    for (int i = 0; i < kPhases; ++i) {
-      std::fprintf(stderr, "  %-18s %10.3f ms  (%.3f ms/it)\n", names[i], ms[i],
-                   iterations > 0 ? ms[i] / iterations : 0.0);
+  void Dump(long long iterations);
+};
+
+// Finer split inside the phases (same switch): wall time of named sections.
+enum SubPhase {
+  kSubBtranY, kSubPricingCall, kSubCandidatesFull, kSubGetMaximum, kSubBtranW,
+  kSubUpdateRowCall, kSubNormLoop, kSubQueue, kSubLuUpdate, kSubRefactorize, kNumSubPhases
+};
+const char* const kSubPhaseNames[kNumSubPhases] = {
+    "btran y (c_B B^-1)", "pricing device call", "prices full rebuild", "GetMaximum",
+    "btran w (B^-T d)",   "update-row device",   "norm update loop",    "price queue/replay",
+    "basis update (MPF)", "refactorize (LU)"};
+double g_sub_ms[kNumSubPhases] = {};
+const bool g_sub_on = std::getenv("MILP_PHASE_TIMING") != nullptr;
+struct SubTimer {
+  SubPhase p;
+  std::chrono::steady_clock::time_point t0;
+  explicit SubTimer(SubPhase q) : p(q) {
+    if (g_sub_on) t0 = std::chrono::steady_clock::now();
+  }
+  ~SubTimer() {
+    if (g_sub_on) {
+      g_sub_ms[p] += std::chrono::duration<double, std::milli>(
+                         std::chrono::steady_clock::now() - t0).count();
     }
   }
 };
+
+PhaseClock::PhaseClock(bool dual) : names(dual ? kDual : kPrimal) {
+  if (on) std::fill(g_sub_ms, g_sub_ms + kNumSubPhases, 0.0);
+}
+
+void PhaseClock::Dump(long long iterations) {
+  if (!on) return;
+  std::fprintf(stderr, "[phase timing] %lld iterations\n", iterations);
+  for (int i = 0; i < kPhases; ++i) {
+    std::fprintf(stderr, "  %-18s %10.3f ms  (%.3f ms/it)\n", names[i], ms[i],
+                 iterations > 0 ? ms[i] / iterations : 0.0);
+  }
+  std::fprintf(stderr, "  -- sections:\n");
+  for (int i = 0; i < kNumSubPhases; ++i) {
+    std::fprintf(stderr, "  %-22s %10.3f ms  (%.3f ms/it)\n", kSubPhaseNames[i], g_sub_ms[i],
+                 iterations > 0 ? g_sub_ms[i] / iterations : 0.0);
+  }
+}
 }  // namespace
 }  // namespace milp
 
@@ -692,6 +728,7 @@ void UpdateRow::FetchFromDevice() {
 
 // update_row.cc:196-216
 void UpdateRow::ComputeUpdatesRowWise() {
+  SubTimer timer(kSubUpdateRowCall);
   coefficient_.resize(matrix_.num_cols(), 0.0);
   listed_.resize(matrix_.num_cols(), 0);
   dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
@@ -702,6 +739,7 @@ void UpdateRow::ComputeUpdatesRowWise() {
 
 // update_row.cc:220-259
 void UpdateRow::ComputeUpdatesRowWiseHypersparse() {
+  SubTimer timer(kSubUpdateRowCall);
   coefficient_.resize(matrix_.num_cols(), 0.0);
   listed_.resize(matrix_.num_cols(), 0);
   dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
@@ -712,6 +750,7 @@ void UpdateRow::ComputeUpdatesRowWiseHypersparse() {
 
 // update_row.cc:261-280
 void UpdateRow::ComputeUpdatesForSingleRow(int row_as_col) {
+  SubTimer timer(kSubUpdateRowCall);
   coefficient_.resize(matrix_.num_cols(), 0.0);
   listed_.resize(matrix_.num_cols(), 0);
   dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
@@ -732,6 +771,7 @@ void UpdateRow::ComputeUpdatesColumnWise() {
 }
 
 void UpdateRow::RunColumnWise(const std::vector<Fractional>* w) {
+  SubTimer timer(kSubUpdateRowCall);
   pending_column_wise_ = false;
   dev_->SetMask(DeviceLp::kRelevant, pending_mask_.data(),
                 static_cast<int>(pending_mask_.size()));
@@ -961,6 +1001,7 @@ void PrimalEdgeNorms::UpdateBeforeBasisPivot(int entering_col, int leaving_col,
 // primal_edge_norms.cc:166-199
 void PrimalEdgeNorms::ComputeDirectionLeftInverse(int /*entering_col*/,
                                                   const ScatteredVector& d) {
+  SubTimer timer(kSubBtranW);
   const int size = d.size();
   const double kThreshold = 0.05 * size;
   if (!direction_left_inverse_.non_zeros.empty() &&
@@ -988,6 +1029,7 @@ void PrimalEdgeNorms::UpdateEdgeSquaredNorms(int entering_col, int leaving_col,
   const Fractional leaving_squared_norm =
       std::max(1.0, entering_squared_norm / Square(pivot));
   const Fractional factor = 2.0 / pivot;
+  SubTimer timer(kSubNormLoop);
   // a_j . (B^-T d) for every listed column in one GPU pass.
   dev_->ListDotsOverUpdateRow(direction_left_inverse_.values, &dots_);
   const std::vector<int>& positions = update_row.GetNonZeroPositions();
@@ -1039,6 +1081,7 @@ void PrimalEdgeNorms::CompletePendingUpdate(const std::vector<Fractional>& dots)
   const std::vector<int>& positions = pending_update_row_->GetNonZeroPositions();
   const std::vector<Fractional>& coefficients = pending_update_row_->GetCoefficients();
   if (dots.size() != positions.size()) throw DeviceError("edge-norm dots size mismatch");
+  SubTimer timer(kSubNormLoop);
   for (size_t k = 0; k < positions.size(); ++k) {
     const int col = positions[k];
     const Fractional coeff = coefficients[col];
@@ -1178,6 +1221,7 @@ class ReducedCosts {
   }
   void ComputeReducedCosts();
   void ComputeBasicObjectiveLeftInverse() {  // reduced_costs.cc:425-439
+    SubTimer timer(kSubBtranY);
     if (recompute_basic_objective_) ComputeBasicObjective();
     basic_objective_left_inverse_.values = basic_objective_;
     basic_objective_left_inverse_.non_zeros.clear();
@@ -1350,6 +1394,7 @@ void ReducedCosts::ComputeReducedCosts() {
     shifted_objective_[col] = objective_[col] + cost_perturbations_[col];
   // rc_j = (c_j + delta_j) - a_j . y for all N columns: the pricing SpMV.
   const std::vector<Fractional>& y = basic_objective_left_inverse_.values;
+  SubTimer pricing_timer(kSubPricingCall);
   if (deferred_norms_ != nullptr && deferred_norms_->HasPendingUpdate()) {
     if (dev_->list_epoch() == deferred_norms_->PendingListEpoch()) {
       // One pass over A: rc for every column plus the parked edge-norm dots.
@@ -1421,11 +1466,13 @@ class PrimalPrices {
     if (recompute_) {
       const std::vector<Fractional>& rc = reduced_costs_->GetReducedCosts();
       primal_edge_norms_->FlushPendingUpdate();  // no-op after the fused pass
+      SubTimer timer(kSubCandidatesFull);
       prices_.ClearAndResize(static_cast<int>(rc.size()));
       const std::vector<int> cols = variables_info_.GetIsRelevantBitRow().ToVector();
       UpdateEnteringCandidates<true>(cols);
       recompute_ = false;
     }
+    SubTimer timer(kSubGetMaximum);
     return prices_.GetMaximum();
   }
   void UpdateBeforeBasisPivot(int /*entering_col*/, UpdateRow* update_row) {
@@ -1471,6 +1518,7 @@ class PrimalPrices {
     bool add;  // AddOrUpdate(col, price) if true, Remove(col) otherwise
   };
   void QueueEnteringCandidates(const std::vector<int>& cols) {
+    SubTimer timer(kSubQueue);
     const Fractional tolerance = reduced_costs_->GetDualFeasibilityTolerance();
     const Bitset& dec = variables_info_.GetCanDecreaseBitRow();
     const Bitset& inc = variables_info_.GetCanIncreaseBitRow();
@@ -1484,6 +1532,7 @@ class PrimalPrices {
     }
   }
   void ReplayQueue() {
+    SubTimer timer(kSubQueue);
     const std::vector<Fractional>& sn = primal_edge_norms_->RawEdgeNorms();
     const std::vector<Fractional>& rc = reduced_costs_->RawReducedCosts();
     for (const QueuedOp& op : queue_) {
@@ -2189,6 +2238,7 @@ class RevisedSimplex {
   Status UpdateAndPivot(int entering_col, int leaving_row, Fractional target_bound);
   Status RefactorizeBasisIfNeeded(bool* refactorize) {
     if (*refactorize && !basis_factorization_.IsRefactorized()) {
+      SubTimer timer(kSubRefactorize);
       MILP_RETURN_IF_ERROR(basis_factorization_.Refactorize());
       update_row_.Invalidate();
       PermuteBasis();
@@ -3405,8 +3455,10 @@ Status RevisedSimplex::UpdateAndPivot(int entering_col, int leaving_row,
       parameters_.lu_factorization_pivot_threshold = threshold;
       basis_factorization_.SetLuParameters(parameters_.lu());
     }
+    SubTimer timer(kSubRefactorize);
     MILP_RETURN_IF_ERROR(basis_factorization_.ForceRefactorization());
   } else {
+    SubTimer timer(kSubLuUpdate);
     MILP_RETURN_IF_ERROR(basis_factorization_.Update(entering_col, leaving_row, direction_));
   }
   if (basis_factorization_.IsRefactorized()) PermuteBasis();

@@ -26,14 +26,14 @@ struct DotArgs {
 };
 
 // Dense column block: the structural columns whose CSC column is full (all m
-// rows). Values only, chain-interleaved so that lane (4j + k) streams chain k
-// of column j (Glop's accumulator r_{k+1} in ColumnScalarProduct,
-// sparse.h:514-542, since a full column's entry index equals its row index)
-// with 16-byte loads that are contiguous across the wave. With
-// steps = m / 4 chain elements per lane and pairs = steps / 2:
-//   body[((t2 * nd + j) * 4 + k) * 2 + h] = A[4 (2 t2 + h) + k, col_j], t2 < pairs
-//   body[pairs * nd * 8 + j * 4 + k]     = A[4 (steps - 1) + k, col_j] if steps odd
-//   tail[r * nd + j]                     = A[4 steps + r, col_j],       r < m % 4
+// rows). Values only, chain-major so that lane j of the wave for chain k
+// streams chain k of column j (Glop's accumulator r_{k+1} in
+// ColumnScalarProduct, sparse.h:514-542, since a full column's entry index
+// equals its row index) with 16-byte loads that are contiguous across the
+// wave. With steps = m / 4 chain elements per chain and pairs = steps / 2:
+//   body[((t2 * 4 + k) * nd + j) * 2 + h] = A[4 (2 t2 + h) + k, col_j], t2 < pairs
+//   body[pairs * nd * 8 + k * nd + j]     = A[4 (steps - 1) + k, col_j] if steps odd
+//   tail[r * nd + j]                      = A[4 steps + r, col_j],       r < m % 4
 struct DenseArgs {
   const double* body;
   const double* tail;

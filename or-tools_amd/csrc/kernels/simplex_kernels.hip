@@ -163,21 +163,29 @@ __global__ __launch_bounds__(256) void column_dot_kernel(DotArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Dense block dots (layout in kernel_args.h). Lane 4j+k owns chain k of dense
-// column j and walks it sequentially, two chain elements per 16-byte load, so
-// one wave step is one contiguous 1-KiB load. UNROLL loads are issued ahead
-// of the dependent adds. Lane 4j then folds ((r1 + r2) + r3) + r4 and adds the
-// <= 3 tail terms in order, exactly as ColumnScalarProduct.
+// Dense block dots (layout in kernel_args.h). A workgroup owns 64 dense
+// columns; its wave k streams chain k (Glop's accumulator r_{k+1} in
+// ColumnScalarProduct, sparse.h:514-542) of those columns, lane j walking
+// column j sequentially, two chain elements per 16-byte load: one wave step
+// is one contiguous 1-KiB load. The chain index is wave-uniform, so the y
+// (and w) elements a step needs are the same for every lane and come from
+// scalar loads: the vector memory path carries only A. UNROLL loads are
+// issued ahead of the dependent adds. The four partial sums meet in LDS and
+// lane j of wave 0 folds ((r1 + r2) + r3) + r4, then adds the <= 3 tail
+// terms in order, exactly as ColumnScalarProduct.
 typedef double dbl2 __attribute__((ext_vector_type(2)));
+constexpr int kDenseColsPerBlock = 64;
 
 template <int MODE, int UNROLL>
 __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
-  constexpr int kUnroll = UNROLL;
   constexpr bool kTwo = MODE == kUpdateRowWithDots || MODE == kPricingWithDots;
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int j = tid >> 2;
-  const int k = tid & 3;
-  const bool in_range = j < a.nd;
+  __shared__ double part[4][kDenseColsPerBlock];
+  __shared__ double part2[kTwo ? 4 : 1][kDenseColsPerBlock];
+  const int lane = threadIdx.x & 63;
+  const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // chain of this wave
+  const int j = blockIdx.x * kDenseColsPerBlock + lane;
+  const int nd = a.nd;
+  const bool in_range = j < nd;
   const int col = in_range ? a.dense_cols[j] : 0;
   bool active = in_range;
   if (MODE == kUpdateRowColumnWise || MODE == kUpdateRowWithDots)
@@ -189,17 +197,17 @@ __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
   double acc2 = 0.0;
   if (active) {
     const dbl2* __restrict__ p =
-        reinterpret_cast<const dbl2*>(a.body) + static_cast<int64_t>(j) * 4 + k;
+        reinterpret_cast<const dbl2*>(a.body) + static_cast<int64_t>(k) * nd + j;
     const double* __restrict__ y = a.y + k;
     const double* __restrict__ y2 = kTwo ? a.y2 + k : nullptr;
-    const int64_t stride = static_cast<int64_t>(a.nd) * 4;  // in double2
+    const int64_t stride = static_cast<int64_t>(nd) * 4;  // double2 per pair step
     int t = 0;
-    for (; t + kUnroll <= pairs; t += kUnroll) {
-      dbl2 v[kUnroll];
+    for (; t + UNROLL <= pairs; t += UNROLL) {
+      dbl2 v[UNROLL];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = __builtin_nontemporal_load(p + (t + u) * stride);
+      for (int u = 0; u < UNROLL; ++u) v[u] = __builtin_nontemporal_load(p + (t + u) * stride);
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
+      for (int u = 0; u < UNROLL; ++u) {
         const int r = (t + u) * 8;
         acc += v[u].x * y[r];
         acc += v[u].y * y[r + 4];
@@ -219,26 +227,22 @@ __global__ __launch_bounds__(256) void dense_dot_kernel(DenseArgs a) {
       }
     }
     if (steps & 1) {
-      const double v = a.body[static_cast<int64_t>(pairs) * a.nd * 8 + j * 4 + k];
+      const double v = a.body[static_cast<int64_t>(pairs) * nd * 8 +
+                              static_cast<int64_t>(k) * nd + j];
       acc += v * y[(steps - 1) * 4];
       if (kTwo) acc2 += v * y2[(steps - 1) * 4];
     }
   }
-  const double r2 = __shfl_down(acc, 1, kWave);
-  const double r3 = __shfl_down(acc, 2, kWave);
-  const double r4 = __shfl_down(acc, 3, kWave);
-  double q2 = 0.0, q3 = 0.0, q4 = 0.0;
-  if (kTwo) {
-    q2 = __shfl_down(acc2, 1, kWave);
-    q3 = __shfl_down(acc2, 2, kWave);
-    q4 = __shfl_down(acc2, 3, kWave);
-  }
+  part[k][lane] = acc;
+  if (kTwo) part2[k][lane] = acc2;
+  __syncthreads();
   if (k != 0 || !in_range) return;
-  double result = acc + r2 + r3 + r4;
-  double result2 = acc2 + q2 + q3 + q4;
+  double result = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+  double result2 = 0.0;
+  if (kTwo) result2 = part2[0][lane] + part2[1][lane] + part2[2][lane] + part2[3][lane];
   const int base = steps * 4;
   for (int r = 0; base + r < a.m; ++r) {
-    const double v = a.tail[static_cast<int64_t>(r) * a.nd + j];
+    const double v = a.tail[static_cast<int64_t>(r) * nd + j];
     result += v * a.y[base + r];
     if (kTwo) result2 += v * a.y2[base + r];
   }
@@ -273,18 +277,18 @@ __global__ __launch_bounds__(256) void dense_pack_kernel(const int64_t* starts,
   const int64_t total = pair_total + odd_total + tail_total;
   for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
        e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    if (e < pair_total) {
+    if (e < pair_total) {  // e = ((t2 * 4 + k) * nd + j) * 2 + h
       const int h = static_cast<int>(e & 1);
       const int64_t q = e >> 1;
-      const int k = static_cast<int>(q & 3);
-      const int64_t q2 = q >> 2;
-      const int j = static_cast<int>(q2 % nd);
-      const int t2 = static_cast<int>(q2 / nd);
+      const int j = static_cast<int>(q % nd);
+      const int64_t q2 = q / nd;
+      const int k = static_cast<int>(q2 & 3);
+      const int t2 = static_cast<int>(q2 >> 2);
       body[e] = vals[starts[dense_cols[j]] + 4 * (2 * t2 + h) + k];
-    } else if (e < pair_total + odd_total) {
+    } else if (e < pair_total + odd_total) {  // f = k * nd + j
       const int64_t f = e - pair_total;
-      const int k = static_cast<int>(f & 3);
-      const int j = static_cast<int>(f >> 2);
+      const int k = static_cast<int>(f / nd);
+      const int j = static_cast<int>(f % nd);
       body[e] = vals[starts[dense_cols[j]] + 4 * (steps - 1) + k];
     } else {
       const int64_t f = e - pair_total - odd_total;
@@ -475,7 +479,7 @@ static hipError_t launch_dense_dot(int mode, int blocks, const DenseArgs& args, 
 
 hipError_t dense_dot(int mode, int unroll, const DenseArgs& args, hipStream_t s) {
   if (args.nd <= 0) return hipSuccess;
-  const int blocks = div_up(static_cast<long>(args.nd) * 4, 256);
+  const int blocks = div_up(args.nd, kDenseColsPerBlock);
   if (unroll >= 32) return launch_dense_dot<32>(mode, blocks, args, s);
   if (unroll >= 16) return launch_dense_dot<16>(mode, blocks, args, s);
   return launch_dense_dot<8>(mode, blocks, args, s);

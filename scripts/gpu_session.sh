@@ -13,8 +13,7 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 if [ -z "$SKIP_C2" ]; then
   MILP_PHASE_TIMING=1 timeout -k 10 600 python -u $R/scripts/probe.py --config c2 --steps 20 \
-    --variants "MILP_DENSE_UNROLL=8,MILP_DEFER_NORMS=0" "MILP_DENSE_UNROLL=8" \
-               "MILP_DENSE_UNROLL=16" "MILP_DENSE_UNROLL=32" \
+    --variants ${C2_VARIANTS:-"MILP_DENSE_UNROLL=8" "MILP_DENSE_UNROLL=16"} \
     > $OUT/probe_c2.json 2> $OUT/probe_c2.err || { echo "c2 probe failed"; tail -30 $OUT/probe_c2.err; exit 1; }
   cat $OUT/probe_c2.json
 fi
@@ -23,5 +22,9 @@ if [ -z "$SKIP_C5" ]; then
     --warmup ${C5_WARMUP:-2000} --steps ${C5_STEPS:-500} \
     > $OUT/probe_c5.json 2> $OUT/probe_c5.err || { echo "c5 probe failed"; tail -30 $OUT/probe_c5.err; exit 1; }
   cat $OUT/probe_c5.json
+fi
+if [ -n "$RUN_BENCH" ]; then
+  timeout -k 10 900 python -u $R/bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
+  cat $OUT/bench.json
 fi
 echo "done $(date +%T)"
