@@ -159,6 +159,9 @@ class DeviceLp {
   double* d_out_list_ = nullptr; // per-list-slot results
   int32_t* d_cols_ = nullptr;    // arbitrary column list / filtered rows
   double* d_rho_vals_ = nullptr; // filtered rho values
+  uint32_t* d_row_tag_ = nullptr; // filtered-row marks of the column-order row-wise kernel
+  int32_t* d_row_pos_ = nullptr;
+  uint32_t row_tag_ = 0;
   void* d_cub_temp_ = nullptr;
   size_t cub_temp_bytes_ = 0;
   double* d_out_n2_ = nullptr;   // w . a_j of the fused pricing pass
@@ -166,7 +169,10 @@ class DeviceLp {
   uint64_t list_epoch_ = 0;
   int64_t list_entries_ = 0;  // CSC entries over the listed sparse columns
   int64_t list_dense_ = 0;    // listed dense columns
-  int dense_unroll_ = 16;     // MILP_DENSE_UNROLL: 16-B loads in flight per lane
+  int dense_unroll_ = 8;      // MILP_DENSE_UNROLL: 16-B loads in flight per lane
+  // Above this many filtered rows the row-wise update row runs column by
+  // column (MILP_ROWWISE_CHUNK_MAX_ROWS); both kernels give identical bits.
+  int rowwise_chunk_max_rows_ = 16;
 
   // pinned staging
   int32_t* h_pin_i_ = nullptr;

@@ -71,6 +71,9 @@ void DeviceLp::Init(int device) {
     const int v = std::atoi(u);
     if (v == 8 || v == 16 || v == 32) dense_unroll_ = v;
   }
+  if (const char* r = std::getenv("MILP_ROWWISE_CHUNK_MAX_ROWS")) {
+    rowwise_chunk_max_rows_ = std::atoi(r);
+  }
 }
 
 template <typename T>
@@ -156,6 +159,10 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   d_out_list_ = Alloc<double>(std::max(n_total_, m_));
   d_cols_ = Alloc<int32_t>(std::max(n_total_, m_));
   d_rho_vals_ = Alloc<double>(m_);
+  d_row_tag_ = Alloc<uint32_t>(m_);
+  d_row_pos_ = Alloc<int32_t>(m_);
+  Check(hipMemsetAsync(d_row_tag_, 0, std::max(1, m_) * sizeof(uint32_t), S(stream_)), "memset");
+  row_tag_ = 0;
   Check(hipMemsetAsync(d_coeff_, 0, n_total_ * sizeof(double), S(stream_)), "memset");
   // hipcub temp storage for the flag compaction.
   cub_temp_bytes_ = 0;
@@ -349,7 +356,34 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
   a.algorithm = algorithm;
   const int id = algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW;
   BeginKernel(id);
-  Check(milp_launch::row_wise_update(a, S(stream_)), "rowwise");
+  if (k <= rowwise_chunk_max_rows_) {
+    // Few rows: workgroups own column chunks and merge the rows in order.
+    Check(milp_launch::row_wise_update(a, S(stream_)), "rowwise");
+  } else {
+    // Many rows: one thread per column gathers its filtered entries from the
+    // CSC copy (same arithmetic, same order).
+    if (++row_tag_ == 0) {  // wrapped: clear the marks
+      Check(hipMemsetAsync(d_row_tag_, 0, m_ * sizeof(uint32_t), S(stream_)), "memset");
+      row_tag_ = 1;
+    }
+    Check(milp_launch::tag_rows(d_cols_, k, row_tag_, d_row_tag_, d_row_pos_, S(stream_)),
+          "tag rows");
+    milp_kernels::RowWiseColArgs c{};
+    c.starts = d_starts_;
+    c.rows = d_rows_;
+    c.vals = d_vals_;
+    c.row_tag = d_row_tag_;
+    c.row_pos = d_row_pos_;
+    c.tag = row_tag_;
+    c.rho = d_rho_vals_;
+    c.num_cols = n_total_;
+    c.relevant = d_masks_[kRelevant];
+    c.coefficient = d_coeff_;
+    c.flags = d_flags_;
+    c.drop_tolerance = drop;
+    c.algorithm = algorithm;
+    Check(milp_launch::row_wise_update_by_column(c, S(stream_)), "rowwise by column");
+  }
   double entries = 0.0;
   for (int r : filtered_rows) entries += double(h_t_starts_[r + 1] - h_t_starts_[r]);
   EndKernel(id, 12.0 * entries + 12.0 * k + 9.0 * n_total_);

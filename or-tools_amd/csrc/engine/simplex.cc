@@ -1468,8 +1468,7 @@ class PrimalPrices {
       primal_edge_norms_->FlushPendingUpdate();  // no-op after the fused pass
       SubTimer timer(kSubCandidatesFull);
       prices_.ClearAndResize(static_cast<int>(rc.size()));
-      const std::vector<int> cols = variables_info_.GetIsRelevantBitRow().ToVector();
-      UpdateEnteringCandidates<true>(cols);
+      RebuildEnteringCandidates();
       recompute_ = false;
     }
     SubTimer timer(kSubGetMaximum);
@@ -1535,16 +1534,52 @@ class PrimalPrices {
     SubTimer timer(kSubQueue);
     const std::vector<Fractional>& sn = primal_edge_norms_->RawEdgeNorms();
     const std::vector<Fractional>& rc = reduced_costs_->RawReducedCosts();
-    for (const QueuedOp& op : queue_) {
-      if (op.add) {
-        prices_.AddOrUpdate(op.col, Square(rc[op.col]) / sn[op.col]);
-      } else {
-        prices_.Remove(op.col);
+    if (recompute_) {
+      // The prices are rebuilt from scratch before anything reads them
+      // (every reader checks recompute_ first, GetBestEnteringColumn clears
+      // them): of the queued updates only the top-k draws from the RNG
+      // matter.
+      for (const QueuedOp& op : queue_) {
+        if (op.add) prices_.AddOrUpdateBeforeClear(op.col, Square(rc[op.col]) / sn[op.col]);
+      }
+    } else {
+      for (const QueuedOp& op : queue_) {
+        if (op.add) {
+          prices_.AddOrUpdate(op.col, Square(rc[op.col]) / sn[op.col]);
+        } else {
+          prices_.Remove(op.col);
+        }
       }
     }
     queue_.clear();
   }
   std::vector<QueuedOp> queue_;
+  // UpdateEnteringCandidates<from_clean_state=true> over the relevant
+  // columns (reduced_costs.cc:557-600), walking the bitset words directly.
+  void RebuildEnteringCandidates() {
+    const Fractional tolerance = reduced_costs_->GetDualFeasibilityTolerance();
+    const uint64_t* dec = variables_info_.GetCanDecreaseBitRow().data();
+    const uint64_t* inc = variables_info_.GetCanIncreaseBitRow().data();
+    const Bitset& relevant = variables_info_.GetIsRelevantBitRow();
+    const uint64_t* rel = relevant.data();
+    const Fractional* sn = primal_edge_norms_->GetSquaredNorms().data();
+    const Fractional* rc = reduced_costs_->GetReducedCosts().data();
+    const int num_words = relevant.NumWords();
+    for (int w = 0; w < num_words; ++w) {
+      uint64_t bits = rel[w];
+      const uint64_t dec_w = dec[w];
+      const uint64_t inc_w = inc[w];
+      while (bits != 0) {
+        const int b = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        const int col = (w << 6) + b;
+        const Fractional reduced_cost = rc[col];
+        const bool is_dual_infeasible = ((reduced_cost > tolerance) && ((dec_w >> b) & 1)) !=
+                                        ((reduced_cost < -tolerance) && ((inc_w >> b) & 1));
+        if (is_dual_infeasible) prices_.AddOrUpdate(col, Square(reduced_cost) / sn[col]);
+      }
+    }
+  }
   template <bool from_clean_state>
   void UpdateEnteringCandidates(const std::vector<int>& cols) {
     const Fractional tolerance = reduced_costs_->GetDualFeasibilityTolerance();

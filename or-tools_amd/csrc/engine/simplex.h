@@ -149,6 +149,12 @@ class DynamicMaximum {
     values_[position] = value;
     if (value >= threshold_) UpdateTopK(position, value);
   }
+  // AddOrUpdate on a state that is cleared (ClearAndResize) before it is
+  // read again: only the top-k bookkeeping, which may draw from the RNG
+  // (pricing.h:303-307), has an effect that outlives the clear.
+  void AddOrUpdateBeforeClear(int position, Fractional value) {
+    if (value >= threshold_) UpdateTopK(position, value);
+  }
   int GetMaximum();
 
  private:

@@ -65,6 +65,25 @@ struct RowWiseArgs {
   int algorithm;  // 0 single row, 1 hypersparse, 2 row-wise
 };
 
+// The same row-wise update row evaluated column by column from the CSC copy
+// (for many filtered rows): row r of the filtered list sits at position
+// row_pos[r] when row_tag[r] == tag.
+struct RowWiseColArgs {
+  const int64_t* starts;  // CSC of [A | I]
+  const int32_t* rows;
+  const double* vals;
+  const uint32_t* row_tag;
+  const int32_t* row_pos;
+  uint32_t tag;
+  const double* rho;  // rho value per filtered row, list order
+  int num_cols;
+  const uint64_t* relevant;
+  double* coefficient;
+  uint8_t* flags;
+  double drop_tolerance;
+  int algorithm;  // 0 single row, 1 hypersparse, 2 row-wise
+};
+
 struct RowSumArgs {
   const int64_t* t_starts;
   const int32_t* t_cols;
@@ -87,6 +106,10 @@ hipError_t dense_pack(const int64_t* starts, const double* vals, const int32_t* 
                       int nd, int m, double* body, double* tail, hipStream_t s);
 hipError_t gather(const int32_t* list, int n, const double* src, double* dst, hipStream_t s);
 hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s);
+// Marks the filtered rows (row_tag[r] = tag, row_pos[r] = list position).
+hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag,
+                    uint32_t* row_tag, int32_t* row_pos, hipStream_t s);
+hipError_t row_wise_update_by_column(const milp_kernels::RowWiseColArgs& args, hipStream_t s);
 hipError_t row_sums(const milp_kernels::RowSumArgs& args, hipStream_t s);
 hipError_t column_squared_norms(const int64_t* starts, const double* vals,
                                 const uint64_t* relevant, int ncols, double* out,

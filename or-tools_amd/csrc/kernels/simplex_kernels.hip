@@ -371,6 +371,105 @@ __global__ __launch_bounds__(256) void row_wise_update_kernel(RowWiseArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// The row-wise update row for many filtered rows, one thread per column.
+// Per column the result must be the host scatter's: contributions
+// rho_k * A[r_k, j] accumulated in the order k of the filtered list (which
+// need not be ascending in r). The thread collects its column's filtered
+// entries (a CSC column holds ~nnz/N of them), orders them by k with an
+// in-register insertion sort, and accumulates in that order with the same
+// first-write rule as row_wise_update_kernel. Columns with more than
+// kMaxColumnHits filtered entries fall back to repeated minimum selection.
+constexpr int kMaxColumnHits = 16;
+
+__device__ __forceinline__ double row_wise_accumulate(double acc, bool first, double v,
+                                                      int algorithm) {
+  if (!first) return acc + v;
+  return algorithm == 2 ? 0.0 + v : v;  // AssignToZero then +=, or first assign
+}
+
+__global__ __launch_bounds__(256) void row_wise_by_column_kernel(RowWiseColArgs a) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= a.num_cols) return;
+  const int64_t s = a.starts[col];
+  const int64_t e = a.starts[col + 1];
+  int hits = 0;
+  for (int64_t i = s; i < e; ++i) hits += (a.row_tag[a.rows[i]] == a.tag) ? 1 : 0;
+  double acc = 0.0;
+  if (hits > 0 && hits <= kMaxColumnHits) {
+    int ks[kMaxColumnHits];
+    double vs[kMaxColumnHits];
+    int c = 0;
+    for (int64_t i = s; i < e; ++i) {
+      const int r = a.rows[i];
+      if (a.row_tag[r] != a.tag) continue;
+      const int k = a.row_pos[r];
+      const double v = a.rho[k] * a.vals[i];
+      int p = c;
+#pragma unroll
+      for (int q = kMaxColumnHits - 1; q > 0; --q) {
+        if (q <= c && ks[q - 1] > k) {
+          ks[q] = ks[q - 1];
+          vs[q] = vs[q - 1];
+          p = q - 1;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kMaxColumnHits; ++q) {
+        if (q == p) {
+          ks[q] = k;
+          vs[q] = v;
+        }
+      }
+      ++c;
+    }
+#pragma unroll
+    for (int q = 0; q < kMaxColumnHits; ++q) {
+      if (q < c) acc = row_wise_accumulate(acc, q == 0, vs[q], a.algorithm);
+    }
+  } else if (hits > kMaxColumnHits) {
+    int last = -1;
+    for (int h = 0; h < hits; ++h) {
+      int best_k = 0x7fffffff;
+      double best_v = 0.0;
+      for (int64_t i = s; i < e; ++i) {
+        const int r = a.rows[i];
+        if (a.row_tag[r] != a.tag) continue;
+        const int k = a.row_pos[r];
+        if (k > last && k < best_k) {
+          best_k = k;
+          best_v = a.rho[k] * a.vals[i];
+        }
+      }
+      acc = row_wise_accumulate(acc, h == 0, best_v, a.algorithm);
+      last = best_k;
+    }
+  }
+  const bool touched = hits > 0;
+  const bool rel = bit_set(a.relevant, col);
+  bool listed;
+  if (a.algorithm == 0) {
+    listed = touched && rel && fabs(acc) > a.drop_tolerance;
+    if (listed) a.coefficient[col] = acc;
+  } else if (a.algorithm == 1) {
+    listed = touched && rel && fabs(acc) > a.drop_tolerance;
+    if (touched) a.coefficient[col] = acc;
+  } else {
+    listed = rel && fabs(acc) > a.drop_tolerance;
+    a.coefficient[col] = touched ? acc : 0.0;
+  }
+  a.flags[col] = listed ? 1 : 0;
+}
+
+__global__ void tag_rows_kernel(const int32_t* filtered_rows, int n, uint32_t tag,
+                                uint32_t* row_tag, int32_t* row_pos) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    const int r = filtered_rows[k];
+    row_tag[r] = tag;
+    row_pos[r] = k;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Row sums sum_j mult_j * A[r, j] in increasing j (the order the host scatter
 // ColumnAddMultipleToDenseColumn produces), zero multipliers skipped
 // (sparse.h:393). One wave per row: lanes load 64 consecutive CSR entries,
@@ -501,6 +600,20 @@ hipError_t gather(const int32_t* list, int n, const double* src, double* dst, hi
 hipError_t row_wise_update(const RowWiseArgs& args, hipStream_t s) {
   const int blocks = div_up(args.num_cols, kChunk);
   row_wise_update_kernel<<<blocks, 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag,
+                    uint32_t* row_tag, int32_t* row_pos, hipStream_t s) {
+  if (num_filtered <= 0) return hipSuccess;
+  tag_rows_kernel<<<std::min(1024, div_up(num_filtered, 256)), 256, 0, s>>>(
+      filtered_rows, num_filtered, tag, row_tag, row_pos);
+  return hipGetLastError();
+}
+
+hipError_t row_wise_update_by_column(const RowWiseColArgs& args, hipStream_t s) {
+  if (args.num_cols <= 0) return hipSuccess;
+  row_wise_by_column_kernel<<<div_up(args.num_cols, 256), 256, 0, s>>>(args);
   return hipGetLastError();
 }
 

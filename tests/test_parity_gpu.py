@@ -83,6 +83,22 @@ def test_parked_edge_norm_update_parity(shape, block, monkeypatch):
     assert launches["1"] < launches["0"], launches
 
 
+@pytest.mark.parametrize("chunk_max", ["0", "1000000"])
+@pytest.mark.parametrize("seed", [21, 22, 23])
+def test_row_wise_kernel_choice_parity(seed, chunk_max, monkeypatch):
+    """Row-wise update rows through the column-order kernel (every filtered
+    rho, chunk_max=0) or the row-chunk kernel (always): both must reproduce
+    the host scatter order, so the dual simplex matches the oracle bit for bit
+    either way. Config-5-shaped LPs (a few entries per column)."""
+    monkeypatch.setenv("MILP_ROWWISE_CHUNK_MAX_ROWS", chunk_max)
+    lp = lp_gen.sparse_c5_lp(300 + 50 * (seed % 3), 3000, 6, seed)
+    p = abi.default_params(use_dual_simplex=1)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    st = g.kernel_stats()
+    assert st["update_row"]["launches"] > 0
+
+
 @pytest.mark.parametrize("unroll", ["8", "32"])
 def test_dense_block_unroll_parity(unroll, monkeypatch):
     """The dense-block kernel's load depth does not change any result."""
