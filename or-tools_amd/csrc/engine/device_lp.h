@@ -96,7 +96,7 @@ class DeviceLp {
   void Download(void* dst, const void* src, size_t bytes);
   void BeginKernel(int id);
   void EndKernel(int id, double bytes);
-  void Compact(int n);  // flags_ -> list_ (ascending), count -> list_count_
+  void Compact(int n);  // flags_ -> list_ (ascending) + coefficients, async
   void BuildDenseBlock();
   // Launches the CSC kernel over the sparse columns (all columns when there is
   // no dense block) and the dense-block kernel; mode as in column_dot.
@@ -173,12 +173,18 @@ class DeviceLp {
   // Above this many filtered rows the row-wise update row runs column by
   // column (MILP_ROWWISE_CHUNK_MAX_ROWS); both kernels give identical bits.
   int rowwise_chunk_max_rows_ = 16;
+  // The column-order kernel sorts a column's hits in registers: used only
+  // when no column is longer than this (kernel kMaxColumnHits).
+  static constexpr int kColumnKernelMaxColumnLength = 32;
+  int64_t max_col_len_ = 0;
 
   // pinned staging
   int32_t* h_pin_i_ = nullptr;
   double* h_pin_d_ = nullptr;
   double* h_pin_d2_ = nullptr;
   double* h_pin_w_ = nullptr;
+  int* h_pin_count_ = nullptr;
+  int last_list_len_ = 0;
 };
 
 }  // namespace milp

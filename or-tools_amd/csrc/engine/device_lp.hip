@@ -46,6 +46,7 @@ DeviceLp::~DeviceLp() {
   if (h_pin_d_) (void)hipHostFree(h_pin_d_);
   if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
   if (h_pin_w_) (void)hipHostFree(h_pin_w_);
+  if (h_pin_count_) (void)hipHostFree(h_pin_count_);
   if (ev_start_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_start_));
   if (ev_stop_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_stop_));
   if (stream_) (void)hipStreamDestroy(S(stream_));
@@ -126,6 +127,10 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   n_total_ = csc.num_cols();
   nnz_ = csc.num_entries();
   avg_col_len_ = n_total_ > 0 ? static_cast<double>(nnz_) / n_total_ : 0.0;
+  max_col_len_ = 0;
+  for (int c = 0; c < n_total_; ++c) {
+    max_col_len_ = std::max<int64_t>(max_col_len_, csc.starts_[c + 1] - csc.starts_[c]);
+  }
   h_starts_ = csc.starts_;
   h_t_starts_ = csr.starts_;
   d_starts_ = Alloc<int64_t>(n_total_ + 1);
@@ -180,7 +185,11 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d_), big * sizeof(double)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d2_), big * sizeof(double)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_w_), (m_ + 1) * sizeof(double)), "pin");
+  if (h_pin_count_ == nullptr) {
+    Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_count_), sizeof(int)), "pin");
+  }
   list_count_ = 0;
+  last_list_len_ = 0;
   ++list_epoch_;
   BuildDenseBlock();
   Synchronize();
@@ -281,16 +290,25 @@ void DeviceLp::SetMask(Mask which, const uint64_t* words, int num_words) {
   Upload(d_masks_[which], h.data(), num_words * sizeof(uint64_t));
 }
 
+// Compaction of the update-row flags into the ascending list of listed
+// positions plus their coefficients. No host synchronization here: the count
+// comes back with the list in FetchUpdateRow (one round trip per update row).
 void DeviceLp::Compact(int n) {
-  size_t bytes = cub_temp_bytes_;
-  Check(hipcub::DeviceSelect::Flagged(d_cub_temp_, bytes,
-                                      hipcub::CountingInputIterator<int32_t>(0), d_flags_,
-                                      d_list_, d_count_, n, S(stream_)),
-        "cub flagged");
-  int count = 0;
-  Download(h_pin_i_, d_count_, sizeof(int));
-  count = h_pin_i_[0];
-  list_count_ = count;
+  if (n <= milp_launch::kSmallCompactMax) {
+    // One workgroup: flags -> list + coefficients + count in a single launch.
+    Check(milp_launch::compact_small(d_flags_, n, d_coeff_, d_list_, d_out_list_, d_count_,
+                                     S(stream_)),
+          "compact small");
+  } else {
+    size_t bytes = cub_temp_bytes_;
+    Check(hipcub::DeviceSelect::Flagged(d_cub_temp_, bytes,
+                                        hipcub::CountingInputIterator<int32_t>(0), d_flags_,
+                                        d_list_, d_count_, n, S(stream_)),
+          "cub flagged");
+    Check(milp_launch::gather_counted(d_list_, d_count_, n, d_coeff_, d_out_list_, S(stream_)),
+          "gather");
+  }
+  list_count_ = -1;  // known after FetchUpdateRow
   ++list_epoch_;
 }
 
@@ -356,7 +374,7 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
   a.algorithm = algorithm;
   const int id = algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW;
   BeginKernel(id);
-  if (k <= rowwise_chunk_max_rows_) {
+  if (k <= rowwise_chunk_max_rows_ || max_col_len_ > kColumnKernelMaxColumnLength) {
     // Few rows: workgroups own column chunks and merge the rows in order.
     Check(milp_launch::row_wise_update(a, S(stream_)), "rowwise");
   } else {
@@ -392,17 +410,30 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
 
 void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* values) {
   CallTimer timer(&stats_, MI_K_READBACK);
-  const int n = list_count_;
+  // Count, and a prefix of the list sized from the previous update row, in
+  // one round trip; the rest (if any) in a second one.
+  const int cap = std::min<int64_t>(n_total_, std::max<int64_t>(4096, 2 * int64_t(last_list_len_)));
+  Check(hipMemcpyAsync(h_pin_count_, d_count_, sizeof(int), hipMemcpyDeviceToHost, S(stream_)),
+        "D2H");
+  Check(hipMemcpyAsync(h_pin_i_, d_list_, cap * sizeof(int32_t), hipMemcpyDeviceToHost,
+                       S(stream_)),
+        "D2H");
+  Download(h_pin_d_, d_out_list_, cap * sizeof(double));
+  const int n = *h_pin_count_;
+  if (n < 0 || n > n_total_) throw DeviceError("bad update-row count");
+  if (n > cap) {
+    Check(hipMemcpyAsync(h_pin_i_ + cap, d_list_ + cap, (n - cap) * sizeof(int32_t),
+                         hipMemcpyDeviceToHost, S(stream_)),
+          "D2H");
+    Download(h_pin_d_ + cap, d_out_list_ + cap, (n - cap) * sizeof(double));
+  }
+  list_count_ = n;
+  last_list_len_ = n;
   positions->resize(n);
   values->resize(n);
   list_entries_ = 0;
   list_dense_ = 0;
   if (n == 0) return;
-  Check(milp_launch::gather(d_list_, n, d_coeff_, d_out_list_, S(stream_)), "gather");
-  Check(hipMemcpyAsync(h_pin_i_, d_list_, n * sizeof(int32_t), hipMemcpyDeviceToHost,
-                       S(stream_)),
-        "D2H");
-  Download(h_pin_d_, d_out_list_, n * sizeof(double));
   std::memcpy(positions->data(), h_pin_i_, n * sizeof(int32_t));
   std::memcpy(values->data(), h_pin_d_, n * sizeof(double));
   for (int i = 0; i < n; ++i) {
@@ -425,6 +456,7 @@ double DeviceLp::ReadCoefficient(int col) {
 
 void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<double>* out) {
   CallTimer timer(&stats_, MI_K_PRIMAL_NORMS);
+  if (list_count_ < 0) throw DeviceError("update-row list used before FetchUpdateRow");
   const int n = list_count_;
   out->resize(n);
   if (n == 0) return;
@@ -493,6 +525,7 @@ void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& 
     std::memcpy(h_pin_w_, w->data(), m_ * sizeof(double));
     Upload(d_vec_w_, h_pin_w_, m_ * sizeof(double));
   }
+  if (fused && list_count_ < 0) throw DeviceError("update-row list used before FetchUpdateRow");
   const int n_list = fused ? list_count_ : 0;
   BeginKernel(MI_K_PRICING);
   if (fused) {

@@ -105,6 +105,14 @@ hipError_t dense_dot(int mode, int unroll, const milp_kernels::DenseArgs& args, 
 hipError_t dense_pack(const int64_t* starts, const double* vals, const int32_t* dense_cols,
                       int nd, int m, double* body, double* tail, hipStream_t s);
 hipError_t gather(const int32_t* list, int n, const double* src, double* dst, hipStream_t s);
+// dst[i] = src[list[i]] for i < *count (count on the device, at most n).
+hipError_t gather_counted(const int32_t* list, const int* count, int n, const double* src,
+                          double* dst, hipStream_t s);
+// Flags -> ascending list + coefficient gather + count, one workgroup, for
+// n <= kSmallCompactMax.
+constexpr int kSmallCompactMax = 1 << 17;
+hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32_t* list,
+                         double* vals, int* count, hipStream_t s);
 hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s);
 // Marks the filtered rows (row_tag[r] = tag, row_pos[r] = list position).
 hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag,

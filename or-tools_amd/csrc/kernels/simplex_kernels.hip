@@ -304,6 +304,46 @@ __global__ void gather_kernel(const int32_t* list, int n, const double* src, dou
     dst[i] = src[list[i]];
 }
 
+__global__ void gather_counted_kernel(const int32_t* list, const int* count, const double* src,
+                                      double* dst) {
+  const int n = *count;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    dst[i] = src[list[i]];
+}
+
+// Update-row compaction for small N in one workgroup: thread t owns a
+// contiguous slice of the flags, a block-wide exclusive scan of the slice
+// counts gives each thread its output offset, so the list comes out in
+// ascending position order, as hipcub's select would produce it.
+constexpr int kCompactThreads = 1024;
+__global__ __launch_bounds__(kCompactThreads) void compact_small_kernel(
+    const uint8_t* flags, int n, const double* coeff, int32_t* list, double* vals, int* count) {
+  __shared__ int sums[kCompactThreads];
+  const int t = threadIdx.x;
+  const int per = (n + kCompactThreads - 1) / kCompactThreads;
+  const int b = min(n, t * per);
+  const int e = min(n, b + per);
+  int c = 0;
+  for (int i = b; i < e; ++i) c += flags[i] != 0;
+  sums[t] = c;
+  __syncthreads();
+  for (int off = 1; off < kCompactThreads; off <<= 1) {
+    const int v = t >= off ? sums[t - off] : 0;
+    __syncthreads();
+    sums[t] += v;
+    __syncthreads();
+  }
+  int pos = sums[t] - c;
+  for (int i = b; i < e; ++i) {
+    if (flags[i] != 0) {
+      list[pos] = i;
+      vals[pos] = coeff[i];
+      ++pos;
+    }
+  }
+  if (t == kCompactThreads - 1) *count = sums[t];
+}
+
 // ---------------------------------------------------------------------------
 // Row-wise update row (update_row.cc:196-280). The filtered non-zeros of rho
 // (ascending rows) are merged column-chunk by column-chunk: a workgroup owns
@@ -379,7 +419,7 @@ __global__ __launch_bounds__(256) void row_wise_update_kernel(RowWiseArgs a) {
 // in-register insertion sort, and accumulates in that order with the same
 // first-write rule as row_wise_update_kernel. Columns with more than
 // kMaxColumnHits filtered entries fall back to repeated minimum selection.
-constexpr int kMaxColumnHits = 16;
+constexpr int kMaxColumnHits = 32;  // = DeviceLp::kColumnKernelMaxColumnLength
 
 __device__ __forceinline__ double row_wise_accumulate(double acc, bool first, double v,
                                                       int algorithm) {
@@ -594,6 +634,20 @@ hipError_t dense_pack(const int64_t* starts, const double* vals, const int32_t* 
 hipError_t gather(const int32_t* list, int n, const double* src, double* dst, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   gather_kernel<<<std::min(2048, div_up(n, 256)), 256, 0, s>>>(list, n, src, dst);
+  return hipGetLastError();
+}
+
+hipError_t gather_counted(const int32_t* list, const int* count, int n, const double* src,
+                          double* dst, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  gather_counted_kernel<<<std::min(2048, div_up(n, 256)), 256, 0, s>>>(list, count, src, dst);
+  return hipGetLastError();
+}
+
+hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32_t* list,
+                         double* vals, int* count, hipStream_t s) {
+  if (n > kSmallCompactMax) return hipErrorInvalidValue;
+  compact_small_kernel<<<1, kCompactThreads, 0, s>>>(flags, n, coeff, list, vals, count);
   return hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ if [ -z "$SKIP_C5" ]; then
   cat $OUT/probe_c5.json
 fi
 if [ -n "$RUN_BENCH" ]; then
-  timeout -k 10 900 python -u $R/bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
+  timeout -k 10 900 python -u $R/bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
   cat $OUT/bench.json
 fi
 echo "done $(date +%T)"
