@@ -142,6 +142,8 @@ class DeviceLp {
   // masks
   uint64_t* d_masks_[kNumMasks] = {nullptr, nullptr, nullptr};
   std::vector<uint64_t> h_masks_[kNumMasks];
+  uint64_t* h_pin_mask_[kNumMasks] = {nullptr, nullptr, nullptr};
+  void* ev_mask_[kNumMasks] = {nullptr, nullptr, nullptr};  // hipEvent_t: slot reusable
   int mask_words_ = 0;
 
   // scratch

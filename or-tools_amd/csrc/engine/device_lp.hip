@@ -47,6 +47,10 @@ DeviceLp::~DeviceLp() {
   if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
   if (h_pin_w_) (void)hipHostFree(h_pin_w_);
   if (h_pin_count_) (void)hipHostFree(h_pin_count_);
+  for (int k = 0; k < kNumMasks; ++k) {
+    if (h_pin_mask_[k]) (void)hipHostFree(h_pin_mask_[k]);
+    if (ev_mask_[k]) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_mask_[k]));
+  }
   if (ev_start_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_start_));
   if (ev_stop_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_stop_));
   if (stream_) (void)hipStreamDestroy(S(stream_));
@@ -68,6 +72,11 @@ void DeviceLp::Init(int device) {
   Check(hipEventCreate(&b), "hipEventCreate");
   ev_start_ = a;
   ev_stop_ = b;
+  for (int k = 0; k < kNumMasks; ++k) {
+    hipEvent_t e;
+    Check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    ev_mask_[k] = e;
+  }
   if (const char* u = std::getenv("MILP_DENSE_UNROLL")) {
     const int v = std::atoi(u);
     if (v == 8 || v == 16 || v == 32) dense_unroll_ = v;
@@ -149,6 +158,11 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   for (int k = 0; k < kNumMasks; ++k) {
     d_masks_[k] = Alloc<uint64_t>(mask_words_);
     h_masks_[k].assign(mask_words_, ~0ull);  // force first upload
+    Check(hipEventSynchronize(reinterpret_cast<hipEvent_t>(ev_mask_[k])), "mask event");
+    if (h_pin_mask_[k]) (void)hipHostFree(h_pin_mask_[k]);
+    Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_mask_[k]),
+                        std::max(1, mask_words_) * sizeof(uint64_t)),
+          "pin");
   }
   d_vec_m_ = Alloc<double>(m_);
   d_vec_m2_ = Alloc<double>(m_);
@@ -287,7 +301,13 @@ void DeviceLp::SetMask(Mask which, const uint64_t* words, int num_words) {
   if (num_words != mask_words_) throw DeviceError("mask size mismatch");
   if (std::memcmp(h.data(), words, num_words * sizeof(uint64_t)) == 0) return;
   std::memcpy(h.data(), words, num_words * sizeof(uint64_t));
-  Upload(d_masks_[which], h.data(), num_words * sizeof(uint64_t));
+  // Asynchronous copy from a pinned slot; the slot is reused only once its
+  // previous copy has completed.
+  hipEvent_t done = reinterpret_cast<hipEvent_t>(ev_mask_[which]);
+  Check(hipEventSynchronize(done), "mask event");
+  std::memcpy(h_pin_mask_[which], words, num_words * sizeof(uint64_t));
+  Upload(d_masks_[which], h_pin_mask_[which], num_words * sizeof(uint64_t));
+  Check(hipEventRecord(done, S(stream_)), "mask event");
 }
 
 // Compaction of the update-row flags into the ascending list of listed
@@ -412,7 +432,8 @@ void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* 
   CallTimer timer(&stats_, MI_K_READBACK);
   // Count, and a prefix of the list sized from the previous update row, in
   // one round trip; the rest (if any) in a second one.
-  const int cap = std::min<int64_t>(n_total_, std::max<int64_t>(4096, 2 * int64_t(last_list_len_)));
+  const int cap = std::min<int64_t>(
+      n_total_, std::max<int64_t>(4096, int64_t(last_list_len_) + last_list_len_ / 4));
   Check(hipMemcpyAsync(h_pin_count_, d_count_, sizeof(int), hipMemcpyDeviceToHost, S(stream_)),
         "D2H");
   Check(hipMemcpyAsync(h_pin_i_, d_list_, cap * sizeof(int32_t), hipMemcpyDeviceToHost,

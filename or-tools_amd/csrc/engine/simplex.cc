@@ -51,6 +51,18 @@ struct PhaseClock {
     t = now;
   }
   void Dump(long long iterations);
+  // MILP_PHASE_TIMING_EVERY=k: dump and restart every k iterations.
+  const long long every = [] {
+    const char* e = std::getenv("MILP_PHASE_TIMING_EVERY");
+    return e ? std::atoll(e) : 0LL;
+  }();
+  long long window = 0;
+  void Tick() {
+    if (!on || every <= 0 || ++window < every) return;
+    Dump(window);
+    Reset();
+  }
+  void Reset();
 };
 
 // Finer split inside the phases (same switch): wall time of named sections.
@@ -80,6 +92,12 @@ struct SubTimer {
 
 PhaseClock::PhaseClock(bool dual) : names(dual ? kDual : kPrimal) {
   if (on) std::fill(g_sub_ms, g_sub_ms + kNumSubPhases, 0.0);
+}
+
+void PhaseClock::Reset() {
+  std::fill(ms, ms + kPhases, 0.0);
+  std::fill(g_sub_ms, g_sub_ms + kNumSubPhases, 0.0);
+  window = 0;
 }
 
 void PhaseClock::Dump(long long iterations) {
@@ -3844,6 +3862,7 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     clock.Mark(8);
     OnIterationDone(time_limit);
     clock.Mark(9);
+    clock.Tick();
   }
   return Status::OK();
 }
