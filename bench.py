@@ -163,6 +163,64 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     return out
 
 
+def run_c3(args, rank, world, local_rank, dist, barrier, sync):
+    """Config 3: a suite of 94 Netlib-shaped LPs solved
+    concurrently on one GPU (tests/netlib_suite.py; the Netlib files are not
+    available offline). Unit of work = one LP solved from scratch, device
+    upload included. Each rank solves its own copy of the suite (weak
+    scaling, no collective)."""
+    import concurrent.futures
+    import netlib_suite
+    import lp_gen
+    lps = netlib_suite.suite(max_rows=args.c3_max_rows)
+    p = abi.default_params()
+    warm = engine.LpHandle(p, device=local_rank)  # module load / first launches
+    warm.load(lp_gen.random_sparse_lp(40, 100, 0.1, 1))
+    warm.solve()
+    handles = []
+    for lp in lps:
+        h = engine.LpHandle(p, device=local_rank)
+        h.load(lp)
+        handles.append(h)
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    res = engine.batch_solve(handles, num_threads=args.c3_workers)
+    sync()
+    barrier()
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+    statuses = [r.problem_status for r in res]
+    out = {
+        "metric": "batched LPs/sec", "unit": "LPs/s",
+        "value": len(lps) * world / elapsed, "lps": len(lps) * world, "seconds": elapsed,
+        "workers_per_gpu": args.c3_workers,
+        "iterations": int(sum(r.iterations for r in res)),
+        "optimal": int(sum(s == abi.OPTIMAL for s in statuses)),
+        "workload": (f"config 3: {len(lps)} Netlib-shaped seeded LPs (tests/netlib_suite.py, "
+                     f"m 27..{args.c3_max_rows}, 1.5-4 columns per row, all bound types), "
+                     f"primal simplex, Glop defaults, solved from scratch"),
+    }
+    for h in handles:
+        h.close()
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import oracle_lib
+        log("c3: cpu baseline (oracle)")
+
+        def solve_one(lp):
+            o = oracle_lib.OracleLp(p)
+            o.load(lp)
+            return o.solve().iterations
+
+        t = time.perf_counter()
+        with concurrent.futures.ThreadPoolExecutor(args.c3_cpu_threads) as ex:
+            list(ex.map(solve_one, lps))
+        dt = time.perf_counter() - t
+        out["cpu_baseline"] = {
+            "value": len(lps) / dt, "unit": "LPs/s", "cores": args.c3_cpu_threads, "kind": "port",
+            "sample": f"oracle, {args.c3_cpu_threads} threads, the same {len(lps)} LPs"}
+    return out
+
+
 def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     """Config 4: children of one CP-SAT-style search node,
     sharded across ranks (each rank its own children, weak scaling), solved
@@ -240,6 +298,10 @@ def main():
     ap.add_argument("--batch-machines", type=int, default=10)
     ap.add_argument("--batch-cpu-lps", type=int, default=512)
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 section")
+    ap.add_argument("--no-c3", action="store_true", help="skip the config-3 section")
+    ap.add_argument("--c3-max-rows", type=int, default=1000)
+    ap.add_argument("--c3-workers", type=int, default=8)
+    ap.add_argument("--c3-cpu-threads", type=int, default=8)
     ap.add_argument("--c5-m", type=int, default=100000)
     ap.add_argument("--c5-n", type=int, default=1000000)
     ap.add_argument("--c5-warmup", type=int, default=20000)
@@ -320,6 +382,11 @@ def main():
         log(f"config-5 section: {args.c5_m}x{args.c5_n}")
         c5 = run_c5(args, rank, world, local_rank, dist, barrier, sync)
         log(f"c5: {c5['value']:.1f} iterations/s")
+    c3 = None
+    if not args.no_c3:
+        log("config-3 section: Netlib-shaped suite")
+        c3 = run_c3(args, rank, world, local_rank, dist, barrier, sync)
+        log(f"c3: {c3['value']:.1f} LPs/s")
     batched = None
     if args.batch_lps > 0:
         log(f"batched section: {args.batch_lps} children per GPU")
@@ -364,6 +431,7 @@ def main():
                                   / max(1, done), 3),
         "cpu_baseline": cpu,
         "c5": c5,
+        "c3": c3,
         "batched": batched,
     }
     print(json.dumps(line), flush=True)

@@ -97,6 +97,7 @@ class DeviceLp {
   void BeginKernel(int id);
   void EndKernel(int id, double bytes);
   void Compact(int n);  // flags_ -> list_ (ascending) + coefficients, async
+  void AccountList(const std::vector<int>& positions);
   void BuildDenseBlock();
   // Launches the CSC kernel over the sparse columns (all columns when there is
   // no dense block) and the dense-block kernel; mode as in column_dot.
@@ -187,6 +188,15 @@ class DeviceLp {
   double* h_pin_w_ = nullptr;
   int* h_pin_count_ = nullptr;
   int last_list_len_ = 0;
+  // Mapped host memory written by the small-N compaction kernel.
+  void* h_map_ = nullptr;
+  int* h_map_count_ = nullptr;
+  int32_t* h_map_list_ = nullptr;
+  double* h_map_vals_ = nullptr;
+  int* d_map_count_ = nullptr;
+  int32_t* d_map_list_ = nullptr;
+  double* d_map_vals_ = nullptr;
+  bool mapped_result_ = false;  // the last Compact wrote to h_map_
 };
 
 }  // namespace milp

@@ -47,6 +47,7 @@ DeviceLp::~DeviceLp() {
   if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
   if (h_pin_w_) (void)hipHostFree(h_pin_w_);
   if (h_pin_count_) (void)hipHostFree(h_pin_count_);
+  if (h_map_) (void)hipHostFree(h_map_);
   for (int k = 0; k < kNumMasks; ++k) {
     if (h_pin_mask_[k]) (void)hipHostFree(h_pin_mask_[k]);
     if (ev_mask_[k]) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_mask_[k]));
@@ -202,6 +203,29 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   if (h_pin_count_ == nullptr) {
     Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_count_), sizeof(int)), "pin");
   }
+  // Mapped host buffer for the small-N compaction result: count, list, values.
+  if (h_map_ != nullptr) (void)hipHostFree(h_map_);
+  h_map_ = nullptr;
+  d_map_count_ = nullptr;
+  d_map_list_ = nullptr;
+  d_map_vals_ = nullptr;
+  if (n_total_ <= milp_launch::kSmallCompactMax) {
+    const size_t list_off = 64;
+    const size_t vals_off = (list_off + size_t(n_total_) * sizeof(int32_t) + 63) / 64 * 64;
+    const size_t bytes = vals_off + size_t(n_total_) * sizeof(double);
+    Check(hipHostMalloc(&h_map_, bytes, hipHostMallocMapped), "mapped");
+    char* base = static_cast<char*>(h_map_);
+    h_map_count_ = reinterpret_cast<int*>(base);
+    h_map_list_ = reinterpret_cast<int32_t*>(base + list_off);
+    h_map_vals_ = reinterpret_cast<double*>(base + vals_off);
+    void* dev = nullptr;
+    Check(hipHostGetDevicePointer(&dev, h_map_, 0), "mapped pointer");
+    char* dbase = static_cast<char*>(dev);
+    d_map_count_ = reinterpret_cast<int*>(dbase);
+    d_map_list_ = reinterpret_cast<int32_t*>(dbase + list_off);
+    d_map_vals_ = reinterpret_cast<double*>(dbase + vals_off);
+  }
+  mapped_result_ = false;
   list_count_ = 0;
   last_list_len_ = 0;
   ++list_epoch_;
@@ -316,9 +340,11 @@ void DeviceLp::SetMask(Mask which, const uint64_t* words, int num_words) {
 void DeviceLp::Compact(int n) {
   if (n <= milp_launch::kSmallCompactMax) {
     // One workgroup: flags -> list + coefficients + count in a single launch.
+    // The result also lands in mapped host memory: the readback is the sync.
     Check(milp_launch::compact_small(d_flags_, n, d_coeff_, d_list_, d_out_list_, d_count_,
-                                     S(stream_)),
+                                     d_map_list_, d_map_vals_, d_map_count_, S(stream_)),
           "compact small");
+    mapped_result_ = true;
   } else {
     size_t bytes = cub_temp_bytes_;
     Check(hipcub::DeviceSelect::Flagged(d_cub_temp_, bytes,
@@ -327,6 +353,7 @@ void DeviceLp::Compact(int n) {
           "cub flagged");
     Check(milp_launch::gather_counted(d_list_, d_count_, n, d_coeff_, d_out_list_, S(stream_)),
           "gather");
+    mapped_result_ = false;
   }
   list_count_ = -1;  // known after FetchUpdateRow
   ++list_epoch_;
@@ -430,6 +457,17 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
 
 void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* values) {
   CallTimer timer(&stats_, MI_K_READBACK);
+  if (mapped_result_) {
+    Synchronize();
+    const int n = *h_map_count_;
+    if (n < 0 || n > n_total_) throw DeviceError("bad update-row count");
+    list_count_ = n;
+    last_list_len_ = n;
+    positions->assign(h_map_list_, h_map_list_ + n);
+    values->assign(h_map_vals_, h_map_vals_ + n);
+    AccountList(*positions);
+    return;
+  }
   // Count, and a prefix of the list sized from the previous update row, in
   // one round trip; the rest (if any) in a second one.
   const int cap = std::min<int64_t>(
@@ -452,13 +490,18 @@ void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* 
   last_list_len_ = n;
   positions->resize(n);
   values->resize(n);
+  if (n > 0) {
+    std::memcpy(positions->data(), h_pin_i_, n * sizeof(int32_t));
+    std::memcpy(values->data(), h_pin_d_, n * sizeof(double));
+  }
+  AccountList(*positions);
+}
+
+// Byte accounting of the listed columns (ListDotsOverUpdateRow).
+void DeviceLp::AccountList(const std::vector<int>& positions) {
   list_entries_ = 0;
   list_dense_ = 0;
-  if (n == 0) return;
-  std::memcpy(positions->data(), h_pin_i_, n * sizeof(int32_t));
-  std::memcpy(values->data(), h_pin_d_, n * sizeof(double));
-  for (int i = 0; i < n; ++i) {
-    const int c = (*positions)[i];
+  for (const int c : positions) {
     if (!h_is_dense_.empty() && h_is_dense_[c]) {
       ++list_dense_;
     } else {

@@ -68,12 +68,15 @@ struct PhaseClock {
 // Finer split inside the phases (same switch): wall time of named sections.
 enum SubPhase {
   kSubBtranY, kSubPricingCall, kSubCandidatesFull, kSubGetMaximum, kSubBtranW,
-  kSubUpdateRowCall, kSubNormLoop, kSubQueue, kSubLuUpdate, kSubRefactorize, kNumSubPhases
+  kSubUpdateRowCall, kSubNormLoop, kSubQueue, kSubLuUpdate, kSubRefactorize,
+  kSubBoxedScan, kSubFlipFtran, kSubRecomputeValues, kSubDualPrices, kSubFtranDirection,
+  kSubTau, kNumSubPhases
 };
 const char* const kSubPhaseNames[kNumSubPhases] = {
     "btran y (c_B B^-1)", "pricing device call", "prices full rebuild", "GetMaximum",
     "btran w (B^-T d)",   "update-row device",   "norm update loop",    "price queue/replay",
-    "basis update (MPF)", "refactorize (LU)"};
+    "basis update (MPF)", "refactorize (LU)", "boxed dual-feas scan", "flip update (FTRAN)",
+    "recompute x_B",      "dual prices",       "ftran direction",   "tau ftran"};
 double g_sub_ms[kNumSubPhases] = {};
 const bool g_sub_on = std::getenv("MILP_PHASE_TIMING") != nullptr;
 struct SubTimer {
@@ -542,6 +545,7 @@ class DualEdgeNorms {
                               const ScatteredVector& direction,
                               const ScatteredVector& rho) {
     if (recompute_) return;
+    SubTimer tau_timer(kSubTau);
     const std::vector<Fractional>& tau = bf_.RightSolveForTau(rho);
     const Fractional pivot = direction[leaving_row];
     const Fractional new_leaving_squared_norm = norms_[leaving_row] / Square(pivot);
@@ -1947,6 +1951,7 @@ void VariableValues::ResetAllNonBasicVariableValues(const std::vector<Fractional
 
 // variable_values.cc:101-118
 void VariableValues::RecomputeBasicVariableValues() {
+  SubTimer timer(kSubRecomputeValues);
   const int num_rows = matrix_.num_rows();
   scratchpad_.non_zeros.clear();
   // -sum over non-basic columns of x_j a_j, per row in column order (GPU).
@@ -2019,6 +2024,7 @@ void VariableValues::UpdateGivenNonBasicVariables(const std::vector<int>& cols,
 
 // variable_values.cc:229-262
 void VariableValues::RecomputeDualPrices(bool put_more_importance_on_norm) {
+  SubTimer timer(kSubDualPrices);
   const int num_rows = matrix_.num_rows();
   dual_prices_->ClearAndResize(num_rows);
   dual_prices_->StartDenseUpdates();
@@ -3061,6 +3067,7 @@ void RevisedSimplex::ComputeVariableValuesError() {
 
 // revised_simplex.cc:1695-1720
 void RevisedSimplex::ComputeDirection(int col) {
+  SubTimer timer(kSubFtranDirection);
   basis_factorization_.RightSolveForProblemColumn(col, &direction_);
   direction_infinity_norm_ = 0.0;
   if (direction_.non_zeros.empty()) {
@@ -3439,6 +3446,7 @@ Status RevisedSimplex::DualPhaseIChooseLeavingVariableRow(int* leaving_row,
 // revised_simplex.cc:2390-2437
 void RevisedSimplex::MakeBoxedVariableDualFeasible(const std::vector<int>& cols,
                                                    bool update_basic_values) {
+  SubTimer timer(kSubBoxedScan);
   std::vector<int> changed_cols;
   const Fractional threshold = reduced_costs_.GetDualFeasibilityTolerance();
   const std::vector<Fractional>& reduced_costs = reduced_costs_.GetReducedCosts();
@@ -3455,6 +3463,7 @@ void RevisedSimplex::MakeBoxedVariableDualFeasible(const std::vector<int>& cols,
     }
   }
   if (!changed_cols.empty()) {
+    SubTimer flip_timer(kSubFlipFtran);
     variable_values_.UpdateGivenNonBasicVariables(changed_cols, update_basic_values);
   }
 }

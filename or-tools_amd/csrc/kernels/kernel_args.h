@@ -111,8 +111,10 @@ hipError_t gather_counted(const int32_t* list, const int* count, int n, const do
 // Flags -> ascending list + coefficient gather + count, one workgroup, for
 // n <= kSmallCompactMax.
 constexpr int kSmallCompactMax = 1 << 17;
+// host_* (optional, device-visible mapped host memory) receive a copy.
 hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32_t* list,
-                         double* vals, int* count, hipStream_t s);
+                         double* vals, int* count, int32_t* host_list, double* host_vals,
+                         int* host_count, hipStream_t s);
 hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s);
 // Marks the filtered rows (row_tag[r] = tag, row_pos[r] = list position).
 hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag,

@@ -317,7 +317,8 @@ __global__ void gather_counted_kernel(const int32_t* list, const int* count, con
 // ascending position order, as hipcub's select would produce it.
 constexpr int kCompactThreads = 1024;
 __global__ __launch_bounds__(kCompactThreads) void compact_small_kernel(
-    const uint8_t* flags, int n, const double* coeff, int32_t* list, double* vals, int* count) {
+    const uint8_t* flags, int n, const double* coeff, int32_t* list, double* vals, int* count,
+    int32_t* host_list, double* host_vals, int* host_count) {
   __shared__ int sums[kCompactThreads];
   const int t = threadIdx.x;
   const int per = (n + kCompactThreads - 1) / kCompactThreads;
@@ -336,12 +337,20 @@ __global__ __launch_bounds__(kCompactThreads) void compact_small_kernel(
   int pos = sums[t] - c;
   for (int i = b; i < e; ++i) {
     if (flags[i] != 0) {
+      const double v = coeff[i];
       list[pos] = i;
-      vals[pos] = coeff[i];
+      vals[pos] = v;
+      if (host_list != nullptr) {  // zero-copy readback into mapped host memory
+        host_list[pos] = i;
+        host_vals[pos] = v;
+      }
       ++pos;
     }
   }
-  if (t == kCompactThreads - 1) *count = sums[t];
+  if (t == kCompactThreads - 1) {
+    *count = sums[t];
+    if (host_count != nullptr) *host_count = sums[t];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -645,9 +654,11 @@ hipError_t gather_counted(const int32_t* list, const int* count, int n, const do
 }
 
 hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32_t* list,
-                         double* vals, int* count, hipStream_t s) {
+                         double* vals, int* count, int32_t* host_list, double* host_vals,
+                         int* host_count, hipStream_t s) {
   if (n > kSmallCompactMax) return hipErrorInvalidValue;
-  compact_small_kernel<<<1, kCompactThreads, 0, s>>>(flags, n, coeff, list, vals, count);
+  compact_small_kernel<<<1, kCompactThreads, 0, s>>>(flags, n, coeff, list, vals, count,
+                                                     host_list, host_vals, host_count);
   return hipGetLastError();
 }
 

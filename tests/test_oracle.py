@@ -133,3 +133,21 @@ def test_oracle_batched_children_match_sequential():
         r = o.solve()
         assert (res[i].problem_status, res[i].iterations, res[i].objective) == \
             (r.problem_status, r.iterations, r.objective)
+
+
+def test_netlib_suite_shapes_and_oracle_on_smallest():
+    """Config-3 stand-in suite: 94 deterministic LPs from 27 rows up; the
+    smallest members solve to OPTIMAL on the oracle and agree with HiGHS."""
+    import netlib_suite
+    shapes = netlib_suite.suite_shapes(max_rows=1000)
+    assert len(shapes) == 94
+    assert shapes[0][0] == 27 and shapes[-1][0] == 1000
+    assert shapes == netlib_suite.suite_shapes(max_rows=1000)  # deterministic
+    lps = netlib_suite.suite(count=94, max_rows=1000)[:6]
+    for lp in lps:
+        o = oracle_lib.OracleLp(abi.default_params())
+        o.load(lp)
+        r = o.solve()
+        assert r.problem_status == abi.OPTIMAL
+        st, val = lp_gen.to_scipy(lp)
+        assert st == 0 and abs(r.objective - val) <= 1e-6 * max(1.0, abs(val))
