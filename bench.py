@@ -136,7 +136,7 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
         "finished_early": bool(fin), "setup_and_warmup_s": round(setup, 2),
         "workload": (f"config 5: sparse {args.c5_m}x{args.c5_n}, 10 nnz/column "
                      f"(nnz={int(lp.nnz)}), dual simplex, dual steepest edge, Glop defaults"),
-        "roofline": kernel_roofline(stats),
+        "roofline": kernel_roofline(stats, args.c5_traffic_json),
         "kernels": kernel_table(stats),
         "kernel_window": [args.c5_warmup + done, args.c5_warmup + 2 * done],
     }
@@ -307,8 +307,11 @@ def main():
     ap.add_argument("--c5-warmup", type=int, default=20000)
     ap.add_argument("--c5-steps", type=int, default=1000)
     ap.add_argument("--c5-cpu-steps", type=int, default=300)
+    ap.add_argument("--c5-traffic-json",
+                    default=os.path.join(REPO, "profiles", "traffic_c5.json"),
+                    help="per-launch HBM bytes of the config-5 kernels (profiles/)")
     ap.add_argument("--traffic-json",
-                    default=os.path.join(REPO, "profiles", "traffic_latest.json"),
+                    default=os.path.join(REPO, "profiles", "traffic_c2.json"),
                     help="per-launch HBM bytes of the dominant kernel from a "
                          "separate rocprofv3 --pmc pass (profiles/)")
     args = ap.parse_args()

@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
+timeout -k 10 300 python -u scripts/probe_batch.py --lps 128 --workers 1 4 8 > gpurun_out/probe_batch.json 2> gpurun_out/probe_batch.err || { echo "batch probe failed"; tail -20 gpurun_out/probe_batch.err; exit 1; }
+cat gpurun_out/probe_batch.json
+MILP_PHASE_TIMING=1 MILP_PHASE_TIMING_EVERY=1000 timeout -k 10 600 python -u scripts/probe.py --config c5 --m 100000 --n 1000000 --warmup 20000 --steps 1000 > gpurun_out/probe_c5.json 2> gpurun_out/probe_c5.err || { echo "c5 probe failed"; tail -30 gpurun_out/probe_c5.err; exit 1; }
+cat gpurun_out/probe_c5.json
+MILP_PHASE_TIMING=1 timeout -k 10 600 python -u scripts/probe.py --config c2 --steps 20 > gpurun_out/probe_c2.json 2> gpurun_out/probe_c2.err || { echo "c2 probe failed"; tail -30 gpurun_out/probe_c2.err; exit 1; }
+cat gpurun_out/probe_c2.json

@@ -7,7 +7,8 @@ WRITE_SIZE passes, each its own run) into profiles/<tag>/:
 
 FETCH_SIZE / WRITE_SIZE are in KiB. On gfx950 FETCH_SIZE reports half of
 the bytes of a streaming read (MI355X_MICROARCH.md, HBM section); it is
-doubled here. Usage: python scripts/profile_summary.py gpurun_out/prof <tag>
+doubled here. Usage: python scripts/profile_summary.py gpurun_out/prof <tag> [c2|c5]
+(writes profiles/<tag>/ and profiles/traffic_<c2|c5>.json for bench.py)
 """
 import collections
 import csv
@@ -17,11 +18,13 @@ import shutil
 import sys
 
 GROUPS = {  # HIP kernel name fragment -> engine kernel id (bench.py names)
-    "dense_dot_kernel<1>": "pricing", "column_dot_kernel<1,": "pricing",
-    "dense_dot_kernel<0>": "update_row", "column_dot_kernel<0,": "update_row",
-    "dense_dot_kernel<4>": "update_row", "column_dot_kernel<4,": "update_row",
-    "row_wise_update_kernel": "update_row",
-    "dense_dot_kernel<2>": "primal_norms", "column_dot_kernel<2,": "primal_norms",
+    "dense_dot_kernel<1,": "pricing", "column_dot_kernel<1,": "pricing",
+    "dense_dot_kernel<5,": "pricing", "column_dot_kernel<5,": "pricing",
+    "dense_dot_kernel<0,": "update_row", "column_dot_kernel<0,": "update_row",
+    "dense_dot_kernel<4,": "update_row", "column_dot_kernel<4,": "update_row",
+    "row_wise_update_kernel": "update_row", "row_wise_by_column_kernel": "update_row",
+    "tag_rows_kernel": "update_row",
+    "dense_dot_kernel<2,": "primal_norms", "column_dot_kernel<2,": "primal_norms",
     "row_sum_kernel": "spmv_rows", "column_squared_norm_kernel": "col_norms",
 }
 
@@ -33,7 +36,7 @@ def group_of(name):
     return None
 
 
-def main(src, tag):
+def main(src, tag, workload):
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                        "profiles", tag)
     os.makedirs(out, exist_ok=True)
@@ -76,7 +79,7 @@ def main(src, tag):
                    "launches": v[3]} for g, v in groups.items()}
     json.dump(traffic, open(os.path.join(out, "traffic.json"), "w"), indent=1)
     latest = dict(traffic, _source=f"profiles/{tag}")
-    json.dump(latest, open(os.path.join(os.path.dirname(out), "traffic_latest.json"), "w"),
+    json.dump(latest, open(os.path.join(os.path.dirname(out), f"traffic_{workload}.json"), "w"),
               indent=1)
     lines += ["", "Per engine kernel id (bytes per logical launch, all HIP kernels of the id):", ""]
     for g, v in traffic.items():
@@ -87,4 +90,4 @@ def main(src, tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "c2")
