@@ -110,7 +110,7 @@ hipError_t gather_counted(const int32_t* list, const int* count, int n, const do
                           double* dst, hipStream_t s);
 // Flags -> ascending list + coefficient gather + count, one workgroup, for
 // n <= kSmallCompactMax.
-constexpr int kSmallCompactMax = 1 << 17;
+constexpr int kSmallCompactMax = 1 << 14;  // one workgroup writes the list to host memory
 // host_* (optional, device-visible mapped host memory) receive a copy.
 hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32_t* list,
                          double* vals, int* count, int32_t* host_list, double* host_vals,

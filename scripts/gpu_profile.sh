@@ -23,4 +23,11 @@ for W in ${WORKLOADS:-c2 c5}; do
   timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -f csv -d $P/write -o run -- $CMD > $P/write.log 2>&1 || { echo "$W write failed"; tail -20 $P/write.log; exit 1; }
   echo "$W write done $(date +%T)"
 done
-find $OUT/prof_c2 $OUT/prof_c5 -name "*.csv" 2>/dev/null | head -20
+# Summaries come back under gpurun_out/profiles/ (the raw traces exceed the
+# 64 MiB merge limit and are deleted here).
+for W in ${WORKLOADS:-c2 c5}; do
+  PROFILE_OUT_ROOT=$OUT/profiles python3 $R/scripts/profile_summary.py $OUT/prof_$W ${TAG:-r01}_$W $W > /dev/null || { echo "summary $W failed"; exit 1; }
+  cp $OUT/prof_$W/*.log $OUT/profiles/${TAG:-r01}_$W/ 2>/dev/null
+  rm -rf $OUT/prof_$W
+done
+ls -R $OUT/profiles

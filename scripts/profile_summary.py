@@ -37,8 +37,9 @@ def group_of(name):
 
 
 def main(src, tag, workload):
-    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                       "profiles", tag)
+    root = os.environ.get("PROFILE_OUT_ROOT") or os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
+    out = os.path.join(root, tag)
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(out, "kernel_stats.csv"))
