@@ -1496,10 +1496,10 @@ class PrimalPrices {
     SubTimer timer(kSubGetMaximum);
     return prices_.GetMaximum();
   }
-  void UpdateBeforeBasisPivot(int /*entering_col*/, UpdateRow* update_row) {
+  void UpdateBeforeBasisPivot(int entering_col, UpdateRow* update_row) {
     if (recompute_) return;
     if (primal_edge_norms_->HasPendingUpdate()) {
-      QueueEnteringCandidates(update_row->GetNonZeroPositions());
+      QueueEnteringCandidates(entering_col, *update_row);
       return;
     }
     UpdateEnteringCandidates<false>(update_row->GetNonZeroPositions());
@@ -1509,7 +1509,7 @@ class PrimalPrices {
     if (primal_edge_norms_->HasPendingUpdate()) {
       const bool valid = reduced_costs_->IsValidPrimalEnteringCandidate(col);
       if (valid) reduced_costs_->GetReducedCosts();  // its side effects happen now
-      queue_.push_back(QueuedOp{col, valid});
+      queue_.push_back(QueuedOp{col, valid ? kAdd : kRemove});
       return;
     }
     if (reduced_costs_->IsValidPrimalEnteringCandidate(col)) {
@@ -1523,7 +1523,7 @@ class PrimalPrices {
   void SetAndDebugCheckThatColumnIsDualFeasible(int col) {
     if (recompute_) return;
     if (primal_edge_norms_->HasPendingUpdate()) {
-      queue_.push_back(QueuedOp{col, false});
+      queue_.push_back(QueuedOp{col, kRemove});
       return;
     }
     prices_.Remove(col);
@@ -1531,50 +1531,80 @@ class PrimalPrices {
   void ForceRecomputation() { recompute_ = true; }
 
  private:
-  // A price update issued while the edge-norm update is parked: the
-  // candidate test is done at issue time (it does not read the norms); the
-  // price rc^2 / norm is computed at replay, before any reduced cost changes.
+  // Price updates issued while the edge-norm update is parked, replayed in
+  // order once the norms are complete and before any reduced cost changes.
+  // A single-column op has its candidate test done at issue time. The
+  // update-row block (UpdateEnteringCandidates<false> over the listed
+  // positions) is re-evaluated at replay from the live state: until then the
+  // reduced costs of those positions, the tolerance and the can-increase /
+  // can-decrease bits do not change, except the bits of the entering column
+  // (UpdateBasis), whose decision is taken at issue time.
+  enum OpKind : int8_t { kRemove = 0, kAdd = 1, kUpdateRowBlock = 2 };
   struct QueuedOp {
     int col;
-    bool add;  // AddOrUpdate(col, price) if true, Remove(col) otherwise
+    OpKind kind;
   };
-  void QueueEnteringCandidates(const std::vector<int>& cols) {
+  bool IsDualInfeasible(int col, Fractional reduced_cost, Fractional tolerance) const {
+    return ((reduced_cost > tolerance) && variables_info_.GetCanDecreaseBitRow().IsSet(col)) !=
+           ((reduced_cost < -tolerance) && variables_info_.GetCanIncreaseBitRow().IsSet(col));
+  }
+  void QueueEnteringCandidates(int entering_col, const UpdateRow& update_row) {
     SubTimer timer(kSubQueue);
-    const Fractional tolerance = reduced_costs_->GetDualFeasibilityTolerance();
-    const Bitset& dec = variables_info_.GetCanDecreaseBitRow();
-    const Bitset& inc = variables_info_.GetCanIncreaseBitRow();
+    block_tolerance_ = reduced_costs_->GetDualFeasibilityTolerance();
     const std::vector<Fractional>& rc = reduced_costs_->GetReducedCosts();
-    for (const int col : cols) {
-      const Fractional reduced_cost = rc[col];
-      const bool is_dual_infeasible =
-          ((reduced_cost > tolerance) && dec.IsSet(col)) !=
-          ((reduced_cost < -tolerance) && inc.IsSet(col));
-      queue_.push_back(QueuedOp{col, is_dual_infeasible});
-    }
+    block_row_ = &update_row;
+    block_epoch_ = update_row.epoch();
+    block_entering_col_ = entering_col;
+    block_entering_infeasible_ = IsDualInfeasible(entering_col, rc[entering_col],
+                                                  block_tolerance_);
+    queue_.push_back(QueuedOp{entering_col, kUpdateRowBlock});
   }
   void ReplayQueue() {
     SubTimer timer(kSubQueue);
     const std::vector<Fractional>& sn = primal_edge_norms_->RawEdgeNorms();
     const std::vector<Fractional>& rc = reduced_costs_->RawReducedCosts();
-    if (recompute_) {
-      // The prices are rebuilt from scratch before anything reads them
-      // (every reader checks recompute_ first, GetBestEnteringColumn clears
-      // them): of the queued updates only the top-k draws from the RNG
-      // matter.
-      for (const QueuedOp& op : queue_) {
-        if (op.add) prices_.AddOrUpdateBeforeClear(op.col, Square(rc[op.col]) / sn[op.col]);
-      }
-    } else {
-      for (const QueuedOp& op : queue_) {
-        if (op.add) {
-          prices_.AddOrUpdate(op.col, Square(rc[op.col]) / sn[op.col]);
-        } else {
-          prices_.Remove(op.col);
+    // When the prices are about to be rebuilt from scratch (every reader
+    // checks recompute_ first, GetBestEnteringColumn clears them), only the
+    // top-k bookkeeping matters: it may draw from the RNG.
+    const bool before_clear = recompute_;
+    for (const QueuedOp& op : queue_) {
+      if (op.kind == kUpdateRowBlock) {
+        if (block_row_->epoch() != block_epoch_) {
+          throw DeviceError("update row recomputed under queued price updates");
         }
+        for (const int col : block_row_->GetNonZeroPositions()) {
+          const bool add = col == block_entering_col_
+                               ? block_entering_infeasible_
+                               : IsDualInfeasible(col, rc[col], block_tolerance_);
+          if (add) {
+            const Fractional price = Square(rc[col]) / sn[col];
+            if (before_clear) {
+              prices_.AddOrUpdateBeforeClear(col, price);
+            } else {
+              prices_.AddOrUpdate(col, price);
+            }
+          } else if (!before_clear) {
+            prices_.Remove(col);
+          }
+        }
+      } else if (op.kind == kAdd) {
+        const Fractional price = Square(rc[op.col]) / sn[op.col];
+        if (before_clear) {
+          prices_.AddOrUpdateBeforeClear(op.col, price);
+        } else {
+          prices_.AddOrUpdate(op.col, price);
+        }
+      } else if (!before_clear) {
+        prices_.Remove(op.col);
       }
     }
     queue_.clear();
   }
+  const UpdateRow* block_row_ = nullptr;
+  uint64_t block_epoch_ = 0;
+  int block_entering_col_ = -1;
+  bool block_entering_infeasible_ = false;
+  Fractional block_tolerance_ = 0.0;
   std::vector<QueuedOp> queue_;
   // UpdateEnteringCandidates<from_clean_state=true> over the relevant
   // columns (reduced_costs.cc:557-600), walking the bitset words directly.

@@ -29,6 +29,21 @@ GROUPS = {  # HIP kernel name fragment -> engine kernel id (bench.py names)
 }
 
 
+# Kernels that define one logical launch of an engine id (the first list
+# that has calls is used): e.g. a pricing pass is one dense-block launch plus
+# one CSC launch over the remaining columns.
+PRIMARY = {
+    "pricing": [["dense_dot_kernel<5,", "dense_dot_kernel<1,"],
+                ["column_dot_kernel<5,", "column_dot_kernel<1,"]],
+    "update_row": [["row_wise_update_kernel", "row_wise_by_column_kernel",
+                    "dense_dot_kernel<0,", "dense_dot_kernel<4,"],
+                   ["column_dot_kernel<0,", "column_dot_kernel<4,"]],
+    "primal_norms": [["dense_dot_kernel<2,"], ["column_dot_kernel<2,"]],
+    "spmv_rows": [["row_sum_kernel"]],
+    "col_norms": [["column_squared_norm_kernel"]],
+}
+
+
 def group_of(name):
     for frag, g in GROUPS.items():
         if frag in name:
@@ -61,6 +76,7 @@ def main(src, tag, workload):
              "| kernel | calls | avg us | HBM read MB/launch (FETCH_SIZE x2) | write MB/launch |",
              "|---|---|---|---|---|"]
     groups = collections.defaultdict(lambda: [0.0, 0.0, None, 0])  # bytes, ns, anchor, calls
+    primary_calls = collections.defaultdict(lambda: collections.defaultdict(int))
     for s in stats:
         name = s["Name"]
         c = counters.get(name, {})
@@ -76,8 +92,18 @@ def main(src, tag, workload):
             gg[0] += (c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0))
             if gg[2] is None or total_ns > gg[1]:
                 gg[1], gg[2], gg[3] = total_ns, name, calls.get(name, int(s["Calls"]))
-    traffic = {g: {"traffic_bytes_per_launch": v[0] / max(1, v[3]), "anchor_kernel": v[2],
-                   "launches": v[3]} for g, v in groups.items()}
+            for level, frags in enumerate(PRIMARY.get(g, [])):
+                if any(f in name for f in frags):
+                    primary_calls[g][level] += calls.get(name, int(s["Calls"]))
+    def logical_launches(g, v):
+        for level in sorted(primary_calls[g]):
+            if primary_calls[g][level] > 0:
+                return primary_calls[g][level]
+        return v[3]
+
+    traffic = {g: {"traffic_bytes_per_launch": v[0] / max(1, logical_launches(g, v)),
+                   "anchor_kernel": v[2], "launches": logical_launches(g, v)}
+               for g, v in groups.items()}
     json.dump(traffic, open(os.path.join(out, "traffic.json"), "w"), indent=1)
     latest = dict(traffic, _source=f"profiles/{tag}")
     json.dump(latest, open(os.path.join(os.path.dirname(out), f"traffic_{workload}.json"), "w"),
