@@ -82,6 +82,34 @@ class DeviceLp {
   void RowSums(const std::vector<double>& x, bool skip_basic, double sign,
                std::vector<double>* out);
 
+  // --- dual device mode: device-resident reduced costs ------------------
+  // (see simplex.cc RevisedSimplex::DualDeviceMode). colbits: one byte per
+  // column (kernel_args.h kCol*), bound_diff: upper - lower per column.
+  void DualBegin(const std::vector<double>& rc, const std::vector<uint8_t>& colbits,
+                 const std::vector<double>& bound_diff);
+  void DualSetColBits(const std::vector<int32_t>& cols, const std::vector<uint8_t>& bits);
+  // The reduced costs of the last Pricing() call become the device copy.
+  void DualTakePricedReducedCosts();
+  void DualDownloadReducedCosts(std::vector<double>* rc);
+  void DualSetReducedCost(int col, double value);
+  struct DualCandidates {
+    std::vector<int> col;
+    std::vector<double> coeff;  // update-row coefficient
+    std::vector<double> rc;
+    int list_count = 0;         // update-row positions
+  };
+  // entering_variable.cc:37-130 filter over the last update row.
+  void DualRatioCandidates(double sign, double threshold, double harris_tolerance,
+                           double minimum_delta, double variation_magnitude,
+                           DualCandidates* out);
+  // reduced_costs.cc:444-488 over the last update row.
+  void DualUpdateReducedCosts(double mult, int leaving_col, double leaving_value,
+                              int entering_col);
+  // revised_simplex.cc:2391-2437 decisions; cols == nullptr: every non-basic
+  // boxed column. flags[i] = 1 if (cols ? cols[i] : i) flips.
+  void DualBoxedFlips(const std::vector<int>* cols, double threshold,
+                      std::vector<uint8_t>* flags);
+
   // Accounting (roofline): launches, algorithmic bytes, HIP-event time.
   void SetTiming(bool on) { timing_ = on; }
   const mi_lp_kernel_stats& stats() const { return stats_; }
@@ -197,6 +225,30 @@ class DeviceLp {
   int32_t* d_map_list_ = nullptr;
   double* d_map_vals_ = nullptr;
   bool mapped_result_ = false;  // the last Compact wrote to h_map_
+  // dual device mode
+  bool dual_ready_ = false;
+  double* d_rc_ = nullptr;
+  uint8_t* d_colbits_ = nullptr;
+  double* d_bound_diff_ = nullptr;
+  unsigned long long* d_best_ = nullptr;
+  uint8_t* d_slot_flags_ = nullptr;
+  int32_t* d_slots_ = nullptr;
+  int* d_num_slots_ = nullptr;
+  int32_t* d_cand_col_ = nullptr;
+  double* d_cand_coeff_ = nullptr;
+  double* d_cand_rc_ = nullptr;
+  int32_t* d_small_cols_ = nullptr;
+  uint8_t* d_small_bits_ = nullptr;
+  int32_t* h_cand_col_ = nullptr;
+  double* h_cand_coeff_ = nullptr;
+  double* h_cand_rc_ = nullptr;
+  int* h_dual_counts_ = nullptr;  // [num candidates, list count]
+  int32_t* h_cb_cols_ = nullptr;  // column-bit changes (pinned, event-guarded)
+  uint8_t* h_cb_bits_ = nullptr;
+  void* ev_cb_ = nullptr;
+  int32_t* h_flip_cols_ = nullptr;
+  uint8_t* h_flip_flags_ = nullptr;
+  int last_candidates_ = 0;
 };
 
 }  // namespace milp

@@ -48,6 +48,13 @@ DeviceLp::~DeviceLp() {
   if (h_pin_w_) (void)hipHostFree(h_pin_w_);
   if (h_pin_count_) (void)hipHostFree(h_pin_count_);
   if (h_map_) (void)hipHostFree(h_map_);
+  for (void* p : {static_cast<void*>(h_cand_col_), static_cast<void*>(h_cand_coeff_),
+                  static_cast<void*>(h_cand_rc_), static_cast<void*>(h_dual_counts_),
+                  static_cast<void*>(h_cb_cols_), static_cast<void*>(h_cb_bits_),
+                  static_cast<void*>(h_flip_cols_), static_cast<void*>(h_flip_flags_)}) {
+    if (p) (void)hipHostFree(p);
+  }
+  if (ev_cb_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_cb_));
   for (int k = 0; k < kNumMasks; ++k) {
     if (h_pin_mask_[k]) (void)hipHostFree(h_pin_mask_[k]);
     if (ev_mask_[k]) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_mask_[k]));
@@ -227,6 +234,7 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   }
   mapped_result_ = false;
   list_count_ = 0;
+  dual_ready_ = false;
   last_list_len_ = 0;
   ++list_epoch_;
   BuildDenseBlock();
@@ -653,6 +661,198 @@ void DeviceLp::RowSums(const std::vector<double>& x, bool skip_basic, double sig
   out->resize(m_);
   Download(h_pin_d_, d_vec_m2_, m_ * sizeof(double));
   std::memcpy(out->data(), h_pin_d_, m_ * sizeof(double));
+}
+
+
+// ---------------------------------------------------------------------------
+// Dual device mode.
+namespace {
+template <typename T>
+void PinnedResize(T** p, size_t n) {
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(p), std::max<size_t>(1, n) * sizeof(T)) !=
+      hipSuccess) {
+    throw DeviceError("hipHostMalloc");
+  }
+}
+}  // namespace
+
+void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_t>& colbits,
+                         const std::vector<double>& bound_diff) {
+  if (!dual_ready_) {
+    d_rc_ = Alloc<double>(n_total_);
+    d_colbits_ = Alloc<uint8_t>(n_total_);
+    d_bound_diff_ = Alloc<double>(n_total_);
+    d_best_ = Alloc<unsigned long long>(1);
+    d_slot_flags_ = Alloc<uint8_t>(n_total_);
+    d_slots_ = Alloc<int32_t>(n_total_);
+    d_num_slots_ = Alloc<int>(1);
+    d_cand_col_ = Alloc<int32_t>(n_total_);
+    d_cand_coeff_ = Alloc<double>(n_total_);
+    d_cand_rc_ = Alloc<double>(n_total_);
+    d_small_cols_ = Alloc<int32_t>(n_total_);
+    d_small_bits_ = Alloc<uint8_t>(n_total_);
+    Synchronize();  // the pinned buffers below may still feed earlier copies
+    PinnedResize(&h_cand_col_, n_total_);
+    PinnedResize(&h_cand_coeff_, n_total_);
+    PinnedResize(&h_cand_rc_, n_total_);
+    PinnedResize(&h_dual_counts_, 2);
+    PinnedResize(&h_cb_cols_, n_total_);
+    PinnedResize(&h_cb_bits_, n_total_);
+    PinnedResize(&h_flip_cols_, n_total_);
+    PinnedResize(&h_flip_flags_, n_total_);
+    if (ev_cb_ == nullptr) {
+      hipEvent_t e;
+      Check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+      ev_cb_ = e;
+    }
+    last_candidates_ = 0;
+    dual_ready_ = true;
+  }
+  if (static_cast<int>(rc.size()) != n_total_ || static_cast<int>(colbits.size()) != n_total_ ||
+      static_cast<int>(bound_diff.size()) != n_total_) {
+    throw DeviceError("dual device mode: size mismatch");
+  }
+  Upload(d_rc_, rc.data(), n_total_ * sizeof(double));
+  Upload(d_colbits_, colbits.data(), n_total_);
+  Upload(d_bound_diff_, bound_diff.data(), n_total_ * sizeof(double));
+  Synchronize();  // pageable sources
+}
+
+void DeviceLp::DualSetColBits(const std::vector<int32_t>& cols,
+                              const std::vector<uint8_t>& bits) {
+  const int n = static_cast<int>(cols.size());
+  if (n == 0) return;
+  if (n > n_total_) throw DeviceError("dual device mode: too many column changes");
+  hipEvent_t done = reinterpret_cast<hipEvent_t>(ev_cb_);
+  Check(hipEventSynchronize(done), "colbits event");
+  std::memcpy(h_cb_cols_, cols.data(), n * sizeof(int32_t));
+  std::memcpy(h_cb_bits_, bits.data(), n);
+  Upload(d_small_cols_, h_cb_cols_, n * sizeof(int32_t));
+  Upload(d_small_bits_, h_cb_bits_, n);
+  Check(milp_launch::set_colbits(d_small_cols_, d_small_bits_, n, d_colbits_, S(stream_)),
+        "colbits");
+  Check(hipEventRecord(done, S(stream_)), "colbits event");
+}
+
+void DeviceLp::DualTakePricedReducedCosts() {
+  Check(hipMemcpyAsync(d_rc_, d_out_n_, n_total_ * sizeof(double), hipMemcpyDeviceToDevice,
+                       S(stream_)),
+        "D2D");
+}
+
+void DeviceLp::DualDownloadReducedCosts(std::vector<double>* rc) {
+  CallTimer timer(&stats_, MI_K_READBACK);
+  rc->resize(n_total_);
+  Download(h_pin_d_, d_rc_, n_total_ * sizeof(double));
+  std::memcpy(rc->data(), h_pin_d_, n_total_ * sizeof(double));
+}
+
+void DeviceLp::DualSetReducedCost(int col, double value) {
+  Check(milp_launch::set_double(d_rc_ + col, value, S(stream_)), "set rc");
+}
+
+void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_tolerance,
+                                   double minimum_delta, double variation_magnitude,
+                                   DualCandidates* out) {
+  CallTimer timer(&stats_, MI_K_DUAL_RATIO);
+  milp_kernels::DualRatioArgs a{};
+  a.list = d_list_;
+  a.list_coeff = d_out_list_;
+  a.count = d_count_;
+  a.max_count = n_total_;
+  a.rc = d_rc_;
+  a.colbits = d_colbits_;
+  a.bound_diff = d_bound_diff_;
+  a.sign = sign;
+  a.threshold = threshold;
+  a.harris_tolerance = harris_tolerance;
+  a.minimum_delta = minimum_delta;
+  a.variation_magnitude = variation_magnitude;
+  a.best = d_best_;
+  a.flags = d_slot_flags_;
+  BeginKernel(MI_K_DUAL_RATIO);
+  Check(hipMemsetAsync(d_best_, 0xff, sizeof(unsigned long long), S(stream_)), "memset");
+  Check(milp_launch::dual_ratio_bound(a, S(stream_)), "dual ratio bound");
+  Check(milp_launch::dual_ratio_flags(a, S(stream_)), "dual ratio flags");
+  size_t bytes = cub_temp_bytes_;
+  Check(hipcub::DeviceSelect::Flagged(d_cub_temp_, bytes,
+                                      hipcub::CountingInputIterator<int32_t>(0), d_slot_flags_,
+                                      d_slots_, d_num_slots_, n_total_, S(stream_)),
+        "cub flagged");
+  Check(milp_launch::gather_candidates(d_slots_, d_num_slots_, n_total_, d_list_, d_out_list_,
+                                       d_rc_, d_cand_col_, d_cand_coeff_, d_cand_rc_,
+                                       S(stream_)),
+        "gather candidates");
+  // Algorithmic bytes: the list (position + coefficient), the reduced cost,
+  // column byte and bound difference of each position, twice; flags.
+  EndKernel(MI_K_DUAL_RATIO, 2.0 * 29.0 * (list_count_ >= 0 ? list_count_ : last_list_len_) +
+                                 2.0 * n_total_);
+  const int cap = std::min<int64_t>(n_total_, std::max<int64_t>(1024, int64_t(last_candidates_) +
+                                                                          last_candidates_ / 4));
+  Check(hipMemcpyAsync(h_dual_counts_, d_num_slots_, sizeof(int), hipMemcpyDeviceToHost,
+                       S(stream_)),
+        "D2H");
+  Check(hipMemcpyAsync(h_dual_counts_ + 1, d_count_, sizeof(int), hipMemcpyDeviceToHost,
+                       S(stream_)),
+        "D2H");
+  Check(hipMemcpyAsync(h_cand_col_, d_cand_col_, cap * sizeof(int32_t), hipMemcpyDeviceToHost,
+                       S(stream_)),
+        "D2H");
+  Check(hipMemcpyAsync(h_cand_coeff_, d_cand_coeff_, cap * sizeof(double),
+                       hipMemcpyDeviceToHost, S(stream_)),
+        "D2H");
+  Download(h_cand_rc_, d_cand_rc_, cap * sizeof(double));
+  const int k = h_dual_counts_[0];
+  const int count = h_dual_counts_[1];
+  if (k < 0 || k > n_total_ || count < 0 || count > n_total_) {
+    throw DeviceError("dual ratio test: bad counts");
+  }
+  if (k > cap) {
+    Check(hipMemcpyAsync(h_cand_col_ + cap, d_cand_col_ + cap, (k - cap) * sizeof(int32_t),
+                         hipMemcpyDeviceToHost, S(stream_)),
+          "D2H");
+    Check(hipMemcpyAsync(h_cand_coeff_ + cap, d_cand_coeff_ + cap, (k - cap) * sizeof(double),
+                         hipMemcpyDeviceToHost, S(stream_)),
+          "D2H");
+    Download(h_cand_rc_ + cap, d_cand_rc_ + cap, (k - cap) * sizeof(double));
+  }
+  last_candidates_ = k;
+  out->col.assign(h_cand_col_, h_cand_col_ + k);
+  out->coeff.assign(h_cand_coeff_, h_cand_coeff_ + k);
+  out->rc.assign(h_cand_rc_, h_cand_rc_ + k);
+  out->list_count = count;
+}
+
+void DeviceLp::DualUpdateReducedCosts(double mult, int leaving_col, double leaving_value,
+                                      int entering_col) {
+  CallTimer timer(&stats_, MI_K_RC_UPDATE);
+  BeginKernel(MI_K_RC_UPDATE);
+  Check(milp_launch::update_reduced_costs(d_list_, d_out_list_, d_count_, n_total_, mult,
+                                          leaving_col, leaving_value, entering_col, d_rc_,
+                                          S(stream_)),
+        "rc update");
+  EndKernel(MI_K_RC_UPDATE, 28.0 * (list_count_ >= 0 ? list_count_ : last_list_len_));
+}
+
+void DeviceLp::DualBoxedFlips(const std::vector<int>* cols, double threshold,
+                              std::vector<uint8_t>* flags) {
+  CallTimer timer(&stats_, MI_K_DUAL_RATIO);
+  const int n = cols != nullptr ? static_cast<int>(cols->size()) : n_total_;
+  flags->assign(n, 0);
+  if (n == 0) return;
+  const int32_t* d_cols = nullptr;
+  if (cols != nullptr) {
+    std::memcpy(h_flip_cols_, cols->data(), n * sizeof(int32_t));
+    Upload(d_slots_, h_flip_cols_, n * sizeof(int32_t));
+    d_cols = d_slots_;
+  }
+  Check(milp_launch::boxed_flips(d_cols, n, d_rc_, d_colbits_, threshold, d_slot_flags_,
+                                 S(stream_)),
+        "boxed flips");
+  Download(h_flip_flags_, d_slot_flags_, n);
+  std::memcpy(flags->data(), h_flip_flags_, n);
 }
 
 }  // namespace milp

@@ -374,6 +374,7 @@ void VariablesInfo::UpdateToBasicStatus(int col) {
     if (upper_bounds_[col] != 0.0) upper_bounds_[col] = +kInfinity;
     variable_type_[col] = ComputeVariableType(col);
   }
+  if (change_log_ != nullptr) change_log_->push_back(col);
   variable_status_[col] = VariableStatus::BASIC;
   is_basic_.Set(col, true);
   not_basic_.Set(col, false);
@@ -384,6 +385,7 @@ void VariablesInfo::UpdateToBasicStatus(int col) {
 }
 
 void VariablesInfo::UpdateToNonBasicStatus(int col, VariableStatus status) {
+  if (change_log_ != nullptr) change_log_->push_back(col);
   variable_status_[col] = status;
   is_basic_.Set(col, false);
   not_basic_.Set(col, true);
@@ -607,10 +609,12 @@ class UpdateRow {
   }
   const std::vector<Fractional>& GetCoefficients() const {
     Materialize();
+    EnsureHost();
     return coefficient_;
   }
   const std::vector<int>& GetNonZeroPositions() const {
     Materialize();
+    EnsureHost();
     return non_zero_position_list_;
   }
   // Listed positions are mirrored on the host; any other position holds
@@ -618,9 +622,20 @@ class UpdateRow {
   // the host loops), so it is read back from the device.
   Fractional GetCoefficient(int col) const {
     Materialize();
+    if (host_stale_ && col == known_col_) return known_value_;
+    EnsureHost();
     if (col < static_cast<int>(listed_.size()) && listed_[col]) return coefficient_[col];
     return dev_->ReadCoefficient(col);
   }
+  // Dual device mode: the update row stays on the device; the host copy is
+  // read back only if host code asks for it. A coefficient the device ratio
+  // test already returned can be registered and served without a readback.
+  void SetLazyFetch(bool on) { lazy_fetch_ = on; }
+  void SetKnownCoefficient(int col, Fractional value) {
+    known_col_ = col;
+    known_value_ = value;
+  }
+  void MaterializeOnDevice() { Materialize(); }
   // The column-wise pass is deferred until its result is first read, so the
   // primal edge-norm update can fuse its a_j . w dots into the same pass over
   // A. Returns true when that fused pass ran now; the dots are then served by
@@ -648,6 +663,21 @@ class UpdateRow {
   void ComputeUpdatesColumnWise();
   void ComputeUpdatesForSingleRow(int row_as_col);
   void FetchFromDevice();
+  void FetchOrDefer() {
+    known_col_ = -1;
+    if (lazy_fetch_) {
+      host_stale_ = true;
+    } else {
+      host_stale_ = false;
+      FetchFromDevice();
+    }
+  }
+  void EnsureHost() const {
+    if (!host_stale_) return;
+    UpdateRow* self = const_cast<UpdateRow*>(this);
+    self->host_stale_ = false;
+    self->FetchFromDevice();
+  }
   void RunColumnWise(const std::vector<Fractional>* w);
 
   const CompactSparseMatrix& matrix_;
@@ -669,6 +699,10 @@ class UpdateRow {
   int64_t num_operations_ = 0;
   int last_algorithm_ = -1;
   uint64_t epoch_ = 0;
+  bool lazy_fetch_ = false;
+  bool host_stale_ = false;
+  int known_col_ = -1;
+  Fractional known_value_ = 0.0;
   // Deferred column-wise pass: the relevance mask and work count it uses are
   // captured when Glop would have run it (update_row.cc:282-306).
   bool pending_column_wise_ = false;
@@ -756,7 +790,7 @@ void UpdateRow::ComputeUpdatesRowWise() {
   dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
                 variables_info_.GetIsRelevantBitRow().NumWords());
   dev_->UpdateRowRowWise(rho_filtered_non_zeros_, rho_.values, 2, params_.drop_tolerance);
-  FetchFromDevice();
+  FetchOrDefer();
 }
 
 // update_row.cc:220-259
@@ -767,7 +801,7 @@ void UpdateRow::ComputeUpdatesRowWiseHypersparse() {
   dev_->SetMask(DeviceLp::kRelevant, variables_info_.GetIsRelevantBitRow().data(),
                 variables_info_.GetIsRelevantBitRow().NumWords());
   dev_->UpdateRowRowWise(rho_filtered_non_zeros_, rho_.values, 1, params_.drop_tolerance);
-  FetchFromDevice();
+  FetchOrDefer();
 }
 
 // update_row.cc:261-280
@@ -779,7 +813,7 @@ void UpdateRow::ComputeUpdatesForSingleRow(int row_as_col) {
                 variables_info_.GetIsRelevantBitRow().NumWords());
   const std::vector<int> one(1, row_as_col);
   dev_->UpdateRowRowWise(one, rho_.values, 0, params_.drop_tolerance);
-  FetchFromDevice();
+  FetchOrDefer();
 }
 
 // update_row.cc:282-306
@@ -799,7 +833,7 @@ void UpdateRow::RunColumnWise(const std::vector<Fractional>* w) {
                 static_cast<int>(pending_mask_.size()));
   dev_->UpdateRowColumnWise(rho_.values, params_.drop_tolerance, pending_relevant_entries_,
                             w);
-  FetchFromDevice();
+  FetchOrDefer();
 }
 
 // update_row.cc:311-332
@@ -1171,8 +1205,33 @@ class ReducedCosts {
     UpdateBasicObjective(entering_col, leaving_row);
   }
   void SetNonBasicVariableCostToZero(int col, Fractional* current_cost) {
+    SyncHost();  // primal only; never in dual device mode
     reduced_costs_[col] -= objective_[col];
     *current_cost = 0.0;
+  }
+  // Dual device mode (RevisedSimplex::DualDeviceMode): the device copy of the
+  // reduced costs is the reference; the host vector is refreshed from it
+  // only when host code reads it. The entering column's value is handed over
+  // by the device ratio test.
+  void EnterDeviceMode() {
+    device_mode_ = true;
+    host_stale_ = false;
+  }
+  void LeaveDeviceMode() {
+    SyncHost();
+    device_mode_ = false;
+    known_col_ = -1;
+  }
+  bool InDeviceMode() const { return device_mode_; }
+  void SetKnownReducedCost(int col, Fractional value) {
+    known_col_ = col;
+    known_value_ = value;
+  }
+  // The side effects of GetReducedCosts() (recompute, refactorization flag)
+  // without refreshing the host copy.
+  void PrepareForDeviceUse() {
+    if (bf_.IsRefactorized()) must_refactorize_basis_ = false;
+    if (recompute_reduced_costs_) ComputeReducedCosts();
   }
   bool AreReducedCostsPrecise() const { return are_reduced_costs_precise_; }
   bool AreReducedCostsRecomputed() const {
@@ -1206,11 +1265,15 @@ class ReducedCosts {
     recompute_basic_objective_left_inverse_ = true;
   }
   const std::vector<Fractional>& GetReducedCosts() {
+    SyncHost();
     if (bf_.IsRefactorized()) must_refactorize_basis_ = false;
     if (recompute_reduced_costs_) ComputeReducedCosts();
     return reduced_costs_;
   }
-  const std::vector<Fractional>& RawReducedCosts() const { return reduced_costs_; }
+  const std::vector<Fractional>& RawReducedCosts() const {
+    const_cast<ReducedCosts*>(this)->SyncHost();
+    return reduced_costs_;
+  }
   const std::vector<Fractional>& GetFullReducedCosts() {
     if (!are_reduced_costs_recomputed_) SetRecomputeReducedCostsAndNotifyWatchers();
     return GetReducedCosts();
@@ -1261,6 +1324,11 @@ class ReducedCosts {
     recompute_reduced_costs_ = true;
     for (bool* w : watchers_) *w = true;
   }
+  void SyncHost() {
+    if (!device_mode_ || !host_stale_) return;
+    dev_->DualDownloadReducedCosts(&reduced_costs_);
+    host_stale_ = false;
+  }
 
   const CompactSparseMatrix& matrix_;
   const std::vector<Fractional>& objective_;
@@ -1270,6 +1338,10 @@ class ReducedCosts {
   Rng* random_;
   DeviceLp* dev_;
   PrimalEdgeNorms* deferred_norms_ = nullptr;
+  bool device_mode_ = false;
+  bool host_stale_ = false;
+  int known_col_ = -1;
+  Fractional known_value_ = 0.0;
   std::vector<Fractional> fused_rc_;
   std::vector<Fractional> fused_dots_;
   std::vector<Fractional> shifted_objective_;
@@ -1394,6 +1466,18 @@ void ReducedCosts::PerturbCosts() {
 void ReducedCosts::ShiftCostIfNeeded(bool increasing_rc_is_needed, int col) {
   const Fractional minimum_delta =
       params_.degenerate_ministep_factor * dual_feasibility_tolerance_;
+  if (device_mode_) {
+    if (known_col_ != col) throw DeviceError("dual device mode: entering reduced cost unknown");
+    if (increasing_rc_is_needed && known_value_ <= -minimum_delta) return;
+    if (!increasing_rc_is_needed && known_value_ >= minimum_delta) return;
+    const Fractional delta = increasing_rc_is_needed ? minimum_delta : -minimum_delta;
+    cost_perturbations_[col] -= known_value_ + delta;
+    known_value_ = -delta;
+    dev_->DualSetReducedCost(col, known_value_);
+    host_stale_ = true;
+    has_cost_shift_ = true;
+    return;
+  }
   if (increasing_rc_is_needed && reduced_costs_[col] <= -minimum_delta) return;
   if (!increasing_rc_is_needed && reduced_costs_[col] >= minimum_delta) return;
   const Fractional delta = increasing_rc_is_needed ? minimum_delta : -minimum_delta;
@@ -1433,6 +1517,10 @@ void ReducedCosts::ComputeReducedCosts() {
   } else {
     dev_->Pricing(shifted_objective_, y, &reduced_costs_);
   }
+  if (device_mode_) {
+    dev_->DualTakePricedReducedCosts();
+    host_stale_ = false;
+  }
   is_basic.ForEach([&](int col) {
     dual_residual_error = std::max(dual_residual_error, std::fabs(reduced_costs_[col]));
   });
@@ -1450,6 +1538,25 @@ void ReducedCosts::ComputeReducedCosts() {
 void ReducedCosts::UpdateReducedCosts(int entering_col, int leaving_col, int leaving_row,
                                       Fractional pivot, UpdateRow* update_row) {
   if (recompute_reduced_costs_) return;
+  if (device_mode_) {
+    if (known_col_ != entering_col) {
+      throw DeviceError("dual device mode: entering reduced cost unknown");
+    }
+    const Fractional entering_reduced_cost = known_value_;
+    if (entering_reduced_cost == 0.0) {
+      are_reduced_costs_precise_ = false;
+      return;
+    }
+    are_reduced_costs_recomputed_ = false;
+    are_reduced_costs_precise_ = false;
+    update_row->ComputeUpdateRow(leaving_row);
+    const Fractional new_leaving_reduced_cost = entering_reduced_cost / -pivot;
+    dev_->DualUpdateReducedCosts(new_leaving_reduced_cost, leaving_col,
+                                 new_leaving_reduced_cost, entering_col);
+    host_stale_ = true;
+    known_col_ = -1;
+    return;
+  }
   const Fractional entering_reduced_cost = reduced_costs_[entering_col];
   if (entering_reduced_cost == 0.0) {
     are_reduced_costs_precise_ = false;
@@ -1672,6 +1779,15 @@ class EnteringVariable {
   Status DualPhaseIChooseEnteringColumn(bool nothing_to_recompute,
                                         const UpdateRow& update_row,
                                         Fractional cost_variation, int* entering_col);
+  // DualChooseEnteringColumn in dual device mode: the device filters the
+  // update row down to the breakpoints that can matter, the two Glop loops
+  // run on them. Also returns the entering column's update-row coefficient
+  // and reduced cost.
+  Status DualChooseEnteringColumnDevice(bool nothing_to_recompute, DeviceLp* dev,
+                                        Fractional cost_variation,
+                                        std::vector<int>* bound_flip_candidates,
+                                        int* entering_col, Fractional* entering_coeff,
+                                        Fractional* entering_rc);
   double DeterministicTime() const {
     return DeterministicTimeForFpOperations(num_operations_);
   }
@@ -1698,8 +1814,135 @@ class EnteringVariable {
   GlopParameters params_;
   std::vector<int> equivalent_entering_choices_;
   std::vector<ColWithRatio> breakpoints_;
+  std::vector<Fractional> bound_flip_magnitudes_;
+  DeviceLp::DualCandidates candidates_;
   int64_t num_operations_ = 0;
 };
+
+// entering_variable.cc:37-239 over the device-filtered breakpoints. Only the
+// slots with ratio <= B (1 + 1e-9) come back, B being the smallest Harris
+// ratio over the breakpoints that can never be bound flipped: in the second
+// loop such a breakpoint (or an earlier accepted one, with a larger
+// coefficient and a smaller ratio) caps harris_ratio at <= B, so nothing
+// with a larger ratio is popped, and a breakpoint beyond B can only prune
+// breakpoints beyond B in the first loop. Both loops below are Glop's, in
+// list order, over that subset.
+Status EnteringVariable::DualChooseEnteringColumnDevice(bool nothing_to_recompute,
+                                                        DeviceLp* dev,
+                                                        Fractional cost_variation,
+                                                        std::vector<int>* bound_flip_candidates,
+                                                        int* entering_col,
+                                                        Fractional* entering_coeff,
+                                                        Fractional* entering_rc) {
+  const Bitset& can_decrease = variables_info_.GetCanDecreaseBitRow();
+  const Bitset& can_increase = variables_info_.GetCanIncreaseBitRow();
+  const Bitset& is_boxed = variables_info_.GetNonBasicBoxedVariables();
+  const Fractional threshold = nothing_to_recompute ? params_.minimum_acceptable_pivot
+                                                    : params_.ratio_test_zero_threshold;
+  Fractional variation_magnitude = std::fabs(cost_variation) - threshold;
+  const Fractional harris_tolerance =
+      params_.harris_tolerance_ratio * reduced_costs_->GetDualFeasibilityTolerance();
+  const Fractional minimum_delta =
+      params_.degenerate_ministep_factor * reduced_costs_->GetDualFeasibilityTolerance();
+  dev->DualRatioCandidates(cost_variation > 0.0 ? 1.0 : -1.0, threshold, harris_tolerance,
+                           minimum_delta, variation_magnitude, &candidates_);
+  const DeviceLp::DualCandidates& cand = candidates_;
+  num_operations_ += 10 * static_cast<int64_t>(cand.list_count);
+  breakpoints_.clear();
+  Fractional harris_ratio = std::numeric_limits<Fractional>::max();
+  const int num_candidates = static_cast<int>(cand.col.size());
+  for (int k = 0; k < num_candidates; ++k) {
+    const int col = cand.col[k];
+    const Fractional coeff = (cost_variation > 0.0) ? cand.coeff[k] : -cand.coeff[k];
+    const Fractional reduced_cost = cand.rc[k];
+    ColWithRatio entry;
+    if (can_decrease.IsSet(col) && coeff > threshold) {
+      if (-reduced_cost > harris_ratio * coeff) continue;
+      entry = ColWithRatio(col, -reduced_cost, coeff);
+    } else if (can_increase.IsSet(col) && coeff < -threshold) {
+      if (reduced_cost > harris_ratio * -coeff) continue;
+      entry = ColWithRatio(col, reduced_cost, -coeff);
+    } else {
+      continue;
+    }
+    const Fractional hr = std::max(minimum_delta / entry.coeff_magnitude,
+                                   entry.ratio + harris_tolerance / entry.coeff_magnitude);
+    if (hr < harris_ratio) {
+      if (is_boxed[col]) {
+        const Fractional delta =
+            variables_info_.GetBoundDifference(col) * entry.coeff_magnitude;
+        if (delta >= variation_magnitude) harris_ratio = hr;
+      } else {
+        harris_ratio = hr;
+      }
+    }
+    breakpoints_.push_back(entry);
+  }
+  std::make_heap(breakpoints_.begin(), breakpoints_.end());
+  harris_ratio = std::numeric_limits<Fractional>::max();
+  *entering_col = kInvalidCol;
+  bound_flip_candidates->clear();
+  bound_flip_magnitudes_.clear();
+  Fractional step = 0.0;
+  Fractional best_coeff = -1.0;
+  equivalent_entering_choices_.clear();
+  while (!breakpoints_.empty()) {
+    const ColWithRatio top = breakpoints_.front();
+    if (top.ratio > harris_ratio) break;
+    if (variation_magnitude > 0.0) {
+      if (is_boxed[top.col]) {
+        variation_magnitude -=
+            variables_info_.GetBoundDifference(top.col) * top.coeff_magnitude;
+        if (variation_magnitude > 0.0) {
+          bound_flip_candidates->push_back(top.col);
+          bound_flip_magnitudes_.push_back(top.coeff_magnitude);
+          std::pop_heap(breakpoints_.begin(), breakpoints_.end());
+          breakpoints_.pop_back();
+          continue;
+        }
+      }
+    }
+    if (top.coeff_magnitude >= best_coeff) {
+      harris_ratio = std::min(
+          harris_ratio, std::max(minimum_delta / top.coeff_magnitude,
+                                 top.ratio + harris_tolerance / top.coeff_magnitude));
+      if (top.coeff_magnitude == best_coeff && top.ratio == step) {
+        equivalent_entering_choices_.push_back(top.col);
+      } else {
+        equivalent_entering_choices_.clear();
+        best_coeff = top.coeff_magnitude;
+        *entering_col = top.col;
+        step = top.ratio;
+      }
+    }
+    std::pop_heap(breakpoints_.begin(), breakpoints_.end());
+    breakpoints_.pop_back();
+  }
+  if (!equivalent_entering_choices_.empty()) {
+    equivalent_entering_choices_.push_back(*entering_col);
+    *entering_col = equivalent_entering_choices_[UniformInt(
+        *random_, static_cast<int>(equivalent_entering_choices_.size()) - 1)];
+  }
+  if (*entering_col == kInvalidCol) return Status::OK();
+  const Fractional pivot_limit = params_.minimum_acceptable_pivot;
+  if (best_coeff < pivot_limit && !bound_flip_candidates->empty()) {
+    // |update_coefficients[col]| is the breakpoint's coefficient magnitude.
+    for (int i = static_cast<int>(bound_flip_candidates->size()) - 1; i >= 0; --i) {
+      const int col = (*bound_flip_candidates)[i];
+      if (bound_flip_magnitudes_[i] < pivot_limit) continue;
+      *entering_col = col;
+      break;
+    }
+  }
+  for (int k = 0; k < num_candidates; ++k) {
+    if (cand.col[k] == *entering_col) {
+      *entering_coeff = cand.coeff[k];
+      *entering_rc = cand.rc[k];
+      return Status::OK();
+    }
+  }
+  throw DeviceError("dual device mode: entering column not among the candidates");
+}
 
 // entering_variable.cc:37-239
 Status EnteringVariable::DualChooseEnteringColumn(bool nothing_to_recompute,
@@ -2318,6 +2561,18 @@ class RevisedSimplex {
   Status DualPhaseIChooseLeavingVariableRow(int* leaving_row, Fractional* cost_variation,
                                             Fractional* target_bound);
   void MakeBoxedVariableDualFeasible(const std::vector<int>& cols, bool update_basic_values);
+  // Dual device mode: phase II of the dual simplex keeps the reduced costs
+  // and the update row on the device (MILP_DEVICE_DUAL=auto|force|off; auto:
+  // N >= 65536). The host copy of the column status bits is mirrored on the
+  // device through the VariablesInfo change log.
+  bool DualDeviceEnabled() const;
+  void BeginDualDeviceMode();
+  void EndDualDeviceMode();
+  void FlushColumnBits();
+  // MakeBoxedVariableDualFeasible with the decisions taken on the device;
+  // cols == nullptr: every non-basic boxed column.
+  void MakeBoxedVariableDualFeasibleOnDevice(const std::vector<int>* cols,
+                                             bool update_basic_values);
   Fractional ComputeStepToMoveBasicVariableToBound(int leaving_row, Fractional target_bound) {
     const int leaving_col = basis_[leaving_row];
     const Fractional unscaled_step = variable_values_.Get(leaving_col) - target_bound;
@@ -2461,6 +2716,11 @@ class RevisedSimplex {
   bool objective_limit_reached_ = false;
   SparseColumn leaving_candidates_;
   std::vector<int> equivalent_leaving_choices_;
+  bool dual_device_mode_ = false;
+  std::vector<int> status_log_;
+  std::vector<int> flush_cols_;
+  std::vector<uint8_t> flush_bits_;
+  std::vector<uint8_t> flip_flags_;
 };
 
 RevisedSimplex::RevisedSimplex()
@@ -3740,6 +4000,84 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
   return Status::OK();
 }
 
+bool RevisedSimplex::DualDeviceEnabled() const {
+  const char* e = std::getenv("MILP_DEVICE_DUAL");
+  if (e != nullptr && std::strcmp(e, "off") == 0) return false;
+  if (e != nullptr && std::strcmp(e, "force") == 0) return true;
+  return num_cols_ >= 65536;
+}
+
+void RevisedSimplex::BeginDualDeviceMode() {
+  std::vector<uint8_t> bits(num_cols_);
+  std::vector<Fractional> bound_diff(num_cols_);
+  for (int col = 0; col < num_cols_; ++col) {
+    bits[col] = variables_info_.ColumnBits(col);
+    bound_diff[col] = variables_info_.GetBoundDifference(col);
+  }
+  // The raw host values: if a recompute is pending it replaces them (on the
+  // device) at the first read, exactly when Glop would recompute.
+  device_.DualBegin(reduced_costs_.RawReducedCosts(), bits, bound_diff);
+  reduced_costs_.EnterDeviceMode();
+  update_row_.SetLazyFetch(true);
+  status_log_.clear();
+  variables_info_.SetChangeLog(&status_log_);
+  dual_device_mode_ = true;
+}
+
+void RevisedSimplex::EndDualDeviceMode() {
+  dual_device_mode_ = false;
+  variables_info_.SetChangeLog(nullptr);
+  status_log_.clear();
+  update_row_.SetLazyFetch(false);
+  // Bring the last update row to the host while the device list is intact
+  // (later ListDots calls reuse the list-value buffer).
+  update_row_.GetNonZeroPositions();
+  reduced_costs_.LeaveDeviceMode();
+}
+
+void RevisedSimplex::FlushColumnBits() {
+  if (status_log_.empty()) return;
+  std::sort(status_log_.begin(), status_log_.end());
+  status_log_.erase(std::unique(status_log_.begin(), status_log_.end()), status_log_.end());
+  flush_cols_.assign(status_log_.begin(), status_log_.end());
+  flush_bits_.resize(flush_cols_.size());
+  for (size_t i = 0; i < flush_cols_.size(); ++i) {
+    flush_bits_[i] = variables_info_.ColumnBits(flush_cols_[i]);
+  }
+  status_log_.clear();
+  device_.DualSetColBits(flush_cols_, flush_bits_);
+}
+
+// revised_simplex.cc:2391-2437. The per-column decisions do not depend on
+// each other, so they are taken in one device pass and applied in order.
+void RevisedSimplex::MakeBoxedVariableDualFeasibleOnDevice(const std::vector<int>* cols,
+                                                           bool update_basic_values) {
+  std::vector<int> changed_cols;
+  const Fractional threshold = reduced_costs_.GetDualFeasibilityTolerance();
+  reduced_costs_.PrepareForDeviceUse();  // GetReducedCosts() side effects
+  {
+    SubTimer timer(kSubBoxedScan);
+    FlushColumnBits();
+    device_.DualBoxedFlips(cols, threshold, &flip_flags_);
+    const std::vector<VariableStatus>& variable_status = variables_info_.GetStatusRow();
+    const int n = static_cast<int>(flip_flags_.size());
+    for (int i = 0; i < n; ++i) {
+      if (!flip_flags_[i]) continue;
+      const int col = cols != nullptr ? (*cols)[i] : i;
+      if (variable_status[col] == VariableStatus::AT_UPPER_BOUND) {
+        variables_info_.UpdateToNonBasicStatus(col, VariableStatus::AT_LOWER_BOUND);
+      } else {
+        variables_info_.UpdateToNonBasicStatus(col, VariableStatus::AT_UPPER_BOUND);
+      }
+      changed_cols.push_back(col);
+    }
+  }
+  if (!changed_cols.empty()) {
+    SubTimer flip_timer(kSubFlipFtran);
+    variable_values_.UpdateGivenNonBasicVariables(changed_cols, update_basic_values);
+  }
+}
+
 // revised_simplex.cc:3058-3367
 Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limit) {
   struct Cleanup {
@@ -3754,6 +4092,20 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     int64_t first;
     ~DumpAtExit() { c->Dump(static_cast<long long>(*it - first)); }
   } dump{&clock, &num_iterations_, first_iteration};
+  const bool device_mode = !feasibility_phase && DualDeviceEnabled();
+  if (device_mode) BeginDualDeviceMode();
+  struct EndDeviceMode {
+    RevisedSimplex* s;
+    bool on;
+    ~EndDeviceMode() {
+      if (!on) return;
+      try {
+        s->EndDualDeviceMode();
+      } catch (const DeviceError&) {
+        // The device failed; the next device call reports it.
+      }
+    }
+  } end_device_mode{this, device_mode};
   bool refactorize = false;
   bound_flip_candidates_.clear();
   int leaving_row;
@@ -3770,8 +4122,12 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
         reduced_costs_.MakeReducedCostsPrecise();
       }
       if (!feasibility_phase) {
-        MakeBoxedVariableDualFeasible(
-            variables_info_.GetNonBasicBoxedVariables().ToVector(), false);
+        if (dual_device_mode_) {
+          MakeBoxedVariableDualFeasibleOnDevice(nullptr, false);
+        } else {
+          MakeBoxedVariableDualFeasible(
+              variables_info_.GetNonBasicBoxedVariables().ToVector(), false);
+        }
         variable_values_.RecomputeBasicVariableValues();
         variable_values_.RecomputeDualPrices(parameters_.dual_price_prioritize_norm);
         if (phase_ == Phase::OPTIMIZATION && dual_objective_limit_ != kInfinity &&
@@ -3783,7 +4139,11 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
       }
     } else {
       if (!feasibility_phase) {
-        MakeBoxedVariableDualFeasible(bound_flip_candidates_, true);
+        if (dual_device_mode_) {
+          MakeBoxedVariableDualFeasibleOnDevice(&bound_flip_candidates_, true);
+        } else {
+          MakeBoxedVariableDualFeasible(bound_flip_candidates_, true);
+        }
         bound_flip_candidates_.clear();
         variable_values_.UpdateDualPrices(direction_.non_zeros);
       }
@@ -3827,13 +4187,27 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
       continue;
     }
     update_row_.ComputeUpdateRow(leaving_row);
-    update_row_.GetNonZeroPositions();  // materialize (timed as the update row)
+    if (!dual_device_mode_) update_row_.GetNonZeroPositions();  // timed as the update row
     clock.Mark(3);
 
     if (feasibility_phase) {
       MILP_RETURN_IF_ERROR(entering_variable_.DualPhaseIChooseEnteringColumn(
           reduced_costs_.AreReducedCostsPrecise(), update_row_, cost_variation,
           &entering_col));
+    } else if (dual_device_mode_) {
+      const bool nothing_to_recompute = reduced_costs_.AreReducedCostsPrecise();
+      update_row_.MaterializeOnDevice();
+      reduced_costs_.PrepareForDeviceUse();  // GetReducedCosts() side effects
+      FlushColumnBits();
+      Fractional coeff = 0.0;
+      Fractional rc = 0.0;
+      MILP_RETURN_IF_ERROR(entering_variable_.DualChooseEnteringColumnDevice(
+          nothing_to_recompute, &device_, cost_variation, &bound_flip_candidates_,
+          &entering_col, &coeff, &rc));
+      if (entering_col != kInvalidCol) {
+        update_row_.SetKnownCoefficient(entering_col, coeff);
+        reduced_costs_.SetKnownReducedCost(entering_col, rc);
+      }
     } else {
       MILP_RETURN_IF_ERROR(entering_variable_.DualChooseEnteringColumn(
           reduced_costs_.AreReducedCostsPrecise(), update_row_, cost_variation,

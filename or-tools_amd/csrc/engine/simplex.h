@@ -213,6 +213,17 @@ class VariablesInfo {
   Fractional GetBoundDifference(int col) const {
     return upper_bounds_[col] - lower_bounds_[col];
   }
+  // Status changes are appended to *log while set (dual device mode keeps a
+  // device copy of the column bits in sync with it).
+  void SetChangeLog(std::vector<int>* log) { change_log_ = log; }
+  // can_decrease | can_increase << 1 | non-basic boxed << 2 | status << 3
+  // (kernel_args.h kCol*).
+  uint8_t ColumnBits(int col) const {
+    return static_cast<uint8_t>((can_decrease_.IsSet(col) ? 1 : 0) |
+                                (can_increase_.IsSet(col) ? 2 : 0) |
+                                (non_basic_boxed_variables_.IsSet(col) ? 4 : 0) |
+                                (static_cast<int>(variable_status_[col]) << 3));
+  }
 
  private:
   void ResetStatusInfo();
@@ -230,6 +241,7 @@ class VariablesInfo {
   int64_t num_entries_in_relevant_columns_ = 0;
   bool boxed_variables_are_relevant_ = true;
   bool in_dual_phase_one_ = false;
+  std::vector<int>* change_log_ = nullptr;
 };
 
 }  // namespace milp

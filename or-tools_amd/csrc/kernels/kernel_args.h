@@ -84,6 +84,34 @@ struct RowWiseColArgs {
   int algorithm;  // 0 single row, 1 hypersparse, 2 row-wise
 };
 
+// Dual simplex with device-resident reduced costs (engine/device_lp.h
+// "dual device mode"). Per column one status byte:
+//   bit 0 can_decrease, bit 1 can_increase, bit 2 non-basic boxed,
+//   bits 3-5 glop::VariableStatus.
+enum : uint8_t { kColCanDecrease = 1, kColCanIncrease = 2, kColBoxed = 4 };
+__host__ __device__ inline int ColStatus(uint8_t b) { return (b >> 3) & 7; }
+
+// Bound-flipping ratio test filter (entering_variable.cc:37-130) over the
+// update-row list: pass 1 bounds the breakpoints that can matter, pass 2
+// flags them.
+struct DualRatioArgs {
+  const int32_t* list;       // update-row positions (list order)
+  const double* list_coeff;  // their coefficients
+  const int* count;          // list length (device)
+  int max_count;             // N (grid bound)
+  const double* rc;
+  const uint8_t* colbits;
+  const double* bound_diff;  // upper - lower per column
+  double sign;               // +1 if cost_variation > 0 else -1
+  double threshold;          // minimum pivot magnitude
+  double harris_tolerance;
+  double minimum_delta;
+  double variation_magnitude;
+  unsigned long long* best;  // pass 1: min over H-setting breakpoints of the
+                             // Harris ratio, as ordered bits (all values > 0)
+  uint8_t* flags;            // pass 2: per list slot, kept for the host replay
+};
+
 struct RowSumArgs {
   const int64_t* t_starts;
   const int32_t* t_cols;
@@ -121,6 +149,30 @@ hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag
                     uint32_t* row_tag, int32_t* row_pos, hipStream_t s);
 hipError_t row_wise_update_by_column(const milp_kernels::RowWiseColArgs& args, hipStream_t s);
 hipError_t row_sums(const milp_kernels::RowSumArgs& args, hipStream_t s);
+// Dual device mode.
+hipError_t dual_ratio_bound(const milp_kernels::DualRatioArgs& args, hipStream_t s);
+hipError_t dual_ratio_flags(const milp_kernels::DualRatioArgs& args, hipStream_t s);
+// cand_* [k] = (list[slot], list_coeff[slot], rc[list[slot]]) for the flagged
+// slots k in slot order (flag compaction done by the caller).
+hipError_t gather_candidates(const int32_t* slots, const int* num_slots, int max_slots,
+                             const int32_t* list, const double* list_coeff, const double* rc,
+                             int32_t* cand_col, double* cand_coeff, double* cand_rc,
+                             hipStream_t s);
+// rc[list[i]] += mult * list_coeff[i] (reduced_costs.cc:466-470), then
+// rc[leaving] = leaving_value, rc[entering] = 0.
+hipError_t update_reduced_costs(const int32_t* list, const double* list_coeff, const int* count,
+                                int max_count, double mult, int leaving_col,
+                                double leaving_value, int entering_col, double* rc,
+                                hipStream_t s);
+hipError_t set_double(double* dst, double value, hipStream_t s);
+// colbits[cols[i]] = bits[i].
+hipError_t set_colbits(const int32_t* cols, const uint8_t* bits, int n, uint8_t* colbits,
+                       hipStream_t s);
+// MakeBoxedVariableDualFeasible (revised_simplex.cc:2391-2437) decisions:
+// flag[i] = new status (AT_LOWER/AT_UPPER) if cols[i] flips, else 0xff.
+// cols == nullptr: every column whose bit 2 (non-basic boxed) is set.
+hipError_t boxed_flips(const int32_t* cols, int n, const double* rc, const uint8_t* colbits,
+                       double threshold, uint8_t* flag, hipStream_t s);
 hipError_t column_squared_norms(const int64_t* starts, const double* vals,
                                 const uint64_t* relevant, int ncols, double* out,
                                 hipStream_t s);

@@ -519,6 +519,145 @@ __global__ void tag_rows_kernel(const int32_t* filtered_rows, int n, uint32_t ta
 }
 
 // ---------------------------------------------------------------------------
+// Dual device mode: the bound-flipping ratio test filter, the reduced-cost
+// update and the boxed dual-feasibility decisions where the update row and
+// the reduced costs already are.
+
+// One update-row slot as a breakpoint candidate (entering_variable.cc:68-96,
+// same expressions): returns false if the slot is not eligible.
+__device__ __forceinline__ bool dual_breakpoint(const DualRatioArgs& a, int slot, double* ratio,
+                                                double* harris, bool* sets_bound) {
+  const int col = a.list[slot];
+  const double c = a.list_coeff[slot];
+  const double coeff = a.sign > 0.0 ? c : -c;
+  const uint8_t bits = a.colbits[col];
+  double reduced_cost, magnitude;
+  if ((bits & kColCanDecrease) && coeff > a.threshold) {
+    reduced_cost = -a.rc[col];
+    magnitude = coeff;
+  } else if ((bits & kColCanIncrease) && coeff < -a.threshold) {
+    reduced_cost = a.rc[col];
+    magnitude = -coeff;
+  } else {
+    return false;
+  }
+  *ratio = reduced_cost / magnitude;
+  *harris = fmax(a.minimum_delta / magnitude, *ratio + a.harris_tolerance / magnitude);
+  *sets_bound = !(bits & kColBoxed) || (a.bound_diff[col] * magnitude >= a.variation_magnitude);
+  return true;
+}
+
+// Pass 1: B = min Harris ratio over the breakpoints that can never be bound
+// flipped. In the host loop such a breakpoint, once popped, bounds the
+// search by a value <= B, so no breakpoint with ratio > B is ever popped.
+__global__ __launch_bounds__(256) void dual_ratio_bound_kernel(DualRatioArgs a) {
+  __shared__ unsigned long long block_min[4];
+  const int n = *a.count;
+  unsigned long long best = ~0ull;
+  for (int slot = blockIdx.x * blockDim.x + threadIdx.x; slot < n;
+       slot += gridDim.x * blockDim.x) {
+    double ratio, harris;
+    bool sets_bound;
+    if (dual_breakpoint(a, slot, &ratio, &harris, &sets_bound) && sets_bound) {
+      const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(harris));
+      best = b < best ? b : best;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_down(best, off, kWave);
+    best = o < best ? o : best;
+  }
+  if ((threadIdx.x & 63) == 0) block_min[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = block_min[0];
+    for (int w = 1; w < (blockDim.x >> 6); ++w) m = block_min[w] < m ? block_min[w] : m;
+    if (m != ~0ull) atomicMin(a.best, m);
+  }
+}
+
+// Pass 2: keep the eligible slots with ratio <= B (1 + 1e-9); the host
+// replays Glop's two loops over them in list order.
+__global__ __launch_bounds__(256) void dual_ratio_flags_kernel(DualRatioArgs a) {
+  const int n = *a.count;
+  const unsigned long long best = *a.best;
+  const double bound = best == ~0ull ? HUGE_VAL
+                                     : __longlong_as_double(static_cast<long long>(best)) *
+                                           (1.0 + 1e-9);
+  for (int slot = blockIdx.x * blockDim.x + threadIdx.x; slot < a.max_count;
+       slot += gridDim.x * blockDim.x) {
+    bool keep = false;
+    if (slot < n) {
+      double ratio, harris;
+      bool sets_bound;
+      keep = dual_breakpoint(a, slot, &ratio, &harris, &sets_bound) && ratio <= bound;
+    }
+    a.flags[slot] = keep ? 1 : 0;
+  }
+}
+
+__global__ void gather_candidates_kernel(const int32_t* slots, const int* num_slots,
+                                         const int32_t* list, const double* list_coeff,
+                                         const double* rc, int32_t* cand_col,
+                                         double* cand_coeff, double* cand_rc) {
+  const int n = *num_slots;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    const int slot = slots[k];
+    const int col = list[slot];
+    cand_col[k] = col;
+    cand_coeff[k] = list_coeff[slot];
+    cand_rc[k] = rc[col];
+  }
+}
+
+__global__ void update_reduced_costs_kernel(const int32_t* list, const double* list_coeff,
+                                            const int* count, double mult, int leaving_col,
+                                            double leaving_value, int entering_col,
+                                            double* rc) {
+  const int n = *count;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int col = list[i];
+    if (col == entering_col) continue;  // set to 0 below
+    rc[col] += mult * list_coeff[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    rc[leaving_col] = leaving_value;  // basic before the pivot: never listed
+    rc[entering_col] = 0.0;
+  }
+}
+
+__global__ void set_double_kernel(double* dst, double value) { *dst = value; }
+
+__global__ void set_colbits_kernel(const int32_t* cols, const uint8_t* bits, int n,
+                                   uint8_t* colbits) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    colbits[cols[i]] = bits[i];
+}
+
+// glop::VariableStatus values (lp_types.h:188-219).
+constexpr int kAtLowerBound = 2;
+constexpr int kAtUpperBound = 3;
+
+__global__ void boxed_flips_kernel(const int32_t* cols, int n, const double* rc,
+                                   const uint8_t* colbits, double threshold, uint8_t* flag) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int col = cols != nullptr ? cols[i] : i;
+    const uint8_t bits = colbits[col];
+    uint8_t f = 0;
+    if (cols != nullptr || (bits & kColBoxed)) {
+      const double reduced_cost = rc[col];
+      const int status = ColStatus(bits);
+      if (reduced_cost > threshold && status == kAtUpperBound) {
+        f = 1;
+      } else if (reduced_cost < -threshold && status == kAtLowerBound) {
+        f = 1;
+      }
+    }
+    flag[i] = f;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Row sums sum_j mult_j * A[r, j] in increasing j (the order the host scatter
 // ColumnAddMultipleToDenseColumn produces), zero multipliers skipped
 // (sparse.h:393). One wave per row: lanes load 64 consecutive CSR entries,
@@ -679,6 +818,56 @@ hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag
 hipError_t row_wise_update_by_column(const RowWiseColArgs& args, hipStream_t s) {
   if (args.num_cols <= 0) return hipSuccess;
   row_wise_by_column_kernel<<<div_up(args.num_cols, 256), 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+static inline int grid_for(int n) { return std::max(1, std::min(4096, div_up(n, 256))); }
+
+hipError_t dual_ratio_bound(const DualRatioArgs& args, hipStream_t s) {
+  dual_ratio_bound_kernel<<<grid_for(args.max_count), 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t dual_ratio_flags(const DualRatioArgs& args, hipStream_t s) {
+  dual_ratio_flags_kernel<<<grid_for(args.max_count), 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t gather_candidates(const int32_t* slots, const int* num_slots, int max_slots,
+                             const int32_t* list, const double* list_coeff, const double* rc,
+                             int32_t* cand_col, double* cand_coeff, double* cand_rc,
+                             hipStream_t s) {
+  gather_candidates_kernel<<<grid_for(max_slots), 256, 0, s>>>(slots, num_slots, list,
+                                                               list_coeff, rc, cand_col,
+                                                               cand_coeff, cand_rc);
+  return hipGetLastError();
+}
+
+hipError_t update_reduced_costs(const int32_t* list, const double* list_coeff, const int* count,
+                                int max_count, double mult, int leaving_col,
+                                double leaving_value, int entering_col, double* rc,
+                                hipStream_t s) {
+  update_reduced_costs_kernel<<<grid_for(max_count), 256, 0, s>>>(
+      list, list_coeff, count, mult, leaving_col, leaving_value, entering_col, rc);
+  return hipGetLastError();
+}
+
+hipError_t set_double(double* dst, double value, hipStream_t s) {
+  set_double_kernel<<<1, 1, 0, s>>>(dst, value);
+  return hipGetLastError();
+}
+
+hipError_t set_colbits(const int32_t* cols, const uint8_t* bits, int n, uint8_t* colbits,
+                       hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  set_colbits_kernel<<<grid_for(n), 256, 0, s>>>(cols, bits, n, colbits);
+  return hipGetLastError();
+}
+
+hipError_t boxed_flips(const int32_t* cols, int n, const double* rc, const uint8_t* colbits,
+                       double threshold, uint8_t* flag, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  boxed_flips_kernel<<<grid_for(n), 256, 0, s>>>(cols, n, rc, colbits, threshold, flag);
   return hipGetLastError();
 }
 

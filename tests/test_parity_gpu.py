@@ -215,3 +215,50 @@ def test_batched_children_parity(shape):
         assert (r.error_code, r.problem_status, r.iterations) == \
             (ro.error_code, ro.problem_status, ro.iterations), i
         assert r.objective == ro.objective, (i, r.objective, ro.objective)
+
+
+def _device_dual_cases():
+    cases = []
+    for seed in range(6):
+        m = [30, 90, 200][seed % 3]
+        n = [90, 300, 900][seed % 3]
+        cases.append(("sparse", lambda m=m, n=n, s=seed: lp_gen.random_sparse_lp(
+            m, n, 0.25 if m < 40 else 0.04, 300 + s, maximize=bool(s % 2))))
+    for seed in (31, 32):
+        cases.append(("c5", lambda s=seed: lp_gen.sparse_c5_lp(400, 4000, 6, s)))
+    cases.append(("dense", lambda: lp_gen.dense_box_lp(93, 300, 13)))
+    for builder in kat_lps.ALL:
+        cases.append((builder.__name__, lambda b=builder: b()[0]))
+    return cases
+
+
+@pytest.mark.parametrize("case", _device_dual_cases(), ids=lambda c: c[0])
+def test_device_dual_mode_parity(case, monkeypatch):
+    """Dual phase II with the reduced costs and the update row kept on the
+    device (device-filtered bound-flipping ratio test, device rc update,
+    device boxed dual-feasibility decisions), forced on small LPs: every
+    result must equal the oracle's, which runs Glop's host loops."""
+    monkeypatch.setenv("MILP_DEVICE_DUAL", "force")
+    lp = case[1]()
+    p = abi.default_params(use_dual_simplex=1)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+
+
+def test_device_dual_mode_warm_start_and_children(monkeypatch):
+    """CP-SAT-style re-solves in dual device mode: bound change + warm start."""
+    monkeypatch.setenv("MILP_DEVICE_DUAL", "force")
+    import jobshop
+    lp, ycols = jobshop.relaxation(jobshop.FT06)
+    p = abi.default_params(use_dual_simplex=1)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    state = o.state()
+    lbs, ubs = jobshop.child_bounds(lp, ycols, 6, 5)
+    for i in range(len(lbs)):
+        for h in (o, g):
+            h.set_variable_bounds(lbs[i], ubs[i])
+            h.load_basis_state(state)
+        ro2 = o.solve()
+        rg2 = g.solve()
+        parity_util.compare(o, ro2, g, rg2, lp)
