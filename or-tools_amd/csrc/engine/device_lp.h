@@ -249,6 +249,7 @@ class DeviceLp {
   int32_t* h_flip_cols_ = nullptr;
   uint8_t* h_flip_flags_ = nullptr;
   int last_candidates_ = 0;
+  int dual_list_count_ = 0;  // update-row length seen by the last ratio test
 };
 
 }  // namespace milp

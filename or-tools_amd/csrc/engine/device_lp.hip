@@ -785,10 +785,7 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
                                        d_rc_, d_cand_col_, d_cand_coeff_, d_cand_rc_,
                                        S(stream_)),
         "gather candidates");
-  // Algorithmic bytes: the list (position + coefficient), the reduced cost,
-  // column byte and bound difference of each position, twice; flags.
-  EndKernel(MI_K_DUAL_RATIO, 2.0 * 29.0 * (list_count_ >= 0 ? list_count_ : last_list_len_) +
-                                 2.0 * n_total_);
+  EndKernel(MI_K_DUAL_RATIO, 0.0);  // bytes added once the list length is known
   const int cap = std::min<int64_t>(n_total_, std::max<int64_t>(1024, int64_t(last_candidates_) +
                                                                           last_candidates_ / 4));
   Check(hipMemcpyAsync(h_dual_counts_, d_num_slots_, sizeof(int), hipMemcpyDeviceToHost,
@@ -819,6 +816,11 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
     Download(h_cand_rc_ + cap, d_cand_rc_ + cap, (k - cap) * sizeof(double));
   }
   last_candidates_ = k;
+  dual_list_count_ = count;
+  // Algorithmic bytes: the list (position + coefficient), the reduced cost,
+  // column byte and bound difference of each position, twice; the flags; the
+  // candidates.
+  stats_.algorithmic_bytes[MI_K_DUAL_RATIO] += 2.0 * 29.0 * count + 2.0 * n_total_ + 20.0 * k;
   out->col.assign(h_cand_col_, h_cand_col_ + k);
   out->coeff.assign(h_cand_coeff_, h_cand_coeff_ + k);
   out->rc.assign(h_cand_rc_, h_cand_rc_ + k);
@@ -833,7 +835,8 @@ void DeviceLp::DualUpdateReducedCosts(double mult, int leaving_col, double leavi
                                           leaving_col, leaving_value, entering_col, d_rc_,
                                           S(stream_)),
         "rc update");
-  EndKernel(MI_K_RC_UPDATE, 28.0 * (list_count_ >= 0 ? list_count_ : last_list_len_));
+  // The list (position + coefficient) and a read-modify-write of rc.
+  EndKernel(MI_K_RC_UPDATE, 28.0 * dual_list_count_);
 }
 
 void DeviceLp::DualBoxedFlips(const std::vector<int>* cols, double threshold,

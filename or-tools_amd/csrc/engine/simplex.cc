@@ -78,6 +78,8 @@ const char* const kSubPhaseNames[kNumSubPhases] = {
     "basis update (MPF)", "refactorize (LU)", "boxed dual-feas scan", "flip update (FTRAN)",
     "recompute x_B",      "dual prices",       "ftran direction",   "tau ftran"};
 double g_sub_ms[kNumSubPhases] = {};
+double g_dual_candidates = 0.0;  // device ratio test: candidates returned
+double g_dual_list = 0.0;        // update-row positions they were filtered from
 const bool g_sub_on = std::getenv("MILP_PHASE_TIMING") != nullptr;
 struct SubTimer {
   SubPhase p;
@@ -100,6 +102,7 @@ PhaseClock::PhaseClock(bool dual) : names(dual ? kDual : kPrimal) {
 void PhaseClock::Reset() {
   std::fill(ms, ms + kPhases, 0.0);
   std::fill(g_sub_ms, g_sub_ms + kNumSubPhases, 0.0);
+  g_dual_candidates = g_dual_list = 0.0;
   window = 0;
 }
 
@@ -109,6 +112,10 @@ void PhaseClock::Dump(long long iterations) {
   for (int i = 0; i < kPhases; ++i) {
     std::fprintf(stderr, "  %-18s %10.3f ms  (%.3f ms/it)\n", names[i], ms[i],
                  iterations > 0 ? ms[i] / iterations : 0.0);
+  }
+  if (g_dual_list > 0.0) {
+    std::fprintf(stderr, "  device ratio test: %.0f candidates from %.0f update-row positions\n",
+                 g_dual_candidates, g_dual_list);
   }
   std::fprintf(stderr, "  -- sections:\n");
   for (int i = 0; i < kNumSubPhases; ++i) {
@@ -1848,6 +1855,10 @@ Status EnteringVariable::DualChooseEnteringColumnDevice(bool nothing_to_recomput
                            minimum_delta, variation_magnitude, &candidates_);
   const DeviceLp::DualCandidates& cand = candidates_;
   num_operations_ += 10 * static_cast<int64_t>(cand.list_count);
+  if (g_sub_on) {
+    g_dual_candidates += static_cast<double>(cand.col.size());
+    g_dual_list += cand.list_count;
+  }
   breakpoints_.clear();
   Fractional harris_ratio = std::numeric_limits<Fractional>::max();
   const int num_candidates = static_cast<int>(cand.col.size());
