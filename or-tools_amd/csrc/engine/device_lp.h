@@ -250,6 +250,15 @@ class DeviceLp {
   uint8_t* h_flip_flags_ = nullptr;
   int last_candidates_ = 0;
   int dual_list_count_ = 0;  // update-row length seen by the last ratio test
+  // Above this many breakpoints under the first bound, the dual ratio test
+  // tightens it on the device (MILP_DUAL_TIGHTEN_MIN).
+  int tighten_min_candidates_ = 512;
+  unsigned long long* d_best2_ = nullptr;
+  unsigned long long* d_keys_in_ = nullptr;
+  unsigned long long* d_keys_out_ = nullptr;
+  int32_t* d_sorted_slots_ = nullptr;
+  void* d_sort_temp_ = nullptr;
+  size_t sort_temp_bytes_ = 0;
 };
 
 }  // namespace milp

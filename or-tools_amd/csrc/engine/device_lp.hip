@@ -89,6 +89,9 @@ void DeviceLp::Init(int device) {
     const int v = std::atoi(u);
     if (v == 8 || v == 16 || v == 32) dense_unroll_ = v;
   }
+  if (const char* t = std::getenv("MILP_DUAL_TIGHTEN_MIN")) {
+    tighten_min_candidates_ = std::atoi(t);
+  }
   if (const char* r = std::getenv("MILP_ROWWISE_CHUNK_MAX_ROWS")) {
     rowwise_chunk_max_rows_ = std::atoi(r);
   }
@@ -693,6 +696,16 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
     d_cand_rc_ = Alloc<double>(n_total_);
     d_small_cols_ = Alloc<int32_t>(n_total_);
     d_small_bits_ = Alloc<uint8_t>(n_total_);
+    d_best2_ = Alloc<unsigned long long>(1);
+    d_keys_in_ = Alloc<unsigned long long>(n_total_);
+    d_keys_out_ = Alloc<unsigned long long>(n_total_);
+    d_sorted_slots_ = Alloc<int32_t>(n_total_);
+    sort_temp_bytes_ = 0;
+    Check(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_temp_bytes_, d_keys_in_, d_keys_out_,
+                                             d_slots_, d_sorted_slots_, n_total_, 0, 64,
+                                             S(stream_)),
+          "radix sizing");
+    d_sort_temp_ = Alloc<uint8_t>(sort_temp_bytes_);
     Synchronize();  // the pinned buffers below may still feed earlier copies
     PinnedResize(&h_cand_col_, n_total_);
     PinnedResize(&h_cand_coeff_, n_total_);
@@ -772,15 +785,35 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
   a.variation_magnitude = variation_magnitude;
   a.best = d_best_;
   a.flags = d_slot_flags_;
+  a.bound = d_best_;
   BeginKernel(MI_K_DUAL_RATIO);
   Check(hipMemsetAsync(d_best_, 0xff, sizeof(unsigned long long), S(stream_)), "memset");
   Check(milp_launch::dual_ratio_bound(a, S(stream_)), "dual ratio bound");
   Check(milp_launch::dual_ratio_flags(a, S(stream_)), "dual ratio flags");
-  size_t bytes = cub_temp_bytes_;
-  Check(hipcub::DeviceSelect::Flagged(d_cub_temp_, bytes,
-                                      hipcub::CountingInputIterator<int32_t>(0), d_slot_flags_,
-                                      d_slots_, d_num_slots_, n_total_, S(stream_)),
-        "cub flagged");
+  auto select = [&]() {
+    size_t bytes = cub_temp_bytes_;
+    Check(hipcub::DeviceSelect::Flagged(d_cub_temp_, bytes,
+                                        hipcub::CountingInputIterator<int32_t>(0),
+                                        d_slot_flags_, d_slots_, d_num_slots_, n_total_,
+                                        S(stream_)),
+          "cub flagged");
+  };
+  select();
+  // Many breakpoints under B: tighten the bound by walking them in pop order
+  // (the sort needs their number on the host).
+  Download(h_dual_counts_, d_num_slots_, sizeof(int));
+  const int k1 = h_dual_counts_[0];
+  if (k1 > tighten_min_candidates_) {
+    Check(milp_launch::dual_ratio_keys(a, d_slots_, k1, d_keys_in_, S(stream_)), "keys");
+    size_t bytes = sort_temp_bytes_;
+    Check(hipcub::DeviceRadixSort::SortPairs(d_sort_temp_, bytes, d_keys_in_, d_keys_out_,
+                                             d_slots_, d_sorted_slots_, k1, 0, 64, S(stream_)),
+          "radix sort");
+    Check(milp_launch::dual_flip_walk(a, d_sorted_slots_, k1, d_best2_, S(stream_)), "walk");
+    a.bound = d_best2_;
+    Check(milp_launch::dual_ratio_flags(a, S(stream_)), "dual ratio flags");
+    select();
+  }
   Check(milp_launch::gather_candidates(d_slots_, d_num_slots_, n_total_, d_list_, d_out_list_,
                                        d_rc_, d_cand_col_, d_cand_coeff_, d_cand_rc_,
                                        S(stream_)),
@@ -820,7 +853,9 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
   // Algorithmic bytes: the list (position + coefficient), the reduced cost,
   // column byte and bound difference of each position, twice; the flags; the
   // candidates.
-  stats_.algorithmic_bytes[MI_K_DUAL_RATIO] += 2.0 * 29.0 * count + 2.0 * n_total_ + 20.0 * k;
+  stats_.algorithmic_bytes[MI_K_DUAL_RATIO] +=
+      (k1 > tighten_min_candidates_ ? 3.0 : 2.0) * 29.0 * count + 2.0 * n_total_ + 20.0 * k +
+      (k1 > tighten_min_candidates_ ? 36.0 * k1 : 0.0);
   out->col.assign(h_cand_col_, h_cand_col_ + k);
   out->coeff.assign(h_cand_coeff_, h_cand_coeff_ + k);
   out->rc.assign(h_cand_rc_, h_cand_rc_ + k);

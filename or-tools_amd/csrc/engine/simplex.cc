@@ -1832,8 +1832,12 @@ class EnteringVariable {
 // loop such a breakpoint (or an earlier accepted one, with a larger
 // coefficient and a smaller ratio) caps harris_ratio at <= B, so nothing
 // with a larger ratio is popped, and a breakpoint beyond B can only prune
-// breakpoints beyond B in the first loop. Both loops below are Glop's, in
-// list order, over that subset.
+// breakpoints beyond B in the first loop. When many breakpoints remain, the
+// device sorts them by ratio and walks them in pop order up to the first
+// accepted one, a, and B becomes min(B, Harris ratio of a): no breakpoint
+// before a is pruned by the first loop (a pruning breakpoint would have been
+// accepted first), so the walk sees what the heap would pop. Both loops
+// below are Glop's, in list order, over the returned subset.
 Status EnteringVariable::DualChooseEnteringColumnDevice(bool nothing_to_recompute,
                                                         DeviceLp* dev,
                                                         Fractional cost_variation,

@@ -110,6 +110,7 @@ struct DualRatioArgs {
   unsigned long long* best;  // pass 1: min over H-setting breakpoints of the
                              // Harris ratio, as ordered bits (all values > 0)
   uint8_t* flags;            // pass 2: per list slot, kept for the host replay
+  const unsigned long long* bound;  // pass 2: the bound it filters with
 };
 
 struct RowSumArgs {
@@ -152,6 +153,15 @@ hipError_t row_sums(const milp_kernels::RowSumArgs& args, hipStream_t s);
 // Dual device mode.
 hipError_t dual_ratio_bound(const milp_kernels::DualRatioArgs& args, hipStream_t s);
 hipError_t dual_ratio_flags(const milp_kernels::DualRatioArgs& args, hipStream_t s);
+// Tighter bound: sort keys (ratio, order-preserving bits) of the pass-2 slots.
+hipError_t dual_ratio_keys(const milp_kernels::DualRatioArgs& args, const int32_t* slots,
+                           int num_slots, unsigned long long* keys, hipStream_t s);
+// Walks the ratio-sorted breakpoints the way the second Glop loop pops them
+// (flipping boxed ones while the variation stays positive) up to the first
+// accepted breakpoint; *bound2 = min(B, its Harris ratio) (or B = *args.best
+// on a ratio tie, where the pop order also depends on magnitudes).
+hipError_t dual_flip_walk(const milp_kernels::DualRatioArgs& args, const int32_t* sorted_slots,
+                          int num_slots, unsigned long long* bound2, hipStream_t s);
 // cand_* [k] = (list[slot], list_coeff[slot], rc[list[slot]]) for the flagged
 // slots k in slot order (flag compaction done by the caller).
 hipError_t gather_candidates(const int32_t* slots, const int* num_slots, int max_slots,

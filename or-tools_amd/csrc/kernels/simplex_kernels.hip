@@ -526,7 +526,8 @@ __global__ void tag_rows_kernel(const int32_t* filtered_rows, int n, uint32_t ta
 // One update-row slot as a breakpoint candidate (entering_variable.cc:68-96,
 // same expressions): returns false if the slot is not eligible.
 __device__ __forceinline__ bool dual_breakpoint(const DualRatioArgs& a, int slot, double* ratio,
-                                                double* harris, bool* sets_bound) {
+                                                double* harris, bool* sets_bound,
+                                                double* flip_delta = nullptr) {
   const int col = a.list[slot];
   const double c = a.list_coeff[slot];
   const double coeff = a.sign > 0.0 ? c : -c;
@@ -544,6 +545,8 @@ __device__ __forceinline__ bool dual_breakpoint(const DualRatioArgs& a, int slot
   *ratio = reduced_cost / magnitude;
   *harris = fmax(a.minimum_delta / magnitude, *ratio + a.harris_tolerance / magnitude);
   *sets_bound = !(bits & kColBoxed) || (a.bound_diff[col] * magnitude >= a.variation_magnitude);
+  // Variation a bound flip of this breakpoint absorbs (0: not boxed).
+  if (flip_delta != nullptr) *flip_delta = (bits & kColBoxed) ? a.bound_diff[col] * magnitude : 0.0;
   return true;
 }
 
@@ -580,7 +583,7 @@ __global__ __launch_bounds__(256) void dual_ratio_bound_kernel(DualRatioArgs a) 
 // replays Glop's two loops over them in list order.
 __global__ __launch_bounds__(256) void dual_ratio_flags_kernel(DualRatioArgs a) {
   const int n = *a.count;
-  const unsigned long long best = *a.best;
+  const unsigned long long best = *a.bound;
   const double bound = best == ~0ull ? HUGE_VAL
                                      : __longlong_as_double(static_cast<long long>(best)) *
                                            (1.0 + 1e-9);
@@ -594,6 +597,54 @@ __global__ __launch_bounds__(256) void dual_ratio_flags_kernel(DualRatioArgs a) 
     }
     a.flags[slot] = keep ? 1 : 0;
   }
+}
+
+__device__ __forceinline__ unsigned long long order_bits(double x) {
+  const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(x));
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__global__ void dual_ratio_keys_kernel(DualRatioArgs a, const int32_t* slots, int num_slots,
+                                       unsigned long long* keys) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < num_slots;
+       i += gridDim.x * blockDim.x) {
+    double ratio = 0.0, harris;
+    bool sets_bound;
+    dual_breakpoint(a, slots[i], &ratio, &harris, &sets_bound);
+    keys[i] = order_bits(ratio);
+  }
+}
+
+// One thread: entering_variable.cc:163-207 in pop order (ratio ascending;
+// a ratio tie would also order by magnitude and column, so it falls back).
+__global__ void dual_flip_walk_kernel(DualRatioArgs a, const int32_t* sorted_slots,
+                                      int num_slots, unsigned long long* bound2) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  double variation = a.variation_magnitude;
+  double prev_ratio = 0.0;
+  for (int i = 0; i < num_slots; ++i) {
+    double ratio, harris, delta;
+    bool sets_bound;
+    dual_breakpoint(a, sorted_slots[i], &ratio, &harris, &sets_bound, &delta);
+    if (i > 0 && ratio == prev_ratio) break;  // tie: keep the looser bound
+    prev_ratio = ratio;
+    if (variation > 0.0 && delta > 0.0) {
+      variation -= delta;
+      if (variation > 0.0) continue;  // flipped
+    }
+    // First accepted breakpoint: it caps harris_ratio at its Harris ratio.
+    if (i + 1 < num_slots) {
+      double next_ratio, h2, d2;
+      bool s2;
+      dual_breakpoint(a, sorted_slots[i + 1], &next_ratio, &h2, &s2, &d2);
+      if (next_ratio == ratio) break;
+    }
+    // harris_ratio <= min(B, its Harris ratio) from here on (B: pass 1).
+    const unsigned long long h = static_cast<unsigned long long>(__double_as_longlong(harris));
+    *bound2 = h < *a.best ? h : *a.best;
+    return;
+  }
+  *bound2 = *a.best;
 }
 
 __global__ void gather_candidates_kernel(const int32_t* slots, const int* num_slots,
@@ -830,6 +881,19 @@ hipError_t dual_ratio_bound(const DualRatioArgs& args, hipStream_t s) {
 
 hipError_t dual_ratio_flags(const DualRatioArgs& args, hipStream_t s) {
   dual_ratio_flags_kernel<<<grid_for(args.max_count), 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t dual_ratio_keys(const DualRatioArgs& args, const int32_t* slots, int num_slots,
+                           unsigned long long* keys, hipStream_t s) {
+  if (num_slots <= 0) return hipSuccess;
+  dual_ratio_keys_kernel<<<grid_for(num_slots), 256, 0, s>>>(args, slots, num_slots, keys);
+  return hipGetLastError();
+}
+
+hipError_t dual_flip_walk(const DualRatioArgs& args, const int32_t* sorted_slots,
+                          int num_slots, unsigned long long* bound2, hipStream_t s) {
+  dual_flip_walk_kernel<<<1, 64, 0, s>>>(args, sorted_slots, num_slots, bound2);
   return hipGetLastError();
 }
 

@@ -232,13 +232,15 @@ def _device_dual_cases():
     return cases
 
 
+@pytest.mark.parametrize("tighten", ["0", "100000000"])
 @pytest.mark.parametrize("case", _device_dual_cases(), ids=lambda c: c[0])
-def test_device_dual_mode_parity(case, monkeypatch):
+def test_device_dual_mode_parity(case, tighten, monkeypatch):
     """Dual phase II with the reduced costs and the update row kept on the
     device (device-filtered bound-flipping ratio test, device rc update,
     device boxed dual-feasibility decisions), forced on small LPs: every
     result must equal the oracle's, which runs Glop's host loops."""
     monkeypatch.setenv("MILP_DEVICE_DUAL", "force")
+    monkeypatch.setenv("MILP_DUAL_TIGHTEN_MIN", tighten)  # 0: always tighten
     lp = case[1]()
     p = abi.default_params(use_dual_simplex=1)
     o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
