@@ -125,6 +125,8 @@ class DeviceLp {
   void BeginKernel(int id);
   void EndKernel(int id, double bytes);
   void Compact(int n);  // flags_ -> list_ (ascending) + coefficients, async
+  void NextRowTag();
+  void CopyHost(void* dst, const void* src, size_t bytes);
   void AccountList(const std::vector<int>& positions);
   void BuildDenseBlock();
   // Launches the CSC kernel over the sparse columns (all columns when there is
@@ -204,6 +206,11 @@ class DeviceLp {
   // Above this many filtered rows the row-wise update row runs column by
   // column (MILP_ROWWISE_CHUNK_MAX_ROWS); both kernels give identical bits.
   int rowwise_chunk_max_rows_ = 16;
+  // Rows holding every structural column (MILP_FULL_ROWS=off disables the
+  // full-row kernel).
+  std::vector<uint8_t> h_row_full_;
+  int num_structural_ = 0;
+  bool full_rows_enabled_ = true;
   // The column-order kernel sorts a column's hits in registers: used only
   // when no column is longer than this (kernel kMaxColumnHits).
   static constexpr int kColumnKernelMaxColumnLength = 32;
@@ -212,6 +219,8 @@ class DeviceLp {
   // pinned staging
   int32_t* h_pin_i_ = nullptr;
   double* h_pin_d_ = nullptr;
+  int64_t* h_pin_off_ = nullptr;  // CSR row starts of the filtered rows (full-row kernel)
+  int64_t* d_row_offsets_ = nullptr;
   double* h_pin_d2_ = nullptr;
   double* h_pin_w_ = nullptr;
   int* h_pin_count_ = nullptr;

@@ -1,5 +1,6 @@
 // DeviceLp: device buffers + kernel launch plumbing (see device_lp.h).
 #include "device_lp.h"
+#include "host_pool.h"
 
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -46,6 +47,7 @@ DeviceLp::~DeviceLp() {
   if (h_pin_d_) (void)hipHostFree(h_pin_d_);
   if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
   if (h_pin_w_) (void)hipHostFree(h_pin_w_);
+  if (h_pin_off_) (void)hipHostFree(h_pin_off_);
   if (h_pin_count_) (void)hipHostFree(h_pin_count_);
   if (h_map_) (void)hipHostFree(h_map_);
   for (void* p : {static_cast<void*>(h_cand_col_), static_cast<void*>(h_cand_coeff_),
@@ -94,6 +96,9 @@ void DeviceLp::Init(int device) {
   }
   if (const char* r = std::getenv("MILP_ROWWISE_CHUNK_MAX_ROWS")) {
     rowwise_chunk_max_rows_ = std::atoi(r);
+  }
+  if (const char* f = std::getenv("MILP_FULL_ROWS")) {
+    full_rows_enabled_ = std::strcmp(f, "off") != 0;
   }
 }
 
@@ -153,6 +158,12 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   }
   h_starts_ = csc.starts_;
   h_t_starts_ = csr.starts_;
+  // Full rows: every structural column present (then entry j is column j).
+  num_structural_ = n_total_ - m_;
+  h_row_full_.assign(m_, 0);
+  for (int r = 0; r < m_; ++r) {
+    h_row_full_[r] = (csr.starts_[r + 1] - csr.starts_[r] == int64_t(num_structural_) + 1) ? 1 : 0;
+  }
   d_starts_ = Alloc<int64_t>(n_total_ + 1);
   d_rows_ = Alloc<int32_t>(nnz_);
   d_vals_ = Alloc<double>(nnz_);
@@ -189,6 +200,7 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   d_out_list_ = Alloc<double>(std::max(n_total_, m_));
   d_cols_ = Alloc<int32_t>(std::max(n_total_, m_));
   d_rho_vals_ = Alloc<double>(m_);
+  d_row_offsets_ = Alloc<int64_t>(m_ + 1);
   d_row_tag_ = Alloc<uint32_t>(m_);
   d_row_pos_ = Alloc<int32_t>(m_);
   Check(hipMemsetAsync(d_row_tag_, 0, std::max(1, m_) * sizeof(uint32_t), S(stream_)), "memset");
@@ -205,11 +217,13 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   if (h_pin_d_) (void)hipHostFree(h_pin_d_);
   if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
   if (h_pin_w_) (void)hipHostFree(h_pin_w_);
+  if (h_pin_off_) (void)hipHostFree(h_pin_off_);
   const size_t big = std::max(n_total_, m_) + 1;
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_i_), big * sizeof(int32_t)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d_), big * sizeof(double)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d2_), big * sizeof(double)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_w_), (m_ + 1) * sizeof(double)), "pin");
+  Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_off_), (m_ + 1) * sizeof(int64_t)), "pin");
   if (h_pin_count_ == nullptr) {
     Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_count_), sizeof(int)), "pin");
   }
@@ -432,16 +446,44 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
   a.algorithm = algorithm;
   const int id = algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW;
   BeginKernel(id);
+  bool all_full = full_rows_enabled_ && k > 0;
+  for (int i = 0; i < k && all_full; ++i) all_full = h_row_full_[filtered_rows[i]] != 0;
+  if (all_full) {
+    // Full rows: a thread per column reads each row's entry directly.
+    for (int i = 0; i < k; ++i) h_pin_off_[i] = h_t_starts_[filtered_rows[i]];
+    Upload(d_row_offsets_, h_pin_off_, k * sizeof(int64_t));
+    NextRowTag();
+    Check(milp_launch::tag_rows(d_cols_, k, row_tag_, d_row_tag_, d_row_pos_, S(stream_)),
+          "tag rows");
+    milp_kernels::RowWiseFullArgs f{};
+    f.t_starts = d_t_starts_;
+    f.t_vals = d_t_vals_;
+    f.row_offsets = d_row_offsets_;
+    f.rho = d_rho_vals_;
+    f.num_filtered = k;
+    f.num_structural = num_structural_;
+    f.num_cols = n_total_;
+    f.row_tag = d_row_tag_;
+    f.row_pos = d_row_pos_;
+    f.tag = row_tag_;
+    f.relevant = d_masks_[kRelevant];
+    f.coefficient = d_coeff_;
+    f.flags = d_flags_;
+    f.drop_tolerance = drop;
+    f.algorithm = algorithm;
+    Check(milp_launch::row_wise_update_full_rows(f, S(stream_)), "rowwise full rows");
+    // Values only (the column index of entry j is j), the list, the outputs.
+    EndKernel(id, 8.0 * double(k) * (num_structural_ + 1) + 12.0 * k + 9.0 * n_total_);
+    Compact(n_total_);
+    return;
+  }
   if (k <= rowwise_chunk_max_rows_ || max_col_len_ > kColumnKernelMaxColumnLength) {
     // Few rows: workgroups own column chunks and merge the rows in order.
     Check(milp_launch::row_wise_update(a, S(stream_)), "rowwise");
   } else {
     // Many rows: one thread per column gathers its filtered entries from the
     // CSC copy (same arithmetic, same order).
-    if (++row_tag_ == 0) {  // wrapped: clear the marks
-      Check(hipMemsetAsync(d_row_tag_, 0, m_ * sizeof(uint32_t), S(stream_)), "memset");
-      row_tag_ = 1;
-    }
+    NextRowTag();
     Check(milp_launch::tag_rows(d_cols_, k, row_tag_, d_row_tag_, d_row_pos_, S(stream_)),
           "tag rows");
     milp_kernels::RowWiseColArgs c{};
@@ -464,6 +506,13 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
   for (int r : filtered_rows) entries += double(h_t_starts_[r + 1] - h_t_starts_[r]);
   EndKernel(id, 12.0 * entries + 12.0 * k + 9.0 * n_total_);
   Compact(n_total_);
+}
+
+void DeviceLp::NextRowTag() {
+  if (++row_tag_ == 0) {  // wrapped: clear the marks
+    Check(hipMemsetAsync(d_row_tag_, 0, m_ * sizeof(uint32_t), S(stream_)), "memset");
+    row_tag_ = 1;
+  }
 }
 
 void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* values) {
@@ -502,23 +551,45 @@ void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* 
   positions->resize(n);
   values->resize(n);
   if (n > 0) {
-    std::memcpy(positions->data(), h_pin_i_, n * sizeof(int32_t));
-    std::memcpy(values->data(), h_pin_d_, n * sizeof(double));
+    CopyHost(positions->data(), h_pin_i_, n * sizeof(int32_t));
+    CopyHost(values->data(), h_pin_d_, n * sizeof(double));
   }
   AccountList(*positions);
 }
 
 // Byte accounting of the listed columns (ListDotsOverUpdateRow).
 void DeviceLp::AccountList(const std::vector<int>& positions) {
+  int64_t part_entries[16] = {0};
+  int64_t part_dense[16] = {0};
+  const bool has_dense = !h_is_dense_.empty();
+  const int parts = ParallelRanges(static_cast<int64_t>(positions.size()), 16384, 1,
+                                   [&](int p, int64_t b, int64_t e) {
+    int64_t entries = 0;
+    int64_t dense = 0;
+    for (int64_t k = b; k < e; ++k) {
+      const int c = positions[k];
+      if (has_dense && h_is_dense_[c]) {
+        ++dense;
+      } else {
+        entries += h_starts_[c + 1] - h_starts_[c];
+      }
+    }
+    part_entries[p] = entries;
+    part_dense[p] = dense;
+  });
   list_entries_ = 0;
   list_dense_ = 0;
-  for (const int c : positions) {
-    if (!h_is_dense_.empty() && h_is_dense_[c]) {
-      ++list_dense_;
-    } else {
-      list_entries_ += h_starts_[c + 1] - h_starts_[c];
-    }
+  for (int p = 0; p < parts; ++p) {
+    list_entries_ += part_entries[p];
+    list_dense_ += part_dense[p];
   }
+}
+
+// memcpy split over the host pool (large host <-> pinned staging copies).
+void DeviceLp::CopyHost(void* dst, const void* src, size_t bytes) {
+  ParallelRanges(static_cast<int64_t>(bytes), 1 << 18, 4096, [&](int, int64_t b, int64_t e) {
+    std::memcpy(static_cast<char*>(dst) + b, static_cast<const char*>(src) + b, e - b);
+  });
 }
 
 double DeviceLp::ReadCoefficient(int col) {
@@ -592,7 +663,7 @@ void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& 
   fused_ready_ = false;  // d_out_n_ is reused below
   const bool fused = (w != nullptr);
   if (fused && list_dots == nullptr) throw DeviceError("fused pricing needs list_dots");
-  std::memcpy(h_pin_d_, c.data(), n_total_ * sizeof(double));
+  CopyHost(h_pin_d_, c.data(), n_total_ * sizeof(double));
   Upload(d_vec_n_, h_pin_d_, n_total_ * sizeof(double));
   std::memcpy(h_pin_d2_, y.data(), m_ * sizeof(double));
   Upload(d_vec_m_, h_pin_d2_, m_ * sizeof(double));
@@ -627,8 +698,8 @@ void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& 
     }
   }
   Download(h_pin_d_, d_out_n_, n_total_ * sizeof(double));
-  std::memcpy(rc->data(), h_pin_d_, n_total_ * sizeof(double));
-  if (fused && n_list > 0) std::memcpy(list_dots->data(), h_pin_d2_, n_list * sizeof(double));
+  CopyHost(rc->data(), h_pin_d_, n_total_ * sizeof(double));
+  if (fused && n_list > 0) CopyHost(list_dots->data(), h_pin_d2_, n_list * sizeof(double));
 }
 
 void DeviceLp::ColumnSquaredNorms(std::vector<double>* out) {

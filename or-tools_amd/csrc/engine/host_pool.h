@@ -1,0 +1,183 @@
+// Fork-join pool for the engine's O(N) host loops.
+//
+// Only element-independent work is split: every element is computed by the
+// same expression as in the serial loop and written to its own slot, and
+// anything order-dependent (the DynamicMaximum top-k heap, RNG draws) is
+// replayed serially afterwards, in the serial loop's order. Results therefore
+// do not depend on the number of threads or on the partition.
+//
+// One process-wide pool. A caller that finds it busy (another handle's loop)
+// runs all parts itself. MILP_HOST_THREADS sets the thread count (caller
+// included; 1 disables the pool).
+#ifndef MILP_HOST_POOL_H_
+#define MILP_HOST_POOL_H_
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace milp {
+
+class HostPool {
+ public:
+  static HostPool& Get() {
+    static HostPool pool;
+    return pool;
+  }
+  int threads() const { return num_threads_; }
+
+  // fn(part) for part in [0, parts); part 0 runs on the caller.
+  void Run(int parts, const std::function<void(int)>& fn) {
+    if (parts <= 1 || num_threads_ <= 1) {
+      for (int p = 0; p < parts; ++p) fn(p);
+      return;
+    }
+    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+    if (!busy.owns_lock()) {
+      for (int p = 0; p < parts; ++p) fn(p);
+      return;
+    }
+    // Publish the job (its pointer last), then wake the workers; sleeping
+    // ones need the condition variable, spinning ones see the generation.
+    next_part_.store(1, std::memory_order_relaxed);
+    pending_.store(parts - 1, std::memory_order_relaxed);
+    job_parts_.store(parts, std::memory_order_relaxed);
+    job_.store(&fn, std::memory_order_release);
+    generation_.fetch_add(1, std::memory_order_acq_rel);
+    if (sleepers_.load(std::memory_order_acquire) > 0) {
+      { std::lock_guard<std::mutex> l(mu_); }
+      cv_.notify_all();
+    }
+    fn(0);
+    // The caller helps with the parts no worker has picked up yet.
+    for (int p = next_part_.fetch_add(1, std::memory_order_acq_rel); p < parts;
+         p = next_part_.fetch_add(1, std::memory_order_acq_rel)) {
+      fn(p);
+      pending_.fetch_sub(1, std::memory_order_acq_rel);
+    }
+    while (pending_.load(std::memory_order_acquire) != 0) Pause();
+    // Retire the job; return only when no worker can still be reading it.
+    job_.store(nullptr, std::memory_order_release);
+    while (active_.load(std::memory_order_acquire) != 0) Pause();
+  }
+
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_.store(true, std::memory_order_release);
+      generation_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    for (std::thread& t : workers_) t.join();
+  }
+
+ private:
+  HostPool() {
+    int n = 4;
+    if (const char* e = std::getenv("MILP_HOST_THREADS")) n = std::atoi(e);
+    const int hw = static_cast<int>(std::thread::hardware_concurrency());
+    if (hw > 0) n = std::min(n, hw);
+    num_threads_ = std::max(1, std::min(n, 16));
+    for (int i = 1; i < num_threads_; ++i) workers_.emplace_back([this]() { Work(); });
+  }
+  static void Pause() { __builtin_ia32_pause(); }
+
+  void Work() {
+    uint64_t seen = 0;
+    while (true) {
+      // Spin (the engine's loops come every few hundred microseconds while
+      // a solve runs), then sleep until the next job.
+      uint64_t g = generation_.load(std::memory_order_acquire);
+      if (g == seen) {
+        const auto start = std::chrono::steady_clock::now();
+        for (int spin = 1; g == seen; ++spin) {
+          Pause();
+          g = generation_.load(std::memory_order_acquire);
+          if ((spin & 1023) == 0 &&
+              std::chrono::steady_clock::now() - start > std::chrono::milliseconds(5)) {
+            break;
+          }
+        }
+      }
+      if (g == seen) {
+        std::unique_lock<std::mutex> l(mu_);
+        sleepers_.fetch_add(1, std::memory_order_acq_rel);
+        cv_.wait(l, [&]() { return generation_.load(std::memory_order_acquire) != seen; });
+        sleepers_.fetch_sub(1, std::memory_order_acq_rel);
+        g = generation_.load(std::memory_order_acquire);
+      }
+      seen = g;
+      if (stop_.load(std::memory_order_acquire)) return;
+      active_.fetch_add(1, std::memory_order_acq_rel);
+      const std::function<void(int)>* job = job_.load(std::memory_order_acquire);
+      if (job != nullptr) {
+        const int parts = job_parts_.load(std::memory_order_relaxed);
+        for (int p = next_part_.fetch_add(1, std::memory_order_acq_rel); p < parts;
+             p = next_part_.fetch_add(1, std::memory_order_acq_rel)) {
+          (*job)(p);
+          pending_.fetch_sub(1, std::memory_order_acq_rel);
+        }
+      }
+      active_.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+
+  int num_threads_ = 1;
+  std::vector<std::thread> workers_;
+  std::mutex run_mu_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> generation_{0};
+  std::atomic<int> next_part_{0};
+  std::atomic<int> pending_{0};
+  std::atomic<int> active_{0};
+  std::atomic<const std::function<void(int)>*> job_{nullptr};
+  std::atomic<int> job_parts_{0};
+  std::atomic<int> sleepers_{0};
+  std::atomic<bool> stop_{false};
+};
+
+// Splits [0, n) into at most HostPool threads parts whose boundaries are
+// multiples of `align` (64 keeps bitset words whole), and runs
+// fn(part, begin, end) on each. Runs serially when n < min_parallel.
+// MILP_HOST_PARALLEL_MIN overrides every size threshold (tests set it low to
+// run the split loops on small LPs).
+inline int64_t ParallelMinOverride() {
+  const char* e = std::getenv("MILP_HOST_PARALLEL_MIN");
+  return e != nullptr ? std::atoll(e) : -1;
+}
+
+template <typename F>
+int ParallelRanges(int64_t n, int64_t min_parallel, int64_t align, F&& fn) {
+  HostPool& pool = HostPool::Get();
+  const int64_t override_min = ParallelMinOverride();
+  if (override_min >= 0) min_parallel = override_min;
+  int parts = (n >= min_parallel && n > 0) ? pool.threads() : 1;
+  if (const char* cap = std::getenv("MILP_HOST_THREADS")) {  // read per call: probes vary it
+    parts = std::max(1, std::min(parts, std::atoi(cap)));
+  }
+  if (parts <= 1) {
+    fn(0, int64_t{0}, n);
+    return 1;
+  }
+  const int64_t per = ((n + parts - 1) / parts + align - 1) / align * align;
+  parts = static_cast<int>((n + per - 1) / per);
+  const std::function<void(int)> job = [&](int p) {
+    const int64_t b = p * per;
+    const int64_t e = std::min(n, b + per);
+    fn(p, b, e);
+  };
+  pool.Run(parts, job);
+  return parts;
+}
+
+}  // namespace milp
+
+#endif  // MILP_HOST_POOL_H_

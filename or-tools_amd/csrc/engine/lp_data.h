@@ -118,6 +118,7 @@ class Bitset {
   }
   uint64_t Word(int b) const { return w_[b]; }
   const uint64_t* data() const { return w_.data(); }
+  uint64_t* mutable_data() { return w_.data(); }
   int NumWords() const { return static_cast<int>(w_.size()); }
   template <typename F>
   void ForEach(F&& f) const {

@@ -23,6 +23,7 @@
 
 #include "../../../include/mi_lp.h"
 #include "device_lp.h"
+#include "host_pool.h"
 
 #include <chrono>
 
@@ -779,14 +780,26 @@ void UpdateRow::ComputeUpdateRow(int leaving_row) {
 // the listed positions.
 void UpdateRow::FetchFromDevice() {
   ++epoch_;
-  for (const int col : non_zero_position_list_) listed_[col] = 0;
-  dev_->FetchUpdateRow(&non_zero_position_list_, &fetched_values_);
-  const int n = static_cast<int>(non_zero_position_list_.size());
-  for (int k = 0; k < n; ++k) {
-    const int col = non_zero_position_list_[k];
-    listed_[col] = 1;
-    coefficient_[col] = fetched_values_[k];
+  {
+    const int* pos = non_zero_position_list_.data();
+    char* listed = listed_.data();
+    ParallelRanges(static_cast<int64_t>(non_zero_position_list_.size()), 16384, 1,
+                   [&](int, int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k) listed[pos[k]] = 0;
+    });
   }
+  dev_->FetchUpdateRow(&non_zero_position_list_, &fetched_values_);
+  const int* pos = non_zero_position_list_.data();
+  const Fractional* vals = fetched_values_.data();
+  char* listed = listed_.data();
+  Fractional* coeff = coefficient_.data();
+  ParallelRanges(static_cast<int64_t>(non_zero_position_list_.size()), 16384, 1,
+                 [&](int, int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) {
+      listed[pos[k]] = 1;
+      coeff[pos[k]] = vals[k];
+    }
+  });
 }
 
 // update_row.cc:196-216
@@ -966,6 +979,11 @@ class PrimalEdgeNorms {
   void UpdateEdgeSquaredNorms(int entering_col, int leaving_col, int leaving_row,
                               const std::vector<Fractional>& direction,
                               const UpdateRow& update_row);
+  void ApplyNormUpdate(const std::vector<int>& positions,
+                       const std::vector<Fractional>& coefficients,
+                       const std::vector<Fractional>& dots, Fractional pivot,
+                       Fractional leaving_squared_norm);
+  int64_t CountEntries(const std::vector<int>& positions) const;
   void DeferEdgeSquaredNormsUpdate(int entering_col, int leaving_col, int leaving_row,
                                    const std::vector<Fractional>& direction,
                                    const UpdateRow& update_row);
@@ -1091,23 +1109,47 @@ void PrimalEdgeNorms::UpdateEdgeSquaredNorms(int entering_col, int leaving_col,
   const Fractional entering_squared_norm = edge_squared_norms_[entering_col];
   const Fractional leaving_squared_norm =
       std::max(1.0, entering_squared_norm / Square(pivot));
-  const Fractional factor = 2.0 / pivot;
   SubTimer timer(kSubNormLoop);
   // a_j . (B^-T d) for every listed column in one GPU pass.
   dev_->ListDotsOverUpdateRow(direction_left_inverse_.values, &dots_);
   const std::vector<int>& positions = update_row.GetNonZeroPositions();
-  const std::vector<Fractional>& coefficients = update_row.GetCoefficients();
-  for (size_t k = 0; k < positions.size(); ++k) {
-    const int col = positions[k];
-    const Fractional coeff = coefficients[col];
-    const Fractional scalar_product = dots_[k];
-    num_operations_ += matrix_.ColumnNumEntries(col);
-    edge_squared_norms_[col] +=
-        coeff * (coeff * leaving_squared_norm + factor * scalar_product);
-    const Fractional lower_bound = 1.0 + Square(coeff / pivot);
-    if (edge_squared_norms_[col] < lower_bound) edge_squared_norms_[col] = lower_bound;
-  }
+  num_operations_ += CountEntries(positions);
+  ApplyNormUpdate(positions, update_row.GetCoefficients(), dots_, pivot, leaving_squared_norm);
   edge_squared_norms_[leaving_col] = leaving_squared_norm;
+}
+
+// The per-column loop of UpdateEdgeSquaredNorms (primal_edge_norms.cc:229-
+// 244), positions in parallel (each writes its own norm).
+void PrimalEdgeNorms::ApplyNormUpdate(const std::vector<int>& positions,
+                                      const std::vector<Fractional>& coefficients,
+                                      const std::vector<Fractional>& dots, Fractional pivot,
+                                      Fractional leaving_squared_norm) {
+  const Fractional factor = 2.0 / pivot;
+  Fractional* norms = edge_squared_norms_.data();
+  const Fractional* coeffs = coefficients.data();
+  ParallelRanges(static_cast<int64_t>(positions.size()), 16384, 1,
+                 [&](int, int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) {
+      const int col = positions[k];
+      const Fractional coeff = coeffs[col];
+      norms[col] += coeff * (coeff * leaving_squared_norm + factor * dots[k]);
+      const Fractional lower_bound = 1.0 + Square(coeff / pivot);
+      if (norms[col] < lower_bound) norms[col] = lower_bound;
+    }
+  });
+}
+
+int64_t PrimalEdgeNorms::CountEntries(const std::vector<int>& positions) const {
+  std::vector<int64_t> part(HostPool::Get().threads(), 0);
+  const int parts = ParallelRanges(static_cast<int64_t>(positions.size()), 16384, 1,
+                                   [&](int p, int64_t b, int64_t e) {
+    int64_t n = 0;
+    for (int64_t k = b; k < e; ++k) n += matrix_.ColumnNumEntries(positions[k]);
+    part[p] = n;
+  });
+  int64_t total = 0;
+  for (int p = 0; p < parts; ++p) total += part[p];
+  return total;
 }
 
 // UpdateEdgeSquaredNorms split in two: the scalars now, the loop over the
@@ -1120,9 +1162,7 @@ void PrimalEdgeNorms::DeferEdgeSquaredNormsUpdate(int entering_col, int leaving_
   const Fractional entering_squared_norm = edge_squared_norms_[entering_col];
   pending_leaving_squared_norm_ =
       std::max(1.0, entering_squared_norm / Square(pending_pivot_));
-  for (const int col : update_row.GetNonZeroPositions()) {
-    num_operations_ += matrix_.ColumnNumEntries(col);
-  }
+  num_operations_ += CountEntries(update_row.GetNonZeroPositions());
   // The leaving column is basic, hence not relevant and never one of the
   // listed positions: its final value can be written now.
   edge_squared_norms_[leaving_col] = pending_leaving_squared_norm_;
@@ -1138,19 +1178,12 @@ void PrimalEdgeNorms::CompletePendingUpdate(const std::vector<Fractional>& dots)
   if (pending_update_row_->epoch() != pending_row_epoch_) {
     throw DeviceError("update row recomputed under a parked edge-norm update");
   }
-  const Fractional pivot = pending_pivot_;
-  const Fractional leaving_squared_norm = pending_leaving_squared_norm_;
-  const Fractional factor = 2.0 / pivot;
   const std::vector<int>& positions = pending_update_row_->GetNonZeroPositions();
-  const std::vector<Fractional>& coefficients = pending_update_row_->GetCoefficients();
   if (dots.size() != positions.size()) throw DeviceError("edge-norm dots size mismatch");
-  SubTimer timer(kSubNormLoop);
-  for (size_t k = 0; k < positions.size(); ++k) {
-    const int col = positions[k];
-    const Fractional coeff = coefficients[col];
-    edge_squared_norms_[col] += coeff * (coeff * leaving_squared_norm + factor * dots[k]);
-    const Fractional lower_bound = 1.0 + Square(coeff / pivot);
-    if (edge_squared_norms_[col] < lower_bound) edge_squared_norms_[col] = lower_bound;
+  {
+    SubTimer timer(kSubNormLoop);
+    ApplyNormUpdate(positions, pending_update_row_->GetCoefficients(), dots, pending_pivot_,
+                    pending_leaving_squared_norm_);
   }
   if (on_complete_) on_complete_();
 }
@@ -1573,10 +1606,16 @@ void ReducedCosts::UpdateReducedCosts(int entering_col, int leaving_col, int lea
   are_reduced_costs_precise_ = false;
   update_row->ComputeUpdateRow(leaving_row);
   const Fractional new_leaving_reduced_cost = entering_reduced_cost / -pivot;
-  for (const int col : update_row->GetNonZeroPositions()) {
-    const Fractional coeff = update_row->GetCoefficient(col);
-    reduced_costs_[col] += new_leaving_reduced_cost * coeff;
-  }
+  const std::vector<int>& positions = update_row->GetNonZeroPositions();
+  const Fractional* coeffs = update_row->GetCoefficients().data();
+  Fractional* rc = reduced_costs_.data();
+  ParallelRanges(static_cast<int64_t>(positions.size()), 16384, 1,
+                 [&](int, int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) {
+      const int col = positions[k];
+      rc[col] += new_leaving_reduced_cost * coeffs[col];
+    }
+  });
   reduced_costs_[leaving_col] = new_leaving_reduced_cost;
   reduced_costs_[entering_col] = 0.0;
 }
@@ -1686,21 +1725,12 @@ class PrimalPrices {
         if (block_row_->epoch() != block_epoch_) {
           throw DeviceError("update row recomputed under queued price updates");
         }
-        for (const int col : block_row_->GetNonZeroPositions()) {
-          const bool add = col == block_entering_col_
-                               ? block_entering_infeasible_
-                               : IsDualInfeasible(col, rc[col], block_tolerance_);
-          if (add) {
-            const Fractional price = Square(rc[col]) / sn[col];
-            if (before_clear) {
-              prices_.AddOrUpdateBeforeClear(col, price);
-            } else {
-              prices_.AddOrUpdate(col, price);
-            }
-          } else if (!before_clear) {
-            prices_.Remove(col);
-          }
-        }
+        const int entering = block_entering_col_;
+        const bool entering_infeasible = block_entering_infeasible_;
+        const Fractional tolerance = block_tolerance_;
+        UpdatePricesOver(block_row_->GetNonZeroPositions(), !before_clear, [&](int col) {
+          return col == entering ? entering_infeasible : IsDualInfeasible(col, rc[col], tolerance);
+        }, rc.data(), sn.data());
       } else if (op.kind == kAdd) {
         const Fractional price = Square(rc[op.col]) / sn[op.col];
         if (before_clear) {
@@ -1730,22 +1760,91 @@ class PrimalPrices {
     const uint64_t* rel = relevant.data();
     const Fractional* sn = primal_edge_norms_->GetSquaredNorms().data();
     const Fractional* rc = reduced_costs_->GetReducedCosts().data();
+    Fractional* values = prices_.mutable_values();
+    uint64_t* candidate = prices_.mutable_candidate_words();
     const int num_words = relevant.NumWords();
-    for (int w = 0; w < num_words; ++w) {
-      uint64_t bits = rel[w];
-      const uint64_t dec_w = dec[w];
-      const uint64_t inc_w = inc[w];
-      while (bits != 0) {
-        const int b = __builtin_ctzll(bits);
-        bits &= bits - 1;
-        const int col = (w << 6) + b;
-        const Fractional reduced_cost = rc[col];
-        const bool is_dual_infeasible = ((reduced_cost > tolerance) && ((dec_w >> b) & 1)) !=
-                                        ((reduced_cost < -tolerance) && ((inc_w >> b) & 1));
-        if (is_dual_infeasible) prices_.AddOrUpdate(col, Square(reduced_cost) / sn[col]);
+    part_adds_.resize(HostPool::Get().threads());
+    // Words are split whole, so each candidate word has one writer.
+    const int parts = ParallelRanges(num_words, kMinParallelWords, 1,
+                                     [&](int p, int64_t w0, int64_t w1) {
+      // A local vector (header on this thread's stack), handed back at the end.
+      std::vector<PriceUpdate> adds;
+      adds.swap(part_adds_[p].v);
+      adds.clear();
+      for (int64_t w = w0; w < w1; ++w) {
+        uint64_t bits = rel[w];
+        const uint64_t dec_w = dec[w];
+        const uint64_t inc_w = inc[w];
+        uint64_t set = 0;
+        while (bits != 0) {
+          const int b = __builtin_ctzll(bits);
+          bits &= bits - 1;
+          const int col = static_cast<int>(w << 6) + b;
+          const Fractional reduced_cost = rc[col];
+          const bool is_dual_infeasible = ((reduced_cost > tolerance) && ((dec_w >> b) & 1)) !=
+                                          ((reduced_cost < -tolerance) && ((inc_w >> b) & 1));
+          if (is_dual_infeasible) {
+            const Fractional price = Square(reduced_cost) / sn[col];
+            values[col] = price;
+            set |= uint64_t{1} << b;
+            adds.push_back(PriceUpdate{col, price});
+          }
+        }
+        candidate[w] |= set;
       }
+      part_adds_[p].v.swap(adds);
+    });
+    for (int p = 0; p < parts; ++p) {
+      for (const PriceUpdate& u : part_adds_[p].v) prices_.ReplayTopK(u.col, u.price);
     }
   }
+  // The per-position loop of UpdateEnteringCandidates / the queued
+  // update-row block: add(col) decides dual infeasibility; with
+  // write_state, AddOrUpdate or Remove, else only the top-k bookkeeping of
+  // the adds (AddOrUpdateBeforeClear). Prices and candidate bits are written
+  // in parallel (positions are distinct; bits with atomic word updates), the
+  // top-k replay runs serially in position order.
+  template <typename AddFn>
+  void UpdatePricesOver(const std::vector<int>& cols, bool write_state, AddFn&& add,
+                        const Fractional* rc, const Fractional* sn) {
+    Fractional* values = prices_.mutable_values();
+    uint64_t* candidate = prices_.mutable_candidate_words();
+    part_adds_.resize(HostPool::Get().threads());
+    const int parts = ParallelRanges(static_cast<int64_t>(cols.size()), kMinParallelPositions, 1,
+                                     [&](int p, int64_t b, int64_t e) {
+      std::vector<PriceUpdate> adds;
+      adds.swap(part_adds_[p].v);
+      adds.clear();
+      for (int64_t k = b; k < e; ++k) {
+        const int col = cols[k];
+        const uint64_t mask = uint64_t{1} << (col & 63);
+        if (add(col)) {
+          const Fractional price = Square(rc[col]) / sn[col];
+          if (write_state) {
+            values[col] = price;
+            __atomic_fetch_or(&candidate[col >> 6], mask, __ATOMIC_RELAXED);
+          }
+          adds.push_back(PriceUpdate{col, price});
+        } else if (write_state) {
+          __atomic_fetch_and(&candidate[col >> 6], ~mask, __ATOMIC_RELAXED);
+        }
+      }
+      part_adds_[p].v.swap(adds);
+    });
+    for (int p = 0; p < parts; ++p) {
+      for (const PriceUpdate& u : part_adds_[p].v) prices_.ReplayTopK(u.col, u.price);
+    }
+  }
+  struct PriceUpdate {
+    int col;
+    Fractional price;
+  };
+  static constexpr int64_t kMinParallelWords = 256;        // 16384 columns
+  static constexpr int64_t kMinParallelPositions = 16384;
+  struct alignas(64) PartAdds {
+    std::vector<PriceUpdate> v;
+  };
+  std::vector<PartAdds> part_adds_;
   template <bool from_clean_state>
   void UpdateEnteringCandidates(const std::vector<int>& cols) {
     const Fractional tolerance = reduced_costs_->GetDualFeasibilityTolerance();
@@ -1753,17 +1852,12 @@ class PrimalPrices {
     const Bitset& inc = variables_info_.GetCanIncreaseBitRow();
     const std::vector<Fractional>& sn = primal_edge_norms_->GetSquaredNorms();
     const std::vector<Fractional>& rc = reduced_costs_->GetReducedCosts();
-    for (const int col : cols) {
+    UpdatePricesOver(cols, true, [&](int col) {
       const Fractional reduced_cost = rc[col];
-      const bool is_dual_infeasible =
-          ((reduced_cost > tolerance) && dec.IsSet(col)) !=
-          ((reduced_cost < -tolerance) && inc.IsSet(col));
-      if (is_dual_infeasible) {
-        prices_.AddOrUpdate(col, Square(reduced_cost) / sn[col]);
-      } else {
-        if (!from_clean_state) prices_.Remove(col);
-      }
-    }
+      return ((reduced_cost > tolerance) && dec.IsSet(col)) !=
+             ((reduced_cost < -tolerance) && inc.IsSet(col));
+    }, rc.data(), sn.data());
+    (void)from_clean_state;  // a clean state has no candidate to remove
   }
   bool recompute_ = true;
   DynamicMaximum prices_;

@@ -156,6 +156,14 @@ class DynamicMaximum {
     if (value >= threshold_) UpdateTopK(position, value);
   }
   int GetMaximum();
+  // Bulk access for the parallel host loops (host_pool.h): the values and
+  // candidate bits are written element by element in parallel, then the
+  // top-k bookkeeping of each AddOrUpdate is replayed serially, in order.
+  Fractional* mutable_values() { return values_.data(); }
+  uint64_t* mutable_candidate_words() { return is_candidate_.mutable_data(); }
+  void ReplayTopK(int position, Fractional value) {
+    if (value >= threshold_) UpdateTopK(position, value);
+  }
 
  private:
   struct HeapElement {

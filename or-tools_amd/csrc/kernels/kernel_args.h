@@ -65,6 +65,27 @@ struct RowWiseArgs {
   int algorithm;  // 0 single row, 1 hypersparse, 2 row-wise
 };
 
+// The row-wise update row when every filtered row is full (all structural
+// columns present): entry j < num_structural of CSR row r is column j and the
+// row's last entry is its slack column. Slack outputs use the row tags.
+struct RowWiseFullArgs {
+  const int64_t* t_starts;  // CSR of [A | I]
+  const double* t_vals;
+  const int64_t* row_offsets;  // t_starts of each filtered row, list order k
+  const double* rho;           // rho value per filtered row
+  int num_filtered;
+  int num_structural;
+  int num_cols;
+  const uint32_t* row_tag;
+  const int32_t* row_pos;
+  uint32_t tag;
+  const uint64_t* relevant;
+  double* coefficient;
+  uint8_t* flags;
+  double drop_tolerance;
+  int algorithm;
+};
+
 // The same row-wise update row evaluated column by column from the CSC copy
 // (for many filtered rows): row r of the filtered list sits at position
 // row_pos[r] when row_tag[r] == tag.
@@ -149,6 +170,7 @@ hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s)
 hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag,
                     uint32_t* row_tag, int32_t* row_pos, hipStream_t s);
 hipError_t row_wise_update_by_column(const milp_kernels::RowWiseColArgs& args, hipStream_t s);
+hipError_t row_wise_update_full_rows(const milp_kernels::RowWiseFullArgs& args, hipStream_t s);
 hipError_t row_sums(const milp_kernels::RowSumArgs& args, hipStream_t s);
 // Dual device mode.
 hipError_t dual_ratio_bound(const milp_kernels::DualRatioArgs& args, hipStream_t s);

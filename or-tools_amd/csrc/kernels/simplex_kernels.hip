@@ -509,6 +509,65 @@ __global__ __launch_bounds__(256) void row_wise_by_column_kernel(RowWiseColArgs 
   a.flags[col] = listed ? 1 : 0;
 }
 
+// ---------------------------------------------------------------------------
+// Row-wise update row over full rows (config 2's dense A). A thread owns one
+// column and reads that column's entry of each filtered row directly (no
+// search): lanes of a wave read consecutive entries of one CSR row, and the
+// row start (uploaded per filtered row) and rho value are wave-uniform
+// (scalar loads). The loads of
+// kFullRowsUnroll rows are in flight before their products are accumulated,
+// in list order k, with the first-write rule of row_wise_update_kernel.
+constexpr int kFullRowsUnroll = 16;
+
+__global__ __launch_bounds__(256) void row_wise_full_rows_kernel(RowWiseFullArgs a) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= a.num_cols) return;
+  double acc = 0.0;
+  bool touched = false;
+  if (col < a.num_structural) {
+    const int num = a.num_filtered;
+    int k = 0;
+    for (; k + kFullRowsUnroll <= num; k += kFullRowsUnroll) {
+      double v[kFullRowsUnroll];
+#pragma unroll
+      for (int u = 0; u < kFullRowsUnroll; ++u) {
+        v[u] = a.t_vals[a.row_offsets[k + u] + col];
+      }
+#pragma unroll
+      for (int u = 0; u < kFullRowsUnroll; ++u) {
+        acc = row_wise_accumulate(acc, !touched, a.rho[k + u] * v[u], a.algorithm);
+        touched = true;
+      }
+    }
+    for (; k < num; ++k) {
+      acc = row_wise_accumulate(acc, !touched, a.rho[k] * a.t_vals[a.row_offsets[k] + col],
+                                a.algorithm);
+      touched = true;
+    }
+  } else {
+    const int r = col - a.num_structural;
+    if (a.row_tag[r] == a.tag) {
+      const int k = a.row_pos[r];
+      acc = row_wise_accumulate(0.0, true, a.rho[k] * a.t_vals[a.t_starts[r + 1] - 1],
+                                a.algorithm);
+      touched = true;
+    }
+  }
+  const bool rel = bit_set(a.relevant, col);
+  bool listed;
+  if (a.algorithm == 0) {
+    listed = touched && rel && fabs(acc) > a.drop_tolerance;
+    if (listed) a.coefficient[col] = acc;
+  } else if (a.algorithm == 1) {
+    listed = touched && rel && fabs(acc) > a.drop_tolerance;
+    if (touched) a.coefficient[col] = acc;
+  } else {
+    listed = rel && fabs(acc) > a.drop_tolerance;
+    a.coefficient[col] = touched ? acc : 0.0;
+  }
+  a.flags[col] = listed ? 1 : 0;
+}
+
 __global__ void tag_rows_kernel(const int32_t* filtered_rows, int n, uint32_t tag,
                                 uint32_t* row_tag, int32_t* row_pos) {
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
@@ -711,36 +770,91 @@ __global__ void boxed_flips_kernel(const int32_t* cols, int n, const double* rc,
 // ---------------------------------------------------------------------------
 // Row sums sum_j mult_j * A[r, j] in increasing j (the order the host scatter
 // ColumnAddMultipleToDenseColumn produces), zero multipliers skipped
-// (sparse.h:393). One wave per row: lanes load 64 consecutive CSR entries,
-// lane 0 folds the products in order.
+// (sparse.h:393). A workgroup owns kSumRows rows and walks them in chunks of
+// kSumChunk entries: both waves load their rows' chunk (coalesced, one row
+// per wave instruction) and write the products transposed into LDS, then lane
+// i of wave 0 adds row i's chunk in entry order. A skipped entry is stored as
+// -0.0, which leaves every sum unchanged (x + -0.0 == x, also for x = +-0.0).
+// Chunk c + 1 is loaded while chunk c is added (double buffer).
+constexpr int kSumRows = 32;
+constexpr int kSumChunk = 64;
+constexpr int kSumRowsPerWave = kSumRows / 2;
 
-__global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= a.num_rows) return;  // whole wave exits together
-  const int64_t s = a.t_starts[row];
-  const int64_t e = a.t_starts[row + 1];
-  double acc = 0.0;
-  for (int64_t base = s; base < e; base += kWave) {
-    const int64_t i = base + lane;
-    double p = 0.0;
-    bool use = false;
-    if (i < e) {
-      const int col = a.t_cols[i];
-      double m = a.x[col];
-      if (a.skip != nullptr && bit_set(a.skip, col)) m = 0.0;
-      m = a.sign * m;  // exact (sign is +-1)
-      use = (m != 0.0);
-      p = m * a.t_vals[i];
-    }
-    const int nvalid = (e - base) < kWave ? static_cast<int>(e - base) : kWave;
-    for (int t = 0; t < kWave; ++t) {
-      const double q = __shfl(p, t, kWave);
-      const int u = __shfl(static_cast<int>(use), t, kWave);
-      if (t < nvalid && u) acc += q;
-    }
+__device__ __forceinline__ void row_sum_load(const RowSumArgs& a, const int64_t* rs,
+                                             const int64_t* re, int chunk, int wave, int lane,
+                                             double* p) {
+  int64_t idx[kSumRowsPerWave];
+  int col[kSumRowsPerWave];
+#pragma unroll
+  for (int j = 0; j < kSumRowsPerWave; ++j) {
+    const int i = wave * kSumRowsPerWave + j;
+    idx[j] = rs[i] + int64_t(chunk) * kSumChunk + lane;
+    col[j] = idx[j] < re[i] ? a.t_cols[idx[j]] : -1;
   }
-  if (lane == 0) a.out[row] = acc;
+#pragma unroll
+  for (int j = 0; j < kSumRowsPerWave; ++j) {
+    double m = 0.0;
+    if (col[j] >= 0) {
+      m = a.x[col[j]];
+      if (a.skip != nullptr && bit_set(a.skip, col[j])) m = 0.0;
+      m = a.sign * m;  // exact (sign is +-1)
+    }
+    p[j] = m != 0.0 ? m * a.t_vals[idx[j]] : -0.0;
+  }
+}
+
+__global__ __launch_bounds__(128) void row_sum_kernel(RowSumArgs a) {
+  __shared__ double tile[2][kSumChunk][kSumRows + 1];
+  __shared__ int64_t rs[kSumRows];
+  __shared__ int64_t re[kSumRows];
+  __shared__ int num_chunks;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * kSumRows;
+  if (wave == 0) {
+    int chunks = 0;
+    if (lane < kSumRows) {
+      const int row = r0 + lane;
+      int64_t s = 0;
+      int64_t e = 0;
+      if (row < a.num_rows) {
+        s = a.t_starts[row];
+        e = a.t_starts[row + 1];
+      }
+      rs[lane] = s;
+      re[lane] = e;
+      chunks = static_cast<int>((e - s + kSumChunk - 1) / kSumChunk);
+    }
+    for (int off = 32; off > 0; off >>= 1) chunks = max(chunks, __shfl_xor(chunks, off));
+    if (lane == 0) num_chunks = chunks;
+  }
+  __syncthreads();
+  const int nchunks = num_chunks;
+  double p[kSumRowsPerWave];
+  if (nchunks > 0) {
+    row_sum_load(a, rs, re, 0, wave, lane, p);
+#pragma unroll
+    for (int j = 0; j < kSumRowsPerWave; ++j) tile[0][lane][wave * kSumRowsPerWave + j] = p[j];
+  }
+  __syncthreads();
+  double acc = 0.0;
+  for (int c = 0; c < nchunks; ++c) {
+    const int b = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) row_sum_load(a, rs, re, c + 1, wave, lane, p);
+    if (wave == 0 && lane < kSumRows) {
+#pragma unroll 16
+      for (int e = 0; e < kSumChunk; ++e) acc += tile[b][e][lane];
+    }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < kSumRowsPerWave; ++j) {
+        tile[b ^ 1][lane][wave * kSumRowsPerWave + j] = p[j];
+      }
+    }
+    __syncthreads();
+  }
+  if (wave == 0 && lane < kSumRows && r0 + lane < a.num_rows) a.out[r0 + lane] = acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -872,6 +986,12 @@ hipError_t row_wise_update_by_column(const RowWiseColArgs& args, hipStream_t s) 
   return hipGetLastError();
 }
 
+hipError_t row_wise_update_full_rows(const RowWiseFullArgs& args, hipStream_t s) {
+  if (args.num_cols <= 0) return hipSuccess;
+  row_wise_full_rows_kernel<<<div_up(args.num_cols, 256), 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
 static inline int grid_for(int n) { return std::max(1, std::min(4096, div_up(n, 256))); }
 
 hipError_t dual_ratio_bound(const DualRatioArgs& args, hipStream_t s) {
@@ -937,7 +1057,7 @@ hipError_t boxed_flips(const int32_t* cols, int n, const double* rc, const uint8
 
 hipError_t row_sums(const RowSumArgs& args, hipStream_t s) {
   if (args.num_rows <= 0) return hipSuccess;
-  row_sum_kernel<<<div_up(args.num_rows, 4), 256, 0, s>>>(args);
+  row_sum_kernel<<<div_up(args.num_rows, kSumRows), 128, 0, s>>>(args);
   return hipGetLastError();
 }
 

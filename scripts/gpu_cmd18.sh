@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "host_parallel" > gpurun_out/gpu_tests_hp.log 2>&1 || { echo "host-parallel tests failed"; tail -60 gpurun_out/gpu_tests_hp.log; exit 1; }
+tail -1 gpurun_out/gpu_tests_hp.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
+bash scripts/gpu_phase.sh

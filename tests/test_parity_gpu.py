@@ -99,6 +99,40 @@ def test_row_wise_kernel_choice_parity(seed, chunk_max, monkeypatch):
     assert st["update_row"]["launches"] > 0
 
 
+@pytest.mark.parametrize("full_rows", ["on", "off"])
+@pytest.mark.parametrize("dual", [0, 1])
+@pytest.mark.parametrize("shape", [(97, 500, 31), (160, 1200, 32)])
+def test_full_row_kernel_parity(shape, dual, full_rows, monkeypatch):
+    """Dense A: every CSR row holds all structural columns, so row-wise
+    update rows go through the full-row kernel (direct entry addressing, list
+    order k, slack outputs through the row tags) unless disabled. Both ways
+    must match the oracle bit for bit, in primal and dual simplex."""
+    monkeypatch.setenv("MILP_FULL_ROWS", full_rows)
+    m, n, seed = shape
+    lp = lp_gen.dense_box_lp(m, n, seed)
+    p = abi.default_params(use_dual_simplex=dual)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    st = g.kernel_stats()
+    assert st["update_row"]["launches"] + st["single_row"]["launches"] > 0
+
+
+def test_full_and_partial_rows_parity(monkeypatch):
+    """Some rows full, some not: a filtered list that mixes them takes the
+    general row-wise kernels, an all-full list the full-row kernel."""
+    rng = np.random.default_rng(9)
+    m, n = 70, 400
+    dense = rng.uniform(-1, 1, size=(m, n))
+    holes = rng.random(size=(m, n)) < 0.3
+    holes[: m // 2] = False  # the first half of the rows stays full
+    dense[holes] = 0.0
+    lp = lp_gen.from_dense_box(dense, rng)
+    for dual in (0, 1):
+        p = abi.default_params(use_dual_simplex=dual)
+        o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+        parity_util.compare(o, ro, g, rg, lp)
+
+
 @pytest.mark.parametrize("unroll", ["8", "32"])
 def test_dense_block_unroll_parity(unroll, monkeypatch):
     """The dense-block kernel's load depth does not change any result."""
@@ -264,3 +298,19 @@ def test_device_dual_mode_warm_start_and_children(monkeypatch):
         ro2 = o.solve()
         rg2 = g.solve()
         parity_util.compare(o, ro2, g, rg2, lp)
+
+
+@pytest.mark.parametrize("dual", [0, 1])
+@pytest.mark.parametrize("case", ["dense", "sparse"])
+def test_host_parallel_loops_parity(case, dual, monkeypatch):
+    """The engine's O(N) host loops (price rebuild and updates, edge-norm
+    update, reduced-cost update, dual prices, update-row fetch) split over the
+    host pool at every size: results must not change."""
+    monkeypatch.setenv("MILP_HOST_PARALLEL_MIN", "1")
+    if case == "dense":
+        lp = lp_gen.dense_box_lp(120, 900, 41)
+    else:
+        lp = lp_gen.sparse_c5_lp(400, 4000, 6, 42)
+    p = abi.default_params(use_dual_simplex=dual)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
