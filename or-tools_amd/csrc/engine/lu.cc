@@ -1,6 +1,13 @@
 // Host basis factorization of the MI355X simplex engine (see lu.h).
 #include "lu.h"
 
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+
 namespace milp {
 
 // ---------------------------------------------------------------------------
@@ -414,26 +421,26 @@ Fractional ComputeSquaredNormAndResetToZero(const std::vector<int>& nz,
 Fractional LuFactorization::RightSolveSquaredNorm(const ColumnView& a) const {
   if (is_identity_factorization_) return SquaredNorm(a);
   non_zero_rows_.clear();
-  dense_zero_scratchpad_.resize(lower_.num_rows(), 0.0);
+  DenseZeroScratch().resize(lower_.num_rows(), 0.0);
   for (int64_t i = 0; i < a.n; ++i) {
     const int permuted_row = row_perm_[a.rows[i]];
-    dense_zero_scratchpad_[permuted_row] = a.coefs[i];
+    DenseZeroScratch()[permuted_row] = a.coefs[i];
     non_zero_rows_.push_back(permuted_row);
   }
   lower_.ComputeRowsToConsiderInSortedOrder(&non_zero_rows_);
   if (non_zero_rows_.empty()) {
-    lower_.LowerSolve(&dense_zero_scratchpad_);
+    lower_.LowerSolve(&DenseZeroScratch());
   } else {
-    lower_.HyperSparseSolve(&dense_zero_scratchpad_, &non_zero_rows_);
+    lower_.HyperSparseSolve(&DenseZeroScratch(), &non_zero_rows_);
     upper_.ComputeRowsToConsiderInSortedOrder(&non_zero_rows_);
   }
   if (non_zero_rows_.empty()) {
-    upper_.UpperSolve(&dense_zero_scratchpad_);
+    upper_.UpperSolve(&DenseZeroScratch());
   } else {
-    upper_.HyperSparseSolveWithReversedNonZeros(&dense_zero_scratchpad_,
+    upper_.HyperSparseSolveWithReversedNonZeros(&DenseZeroScratch(),
                                                 &non_zero_rows_);
   }
-  return ComputeSquaredNormAndResetToZero(non_zero_rows_, &dense_zero_scratchpad_);
+  return ComputeSquaredNormAndResetToZero(non_zero_rows_, &DenseZeroScratch());
 }
 
 // lu_factorization.cc:158-186
@@ -441,23 +448,23 @@ Fractional LuFactorization::DualEdgeSquaredNorm(int row) const {
   if (is_identity_factorization_) return 1.0;
   const int permuted_row = col_perm_.empty() ? row : col_perm_[row];
   non_zero_rows_.clear();
-  dense_zero_scratchpad_.resize(lower_.num_rows(), 0.0);
-  dense_zero_scratchpad_[permuted_row] = 1.0;
+  DenseZeroScratch().resize(lower_.num_rows(), 0.0);
+  DenseZeroScratch()[permuted_row] = 1.0;
   non_zero_rows_.push_back(permuted_row);
   transpose_upper_.ComputeRowsToConsiderInSortedOrder(&non_zero_rows_);
   if (non_zero_rows_.empty()) {
-    transpose_upper_.LowerSolveStartingAt(permuted_row, &dense_zero_scratchpad_);
+    transpose_upper_.LowerSolveStartingAt(permuted_row, &DenseZeroScratch());
   } else {
-    transpose_upper_.HyperSparseSolve(&dense_zero_scratchpad_, &non_zero_rows_);
+    transpose_upper_.HyperSparseSolve(&DenseZeroScratch(), &non_zero_rows_);
     transpose_lower_.ComputeRowsToConsiderInSortedOrder(&non_zero_rows_);
   }
   if (non_zero_rows_.empty()) {
-    transpose_lower_.UpperSolve(&dense_zero_scratchpad_);
+    transpose_lower_.UpperSolve(&DenseZeroScratch());
   } else {
-    transpose_lower_.HyperSparseSolveWithReversedNonZeros(&dense_zero_scratchpad_,
+    transpose_lower_.HyperSparseSolveWithReversedNonZeros(&DenseZeroScratch(),
                                                           &non_zero_rows_);
   }
-  return ComputeSquaredNormAndResetToZero(non_zero_rows_, &dense_zero_scratchpad_);
+  return ComputeSquaredNormAndResetToZero(non_zero_rows_, &DenseZeroScratch());
 }
 
 // lu_factorization.cc:200-212
@@ -530,24 +537,24 @@ void LuFactorization::RightSolveLWithNonZeros(ScatteredVector* x) const {
   if (is_identity_factorization_) return;
   if (x->non_zeros.empty()) {
     // PermuteWithScratchpad (lp_utils.h:240-257)
-    dense_zero_scratchpad_.assign(x->values.size(), 0.0);
-    dense_zero_scratchpad_.swap(x->values);
-    x->values.assign(dense_zero_scratchpad_.size(), 0.0);
-    for (size_t i = 0; i < dense_zero_scratchpad_.size(); ++i) {
-      const Fractional v = dense_zero_scratchpad_[i];
+    DenseZeroScratch().assign(x->values.size(), 0.0);
+    DenseZeroScratch().swap(x->values);
+    x->values.assign(DenseZeroScratch().size(), 0.0);
+    for (size_t i = 0; i < DenseZeroScratch().size(); ++i) {
+      const Fractional v = DenseZeroScratch()[i];
       if (v != 0.0) x->values[row_perm_[i]] = v;
     }
-    dense_zero_scratchpad_.assign(x->values.size(), 0.0);
+    DenseZeroScratch().assign(x->values.size(), 0.0);
     lower_.LowerSolve(&x->values);
     return;
   }
   // PermuteWithKnownNonZeros (lp_utils.h:262-277)
-  dense_zero_scratchpad_.assign(x->values.size(), 0.0);
-  dense_zero_scratchpad_.swap(x->values);
-  x->values.assign(dense_zero_scratchpad_.size(), 0.0);
+  DenseZeroScratch().assign(x->values.size(), 0.0);
+  DenseZeroScratch().swap(x->values);
+  x->values.assign(DenseZeroScratch().size(), 0.0);
   for (int& ref : x->non_zeros) {
-    const Fractional v = dense_zero_scratchpad_[ref];
-    dense_zero_scratchpad_[ref] = 0.0;
+    const Fractional v = DenseZeroScratch()[ref];
+    DenseZeroScratch()[ref] = 0.0;
     const int p = row_perm_[ref];
     x->values[p] = v;
     ref = p;
@@ -617,21 +624,21 @@ bool LuFactorization::LeftSolveLWithNonZeros(
   }
   if (result_before_permutation == nullptr) {
     if (nz->empty()) {
-      dense_zero_scratchpad_.assign(x->size(), 0.0);
-      dense_zero_scratchpad_.swap(*x);
-      x->assign(dense_zero_scratchpad_.size(), 0.0);
-      for (size_t i = 0; i < dense_zero_scratchpad_.size(); ++i) {
-        const Fractional v = dense_zero_scratchpad_[i];
+      DenseZeroScratch().assign(x->size(), 0.0);
+      DenseZeroScratch().swap(*x);
+      x->assign(DenseZeroScratch().size(), 0.0);
+      for (size_t i = 0; i < DenseZeroScratch().size(); ++i) {
+        const Fractional v = DenseZeroScratch()[i];
         if (v != 0.0) (*x)[inverse_row_perm_[i]] = v;
       }
-      dense_zero_scratchpad_.assign(x->size(), 0.0);
+      DenseZeroScratch().assign(x->size(), 0.0);
     } else {
-      dense_zero_scratchpad_.assign(x->size(), 0.0);
-      dense_zero_scratchpad_.swap(*x);
-      x->assign(dense_zero_scratchpad_.size(), 0.0);
+      DenseZeroScratch().assign(x->size(), 0.0);
+      DenseZeroScratch().swap(*x);
+      x->assign(DenseZeroScratch().size(), 0.0);
       for (int& ref : *nz) {
-        const Fractional v = dense_zero_scratchpad_[ref];
-        dense_zero_scratchpad_[ref] = 0.0;
+        const Fractional v = DenseZeroScratch()[ref];
+        DenseZeroScratch()[ref] = 0.0;
         const int p = inverse_row_perm_[ref];
         (*x)[p] = v;
         ref = p;
@@ -700,7 +707,112 @@ const SparseColumn& LuFactorization::GetColumnOfU(int col) const {
 
 // ---------------------------------------------------------------------------
 // BasisFactorization (basis_representation.cc:176-627)
+
+// One worker thread, one job at a time (the tau FTRAN).
+struct BasisFactorization::AsyncWorker {
+  AsyncWorker() : thread([this]() { Loop(); }) {}
+  ~AsyncWorker() {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    thread.join();
+  }
+  void Submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      job = std::move(f);
+      busy = true;
+    }
+    cv.notify_all();
+  }
+  void Wait() {
+    std::unique_lock<std::mutex> l(mu);
+    done_cv.wait(l, [&]() { return !busy; });
+  }
+  void Loop() {
+    g_lu_slot = 1;
+    std::unique_lock<std::mutex> l(mu);
+    while (true) {
+      cv.wait(l, [&]() { return stop || static_cast<bool>(job); });
+      if (stop) return;
+      std::function<void()> f = std::move(job);
+      job = nullptr;
+      l.unlock();
+      f();
+      l.lock();
+      busy = false;
+      done_cv.notify_all();
+    }
+  }
+  std::mutex mu;
+  std::condition_variable cv;
+  std::condition_variable done_cv;
+  std::function<void()> job;
+  bool busy = false;
+  bool stop = false;
+  std::thread thread;
+};
+
+BasisFactorization::BasisFactorization(const CompactSparseMatrix* matrix,
+                                       const std::vector<int>* basis)
+    : compact_matrix_(*matrix), basis_(*basis) {
+  if (const char* e = std::getenv("MILP_ASYNC_TAU")) {
+    if (std::strcmp(e, "off") == 0) async_min_rows_ = -1;
+    if (std::strcmp(e, "force") == 0) async_min_rows_ = 0;
+  }
+}
+
+BasisFactorization::~BasisFactorization() {
+  if (async_) async_->Wait();
+}
+
+bool BasisFactorization::AsyncTauEnabled() const {
+  return async_min_rows_ >= 0 && compact_matrix_.num_rows() >= async_min_rows_;
+}
+
+// The body of RightSolveForTau (basis_representation.cc:374-398) into *out,
+// without the flag updates.
+void BasisFactorization::ComputeTauInto(bool can_be_optimized, const ScatteredVector& a,
+                                        ScatteredVector* out) const {
+  if (can_be_optimized) {
+    lu_factorization_.RightSolveLWithPermutedInput(a.values, out);
+  } else {
+    ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), out);
+    lu_factorization_.RightSolveLForScatteredColumn(a, out);
+  }
+  rank_one_factorization_.RightSolveWithNonZeros(out);
+  lu_factorization_.RightSolveUWithNonZeros(out);
+  BumpDeterministicTimeForSolve(static_cast<int64_t>(out->NumNonZerosEstimate()));
+}
+
+void BasisFactorization::StartAsyncTau(const ScatteredVector& rho) const {
+  SyncAsyncTau();
+  if (!AsyncTauEnabled()) return;
+  if (!async_) async_.reset(new AsyncWorker());
+  const bool can_be_optimized = tau_computation_can_be_optimized_;
+  async_pending_ = true;
+  async_input_ = &rho;
+  async_->Submit([this, can_be_optimized, &rho]() {
+    // The permuted intermediate of the last BTRAN is copied, not consumed:
+    // a discarded result leaves tau_ as the serial code would.
+    if (can_be_optimized) async_tau_ = tau_;
+    ComputeTauInto(can_be_optimized, rho, &async_tau_);
+  });
+}
+
+void BasisFactorization::SyncAsyncTau() const {
+  if (!async_pending_) return;
+  async_->Wait();
+  async_pending_ = false;
+  async_input_ = nullptr;
+  rank_one_factorization_.TakeDeferredBumps(false);
+  deferred_solve_entries_.clear();
+}
+
 void BasisFactorization::Clear() {
+  SyncAsyncTau();
   num_updates_ = 0;
   tau_computation_can_be_optimized_ = false;
   lu_factorization_.Clear();
@@ -712,6 +824,7 @@ void BasisFactorization::Clear() {
 }
 
 Status BasisFactorization::Initialize() {
+  SyncAsyncTau();
   Clear();
   if (IsIdentityBasis()) return Status::OK();
   return ComputeFactorization();
@@ -719,6 +832,7 @@ Status BasisFactorization::Initialize() {
 
 std::vector<int> BasisFactorization::ComputeInitialBasis(
     const std::vector<int>& candidates) {
+  SyncAsyncTau();
   std::vector<int> basis =
       lu_factorization_.ComputeInitialBasis(compact_matrix_, candidates);
   deterministic_time_ += lu_factorization_.DeterministicTimeOfLastFactorization();
@@ -731,6 +845,7 @@ Status BasisFactorization::Refactorize() {
 }
 
 Status BasisFactorization::ForceRefactorization() {
+  SyncAsyncTau();
   Clear();
   return ComputeFactorization();
 }
@@ -785,6 +900,7 @@ Status BasisFactorization::MiddleProductFormUpdate(int entering_col,
 // basis_representation.cc:304-340
 Status BasisFactorization::Update(int entering_col, int leaving_variable_row,
                                   const ScatteredVector& /*direction*/) {
+  SyncAsyncTau();
   if (num_updates_ >= max_num_updates_) {
     if (!dynamic_period_) return ForceRefactorization();
     if (last_factorization_deterministic_time_ <
@@ -819,6 +935,21 @@ void BasisFactorization::RightSolve(ScatteredVector* d) const {
 // basis_representation.cc:374-398
 const std::vector<Fractional>& BasisFactorization::RightSolveForTau(
     const ScatteredVector& a) const {
+  if (async_pending_ && async_input_ == &a) {
+    async_->Wait();
+    async_pending_ = false;
+    async_input_ = nullptr;
+    // The worker's deterministic-time bumps land now, where the serial
+    // solve would have made them.
+    rank_one_factorization_.TakeDeferredBumps(true);
+    for (const int64_t n : deferred_solve_entries_) BumpDeterministicTimeForSolve(n);
+    deferred_solve_entries_.clear();
+    std::swap(tau_, async_tau_);
+    tau_computation_can_be_optimized_ = false;
+    tau_is_computed_ = true;
+    return tau_.values;
+  }
+  SyncAsyncTau();
   if (tau_computation_can_be_optimized_) {
     tau_computation_can_be_optimized_ = false;
     lu_factorization_.RightSolveLWithPermutedInput(a.values, &tau_);
@@ -835,6 +966,7 @@ const std::vector<Fractional>& BasisFactorization::RightSolveForTau(
 
 // basis_representation.cc:400-453
 void BasisFactorization::LeftSolveForUnitRow(int j, ScatteredVector* y) const {
+  SyncAsyncTau();
   ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), y);
   if (j >= static_cast<int>(left_pool_mapping_.size())) {
     left_pool_mapping_.resize(j + 1, kInvalidCol);
@@ -865,6 +997,7 @@ void BasisFactorization::LeftSolveForUnitRow(int j, ScatteredVector* y) const {
 
 // basis_representation.cc:455-466
 void BasisFactorization::TemporaryLeftSolveForUnitRow(int j, ScatteredVector* y) const {
+  SyncAsyncTau();
   ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), y);
   lu_factorization_.LeftSolveUForUnitRow(j, y);
   lu_factorization_.LeftSolveLWithNonZeros(y, nullptr);
@@ -925,6 +1058,10 @@ Fractional BasisFactorization::ComputeInfinityNormConditionNumberUpperBound() co
 
 // basis_representation.cc:607-624
 void BasisFactorization::BumpDeterministicTimeForSolve(int64_t num_entries) const {
+  if (g_lu_slot != 0) {  // tau worker: applied when the result is taken
+    deferred_solve_entries_.push_back(num_entries);
+    return;
+  }
   if (compact_matrix_.num_rows() == 0) return;
   const double density = static_cast<double>(num_entries) /
                          static_cast<double>(compact_matrix_.num_rows());

@@ -7,11 +7,16 @@
 #ifndef MILP_LU_H_
 #define MILP_LU_H_
 
+#include <memory>
 #include <string>
 
 #include "lp_data.h"
 
 namespace milp {
+
+// Which copy of the solve scratch a thread uses: 0 on the solver's thread,
+// 1 on BasisFactorization's tau worker (the two run FTRANs concurrently).
+inline thread_local int g_lu_slot = 0;
 
 // ---------------------------------------------------------------------------
 // TriangularMatrix (sparse.h:583-921).
@@ -356,6 +361,7 @@ class TriangularMatrix : public CompactSparseMatrix {
                                      const std::vector<int>& row_perm,
                                      std::vector<int>* lower_rows,
                                      std::vector<int>* upper_rows) {
+    std::vector<char>& stored_ = stored_slots_[g_lu_slot];
     stored_.resize(num_rows_, false);
     marked_.resize(num_rows_, false);
     lower_rows->clear();
@@ -421,6 +427,7 @@ class TriangularMatrix : public CompactSparseMatrix {
   // sparse.cc:1445-1492 (the ratio arguments are ignored upstream).
   void ComputeRowsToConsiderInSortedOrder(std::vector<int>* nz) const {
     if (nz->empty()) return;
+    std::vector<char>& stored_ = stored_slots_[g_lu_slot];
     const int sparsity_threshold = static_cast<int>(0.025 * num_rows_);
     const int num_ops_threshold = static_cast<int>(0.05 * num_rows_);
     int num_ops = static_cast<int>(nz->size());
@@ -470,7 +477,7 @@ class TriangularMatrix : public CompactSparseMatrix {
   std::vector<int64_t> pruned_ends_;
 
  private:
-  mutable std::vector<char> stored_;
+  mutable std::vector<char> stored_slots_[2];
   std::vector<char> marked_;
   std::vector<int> nodes_to_explore_;
   int64_t num_fp_operations_ = 0;
@@ -833,7 +840,10 @@ class LuFactorization {
   std::vector<int> row_perm_;
   std::vector<int> inverse_row_perm_;
   mutable std::vector<Fractional> dense_column_scratchpad_;
-  mutable std::vector<Fractional> dense_zero_scratchpad_;
+  mutable std::vector<Fractional> dense_zero_scratchpad_slots_[2];
+  std::vector<Fractional>& DenseZeroScratch() const {
+    return dense_zero_scratchpad_slots_[g_lu_slot];
+  }
   mutable std::vector<int> non_zero_rows_;
   mutable SparseColumn column_of_upper_;
   Markowitz markowitz_;
@@ -898,7 +908,7 @@ class RankOneUpdateFactorization {
   void LeftSolve(std::vector<Fractional>* y) const {
     for (int i = static_cast<int>(elementary_matrices_.size()) - 1; i >= 0; --i)
       elementary_matrices_[i].LeftSolve(y);
-    dtime_ += DeterministicTimeForFpOperations(num_entries_);
+    BumpTime();
   }
   void LeftSolveWithNonZeros(ScatteredVector* y) const {
     if (y->non_zeros.empty()) {
@@ -917,12 +927,12 @@ class RankOneUpdateFactorization {
     }
     y->ClearSparseMask();
     y->ClearNonZerosIfTooDense(hypersparse_ratio_);
-    dtime_ += DeterministicTimeForFpOperations(num_entries_);
+    BumpTime();
   }
   void RightSolve(std::vector<Fractional>* d) const {
     for (size_t i = 0; i < elementary_matrices_.size(); ++i)
       elementary_matrices_[i].RightSolve(d);
-    dtime_ += DeterministicTimeForFpOperations(num_entries_);
+    BumpTime();
   }
   void RightSolveWithNonZeros(ScatteredVector* d) const {
     if (d->non_zeros.empty()) {
@@ -941,15 +951,30 @@ class RankOneUpdateFactorization {
     }
     d->ClearSparseMask();
     d->ClearNonZerosIfTooDense(hypersparse_ratio_);
-    dtime_ += DeterministicTimeForFpOperations(num_entries_);
+    BumpTime();
   }
   int64_t num_entries() const { return num_entries_; }
+  // A solve on the tau worker defers its bump; the solver's thread applies
+  // it (or drops it, if the result is discarded) in program order.
+  void BumpTime() const {
+    if (g_lu_slot != 0) {
+      ++deferred_bumps_;
+      return;
+    }
+    dtime_ += DeterministicTimeForFpOperations(num_entries_);
+  }
+  void TakeDeferredBumps(bool apply) const {
+    for (; deferred_bumps_ > 0; --deferred_bumps_) {
+      if (apply) dtime_ += DeterministicTimeForFpOperations(num_entries_);
+    }
+  }
   double DeterministicTimeSinceLastReset() const { return dtime_; }
   void ResetDeterministicTime() { dtime_ = 0.0; }
   int size() const { return static_cast<int>(elementary_matrices_.size()); }
 
  private:
   mutable double dtime_ = 0.0;
+  mutable int deferred_bumps_ = 0;
   double hypersparse_ratio_ = 0.05;
   int64_t num_entries_ = 0;
   std::vector<RankOneUpdateElementaryMatrix> elementary_matrices_;
@@ -958,10 +983,24 @@ class RankOneUpdateFactorization {
 // basis_representation.cc:176-627 (middle-product-form path).
 class BasisFactorization {
  public:
-  BasisFactorization(const CompactSparseMatrix* matrix, const std::vector<int>* basis)
-      : compact_matrix_(*matrix), basis_(*basis) {}
+  BasisFactorization(const CompactSparseMatrix* matrix, const std::vector<int>* basis);
+  ~BasisFactorization();
+  BasisFactorization(const BasisFactorization&) = delete;
+  BasisFactorization& operator=(const BasisFactorization&) = delete;
+
+  // Tau FTRAN off the solver's thread (engine scheduling, no Glop
+  // counterpart). The dual loop knows rho, the only input of
+  // RightSolveForTau, right after the BTRAN; the worker computes tau then,
+  // while the update row, ratio test and direction FTRAN run. The next
+  // RightSolveForTau(rho) takes the result; any other use of the
+  // factorization first waits for the worker and drops it. The solve is the
+  // same code on a private scratch copy, and its deterministic-time bumps are
+  // applied when it is taken, so results and timing match the serial order.
+  void StartAsyncTau(const ScatteredVector& rho) const;
+  bool AsyncTauEnabled() const;
   void SetParameters(int refactorization_period, bool dynamic_period,
                      const LuParameters& lu) {
+    SyncAsyncTau();
     max_num_updates_ = refactorization_period;
     dynamic_period_ = dynamic_period;
     lu_factorization_.SetParameters(lu);
@@ -991,9 +1030,13 @@ class BasisFactorization {
     return lu_factorization_.GetColumnPermutation();
   }
   void SetColumnPermutationToIdentity() {
+    SyncAsyncTau();
     lu_factorization_.SetColumnPermutationToIdentity();
   }
-  void SetLuParameters(const LuParameters& lu) { lu_factorization_.SetParameters(lu); }
+  void SetLuParameters(const LuParameters& lu) {
+    SyncAsyncTau();
+    lu_factorization_.SetParameters(lu);
+  }
   const LuFactorization& lu() const { return lu_factorization_; }
 
   // basis_representation.cc:607-624 (public: replayed by the GPU paths).
@@ -1003,8 +1046,20 @@ class BasisFactorization {
   Status ComputeFactorization();
   Status MiddleProductFormUpdate(int entering_col, int leaving_variable_row);
 
+  // Waits for the tau worker; drop=true discards its result.
+  void SyncAsyncTau() const;
+  void ComputeTauInto(bool can_be_optimized, const ScatteredVector& a,
+                      ScatteredVector* out) const;
+
   const CompactSparseMatrix& compact_matrix_;
   const std::vector<int>& basis_;
+  struct AsyncWorker;
+  mutable std::unique_ptr<AsyncWorker> async_;
+  mutable bool async_pending_ = false;
+  mutable const ScatteredVector* async_input_ = nullptr;
+  mutable ScatteredVector async_tau_;
+  mutable std::vector<int64_t> deferred_solve_entries_;
+  int async_min_rows_ = 16384;
   mutable bool tau_is_computed_ = false;
   mutable bool tau_computation_can_be_optimized_ = false;
   mutable ScatteredVector tau_;

@@ -550,6 +550,8 @@ class DualEdgeNorms {
     norms_[leaving_row] = leaving_squared_norm;
     return old_squared_norm > 0.25 * leaving_squared_norm;
   }
+  // UpdateBeforeBasisPivot will compute tau (if the iteration gets there).
+  bool WillComputeTau() const { return !recompute_; }
   // dual_edge_norms.cc:82-118
   void UpdateBeforeBasisPivot(int /*entering_col*/, int leaving_row,
                               const ScatteredVector& direction,
@@ -4294,6 +4296,11 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
         variable_values_.UpdateDualPrices({leaving_row});
       }
       continue;
+    }
+    // tau = B^-1 rho needs only rho: it is computed on the factorization's
+    // worker thread while the update row, ratio test and direction run.
+    if (dual_edge_norms_.WillComputeTau()) {
+      basis_factorization_.StartAsyncTau(update_row_.GetUnitRowLeftInverse());
     }
     update_row_.ComputeUpdateRow(leaving_row);
     if (!dual_device_mode_) update_row_.GetNonZeroPositions();  // timed as the update row

@@ -23,7 +23,11 @@ GROUPS = {  # HIP kernel name fragment -> engine kernel id (bench.py names)
     "dense_dot_kernel<0,": "update_row", "column_dot_kernel<0,": "update_row",
     "dense_dot_kernel<4,": "update_row", "column_dot_kernel<4,": "update_row",
     "row_wise_update_kernel": "update_row", "row_wise_by_column_kernel": "update_row",
-    "tag_rows_kernel": "update_row",
+    "tag_rows_kernel": "update_row", "row_wise_full_rows_kernel": "update_row",
+    "dual_ratio_bound_kernel": "dual_ratio", "dual_ratio_flags_kernel": "dual_ratio",
+    "dual_ratio_keys_kernel": "dual_ratio", "dual_flip_walk_kernel": "dual_ratio",
+    "gather_candidates_kernel": "dual_ratio", "boxed_flips_kernel": "dual_ratio",
+    "update_reduced_costs_kernel": "rc_update",
     "dense_dot_kernel<2,": "primal_norms", "column_dot_kernel<2,": "primal_norms",
     "row_sum_kernel": "spmv_rows", "column_squared_norm_kernel": "col_norms",
 }
@@ -35,7 +39,10 @@ GROUPS = {  # HIP kernel name fragment -> engine kernel id (bench.py names)
 PRIMARY = {
     "pricing": [["dense_dot_kernel<5,", "dense_dot_kernel<1,"],
                 ["column_dot_kernel<5,", "column_dot_kernel<1,"]],
+    "dual_ratio": [["dual_ratio_bound_kernel"]],
+    "rc_update": [["update_reduced_costs_kernel"]],
     "update_row": [["row_wise_update_kernel", "row_wise_by_column_kernel",
+                    "row_wise_full_rows_kernel",
                     "dense_dot_kernel<0,", "dense_dot_kernel<4,"],
                    ["column_dot_kernel<0,", "column_dot_kernel<4,"]],
     "primal_norms": [["dense_dot_kernel<2,"], ["column_dot_kernel<2,"]],

@@ -314,3 +314,19 @@ def test_host_parallel_loops_parity(case, dual, monkeypatch):
     p = abi.default_params(use_dual_simplex=dual)
     o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
     parity_util.compare(o, ro, g, rg, lp)
+
+
+@pytest.mark.parametrize("seed", [51, 52, 53])
+@pytest.mark.parametrize("device_dual", ["off", "force"])
+def test_async_tau_parity(seed, device_dual, monkeypatch):
+    """The dual loop's tau FTRAN runs on the factorization's worker thread
+    (MILP_ASYNC_TAU=force at test size) while the update row, ratio test and
+    direction FTRAN run: same results, same iteration count, and the same
+    deterministic time, since the worker's bumps are applied in serial order."""
+    monkeypatch.setenv("MILP_ASYNC_TAU", "force")
+    monkeypatch.setenv("MILP_DEVICE_DUAL", device_dual)
+    lp = lp_gen.sparse_c5_lp(500 + 40 * (seed % 3), 5000, 6, seed)
+    p = abi.default_params(use_dual_simplex=1)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    assert rg.deterministic_time == ro.deterministic_time
