@@ -342,29 +342,78 @@ struct SparseColumn {
   ColumnView view() const {
     return ColumnView{rows.data(), coefs.data(), num_entries()};
   }
-  // sparse_vector.h:546-580
+  // sparse_vector.h:546-580: entries sorted by row (stable), zeros
+  // dropped, of equal rows only the last kept. Already strictly increasing
+  // rows need no sort; long columns use a stable LSD radix sort on the row,
+  // which orders exactly as the stable comparison sort does.
   void CleanUp() {
-    std::vector<std::pair<int, Fractional>> e;
-    e.reserve(rows.size());
-    for (size_t i = 0; i < rows.size(); ++i) e.emplace_back(rows[i], coefs[i]);
-    std::stable_sort(e.begin(), e.end(),
-                     [](const std::pair<int, Fractional>& a,
-                        const std::pair<int, Fractional>& b) {
-                       return a.first < b.first;
-                     });
+    const size_t n = rows.size();
+    bool sorted = true;
+    for (size_t i = 1; i < n; ++i) {
+      if (rows[i] <= rows[i - 1]) {
+        sorted = false;
+        break;
+      }
+    }
+    if (!sorted) {
+      if (n >= 256) {
+        RadixSortByRow();
+      } else {
+        std::vector<std::pair<int, Fractional>> e;
+        e.reserve(n);
+        for (size_t i = 0; i < n; ++i) e.emplace_back(rows[i], coefs[i]);
+        std::stable_sort(e.begin(), e.end(),
+                         [](const std::pair<int, Fractional>& a,
+                            const std::pair<int, Fractional>& b) {
+                           return a.first < b.first;
+                         });
+        for (size_t i = 0; i < n; ++i) {
+          rows[i] = e[i].first;
+          coefs[i] = e[i].second;
+        }
+      }
+    }
     size_t new_size = 0;
-    const size_t n = e.size();
     for (size_t i = 0; i < n; ++i) {
-      if (e[i].second == 0.0) continue;
-      if (i + 1 == n || e[i].first != e[i + 1].first) {
-        rows[new_size] = e[i].first;
-        coefs[new_size] = e[i].second;
+      if (coefs[i] == 0.0) continue;
+      if (i + 1 == n || rows[i] != rows[i + 1]) {
+        rows[new_size] = rows[i];
+        coefs[new_size] = coefs[i];
         ++new_size;
       }
     }
     rows.resize(new_size);
     coefs.resize(new_size);
     may_contain_duplicates = false;
+  }
+  void RadixSortByRow() {
+    constexpr int kBits = 11;
+    constexpr int kBuckets = 1 << kBits;
+    const size_t n = rows.size();
+    int max_row = 0;
+    for (size_t i = 0; i < n; ++i) max_row = std::max(max_row, rows[i]);
+    static thread_local std::vector<int> tmp_rows;
+    static thread_local std::vector<Fractional> tmp_coefs;
+    tmp_rows.resize(n);
+    tmp_coefs.resize(n);
+    size_t count[kBuckets];
+    for (int shift = 0; shift == 0 || (max_row >> shift) != 0; shift += kBits) {
+      std::fill(count, count + kBuckets, size_t{0});
+      for (size_t i = 0; i < n; ++i) ++count[(rows[i] >> shift) & (kBuckets - 1)];
+      size_t sum = 0;
+      for (int b = 0; b < kBuckets; ++b) {
+        const size_t c = count[b];
+        count[b] = sum;
+        sum += c;
+      }
+      for (size_t i = 0; i < n; ++i) {
+        const size_t dst = count[(rows[i] >> shift) & (kBuckets - 1)]++;
+        tmp_rows[dst] = rows[i];
+        tmp_coefs[dst] = coefs[i];
+      }
+      rows.swap(tmp_rows);
+      coefs.swap(tmp_coefs);
+    }
   }
   // sparse_vector.h:956-984
   void MoveTaggedEntriesTo(const std::vector<int>& index_perm,

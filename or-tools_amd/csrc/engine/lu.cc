@@ -758,7 +758,7 @@ struct BasisFactorization::AsyncWorker {
 BasisFactorization::BasisFactorization(const CompactSparseMatrix* matrix,
                                        const std::vector<int>* basis)
     : compact_matrix_(*matrix), basis_(*basis) {
-  if (const char* e = std::getenv("MILP_ASYNC_TAU")) {
+  if (const char* e = std::getenv("MILP_ASYNC_SOLVES")) {
     if (std::strcmp(e, "off") == 0) async_min_rows_ = -1;
     if (std::strcmp(e, "force") == 0) async_min_rows_ = 0;
   }
@@ -768,8 +768,42 @@ BasisFactorization::~BasisFactorization() {
   if (async_) async_->Wait();
 }
 
-bool BasisFactorization::AsyncTauEnabled() const {
+bool BasisFactorization::AsyncEnabled() const {
   return async_min_rows_ >= 0 && compact_matrix_.num_rows() >= async_min_rows_;
+}
+
+uint64_t BasisFactorization::StartAsync(AsyncKind kind, std::function<void()> job) const {
+  DropAsync();
+  if (!async_) async_.reset(new AsyncWorker());
+  async_kind_ = kind;
+  async_->Submit(std::move(job));
+  return ++async_ticket_;
+}
+
+bool BasisFactorization::TakeAsync(uint64_t ticket) const {
+  if (async_kind_ == AsyncKind::kNone || ticket != async_ticket_) return false;
+  async_->Wait();
+  async_kind_ = AsyncKind::kNone;
+  async_input_ = nullptr;
+  // The worker's deterministic-time bumps land now, where the serial solve
+  // would have made them.
+  rank_one_factorization_.TakeDeferredBumps(true);
+  for (const int64_t n : deferred_solve_entries_) BumpDeterministicTimeForSolve(n);
+  deferred_solve_entries_.clear();
+  return true;
+}
+
+void BasisFactorization::DropAsync() const {
+  if (async_kind_ == AsyncKind::kNone) return;
+  async_->Wait();
+  async_kind_ = AsyncKind::kNone;
+  async_input_ = nullptr;
+  rank_one_factorization_.TakeDeferredBumps(false);
+  deferred_solve_entries_.clear();
+}
+
+void BasisFactorization::WaitAsync() const {
+  if (async_kind_ != AsyncKind::kNone) async_->Wait();
 }
 
 // The body of RightSolveForTau (basis_representation.cc:374-398) into *out,
@@ -788,31 +822,37 @@ void BasisFactorization::ComputeTauInto(bool can_be_optimized, const ScatteredVe
 }
 
 void BasisFactorization::StartAsyncTau(const ScatteredVector& rho) const {
-  SyncAsyncTau();
-  if (!AsyncTauEnabled()) return;
-  if (!async_) async_.reset(new AsyncWorker());
+  DropAsync();
+  if (!AsyncEnabled()) return;
   const bool can_be_optimized = tau_computation_can_be_optimized_;
-  async_pending_ = true;
-  async_input_ = &rho;
-  async_->Submit([this, can_be_optimized, &rho]() {
+  tau_ticket_ = StartAsync(AsyncKind::kTau, [this, can_be_optimized, &rho]() {
     // The permuted intermediate of the last BTRAN is copied, not consumed:
     // a discarded result leaves tau_ as the serial code would.
     if (can_be_optimized) async_tau_ = tau_;
     ComputeTauInto(can_be_optimized, rho, &async_tau_);
   });
+  async_input_ = &rho;
 }
 
-void BasisFactorization::SyncAsyncTau() const {
-  if (!async_pending_) return;
-  async_->Wait();
-  async_pending_ = false;
-  async_input_ = nullptr;
-  rank_one_factorization_.TakeDeferredBumps(false);
-  deferred_solve_entries_.clear();
+uint64_t BasisFactorization::StartAsyncLeftSolve(std::function<void()> job) const {
+  DropAsync();
+  if (!AsyncEnabled()) return 0;
+  return StartAsync(AsyncKind::kLeftSolve, std::move(job));
+}
+
+// A BTRAN for a unit row reads and extends the left pool (storage_): a
+// pending tau was not taken and is dropped; a pending left solve (which
+// reads storage_) is waited for and kept.
+void BasisFactorization::SyncForUnitRow() const {
+  if (async_kind_ == AsyncKind::kLeftSolve) {
+    WaitAsync();
+  } else {
+    DropAsync();
+  }
 }
 
 void BasisFactorization::Clear() {
-  SyncAsyncTau();
+  DropAsync();
   num_updates_ = 0;
   tau_computation_can_be_optimized_ = false;
   lu_factorization_.Clear();
@@ -824,7 +864,7 @@ void BasisFactorization::Clear() {
 }
 
 Status BasisFactorization::Initialize() {
-  SyncAsyncTau();
+  DropAsync();
   Clear();
   if (IsIdentityBasis()) return Status::OK();
   return ComputeFactorization();
@@ -832,7 +872,7 @@ Status BasisFactorization::Initialize() {
 
 std::vector<int> BasisFactorization::ComputeInitialBasis(
     const std::vector<int>& candidates) {
-  SyncAsyncTau();
+  DropAsync();
   std::vector<int> basis =
       lu_factorization_.ComputeInitialBasis(compact_matrix_, candidates);
   deterministic_time_ += lu_factorization_.DeterministicTimeOfLastFactorization();
@@ -845,7 +885,7 @@ Status BasisFactorization::Refactorize() {
 }
 
 Status BasisFactorization::ForceRefactorization() {
-  SyncAsyncTau();
+  DropAsync();
   Clear();
   return ComputeFactorization();
 }
@@ -900,7 +940,7 @@ Status BasisFactorization::MiddleProductFormUpdate(int entering_col,
 // basis_representation.cc:304-340
 Status BasisFactorization::Update(int entering_col, int leaving_variable_row,
                                   const ScatteredVector& /*direction*/) {
-  SyncAsyncTau();
+  DropAsync();
   if (num_updates_ >= max_num_updates_) {
     if (!dynamic_period_) return ForceRefactorization();
     if (last_factorization_deterministic_time_ <
@@ -935,21 +975,13 @@ void BasisFactorization::RightSolve(ScatteredVector* d) const {
 // basis_representation.cc:374-398
 const std::vector<Fractional>& BasisFactorization::RightSolveForTau(
     const ScatteredVector& a) const {
-  if (async_pending_ && async_input_ == &a) {
-    async_->Wait();
-    async_pending_ = false;
-    async_input_ = nullptr;
-    // The worker's deterministic-time bumps land now, where the serial
-    // solve would have made them.
-    rank_one_factorization_.TakeDeferredBumps(true);
-    for (const int64_t n : deferred_solve_entries_) BumpDeterministicTimeForSolve(n);
-    deferred_solve_entries_.clear();
+  if (async_kind_ == AsyncKind::kTau && async_input_ == &a && TakeAsync(tau_ticket_)) {
     std::swap(tau_, async_tau_);
     tau_computation_can_be_optimized_ = false;
     tau_is_computed_ = true;
     return tau_.values;
   }
-  SyncAsyncTau();
+  DropAsync();
   if (tau_computation_can_be_optimized_) {
     tau_computation_can_be_optimized_ = false;
     lu_factorization_.RightSolveLWithPermutedInput(a.values, &tau_);
@@ -966,7 +998,7 @@ const std::vector<Fractional>& BasisFactorization::RightSolveForTau(
 
 // basis_representation.cc:400-453
 void BasisFactorization::LeftSolveForUnitRow(int j, ScatteredVector* y) const {
-  SyncAsyncTau();
+  SyncForUnitRow();
   ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), y);
   if (j >= static_cast<int>(left_pool_mapping_.size())) {
     left_pool_mapping_.resize(j + 1, kInvalidCol);
@@ -997,7 +1029,7 @@ void BasisFactorization::LeftSolveForUnitRow(int j, ScatteredVector* y) const {
 
 // basis_representation.cc:455-466
 void BasisFactorization::TemporaryLeftSolveForUnitRow(int j, ScatteredVector* y) const {
-  SyncAsyncTau();
+  SyncForUnitRow();
   ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), y);
   lu_factorization_.LeftSolveUForUnitRow(j, y);
   lu_factorization_.LeftSolveLWithNonZeros(y, nullptr);

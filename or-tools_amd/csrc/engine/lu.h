@@ -7,6 +7,8 @@
 #ifndef MILP_LU_H_
 #define MILP_LU_H_
 
+#include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 
@@ -996,11 +998,22 @@ class BasisFactorization {
   // factorization first waits for the worker and drops it. The solve is the
   // same code on a private scratch copy, and its deterministic-time bumps are
   // applied when it is taken, so results and timing match the serial order.
+  enum class AsyncKind { kNone, kTau, kLeftSolve };
   void StartAsyncTau(const ScatteredVector& rho) const;
-  bool AsyncTauEnabled() const;
+  // The same for a caller's BTRAN (the primal loop's B^-T d): job runs
+  // LeftSolve on the worker; TakeAsync(ticket) waits for it and applies its
+  // bumps, and returns false if it was dropped (then the caller solves).
+  uint64_t StartAsyncLeftSolve(std::function<void()> job) const;
+  bool TakeAsync(uint64_t ticket) const;
+  // Waits for and discards any worker job / the job of one ticket.
+  void DropAsync() const;
+  void DropAsync(uint64_t ticket) const {
+    if (async_kind_ != AsyncKind::kNone && ticket == async_ticket_) DropAsync();
+  }
+  bool AsyncEnabled() const;
   void SetParameters(int refactorization_period, bool dynamic_period,
                      const LuParameters& lu) {
-    SyncAsyncTau();
+    DropAsync();
     max_num_updates_ = refactorization_period;
     dynamic_period_ = dynamic_period;
     lu_factorization_.SetParameters(lu);
@@ -1030,11 +1043,11 @@ class BasisFactorization {
     return lu_factorization_.GetColumnPermutation();
   }
   void SetColumnPermutationToIdentity() {
-    SyncAsyncTau();
+    DropAsync();
     lu_factorization_.SetColumnPermutationToIdentity();
   }
   void SetLuParameters(const LuParameters& lu) {
-    SyncAsyncTau();
+    DropAsync();
     lu_factorization_.SetParameters(lu);
   }
   const LuFactorization& lu() const { return lu_factorization_; }
@@ -1046,8 +1059,9 @@ class BasisFactorization {
   Status ComputeFactorization();
   Status MiddleProductFormUpdate(int entering_col, int leaving_variable_row);
 
-  // Waits for the tau worker; drop=true discards its result.
-  void SyncAsyncTau() const;
+  uint64_t StartAsync(AsyncKind kind, std::function<void()> job) const;
+  void WaitAsync() const;
+  void SyncForUnitRow() const;
   void ComputeTauInto(bool can_be_optimized, const ScatteredVector& a,
                       ScatteredVector* out) const;
 
@@ -1055,7 +1069,9 @@ class BasisFactorization {
   const std::vector<int>& basis_;
   struct AsyncWorker;
   mutable std::unique_ptr<AsyncWorker> async_;
-  mutable bool async_pending_ = false;
+  mutable AsyncKind async_kind_ = AsyncKind::kNone;
+  mutable uint64_t async_ticket_ = 0;
+  mutable uint64_t tau_ticket_ = 0;
   mutable const ScatteredVector* async_input_ = nullptr;
   mutable ScatteredVector async_tau_;
   mutable std::vector<int64_t> deferred_solve_entries_;

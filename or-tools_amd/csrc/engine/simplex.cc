@@ -935,6 +935,8 @@ class PrimalEdgeNorms {
   }
   const std::vector<Fractional>& RawEdgeNorms() const { return edge_squared_norms_; }
   bool TestEnteringEdgeNormPrecision(int entering_col, const ScatteredVector& d);
+  void StartDirectionLeftInverse(const ScatteredVector& d);
+  void DropDirectionLeftInverse();
   void UpdateBeforeBasisPivot(int entering_col, int leaving_col, int leaving_row,
                               const ScatteredVector& direction, UpdateRow* update_row);
   void AddRecomputationWatcher(bool* w) { watchers_.push_back(w); }
@@ -978,6 +980,7 @@ class PrimalEdgeNorms {
     recompute_edge_squared_norms_ = false;
   }
   void ComputeDirectionLeftInverse(int entering_col, const ScatteredVector& d);
+  void SolveDirectionLeftInverse(const ScatteredVector& d, ScatteredVector* out) const;
   void UpdateEdgeSquaredNorms(int entering_col, int leaving_col, int leaving_row,
                               const std::vector<Fractional>& direction,
                               const UpdateRow& update_row);
@@ -1017,6 +1020,8 @@ class PrimalEdgeNorms {
   std::vector<Fractional> devex_weights_;
   int num_devex_updates_since_reset_ = 0;
   ScatteredVector direction_left_inverse_;
+  ScatteredVector async_w_;
+  uint64_t w_ticket_ = 0;
   int64_t num_operations_ = 0;
   std::vector<bool*> watchers_;
   // Parked update (see SetDeferral).
@@ -1081,10 +1086,40 @@ void PrimalEdgeNorms::UpdateBeforeBasisPivot(int entering_col, int leaving_col,
   }
 }
 
+// B^-T d needs only the direction: the factorization's worker computes it
+// while the entering tests, the ratio test and the update row run
+// (BasisFactorization::StartAsyncLeftSolve), into a copy of
+// direction_left_inverse_ that replaces it when taken.
+void PrimalEdgeNorms::StartDirectionLeftInverse(const ScatteredVector& d) {
+  w_ticket_ = 0;
+  if (pricing_rule_ != 1 || recompute_edge_squared_norms_ || pending_) return;
+  w_ticket_ = bf_.StartAsyncLeftSolve([this, &d]() {
+    async_w_ = direction_left_inverse_;
+    SolveDirectionLeftInverse(d, &async_w_);
+  });
+}
+
+void PrimalEdgeNorms::DropDirectionLeftInverse() {
+  if (w_ticket_ != 0) bf_.DropAsync(w_ticket_);
+  w_ticket_ = 0;
+}
+
 // primal_edge_norms.cc:166-199
 void PrimalEdgeNorms::ComputeDirectionLeftInverse(int /*entering_col*/,
                                                   const ScatteredVector& d) {
   SubTimer timer(kSubBtranW);
+  const uint64_t ticket = w_ticket_;
+  w_ticket_ = 0;
+  if (ticket != 0 && bf_.TakeAsync(ticket)) {
+    std::swap(direction_left_inverse_, async_w_);
+    return;
+  }
+  SolveDirectionLeftInverse(d, &direction_left_inverse_);
+}
+
+void PrimalEdgeNorms::SolveDirectionLeftInverse(const ScatteredVector& d,
+                                                ScatteredVector* out) const {
+  ScatteredVector& direction_left_inverse_ = *out;
   const int size = d.size();
   const double kThreshold = 0.05 * size;
   if (!direction_left_inverse_.non_zeros.empty() &&
@@ -3469,6 +3504,7 @@ void RevisedSimplex::ComputeVariableValuesError() {
 // revised_simplex.cc:1695-1720
 void RevisedSimplex::ComputeDirection(int col) {
   SubTimer timer(kSubFtranDirection);
+  primal_edge_norms_.DropDirectionLeftInverse();  // its job reads direction_
   basis_factorization_.RightSolveForProblemColumn(col, &direction_);
   direction_infinity_norm_ = 0.0;
   if (direction_.non_zeros.empty()) {
@@ -4011,6 +4047,7 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
     }
 
     ComputeDirection(entering_col);
+    primal_edge_norms_.StartDirectionLeftInverse(direction_);
     if (!primal_edge_norms_.TestEnteringEdgeNormPrecision(entering_col, direction_)) {
       primal_prices_.RecomputePriceAt(entering_col);
       continue;

@@ -320,13 +320,36 @@ def test_host_parallel_loops_parity(case, dual, monkeypatch):
 @pytest.mark.parametrize("device_dual", ["off", "force"])
 def test_async_tau_parity(seed, device_dual, monkeypatch):
     """The dual loop's tau FTRAN runs on the factorization's worker thread
-    (MILP_ASYNC_TAU=force at test size) while the update row, ratio test and
-    direction FTRAN run: same results, same iteration count, and the same
-    deterministic time, since the worker's bumps are applied in serial order."""
-    monkeypatch.setenv("MILP_ASYNC_TAU", "force")
+    (MILP_ASYNC_SOLVES=force at test size) while the update row, ratio test and
+    direction FTRAN run: same results and iteration count as the oracle, and the
+    same deterministic time as the serial engine (the worker's bumps are
+    applied in serial order)."""
     monkeypatch.setenv("MILP_DEVICE_DUAL", device_dual)
     lp = lp_gen.sparse_c5_lp(500 + 40 * (seed % 3), 5000, 6, seed)
     p = abi.default_params(use_dual_simplex=1)
-    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
-    parity_util.compare(o, ro, g, rg, lp)
-    assert rg.deterministic_time == ro.deterministic_time
+    dtime = {}
+    for mode in ("off", "force"):
+        monkeypatch.setenv("MILP_ASYNC_SOLVES", mode)
+        o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+        parity_util.compare(o, ro, g, rg, lp)
+        dtime[mode] = rg.deterministic_time
+    assert dtime["force"] == dtime["off"]
+
+
+@pytest.mark.parametrize("shape", [(97, 500, 61), (160, 1200, 62)])
+@pytest.mark.parametrize("block", ["off", "force"])
+def test_async_direction_left_inverse_parity(shape, block, monkeypatch):
+    """Primal steepest edge: B^-T d runs on the factorization's worker while
+    the entering tests, ratio test and update row run, and is taken by the
+    edge-norm update (or dropped when the iteration restarts). Dense LPs
+    (phase I every iteration): results and deterministic time unchanged."""
+    monkeypatch.setenv("MILP_DENSE_BLOCK", block)
+    m, n, seed = shape
+    lp = lp_gen.dense_box_lp(m, n, seed)
+    dtime = {}
+    for mode in ("off", "force"):
+        monkeypatch.setenv("MILP_ASYNC_SOLVES", mode)
+        o, ro, g, rg = parity_util.solve_both(lp, abi.default_params(), _handle)
+        parity_util.compare(o, ro, g, rg, lp)
+        dtime[mode] = rg.deterministic_time
+    assert dtime["force"] == dtime["off"]
