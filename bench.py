@@ -283,7 +283,7 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--m", type=int, default=10000)
     ap.add_argument("--n", type=int, default=50000)

@@ -5,7 +5,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
-TAG=${TAG:-r01_v4} bash $R/scripts/gpu_profile.sh > $OUT/profile.log 2>&1 || { echo "profile failed"; tail -30 $OUT/profile.log; exit 1; }
+TAG=${TAG:-r01_v5} bash $R/scripts/gpu_profile.sh > $OUT/profile.log 2>&1 || { echo "profile failed"; tail -30 $OUT/profile.log; exit 1; }
 tail -3 $OUT/profile.log
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/gpu_tests.log; exit 1; }
