@@ -247,6 +247,33 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
                              const double* lbs, const double* ubs, const int8_t* warm_state,
                              int32_t warm_len, mi_lp_result* results);
 
+/* MPS ingestion: the reader that fills the
+ * LinearProgram handed to mi_lp_load, replacing
+ *   glop::MPSReader::ParseFile / ParseString   (ortools/lp_data/mps_reader.h:39-60,
+ *                                               mps_reader_template.h ParseFile)
+ * with the LinearProgram data wrapper (mps_reader.cc:22-112). Formats as
+ * MPSReaderFormat: auto-detection tries fixed, then free. On error the return
+ * code is MI_LP_ERROR_INVALID_PROBLEM (absl::InvalidArgumentError upstream)
+ * and mi_mps_error() holds the message; the model is always allocated and
+ * must be released with mi_mps_free. The matrix comes back cleaned up (CSC,
+ * rows sorted per column, no zeros), ready for mi_lp_load. */
+typedef struct mi_mps_model mi_mps_model;
+enum { MI_MPS_AUTO = 0, MI_MPS_FREE = 1, MI_MPS_FIXED = 2 };
+int mi_mps_read_file(const char* path, int32_t format, mi_mps_model** out,
+                     int32_t* format_used);
+int mi_mps_parse_string(const char* text, int32_t format, mi_mps_model** out,
+                        int32_t* format_used);
+const char* mi_mps_error(const mi_mps_model* m);
+int mi_mps_dims(const mi_mps_model* m, int32_t* num_rows, int32_t* num_cols, int64_t* nnz);
+/* Any output pointer may be NULL. col_starts has num_cols + 1 entries. */
+int mi_mps_get(const mi_mps_model* m, int64_t* col_starts, int32_t* row_idx, double* vals,
+               double* col_lb, double* col_ub, double* row_lb, double* row_ub, double* obj,
+               double* obj_offset, int32_t* maximize, int8_t* is_integer);
+const char* mi_mps_name(const mi_mps_model* m);
+const char* mi_mps_col_name(const mi_mps_model* m, int32_t col);
+const char* mi_mps_row_name(const mi_mps_model* m, int32_t row);
+void mi_mps_free(mi_mps_model* m);
+
 #ifdef __cplusplus
 }
 #endif

@@ -153,4 +153,6 @@ EXPORTED_SYMBOLS = [
     "mi_lp_finish", "mi_lp_stop", "mi_lp_get_kernel_stats", "mi_lp_reset_kernel_stats",
     "mi_lp_set_kernel_timing", "mi_lp_batch_solve", "mi_lp_set_variable_bounds",
     "mi_lp_batch_solve_bounds",
+    "mi_mps_read_file", "mi_mps_parse_string", "mi_mps_error", "mi_mps_dims", "mi_mps_get",
+    "mi_mps_name", "mi_mps_col_name", "mi_mps_row_name", "mi_mps_free",
 ]

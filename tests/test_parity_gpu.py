@@ -353,3 +353,16 @@ def test_async_direction_left_inverse_parity(shape, block, monkeypatch):
         parity_util.compare(o, ro, g, rg, lp)
         dtime[mode] = rg.deterministic_time
     assert dtime["force"] == dtime["off"]
+
+
+@pytest.mark.parametrize("name", ["test2.mps", "maximization.mps", "solomon_bp_c101.mps"])
+@pytest.mark.parametrize("dual", [0, 1])
+def test_mps_file_parity(name, dual):
+    """LPs read from the reference's MPS fixtures (mi_mps_read_file) solve on
+    the GPU exactly as on the oracle (solomon_bp_c101: its LP relaxation)."""
+    import os
+    from mi_glop import mps
+    lp = mps.read_mps(os.path.join(os.path.dirname(__file__), "golden", "mps", name))
+    p = abi.default_params(use_dual_simplex=dual)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
