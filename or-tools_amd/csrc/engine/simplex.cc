@@ -2277,7 +2277,11 @@ class VariableValues {
   Fractional ComputeMaximumPrimalInfeasibility() const;
   void UpdateOnPivoting(const ScatteredVector& direction, int entering_col,
                         Fractional step) {
-    for (const int row : direction.non_zeros) {
+    const std::vector<int>& rows = direction.non_zeros;
+    const size_t n = rows.size();
+    for (size_t k = 0; k < n; ++k) {
+      if (k + 16 < n) __builtin_prefetch(variable_values_.data() + basis_[rows[k + 16]], 1);
+      const int row = rows[k];
       const int col = basis_[row];
       variable_values_[col] -= direction.values[row] * step;
     }
@@ -2427,8 +2431,12 @@ void VariableValues::UpdateGivenNonBasicVariables(const std::vector<int>& cols,
   initially_all_zero_scratchpad_.ClearNonZerosIfTooDense();
   bf_.RightSolve(&initially_all_zero_scratchpad_);
   if (initially_all_zero_scratchpad_.non_zeros.empty()) {
-    for (int row = 0; row < num_rows; ++row)
-      variable_values_[basis_[row]] -= initially_all_zero_scratchpad_[row];
+    Fractional* x = variable_values_.data();
+    constexpr int kAhead = 16;
+    for (int row = 0; row < num_rows; ++row) {
+      if (row + kAhead < num_rows) __builtin_prefetch(x + basis_[row + kAhead], 1);
+      x[basis_[row]] -= initially_all_zero_scratchpad_[row];
+    }
     initially_all_zero_scratchpad_.values.assign(num_rows, 0.0);
     RecomputeDualPrices();
     return;
@@ -2450,7 +2458,19 @@ void VariableValues::RecomputeDualPrices(bool put_more_importance_on_norm) {
   put_more_importance_on_norm_ = put_more_importance_on_norm;
   const Fractional tolerance = params_.primal_feasibility_tolerance;
   const std::vector<Fractional>& sn = dual_edge_norms_->GetEdgeSquaredNorms();
+  // The basic columns are scattered over arrays of N entries: their values
+  // and bounds are prefetched a few rows ahead.
+  const Fractional* x = variable_values_.data();
+  const Fractional* lb = variables_info_.GetVariableLowerBounds().data();
+  const Fractional* ub = variables_info_.GetVariableUpperBounds().data();
+  constexpr int kAhead = 16;
   for (int row = 0; row < num_rows; ++row) {
+    if (row + kAhead < num_rows) {
+      const int ahead = basis_[row + kAhead];
+      __builtin_prefetch(x + ahead);
+      __builtin_prefetch(lb + ahead);
+      __builtin_prefetch(ub + ahead);
+    }
     const int col = basis_[row];
     const Fractional inf =
         std::max(GetUpperBoundInfeasibility(col), GetLowerBoundInfeasibility(col));
@@ -2469,7 +2489,18 @@ void VariableValues::UpdateDualPrices(const std::vector<int>& rows) {
   }
   const Fractional tolerance = params_.primal_feasibility_tolerance;
   const std::vector<Fractional>& sn = dual_edge_norms_->GetEdgeSquaredNorms();
-  for (const int row : rows) {
+  const Fractional* x = variable_values_.data();
+  const Fractional* lb = variables_info_.GetVariableLowerBounds().data();
+  const Fractional* ub = variables_info_.GetVariableUpperBounds().data();
+  const size_t n = rows.size();
+  for (size_t k = 0; k < n; ++k) {
+    if (k + 16 < n) {
+      const int ahead = basis_[rows[k + 16]];
+      __builtin_prefetch(x + ahead);
+      __builtin_prefetch(lb + ahead);
+      __builtin_prefetch(ub + ahead);
+    }
+    const int row = rows[k];
     const int col = basis_[row];
     const Fractional inf =
         std::max(GetUpperBoundInfeasibility(col), GetLowerBoundInfeasibility(col));

@@ -3,6 +3,9 @@
 // glop/markowitz.cc, glop/lu_factorization.cc, glop/basis_representation.cc.
 #include "oracle_lu.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace oracle {
 
 // ---------------------------------------------------------------------------
@@ -396,6 +399,53 @@ std::vector<int> LuFactorization::ComputeInitialBasis(
 }
 
 namespace {
+// lp_utils.h:240-277. The zero scratchpad is all zeros between uses (every
+// user leaves it so, as upstream DCHECKs), which keeps the sparse permute
+// O(nnz) instead of O(m). MILP_CHECK_SCRATCH=1 verifies the invariant.
+bool CheckScratchEnabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MILP_CHECK_SCRATCH");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+void CheckAllZero(const std::vector<Fractional>& v) {
+  if (!CheckScratchEnabled()) return;
+  for (const Fractional x : v) {
+    if (x != 0.0) {
+      std::fprintf(stderr, "zero scratchpad invariant violated\n");
+      std::abort();
+    }
+  }
+}
+void PermuteWithScratchpad(const std::vector<int>& perm, std::vector<Fractional>* zero_scratchpad,
+                           std::vector<Fractional>* io) {
+  CheckAllZero(*zero_scratchpad);
+  const size_t size = io->size();
+  zero_scratchpad->swap(*io);
+  io->resize(size, 0.0);
+  for (size_t i = 0; i < size; ++i) {
+    const Fractional v = (*zero_scratchpad)[i];
+    if (v != 0.0) (*io)[perm[i]] = v;
+  }
+  zero_scratchpad->assign(size, 0.0);
+}
+void PermuteWithKnownNonZeros(const std::vector<int>& perm,
+                              std::vector<Fractional>* zero_scratchpad,
+                              std::vector<Fractional>* output, std::vector<int>* non_zeros) {
+  CheckAllZero(*zero_scratchpad);
+  zero_scratchpad->swap(*output);
+  output->resize(zero_scratchpad->size(), 0.0);
+  for (int& ref : *non_zeros) {
+    const Fractional v = (*zero_scratchpad)[ref];
+    (*zero_scratchpad)[ref] = 0.0;
+    const int p = perm[ref];
+    (*output)[p] = v;
+    ref = p;
+  }
+  CheckAllZero(*zero_scratchpad);
+}
+
 Fractional ComputeSquaredNormAndResetToZero(const std::vector<int>& nz,
                                             std::vector<Fractional>* column) {
   Fractional sum = 0.0;
@@ -531,29 +581,11 @@ void LuFactorization::RightSolveLForColumnView(const ColumnView& b,
 void LuFactorization::RightSolveLWithNonZeros(ScatteredVector* x) const {
   if (is_identity_factorization_) return;
   if (x->non_zeros.empty()) {
-    // PermuteWithScratchpad (lp_utils.h:240-257)
-    dense_zero_scratchpad_.assign(x->values.size(), 0.0);
-    dense_zero_scratchpad_.swap(x->values);
-    x->values.assign(dense_zero_scratchpad_.size(), 0.0);
-    for (size_t i = 0; i < dense_zero_scratchpad_.size(); ++i) {
-      const Fractional v = dense_zero_scratchpad_[i];
-      if (v != 0.0) x->values[row_perm_[i]] = v;
-    }
-    dense_zero_scratchpad_.assign(x->values.size(), 0.0);
+    PermuteWithScratchpad(row_perm_, &dense_zero_scratchpad_, &x->values);
     lower_.LowerSolve(&x->values);
     return;
   }
-  // PermuteWithKnownNonZeros (lp_utils.h:262-277)
-  dense_zero_scratchpad_.assign(x->values.size(), 0.0);
-  dense_zero_scratchpad_.swap(x->values);
-  x->values.assign(dense_zero_scratchpad_.size(), 0.0);
-  for (int& ref : x->non_zeros) {
-    const Fractional v = dense_zero_scratchpad_[ref];
-    dense_zero_scratchpad_[ref] = 0.0;
-    const int p = row_perm_[ref];
-    x->values[p] = v;
-    ref = p;
-  }
+  PermuteWithKnownNonZeros(row_perm_, &dense_zero_scratchpad_, &x->values, &x->non_zeros);
   lower_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
   x->non_zeros_are_sorted = true;
   if (x->non_zeros.empty()) {
@@ -619,25 +651,9 @@ bool LuFactorization::LeftSolveLWithNonZeros(
   }
   if (result_before_permutation == nullptr) {
     if (nz->empty()) {
-      dense_zero_scratchpad_.assign(x->size(), 0.0);
-      dense_zero_scratchpad_.swap(*x);
-      x->assign(dense_zero_scratchpad_.size(), 0.0);
-      for (size_t i = 0; i < dense_zero_scratchpad_.size(); ++i) {
-        const Fractional v = dense_zero_scratchpad_[i];
-        if (v != 0.0) (*x)[inverse_row_perm_[i]] = v;
-      }
-      dense_zero_scratchpad_.assign(x->size(), 0.0);
+      PermuteWithScratchpad(inverse_row_perm_, &dense_zero_scratchpad_, x);
     } else {
-      dense_zero_scratchpad_.assign(x->size(), 0.0);
-      dense_zero_scratchpad_.swap(*x);
-      x->assign(dense_zero_scratchpad_.size(), 0.0);
-      for (int& ref : *nz) {
-        const Fractional v = dense_zero_scratchpad_[ref];
-        dense_zero_scratchpad_[ref] = 0.0;
-        const int p = inverse_row_perm_[ref];
-        (*x)[p] = v;
-        ref = p;
-      }
+      PermuteWithKnownNonZeros(inverse_row_perm_, &dense_zero_scratchpad_, x, nz);
     }
     return false;
   }
