@@ -12,7 +12,7 @@ import numpy as np
 from . import abi
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libmi_lp.so")
+LIB_PATH = os.environ.get("MI_LP_LIB") or os.path.join(PKG_DIR, "lib", "libmi_lp.so")
 
 _lib = None
 
