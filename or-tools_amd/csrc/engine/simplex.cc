@@ -2678,7 +2678,8 @@ class RevisedSimplex {
   void PropagateParameters() {
     basis_factorization_.SetParameters(parameters_.basis_refactorization_period,
                                        parameters_.dynamically_adjust_refactorization_period,
-                                       parameters_.lu());
+                                       parameters_.lu(),
+                                       parameters_.use_middle_product_form_update);
     entering_variable_.SetParameters(parameters_);
     reduced_costs_.SetParameters(parameters_);
     dual_edge_norms_.SetParameters(parameters_);
@@ -4789,10 +4790,6 @@ const char* mi_lp_last_error(const mi_lp* h) {
 
 int mi_lp_set_params(mi_lp* h, const mi_glop_params* p) {
   if (h == nullptr || p == nullptr) return MI_LP_ERROR_NULL;
-  if (!p->use_middle_product_form_update) {
-    h->error = "only use_middle_product_form_update=true is implemented";
-    return MI_LP_ERROR_INVALID_PROBLEM;
-  }
   h->params = FromAbi(*p);
   return MI_LP_OK;
 }

@@ -716,6 +716,101 @@ const SparseColumn& LuFactorization::GetColumnOfU(int col) const {
   return column_of_upper_;
 }
 
+// lu_factorization.cc:102-122 with permutation.h:200-235 (ApplyPermutation,
+// ApplyInversePermutation: an empty permutation copies).
+namespace {
+void ApplyPermutationTo(const std::vector<int>& perm, const std::vector<Fractional>& b,
+                        std::vector<Fractional>* result) {
+  if (perm.empty()) {
+    *result = b;
+    return;
+  }
+  result->resize(b.size(), b.back());
+  for (size_t i = 0; i < perm.size(); ++i) (*result)[perm[i]] = b[i];
+}
+void ApplyInversePermutationTo(const std::vector<int>& perm, const std::vector<Fractional>& b,
+                               std::vector<Fractional>* result) {
+  if (perm.empty()) {
+    *result = b;
+    return;
+  }
+  result->resize(b.size(), b.back());
+  for (size_t i = 0; i < perm.size(); ++i) (*result)[i] = b[perm[i]];
+}
+}  // namespace
+
+void LuFactorization::RightSolve(std::vector<Fractional>* x) const {
+  if (is_identity_factorization_) return;
+  ApplyPermutationTo(row_perm_, *x, &dense_column_scratchpad_);
+  lower_.LowerSolve(&dense_column_scratchpad_);
+  upper_.UpperSolve(&dense_column_scratchpad_);
+  ApplyPermutationTo(inverse_col_perm_, dense_column_scratchpad_, x);
+}
+
+void LuFactorization::LeftSolve(std::vector<Fractional>* y) const {
+  if (is_identity_factorization_) return;
+  ApplyInversePermutationTo(inverse_col_perm_, *y, &dense_column_scratchpad_);
+  upper_.TransposeUpperSolve(&dense_column_scratchpad_);
+  lower_.TransposeLowerSolve(&dense_column_scratchpad_);
+  ApplyInversePermutationTo(row_perm_, dense_column_scratchpad_, y);
+}
+
+// basis_representation.cc:25-125 (EtaMatrix, kSparseThreshold 0.5).
+EtaMatrix::EtaMatrix(int eta_col, const ScatteredVector& direction)
+    : eta_col_(eta_col), eta_col_coefficient_(direction[eta_col]) {
+  eta_coeff_ = direction.values;
+  eta_coeff_[eta_col_] = 0.0;
+  if (static_cast<double>(direction.non_zeros.size()) < 0.5 * eta_coeff_.size()) {
+    for (const int row : direction.non_zeros) {
+      if (row == eta_col) continue;
+      sparse_eta_coeff_.AddEntry(row, eta_coeff_[row]);
+    }
+  }
+}
+
+void EtaMatrix::LeftSolve(std::vector<Fractional>* y) const {
+  Fractional y_value = (*y)[eta_col_];
+  if (!sparse_eta_coeff_.IsEmpty()) {
+    for (int64_t i = 0; i < sparse_eta_coeff_.num_entries(); ++i) {
+      y_value -= (*y)[sparse_eta_coeff_.rows[i]] * sparse_eta_coeff_.coefs[i];
+    }
+  } else {
+    const size_t n = eta_coeff_.size();
+    for (size_t row = 0; row < n; ++row) y_value -= (*y)[row] * eta_coeff_[row];
+  }
+  (*y)[eta_col_] = y_value / eta_col_coefficient_;
+}
+
+void EtaMatrix::RightSolve(std::vector<Fractional>* d) const {
+  if ((*d)[eta_col_] == 0.0) return;
+  const Fractional coeff = (*d)[eta_col_] / eta_col_coefficient_;
+  if (!sparse_eta_coeff_.IsEmpty()) {
+    for (int64_t i = 0; i < sparse_eta_coeff_.num_entries(); ++i) {
+      (*d)[sparse_eta_coeff_.rows[i]] -= sparse_eta_coeff_.coefs[i] * coeff;
+    }
+  } else {
+    const size_t n = eta_coeff_.size();
+    for (size_t row = 0; row < n; ++row) (*d)[row] -= eta_coeff_[row] * coeff;
+  }
+  (*d)[eta_col_] = coeff;
+}
+
+void EtaMatrix::SparseLeftSolve(std::vector<Fractional>* y, std::vector<int>* pos) const {
+  Fractional y_value = (*y)[eta_col_];
+  bool is_eta_col_in_pos = false;
+  const int size = static_cast<int>(pos->size());
+  for (int i = 0; i < size; ++i) {
+    const int col = (*pos)[i];
+    if (col == eta_col_) {
+      is_eta_col_in_pos = true;
+      continue;
+    }
+    y_value -= (*y)[col] * eta_coeff_[col];
+  }
+  (*y)[eta_col_] = y_value / eta_col_coefficient_;
+  if (!is_eta_col_in_pos) pos->push_back(eta_col_);
+}
+
 // ---------------------------------------------------------------------------
 // BasisFactorization (basis_representation.cc:176-627)
 void BasisFactorization::Clear() {
@@ -723,6 +818,7 @@ void BasisFactorization::Clear() {
   tau_computation_can_be_optimized_ = false;
   lu_factorization_.Clear();
   rank_one_factorization_.Clear();
+  eta_factorization_.Clear();
   storage_.Reset(compact_matrix_.num_rows());
   right_storage_.Reset(compact_matrix_.num_rows());
   left_pool_mapping_.clear();
@@ -802,7 +898,7 @@ Status BasisFactorization::MiddleProductFormUpdate(int entering_col,
 
 // basis_representation.cc:304-340
 Status BasisFactorization::Update(int entering_col, int leaving_variable_row,
-                                  const ScatteredVector& /*direction*/) {
+                                  const ScatteredVector& direction) {
   if (num_updates_ >= max_num_updates_) {
     if (!dynamic_period_) return ForceRefactorization();
     if (last_factorization_deterministic_time_ <
@@ -811,13 +907,24 @@ Status BasisFactorization::Update(int entering_col, int leaving_variable_row,
     }
   }
   ++num_updates_;
-  ORACLE_RETURN_IF_ERROR(MiddleProductFormUpdate(entering_col, leaving_variable_row));
+  if (use_middle_product_form_update_) {
+    ORACLE_RETURN_IF_ERROR(MiddleProductFormUpdate(entering_col, leaving_variable_row));
+  } else {
+    eta_factorization_.Update(entering_col, leaving_variable_row, direction);
+  }
   tau_computation_can_be_optimized_ = false;
   return Status::OK();
 }
 
 // basis_representation.cc:342-356
 void BasisFactorization::LeftSolve(ScatteredVector* y) const {
+  if (!use_middle_product_form_update_) {
+    y->non_zeros.clear();
+    eta_factorization_.LeftSolve(&y->values);
+    lu_factorization_.LeftSolve(&y->values);
+    BumpDeterministicTimeForSolve(static_cast<int64_t>(y->NumNonZerosEstimate()));
+    return;
+  }
   lu_factorization_.LeftSolveUWithNonZeros(y);
   rank_one_factorization_.LeftSolveWithNonZeros(y);
   lu_factorization_.LeftSolveLWithNonZeros(y, nullptr);
@@ -827,6 +934,13 @@ void BasisFactorization::LeftSolve(ScatteredVector* y) const {
 
 // basis_representation.cc:358-372
 void BasisFactorization::RightSolve(ScatteredVector* d) const {
+  if (!use_middle_product_form_update_) {
+    d->non_zeros.clear();
+    lu_factorization_.RightSolve(&d->values);
+    eta_factorization_.RightSolve(&d->values);
+    BumpDeterministicTimeForSolve(static_cast<int64_t>(d->NumNonZerosEstimate()));
+    return;
+  }
   lu_factorization_.RightSolveLWithNonZeros(d);
   rank_one_factorization_.RightSolveWithNonZeros(d);
   lu_factorization_.RightSolveUWithNonZeros(d);
@@ -837,6 +951,15 @@ void BasisFactorization::RightSolve(ScatteredVector* d) const {
 // basis_representation.cc:374-398
 const std::vector<Fractional>& BasisFactorization::RightSolveForTau(
     const ScatteredVector& a) const {
+  if (!use_middle_product_form_update_) {
+    tau_.non_zeros.clear();
+    tau_.values = a.values;
+    lu_factorization_.RightSolve(&tau_.values);
+    eta_factorization_.RightSolve(&tau_.values);
+    tau_is_computed_ = true;
+    BumpDeterministicTimeForSolve(static_cast<int64_t>(tau_.NumNonZerosEstimate()));
+    return tau_.values;
+  }
   if (tau_computation_can_be_optimized_) {
     tau_computation_can_be_optimized_ = false;
     lu_factorization_.RightSolveLWithPermutedInput(a.values, &tau_);
@@ -854,6 +977,14 @@ const std::vector<Fractional>& BasisFactorization::RightSolveForTau(
 // basis_representation.cc:400-453
 void BasisFactorization::LeftSolveForUnitRow(int j, ScatteredVector* y) const {
   ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), y);
+  if (!use_middle_product_form_update_) {
+    (*y)[j] = 1.0;
+    y->non_zeros.push_back(j);
+    eta_factorization_.SparseLeftSolve(&y->values, &y->non_zeros);
+    lu_factorization_.LeftSolve(&y->values);
+    BumpDeterministicTimeForSolve(static_cast<int64_t>(y->NumNonZerosEstimate()));
+    return;
+  }
   if (j >= static_cast<int>(left_pool_mapping_.size())) {
     left_pool_mapping_.resize(j + 1, kInvalidCol);
   }
@@ -893,6 +1024,15 @@ void BasisFactorization::TemporaryLeftSolveForUnitRow(int j, ScatteredVector* y)
 // basis_representation.cc:468-501
 void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d) const {
   ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), d);
+  if (!use_middle_product_form_update_) {
+    const ColumnView c = compact_matrix_.column(col);  // ColumnCopyToClearedDenseColumn
+    d->values.resize(compact_matrix_.num_rows(), 0.0);
+    for (int64_t i = 0; i < c.n; ++i) d->values[c.rows[i]] = c.coefs[i];
+    lu_factorization_.RightSolve(&d->values);
+    eta_factorization_.RightSolve(&d->values);
+    BumpDeterministicTimeForSolve(static_cast<int64_t>(d->NumNonZerosEstimate()));
+    return;
+  }
   lu_factorization_.RightSolveLForColumnView(compact_matrix_.column(col), d);
   rank_one_factorization_.RightSolveWithNonZeros(d);
   if (col >= static_cast<int>(right_pool_mapping_.size())) {

@@ -9,6 +9,7 @@
 #ifndef ORACLE_LU_H_
 #define ORACLE_LU_H_
 
+#include <memory>
 #include <string>
 
 #include "oracle_lp_data.h"
@@ -805,6 +806,9 @@ class LuFactorization {
            upper_.ComputeInverseInfinityNormUpperBound();
   }
   const std::vector<int>& GetColumnPermutation() const { return col_perm_; }
+  // lu_factorization.cc:102-122, dense solves (product-form path only).
+  void RightSolve(std::vector<Fractional>* x) const;
+  void LeftSolve(std::vector<Fractional>* y) const;
   void SetColumnPermutationToIdentity() {
     col_perm_.clear();
     inverse_col_perm_.clear();
@@ -958,12 +962,53 @@ class RankOneUpdateFactorization {
 };
 
 // basis_representation.cc:176-627 (middle-product-form path).
+// basis_representation.h:55-141, .cc:25-176: product-form (eta) updates,
+// used instead of the middle-product form when
+// use_middle_product_form_update is false.
+class EtaMatrix {
+ public:
+  EtaMatrix(int eta_col, const ScatteredVector& direction);
+  void LeftSolve(std::vector<Fractional>* y) const;
+  void RightSolve(std::vector<Fractional>* d) const;
+  void SparseLeftSolve(std::vector<Fractional>* y, std::vector<int>* pos) const;
+
+ private:
+  int eta_col_;
+  Fractional eta_col_coefficient_;
+  std::vector<Fractional> eta_coeff_;
+  SparseColumn sparse_eta_coeff_;  // entries in direction.non_zeros order
+};
+
+class EtaFactorization {
+ public:
+  void Clear() { eta_matrix_.clear(); }
+  void Update(int /*entering_col*/, int leaving_variable_row,
+              const ScatteredVector& direction) {
+    eta_matrix_.emplace_back(new EtaMatrix(leaving_variable_row, direction));
+  }
+  void LeftSolve(std::vector<Fractional>* y) const {
+    for (int i = static_cast<int>(eta_matrix_.size()) - 1; i >= 0; --i)
+      eta_matrix_[i]->LeftSolve(y);
+  }
+  void SparseLeftSolve(std::vector<Fractional>* y, std::vector<int>* pos) const {
+    for (int i = static_cast<int>(eta_matrix_.size()) - 1; i >= 0; --i)
+      eta_matrix_[i]->SparseLeftSolve(y, pos);
+  }
+  void RightSolve(std::vector<Fractional>* d) const {
+    for (size_t i = 0; i < eta_matrix_.size(); ++i) eta_matrix_[i]->RightSolve(d);
+  }
+
+ private:
+  std::vector<std::unique_ptr<EtaMatrix>> eta_matrix_;
+};
+
 class BasisFactorization {
  public:
   BasisFactorization(const CompactSparseMatrix* matrix, const std::vector<int>* basis)
       : compact_matrix_(*matrix), basis_(*basis) {}
   void SetParameters(int refactorization_period, bool dynamic_period,
-                     const LuParameters& lu) {
+                     const LuParameters& lu, bool use_middle_product_form_update = true) {
+    use_middle_product_form_update_ = use_middle_product_form_update;
     max_num_updates_ = refactorization_period;
     dynamic_period_ = dynamic_period;
     lu_factorization_.SetParameters(lu);
@@ -1018,6 +1063,8 @@ class BasisFactorization {
   std::vector<Fractional> scratchpad_;
   std::vector<int> scratchpad_non_zeros_;
   RankOneUpdateFactorization rank_one_factorization_;
+  EtaFactorization eta_factorization_;
+  bool use_middle_product_form_update_ = true;
   LuFactorization lu_factorization_;
   double last_factorization_deterministic_time_ = 0.0;
   mutable double deterministic_time_ = 0.0;

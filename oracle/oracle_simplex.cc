@@ -3,9 +3,10 @@
 // Restatement of glop::RevisedSimplex (OR-Tools 9.7, ortools/glop/*.cc) and
 // the oracle_lp_* C ABI used by tests/ and bench.py's cpu_baseline leg.
 // Every method cites the reference lines it follows. Intentional omissions
-// (all non-default paths, see DESIGN.md "Oracle scope"): the PFI/eta basis
-// update (use_middle_product_form_update=false), MAROS/BIXBY crash bases,
-// Polish() (needs SetIntegralityScale), logging/stats.
+// (all non-default paths, see DESIGN.md "Oracle scope"): MAROS/BIXBY crash
+// bases, Polish() (needs SetIntegralityScale), logging/stats. The product-form
+// (eta) basis update (use_middle_product_form_update=false) is restated in
+// oracle_lu.cc.
 #include "oracle_simplex.h"
 
 #include <cstdio>
@@ -1846,7 +1847,8 @@ class RevisedSimplex {
   void PropagateParameters() {
     basis_factorization_.SetParameters(parameters_.basis_refactorization_period,
                                        parameters_.dynamically_adjust_refactorization_period,
-                                       parameters_.lu());
+                                       parameters_.lu(),
+                                       parameters_.use_middle_product_form_update);
     entering_variable_.SetParameters(parameters_);
     reduced_costs_.SetParameters(parameters_);
     dual_edge_norms_.SetParameters(parameters_);

@@ -366,3 +366,34 @@ def test_mps_file_parity(name, dual):
     p = abi.default_params(use_dual_simplex=dual)
     o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
     parity_util.compare(o, ro, g, rg, lp)
+
+
+@pytest.mark.parametrize("builder", kat_lps.ALL, ids=lambda f: f.__name__)
+@pytest.mark.parametrize("dual", [0, 1])
+def test_product_form_known_answer_parity(builder, dual):
+    """use_middle_product_form_update=false (product-form etas, SURVEY 8(a)
+    a14): engine and oracle agree bit for bit, including where upstream's
+    eta path ends ABNORMAL/IMPRECISE (see test_oracle.py)."""
+    lp, _ = builder()
+    p = abi.default_params(use_dual_simplex=dual, use_middle_product_form_update=0)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("dual", [0, 1])
+def test_product_form_random_parity(seed, dual):
+    m = [30, 90, 200][seed % 3]
+    n = [90, 300, 900][seed % 3]
+    lp = lp_gen.random_sparse_lp(m, n, 0.25 if m < 40 else 0.04, 700 + seed,
+                                 maximize=bool(seed % 2))
+    p = abi.default_params(use_dual_simplex=dual, use_middle_product_form_update=0)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+
+
+def test_product_form_dense_parity():
+    lp = lp_gen.dense_box_lp(97, 400, 3)
+    p = abi.default_params(use_middle_product_form_update=0)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
