@@ -3,10 +3,10 @@
 // Restatement of glop::RevisedSimplex (OR-Tools 9.7, ortools/glop/*.cc) and
 // the oracle_lp_* C ABI used by tests/ and bench.py's cpu_baseline leg.
 // Every method cites the reference lines it follows. Intentional omissions
-// (all non-default paths, see DESIGN.md "Oracle scope"): MAROS/BIXBY crash
-// bases, Polish() (needs SetIntegralityScale), logging/stats. The product-form
-// (eta) basis update (use_middle_product_form_update=false) is restated in
-// oracle_lu.cc.
+// (non-default, see DESIGN.md "Oracle scope"): Polish() (needs
+// SetIntegralityScale), logging/stats. The product-form (eta) basis update
+// (use_middle_product_form_update=false) is restated in oracle_lu.cc, the
+// BIXBY/MAROS crash bases here.
 #include "oracle_simplex.h"
 
 #include <cstdio>
@@ -1781,6 +1781,197 @@ void CompleteTriangularBasis(const CompactSparseMatrix& matrix,
     }
   }
 }
+// initial_basis.cc:208-356 (GetMarosPriority, GetMarosBasis), restated as is:
+// the first availability test of the residual pattern indexes `available`
+// with the row number (upstream's expression).
+int GetMarosPriority(VariableType t) {
+  switch (t) {
+    case VariableType::UNCONSTRAINED:
+      return 3;
+    case VariableType::LOWER_BOUNDED:
+    case VariableType::UPPER_BOUNDED:
+      return 2;
+    case VariableType::UPPER_AND_LOWER_BOUNDED:
+      return 1;
+    case VariableType::FIXED_VARIABLE:
+      return 0;
+  }
+  return 0;
+}
+
+template <bool only_allow_zero_cost_column>
+void GetMarosBasis(const CompactSparseMatrix& matrix, const std::vector<Fractional>& objective,
+                   const std::vector<VariableType>& type, int num_cols,
+                   std::vector<int>* basis) {
+  const int num_rows = matrix.num_rows();
+  const int first_slack = num_cols - num_rows;
+  basis->resize(num_rows);
+  for (int row = 0; row < num_rows; ++row) (*basis)[row] = first_slack + row;
+  std::vector<char> available(num_cols, true);
+  for (int col = 0; col < first_slack; ++col) {
+    if (type[col] == VariableType::FIXED_VARIABLE ||
+        (only_allow_zero_cost_column && objective[col] != 0.0)) {
+      available[col] = false;
+    }
+  }
+  for (int col = first_slack; col < num_cols; ++col) {
+    if (type[col] == VariableType::UNCONSTRAINED) available[col] = false;
+  }
+  MatrixNonZeroPattern residual_pattern;
+  residual_pattern.Reset(num_rows, num_cols);
+  for (int col = 0; col < first_slack; ++col) {
+    const ColumnView c = matrix.column(col);
+    for (int64_t i = 0; i < c.n; ++i) {
+      if (available[c.rows[i]] && available[col]) residual_pattern.AddEntry(c.rows[i], col);
+    }
+  }
+  for (int row = 0; row < num_rows; ++row) {
+    if (residual_pattern.RowDegree(row) == 0) available[row + first_slack] = false;
+  }
+  auto row_priority = [&](int row) { return GetMarosPriority(type[row + first_slack]); };
+  for (;;) {
+    int max_row_priority_function = std::numeric_limits<int>::min();
+    int max_rpf_row = kInvalidRow;
+    for (int row = 0; row < num_rows; ++row) {
+      if (available[row + first_slack]) {
+        const int rpf = 10 * (3 - row_priority(row)) - residual_pattern.RowDegree(row);
+        if (rpf > max_row_priority_function) {
+          max_row_priority_function = rpf;
+          max_rpf_row = row;
+        }
+      }
+    }
+    if (max_rpf_row == kInvalidRow) break;
+    const Fractional kStabilityThreshold = 1e-3;
+    int max_cpf_col = kInvalidCol;
+    int max_col_priority_function = std::numeric_limits<int>::min();
+    Fractional pivot_absolute_value = 0.0;
+    for (const int col : residual_pattern.RowNonZero(max_rpf_row)) {
+      if (!available[col]) continue;
+      const int cpf = 10 * GetMarosPriority(type[col]) - residual_pattern.ColDegree(col);
+      if (cpf > max_col_priority_function) {
+        Fractional max_magnitude = 0;
+        pivot_absolute_value = 0.0;
+        const ColumnView c = matrix.column(col);
+        for (int64_t i = 0; i < c.n; ++i) {
+          const Fractional absolute_value = std::fabs(c.coefs[i]);
+          if (c.rows[i] == max_rpf_row) pivot_absolute_value = absolute_value;
+          max_magnitude = std::max(max_magnitude, absolute_value);
+        }
+        if (pivot_absolute_value >= kStabilityThreshold * max_magnitude) {
+          max_col_priority_function = cpf;
+          max_cpf_col = col;
+        }
+      }
+    }
+    if (max_cpf_col == kInvalidCol) {
+      available[max_rpf_row + first_slack] = false;
+      continue;
+    }
+    if (row_priority(max_rpf_row) >= GetMarosPriority(type[max_cpf_col])) {
+      available[max_rpf_row + first_slack] = false;
+      continue;
+    }
+    (*basis)[max_rpf_row] = max_cpf_col;
+    available[max_cpf_col] = false;
+    available[first_slack + max_rpf_row] = false;
+    residual_pattern.DeleteRowAndColumn(max_rpf_row, max_cpf_col);
+    for (const int col : residual_pattern.RowNonZero(max_rpf_row)) available[col] = false;
+  }
+}
+
+// initial_basis.cc:43-103 (CompleteBixbyBasis) with ComputeCandidates and
+// BixbyColumnComparator (:358-419) and lp_utils.cc:115-172 helpers.
+void CompleteBixbyBasis(const CompactSparseMatrix& matrix, const std::vector<Fractional>& objective,
+                        const std::vector<Fractional>& lb, const std::vector<Fractional>& ub,
+                        const std::vector<VariableType>& type, int num_cols,
+                        std::vector<int>* basis) {
+  const int num_rows = matrix.num_rows();
+  std::vector<char> can_be_replaced(num_rows, false);
+  std::vector<char> has_zero_coefficient(num_rows, false);
+  basis->resize(num_rows, kInvalidCol);
+  for (int row = 0; row < num_rows; ++row) {
+    if ((*basis)[row] == kInvalidCol) {
+      can_be_replaced[row] = true;
+      has_zero_coefficient[row] = true;
+    }
+  }
+  std::vector<Fractional> scaled_diagonal_abs(num_rows, kInfinity);
+  std::vector<int> candidates;
+  Fractional max_scaled_abs_cost = 0.0;
+  for (int col = 0; col < num_cols; ++col) {
+    if (type[col] != VariableType::FIXED_VARIABLE && matrix.ColumnNumEntries(col) > 0) {
+      candidates.push_back(col);
+      max_scaled_abs_cost = std::max(max_scaled_abs_cost, std::fabs(objective[col]));
+    }
+  }
+  const Fractional kBixbyWeight = 1000.0;
+  max_scaled_abs_cost = (max_scaled_abs_cost == 0.0) ? 1.0 : kBixbyWeight * max_scaled_abs_cost;
+  auto penalty = [&](int col) {
+    const VariableType t = type[col];
+    Fractional p = 0.0;
+    if (t == VariableType::LOWER_BOUNDED) p = lb[col];
+    if (t == VariableType::UPPER_BOUNDED) p = -ub[col];
+    if (t == VariableType::UPPER_AND_LOWER_BOUNDED) p = lb[col] - ub[col];
+    return p + std::fabs(objective[col]) / max_scaled_abs_cost;
+  };
+  std::sort(candidates.begin(), candidates.end(), [&](int a, int b) {
+    if (a == b) return false;
+    const int ca = GetColumnCategory(type[a]);
+    const int cb = GetColumnCategory(type[b]);
+    if (ca != cb) return ca < cb;
+    return penalty(a) < penalty(b);
+  });
+  auto restricted_inf_norm = [](const ColumnView& c, const std::vector<char>& rows,
+                                int* row_index) {
+    Fractional norm = 0.0;
+    for (int64_t i = 0; i < c.n; ++i) {
+      if (rows[c.rows[i]] && std::fabs(c.coefs[i]) > norm) {
+        norm = std::fabs(c.coefs[i]);
+        *row_index = c.rows[i];
+      }
+    }
+    return norm;
+  };
+  for (const int candidate_col_index : candidates) {
+    bool enter_basis = false;
+    const ColumnView candidate_col = matrix.column(candidate_col_index);
+    Fractional inf_norm = 0.0;
+    for (int64_t i = 0; i < candidate_col.n; ++i) {
+      inf_norm = std::max(inf_norm, std::fabs(candidate_col.coefs[i]));
+    }
+    if (inf_norm != 1.0) continue;
+    int candidate_row = kInvalidRow;
+    Fractional candidate_coeff =
+        restricted_inf_norm(candidate_col, has_zero_coefficient, &candidate_row);
+    const Fractional kBixbyHighThreshold = 0.99;
+    if (candidate_coeff > kBixbyHighThreshold) {
+      enter_basis = true;
+    } else {
+      bool dominated = true;
+      for (int64_t i = 0; i < candidate_col.n; ++i) {
+        if (std::fabs(candidate_col.coefs[i]) > scaled_diagonal_abs[candidate_col.rows[i]]) {
+          dominated = false;
+          break;
+        }
+      }
+      if (dominated) {
+        candidate_coeff = restricted_inf_norm(candidate_col, can_be_replaced, &candidate_row);
+        if (candidate_coeff != 0.0) enter_basis = true;
+      }
+    }
+    if (enter_basis) {
+      can_be_replaced[candidate_row] = false;
+      for (int64_t i = 0; i < candidate_col.n; ++i) {
+        if (candidate_col.coefs[i] != 0.0) has_zero_coefficient[candidate_col.rows[i]] = false;
+      }
+      const Fractional kBixbyLowThreshold = 0.01;
+      scaled_diagonal_abs[candidate_row] = kBixbyLowThreshold * std::fabs(candidate_coeff);
+      (*basis)[candidate_row] = candidate_col_index;
+    }
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -2518,6 +2709,31 @@ Status RevisedSimplex::CreateInitialBasis() {
       if (basis[row] == kInvalidCol) basis[row] = first_slack_col_ + row;
   }
   if (parameters_.initial_basis == 0) return InitializeFirstBasis(basis);
+  if (parameters_.initial_basis == 3) {  // MAROS (revised_simplex.cc:1200-1216)
+    if (parameters_.use_dual_simplex) {
+      GetMarosBasis<true>(compact_matrix_, objective_, variables_info_.GetTypeRow(), num_cols_,
+                          &basis);
+    } else {
+      GetMarosBasis<false>(compact_matrix_, objective_, variables_info_.GetTypeRow(), num_cols_,
+                           &basis);
+    }
+    return InitializeFirstBasis(basis);
+  }
+  if (parameters_.initial_basis == 1 && parameters_.use_scaling) {  // BIXBY
+    int num_fixed_variables = 0;
+    for (int row = 0; row < static_cast<int>(basis.size()); ++row) {
+      const int col = basis[row];
+      if (lb[col] == ub[col]) {
+        basis[row] = kInvalidCol;
+        ++num_fixed_variables;
+      }
+    }
+    if (num_fixed_variables != 0) {
+      CompleteBixbyBasis(compact_matrix_, objective_, lb, ub, variables_info_.GetTypeRow(),
+                         first_slack_col_, &basis);
+    }
+    return InitializeFirstBasis(basis);
+  }
   if (parameters_.initial_basis == 2) {  // TRIANGULAR
     int num_fixed_variables = 0;
     for (int row = 0; row < static_cast<int>(basis.size()); ++row) {
@@ -2540,7 +2756,6 @@ Status RevisedSimplex::CreateInitialBasis() {
       for (int row = 0; row < num_rows_; ++row) basis[row] = first_slack_col_ + row;
     }
   }
-  // MAROS / BIXBY are not restated (non-default): they behave as NONE here.
   return InitializeFirstBasis(basis);
 }
 

@@ -199,3 +199,49 @@ def test_product_form_against_highs(seed, dual):
         return
     assert r.problem_status == abi.OPTIMAL
     assert abs(r.objective - ref) <= 1e-6 * max(1.0, abs(ref))
+
+
+@pytest.mark.parametrize("basis", [1, 3])  # BIXBY, MAROS
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("dual", [0, 1])
+def test_crash_bases_against_highs(basis, seed, dual):
+    """initial_basis BIXBY and MAROS (initial_basis.cc:43-103, 208-356;
+    revised_simplex.cc:1197-1275), SURVEY 8(a) a26: optimal objective
+    unchanged. LPs with equality rows (fixed slacks) and all bound types,
+    so both crash procedures replace slacks."""
+    m = [12, 40, 90, 150][seed % 4]
+    n = [30, 70, 250, 400][seed % 4]
+    lp = lp_gen.random_sparse_lp(m, n, 0.3 if m < 30 else 0.06, 900 + seed,
+                                 eq_frac=0.5, maximize=bool(seed % 2))
+    # Columns scaled to infinity norm 1 (what BIXBY expects of a scaled LP).
+    for j in range(lp.n):
+        s0, s1 = lp.col_starts[j], lp.col_starts[j + 1]
+        if s1 > s0:
+            scale = np.abs(lp.vals[s0:s1]).max()
+            lp.vals[s0:s1] /= scale
+            lp.obj[j] /= scale
+            lp.col_lb[j] *= scale
+            lp.col_ub[j] *= scale
+    st, ref = lp_gen.to_scipy(lp)
+    o = oracle_lib.OracleLp(abi.default_params(use_dual_simplex=dual, initial_basis=basis))
+    o.load(lp)
+    r = o.solve()
+    if st != 0:
+        assert r.problem_status != abi.OPTIMAL
+        return
+    assert r.problem_status == abi.OPTIMAL
+    assert abs(r.objective - ref) <= 1e-6 * max(1.0, abs(ref))
+
+
+@pytest.mark.parametrize("basis", [1, 3])
+@pytest.mark.parametrize("builder", kat_lps.ALL, ids=lambda f: f.__name__)
+def test_crash_bases_known_answers(builder, basis):
+    lp, exp = builder()
+    o = oracle_lib.OracleLp(abi.default_params(initial_basis=basis))
+    o.load(lp)
+    r = o.solve()
+    if "status_in" in exp:
+        assert abi.PROBLEM_STATUS[r.problem_status] in exp["status_in"]
+        return
+    assert r.problem_status == exp["status"]
+    assert r.objective == pytest.approx(exp["objective"], rel=1e-9, abs=1e-9)

@@ -397,3 +397,24 @@ def test_product_form_dense_parity():
     p = abi.default_params(use_middle_product_form_update=0)
     o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
     parity_util.compare(o, ro, g, rg, lp)
+
+
+@pytest.mark.parametrize("basis", [1, 3])  # BIXBY, MAROS
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("dual", [0, 1])
+def test_crash_basis_parity(basis, seed, dual):
+    """initial_basis BIXBY / MAROS: engine == oracle."""
+    m = [40, 90, 150, 200][seed % 4]
+    n = [70, 250, 400, 900][seed % 4]
+    lp = lp_gen.random_sparse_lp(m, n, 0.06, 900 + seed, eq_frac=0.5, maximize=bool(seed % 2))
+    for j in range(lp.n):
+        s0, s1 = lp.col_starts[j], lp.col_starts[j + 1]
+        if s1 > s0:
+            scale = np.abs(lp.vals[s0:s1]).max()
+            lp.vals[s0:s1] /= scale
+            lp.obj[j] /= scale
+            lp.col_lb[j] *= scale
+            lp.col_ub[j] *= scale
+    p = abi.default_params(use_dual_simplex=dual, initial_basis=basis)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
