@@ -126,6 +126,11 @@ class DeviceLp {
   void EndKernel(int id, double bytes);
   void Compact(int n);  // flags_ -> list_ (ascending) + coefficients, async
   void NextRowTag();
+  void UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
+                             const std::vector<double>& rho, int algorithm, double drop,
+                             double entries);
+  void UploadMask(Mask which);
+  void FlushRelevantMask();
   void CopyHost(void* dst, const void* src, size_t bytes);
   void AccountList(const std::vector<int>& positions);
   void BuildDenseBlock();
@@ -234,6 +239,19 @@ class DeviceLp {
   int32_t* d_map_list_ = nullptr;
   double* d_map_vals_ = nullptr;
   bool mapped_result_ = false;  // the last Compact wrote to h_map_
+  // Small LPs (N <= kSmallLdsCols): the row-wise update row is one launch
+  // (row_wise_small_kernel) reading its inputs, including the relevant mask,
+  // from mapped host memory (MILP_SMALL_FUSED=off disables).
+  bool small_fused_enabled_ = true;
+  void* h_small_in_ = nullptr;
+  int32_t* h_small_rows_ = nullptr;
+  double* h_small_rho_ = nullptr;
+  uint64_t* h_small_mask_ = nullptr;
+  const int32_t* d_small_rows_ = nullptr;
+  const double* d_small_rho_ = nullptr;
+  const uint64_t* d_small_mask_ = nullptr;
+  bool mask_dirty_ = false;  // h_masks_[kRelevant] not yet uploaded
+  bool small_inflight_ = false;  // a launch may still read h_small_in_
   // dual device mode
   bool dual_ready_ = false;
   double* d_rc_ = nullptr;

@@ -50,6 +50,7 @@ DeviceLp::~DeviceLp() {
   if (h_pin_off_) (void)hipHostFree(h_pin_off_);
   if (h_pin_count_) (void)hipHostFree(h_pin_count_);
   if (h_map_) (void)hipHostFree(h_map_);
+  if (h_small_in_) (void)hipHostFree(h_small_in_);
   for (void* p : {static_cast<void*>(h_cand_col_), static_cast<void*>(h_cand_coeff_),
                   static_cast<void*>(h_cand_rc_), static_cast<void*>(h_dual_counts_),
                   static_cast<void*>(h_cb_cols_), static_cast<void*>(h_cb_bits_),
@@ -100,6 +101,9 @@ void DeviceLp::Init(int device) {
   if (const char* f = std::getenv("MILP_FULL_ROWS")) {
     full_rows_enabled_ = std::strcmp(f, "off") != 0;
   }
+  if (const char* f = std::getenv("MILP_SMALL_FUSED")) {
+    small_fused_enabled_ = std::strcmp(f, "off") != 0;
+  }
 }
 
 template <typename T>
@@ -121,7 +125,10 @@ void DeviceLp::Download(void* dst, const void* src, size_t bytes) {
   Check(hipStreamSynchronize(S(stream_)), "sync");
 }
 
-void DeviceLp::Synchronize() { Check(hipStreamSynchronize(S(stream_)), "sync"); }
+void DeviceLp::Synchronize() {
+  Check(hipStreamSynchronize(S(stream_)), "sync");
+  small_inflight_ = false;
+}
 
 void DeviceLp::ResetStats() { std::memset(&stats_, 0, sizeof(stats_)); }
 
@@ -249,6 +256,28 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
     d_map_list_ = reinterpret_cast<int32_t*>(dbase + list_off);
     d_map_vals_ = reinterpret_cast<double*>(dbase + vals_off);
   }
+  if (h_small_in_ != nullptr) (void)hipHostFree(h_small_in_);
+  h_small_in_ = nullptr;
+  small_inflight_ = false;
+  mask_dirty_ = false;
+  if (n_total_ <= milp_kernels::kSmallLdsCols) {
+    const int cap = milp_kernels::kSmallRowsMax;
+    const size_t rho_off = size_t(cap) * sizeof(int32_t);
+    const size_t mask_off = rho_off + size_t(cap) * sizeof(double);
+    Check(hipHostMalloc(&h_small_in_, mask_off + size_t(mask_words_) * sizeof(uint64_t),
+                        hipHostMallocMapped),
+          "mapped");
+    char* base = static_cast<char*>(h_small_in_);
+    h_small_rows_ = reinterpret_cast<int32_t*>(base);
+    h_small_rho_ = reinterpret_cast<double*>(base + rho_off);
+    h_small_mask_ = reinterpret_cast<uint64_t*>(base + mask_off);
+    void* dev = nullptr;
+    Check(hipHostGetDevicePointer(&dev, h_small_in_, 0), "mapped pointer");
+    const char* dbase = static_cast<const char*>(dev);
+    d_small_rows_ = reinterpret_cast<const int32_t*>(dbase);
+    d_small_rho_ = reinterpret_cast<const double*>(dbase + rho_off);
+    d_small_mask_ = reinterpret_cast<const uint64_t*>(dbase + mask_off);
+  }
   mapped_result_ = false;
   list_count_ = 0;
   dual_ready_ = false;
@@ -301,6 +330,7 @@ void DeviceLp::BuildDenseBlock() {
 
 void DeviceLp::LaunchColumnDots(int mode, const double* d_y, const double* d_c,
                                 double* d_out, const double* d_y2, double* d_out2) {
+  FlushRelevantMask();
   milp_kernels::DotArgs a{};
   a.starts = d_starts_;
   a.rows = d_rows_;
@@ -350,13 +380,28 @@ void DeviceLp::SetMask(Mask which, const uint64_t* words, int num_words) {
   if (num_words != mask_words_) throw DeviceError("mask size mismatch");
   if (std::memcmp(h.data(), words, num_words * sizeof(uint64_t)) == 0) return;
   std::memcpy(h.data(), words, num_words * sizeof(uint64_t));
+  if (which == kRelevant && small_fused_enabled_ && h_small_in_ != nullptr) {
+    // Small LPs: the relevant set changes every pivot and the small update
+    // row reads it from mapped host memory; other kernels flush it first.
+    mask_dirty_ = true;
+    return;
+  }
+  UploadMask(which);
+}
+
+void DeviceLp::UploadMask(Mask which) {
   // Asynchronous copy from a pinned slot; the slot is reused only once its
   // previous copy has completed.
   hipEvent_t done = reinterpret_cast<hipEvent_t>(ev_mask_[which]);
   Check(hipEventSynchronize(done), "mask event");
-  std::memcpy(h_pin_mask_[which], words, num_words * sizeof(uint64_t));
-  Upload(d_masks_[which], h_pin_mask_[which], num_words * sizeof(uint64_t));
+  std::memcpy(h_pin_mask_[which], h_masks_[which].data(), mask_words_ * sizeof(uint64_t));
+  Upload(d_masks_[which], h_pin_mask_[which], mask_words_ * sizeof(uint64_t));
   Check(hipEventRecord(done, S(stream_)), "mask event");
+  if (which == kRelevant) mask_dirty_ = false;
+}
+
+void DeviceLp::FlushRelevantMask() {
+  if (mask_dirty_) UploadMask(kRelevant);
 }
 
 // Compaction of the update-row flags into the ascending list of listed
@@ -427,6 +472,15 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
   CallTimer timer(&stats_, algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW);
   const int k = static_cast<int>(filtered_rows.size());
   fused_ready_ = false;
+  if (small_fused_enabled_ && h_small_in_ != nullptr && k <= milp_kernels::kSmallRowsMax) {
+    double entries = 0.0;
+    for (int r : filtered_rows) entries += double(h_t_starts_[r + 1] - h_t_starts_[r]);
+    if (entries <= milp_kernels::kSmallEntries) {
+      UpdateRowRowWiseSmall(filtered_rows, rho, algorithm, drop, entries);
+      return;
+    }
+  }
+  FlushRelevantMask();
   std::memcpy(h_pin_i_, filtered_rows.data(), k * sizeof(int32_t));
   for (int i = 0; i < k; ++i) h_pin_d_[i] = rho[filtered_rows[i]];
   Upload(d_cols_, h_pin_i_, k * sizeof(int32_t));
@@ -506,6 +560,50 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
   for (int r : filtered_rows) entries += double(h_t_starts_[r + 1] - h_t_starts_[r]);
   EndKernel(id, 12.0 * entries + 12.0 * k + 9.0 * n_total_);
   Compact(n_total_);
+}
+
+// Small LPs: inputs in mapped host memory, one launch, the list comes back in
+// mapped host memory (FetchUpdateRow's stream sync is the only round trip).
+void DeviceLp::UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
+                                     const std::vector<double>& rho, int algorithm,
+                                     double drop, double entries) {
+  const int k = static_cast<int>(filtered_rows.size());
+  // The previous launch may still be reading the inputs when no sync came
+  // in between (not the case in the simplex loop, which fetches every row).
+  if (small_inflight_) Synchronize();
+  for (int i = 0; i < k; ++i) {
+    h_small_rows_[i] = filtered_rows[i];
+    h_small_rho_[i] = rho[filtered_rows[i]];
+  }
+  std::memcpy(h_small_mask_, h_masks_[kRelevant].data(), mask_words_ * sizeof(uint64_t));
+  milp_kernels::RowWiseSmallArgs a{};
+  a.t_starts = d_t_starts_;
+  a.t_cols = d_t_cols_;
+  a.t_vals = d_t_vals_;
+  a.filtered_rows = d_small_rows_;
+  a.rho = d_small_rho_;
+  a.num_filtered = k;
+  a.num_cols = n_total_;
+  a.relevant = d_small_mask_;
+  a.coefficient = d_coeff_;
+  a.flags = d_flags_;
+  a.drop_tolerance = drop;
+  a.algorithm = algorithm;
+  a.list = d_list_;
+  a.vals = d_out_list_;
+  a.count = d_count_;
+  a.host_list = d_map_list_;
+  a.host_vals = d_map_vals_;
+  a.host_count = d_map_count_;
+  const int id = algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW;
+  BeginKernel(id);
+  Check(milp_launch::row_wise_update_small(a, S(stream_)), "rowwise small");
+  // Rows and multipliers, the CSR entries, N-sized flags/coefficients, the list.
+  EndKernel(id, 12.0 * entries + 12.0 * k + 9.0 * n_total_);
+  small_inflight_ = true;
+  mapped_result_ = true;
+  list_count_ = -1;  // known after FetchUpdateRow
+  ++list_epoch_;
 }
 
 void DeviceLp::NextRowTag() {
@@ -705,6 +803,7 @@ void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& 
 void DeviceLp::ColumnSquaredNorms(std::vector<double>* out) {
   CallTimer timer(&stats_, MI_K_COL_NORMS);
   fused_ready_ = false;  // d_out_n_ is reused below
+  FlushRelevantMask();
   BeginKernel(MI_K_COL_NORMS);
   Check(milp_launch::column_squared_norms(d_starts_, d_vals_, d_masks_[kRelevant], n_total_,
                                           d_out_n_, S(stream_)),

@@ -65,6 +65,35 @@ struct RowWiseArgs {
   int algorithm;  // 0 single row, 1 hypersparse, 2 row-wise
 };
 
+// The whole row-wise update row of a small LP in ONE workgroup and one launch
+// (row_wise_small_kernel): N <= kSmallLdsCols, 1 <= filtered rows <=
+// kSmallRowsMax, their entries <= kSmallEntries (checked by the host). The
+// filtered rows, their rho values and the relevant mask are read from mapped
+// host memory; the list lands in mapped host memory (and the device copies).
+constexpr int kSmallLdsCols = 8192;
+constexpr int kSmallRowsMax = 1024;
+constexpr int kSmallEntries = 4096;
+struct RowWiseSmallArgs {
+  const int64_t* t_starts;
+  const int32_t* t_cols;
+  const double* t_vals;
+  const int32_t* filtered_rows;  // mapped host memory, list order
+  const double* rho;             // mapped host memory, rho per filtered row
+  int num_filtered;
+  int num_cols;
+  const uint64_t* relevant;      // mapped host memory
+  double* coefficient;
+  uint8_t* flags;
+  double drop_tolerance;
+  int algorithm;  // 0 single row, 1 hypersparse, 2 row-wise
+  int32_t* list;  // device copies of the compacted list
+  double* vals;
+  int* count;
+  int32_t* host_list;  // mapped host memory
+  double* host_vals;
+  int* host_count;
+};
+
 // The row-wise update row when every filtered row is full (all structural
 // columns present): entry j < num_structural of CSR row r is column j and the
 // row's last entry is its slack column. Slack outputs use the row tags.
@@ -166,6 +195,7 @@ hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32
                          double* vals, int* count, int32_t* host_list, double* host_vals,
                          int* host_count, hipStream_t s);
 hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s);
+hipError_t row_wise_update_small(const milp_kernels::RowWiseSmallArgs& args, hipStream_t s);
 // Marks the filtered rows (row_tag[r] = tag, row_pos[r] = list position).
 hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag,
                     uint32_t* row_tag, int32_t* row_pos, hipStream_t s);

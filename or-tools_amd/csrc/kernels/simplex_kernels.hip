@@ -420,6 +420,134 @@ __global__ __launch_bounds__(256) void row_wise_update_kernel(RowWiseArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Small LPs: the row-wise update row, its epilogue and the compaction in one
+// workgroup and one launch (RowWiseSmallArgs), with no copies: for LPs with a
+// few thousand columns the queue latency per operation, not the bytes, bounds
+// an iteration, and a serial walk over global memory would pay a memory
+// round trip per row. So every global load is issued in one of two parallel
+// waves (row extents, then all entries, products formed on the way), the
+// accumulation runs out of LDS, and the list goes straight to mapped host
+// memory. Arithmetic as row_wise_update_kernel: the rows are applied in list
+// order with a barrier between rows (a position appears once per row, so one
+// thread owns it within a row), with the same first-write rule per algorithm.
+__global__ __launch_bounds__(kCompactThreads) void row_wise_small_kernel(RowWiseSmallArgs a) {
+  __shared__ double acc[kSmallLdsCols];
+  __shared__ uint8_t touched[kSmallLdsCols];
+  __shared__ uint64_t rel[kSmallLdsCols / 64];
+  __shared__ int32_t ent_pos[kSmallEntries];
+  __shared__ double ent_val[kSmallEntries];
+  __shared__ double s_rho[kSmallRowsMax];
+  __shared__ int64_t s_off[kSmallRowsMax];
+  __shared__ int s_beg[kSmallRowsMax + 1];
+  __shared__ int sums[kCompactThreads];
+  const int t = threadIdx.x;
+  const int n = a.num_cols;
+  const int k_rows = a.num_filtered;
+  for (int i = t; i < n; i += kCompactThreads) touched[i] = 0;
+  for (int w = t; w < (n + 63) / 64; w += kCompactThreads) rel[w] = a.relevant[w];
+  // Wave 1: row extents (one row per thread; k_rows <= kCompactThreads).
+  int len = 0;
+  if (t < k_rows) {
+    const int r = a.filtered_rows[t];
+    s_rho[t] = a.rho[t];
+    const int64_t b = a.t_starts[r];
+    s_off[t] = b;
+    len = static_cast<int>(a.t_starts[r + 1] - b);
+  }
+  sums[t] = len;
+  __syncthreads();
+  for (int off = 1; off < kCompactThreads; off <<= 1) {
+    const int v = t >= off ? sums[t - off] : 0;
+    __syncthreads();
+    sums[t] += v;
+    __syncthreads();
+  }
+  if (t < k_rows) s_beg[t] = sums[t] - len;
+  if (t == 0) s_beg[k_rows] = sums[kCompactThreads - 1];
+  __syncthreads();
+  // Wave 2: every entry of every filtered row, product rho_k * A[r_k, pos].
+  const int num_entries = s_beg[k_rows];  // <= kSmallEntries (host-checked)
+  for (int e = t; e < num_entries; e += kCompactThreads) {
+    int lo = 0;
+    int hi = k_rows - 1;
+    while (lo < hi) {  // last row k with s_beg[k] <= e
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_beg[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    const int64_t i = s_off[lo] + (e - s_beg[lo]);
+    ent_pos[e] = a.t_cols[i];
+    ent_val[e] = s_rho[lo] * a.t_vals[i];
+  }
+  __syncthreads();
+  for (int k = 0; k < k_rows; ++k) {
+    for (int e = s_beg[k] + t; e < s_beg[k + 1]; e += kCompactThreads) {
+      const int pos = ent_pos[e];
+      const double v = ent_val[e];
+      double out;
+      if (a.algorithm == 0) {
+        out = v;
+      } else if (!touched[pos]) {
+        out = a.algorithm == 2 ? 0.0 + v : v;
+      } else {
+        out = acc[pos] + v;
+      }
+      acc[pos] = out;
+      touched[pos] = 1;
+    }
+    __syncthreads();  // rows are applied in order
+  }
+  // Epilogue over this thread's slice of positions (<= 8 with N <= 8192).
+  const int per = (n + kCompactThreads - 1) / kCompactThreads;
+  const int b = min(n, t * per);
+  const int e = min(n, b + per);
+  uint32_t listed_bits = 0;
+  int c = 0;
+  for (int pos = b; pos < e; ++pos) {
+    const bool was_touched = touched[pos] != 0;
+    const double v = was_touched ? acc[pos] : 0.0;
+    const bool is_rel = (rel[pos >> 6] >> (pos & 63)) & 1ull;
+    bool listed;
+    if (a.algorithm == 0) {
+      listed = was_touched && is_rel && fabs(v) > a.drop_tolerance;
+      if (listed) a.coefficient[pos] = v;
+    } else if (a.algorithm == 1) {
+      listed = was_touched && is_rel && fabs(v) > a.drop_tolerance;
+      if (was_touched) a.coefficient[pos] = v;
+    } else {
+      listed = is_rel && fabs(v) > a.drop_tolerance;
+      a.coefficient[pos] = was_touched ? v : 0.0;
+    }
+    a.flags[pos] = listed ? 1 : 0;
+    listed_bits |= uint32_t(listed) << (pos - b);
+    c += listed;
+  }
+  __syncthreads();
+  sums[t] = c;
+  __syncthreads();
+  for (int off = 1; off < kCompactThreads; off <<= 1) {
+    const int v = t >= off ? sums[t - off] : 0;
+    __syncthreads();
+    sums[t] += v;
+    __syncthreads();
+  }
+  int out_pos = sums[t] - c;
+  for (int pos = b; pos < e; ++pos) {
+    if ((listed_bits >> (pos - b)) & 1u) {
+      const double v = acc[pos];  // a listed position was touched: its value
+      a.list[out_pos] = pos;
+      a.vals[out_pos] = v;
+      a.host_list[out_pos] = pos;
+      a.host_vals[out_pos] = v;
+      ++out_pos;
+    }
+  }
+  if (t == kCompactThreads - 1) {
+    *a.count = sums[t];
+    *a.host_count = sums[t];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // The row-wise update row for many filtered rows, one thread per column.
 // Per column the result must be the host scatter's: contributions
 // rho_k * A[r_k, j] accumulated in the order k of the filtered list (which
@@ -969,6 +1097,15 @@ hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32
 hipError_t row_wise_update(const RowWiseArgs& args, hipStream_t s) {
   const int blocks = div_up(args.num_cols, kChunk);
   row_wise_update_kernel<<<blocks, 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t row_wise_update_small(const RowWiseSmallArgs& args, hipStream_t s) {
+  if (args.num_cols > kSmallLdsCols || args.num_filtered > kSmallRowsMax ||
+      args.num_filtered < 0) {
+    return hipErrorInvalidValue;
+  }
+  row_wise_small_kernel<<<1, kCompactThreads, 0, s>>>(args);
   return hipGetLastError();
 }
 

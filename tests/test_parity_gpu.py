@@ -91,6 +91,7 @@ def test_row_wise_kernel_choice_parity(seed, chunk_max, monkeypatch):
     the host scatter order, so the dual simplex matches the oracle bit for bit
     either way. Config-5-shaped LPs (a few entries per column)."""
     monkeypatch.setenv("MILP_ROWWISE_CHUNK_MAX_ROWS", chunk_max)
+    monkeypatch.setenv("MILP_SMALL_FUSED", "off")  # these N would take the one-launch kernel
     lp = lp_gen.sparse_c5_lp(300 + 50 * (seed % 3), 3000, 6, seed)
     p = abi.default_params(use_dual_simplex=1)
     o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
@@ -108,6 +109,7 @@ def test_full_row_kernel_parity(shape, dual, full_rows, monkeypatch):
     order k, slack outputs through the row tags) unless disabled. Both ways
     must match the oracle bit for bit, in primal and dual simplex."""
     monkeypatch.setenv("MILP_FULL_ROWS", full_rows)
+    monkeypatch.setenv("MILP_SMALL_FUSED", "off")
     m, n, seed = shape
     lp = lp_gen.dense_box_lp(m, n, seed)
     p = abi.default_params(use_dual_simplex=dual)
@@ -120,6 +122,7 @@ def test_full_row_kernel_parity(shape, dual, full_rows, monkeypatch):
 def test_full_and_partial_rows_parity(monkeypatch):
     """Some rows full, some not: a filtered list that mixes them takes the
     general row-wise kernels, an all-full list the full-row kernel."""
+    monkeypatch.setenv("MILP_SMALL_FUSED", "off")
     rng = np.random.default_rng(9)
     m, n = 70, 400
     dense = rng.uniform(-1, 1, size=(m, n))
@@ -220,6 +223,33 @@ def test_invalid_problem_status():
     assert r.problem_status == abi.INVALID_PROBLEM
     o, ro, g, rg = parity_util.solve_both(lp, abi.default_params(), _handle)
     parity_util.compare(o, ro, g, rg, lp)
+
+
+@pytest.mark.parametrize("fused", ["on", "off"])
+@pytest.mark.parametrize("dual", [0, 1])
+@pytest.mark.parametrize("case", ["sparse", "c5", "dense", "jobshop"])
+def test_small_lp_one_launch_update_row_parity(case, dual, fused, monkeypatch):
+    """Small LPs (N <= 8192): the row-wise update row runs as one launch
+    (row_wise_small_kernel: inputs and the relevant mask from mapped host
+    memory, LDS accumulation in list order, compaction into mapped host
+    memory). Dense rows overflow its entry budget, so the dense case mixes it
+    with the generic kernels within one solve (deferred mask uploads). Bit
+    for bit equal to the oracle, fused or not."""
+    monkeypatch.setenv("MILP_SMALL_FUSED", fused)
+    if case == "sparse":
+        lp = lp_gen.random_sparse_lp(200, 900, 0.04, 7, maximize=True)
+    elif case == "c5":
+        lp = lp_gen.sparse_c5_lp(400, 4000, 6, 41)
+    elif case == "dense":
+        lp = lp_gen.dense_box_lp(120, 900, 5)
+    else:
+        import jobshop
+        lp, _ = jobshop.relaxation(jobshop.random_instance(8, 6, 5))
+    p = abi.default_params(use_dual_simplex=dual)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    st = g.kernel_stats()
+    assert st["update_row"]["launches"] + st["single_row"]["launches"] > 0
 
 
 @pytest.mark.parametrize("shape", [(6, 6), (10, 10)])
