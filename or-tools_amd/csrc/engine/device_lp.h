@@ -250,6 +250,10 @@ class DeviceLp {
   const int32_t* d_small_rows_ = nullptr;
   const double* d_small_rho_ = nullptr;
   const uint64_t* d_small_mask_ = nullptr;
+  double* h_small_y_ = nullptr;    // list-dots input (m)
+  double* h_small_out_ = nullptr;  // list-dots output (N)
+  const double* d_small_y_ = nullptr;
+  double* d_small_out_ = nullptr;
   bool mask_dirty_ = false;  // h_masks_[kRelevant] not yet uploaded
   bool small_inflight_ = false;  // a launch may still read h_small_in_
   // dual device mode

@@ -264,7 +264,9 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
     const int cap = milp_kernels::kSmallRowsMax;
     const size_t rho_off = size_t(cap) * sizeof(int32_t);
     const size_t mask_off = rho_off + size_t(cap) * sizeof(double);
-    Check(hipHostMalloc(&h_small_in_, mask_off + size_t(mask_words_) * sizeof(uint64_t),
+    const size_t y_off = mask_off + size_t(mask_words_) * sizeof(uint64_t);
+    const size_t out_off = y_off + size_t(m_) * sizeof(double);
+    Check(hipHostMalloc(&h_small_in_, out_off + size_t(n_total_) * sizeof(double),
                         hipHostMallocMapped),
           "mapped");
     char* base = static_cast<char*>(h_small_in_);
@@ -277,6 +279,10 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
     d_small_rows_ = reinterpret_cast<const int32_t*>(dbase);
     d_small_rho_ = reinterpret_cast<const double*>(dbase + rho_off);
     d_small_mask_ = reinterpret_cast<const uint64_t*>(dbase + mask_off);
+    h_small_y_ = reinterpret_cast<double*>(base + y_off);
+    h_small_out_ = reinterpret_cast<double*>(base + out_off);
+    d_small_y_ = reinterpret_cast<const double*>(dbase + y_off);
+    d_small_out_ = reinterpret_cast<double*>(const_cast<char*>(dbase) + out_off);
   }
   mapped_result_ = false;
   list_count_ = 0;
@@ -714,6 +720,26 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
     return;
   }
   fused_ready_ = false;
+  if (small_fused_enabled_ && h_small_in_ != nullptr && nd_ == 0) {
+    // Small LP: one launch, v in and the dots out through mapped host memory.
+    if (small_inflight_) Synchronize();
+    std::memcpy(h_small_y_, v.data(), m_ * sizeof(double));
+    milp_kernels::ListDotsSmallArgs a{};
+    a.starts = d_starts_;
+    a.rows = d_rows_;
+    a.vals = d_vals_;
+    a.y = d_small_y_;
+    a.m = m_;
+    a.list = d_list_;
+    a.n = n;
+    a.out = d_small_out_;
+    BeginKernel(MI_K_PRIMAL_NORMS);
+    Check(milp_launch::list_dots_small(a, S(stream_)), "list dots small");
+    EndKernel(MI_K_PRIMAL_NORMS, 12.0 * double(list_entries_) + 8.0 * m_ + 4.0 * n + 8.0 * n);
+    Synchronize();
+    std::memcpy(out->data(), h_small_out_, n * sizeof(double));
+    return;
+  }
   std::memcpy(h_pin_d2_, v.data(), m_ * sizeof(double));
   Upload(d_vec_m_, h_pin_d2_, m_ * sizeof(double));
   BeginKernel(MI_K_PRIMAL_NORMS);

@@ -871,6 +871,7 @@ BasisFactorization::BasisFactorization(const CompactSparseMatrix* matrix,
     if (std::strcmp(e, "off") == 0) async_min_rows_ = -1;
     if (std::strcmp(e, "force") == 0) async_min_rows_ = 0;
   }
+  if (const char* e = std::getenv("MILP_INLINE_TAU")) inline_tau_ = std::strcmp(e, "off") != 0;
 }
 
 BasisFactorization::~BasisFactorization() {
@@ -893,7 +894,7 @@ uint64_t BasisFactorization::StartAsync(AsyncKind kind, std::function<void()> jo
 
 bool BasisFactorization::TakeAsync(uint64_t ticket) const {
   if (async_kind_ == AsyncKind::kNone || ticket != async_ticket_) return false;
-  async_->Wait();
+  if (async_) async_->Wait();
   async_kind_ = AsyncKind::kNone;
   async_input_ = nullptr;
   // The worker's deterministic-time bumps land now, where the serial solve
@@ -906,7 +907,7 @@ bool BasisFactorization::TakeAsync(uint64_t ticket) const {
 
 void BasisFactorization::DropAsync() const {
   if (async_kind_ == AsyncKind::kNone) return;
-  async_->Wait();
+  if (async_) async_->Wait();
   async_kind_ = AsyncKind::kNone;
   async_input_ = nullptr;
   rank_one_factorization_.TakeDeferredBumps(false);
@@ -914,7 +915,7 @@ void BasisFactorization::DropAsync() const {
 }
 
 void BasisFactorization::WaitAsync() const {
-  if (async_kind_ != AsyncKind::kNone) async_->Wait();
+  if (async_kind_ != AsyncKind::kNone && async_) async_->Wait();
 }
 
 // The body of RightSolveForTau (basis_representation.cc:374-398) into *out,
@@ -942,6 +943,28 @@ void BasisFactorization::StartAsyncTau(const ScatteredVector& rho) const {
     if (can_be_optimized) async_tau_ = tau_;
     ComputeTauInto(can_be_optimized, rho, &async_tau_);
   });
+  async_input_ = &rho;
+}
+
+// Below the worker-thread size the same tau is computed on the calling thread
+// while the GPU computes the update row (the caller launches it first): the
+// result and its deferred deterministic-time bumps are handed over through
+// the same slot and ticket as the worker's, so TakeAsync/DropAsync behave
+// identically (solve scratch slot 1, bumps applied when taken).
+bool BasisFactorization::InlineTauEnabled() const {
+  return inline_tau_ && use_middle_product_form_update_ && !AsyncEnabled();
+}
+
+void BasisFactorization::ComputeTauNow(const ScatteredVector& rho) const {
+  DropAsync();
+  const bool can_be_optimized = tau_computation_can_be_optimized_;
+  async_kind_ = AsyncKind::kTau;
+  tau_ticket_ = ++async_ticket_;
+  const int saved_slot = g_lu_slot;
+  g_lu_slot = 1;
+  if (can_be_optimized) async_tau_ = tau_;
+  ComputeTauInto(can_be_optimized, rho, &async_tau_);
+  g_lu_slot = saved_slot;
   async_input_ = &rho;
 }
 

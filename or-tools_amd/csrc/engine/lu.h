@@ -1043,6 +1043,9 @@ class BasisFactorization {
   // applied when it is taken, so results and timing match the serial order.
   enum class AsyncKind { kNone, kTau, kLeftSolve };
   void StartAsyncTau(const ScatteredVector& rho) const;
+  // Small bases: tau on the calling thread, overlapped with the GPU update row.
+  bool InlineTauEnabled() const;
+  void ComputeTauNow(const ScatteredVector& rho) const;
   // The same for a caller's BTRAN (the primal loop's B^-T d): job runs
   // LeftSolve on the worker; TakeAsync(ticket) waits for it and applies its
   // bumps, and returns false if it was dropped (then the caller solves).
@@ -1120,6 +1123,7 @@ class BasisFactorization {
   mutable ScatteredVector async_tau_;
   mutable std::vector<int64_t> deferred_solve_entries_;
   int async_min_rows_ = 16384;
+  bool inline_tau_ = true;  // MILP_INLINE_TAU=off disables ComputeTauNow's use
   mutable bool tau_is_computed_ = false;
   mutable bool tau_computation_can_be_optimized_ = false;
   mutable ScatteredVector tau_;

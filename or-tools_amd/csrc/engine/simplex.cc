@@ -4583,10 +4583,19 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     }
     // tau = B^-1 rho needs only rho: it is computed on the factorization's
     // worker thread while the update row, ratio test and direction run.
-    if (dual_edge_norms_.WillComputeTau()) {
+    // Small bases compute it on this thread while the GPU computes the update
+    // row (launched first, fetched after).
+    const bool tau_inline = dual_edge_norms_.WillComputeTau() && !dual_device_mode_ &&
+                            basis_factorization_.InlineTauEnabled();
+    if (dual_edge_norms_.WillComputeTau() && !tau_inline) {
       basis_factorization_.StartAsyncTau(update_row_.GetUnitRowLeftInverse());
     }
+    if (tau_inline) update_row_.SetLazyFetch(true);
     update_row_.ComputeUpdateRow(leaving_row);
+    if (tau_inline) {
+      basis_factorization_.ComputeTauNow(update_row_.GetUnitRowLeftInverse());
+      update_row_.SetLazyFetch(false);
+    }
     if (!dual_device_mode_) update_row_.GetNonZeroPositions();  // timed as the update row
     clock.Mark(3);
 

@@ -71,6 +71,20 @@ struct RowWiseArgs {
 // filtered rows, their rho values and the relevant mask are read from mapped
 // host memory; the list lands in mapped host memory (and the device copies).
 constexpr int kSmallLdsCols = 8192;
+// out[k] = a_{list[k]} . y for a small LP without a dense block, one
+// workgroup: y (m <= kSmallLdsCols) staged from mapped host memory into LDS,
+// 4 lanes per column in ColumnScalarProduct's chain order, the results
+// written straight to mapped host memory.
+struct ListDotsSmallArgs {
+  const int64_t* starts;
+  const int32_t* rows;
+  const double* vals;
+  const double* y;  // mapped host memory, m values
+  int m;
+  const int32_t* list;  // device: compacted update-row list
+  int n;
+  double* out;  // mapped host memory
+};
 constexpr int kSmallRowsMax = 1024;
 constexpr int kSmallEntries = 4096;
 struct RowWiseSmallArgs {
@@ -196,6 +210,7 @@ hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32
                          int* host_count, hipStream_t s);
 hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s);
 hipError_t row_wise_update_small(const milp_kernels::RowWiseSmallArgs& args, hipStream_t s);
+hipError_t list_dots_small(const milp_kernels::ListDotsSmallArgs& args, hipStream_t s);
 // Marks the filtered rows (row_tag[r] = tag, row_pos[r] = list position).
 hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag,
                     uint32_t* row_tag, int32_t* row_pos, hipStream_t s);

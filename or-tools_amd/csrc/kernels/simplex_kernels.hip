@@ -547,6 +547,27 @@ __global__ __launch_bounds__(kCompactThreads) void row_wise_small_kernel(RowWise
   }
 }
 
+// Small LPs: the primal edge-norm dots over the update-row list in one launch
+// (ListDotsSmallArgs). The loop bound is uniform, so the 4 lanes of a column
+// stay converged through quad_column_dot's shuffles.
+__global__ __launch_bounds__(kCompactThreads) void list_dots_small_kernel(ListDotsSmallArgs a) {
+  __shared__ double s_y[kSmallLdsCols];
+  const int t = threadIdx.x;
+  for (int i = t; i < a.m; i += kCompactThreads) s_y[i] = a.y[i];
+  __syncthreads();
+  const int sub = t & 3;
+  const int lane = t & 63;
+  for (int base = 0; base < a.n; base += kCompactThreads / 4) {
+    const int slot = base + (t >> 2);
+    const bool in_range = slot < a.n;
+    const int col = a.list[in_range ? slot : 0];
+    const int64_t s = a.starts[col];
+    const int64_t e = in_range ? a.starts[col + 1] : s;
+    const double dot = quad_column_dot(s, e, a.rows, a.vals, s_y, sub, lane);
+    if (sub == 0 && in_range) a.out[slot] = dot;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // The row-wise update row for many filtered rows, one thread per column.
 // Per column the result must be the host scatter's: contributions
@@ -1106,6 +1127,12 @@ hipError_t row_wise_update_small(const RowWiseSmallArgs& args, hipStream_t s) {
     return hipErrorInvalidValue;
   }
   row_wise_small_kernel<<<1, kCompactThreads, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t list_dots_small(const ListDotsSmallArgs& args, hipStream_t s) {
+  if (args.m > kSmallLdsCols || args.n < 1) return hipErrorInvalidValue;
+  list_dots_small_kernel<<<1, kCompactThreads, 0, s>>>(args);
   return hipGetLastError();
 }
 

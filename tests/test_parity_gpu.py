@@ -233,9 +233,11 @@ def test_small_lp_one_launch_update_row_parity(case, dual, fused, monkeypatch):
     (row_wise_small_kernel: inputs and the relevant mask from mapped host
     memory, LDS accumulation in list order, compaction into mapped host
     memory). Dense rows overflow its entry budget, so the dense case mixes it
-    with the generic kernels within one solve (deferred mask uploads). Bit
-    for bit equal to the oracle, fused or not."""
+    with the generic kernels within one solve (deferred mask uploads). The
+    dual simplex computes tau while that launch runs (MILP_INLINE_TAU). Bit
+    for bit equal to the oracle (deterministic time included), either way."""
     monkeypatch.setenv("MILP_SMALL_FUSED", fused)
+    monkeypatch.setenv("MILP_INLINE_TAU", fused)  # tau overlapped with the launch
     if case == "sparse":
         lp = lp_gen.random_sparse_lp(200, 900, 0.04, 7, maximize=True)
     elif case == "c5":
