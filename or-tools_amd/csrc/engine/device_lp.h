@@ -129,6 +129,8 @@ class DeviceLp {
   void UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
                              const std::vector<double>& rho, int algorithm, double drop,
                              double entries);
+  void UpdateRowColumnWiseSmall(const std::vector<double>& rho, double drop,
+                                int64_t relevant_entries, const std::vector<double>* w);
   void UploadMask(Mask which);
   void FlushRelevantMask();
   void CopyHost(void* dst, const void* src, size_t bytes);
@@ -254,6 +256,11 @@ class DeviceLp {
   double* h_small_out_ = nullptr;  // list-dots output (N)
   const double* d_small_y_ = nullptr;
   double* d_small_out_ = nullptr;
+  double* h_small_w_ = nullptr;     // column-wise update row: w (m)
+  double* h_small_dots_ = nullptr;  // its w dots, list order (N)
+  const double* d_small_w_ = nullptr;
+  double* d_small_dots_ = nullptr;
+  bool small_dots_mapped_ = false;  // fused_ready_ dots are in h_small_dots_
   bool mask_dirty_ = false;  // h_masks_[kRelevant] not yet uploaded
   bool small_inflight_ = false;  // a launch may still read h_small_in_
   // dual device mode

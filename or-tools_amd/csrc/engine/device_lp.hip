@@ -265,8 +265,10 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
     const size_t rho_off = size_t(cap) * sizeof(int32_t);
     const size_t mask_off = rho_off + size_t(cap) * sizeof(double);
     const size_t y_off = mask_off + size_t(mask_words_) * sizeof(uint64_t);
-    const size_t out_off = y_off + size_t(m_) * sizeof(double);
-    Check(hipHostMalloc(&h_small_in_, out_off + size_t(n_total_) * sizeof(double),
+    const size_t w_off = y_off + size_t(m_) * sizeof(double);
+    const size_t out_off = w_off + size_t(m_) * sizeof(double);
+    const size_t dots_off = out_off + size_t(n_total_) * sizeof(double);
+    Check(hipHostMalloc(&h_small_in_, dots_off + size_t(n_total_) * sizeof(double),
                         hipHostMallocMapped),
           "mapped");
     char* base = static_cast<char*>(h_small_in_);
@@ -283,6 +285,10 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
     h_small_out_ = reinterpret_cast<double*>(base + out_off);
     d_small_y_ = reinterpret_cast<const double*>(dbase + y_off);
     d_small_out_ = reinterpret_cast<double*>(const_cast<char*>(dbase) + out_off);
+    h_small_w_ = reinterpret_cast<double*>(base + w_off);
+    h_small_dots_ = reinterpret_cast<double*>(base + dots_off);
+    d_small_w_ = reinterpret_cast<const double*>(dbase + w_off);
+    d_small_dots_ = reinterpret_cast<double*>(const_cast<char*>(dbase) + dots_off);
   }
   mapped_result_ = false;
   list_count_ = 0;
@@ -438,6 +444,12 @@ void DeviceLp::Compact(int n) {
 void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
                                    int64_t relevant_entries, const std::vector<double>* w) {
   CallTimer timer(&stats_, MI_K_UPDATE_ROW);
+  small_dots_mapped_ = false;
+  if (small_fused_enabled_ && h_small_in_ != nullptr && nd_ == 0 &&
+      m_ <= milp_kernels::kSmallColWiseRows) {
+    UpdateRowColumnWiseSmall(rho, drop, relevant_entries, w);
+    return;
+  }
   std::memcpy(h_pin_d_, rho.data(), m_ * sizeof(double));
   Upload(d_vec_m_, h_pin_d_, m_ * sizeof(double));
   if (w != nullptr) {
@@ -470,6 +482,52 @@ void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
                                  (w != nullptr ? 8.0 * m_ : 0.0));
   Compact(n_total_);
   fused_ready_ = (w != nullptr);
+}
+
+// Small LPs: rho (and w), the relevant mask, and the results through mapped
+// host memory, one launch; the w dots come back in list order with the list.
+void DeviceLp::UpdateRowColumnWiseSmall(const std::vector<double>& rho, double drop,
+                                        int64_t relevant_entries,
+                                        const std::vector<double>* w) {
+  if (small_inflight_) Synchronize();
+  std::memcpy(h_small_y_, rho.data(), m_ * sizeof(double));
+  if (w != nullptr) {
+    std::memcpy(h_small_w_, w->data(), m_ * sizeof(double));
+    fused_w_ = *w;
+  }
+  std::memcpy(h_small_mask_, h_masks_[kRelevant].data(), mask_words_ * sizeof(uint64_t));
+  fused_ready_ = false;
+  drop_ = drop;
+  milp_kernels::ColWiseSmallArgs a{};
+  a.starts = d_starts_;
+  a.rows = d_rows_;
+  a.vals = d_vals_;
+  a.rho = d_small_y_;
+  a.w = w != nullptr ? d_small_w_ : nullptr;
+  a.m = m_;
+  a.num_cols = n_total_;
+  a.relevant = d_small_mask_;
+  a.coefficient = d_coeff_;
+  a.flags = d_flags_;
+  a.out2 = d_out_n_;
+  a.drop_tolerance = drop;
+  a.list = d_list_;
+  a.vals_out = d_out_list_;
+  a.count = d_count_;
+  a.host_list = d_map_list_;
+  a.host_vals = d_map_vals_;
+  a.host_count = d_map_count_;
+  a.host_dots = d_small_dots_;
+  BeginKernel(MI_K_UPDATE_ROW);
+  Check(milp_launch::column_wise_update_small(a, S(stream_)), "colwise small");
+  EndKernel(MI_K_UPDATE_ROW, 12.0 * double(relevant_entries) + 8.0 * m_ + 9.0 * n_total_ +
+                                 (w != nullptr ? 8.0 * m_ : 0.0));
+  small_inflight_ = true;
+  mapped_result_ = true;
+  list_count_ = -1;  // known after FetchUpdateRow
+  ++list_epoch_;
+  fused_ready_ = (w != nullptr);
+  small_dots_mapped_ = (w != nullptr);
 }
 
 void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
@@ -714,6 +772,11 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
       std::memcmp(v.data(), fused_w_.data(), v.size() * sizeof(double)) == 0) {
     // Computed by the fused update-row pass: only the gather remains.
     fused_ready_ = false;
+    if (small_dots_mapped_) {  // already gathered, in list order
+      small_dots_mapped_ = false;
+      std::memcpy(out->data(), h_small_dots_, n * sizeof(double));
+      return;
+    }
     Check(milp_launch::gather(d_list_, n, d_out_n_, d_out_list_, S(stream_)), "gather");
     Download(h_pin_d_, d_out_list_, n * sizeof(double));
     std::memcpy(out->data(), h_pin_d_, n * sizeof(double));

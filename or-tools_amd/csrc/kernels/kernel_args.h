@@ -71,9 +71,38 @@ struct RowWiseArgs {
 // filtered rows, their rho values and the relevant mask are read from mapped
 // host memory; the list lands in mapped host memory (and the device copies).
 constexpr int kSmallLdsCols = 8192;
+// The column-wise update row of a small LP without a dense block (m <=
+// kSmallColWiseRows) in one workgroup: rho (and w) staged from mapped host
+// memory into LDS, one thread per relevant column in ColumnScalarProduct's chain
+// order, column_dot_kernel's kUpdateRowColumnWise / kUpdateRowWithDots write
+// rules, then the compaction; list, values (and the w dots, list order) land
+// in mapped host memory.
+constexpr int kSmallColWiseRows = 4096;
+struct ColWiseSmallArgs {
+  const int64_t* starts;
+  const int32_t* rows;
+  const double* vals;
+  const double* rho;       // mapped host memory, m values
+  const double* w;         // mapped host memory, m values, or nullptr
+  int m;
+  int num_cols;            // <= kSmallLdsCols
+  const uint64_t* relevant;  // mapped host memory
+  double* coefficient;
+  uint8_t* flags;
+  double* out2;            // w . a_j of kept columns (device, per column)
+  double drop_tolerance;
+  int32_t* list;  // device copies of the compacted list
+  double* vals_out;
+  int* count;
+  int32_t* host_list;  // mapped host memory
+  double* host_vals;
+  int* host_count;
+  double* host_dots;   // mapped host memory, list order (with w)
+};
+
 // out[k] = a_{list[k]} . y for a small LP without a dense block, one
 // workgroup: y (m <= kSmallLdsCols) staged from mapped host memory into LDS,
-// 4 lanes per column in ColumnScalarProduct's chain order, the results
+// one thread per column in ColumnScalarProduct's chain order, the results
 // written straight to mapped host memory.
 struct ListDotsSmallArgs {
   const int64_t* starts;
@@ -211,6 +240,7 @@ hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32
 hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s);
 hipError_t row_wise_update_small(const milp_kernels::RowWiseSmallArgs& args, hipStream_t s);
 hipError_t list_dots_small(const milp_kernels::ListDotsSmallArgs& args, hipStream_t s);
+hipError_t column_wise_update_small(const milp_kernels::ColWiseSmallArgs& args, hipStream_t s);
 // Marks the filtered rows (row_tag[r] = tag, row_pos[r] = list position).
 hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag,
                     uint32_t* row_tag, int32_t* row_pos, hipStream_t s);

@@ -80,6 +80,27 @@ __device__ __forceinline__ double quad_column_dot(const int64_t s, const int64_t
   return result;
 }
 
+// One thread per column, the four chains in registers: the same terms in the
+// same order as quad_column_dot (chain k = entries s+k, s+k+4, ...), for the
+// one-workgroup kernels of small LPs whose columns are a few entries long.
+__device__ __forceinline__ double thread_column_dot(const int64_t s, const int64_t e,
+                                                    const int32_t* __restrict__ rows,
+                                                    const double* __restrict__ vals,
+                                                    const double* __restrict__ y) {
+  const int64_t len = e - s;
+  const int64_t full = (len >= 4) ? (len / 4) * 4 : 0;
+  double r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0;
+  for (int64_t i = s; i < s + full; i += 4) {
+    r1 += vals[i] * y[rows[i]];
+    r2 += vals[i + 1] * y[rows[i + 1]];
+    r3 += vals[i + 2] * y[rows[i + 2]];
+    r4 += vals[i + 3] * y[rows[i + 3]];
+  }
+  double result = r1 + r2 + r3 + r4;
+  for (int64_t i = s + full; i < e; ++i) result += vals[i] * y[rows[i]];
+  return result;
+}
+
 // Modes of the column-dot kernel.
 enum DotMode : int {
   kUpdateRowColumnWise = 0,  // update_row.cc:282-306 over relevant columns
@@ -547,24 +568,79 @@ __global__ __launch_bounds__(kCompactThreads) void row_wise_small_kernel(RowWise
   }
 }
 
+// Small LPs: the column-wise update row (with the primal edge-norm dots when
+// w is given) and its compaction in one launch (ColWiseSmallArgs). Per column
+// the arithmetic and the write rule are column_dot_kernel's: kept columns
+// (relevant, |rho.a_j| > drop) get coefficient and w.a_j, the others keep their
+// stale coefficient. One thread per column (thread_column_dot).
+__global__ __launch_bounds__(kCompactThreads) void column_wise_small_kernel(ColWiseSmallArgs a) {
+  __shared__ double s_y[kSmallColWiseRows];
+  __shared__ double s_w[kSmallColWiseRows];
+  __shared__ uint8_t keep_flag[kSmallLdsCols];
+  __shared__ int sums[kCompactThreads];
+  const int t = threadIdx.x;
+  const int n = a.num_cols;
+  const bool with_dots = a.w != nullptr;
+  for (int i = t; i < a.m; i += kCompactThreads) {
+    s_y[i] = a.rho[i];
+    if (with_dots) s_w[i] = a.w[i];
+  }
+  __syncthreads();
+  for (int col = t; col < n; col += kCompactThreads) {
+    const bool active = bit_set(a.relevant, col);
+    const int64_t s = a.starts[col];
+    const int64_t e = active ? a.starts[col + 1] : s;
+    const double dot = thread_column_dot(s, e, a.rows, a.vals, s_y);
+    const bool keep = active && fabs(dot) > a.drop_tolerance;
+    a.flags[col] = keep ? 1 : 0;
+    keep_flag[col] = keep ? 1 : 0;
+    if (keep) {
+      a.coefficient[col] = dot;
+      if (with_dots) a.out2[col] = thread_column_dot(s, e, a.rows, a.vals, s_w);
+    }
+  }
+  __syncthreads();
+  const int per = (n + kCompactThreads - 1) / kCompactThreads;
+  const int b = min(n, t * per);
+  const int e = min(n, b + per);
+  int c = 0;
+  for (int pos = b; pos < e; ++pos) c += keep_flag[pos];
+  sums[t] = c;
+  __syncthreads();
+  for (int off = 1; off < kCompactThreads; off <<= 1) {
+    const int v = t >= off ? sums[t - off] : 0;
+    __syncthreads();
+    sums[t] += v;
+    __syncthreads();
+  }
+  int out_pos = sums[t] - c;
+  for (int pos = b; pos < e; ++pos) {
+    if (keep_flag[pos]) {
+      const double v = a.coefficient[pos];  // written above by this workgroup
+      a.list[out_pos] = pos;
+      a.vals_out[out_pos] = v;
+      a.host_list[out_pos] = pos;
+      a.host_vals[out_pos] = v;
+      if (with_dots) a.host_dots[out_pos] = a.out2[pos];
+      ++out_pos;
+    }
+  }
+  if (t == kCompactThreads - 1) {
+    *a.count = sums[t];
+    *a.host_count = sums[t];
+  }
+}
+
 // Small LPs: the primal edge-norm dots over the update-row list in one launch
-// (ListDotsSmallArgs). The loop bound is uniform, so the 4 lanes of a column
-// stay converged through quad_column_dot's shuffles.
+// (ListDotsSmallArgs), one thread per listed column.
 __global__ __launch_bounds__(kCompactThreads) void list_dots_small_kernel(ListDotsSmallArgs a) {
   __shared__ double s_y[kSmallLdsCols];
   const int t = threadIdx.x;
   for (int i = t; i < a.m; i += kCompactThreads) s_y[i] = a.y[i];
   __syncthreads();
-  const int sub = t & 3;
-  const int lane = t & 63;
-  for (int base = 0; base < a.n; base += kCompactThreads / 4) {
-    const int slot = base + (t >> 2);
-    const bool in_range = slot < a.n;
-    const int col = a.list[in_range ? slot : 0];
-    const int64_t s = a.starts[col];
-    const int64_t e = in_range ? a.starts[col + 1] : s;
-    const double dot = quad_column_dot(s, e, a.rows, a.vals, s_y, sub, lane);
-    if (sub == 0 && in_range) a.out[slot] = dot;
+  for (int slot = t; slot < a.n; slot += kCompactThreads) {
+    const int col = a.list[slot];
+    a.out[slot] = thread_column_dot(a.starts[col], a.starts[col + 1], a.rows, a.vals, s_y);
   }
 }
 
@@ -1133,6 +1209,12 @@ hipError_t row_wise_update_small(const RowWiseSmallArgs& args, hipStream_t s) {
 hipError_t list_dots_small(const ListDotsSmallArgs& args, hipStream_t s) {
   if (args.m > kSmallLdsCols || args.n < 1) return hipErrorInvalidValue;
   list_dots_small_kernel<<<1, kCompactThreads, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t column_wise_update_small(const ColWiseSmallArgs& args, hipStream_t s) {
+  if (args.m > kSmallColWiseRows || args.num_cols > kSmallLdsCols) return hipErrorInvalidValue;
+  column_wise_small_kernel<<<1, kCompactThreads, 0, s>>>(args);
   return hipGetLastError();
 }
 
