@@ -128,7 +128,7 @@ class DeviceLp {
   void NextRowTag();
   void UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
                              const std::vector<double>& rho, int algorithm, double drop,
-                             double entries);
+                             double entries, bool serial);
   void UpdateRowColumnWiseSmall(const std::vector<double>& rho, double drop,
                                 int64_t relevant_entries, const std::vector<double>* w);
   void UploadMask(Mask which);
@@ -245,6 +245,11 @@ class DeviceLp {
   // (row_wise_small_kernel) reading its inputs, including the relevant mask,
   // from mapped host memory (MILP_SMALL_FUSED=off disables).
   bool small_fused_enabled_ = true;
+  // Up to this many filtered rows (and kSmallEntries entries) the small
+  // row-wise update row applies rows in turn, above it column by column
+  // (MILP_SMALL_SERIAL_ROWS). Measured on configs 3 and 4: rows in turn win
+  // whenever they fit; the column pass reads all of A.
+  int small_serial_rows_ = 1024;
   void* h_small_in_ = nullptr;
   int32_t* h_small_rows_ = nullptr;
   double* h_small_rho_ = nullptr;

@@ -104,6 +104,7 @@ void DeviceLp::Init(int device) {
   if (const char* f = std::getenv("MILP_SMALL_FUSED")) {
     small_fused_enabled_ = std::strcmp(f, "off") != 0;
   }
+  if (const char* r = std::getenv("MILP_SMALL_SERIAL_ROWS")) small_serial_rows_ = std::atoi(r);
 }
 
 template <typename T>
@@ -261,8 +262,8 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   small_inflight_ = false;
   mask_dirty_ = false;
   if (n_total_ <= milp_kernels::kSmallLdsCols) {
-    const int cap = milp_kernels::kSmallRowsMax;
-    const size_t rho_off = size_t(cap) * sizeof(int32_t);
+    const int cap = std::max(1, m_);  // filtered rows
+    const size_t rho_off = (size_t(cap) * sizeof(int32_t) + 63) / 64 * 64;
     const size_t mask_off = rho_off + size_t(cap) * sizeof(double);
     const size_t y_off = mask_off + size_t(mask_words_) * sizeof(uint64_t);
     const size_t w_off = y_off + size_t(m_) * sizeof(double);
@@ -536,13 +537,14 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
   CallTimer timer(&stats_, algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW);
   const int k = static_cast<int>(filtered_rows.size());
   fused_ready_ = false;
-  if (small_fused_enabled_ && h_small_in_ != nullptr && k <= milp_kernels::kSmallRowsMax) {
+  if (small_fused_enabled_ && h_small_in_ != nullptr) {
     double entries = 0.0;
     for (int r : filtered_rows) entries += double(h_t_starts_[r + 1] - h_t_starts_[r]);
-    if (entries <= milp_kernels::kSmallEntries) {
-      UpdateRowRowWiseSmall(filtered_rows, rho, algorithm, drop, entries);
-      return;
-    }
+    // Few short rows: applied row by row; otherwise column by column.
+    const bool serial = k <= small_serial_rows_ && k <= milp_kernels::kSmallRowsMax &&
+                        entries <= milp_kernels::kSmallEntries;
+    UpdateRowRowWiseSmall(filtered_rows, rho, algorithm, drop, entries, serial);
+    return;
   }
   FlushRelevantMask();
   std::memcpy(h_pin_i_, filtered_rows.data(), k * sizeof(int32_t));
@@ -630,7 +632,7 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
 // mapped host memory (FetchUpdateRow's stream sync is the only round trip).
 void DeviceLp::UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
                                      const std::vector<double>& rho, int algorithm,
-                                     double drop, double entries) {
+                                     double drop, double entries, bool serial) {
   const int k = static_cast<int>(filtered_rows.size());
   // The previous launch may still be reading the inputs when no sync came
   // in between (not the case in the simplex loop, which fetches every row).
@@ -640,6 +642,38 @@ void DeviceLp::UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
     h_small_rho_[i] = rho[filtered_rows[i]];
   }
   std::memcpy(h_small_mask_, h_masks_[kRelevant].data(), mask_words_ * sizeof(uint64_t));
+  const int id = algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW;
+  if (!serial) {
+    milp_kernels::RowWiseSmallColArgs c{};
+    c.starts = d_starts_;
+    c.rows = d_rows_;
+    c.vals = d_vals_;
+    c.filtered_rows = d_small_rows_;
+    c.rho = d_small_rho_;
+    c.num_filtered = k;
+    c.m = m_;
+    c.num_cols = n_total_;
+    c.relevant = d_small_mask_;
+    c.coefficient = d_coeff_;
+    c.flags = d_flags_;
+    c.drop_tolerance = drop;
+    c.algorithm = algorithm;
+    c.list = d_list_;
+    c.list_vals = d_out_list_;
+    c.count = d_count_;
+    c.host_list = d_map_list_;
+    c.host_vals = d_map_vals_;
+    c.host_count = d_map_count_;
+    BeginKernel(id);
+    Check(milp_launch::row_wise_update_small_by_column(c, S(stream_)), "rowwise small by column");
+    // The whole CSC copy, the filtered rows and multipliers, flags/coefficients.
+    EndKernel(id, 12.0 * double(nnz_) + 8.0 * (n_total_ + 1) + 12.0 * k + 9.0 * n_total_);
+    small_inflight_ = true;
+    mapped_result_ = true;
+    list_count_ = -1;
+    ++list_epoch_;
+    return;
+  }
   milp_kernels::RowWiseSmallArgs a{};
   a.t_starts = d_t_starts_;
   a.t_cols = d_t_cols_;
@@ -659,7 +693,6 @@ void DeviceLp::UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
   a.host_list = d_map_list_;
   a.host_vals = d_map_vals_;
   a.host_count = d_map_count_;
-  const int id = algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW;
   BeginKernel(id);
   Check(milp_launch::row_wise_update_small(a, S(stream_)), "rowwise small");
   // Rows and multipliers, the CSR entries, N-sized flags/coefficients, the list.

@@ -100,6 +100,32 @@ struct ColWiseSmallArgs {
   double* host_dots;   // mapped host memory, list order (with w)
 };
 
+// The row-wise update row of a small LP with many filtered rows (or rows too
+// long for kSmallEntries), one workgroup: thread per column over the CSC copy
+// (row_wise_by_column_kernel's per-column order), row positions in LDS, then
+// the compaction. m, N <= kSmallLdsCols; filtered rows <= m.
+struct RowWiseSmallColArgs {
+  const int64_t* starts;  // CSC of [A | I]
+  const int32_t* rows;
+  const double* vals;
+  const int32_t* filtered_rows;  // mapped host memory, list order
+  const double* rho;             // mapped host memory, rho per filtered row
+  int num_filtered;
+  int m;
+  int num_cols;
+  const uint64_t* relevant;      // mapped host memory
+  double* coefficient;
+  uint8_t* flags;
+  double drop_tolerance;
+  int algorithm;
+  int32_t* list;
+  double* list_vals;
+  int* count;
+  int32_t* host_list;
+  double* host_vals;
+  int* host_count;
+};
+
 // out[k] = a_{list[k]} . y for a small LP without a dense block, one
 // workgroup: y (m <= kSmallLdsCols) staged from mapped host memory into LDS,
 // one thread per column in ColumnScalarProduct's chain order, the results
@@ -240,6 +266,8 @@ hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32
 hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s);
 hipError_t row_wise_update_small(const milp_kernels::RowWiseSmallArgs& args, hipStream_t s);
 hipError_t list_dots_small(const milp_kernels::ListDotsSmallArgs& args, hipStream_t s);
+hipError_t row_wise_update_small_by_column(const milp_kernels::RowWiseSmallColArgs& args,
+                                           hipStream_t s);
 hipError_t column_wise_update_small(const milp_kernels::ColWiseSmallArgs& args, hipStream_t s);
 // Marks the filtered rows (row_tag[r] = tag, row_pos[r] = list position).
 hipError_t tag_rows(const int32_t* filtered_rows, int num_filtered, uint32_t tag,

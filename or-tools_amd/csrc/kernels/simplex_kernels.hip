@@ -661,23 +661,27 @@ __device__ __forceinline__ double row_wise_accumulate(double acc, bool first, do
   return algorithm == 2 ? 0.0 + v : v;  // AssignToZero then +=, or first assign
 }
 
-__global__ __launch_bounds__(256) void row_wise_by_column_kernel(RowWiseColArgs a) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= a.num_cols) return;
-  const int64_t s = a.starts[col];
-  const int64_t e = a.starts[col + 1];
+// Per-column accumulation of the row-wise update row from the CSC copy:
+// k_of(r) = list position of row r, or -1 if r is not filtered. The hits are
+// ordered by k (insertion in registers, or repeated minimum selection past
+// kMaxColumnHits) and accumulated with the first-write rule of the algorithm.
+template <typename KOf>
+__device__ __forceinline__ double column_hits_accumulate(int64_t s, int64_t e,
+                                                         const int32_t* rows,
+                                                         const double* vals,
+                                                         const double* rho, KOf k_of,
+                                                         int algorithm, bool* touched) {
   int hits = 0;
-  for (int64_t i = s; i < e; ++i) hits += (a.row_tag[a.rows[i]] == a.tag) ? 1 : 0;
+  for (int64_t i = s; i < e; ++i) hits += k_of(rows[i]) >= 0 ? 1 : 0;
   double acc = 0.0;
   if (hits > 0 && hits <= kMaxColumnHits) {
     int ks[kMaxColumnHits];
     double vs[kMaxColumnHits];
     int c = 0;
     for (int64_t i = s; i < e; ++i) {
-      const int r = a.rows[i];
-      if (a.row_tag[r] != a.tag) continue;
-      const int k = a.row_pos[r];
-      const double v = a.rho[k] * a.vals[i];
+      const int k = k_of(rows[i]);
+      if (k < 0) continue;
+      const double v = rho[k] * vals[i];
       int p = c;
 #pragma unroll
       for (int q = kMaxColumnHits - 1; q > 0; --q) {
@@ -698,7 +702,7 @@ __global__ __launch_bounds__(256) void row_wise_by_column_kernel(RowWiseColArgs 
     }
 #pragma unroll
     for (int q = 0; q < kMaxColumnHits; ++q) {
-      if (q < c) acc = row_wise_accumulate(acc, q == 0, vs[q], a.algorithm);
+      if (q < c) acc = row_wise_accumulate(acc, q == 0, vs[q], algorithm);
     }
   } else if (hits > kMaxColumnHits) {
     int last = -1;
@@ -706,32 +710,110 @@ __global__ __launch_bounds__(256) void row_wise_by_column_kernel(RowWiseColArgs 
       int best_k = 0x7fffffff;
       double best_v = 0.0;
       for (int64_t i = s; i < e; ++i) {
-        const int r = a.rows[i];
-        if (a.row_tag[r] != a.tag) continue;
-        const int k = a.row_pos[r];
+        const int k = k_of(rows[i]);
         if (k > last && k < best_k) {
           best_k = k;
-          best_v = a.rho[k] * a.vals[i];
+          best_v = rho[k] * vals[i];
         }
       }
-      acc = row_wise_accumulate(acc, h == 0, best_v, a.algorithm);
+      acc = row_wise_accumulate(acc, h == 0, best_v, algorithm);
       last = best_k;
     }
   }
-  const bool touched = hits > 0;
-  const bool rel = bit_set(a.relevant, col);
+  *touched = hits > 0;
+  return acc;
+}
+
+// The update-row write rule per algorithm (update_row.cc:196-280); returns
+// whether the position is listed.
+__device__ __forceinline__ bool row_wise_store(int algorithm, bool touched, bool rel, double acc,
+                                               double drop_tolerance, double* coefficient,
+                                               int col) {
   bool listed;
-  if (a.algorithm == 0) {
-    listed = touched && rel && fabs(acc) > a.drop_tolerance;
-    if (listed) a.coefficient[col] = acc;
-  } else if (a.algorithm == 1) {
-    listed = touched && rel && fabs(acc) > a.drop_tolerance;
-    if (touched) a.coefficient[col] = acc;
+  if (algorithm == 0) {
+    listed = touched && rel && fabs(acc) > drop_tolerance;
+    if (listed) coefficient[col] = acc;
+  } else if (algorithm == 1) {
+    listed = touched && rel && fabs(acc) > drop_tolerance;
+    if (touched) coefficient[col] = acc;
   } else {
-    listed = rel && fabs(acc) > a.drop_tolerance;
-    a.coefficient[col] = touched ? acc : 0.0;
+    listed = rel && fabs(acc) > drop_tolerance;
+    coefficient[col] = touched ? acc : 0.0;
   }
+  return listed;
+}
+
+__global__ __launch_bounds__(256) void row_wise_by_column_kernel(RowWiseColArgs a) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= a.num_cols) return;
+  auto k_of = [&](int r) { return a.row_tag[r] == a.tag ? a.row_pos[r] : -1; };
+  bool touched = false;
+  const double acc = column_hits_accumulate(a.starts[col], a.starts[col + 1], a.rows, a.vals,
+                                            a.rho, k_of, a.algorithm, &touched);
+  const bool listed = row_wise_store(a.algorithm, touched, bit_set(a.relevant, col), acc,
+                                     a.drop_tolerance, a.coefficient, col);
   a.flags[col] = listed ? 1 : 0;
+}
+
+// Small LPs with many filtered rows: the same per-column accumulation in one
+// workgroup (row positions in LDS instead of the tag pass), then the
+// compaction into mapped host memory, as row_wise_small_kernel.
+__global__ __launch_bounds__(kCompactThreads) void row_wise_small_by_column_kernel(
+    RowWiseSmallColArgs a) {
+  __shared__ int32_t s_pos[kSmallLdsCols];
+  __shared__ double s_rho[kSmallLdsCols];
+  __shared__ uint64_t rel[kSmallLdsCols / 64];
+  __shared__ int sums[kCompactThreads];
+  const int t = threadIdx.x;
+  const int n = a.num_cols;
+  for (int r = t; r < a.m; r += kCompactThreads) s_pos[r] = -1;
+  for (int w = t; w < (n + 63) / 64; w += kCompactThreads) rel[w] = a.relevant[w];
+  __syncthreads();
+  for (int k = t; k < a.num_filtered; k += kCompactThreads) {
+    s_pos[a.filtered_rows[k]] = k;
+    s_rho[k] = a.rho[k];
+  }
+  __syncthreads();
+  auto k_of = [&](int r) { return s_pos[r]; };
+  const int per = (n + kCompactThreads - 1) / kCompactThreads;
+  const int b = min(n, t * per);
+  const int e = min(n, b + per);
+  uint32_t listed_bits = 0;
+  int c = 0;
+  for (int col = b; col < e; ++col) {
+    bool touched = false;
+    const double acc = column_hits_accumulate(a.starts[col], a.starts[col + 1], a.rows, a.vals,
+                                              s_rho, k_of, a.algorithm, &touched);
+    const bool is_rel = (rel[col >> 6] >> (col & 63)) & 1ull;
+    const bool listed = row_wise_store(a.algorithm, touched, is_rel, acc, a.drop_tolerance,
+                                       a.coefficient, col);
+    a.flags[col] = listed ? 1 : 0;
+    listed_bits |= uint32_t(listed) << (col - b);
+    c += listed;
+  }
+  sums[t] = c;
+  __syncthreads();
+  for (int off = 1; off < kCompactThreads; off <<= 1) {
+    const int v = t >= off ? sums[t - off] : 0;
+    __syncthreads();
+    sums[t] += v;
+    __syncthreads();
+  }
+  int out_pos = sums[t] - c;
+  for (int col = b; col < e; ++col) {
+    if ((listed_bits >> (col - b)) & 1u) {
+      const double v = a.coefficient[col];  // this thread's own store above
+      a.list[out_pos] = col;
+      a.list_vals[out_pos] = v;
+      a.host_list[out_pos] = col;
+      a.host_vals[out_pos] = v;
+      ++out_pos;
+    }
+  }
+  if (t == kCompactThreads - 1) {
+    *a.count = sums[t];
+    *a.host_count = sums[t];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1215,6 +1297,15 @@ hipError_t list_dots_small(const ListDotsSmallArgs& args, hipStream_t s) {
 hipError_t column_wise_update_small(const ColWiseSmallArgs& args, hipStream_t s) {
   if (args.m > kSmallColWiseRows || args.num_cols > kSmallLdsCols) return hipErrorInvalidValue;
   column_wise_small_kernel<<<1, kCompactThreads, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t row_wise_update_small_by_column(const RowWiseSmallColArgs& args, hipStream_t s) {
+  if (args.num_cols > kSmallLdsCols || args.m > kSmallLdsCols || args.num_filtered < 0 ||
+      args.num_filtered > args.m) {
+    return hipErrorInvalidValue;
+  }
+  row_wise_small_by_column_kernel<<<1, kCompactThreads, 0, s>>>(args);
   return hipGetLastError();
 }
 

@@ -225,19 +225,22 @@ def test_invalid_problem_status():
     parity_util.compare(o, ro, g, rg, lp)
 
 
-@pytest.mark.parametrize("fused", ["on", "off"])
+@pytest.mark.parametrize("fused", ["auto", "serial", "by_column", "off"])
 @pytest.mark.parametrize("dual", [0, 1])
 @pytest.mark.parametrize("case", ["sparse", "c5", "dense", "jobshop"])
 def test_small_lp_one_launch_update_row_parity(case, dual, fused, monkeypatch):
-    """Small LPs (N <= 8192): the row-wise update row runs as one launch
-    (row_wise_small_kernel: inputs and the relevant mask from mapped host
-    memory, LDS accumulation in list order, compaction into mapped host
-    memory). Dense rows overflow its entry budget, so the dense case mixes it
-    with the generic kernels within one solve (deferred mask uploads). The
+    """Small LPs (N <= 8192): every update row is one launch with its inputs,
+    the relevant mask and the list in mapped host memory: row-wise rows
+    applied in turn out of LDS (few rows) or column by column (many rows),
+    and the column-wise row with the edge-norm dots. The dense case (a dense
+    block) mixes them with the generic kernels within one solve (deferred
+    mask uploads). The
     dual simplex computes tau while that launch runs (MILP_INLINE_TAU). Bit
     for bit equal to the oracle (deterministic time included), either way."""
-    monkeypatch.setenv("MILP_SMALL_FUSED", fused)
-    monkeypatch.setenv("MILP_INLINE_TAU", fused)  # tau overlapped with the launch
+    monkeypatch.setenv("MILP_SMALL_FUSED", "off" if fused == "off" else "on")
+    monkeypatch.setenv("MILP_INLINE_TAU", "off" if fused == "off" else "on")
+    if fused != "auto":  # row-wise rows applied in turn, or column by column
+        monkeypatch.setenv("MILP_SMALL_SERIAL_ROWS", "1000000" if fused == "serial" else "0")
     if case == "sparse":
         lp = lp_gen.random_sparse_lp(200, 900, 0.04, 7, maximize=True)
     elif case == "c5":
