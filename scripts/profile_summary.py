@@ -7,7 +7,7 @@ WRITE_SIZE passes, each its own run) into profiles/<tag>/:
 
 FETCH_SIZE / WRITE_SIZE are in KiB. On gfx950 FETCH_SIZE reports half of
 the bytes of a streaming read (MI355X_MICROARCH.md, HBM section); it is
-doubled here. Usage: python scripts/profile_summary.py gpurun_out/prof <tag> [c2|c5]
+doubled here. Usage: python scripts/profile_summary.py gpurun_out/prof <tag> [c2|c4|c5]
 (writes profiles/<tag>/ and profiles/traffic_<c2|c5>.json for bench.py)
 """
 import collections
@@ -30,6 +30,9 @@ GROUPS = {  # HIP kernel name fragment -> engine kernel id (bench.py names)
     "update_reduced_costs_kernel": "rc_update",
     "dense_dot_kernel<2,": "primal_norms", "column_dot_kernel<2,": "primal_norms",
     "row_sum_kernel": "spmv_rows", "column_squared_norm_kernel": "col_norms",
+    # one-launch kernels of small LPs (N <= 8192)
+    "row_wise_small_kernel": "update_row", "row_wise_small_by_column_kernel": "update_row",
+    "column_wise_small_kernel": "update_row", "list_dots_small_kernel": "primal_norms",
 }
 
 
@@ -43,9 +46,12 @@ PRIMARY = {
     "rc_update": [["update_reduced_costs_kernel"]],
     "update_row": [["row_wise_update_kernel", "row_wise_by_column_kernel",
                     "row_wise_full_rows_kernel",
-                    "dense_dot_kernel<0,", "dense_dot_kernel<4,"],
+                    "dense_dot_kernel<0,", "dense_dot_kernel<4,",
+                    "row_wise_small_kernel", "row_wise_small_by_column_kernel",
+                    "column_wise_small_kernel"],
                    ["column_dot_kernel<0,", "column_dot_kernel<4,"]],
-    "primal_norms": [["dense_dot_kernel<2,"], ["column_dot_kernel<2,"]],
+    "primal_norms": [["dense_dot_kernel<2,", "list_dots_small_kernel"],
+                     ["column_dot_kernel<2,"]],
     "spmv_rows": [["row_sum_kernel"]],
     "col_norms": [["column_squared_norm_kernel"]],
 }
