@@ -250,6 +250,9 @@ class DeviceLp {
   // (MILP_SMALL_SERIAL_ROWS). Measured on configs 3 and 4: rows in turn win
   // whenever they fit; the column pass reads all of A.
   int small_serial_rows_ = 1024;
+  // Workgroup size of row_wise_small_kernel (MILP_SMALL_THREADS: 1024 or 256;
+  // 256 measured 4-5 % slower on the config-4 probe).
+  int small_threads_ = 1024;
   void* h_small_in_ = nullptr;
   int32_t* h_small_rows_ = nullptr;
   double* h_small_rho_ = nullptr;

@@ -105,6 +105,7 @@ void DeviceLp::Init(int device) {
     small_fused_enabled_ = std::strcmp(f, "off") != 0;
   }
   if (const char* r = std::getenv("MILP_SMALL_SERIAL_ROWS")) small_serial_rows_ = std::atoi(r);
+  if (const char* r = std::getenv("MILP_SMALL_THREADS")) small_threads_ = std::atoi(r);
 }
 
 template <typename T>
@@ -694,7 +695,7 @@ void DeviceLp::UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
   a.host_vals = d_map_vals_;
   a.host_count = d_map_count_;
   BeginKernel(id);
-  Check(milp_launch::row_wise_update_small(a, S(stream_)), "rowwise small");
+  Check(milp_launch::row_wise_update_small(a, small_threads_, S(stream_)), "rowwise small");
   // Rows and multipliers, the CSR entries, N-sized flags/coefficients, the list.
   EndKernel(id, 12.0 * entries + 12.0 * k + 9.0 * n_total_);
   small_inflight_ = true;

@@ -264,7 +264,9 @@ hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32
                          double* vals, int* count, int32_t* host_list, double* host_vals,
                          int* host_count, hipStream_t s);
 hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s);
-hipError_t row_wise_update_small(const milp_kernels::RowWiseSmallArgs& args, hipStream_t s);
+// threads: 1024, or 256 (used when the filtered rows fit one per thread).
+hipError_t row_wise_update_small(const milp_kernels::RowWiseSmallArgs& args, int threads,
+                                 hipStream_t s);
 hipError_t list_dots_small(const milp_kernels::ListDotsSmallArgs& args, hipStream_t s);
 hipError_t row_wise_update_small_by_column(const milp_kernels::RowWiseSmallColArgs& args,
                                            hipStream_t s);

@@ -451,7 +451,8 @@ __global__ __launch_bounds__(256) void row_wise_update_kernel(RowWiseArgs a) {
 // memory. Arithmetic as row_wise_update_kernel: the rows are applied in list
 // order with a barrier between rows (a position appears once per row, so one
 // thread owns it within a row), with the same first-write rule per algorithm.
-__global__ __launch_bounds__(kCompactThreads) void row_wise_small_kernel(RowWiseSmallArgs a) {
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void row_wise_small_kernel(RowWiseSmallArgs a) {
   __shared__ double acc[kSmallLdsCols];
   __shared__ uint8_t touched[kSmallLdsCols];
   __shared__ uint64_t rel[kSmallLdsCols / 64];
@@ -460,13 +461,13 @@ __global__ __launch_bounds__(kCompactThreads) void row_wise_small_kernel(RowWise
   __shared__ double s_rho[kSmallRowsMax];
   __shared__ int64_t s_off[kSmallRowsMax];
   __shared__ int s_beg[kSmallRowsMax + 1];
-  __shared__ int sums[kCompactThreads];
+  __shared__ int sums[THREADS];
   const int t = threadIdx.x;
   const int n = a.num_cols;
   const int k_rows = a.num_filtered;
-  for (int i = t; i < n; i += kCompactThreads) touched[i] = 0;
-  for (int w = t; w < (n + 63) / 64; w += kCompactThreads) rel[w] = a.relevant[w];
-  // Wave 1: row extents (one row per thread; k_rows <= kCompactThreads).
+  for (int i = t; i < n; i += THREADS) touched[i] = 0;
+  for (int w = t; w < (n + 63) / 64; w += THREADS) rel[w] = a.relevant[w];
+  // Wave 1: row extents (one row per thread; k_rows <= THREADS).
   int len = 0;
   if (t < k_rows) {
     const int r = a.filtered_rows[t];
@@ -477,18 +478,18 @@ __global__ __launch_bounds__(kCompactThreads) void row_wise_small_kernel(RowWise
   }
   sums[t] = len;
   __syncthreads();
-  for (int off = 1; off < kCompactThreads; off <<= 1) {
+  for (int off = 1; off < THREADS; off <<= 1) {
     const int v = t >= off ? sums[t - off] : 0;
     __syncthreads();
     sums[t] += v;
     __syncthreads();
   }
   if (t < k_rows) s_beg[t] = sums[t] - len;
-  if (t == 0) s_beg[k_rows] = sums[kCompactThreads - 1];
+  if (t == 0) s_beg[k_rows] = sums[THREADS - 1];
   __syncthreads();
   // Wave 2: every entry of every filtered row, product rho_k * A[r_k, pos].
   const int num_entries = s_beg[k_rows];  // <= kSmallEntries (host-checked)
-  for (int e = t; e < num_entries; e += kCompactThreads) {
+  for (int e = t; e < num_entries; e += THREADS) {
     int lo = 0;
     int hi = k_rows - 1;
     while (lo < hi) {  // last row k with s_beg[k] <= e
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(kCompactThreads) void row_wise_small_kernel(RowWise
   }
   __syncthreads();
   for (int k = 0; k < k_rows; ++k) {
-    for (int e = s_beg[k] + t; e < s_beg[k + 1]; e += kCompactThreads) {
+    for (int e = s_beg[k] + t; e < s_beg[k + 1]; e += THREADS) {
       const int pos = ent_pos[e];
       const double v = ent_val[e];
       double out;
@@ -517,8 +518,8 @@ __global__ __launch_bounds__(kCompactThreads) void row_wise_small_kernel(RowWise
     }
     __syncthreads();  // rows are applied in order
   }
-  // Epilogue over this thread's slice of positions (<= 8 with N <= 8192).
-  const int per = (n + kCompactThreads - 1) / kCompactThreads;
+  // Epilogue over this thread's slice of positions (<= 32 with N <= 8192).
+  const int per = (n + THREADS - 1) / THREADS;
   const int b = min(n, t * per);
   const int e = min(n, b + per);
   uint32_t listed_bits = 0;
@@ -545,7 +546,7 @@ __global__ __launch_bounds__(kCompactThreads) void row_wise_small_kernel(RowWise
   __syncthreads();
   sums[t] = c;
   __syncthreads();
-  for (int off = 1; off < kCompactThreads; off <<= 1) {
+  for (int off = 1; off < THREADS; off <<= 1) {
     const int v = t >= off ? sums[t - off] : 0;
     __syncthreads();
     sums[t] += v;
@@ -562,7 +563,7 @@ __global__ __launch_bounds__(kCompactThreads) void row_wise_small_kernel(RowWise
       ++out_pos;
     }
   }
-  if (t == kCompactThreads - 1) {
+  if (t == THREADS - 1) {
     *a.count = sums[t];
     *a.host_count = sums[t];
   }
@@ -1279,12 +1280,17 @@ hipError_t row_wise_update(const RowWiseArgs& args, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t row_wise_update_small(const RowWiseSmallArgs& args, hipStream_t s) {
+hipError_t row_wise_update_small(const RowWiseSmallArgs& args, int threads, hipStream_t s) {
   if (args.num_cols > kSmallLdsCols || args.num_filtered > kSmallRowsMax ||
       args.num_filtered < 0) {
     return hipErrorInvalidValue;
   }
-  row_wise_small_kernel<<<1, kCompactThreads, 0, s>>>(args);
+  // 256 threads (4 waves: cheaper barriers between rows) when the rows fit.
+  if (threads == 256 && args.num_filtered <= 256) {
+    row_wise_small_kernel<256><<<1, 256, 0, s>>>(args);
+  } else {
+    row_wise_small_kernel<kCompactThreads><<<1, kCompactThreads, 0, s>>>(args);
+  }
   return hipGetLastError();
 }
 

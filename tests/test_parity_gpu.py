@@ -225,7 +225,7 @@ def test_invalid_problem_status():
     parity_util.compare(o, ro, g, rg, lp)
 
 
-@pytest.mark.parametrize("fused", ["auto", "serial", "by_column", "off"])
+@pytest.mark.parametrize("fused", ["auto", "serial", "serial256", "by_column", "off"])
 @pytest.mark.parametrize("dual", [0, 1])
 @pytest.mark.parametrize("case", ["sparse", "c5", "dense", "jobshop"])
 def test_small_lp_one_launch_update_row_parity(case, dual, fused, monkeypatch):
@@ -240,7 +240,10 @@ def test_small_lp_one_launch_update_row_parity(case, dual, fused, monkeypatch):
     monkeypatch.setenv("MILP_SMALL_FUSED", "off" if fused == "off" else "on")
     monkeypatch.setenv("MILP_INLINE_TAU", "off" if fused == "off" else "on")
     if fused != "auto":  # row-wise rows applied in turn, or column by column
-        monkeypatch.setenv("MILP_SMALL_SERIAL_ROWS", "1000000" if fused == "serial" else "0")
+        serial = fused.startswith("serial")
+        monkeypatch.setenv("MILP_SMALL_SERIAL_ROWS", "1000000" if serial else "0")
+    if fused == "serial256":  # the 4-wave workgroup variant
+        monkeypatch.setenv("MILP_SMALL_THREADS", "256")
     if case == "sparse":
         lp = lp_gen.random_sparse_lp(200, 900, 0.04, 7, maximize=True)
     elif case == "c5":
