@@ -293,15 +293,15 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--batch-lps", type=int, default=512,
                     help="config-4 children per GPU (0 disables the batched section)")
-    ap.add_argument("--batch-workers", type=int, default=8)
+    ap.add_argument("--batch-workers", type=int, default=16)
     ap.add_argument("--batch-jobs", type=int, default=15)
     ap.add_argument("--batch-machines", type=int, default=10)
     ap.add_argument("--batch-cpu-lps", type=int, default=512)
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 section")
     ap.add_argument("--no-c3", action="store_true", help="skip the config-3 section")
     ap.add_argument("--c3-max-rows", type=int, default=1000)
-    ap.add_argument("--c3-workers", type=int, default=8)
-    ap.add_argument("--c3-cpu-threads", type=int, default=8)
+    ap.add_argument("--c3-workers", type=int, default=16)
+    ap.add_argument("--c3-cpu-threads", type=int, default=16)
     ap.add_argument("--c5-m", type=int, default=100000)
     ap.add_argument("--c5-n", type=int, default=1000000)
     ap.add_argument("--c5-warmup", type=int, default=20000)
