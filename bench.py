@@ -1,18 +1,22 @@
 #!/usr/bin/env python3
-"""Benchmark: simplex iterations/sec of the MI355X engine on BASELINE.json
-config 2 (dense random LP 10k x 50k, primal simplex, 1 MI355X), with the
-dominant kernel's roofline and the CPU oracle (Glop restatement) timed on the
-host in the same run.
+"""Benchmark: simplex iterations/sec of the MI355X engine on BASELINE.json's
+north-star workload, config 5 (synthetic sparse LP 100k x 1M, 0.01% dense,
+dual simplex with dual steepest edge, 1 MI355X), with the dominant kernel's
+roofline and the CPU oracle (Glop restatement) timed on the host in the same
+run. Config 2 (dense 10k x 50k, primal), config 3 (Netlib-shaped suite) and
+config 4 (CP-SAT-style children) follow as extra sections of the same line.
 
-A "step" is one simplex iteration (RevisedSimplex::PrimalMinimize loop body,
-revised_simplex.cc:2772-3039). W warm-up iterations run untimed (they include
-loading, the initial factorization and the first edge norms); then exactly K
-iterations are timed, bracketed by barrier + device synchronize.
+A "step" is one simplex iteration (RevisedSimplex::DualMinimize loop body,
+revised_simplex.cc:3058-3367) at iteration 20 000 of the solve (--c5-window):
+the solve runs untimed up to there (loading, factorizations, the hypersparse
+early phase), then W more warm-up iterations, then exactly K iterations are
+timed, bracketed by barrier + device synchronize, with HIP-event kernel
+timing on (events are collected after the window, no per-kernel sync).
 
-Multi-GPU: one process per GPU (torchrun). A single LP does not shard in this
-round, so each rank solves its own replica LP (seed + rank): "replicas only",
-weak scaling, no collective in the data path; value = sum of iterations over
-ranks / max wall time over ranks.
+Multi-GPU: one process per GPU (torchrun). A single LP does not shard yet
+(DESIGN.md 8), so each rank solves its own replica LP (seed + rank):
+"replicas only", no collective in the data path; value = sum of iterations
+over ranks / max wall time over ranks.
 """
 import argparse
 import json
@@ -97,54 +101,52 @@ def kernel_table(stats):
 def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     """Config 5: synthetic sparse LP 100k x 1M, 0.01% nnz,
     dual simplex with dual steepest edge. One LP per rank (replicas, seed +
-    rank). The window [c5_warmup, c5_warmup + c5_steps) is timed: early
-    iterations are hypersparse, and the window sits where the update row
-    has become the dominant pass. The rate is measured with kernel timing
-    off; a second window of the same length, with HIP-event timing on,
-    gives the kernel split and the roofline."""
+    rank). The solve runs untimed to iteration c5_window + warmup; then
+    exactly `steps` iterations are timed with the kernel timing on."""
     import lp_gen
     lp = lp_gen.sparse_c5_lp(args.c5_m, args.c5_n, 10, args.seed + rank)
     p = abi.default_params(use_dual_simplex=1)
     h = engine.LpHandle(p, device=local_rank)
     h.load(lp)
     t = time.perf_counter()
-    h.begin(args.c5_warmup)
+    start = args.c5_window + args.warmup
+    h.begin(start)
     setup = time.perf_counter() - t
-    log(f"c5: warm-up to iteration {args.c5_warmup} in {setup:.1f}s")
+    log(f"c5: solve ran to iteration {start} in {setup:.1f}s (untimed)")
     h.reset_kernel_stats()
+    h.set_kernel_timing(True)
     barrier()
     sync()
     t0 = time.perf_counter()
-    fin, it = h.run_until(args.c5_warmup + args.c5_steps)
+    fin, it = h.run_until(start + args.steps)
     sync()
     barrier()
     elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
-    done = it - args.c5_warmup
-    total_done = done * world  # replicas: every rank runs the same window length
-    h.reset_kernel_stats()
-    h.set_kernel_timing(True)
-    h.run_until(it + args.c5_steps)
     stats = h.kernel_stats()
+    done = it - start
+    total_done = distributed.sum_over_ranks(done, dist, "cuda")
     h.stop()
     h.finish()
     del h
+    log(f"c5: timed {done} iterations in {elapsed:.3f}s")
     out = {
-        "metric": "simplex iterations/sec", "unit": "iterations/s",
         "value": total_done / elapsed if elapsed > 0 else 0.0,
-        "ms_per_iteration": 1000.0 * elapsed / max(1, done),
-        "timed_iterations": [args.c5_warmup, args.c5_warmup + done],
+        "ms_per_step": 1000.0 * elapsed / max(1, done),
+        "timed_iterations": [start, start + done],
         "finished_early": bool(fin), "setup_and_warmup_s": round(setup, 2),
-        "workload": (f"config 5: sparse {args.c5_m}x{args.c5_n}, 10 nnz/column "
-                     f"(nnz={int(lp.nnz)}), dual simplex, dual steepest edge, Glop defaults"),
+        "nnz": int(lp.nnz),
         "roofline": kernel_roofline(stats, args.c5_traffic_json),
         "kernels": kernel_table(stats),
-        "kernel_window": [args.c5_warmup + done, args.c5_warmup + 2 * done],
+        "host_ms_per_step": round((1000.0 * elapsed - sum(v["call_ms"] for v in stats.values()))
+                                  / max(1, done), 3),
+        "device_call_ms_per_step": round(sum(v["call_ms"] for v in stats.values())
+                                         / max(1, done), 3),
     }
     if rank == 0 and world == 1 and not args.no_cpu and args.c5_cpu_steps > 0:
         import oracle_lib
         log("c5: cpu baseline (oracle)")
         po = abi.default_params(use_dual_simplex=1,
-                                max_number_of_iterations=args.c5_warmup + args.c5_cpu_steps)
+                                max_number_of_iterations=start + args.c5_cpu_steps)
         o = oracle_lib.OracleLp(po)
         o.record_iteration_times(True)
         o.load(lp)
@@ -153,13 +155,64 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
         wall = time.perf_counter() - t
         ts = o.iteration_times()
         k = args.c5_cpu_steps
-        if len(ts) >= args.c5_warmup + k:
-            dt = ts[args.c5_warmup + k - 1] - ts[args.c5_warmup - 1]
+        if len(ts) >= start + k:
+            dt = ts[start + k - 1] - ts[start - 1]
             out["cpu_baseline"] = {
                 "value": k / dt, "unit": "iterations/s", "cores": 1, "kind": "port",
                 "sample": (f"oracle (C++ restatement of Glop, -O3, 1 thread) on the same LP: "
-                           f"iterations {args.c5_warmup}..{args.c5_warmup + k} "
-                           f"({wall:.1f}s wall incl. the warm-up)")}
+                           f"iterations {start}..{start + k} of the same solve "
+                           f"({wall:.1f}s wall incl. the untimed part)")}
+    return out
+
+
+def run_c2(args, rank, world, local_rank, dist, barrier, sync):
+    """Config 2: dense random LP 10k x 50k, primal simplex, Glop defaults.
+    Iterations c2_warmup..c2_warmup + c2_steps are timed (replicas per rank)."""
+    lp = dense_box_lp(args.m, args.n, args.seed + rank)
+    params = abi.default_params()  # Glop defaults: primal simplex, steepest edge
+    h = engine.LpHandle(params, device=local_rank)
+    h.load(lp)
+    t_setup = time.perf_counter()
+    h.begin(args.c2_warmup)  # load to HBM, factorize, first norms, warm-up iterations
+    t_setup = time.perf_counter() - t_setup
+    log(f"c2: warm-up done in {t_setup:.1f}s; timing {args.c2_steps} iterations")
+    h.reset_kernel_stats()
+    h.set_kernel_timing(True)
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    finished, it = h.run_until(args.c2_warmup + args.c2_steps)
+    sync()
+    barrier()
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+    stats = h.kernel_stats()
+    done = it - args.c2_warmup
+    total_done = distributed.sum_over_ranks(done, dist, "cuda")
+    h.stop()
+    h.finish()
+    del h
+    out = {
+        "metric": "simplex iterations/sec", "unit": "iterations/s",
+        "value": total_done / elapsed if elapsed > 0 else 0.0,
+        "ms_per_step": 1000.0 * elapsed / max(1, done),
+        "timed_iterations": [args.c2_warmup, args.c2_warmup + done],
+        "finished_early": bool(finished), "setup_and_warmup_s": round(t_setup, 3),
+        "workload": (f"config 2: dense random LP {args.m}x{args.n} (nnz={int(lp.nnz)}), "
+                     f"primal simplex, Glop defaults"),
+        "roofline": kernel_roofline(stats, args.traffic_json),
+        "kernels": kernel_table(stats),
+        "host_ms_per_step": round((1000.0 * elapsed - sum(v["call_ms"] for v in stats.values()))
+                                  / max(1, done), 3),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        log("c2: cpu baseline (oracle)")
+        rate, info = cpu_baseline(lp, args.cpu_warmup, args.cpu_iters)
+        out["cpu_baseline"] = {
+            "value": rate, "unit": "iterations/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle (C++ restatement of Glop, -O3, 1 thread) on the same "
+                       f"{args.m}x{args.n} LP: iterations {args.cpu_warmup}.."
+                       f"{args.cpu_warmup + args.cpu_iters} timed "
+                       f"({info['wall_s']:.1f}s wall incl. setup)")}
     return out
 
 
@@ -283,37 +336,41 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--m", type=int, default=10000)
-    ap.add_argument("--n", type=int, default=50000)
+    ap.add_argument("--steps", type=int, default=1000,
+                    help="timed config-5 iterations (the headline)")
+    ap.add_argument("--warmup", type=int, default=20,
+                    help="untimed config-5 iterations after --c5-window")
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--c5-m", type=int, default=100000)
+    ap.add_argument("--c5-n", type=int, default=1000000)
+    ap.add_argument("--c5-window", type=int, default=20000,
+                    help="config-5 iteration where the timed window starts")
+    ap.add_argument("--c5-cpu-steps", type=int, default=300)
+    ap.add_argument("--c5-traffic-json",
+                    default=os.path.join(REPO, "profiles", "traffic_c5.json"),
+                    help="per-launch HBM bytes of the config-5 kernels (profiles/)")
+    ap.add_argument("--no-c2", action="store_true", help="skip the config-2 section")
+    ap.add_argument("--m", type=int, default=10000, help="config-2 rows")
+    ap.add_argument("--n", type=int, default=50000, help="config-2 columns")
+    ap.add_argument("--c2-steps", type=int, default=64)
+    ap.add_argument("--c2-warmup", type=int, default=3)
     ap.add_argument("--cpu-iters", type=int, default=6)
     ap.add_argument("--cpu-warmup", type=int, default=2)
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json",
+                    default=os.path.join(REPO, "profiles", "traffic_c2.json"),
+                    help="per-launch HBM bytes of the config-2 dominant kernel from a "
+                         "separate rocprofv3 --pmc pass (profiles/)")
     ap.add_argument("--batch-lps", type=int, default=512,
                     help="config-4 children per GPU (0 disables the batched section)")
     ap.add_argument("--batch-workers", type=int, default=16)
     ap.add_argument("--batch-jobs", type=int, default=15)
     ap.add_argument("--batch-machines", type=int, default=10)
     ap.add_argument("--batch-cpu-lps", type=int, default=512)
-    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 section")
     ap.add_argument("--no-c3", action="store_true", help="skip the config-3 section")
     ap.add_argument("--c3-max-rows", type=int, default=1000)
     ap.add_argument("--c3-workers", type=int, default=16)
     ap.add_argument("--c3-cpu-threads", type=int, default=16)
-    ap.add_argument("--c5-m", type=int, default=100000)
-    ap.add_argument("--c5-n", type=int, default=1000000)
-    ap.add_argument("--c5-warmup", type=int, default=20000)
-    ap.add_argument("--c5-steps", type=int, default=1000)
-    ap.add_argument("--c5-cpu-steps", type=int, default=300)
-    ap.add_argument("--c5-traffic-json",
-                    default=os.path.join(REPO, "profiles", "traffic_c5.json"),
-                    help="per-launch HBM bytes of the config-5 kernels (profiles/)")
-    ap.add_argument("--traffic-json",
-                    default=os.path.join(REPO, "profiles", "traffic_c2.json"),
-                    help="per-launch HBM bytes of the dominant kernel from a "
-                         "separate rocprofv3 --pmc pass (profiles/)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -336,55 +393,14 @@ def main():
             import torch
             torch.cuda.synchronize()
 
-    log(f"generating {args.m}x{args.n} dense LP")
-    lp = dense_box_lp(args.m, args.n, args.seed + rank)
-    params = abi.default_params()  # Glop defaults: primal simplex, steepest edge
-    h = engine.LpHandle(params, device=local_rank)
-    log("loading")
-    h.load(lp)
-    log("begin (upload, initial basis, norms, warm-up iterations)")
-    t_setup = time.perf_counter()
-    h.begin(args.warmup)  # load to HBM, factorize, first norms, W iterations
-    t_setup = time.perf_counter() - t_setup
-    log(f"warm-up done in {t_setup:.1f}s; timing {args.steps} iterations")
-    h.reset_kernel_stats()
-    h.set_kernel_timing(True)
-
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    finished, it = h.run_until(args.warmup + args.steps)
-    sync()
-    barrier()
-    t1 = time.perf_counter()
-    stats = h.kernel_stats()
-    h.set_kernel_timing(False)
-    done = it - args.warmup
-    elapsed = t1 - t0
-
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([float(done)], dtype=torch.float64, device="cuda")
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        total_done = float(c.item())
-    else:
-        total_done = float(done)
-    log(f"timed window: {done} iterations in {elapsed:.3f}s")
-    h.stop()  # the bench times a window, not the whole solve
-    h.finish()
-    del h  # release the C2 matrix copies before the batched section
-
-    # Dominant kernel in the timed region: roofline vs HBM peak.
-    roofline = kernel_roofline(stats, args.traffic_json)
-
-    c5 = None
-    if not args.no_c5:
-        log(f"config-5 section: {args.c5_m}x{args.c5_n}")
-        c5 = run_c5(args, rank, world, local_rank, dist, barrier, sync)
-        log(f"c5: {c5['value']:.1f} iterations/s")
+    log(f"config-5 headline: {args.c5_m}x{args.c5_n}")
+    c5 = run_c5(args, rank, world, local_rank, dist, barrier, sync)
+    log(f"c5: {c5['value']:.1f} iterations/s")
+    c2 = None
+    if not args.no_c2:
+        log(f"config-2 section: {args.m}x{args.n} dense")
+        c2 = run_c2(args, rank, world, local_rank, dist, barrier, sync)
+        log(f"c2: {c2['value']:.1f} iterations/s")
     c3 = None
     if not args.no_c3:
         log("config-3 section: Netlib-shaped suite")
@@ -397,43 +413,35 @@ def main():
         log(f"batched: {batched['value']:.1f} LPs/s")
     if rank != 0:
         return
-    cpu = None
-    if not args.no_cpu and world == 1:
-        log("cpu baseline (oracle)")
-        rate, info = cpu_baseline(lp, args.cpu_warmup, args.cpu_iters)
-        cpu = {"value": rate, "unit": "iterations/s", "cores": 1, "kind": "port",
-               "sample": (f"oracle (C++ restatement of Glop, -O3, 1 thread) on the same "
-                          f"{args.m}x{args.n} LP: iterations {args.cpu_warmup}.."
-                          f"{args.cpu_warmup + args.cpu_iters} timed "
-                          f"({info['wall_s']:.1f}s wall incl. setup)")}
-    value = total_done / elapsed if elapsed > 0 else 0.0
     line = {
         "metric": METRIC,
-        "value": value,
+        "value": c5["value"],
         "unit": "iterations/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": 1000.0 * elapsed / max(1, done),
+        "ms_per_step": c5["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (seeded dense random LP, BASELINE.json config 2 generator)",
+        "data": "synthetic (seeded sparse LP, BASELINE.json config 5 generator, tests/lp_gen.py)",
         "config": {
-            "workload": "config 2: dense random LP, primal simplex, Glop defaults",
-            "m": args.m, "n": args.n, "nnz": int(lp.nnz), "seed": args.seed,
-            "timed_iterations": [args.warmup, args.warmup + done],
-            "finished_early": bool(finished),
-            "setup_and_warmup_s": round(t_setup, 3),
+            "workload": (f"config 5: sparse LP {args.c5_m}x{args.c5_n}, 10 nnz/column "
+                         f"(nnz={c5['nnz']}), dual simplex, dual steepest edge, Glop defaults; "
+                         f"iterations {c5['timed_iterations'][0]}..{c5['timed_iterations'][1]}"),
+            "m": args.c5_m, "n": args.c5_n, "seed": args.seed,
+            "timed_iterations": c5["timed_iterations"],
+            "finished_early": c5["finished_early"],
+            "setup_and_warmup_s": c5["setup_and_warmup_s"],
             "parallelism": f"replicas{world}",
         },
-        "roofline": roofline,
-        "kernels": kernel_table(stats),
-        "host_ms_per_step": round((1000.0 * elapsed - sum(v["call_ms"] for v in stats.values()))
-                                  / max(1, done), 3),
-        "cpu_baseline": cpu,
-        "c5": c5,
+        "roofline": c5["roofline"],
+        "kernels": c5["kernels"],
+        "host_ms_per_step": c5["host_ms_per_step"],
+        "device_call_ms_per_step": c5["device_call_ms_per_step"],
+        "cpu_baseline": c5.get("cpu_baseline"),
+        "c2": c2,
         "c3": c3,
         "batched": batched,
     }

@@ -59,7 +59,9 @@ enum {
   MI_LP_ERROR_NULL = 3,
   MI_LP_ERROR_INVALID_PROBLEM = 4,
   MI_LP_ERROR_DEVICE = 100, /* HIP runtime failure or missing GPU */
-  MI_LP_ERROR_STATE = 101   /* call out of order (e.g. getter before solve) */
+  MI_LP_ERROR_STATE = 101,  /* call out of order (e.g. getter before solve) */
+  MI_LP_ERROR_INTERNAL = 102 /* host exception inside the engine (e.g. out of
+                                memory); the handle stays usable */
 };
 
 /* glop::ProblemStatus (ortools/lp_data/lp_types.h:106-168). */
@@ -107,7 +109,8 @@ typedef struct mi_glop_params {
   int32_t markowitz_zlatev_parameter;                /* 29, 3 */
   int32_t allow_simplex_algorithm_change;            /* 32, false */
   int32_t devex_weights_reset_period;                /* 33, 150 */
-  int32_t use_middle_product_form_update;            /* 35, true (only true supported) */
+  int32_t use_middle_product_form_update;            /* 35, true; false = product-form etas
+                                                        (async/inline tau off) */
   int32_t initialize_devex_with_column_norms;        /* 36, true */
   int32_t exploit_singleton_column_in_initial_basis; /* 37, true */
   int32_t random_seed;                               /* 43, 1 */
@@ -166,7 +169,8 @@ enum {
   MI_K_UPDATE_ROW = 1,  /* UpdateRow column/row-wise (update_row.cc:196-306) */
   MI_K_PRIMAL_NORMS = 2,/* UpdateEdgeSquaredNorms (primal_edge_norms.cc:208-258) */
   MI_K_RC_UPDATE = 3,   /* UpdateReducedCosts (reduced_costs.cc:444-488) */
-  MI_K_PRICES = 4,      /* PrimalPrices candidate values (reduced_costs.cc:576-600) */
+  MI_K_TRI_SOLVE = 4,   /* dense U solve of FTRAN, TriangularMatrix::TransposeLowerSolve
+                           (sparse.cc:899-955, lu_factorization.cc:314-331) */
   MI_K_COL_NORMS = 5,   /* initial edge norms, identity basis (primal_edge_norms.cc:147-161) */
   MI_K_SPMV_ROWS = 6,   /* A x row sums: residual / basic values (variable_values.cc:101-133) */
   MI_K_SINGLE_ROW = 7,  /* ComputeUpdatesForSingleRow (update_row.cc:261-280) */
@@ -236,13 +240,17 @@ int mi_lp_reset_kernel_stats(mi_lp* h);
 int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable);
 
 /* Batch API: solves count independent LPs already loaded in handles (all on
- * the same device), using worker threads each owning its own stream. */
+ * the same device), using worker threads each owning its own stream.
+ * Returns non-OK only for bad arguments; each LP's outcome (including its
+ * error code) is in results[i]. No exception crosses this boundary. */
 int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
                       mi_lp_result* results);
 /* Batched children of one search node: count LPs that share
  * the workers' loaded matrix and differ in variable bounds (lbs/ubs are
  * count x n, row-major), each warm-started from warm_state (n+m statuses,
- * may be NULL) like LoadStateForNextSolve. One host thread per worker. */
+ * may be NULL, else warm_len must be n+m) like LoadStateForNextSolve. One
+ * host thread per worker. A child whose bounds or state cannot be loaded is
+ * not solved: results[i] = {ABNORMAL, that error code}. */
 int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t count,
                              const double* lbs, const double* ubs, const int8_t* warm_state,
                              int32_t warm_len, mi_lp_result* results);

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../../include/mi_lp.h"
+#include "device_solver.h"
 
 namespace milp {
 
@@ -21,10 +22,10 @@ struct DeviceError : public std::runtime_error {
   explicit DeviceError(const std::string& s) : std::runtime_error(s) {}
 };
 
-class DeviceLp {
+class DeviceLp : public DeviceSolver {
  public:
   DeviceLp() = default;
-  ~DeviceLp();
+  ~DeviceLp() override;
   DeviceLp(const DeviceLp&) = delete;
   DeviceLp& operator=(const DeviceLp&) = delete;
 
@@ -110,9 +111,15 @@ class DeviceLp {
   void DualBoxedFlips(const std::vector<int>* cols, double threshold,
                       std::vector<uint8_t>* flags);
 
+  // --- dense triangular solves of the LU (device_solve.hip) -------------
+  // TriangularMatrix::TransposeLowerSolve (sparse.cc:899-955) on one CU,
+  // bit-identical. MILP_DEVICE_SOLVE=off|force|auto (auto: m >= 16384).
+  bool TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
+                           std::vector<double>* x) override;
+
   // Accounting (roofline): launches, algorithmic bytes, HIP-event time.
   void SetTiming(bool on) { timing_ = on; }
-  const mi_lp_kernel_stats& stats() const { return stats_; }
+  const mi_lp_kernel_stats& stats();  // collects the pending event timings
   void ResetStats();
   void Synchronize();
   int dense_columns() const { return nd_; }
@@ -124,6 +131,8 @@ class DeviceLp {
   void Download(void* dst, const void* src, size_t bytes);
   void BeginKernel(int id);
   void EndKernel(int id, double bytes);
+  void* TakeEvent();
+  void DrainTimings();
   void Compact(int n);  // flags_ -> list_ (ascending) + coefficients, async
   void NextRowTag();
   void UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
@@ -141,12 +150,22 @@ class DeviceLp {
   void LaunchColumnDots(int mode, const double* d_y, const double* d_c, double* d_out,
                         const double* d_y2 = nullptr, double* d_out2 = nullptr);
   void Check(int err, const char* what);
+  void BuildTriSchedule(const TriangularMatrix& t, uint64_t key);
+  void FreeTriBuffers();
 
   int device_ = -1;
   void* stream_ = nullptr;  // hipStream_t
   void* ev_start_ = nullptr;
   void* ev_stop_ = nullptr;
   bool timing_ = false;
+  struct PendingTiming {
+    void* start;  // hipEvent_t
+    void* stop;
+    int id;
+  };
+  std::vector<PendingTiming> ev_pending_;
+  std::vector<void*> ev_pool_;
+  void* ev_open_ = nullptr;  // recorded by BeginKernel, closed by EndKernel
   double drop_ = 0.0;  // drop tolerance of the current update row
   mi_lp_kernel_stats stats_{};
   std::vector<void*> allocations_;
@@ -305,6 +324,35 @@ class DeviceLp {
   int32_t* d_sorted_slots_ = nullptr;
   void* d_sort_temp_ = nullptr;
   size_t sort_temp_bytes_ = 0;
+  // dense triangular solve (device_solve.hip): the level-ordered schedule of
+  // the last factorization's matrix, rebuilt when its key changes.
+  int tri_mode_ = 0;  // 0 auto, 1 force, 2 off
+  int tri_min_rows_ = 16384;
+  uint64_t tri_key_ = 0;
+  bool tri_ok_ = false;
+  int tri_rows_ = 0;
+  int tri_first_col_ = 0;
+  int tri_work_ = 0;
+  bool tri_ones_ = true;
+  int tri_levels_ = 0;
+  std::vector<int32_t> tri_level_width_;
+  int tri_debug_left_ = 0;
+  uint64_t* d_tri_clock_ = nullptr;
+  int32_t* d_tri_level_start_ = nullptr;
+  int32_t* d_tri_work_row_ = nullptr;
+  int32_t* d_tri_work_begin_ = nullptr;
+  int32_t* d_tri_entry_row_ = nullptr;
+  double* d_tri_entry_coef_ = nullptr;
+  double* d_tri_diag_ = nullptr;
+  double* d_tri_x_ = nullptr;
+  double* h_tri_x_ = nullptr;  // pinned staging, tri_rows_
+  void* h_tri_stage_ = nullptr;  // pinned staging of the schedule upload
+  size_t tri_stage_bytes_ = 0;
+  struct TriCaps {  // allocated elements of the d_tri_* buffers
+    size_t levels = 0, work = 0, begin = 0, entries = 0, coefs = 0, diag = 0, x = 0;
+  } tri_caps_;
+  std::vector<int32_t> tri_rows_upto_;     // work rows with output row <= r
+  std::vector<int64_t> tri_entries_upto_;  // their entries
 };
 
 }  // namespace milp

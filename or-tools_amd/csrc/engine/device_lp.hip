@@ -42,6 +42,7 @@ void DeviceLp::Check(int err, const char* what) {
 DeviceLp::~DeviceLp() {
   if (device_ >= 0) (void)hipSetDevice(device_);
   if (stream_ != nullptr) (void)hipStreamSynchronize(S(stream_));
+  FreeTriBuffers();
   for (void* p : allocations_) (void)hipFree(p);
   if (h_pin_i_) (void)hipHostFree(h_pin_i_);
   if (h_pin_d_) (void)hipHostFree(h_pin_d_);
@@ -64,6 +65,12 @@ DeviceLp::~DeviceLp() {
   }
   if (ev_start_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_start_));
   if (ev_stop_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_stop_));
+  for (const PendingTiming& t : ev_pending_) {
+    ev_pool_.push_back(t.start);
+    ev_pool_.push_back(t.stop);
+  }
+  if (ev_open_ != nullptr) ev_pool_.push_back(ev_open_);
+  for (void* e : ev_pool_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e));
   if (stream_) (void)hipStreamDestroy(S(stream_));
 }
 
@@ -106,6 +113,11 @@ void DeviceLp::Init(int device) {
   }
   if (const char* r = std::getenv("MILP_SMALL_SERIAL_ROWS")) small_serial_rows_ = std::atoi(r);
   if (const char* r = std::getenv("MILP_SMALL_THREADS")) small_threads_ = std::atoi(r);
+  if (const char* v = std::getenv("MILP_DEVICE_SOLVE")) {
+    if (std::strcmp(v, "force") == 0) tri_mode_ = 1;
+    if (std::strcmp(v, "off") == 0) tri_mode_ = 2;
+  }
+  if (const char* v = std::getenv("MILP_DEVICE_SOLVE_MIN_ROWS")) tri_min_rows_ = std::atoi(v);
 }
 
 template <typename T>
@@ -132,24 +144,61 @@ void DeviceLp::Synchronize() {
   small_inflight_ = false;
 }
 
-void DeviceLp::ResetStats() { std::memset(&stats_, 0, sizeof(stats_)); }
+void DeviceLp::ResetStats() {
+  DrainTimings();
+  std::memset(&stats_, 0, sizeof(stats_));
+}
+
+const mi_lp_kernel_stats& DeviceLp::stats() {
+  DrainTimings();
+  return stats_;
+}
+
+// Kernel timing: every logical launch is bracketed by two events recorded on
+// the stream; their elapsed times are collected later (when the stats are
+// read, or every 512 launches), so timing adds no synchronization to the
+// iteration it measures.
+void* DeviceLp::TakeEvent() {
+  if (!ev_pool_.empty()) {
+    void* e = ev_pool_.back();
+    ev_pool_.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  Check(hipEventCreate(&e), "hipEventCreate");
+  return e;
+}
+
+void DeviceLp::DrainTimings() {
+  for (const PendingTiming& t : ev_pending_) {
+    Check(hipEventSynchronize(reinterpret_cast<hipEvent_t>(t.stop)), "ev sync");
+    float ms = 0.0f;
+    Check(hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(t.start),
+                              reinterpret_cast<hipEvent_t>(t.stop)),
+          "ev time");
+    stats_.device_ms[t.id] += ms;
+    ev_pool_.push_back(t.start);
+    ev_pool_.push_back(t.stop);
+  }
+  ev_pending_.clear();
+}
 
 void DeviceLp::BeginKernel(int /*id*/) {
-  if (timing_) Check(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_start_), S(stream_)), "ev");
+  if (!timing_) return;
+  if (ev_open_ == nullptr) ev_open_ = TakeEvent();
+  Check(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_open_), S(stream_)), "ev");
 }
 
 void DeviceLp::EndKernel(int id, double bytes) {
   Check(hipGetLastError(), "kernel launch");
   stats_.launches[id] += 1;
   stats_.algorithmic_bytes[id] += bytes;
-  if (timing_) {
-    Check(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_stop_), S(stream_)), "ev");
-    Check(hipEventSynchronize(reinterpret_cast<hipEvent_t>(ev_stop_)), "ev sync");
-    float ms = 0.0f;
-    Check(hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(ev_start_),
-                              reinterpret_cast<hipEvent_t>(ev_stop_)),
-          "ev time");
-    stats_.device_ms[id] += ms;
+  if (timing_ && ev_open_ != nullptr) {
+    void* stop = TakeEvent();
+    Check(hipEventRecord(reinterpret_cast<hipEvent_t>(stop), S(stream_)), "ev");
+    ev_pending_.push_back(PendingTiming{ev_open_, stop, id});
+    ev_open_ = nullptr;
+    if (ev_pending_.size() >= 512) DrainTimings();
   }
 }
 

@@ -64,8 +64,12 @@ class HostPool {
     }
     while (pending_.load(std::memory_order_acquire) != 0) Pause();
     // Retire the job; return only when no worker can still be reading it.
-    job_.store(nullptr, std::memory_order_release);
-    while (active_.load(std::memory_order_acquire) != 0) Pause();
+    // The retire store and the active_ load are seq_cst, as are the worker's
+    // active_ increment and job_ load: release/acquire would let this load be
+    // ordered before the store (store-load reordering), and a worker that
+    // registers in that window would still read the retired job.
+    job_.store(nullptr, std::memory_order_seq_cst);
+    while (active_.load(std::memory_order_seq_cst) != 0) Pause();
   }
 
   ~HostPool() {
@@ -115,8 +119,8 @@ class HostPool {
       }
       seen = g;
       if (stop_.load(std::memory_order_acquire)) return;
-      active_.fetch_add(1, std::memory_order_acq_rel);
-      const std::function<void(int)>* job = job_.load(std::memory_order_acquire);
+      active_.fetch_add(1, std::memory_order_seq_cst);
+      const std::function<void(int)>* job = job_.load(std::memory_order_seq_cst);
       if (job != nullptr) {
         const int parts = job_parts_.load(std::memory_order_relaxed);
         for (int p = next_part_.fetch_add(1, std::memory_order_acq_rel); p < parts;

@@ -1,6 +1,7 @@
 // Host basis factorization of the MI355X simplex engine (see lu.h).
 #include "lu.h"
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -351,7 +352,15 @@ void Markowitz::UpdateResidualMatrix(int pivot_row, int pivot_col) {
 
 // ---------------------------------------------------------------------------
 // LuFactorization (lu_factorization.cc)
+namespace {
+uint64_t NextFactorizationKey() {
+  static std::atomic<uint64_t> next{1};
+  return next.fetch_add(1, std::memory_order_relaxed);
+}
+}  // namespace
+
 void LuFactorization::Clear() {
+  factorization_key_ = NextFactorizationKey();
   lower_.Reset(0, 0);
   upper_.Reset(0, 0);
   transpose_upper_.Reset(0, 0);
@@ -632,7 +641,13 @@ void LuFactorization::RightSolveUWithNonZeros(ScatteredVector* x) const {
   upper_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
   x->non_zeros_are_sorted = true;
   if (x->non_zeros.empty()) {
-    transpose_upper_.TransposeLowerSolve(&x->values);
+    // The dense U solve: on the device for the solver's thread (the tau
+    // worker keeps the host loop), same result bits.
+    if (device_solver_ == nullptr || g_lu_slot != 0 ||
+        !device_solver_->TransposeLowerSolve(transpose_upper_, factorization_key_,
+                                             &x->values)) {
+      transpose_upper_.TransposeLowerSolve(&x->values);
+    }
   } else {
     transpose_upper_.TransposeHyperSparseSolveWithReversedNonZeros(
         &x->values, &x->non_zeros);

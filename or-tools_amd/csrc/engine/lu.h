@@ -12,6 +12,7 @@
 #include <memory>
 #include <string>
 
+#include "device_solver.h"
 #include "lp_data.h"
 
 namespace milp {
@@ -821,6 +822,9 @@ class LuFactorization {
   }
   void SetParameters(const LuParameters& p) { markowitz_.SetParameters(p); }
   bool IsIdentityFactorization() const { return is_identity_factorization_; }
+  // Dense U solves of the solver's thread go to this device (engine
+  // substitution, bit-identical; see device_solver.h).
+  void SetDeviceSolver(DeviceSolver* d) { device_solver_ = d; }
 
   // Exposed for the factor-structure parity tests.
   const TriangularMatrix& lower() const { return lower_; }
@@ -852,6 +856,10 @@ class LuFactorization {
   mutable std::vector<int> non_zero_rows_;
   mutable SparseColumn column_of_upper_;
   Markowitz markowitz_;
+  DeviceSolver* device_solver_ = nullptr;
+  // Unique per factorization (process-wide), so that a device copy of U is
+  // never mistaken for the U of another factorization or handle.
+  uint64_t factorization_key_ = 0;
 };
 
 // rank_one_update.h:30-148
@@ -1098,6 +1106,7 @@ class BasisFactorization {
     lu_factorization_.SetParameters(lu);
   }
   const LuFactorization& lu() const { return lu_factorization_; }
+  void SetDeviceSolver(DeviceSolver* d) { lu_factorization_.SetDeviceSolver(d); }
 
   // basis_representation.cc:607-624 (public: replayed by the GPU paths).
   void BumpDeterministicTimeForSolve(int64_t num_entries) const;

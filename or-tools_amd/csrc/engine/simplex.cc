@@ -2289,6 +2289,7 @@ class VariableValues {
   }
   void UpdateGivenNonBasicVariables(const std::vector<int>& cols, bool update_basic);
   void RecomputeDualPrices(bool put_more_importance_on_norm = false);
+  void RecomputeDualPricesImpl(bool put_more_importance_on_norm, Fractional* delta);
   void UpdateDualPrices(const std::vector<int>& rows);
   template <typename Rows>
   bool UpdatePrimalPhaseICosts(const Rows& rows, std::vector<Fractional>* objective) {
@@ -2431,14 +2432,10 @@ void VariableValues::UpdateGivenNonBasicVariables(const std::vector<int>& cols,
   initially_all_zero_scratchpad_.ClearNonZerosIfTooDense();
   bf_.RightSolve(&initially_all_zero_scratchpad_);
   if (initially_all_zero_scratchpad_.non_zeros.empty()) {
-    Fractional* x = variable_values_.data();
-    constexpr int kAhead = 16;
-    for (int row = 0; row < num_rows; ++row) {
-      if (row + kAhead < num_rows) __builtin_prefetch(x + basis_[row + kAhead], 1);
-      x[basis_[row]] -= initially_all_zero_scratchpad_[row];
-    }
-    initially_all_zero_scratchpad_.values.assign(num_rows, 0.0);
-    RecomputeDualPrices();
+    // x_B update, scratch reset and RecomputeDualPrices() in one pass: a
+    // row's price reads only its own basic variable, so the three loops of
+    // variable_values.cc:211-217 and :229-262 fuse row by row.
+    RecomputeDualPricesImpl(false, initially_all_zero_scratchpad_.values.data());
     return;
   }
   for (const int row : initially_all_zero_scratchpad_.non_zeros) {
@@ -2451,6 +2448,15 @@ void VariableValues::UpdateGivenNonBasicVariables(const std::vector<int>& cols,
 
 // variable_values.cc:229-262
 void VariableValues::RecomputeDualPrices(bool put_more_importance_on_norm) {
+  RecomputeDualPricesImpl(put_more_importance_on_norm, nullptr);
+}
+
+// With delta != nullptr, first x[basis[row]] -= delta[row] and delta[row] =
+// 0 (UpdateGivenNonBasicVariables' dense update). Rows are split over the
+// host pool in 64-row ranges, so every candidate-bit word has one writer;
+// DenseAddOrUpdate touches no shared state besides its own value and bit.
+void VariableValues::RecomputeDualPricesImpl(bool put_more_importance_on_norm,
+                                             Fractional* delta) {
   SubTimer timer(kSubDualPrices);
   const int num_rows = matrix_.num_rows();
   dual_prices_->ClearAndResize(num_rows);
@@ -2460,25 +2466,35 @@ void VariableValues::RecomputeDualPrices(bool put_more_importance_on_norm) {
   const std::vector<Fractional>& sn = dual_edge_norms_->GetEdgeSquaredNorms();
   // The basic columns are scattered over arrays of N entries: their values
   // and bounds are prefetched a few rows ahead.
-  const Fractional* x = variable_values_.data();
+  Fractional* x = variable_values_.data();
   const Fractional* lb = variables_info_.GetVariableLowerBounds().data();
   const Fractional* ub = variables_info_.GetVariableUpperBounds().data();
-  constexpr int kAhead = 16;
-  for (int row = 0; row < num_rows; ++row) {
-    if (row + kAhead < num_rows) {
-      const int ahead = basis_[row + kAhead];
-      __builtin_prefetch(x + ahead);
-      __builtin_prefetch(lb + ahead);
-      __builtin_prefetch(ub + ahead);
+  const int* basis = basis_.data();
+  Fractional* values = dual_prices_->mutable_values();
+  uint64_t* words = dual_prices_->mutable_candidate_words();
+  ParallelRanges(num_rows, 16384, 64, [&](int, int64_t begin, int64_t end) {
+    constexpr int kAhead = 16;
+    for (int64_t row = begin; row < end; ++row) {
+      if (row + kAhead < end) {
+        const int ahead = basis[row + kAhead];
+        __builtin_prefetch(x + ahead, 1);
+        __builtin_prefetch(lb + ahead);
+        __builtin_prefetch(ub + ahead);
+      }
+      const int col = basis[row];
+      if (delta != nullptr) {
+        x[col] -= delta[row];
+        delta[row] = 0.0;
+      }
+      // GetUpperBoundInfeasibility / GetLowerBoundInfeasibility
+      const Fractional inf = std::max(x[col] - ub[col], lb[col] - x[col]);
+      if (inf > tolerance) {
+        words[row >> 6] |= uint64_t{1} << (row & 63);
+        values[row] =
+            put_more_importance_on_norm ? std::fabs(inf) / sn[row] : Square(inf) / sn[row];
+      }
     }
-    const int col = basis_[row];
-    const Fractional inf =
-        std::max(GetUpperBoundInfeasibility(col), GetLowerBoundInfeasibility(col));
-    if (inf > tolerance) {
-      dual_prices_->DenseAddOrUpdate(
-          row, put_more_importance_on_norm ? std::fabs(inf) / sn[row] : Square(inf) / sn[row]);
-    }
-  }
+  });
 }
 
 // variable_values.cc:264-297
@@ -3108,6 +3124,7 @@ RevisedSimplex::RevisedSimplex()
       entering_variable_(variables_info_, &random_, &reduced_costs_),
       primal_prices_(&random_, variables_info_, &primal_edge_norms_, &reduced_costs_) {
   reduced_costs_.SetDeferredNorms(&primal_edge_norms_);
+  basis_factorization_.SetDeviceSolver(&device_);
   SetParameters(parameters_);
 }
 
@@ -4914,8 +4931,34 @@ void RunSolve(mi_lp* h, const volatile int32_t* interrupt, mi_lp_result* out) {
     out->error_code = MI_LP_ERROR_DEVICE;
     out->problem_status = MI_LP_ABNORMAL;
     h->solved = false;
+  } catch (const std::exception& e) {
+    // Nothing may unwind through extern "C" or out of a batch worker thread.
+    h->error = std::string("engine exception: ") + e.what();
+    out->error_code = MI_LP_ERROR_INTERNAL;
+    out->problem_status = MI_LP_ABNORMAL;
+    h->solved = false;
+  } catch (...) {
+    h->error = "engine exception";
+    out->error_code = MI_LP_ERROR_INTERNAL;
+    out->problem_status = MI_LP_ABNORMAL;
+    h->solved = false;
   }
 }
+
+// A batch entry whose setup failed: reported like a failed solve, the other
+// entries of the batch are unaffected.
+void FailEntry(mi_lp* h, int code, const char* what, mi_lp_result* out) {
+  std::memset(out, 0, sizeof(*out));
+  out->error_code = code;
+  out->problem_status = MI_LP_ABNORMAL;
+  h->error = what;
+  h->solved = false;
+}
+
+int LoadLp(mi_lp* h, int32_t m, int32_t n, const int64_t* cs, const int32_t* ri,
+           const double* vals, const double* clb, const double* cub, const double* rlb,
+           const double* rub, const double* obj, double obj_offset, double obj_scale,
+           int32_t maximize);
 
 }  // namespace
 
@@ -4978,7 +5021,8 @@ int mi_lp_device_count(void) {
 int mi_lp_create(int device, mi_lp** out) {
   if (out == nullptr) return MI_LP_ERROR_NULL;
   *out = nullptr;
-  mi_lp* h = new mi_lp();
+  mi_lp* h = new (std::nothrow) mi_lp();
+  if (h == nullptr) return MI_LP_ERROR_INTERNAL;
   try {
     h->simplex.device().Init(device);
   } catch (const milp::DeviceError& e) {
@@ -5024,6 +5068,30 @@ int mi_lp_load(mi_lp* h, int32_t m, int32_t n, const int64_t* cs, const int32_t*
                int32_t maximize) {
   if (h == nullptr || cs == nullptr) return MI_LP_ERROR_NULL;
   if (m < 0 || n < 0) return MI_LP_ERROR_INVALID_PROBLEM;
+  if (h->running) return MI_LP_ERROR_STATE;
+  if (cs[n] > 0 && (ri == nullptr || vals == nullptr)) return MI_LP_ERROR_NULL;
+  if ((n > 0 && (clb == nullptr || cub == nullptr || obj == nullptr)) ||
+      (m > 0 && (rlb == nullptr || rub == nullptr))) {
+    return MI_LP_ERROR_NULL;
+  }
+  try {
+    return LoadLp(h, m, n, cs, ri, vals, clb, cub, rlb, rub, obj, obj_offset, obj_scale,
+                  maximize);
+  } catch (const std::exception& e) {
+    h->loaded = false;
+    h->solved = false;
+    h->error = std::string("mi_lp_load: ") + e.what();
+    return MI_LP_ERROR_INTERNAL;
+  }
+}
+
+}  // extern "C"
+
+namespace {
+int LoadLp(mi_lp* h, int32_t m, int32_t n, const int64_t* cs, const int32_t* ri,
+           const double* vals, const double* clb, const double* cub, const double* rlb,
+           const double* rub, const double* obj, double obj_offset, double obj_scale,
+           int32_t maximize) {
   milp::LinearProgram& lp = h->lp;
   lp.m = m;
   lp.n = n;
@@ -5044,6 +5112,9 @@ int mi_lp_load(mi_lp* h, int32_t m, int32_t n, const int64_t* cs, const int32_t*
   h->solved = false;
   return MI_LP_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int mi_lp_load_basis_state(mi_lp* h, const int8_t* st, int32_t len) {
   if (h == nullptr || (st == nullptr && len > 0)) return MI_LP_ERROR_NULL;
@@ -5239,6 +5310,10 @@ int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable) {
 int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
                       mi_lp_result* results) {
   if (handles == nullptr || results == nullptr) return MI_LP_ERROR_NULL;
+  if (count < 0) return MI_LP_ERROR_INVALID_PROBLEM;
+  for (int i = 0; i < count; ++i) {
+    if (handles[i] == nullptr) return MI_LP_ERROR_NULL;
+  }
   if (num_threads < 1) num_threads = 1;
   std::atomic<int> next(0);
   std::vector<std::thread> pool;
@@ -5252,27 +5327,35 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
     });
   }
   for (auto& th : pool) th.join();
-  return MI_LP_OK;
+  return MI_LP_OK;  // per-entry outcomes are in results[i]
 }
 
 // One search node's children: LP i = the workers' common LP with variable
 // bounds lbs/ubs[i * n ...], warm-started from warm_state when given.
 // Workers (handles loaded with the same LP, any devices) pull LPs from a
-// shared counter, one host thread per worker.
+// shared counter, one host thread per worker. n and warm_len are checked
+// against the workers' LP; a child whose setup fails is reported in its own
+// result (ABNORMAL + error code) and is not solved.
 int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t count,
                              const double* lbs, const double* ubs, const int8_t* warm_state,
                              int32_t warm_len, mi_lp_result* results) {
   if (workers == nullptr || lbs == nullptr || ubs == nullptr || results == nullptr) {
     return MI_LP_ERROR_NULL;
   }
-  if (num_workers < 1) return MI_LP_ERROR_INVALID_PROBLEM;
+  if (num_workers < 1 || count < 0) return MI_LP_ERROR_INVALID_PROBLEM;
   for (int w = 0; w < num_workers; ++w) {
     if (workers[w] == nullptr) return MI_LP_ERROR_NULL;
-    if (!workers[w]->loaded || workers[w]->lp.n != workers[0]->lp.n) return MI_LP_ERROR_STATE;
+    if (!workers[w]->loaded || workers[w]->lp.n != workers[0]->lp.n ||
+        workers[w]->lp.m != workers[0]->lp.m) {
+      return MI_LP_ERROR_STATE;
+    }
+    if (workers[w]->running) return MI_LP_ERROR_STATE;
   }
   const int64_t n = workers[0]->lp.n;
+  if (warm_state != nullptr && warm_len != n + workers[0]->lp.m) {
+    return MI_LP_ERROR_INVALID_PROBLEM;
+  }
   std::atomic<int> next(0);
-  std::atomic<int> first_error(MI_LP_OK);
   std::vector<std::thread> pool;
   for (int w = 0; w < num_workers; ++w) {
     pool.emplace_back([&, w]() {
@@ -5281,12 +5364,16 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
       while (true) {
         const int i = next.fetch_add(1);
         if (i >= count) break;
-        mi_lp_set_variable_bounds(h, lbs + i * n, ubs + i * n);
+        int rc = mi_lp_set_variable_bounds(h, lbs + i * n, ubs + i * n);
+        if (rc != MI_LP_OK) {
+          FailEntry(h, rc, "mi_lp_set_variable_bounds failed", &results[i]);
+          continue;
+        }
         if (warm_state != nullptr) {
-          const int rc = mi_lp_load_basis_state(h, warm_state, warm_len);
+          rc = mi_lp_load_basis_state(h, warm_state, warm_len);
           if (rc != MI_LP_OK) {
-            int expected = MI_LP_OK;
-            first_error.compare_exchange_strong(expected, rc);
+            FailEntry(h, rc, "mi_lp_load_basis_state failed", &results[i]);
+            continue;
           }
         }
         RunSolve(h, nullptr, &results[i]);
@@ -5294,7 +5381,7 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
     });
   }
   for (auto& th : pool) th.join();
-  return first_error.load();
+  return MI_LP_OK;  // per-entry outcomes are in results[i]
 }
 
 }  // extern "C"

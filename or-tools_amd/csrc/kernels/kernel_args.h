@@ -243,6 +243,25 @@ struct RowSumArgs {
   double* out;
 };
 
+
+// Dense triangular solve on one CU (tri_solve.hip): TransposeLowerSolve of a
+// TriangularMatrix with its outputs listed in dependency-level order.
+constexpr int kTriThreads = 1024;
+constexpr int kTriUnroll = 2;  // outputs per thread whose loads overlap
+struct TriSolveArgs {
+  const int32_t* level_start; // [num_levels + 1] list positions of each level
+  const int32_t* work_row;    // [num_work] output row of each listed position
+  const int32_t* work_begin;  // [num_work + 1] its entries in entry_row/coef
+  const int32_t* entry_row;   // entries in evaluation order (sparse.cc:857-897)
+  const double* entry_coef;
+  const double* diag;         // [num_work] diagonal, nullptr when all are 1
+  double* x;                  // [num_rows] in/out
+  int num_work;
+  int num_levels;
+  int num_rows;
+  int top;                    // rows above it are not computed (host: last non-zero)
+  uint64_t* clock;            // debug (MILP_TRI_DEBUG): wall clock after each level, or null
+};
 }  // namespace milp_kernels
 
 namespace milp_launch {
@@ -310,6 +329,8 @@ hipError_t set_colbits(const int32_t* cols, const uint8_t* bits, int n, uint8_t*
 // cols == nullptr: every column whose bit 2 (non-basic boxed) is set.
 hipError_t boxed_flips(const int32_t* cols, int n, const double* rc, const uint8_t* colbits,
                        double threshold, uint8_t* flag, hipStream_t s);
+// One workgroup (one CU).
+hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, hipStream_t s);
 hipError_t column_squared_norms(const int64_t* starts, const double* vals,
                                 const uint64_t* relevant, int ncols, double* out,
                                 hipStream_t s);

@@ -137,7 +137,7 @@ INVALID_PROBLEM = 10
 IMPRECISE = 11
 
 # Kernel ids (include/mi_lp.h MI_K_*)
-KERNEL_NAMES = ["pricing", "update_row", "primal_norms", "rc_update", "prices",
+KERNEL_NAMES = ["pricing", "update_row", "primal_norms", "rc_update", "tri_solve",
                 "col_norms", "spmv_rows", "single_row", "dual_ratio", "readback"]
 
 # Names of every exported entry point of include/mi_lp.h (checked by tests).

@@ -43,3 +43,13 @@ def max_over_ranks(x, dist=None, device=None):
     t = torch.tensor([x], dtype=torch.float64, device=device or "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(x, dist=None, device=None):
+    """Total of a per-rank count (iterations or LPs done by every rank)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return x
+    import torch
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device or "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())

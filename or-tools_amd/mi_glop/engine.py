@@ -245,8 +245,20 @@ def batch_solve_bounds(workers, lbs, ubs, warm_state=None):
     L = lib()
     for w in workers:
         w._push_params()
+    if not workers:
+        raise ValueError("batch_solve_bounds needs at least one worker")
+    lp = workers[0].lp
+    if lp is None or any(w.lp is None or (w.lp.m, w.lp.n) != (lp.m, lp.n) for w in workers):
+        raise ValueError("every worker must have the same LP shape loaded")
     lbs = np.ascontiguousarray(lbs, dtype=np.float64)
     ubs = np.ascontiguousarray(ubs, dtype=np.float64)
+    if lbs.ndim != 2 or lbs.shape[1] != lp.n:
+        raise ValueError(f"lbs must be (count, {lp.n}), got {lbs.shape}")
+    if ubs.shape != lbs.shape:
+        raise ValueError(f"ubs shape {ubs.shape} != lbs shape {lbs.shape}")
+    if warm_state is not None and len(warm_state) != lp.n + lp.m:
+        raise ValueError(f"warm_state must have n+m={lp.n + lp.m} entries, "
+                         f"got {len(warm_state)}")
     count = lbs.shape[0]
     arr = (ctypes.c_void_p * len(workers))(*[w.h.value for w in workers])
     res = (abi.MiLpResult * count)()

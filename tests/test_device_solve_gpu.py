@@ -1,0 +1,97 @@
+"""Dense U solves of FTRAN on the device (engine/device_solve.hip,
+kernels/tri_solve.hip) vs the CPU oracle, which runs Glop's host loop
+TriangularMatrix::TransposeLowerSolve (sparse.cc:899-955).
+
+MILP_DEVICE_SOLVE=force sends every dense U solve of the solver's thread to
+the single-CU level-scheduled kernel at test size; the engine must still
+reproduce the oracle bit for bit (basis, statuses, values, iterations) and
+its deterministic time must not move."""
+import pytest
+
+from mi_glop import abi, engine
+
+import kat_lps
+import lp_gen
+import parity_util
+
+pytestmark = pytest.mark.gpu
+
+
+def _handle(params):
+    return engine.LpHandle(params)
+
+
+def _cases():
+    cases = []
+    for seed in (71, 72, 73):
+        cases.append((f"c5_{seed}", lambda s=seed: lp_gen.sparse_c5_lp(400 + 40 * (s % 3),
+                                                                      4000, 6, s), 1))
+    # Its U fills in (a hundred entries per row, depth ~250 by iteration
+    # 4000): long outputs go through the batched-entries path.
+    cases.append(("c5_wide", lambda: lp_gen.sparse_c5_lp(1500, 12000, 8, 74), 1))
+    cases.append(("sparse_primal", lambda: lp_gen.random_sparse_lp(200, 900, 0.04, 75), 0))
+    cases.append(("dense_primal", lambda: lp_gen.dense_box_lp(97, 400, 76), 0))
+    cases.append(("dense_dual", lambda: lp_gen.dense_box_lp(120, 600, 77), 1))
+    return cases
+
+
+@pytest.mark.parametrize("case", _cases(), ids=lambda c: c[0])
+def test_device_u_solve_parity(case, monkeypatch):
+    name, build, dual = case
+    lp = build()
+    p = abi.default_params(use_dual_simplex=dual, max_number_of_iterations=4000)
+    monkeypatch.setenv("MILP_DEVICE_SOLVE", "off")
+    _, _, _, r_host = parity_util.solve_both(lp, p, _handle)
+    monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    assert rg.deterministic_time == r_host.deterministic_time
+    st = g.kernel_stats()["tri_solve"]
+    if name.startswith("c5") or name.startswith("dense"):
+        assert st["launches"] > 0, f"{name}: no dense U solve reached the device"
+
+
+@pytest.mark.parametrize("device_dual", ["off", "force"])
+@pytest.mark.parametrize("async_solves", ["off", "force"])
+def test_device_u_solve_with_async_tau_and_device_dual(device_dual, async_solves, monkeypatch):
+    """The tau FTRAN keeps the host loop on the factorization's worker while
+    the solver's thread sends its dense U solves to the device; with the
+    dual device mode on or off, the results are the oracle's."""
+    monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
+    monkeypatch.setenv("MILP_DEVICE_DUAL", device_dual)
+    monkeypatch.setenv("MILP_ASYNC_SOLVES", async_solves)
+    lp = lp_gen.sparse_c5_lp(600, 6000, 6, 78)
+    p = abi.default_params(use_dual_simplex=1)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    assert g.kernel_stats()["tri_solve"]["launches"] > 0
+
+
+@pytest.mark.parametrize("builder", kat_lps.ALL, ids=lambda f: f.__name__)
+@pytest.mark.parametrize("dual", [0, 1])
+def test_device_u_solve_known_answers(builder, dual, monkeypatch):
+    monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
+    lp, _ = builder()
+    p = abi.default_params(use_dual_simplex=dual)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+
+
+def test_device_u_solve_warm_started_children(monkeypatch):
+    """CP-SAT-style re-solves: each child refactorizes, so the device schedule
+    is rebuilt for every factorization key."""
+    monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
+    import jobshop
+    lp, ycols = jobshop.relaxation(jobshop.FT06)
+    p = abi.default_params(use_dual_simplex=1)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    state = o.state()
+    lbs, ubs = jobshop.child_bounds(lp, ycols, 6, 5)
+    for i in range(len(lbs)):
+        for h in (o, g):
+            h.set_variable_bounds(lbs[i], ubs[i])
+            h.load_basis_state(state)
+        ro2 = o.solve()
+        rg2 = g.solve()
+        parity_util.compare(o, ro2, g, rg2, lp)

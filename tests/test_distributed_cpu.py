@@ -50,8 +50,9 @@ def _worker(rank, world, port, out_dir):
     local = distributed.best_bound(res, abi.OPTIMAL)
     shared = distributed.share_bound(local, dist)
     slowest = distributed.max_over_ranks(float(rank + 1), dist)
+    total = distributed.sum_over_ranks(e - b, dist)
     with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
-        f.write(f"{b} {e} {local!r} {shared!r} {slowest!r}\n")
+        f.write(f"{b} {e} {local!r} {shared!r} {slowest!r} {total!r}\n")
     dist.destroy_process_group()
 
 
@@ -89,4 +90,5 @@ def test_bound_share_world2(tmp_path):
     for row in rows:
         assert float(row[3]) == best  # all-reduce(min) = global best bound
         assert float(row[4]) == 2.0   # max over ranks
+        assert float(row[5]) == 10.0  # sum over ranks: every child counted once
     assert min(float(rows[0][2]), float(rows[1][2])) == best
