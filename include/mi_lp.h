@@ -206,6 +206,35 @@ int mi_lp_clear_basis_state(mi_lp* h);
 int mi_lp_set_variable_bounds(mi_lp* h, const double* col_lb, const double* col_ub);
 int mi_lp_notify_matrix_unchanged(mi_lp* h);
 
+/* CP-SAT's calls on the RevisedSimplex it keeps per LP constraint
+ * (sat/linear_programming_constraint.cc:319,430,1247,1264):
+ *   mi_lp_notify_matrix_changed          NotifyThatMatrixIsChangedForNextSolve
+ *                                        (revised_simplex.h:169, .cc:135)
+ *   mi_lp_set_starting_variable_values   SetStartingVariableValuesForNextSolve
+ *                                        (revised_simplex.h:161, .cc:126); n+m values
+ *   mi_lp_set_integrality_scale          SetIntegralityScale (revised_simplex.h:237,
+ *                                        .cc:2588); a later OPTIMAL solve then runs
+ *                                        Polish() (.cc:341-344, 2595-2734)
+ *   mi_lp_objective_limit_reached        objective_limit_reached (revised_simplex.h:186)
+ *   mi_lp_get_unit_row_left_inverse      GetUnitRowLeftInverse (revised_simplex.h:209):
+ *                                        e_row^T B^-1 of the current basis, m dense
+ *                                        values + its non-zero rows (non_zeros may be
+ *                                        NULL; an empty list means "dense")
+ *   mi_lp_compute_dictionary /           ComputeDictionary (revised_simplex.h:226,
+ *   mi_lp_get_dictionary                 .cc:3785): B^-1 A row by row, scaled by
+ *                                        column_scales (NULL: unscaled); the first call
+ *                                        returns the entry count, the second copies
+ *                                        row_starts (m+1), cols and values out. */
+int mi_lp_notify_matrix_changed(mi_lp* h);
+int mi_lp_set_starting_variable_values(mi_lp* h, const double* values, int32_t len);
+int mi_lp_set_integrality_scale(mi_lp* h, int32_t col, double scale);
+int mi_lp_objective_limit_reached(const mi_lp* h, int32_t* reached);
+int mi_lp_get_unit_row_left_inverse(mi_lp* h, int32_t row, double* values, int32_t* non_zeros,
+                                    int32_t* num_non_zeros);
+int mi_lp_compute_dictionary(mi_lp* h, const double* column_scales, int32_t scales_len,
+                             int64_t* nnz);
+int mi_lp_get_dictionary(const mi_lp* h, int64_t* row_starts, int32_t* cols, double* values);
+
 /* interrupt may be NULL; a non-zero value stops the solve like a time limit
  * (glop_interface.cc:138-140). */
 int mi_lp_solve(mi_lp* h, const volatile int32_t* interrupt, mi_lp_result* out);

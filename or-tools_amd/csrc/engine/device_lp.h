@@ -151,6 +151,7 @@ class DeviceLp : public DeviceSolver {
                         const double* d_y2 = nullptr, double* d_out2 = nullptr);
   void Check(int err, const char* what);
   void BuildTriSchedule(const TriangularMatrix& t, uint64_t key);
+  void TriReserve(int which, size_t bytes);
   void FreeTriBuffers();
 
   int device_ = -1;
@@ -336,21 +337,25 @@ class DeviceLp : public DeviceSolver {
   bool tri_ones_ = true;
   int tri_levels_ = 0;
   std::vector<int32_t> tri_level_width_;
+  std::vector<int> tri_segments_;  // tri_transpose_lower launch plan
+  int tri_wide_level_ = 6144;      // MILP_TRI_WIDE: wider levels run over the chip
   int tri_debug_left_ = 0;
   uint64_t* d_tri_clock_ = nullptr;
-  int32_t* d_tri_level_start_ = nullptr;
-  int32_t* d_tri_work_row_ = nullptr;
-  int32_t* d_tri_work_begin_ = nullptr;
-  int32_t* d_tri_entry_row_ = nullptr;
-  double* d_tri_entry_coef_ = nullptr;
-  double* d_tri_diag_ = nullptr;
-  double* d_tri_x_ = nullptr;
+  // Device buffers of the schedule (staged in this order) and of the values.
+  enum TriBuf {
+    kTriLevels, kTriRecRow, kTriRecN, kTriRecEntry, kTriRecValue, kTriDiag, kTriOvfPos,
+    kTriOvfValue, kTriPosRow, kTriNumStaged, kTriX = kTriNumStaged, kTriY, kTriNumBuffers
+  };
+  struct TriBuffer {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+  };
+  TriBuffer tri_buf_[kTriNumBuffers];
+  int tri_pos_ = 0;
+  size_t h_tri_x_elems_ = 0;
   double* h_tri_x_ = nullptr;  // pinned staging, tri_rows_
   void* h_tri_stage_ = nullptr;  // pinned staging of the schedule upload
   size_t tri_stage_bytes_ = 0;
-  struct TriCaps {  // allocated elements of the d_tri_* buffers
-    size_t levels = 0, work = 0, begin = 0, entries = 0, coefs = 0, diag = 0, x = 0;
-  } tri_caps_;
   std::vector<int32_t> tri_rows_upto_;     // work rows with output row <= r
   std::vector<int64_t> tri_entries_upto_;  // their entries
 };

@@ -118,6 +118,7 @@ void DeviceLp::Init(int device) {
     if (std::strcmp(v, "off") == 0) tri_mode_ = 2;
   }
   if (const char* v = std::getenv("MILP_DEVICE_SOLVE_MIN_ROWS")) tri_min_rows_ = std::atoi(v);
+  if (const char* v = std::getenv("MILP_TRI_WIDE")) tri_wide_level_ = std::atoi(v);
 }
 
 template <typename T>

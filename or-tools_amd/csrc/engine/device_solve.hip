@@ -38,45 +38,43 @@ struct SolveCallTimer {
   }
 };
 
-template <typename T>
-void Grow(T** p, size_t* cap_elems, size_t need, const char* what) {
-  if (*p != nullptr && *cap_elems >= need) return;
-  if (*p != nullptr) (void)hipFree(*p);
-  *p = nullptr;
-  const size_t n = std::max<size_t>(need, 1) + need / 4;
-  if (hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)) != hipSuccess) {
-    throw DeviceError(std::string("hipMalloc (") + what + ")");
-  }
-  *cap_elems = n;
-}
-
 }  // namespace
 
+void DeviceLp::TriReserve(int which, size_t bytes) {
+  TriBuffer& b = tri_buf_[which];
+  if (b.ptr != nullptr && b.bytes >= bytes) return;
+  if (b.ptr != nullptr) (void)hipFree(b.ptr);
+  b.ptr = nullptr;
+  b.bytes = 0;
+  const size_t n = std::max<size_t>(bytes, 16) + bytes / 4;
+  Check(hipMalloc(&b.ptr, n), "hipMalloc (triangular solve)");
+  b.bytes = n;
+}
+
 void DeviceLp::FreeTriBuffers() {
-  for (void* p : {static_cast<void*>(d_tri_level_start_), static_cast<void*>(d_tri_work_row_),
-                  static_cast<void*>(d_tri_work_begin_),
-                  static_cast<void*>(d_tri_entry_row_), static_cast<void*>(d_tri_entry_coef_),
-                  static_cast<void*>(d_tri_diag_), static_cast<void*>(d_tri_x_)}) {
-    if (p != nullptr) (void)hipFree(p);
+  for (TriBuffer& b : tri_buf_) {
+    if (b.ptr != nullptr) (void)hipFree(b.ptr);
+    b = TriBuffer();
   }
-  d_tri_level_start_ = d_tri_work_row_ = d_tri_work_begin_ = d_tri_entry_row_ = nullptr;
-  d_tri_entry_coef_ = d_tri_diag_ = d_tri_x_ = nullptr;
   if (d_tri_clock_ != nullptr) (void)hipFree(d_tri_clock_);
   d_tri_clock_ = nullptr;
   if (h_tri_x_ != nullptr) (void)hipHostFree(h_tri_x_);
   if (h_tri_stage_ != nullptr) (void)hipHostFree(h_tri_stage_);
   h_tri_x_ = nullptr;
+  h_tri_x_elems_ = 0;
   h_tri_stage_ = nullptr;
   tri_stage_bytes_ = 0;
   tri_key_ = 0;
   tri_ok_ = false;
-  tri_caps_ = TriCaps();
 }
 
 // Level schedule of t's TransposeLowerSolve: output c (a column of t, rows
 // first_non_identity .. num_cols-1) depends on the rows of its entries, all
 // > c. level(c) = 0 without entries, else 1 + the deepest entry. Outputs
 // with no entries and a unit diagonal are the identity and are not listed.
+// Positions: the listed outputs by level (descending c inside a level, the
+// host order), then the other rows >= first_non_identity (read, never
+// written). Entries refer to positions.
 void DeviceLp::BuildTriSchedule(const TriangularMatrix& t, uint64_t key) {
   tri_key_ = key;
   tri_ok_ = false;
@@ -99,91 +97,144 @@ void DeviceLp::BuildTriSchedule(const TriangularMatrix& t, uint64_t key) {
     depth = std::max(depth, l);
     if (l > 0 || !tri_ones_) ++num_work;
   }
-  // Counting sort by level; inside a level, descending c (the host order).
+  const int num_pos = nc - fni;
+  // Counting sort by level.
   std::vector<int32_t> level_start(depth + 2, 0);
   for (int c = nc - 1; c >= fni; --c) {
     if (level[c] > 0 || !tri_ones_) ++level_start[level[c] + 1];
   }
   for (int l = 0; l <= depth; ++l) level_start[l + 1] += level_start[l];
   tri_work_ = num_work;
+  tri_pos_ = num_pos;
+  tri_levels_ = depth + 1;
   tri_level_width_.resize(depth + 1);
   for (int l = 0; l <= depth; ++l) tri_level_width_[l] = level_start[l + 1] - level_start[l];
+  // Launch segments: each wide level alone over the chip, each run of narrow
+  // levels as one single-CU launch (tri_solve.hip).
+  tri_segments_.clear();
+  for (int l = 0; l <= depth;) {
+    const int w = tri_level_width_[l];
+    if (w == 0) {
+      ++l;
+      continue;
+    }
+    if (w > tri_wide_level_) {
+      tri_segments_.push_back(-l - 1);
+      tri_segments_.push_back(std::min(1024, (w + 255) / 256));
+      ++l;
+      continue;
+    }
+    int e = l;
+    while (e <= depth && tri_level_width_[e] <= tri_wide_level_) ++e;
+    tri_segments_.push_back(l);
+    tri_segments_.push_back(e);
+    l = e;
+  }
   if (const char* d = std::getenv("MILP_TRI_DEBUG")) tri_debug_left_ = std::atoi(d);
-  // Levels that hold listed outputs (level 0 is empty when every diagonal is 1).
-  tri_levels_ = depth + 1;
-  // Staging layout: level_start | work_row | work_begin | entry_row | (pad)
-  // entry_coef | diag.
-  const size_t off_work = size_t(depth + 2) * 4;
-  const size_t off_begin = off_work + size_t(num_work) * 4;
-  const size_t off_entry = off_begin + size_t(num_work + 1) * 4;
-  const size_t off_coef = (off_entry + size_t(nnz) * 4 + 7) / 8 * 8;
-  const size_t off_diag = off_coef + size_t(nnz) * 8;
-  const size_t bytes = off_diag + (tri_ones_ ? 0 : size_t(num_work) * 8);
+  // Positions.
+  std::vector<int32_t> pos_row(num_pos);
+  std::vector<int32_t> pos_of(nc, -1);
+  {
+    std::vector<int32_t> next(level_start.begin(), level_start.end() - 1);
+    int tail = num_work;
+    for (int c = nc - 1; c >= fni; --c) {
+      const int k = (level[c] > 0 || !tri_ones_) ? next[level[c]]++ : tail++;
+      pos_row[k] = c;
+      pos_of[c] = k;
+    }
+  }
+  int64_t num_ovf = 0;
+  for (int k = 0; k < num_work; ++k) {
+    const int c = pos_row[k];
+    const int64_t n = t.starts_[c + 1] - t.starts_[c];
+    if (n > 4) num_ovf += n;
+  }
+  // Staging layout, 16-byte aligned pieces.
+  auto al = [](size_t b) { return (b + 15) / 16 * 16; };
+  const size_t b_levels = al(size_t(depth + 2) * 4);
+  const size_t b_row = al(size_t(num_work) * 4);
+  const size_t b_n = al(size_t(num_work) * 4);
+  const size_t b_entry = size_t(num_work) * 16;
+  const size_t b_value = size_t(num_work) * 32;
+  const size_t b_diag = tri_ones_ ? 0 : al(size_t(num_work) * 8);
+  const size_t b_ovf_pos = al(size_t(num_ovf) * 4);
+  const size_t b_ovf_val = al(size_t(num_ovf) * 8);
+  const size_t b_pos_row = al(size_t(num_pos) * 4);
+  const size_t sizes[kTriNumStaged] = {b_levels, b_row,     b_n,       b_entry,  b_value,
+                                       b_diag,   b_ovf_pos, b_ovf_val, b_pos_row};
+  size_t offs[kTriNumStaged];
+  size_t bytes = 0;
+  for (int b = 0; b < kTriNumStaged; ++b) {
+    offs[b] = bytes;
+    bytes += sizes[b];
+  }
   if (tri_stage_bytes_ < bytes) {
     if (h_tri_stage_ != nullptr) (void)hipHostFree(h_tri_stage_);
     h_tri_stage_ = nullptr;
-    Check(hipHostMalloc(&h_tri_stage_, bytes + bytes / 4), "pin");
-    tri_stage_bytes_ = bytes + bytes / 4;
+    Check(hipHostMalloc(&h_tri_stage_, bytes + bytes / 4 + 16), "pin");
+    tri_stage_bytes_ = bytes + bytes / 4 + 16;
   }
   char* st = static_cast<char*>(h_tri_stage_);
-  int32_t* lstart = reinterpret_cast<int32_t*>(st);
+  int32_t* lstart = reinterpret_cast<int32_t*>(st + offs[kTriLevels]);
+  int32_t* rec_row = reinterpret_cast<int32_t*>(st + offs[kTriRecRow]);
+  int32_t* rec_n = reinterpret_cast<int32_t*>(st + offs[kTriRecN]);
+  int32_t* rec_entry = reinterpret_cast<int32_t*>(st + offs[kTriRecEntry]);
+  double* rec_value = reinterpret_cast<double*>(st + offs[kTriRecValue]);
+  double* diag = reinterpret_cast<double*>(st + offs[kTriDiag]);
+  int32_t* ovf_pos = reinterpret_cast<int32_t*>(st + offs[kTriOvfPos]);
+  double* ovf_value = reinterpret_cast<double*>(st + offs[kTriOvfValue]);
   std::copy(level_start.begin(), level_start.end(), lstart);
-  int32_t* work_row = reinterpret_cast<int32_t*>(st + off_work);
-  int32_t* work_begin = reinterpret_cast<int32_t*>(st + off_begin);
-  int32_t* entry_row = reinterpret_cast<int32_t*>(st + off_entry);
-  double* entry_coef = reinterpret_cast<double*>(st + off_coef);
-  double* diag = reinterpret_cast<double*>(st + off_diag);
-  std::vector<int32_t> next(level_start.begin(), level_start.end() - 1);
-  std::vector<int32_t> pos_of(nc, -1);
-  for (int c = nc - 1; c >= fni; --c) {
-    if (level[c] == 0 && tri_ones_) continue;
-    const int k = next[level[c]]++;
-    work_row[k] = c;
-    pos_of[c] = k;
-  }
+  std::copy(pos_row.begin(), pos_row.end(), reinterpret_cast<int32_t*>(st + offs[kTriPosRow]));
   // Entries of each listed output in evaluation order: the host walks the
   // column from its last entry down (sparse.cc:908-955).
-  int32_t e = 0;
+  int64_t o = 0;
   for (int k = 0; k < num_work; ++k) {
-    const int c = work_row[k];
-    work_begin[k] = e;
-    for (int64_t i = t.starts_[c + 1] - 1; i >= t.starts_[c]; --i) {
-      entry_row[e] = t.rows_[i];
-      entry_coef[e] = t.coefficients_[i];
-      ++e;
+    const int c = pos_row[k];
+    const int64_t b = t.starts_[c], e = t.starts_[c + 1];
+    const int n = static_cast<int>(e - b);
+    rec_row[k] = c;
+    rec_n[k] = n;
+    if (n <= 4) {
+      for (int j = 0; j < 4; ++j) {
+        rec_entry[4 * k + j] = j < n ? pos_of[t.rows_[e - 1 - j]] : 0;
+        rec_value[4 * k + j] = j < n ? t.coefficients_[e - 1 - j] : 0.0;
+      }
+    } else {
+      rec_entry[4 * k] = static_cast<int32_t>(o);
+      rec_entry[4 * k + 1] = rec_entry[4 * k + 2] = rec_entry[4 * k + 3] = 0;
+      for (int j = 0; j < 4; ++j) rec_value[4 * k + j] = 0.0;
+      for (int64_t i = e - 1; i >= b; --i) {
+        ovf_pos[o] = pos_of[t.rows_[i]];
+        ovf_value[o] = t.coefficients_[i];
+        ++o;
+      }
     }
     if (!tri_ones_) diag[k] = t.diagonal_coefficients_[c];
   }
-  work_begin[num_work] = e;
   // Prefix counts by output row, for the byte accounting of a solve that
   // stops at `top`.
   tri_rows_upto_.assign(nc + 1, 0);
   tri_entries_upto_.assign(nc + 1, 0);
   for (int c = 0; c < nc; ++c) {
-    const bool listed = pos_of[c] >= 0;
+    const bool listed = c >= fni && pos_of[c] < num_work;
     tri_rows_upto_[c + 1] = tri_rows_upto_[c] + (listed ? 1 : 0);
     tri_entries_upto_[c + 1] =
         tri_entries_upto_[c] + (listed ? t.starts_[c + 1] - t.starts_[c] : 0);
   }
-  TriCaps& caps = tri_caps_;
-  Grow(&d_tri_level_start_, &caps.levels, size_t(depth) + 2, "tri levels");
-  Grow(&d_tri_work_row_, &caps.work, num_work, "tri work");
-  Grow(&d_tri_work_begin_, &caps.begin, size_t(num_work) + 1, "tri begin");
-  Grow(&d_tri_entry_row_, &caps.entries, size_t(nnz), "tri entries");
-  Grow(&d_tri_entry_coef_, &caps.coefs, size_t(nnz), "tri coefs");
-  if (!tri_ones_) Grow(&d_tri_diag_, &caps.diag, num_work, "tri diag");
-  if (caps.x < size_t(nc) || h_tri_x_ == nullptr) {
-    Grow(&d_tri_x_, &caps.x, nc, "tri x");
+  for (int b = 0; b < kTriNumStaged; ++b) {
+    if (sizes[b] == 0) continue;
+    TriReserve(b, sizes[b]);
+    Upload(tri_buf_[b].ptr, st + offs[b], sizes[b]);
+  }
+  TriReserve(kTriX, size_t(nc) * 8);
+  TriReserve(kTriY, size_t(std::max(num_pos, 1)) * 8);
+  if (h_tri_x_elems_ < size_t(nc)) {
     if (h_tri_x_ != nullptr) (void)hipHostFree(h_tri_x_);
     h_tri_x_ = nullptr;
-    Check(hipHostMalloc(reinterpret_cast<void**>(&h_tri_x_), caps.x * sizeof(double)), "pin");
+    h_tri_x_elems_ = size_t(nc) + size_t(nc) / 4;
+    Check(hipHostMalloc(reinterpret_cast<void**>(&h_tri_x_), h_tri_x_elems_ * sizeof(double)),
+          "pin");
   }
-  Upload(d_tri_level_start_, lstart, size_t(depth + 2) * 4);
-  Upload(d_tri_work_row_, work_row, size_t(num_work) * 4);
-  Upload(d_tri_work_begin_, work_begin, size_t(num_work + 1) * 4);
-  Upload(d_tri_entry_row_, entry_row, size_t(nnz) * 4);
-  Upload(d_tri_entry_coef_, entry_coef, size_t(nnz) * 8);
-  if (!tri_ones_) Upload(d_tri_diag_, diag, size_t(num_work) * 8);
   // The staging buffer is reused by the next build: wait for the copies.
   Check(hipStreamSynchronize(Stream(stream_)), "sync");
   tri_ok_ = true;
@@ -207,19 +258,24 @@ bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
   if (tri_rows_upto_[top + 1] - tri_rows_upto_[fni] == 0) return true;  // identity part only
   // Outputs c >= fni read rows > c only: x[fni..nc) in, x[fni..top] out.
   const size_t in = size_t(nc - fni);
+  double* d_x = static_cast<double*>(tri_buf_[kTriX].ptr);
   CopyHost(h_tri_x_ + fni, xv + fni, in * sizeof(double));
-  Upload(d_tri_x_ + fni, h_tri_x_ + fni, in * sizeof(double));
+  Upload(d_x + fni, h_tri_x_ + fni, in * sizeof(double));
   milp_kernels::TriSolveArgs a;
-  a.level_start = d_tri_level_start_;
-  a.num_levels = tri_levels_;
-  a.work_row = d_tri_work_row_;
-  a.work_begin = d_tri_work_begin_;
-  a.entry_row = d_tri_entry_row_;
-  a.entry_coef = d_tri_entry_coef_;
-  a.diag = tri_ones_ ? nullptr : d_tri_diag_;
-  a.x = d_tri_x_;
+  a.level_start = static_cast<const int32_t*>(tri_buf_[kTriLevels].ptr);
+  a.rec_row = static_cast<const int32_t*>(tri_buf_[kTriRecRow].ptr);
+  a.rec_n = static_cast<const int32_t*>(tri_buf_[kTriRecN].ptr);
+  a.rec_entry = static_cast<const int4*>(tri_buf_[kTriRecEntry].ptr);
+  a.rec_value = static_cast<const double2*>(tri_buf_[kTriRecValue].ptr);
+  a.diag = tri_ones_ ? nullptr : static_cast<const double*>(tri_buf_[kTriDiag].ptr);
+  a.ovf_pos = static_cast<const int32_t*>(tri_buf_[kTriOvfPos].ptr);
+  a.ovf_value = static_cast<const double*>(tri_buf_[kTriOvfValue].ptr);
+  a.pos_row = static_cast<const int32_t*>(tri_buf_[kTriPosRow].ptr);
+  a.x = d_x;
+  a.y = static_cast<double*>(tri_buf_[kTriY].ptr);
   a.num_work = tri_work_;
-  a.num_rows = nc;
+  a.num_pos = tri_pos_;
+  a.num_levels = tri_levels_;
   a.top = top;
   a.clock = nullptr;
   // MILP_TRI_DEBUG=k: per-level wall clock of the first k solves after each
@@ -229,33 +285,44 @@ bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
     if (d_tri_clock_ == nullptr) {
       Check(hipMalloc(reinterpret_cast<void**>(&d_tri_clock_), 65536 * sizeof(uint64_t)),
             "hipMalloc");
+      Check(hipMemsetAsync(d_tri_clock_, 0, 65536 * sizeof(uint64_t), Stream(stream_)),
+            "memset");
     }
     if (tri_levels_ + 1 < 65536) a.clock = d_tri_clock_;
   }
   BeginKernel(MI_K_TRI_SOLVE);
-  Check(milp_launch::tri_transpose_lower(a, Stream(stream_)), "tri_transpose_lower");
+  Check(milp_launch::tri_transpose_lower(a, tri_segments_.data(),
+                                         static_cast<int>(tri_segments_.size() / 2),
+                                         Stream(stream_)),
+        "tri_transpose_lower");
   const double rows = tri_rows_upto_[top + 1] - tri_rows_upto_[fni];
   const double entries =
       static_cast<double>(tri_entries_upto_[top + 1] - tri_entries_upto_[fni]);
-  // Per computed output: its list slot (4 + 4 B), x in and out (16 B), the
-  // diagonal (8 B) unless unit; per entry: row and value (12 B) and the
-  // gathered x (8 B).
-  EndKernel(MI_K_TRI_SOLVE, rows * (24.0 + (tri_ones_ ? 0.0 : 8.0)) + entries * 20.0);
+  // Per computed output: its record (row, count: 8 B), its value in and out
+  // (16 B), the diagonal (8 B) unless unit; per entry: position and value
+  // (12 B) and the value it reads (8 B). The permutes in and out: 8 B in, 8 B
+  // out and the 4-B row index per position, both ways.
+  EndKernel(MI_K_TRI_SOLVE, rows * (24.0 + (tri_ones_ ? 0.0 : 8.0)) + entries * 20.0 +
+                                double(tri_pos_) * 20.0 + rows * 20.0);
   const size_t out = size_t(top - fni + 1);
   if (a.clock != nullptr) {
+    // Single-CU segments only (a wide level leaves its slot untouched: 0).
     --tri_debug_left_;
+    Synchronize();
     std::vector<uint64_t> clk(tri_levels_ + 1);
     Check(hipMemcpy(clk.data(), d_tri_clock_, clk.size() * sizeof(uint64_t),
                     hipMemcpyDeviceToHost), "D2H");
-    std::fprintf(stderr, "[tri] rows %d work %d levels %d top %d: total %.1f us; per level (us/width):",
-                 nc, tri_work_, tri_levels_, top, (clk.back() - clk[0]) / 100.0);
+    std::fprintf(stderr, "[tri] rows %d work %d levels %d segments %zu top %d; per level (us/width):",
+                 nc, tri_work_, tri_levels_, tri_segments_.size() / 2, top);
     for (int l = 0; l < tri_levels_; ++l) {
-      std::fprintf(stderr, " %.2f/%d", (clk[l + 1] - clk[l]) / 100.0,
+      const bool ok = clk[l] != 0 && clk[l + 1] >= clk[l];
+      std::fprintf(stderr, " %.2f/%d", ok ? (clk[l + 1] - clk[l]) / 100.0 : -1.0,
                    tri_level_width_[l]);
     }
     std::fprintf(stderr, "\n");
+    Check(hipMemsetAsync(d_tri_clock_, 0, 65536 * sizeof(uint64_t), Stream(stream_)), "memset");
   }
-  Download(h_tri_x_ + fni, d_tri_x_ + fni, out * sizeof(double));
+  Download(h_tri_x_ + fni, d_x + fni, out * sizeof(double));
   CopyHost(xv + fni, h_tri_x_ + fni, out * sizeof(double));
   return true;
 }

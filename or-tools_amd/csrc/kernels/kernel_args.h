@@ -244,23 +244,28 @@ struct RowSumArgs {
 };
 
 
-// Dense triangular solve on one CU (tri_solve.hip): TransposeLowerSolve of a
-// TriangularMatrix with its outputs listed in dependency-level order.
+// Dense triangular solve (tri_solve.hip): TransposeLowerSolve of a
+// TriangularMatrix with its outputs listed in dependency-level order and the
+// values kept in that order on the device.
 constexpr int kTriThreads = 1024;
-constexpr int kTriUnroll = 2;  // outputs per thread whose loads overlap
+constexpr int kTriPrefetch = 2;  // outputs per thread loaded ahead of their level
 struct TriSolveArgs {
-  const int32_t* level_start; // [num_levels + 1] list positions of each level
-  const int32_t* work_row;    // [num_work] output row of each listed position
-  const int32_t* work_begin;  // [num_work + 1] its entries in entry_row/coef
-  const int32_t* entry_row;   // entries in evaluation order (sparse.cc:857-897)
-  const double* entry_coef;
-  const double* diag;         // [num_work] diagonal, nullptr when all are 1
-  double* x;                  // [num_rows] in/out
+  const int32_t* level_start;  // [num_levels + 1] list positions of each level
+  const int32_t* rec_row;      // [num_work] row (index into x) of each listed output
+  const int32_t* rec_n;        // [num_work] its number of entries
+  const int4* rec_entry;       // [num_work] entry positions (n <= 4) / overflow start
+  const double2* rec_value;    // [2 * num_work] entry values (n <= 4)
+  const double* diag;          // [num_work] diagonal, nullptr when all are 1
+  const int32_t* ovf_pos;      // entries of the outputs with n > 4
+  const double* ovf_value;
+  const int32_t* pos_row;      // [num_pos] row of every position (listed first)
+  double* x;                   // rows, in/out
+  double* y;                   // [num_pos] values in position order (scratch)
   int num_work;
+  int num_pos;
   int num_levels;
-  int num_rows;
-  int top;                    // rows above it are not computed (host: last non-zero)
-  uint64_t* clock;            // debug (MILP_TRI_DEBUG): wall clock after each level, or null
+  int top;                     // rows above it are not computed (host: last non-zero)
+  uint64_t* clock;             // debug (MILP_TRI_DEBUG): wall clock after each level, or null
 };
 }  // namespace milp_kernels
 
@@ -329,8 +334,10 @@ hipError_t set_colbits(const int32_t* cols, const uint8_t* bits, int n, uint8_t*
 // cols == nullptr: every column whose bit 2 (non-basic boxed) is set.
 hipError_t boxed_flips(const int32_t* cols, int n, const double* rc, const uint8_t* colbits,
                        double threshold, uint8_t* flag, hipStream_t s);
-// One workgroup (one CU).
-hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, hipStream_t s);
+// segments: num_segments pairs; (lb, le) with lb >= 0 = levels [lb, le) on
+// one CU; (-level - 1, blocks) = one wide level over `blocks` workgroups.
+hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, const int* segments,
+                               int num_segments, hipStream_t s);
 hipError_t column_squared_norms(const int64_t* starts, const double* vals,
                                 const uint64_t* relevant, int ncols, double* out,
                                 hipStream_t s);

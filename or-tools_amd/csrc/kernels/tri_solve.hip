@@ -1,4 +1,4 @@
-// Dense triangular solve of the basis factorization on one CU.
+// Dense triangular solve of the basis factorization.
 //
 // Replaces TriangularMatrix::TransposeLowerSolve (lp_data/sparse.cc:899-955),
 // which Glop runs for the U part of an FTRAN whenever the result is too
@@ -10,125 +10,177 @@
 // reads only rows r > c, and the subtraction order of one output is fixed by
 // its own entries: groups of four products, summed left to right, subtracted
 // one group at a time, then the 1-3 remaining products one by one, entries
-// taken from the end of the column. A thread that computes x[c] from its
-// entries in that order gets Glop's bits, whatever the order in which the
-// outputs are computed, as long as every x[r] it reads is final.
+// taken from the end of the column. Computing x[c] from its entries in that
+// order gives Glop's bits, whatever the order in which the outputs are
+// computed, as long as every x[r] read is final.
 //
-// Schedule: the host lists the outputs by dependency level (level 0: no
-// entries), entries in evaluation order (engine/device_solve.hip). One
-// 1024-thread workgroup (one CU, so every hand-off stays inside one L1/L2)
-// computes the levels in turn with a barrier between them. x values are read
-// at agent scope (L2), never from a possibly stale L1 line.
-
+// Layout (engine/device_solve.hip builds it once per factorization): the
+// outputs are listed by dependency level (level 0: no entries) and the
+// values live in that order, y[k] = x[row(k)], so that an output's own read
+// and write are coalesced and its entries are positions into y. Per
+// position, structure-of-arrays records: row, entry count, up to 4 entries
+// (positions and values) inline, the diagonal; longer outputs point into
+// overflow arrays. A solve permutes x into y, computes the levels, permutes
+// back.
+//
+// Schedule: the level sequence is cut into segments. A wide level (thousands
+// of independent outputs, e.g. the diagonal-only level 0) is one launch over
+// the whole chip. A run of narrow levels is one launch of one 1024-thread
+// workgroup (one CU: every hand-off stays inside one L1/L2) that computes the
+// levels in turn with a barrier between them; the next level's records are
+// loaded while the current one computes. Values written in the same launch
+// are read at agent scope (L2), never from a possibly stale L1 line.
 #include <hip/hip_runtime.h>
 
 #include "kernel_args.h"
 
 namespace milp_kernels {
 
-__device__ __forceinline__ double load_final(const double* x, int r) {
-  return __hip_atomic_load(x + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ double load_final(const double* y, int k) {
+  return __hip_atomic_load(y + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Glop's evaluation of one output from its entries e0, e1, ... (evaluation
-// order): groups of four products summed left to right, each group
-// subtracted, then the 1-3 remaining products one by one.
-__device__ __forceinline__ double group_sum(const TriSolveArgs& a, const double* x, int e) {
-  return a.entry_coef[e] * load_final(x, a.entry_row[e]) +
-         a.entry_coef[e + 1] * load_final(x, a.entry_row[e + 1]) +
-         a.entry_coef[e + 2] * load_final(x, a.entry_row[e + 2]) +
-         a.entry_coef[e + 3] * load_final(x, a.entry_row[e + 3]);
+// The structure of one listed output.
+struct TriRec {
+  int row;  // a.top + 1 when the position is empty
+  int n;
+  int4 e;   // entry positions (n <= 4); e.x = overflow start when n > 4
+  double v[4];
+  double d;
+};
+
+__device__ __forceinline__ void tri_load(const TriSolveArgs& a, int k, int le, TriRec* r) {
+  const bool in = k < le;
+  const int kk = in ? k : 0;  // a valid address for an empty slot
+  r->row = in ? a.rec_row[kk] : a.top + 1;
+  r->n = a.rec_n[kk];
+  r->e = a.rec_entry[kk];
+  const double2 v01 = a.rec_value[2 * kk];
+  const double2 v23 = a.rec_value[2 * kk + 1];
+  r->v[0] = v01.x;
+  r->v[1] = v01.y;
+  r->v[2] = v23.x;
+  r->v[3] = v23.y;
+  r->d = a.diag != nullptr ? a.diag[kk] : 1.0;
 }
 
-__device__ __forceinline__ double tail_subtract(const TriSolveArgs& a, const double* x,
-                                                double sum, int e, int end) {
+// Entries of a long output (overflow arrays), in evaluation order, by batches
+// of 8 whose loads go out together.
+__device__ __forceinline__ double subtract_overflow(const TriSolveArgs& a, const double* y,
+                                                   double sum, int e, int end) {
+  for (; e + 7 < end; e += 8) {
+    double p[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p[i] = a.ovf_value[e + i] * load_final(y, a.ovf_pos[e + i]);
+    sum -= p[0] + p[1] + p[2] + p[3];
+    sum -= p[4] + p[5] + p[6] + p[7];
+  }
+  for (; e + 3 < end; e += 4) {
+    sum -= a.ovf_value[e] * load_final(y, a.ovf_pos[e]) +
+           a.ovf_value[e + 1] * load_final(y, a.ovf_pos[e + 1]) +
+           a.ovf_value[e + 2] * load_final(y, a.ovf_pos[e + 2]) +
+           a.ovf_value[e + 3] * load_final(y, a.ovf_pos[e + 3]);
+  }
   if (e < end) {
-    sum -= a.entry_coef[e] * load_final(x, a.entry_row[e]);
+    sum -= a.ovf_value[e] * load_final(y, a.ovf_pos[e]);
     if (e + 1 < end) {
-      sum -= a.entry_coef[e + 1] * load_final(x, a.entry_row[e + 1]);
-      if (e + 2 < end) sum -= a.entry_coef[e + 2] * load_final(x, a.entry_row[e + 2]);
+      sum -= a.ovf_value[e + 1] * load_final(y, a.ovf_pos[e + 1]);
+      if (e + 2 < end) sum -= a.ovf_value[e + 2] * load_final(y, a.ovf_pos[e + 2]);
     }
   }
   return sum;
 }
 
-// Entries of one output, in evaluation order, by batches of 8 (2 groups):
-// the 8 x loads of a batch are independent and go out together.
-__device__ __forceinline__ double subtract_entries(const TriSolveArgs& a, const double* x,
-                                                   double sum, int e, int end) {
-  for (; e + 7 < end; e += 8) {
-    double p[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) p[i] = a.entry_coef[e + i] * load_final(x, a.entry_row[e + i]);
-    sum -= p[0] + p[1] + p[2] + p[3];
-    sum -= p[4] + p[5] + p[6] + p[7];
-  }
-  for (; e + 3 < end; e += 4) sum -= group_sum(a, x, e);
-  return tail_subtract(a, x, sum, e, end);
-}
-
-// One output c from its entries (evaluation order) and the final x.
-__device__ __forceinline__ double solve_output(const TriSolveArgs& a, const double* x, int k,
-                                               int c, int beg, int end) {
-  double sum = x[c];
-  const int n = end - beg;
-  if (n <= 4) {
-    // Short rows (almost all of them): the 4 loads go out together.
-    int r[4];
-    double v[4], xr[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      r[i] = i < n ? a.entry_row[beg + i] : c;
-      v[i] = i < n ? a.entry_coef[beg + i] : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xr[i] = i < n ? load_final(x, r[i]) : 0.0;
+__device__ __forceinline__ void tri_compute(const TriSolveArgs& a, double* y, int k,
+                                            const TriRec& r) {
+  if (r.row > a.top) return;
+  double sum = y[k];
+  if (r.n <= 4) {
+    const int n = r.n;
+    const double y0 = n > 0 ? load_final(y, r.e.x) : 0.0;
+    const double y1 = n > 1 ? load_final(y, r.e.y) : 0.0;
+    const double y2 = n > 2 ? load_final(y, r.e.z) : 0.0;
+    const double y3 = n > 3 ? load_final(y, r.e.w) : 0.0;
     if (n == 4) {
-      sum -= v[0] * xr[0] + v[1] * xr[1] + v[2] * xr[2] + v[3] * xr[3];
+      sum -= r.v[0] * y0 + r.v[1] * y1 + r.v[2] * y2 + r.v[3] * y3;
     } else {
-      if (n > 0) sum -= v[0] * xr[0];
-      if (n > 1) sum -= v[1] * xr[1];
-      if (n > 2) sum -= v[2] * xr[2];
+      if (n > 0) sum -= r.v[0] * y0;
+      if (n > 1) sum -= r.v[1] * y1;
+      if (n > 2) sum -= r.v[2] * y2;
     }
   } else {
-    sum = subtract_entries(a, x, sum, beg, end);
+    sum = subtract_overflow(a, y, sum, r.e.x, r.e.x + r.n);
   }
-  return a.diag != nullptr ? sum / a.diag[k] : sum;
+  y[k] = a.diag != nullptr ? sum / r.d : sum;
 }
 
-// Level-synchronous: the outputs of one level depend only on earlier
-// levels, so the workgroup computes a level, then meets at a barrier
-// (every store has completed: explicit s_waitcnt vmcnt(0), s_barrier), then the
-// next. Inside a level each thread takes up to kTriUnroll outputs at once so
-// that their loads overlap.
-__global__ __launch_bounds__(kTriThreads) void tri_transpose_lower_kernel(TriSolveArgs a) {
-  double* x = a.x;
+// y[k] = x[row(k)] for every position (listed or not).
+__global__ __launch_bounds__(256) void tri_gather_kernel(TriSolveArgs a) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.num_pos;
+       k += gridDim.x * blockDim.x) {
+    a.y[k] = a.x[a.pos_row[k]];
+  }
+}
+
+// x[row(k)] = y[k] for the computed outputs.
+__global__ __launch_bounds__(256) void tri_scatter_kernel(TriSolveArgs a) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.num_work;
+       k += gridDim.x * blockDim.x) {
+    const int row = a.rec_row[k];
+    if (row <= a.top) a.x[row] = a.y[k];
+  }
+}
+
+// One wide level over the whole chip; kernel boundaries order it with the
+// other levels.
+__global__ __launch_bounds__(256) void tri_level_grid_kernel(TriSolveArgs a, int level) {
+  const int lb = a.level_start[level];
+  const int le = a.level_start[level + 1];
+  for (int k = lb + blockIdx.x * blockDim.x + threadIdx.x; k < le;
+       k += gridDim.x * blockDim.x) {
+    TriRec r;
+    tri_load(a, k, le, &r);
+    tri_compute(a, a.y, k, r);
+  }
+}
+
+// Narrow levels [level_begin, level_end) on one CU, one level after the
+// other with a barrier between them (the level's stores have reached L2:
+// explicit s_waitcnt vmcnt(0), then s_barrier; __syncthreads alone does not
+// wait for them at workgroup scope).
+__global__ __launch_bounds__(kTriThreads) void tri_levels_cu_kernel(TriSolveArgs a,
+                                                                    int level_begin,
+                                                                    int level_end) {
+  double* y = a.y;
   const int tid = threadIdx.x;
-  if (a.clock != nullptr && tid == 0) a.clock[0] = wall_clock64();
-  for (int l = 0; l < a.num_levels; ++l) {
+  if (a.clock != nullptr && tid == 0) a.clock[level_begin] = wall_clock64();
+  TriRec pre[kTriPrefetch];
+  {
+    const int lb = a.level_start[level_begin];
+    const int le = a.level_start[level_begin + 1];
+#pragma unroll
+    for (int j = 0; j < kTriPrefetch; ++j) tri_load(a, lb + j * kTriThreads + tid, le, &pre[j]);
+  }
+  for (int l = level_begin; l < level_end; ++l) {
     const int lb = a.level_start[l];
     const int le = a.level_start[l + 1];
-    for (int base = lb; base < le; base += kTriUnroll * kTriThreads) {
-      int kk[kTriUnroll], cc[kTriUnroll], bb[kTriUnroll], ee[kTriUnroll];
+    TriRec cur[kTriPrefetch];
 #pragma unroll
-      for (int j = 0; j < kTriUnroll; ++j) {
-        kk[j] = base + j * kTriThreads + tid;
-        cc[j] = kk[j] < le ? a.work_row[kk[j]] : a.top + 1;
-        bb[j] = kk[j] < le ? a.work_begin[kk[j]] : 0;
-        ee[j] = kk[j] < le ? a.work_begin[kk[j] + 1] : 0;
-      }
-      double out[kTriUnroll];
+    for (int j = 0; j < kTriPrefetch; ++j) cur[j] = pre[j];
+    if (l + 1 < level_end) {
+      const int nb = a.level_start[l + 1];
+      const int ne = a.level_start[l + 2];
 #pragma unroll
-      for (int j = 0; j < kTriUnroll; ++j) {
-        if (cc[j] <= a.top) out[j] = solve_output(a, x, kk[j], cc[j], bb[j], ee[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < kTriUnroll; ++j) {
-        if (cc[j] <= a.top) x[cc[j]] = out[j];
-      }
+      for (int j = 0; j < kTriPrefetch; ++j) tri_load(a, nb + j * kTriThreads + tid, ne, &pre[j]);
     }
-    // The level's stores must have reached L2 before any wave reads them:
-    // __syncthreads alone does not wait for them here (workgroup scope).
+#pragma unroll
+    for (int j = 0; j < kTriPrefetch; ++j) tri_compute(a, y, lb + j * kTriThreads + tid, cur[j]);
+    // Positions beyond the prefetched ones (levels wider than the prefetch).
+    for (int k = lb + kTriPrefetch * kTriThreads + tid; k < le; k += kTriThreads) {
+      TriRec r;
+      tri_load(a, k, le, &r);
+      tri_compute(a, y, k, r);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (a.clock != nullptr && tid == 0) a.clock[l + 1] = wall_clock64();
@@ -139,9 +191,27 @@ __global__ __launch_bounds__(kTriThreads) void tri_transpose_lower_kernel(TriSol
 
 namespace milp_launch {
 
-hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, hipStream_t s) {
+hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, const int* segments,
+                               int num_segments, hipStream_t s) {
   if (args.num_work <= 0) return hipSuccess;
-  milp_kernels::tri_transpose_lower_kernel<<<1, milp_kernels::kTriThreads, 0, s>>>(args);
+  const int pos_blocks = std::min(1024, (args.num_pos + 255) / 256);
+  milp_kernels::tri_gather_kernel<<<pos_blocks, 256, 0, s>>>(args);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  for (int i = 0; i < num_segments; ++i) {
+    const int lb = segments[2 * i];
+    const int le = segments[2 * i + 1];
+    if (le <= lb) continue;
+    if (lb < 0) {  // a wide level on the whole chip: (-level - 1, blocks)
+      milp_kernels::tri_level_grid_kernel<<<le, 256, 0, s>>>(args, -lb - 1);
+    } else {
+      milp_kernels::tri_levels_cu_kernel<<<1, milp_kernels::kTriThreads, 0, s>>>(args, lb, le);
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const int work_blocks = std::min(1024, (args.num_work + 255) / 256);
+  milp_kernels::tri_scatter_kernel<<<work_blocks, 256, 0, s>>>(args);
   return hipGetLastError();
 }
 

@@ -152,7 +152,10 @@ EXPORTED_SYMBOLS = [
     "mi_lp_get_dual_ray_row_combination", "mi_lp_begin", "mi_lp_run_until",
     "mi_lp_finish", "mi_lp_stop", "mi_lp_get_kernel_stats", "mi_lp_reset_kernel_stats",
     "mi_lp_set_kernel_timing", "mi_lp_batch_solve", "mi_lp_set_variable_bounds",
-    "mi_lp_batch_solve_bounds",
+    "mi_lp_batch_solve_bounds", "mi_lp_notify_matrix_changed",
+    "mi_lp_set_starting_variable_values", "mi_lp_set_integrality_scale",
+    "mi_lp_objective_limit_reached", "mi_lp_get_unit_row_left_inverse",
+    "mi_lp_compute_dictionary", "mi_lp_get_dictionary",
     "mi_mps_read_file", "mi_mps_parse_string", "mi_mps_error", "mi_mps_dims", "mi_mps_get",
     "mi_mps_name", "mi_mps_col_name", "mi_mps_row_name", "mi_mps_free",
 ]

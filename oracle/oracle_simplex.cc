@@ -1995,6 +1995,23 @@ class RevisedSimplex {
     solution_state_has_been_set_externally_ = true;
   }
   void NotifyThatMatrixIsUnchangedForNextSolve() { notify_that_matrix_is_unchanged_ = true; }
+  // revised_simplex.cc:135-137
+  void NotifyThatMatrixIsChangedForNextSolve() { notify_that_matrix_is_unchanged_ = false; }
+  // revised_simplex.cc:126-129
+  void SetStartingVariableValuesForNextSolve(const std::vector<Fractional>& values) {
+    variable_starting_values_ = values;
+  }
+  void SetIntegralityScale(int col, Fractional scale);
+  bool objective_limit_reached() const { return objective_limit_reached_; }
+  // revised_simplex.h:209-211 (UpdateRow::ComputeAndGetUnitRowLeftInverse).
+  const ScatteredVector& GetUnitRowLeftInverse(int row) {
+    return update_row_.ComputeAndGetUnitRowLeftInverse(row);
+  }
+  // revised_simplex.cc:3785-3806: row r of B^-1 A, one direction per column.
+  // Returns triplets (row, col, value) in the order the reference fills its
+  // per-row sparse rows.
+  void ComputeDictionary(const std::vector<Fractional>* column_scales,
+                         std::vector<std::vector<std::pair<int, Fractional>>>* rows);
 
   ProblemStatus GetProblemStatus() const { return problem_status_; }
   Fractional GetObjectiveValue() const { return solution_objective_value_; }
@@ -2118,6 +2135,7 @@ class RevisedSimplex {
   Status PrimalMinimize(TimeLimit* time_limit);
   Status DualMinimize(bool feasibility_phase, TimeLimit* time_limit);
   Status PrimalPush(TimeLimit* time_limit);
+  Status Polish(TimeLimit* time_limit);
   Fractional ComputeObjectiveValue() const {
     return PreciseScalarProduct(objective_, variable_values_.GetDenseRow());
   }
@@ -2211,6 +2229,7 @@ class RevisedSimplex {
   std::vector<VariableStatus> solution_state_;
   bool solution_state_has_been_set_externally_ = true;
   std::vector<Fractional> variable_starting_values_;
+  std::vector<Fractional> integrality_scale_;  // SetIntegralityScale
   bool notify_that_matrix_is_unchanged_ = false;
   ScatteredVector direction_;
   Fractional direction_infinity_norm_ = 0.0;
@@ -2345,6 +2364,10 @@ Status RevisedSimplex::Solve(const LinearProgram& lp, TimeLimit* time_limit) {
       ORACLE_RETURN_IF_ERROR(PrimalMinimize(time_limit));
     } else {
       ORACLE_RETURN_IF_ERROR(DualMinimize(phase_ == Phase::FEASIBILITY, time_limit));
+    }
+    // revised_simplex.cc:341-344
+    if (!integrality_scale_.empty() && problem_status_ == ProblemStatus::OPTIMAL) {
+      ORACLE_RETURN_IF_ERROR(Polish(time_limit));
     }
     variable_values_.ResetAllNonBasicVariableValues(variable_starting_values_);
     ORACLE_RETURN_IF_ERROR(basis_factorization_.Refactorize());
@@ -3653,6 +3676,123 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
   return Status::OK();
 }
 
+// revised_simplex.cc:2588-2593
+void RevisedSimplex::SetIntegralityScale(int col, Fractional scale) {
+  if (col >= static_cast<int>(integrality_scale_.size())) {
+    integrality_scale_.resize(col + 1, 0.0);
+  }
+  integrality_scale_[col] = scale;
+}
+
+// revised_simplex.cc:2595-2734: after an optimal solve with integrality
+// scales set, up to 5 degenerate pivots among zero-reduced-cost columns that
+// make the basic solution less fractional.
+Status RevisedSimplex::Polish(TimeLimit* time_limit) {
+  struct Cleanup {
+    std::function<void()> f;
+    ~Cleanup() { f(); }
+  } cleanup{[this, time_limit]() { AdvanceDeterministicTime(time_limit); }};
+  const std::vector<Fractional>& rc = reduced_costs_.GetReducedCosts();
+  std::vector<int> candidates;
+  variables_info_.GetNotBasicBitRow().ForEach([&](int col) {
+    if (!variables_info_.GetIsRelevantBitRow()[col]) return;
+    if (std::fabs(rc[col]) < 1e-9) candidates.push_back(col);
+  });
+  bool refactorize = false;
+  int num_pivots = 0;
+  for (int i = 0; i < 10; ++i) {
+    AdvanceDeterministicTime(time_limit);
+    if (time_limit->LimitReached()) break;
+    if (num_pivots >= 5) break;
+    if (candidates.empty()) break;
+    const int index = UniformInt(random_, static_cast<int>(candidates.size()) - 1);
+    const int entering_col = candidates[index];
+    std::swap(candidates[index], candidates.back());
+    candidates.pop_back();
+    // The entering variable must move in a feasible direction.
+    Fractional fake_rc = 1.0;
+    if (!variables_info_.GetCanDecreaseBitRow()[entering_col]) fake_rc = -1.0;
+    if (reduced_costs_.NeedsBasisRefactorization()) refactorize = true;
+    ORACLE_RETURN_IF_ERROR(RefactorizeBasisIfNeeded(&refactorize));
+    ComputeDirection(entering_col);
+    Fractional step_length;
+    int leaving_row;
+    Fractional target_bound;
+    bool local_refactorize = false;
+    ORACLE_RETURN_IF_ERROR(ChooseLeavingVariableRow(entering_col, fake_rc, &local_refactorize,
+                                             &leaving_row, &step_length, &target_bound));
+    if (local_refactorize) continue;
+    if (step_length == kInfinity || step_length == -kInfinity) continue;
+    if (std::fabs(step_length) <= 1e-6) continue;
+    if (leaving_row != kInvalidRow && std::fabs(direction_[leaving_row]) < 0.1) continue;
+    const Fractional step = (fake_rc > 0.0) ? -step_length : step_length;
+    // Change of the total fractionality if the pivot is made.
+    const auto get_diff = [this](int col, Fractional old_value, Fractional new_value) {
+      if (col >= static_cast<int>(integrality_scale_.size()) ||
+          integrality_scale_[col] == 0.0) {
+        return 0.0;
+      }
+      const Fractional s = integrality_scale_[col];
+      return (std::fabs(new_value * s - std::round(new_value * s)) -
+              std::fabs(old_value * s - std::round(old_value * s)));
+    };
+    Fractional diff = get_diff(entering_col, variable_values_.Get(entering_col),
+                               variable_values_.Get(entering_col) + step);
+    for (const int row : direction_.non_zeros) {
+      const int col = basis_[row];
+      const Fractional old_value = variable_values_.Get(col);
+      const Fractional new_value = old_value - direction_[row] * step;
+      diff += get_diff(col, old_value, new_value);
+    }
+    if (diff > -1e-2) continue;
+    num_pivots++;
+    variable_values_.UpdateOnPivoting(direction_, entering_col, step);
+    if (leaving_row == kInvalidRow) {  // a bound flip of the entering column
+      if (step > 0.0) {
+        SetNonBasicVariableStatusAndDeriveValue(entering_col, VariableStatus::AT_UPPER_BOUND);
+      } else if (step < 0.0) {
+        SetNonBasicVariableStatusAndDeriveValue(entering_col, VariableStatus::AT_LOWER_BOUND);
+      }
+      continue;
+    }
+    const int leaving_col = basis_[leaving_row];
+    update_row_.ComputeUpdateRow(leaving_row);
+    primal_edge_norms_.UpdateBeforeBasisPivot(entering_col, leaving_col, leaving_row,
+                                              direction_, &update_row_);
+    dual_edge_norms_.UpdateBeforeBasisPivot(entering_col, leaving_row, direction_,
+                                            update_row_.GetUnitRowLeftInverse());
+    reduced_costs_.UpdateBeforeBasisPivot(entering_col, leaving_row, direction_, &update_row_);
+    const Fractional dir = -direction_[leaving_row] * step;
+    const bool is_degenerate =
+        (dir == 0.0) ||
+        (dir > 0.0 && variable_values_.Get(leaving_col) >= target_bound) ||
+        (dir < 0.0 && variable_values_.Get(leaving_col) <= target_bound);
+    if (!is_degenerate) variable_values_.Set(leaving_col, target_bound);
+    ORACLE_RETURN_IF_ERROR(UpdateAndPivot(entering_col, leaving_row, target_bound));
+  }
+  return Status::OK();
+}
+
+void RevisedSimplex::ComputeDictionary(const std::vector<Fractional>* column_scales,
+                                       std::vector<std::vector<std::pair<int, Fractional>>>* rows) {
+  rows->assign(num_rows_, {});
+  for (int col = 0; col < num_cols_; ++col) {
+    ComputeDirection(col);
+    for (const int row : direction_.non_zeros) {
+      if (column_scales == nullptr) {
+        (*rows)[row].emplace_back(col, direction_[row]);
+        continue;
+      }
+      const Fractional numerator =
+          col < static_cast<int>(column_scales->size()) ? (*column_scales)[col] : 1.0;
+      const Fractional denominator =
+          basis_[row] < static_cast<int>(column_scales->size()) ? (*column_scales)[basis_[row]]
+                                                                : 1.0;
+      (*rows)[row].emplace_back(col, direction_[row] * (numerator / denominator));
+    }
+  }
+}
+
 // revised_simplex.cc:3369-3543
 Status RevisedSimplex::PrimalPush(TimeLimit* time_limit) {
   bool refactorize = false;
@@ -3734,6 +3874,7 @@ Status RevisedSimplex::PrimalPush(TimeLimit* time_limit) {
 namespace {
 struct OracleHandle {
   oracle::RevisedSimplex simplex;
+  std::vector<std::vector<std::pair<int, double>>> dictionary;
   oracle::GlopParameters params;
   oracle::LinearProgram lp;
   bool solved = false;
@@ -3839,6 +3980,59 @@ int oracle_lp_clear_basis_state(void* hv) {
 }
 int oracle_lp_notify_matrix_unchanged(void* hv) {
   static_cast<OracleHandle*>(hv)->simplex.NotifyThatMatrixIsUnchangedForNextSolve();
+  return 0;
+}
+int oracle_lp_notify_matrix_changed(void* hv) {
+  static_cast<OracleHandle*>(hv)->simplex.NotifyThatMatrixIsChangedForNextSolve();
+  return 0;
+}
+int oracle_lp_set_starting_variable_values(void* hv, const double* values, int32_t len) {
+  static_cast<OracleHandle*>(hv)->simplex.SetStartingVariableValuesForNextSolve(
+      std::vector<double>(values, values + len));
+  return 0;
+}
+int oracle_lp_set_integrality_scale(void* hv, int32_t col, double scale) {
+  static_cast<OracleHandle*>(hv)->simplex.SetIntegralityScale(col, scale);
+  return 0;
+}
+int oracle_lp_objective_limit_reached(void* hv, int32_t* reached) {
+  *reached = static_cast<OracleHandle*>(hv)->simplex.objective_limit_reached() ? 1 : 0;
+  return 0;
+}
+int oracle_lp_get_unit_row_left_inverse(void* hv, int32_t row, double* values,
+                                        int32_t* non_zeros, int32_t* num_non_zeros) {
+  auto* h = static_cast<OracleHandle*>(hv);
+  const oracle::ScatteredVector& v = h->simplex.GetUnitRowLeftInverse(row);
+  for (int r = 0; r < h->lp.m; ++r) values[r] = v.values[r];
+  if (num_non_zeros != nullptr) *num_non_zeros = static_cast<int32_t>(v.non_zeros.size());
+  if (non_zeros != nullptr) {
+    for (size_t k = 0; k < v.non_zeros.size(); ++k) non_zeros[k] = v.non_zeros[k];
+  }
+  return 0;
+}
+int oracle_lp_compute_dictionary(void* hv, const double* column_scales, int32_t scales_len,
+                                 int64_t* nnz) {
+  auto* h = static_cast<OracleHandle*>(hv);
+  std::vector<double> scales;
+  if (column_scales != nullptr) scales.assign(column_scales, column_scales + scales_len);
+  h->simplex.ComputeDictionary(column_scales != nullptr ? &scales : nullptr, &h->dictionary);
+  int64_t total = 0;
+  for (const auto& r : h->dictionary) total += static_cast<int64_t>(r.size());
+  *nnz = total;
+  return 0;
+}
+int oracle_lp_get_dictionary(void* hv, int64_t* row_starts, int32_t* cols, double* values) {
+  auto* h = static_cast<OracleHandle*>(hv);
+  int64_t k = 0;
+  for (int r = 0; r < h->lp.m; ++r) {
+    row_starts[r] = k;
+    for (const auto& e : h->dictionary[r]) {
+      cols[k] = e.first;
+      values[k] = e.second;
+      ++k;
+    }
+  }
+  row_starts[h->lp.m] = k;
   return 0;
 }
 int oracle_lp_record_iteration_times(void* hv, int32_t enable) {

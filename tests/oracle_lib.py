@@ -50,6 +50,13 @@ def lib():
                                                    vp, ctypes.c_int32,
                                                    ctypes.POINTER(abi.MiLpResult)]
         L.oracle_lp_get_iteration_times.restype = ctypes.c_int64
+        L.oracle_lp_notify_matrix_changed.argtypes = [vp]
+        L.oracle_lp_set_starting_variable_values.argtypes = [vp, vp, ctypes.c_int32]
+        L.oracle_lp_set_integrality_scale.argtypes = [vp, ctypes.c_int32, ctypes.c_double]
+        L.oracle_lp_objective_limit_reached.argtypes = [vp, vp]
+        L.oracle_lp_get_unit_row_left_inverse.argtypes = [vp, ctypes.c_int32, vp, vp, vp]
+        L.oracle_lp_compute_dictionary.argtypes = [vp, vp, ctypes.c_int32, vp]
+        L.oracle_lp_get_dictionary.argtypes = [vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -150,6 +157,48 @@ class OracleLp:
 
     def dual_ray(self):
         return self._get("oracle_lp_get_dual_ray", self.lp.m, np.float64)
+
+    def _call(self, name, *args):
+        getattr(self._L, "oracle_lp_" + name)(self.h, *args)
+
+    # --- CP-SAT boundary (include/mi_lp.h) ---------------------------------
+    def notify_matrix_changed(self):
+        self._call("notify_matrix_changed")
+
+    def set_starting_variable_values(self, values):
+        self._start_values = np.ascontiguousarray(values, dtype=np.float64)
+        self._call("set_starting_variable_values", _p(self._start_values),
+                   len(self._start_values))
+
+    def set_integrality_scale(self, col, scale):
+        self._call("set_integrality_scale", int(col), ctypes.c_double(scale))
+
+    def objective_limit_reached(self):
+        r = ctypes.c_int32()
+        self._call("objective_limit_reached", ctypes.byref(r))
+        return bool(r.value)
+
+    def unit_row_left_inverse(self, row):
+        """(dense values[m], non-zero rows) of e_row^T B^-1."""
+        vals = np.zeros(self.lp.m, np.float64)
+        nz = np.zeros(self.lp.m, np.int32)
+        cnt = ctypes.c_int32()
+        self._call("get_unit_row_left_inverse", int(row), _p(vals), _p(nz), ctypes.byref(cnt))
+        return vals, nz[:cnt.value].copy()
+
+    def dictionary(self, column_scales=None):
+        """B^-1 A as (row_starts[m+1], cols, values), rows in basis order."""
+        nnz = ctypes.c_int64()
+        if column_scales is None:
+            self._call("compute_dictionary", None, 0, ctypes.byref(nnz))
+        else:
+            sc = np.ascontiguousarray(column_scales, dtype=np.float64)
+            self._call("compute_dictionary", _p(sc), len(sc), ctypes.byref(nnz))
+        starts = np.zeros(self.lp.m + 1, np.int64)
+        cols = np.zeros(max(1, nnz.value), np.int32)
+        vals = np.zeros(max(1, nnz.value), np.float64)
+        self._call("get_dictionary", _p(starts), _p(cols), _p(vals))
+        return starts, cols[:nnz.value], vals[:nnz.value]
 
 
 def batch_solve_bounds(workers, lbs, ubs, warm_state=None):

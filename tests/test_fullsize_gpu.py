@@ -1,0 +1,63 @@
+"""Parity at the benchmark's own sizes (BASELINE.json configs 2, 3 and 5).
+
+The engine and the CPU oracle run the same LP with the same iteration cap;
+at the cap everything the drop-in contract names must agree bit for bit
+(status, iteration count, basis, statuses, primal / dual / reduced-cost
+values). The windows cover the iterations bench.py times:
+  * config 5 (100k x 1M, dual simplex): up to iteration 20 600, past the
+    start of the timed window (20 000 + warm-up), with the device U solves
+    and the dual device mode on (their default at this size);
+  * config 2 (10k x 50k dense, primal simplex): the first 40 iterations
+    (the oracle needs ~0.5 s per iteration here);
+  * config 3: eleven members of the Netlib-shaped suite solved to the end,
+    the largest included.
+"""
+import pytest
+
+from mi_glop import abi, engine
+
+import lp_gen
+import netlib_suite
+import parity_util
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20261015
+
+
+def _handle(params):
+    return engine.LpHandle(params)
+
+
+def test_config5_window_parity():
+    lp = lp_gen.sparse_c5_lp(100000, 1000000, 10, SEED)
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=20600)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    assert rg.iterations == 20600
+    parity_util.compare(o, ro, g, rg, lp)
+    st = g.kernel_stats()
+    assert st["tri_solve"]["launches"] > 0, "the device U solve did not run at config-5 size"
+    assert st["dual_ratio"]["launches"] > 0, "the dual device mode did not run"
+
+
+def test_config2_window_parity():
+    lp = lp_gen.dense_box_lp(10000, 50000, SEED)
+    p = abi.default_params(max_number_of_iterations=40)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    assert rg.iterations == 40
+    parity_util.compare(o, ro, g, rg, lp)
+    assert g.kernel_stats()["pricing"]["launches"] > 0
+
+
+def _suite_members():
+    lps = netlib_suite.suite(max_rows=1000)  # bench.py's config-3 suite
+    picks = sorted(set(list(range(0, len(lps), 9)) + [len(lps) - 1]))
+    return [(i, lps[i]) for i in picks]
+
+
+@pytest.mark.parametrize("member", _suite_members(), ids=lambda m: f"lp{m[0]}_{m[1].m}x{m[1].n}")
+def test_config3_suite_parity(member):
+    _, lp = member
+    o, ro, g, rg = parity_util.solve_both(lp, abi.default_params(), _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    assert ro.problem_status == abi.OPTIMAL
