@@ -14,6 +14,10 @@
 #include "../../../include/mi_lp.h"
 #include "device_solver.h"
 
+namespace milp_kernels {
+struct TriSolveArgs;
+}
+
 namespace milp {
 
 class CompactSparseMatrix;
@@ -152,6 +156,11 @@ class DeviceLp : public DeviceSolver {
   void Check(int err, const char* what);
   void BuildTriSchedule(const TriangularMatrix& t, uint64_t key);
   void TriReserve(int which, size_t bytes);
+  milp_kernels::TriSolveArgs TriArgs() const;
+  void TriCopyIn();
+  void TriCopyOut();
+  void EnqueueTriKernels(const milp_kernels::TriSolveArgs& a);
+  void CaptureTriGraph();
   void FreeTriBuffers();
 
   int device_ = -1;
@@ -338,13 +347,14 @@ class DeviceLp : public DeviceSolver {
   int tri_levels_ = 0;
   std::vector<int32_t> tri_level_width_;
   std::vector<int> tri_segments_;  // tri_transpose_lower launch plan
-  int tri_wide_level_ = 6144;      // MILP_TRI_WIDE: wider levels run over the chip
+  int tri_wide_level_ = 600;       // MILP_TRI_WIDE: wider levels run over the chip
   int tri_debug_left_ = 0;
   uint64_t* d_tri_clock_ = nullptr;
   // Device buffers of the schedule (staged in this order) and of the values.
   enum TriBuf {
     kTriLevels, kTriRecRow, kTriRecN, kTriRecEntry, kTriRecValue, kTriDiag, kTriOvfPos,
-    kTriOvfValue, kTriPosRow, kTriNumStaged, kTriX = kTriNumStaged, kTriY, kTriNumBuffers
+    kTriOvfValue, kTriPosRow, kTriNumStaged, kTriX = kTriNumStaged, kTriY, kTriTop,
+    kTriNumBuffers
   };
   struct TriBuffer {
     void* ptr = nullptr;
@@ -352,6 +362,9 @@ class DeviceLp : public DeviceSolver {
   };
   TriBuffer tri_buf_[kTriNumBuffers];
   int tri_pos_ = 0;
+  int* h_tri_top_ = nullptr;        // pinned: the solve's top row
+  void* tri_graph_exec_ = nullptr;  // hipGraphExec_t of one solve, per factorization
+  bool tri_graph_ready_ = false;
   size_t h_tri_x_elems_ = 0;
   double* h_tri_x_ = nullptr;  // pinned staging, tri_rows_
   void* h_tri_stage_ = nullptr;  // pinned staging of the schedule upload

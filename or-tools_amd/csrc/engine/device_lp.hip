@@ -3,7 +3,9 @@
 #include "host_pool.h"
 
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <chrono>
 #include <cstdlib>
@@ -265,10 +267,10 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   Check(hipMemsetAsync(d_row_tag_, 0, std::max(1, m_) * sizeof(uint32_t), S(stream_)), "memset");
   row_tag_ = 0;
   Check(hipMemsetAsync(d_coeff_, 0, n_total_ * sizeof(double), S(stream_)), "memset");
-  // hipcub temp storage for the flag compaction.
+  // rocPRIM temp storage for the flag compaction.
   cub_temp_bytes_ = 0;
-  Check(hipcub::DeviceSelect::Flagged(nullptr, cub_temp_bytes_,
-                                      hipcub::CountingInputIterator<int32_t>(0), d_flags_,
+  Check(rocprim::select(nullptr, cub_temp_bytes_,
+                                      rocprim::counting_iterator<int32_t>(0), d_flags_,
                                       d_list_, d_count_, n_total_, S(stream_)),
         "cub sizing");
   d_cub_temp_ = Alloc<uint8_t>(cub_temp_bytes_);
@@ -481,8 +483,8 @@ void DeviceLp::Compact(int n) {
     mapped_result_ = true;
   } else {
     size_t bytes = cub_temp_bytes_;
-    Check(hipcub::DeviceSelect::Flagged(d_cub_temp_, bytes,
-                                        hipcub::CountingInputIterator<int32_t>(0), d_flags_,
+    Check(rocprim::select(d_cub_temp_, bytes,
+                                        rocprim::counting_iterator<int32_t>(0), d_flags_,
                                         d_list_, d_count_, n, S(stream_)),
           "cub flagged");
     Check(milp_launch::gather_counted(d_list_, d_count_, n, d_coeff_, d_out_list_, S(stream_)),
@@ -1044,7 +1046,7 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
     d_keys_out_ = Alloc<unsigned long long>(n_total_);
     d_sorted_slots_ = Alloc<int32_t>(n_total_);
     sort_temp_bytes_ = 0;
-    Check(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_temp_bytes_, d_keys_in_, d_keys_out_,
+    Check(rocprim::radix_sort_pairs(nullptr, sort_temp_bytes_, d_keys_in_, d_keys_out_,
                                              d_slots_, d_sorted_slots_, n_total_, 0, 64,
                                              S(stream_)),
           "radix sizing");
@@ -1135,8 +1137,8 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
   Check(milp_launch::dual_ratio_flags(a, S(stream_)), "dual ratio flags");
   auto select = [&]() {
     size_t bytes = cub_temp_bytes_;
-    Check(hipcub::DeviceSelect::Flagged(d_cub_temp_, bytes,
-                                        hipcub::CountingInputIterator<int32_t>(0),
+    Check(rocprim::select(d_cub_temp_, bytes,
+                                        rocprim::counting_iterator<int32_t>(0),
                                         d_slot_flags_, d_slots_, d_num_slots_, n_total_,
                                         S(stream_)),
           "cub flagged");
@@ -1149,7 +1151,7 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
   if (k1 > tighten_min_candidates_) {
     Check(milp_launch::dual_ratio_keys(a, d_slots_, k1, d_keys_in_, S(stream_)), "keys");
     size_t bytes = sort_temp_bytes_;
-    Check(hipcub::DeviceRadixSort::SortPairs(d_sort_temp_, bytes, d_keys_in_, d_keys_out_,
+    Check(rocprim::radix_sort_pairs(d_sort_temp_, bytes, d_keys_in_, d_keys_out_,
                                              d_slots_, d_sorted_slots_, k1, 0, 64, S(stream_)),
           "radix sort");
     Check(milp_launch::dual_flip_walk(a, d_sorted_slots_, k1, d_best2_, S(stream_)), "walk");

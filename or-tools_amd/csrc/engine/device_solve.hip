@@ -58,6 +58,13 @@ void DeviceLp::FreeTriBuffers() {
   }
   if (d_tri_clock_ != nullptr) (void)hipFree(d_tri_clock_);
   d_tri_clock_ = nullptr;
+  if (tri_graph_exec_ != nullptr) {
+    (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(tri_graph_exec_));
+  }
+  tri_graph_exec_ = nullptr;
+  tri_graph_ready_ = false;
+  if (h_tri_top_ != nullptr) (void)hipHostFree(h_tri_top_);
+  h_tri_top_ = nullptr;
   if (h_tri_x_ != nullptr) (void)hipHostFree(h_tri_x_);
   if (h_tri_stage_ != nullptr) (void)hipHostFree(h_tri_stage_);
   h_tri_x_ = nullptr;
@@ -235,9 +242,81 @@ void DeviceLp::BuildTriSchedule(const TriangularMatrix& t, uint64_t key) {
     Check(hipHostMalloc(reinterpret_cast<void**>(&h_tri_x_), h_tri_x_elems_ * sizeof(double)),
           "pin");
   }
+  TriReserve(kTriTop, 16);
+  if (h_tri_top_ == nullptr) {
+    Check(hipHostMalloc(reinterpret_cast<void**>(&h_tri_top_), 64), "pin");
+  }
   // The staging buffer is reused by the next build: wait for the copies.
   Check(hipStreamSynchronize(Stream(stream_)), "sync");
   tri_ok_ = true;
+  tri_graph_ready_ = false;  // captured at the first solve of this factorization
+}
+
+milp_kernels::TriSolveArgs DeviceLp::TriArgs() const {
+  milp_kernels::TriSolveArgs a;
+  a.level_start = static_cast<const int32_t*>(tri_buf_[kTriLevels].ptr);
+  a.rec_row = static_cast<const int32_t*>(tri_buf_[kTriRecRow].ptr);
+  a.rec_n = static_cast<const int32_t*>(tri_buf_[kTriRecN].ptr);
+  a.rec_entry = static_cast<const int4*>(tri_buf_[kTriRecEntry].ptr);
+  a.rec_value = static_cast<const double2*>(tri_buf_[kTriRecValue].ptr);
+  a.diag = tri_ones_ ? nullptr : static_cast<const double*>(tri_buf_[kTriDiag].ptr);
+  a.ovf_pos = static_cast<const int32_t*>(tri_buf_[kTriOvfPos].ptr);
+  a.ovf_value = static_cast<const double*>(tri_buf_[kTriOvfValue].ptr);
+  a.pos_row = static_cast<const int32_t*>(tri_buf_[kTriPosRow].ptr);
+  a.x = static_cast<double*>(tri_buf_[kTriX].ptr);
+  a.y = static_cast<double*>(tri_buf_[kTriY].ptr);
+  a.top = static_cast<const int*>(tri_buf_[kTriTop].ptr);
+  a.num_work = tri_work_;
+  a.num_pos = tri_pos_;
+  a.num_levels = tri_levels_;
+  a.clock = nullptr;
+  return a;
+}
+
+// One solve = copy in (x[fni..nc), top), the launches of the segment plan,
+// copy out (x[fni..nc)). Without debugging the launches are captured once per
+// factorization into a HIP graph and replayed with one launch: the plan has
+// tens of kernels, whose individual launches would cost more host time than
+// their GPU time.
+void DeviceLp::TriCopyIn() {
+  const int fni = tri_first_col_;
+  const size_t in = size_t(tri_rows_ - fni);
+  double* d_x = static_cast<double*>(tri_buf_[kTriX].ptr);
+  Upload(d_x + fni, h_tri_x_ + fni, in * sizeof(double));
+  Upload(tri_buf_[kTriTop].ptr, h_tri_top_, sizeof(int));
+}
+
+void DeviceLp::TriCopyOut() {
+  const int fni = tri_first_col_;
+  const size_t in = size_t(tri_rows_ - fni);
+  double* d_x = static_cast<double*>(tri_buf_[kTriX].ptr);
+  Check(hipMemcpyAsync(h_tri_x_ + fni, d_x + fni, in * sizeof(double), hipMemcpyDeviceToHost,
+                       Stream(stream_)),
+        "D2H");
+}
+
+void DeviceLp::EnqueueTriKernels(const milp_kernels::TriSolveArgs& a) {
+  Check(milp_launch::tri_transpose_lower(a, tri_segments_.data(),
+                                         static_cast<int>(tri_segments_.size() / 2),
+                                         Stream(stream_)),
+        "tri_transpose_lower");
+}
+
+void DeviceLp::CaptureTriGraph() {
+  if (tri_graph_exec_ != nullptr) {
+    (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(tri_graph_exec_));
+    tri_graph_exec_ = nullptr;
+  }
+  hipGraph_t graph = nullptr;
+  Check(hipStreamBeginCapture(Stream(stream_), hipStreamCaptureModeThreadLocal), "capture");
+  EnqueueTriKernels(TriArgs());
+  Check(hipStreamEndCapture(Stream(stream_), &graph), "capture end");
+  hipGraphExec_t exec = nullptr;
+  const hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  Check(e, "graph instantiate");
+  tri_graph_exec_ = exec;
+  tri_graph_ready_ = true;
 }
 
 bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
@@ -256,45 +335,10 @@ bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
   while (top >= fni && xv[top] == 0.0) --top;
   if (top < fni) return true;
   if (tri_rows_upto_[top + 1] - tri_rows_upto_[fni] == 0) return true;  // identity part only
-  // Outputs c >= fni read rows > c only: x[fni..nc) in, x[fni..top] out.
+  // Outputs c >= fni read rows > c only: x[fni..nc) in and out.
   const size_t in = size_t(nc - fni);
-  double* d_x = static_cast<double*>(tri_buf_[kTriX].ptr);
   CopyHost(h_tri_x_ + fni, xv + fni, in * sizeof(double));
-  Upload(d_x + fni, h_tri_x_ + fni, in * sizeof(double));
-  milp_kernels::TriSolveArgs a;
-  a.level_start = static_cast<const int32_t*>(tri_buf_[kTriLevels].ptr);
-  a.rec_row = static_cast<const int32_t*>(tri_buf_[kTriRecRow].ptr);
-  a.rec_n = static_cast<const int32_t*>(tri_buf_[kTriRecN].ptr);
-  a.rec_entry = static_cast<const int4*>(tri_buf_[kTriRecEntry].ptr);
-  a.rec_value = static_cast<const double2*>(tri_buf_[kTriRecValue].ptr);
-  a.diag = tri_ones_ ? nullptr : static_cast<const double*>(tri_buf_[kTriDiag].ptr);
-  a.ovf_pos = static_cast<const int32_t*>(tri_buf_[kTriOvfPos].ptr);
-  a.ovf_value = static_cast<const double*>(tri_buf_[kTriOvfValue].ptr);
-  a.pos_row = static_cast<const int32_t*>(tri_buf_[kTriPosRow].ptr);
-  a.x = d_x;
-  a.y = static_cast<double*>(tri_buf_[kTriY].ptr);
-  a.num_work = tri_work_;
-  a.num_pos = tri_pos_;
-  a.num_levels = tri_levels_;
-  a.top = top;
-  a.clock = nullptr;
-  // MILP_TRI_DEBUG=k: per-level wall clock of the first k solves after each
-  // schedule build, printed to stderr with the level widths.
-  const bool debug = tri_debug_left_ > 0;
-  if (debug) {
-    if (d_tri_clock_ == nullptr) {
-      Check(hipMalloc(reinterpret_cast<void**>(&d_tri_clock_), 65536 * sizeof(uint64_t)),
-            "hipMalloc");
-      Check(hipMemsetAsync(d_tri_clock_, 0, 65536 * sizeof(uint64_t), Stream(stream_)),
-            "memset");
-    }
-    if (tri_levels_ + 1 < 65536) a.clock = d_tri_clock_;
-  }
-  BeginKernel(MI_K_TRI_SOLVE);
-  Check(milp_launch::tri_transpose_lower(a, tri_segments_.data(),
-                                         static_cast<int>(tri_segments_.size() / 2),
-                                         Stream(stream_)),
-        "tri_transpose_lower");
+  *h_tri_top_ = top;
   const double rows = tri_rows_upto_[top + 1] - tri_rows_upto_[fni];
   const double entries =
       static_cast<double>(tri_entries_upto_[top + 1] - tri_entries_upto_[fni]);
@@ -302,13 +346,25 @@ bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
   // (16 B), the diagonal (8 B) unless unit; per entry: position and value
   // (12 B) and the value it reads (8 B). The permutes in and out: 8 B in, 8 B
   // out and the 4-B row index per position, both ways.
-  EndKernel(MI_K_TRI_SOLVE, rows * (24.0 + (tri_ones_ ? 0.0 : 8.0)) + entries * 20.0 +
-                                double(tri_pos_) * 20.0 + rows * 20.0);
-  const size_t out = size_t(top - fni + 1);
-  if (a.clock != nullptr) {
-    // Single-CU segments only (a wide level leaves its slot untouched: 0).
-    --tri_debug_left_;
+  const double bytes = rows * (24.0 + (tri_ones_ ? 0.0 : 8.0)) + entries * 20.0 +
+                       double(tri_pos_) * 20.0 + rows * 20.0;
+  if (tri_debug_left_ > 0) {
+    // MILP_TRI_DEBUG=k: per-level wall clock of the first k solves after each
+    // schedule build (single-CU segments), printed with the level widths.
+    milp_kernels::TriSolveArgs a = TriArgs();
+    if (d_tri_clock_ == nullptr) {
+      Check(hipMalloc(reinterpret_cast<void**>(&d_tri_clock_), 65536 * sizeof(uint64_t)),
+            "hipMalloc");
+    }
+    Check(hipMemsetAsync(d_tri_clock_, 0, 65536 * sizeof(uint64_t), Stream(stream_)), "memset");
+    if (tri_levels_ + 1 < 65536) a.clock = d_tri_clock_;
+    TriCopyIn();
+    BeginKernel(MI_K_TRI_SOLVE);
+    EnqueueTriKernels(a);
+    EndKernel(MI_K_TRI_SOLVE, bytes);
+    TriCopyOut();
     Synchronize();
+    --tri_debug_left_;
     std::vector<uint64_t> clk(tri_levels_ + 1);
     Check(hipMemcpy(clk.data(), d_tri_clock_, clk.size() * sizeof(uint64_t),
                     hipMemcpyDeviceToHost), "D2H");
@@ -320,10 +376,17 @@ bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
                    tri_level_width_[l]);
     }
     std::fprintf(stderr, "\n");
-    Check(hipMemsetAsync(d_tri_clock_, 0, 65536 * sizeof(uint64_t), Stream(stream_)), "memset");
+  } else {
+    if (!tri_graph_ready_) CaptureTriGraph();
+    TriCopyIn();
+    BeginKernel(MI_K_TRI_SOLVE);  // events around the graph: the kernels only
+    Check(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(tri_graph_exec_), Stream(stream_)),
+          "graph launch");
+    EndKernel(MI_K_TRI_SOLVE, bytes);
+    TriCopyOut();
+    Synchronize();
   }
-  Download(h_tri_x_ + fni, d_x + fni, out * sizeof(double));
-  CopyHost(xv + fni, h_tri_x_ + fni, out * sizeof(double));
+  CopyHost(xv + fni, h_tri_x_ + fni, size_t(top - fni + 1) * sizeof(double));
   return true;
 }
 

@@ -264,7 +264,7 @@ struct TriSolveArgs {
   int num_work;
   int num_pos;
   int num_levels;
-  int top;                     // rows above it are not computed (host: last non-zero)
+  const int* top;              // rows above *top are not computed (host: last non-zero)
   uint64_t* clock;             // debug (MILP_TRI_DEBUG): wall clock after each level, or null
 };
 }  // namespace milp_kernels

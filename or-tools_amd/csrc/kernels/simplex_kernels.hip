@@ -335,7 +335,7 @@ __global__ void gather_counted_kernel(const int32_t* list, const int* count, con
 // Update-row compaction for small N in one workgroup: thread t owns a
 // contiguous slice of the flags, a block-wide exclusive scan of the slice
 // counts gives each thread its output offset, so the list comes out in
-// ascending position order, as hipcub's select would produce it.
+// ascending position order, as rocprim::select would produce it.
 constexpr int kCompactThreads = 1024;
 __global__ __launch_bounds__(kCompactThreads) void compact_small_kernel(
     const uint8_t* flags, int n, const double* coeff, int32_t* list, double* vals, int* count,

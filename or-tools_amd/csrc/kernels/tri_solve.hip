@@ -42,17 +42,18 @@ __device__ __forceinline__ double load_final(const double* y, int k) {
 
 // The structure of one listed output.
 struct TriRec {
-  int row;  // a.top + 1 when the position is empty
+  int row;  // top + 1 when the position is empty
   int n;
   int4 e;   // entry positions (n <= 4); e.x = overflow start when n > 4
   double v[4];
   double d;
 };
 
-__device__ __forceinline__ void tri_load(const TriSolveArgs& a, int k, int le, TriRec* r) {
+__device__ __forceinline__ void tri_load(const TriSolveArgs& a, int k, int le, int top,
+                                         TriRec* r) {
   const bool in = k < le;
   const int kk = in ? k : 0;  // a valid address for an empty slot
-  r->row = in ? a.rec_row[kk] : a.top + 1;
+  r->row = in ? a.rec_row[kk] : top + 1;
   r->n = a.rec_n[kk];
   r->e = a.rec_entry[kk];
   const double2 v01 = a.rec_value[2 * kk];
@@ -91,9 +92,9 @@ __device__ __forceinline__ double subtract_overflow(const TriSolveArgs& a, const
   return sum;
 }
 
-__device__ __forceinline__ void tri_compute(const TriSolveArgs& a, double* y, int k,
+__device__ __forceinline__ void tri_compute(const TriSolveArgs& a, double* y, int k, int top,
                                             const TriRec& r) {
-  if (r.row > a.top) return;
+  if (r.row > top) return;
   double sum = y[k];
   if (r.n <= 4) {
     const int n = r.n;
@@ -124,23 +125,25 @@ __global__ __launch_bounds__(256) void tri_gather_kernel(TriSolveArgs a) {
 
 // x[row(k)] = y[k] for the computed outputs.
 __global__ __launch_bounds__(256) void tri_scatter_kernel(TriSolveArgs a) {
+  const int top = *a.top;
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.num_work;
        k += gridDim.x * blockDim.x) {
     const int row = a.rec_row[k];
-    if (row <= a.top) a.x[row] = a.y[k];
+    if (row <= top) a.x[row] = a.y[k];
   }
 }
 
 // One wide level over the whole chip; kernel boundaries order it with the
 // other levels.
 __global__ __launch_bounds__(256) void tri_level_grid_kernel(TriSolveArgs a, int level) {
+  const int top = *a.top;
   const int lb = a.level_start[level];
   const int le = a.level_start[level + 1];
   for (int k = lb + blockIdx.x * blockDim.x + threadIdx.x; k < le;
        k += gridDim.x * blockDim.x) {
     TriRec r;
-    tri_load(a, k, le, &r);
-    tri_compute(a, a.y, k, r);
+    tri_load(a, k, le, top, &r);
+    tri_compute(a, a.y, k, top, r);
   }
 }
 
@@ -153,13 +156,16 @@ __global__ __launch_bounds__(kTriThreads) void tri_levels_cu_kernel(TriSolveArgs
                                                                     int level_end) {
   double* y = a.y;
   const int tid = threadIdx.x;
+  const int top = *a.top;
   if (a.clock != nullptr && tid == 0) a.clock[level_begin] = wall_clock64();
   TriRec pre[kTriPrefetch];
   {
     const int lb = a.level_start[level_begin];
     const int le = a.level_start[level_begin + 1];
 #pragma unroll
-    for (int j = 0; j < kTriPrefetch; ++j) tri_load(a, lb + j * kTriThreads + tid, le, &pre[j]);
+    for (int j = 0; j < kTriPrefetch; ++j) {
+      tri_load(a, lb + j * kTriThreads + tid, le, top, &pre[j]);
+    }
   }
   for (int l = level_begin; l < level_end; ++l) {
     const int lb = a.level_start[l];
@@ -171,15 +177,19 @@ __global__ __launch_bounds__(kTriThreads) void tri_levels_cu_kernel(TriSolveArgs
       const int nb = a.level_start[l + 1];
       const int ne = a.level_start[l + 2];
 #pragma unroll
-      for (int j = 0; j < kTriPrefetch; ++j) tri_load(a, nb + j * kTriThreads + tid, ne, &pre[j]);
+      for (int j = 0; j < kTriPrefetch; ++j) {
+        tri_load(a, nb + j * kTriThreads + tid, ne, top, &pre[j]);
+      }
     }
 #pragma unroll
-    for (int j = 0; j < kTriPrefetch; ++j) tri_compute(a, y, lb + j * kTriThreads + tid, cur[j]);
+    for (int j = 0; j < kTriPrefetch; ++j) {
+      tri_compute(a, y, lb + j * kTriThreads + tid, top, cur[j]);
+    }
     // Positions beyond the prefetched ones (levels wider than the prefetch).
     for (int k = lb + kTriPrefetch * kTriThreads + tid; k < le; k += kTriThreads) {
       TriRec r;
-      tri_load(a, k, le, &r);
-      tri_compute(a, y, k, r);
+      tri_load(a, k, le, top, &r);
+      tri_compute(a, y, k, top, r);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

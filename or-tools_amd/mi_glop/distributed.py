@@ -18,6 +18,27 @@ def shard(count, rank, world):
     return begin, begin + base + (1 if rank < extra else 0)
 
 
+def lpt_partition(costs, world):
+    """Longest-processing-time-first assignment of independent LPs to ranks
+    (SURVEY.md 8(e)): LPs in decreasing cost order, each to the rank with the
+    smallest load so far (ties: lowest rank). Deterministic, so every rank
+    computes the same partition without a collective. Returns one index list
+    per rank, each in increasing LP index order."""
+    loads = [0.0] * world
+    parts = [[] for _ in range(world)]
+    for i in sorted(range(len(costs)), key=lambda i: (-costs[i], i)):
+        r = min(range(world), key=lambda q: (loads[q], q))
+        loads[r] += costs[i]
+        parts[r].append(i)
+    return [sorted(p) for p in parts]
+
+
+def lp_cost(lp):
+    """LPT weight of one LP: non-zeros x rows (work per iteration x a
+    row-proportional iteration count)."""
+    return float(lp.nnz + lp.m) * float(lp.m)
+
+
 def best_bound(results, optimal_status=0):
     """Minimum objective over the children that reached OPTIMAL (inf if none)."""
     vals = [r.objective for r in results if r.problem_status == optimal_status]

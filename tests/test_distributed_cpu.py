@@ -67,6 +67,23 @@ def test_shard_partition():
             assert max(sizes) - min(sizes) <= 1
 
 
+def test_lpt_partition():
+    from mi_glop import distributed
+    costs = [5.0, 1.0, 7.0, 3.0, 3.0, 2.0, 9.0, 4.0]
+    for world in (1, 2, 3, 8):
+        parts = distributed.lpt_partition(costs, world)
+        assert sorted(i for p in parts for i in p) == list(range(len(costs)))
+        loads = [sum(costs[i] for i in p) for p in parts]
+        # LPT bound: makespan <= 4/3 of the optimum; the optimum >= both
+        # the average load and the largest job.
+        assert max(loads) <= 4.0 / 3.0 * max(sum(costs) / world, max(costs)) + 1e-9
+    assert distributed.lpt_partition(costs, 2) == [[1, 4, 6, 7], [0, 2, 3, 5]]  # 17 + 17
+    import netlib_suite
+    suite = netlib_suite.suite(max_rows=200)
+    parts = distributed.lpt_partition([distributed.lp_cost(lp) for lp in suite], 4)
+    assert sum(len(p) for p in parts) == len(suite)
+
+
 def test_bound_share_world2(tmp_path):
     from mi_glop import abi, distributed
     import oracle_lib

@@ -1,0 +1,150 @@
+"""MPSolver-shaped front end (mi_glop.linear_solver), config 1 plumbing.
+
+The models are the reference's own MPSolver examples with their stated
+answers: examples/tests/lp_test.cc:55-85 (34 at (6, 4)),
+glop/samples/simple_glop_program.cc (4), linear_solver/python/
+model_builder_test.py:49-135 (733.3333 - 5.5). The CPU part checks the
+model extraction (GLOPInterface::ExtractModel + LinearProgram::CleanUp)
+against the known-answer LPs and solves it with the oracle; the GPU part
+solves through the engine and checks the answers, the status maps of
+glop_utils.cc:18-125 and bit-equality with the oracle."""
+import math
+
+import numpy as np
+import pytest
+
+from mi_glop import abi, linear_solver
+
+import kat_lps
+import oracle_lib
+
+INF = math.inf
+
+
+def lp_test_model():
+    solver = linear_solver.Solver("LinearProgrammingExample",
+                                  linear_solver.GLOP_LINEAR_PROGRAMMING)
+    x = solver.MakeNumVar(0.0, INF, "x")
+    y = solver.MakeNumVar(0.0, INF, "y")
+    obj = solver.MutableObjective()
+    obj.SetCoefficient(x, 3)
+    obj.SetCoefficient(y, 4)
+    obj.SetMaximization()
+    c0 = solver.MakeRowConstraint(-INF, 14.0, "c0")
+    c0.SetCoefficient(x, 1)
+    c0.SetCoefficient(y, 2)
+    c1 = solver.MakeRowConstraint(0.0, INF, "c1")
+    c1.SetCoefficient(x, 3)
+    c1.SetCoefficient(y, -1)
+    c2 = solver.MakeRowConstraint(-INF, 2.0, "c2")
+    c2.SetCoefficient(x, 1)
+    c2.SetCoefficient(y, -1)
+    return solver, (x, y), (c0, c1, c2)
+
+
+def simple_glop_model():
+    solver = linear_solver.Solver.CreateSolver("GLOP")
+    x = solver.NumVar(0, 1, "x")
+    y = solver.NumVar(0, 2, "y")
+    ct = solver.Constraint(-solver.infinity(), 2, "ct")
+    ct.SetCoefficient(x, 1)
+    ct.SetCoefficient(y, 1)
+    solver.Objective().SetCoefficient(x, 3)
+    solver.Objective().SetCoefficient(y, 1)
+    solver.Objective().SetMaximization()
+    return solver, (x, y), (ct,)
+
+
+def model_builder_model():
+    solver = linear_solver.Solver.CreateSolver("glop")
+    xs = [solver.NumVar(1 if i == 0 else 0, INF, f"x{i + 1}") for i in range(3)]
+    rows = [([1, 1, 1], 100), ([10, 4, 5], 600), ([2, 2, 6], 300)]
+    cons = []
+    for coefs, ub in rows:
+        c = solver.Constraint(-INF, ub)
+        for v, a in zip(xs, coefs):
+            c.SetCoefficient(v, a)
+        cons.append(c)
+    solver.Maximize({xs[0]: 10, xs[1]: 6, xs[2]: 4})
+    solver.Objective().SetOffset(-5.5)
+    return solver, tuple(xs), tuple(cons)
+
+
+def _same_lp(a, b):
+    for f in ("col_starts", "row_idx", "vals", "col_lb", "col_ub", "row_lb", "row_ub", "obj"):
+        np.testing.assert_array_equal(np.asarray(getattr(a, f), float),
+                                      np.asarray(getattr(b, f), float), err_msg=f)
+    assert (a.m, a.n, a.maximize, a.obj_offset) == (b.m, b.n, b.maximize, b.obj_offset)
+
+
+@pytest.mark.parametrize("model,kat", [(lp_test_model, kat_lps.lp_test_cc),
+                                       (simple_glop_model, kat_lps.mutable_objective_lp),
+                                       (model_builder_model, kat_lps.model_builder_lp)])
+def test_extraction_matches_known_answer_lp(model, kat):
+    solver, _, _ = model()
+    lp = solver.to_linear_program()
+    ref, expect = kat()
+    _same_lp(lp, ref)
+    o = oracle_lib.OracleLp(abi.default_params())
+    o.load(lp)
+    r = o.solve()
+    assert r.problem_status == abi.OPTIMAL
+    assert abs(r.objective - expect["objective"]) <= 1e-6 * max(1.0, abs(expect["objective"]))
+
+
+def test_cleanup_merges_and_drops():
+    solver = linear_solver.Solver.CreateSolver("GLOP")
+    x = solver.NumVar(0, 1)
+    y = solver.NumVar(0, 1)
+    c = solver.Constraint(0, 1)
+    c.SetCoefficient(y, 2.0)
+    c.SetCoefficient(x, 0.0)   # explicit zero: dropped
+    c2 = solver.Constraint(0, 1)
+    c2.SetCoefficient(x, 1.0)
+    c2.SetCoefficient(x, 3.0)  # last write wins, as MPConstraint::SetCoefficient
+    lp = solver.to_linear_program()
+    assert list(lp.col_starts) == [0, 1, 2]
+    assert list(lp.row_idx) == [1, 0] and list(lp.vals) == [3.0, 2.0]
+    assert solver.CreateSolver("SCIP") is None
+    with pytest.raises(ValueError):
+        solver.IntVar(0, 1, "b")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,expect", [
+    (lp_test_model, dict(objective=34.0, primal=[6, 4])),
+    (simple_glop_model, dict(objective=4.0, primal=[1, 1])),
+    (model_builder_model, dict(objective=733.3333333333334 - 5.5,
+                               primal=[100.0 / 3, 200.0 / 3, 0.0]))])
+def test_solve_through_engine(model, expect):
+    solver, xs, cons = model()
+    assert solver.Solve() == linear_solver.Solver.OPTIMAL
+    assert abs(solver.Objective().Value() - expect["objective"]) <= 1e-6 * abs(expect["objective"])
+    np.testing.assert_allclose([v.solution_value() for v in xs], expect["primal"], atol=1e-7)
+    o = oracle_lib.OracleLp(abi.default_params())
+    o.load(solver.to_linear_program())
+    o.solve()
+    np.testing.assert_array_equal([v.solution_value() for v in xs], o.primal())
+    np.testing.assert_array_equal([v.reduced_cost() for v in xs], o.reduced_costs())
+    np.testing.assert_array_equal([c.dual_value() for c in cons], o.duals())
+    ov, oc = o.statuses()
+    bmap = linear_solver.Solver._BASIS
+    assert [v.basis_status() for v in xs] == [bmap[int(s)] for s in ov]
+    assert [c.basis_status() for c in cons] == [bmap[int(s)] for s in oc]
+    assert solver.iterations() >= 0
+
+
+@pytest.mark.gpu
+def test_infeasible_and_unbounded_status_maps():
+    s = linear_solver.Solver.CreateSolver("GLOP")
+    x = s.NumVar(0, 1, "x")
+    c = s.Constraint(2, INF)
+    c.SetCoefficient(x, 1)
+    assert s.Solve() == linear_solver.Solver.INFEASIBLE
+    s2 = linear_solver.Solver.CreateSolver("GLOP")
+    y = s2.NumVar(0, INF, "y")
+    s2.Objective().SetCoefficient(y, 1)
+    s2.Objective().SetMaximization()
+    c2 = s2.Constraint(0, INF)
+    c2.SetCoefficient(y, 1)
+    assert s2.Solve() == linear_solver.Solver.UNBOUNDED
