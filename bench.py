@@ -167,7 +167,10 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
 
 def run_c2(args, rank, world, local_rank, dist, barrier, sync):
     """Config 2: dense random LP 10k x 50k, primal simplex, Glop defaults.
-    Iterations c2_warmup..c2_warmup + c2_steps are timed (replicas per rank)."""
+    Iterations c2_warmup..c2_warmup + c2_steps are timed (replicas per rank),
+    then the solve runs on to c2_late and the same number of iterations is
+    timed again (late_window). The CPU oracle (0.5 s per iteration here) is
+    timed on the early window only."""
     lp = dense_box_lp(args.m, args.n, args.seed + rank)
     params = abi.default_params()  # Glop defaults: primal simplex, steepest edge
     h = engine.LpHandle(params, device=local_rank)
@@ -188,12 +191,31 @@ def run_c2(args, rank, world, local_rank, dist, barrier, sync):
     stats = h.kernel_stats()
     done = it - args.c2_warmup
     total_done = distributed.sum_over_ranks(done, dist, "cuda")
+    # A late window of the same length: the host LU solves grow as dense
+    # columns enter the basis, so the early rate overstates the solve.
+    late = None
+    if args.c2_late > args.c2_warmup + args.c2_steps and not finished:
+        t = time.perf_counter()
+        fin_l, it_l = h.run_until(args.c2_late)
+        reach_s = time.perf_counter() - t
+        if not fin_l:
+            sync()
+            t0l = time.perf_counter()
+            fin_l, it_l2 = h.run_until(it_l + args.c2_steps)
+            sync()
+            el = distributed.max_over_ranks(time.perf_counter() - t0l, dist, "cuda")
+            late = {"timed_iterations": [it_l, it_l2], "reached_in_s": round(reach_s, 2),
+                    "value": distributed.sum_over_ranks(it_l2 - it_l, dist, "cuda") / el
+                    if el > 0 else 0.0,
+                    "ms_per_step": 1000.0 * el / max(1, it_l2 - it_l)}
+            log(f"c2: late window {it_l}..{it_l2}: {late['value']:.1f} it/s")
     h.stop()
     h.finish()
     del h
     out = {
         "metric": "simplex iterations/sec", "unit": "iterations/s",
         "value": total_done / elapsed if elapsed > 0 else 0.0,
+        "late_window": late,
         "ms_per_step": 1000.0 * elapsed / max(1, done),
         "timed_iterations": [args.c2_warmup, args.c2_warmup + done],
         "finished_early": bool(finished), "setup_and_warmup_s": round(t_setup, 3),
@@ -361,6 +383,8 @@ def main():
     ap.add_argument("--n", type=int, default=50000, help="config-2 columns")
     ap.add_argument("--c2-steps", type=int, default=64)
     ap.add_argument("--c2-warmup", type=int, default=3)
+    ap.add_argument("--c2-late", type=int, default=1500,
+                    help="config-2 iteration where a second (late) window starts (0: none)")
     ap.add_argument("--cpu-iters", type=int, default=6)
     ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--traffic-json",

@@ -176,7 +176,9 @@ enum {
   MI_K_SINGLE_ROW = 7,  /* ComputeUpdatesForSingleRow (update_row.cc:261-280) */
   MI_K_DUAL_RATIO = 8,  /* dual ratio-test candidate filter (entering_variable.cc:37-130) */
   MI_K_READBACK = 9,    /* update-row list download / single-coefficient reads */
-  MI_K_COUNT = 10
+  MI_K_TRI_SOLVE_TAU = 10, /* the same dense U solve for the tau FTRAN on the
+                              factorization's worker thread (dual_edge_norms.cc:134-141) */
+  MI_K_COUNT = 11
 };
 
 void mi_glop_params_default(mi_glop_params* p);

@@ -7,6 +7,7 @@
 #define MILP_DEVICE_LP_H_
 
 #include <cstdint>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -16,6 +17,7 @@
 
 namespace milp_kernels {
 struct TriSolveArgs;
+struct ScanState;
 }
 
 namespace milp {
@@ -116,6 +118,21 @@ class DeviceLp : public DeviceSolver {
                       std::vector<uint8_t>* flags);
 
   // --- dense triangular solves of the LU (device_solve.hip) -------------
+  struct TriBuffer {  // a device buffer of the triangular-solve state
+    void* ptr = nullptr;
+    size_t bytes = 0;
+  };
+  struct TriContext {  // one solving thread's stream, values and graph
+    void* stream = nullptr;
+    TriBuffer x, y, top;         // rows, positions, the solve's top row
+    double* h_x = nullptr;       // pinned, mapped staging of x (+ the top row)
+    double* m_x = nullptr;       // its device-visible address
+    size_t h_x_elems = 0;
+    int* h_top = nullptr;        // pinned
+    void* graph_exec = nullptr;  // hipGraphExec_t of the launch plan
+    uint64_t graph_key = 0;      // the schedule it was captured for
+    void* ev[2] = {nullptr, nullptr};
+  };
   // TriangularMatrix::TransposeLowerSolve (sparse.cc:899-955) on one CU,
   // bit-identical. MILP_DEVICE_SOLVE=off|force|auto (auto: m >= 16384).
   bool TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
@@ -134,9 +151,10 @@ class DeviceLp : public DeviceSolver {
   void Upload(void* dst, const void* src, size_t bytes);
   void Download(void* dst, const void* src, size_t bytes);
   void BeginKernel(int id);
-  void EndKernel(int id, double bytes);
+  void EndKernel(int id, double bytes, bool count_launch = true);
   void* TakeEvent();
   void DrainTimings();
+  milp_kernels::ScanState NextScan();
   void Compact(int n);  // flags_ -> list_ (ascending) + coefficients, async
   void NextRowTag();
   void UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
@@ -154,13 +172,14 @@ class DeviceLp : public DeviceSolver {
   void LaunchColumnDots(int mode, const double* d_y, const double* d_c, double* d_out,
                         const double* d_y2 = nullptr, double* d_out2 = nullptr);
   void Check(int err, const char* what);
-  void BuildTriSchedule(const TriangularMatrix& t, uint64_t key);
-  void TriReserve(int which, size_t bytes);
-  milp_kernels::TriSolveArgs TriArgs() const;
-  void TriCopyIn();
-  void TriCopyOut();
-  void EnqueueTriKernels(const milp_kernels::TriSolveArgs& a);
-  void CaptureTriGraph();
+  void BuildTriSchedule(const TriangularMatrix& t, uint64_t key, void* stream);
+  void TriReserve(TriBuffer* b, size_t bytes);
+  void PrepareTriContext(int slot, int rows);
+  milp_kernels::TriSolveArgs TriArgs(const TriContext& c) const;
+  void TriCopyIn(const TriContext& c);
+  void TriCopyOut(const TriContext& c);
+  void EnqueueTriKernels(const milp_kernels::TriSolveArgs& a, void* stream);
+  void CaptureTriGraph(TriContext* c);
   void FreeTriBuffers();
 
   int device_ = -1;
@@ -227,12 +246,15 @@ class DeviceLp : public DeviceSolver {
   double* d_out_n_ = nullptr;    // per-column results
   double* d_out_list_ = nullptr; // per-list-slot results
   int32_t* d_cols_ = nullptr;    // arbitrary column list / filtered rows
-  double* d_rho_vals_ = nullptr; // filtered rho values
+  void* d_upd_in_ = nullptr;     // row-wise inputs: rows, multipliers, CSR offsets
+  void* h_upd_in_ = nullptr;     // pinned staging of d_upd_in_
   uint32_t* d_row_tag_ = nullptr; // filtered-row marks of the column-order row-wise kernel
   int32_t* d_row_pos_ = nullptr;
   uint32_t row_tag_ = 0;
-  void* d_cub_temp_ = nullptr;
-  size_t cub_temp_bytes_ = 0;
+  unsigned long long* d_scan_status_ = nullptr;  // ordered compactions (kernel_args.h)
+  unsigned int* d_scan_ticket_ = nullptr;
+  unsigned int scan_epoch_ = 0;
+  uint64_t dual_calls_ = 0;  // alternates the pass-1 bound slots
   double* d_out_n2_ = nullptr;   // w . a_j of the fused pricing pass
   int list_count_ = 0;
   uint64_t list_epoch_ = 0;
@@ -255,8 +277,6 @@ class DeviceLp : public DeviceSolver {
   // pinned staging
   int32_t* h_pin_i_ = nullptr;
   double* h_pin_d_ = nullptr;
-  int64_t* h_pin_off_ = nullptr;  // CSR row starts of the filtered rows (full-row kernel)
-  int64_t* d_row_offsets_ = nullptr;
   double* h_pin_d2_ = nullptr;
   double* h_pin_w_ = nullptr;
   int* h_pin_count_ = nullptr;
@@ -317,7 +337,11 @@ class DeviceLp : public DeviceSolver {
   int32_t* h_cand_col_ = nullptr;
   double* h_cand_coeff_ = nullptr;
   double* h_cand_rc_ = nullptr;
-  int* h_dual_counts_ = nullptr;  // [num candidates, list count]
+  int* h_dual_counts_ = nullptr;  // [num candidates, list count] (mapped)
+  int* m_dual_counts_ = nullptr;  // its device pointer
+  int32_t* m_cand_col_ = nullptr;  // device pointers of the mapped h_cand_*
+  double* m_cand_coeff_ = nullptr;
+  double* m_cand_rc_ = nullptr;
   int32_t* h_cb_cols_ = nullptr;  // column-bit changes (pinned, event-guarded)
   uint8_t* h_cb_bits_ = nullptr;
   void* ev_cb_ = nullptr;
@@ -349,24 +373,24 @@ class DeviceLp : public DeviceSolver {
   std::vector<int> tri_segments_;  // tri_transpose_lower launch plan
   int tri_wide_level_ = 600;       // MILP_TRI_WIDE: wider levels run over the chip
   int tri_debug_left_ = 0;
+  bool tri_graph_ = true;  // MILP_TRI_GRAPH
+  bool tri_tau_ = true;    // MILP_TRI_TAU
+  bool tri_mapped_ = true; // MILP_TRI_MAPPED: zero-copy staging inside the plan
+  bool tri_syncfree_ = true;  // MILP_TRI_SYNCFREE: readiness-driven single launch
+  int tri_max_entries_ = 0;   // schedule statistics (MILP_TRI_DEBUG)
+  int tri_rows_over_[3] = {0, 0, 0};
   uint64_t* d_tri_clock_ = nullptr;
-  // Device buffers of the schedule (staged in this order) and of the values.
+  // Device buffers of the schedule (staged in this order).
   enum TriBuf {
     kTriLevels, kTriRecRow, kTriRecN, kTriRecEntry, kTriRecValue, kTriDiag, kTriOvfPos,
-    kTriOvfValue, kTriPosRow, kTriNumStaged, kTriX = kTriNumStaged, kTriY, kTriTop,
-    kTriNumBuffers
+    kTriOvfValue, kTriPosRow, kTriNumStaged
   };
-  struct TriBuffer {
-    void* ptr = nullptr;
-    size_t bytes = 0;
-  };
-  TriBuffer tri_buf_[kTriNumBuffers];
+  TriBuffer tri_buf_[kTriNumStaged];
   int tri_pos_ = 0;
-  int* h_tri_top_ = nullptr;        // pinned: the solve's top row
-  void* tri_graph_exec_ = nullptr;  // hipGraphExec_t of one solve, per factorization
-  bool tri_graph_ready_ = false;
-  size_t h_tri_x_elems_ = 0;
-  double* h_tri_x_ = nullptr;  // pinned staging, tri_rows_
+  // Per solving thread: 0 = the solver's thread (the handle's stream),
+  // 1 = BasisFactorization's tau worker (its own stream).
+  TriContext tri_ctx_[2];
+  std::mutex tri_mu_;  // schedule (re)build
   void* h_tri_stage_ = nullptr;  // pinned staging of the schedule upload
   size_t tri_stage_bytes_ = 0;
   std::vector<int32_t> tri_rows_upto_;     // work rows with output row <= r

@@ -4,8 +4,6 @@
 
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_select.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <chrono>
 #include <cstdlib>
@@ -50,7 +48,7 @@ DeviceLp::~DeviceLp() {
   if (h_pin_d_) (void)hipHostFree(h_pin_d_);
   if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
   if (h_pin_w_) (void)hipHostFree(h_pin_w_);
-  if (h_pin_off_) (void)hipHostFree(h_pin_off_);
+  if (h_upd_in_) (void)hipHostFree(h_upd_in_);
   if (h_pin_count_) (void)hipHostFree(h_pin_count_);
   if (h_map_) (void)hipHostFree(h_map_);
   if (h_small_in_) (void)hipHostFree(h_small_in_);
@@ -121,6 +119,12 @@ void DeviceLp::Init(int device) {
   }
   if (const char* v = std::getenv("MILP_DEVICE_SOLVE_MIN_ROWS")) tri_min_rows_ = std::atoi(v);
   if (const char* v = std::getenv("MILP_TRI_WIDE")) tri_wide_level_ = std::atoi(v);
+  // MILP_TRI_GRAPH=0: launch the plan kernel by kernel instead of replaying
+  // a captured graph; MILP_TRI_TAU=0: the tau worker keeps the host loop.
+  if (const char* v = std::getenv("MILP_TRI_GRAPH")) tri_graph_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_TRI_TAU")) tri_tau_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_TRI_MAPPED")) tri_mapped_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_TRI_SYNCFREE")) tri_syncfree_ = std::atoi(v) != 0;
 }
 
 template <typename T>
@@ -192,9 +196,9 @@ void DeviceLp::BeginKernel(int /*id*/) {
   Check(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_open_), S(stream_)), "ev");
 }
 
-void DeviceLp::EndKernel(int id, double bytes) {
+void DeviceLp::EndKernel(int id, double bytes, bool count_launch) {
   Check(hipGetLastError(), "kernel launch");
-  stats_.launches[id] += 1;
+  if (count_launch) stats_.launches[id] += 1;
   stats_.algorithmic_bytes[id] += bytes;
   if (timing_ && ev_open_ != nullptr) {
     void* stop = TakeEvent();
@@ -260,31 +264,33 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   d_out_n2_ = Alloc<double>(n_total_);
   d_out_list_ = Alloc<double>(std::max(n_total_, m_));
   d_cols_ = Alloc<int32_t>(std::max(n_total_, m_));
-  d_rho_vals_ = Alloc<double>(m_);
-  d_row_offsets_ = Alloc<int64_t>(m_ + 1);
+  // Row-wise update-row inputs: rows, multipliers, CSR offsets (one upload).
+  const size_t upd_bytes = size_t(m_ + 2) * (sizeof(int32_t) + 2 * sizeof(double));
+  d_upd_in_ = Alloc<uint8_t>(upd_bytes);
   d_row_tag_ = Alloc<uint32_t>(m_);
   d_row_pos_ = Alloc<int32_t>(m_);
   Check(hipMemsetAsync(d_row_tag_, 0, std::max(1, m_) * sizeof(uint32_t), S(stream_)), "memset");
   row_tag_ = 0;
   Check(hipMemsetAsync(d_coeff_, 0, n_total_ * sizeof(double), S(stream_)), "memset");
-  // rocPRIM temp storage for the flag compaction.
-  cub_temp_bytes_ = 0;
-  Check(rocprim::select(nullptr, cub_temp_bytes_,
-                                      rocprim::counting_iterator<int32_t>(0), d_flags_,
-                                      d_list_, d_count_, n_total_, S(stream_)),
-        "cub sizing");
-  d_cub_temp_ = Alloc<uint8_t>(cub_temp_bytes_);
+  // Tile status words and tickets of the ordered compactions.
+  const int tiles = milp_launch::scan_tiles(n_total_);
+  d_scan_status_ = Alloc<unsigned long long>(tiles);
+  d_scan_ticket_ = Alloc<unsigned int>(2);
+  Check(hipMemsetAsync(d_scan_status_, 0, tiles * sizeof(unsigned long long), S(stream_)),
+        "memset");
+  Check(hipMemsetAsync(d_scan_ticket_, 0, 2 * sizeof(unsigned int), S(stream_)), "memset");
+  scan_epoch_ = 0;
   if (h_pin_i_) (void)hipHostFree(h_pin_i_);
   if (h_pin_d_) (void)hipHostFree(h_pin_d_);
   if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
   if (h_pin_w_) (void)hipHostFree(h_pin_w_);
-  if (h_pin_off_) (void)hipHostFree(h_pin_off_);
+  if (h_upd_in_) (void)hipHostFree(h_upd_in_);
+  Check(hipHostMalloc(&h_upd_in_, upd_bytes), "pin");
   const size_t big = std::max(n_total_, m_) + 1;
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_i_), big * sizeof(int32_t)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d_), big * sizeof(double)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_d2_), big * sizeof(double)), "pin");
   Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_w_), (m_ + 1) * sizeof(double)), "pin");
-  Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_off_), (m_ + 1) * sizeof(int64_t)), "pin");
   if (h_pin_count_ == nullptr) {
     Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_count_), sizeof(int)), "pin");
   }
@@ -294,7 +300,7 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   d_map_count_ = nullptr;
   d_map_list_ = nullptr;
   d_map_vals_ = nullptr;
-  if (n_total_ <= milp_launch::kSmallCompactMax) {
+  {
     const size_t list_off = 64;
     const size_t vals_off = (list_off + size_t(n_total_) * sizeof(int32_t) + 63) / 64 * 64;
     const size_t bytes = vals_off + size_t(n_total_) * sizeof(double);
@@ -482,14 +488,13 @@ void DeviceLp::Compact(int n) {
           "compact small");
     mapped_result_ = true;
   } else {
-    size_t bytes = cub_temp_bytes_;
-    Check(rocprim::select(d_cub_temp_, bytes,
-                                        rocprim::counting_iterator<int32_t>(0), d_flags_,
-                                        d_list_, d_count_, n, S(stream_)),
-          "cub flagged");
-    Check(milp_launch::gather_counted(d_list_, d_count_, n, d_coeff_, d_out_list_, S(stream_)),
-          "gather");
-    mapped_result_ = false;
+    // Ordered single-pass compaction over the chip, the list also into
+    // mapped host memory.
+    Check(milp_launch::compact_flags(d_flags_, n, d_coeff_, d_list_, d_out_list_, d_count_,
+                                     d_map_list_, d_map_vals_, d_map_count_, NextScan(),
+                                     S(stream_)),
+          "compact");
+    mapped_result_ = true;
   }
   list_count_ = -1;  // known after FetchUpdateRow
   ++list_epoch_;
@@ -600,16 +605,31 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
     return;
   }
   FlushRelevantMask();
-  std::memcpy(h_pin_i_, filtered_rows.data(), k * sizeof(int32_t));
-  for (int i = 0; i < k; ++i) h_pin_d_[i] = rho[filtered_rows[i]];
-  Upload(d_cols_, h_pin_i_, k * sizeof(int32_t));
-  Upload(d_rho_vals_, h_pin_d_, k * sizeof(double));
+  bool all_full = full_rows_enabled_ && k > 0;
+  for (int i = 0; i < k && all_full; ++i) all_full = h_row_full_[filtered_rows[i]] != 0;
+  // One upload: the rows, their multipliers and (full rows) their CSR offsets.
+  const size_t rho_off = (size_t(k) * sizeof(int32_t) + 7) / 8 * 8;
+  const size_t offs_off = rho_off + size_t(k) * sizeof(double);
+  char* hin = static_cast<char*>(h_upd_in_);
+  int32_t* h_rows = reinterpret_cast<int32_t*>(hin);
+  double* h_rho = reinterpret_cast<double*>(hin + rho_off);
+  int64_t* h_offs = reinterpret_cast<int64_t*>(hin + offs_off);
+  std::memcpy(h_rows, filtered_rows.data(), k * sizeof(int32_t));
+  for (int i = 0; i < k; ++i) h_rho[i] = rho[filtered_rows[i]];
+  if (all_full) {
+    for (int i = 0; i < k; ++i) h_offs[i] = h_t_starts_[filtered_rows[i]];
+  }
+  Upload(d_upd_in_, h_upd_in_, all_full ? offs_off + size_t(k) * sizeof(int64_t) : offs_off);
+  char* din = static_cast<char*>(d_upd_in_);
+  const int32_t* d_rows = reinterpret_cast<const int32_t*>(din);
+  const double* d_rho = reinterpret_cast<const double*>(din + rho_off);
+  const int64_t* d_offs = reinterpret_cast<const int64_t*>(din + offs_off);
   milp_kernels::RowWiseArgs a{};
   a.t_starts = d_t_starts_;
   a.t_cols = d_t_cols_;
   a.t_vals = d_t_vals_;
-  a.filtered_rows = d_cols_;
-  a.rho = d_rho_vals_;
+  a.filtered_rows = d_rows;
+  a.rho = d_rho;
   a.num_filtered = k;
   a.num_cols = n_total_;
   a.relevant = d_masks_[kRelevant];
@@ -619,20 +639,16 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
   a.algorithm = algorithm;
   const int id = algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW;
   BeginKernel(id);
-  bool all_full = full_rows_enabled_ && k > 0;
-  for (int i = 0; i < k && all_full; ++i) all_full = h_row_full_[filtered_rows[i]] != 0;
   if (all_full) {
     // Full rows: a thread per column reads each row's entry directly.
-    for (int i = 0; i < k; ++i) h_pin_off_[i] = h_t_starts_[filtered_rows[i]];
-    Upload(d_row_offsets_, h_pin_off_, k * sizeof(int64_t));
     NextRowTag();
-    Check(milp_launch::tag_rows(d_cols_, k, row_tag_, d_row_tag_, d_row_pos_, S(stream_)),
+    Check(milp_launch::tag_rows(d_rows, k, row_tag_, d_row_tag_, d_row_pos_, S(stream_)),
           "tag rows");
     milp_kernels::RowWiseFullArgs f{};
     f.t_starts = d_t_starts_;
     f.t_vals = d_t_vals_;
-    f.row_offsets = d_row_offsets_;
-    f.rho = d_rho_vals_;
+    f.row_offsets = d_offs;
+    f.rho = d_rho;
     f.num_filtered = k;
     f.num_structural = num_structural_;
     f.num_cols = n_total_;
@@ -657,7 +673,7 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
     // Many rows: one thread per column gathers its filtered entries from the
     // CSC copy (same arithmetic, same order).
     NextRowTag();
-    Check(milp_launch::tag_rows(d_cols_, k, row_tag_, d_row_tag_, d_row_pos_, S(stream_)),
+    Check(milp_launch::tag_rows(d_rows, k, row_tag_, d_row_tag_, d_row_pos_, S(stream_)),
           "tag rows");
     milp_kernels::RowWiseColArgs c{};
     c.starts = d_starts_;
@@ -666,7 +682,7 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
     c.row_tag = d_row_tag_;
     c.row_pos = d_row_pos_;
     c.tag = row_tag_;
-    c.rho = d_rho_vals_;
+    c.rho = d_rho;
     c.num_cols = n_total_;
     c.relevant = d_masks_[kRelevant];
     c.coefficient = d_coeff_;
@@ -1024,6 +1040,20 @@ void PinnedResize(T** p, size_t n) {
     throw DeviceError("hipHostMalloc");
   }
 }
+// Pinned host memory the kernels write directly (device pointer in *dev).
+template <typename T>
+void MappedResize(T** p, T** dev, size_t n) {
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *dev = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(p), std::max<size_t>(1, n) * sizeof(T),
+                    hipHostMallocMapped) != hipSuccess) {
+    throw DeviceError("hipHostMalloc (mapped)");
+  }
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, *p, 0) != hipSuccess) throw DeviceError("mapped pointer");
+  *dev = static_cast<T*>(d);
+}
 }  // namespace
 
 void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_t>& colbits,
@@ -1032,7 +1062,9 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
     d_rc_ = Alloc<double>(n_total_);
     d_colbits_ = Alloc<uint8_t>(n_total_);
     d_bound_diff_ = Alloc<double>(n_total_);
-    d_best_ = Alloc<unsigned long long>(1);
+    d_best_ = Alloc<unsigned long long>(2);  // alternating pass-1 slots
+    Check(hipMemsetAsync(d_best_, 0xff, 2 * sizeof(unsigned long long), S(stream_)), "memset");
+    dual_calls_ = 0;
     d_slot_flags_ = Alloc<uint8_t>(n_total_);
     d_slots_ = Alloc<int32_t>(n_total_);
     d_num_slots_ = Alloc<int>(1);
@@ -1052,10 +1084,10 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
           "radix sizing");
     d_sort_temp_ = Alloc<uint8_t>(sort_temp_bytes_);
     Synchronize();  // the pinned buffers below may still feed earlier copies
-    PinnedResize(&h_cand_col_, n_total_);
-    PinnedResize(&h_cand_coeff_, n_total_);
-    PinnedResize(&h_cand_rc_, n_total_);
-    PinnedResize(&h_dual_counts_, 2);
+    MappedResize(&h_cand_col_, &m_cand_col_, n_total_);
+    MappedResize(&h_cand_coeff_, &m_cand_coeff_, n_total_);
+    MappedResize(&h_cand_rc_, &m_cand_rc_, n_total_);
+    MappedResize(&h_dual_counts_, &m_dual_counts_, 2);
     PinnedResize(&h_cb_cols_, n_total_);
     PinnedResize(&h_cb_bits_, n_total_);
     PinnedResize(&h_flip_cols_, n_total_);
@@ -1111,6 +1143,15 @@ void DeviceLp::DualSetReducedCost(int col, double value) {
   Check(milp_launch::set_double(d_rc_ + col, value, S(stream_)), "set rc");
 }
 
+milp_kernels::ScanState DeviceLp::NextScan() {
+  if (++scan_epoch_ == 0) scan_epoch_ = 1;  // 0 is the zeroed status words' epoch
+  return milp_kernels::ScanState{d_scan_status_, d_scan_ticket_, scan_epoch_};
+}
+
+// Two launches: pass 1 (the bound B), then pass 2 fused with its ordered
+// compaction and the candidate gather into mapped host memory; one stream
+// synchronization, no copies. Only a large pass-2 set (rare) adds the
+// tightening round (keys, radix sort, walk, pass 2 again).
 void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_tolerance,
                                    double minimum_delta, double variation_magnitude,
                                    DualCandidates* out) {
@@ -1128,79 +1169,51 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
   a.harris_tolerance = harris_tolerance;
   a.minimum_delta = minimum_delta;
   a.variation_magnitude = variation_magnitude;
-  a.best = d_best_;
-  a.flags = d_slot_flags_;
-  a.bound = d_best_;
+  const int slot = static_cast<int>(dual_calls_++ & 1);
+  a.best = d_best_ + slot;
+  a.best_next = d_best_ + (slot ^ 1);
+  a.bound = a.best;
+  milp_kernels::DualSelectOut sel{};
+  sel.slots = d_slots_;
+  sel.num_slots = d_num_slots_;
+  sel.cand_col = m_cand_col_;
+  sel.cand_coeff = m_cand_coeff_;
+  sel.cand_rc = m_cand_rc_;
+  sel.counts = m_dual_counts_;
   BeginKernel(MI_K_DUAL_RATIO);
-  Check(hipMemsetAsync(d_best_, 0xff, sizeof(unsigned long long), S(stream_)), "memset");
   Check(milp_launch::dual_ratio_bound(a, S(stream_)), "dual ratio bound");
-  Check(milp_launch::dual_ratio_flags(a, S(stream_)), "dual ratio flags");
-  auto select = [&]() {
-    size_t bytes = cub_temp_bytes_;
-    Check(rocprim::select(d_cub_temp_, bytes,
-                                        rocprim::counting_iterator<int32_t>(0),
-                                        d_slot_flags_, d_slots_, d_num_slots_, n_total_,
-                                        S(stream_)),
-          "cub flagged");
-  };
-  select();
-  // Many breakpoints under B: tighten the bound by walking them in pop order
-  // (the sort needs their number on the host).
-  Download(h_dual_counts_, d_num_slots_, sizeof(int));
+  Check(milp_launch::dual_ratio_select(a, sel, NextScan(), S(stream_)), "dual ratio select");
+  EndKernel(MI_K_DUAL_RATIO, 0.0);  // bytes added once the list length is known
+  Synchronize();
   const int k1 = h_dual_counts_[0];
+  // Many breakpoints under B: tighten the bound by walking them in pop order.
   if (k1 > tighten_min_candidates_) {
+    if (k1 > n_total_) throw DeviceError("dual ratio test: bad counts");
+    BeginKernel(MI_K_DUAL_RATIO);
     Check(milp_launch::dual_ratio_keys(a, d_slots_, k1, d_keys_in_, S(stream_)), "keys");
     size_t bytes = sort_temp_bytes_;
-    Check(rocprim::radix_sort_pairs(d_sort_temp_, bytes, d_keys_in_, d_keys_out_,
-                                             d_slots_, d_sorted_slots_, k1, 0, 64, S(stream_)),
+    Check(rocprim::radix_sort_pairs(d_sort_temp_, bytes, d_keys_in_, d_keys_out_, d_slots_,
+                                    d_sorted_slots_, k1, 0, 64, S(stream_)),
           "radix sort");
     Check(milp_launch::dual_flip_walk(a, d_sorted_slots_, k1, d_best2_, S(stream_)), "walk");
     a.bound = d_best2_;
-    Check(milp_launch::dual_ratio_flags(a, S(stream_)), "dual ratio flags");
-    select();
+    Check(milp_launch::dual_ratio_select(a, sel, NextScan(), S(stream_)), "dual ratio select");
+    EndKernel(MI_K_DUAL_RATIO, 0.0, /*count_launch=*/false);  // same logical launch
+    Synchronize();
   }
-  Check(milp_launch::gather_candidates(d_slots_, d_num_slots_, n_total_, d_list_, d_out_list_,
-                                       d_rc_, d_cand_col_, d_cand_coeff_, d_cand_rc_,
-                                       S(stream_)),
-        "gather candidates");
-  EndKernel(MI_K_DUAL_RATIO, 0.0);  // bytes added once the list length is known
-  const int cap = std::min<int64_t>(n_total_, std::max<int64_t>(1024, int64_t(last_candidates_) +
-                                                                          last_candidates_ / 4));
-  Check(hipMemcpyAsync(h_dual_counts_, d_num_slots_, sizeof(int), hipMemcpyDeviceToHost,
-                       S(stream_)),
-        "D2H");
-  Check(hipMemcpyAsync(h_dual_counts_ + 1, d_count_, sizeof(int), hipMemcpyDeviceToHost,
-                       S(stream_)),
-        "D2H");
-  Check(hipMemcpyAsync(h_cand_col_, d_cand_col_, cap * sizeof(int32_t), hipMemcpyDeviceToHost,
-                       S(stream_)),
-        "D2H");
-  Check(hipMemcpyAsync(h_cand_coeff_, d_cand_coeff_, cap * sizeof(double),
-                       hipMemcpyDeviceToHost, S(stream_)),
-        "D2H");
-  Download(h_cand_rc_, d_cand_rc_, cap * sizeof(double));
   const int k = h_dual_counts_[0];
   const int count = h_dual_counts_[1];
   if (k < 0 || k > n_total_ || count < 0 || count > n_total_) {
     throw DeviceError("dual ratio test: bad counts");
   }
-  if (k > cap) {
-    Check(hipMemcpyAsync(h_cand_col_ + cap, d_cand_col_ + cap, (k - cap) * sizeof(int32_t),
-                         hipMemcpyDeviceToHost, S(stream_)),
-          "D2H");
-    Check(hipMemcpyAsync(h_cand_coeff_ + cap, d_cand_coeff_ + cap, (k - cap) * sizeof(double),
-                         hipMemcpyDeviceToHost, S(stream_)),
-          "D2H");
-    Download(h_cand_rc_ + cap, d_cand_rc_ + cap, (k - cap) * sizeof(double));
-  }
   last_candidates_ = k;
   dual_list_count_ = count;
-  // Algorithmic bytes: the list (position + coefficient), the reduced cost,
-  // column byte and bound difference of each position, twice; the flags; the
-  // candidates.
+  // Algorithmic bytes: per list slot its position and coefficient, and the
+  // reduced cost, column byte and bound difference of its column (29 B), once
+  // per pass; the candidates written (20 B) and their tightening keys.
+  const bool tightened = k1 > tighten_min_candidates_;
   stats_.algorithmic_bytes[MI_K_DUAL_RATIO] +=
-      (k1 > tighten_min_candidates_ ? 3.0 : 2.0) * 29.0 * count + 2.0 * n_total_ + 20.0 * k +
-      (k1 > tighten_min_candidates_ ? 36.0 * k1 : 0.0);
+      (tightened ? 3.0 : 2.0) * 29.0 * count + 20.0 * k + (tightened ? 20.0 * k1 + 36.0 * k1 : 0.0);
   out->col.assign(h_cand_col_, h_cand_col_ + k);
   out->coeff.assign(h_cand_coeff_, h_cand_coeff_ + k);
   out->rc.assign(h_cand_rc_, h_cand_rc_ + k);

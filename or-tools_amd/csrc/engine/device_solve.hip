@@ -8,7 +8,9 @@
 // host time of an iteration, twice per iteration (direction, bound flips).
 // U changes only at refactorization, so its level schedule is built and
 // uploaded once per factorization; each solve then moves the right-hand side
-// in, runs one single-CU kernel and moves the result out.
+// in, replays the captured launch plan and moves the result out. The solver's
+// thread and BasisFactorization's tau worker solve concurrently, each with
+// its own stream, buffers and graph (TriContext); the schedule is shared.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -16,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "../kernels/kernel_args.h"
 #include "device_lp.h"
@@ -29,46 +32,55 @@ inline hipStream_t Stream(void* p) { return reinterpret_cast<hipStream_t>(p); }
 
 struct SolveCallTimer {
   mi_lp_kernel_stats* stats;
+  int id;
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-  explicit SolveCallTimer(mi_lp_kernel_stats* s) : stats(s) {}
+  SolveCallTimer(mi_lp_kernel_stats* s, int i) : stats(s), id(i) {}
   ~SolveCallTimer() {
-    stats->call_ms[MI_K_TRI_SOLVE] +=
+    stats->call_ms[id] +=
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
             .count();
   }
 };
 
+void FreeBuffer(DeviceLp::TriBuffer* b) {
+  if (b->ptr != nullptr) (void)hipFree(b->ptr);
+  *b = DeviceLp::TriBuffer();
+}
+
 }  // namespace
 
-void DeviceLp::TriReserve(int which, size_t bytes) {
-  TriBuffer& b = tri_buf_[which];
-  if (b.ptr != nullptr && b.bytes >= bytes) return;
-  if (b.ptr != nullptr) (void)hipFree(b.ptr);
-  b.ptr = nullptr;
-  b.bytes = 0;
+void DeviceLp::TriReserve(TriBuffer* b, size_t bytes) {
+  if (b->ptr != nullptr && b->bytes >= bytes) return;
+  FreeBuffer(b);
   const size_t n = std::max<size_t>(bytes, 16) + bytes / 4;
-  Check(hipMalloc(&b.ptr, n), "hipMalloc (triangular solve)");
-  b.bytes = n;
+  Check(hipMalloc(&b->ptr, n), "hipMalloc (triangular solve)");
+  b->bytes = n;
 }
 
 void DeviceLp::FreeTriBuffers() {
-  for (TriBuffer& b : tri_buf_) {
-    if (b.ptr != nullptr) (void)hipFree(b.ptr);
-    b = TriBuffer();
-  }
+  for (TriBuffer& b : tri_buf_) FreeBuffer(&b);
   if (d_tri_clock_ != nullptr) (void)hipFree(d_tri_clock_);
   d_tri_clock_ = nullptr;
-  if (tri_graph_exec_ != nullptr) {
-    (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(tri_graph_exec_));
+  for (int slot = 0; slot < 2; ++slot) {
+    TriContext& c = tri_ctx_[slot];
+    if (c.graph_exec != nullptr) {
+      (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(c.graph_exec));
+    }
+    FreeBuffer(&c.x);
+    FreeBuffer(&c.y);
+    FreeBuffer(&c.top);
+    if (c.h_x != nullptr) (void)hipHostFree(c.h_x);
+    if (c.h_top != nullptr) (void)hipHostFree(c.h_top);
+    for (void* e : c.ev) {
+      if (e != nullptr) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e));
+    }
+    if (slot == 1 && c.stream != nullptr) {
+      (void)hipStreamSynchronize(Stream(c.stream));
+      (void)hipStreamDestroy(Stream(c.stream));
+    }
+    c = TriContext();
   }
-  tri_graph_exec_ = nullptr;
-  tri_graph_ready_ = false;
-  if (h_tri_top_ != nullptr) (void)hipHostFree(h_tri_top_);
-  h_tri_top_ = nullptr;
-  if (h_tri_x_ != nullptr) (void)hipHostFree(h_tri_x_);
   if (h_tri_stage_ != nullptr) (void)hipHostFree(h_tri_stage_);
-  h_tri_x_ = nullptr;
-  h_tri_x_elems_ = 0;
   h_tri_stage_ = nullptr;
   tri_stage_bytes_ = 0;
   tri_key_ = 0;
@@ -82,7 +94,7 @@ void DeviceLp::FreeTriBuffers() {
 // Positions: the listed outputs by level (descending c inside a level, the
 // host order), then the other rows >= first_non_identity (read, never
 // written). Entries refer to positions.
-void DeviceLp::BuildTriSchedule(const TriangularMatrix& t, uint64_t key) {
+void DeviceLp::BuildTriSchedule(const TriangularMatrix& t, uint64_t key, void* stream) {
   tri_key_ = key;
   tri_ok_ = false;
   const int nc = t.num_cols();
@@ -151,10 +163,16 @@ void DeviceLp::BuildTriSchedule(const TriangularMatrix& t, uint64_t key) {
     }
   }
   int64_t num_ovf = 0;
+  tri_max_entries_ = 0;
+  tri_rows_over_[0] = tri_rows_over_[1] = tri_rows_over_[2] = 0;
   for (int k = 0; k < num_work; ++k) {
     const int c = pos_row[k];
     const int64_t n = t.starts_[c + 1] - t.starts_[c];
     if (n > 4) num_ovf += n;
+    tri_max_entries_ = std::max<int>(tri_max_entries_, static_cast<int>(n));
+    tri_rows_over_[0] += n > 4;
+    tri_rows_over_[1] += n > 16;
+    tri_rows_over_[2] += n > 64;
   }
   // Staging layout, 16-byte aligned pieces.
   auto al = [](size_t b) { return (b + 15) / 16 * 16; };
@@ -230,29 +248,55 @@ void DeviceLp::BuildTriSchedule(const TriangularMatrix& t, uint64_t key) {
   }
   for (int b = 0; b < kTriNumStaged; ++b) {
     if (sizes[b] == 0) continue;
-    TriReserve(b, sizes[b]);
-    Upload(tri_buf_[b].ptr, st + offs[b], sizes[b]);
-  }
-  TriReserve(kTriX, size_t(nc) * 8);
-  TriReserve(kTriY, size_t(std::max(num_pos, 1)) * 8);
-  if (h_tri_x_elems_ < size_t(nc)) {
-    if (h_tri_x_ != nullptr) (void)hipHostFree(h_tri_x_);
-    h_tri_x_ = nullptr;
-    h_tri_x_elems_ = size_t(nc) + size_t(nc) / 4;
-    Check(hipHostMalloc(reinterpret_cast<void**>(&h_tri_x_), h_tri_x_elems_ * sizeof(double)),
-          "pin");
-  }
-  TriReserve(kTriTop, 16);
-  if (h_tri_top_ == nullptr) {
-    Check(hipHostMalloc(reinterpret_cast<void**>(&h_tri_top_), 64), "pin");
+    TriReserve(&tri_buf_[b], sizes[b]);
+    Check(hipMemcpyAsync(tri_buf_[b].ptr, st + offs[b], sizes[b], hipMemcpyHostToDevice,
+                         Stream(stream)),
+          "H2D");
   }
   // The staging buffer is reused by the next build: wait for the copies.
-  Check(hipStreamSynchronize(Stream(stream_)), "sync");
-  tri_ok_ = true;
-  tri_graph_ready_ = false;  // captured at the first solve of this factorization
+  Check(hipStreamSynchronize(Stream(stream)), "sync");
+  tri_ok_ = true;  // each context recaptures its graph for the new key
 }
 
-milp_kernels::TriSolveArgs DeviceLp::TriArgs() const {
+void DeviceLp::PrepareTriContext(int slot, int rows) {
+  TriContext& c = tri_ctx_[slot];
+  if (c.stream == nullptr) {
+    if (slot == 0) {
+      c.stream = stream_;
+    } else {
+      hipStream_t st;
+      Check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+      c.stream = st;
+    }
+    for (void*& e : c.ev) {
+      hipEvent_t ev;
+      Check(hipEventCreate(&ev), "hipEventCreate");
+      e = ev;
+    }
+    Check(hipHostMalloc(reinterpret_cast<void**>(&c.h_top), 64), "pin");
+    TriReserve(&c.top, 16);
+  }
+  const void* old_x = c.x.ptr;
+  const void* old_y = c.y.ptr;
+  TriReserve(&c.x, size_t(rows) * 8);
+  TriReserve(&c.y, size_t(std::max(tri_pos_, 1)) * 8);
+  if (c.x.ptr != old_x || c.y.ptr != old_y) c.graph_key = 0;  // buffers moved
+  // rows values + the top row (an int in the slot after them), mapped.
+  if (c.h_x_elems < size_t(rows) + 1) {
+    if (c.h_x != nullptr) (void)hipHostFree(c.h_x);
+    c.h_x = nullptr;
+    c.h_x_elems = size_t(rows) + size_t(rows) / 4 + 1;
+    Check(hipHostMalloc(reinterpret_cast<void**>(&c.h_x), c.h_x_elems * sizeof(double),
+                        hipHostMallocMapped),
+          "pin");
+    void* dev = nullptr;
+    Check(hipHostGetDevicePointer(&dev, c.h_x, 0), "mapped pointer");
+    c.m_x = static_cast<double*>(dev);
+    c.graph_key = 0;
+  }
+}
+
+milp_kernels::TriSolveArgs DeviceLp::TriArgs(const TriContext& c) const {
   milp_kernels::TriSolveArgs a;
   a.level_start = static_cast<const int32_t*>(tri_buf_[kTriLevels].ptr);
   a.rec_row = static_cast<const int32_t*>(tri_buf_[kTriRecRow].ptr);
@@ -263,9 +307,13 @@ milp_kernels::TriSolveArgs DeviceLp::TriArgs() const {
   a.ovf_pos = static_cast<const int32_t*>(tri_buf_[kTriOvfPos].ptr);
   a.ovf_value = static_cast<const double*>(tri_buf_[kTriOvfValue].ptr);
   a.pos_row = static_cast<const int32_t*>(tri_buf_[kTriPosRow].ptr);
-  a.x = static_cast<double*>(tri_buf_[kTriX].ptr);
-  a.y = static_cast<double*>(tri_buf_[kTriY].ptr);
-  a.top = static_cast<const int*>(tri_buf_[kTriTop].ptr);
+  a.x = static_cast<double*>(c.x.ptr);
+  a.y = static_cast<double*>(c.y.ptr);
+  a.top = static_cast<int*>(c.top.ptr);
+  a.host_x = tri_mapped_ ? c.m_x : nullptr;
+  a.first_col = tri_first_col_;
+  a.num_rows = tri_rows_;
+  a.fail = reinterpret_cast<int*>(c.m_x + tri_rows_) + 1;
   a.num_work = tri_work_;
   a.num_pos = tri_pos_;
   a.num_levels = tri_levels_;
@@ -275,48 +323,58 @@ milp_kernels::TriSolveArgs DeviceLp::TriArgs() const {
 
 // One solve = copy in (x[fni..nc), top), the launches of the segment plan,
 // copy out (x[fni..nc)). Without debugging the launches are captured once per
-// factorization into a HIP graph and replayed with one launch: the plan has
-// tens of kernels, whose individual launches would cost more host time than
-// their GPU time.
-void DeviceLp::TriCopyIn() {
+// factorization (and context) into a HIP graph and replayed with one launch:
+// the plan has tens of kernels, whose individual launches would cost more
+// host time than their GPU time.
+// Without zero-copy staging (MILP_TRI_MAPPED=0): copy-engine transfers.
+void DeviceLp::TriCopyIn(const TriContext& c) {
+  if (tri_mapped_) return;
   const int fni = tri_first_col_;
   const size_t in = size_t(tri_rows_ - fni);
-  double* d_x = static_cast<double*>(tri_buf_[kTriX].ptr);
-  Upload(d_x + fni, h_tri_x_ + fni, in * sizeof(double));
-  Upload(tri_buf_[kTriTop].ptr, h_tri_top_, sizeof(int));
+  double* d_x = static_cast<double*>(c.x.ptr);
+  Check(hipMemcpyAsync(d_x + fni, c.h_x + fni, in * sizeof(double), hipMemcpyHostToDevice,
+                       Stream(c.stream)),
+        "H2D");
+  Check(hipMemcpyAsync(c.top.ptr, c.h_top, sizeof(int), hipMemcpyHostToDevice, Stream(c.stream)),
+        "H2D");
 }
 
-void DeviceLp::TriCopyOut() {
+void DeviceLp::TriCopyOut(const TriContext& c) {
+  if (tri_mapped_) return;
   const int fni = tri_first_col_;
   const size_t in = size_t(tri_rows_ - fni);
-  double* d_x = static_cast<double*>(tri_buf_[kTriX].ptr);
-  Check(hipMemcpyAsync(h_tri_x_ + fni, d_x + fni, in * sizeof(double), hipMemcpyDeviceToHost,
-                       Stream(stream_)),
+  const double* d_x = static_cast<const double*>(c.x.ptr);
+  Check(hipMemcpyAsync(c.h_x + fni, d_x + fni, in * sizeof(double), hipMemcpyDeviceToHost,
+                       Stream(c.stream)),
         "D2H");
 }
 
-void DeviceLp::EnqueueTriKernels(const milp_kernels::TriSolveArgs& a) {
+void DeviceLp::EnqueueTriKernels(const milp_kernels::TriSolveArgs& a, void* stream) {
+  if (tri_syncfree_ && a.clock == nullptr && a.num_work <= milp_kernels::kTriSyncFreeMaxWork) {
+    Check(milp_launch::tri_transpose_lower_syncfree(a, Stream(stream)), "tri syncfree");
+    return;
+  }
   Check(milp_launch::tri_transpose_lower(a, tri_segments_.data(),
                                          static_cast<int>(tri_segments_.size() / 2),
-                                         Stream(stream_)),
+                                         Stream(stream)),
         "tri_transpose_lower");
 }
 
-void DeviceLp::CaptureTriGraph() {
-  if (tri_graph_exec_ != nullptr) {
-    (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(tri_graph_exec_));
-    tri_graph_exec_ = nullptr;
+void DeviceLp::CaptureTriGraph(TriContext* c) {
+  if (c->graph_exec != nullptr) {
+    (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(c->graph_exec));
+    c->graph_exec = nullptr;
   }
   hipGraph_t graph = nullptr;
-  Check(hipStreamBeginCapture(Stream(stream_), hipStreamCaptureModeThreadLocal), "capture");
-  EnqueueTriKernels(TriArgs());
-  Check(hipStreamEndCapture(Stream(stream_), &graph), "capture end");
+  Check(hipStreamBeginCapture(Stream(c->stream), hipStreamCaptureModeThreadLocal), "capture");
+  EnqueueTriKernels(TriArgs(*c), c->stream);
+  Check(hipStreamEndCapture(Stream(c->stream), &graph), "capture end");
   hipGraphExec_t exec = nullptr;
   const hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
   (void)hipGraphDestroy(graph);
   Check(e, "graph instantiate");
-  tri_graph_exec_ = exec;
-  tri_graph_ready_ = true;
+  c->graph_exec = exec;
+  c->graph_key = tri_key_;
 }
 
 bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
@@ -325,9 +383,23 @@ bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
   const int nc = t.num_cols();
   if (tri_mode_ == 0 && nc < tri_min_rows_) return false;
   if (static_cast<int>(x->size()) < nc) return false;
-  SolveCallTimer timer(&stats_);
-  if (tri_key_ != key) BuildTriSchedule(t, key);
-  if (!tri_ok_) return false;
+  // The solver's thread (slot 0) or the factorization's tau worker (slot 1).
+  const int slot = g_lu_slot == 0 ? 0 : 1;
+  if (slot != 0 && !tri_tau_) return false;
+  const int id = slot == 0 ? MI_K_TRI_SOLVE : MI_K_TRI_SOLVE_TAU;
+  SolveCallTimer timer(&stats_, id);
+  if (slot != 0) Check(hipSetDevice(device_), "hipSetDevice");
+  TriContext& c = tri_ctx_[slot];
+  {
+    // The schedule is shared: the first solve after a refactorization
+    // builds it, the other thread waits. (No solve can be in flight with the
+    // previous key: the tau worker is joined before every refactorization.)
+    std::lock_guard<std::mutex> lock(tri_mu_);
+    if (c.stream == nullptr) PrepareTriContext(slot, nc);
+    if (tri_key_ != key) BuildTriSchedule(t, key, c.stream);
+    if (!tri_ok_) return false;
+    PrepareTriContext(slot, nc);
+  }
   double* xv = x->data();
   const int fni = tri_first_col_;
   // sparse.cc:908-912: the host loop starts at the last non-zero.
@@ -337,8 +409,11 @@ bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
   if (tri_rows_upto_[top + 1] - tri_rows_upto_[fni] == 0) return true;  // identity part only
   // Outputs c >= fni read rows > c only: x[fni..nc) in and out.
   const size_t in = size_t(nc - fni);
-  CopyHost(h_tri_x_ + fni, xv + fni, in * sizeof(double));
-  *h_tri_top_ = top;
+  CopyHost(c.h_x + fni, xv + fni, in * sizeof(double));
+  *c.h_top = top;
+  int* h_words = reinterpret_cast<int*>(c.h_x + nc);
+  h_words[0] = top;  // zero-copy plan reads it here
+  h_words[1] = 0;    // the sync-free kernel's failure word
   const double rows = tri_rows_upto_[top + 1] - tri_rows_upto_[fni];
   const double entries =
       static_cast<double>(tri_entries_upto_[top + 1] - tri_entries_upto_[fni]);
@@ -348,28 +423,32 @@ bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
   // out and the 4-B row index per position, both ways.
   const double bytes = rows * (24.0 + (tri_ones_ ? 0.0 : 8.0)) + entries * 20.0 +
                        double(tri_pos_) * 20.0 + rows * 20.0;
-  if (tri_debug_left_ > 0) {
+  if (slot == 0 && tri_debug_left_ > 0) {
     // MILP_TRI_DEBUG=k: per-level wall clock of the first k solves after each
     // schedule build (single-CU segments), printed with the level widths.
-    milp_kernels::TriSolveArgs a = TriArgs();
+    milp_kernels::TriSolveArgs a = TriArgs(c);
     if (d_tri_clock_ == nullptr) {
       Check(hipMalloc(reinterpret_cast<void**>(&d_tri_clock_), 65536 * sizeof(uint64_t)),
             "hipMalloc");
     }
-    Check(hipMemsetAsync(d_tri_clock_, 0, 65536 * sizeof(uint64_t), Stream(stream_)), "memset");
+    Check(hipMemsetAsync(d_tri_clock_, 0, 65536 * sizeof(uint64_t), Stream(c.stream)),
+          "memset");
     if (tri_levels_ + 1 < 65536) a.clock = d_tri_clock_;
-    TriCopyIn();
+    TriCopyIn(c);
     BeginKernel(MI_K_TRI_SOLVE);
-    EnqueueTriKernels(a);
+    EnqueueTriKernels(a, c.stream);
     EndKernel(MI_K_TRI_SOLVE, bytes);
-    TriCopyOut();
+    TriCopyOut(c);
     Synchronize();
     --tri_debug_left_;
     std::vector<uint64_t> clk(tri_levels_ + 1);
     Check(hipMemcpy(clk.data(), d_tri_clock_, clk.size() * sizeof(uint64_t),
                     hipMemcpyDeviceToHost), "D2H");
-    std::fprintf(stderr, "[tri] rows %d work %d levels %d segments %zu top %d; per level (us/width):",
-                 nc, tri_work_, tri_levels_, tri_segments_.size() / 2, top);
+    std::fprintf(stderr,
+                 "[tri] rows %d work %d levels %d segments %zu top %d entries/row max %d "
+                 ">4 %d >16 %d >64 %d; per level (us/width):",
+                 nc, tri_work_, tri_levels_, tri_segments_.size() / 2, top, tri_max_entries_,
+                 tri_rows_over_[0], tri_rows_over_[1], tri_rows_over_[2]);
     for (int l = 0; l < tri_levels_; ++l) {
       const bool ok = clk[l] != 0 && clk[l + 1] >= clk[l];
       std::fprintf(stderr, " %.2f/%d", ok ? (clk[l + 1] - clk[l]) / 100.0 : -1.0,
@@ -377,16 +456,44 @@ bool DeviceLp::TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
     }
     std::fprintf(stderr, "\n");
   } else {
-    if (!tri_graph_ready_) CaptureTriGraph();
-    TriCopyIn();
-    BeginKernel(MI_K_TRI_SOLVE);  // events around the graph: the kernels only
-    Check(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(tri_graph_exec_), Stream(stream_)),
-          "graph launch");
-    EndKernel(MI_K_TRI_SOLVE, bytes);
-    TriCopyOut();
-    Synchronize();
+    if (tri_graph_ && (c.graph_key != tri_key_ || c.graph_exec == nullptr)) {
+      std::lock_guard<std::mutex> lock(tri_mu_);  // one capture at a time
+      CaptureTriGraph(&c);
+    }
+    TriCopyIn(c);
+    if (slot == 0) {
+      BeginKernel(MI_K_TRI_SOLVE);  // events around the graph: the kernels only
+    } else if (timing_) {
+      Check(hipEventRecord(reinterpret_cast<hipEvent_t>(c.ev[0]), Stream(c.stream)), "ev");
+    }
+    if (tri_graph_) {
+      Check(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(c.graph_exec), Stream(c.stream)),
+            "graph launch");
+    } else {
+      EnqueueTriKernels(TriArgs(c), c.stream);
+    }
+    if (slot == 0) {
+      EndKernel(MI_K_TRI_SOLVE, bytes);
+    } else if (timing_) {
+      Check(hipEventRecord(reinterpret_cast<hipEvent_t>(c.ev[1]), Stream(c.stream)), "ev");
+    }
+    TriCopyOut(c);
+    Check(hipStreamSynchronize(Stream(c.stream)), "sync");
+    if (slot != 0) {
+      // The worker's own counters (its id is written by this thread only).
+      stats_.launches[id] += 1;
+      stats_.algorithmic_bytes[id] += bytes;
+      if (timing_) {
+        float ms = 0.0f;
+        Check(hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(c.ev[0]),
+                                  reinterpret_cast<hipEvent_t>(c.ev[1])),
+              "ev time");
+        stats_.device_ms[id] += ms;
+      }
+    }
   }
-  CopyHost(xv + fni, h_tri_x_ + fni, size_t(top - fni + 1) * sizeof(double));
+  if (*static_cast<volatile int*>(h_words + 1) != 0) throw DeviceError("triangular solve: dependency wait timed out");
+  CopyHost(xv + fni, c.h_x + fni, size_t(top - fni + 1) * sizeof(double));
   return true;
 }
 

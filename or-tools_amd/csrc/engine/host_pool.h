@@ -13,6 +13,7 @@
 #define MILP_HOST_POOL_H_
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -180,6 +181,45 @@ int ParallelRanges(int64_t n, int64_t min_parallel, int64_t align, F&& fn) {
   };
   pool.Run(parts, job);
   return parts;
+}
+
+// Appends to *rows the indices r in [begin, n) with v[r] != 0 in increasing
+// order (and their values to *vals if not null), scanning the range in
+// parallel parts that are concatenated in order: the same output as the
+// serial loop. Returns the largest |v[r]| over the appended entries when
+// max_abs is requested (std::max over |v| in index order, as the serial
+// scan: a NaN is never selected).
+template <typename Real>
+void ParallelAppendNonZeros(const Real* v, int64_t begin, int64_t n, std::vector<int>* rows,
+                            std::vector<Real>* vals, Real* max_abs = nullptr) {
+  constexpr int kMaxParts = 16;
+  std::vector<int> part_rows[kMaxParts];
+  Real part_max[kMaxParts] = {};
+  const int64_t len = n > begin ? n - begin : 0;
+  const int parts = ParallelRanges(len, 65536, 64, [&](int p, int64_t b, int64_t e) {
+    std::vector<int>& out = part_rows[p];
+    Real m = 0;
+    for (int64_t i = begin + b; i < begin + e; ++i) {
+      if (v[i] != 0.0) {
+        out.push_back(static_cast<int>(i));
+        m = std::max(m, std::fabs(v[i]));
+      }
+    }
+    part_max[p] = m;
+  });
+  size_t total = rows->size();
+  for (int p = 0; p < parts; ++p) total += part_rows[p].size();
+  rows->reserve(total);
+  if (vals != nullptr) vals->reserve(vals->size() + (total - rows->size()));
+  Real m = max_abs != nullptr ? *max_abs : Real(0);
+  for (int p = 0; p < parts; ++p) {
+    for (const int r : part_rows[p]) {
+      rows->push_back(r);
+      if (vals != nullptr) vals->push_back(v[r]);
+    }
+    m = std::max(m, part_max[p]);
+  }
+  if (max_abs != nullptr) *max_abs = m;
 }
 
 }  // namespace milp

@@ -10,6 +10,7 @@
 #ifndef MILP_LP_DATA_H_
 #define MILP_LP_DATA_H_
 
+#include "host_pool.h"
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -571,13 +572,9 @@ class CompactSparseMatrix {
   }
   // sparse.cc:576-623
   int AddDenseColumnPrefix(const std::vector<Fractional>& d, int start) {
-    const int n = static_cast<int>(d.size());
-    for (int r = start; r < n; ++r) {
-      if (d[r] != 0.0) {
-        rows_.push_back(r);
-        coefficients_.push_back(d[r]);
-      }
-    }
+    // The non-zeros of d[start..), increasing (host pool for long columns).
+    ParallelAppendNonZeros(d.data(), start, static_cast<int64_t>(d.size()), &rows_,
+                           &coefficients_);
     starts_.push_back(rows_.size());
     return num_cols_++;
   }

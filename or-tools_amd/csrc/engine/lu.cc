@@ -641,9 +641,9 @@ void LuFactorization::RightSolveUWithNonZeros(ScatteredVector* x) const {
   upper_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
   x->non_zeros_are_sorted = true;
   if (x->non_zeros.empty()) {
-    // The dense U solve: on the device for the solver's thread (the tau
-    // worker keeps the host loop), same result bits.
-    if (device_solver_ == nullptr || g_lu_slot != 0 ||
+    // The dense U solve: on the device (the solver's thread and the tau
+    // worker each with its own stream), same result bits.
+    if (device_solver_ == nullptr ||
         !device_solver_->TransposeLowerSolve(transpose_upper_, factorization_key_,
                                              &x->values)) {
       transpose_upper_.TransposeLowerSolve(&x->values);

@@ -561,15 +561,20 @@ class DualEdgeNorms {
     const std::vector<Fractional>& tau = bf_.RightSolveForTau(rho);
     const Fractional pivot = direction[leaving_row];
     const Fractional new_leaving_squared_norm = norms_[leaving_row] / Square(pivot);
-    for (const int row : direction.non_zeros) {
-      const Fractional c = direction[row];
-      norms_[row] += c * (c * new_leaving_squared_norm - 2.0 / pivot * tau[row]);
-      const Fractional kLowerBound = 1e-4;
-      if (norms_[row] < kLowerBound) {
-        if (row == leaving_row) continue;
-        norms_[row] = kLowerBound;
+    // Element-wise over the direction's distinct rows: split over the host pool.
+    const std::vector<int>& rows = direction.non_zeros;
+    ParallelRanges(static_cast<int64_t>(rows.size()), 16384, 1, [&](int, int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k) {
+        const int row = rows[k];
+        const Fractional c = direction[row];
+        norms_[row] += c * (c * new_leaving_squared_norm - 2.0 / pivot * tau[row]);
+        const Fractional kLowerBound = 1e-4;
+        if (norms_[row] < kLowerBound) {
+          if (row == leaving_row) continue;
+          norms_[row] = kLowerBound;
+        }
       }
-    }
+    });
     norms_[leaving_row] = new_leaving_squared_norm;
   }
 
@@ -2278,13 +2283,15 @@ class VariableValues {
   void UpdateOnPivoting(const ScatteredVector& direction, int entering_col,
                         Fractional step) {
     const std::vector<int>& rows = direction.non_zeros;
-    const size_t n = rows.size();
-    for (size_t k = 0; k < n; ++k) {
-      if (k + 16 < n) __builtin_prefetch(variable_values_.data() + basis_[rows[k + 16]], 1);
-      const int row = rows[k];
-      const int col = basis_[row];
-      variable_values_[col] -= direction.values[row] * step;
-    }
+    // Distinct rows hold distinct basic columns: split over the host pool.
+    ParallelRanges(static_cast<int64_t>(rows.size()), 16384, 1, [&](int, int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k) {
+        if (k + 16 < e) __builtin_prefetch(variable_values_.data() + basis_[rows[k + 16]], 1);
+        const int row = rows[k];
+        const int col = basis_[row];
+        variable_values_[col] -= direction.values[row] * step;
+      }
+    });
     variable_values_[entering_col] += step;
   }
   void UpdateGivenNonBasicVariables(const std::vector<int>& cols, bool update_basic);
@@ -3795,13 +3802,9 @@ void RevisedSimplex::ComputeDirection(int col) {
   basis_factorization_.RightSolveForProblemColumn(col, &direction_);
   direction_infinity_norm_ = 0.0;
   if (direction_.non_zeros.empty()) {
-    for (int row = 0; row < num_rows_; ++row) {
-      const Fractional value = direction_[row];
-      if (value != 0.0) {
-        direction_.non_zeros.push_back(row);
-        direction_infinity_norm_ = std::max(direction_infinity_norm_, std::fabs(value));
-      }
-    }
+    ParallelAppendNonZeros(direction_.values.data(), 0, num_rows_, &direction_.non_zeros,
+                           static_cast<std::vector<Fractional>*>(nullptr),
+                           &direction_infinity_norm_);
   } else {
     for (const int row : direction_.non_zeros) {
       direction_infinity_norm_ =

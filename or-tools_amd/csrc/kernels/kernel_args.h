@@ -228,8 +228,31 @@ struct DualRatioArgs {
   double variation_magnitude;
   unsigned long long* best;  // pass 1: min over H-setting breakpoints of the
                              // Harris ratio, as ordered bits (all values > 0)
-  uint8_t* flags;            // pass 2: per list slot, kept for the host replay
+  unsigned long long* best_next;  // pass 1 sets it to "none" for the next call
   const unsigned long long* bound;  // pass 2: the bound it filters with
+};
+
+// Single-pass ordered compaction (decoupled look-back): a launch takes tiles
+// of kScanTile slots in ticket order; each tile publishes its count, then its
+// inclusive prefix, tagged with the launch's epoch (no reset between
+// launches); the last workgroup to finish rewinds the ticket counters.
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanThreads * kScanItems;
+struct ScanState {
+  unsigned long long* status;  // per tile: epoch << 32 | flag << 30 | count
+  unsigned int* ticket;        // [0] tile ticket, [1] finished workgroups
+  unsigned int epoch;          // distinct per launch, never 0
+};
+
+// The fused dual ratio filter + compaction writes here (mapped host memory).
+struct DualSelectOut {
+  int32_t* slots;      // device: kept list slots, in list order
+  int* num_slots;      // device
+  int32_t* cand_col;   // host-visible
+  double* cand_coeff;  // host-visible
+  double* cand_rc;     // host-visible
+  int* counts;         // host-visible: [0] kept, [1] list length
 };
 
 struct RowSumArgs {
@@ -264,9 +287,20 @@ struct TriSolveArgs {
   int num_work;
   int num_pos;
   int num_levels;
-  const int* top;              // rows above *top are not computed (host: last non-zero)
+  int* top;                    // rows above *top are not computed (host: last non-zero)
   uint64_t* clock;             // debug (MILP_TRI_DEBUG): wall clock after each level, or null
+  // Zero-copy staging (or null: the caller copies x and *top): host_x is
+  // device-visible host memory holding x[first_col, num_rows) and, in the
+  // int at host_x + num_rows, the top row; the plan starts by reading them
+  // and ends by writing x[first_col, top] back.
+  double* host_x;
+  int first_col;
+  int num_rows;
+  int* fail;  // sync-free variant: set (host-visible) if a wait ran out
 };
+// The sync-free variant needs every workgroup resident: at most this many
+// outputs (512 workgroups of 256 threads, 2 per CU).
+constexpr int kTriSyncFreeMaxWork = 512 * 256;
 }  // namespace milp_kernels
 
 namespace milp_launch {
@@ -277,9 +311,6 @@ hipError_t dense_dot(int mode, int unroll, const milp_kernels::DenseArgs& args, 
 hipError_t dense_pack(const int64_t* starts, const double* vals, const int32_t* dense_cols,
                       int nd, int m, double* body, double* tail, hipStream_t s);
 hipError_t gather(const int32_t* list, int n, const double* src, double* dst, hipStream_t s);
-// dst[i] = src[list[i]] for i < *count (count on the device, at most n).
-hipError_t gather_counted(const int32_t* list, const int* count, int n, const double* src,
-                          double* dst, hipStream_t s);
 // Flags -> ascending list + coefficient gather + count, one workgroup, for
 // n <= kSmallCompactMax.
 constexpr int kSmallCompactMax = 1 << 14;  // one workgroup writes the list to host memory
@@ -287,6 +318,15 @@ constexpr int kSmallCompactMax = 1 << 14;  // one workgroup writes the list to h
 hipError_t compact_small(const uint8_t* flags, int n, const double* coeff, int32_t* list,
                          double* vals, int* count, int32_t* host_list, double* host_vals,
                          int* host_count, hipStream_t s);
+// Any n: flags -> ascending list + coefficients + count in one launch
+// (ordered single-pass compaction); host_* as above.
+hipError_t compact_flags(const uint8_t* flags, int n, const double* coeff, int32_t* list,
+                         double* vals, int* count, int32_t* host_list, double* host_vals,
+                         int* host_count, const milp_kernels::ScanState& st, hipStream_t s);
+// Tiles a compaction launch over n slots uses (ScanState::status length).
+inline int scan_tiles(int n) {
+  return n <= 0 ? 1 : (n + milp_kernels::kScanTile - 1) / milp_kernels::kScanTile;
+}
 hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s);
 // threads: 1024, or 256 (used when the filtered rows fit one per thread).
 hipError_t row_wise_update_small(const milp_kernels::RowWiseSmallArgs& args, int threads,
@@ -303,7 +343,11 @@ hipError_t row_wise_update_full_rows(const milp_kernels::RowWiseFullArgs& args, 
 hipError_t row_sums(const milp_kernels::RowSumArgs& args, hipStream_t s);
 // Dual device mode.
 hipError_t dual_ratio_bound(const milp_kernels::DualRatioArgs& args, hipStream_t s);
-hipError_t dual_ratio_flags(const milp_kernels::DualRatioArgs& args, hipStream_t s);
+// Pass 2 fused with its compaction and the candidate gather: the eligible
+// slots with ratio <= *args.bound (1 + 1e-9), in list order, one launch.
+hipError_t dual_ratio_select(const milp_kernels::DualRatioArgs& args,
+                             const milp_kernels::DualSelectOut& out,
+                             const milp_kernels::ScanState& st, hipStream_t s);
 // Tighter bound: sort keys (ratio, order-preserving bits) of the pass-2 slots.
 hipError_t dual_ratio_keys(const milp_kernels::DualRatioArgs& args, const int32_t* slots,
                            int num_slots, unsigned long long* keys, hipStream_t s);
@@ -313,12 +357,6 @@ hipError_t dual_ratio_keys(const milp_kernels::DualRatioArgs& args, const int32_
 // on a ratio tie, where the pop order also depends on magnitudes).
 hipError_t dual_flip_walk(const milp_kernels::DualRatioArgs& args, const int32_t* sorted_slots,
                           int num_slots, unsigned long long* bound2, hipStream_t s);
-// cand_* [k] = (list[slot], list_coeff[slot], rc[list[slot]]) for the flagged
-// slots k in slot order (flag compaction done by the caller).
-hipError_t gather_candidates(const int32_t* slots, const int* num_slots, int max_slots,
-                             const int32_t* list, const double* list_coeff, const double* rc,
-                             int32_t* cand_col, double* cand_coeff, double* cand_rc,
-                             hipStream_t s);
 // rc[list[i]] += mult * list_coeff[i] (reduced_costs.cc:466-470), then
 // rc[leaving] = leaving_value, rc[entering] = 0.
 hipError_t update_reduced_costs(const int32_t* list, const double* list_coeff, const int* count,
@@ -338,6 +376,9 @@ hipError_t boxed_flips(const int32_t* cols, int n, const double* rc, const uint8
 // one CU; (-level - 1, blocks) = one wide level over `blocks` workgroups.
 hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, const int* segments,
                                int num_segments, hipStream_t s);
+// The same solve driven by per-output readiness instead of levels (one
+// launch for the whole triangle; rec_row/x updated in place, no scatter).
+hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, hipStream_t s);
 hipError_t column_squared_norms(const int64_t* starts, const double* vals,
                                 const uint64_t* relevant, int ncols, double* out,
                                 hipStream_t s);

@@ -325,13 +325,6 @@ __global__ void gather_kernel(const int32_t* list, int n, const double* src, dou
     dst[i] = src[list[i]];
 }
 
-__global__ void gather_counted_kernel(const int32_t* list, const int* count, const double* src,
-                                      double* dst) {
-  const int n = *count;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    dst[i] = src[list[i]];
-}
-
 // Update-row compaction for small N in one workgroup: thread t owns a
 // contiguous slice of the flags, a block-wide exclusive scan of the slice
 // counts gives each thread its output offset, so the list comes out in
@@ -372,6 +365,134 @@ __global__ __launch_bounds__(kCompactThreads) void compact_small_kernel(
     *count = sums[t];
     if (host_count != nullptr) *host_count = sums[t];
   }
+}
+
+// ---------------------------------------------------------------------------
+// Ordered single-pass compaction over many workgroups. A workgroup takes the
+// next tile ticket (tiles are taken in order by running workgroups, so a
+// predecessor never waits on an unscheduled one), counts its kept slots,
+// publishes the count, walks back over its predecessors' published values to
+// its exclusive prefix and publishes the inclusive one. Status words carry
+// the launch epoch: words of earlier launches read as "not yet published".
+constexpr unsigned long long kScanAggregate = 1ull << 30;
+constexpr unsigned long long kScanInclusive = 2ull << 30;
+constexpr unsigned long long kScanCountMask = (1ull << 30) - 1;
+
+__device__ __forceinline__ void scan_publish(const ScanState& st, int tile,
+                                             unsigned long long flag, int value) {
+  const unsigned long long w =
+      (static_cast<unsigned long long>(st.epoch) << 32) | flag | static_cast<unsigned>(value);
+  __hip_atomic_store(st.status + tile, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Thread 0 only: the exclusive prefix of `tile`, whose own count is `count`.
+__device__ int scan_look_back(const ScanState& st, int tile, int count) {
+  if (tile == 0) {
+    scan_publish(st, 0, kScanInclusive, count);
+    return 0;
+  }
+  scan_publish(st, tile, kScanAggregate, count);
+  int prefix = 0;
+  for (int j = tile - 1; j >= 0;) {
+    const unsigned long long w =
+        __hip_atomic_load(st.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long flag = w & (3ull << 30);
+    if ((w >> 32) != st.epoch || flag == 0) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    prefix += static_cast<int>(w & kScanCountMask);
+    if (flag == kScanInclusive) break;
+    --j;
+  }
+  scan_publish(st, tile, kScanInclusive, prefix + count);
+  return prefix;
+}
+
+// Block-wide exclusive scan of one int per thread (kScanThreads threads).
+__device__ __forceinline__ int scan_block_exclusive(int c, int* total, int* lds_waves) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  int x = c;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int y = __shfl_up(x, off, kWave);
+    if (lane >= off) x += y;
+  }
+  if (lane == kWave - 1) lds_waves[wave] = x;
+  __syncthreads();
+  int before = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kScanThreads / kWave; ++w) {
+    const int v = lds_waves[w];
+    before += w < wave ? v : 0;
+    all += v;
+  }
+  *total = all;
+  return before + x - c;
+}
+
+__device__ __forceinline__ int scan_take_tile(const ScanState& st, int* lds_tile) {
+  if (threadIdx.x == 0) *lds_tile = static_cast<int>(atomicAdd(st.ticket, 1u));
+  __syncthreads();
+  return *lds_tile;
+}
+
+// The last workgroup to finish rewinds the tickets for the next launch.
+__device__ __forceinline__ void scan_finish(const ScanState& st) {
+  if (threadIdx.x == 0) {
+    const unsigned int done = atomicAdd(st.ticket + 1, 1u);
+    if (done == gridDim.x - 1) {
+      __hip_atomic_store(st.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(st.ticket + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void compact_flags_kernel(
+    const uint8_t* flags, int n, const double* coeff, int32_t* list, double* vals, int* count,
+    int32_t* host_list, double* host_vals, int* host_count, ScanState st) {
+  __shared__ int lds_tile, lds_prefix;
+  __shared__ int lds_waves[kScanThreads / kWave];
+  const int tile = scan_take_tile(st, &lds_tile);
+  const int base = tile * kScanTile + threadIdx.x * kScanItems;
+  // Eight flag bytes per thread in one load when the slice is whole.
+  unsigned keep = 0;
+  if (base + kScanItems <= n) {
+    const uint2 f = *reinterpret_cast<const uint2*>(flags + base);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) keep |= ((f.x >> (8 * i)) & 0xff) ? (1u << i) : 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) keep |= ((f.y >> (8 * i)) & 0xff) ? (1u << (4 + i)) : 0u;
+  } else {
+    for (int i = 0; i < kScanItems; ++i) {
+      if (base + i < n && flags[base + i] != 0) keep |= 1u << i;
+    }
+  }
+  int total;
+  const int excl = scan_block_exclusive(__popc(keep), &total, lds_waves);
+  if (threadIdx.x == 0) lds_prefix = scan_look_back(st, tile, total);
+  __syncthreads();
+  int pos = lds_prefix + excl;
+  while (keep != 0) {
+    const int i = __ffs(keep) - 1;
+    keep &= keep - 1;
+    const int slot = base + i;
+    const double v = coeff[slot];
+    list[pos] = slot;
+    vals[pos] = v;
+    if (host_list != nullptr) {  // zero-copy readback into mapped host memory
+      host_list[pos] = slot;
+      host_vals[pos] = v;
+    }
+    ++pos;
+  }
+  if (tile == static_cast<int>(gridDim.x) - 1 && threadIdx.x == 0) {
+    const int all = lds_prefix + total;
+    *count = all;
+    if (host_count != nullptr) *host_count = all;
+  }
+  scan_finish(st);
 }
 
 // ---------------------------------------------------------------------------
@@ -923,6 +1044,9 @@ __device__ __forceinline__ bool dual_breakpoint(const DualRatioArgs& a, int slot
 __global__ __launch_bounds__(256) void dual_ratio_bound_kernel(DualRatioArgs a) {
   __shared__ unsigned long long block_min[4];
   const int n = *a.count;
+  // The other slot of the pair was last used by the previous call (ordered
+  // before this launch): it starts the next call at "none", no memset.
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.best_next != nullptr) *a.best_next = ~0ull;
   unsigned long long best = ~0ull;
   for (int slot = blockIdx.x * blockDim.x + threadIdx.x; slot < n;
        slot += gridDim.x * blockDim.x) {
@@ -946,24 +1070,57 @@ __global__ __launch_bounds__(256) void dual_ratio_bound_kernel(DualRatioArgs a) 
   }
 }
 
-// Pass 2: keep the eligible slots with ratio <= B (1 + 1e-9); the host
-// replays Glop's two loops over them in list order.
-__global__ __launch_bounds__(256) void dual_ratio_flags_kernel(DualRatioArgs a) {
+// Pass 2 with its compaction: the kept slots come out in list order, their
+// candidates go straight to host memory; the workgroup of the last list tile
+// writes the counts. Grid: scan_tiles(max_count) tiles, those past the list
+// length only take their ticket.
+__global__ __launch_bounds__(kScanThreads) void dual_ratio_select_kernel(DualRatioArgs a,
+                                                                         DualSelectOut out,
+                                                                         ScanState st) {
+  __shared__ int lds_tile, lds_prefix;
+  __shared__ int lds_waves[kScanThreads / kWave];
   const int n = *a.count;
-  const unsigned long long best = *a.bound;
-  const double bound = best == ~0ull ? HUGE_VAL
-                                     : __longlong_as_double(static_cast<long long>(best)) *
-                                           (1.0 + 1e-9);
-  for (int slot = blockIdx.x * blockDim.x + threadIdx.x; slot < a.max_count;
-       slot += gridDim.x * blockDim.x) {
-    bool keep = false;
-    if (slot < n) {
+  const int tile = scan_take_tile(st, &lds_tile);
+  const int last_tile = n > 0 ? (n - 1) / kScanTile : 0;
+  if (tile <= last_tile) {
+    const unsigned long long best = *a.bound;
+    const double bound = best == ~0ull ? HUGE_VAL
+                                       : __longlong_as_double(static_cast<long long>(best)) *
+                                             (1.0 + 1e-9);
+    const int base = tile * kScanTile + threadIdx.x * kScanItems;
+    unsigned keep = 0;
+    for (int i = 0; i < kScanItems; ++i) {
       double ratio, harris;
       bool sets_bound;
-      keep = dual_breakpoint(a, slot, &ratio, &harris, &sets_bound) && ratio <= bound;
+      if (base + i < n && dual_breakpoint(a, base + i, &ratio, &harris, &sets_bound) &&
+          ratio <= bound) {
+        keep |= 1u << i;
+      }
     }
-    a.flags[slot] = keep ? 1 : 0;
+    int total;
+    const int excl = scan_block_exclusive(__popc(keep), &total, lds_waves);
+    if (threadIdx.x == 0) lds_prefix = scan_look_back(st, tile, total);
+    __syncthreads();
+    int pos = lds_prefix + excl;
+    while (keep != 0) {
+      const int i = __ffs(keep) - 1;
+      keep &= keep - 1;
+      const int slot = base + i;
+      const int col = a.list[slot];
+      out.slots[pos] = slot;
+      out.cand_col[pos] = col;
+      out.cand_coeff[pos] = a.list_coeff[slot];
+      out.cand_rc[pos] = a.rc[col];
+      ++pos;
+    }
+    if (tile == last_tile && threadIdx.x == 0) {
+      const int all = lds_prefix + total;
+      *out.num_slots = all;
+      out.counts[0] = all;
+      out.counts[1] = n;
+    }
   }
+  scan_finish(st);
 }
 
 __device__ __forceinline__ unsigned long long order_bits(double x) {
@@ -1012,20 +1169,6 @@ __global__ void dual_flip_walk_kernel(DualRatioArgs a, const int32_t* sorted_slo
     return;
   }
   *bound2 = *a.best;
-}
-
-__global__ void gather_candidates_kernel(const int32_t* slots, const int* num_slots,
-                                         const int32_t* list, const double* list_coeff,
-                                         const double* rc, int32_t* cand_col,
-                                         double* cand_coeff, double* cand_rc) {
-  const int n = *num_slots;
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-    const int slot = slots[k];
-    const int col = list[slot];
-    cand_col[k] = col;
-    cand_coeff[k] = list_coeff[slot];
-    cand_rc[k] = rc[col];
-  }
 }
 
 __global__ void update_reduced_costs_kernel(const int32_t* list, const double* list_coeff,
@@ -1258,10 +1401,11 @@ hipError_t gather(const int32_t* list, int n, const double* src, double* dst, hi
   return hipGetLastError();
 }
 
-hipError_t gather_counted(const int32_t* list, const int* count, int n, const double* src,
-                          double* dst, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  gather_counted_kernel<<<std::min(2048, div_up(n, 256)), 256, 0, s>>>(list, count, src, dst);
+hipError_t compact_flags(const uint8_t* flags, int n, const double* coeff, int32_t* list,
+                         double* vals, int* count, int32_t* host_list, double* host_vals,
+                         int* host_count, const ScanState& st, hipStream_t s) {
+  compact_flags_kernel<<<scan_tiles(n), kScanThreads, 0, s>>>(
+      flags, n, coeff, list, vals, count, host_list, host_vals, host_count, st);
   return hipGetLastError();
 }
 
@@ -1342,8 +1486,9 @@ hipError_t dual_ratio_bound(const DualRatioArgs& args, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t dual_ratio_flags(const DualRatioArgs& args, hipStream_t s) {
-  dual_ratio_flags_kernel<<<grid_for(args.max_count), 256, 0, s>>>(args);
+hipError_t dual_ratio_select(const DualRatioArgs& args, const DualSelectOut& out,
+                             const ScanState& st, hipStream_t s) {
+  dual_ratio_select_kernel<<<scan_tiles(args.max_count), kScanThreads, 0, s>>>(args, out, st);
   return hipGetLastError();
 }
 
@@ -1357,16 +1502,6 @@ hipError_t dual_ratio_keys(const DualRatioArgs& args, const int32_t* slots, int 
 hipError_t dual_flip_walk(const DualRatioArgs& args, const int32_t* sorted_slots,
                           int num_slots, unsigned long long* bound2, hipStream_t s) {
   dual_flip_walk_kernel<<<1, 64, 0, s>>>(args, sorted_slots, num_slots, bound2);
-  return hipGetLastError();
-}
-
-hipError_t gather_candidates(const int32_t* slots, const int* num_slots, int max_slots,
-                             const int32_t* list, const double* list_coeff, const double* rc,
-                             int32_t* cand_col, double* cand_coeff, double* cand_rc,
-                             hipStream_t s) {
-  gather_candidates_kernel<<<grid_for(max_slots), 256, 0, s>>>(slots, num_slots, list,
-                                                               list_coeff, rc, cand_col,
-                                                               cand_coeff, cand_rc);
   return hipGetLastError();
 }
 

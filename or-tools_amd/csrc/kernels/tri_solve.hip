@@ -115,6 +115,26 @@ __device__ __forceinline__ void tri_compute(const TriSolveArgs& a, double* y, in
   y[k] = a.diag != nullptr ? sum / r.d : sum;
 }
 
+// Zero-copy staging in and out of device-visible host memory (coalesced
+// PCIe reads and writes, inside the captured plan: no copy engine calls).
+__global__ __launch_bounds__(256) void tri_copy_in_kernel(TriSolveArgs a) {
+  const int n = a.num_rows - a.first_col;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    a.x[a.first_col + i] = a.host_x[a.first_col + i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *a.top = *reinterpret_cast<const int*>(a.host_x + a.num_rows);
+  }
+}
+
+__global__ __launch_bounds__(256) void tri_copy_out_kernel(TriSolveArgs a) {
+  const int end = *a.top + 1;
+  for (int i = a.first_col + blockIdx.x * blockDim.x + threadIdx.x; i < end;
+       i += gridDim.x * blockDim.x) {
+    a.host_x[i] = a.x[i];
+  }
+}
+
 // y[k] = x[row(k)] for every position (listed or not).
 __global__ __launch_bounds__(256) void tri_gather_kernel(TriSolveArgs a) {
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.num_pos;
@@ -197,16 +217,127 @@ __global__ __launch_bounds__(kTriThreads) void tri_levels_cu_kernel(TriSolveArgs
   }
 }
 
+// ---------------------------------------------------------------------------
+// Dependency-driven ("sync-free") variant: one thread per listed output, all
+// resident at once, no level barriers and no per-level launches. An output's
+// slot in y holds kTriPending until its final value is stored there, so the
+// value is its own ready flag; a thread waits for the entries it reads, then
+// computes with the same arithmetic as tri_compute and stores. Waits only go
+// to lower positions (earlier levels), which belong to the same or earlier
+// workgroups, dispatched first: every wait ends. The wait, the computation
+// and the store sit in one loop body, so a lane whose reader shares its wave
+// stores before the wave spins again.
+constexpr unsigned long long kTriPending = 0x7ff0deadbeef0001ull;  // a NaN no arithmetic makes
+constexpr int kTriMaxSpins = 1 << 21;  // about a second
+
+__device__ __forceinline__ bool tri_pending(double v) {
+  return static_cast<unsigned long long>(__double_as_longlong(v)) == kTriPending;
+}
+
+// y[k] = x[row(k)], or "pending" for the outputs this solve computes.
+__global__ __launch_bounds__(256) void tri_init_kernel(TriSolveArgs a) {
+  const int top = *a.top;
+  const double pending = __longlong_as_double(static_cast<long long>(kTriPending));
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.num_pos;
+       k += gridDim.x * blockDim.x) {
+    const int row = a.pos_row[k];
+    a.y[k] = (k < a.num_work && row <= top) ? pending : a.x[row];
+  }
+}
+
+__device__ __forceinline__ int tri_entry_pos(const TriSolveArgs& a, const int4& e, int n, int j) {
+  if (n > 4) return a.ovf_pos[e.x + j];
+  return j == 0 ? e.x : j == 1 ? e.y : j == 2 ? e.z : e.w;
+}
+
+__global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= a.num_work) return;
+  const int top = *a.top;
+  TriRec r;
+  tri_load(a, k, a.num_work, top, &r);
+  if (r.row > top) return;  // not computed: y[k] already holds x[row]
+  double* y = a.y;
+  int ready = 0;  // entries [0, ready) are known final
+  bool done = false;
+  int spins = 0;
+  while (!done) {
+    for (; ready < r.n; ++ready) {
+      if (tri_pending(load_final(y, tri_entry_pos(a, r.e, r.n, ready)))) break;
+    }
+    if (ready == r.n) {
+      double sum = a.x[r.row];
+      if (r.n <= 4) {
+        const int n = r.n;
+        const double y0 = n > 0 ? load_final(y, r.e.x) : 0.0;
+        const double y1 = n > 1 ? load_final(y, r.e.y) : 0.0;
+        const double y2 = n > 2 ? load_final(y, r.e.z) : 0.0;
+        const double y3 = n > 3 ? load_final(y, r.e.w) : 0.0;
+        if (n == 4) {
+          sum -= r.v[0] * y0 + r.v[1] * y1 + r.v[2] * y2 + r.v[3] * y3;
+        } else {
+          if (n > 0) sum -= r.v[0] * y0;
+          if (n > 1) sum -= r.v[1] * y1;
+          if (n > 2) sum -= r.v[2] * y2;
+        }
+      } else {
+        sum = subtract_overflow(a, y, sum, r.e.x, r.e.x + r.n);
+      }
+      const double out = a.diag != nullptr ? sum / r.d : sum;
+      a.x[r.row] = out;  // the scatter, fused
+      __hip_atomic_store(y + k, out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      done = true;
+    } else if (++spins > kTriMaxSpins) {
+      // Bounded wait (never expected): report and leave, the host fails loudly.
+      if (a.fail != nullptr) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      done = true;
+    } else {
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+}
+
 }  // namespace milp_kernels
 
 namespace milp_launch {
 
+hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, hipStream_t s) {
+  if (args.num_work <= 0) return hipSuccess;
+  const int row_blocks =
+      std::max(1, std::min(1024, (args.num_rows - args.first_col + 255) / 256));
+  hipError_t e;
+  if (args.host_x != nullptr) {
+    milp_kernels::tri_copy_in_kernel<<<row_blocks, 256, 0, s>>>(args);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const int pos_blocks = std::max(1, std::min(1024, (args.num_pos + 255) / 256));
+  milp_kernels::tri_init_kernel<<<pos_blocks, 256, 0, s>>>(args);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // One thread per listed output: every workgroup resident (100k outputs =
+  // 391 workgroups of 256 on 256 CUs).
+  milp_kernels::tri_syncfree_kernel<<<(args.num_work + 255) / 256, 256, 0, s>>>(args);
+  e = hipGetLastError();
+  if (e != hipSuccess || args.host_x == nullptr) return e;
+  milp_kernels::tri_copy_out_kernel<<<row_blocks, 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
 hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, const int* segments,
                                int num_segments, hipStream_t s) {
   if (args.num_work <= 0) return hipSuccess;
+  const int row_blocks =
+      std::max(1, std::min(1024, (args.num_rows - args.first_col + 255) / 256));
+  hipError_t e;
+  if (args.host_x != nullptr) {
+    milp_kernels::tri_copy_in_kernel<<<row_blocks, 256, 0, s>>>(args);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   const int pos_blocks = std::min(1024, (args.num_pos + 255) / 256);
   milp_kernels::tri_gather_kernel<<<pos_blocks, 256, 0, s>>>(args);
-  hipError_t e = hipGetLastError();
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   for (int i = 0; i < num_segments; ++i) {
     const int lb = segments[2 * i];
@@ -222,6 +353,10 @@ hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, const int
   }
   const int work_blocks = std::min(1024, (args.num_work + 255) / 256);
   milp_kernels::tri_scatter_kernel<<<work_blocks, 256, 0, s>>>(args);
+  if (args.host_x == nullptr) return hipGetLastError();
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  milp_kernels::tri_copy_out_kernel<<<row_blocks, 256, 0, s>>>(args);
   return hipGetLastError();
 }
 

@@ -24,15 +24,19 @@ GROUPS = {  # HIP kernel name fragment -> engine kernel id (bench.py names)
     "dense_dot_kernel<4,": "update_row", "column_dot_kernel<4,": "update_row",
     "row_wise_update_kernel": "update_row", "row_wise_by_column_kernel": "update_row",
     "tag_rows_kernel": "update_row", "row_wise_full_rows_kernel": "update_row",
-    "dual_ratio_bound_kernel": "dual_ratio", "dual_ratio_flags_kernel": "dual_ratio",
+    "compact_flags_kernel": "update_row", "compact_small_kernel": "update_row",
+    "dual_ratio_bound_kernel": "dual_ratio", "dual_ratio_select_kernel": "dual_ratio",
     "dual_ratio_keys_kernel": "dual_ratio", "dual_flip_walk_kernel": "dual_ratio",
-    "gather_candidates_kernel": "dual_ratio", "boxed_flips_kernel": "dual_ratio",
+    "boxed_flips_kernel": "dual_ratio",
     "update_reduced_costs_kernel": "rc_update",
     "dense_dot_kernel<2,": "primal_norms", "column_dot_kernel<2,": "primal_norms",
     "row_sum_kernel": "spmv_rows", "column_squared_norm_kernel": "col_norms",
     # one-launch kernels of small LPs (N <= 8192)
     "row_wise_small_kernel": "update_row", "row_wise_small_by_column_kernel": "update_row",
     "column_wise_small_kernel": "update_row", "list_dots_small_kernel": "primal_norms",
+    # dense U solve of FTRAN (tri_solve.hip): permutes in/out, wide levels, CU segments
+    "tri_gather_kernel": "tri_solve", "tri_scatter_kernel": "tri_solve",
+    "tri_level_grid_kernel": "tri_solve", "tri_levels_cu_kernel": "tri_solve",
 }
 
 
@@ -54,6 +58,7 @@ PRIMARY = {
                      ["column_dot_kernel<2,"]],
     "spmv_rows": [["row_sum_kernel"]],
     "col_norms": [["column_squared_norm_kernel"]],
+    "tri_solve": [["tri_gather_kernel"]],
 }
 
 

@@ -2,10 +2,13 @@
 kernels/tri_solve.hip) vs the CPU oracle, which runs Glop's host loop
 TriangularMatrix::TransposeLowerSolve (sparse.cc:899-955).
 
-MILP_DEVICE_SOLVE=force sends every dense U solve of the solver's thread to
-the single-CU level-scheduled kernel at test size; the engine must still
-reproduce the oracle bit for bit (basis, statuses, values, iterations) and
-its deterministic time must not move."""
+MILP_DEVICE_SOLVE=force sends every dense U solve (the solver's thread and
+the tau worker) to the device at test size; the engine must still reproduce
+the oracle bit for bit (basis, statuses, values, iterations) and its
+deterministic time must not move. Three device variants: the default
+readiness-driven single launch (tri_syncfree_kernel) with zero-copy staging,
+the level-scheduled plan (MILP_TRI_SYNCFREE=0), and the level plan with
+copy-engine staging (MILP_TRI_MAPPED=0)."""
 import pytest
 
 from mi_glop import abi, engine
@@ -35,13 +38,23 @@ def _cases():
     return cases
 
 
+VARIANTS = {
+    "syncfree": {},
+    "levels": {"MILP_TRI_SYNCFREE": "0"},
+    "levels_copies": {"MILP_TRI_SYNCFREE": "0", "MILP_TRI_MAPPED": "0"},
+}
+
+
+@pytest.mark.parametrize("variant", list(VARIANTS))
 @pytest.mark.parametrize("case", _cases(), ids=lambda c: c[0])
-def test_device_u_solve_parity(case, monkeypatch):
+def test_device_u_solve_parity(case, variant, monkeypatch):
     name, build, dual = case
     lp = build()
     p = abi.default_params(use_dual_simplex=dual, max_number_of_iterations=4000)
     monkeypatch.setenv("MILP_DEVICE_SOLVE", "off")
     _, _, _, r_host = parity_util.solve_both(lp, p, _handle)
+    for k, v in VARIANTS[variant].items():
+        monkeypatch.setenv(k, v)
     monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
     o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
     parity_util.compare(o, ro, g, rg, lp)
@@ -54,9 +67,10 @@ def test_device_u_solve_parity(case, monkeypatch):
 @pytest.mark.parametrize("device_dual", ["off", "force"])
 @pytest.mark.parametrize("async_solves", ["off", "force"])
 def test_device_u_solve_with_async_tau_and_device_dual(device_dual, async_solves, monkeypatch):
-    """The tau FTRAN keeps the host loop on the factorization's worker while
-    the solver's thread sends its dense U solves to the device; with the
-    dual device mode on or off, the results are the oracle's."""
+    """The tau FTRAN's dense U solves run on the device from the
+    factorization's worker (own stream, own graph) while the solver's thread
+    sends its own; with the dual device mode on or off, the results are the
+    oracle's."""
     monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
     monkeypatch.setenv("MILP_DEVICE_DUAL", device_dual)
     monkeypatch.setenv("MILP_ASYNC_SOLVES", async_solves)
