@@ -178,7 +178,8 @@ enum {
   MI_K_READBACK = 9,    /* update-row list download / single-coefficient reads */
   MI_K_TRI_SOLVE_TAU = 10, /* the same dense U solve for the tau FTRAN on the
                               factorization's worker thread (dual_edge_norms.cc:134-141) */
-  MI_K_COUNT = 11
+  MI_K_TRI_SOLVE_L = 11,   /* dense L solve of FTRAN (sparse.cc:793-812) on the device */
+  MI_K_COUNT = 12
 };
 
 void mi_glop_params_default(mi_glop_params* p);

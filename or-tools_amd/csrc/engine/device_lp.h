@@ -7,6 +7,7 @@
 #define MILP_DEVICE_LP_H_
 
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -23,6 +24,9 @@ struct ScanState;
 namespace milp {
 
 class CompactSparseMatrix;
+
+// Records the device operation under way (MILP_WATCHDOG_S diagnostics).
+void DeviceOp(const char* what);
 
 struct DeviceError : public std::runtime_error {
   explicit DeviceError(const std::string& s) : std::runtime_error(s) {}
@@ -79,7 +83,7 @@ class DeviceLp : public DeviceSolver {
                std::vector<double>* rc, const std::vector<double>* w = nullptr,
                std::vector<double>* list_dots = nullptr);
   // Changes whenever the device-side update-row list (and its flags) changes.
-  uint64_t list_epoch() const { return list_epoch_; }
+  uint64_t list_epoch() const;
 
   // --- 1 + ||a_j||^2 for relevant j (identity basis) -------------------
   void ColumnSquaredNorms(std::vector<double>* out);
@@ -122,28 +126,64 @@ class DeviceLp : public DeviceSolver {
     void* ptr = nullptr;
     size_t bytes = 0;
   };
-  struct TriContext {  // one solving thread's stream, values and graph
+  // Device buffers of a schedule (staged in this order).
+  enum TriBuf {
+    kTriLevels, kTriRecRow, kTriRecN, kTriRecEntry, kTriRecValue, kTriDiag, kTriOvfPos,
+    kTriOvfValue, kTriPosRow, kTriNumStaged
+  };
+  // One triangular matrix's level schedule and records, rebuilt when the
+  // factorization key changes. 0: U (TransposeLowerSolve of U^T), 1: L.
+  enum TriMatrix { kTriU = 0, kTriL = 1, kTriNumMatrices = 2 };
+  struct TriSchedule {
+    uint64_t key = 0;
+    bool ok = false;
+    bool sequential = false;  // L: single subtractions, zero values skipped
+    bool ones = true;
+    int rows = 0, first_col = 0, work = 0, pos = 0, levels = 0;
+    std::vector<int32_t> level_width;
+    std::vector<int> segments;        // tri_transpose_lower launch plan
+    TriBuffer buf[kTriNumStaged];
+    std::vector<int32_t> rows_upto;   // listed outputs with row <= r
+    std::vector<int64_t> entries_upto;  // their entries
+    int max_entries = 0;
+    int rows_over[3] = {0, 0, 0};     // outputs with > 4, 16, 64 entries
+  };
+  struct TriContext {  // one solving thread's stream, values and graphs
     void* stream = nullptr;
     TriBuffer x, y, top;         // rows, positions, the solve's top row
     double* h_x = nullptr;       // pinned, mapped staging of x (+ the top row)
     double* m_x = nullptr;       // its device-visible address
     size_t h_x_elems = 0;
     int* h_top = nullptr;        // pinned
-    void* graph_exec = nullptr;  // hipGraphExec_t of the launch plan
-    uint64_t graph_key = 0;      // the schedule it was captured for
+    void* graph_exec[kTriNumMatrices] = {nullptr, nullptr};  // hipGraphExec_t per matrix
+    uint64_t graph_key[kTriNumMatrices] = {0, 0};            // schedule captured for
     void* ev[2] = {nullptr, nullptr};
   };
   // TriangularMatrix::TransposeLowerSolve (sparse.cc:899-955) on one CU,
   // bit-identical. MILP_DEVICE_SOLVE=off|force|auto (auto: m >= 16384).
   bool TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
                            std::vector<double>* x) override;
+  bool LowerSolve(const TriangularMatrix& lower, uint64_t key,
+                  std::vector<double>* x) override;
 
   // Accounting (roofline): launches, algorithmic bytes, HIP-event time.
-  void SetTiming(bool on) { timing_ = on; }
+  void SetTiming(bool on);
   const mi_lp_kernel_stats& stats();  // collects the pending event timings
   void ResetStats();
   void Synchronize();
   int dense_columns() const { return nd_; }
+
+  // --- column shards ----------------------------------------
+  // MILP_SHARDS=S > 1 splits the columns of [A | I] into S contiguous blocks
+  // (64-column aligned, balanced by entries), each owned by a DeviceLp of its
+  // own on MILP_SHARD_DEVICES (a comma list; default: this handle's device,
+  // the "virtual" split). Every per-column operation (pricing, update row,
+  // list dots, the dual device mode) runs shard by shard and the results are
+  // joined in column order: the bound of the dual ratio test is a min over
+  // shards, the candidates and update-row lists a concatenation. Row sums,
+  // column norms and the triangular solves stay on this handle (full copy).
+  int num_shards() const { return shards_.empty() ? 1 : static_cast<int>(shards_.size()); }
+  int shard_begin(int s) const { return shard_begin_[s]; }
 
  private:
   template <typename T>
@@ -155,6 +195,46 @@ class DeviceLp : public DeviceSolver {
   void* TakeEvent();
   void DrainTimings();
   milp_kernels::ScanState NextScan();
+  void CheckScan();
+  int* h_scan_fail_ = nullptr;  // mapped: a look-back wait ran out
+  int* m_scan_fail_ = nullptr;
+  int ShardOf(int col) const;
+  void CreateShards();
+  DeviceLp& Shard(int s);  // sets the shard's device current
+  void ShardedUpload(const CompactSparseMatrix& csc);
+  void ShardedSetMask(Mask which, const uint64_t* words, int num_words);
+  void ShardedUpdateRowColumnWise(const std::vector<double>& rho, double drop,
+                                  int64_t relevant_entries, const std::vector<double>* w);
+  void ShardedUpdateRowRowWise(const std::vector<int>& filtered_rows,
+                               const std::vector<double>& rho, int algorithm, double drop);
+  void ShardedFetchUpdateRow(std::vector<int>* positions, std::vector<double>* values);
+  double ShardedReadCoefficient(int col);
+  void ShardedListDotsOverUpdateRow(const std::vector<double>& v, std::vector<double>* out);
+  void ShardedListDots(const std::vector<int>& cols, const std::vector<double>& v,
+                       std::vector<double>* out);
+  void ShardedPricing(const std::vector<double>& c, const std::vector<double>& y,
+                      std::vector<double>* rc, const std::vector<double>* w,
+                      std::vector<double>* list_dots);
+  void ShardedDualBegin(const std::vector<double>& rc, const std::vector<uint8_t>& colbits,
+                        const std::vector<double>& bound_diff);
+  void ShardedDualSetColBits(const std::vector<int32_t>& cols, const std::vector<uint8_t>& bits);
+  void ShardedDualTakePricedReducedCosts();
+  void ShardedDualDownloadReducedCosts(std::vector<double>* rc);
+  void ShardedDualSetReducedCost(int col, double value);
+  void ShardedDualRatioCandidates(double sign, double threshold, double harris_tolerance,
+                                  double minimum_delta, double variation_magnitude,
+                                  DualCandidates* out);
+  void ShardedDualUpdateReducedCosts(double mult, int leaving_col, double leaving_value,
+                                     int entering_col);
+  void ShardedDualBoxedFlips(const std::vector<int>* cols, double threshold,
+                             std::vector<uint8_t>* flags);
+  void ShardedStats();
+  void FlushOwnMasks();
+  bool is_shard_ = false;
+  std::vector<std::unique_ptr<DeviceLp>> shards_;
+  std::vector<int> shard_begin_;
+  bool own_mask_dirty_[kNumMasks] = {false, false, false};
+  mi_lp_kernel_stats agg_stats_{};
   void Compact(int n);  // flags_ -> list_ (ascending) + coefficients, async
   void NextRowTag();
   void UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
@@ -172,14 +252,21 @@ class DeviceLp : public DeviceSolver {
   void LaunchColumnDots(int mode, const double* d_y, const double* d_c, double* d_out,
                         const double* d_y2 = nullptr, double* d_out2 = nullptr);
   void Check(int err, const char* what);
-  void BuildTriSchedule(const TriangularMatrix& t, uint64_t key, void* stream);
+  // Gather lists of the outputs c in [fni, nc): entries (dependency row,
+  // value) of output c at [st[c], st[c+1]) of idx/val, evaluated from the end
+  // when `reverse`. Dependencies are rows > c (descending) or < c.
+  void BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, const double* diag,
+                        const int64_t* st, const int32_t* idx, const double* val, bool reverse,
+                        bool descending, bool sequential, uint64_t key, void* stream);
+  bool TriSolve(int which, const TriangularMatrix& t, uint64_t key, std::vector<double>* x);
   void TriReserve(TriBuffer* b, size_t bytes);
-  void PrepareTriContext(int slot, int rows);
-  milp_kernels::TriSolveArgs TriArgs(const TriContext& c) const;
-  void TriCopyIn(const TriContext& c);
-  void TriCopyOut(const TriContext& c);
-  void EnqueueTriKernels(const milp_kernels::TriSolveArgs& a, void* stream);
-  void CaptureTriGraph(TriContext* c);
+  void PrepareTriContext(int slot, int rows, int pos);
+  milp_kernels::TriSolveArgs TriArgs(const TriSchedule& s, const TriContext& c) const;
+  void TriCopyIn(const TriSchedule& s, const TriContext& c);
+  void TriCopyOut(const TriSchedule& s, const TriContext& c);
+  void EnqueueTriKernels(const TriSchedule& s, const milp_kernels::TriSolveArgs& a,
+                         void* stream);
+  void CaptureTriGraph(int which, TriContext* c);
   void FreeTriBuffers();
 
   int device_ = -1;
@@ -358,43 +445,29 @@ class DeviceLp : public DeviceSolver {
   int32_t* d_sorted_slots_ = nullptr;
   void* d_sort_temp_ = nullptr;
   size_t sort_temp_bytes_ = 0;
-  // dense triangular solve (device_solve.hip): the level-ordered schedule of
-  // the last factorization's matrix, rebuilt when its key changes.
+  // dense triangular solves (device_solve.hip): the level-ordered schedules
+  // of the last factorization's U and L, rebuilt when its key changes.
   int tri_mode_ = 0;  // 0 auto, 1 force, 2 off
   int tri_min_rows_ = 16384;
-  uint64_t tri_key_ = 0;
-  bool tri_ok_ = false;
-  int tri_rows_ = 0;
-  int tri_first_col_ = 0;
-  int tri_work_ = 0;
-  bool tri_ones_ = true;
-  int tri_levels_ = 0;
-  std::vector<int32_t> tri_level_width_;
-  std::vector<int> tri_segments_;  // tri_transpose_lower launch plan
-  int tri_wide_level_ = 600;       // MILP_TRI_WIDE: wider levels run over the chip
+  int tri_wide_level_ = 600;  // MILP_TRI_WIDE: wider levels run over the chip
   int tri_debug_left_ = 0;
-  bool tri_graph_ = true;  // MILP_TRI_GRAPH
-  bool tri_tau_ = true;    // MILP_TRI_TAU
-  bool tri_mapped_ = true; // MILP_TRI_MAPPED: zero-copy staging inside the plan
+  bool tri_graph_ = true;     // MILP_TRI_GRAPH
+  bool tri_tau_ = true;       // MILP_TRI_TAU
+  bool tri_mapped_ = true;    // MILP_TRI_MAPPED: zero-copy staging inside the plan
   bool tri_syncfree_ = true;  // MILP_TRI_SYNCFREE: readiness-driven single launch
-  int tri_max_entries_ = 0;   // schedule statistics (MILP_TRI_DEBUG)
-  int tri_rows_over_[3] = {0, 0, 0};
+  bool tri_lower_ = true;     // MILP_TRI_LOWER: the L solves too
+  int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
   uint64_t* d_tri_clock_ = nullptr;
-  // Device buffers of the schedule (staged in this order).
-  enum TriBuf {
-    kTriLevels, kTriRecRow, kTriRecN, kTriRecEntry, kTriRecValue, kTriDiag, kTriOvfPos,
-    kTriOvfValue, kTriPosRow, kTriNumStaged
-  };
-  TriBuffer tri_buf_[kTriNumStaged];
-  int tri_pos_ = 0;
+  TriSchedule tri_sched_[kTriNumMatrices];
   // Per solving thread: 0 = the solver's thread (the handle's stream),
   // 1 = BasisFactorization's tau worker (its own stream).
   TriContext tri_ctx_[2];
-  std::mutex tri_mu_;  // schedule (re)build
+  std::mutex tri_mu_;  // schedule (re)builds and graph captures
   void* h_tri_stage_ = nullptr;  // pinned staging of the schedule upload
   size_t tri_stage_bytes_ = 0;
-  std::vector<int32_t> tri_rows_upto_;     // work rows with output row <= r
-  std::vector<int64_t> tri_entries_upto_;  // their entries
+  std::vector<int64_t> tri_lt_starts_;  // L's rows (gather lists), built per factorization
+  std::vector<int32_t> tri_lt_idx_;
+  std::vector<double> tri_lt_val_;
 };
 
 }  // namespace milp

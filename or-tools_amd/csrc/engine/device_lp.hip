@@ -3,6 +3,11 @@
 #include "host_pool.h"
 
 #include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <thread>
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <chrono>
@@ -39,6 +44,10 @@ void DeviceLp::Check(int err, const char* what) {
   }
 }
 
+namespace {
+void StartWatchdog();
+}  // namespace
+
 DeviceLp::~DeviceLp() {
   if (device_ >= 0) (void)hipSetDevice(device_);
   if (stream_ != nullptr) (void)hipStreamSynchronize(S(stream_));
@@ -52,6 +61,7 @@ DeviceLp::~DeviceLp() {
   if (h_pin_count_) (void)hipHostFree(h_pin_count_);
   if (h_map_) (void)hipHostFree(h_map_);
   if (h_small_in_) (void)hipHostFree(h_small_in_);
+  if (h_scan_fail_) (void)hipHostFree(h_scan_fail_);
   for (void* p : {static_cast<void*>(h_cand_col_), static_cast<void*>(h_cand_coeff_),
                   static_cast<void*>(h_cand_rc_), static_cast<void*>(h_dual_counts_),
                   static_cast<void*>(h_cb_cols_), static_cast<void*>(h_cb_bits_),
@@ -125,6 +135,10 @@ void DeviceLp::Init(int device) {
   if (const char* v = std::getenv("MILP_TRI_TAU")) tri_tau_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_MAPPED")) tri_mapped_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_SYNCFREE")) tri_syncfree_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_TRI_LOWER")) tri_lower_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_TRI_MIN_WIDTH")) tri_min_width_ = std::atoi(v);
+  CreateShards();
+  StartWatchdog();
 }
 
 template <typename T>
@@ -140,6 +154,43 @@ void DeviceLp::Upload(void* dst, const void* src, size_t bytes) {
   Check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream_)), "H2D");
 }
 
+// MILP_WATCHDOG_S=k: a thread that reports the last device operation when
+// none has started or finished for k seconds (hang diagnosis on the GPU box).
+std::atomic<const char*> g_dev_op{"none"};
+std::atomic<uint64_t> g_dev_ops{0};
+
+void DeviceOp(const char* what) {
+  g_dev_op.store(what, std::memory_order_relaxed);
+  g_dev_ops.fetch_add(1, std::memory_order_relaxed);
+}
+
+namespace {
+void StartWatchdog() {
+  static std::once_flag once;
+  std::call_once(once, []() {
+    const char* e = std::getenv("MILP_WATCHDOG_S");
+    if (e == nullptr || std::atoi(e) <= 0) return;
+    const int secs = std::atoi(e);
+    std::thread([secs]() {
+      uint64_t last = ~0ull;
+      int still = 0;
+      while (true) {
+        std::this_thread::sleep_for(std::chrono::seconds(1));
+        const uint64_t n = g_dev_ops.load(std::memory_order_relaxed);
+        still = n == last ? still + 1 : 0;
+        last = n;
+        if (still == secs) {
+          std::fprintf(stderr, "[watchdog] no device operation for %d s; last: %s (#%llu)\n",
+                       secs, g_dev_op.load(std::memory_order_relaxed),
+                       static_cast<unsigned long long>(n));
+          std::fflush(stderr);
+        }
+      }
+    }).detach();
+  });
+}
+}  // namespace
+
 void DeviceLp::Download(void* dst, const void* src, size_t bytes) {
   if (bytes == 0) return;
   Check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, S(stream_)), "D2H");
@@ -147,18 +198,24 @@ void DeviceLp::Download(void* dst, const void* src, size_t bytes) {
 }
 
 void DeviceLp::Synchronize() {
+  DeviceOp("Synchronize");
   Check(hipStreamSynchronize(S(stream_)), "sync");
+  DeviceOp("Synchronize done");
   small_inflight_ = false;
+  for (auto& d : shards_) d->Synchronize();
 }
 
 void DeviceLp::ResetStats() {
   DrainTimings();
   std::memset(&stats_, 0, sizeof(stats_));
+  for (auto& d : shards_) d->ResetStats();
 }
 
 const mi_lp_kernel_stats& DeviceLp::stats() {
   DrainTimings();
-  return stats_;
+  if (shards_.empty()) return stats_;
+  ShardedStats();
+  return agg_stats_;
 }
 
 // Kernel timing: every logical launch is bracketed by two events recorded on
@@ -190,7 +247,12 @@ void DeviceLp::DrainTimings() {
   ev_pending_.clear();
 }
 
-void DeviceLp::BeginKernel(int /*id*/) {
+void DeviceLp::BeginKernel(int id) {
+  static const char* const kNames[] = {"pricing", "update_row", "primal_norms", "rc_update",
+                                       "tri_solve", "col_norms", "spmv_rows", "single_row",
+                                       "dual_ratio", "readback", "tri_solve_tau", "tri_solve_l",
+                                       "?", "?", "?", "?"};
+  DeviceOp(kNames[id & 15]);
   if (!timing_) return;
   if (ev_open_ == nullptr) ev_open_ = TakeEvent();
   Check(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_open_), S(stream_)), "ev");
@@ -280,6 +342,14 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
         "memset");
   Check(hipMemsetAsync(d_scan_ticket_, 0, 2 * sizeof(unsigned int), S(stream_)), "memset");
   scan_epoch_ = 0;
+  if (h_scan_fail_ == nullptr) {
+    Check(hipHostMalloc(reinterpret_cast<void**>(&h_scan_fail_), 64, hipHostMallocMapped),
+          "hipHostMalloc (mapped)");
+    void* d = nullptr;
+    Check(hipHostGetDevicePointer(&d, h_scan_fail_, 0), "mapped pointer");
+    m_scan_fail_ = static_cast<int*>(d);
+  }
+  *h_scan_fail_ = 0;
   if (h_pin_i_) (void)hipHostFree(h_pin_i_);
   if (h_pin_d_) (void)hipHostFree(h_pin_d_);
   if (h_pin_d2_) (void)hipHostFree(h_pin_d2_);
@@ -357,6 +427,7 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   ++list_epoch_;
   BuildDenseBlock();
   Synchronize();
+  if (!shards_.empty()) ShardedUpload(csc);
 }
 
 // Full structural columns go to the value-only dense block (8 B per entry
@@ -448,6 +519,7 @@ void DeviceLp::LaunchColumnDots(int mode, const double* d_y, const double* d_c,
 }
 
 void DeviceLp::SetMask(Mask which, const uint64_t* words, int num_words) {
+  if (!shards_.empty()) return ShardedSetMask(which, words, num_words);
   std::vector<uint64_t>& h = h_masks_[which];
   if (num_words != mask_words_) throw DeviceError("mask size mismatch");
   if (std::memcmp(h.data(), words, num_words * sizeof(uint64_t)) == 0) return;
@@ -502,6 +574,7 @@ void DeviceLp::Compact(int n) {
 
 void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
                                    int64_t relevant_entries, const std::vector<double>* w) {
+  if (!shards_.empty()) return ShardedUpdateRowColumnWise(rho, drop, relevant_entries, w);
   CallTimer timer(&stats_, MI_K_UPDATE_ROW);
   small_dots_mapped_ = false;
   if (small_fused_enabled_ && h_small_in_ != nullptr && nd_ == 0 &&
@@ -592,6 +665,7 @@ void DeviceLp::UpdateRowColumnWiseSmall(const std::vector<double>& rho, double d
 void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
                                 const std::vector<double>& rho, int algorithm,
                                 double drop) {
+  if (!shards_.empty()) return ShardedUpdateRowRowWise(filtered_rows, rho, algorithm, drop);
   CallTimer timer(&stats_, algorithm == 0 ? MI_K_SINGLE_ROW : MI_K_UPDATE_ROW);
   const int k = static_cast<int>(filtered_rows.size());
   fused_ready_ = false;
@@ -780,9 +854,11 @@ void DeviceLp::NextRowTag() {
 }
 
 void DeviceLp::FetchUpdateRow(std::vector<int>* positions, std::vector<double>* values) {
+  if (!shards_.empty()) return ShardedFetchUpdateRow(positions, values);
   CallTimer timer(&stats_, MI_K_READBACK);
   if (mapped_result_) {
     Synchronize();
+    CheckScan();
     const int n = *h_map_count_;
     if (n < 0 || n > n_total_) throw DeviceError("bad update-row count");
     list_count_ = n;
@@ -857,6 +933,7 @@ void DeviceLp::CopyHost(void* dst, const void* src, size_t bytes) {
 }
 
 double DeviceLp::ReadCoefficient(int col) {
+  if (!shards_.empty()) return ShardedReadCoefficient(col);
   CallTimer timer(&stats_, MI_K_READBACK);
   double v = 0.0;
   Download(h_pin_d2_, d_coeff_ + col, sizeof(double));
@@ -865,6 +942,7 @@ double DeviceLp::ReadCoefficient(int col) {
 }
 
 void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<double>* out) {
+  if (!shards_.empty()) return ShardedListDotsOverUpdateRow(v, out);
   CallTimer timer(&stats_, MI_K_PRIMAL_NORMS);
   if (list_count_ < 0) throw DeviceError("update-row list used before FetchUpdateRow");
   const int n = list_count_;
@@ -918,6 +996,7 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
 
 void DeviceLp::ListDots(const std::vector<int>& cols, const std::vector<double>& v,
                         std::vector<double>* out) {
+  if (!shards_.empty()) return ShardedListDots(cols, v, out);
   CallTimer timer(&stats_, MI_K_PRIMAL_NORMS);
   fused_ready_ = false;  // d_out_n_ is reused below
   const int n = static_cast<int>(cols.size());
@@ -948,6 +1027,7 @@ void DeviceLp::ListDots(const std::vector<int>& cols, const std::vector<double>&
 void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& y,
                        std::vector<double>* rc, const std::vector<double>* w,
                        std::vector<double>* list_dots) {
+  if (!shards_.empty()) return ShardedPricing(c, y, rc, w, list_dots);
   CallTimer timer(&stats_, MI_K_PRICING);
   fused_ready_ = false;  // d_out_n_ is reused below
   const bool fused = (w != nullptr);
@@ -992,6 +1072,7 @@ void DeviceLp::Pricing(const std::vector<double>& c, const std::vector<double>& 
 }
 
 void DeviceLp::ColumnSquaredNorms(std::vector<double>* out) {
+  if (!shards_.empty()) FlushOwnMasks();
   CallTimer timer(&stats_, MI_K_COL_NORMS);
   fused_ready_ = false;  // d_out_n_ is reused below
   FlushRelevantMask();
@@ -1007,6 +1088,7 @@ void DeviceLp::ColumnSquaredNorms(std::vector<double>* out) {
 
 void DeviceLp::RowSums(const std::vector<double>& x, bool skip_basic, double sign,
                        std::vector<double>* out) {
+  if (!shards_.empty()) FlushOwnMasks();
   CallTimer timer(&stats_, MI_K_SPMV_ROWS);
   std::memcpy(h_pin_d_, x.data(), n_total_ * sizeof(double));
   Upload(d_vec_n_, h_pin_d_, n_total_ * sizeof(double));
@@ -1058,6 +1140,7 @@ void MappedResize(T** p, T** dev, size_t n) {
 
 void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_t>& colbits,
                          const std::vector<double>& bound_diff) {
+  if (!shards_.empty()) return ShardedDualBegin(rc, colbits, bound_diff);
   if (!dual_ready_) {
     d_rc_ = Alloc<double>(n_total_);
     d_colbits_ = Alloc<uint8_t>(n_total_);
@@ -1112,6 +1195,7 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
 
 void DeviceLp::DualSetColBits(const std::vector<int32_t>& cols,
                               const std::vector<uint8_t>& bits) {
+  if (!shards_.empty()) return ShardedDualSetColBits(cols, bits);
   const int n = static_cast<int>(cols.size());
   if (n == 0) return;
   if (n > n_total_) throw DeviceError("dual device mode: too many column changes");
@@ -1127,12 +1211,14 @@ void DeviceLp::DualSetColBits(const std::vector<int32_t>& cols,
 }
 
 void DeviceLp::DualTakePricedReducedCosts() {
+  if (!shards_.empty()) return ShardedDualTakePricedReducedCosts();
   Check(hipMemcpyAsync(d_rc_, d_out_n_, n_total_ * sizeof(double), hipMemcpyDeviceToDevice,
                        S(stream_)),
         "D2D");
 }
 
 void DeviceLp::DualDownloadReducedCosts(std::vector<double>* rc) {
+  if (!shards_.empty()) return ShardedDualDownloadReducedCosts(rc);
   CallTimer timer(&stats_, MI_K_READBACK);
   rc->resize(n_total_);
   Download(h_pin_d_, d_rc_, n_total_ * sizeof(double));
@@ -1140,12 +1226,20 @@ void DeviceLp::DualDownloadReducedCosts(std::vector<double>* rc) {
 }
 
 void DeviceLp::DualSetReducedCost(int col, double value) {
+  if (!shards_.empty()) return ShardedDualSetReducedCost(col, value);
   Check(milp_launch::set_double(d_rc_ + col, value, S(stream_)), "set rc");
 }
 
 milp_kernels::ScanState DeviceLp::NextScan() {
   if (++scan_epoch_ == 0) scan_epoch_ = 1;  // 0 is the zeroed status words' epoch
-  return milp_kernels::ScanState{d_scan_status_, d_scan_ticket_, scan_epoch_};
+  return milp_kernels::ScanState{d_scan_status_, d_scan_ticket_, scan_epoch_, m_scan_fail_};
+}
+
+void DeviceLp::CheckScan() {
+  if (*static_cast<volatile int*>(h_scan_fail_) != 0) {
+    throw DeviceError("ordered compaction: look-back wait timed out at tile " +
+                      std::to_string(*h_scan_fail_ - 1));
+  }
 }
 
 // Two launches: pass 1 (the bound B), then pass 2 fused with its ordered
@@ -1155,6 +1249,10 @@ milp_kernels::ScanState DeviceLp::NextScan() {
 void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_tolerance,
                                    double minimum_delta, double variation_magnitude,
                                    DualCandidates* out) {
+  if (!shards_.empty()) {
+    return ShardedDualRatioCandidates(sign, threshold, harris_tolerance, minimum_delta,
+                                      variation_magnitude, out);
+  }
   CallTimer timer(&stats_, MI_K_DUAL_RATIO);
   milp_kernels::DualRatioArgs a{};
   a.list = d_list_;
@@ -1185,6 +1283,7 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
   Check(milp_launch::dual_ratio_select(a, sel, NextScan(), S(stream_)), "dual ratio select");
   EndKernel(MI_K_DUAL_RATIO, 0.0);  // bytes added once the list length is known
   Synchronize();
+  CheckScan();
   const int k1 = h_dual_counts_[0];
   // Many breakpoints under B: tighten the bound by walking them in pop order.
   if (k1 > tighten_min_candidates_) {
@@ -1200,6 +1299,7 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
     Check(milp_launch::dual_ratio_select(a, sel, NextScan(), S(stream_)), "dual ratio select");
     EndKernel(MI_K_DUAL_RATIO, 0.0, /*count_launch=*/false);  // same logical launch
     Synchronize();
+    CheckScan();
   }
   const int k = h_dual_counts_[0];
   const int count = h_dual_counts_[1];
@@ -1222,6 +1322,9 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
 
 void DeviceLp::DualUpdateReducedCosts(double mult, int leaving_col, double leaving_value,
                                       int entering_col) {
+  if (!shards_.empty()) {
+    return ShardedDualUpdateReducedCosts(mult, leaving_col, leaving_value, entering_col);
+  }
   CallTimer timer(&stats_, MI_K_RC_UPDATE);
   BeginKernel(MI_K_RC_UPDATE);
   Check(milp_launch::update_reduced_costs(d_list_, d_out_list_, d_count_, n_total_, mult,
@@ -1234,6 +1337,7 @@ void DeviceLp::DualUpdateReducedCosts(double mult, int leaving_col, double leavi
 
 void DeviceLp::DualBoxedFlips(const std::vector<int>* cols, double threshold,
                               std::vector<uint8_t>* flags) {
+  if (!shards_.empty()) return ShardedDualBoxedFlips(cols, threshold, flags);
   CallTimer timer(&stats_, MI_K_DUAL_RATIO);
   const int n = cols != nullptr ? static_cast<int>(cols->size()) : n_total_;
   flags->assign(n, 0);

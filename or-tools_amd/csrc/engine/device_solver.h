@@ -1,7 +1,8 @@
 // Device substitutes for the dense triangular solves of the basis
-// factorization (lp_data/sparse.cc:899-955 TriangularMatrix::TransposeLowerSolve,
-// the row-oriented form Glop uses for the U solve of every FTRAN,
-// lu_factorization.cc:314-331). Implemented by DeviceLp; the LU code only
+// factorization's FTRAN (lu_factorization.cc:214-331): the U solve
+// (lp_data/sparse.cc:899-955 TriangularMatrix::TransposeLowerSolve, a gather
+// over U's rows) and the L solve (sparse.cc:793-812 LowerSolveStartingAt, a
+// column scatter, restated as a gather over L's rows). Implemented by DeviceLp; the LU code only
 // sees this interface so that lu.h stays free of HIP types.
 #ifndef MILP_DEVICE_SOLVER_H_
 #define MILP_DEVICE_SOLVER_H_
@@ -23,6 +24,11 @@ class DeviceSolver {
   // host (MILP_DEVICE_SOLVE and the size threshold decide).
   virtual bool TransposeLowerSolve(const TriangularMatrix& t, uint64_t key,
                                    std::vector<double>* x) = 0;
+  // x <- the result of lower.LowerSolveStartingAt(start, x) (sparse.cc:
+  // 793-812, the L solve of every dense FTRAN), bit for bit. Outputs below
+  // `start` receive nothing in that loop, so the device computes them all.
+  virtual bool LowerSolve(const TriangularMatrix& lower, uint64_t key,
+                          std::vector<double>* x) = 0;
 };
 
 }  // namespace milp

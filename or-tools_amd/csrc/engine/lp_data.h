@@ -512,6 +512,18 @@ class CompactSparseMatrix {
       }
     }
   }
+  // Columns [c0, c1) of input as a matrix of their own (a column shard of
+  // [A | I] for DeviceLp's split over several devices).
+  void PopulateColumnSlice(const CompactSparseMatrix& input, int c0, int c1) {
+    num_rows_ = input.num_rows_;
+    num_cols_ = c1 - c0;
+    const int64_t b = input.starts_[c0];
+    const int64_t e = input.starts_[c1];
+    starts_.resize(num_cols_ + 1);
+    for (int c = 0; c <= num_cols_; ++c) starts_[c] = input.starts_[c0 + c] - b;
+    rows_.assign(input.rows_.begin() + b, input.rows_.begin() + e);
+    coefficients_.assign(input.coefficients_.begin() + b, input.coefficients_.begin() + e);
+  }
   // sparse.cc:554-561
   void Reset(int num_rows) {
     num_rows_ = num_rows;

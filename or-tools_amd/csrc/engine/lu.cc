@@ -524,13 +524,22 @@ Fractional LuFactorization::DualEdgeSquaredNorm(int row) const {
   return ComputeSquaredNormAndResetToZero(non_zero_rows_, &DenseZeroScratch());
 }
 
+// The dense L loop of every FTRAN: on the device (same bits: outputs below
+// `start` receive nothing in the host loop either), else on the host.
+void LuFactorization::DenseLowerSolve(int start, std::vector<Fractional>* x) const {
+  if (device_solver_ == nullptr ||
+      !device_solver_->LowerSolve(lower_, factorization_key_, x)) {
+    lower_.LowerSolveStartingAt(start, x);
+  }
+}
+
 // lu_factorization.cc:200-212
 void LuFactorization::RightSolveLWithPermutedInput(const std::vector<Fractional>& /*a*/,
                                                    ScatteredVector* x) const {
   if (!is_identity_factorization_) {
     lower_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
     if (x->non_zeros.empty()) {
-      lower_.LowerSolve(&x->values);
+      DenseLowerSolve(0, &x->values);
     } else {
       lower_.HyperSparseSolve(&x->values, &x->non_zeros);
     }
@@ -553,7 +562,7 @@ void LuFactorization::RightSolveLInternal(const Column& b, ScatteredVector* x) c
   lower_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
   x->non_zeros_are_sorted = true;
   if (x->non_zeros.empty()) {
-    lower_.LowerSolveStartingAt(first_column_to_consider, &x->values);
+    DenseLowerSolve(first_column_to_consider, &x->values);
   } else {
     lower_.HyperSparseSolve(&x->values, &x->non_zeros);
   }
@@ -594,14 +603,14 @@ void LuFactorization::RightSolveLWithNonZeros(ScatteredVector* x) const {
   if (is_identity_factorization_) return;
   if (x->non_zeros.empty()) {
     PermuteWithScratchpad(row_perm_, &DenseZeroScratch(), &x->values);
-    lower_.LowerSolve(&x->values);
+    DenseLowerSolve(0, &x->values);
     return;
   }
   PermuteWithKnownNonZeros(row_perm_, &DenseZeroScratch(), &x->values, &x->non_zeros);
   lower_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
   x->non_zeros_are_sorted = true;
   if (x->non_zeros.empty()) {
-    lower_.LowerSolve(&x->values);
+    DenseLowerSolve(0, &x->values);
   } else {
     lower_.HyperSparseSolve(&x->values, &x->non_zeros);
   }

@@ -825,6 +825,8 @@ class LuFactorization {
   // Dense U solves of the solver's thread go to this device (engine
   // substitution, bit-identical; see device_solver.h).
   void SetDeviceSolver(DeviceSolver* d) { device_solver_ = d; }
+  // lower_.LowerSolveStartingAt(start, x), on the device when it takes it.
+  void DenseLowerSolve(int start, std::vector<Fractional>* x) const;
 
   // Exposed for the factor-structure parity tests.
   const TriangularMatrix& lower() const { return lower_; }

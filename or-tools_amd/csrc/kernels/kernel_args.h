@@ -243,6 +243,7 @@ struct ScanState {
   unsigned long long* status;  // per tile: epoch << 32 | flag << 30 | count
   unsigned int* ticket;        // [0] tile ticket, [1] finished workgroups
   unsigned int epoch;          // distinct per launch, never 0
+  int* fail;                   // host-visible: set if a look-back wait ran out
 };
 
 // The fused dual ratio filter + compaction writes here (mapped host memory).
@@ -297,6 +298,9 @@ struct TriSolveArgs {
   int first_col;
   int num_rows;
   int* fail;  // sync-free variant: set (host-visible) if a wait ran out
+  // 0: grouped sums (TransposeLowerSolve); 1: LowerSolve's order -- one
+  // subtraction per entry in list order, entries whose value is 0 skipped.
+  int sequential;
 };
 // The sync-free variant needs every workgroup resident: at most this many
 // outputs (512 workgroups of 256 threads, 2 per CU).

@@ -393,11 +393,18 @@ __device__ int scan_look_back(const ScanState& st, int tile, int count) {
   }
   scan_publish(st, tile, kScanAggregate, count);
   int prefix = 0;
+  const uint64_t t0 = wall_clock64();  // 100 MHz
   for (int j = tile - 1; j >= 0;) {
     const unsigned long long w =
         __hip_atomic_load(st.status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long flag = w & (3ull << 30);
     if ((w >> 32) != st.epoch || flag == 0) {
+      if (wall_clock64() - t0 > 20000000) {  // 0.2 s: never expected; the host fails loudly
+        if (st.fail != nullptr) {
+          __hip_atomic_store(st.fail, tile + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
@@ -1182,8 +1189,9 @@ __global__ void update_reduced_costs_kernel(const int32_t* list, const double* l
     rc[col] += mult * list_coeff[i];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    rc[leaving_col] = leaving_value;  // basic before the pivot: never listed
-    rc[entering_col] = 0.0;
+    // -1: the column lives on another column shard.
+    if (leaving_col >= 0) rc[leaving_col] = leaving_value;  // basic before: never listed
+    if (entering_col >= 0) rc[entering_col] = 0.0;
   }
 }
 

@@ -92,10 +92,42 @@ __device__ __forceinline__ double subtract_overflow(const TriSolveArgs& a, const
   return sum;
 }
 
-__device__ __forceinline__ void tri_compute(const TriSolveArgs& a, double* y, int k, int top,
+// LowerSolve's order (sparse.cc:793-812 seen from one output): one
+// subtraction per entry in ascending column order, an entry whose value is
+// zero contributes nothing (the host skips that column). Loads by batches of 8.
+__device__ __forceinline__ double subtract_sequential(const TriSolveArgs& a, const double* y,
+                                                     double sum, int e, int end) {
+  for (; e < end; e += 8) {
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = e + i < end ? load_final(y, a.ovf_pos[e + i]) : 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (e + i < end && v[i] != 0.0) sum -= v[i] * a.ovf_value[e + i];
+    }
+  }
+  return sum;
+}
+
+// The output's value from its input `sum` and its entries (final values).
+__device__ __forceinline__ double tri_apply(const TriSolveArgs& a, const double* y, double sum,
                                             const TriRec& r) {
-  if (r.row > top) return;
-  double sum = y[k];
+  if (a.sequential) {
+    if (r.n <= 4) {
+      const int n = r.n;
+      const double y0 = n > 0 ? load_final(y, r.e.x) : 0.0;
+      const double y1 = n > 1 ? load_final(y, r.e.y) : 0.0;
+      const double y2 = n > 2 ? load_final(y, r.e.z) : 0.0;
+      const double y3 = n > 3 ? load_final(y, r.e.w) : 0.0;
+      if (y0 != 0.0) sum -= y0 * r.v[0];
+      if (y1 != 0.0) sum -= y1 * r.v[1];
+      if (y2 != 0.0) sum -= y2 * r.v[2];
+      if (y3 != 0.0) sum -= y3 * r.v[3];
+    } else {
+      sum = subtract_sequential(a, y, sum, r.e.x, r.e.x + r.n);
+    }
+    return sum;  // unit diagonal (the schedule builder requires it)
+  }
   if (r.n <= 4) {
     const int n = r.n;
     const double y0 = n > 0 ? load_final(y, r.e.x) : 0.0;
@@ -112,7 +144,13 @@ __device__ __forceinline__ void tri_compute(const TriSolveArgs& a, double* y, in
   } else {
     sum = subtract_overflow(a, y, sum, r.e.x, r.e.x + r.n);
   }
-  y[k] = a.diag != nullptr ? sum / r.d : sum;
+  return a.diag != nullptr ? sum / r.d : sum;
+}
+
+__device__ __forceinline__ void tri_compute(const TriSolveArgs& a, double* y, int k, int top,
+                                            const TriRec& r) {
+  if (r.row > top) return;
+  y[k] = tri_apply(a, y, y[k], r);
 }
 
 // Zero-copy staging in and out of device-visible host memory (coalesced
@@ -228,7 +266,7 @@ __global__ __launch_bounds__(kTriThreads) void tri_levels_cu_kernel(TriSolveArgs
 // and the store sit in one loop body, so a lane whose reader shares its wave
 // stores before the wave spins again.
 constexpr unsigned long long kTriPending = 0x7ff0deadbeef0001ull;  // a NaN no arithmetic makes
-constexpr int kTriMaxSpins = 1 << 21;  // about a second
+constexpr uint64_t kTriMaxWaitTicks = 20000000;  // 0.2 s of the 100 MHz wall clock
 
 __device__ __forceinline__ bool tri_pending(double v) {
   return static_cast<unsigned long long>(__double_as_longlong(v)) == kTriPending;
@@ -260,34 +298,17 @@ __global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a) {
   double* y = a.y;
   int ready = 0;  // entries [0, ready) are known final
   bool done = false;
-  int spins = 0;
+  const uint64_t t0 = wall_clock64();  // 100 MHz
   while (!done) {
     for (; ready < r.n; ++ready) {
       if (tri_pending(load_final(y, tri_entry_pos(a, r.e, r.n, ready)))) break;
     }
     if (ready == r.n) {
-      double sum = a.x[r.row];
-      if (r.n <= 4) {
-        const int n = r.n;
-        const double y0 = n > 0 ? load_final(y, r.e.x) : 0.0;
-        const double y1 = n > 1 ? load_final(y, r.e.y) : 0.0;
-        const double y2 = n > 2 ? load_final(y, r.e.z) : 0.0;
-        const double y3 = n > 3 ? load_final(y, r.e.w) : 0.0;
-        if (n == 4) {
-          sum -= r.v[0] * y0 + r.v[1] * y1 + r.v[2] * y2 + r.v[3] * y3;
-        } else {
-          if (n > 0) sum -= r.v[0] * y0;
-          if (n > 1) sum -= r.v[1] * y1;
-          if (n > 2) sum -= r.v[2] * y2;
-        }
-      } else {
-        sum = subtract_overflow(a, y, sum, r.e.x, r.e.x + r.n);
-      }
-      const double out = a.diag != nullptr ? sum / r.d : sum;
+      const double out = tri_apply(a, y, a.x[r.row], r);
       a.x[r.row] = out;  // the scatter, fused
       __hip_atomic_store(y + k, out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       done = true;
-    } else if (++spins > kTriMaxSpins) {
+    } else if (wall_clock64() - t0 > kTriMaxWaitTicks) {
       // Bounded wait (never expected): report and leave, the host fails loudly.
       if (a.fail != nullptr) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       done = true;

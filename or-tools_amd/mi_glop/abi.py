@@ -139,7 +139,7 @@ IMPRECISE = 11
 # Kernel ids (include/mi_lp.h MI_K_*)
 KERNEL_NAMES = ["pricing", "update_row", "primal_norms", "rc_update", "tri_solve",
                 "col_norms", "spmv_rows", "single_row", "dual_ratio", "readback",
-                "tri_solve_tau"]
+                "tri_solve_tau", "tri_solve_l"]
 
 # Names of every exported entry point of include/mi_lp.h (checked by tests).
 EXPORTED_SYMBOLS = [
