@@ -314,6 +314,50 @@ const char* mi_mps_col_name(const mi_mps_model* m, int32_t col);
 const char* mi_mps_row_name(const mi_mps_model* m, int32_t row);
 void mi_mps_free(mi_mps_model* m);
 
+/* LPSolver layer: what glop::LPSolver::SolveWithTimeLimit
+ * (ortools/glop/lp_solver.cc:150-262) does around RevisedSimplex::Solve for
+ * the MPSolver path (glop_interface.cc:104-169): IsCleanedUp / IsValid checks,
+ * ScalingPreprocessor::Run (preprocessor.cc:3855-3876: SparseMatrixScaler
+ * geometric + equilibration passes, matrix_scaler.cc; ScaleObjective /
+ * ScaleBounds, lp_data.cc:1190-1258), the engine solve on handle h, then
+ * ScalingPreprocessor::RecoverSolution (preprocessor.cc:3878-3912) and the
+ * value part of LoadAndVerifySolution (lp_solver.cc:334-367: reduced costs,
+ * Kahan objective, strong-optimal moves, activities). Presolve passes other
+ * than the scaling (use_preprocessing) are not built. out->objective is the
+ * unscaled problem objective; the arrays (n / m entries, any may be NULL)
+ * are the unscaled solution. An invalid LP gives MI_LP_OK with
+ * problem_status MI_LP_INVALID_PROBLEM, as LPSolver returns it. */
+enum { MI_LP_SCALING_DEFAULT = 0, MI_LP_EQUILIBRATION = 1, MI_LP_LINEAR_PROGRAM = 2 };
+enum { MI_LP_NO_COST_SCALING = 0, MI_LP_CONTAIN_ONE_COST_SCALING = 1,
+       MI_LP_MEAN_COST_SCALING = 2, MI_LP_MEDIAN_COST_SCALING = 3 };
+typedef struct mi_lp_solver_params {
+  int32_t use_scaling;                      /* 16, true */
+  int32_t scaling_method;                   /* 57, EQUILIBRATION (LINEAR_PROGRAM not built:
+                                               geometric + equilibration, as upstream
+                                               when its scaling LP fails) */
+  int32_t cost_scaling;                     /* 60, CONTAIN_ONE_COST_SCALING */
+  int32_t provide_strong_optimal_guarantee; /* 24, true */
+  double max_valid_magnitude;               /* 199, 1e30 */
+} mi_lp_solver_params;
+void mi_lp_solver_params_default(mi_lp_solver_params* p);
+/* ScalingPreprocessor::Run alone, in place on the caller's arrays (no device
+ * needed): row_scale (m) / col_scale (n) receive SparseMatrixScaler's
+ * unscaling factors, *cost_factor / *bound_factor the divisors of
+ * ScaleObjective / ScaleBounds. With use_scaling = 0 nothing changes and
+ * every factor is 1. */
+int mi_lp_scale(const mi_lp_solver_params* sp, int32_t m, int32_t n, const int64_t* col_starts,
+                const int32_t* row_idx, double* vals, double* col_lb, double* col_ub,
+                double* row_lb, double* row_ub, double* obj, double* obj_offset,
+                double* obj_scale, double* row_scale, double* col_scale, double* cost_factor,
+                double* bound_factor);
+int mi_lp_solver_solve(mi_lp* h, const mi_lp_solver_params* sp, int32_t m, int32_t n,
+                       const int64_t* col_starts, const int32_t* row_idx, const double* vals,
+                       const double* col_lb, const double* col_ub, const double* row_lb,
+                       const double* row_ub, const double* obj, double obj_offset,
+                       double obj_scale, int32_t maximize, const volatile int32_t* interrupt,
+                       mi_lp_result* out, double* primal, double* duals, double* reduced_costs,
+                       double* activities, int8_t* var_status, int8_t* cons_status);
+
 #ifdef __cplusplus
 }
 #endif

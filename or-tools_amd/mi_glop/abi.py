@@ -159,4 +159,34 @@ EXPORTED_SYMBOLS = [
     "mi_lp_compute_dictionary", "mi_lp_get_dictionary",
     "mi_mps_read_file", "mi_mps_parse_string", "mi_mps_error", "mi_mps_dims", "mi_mps_get",
     "mi_mps_name", "mi_mps_col_name", "mi_mps_row_name", "mi_mps_free",
+    "mi_lp_solver_params_default", "mi_lp_scale", "mi_lp_solver_solve",
 ]
+
+
+class MiLpSolverParams(ctypes.Structure):
+    """include/mi_lp.h mi_lp_solver_params: the GlopParameters fields that
+    glop::LPSolver reads around the simplex (parameters.proto field numbers
+    16, 57, 60, 24, 199)."""
+    _fields_ = [
+        ("use_scaling", ctypes.c_int32),
+        ("scaling_method", ctypes.c_int32),
+        ("cost_scaling", ctypes.c_int32),
+        ("provide_strong_optimal_guarantee", ctypes.c_int32),
+        ("max_valid_magnitude", ctypes.c_double),
+    ]
+
+
+# GlopParameters::ScalingAlgorithm / CostScalingAlgorithm (parameters.proto:34-36, 194-210)
+SCALING_DEFAULT, EQUILIBRATION, LINEAR_PROGRAM = 0, 1, 2
+NO_COST_SCALING, CONTAIN_ONE_COST_SCALING, MEAN_COST_SCALING, MEDIAN_COST_SCALING = 0, 1, 2, 3
+
+
+def default_solver_params(**overrides):
+    p = MiLpSolverParams(use_scaling=1, scaling_method=EQUILIBRATION,
+                         cost_scaling=CONTAIN_ONE_COST_SCALING,
+                         provide_strong_optimal_guarantee=1, max_valid_magnitude=1e30)
+    for k, v in overrides.items():
+        if k not in dict(MiLpSolverParams._fields_):
+            raise KeyError(f"unknown LPSolver parameter {k!r}")
+        setattr(p, k, v)
+    return p

@@ -74,6 +74,13 @@ def lib():
     L.mi_lp_get_unit_row_left_inverse.argtypes = [vp, ctypes.c_int32, vp, vp, vp]
     L.mi_lp_compute_dictionary.argtypes = [vp, vp, ctypes.c_int32, vp]
     L.mi_lp_get_dictionary.argtypes = [vp, vp, vp, vp]
+    L.mi_lp_solver_params_default.argtypes = [ctypes.POINTER(abi.MiLpSolverParams)]
+    L.mi_lp_scale.argtypes = [ctypes.POINTER(abi.MiLpSolverParams), ctypes.c_int32,
+                              ctypes.c_int32] + [vp] * 14
+    L.mi_lp_solver_solve.argtypes = [vp, ctypes.POINTER(abi.MiLpSolverParams), ctypes.c_int32,
+                                     ctypes.c_int32] + [vp] * 8 + [
+        ctypes.c_double, ctypes.c_double, ctypes.c_int32, vp,
+        ctypes.POINTER(abi.MiLpResult)] + [vp] * 6
     _lib = L
     return L
 
@@ -134,6 +141,28 @@ class LpHandle:
                                        _p(clb), _p(cub), _p(rlb), _p(rub), _p(ob),
                                        lp.obj_offset, lp.obj_scale, int(lp.maximize)),
                     "mi_lp_load")
+
+    def solve_lp(self, lp, solver_params=None, interrupt=None):
+        """glop::LPSolver::SolveWithTimeLimit on this handle (mi_lp_solver_solve):
+        scaling preprocessor, engine solve, RecoverSolution, solution values of
+        the unscaled LP. Returns (result, dict of unscaled solution arrays)."""
+        sp = solver_params or abi.default_solver_params()
+        keep = [np.ascontiguousarray(x, dtype=t) for x, t in (
+            (lp.col_starts, np.int64), (lp.row_idx, np.int32), (lp.vals, np.float64),
+            (lp.col_lb, np.float64), (lp.col_ub, np.float64), (lp.row_lb, np.float64),
+            (lp.row_ub, np.float64), (lp.obj, np.float64))]
+        out = {"x": np.zeros(lp.n), "y": np.zeros(lp.m), "rc": np.zeros(lp.n),
+               "act": np.zeros(lp.m), "vstat": np.zeros(lp.n, np.int8),
+               "cstat": np.zeros(lp.m, np.int8)}
+        r = abi.MiLpResult()
+        flag = None if interrupt is None else _p(interrupt)
+        rc = self._L.mi_lp_solver_solve(
+            self.h, ctypes.byref(sp), lp.m, lp.n, *[_p(a) for a in keep], lp.obj_offset,
+            lp.obj_scale, int(lp.maximize), flag, ctypes.byref(r),
+            *[_p(out[k]) for k in ("x", "y", "rc", "act", "vstat", "cstat")])
+        self._check(rc, "mi_lp_solver_solve")
+        self.lp = None  # the handle now holds the scaled LP
+        return r, out
 
     def set_variable_bounds(self, col_lb, col_ub):
         lb = np.ascontiguousarray(col_lb, dtype=np.float64)
@@ -318,3 +347,31 @@ def batch_solve_bounds(workers, lbs, ubs, warm_state=None):
     if rc != 0:
         raise RuntimeError(f"mi_lp_batch_solve_bounds failed ({rc})")
     return list(res)
+
+
+def scale_lp(lp, solver_params=None):
+    """ScalingPreprocessor::Run (mi_lp_scale, host only): returns the scaled
+    copy of `lp` plus row/column unscaling factors and the cost/bound divisors."""
+    from . import lp as lpmod
+    L = lib()
+    sp = solver_params or abi.default_solver_params()
+    cs = np.ascontiguousarray(lp.col_starts, np.int64)
+    ri = np.ascontiguousarray(lp.row_idx, np.int32)
+    arrs = [np.array(a, np.float64) for a in (lp.vals, lp.col_lb, lp.col_ub, lp.row_lb,
+                                              lp.row_ub, lp.obj)]
+    off = ctypes.c_double(lp.obj_offset)
+    sc = ctypes.c_double(lp.obj_scale)
+    rs = np.zeros(lp.m)
+    cl = np.zeros(lp.n)
+    cf = ctypes.c_double()
+    bf = ctypes.c_double()
+    rc = L.mi_lp_scale(ctypes.byref(sp), lp.m, lp.n, _p(cs), _p(ri), *[_p(a) for a in arrs],
+                       ctypes.byref(off), ctypes.byref(sc), _p(rs), _p(cl), ctypes.byref(cf),
+                       ctypes.byref(bf))
+    if rc != 0:
+        raise ValueError(f"mi_lp_scale failed with {rc}")
+    v, clb, cub, rlb, rub, ob = arrs
+    out = lpmod.LinearProgram(lp.m, lp.n, cs, ri, v, clb, cub, rlb, rub, ob, off.value,
+                              sc.value, lp.maximize, lp.name)
+    return out, {"row_scale": rs, "col_scale": cl, "cost_factor": cf.value,
+                 "bound_factor": bf.value}

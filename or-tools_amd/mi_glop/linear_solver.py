@@ -17,9 +17,12 @@ Model -> LinearProgram follows GLOPInterface::ExtractModel + LinearProgram::
 CleanUp: one coefficient per (row, column), the last SetCoefficient wins as in
 MPConstraint; entries of a column sorted by row, zeros dropped (the
 IsCleanedUp precondition of lp_solver.cc:185-191).
-Status maps are glop_utils.cc:18-125. Not replicated: LPSolver's
-presolve/scaling (not built yet), so bases on
-degenerate LPs may differ from upstream MPSolver+GLOP; objectives agree.
+Status maps are glop_utils.cc:18-125. Solve() goes through the engine's
+LPSolver layer (mi_lp_solver_solve: Glop's scaling preprocessor, the simplex
+on the scaled LP, RecoverSolution and the value part of
+LoadAndVerifySolution, lp_solver.cc:150-367). Presolve passes other than
+the scaling (use_preprocessing) are not built, so bases on degenerate LPs
+may differ from upstream MPSolver+GLOP; objectives agree.
 Integer variables are rejected (GLOP is an LP solver: IsMIP() is false).
 """
 import math
@@ -187,6 +190,7 @@ class Solver:
         self._cons = []
         self._objective = Objective(self)
         self._params = abi.default_params()
+        self._solver_params = abi.default_solver_params()
         self._time_limit_ms = 0
         self._handle = None
         self._sol = None
@@ -320,21 +324,44 @@ class Solver:
         if self._handle is None:
             self._handle = engine.LpHandle(p, device=self._device)
         self._handle.set_params(p)
-        self._handle.load(model)
-        r = self._handle.solve()
+        r, sol = self._handle.solve_lp(model, self._solver_params)
         self._iterations = int(r.iterations)
         status = self._STATUS.get(int(r.problem_status), 4)
         self._sol = {"status": status, "objective": r.objective}
         if r.error_code == 0 and r.problem_status != abi.INVALID_PROBLEM:
-            h = self._handle
-            self._sol["x"] = h.primal()
-            self._sol["rc"] = h.reduced_costs()
-            self._sol["y"] = h.duals()
-            self._sol["act"] = h.activities()
-            vs, cs = h.statuses()
-            self._sol["vstat"] = [self._BASIS[int(s)] for s in vs]
-            self._sol["cstat"] = [self._BASIS[int(s)] for s in cs]
+            self._sol["x"] = sol["x"]
+            self._sol["rc"] = sol["rc"]
+            self._sol["y"] = sol["y"]
+            self._sol["act"] = sol["act"]
+            self._sol["vstat"] = [self._BASIS[int(s)] for s in sol["vstat"]]
+            self._sol["cstat"] = [self._BASIS[int(s)] for s in sol["cstat"]]
         return status
+
+    def SetSolverSpecificParametersAsString(self, text):
+        """GLOPInterface::SetSolverSpecificParametersAsString (glop_interface.cc:
+        397-411) reads a GlopParameters text proto; the fields of mi_glop_params
+        and of the LPSolver layer are accepted as `name: value` pairs."""
+        tokens = text.replace(":", " : ").split()
+        i = 0
+        while i < len(tokens):
+            name = tokens[i]
+            if i + 2 >= len(tokens) or tokens[i + 1] != ":":
+                return False
+            value = tokens[i + 2]
+            i += 3
+            v = {"true": 1, "false": 0}.get(value.lower(), None)
+            if v is None:
+                try:
+                    v = float(value) if any(ch in value for ch in ".eE") else int(value)
+                except ValueError:
+                    return False
+            if name in dict(abi.MiLpSolverParams._fields_):
+                setattr(self._solver_params, name, v)
+            elif name in dict(abi.MiGlopParams._fields_):
+                setattr(self._params, name, v)
+            else:
+                return False
+        return True
 
     def _value(self, key, index):
         if self._sol is None or key not in self._sol:

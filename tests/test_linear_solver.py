@@ -15,8 +15,17 @@ import pytest
 
 from mi_glop import abi, linear_solver
 
+import os
+import sys
+
+from mi_glop.lp import LinearProgram
+
 import kat_lps
 import oracle_lib
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "oracle"))
+import oracle_scaling  # noqa: E402
 
 INF = math.inf
 
@@ -121,13 +130,23 @@ def test_solve_through_engine(model, expect):
     assert solver.Solve() == linear_solver.Solver.OPTIMAL
     assert abs(solver.Objective().Value() - expect["objective"]) <= 1e-6 * abs(expect["objective"])
     np.testing.assert_allclose([v.solution_value() for v in xs], expect["primal"], atol=1e-7)
+    # Oracle: the simplex restatement on the scaling restatement's LP, then
+    # the restated recovery (Solve() runs the LPSolver layer, lp_solver.cc).
+    lp = solver.to_linear_program()
+    arr, fac = oracle_scaling.scale_lp(lp)
+    slp = LinearProgram(lp.m, lp.n, lp.col_starts, lp.row_idx, arr["vals"], arr["col_lb"],
+                        arr["col_ub"], arr["row_lb"], arr["row_ub"], arr["obj"],
+                        arr["obj_offset"], arr["obj_scale"], lp.maximize)
     o = oracle_lib.OracleLp(abi.default_params())
-    o.load(solver.to_linear_program())
-    o.solve()
-    np.testing.assert_array_equal([v.solution_value() for v in xs], o.primal())
-    np.testing.assert_array_equal([v.reduced_cost() for v in xs], o.reduced_costs())
-    np.testing.assert_array_equal([c.dual_value() for c in cons], o.duals())
+    o.load(slp)
+    ro = o.solve()
     ov, oc = o.statuses()
+    want = oracle_scaling.recover_and_verify(lp, fac, o.primal(), o.duals(), ov,
+                                             ro.problem_status == abi.OPTIMAL)
+    np.testing.assert_array_equal([v.solution_value() for v in xs], want["x"])
+    np.testing.assert_array_equal([v.reduced_cost() for v in xs], want["rc"])
+    np.testing.assert_array_equal([c.dual_value() for c in cons], want["y"])
+    assert solver.Objective().Value() == want["objective"]
     bmap = linear_solver.Solver._BASIS
     assert [v.basis_status() for v in xs] == [bmap[int(s)] for s in ov]
     assert [c.basis_status() for c in cons] == [bmap[int(s)] for s in oc]
