@@ -156,6 +156,7 @@ class LpHandle:
                "cstat": np.zeros(lp.m, np.int8)}
         r = abi.MiLpResult()
         flag = None if interrupt is None else _p(interrupt)
+        self._push_params()
         rc = self._L.mi_lp_solver_solve(
             self.h, ctypes.byref(sp), lp.m, lp.n, *[_p(a) for a in keep], lp.obj_offset,
             lp.obj_scale, int(lp.maximize), flag, ctypes.byref(r),

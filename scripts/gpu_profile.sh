@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 evidence for the bench's rooflines, one workload per process so
 # that per-kernel-id byte counts are not mixed:
-#   C2: bench.py's config-2 section only   -> gpurun_out/prof_c2/{trace,fetch,write}
+#   C2: scripts/probe.py --config c2        -> gpurun_out/prof_c2/{trace,fetch,write}
 #   C5: scripts/probe.py --config c5        -> gpurun_out/prof_c5/{trace,fetch,write}
 #   C4: scripts/probe_batch.py (256 children, 1 worker: rocprofv3 crashed
 #       under 8 concurrent worker threads) -> gpurun_out/prof_c4/...
@@ -13,7 +13,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-C2="python3 $R/bench.py --no-cpu --no-c5 --no-c3 --batch-lps 0"
+C2="python3 $R/scripts/probe.py --config c2 --warmup 3 --steps 64"
 C4="python3 $R/scripts/probe_batch.py --lps 256 --workers 1"
 C5="python3 $R/scripts/probe.py --config c5 --m 100000 --n 1000000 --warmup ${C5_WARMUP:-20000} --steps ${C5_STEPS:-1000}"
 for W in ${WORKLOADS:-c2 c5}; do

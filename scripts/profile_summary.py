@@ -34,9 +34,12 @@ GROUPS = {  # HIP kernel name fragment -> engine kernel id (bench.py names)
     # one-launch kernels of small LPs (N <= 8192)
     "row_wise_small_kernel": "update_row", "row_wise_small_by_column_kernel": "update_row",
     "column_wise_small_kernel": "update_row", "list_dots_small_kernel": "primal_norms",
-    # dense U solve of FTRAN (tri_solve.hip): permutes in/out, wide levels, CU segments
+    # dense L/U solves of FTRAN (tri_solve.hip): staging, permutes, levels or
+    # the readiness-driven single launch
     "tri_gather_kernel": "tri_solve", "tri_scatter_kernel": "tri_solve",
     "tri_level_grid_kernel": "tri_solve", "tri_levels_cu_kernel": "tri_solve",
+    "tri_copy_in_kernel": "tri_solve", "tri_copy_out_kernel": "tri_solve",
+    "tri_init_kernel": "tri_solve", "tri_syncfree_kernel": "tri_solve",
 }
 
 
@@ -58,7 +61,7 @@ PRIMARY = {
                      ["column_dot_kernel<2,"]],
     "spmv_rows": [["row_sum_kernel"]],
     "col_norms": [["column_squared_norm_kernel"]],
-    "tri_solve": [["tri_gather_kernel"]],
+    "tri_solve": [["tri_init_kernel", "tri_gather_kernel"]],
 }
 
 

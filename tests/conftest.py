@@ -12,3 +12,14 @@ for p in (os.path.join(REPO, "or-tools_amd"), os.path.join(REPO, "tests"), REPO)
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs under gpurun)")
     config.addinivalue_line("markers", "slow: longer CPU oracle runs")
+
+
+_TIMES = os.environ.get("MILP_TEST_TIMES")
+
+
+def pytest_runtest_logreport(report):
+    """MILP_TEST_TIMES=path: append each test's call duration as it ends (a
+    suite cut off by a time limit still leaves its per-test times)."""
+    if _TIMES and report.when == "call":
+        with open(_TIMES, "a") as f:
+            f.write(f"{report.duration:8.2f} {report.outcome} {report.nodeid}\n")
