@@ -451,10 +451,12 @@ class DeviceLp : public DeviceSolver {
   int tri_min_rows_ = 16384;
   int tri_wide_level_ = 600;  // MILP_TRI_WIDE: wider levels run over the chip
   int tri_debug_left_ = 0;
-  bool tri_graph_ = true;     // MILP_TRI_GRAPH
+  bool tri_graph_ = false;    // MILP_TRI_GRAPH=1: replay a captured graph (measured 5-10 % slower on C5 than 4 direct launches)
   bool tri_tau_ = true;       // MILP_TRI_TAU
   bool tri_mapped_ = true;    // MILP_TRI_MAPPED: zero-copy staging inside the plan
   bool tri_syncfree_ = true;  // MILP_TRI_SYNCFREE: readiness-driven single launch
+  int tri_syncfree_min_levels_ = 0;  // MILP_TRI_SYNCFREE_MIN_LEVELS: shallower -> level plan
+  bool tri_fuse0_ = true;     // MILP_TRI_FUSE0: level 0 inside the gather kernel
   bool tri_lower_ = true;     // MILP_TRI_LOWER: the L solves too
   int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
   uint64_t* d_tri_clock_ = nullptr;

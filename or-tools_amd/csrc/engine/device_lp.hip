@@ -137,6 +137,10 @@ void DeviceLp::Init(int device) {
   if (const char* v = std::getenv("MILP_TRI_SYNCFREE")) tri_syncfree_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_LOWER")) tri_lower_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_MIN_WIDTH")) tri_min_width_ = std::atoi(v);
+  if (const char* v = std::getenv("MILP_TRI_SYNCFREE_MIN_LEVELS")) {
+    tri_syncfree_min_levels_ = std::atoi(v);
+  }
+  if (const char* v = std::getenv("MILP_TRI_FUSE0")) tri_fuse0_ = std::atoi(v) != 0;
   CreateShards();
   StartWatchdog();
 }

@@ -353,6 +353,7 @@ milp_kernels::TriSolveArgs DeviceLp::TriArgs(const TriSchedule& s, const TriCont
   a.num_pos = s.pos;
   a.num_levels = s.levels;
   a.sequential = s.sequential ? 1 : 0;
+  a.fuse_level0 = tri_fuse0_ ? 1 : 0;
   a.clock = nullptr;
   return a;
 }
@@ -386,7 +387,10 @@ void DeviceLp::TriCopyOut(const TriSchedule& s, const TriContext& c) {
 
 void DeviceLp::EnqueueTriKernels(const TriSchedule& s, const milp_kernels::TriSolveArgs& a,
                                  void* stream) {
-  if (tri_syncfree_ && a.clock == nullptr && a.num_work <= milp_kernels::kTriSyncFreeMaxWork) {
+  // The single-launch kernel pays a cross-workgroup hand-off per level; a
+  // shallow schedule runs faster as a few level launches.
+  if (tri_syncfree_ && a.clock == nullptr && a.num_work <= milp_kernels::kTriSyncFreeMaxWork &&
+      s.levels >= tri_syncfree_min_levels_) {
     Check(milp_launch::tri_transpose_lower_syncfree(a, Stream(stream)), "tri syncfree");
     return;
   }

@@ -301,6 +301,9 @@ struct TriSolveArgs {
   // 0: grouped sums (TransposeLowerSolve); 1: LowerSolve's order -- one
   // subtraction per entry in list order, entries whose value is 0 skipped.
   int sequential;
+  // Level plan: 1 when level 0 (outputs without entries, only a division)
+  // is computed inside the gather kernel instead of a launch of its own.
+  int fuse_level0;
 };
 // The sync-free variant needs every workgroup resident: at most this many
 // outputs (512 workgroups of 256 threads, 2 per CU).

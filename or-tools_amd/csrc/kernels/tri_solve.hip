@@ -181,6 +181,20 @@ __global__ __launch_bounds__(256) void tri_gather_kernel(TriSolveArgs a) {
   }
 }
 
+// The gather with level 0 fused: y[k] = x[row(k)], divided by the diagonal
+// for the listed outputs of level 0 (no entries: tri_apply's sum is the input
+// itself, then the division).
+__global__ __launch_bounds__(256) void tri_gather_level0_kernel(TriSolveArgs a) {
+  const int top = *a.top;
+  const int l0_end = a.level_start[1];
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.num_pos;
+       k += gridDim.x * blockDim.x) {
+    double v = a.x[a.pos_row[k]];
+    if (k < l0_end && a.rec_row[k] <= top) v = v / a.diag[k];  // padding rows: INT32_MAX
+    a.y[k] = v;
+  }
+}
+
 // x[row(k)] = y[k] for the computed outputs.
 __global__ __launch_bounds__(256) void tri_scatter_kernel(TriSolveArgs a) {
   const int top = *a.top;
@@ -279,13 +293,39 @@ __global__ __launch_bounds__(256) void tri_init_kernel(TriSolveArgs a) {
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.num_pos;
        k += gridDim.x * blockDim.x) {
     const int row = a.pos_row[k];
-    a.y[k] = (k < a.num_work && row <= top) ? pending : a.x[row];
+    // Write-through (sc1) stores: a plain store would leave the line valid in
+    // this XCD's L2, and a reader on this XCD would then poll that stale copy
+    // (pending) until the line is evicted, long after its producer on
+    // another XCD stored the final value.
+    __hip_atomic_store(a.y + k, (k < a.num_work && row <= top) ? pending : a.x[row],
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 __device__ __forceinline__ int tri_entry_pos(const TriSolveArgs& a, const int4& e, int n, int j) {
   if (n > 4) return a.ovf_pos[e.x + j];
   return j == 0 ? e.x : j == 1 ? e.y : j == 2 ? e.z : e.w;
+}
+
+// tri_apply for n <= 4 with the entry values already in registers.
+__device__ __forceinline__ double tri_apply4(const TriSolveArgs& a, double sum, const TriRec& r,
+                                             double y0, double y1, double y2, double y3) {
+  const int n = r.n;
+  if (a.sequential) {
+    if (y0 != 0.0) sum -= y0 * r.v[0];
+    if (y1 != 0.0) sum -= y1 * r.v[1];
+    if (y2 != 0.0) sum -= y2 * r.v[2];
+    if (y3 != 0.0) sum -= y3 * r.v[3];
+    return sum;
+  }
+  if (n == 4) {
+    sum -= r.v[0] * y0 + r.v[1] * y1 + r.v[2] * y2 + r.v[3] * y3;
+  } else {
+    if (n > 0) sum -= r.v[0] * y0;
+    if (n > 1) sum -= r.v[1] * y1;
+    if (n > 2) sum -= r.v[2] * y2;
+  }
+  return a.diag != nullptr ? sum / r.d : sum;
 }
 
 __global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a) {
@@ -296,20 +336,47 @@ __global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a) {
   tri_load(a, k, a.num_work, top, &r);
   if (r.row > top) return;  // not computed: y[k] already holds x[row]
   double* y = a.y;
-  int ready = 0;  // entries [0, ready) are known final
+  const double in = a.x[r.row];
   bool done = false;
   const uint64_t t0 = wall_clock64();  // 100 MHz
+  if (r.n <= 4) {
+    // One poll round loads all entries at once and keeps them: the values
+    // that end the wait are the ones the output is computed from (a hop is
+    // one round trip, not a readiness walk plus a reload).
+    const int n = r.n;
+    while (!done) {
+      const double y0 = n > 0 ? load_final(y, r.e.x) : 0.0;
+      const double y1 = n > 1 ? load_final(y, r.e.y) : 0.0;
+      const double y2 = n > 2 ? load_final(y, r.e.z) : 0.0;
+      const double y3 = n > 3 ? load_final(y, r.e.w) : 0.0;
+      const bool pending = tri_pending(y0) || tri_pending(y1) || tri_pending(y2) ||
+                           tri_pending(y3);
+      if (!pending) {
+        const double out = tri_apply4(a, in, r, y0, y1, y2, y3);
+        a.x[r.row] = out;  // the scatter, fused
+        __hip_atomic_store(y + k, out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        done = true;
+      } else if (wall_clock64() - t0 > kTriMaxWaitTicks) {
+        // Bounded wait (never expected): report and leave, the host fails loudly.
+        if (a.fail != nullptr) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        done = true;
+      } else {
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    return;
+  }
+  int ready = 0;  // entries [0, ready) are known final
   while (!done) {
     for (; ready < r.n; ++ready) {
       if (tri_pending(load_final(y, tri_entry_pos(a, r.e, r.n, ready)))) break;
     }
     if (ready == r.n) {
-      const double out = tri_apply(a, y, a.x[r.row], r);
+      const double out = tri_apply(a, y, in, r);
       a.x[r.row] = out;  // the scatter, fused
       __hip_atomic_store(y + k, out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       done = true;
     } else if (wall_clock64() - t0 > kTriMaxWaitTicks) {
-      // Bounded wait (never expected): report and leave, the host fails loudly.
       if (a.fail != nullptr) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       done = true;
     } else {
@@ -357,10 +424,18 @@ hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, const int
     if (e != hipSuccess) return e;
   }
   const int pos_blocks = std::min(1024, (args.num_pos + 255) / 256);
-  milp_kernels::tri_gather_kernel<<<pos_blocks, 256, 0, s>>>(args);
+  // Level 0 alone over the chip (the first segment is (-1, blocks)) and a
+  // diagonal to divide by: fused into the gather.
+  const bool fuse0 = args.fuse_level0 && args.diag != nullptr && num_segments > 0 &&
+                     segments[0] == -1;
+  if (fuse0) {
+    milp_kernels::tri_gather_level0_kernel<<<pos_blocks, 256, 0, s>>>(args);
+  } else {
+    milp_kernels::tri_gather_kernel<<<pos_blocks, 256, 0, s>>>(args);
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  for (int i = 0; i < num_segments; ++i) {
+  for (int i = fuse0 ? 1 : 0; i < num_segments; ++i) {
     const int lb = segments[2 * i];
     const int le = segments[2 * i + 1];
     if (le <= lb) continue;
@@ -373,6 +448,9 @@ hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, const int
     if (e != hipSuccess) return e;
   }
   const int work_blocks = std::min(1024, (args.num_work + 255) / 256);
+  // (A scatter straight into mapped host memory, tri_scatter_host_kernel,
+  // measured 80 us against 5 + 15 us for this scatter plus the coalesced
+  // copy-out: scattered 8-byte PCIe writes.)
   milp_kernels::tri_scatter_kernel<<<work_blocks, 256, 0, s>>>(args);
   if (args.host_x == nullptr) return hipGetLastError();
   e = hipGetLastError();
