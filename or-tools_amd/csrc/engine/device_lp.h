@@ -316,6 +316,12 @@ class DeviceLp : public DeviceSolver {
   uint64_t* d_masks_[kNumMasks] = {nullptr, nullptr, nullptr};
   std::vector<uint64_t> h_masks_[kNumMasks];
   uint64_t* h_pin_mask_[kNumMasks] = {nullptr, nullptr, nullptr};
+  // Changed-word updates of the masks: (index, word) pairs in mapped memory,
+  // one slot per mask, guarded by ev_mask_ like the full-upload slot.
+  static constexpr int kMaskDiffMax = 512;
+  bool mask_on_device_[kNumMasks] = {false, false, false};  // device copy == h_masks_
+  char* h_mask_diff_ = nullptr;
+  char* m_mask_diff_ = nullptr;
   void* ev_mask_[kNumMasks] = {nullptr, nullptr, nullptr};  // hipEvent_t: slot reusable
   int mask_words_ = 0;
 
@@ -431,7 +437,12 @@ class DeviceLp : public DeviceSolver {
   double* m_cand_rc_ = nullptr;
   int32_t* h_cb_cols_ = nullptr;  // column-bit changes (pinned, event-guarded)
   uint8_t* h_cb_bits_ = nullptr;
-  void* ev_cb_ = nullptr;
+  void* ev_cb_[2] = {nullptr, nullptr};  // column-bit slots (alternating)
+  int cb_slot_ = 0;
+  int32_t* m_cb_cols_ = nullptr;  // device pointers of the mapped h_cb_* / h_flip_*
+  uint8_t* m_cb_bits_ = nullptr;
+  int32_t* m_flip_cols_ = nullptr;
+  uint8_t* m_flip_flags_ = nullptr;
   int32_t* h_flip_cols_ = nullptr;
   uint8_t* h_flip_flags_ = nullptr;
   int last_candidates_ = 0;

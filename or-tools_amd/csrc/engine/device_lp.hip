@@ -68,7 +68,10 @@ DeviceLp::~DeviceLp() {
                   static_cast<void*>(h_flip_cols_), static_cast<void*>(h_flip_flags_)}) {
     if (p) (void)hipHostFree(p);
   }
-  if (ev_cb_) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_cb_));
+  for (void* e : ev_cb_) {
+    if (e) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e));
+  }
+  if (h_mask_diff_) (void)hipHostFree(h_mask_diff_);
   for (int k = 0; k < kNumMasks; ++k) {
     if (h_pin_mask_[k]) (void)hipHostFree(h_pin_mask_[k]);
     if (ev_mask_[k]) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_mask_[k]));
@@ -311,11 +314,20 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   for (int k = 0; k < kNumMasks; ++k) {
     d_masks_[k] = Alloc<uint64_t>(mask_words_);
     h_masks_[k].assign(mask_words_, ~0ull);  // force first upload
+    mask_on_device_[k] = false;               // and no changed-word update before it
     Check(hipEventSynchronize(reinterpret_cast<hipEvent_t>(ev_mask_[k])), "mask event");
     if (h_pin_mask_[k]) (void)hipHostFree(h_pin_mask_[k]);
     Check(hipHostMalloc(reinterpret_cast<void**>(&h_pin_mask_[k]),
                         std::max(1, mask_words_) * sizeof(uint64_t)),
           "pin");
+  }
+  if (h_mask_diff_ == nullptr) {
+    Check(hipHostMalloc(reinterpret_cast<void**>(&h_mask_diff_),
+                        size_t(kNumMasks) * kMaskDiffMax * 12, hipHostMallocMapped),
+          "hipHostMalloc (mapped)");
+    void* dev = nullptr;
+    Check(hipHostGetDevicePointer(&dev, h_mask_diff_, 0), "mapped pointer");
+    m_mask_diff_ = static_cast<char*>(dev);
   }
   d_vec_m_ = Alloc<double>(m_);
   d_vec_m2_ = Alloc<double>(m_);
@@ -526,14 +538,49 @@ void DeviceLp::SetMask(Mask which, const uint64_t* words, int num_words) {
   if (!shards_.empty()) return ShardedSetMask(which, words, num_words);
   std::vector<uint64_t>& h = h_masks_[which];
   if (num_words != mask_words_) throw DeviceError("mask size mismatch");
-  if (std::memcmp(h.data(), words, num_words * sizeof(uint64_t)) == 0) return;
-  std::memcpy(h.data(), words, num_words * sizeof(uint64_t));
+  // Unchanged words are skipped only once the device holds a copy: a mask
+  // equal to the all-ones placeholder (e.g. a column shard with every column
+  // relevant) must still reach the device the first time.
+  if (mask_on_device_[which] && std::memcmp(h.data(), words, num_words * sizeof(uint64_t)) == 0) {
+    return;
+  }
   if (which == kRelevant && small_fused_enabled_ && h_small_in_ != nullptr) {
     // Small LPs: the relevant set changes every pivot and the small update
     // row reads it from mapped host memory; other kernels flush it first.
+    std::memcpy(h.data(), words, num_words * sizeof(uint64_t));
     mask_dirty_ = true;
     return;
   }
+  if (h_mask_diff_ != nullptr && mask_on_device_[which] && !(which == kRelevant && mask_dirty_)) {
+    // A pivot moves a few bits: send only the changed words (mapped pairs +
+    // one small kernel) instead of the whole mask through the copy engine.
+    hipEvent_t done = reinterpret_cast<hipEvent_t>(ev_mask_[which]);
+    Check(hipEventSynchronize(done), "mask event");
+    char* slot = h_mask_diff_ + size_t(which) * kMaskDiffMax * 12;
+    int32_t* idx = reinterpret_cast<int32_t*>(slot);
+    uint64_t* val = reinterpret_cast<uint64_t*>(slot + kMaskDiffMax * 4);
+    int count = 0;
+    for (int w = 0; w < num_words && count <= kMaskDiffMax; ++w) {
+      if (h[w] != words[w]) {
+        if (count < kMaskDiffMax) {
+          idx[count] = w;
+          val[count] = words[w];
+        }
+        ++count;
+      }
+    }
+    if (count <= kMaskDiffMax) {
+      std::memcpy(h.data(), words, num_words * sizeof(uint64_t));
+      char* dslot = m_mask_diff_ + size_t(which) * kMaskDiffMax * 12;
+      Check(milp_launch::set_mask_words(reinterpret_cast<const int32_t*>(dslot),
+                                        reinterpret_cast<const uint64_t*>(dslot + kMaskDiffMax * 4),
+                                        count, d_masks_[which], S(stream_)),
+            "mask words");
+      Check(hipEventRecord(done, S(stream_)), "mask event");
+      return;
+    }
+  }
+  std::memcpy(h.data(), words, num_words * sizeof(uint64_t));
   UploadMask(which);
 }
 
@@ -545,6 +592,7 @@ void DeviceLp::UploadMask(Mask which) {
   std::memcpy(h_pin_mask_[which], h_masks_[which].data(), mask_words_ * sizeof(uint64_t));
   Upload(d_masks_[which], h_pin_mask_[which], mask_words_ * sizeof(uint64_t));
   Check(hipEventRecord(done, S(stream_)), "mask event");
+  mask_on_device_[which] = true;
   if (which == kRelevant) mask_dirty_ = false;
 }
 
@@ -1175,14 +1223,18 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
     MappedResize(&h_cand_coeff_, &m_cand_coeff_, n_total_);
     MappedResize(&h_cand_rc_, &m_cand_rc_, n_total_);
     MappedResize(&h_dual_counts_, &m_dual_counts_, 2);
-    PinnedResize(&h_cb_cols_, n_total_);
-    PinnedResize(&h_cb_bits_, n_total_);
-    PinnedResize(&h_flip_cols_, n_total_);
-    PinnedResize(&h_flip_flags_, n_total_);
-    if (ev_cb_ == nullptr) {
-      hipEvent_t e;
-      Check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-      ev_cb_ = e;
+    // Column-bit changes and the listed boxed flips go through mapped memory
+    // (kernels read their inputs and write the flags there: no copies).
+    MappedResize(&h_cb_cols_, &m_cb_cols_, 2 * size_t(n_total_));
+    MappedResize(&h_cb_bits_, &m_cb_bits_, 2 * size_t(n_total_));
+    MappedResize(&h_flip_cols_, &m_flip_cols_, n_total_);
+    MappedResize(&h_flip_flags_, &m_flip_flags_, n_total_);
+    for (void*& ev : ev_cb_) {
+      if (ev == nullptr) {
+        hipEvent_t e;
+        Check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        ev = e;
+      }
     }
     last_candidates_ = 0;
     dual_ready_ = true;
@@ -1203,13 +1255,16 @@ void DeviceLp::DualSetColBits(const std::vector<int32_t>& cols,
   const int n = static_cast<int>(cols.size());
   if (n == 0) return;
   if (n > n_total_) throw DeviceError("dual device mode: too many column changes");
-  hipEvent_t done = reinterpret_cast<hipEvent_t>(ev_cb_);
+  // Two alternating slots of mapped memory: the host fills one while the
+  // kernel of the previous call may still read the other.
+  const int slot = cb_slot_;
+  cb_slot_ ^= 1;
+  hipEvent_t done = reinterpret_cast<hipEvent_t>(ev_cb_[slot]);
   Check(hipEventSynchronize(done), "colbits event");
-  std::memcpy(h_cb_cols_, cols.data(), n * sizeof(int32_t));
-  std::memcpy(h_cb_bits_, bits.data(), n);
-  Upload(d_small_cols_, h_cb_cols_, n * sizeof(int32_t));
-  Upload(d_small_bits_, h_cb_bits_, n);
-  Check(milp_launch::set_colbits(d_small_cols_, d_small_bits_, n, d_colbits_, S(stream_)),
+  const size_t off = size_t(slot) * n_total_;
+  std::memcpy(h_cb_cols_ + off, cols.data(), n * sizeof(int32_t));
+  std::memcpy(h_cb_bits_ + off, bits.data(), n);
+  Check(milp_launch::set_colbits(m_cb_cols_ + off, m_cb_bits_ + off, n, d_colbits_, S(stream_)),
         "colbits");
   Check(hipEventRecord(done, S(stream_)), "colbits event");
 }
@@ -1346,13 +1401,19 @@ void DeviceLp::DualBoxedFlips(const std::vector<int>* cols, double threshold,
   const int n = cols != nullptr ? static_cast<int>(cols->size()) : n_total_;
   flags->assign(n, 0);
   if (n == 0) return;
-  const int32_t* d_cols = nullptr;
   if (cols != nullptr) {
+    // A list (the candidates of one ratio test): columns in and flags out
+    // through mapped memory; the stream sync is the only round trip.
+    // (The previous listed call ended with a sync: the buffers are free.)
     std::memcpy(h_flip_cols_, cols->data(), n * sizeof(int32_t));
-    Upload(d_slots_, h_flip_cols_, n * sizeof(int32_t));
-    d_cols = d_slots_;
+    Check(milp_launch::boxed_flips(m_flip_cols_, n, d_rc_, d_colbits_, threshold, m_flip_flags_,
+                                   S(stream_)),
+          "boxed flips");
+    Synchronize();
+    std::memcpy(flags->data(), h_flip_flags_, n);
+    return;
   }
-  Check(milp_launch::boxed_flips(d_cols, n, d_rc_, d_colbits_, threshold, d_slot_flags_,
+  Check(milp_launch::boxed_flips(nullptr, n, d_rc_, d_colbits_, threshold, d_slot_flags_,
                                  S(stream_)),
         "boxed flips");
   Download(h_flip_flags_, d_slot_flags_, n);

@@ -807,6 +807,23 @@ void UpdateRow::FetchFromDevice() {
       coeff[pos[k]] = vals[k];
     }
   });
+  // MILP_TRACE: one line per fetched update row (algorithm, list, values).
+  static const char* trace = std::getenv("MILP_TRACE");
+  if (trace != nullptr) {
+    uint64_t hp = 1469598103934665603ull, hv = hp;
+    for (size_t k = 0; k < non_zero_position_list_.size(); ++k) {
+      hp = (hp ^ static_cast<uint32_t>(pos[k])) * 1099511628211ull;
+      uint64_t bits;
+      std::memcpy(&bits, &vals[k], sizeof(bits));
+      hv = (hv ^ bits) * 1099511628211ull;
+    }
+    if (FILE* f = std::fopen((std::string(trace) + ".device").c_str(), "a")) {
+      std::fprintf(f, "  update_row alg=%d n=%zu pos=%016llx val=%016llx\n", last_algorithm_,
+                   non_zero_position_list_.size(), static_cast<unsigned long long>(hp),
+                   static_cast<unsigned long long>(hv));
+      std::fclose(f);
+    }
+  }
 }
 
 // update_row.cc:196-216

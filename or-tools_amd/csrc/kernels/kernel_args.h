@@ -377,6 +377,8 @@ hipError_t set_colbits(const int32_t* cols, const uint8_t* bits, int n, uint8_t*
 // MakeBoxedVariableDualFeasible (revised_simplex.cc:2391-2437) decisions:
 // flag[i] = new status (AT_LOWER/AT_UPPER) if cols[i] flips, else 0xff.
 // cols == nullptr: every column whose bit 2 (non-basic boxed) is set.
+hipError_t set_mask_words(const int32_t* idx, const uint64_t* words, int n, uint64_t* mask,
+                          hipStream_t s);
 hipError_t boxed_flips(const int32_t* cols, int n, const double* rc, const uint8_t* colbits,
                        double threshold, uint8_t* flag, hipStream_t s);
 // segments: num_segments pairs; (lb, le) with lb >= 0 = levels [lb, le) on

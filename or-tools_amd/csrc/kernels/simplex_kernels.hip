@@ -1203,6 +1203,14 @@ __global__ void set_colbits_kernel(const int32_t* cols, const uint8_t* bits, int
     colbits[cols[i]] = bits[i];
 }
 
+// Changed words of a column mask: mask[idx[i]] = words[i] (inputs in mapped
+// host memory: no copy-engine transfer for a mask that moved a few bits).
+__global__ void set_mask_words_kernel(const int32_t* idx, const uint64_t* words, int n,
+                                      uint64_t* mask) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    mask[idx[i]] = words[i];
+}
+
 // glop::VariableStatus values (lp_types.h:188-219).
 constexpr int kAtLowerBound = 2;
 constexpr int kAtUpperBound = 3;
@@ -1531,6 +1539,13 @@ hipError_t set_colbits(const int32_t* cols, const uint8_t* bits, int n, uint8_t*
                        hipStream_t s) {
   if (n <= 0) return hipSuccess;
   set_colbits_kernel<<<grid_for(n), 256, 0, s>>>(cols, bits, n, colbits);
+  return hipGetLastError();
+}
+
+hipError_t set_mask_words(const int32_t* idx, const uint64_t* words, int n, uint64_t* mask,
+                          hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  set_mask_words_kernel<<<grid_for(n), 256, 0, s>>>(idx, words, n, mask);
   return hipGetLastError();
 }
 

@@ -45,10 +45,20 @@ def test_sharded_primal(shards, monkeypatch):
     assert g.kernel_stats()["pricing"]["launches"] > 0
 
 
-@pytest.mark.xfail(reason="known divergence: with shards of more than 8192 columns (the generic "
-                   "per-shard path, also forced on small LPs by MILP_SMALL_FUSED=off) the first "
-                   "pivot differs from the unsplit engine; under investigation (DESIGN.md 8)",
-                   strict=False)
+@pytest.mark.parametrize("small_fused", ["auto", "off"])
+def test_sharded_generic_path_small_lp(small_fused, monkeypatch):
+    """The per-shard generic path (MILP_SMALL_FUSED=off forces it at this
+    size): a shard whose columns are all relevant at the start (slack basis)
+    must still receive its relevant mask (regression: it once kept the
+    device's uninitialized words and its update rows came back empty)."""
+    monkeypatch.setenv("MILP_SHARDS", "2")
+    monkeypatch.setenv("MILP_SMALL_FUSED", small_fused)
+    lp = lp_gen.sparse_c5_lp(2000, 20000, 10, 97)
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+
+
 def test_sharded_c5_shaped_window(monkeypatch):
     """A 20k x 200k config-5-shaped LP, 8 virtual shards, dual device mode
     at its default size threshold, 3000 iterations against the oracle."""
