@@ -148,20 +148,30 @@ void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, cons
   // Launch segments of the level plan: each wide level alone over the chip,
   // each run of narrow levels as one single-CU launch (tri_solve.hip).
   s->segments.clear();
+  // Narrow = fits one CU and its LDS value store.
+  const int wide_level = std::min(tri_wide_level_, milp_kernels::kTriLdsVals - 64);
   for (int l = 0; l <= depth;) {
     const int w = s->level_width[l];
     if (w == 0) {
       ++l;
       continue;
     }
-    if (w > tri_wide_level_) {
+    if (w > wide_level) {
       s->segments.push_back(-l - 1);
       s->segments.push_back(std::min(1024, (w + 255) / 256));
       ++l;
       continue;
     }
+    // A run of narrow levels, cut where its padded positions would overflow
+    // the CU kernel's LDS value store.
     int e = l;
-    while (e <= depth && s->level_width[e] <= tri_wide_level_) ++e;
+    int run = 0;
+    while (e <= depth && s->level_width[e] <= wide_level) {
+      const int padded = (s->level_width[e] + 63) / 64 * 64;
+      if (e > l && run + padded > milp_kernels::kTriLdsVals) break;
+      run += padded;
+      ++e;
+    }
     s->segments.push_back(l);
     s->segments.push_back(e);
     l = e;

@@ -273,6 +273,9 @@ struct RowSumArgs {
 // values kept in that order on the device.
 constexpr int kTriThreads = 1024;
 constexpr int kTriPrefetch = 2;  // outputs per thread loaded ahead of their level
+// Values a single-CU run of levels keeps in LDS (its own outputs): a run's
+// positions never exceed this (the schedule builder cuts runs there).
+constexpr int kTriLdsVals = 16384;
 struct TriSolveArgs {
   const int32_t* level_start;  // [num_levels + 1] list positions of each level
   const int32_t* rec_row;      // [num_work] row (index into x) of each listed output

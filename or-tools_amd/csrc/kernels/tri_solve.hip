@@ -219,16 +219,96 @@ __global__ __launch_bounds__(256) void tri_level_grid_kernel(TriSolveArgs a, int
   }
 }
 
+// The value of position p inside a single-CU run: outputs of this run from
+// LDS (seg_lo = the run's first position), earlier positions from global
+// memory, where an earlier launch left them final (plain loads are safe
+// across a kernel boundary).
+struct TriRunValues {
+  const double* y;
+  const double* lds;
+  int seg_lo;
+  __device__ __forceinline__ double operator()(int p) const {
+    return p >= seg_lo ? lds[p - seg_lo] : y[p];
+  }
+};
+
+// tri_apply with the values read through `val` (same terms, same order).
+template <typename Val>
+__device__ __forceinline__ double tri_apply_vals(const TriSolveArgs& a, const Val& val, double sum,
+                                                 const TriRec& r) {
+  if (a.sequential) {
+    if (r.n <= 4) {
+      const int n = r.n;
+      const double y0 = n > 0 ? val(r.e.x) : 0.0;
+      const double y1 = n > 1 ? val(r.e.y) : 0.0;
+      const double y2 = n > 2 ? val(r.e.z) : 0.0;
+      const double y3 = n > 3 ? val(r.e.w) : 0.0;
+      if (y0 != 0.0) sum -= y0 * r.v[0];
+      if (y1 != 0.0) sum -= y1 * r.v[1];
+      if (y2 != 0.0) sum -= y2 * r.v[2];
+      if (y3 != 0.0) sum -= y3 * r.v[3];
+    } else {
+      for (int e = r.e.x, end = r.e.x + r.n; e < end; ++e) {
+        const double v = val(a.ovf_pos[e]);
+        if (v != 0.0) sum -= v * a.ovf_value[e];
+      }
+    }
+    return sum;  // unit diagonal
+  }
+  if (r.n <= 4) {
+    const int n = r.n;
+    const double y0 = n > 0 ? val(r.e.x) : 0.0;
+    const double y1 = n > 1 ? val(r.e.y) : 0.0;
+    const double y2 = n > 2 ? val(r.e.z) : 0.0;
+    const double y3 = n > 3 ? val(r.e.w) : 0.0;
+    if (n == 4) {
+      sum -= r.v[0] * y0 + r.v[1] * y1 + r.v[2] * y2 + r.v[3] * y3;
+    } else {
+      if (n > 0) sum -= r.v[0] * y0;
+      if (n > 1) sum -= r.v[1] * y1;
+      if (n > 2) sum -= r.v[2] * y2;
+    }
+  } else {
+    // subtract_overflow's grouping: batches of 8 as two groups of 4, then 4s,
+    // then the 1-3 remaining one by one.
+    int e = r.e.x;
+    const int end = r.e.x + r.n;
+    for (; e + 7 < end; e += 8) {
+      double p[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) p[i] = a.ovf_value[e + i] * val(a.ovf_pos[e + i]);
+      sum -= p[0] + p[1] + p[2] + p[3];
+      sum -= p[4] + p[5] + p[6] + p[7];
+    }
+    for (; e + 3 < end; e += 4) {
+      sum -= a.ovf_value[e] * val(a.ovf_pos[e]) + a.ovf_value[e + 1] * val(a.ovf_pos[e + 1]) +
+             a.ovf_value[e + 2] * val(a.ovf_pos[e + 2]) +
+             a.ovf_value[e + 3] * val(a.ovf_pos[e + 3]);
+    }
+    if (e < end) {
+      sum -= a.ovf_value[e] * val(a.ovf_pos[e]);
+      if (e + 1 < end) {
+        sum -= a.ovf_value[e + 1] * val(a.ovf_pos[e + 1]);
+        if (e + 2 < end) sum -= a.ovf_value[e + 2] * val(a.ovf_pos[e + 2]);
+      }
+    }
+  }
+  return a.diag != nullptr ? sum / r.d : sum;
+}
+
 // Narrow levels [level_begin, level_end) on one CU, one level after the
-// other with a barrier between them (the level's stores have reached L2:
-// explicit s_waitcnt vmcnt(0), then s_barrier; __syncthreads alone does not
-// wait for them at workgroup scope).
+// other. The run's own outputs live in LDS (written there and to global
+// memory for the later launches), so a level hands its values to the next
+// through LDS with one barrier, not through L2 with a store drain.
 __global__ __launch_bounds__(kTriThreads) void tri_levels_cu_kernel(TriSolveArgs a,
                                                                     int level_begin,
                                                                     int level_end) {
+  __shared__ double lds_y[kTriLdsVals];
   double* y = a.y;
   const int tid = threadIdx.x;
   const int top = *a.top;
+  const int seg_lo = a.level_start[level_begin];
+  const TriRunValues val{y, lds_y, seg_lo};
   if (a.clock != nullptr && tid == 0) a.clock[level_begin] = wall_clock64();
   TriRec pre[kTriPrefetch];
   {
@@ -253,17 +333,22 @@ __global__ __launch_bounds__(kTriThreads) void tri_levels_cu_kernel(TriSolveArgs
         tri_load(a, nb + j * kTriThreads + tid, ne, top, &pre[j]);
       }
     }
+    auto compute = [&](int k, const TriRec& r) {
+      if (k >= le) return;
+      // Not computed (row above top, or padding): the input, as tri_compute
+      // leaves it in y.
+      const double out = r.row > top ? y[k] : tri_apply_vals(a, val, y[k], r);
+      lds_y[k - seg_lo] = out;
+      if (r.row <= top) y[k] = out;
+    };
 #pragma unroll
-    for (int j = 0; j < kTriPrefetch; ++j) {
-      tri_compute(a, y, lb + j * kTriThreads + tid, top, cur[j]);
-    }
+    for (int j = 0; j < kTriPrefetch; ++j) compute(lb + j * kTriThreads + tid, cur[j]);
     // Positions beyond the prefetched ones (levels wider than the prefetch).
     for (int k = lb + kTriPrefetch * kTriThreads + tid; k < le; k += kTriThreads) {
       TriRec r;
       tri_load(a, k, le, top, &r);
-      tri_compute(a, y, k, top, r);
+      compute(k, r);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (a.clock != nullptr && tid == 0) a.clock[l + 1] = wall_clock64();
   }
