@@ -190,6 +190,7 @@ class DeviceLp : public DeviceSolver {
   T* Alloc(size_t n);
   void Upload(void* dst, const void* src, size_t bytes);
   void Download(void* dst, const void* src, size_t bytes);
+  void WaitStream();
   void BeginKernel(int id);
   void EndKernel(int id, double bytes, bool count_launch = true);
   void* TakeEvent();

@@ -1,5 +1,6 @@
 // DeviceLp: device buffers + kernel launch plumbing (see device_lp.h).
 #include "device_lp.h"
+#include "fibers.h"
 #include "host_pool.h"
 
 #include <hip/hip_runtime.h>
@@ -198,15 +199,25 @@ void StartWatchdog() {
 }
 }  // namespace
 
+// The stream wait of this handle. On a fiber of a batched solve (fibers.h)
+// the fiber yields while the stream is busy, so the thread runs another LP's
+// host work instead of spinning.
+void DeviceLp::WaitStream() {
+  if (InFiber()) {
+    while (hipStreamQuery(S(stream_)) == hipErrorNotReady) FiberYield();
+  }
+  Check(hipStreamSynchronize(S(stream_)), "sync");
+}
+
 void DeviceLp::Download(void* dst, const void* src, size_t bytes) {
   if (bytes == 0) return;
   Check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, S(stream_)), "D2H");
-  Check(hipStreamSynchronize(S(stream_)), "sync");
+  WaitStream();
 }
 
 void DeviceLp::Synchronize() {
   DeviceOp("Synchronize");
-  Check(hipStreamSynchronize(S(stream_)), "sync");
+  WaitStream();
   DeviceOp("Synchronize done");
   small_inflight_ = false;
   for (auto& d : shards_) d->Synchronize();

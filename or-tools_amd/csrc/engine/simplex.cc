@@ -23,6 +23,7 @@
 
 #include "../../../include/mi_lp.h"
 #include "device_lp.h"
+#include "fibers.h"
 #include "host_pool.h"
 
 #include <chrono>
@@ -5577,15 +5578,26 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
     if (handles[i] == nullptr) return MI_LP_ERROR_NULL;
   }
   if (num_threads < 1) num_threads = 1;
+  // MILP_BATCH_FIBERS=k: each thread drives k LPs at once on fibers, switching
+  // at stream waits (fibers.h); 1 = one LP at a time per thread.
+  int fibers = 1;
+  if (const char* e = std::getenv("MILP_BATCH_FIBERS")) fibers = std::max(1, std::atoi(e));
   std::atomic<int> next(0);
   std::vector<std::thread> pool;
   for (int t = 0; t < num_threads; ++t) {
     pool.emplace_back([&]() {
-      while (true) {
-        const int i = next.fetch_add(1);
-        if (i >= count) break;
-        RunSolve(handles[i], nullptr, &results[i]);
+      std::vector<std::function<void()>> tasks;
+      for (int f = 0; f < fibers; ++f) {
+        tasks.push_back([&]() {
+          while (true) {
+            const int i = next.fetch_add(1);
+            if (i >= count) break;
+            (void)hipSetDevice(handles[i]->device);
+            RunSolve(handles[i], nullptr, &results[i]);
+          }
+        });
       }
+      milp::RunFibers(std::move(tasks));
     });
   }
   for (auto& th : pool) th.join();
@@ -5617,29 +5629,43 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
   if (warm_state != nullptr && warm_len != n + workers[0]->lp.m) {
     return MI_LP_ERROR_INVALID_PROBLEM;
   }
+  // MILP_BATCH_THREADS=t < num_workers: t host threads, worker w on thread
+  // w % t, the workers of one thread interleaved as fibers at their stream
+  // waits (fibers.h). Default: one thread per worker.
+  int threads = num_workers;
+  if (const char* e = std::getenv("MILP_BATCH_THREADS")) {
+    threads = std::max(1, std::min(num_workers, std::atoi(e)));
+  }
   std::atomic<int> next(0);
-  std::vector<std::thread> pool;
-  for (int w = 0; w < num_workers; ++w) {
-    pool.emplace_back([&, w]() {
-      mi_lp* h = workers[w];
-      (void)hipSetDevice(h->device);
-      while (true) {
-        const int i = next.fetch_add(1);
-        if (i >= count) break;
-        int rc = mi_lp_set_variable_bounds(h, lbs + i * n, ubs + i * n);
+  auto worker_loop = [&](mi_lp* h) {
+    (void)hipSetDevice(h->device);
+    while (true) {
+      const int i = next.fetch_add(1);
+      if (i >= count) break;
+      int rc = mi_lp_set_variable_bounds(h, lbs + i * n, ubs + i * n);
+      if (rc != MI_LP_OK) {
+        FailEntry(h, rc, "mi_lp_set_variable_bounds failed", &results[i]);
+        continue;
+      }
+      if (warm_state != nullptr) {
+        rc = mi_lp_load_basis_state(h, warm_state, warm_len);
         if (rc != MI_LP_OK) {
-          FailEntry(h, rc, "mi_lp_set_variable_bounds failed", &results[i]);
+          FailEntry(h, rc, "mi_lp_load_basis_state failed", &results[i]);
           continue;
         }
-        if (warm_state != nullptr) {
-          rc = mi_lp_load_basis_state(h, warm_state, warm_len);
-          if (rc != MI_LP_OK) {
-            FailEntry(h, rc, "mi_lp_load_basis_state failed", &results[i]);
-            continue;
-          }
-        }
-        RunSolve(h, nullptr, &results[i]);
       }
+      RunSolve(h, nullptr, &results[i]);
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t) {
+    pool.emplace_back([&, t]() {
+      std::vector<std::function<void()>> tasks;
+      for (int w = t; w < num_workers; w += threads) {
+        mi_lp* h = workers[w];
+        tasks.push_back([&worker_loop, h]() { worker_loop(h); });
+      }
+      milp::RunFibers(std::move(tasks));
     });
   }
   for (auto& th : pool) th.join();

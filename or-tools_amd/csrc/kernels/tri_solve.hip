@@ -219,16 +219,17 @@ __global__ __launch_bounds__(256) void tri_level_grid_kernel(TriSolveArgs a, int
   }
 }
 
-// The value of position p inside a single-CU run: outputs of this run from
-// LDS (seg_lo = the run's first position), earlier positions from global
-// memory, where an earlier launch left them final (plain loads are safe
-// across a kernel boundary).
+// The value of position p inside a single-CU run: outputs of this run
+// ([seg_lo, seg_hi)) from LDS; every other position -- outputs of earlier
+// launches, and the read-only rows listed after all levels -- from global
+// memory, where an earlier launch left it final (plain loads are safe across
+// a kernel boundary).
 struct TriRunValues {
   const double* y;
   const double* lds;
-  int seg_lo;
+  int seg_lo, seg_hi;
   __device__ __forceinline__ double operator()(int p) const {
-    return p >= seg_lo ? lds[p - seg_lo] : y[p];
+    return (p >= seg_lo && p < seg_hi) ? lds[p - seg_lo] : y[p];
   }
 };
 
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(kTriThreads) void tri_levels_cu_kernel(TriSolveArgs
   const int tid = threadIdx.x;
   const int top = *a.top;
   const int seg_lo = a.level_start[level_begin];
-  const TriRunValues val{y, lds_y, seg_lo};
+  const TriRunValues val{y, lds_y, seg_lo, a.level_start[level_end]};
   if (a.clock != nullptr && tid == 0) a.clock[level_begin] = wall_clock64();
   TriRec pre[kTriPrefetch];
   {
