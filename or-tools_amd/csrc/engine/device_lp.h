@@ -191,6 +191,16 @@ class DeviceLp : public DeviceSolver {
   void Upload(void* dst, const void* src, size_t bytes);
   void Download(void* dst, const void* src, size_t bytes);
   void WaitStream();
+  // Batched small-LP launches (MILP_SMALL_BATCH=1): the request goes into
+  // this handle's slot of the device's SmallBatcher instead of a launch of
+  // its own; WaitStream then waits for the slot's done word.
+  template <typename Args>
+  void LaunchSmall(int kind, const Args& args);
+  void WaitSmallBatch();
+  bool small_batch_ = false;
+  int batch_slot_ = -1;
+  unsigned long long batch_seq_ = 0;
+  bool batch_pending_ = false;
   void BeginKernel(int id);
   void EndKernel(int id, double bytes, bool count_launch = true);
   void* TakeEvent();

@@ -49,8 +49,15 @@ namespace {
 void StartWatchdog();
 }  // namespace
 
+void ReleaseSmallBatchSlot(int device, int slot);  // below, with SmallBatcher
+
 DeviceLp::~DeviceLp() {
   if (device_ >= 0) (void)hipSetDevice(device_);
+  try {
+    WaitSmallBatch();  // a batched request may still write this handle's buffers
+  } catch (const std::exception&) {
+  }
+  if (batch_slot_ >= 0) ReleaseSmallBatchSlot(device_, batch_slot_);
   if (stream_ != nullptr) (void)hipStreamSynchronize(S(stream_));
   FreeTriBuffers();
   for (void* p : allocations_) (void)hipFree(p);
@@ -145,6 +152,7 @@ void DeviceLp::Init(int device) {
     tri_syncfree_min_levels_ = std::atoi(v);
   }
   if (const char* v = std::getenv("MILP_TRI_FUSE0")) tri_fuse0_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_SMALL_BATCH")) small_batch_ = std::atoi(v) != 0;
   CreateShards();
   StartWatchdog();
 }
@@ -199,10 +207,209 @@ void StartWatchdog() {
 }
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// SmallBatcher: one per device. Handles of small LPs post their one-launch
+// update rows (and list dots) as requests; whichever thread finds no launch
+// under way becomes the launcher and sends every pending request of a kind
+// in one launch of small_batch_kernel (one workgroup per request) on the
+// batcher's stream, until nothing is pending. A request's completion is a
+// sequence number the kernel writes into mapped memory: waiting costs no HIP
+// call. Many small LPs then cost one HIP launch per batch instead of one per
+// LP iteration (the HIP launch path serializes launches from many threads).
+namespace {
+class SmallBatcher {
+ public:
+  static constexpr int kMaxSlots = 2048;
+  static SmallBatcher& Get(int device) {
+    static std::mutex mu;
+    static std::vector<std::unique_ptr<SmallBatcher>> all;
+    std::lock_guard<std::mutex> lock(mu);
+    if (static_cast<int>(all.size()) <= device) all.resize(device + 1);
+    if (!all[device]) all[device].reset(new SmallBatcher(device));
+    return *all[device];
+  }
+  int AddSlot() {
+    std::lock_guard<std::mutex> lock(mu_);
+    if (!free_slots_.empty()) {
+      const int id = free_slots_.back();
+      free_slots_.pop_back();
+      return id;
+    }
+    if (next_slot_ >= kMaxSlots) throw DeviceError("small batch: too many handles");
+    return next_slot_++;
+  }
+  // A slot whose last request has completed goes back to the pool; its done
+  // word keeps the last sequence number, the next owner starts above it.
+  void FreeSlot(int id) {
+    std::lock_guard<std::mutex> lock(mu_);
+    free_slots_.push_back(id);
+  }
+  milp_kernels::SmallSlot* slot(int id) { return h_slots_ + id; }
+  unsigned long long done(int id) const {
+    return __atomic_load_n(h_done_ + id, __ATOMIC_ACQUIRE);
+  }
+  void Submit(int kind, int id) {
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      pending_[kind].push_back(id);
+      if (launching_) return;
+      launching_ = true;
+    }
+    std::vector<int> batch[milp_kernels::kSmallKinds];
+    while (true) {
+      {
+        std::lock_guard<std::mutex> lock(mu_);
+        bool any = false;
+        for (int k = 0; k < milp_kernels::kSmallKinds; ++k) {
+          batch[k].swap(pending_[k]);
+          pending_[k].clear();
+          any = any || !batch[k].empty();
+        }
+        if (!any) {
+          launching_ = false;
+          return;
+        }
+      }
+      (void)hipSetDevice(device_);
+      for (int k = 0; k < milp_kernels::kSmallKinds; ++k) {
+        for (size_t at = 0; at < batch[k].size(); at += milp_kernels::kSmallBatchMax) {
+          milp_kernels::SmallBatchArgs a{};
+          a.slots = m_slots_;
+          a.done = m_done_;
+          a.count = static_cast<int>(
+              std::min<size_t>(milp_kernels::kSmallBatchMax, batch[k].size() - at));
+          for (int i = 0; i < a.count; ++i) a.ids[i] = batch[k][at + i];
+          const hipError_t e = milp_launch::small_batch(k, a, stream_);
+          if (e != hipSuccess) {
+            std::lock_guard<std::mutex> lock(mu_);
+            launching_ = false;
+            throw DeviceError(std::string("small batch launch: ") + hipGetErrorString(e));
+          }
+        }
+        batch[k].clear();
+      }
+    }
+  }
+
+ private:
+  explicit SmallBatcher(int device) : device_(device) {
+    (void)hipSetDevice(device);
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      throw DeviceError("small batch: stream");
+    }
+    stream_ = s;
+    void* p = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&p, sizeof(milp_kernels::SmallSlot) * kMaxSlots, hipHostMallocMapped) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+      throw DeviceError("small batch: slots");
+    }
+    std::memset(p, 0, sizeof(milp_kernels::SmallSlot) * kMaxSlots);
+    h_slots_ = static_cast<milp_kernels::SmallSlot*>(p);
+    m_slots_ = static_cast<const milp_kernels::SmallSlot*>(d);
+    if (hipHostMalloc(&p, sizeof(unsigned long long) * kMaxSlots, hipHostMallocMapped) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+      throw DeviceError("small batch: done words");
+    }
+    std::memset(p, 0, sizeof(unsigned long long) * kMaxSlots);
+    h_done_ = static_cast<unsigned long long*>(p);
+    m_done_ = static_cast<unsigned long long*>(d);
+  }
+  int device_;
+  hipStream_t stream_ = nullptr;
+  std::mutex mu_;
+  std::vector<int> pending_[milp_kernels::kSmallKinds];
+  bool launching_ = false;
+  int next_slot_ = 0;
+  std::vector<int> free_slots_;
+  milp_kernels::SmallSlot* h_slots_ = nullptr;
+  const milp_kernels::SmallSlot* m_slots_ = nullptr;
+  unsigned long long* h_done_ = nullptr;
+  unsigned long long* m_done_ = nullptr;
+};
+
+void SetSlotArgs(milp_kernels::SmallSlot* s, const milp_kernels::RowWiseSmallArgs& a) { s->rw = a; }
+void SetSlotArgs(milp_kernels::SmallSlot* s, const milp_kernels::ColWiseSmallArgs& a) { s->cw = a; }
+void SetSlotArgs(milp_kernels::SmallSlot* s, const milp_kernels::ListDotsSmallArgs& a) { s->ld = a; }
+void SetSlotArgs(milp_kernels::SmallSlot* s, const milp_kernels::RowWiseSmallColArgs& a) {
+  s->rc = a;
+}
+}  // namespace
+
+void ReleaseSmallBatchSlot(int device, int slot) { SmallBatcher::Get(device).FreeSlot(slot); }
+
+template <typename Args>
+void DeviceLp::LaunchSmall(int kind, const Args& args) {
+  if (!small_batch_) {
+    hipError_t e = hipSuccess;
+    switch (kind) {
+      case milp_kernels::kSmallRowWise:
+        e = milp_launch::row_wise_update_small(
+            reinterpret_cast<const milp_kernels::RowWiseSmallArgs&>(args), small_threads_,
+            S(stream_));
+        break;
+      case milp_kernels::kSmallColWise:
+        e = milp_launch::column_wise_update_small(
+            reinterpret_cast<const milp_kernels::ColWiseSmallArgs&>(args), S(stream_));
+        break;
+      case milp_kernels::kSmallListDots:
+        e = milp_launch::list_dots_small(
+            reinterpret_cast<const milp_kernels::ListDotsSmallArgs&>(args), S(stream_));
+        break;
+      default:
+        e = milp_launch::row_wise_update_small_by_column(
+            reinterpret_cast<const milp_kernels::RowWiseSmallColArgs&>(args), S(stream_));
+        break;
+    }
+    Check(e, "small launch");
+    return;
+  }
+  // The batch kernel runs on the batcher's stream: this handle's own stream
+  // must have nothing in flight that the request reads.
+  if (hipStreamQuery(S(stream_)) != hipSuccess) Check(hipStreamSynchronize(S(stream_)), "sync");
+  if (batch_pending_) WaitSmallBatch();
+  SmallBatcher& b = SmallBatcher::Get(device_);
+  if (batch_slot_ < 0) {
+    batch_slot_ = b.AddSlot();
+    batch_seq_ = b.done(batch_slot_);  // continue above the previous owner's numbers
+  }
+  milp_kernels::SmallSlot* slot = b.slot(batch_slot_);
+  SetSlotArgs(slot, args);
+  slot->kind = kind;
+  slot->seq = ++batch_seq_;
+  batch_pending_ = true;
+  b.Submit(kind, batch_slot_);
+}
+
+void DeviceLp::WaitSmallBatch() {
+  if (!batch_pending_) return;
+  SmallBatcher& b = SmallBatcher::Get(device_);
+  const auto t0 = std::chrono::steady_clock::now();
+  int spins = 0;
+  while (b.done(batch_slot_) != batch_seq_) {
+    if (InFiber()) {
+      FiberYield();
+    } else {
+      __builtin_ia32_pause();
+    }
+    if (++spins == 1 << 16) {
+      spins = 0;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
+        throw DeviceError("small batch: request not completed within 20 s");
+      }
+    }
+  }
+  batch_pending_ = false;
+}
+
 // The stream wait of this handle. On a fiber of a batched solve (fibers.h)
 // the fiber yields while the stream is busy, so the thread runs another LP's
 // host work instead of spinning.
 void DeviceLp::WaitStream() {
+  WaitSmallBatch();
   if (InFiber()) {
     while (hipStreamQuery(S(stream_)) == hipErrorNotReady) FiberYield();
   }
@@ -714,7 +921,7 @@ void DeviceLp::UpdateRowColumnWiseSmall(const std::vector<double>& rho, double d
   a.host_count = d_map_count_;
   a.host_dots = d_small_dots_;
   BeginKernel(MI_K_UPDATE_ROW);
-  Check(milp_launch::column_wise_update_small(a, S(stream_)), "colwise small");
+  LaunchSmall(milp_kernels::kSmallColWise, a);
   EndKernel(MI_K_UPDATE_ROW, 12.0 * double(relevant_entries) + 8.0 * m_ + 9.0 * n_total_ +
                                  (w != nullptr ? 8.0 * m_ : 0.0));
   small_inflight_ = true;
@@ -871,7 +1078,7 @@ void DeviceLp::UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
     c.host_vals = d_map_vals_;
     c.host_count = d_map_count_;
     BeginKernel(id);
-    Check(milp_launch::row_wise_update_small_by_column(c, S(stream_)), "rowwise small by column");
+    LaunchSmall(milp_kernels::kSmallRowWiseByColumn, c);
     // The whole CSC copy, the filtered rows and multipliers, flags/coefficients.
     EndKernel(id, 12.0 * double(nnz_) + 8.0 * (n_total_ + 1) + 12.0 * k + 9.0 * n_total_);
     small_inflight_ = true;
@@ -900,7 +1107,7 @@ void DeviceLp::UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
   a.host_vals = d_map_vals_;
   a.host_count = d_map_count_;
   BeginKernel(id);
-  Check(milp_launch::row_wise_update_small(a, small_threads_, S(stream_)), "rowwise small");
+  LaunchSmall(milp_kernels::kSmallRowWise, a);
   // Rows and multipliers, the CSR entries, N-sized flags/coefficients, the list.
   EndKernel(id, 12.0 * entries + 12.0 * k + 9.0 * n_total_);
   small_inflight_ = true;
@@ -1040,7 +1247,7 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
     a.n = n;
     a.out = d_small_out_;
     BeginKernel(MI_K_PRIMAL_NORMS);
-    Check(milp_launch::list_dots_small(a, S(stream_)), "list dots small");
+    LaunchSmall(milp_kernels::kSmallListDots, a);
     EndKernel(MI_K_PRIMAL_NORMS, 12.0 * double(list_entries_) + 8.0 * m_ + 4.0 * n + 8.0 * n);
     Synchronize();
     std::memcpy(out->data(), h_small_out_, n * sizeof(double));

@@ -268,6 +268,29 @@ struct RowSumArgs {
 };
 
 
+// Batched small-LP launches (simplex_kernels.hip small_batch_kernel): one
+// request per LP in a slot of mapped host memory.
+enum SmallKind { kSmallRowWise = 0, kSmallColWise = 1, kSmallListDots = 2,
+                 kSmallRowWiseByColumn = 3, kSmallKinds = 4 };
+struct SmallSlot {
+  unsigned long long seq;  // published to done[slot] when the request is finished
+  int kind;
+  int pad;
+  union {
+    RowWiseSmallArgs rw;
+    ColWiseSmallArgs cw;
+    ListDotsSmallArgs ld;
+    RowWiseSmallColArgs rc;
+  };
+};
+constexpr int kSmallBatchMax = 128;  // requests per launch
+struct SmallBatchArgs {
+  const SmallSlot* slots;       // device view of the mapped slot table
+  unsigned long long* done;     // device view of the mapped done words
+  int count;
+  int ids[kSmallBatchMax];
+};
+
 // Dense triangular solve (tri_solve.hip): TransposeLowerSolve of a
 // TriangularMatrix with its outputs listed in dependency-level order and the
 // values kept in that order on the device.
@@ -341,6 +364,7 @@ hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s)
 // threads: 1024, or 256 (used when the filtered rows fit one per thread).
 hipError_t row_wise_update_small(const milp_kernels::RowWiseSmallArgs& args, int threads,
                                  hipStream_t s);
+hipError_t small_batch(int kind, const milp_kernels::SmallBatchArgs& args, hipStream_t s);
 hipError_t list_dots_small(const milp_kernels::ListDotsSmallArgs& args, hipStream_t s);
 hipError_t row_wise_update_small_by_column(const milp_kernels::RowWiseSmallColArgs& args,
                                            hipStream_t s);

@@ -580,7 +580,7 @@ __global__ __launch_bounds__(256) void row_wise_update_kernel(RowWiseArgs a) {
 // order with a barrier between rows (a position appears once per row, so one
 // thread owns it within a row), with the same first-write rule per algorithm.
 template <int THREADS>
-__global__ __launch_bounds__(THREADS) void row_wise_small_kernel(RowWiseSmallArgs a) {
+__device__ __forceinline__ void row_wise_small_body(const RowWiseSmallArgs& a) {
   __shared__ double acc[kSmallLdsCols];
   __shared__ uint8_t touched[kSmallLdsCols];
   __shared__ uint64_t rel[kSmallLdsCols / 64];
@@ -697,12 +697,17 @@ __global__ __launch_bounds__(THREADS) void row_wise_small_kernel(RowWiseSmallArg
   }
 }
 
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void row_wise_small_kernel(RowWiseSmallArgs a) {
+  row_wise_small_body<THREADS>(a);
+}
+
 // Small LPs: the column-wise update row (with the primal edge-norm dots when
 // w is given) and its compaction in one launch (ColWiseSmallArgs). Per column
 // the arithmetic and the write rule are column_dot_kernel's: kept columns
 // (relevant, |rho.a_j| > drop) get coefficient and w.a_j, the others keep their
 // stale coefficient. One thread per column (thread_column_dot).
-__global__ __launch_bounds__(kCompactThreads) void column_wise_small_kernel(ColWiseSmallArgs a) {
+__device__ __forceinline__ void column_wise_small_body(const ColWiseSmallArgs& a) {
   __shared__ double s_y[kSmallColWiseRows];
   __shared__ double s_w[kSmallColWiseRows];
   __shared__ uint8_t keep_flag[kSmallLdsCols];
@@ -760,9 +765,13 @@ __global__ __launch_bounds__(kCompactThreads) void column_wise_small_kernel(ColW
   }
 }
 
+__global__ __launch_bounds__(kCompactThreads) void column_wise_small_kernel(ColWiseSmallArgs a) {
+  column_wise_small_body(a);
+}
+
 // Small LPs: the primal edge-norm dots over the update-row list in one launch
 // (ListDotsSmallArgs), one thread per listed column.
-__global__ __launch_bounds__(kCompactThreads) void list_dots_small_kernel(ListDotsSmallArgs a) {
+__device__ __forceinline__ void list_dots_small_body(const ListDotsSmallArgs& a) {
   __shared__ double s_y[kSmallLdsCols];
   const int t = threadIdx.x;
   for (int i = t; i < a.m; i += kCompactThreads) s_y[i] = a.y[i];
@@ -771,6 +780,10 @@ __global__ __launch_bounds__(kCompactThreads) void list_dots_small_kernel(ListDo
     const int col = a.list[slot];
     a.out[slot] = thread_column_dot(a.starts[col], a.starts[col + 1], a.rows, a.vals, s_y);
   }
+}
+
+__global__ __launch_bounds__(kCompactThreads) void list_dots_small_kernel(ListDotsSmallArgs a) {
+  list_dots_small_body(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -887,8 +900,7 @@ __global__ __launch_bounds__(256) void row_wise_by_column_kernel(RowWiseColArgs 
 // Small LPs with many filtered rows: the same per-column accumulation in one
 // workgroup (row positions in LDS instead of the tag pass), then the
 // compaction into mapped host memory, as row_wise_small_kernel.
-__global__ __launch_bounds__(kCompactThreads) void row_wise_small_by_column_kernel(
-    RowWiseSmallColArgs a) {
+__device__ __forceinline__ void row_wise_small_by_column_body(const RowWiseSmallColArgs& a) {
   __shared__ int32_t s_pos[kSmallLdsCols];
   __shared__ double s_rho[kSmallLdsCols];
   __shared__ uint64_t rel[kSmallLdsCols / 64];
@@ -942,6 +954,50 @@ __global__ __launch_bounds__(kCompactThreads) void row_wise_small_by_column_kern
   if (t == kCompactThreads - 1) {
     *a.count = sums[t];
     *a.host_count = sums[t];
+  }
+}
+
+__global__ __launch_bounds__(kCompactThreads) void row_wise_small_by_column_kernel(
+    RowWiseSmallColArgs a) {
+  row_wise_small_by_column_body(a);
+}
+
+// ---------------------------------------------------------------------------
+// Batched small-LP launches: one workgroup per request of many LPs (one launch
+// instead of one per LP; the HIP launch path, not the GPU, bounds many
+// concurrent small LPs). A request's arguments sit in a slot of mapped host
+// memory; the workgroup stages them through LDS once, runs the same body as
+// the single launch, then publishes its slot's sequence number (system
+// scope, after a system fence: the results are visible to the host and to
+// later launches on other streams when the host sees the number).
+template <int KIND>
+__global__ __launch_bounds__(kCompactThreads) void small_batch_kernel(SmallBatchArgs b) {
+  __shared__ SmallSlot s_slot;
+  const SmallSlot* src = b.slots + b.ids[blockIdx.x];
+  {
+    const uint32_t* from = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* to = reinterpret_cast<uint32_t*>(&s_slot);
+    for (int i = threadIdx.x; i < int(sizeof(SmallSlot) / 4); i += blockDim.x) to[i] = from[i];
+  }
+  __syncthreads();
+  if constexpr (KIND == kSmallRowWise) {
+    const RowWiseSmallArgs a = s_slot.rw;
+    row_wise_small_body<kCompactThreads>(a);
+  } else if constexpr (KIND == kSmallColWise) {
+    const ColWiseSmallArgs a = s_slot.cw;
+    column_wise_small_body(a);
+  } else if constexpr (KIND == kSmallListDots) {
+    const ListDotsSmallArgs a = s_slot.ld;
+    list_dots_small_body(a);
+  } else {
+    const RowWiseSmallColArgs a = s_slot.rc;
+    row_wise_small_by_column_body(a);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(b.done + b.ids[blockIdx.x], s_slot.seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1450,6 +1506,28 @@ hipError_t row_wise_update_small(const RowWiseSmallArgs& args, int threads, hipS
     row_wise_small_kernel<256><<<1, 256, 0, s>>>(args);
   } else {
     row_wise_small_kernel<kCompactThreads><<<1, kCompactThreads, 0, s>>>(args);
+  }
+  return hipGetLastError();
+}
+
+hipError_t small_batch(int kind, const SmallBatchArgs& args, hipStream_t s) {
+  if (args.count <= 0) return hipSuccess;
+  if (args.count > kSmallBatchMax) return hipErrorInvalidValue;
+  switch (kind) {
+    case kSmallRowWise:
+      small_batch_kernel<kSmallRowWise><<<args.count, kCompactThreads, 0, s>>>(args);
+      break;
+    case kSmallColWise:
+      small_batch_kernel<kSmallColWise><<<args.count, kCompactThreads, 0, s>>>(args);
+      break;
+    case kSmallListDots:
+      small_batch_kernel<kSmallListDots><<<args.count, kCompactThreads, 0, s>>>(args);
+      break;
+    case kSmallRowWiseByColumn:
+      small_batch_kernel<kSmallRowWiseByColumn><<<args.count, kCompactThreads, 0, s>>>(args);
+      break;
+    default:
+      return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
