@@ -339,6 +339,7 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     out = {
         "metric": "batched LPs/sec", "value": total / elapsed, "unit": "LPs/s",
         "lps": total, "seconds": elapsed, "workers_per_gpu": args.batch_workers,
+        "host_threads_per_gpu": min(args.batch_workers, 16),
         "mean_iterations": float(np.mean([r.iterations for r in res])),
         "best_bound": best, "root_iterations": int(root_res.iterations),
         "workload": (f"config 4: job-shop {args.batch_jobs}x{args.batch_machines} "
@@ -348,7 +349,7 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_lib
-        ows = [oracle_lib.OracleLp(p) for _ in range(args.batch_workers)]
+        ows = [oracle_lib.OracleLp(p) for _ in range(args.batch_cpu_threads)]
         for w in ows:
             w.load(lp)
         n_cpu = min(len(lbs), args.batch_cpu_lps)
@@ -356,8 +357,8 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
         oracle_lib.batch_solve_bounds(ows, lbs[:n_cpu], ubs[:n_cpu], state)
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = {
-            "value": n_cpu / dt, "unit": "LPs/s", "cores": args.batch_workers, "kind": "port",
-            "sample": f"oracle, {args.batch_workers} threads, first {n_cpu} of the same children"}
+            "value": n_cpu / dt, "unit": "LPs/s", "cores": args.batch_cpu_threads, "kind": "port",
+            "sample": f"oracle, {args.batch_cpu_threads} threads, first {n_cpu} of the same children"}
     return out
 
 
@@ -393,7 +394,10 @@ def main():
                          "separate rocprofv3 --pmc pass (profiles/)")
     ap.add_argument("--batch-lps", type=int, default=512,
                     help="config-4 children per GPU (0 disables the batched section)")
-    ap.add_argument("--batch-workers", type=int, default=16)
+    ap.add_argument("--batch-workers", type=int, default=128,
+                    help="config-4 solver handles per GPU (LPs in flight); the engine runs "
+                         "them on at most 16 host threads as fibers with batched launches")
+    ap.add_argument("--batch-cpu-threads", type=int, default=16)
     ap.add_argument("--batch-jobs", type=int, default=15)
     ap.add_argument("--batch-machines", type=int, default=10)
     ap.add_argument("--batch-cpu-lps", type=int, default=512)

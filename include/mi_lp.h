@@ -272,7 +272,11 @@ int mi_lp_reset_kernel_stats(mi_lp* h);
 int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable);
 
 /* Batch API: solves count independent LPs already loaded in handles (all on
- * the same device), using worker threads each owning its own stream.
+ * the same device) on num_threads host threads; each thread drives several
+ * LPs as fibers (MILP_BATCH_FIBERS, default 4) switching at device waits, and
+ * their one-launch update rows go out in batched launches (one workgroup per
+ * LP request; MILP_SMALL_BATCH=0 turns that off). Results are per LP and
+ * identical to one-at-a-time solves.
  * Returns non-OK only for bad arguments; each LP's outcome (including its
  * error code) is in results[i]. No exception crosses this boundary. */
 int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
@@ -280,8 +284,9 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
 /* Batched children of one search node: count LPs that share
  * the workers' loaded matrix and differ in variable bounds (lbs/ubs are
  * count x n, row-major), each warm-started from warm_state (n+m statuses,
- * may be NULL, else warm_len must be n+m) like LoadStateForNextSolve. One
- * host thread per worker. A child whose bounds or state cannot be loaded is
+ * may be NULL, else warm_len must be n+m) like LoadStateForNextSolve. The
+ * workers run on at most 16 host threads (MILP_BATCH_THREADS), a thread's
+ * workers as fibers with batched small-LP launches (as mi_lp_batch_solve). A child whose bounds or state cannot be loaded is
  * not solved: results[i] = {ABNORMAL, that error code}. */
 int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t count,
                              const double* lbs, const double* ubs, const int8_t* warm_state,

@@ -183,6 +183,10 @@ class DeviceLp : public DeviceSolver {
   // shards, the candidates and update-row lists a concatenation. Row sums,
   // column norms and the triangular solves stay on this handle (full copy).
   int num_shards() const { return shards_.empty() ? 1 : static_cast<int>(shards_.size()); }
+  // Batched small-LP launches for this handle (the batch APIs turn it on for
+  // their duration; MILP_SMALL_BATCH=1 turns it on everywhere, =0 nowhere).
+  void SetSmallBatch(bool on);
+  bool small_batch() const { return small_batch_; }
   int shard_begin(int s) const { return shard_begin_[s]; }
 
  private:

@@ -7,6 +7,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -167,6 +168,7 @@ T* DeviceLp::Alloc(size_t n) {
 
 void DeviceLp::Upload(void* dst, const void* src, size_t bytes) {
   if (bytes == 0) return;
+  if (batch_pending_) WaitSmallBatch();  // stream work after a batched request
   Check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream_)), "H2D");
 }
 
@@ -221,12 +223,14 @@ class SmallBatcher {
  public:
   static constexpr int kMaxSlots = 2048;
   static SmallBatcher& Get(int device) {
+    // Never destroyed: the launcher thread sleeps in its wait at process
+    // exit, after the HIP runtime may already be gone.
     static std::mutex mu;
-    static std::vector<std::unique_ptr<SmallBatcher>> all;
+    static std::vector<SmallBatcher*>* all = new std::vector<SmallBatcher*>();
     std::lock_guard<std::mutex> lock(mu);
-    if (static_cast<int>(all.size()) <= device) all.resize(device + 1);
-    if (!all[device]) all[device].reset(new SmallBatcher(device));
-    return *all[device];
+    if (static_cast<int>(all->size()) <= device) all->resize(device + 1, nullptr);
+    if ((*all)[device] == nullptr) (*all)[device] = new SmallBatcher(device);
+    return *(*all)[device];
   }
   int AddSlot() {
     std::lock_guard<std::mutex> lock(mu_);
@@ -252,26 +256,41 @@ class SmallBatcher {
     {
       std::lock_guard<std::mutex> lock(mu_);
       pending_[kind].push_back(id);
-      if (launching_) return;
-      launching_ = true;
+      ++num_pending_;
     }
+    cv_.notify_one();
+  }
+
+  ~SmallBatcher() {
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      stop_ = true;
+    }
+    cv_.notify_one();
+    if (launcher_.joinable()) launcher_.join();
+  }
+
+ private:
+  // The launcher: takes every pending request, launches one kernel per kind
+  // (a workgroup per request), waits for it, repeats. With one batch in
+  // flight the requests of the other LPs gather while it runs, so a batch
+  // holds as many requests as LPs that reached their update row meanwhile.
+  void LauncherLoop() {
+    (void)hipSetDevice(device_);
     std::vector<int> batch[milp_kernels::kSmallKinds];
     while (true) {
       {
-        std::lock_guard<std::mutex> lock(mu_);
-        bool any = false;
+        std::unique_lock<std::mutex> lock(mu_);
+        cv_.wait(lock, [&] { return stop_ || num_pending_ > 0; });
+        if (stop_ && num_pending_ == 0) return;
         for (int k = 0; k < milp_kernels::kSmallKinds; ++k) {
           batch[k].swap(pending_[k]);
           pending_[k].clear();
-          any = any || !batch[k].empty();
         }
-        if (!any) {
-          launching_ = false;
-          return;
-        }
+        num_pending_ = 0;
       }
-      (void)hipSetDevice(device_);
-      for (int k = 0; k < milp_kernels::kSmallKinds; ++k) {
+      bool failed = false;
+      for (int k = 0; k < milp_kernels::kSmallKinds && !failed; ++k) {
         for (size_t at = 0; at < batch[k].size(); at += milp_kernels::kSmallBatchMax) {
           milp_kernels::SmallBatchArgs a{};
           a.slots = m_slots_;
@@ -279,26 +298,26 @@ class SmallBatcher {
           a.count = static_cast<int>(
               std::min<size_t>(milp_kernels::kSmallBatchMax, batch[k].size() - at));
           for (int i = 0; i < a.count; ++i) a.ids[i] = batch[k][at + i];
-          const hipError_t e = milp_launch::small_batch(k, a, stream_);
-          if (e != hipSuccess) {
-            std::lock_guard<std::mutex> lock(mu_);
-            launching_ = false;
-            throw DeviceError(std::string("small batch launch: ") + hipGetErrorString(e));
-          }
+          if (milp_launch::small_batch(k, a, streams_[0]) != hipSuccess) failed = true;
         }
         batch[k].clear();
       }
+      // A failed launch leaves its requests without a done word: their
+      // owners time out and report a DeviceError.
+      (void)hipStreamSynchronize(streams_[0]);
     }
   }
 
  private:
   explicit SmallBatcher(int device) : device_(device) {
     (void)hipSetDevice(device);
-    hipStream_t s;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
-      throw DeviceError("small batch: stream");
+    for (int i = 0; i < kStreams; ++i) {
+      hipStream_t s;
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        throw DeviceError("small batch: stream");
+      }
+      streams_[i] = s;
     }
-    stream_ = s;
     void* p = nullptr;
     void* d = nullptr;
     if (hipHostMalloc(&p, sizeof(milp_kernels::SmallSlot) * kMaxSlots, hipHostMallocMapped) !=
@@ -317,12 +336,17 @@ class SmallBatcher {
     std::memset(p, 0, sizeof(unsigned long long) * kMaxSlots);
     h_done_ = static_cast<unsigned long long*>(p);
     m_done_ = static_cast<unsigned long long*>(d);
+    launcher_ = std::thread([this] { LauncherLoop(); });
   }
   int device_;
-  hipStream_t stream_ = nullptr;
+  static constexpr int kStreams = 1;
+  hipStream_t streams_[kStreams] = {};
   std::mutex mu_;
+  std::condition_variable cv_;
+  std::thread launcher_;
+  bool stop_ = false;
+  int num_pending_ = 0;
   std::vector<int> pending_[milp_kernels::kSmallKinds];
-  bool launching_ = false;
   int next_slot_ = 0;
   std::vector<int> free_slots_;
   milp_kernels::SmallSlot* h_slots_ = nullptr;
@@ -343,7 +367,9 @@ void ReleaseSmallBatchSlot(int device, int slot) { SmallBatcher::Get(device).Fre
 
 template <typename Args>
 void DeviceLp::LaunchSmall(int kind, const Args& args) {
-  if (!small_batch_) {
+  // The dual device mode reads the update row on this handle's own stream
+  // without a host wait in between: its small LPs keep the single launch.
+  if (!small_batch_ || dual_ready_) {
     hipError_t e = hipSuccess;
     switch (kind) {
       case milp_kernels::kSmallRowWise:
@@ -382,6 +408,12 @@ void DeviceLp::LaunchSmall(int kind, const Args& args) {
   slot->seq = ++batch_seq_;
   batch_pending_ = true;
   b.Submit(kind, batch_slot_);
+}
+
+void DeviceLp::SetSmallBatch(bool on) {
+  if (!on) WaitSmallBatch();  // the last request completes before single launches resume
+  if (const char* v = std::getenv("MILP_SMALL_BATCH")) on = std::atoi(v) != 0;
+  small_batch_ = on;
 }
 
 void DeviceLp::WaitSmallBatch() {
@@ -478,6 +510,7 @@ void DeviceLp::BeginKernel(int id) {
                                        "dual_ratio", "readback", "tri_solve_tau", "tri_solve_l",
                                        "?", "?", "?", "?"};
   DeviceOp(kNames[id & 15]);
+  if (batch_pending_) WaitSmallBatch();  // kernels after a batched request see its results
   if (!timing_) return;
   if (ev_open_ == nullptr) ev_open_ = TakeEvent();
   Check(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_open_), S(stream_)), "ev");

@@ -5570,6 +5570,22 @@ int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable) {
   return MI_LP_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Back to single launches after a batch call (a device error there is the
+// handle's next call's to report).
+void SetSmallBatchSafe(mi_lp* h, bool on) {
+  try {
+    h->simplex.device().SetSmallBatch(on);
+  } catch (const std::exception& e) {
+    h->error = e.what();
+  }
+}
+}  // namespace
+
+extern "C" {
+
 int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
                       mi_lp_result* results) {
   if (handles == nullptr || results == nullptr) return MI_LP_ERROR_NULL;
@@ -5578,10 +5594,13 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
     if (handles[i] == nullptr) return MI_LP_ERROR_NULL;
   }
   if (num_threads < 1) num_threads = 1;
-  // MILP_BATCH_FIBERS=k: each thread drives k LPs at once on fibers, switching
-  // at stream waits (fibers.h); 1 = one LP at a time per thread.
-  int fibers = 1;
+  // Each thread drives several LPs at once on fibers (fibers.h), their
+  // small update rows going out in batched launches (SmallBatcher): while one
+  // LP waits for the device, the thread runs another one's host work.
+  // MILP_BATCH_FIBERS=k (default 4), MILP_SMALL_BATCH=0 turns batching off.
+  int fibers = 4;
   if (const char* e = std::getenv("MILP_BATCH_FIBERS")) fibers = std::max(1, std::atoi(e));
+  for (int i = 0; i < count; ++i) handles[i]->simplex.device().SetSmallBatch(true);
   std::atomic<int> next(0);
   std::vector<std::thread> pool;
   for (int t = 0; t < num_threads; ++t) {
@@ -5601,6 +5620,7 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
     });
   }
   for (auto& th : pool) th.join();
+  for (int i = 0; i < count; ++i) SetSmallBatchSafe(handles[i], false);
   return MI_LP_OK;  // per-entry outcomes are in results[i]
 }
 
@@ -5629,13 +5649,16 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
   if (warm_state != nullptr && warm_len != n + workers[0]->lp.m) {
     return MI_LP_ERROR_INVALID_PROBLEM;
   }
-  // MILP_BATCH_THREADS=t < num_workers: t host threads, worker w on thread
-  // w % t, the workers of one thread interleaved as fibers at their stream
-  // waits (fibers.h). Default: one thread per worker.
-  int threads = num_workers;
+  // At most kBatchThreads host threads (MILP_BATCH_THREADS): worker w runs on
+  // thread w % threads, the workers of one thread interleaved as fibers at
+  // their device waits (fibers.h), their small update rows sent in batched
+  // launches (SmallBatcher; MILP_SMALL_BATCH=0 turns batching off).
+  constexpr int kBatchThreads = 16;
+  int threads = std::min(num_workers, kBatchThreads);
   if (const char* e = std::getenv("MILP_BATCH_THREADS")) {
     threads = std::max(1, std::min(num_workers, std::atoi(e)));
   }
+  for (int w = 0; w < num_workers; ++w) workers[w]->simplex.device().SetSmallBatch(true);
   std::atomic<int> next(0);
   auto worker_loop = [&](mi_lp* h) {
     (void)hipSetDevice(h->device);
@@ -5669,6 +5692,7 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
     });
   }
   for (auto& th : pool) th.join();
+  for (int w = 0; w < num_workers; ++w) SetSmallBatchSafe(workers[w], false);
   return MI_LP_OK;  // per-entry outcomes are in results[i]
 }
 
