@@ -5601,6 +5601,18 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
   int fibers = 4;
   if (const char* e = std::getenv("MILP_BATCH_FIBERS")) fibers = std::max(1, std::atoi(e));
   for (int i = 0; i < count; ++i) handles[i]->simplex.device().SetSmallBatch(true);
+  // Largest LPs first (LPT order, weight (nnz + m) * m as in the multi-GPU
+  // partition of mi_glop.distributed): the long solves start early instead of
+  // forming the tail of the batch.
+  std::vector<int> order(count);
+  for (int i = 0; i < count; ++i) order[i] = i;
+  auto weight = [&](int i) {
+    const milp::LinearProgram& lp = handles[i]->lp;
+    const double nnz = lp.col_starts.empty() ? 0.0 : double(lp.col_starts.back());
+    return (nnz + lp.m) * double(lp.m);
+  };
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int a, int b) { return weight(a) > weight(b); });
   std::atomic<int> next(0);
   std::vector<std::thread> pool;
   for (int t = 0; t < num_threads; ++t) {
@@ -5609,8 +5621,9 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
       for (int f = 0; f < fibers; ++f) {
         tasks.push_back([&]() {
           while (true) {
-            const int i = next.fetch_add(1);
-            if (i >= count) break;
+            const int at = next.fetch_add(1);
+            if (at >= count) break;
+            const int i = order[at];
             (void)hipSetDevice(handles[i]->device);
             RunSolve(handles[i], nullptr, &results[i]);
           }

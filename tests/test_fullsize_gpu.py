@@ -18,6 +18,7 @@ from mi_glop import abi, engine
 
 import lp_gen
 import netlib_suite
+import oracle_lib
 import parity_util
 
 pytestmark = pytest.mark.gpu
@@ -61,3 +62,22 @@ def test_config3_suite_parity(member):
     o, ro, g, rg = parity_util.solve_both(lp, abi.default_params(), _handle)
     parity_util.compare(o, ro, g, rg, lp)
     assert ro.problem_status == abi.OPTIMAL
+
+
+def test_config3_batched_suite_parity():
+    """The config-3 path itself: mi_lp_batch_solve over suite members (fibers
+    and batched small-LP launches on, LPT order), every LP against the
+    oracle bit for bit."""
+    lps = netlib_suite.suite(max_rows=1000)
+    picks = list(range(0, len(lps), 3))
+    handles = []
+    for i in picks:
+        h = engine.LpHandle(abi.default_params())
+        h.load(lps[i])
+        handles.append(h)
+    res = engine.batch_solve(handles, num_threads=4)
+    for k, i in enumerate(picks):
+        o = oracle_lib.OracleLp(abi.default_params())
+        o.load(lps[i])
+        ro = o.solve()
+        parity_util.compare(o, ro, handles[k], res[k], lps[i])
