@@ -483,6 +483,7 @@ class DeviceLp : public DeviceSolver {
   bool tri_syncfree_ = true;  // MILP_TRI_SYNCFREE: readiness-driven single launch
   int tri_syncfree_min_levels_ = 0;  // MILP_TRI_SYNCFREE_MIN_LEVELS: shallower -> level plan
   bool tri_fuse0_ = true;     // MILP_TRI_FUSE0: level 0 inside the gather kernel
+  bool stream_priority_ = true;   // MILP_STREAM_PRIORITY=0: default priorities (+3-4 % on C5 with)
   bool tri_lower_ = true;     // MILP_TRI_LOWER: the L solves too
   int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
   uint64_t* d_tri_clock_ = nullptr;

@@ -105,7 +105,17 @@ void DeviceLp::Init(int device) {
   device_ = device;
   Check(hipSetDevice(device), "hipSetDevice");
   hipStream_t s;
-  Check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  // By default (MILP_STREAM_PRIORITY=0 turns it off) this handle's stream (the solver thread's
+  // kernels and triangular solves) at the highest priority, the tau
+  // worker's solve stream (device_solve.hip) at the lowest.
+  if (const char* v = std::getenv("MILP_STREAM_PRIORITY")) stream_priority_ = std::atoi(v) != 0;
+  if (stream_priority_) {
+    int least = 0, greatest = 0;
+    Check(hipDeviceGetStreamPriorityRange(&least, &greatest), "priority range");
+    Check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest), "hipStreamCreate");
+  } else {
+    Check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  }
   stream_ = s;
   hipEvent_t a, b;
   Check(hipEventCreate(&a), "hipEventCreate");

@@ -309,7 +309,13 @@ void DeviceLp::PrepareTriContext(int slot, int rows, int pos) {
       c.stream = stream_;
     } else {
       hipStream_t st;
-      Check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+      if (stream_priority_) {
+        int least = 0, greatest = 0;
+        Check(hipDeviceGetStreamPriorityRange(&least, &greatest), "priority range");
+        Check(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least), "hipStreamCreate");
+      } else {
+        Check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+      }
       c.stream = st;
     }
     for (void*& e : c.ev) {
