@@ -145,6 +145,7 @@ void DeviceLp::Init(int device) {
   }
   if (const char* r = std::getenv("MILP_SMALL_SERIAL_ROWS")) small_serial_rows_ = std::atoi(r);
   if (const char* r = std::getenv("MILP_SMALL_THREADS")) small_threads_ = std::atoi(r);
+  if (const char* f = std::getenv("MILP_MEDIUM")) medium_enabled_ = std::strcmp(f, "off") != 0;
   if (const char* v = std::getenv("MILP_DEVICE_SOLVE")) {
     if (std::strcmp(v, "force") == 0) tri_mode_ = 1;
     if (std::strcmp(v, "off") == 0) tri_mode_ = 2;
@@ -386,6 +387,10 @@ void DeviceLp::LaunchSmall(int kind, const Args& args) {
         e = milp_launch::row_wise_update_small(
             reinterpret_cast<const milp_kernels::RowWiseSmallArgs&>(args), small_threads_,
             S(stream_));
+        break;
+      case milp_kernels::kMediumRowWise:
+        e = milp_launch::row_wise_update_medium(
+            reinterpret_cast<const milp_kernels::RowWiseSmallArgs&>(args), S(stream_));
         break;
       case milp_kernels::kSmallColWise:
         e = milp_launch::column_wise_update_small(
@@ -667,7 +672,16 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   h_small_in_ = nullptr;
   small_inflight_ = false;
   mask_dirty_ = false;
-  if (n_total_ <= milp_kernels::kSmallLdsCols) {
+  medium_ = small_fused_enabled_ && medium_enabled_ && n_total_ > milp_kernels::kSmallLdsCols &&
+            n_total_ <= milp_kernels::kMediumCols;
+  if (medium_) {
+    d_medium_acc_ = Alloc<double>(n_total_);
+    d_medium_touch_ = Alloc<uint32_t>(n_total_);
+    Check(hipMemsetAsync(d_medium_touch_, 0, size_t(n_total_) * sizeof(uint32_t), S(stream_)),
+          "touch init");
+    medium_epoch_ = 0;
+  }
+  if (n_total_ <= milp_kernels::kSmallLdsCols || medium_) {
     const int cap = std::max(1, m_);  // filtered rows
     const size_t rho_off = (size_t(cap) * sizeof(int32_t) + 63) / 64 * 64;
     const size_t mask_off = rho_off + size_t(cap) * sizeof(double);
@@ -890,7 +904,7 @@ void DeviceLp::UpdateRowColumnWise(const std::vector<double>& rho, double drop,
   if (!shards_.empty()) return ShardedUpdateRowColumnWise(rho, drop, relevant_entries, w);
   CallTimer timer(&stats_, MI_K_UPDATE_ROW);
   small_dots_mapped_ = false;
-  if (small_fused_enabled_ && h_small_in_ != nullptr && nd_ == 0 &&
+  if (small_fused_enabled_ && h_small_in_ != nullptr && !medium_ && nd_ == 0 &&
       m_ <= milp_kernels::kSmallColWiseRows) {
     UpdateRowColumnWiseSmall(rho, drop, relevant_entries, w);
     return;
@@ -988,8 +1002,10 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
     // Few short rows: applied row by row; otherwise column by column.
     const bool serial = k <= small_serial_rows_ && k <= milp_kernels::kSmallRowsMax &&
                         entries <= milp_kernels::kSmallEntries;
-    UpdateRowRowWiseSmall(filtered_rows, rho, algorithm, drop, entries, serial);
-    return;
+    if (!medium_ || serial) {
+      UpdateRowRowWiseSmall(filtered_rows, rho, algorithm, drop, entries, serial);
+      return;
+    }
   }
   FlushRelevantMask();
   bool all_full = full_rows_enabled_ && k > 0;
@@ -1149,8 +1165,18 @@ void DeviceLp::UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
   a.host_list = d_map_list_;
   a.host_vals = d_map_vals_;
   a.host_count = d_map_count_;
+  if (medium_) {
+    if (++medium_epoch_ == 0) {  // wrapped: stale tags could match again
+      Check(hipMemsetAsync(d_medium_touch_, 0, size_t(n_total_) * sizeof(uint32_t), S(stream_)),
+            "touch reset");
+      medium_epoch_ = 1;
+    }
+    a.acc = d_medium_acc_;
+    a.touch = d_medium_touch_;
+    a.epoch = medium_epoch_;
+  }
   BeginKernel(id);
-  LaunchSmall(milp_kernels::kSmallRowWise, a);
+  LaunchSmall(medium_ ? milp_kernels::kMediumRowWise : milp_kernels::kSmallRowWise, a);
   // Rows and multipliers, the CSR entries, N-sized flags/coefficients, the list.
   EndKernel(id, 12.0 * entries + 12.0 * k + 9.0 * n_total_);
   small_inflight_ = true;
@@ -1276,7 +1302,8 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
     return;
   }
   fused_ready_ = false;
-  if (small_fused_enabled_ && h_small_in_ != nullptr && nd_ == 0) {
+  if (small_fused_enabled_ && h_small_in_ != nullptr && nd_ == 0 &&
+      m_ <= milp_kernels::kSmallLdsCols) {
     // Small LP: one launch, v in and the dots out through mapped host memory.
     if (small_inflight_) Synchronize();
     std::memcpy(h_small_y_, v.data(), m_ * sizeof(double));

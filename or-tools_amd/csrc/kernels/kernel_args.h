@@ -161,7 +161,13 @@ struct RowWiseSmallArgs {
   int32_t* host_list;  // mapped host memory
   double* host_vals;
   int* host_count;
+  // Medium LPs (kSmallLdsCols < N <= kMediumCols): accumulators in global
+  // memory, a position's accumulator valid when touch[pos] == epoch.
+  double* acc;
+  uint32_t* touch;
+  uint32_t epoch;
 };
+constexpr int kMediumCols = 65536;
 
 // The row-wise update row when every filtered row is full (all structural
 // columns present): entry j < num_structural of CSR row r is column j and the
@@ -271,7 +277,7 @@ struct RowSumArgs {
 // Batched small-LP launches (simplex_kernels.hip small_batch_kernel): one
 // request per LP in a slot of mapped host memory.
 enum SmallKind { kSmallRowWise = 0, kSmallColWise = 1, kSmallListDots = 2,
-                 kSmallRowWiseByColumn = 3, kSmallKinds = 4 };
+                 kSmallRowWiseByColumn = 3, kMediumRowWise = 4, kSmallKinds = 5 };
 struct SmallSlot {
   unsigned long long seq;  // published to done[slot] when the request is finished
   int kind;
@@ -364,6 +370,7 @@ hipError_t row_wise_update(const milp_kernels::RowWiseArgs& args, hipStream_t s)
 // threads: 1024, or 256 (used when the filtered rows fit one per thread).
 hipError_t row_wise_update_small(const milp_kernels::RowWiseSmallArgs& args, int threads,
                                  hipStream_t s);
+hipError_t row_wise_update_medium(const milp_kernels::RowWiseSmallArgs& args, hipStream_t s);
 hipError_t small_batch(int kind, const milp_kernels::SmallBatchArgs& args, hipStream_t s);
 hipError_t list_dots_small(const milp_kernels::ListDotsSmallArgs& args, hipStream_t s);
 hipError_t row_wise_update_small_by_column(const milp_kernels::RowWiseSmallColArgs& args,

@@ -702,6 +702,139 @@ __global__ __launch_bounds__(THREADS) void row_wise_small_kernel(RowWiseSmallArg
   row_wise_small_body<THREADS>(a);
 }
 
+// Medium LPs (N <= kMediumCols): row_wise_small_body's algorithm with the
+// accumulators in global memory (a.acc, valid where a.touch == a.epoch: no
+// clearing pass), read at agent scope after each row's barrier so a value
+// another wave stored is seen from L2. Same arithmetic, same order, same
+// write rules and the same list (increasing positions).
+__device__ __forceinline__ double medium_load(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void row_wise_medium_body(const RowWiseSmallArgs& a) {
+  constexpr int THREADS = kCompactThreads;
+  __shared__ uint64_t rel[kMediumCols / 64];
+  __shared__ unsigned long long listed_w[kMediumCols / 64];
+  __shared__ int32_t ent_pos[kSmallEntries];
+  __shared__ double ent_val[kSmallEntries];
+  __shared__ double s_rho[kSmallRowsMax];
+  __shared__ int64_t s_off[kSmallRowsMax];
+  __shared__ int s_beg[kSmallRowsMax + 1];
+  __shared__ int sums[THREADS];
+  const int t = threadIdx.x;
+  const int n = a.num_cols;
+  const int k_rows = a.num_filtered;
+  const uint32_t epoch = a.epoch;
+  for (int w = t; w < (n + 63) / 64; w += THREADS) rel[w] = a.relevant[w];
+  int len = 0;
+  if (t < k_rows) {
+    const int r = a.filtered_rows[t];
+    s_rho[t] = a.rho[t];
+    const int64_t b = a.t_starts[r];
+    s_off[t] = b;
+    len = static_cast<int>(a.t_starts[r + 1] - b);
+  }
+  sums[t] = len;
+  __syncthreads();
+  for (int off = 1; off < THREADS; off <<= 1) {
+    const int v = t >= off ? sums[t - off] : 0;
+    __syncthreads();
+    sums[t] += v;
+    __syncthreads();
+  }
+  if (t < k_rows) s_beg[t] = sums[t] - len;
+  if (t == 0) s_beg[k_rows] = sums[THREADS - 1];
+  __syncthreads();
+  const int num_entries = s_beg[k_rows];  // <= kSmallEntries (host-checked)
+  for (int e = t; e < num_entries; e += THREADS) {
+    int lo = 0;
+    int hi = k_rows - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_beg[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    const int64_t i = s_off[lo] + (e - s_beg[lo]);
+    ent_pos[e] = a.t_cols[i];
+    ent_val[e] = s_rho[lo] * a.t_vals[i];
+  }
+  __syncthreads();
+  for (int k = 0; k < k_rows; ++k) {
+    for (int e = s_beg[k] + t; e < s_beg[k + 1]; e += THREADS) {
+      const int pos = ent_pos[e];
+      const double v = ent_val[e];
+      const bool first =
+          __hip_atomic_load(a.touch + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch;
+      double out;
+      if (a.algorithm == 0) {
+        out = v;
+      } else if (first) {
+        out = a.algorithm == 2 ? 0.0 + v : v;
+      } else {
+        out = medium_load(a.acc + pos) + v;
+      }
+      a.acc[pos] = out;
+      a.touch[pos] = epoch;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // rows are applied in order
+  }
+  // Epilogue in two passes: the flags and coefficients position-interleaved
+  // over the threads (coalesced), the listed bits into LDS; then thread t
+  // compacts word t (positions 64t..64t+63, n <= 64 * THREADS) in order.
+  for (int w = t; w < (n + 63) / 64; w += THREADS) listed_w[w] = 0;
+  __syncthreads();
+  for (int pos = t; pos < n; pos += THREADS) {
+    const bool was_touched =
+        __hip_atomic_load(a.touch + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+    const double v = was_touched ? medium_load(a.acc + pos) : 0.0;
+    const bool is_rel = (rel[pos >> 6] >> (pos & 63)) & 1ull;
+    bool listed;
+    if (a.algorithm == 0) {
+      listed = was_touched && is_rel && fabs(v) > a.drop_tolerance;
+      if (listed) a.coefficient[pos] = v;
+    } else if (a.algorithm == 1) {
+      listed = was_touched && is_rel && fabs(v) > a.drop_tolerance;
+      if (was_touched) a.coefficient[pos] = v;
+    } else {
+      listed = is_rel && fabs(v) > a.drop_tolerance;
+      a.coefficient[pos] = was_touched ? v : 0.0;
+    }
+    a.flags[pos] = listed ? 1 : 0;
+    if (listed) atomicOr(&listed_w[pos >> 6], 1ull << (pos & 63));
+  }
+  __syncthreads();
+  const uint64_t mine = t < (n + 63) / 64 ? listed_w[t] : 0ull;
+  const int c = __popcll(mine);
+  sums[t] = c;
+  __syncthreads();
+  for (int off = 1; off < THREADS; off <<= 1) {
+    const int v = t >= off ? sums[t - off] : 0;
+    __syncthreads();
+    sums[t] += v;
+    __syncthreads();
+  }
+  int out_pos = sums[t] - c;
+  for (uint64_t bits = mine; bits != 0; bits &= bits - 1) {
+    const int pos = t * 64 + __builtin_ctzll(bits);
+    const double v = medium_load(a.acc + pos);  // a listed position was touched
+    a.list[out_pos] = pos;
+    a.vals[out_pos] = v;
+    a.host_list[out_pos] = pos;
+    a.host_vals[out_pos] = v;
+    ++out_pos;
+  }
+  if (t == THREADS - 1) {
+    *a.count = sums[t];
+    *a.host_count = sums[t];
+  }
+}
+
+static_assert(kMediumCols == 64 * kCompactThreads, "one listed word per thread");
+
+__global__ __launch_bounds__(kCompactThreads) void row_wise_medium_kernel(RowWiseSmallArgs a) {
+  row_wise_medium_body(a);
+}
+
 // Small LPs: the column-wise update row (with the primal edge-norm dots when
 // w is given) and its compaction in one launch (ColWiseSmallArgs). Per column
 // the arithmetic and the write rule are column_dot_kernel's: kept columns
@@ -986,6 +1119,9 @@ __global__ __launch_bounds__(kCompactThreads) void small_batch_kernel(SmallBatch
   } else if constexpr (KIND == kSmallColWise) {
     const ColWiseSmallArgs a = s_slot.cw;
     column_wise_small_body(a);
+  } else if constexpr (KIND == kMediumRowWise) {
+    const RowWiseSmallArgs a = s_slot.rw;
+    row_wise_medium_body(a);
   } else if constexpr (KIND == kSmallListDots) {
     const ListDotsSmallArgs a = s_slot.ld;
     list_dots_small_body(a);
@@ -1526,9 +1662,21 @@ hipError_t small_batch(int kind, const SmallBatchArgs& args, hipStream_t s) {
     case kSmallRowWiseByColumn:
       small_batch_kernel<kSmallRowWiseByColumn><<<args.count, kCompactThreads, 0, s>>>(args);
       break;
+    case kMediumRowWise:
+      small_batch_kernel<kMediumRowWise><<<args.count, kCompactThreads, 0, s>>>(args);
+      break;
     default:
       return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t row_wise_update_medium(const RowWiseSmallArgs& args, hipStream_t s) {
+  if (args.num_cols > kMediumCols || args.num_filtered > kSmallRowsMax ||
+      args.num_filtered < 0 || args.acc == nullptr || args.touch == nullptr) {
+    return hipErrorInvalidValue;
+  }
+  row_wise_medium_kernel<<<1, kCompactThreads, 0, s>>>(args);
   return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ def main():
     lbs, ubs = jobshop.child_bounds(lp, ycols, a.lps, a.seed + 1000)
     p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
     out = {"m": lp.m, "n": lp.n, "lps": a.lps}
+    gpu_res = {}
     for w in a.workers:
         hs = [engine.LpHandle(p) for _ in range(w)]
         for h in hs:
@@ -45,6 +46,7 @@ def main():
         t = time.perf_counter()
         res = engine.batch_solve_bounds(hs, lbs, ubs, state)
         dt = time.perf_counter() - t
+        gpu_res[w] = res
         its = sum(r.iterations for r in res)
         agg = {}
         for h in hs:
@@ -65,6 +67,9 @@ def main():
             t = time.perf_counter()
             res = oracle_lib.batch_solve_bounds(ows, lbs, ubs, state)
             dt = time.perf_counter() - t
+            same = all(g.problem_status == c.problem_status and g.iterations == c.iterations
+                       and g.objective == c.objective for g, c in zip(gpu_res[w], res))
+            out[f"parity_w{w}"] = bool(same)
             out[f"cpu_w{w}"] = {"lps_per_s": a.lps / dt,
                                 "us_per_iteration_per_worker":
                                     1e6 * dt * w / max(1, sum(r.iterations for r in res))}
