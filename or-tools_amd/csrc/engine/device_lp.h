@@ -410,8 +410,8 @@ class DeviceLp : public DeviceSolver {
   // Workgroup size of row_wise_small_kernel (MILP_SMALL_THREADS: 1024 or 256;
   // 256 measured 4-5 % slower on the config-4 probe).
   int small_threads_ = 1024;
-  // Medium LPs (kSmallLdsCols < N <= kMediumCols, MILP_MEDIUM=off disables):
-  // the serial row-wise update row takes the small path's single launch with
+  // Medium LPs (kSmallLdsCols < N <= kMediumCols, MILP_MEDIUM=off disables)
+  // solved in a batch: the serial row-wise update row takes one batched launch with
   // its accumulators in device memory (d_medium_acc_, valid where
   // d_medium_touch_ holds the launch's epoch); everything else is generic.
   bool medium_enabled_ = true;
@@ -492,7 +492,9 @@ class DeviceLp : public DeviceSolver {
   bool tri_syncfree_ = true;  // MILP_TRI_SYNCFREE: readiness-driven single launch
   int tri_syncfree_min_levels_ = 0;  // MILP_TRI_SYNCFREE_MIN_LEVELS: shallower -> level plan
   bool tri_fuse0_ = true;     // MILP_TRI_FUSE0: level 0 inside the gather kernel
-  bool stream_priority_ = true;   // MILP_STREAM_PRIORITY=0: default priorities (+3-4 % on C5 with)
+  bool stream_priority_ = false;  // MILP_STREAM_PRIORITY=1: solver stream high, tau stream low
+  bool stream_prioritized_ = false;  // stream_ was created at the highest priority
+  void SetStreamPriority(bool high);
   bool tri_lower_ = true;     // MILP_TRI_LOWER: the L solves too
   int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
   uint64_t* d_tri_clock_ = nullptr;

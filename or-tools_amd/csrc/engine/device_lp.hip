@@ -104,19 +104,13 @@ void DeviceLp::Init(int device) {
   if (device < 0 || device >= count) throw DeviceError("bad device ordinal");
   device_ = device;
   Check(hipSetDevice(device), "hipSetDevice");
-  hipStream_t s;
-  // By default (MILP_STREAM_PRIORITY=0 turns it off) this handle's stream (the solver thread's
-  // kernels and triangular solves) at the highest priority, the tau
-  // worker's solve stream (device_solve.hip) at the lowest.
+  // The stream starts at the default priority; UploadMatrix sets it
+  // (SetStreamPriority).
   if (const char* v = std::getenv("MILP_STREAM_PRIORITY")) stream_priority_ = std::atoi(v) != 0;
-  if (stream_priority_) {
-    int least = 0, greatest = 0;
-    Check(hipDeviceGetStreamPriorityRange(&least, &greatest), "priority range");
-    Check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest), "hipStreamCreate");
-  } else {
-    Check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
-  }
+  hipStream_t s;
+  Check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
   stream_ = s;
+  stream_prioritized_ = false;
   hipEvent_t a, b;
   Check(hipEventCreate(&a), "hipEventCreate");
   Check(hipEventCreate(&b), "hipEventCreate");
@@ -544,8 +538,31 @@ void DeviceLp::EndKernel(int id, double bytes, bool count_launch) {
   }
 }
 
+// MILP_STREAM_PRIORITY=1: the solver thread's stream at the highest priority
+// and the tau worker's solve stream at the lowest. Off by default: an A/B on
+// C5 alone read +3-4 %, but the full bench with priorities came out lower on
+// every section (C5 575-600 vs 657 it/s, C3 45-61 vs 64, C4 1 740-1 860 vs
+// 2 800 LPs/s) and config-4 probes lost 5-35 % (scripts/gpu_c4_ab.sh).
+void DeviceLp::SetStreamPriority(bool high) {
+  if (high == stream_prioritized_) return;
+  Check(hipStreamSynchronize(S(stream_)), "sync");
+  FreeTriBuffers();  // its contexts hold the old stream (rebuilt on demand)
+  Check(hipStreamDestroy(S(stream_)), "hipStreamDestroy");
+  hipStream_t s;
+  if (high) {
+    int least = 0, greatest = 0;
+    Check(hipDeviceGetStreamPriorityRange(&least, &greatest), "priority range");
+    Check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest), "hipStreamCreate");
+  } else {
+    Check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  }
+  stream_ = s;
+  stream_prioritized_ = high;
+}
+
 void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseMatrix& csr) {
   Check(hipSetDevice(device_), "hipSetDevice");
+  SetStreamPriority(stream_priority_);
   for (void* p : allocations_) (void)hipFree(p);
   allocations_.clear();
   m_ = csc.num_rows();
@@ -819,7 +836,8 @@ void DeviceLp::SetMask(Mask which, const uint64_t* words, int num_words) {
   if (mask_on_device_[which] && std::memcmp(h.data(), words, num_words * sizeof(uint64_t)) == 0) {
     return;
   }
-  if (which == kRelevant && small_fused_enabled_ && h_small_in_ != nullptr) {
+  if (which == kRelevant && small_fused_enabled_ && h_small_in_ != nullptr &&
+      (!medium_ || small_batch_)) {
     // Small LPs: the relevant set changes every pivot and the small update
     // row reads it from mapped host memory; other kernels flush it first.
     std::memcpy(h.data(), words, num_words * sizeof(uint64_t));
@@ -1002,7 +1020,7 @@ void DeviceLp::UpdateRowRowWise(const std::vector<int>& filtered_rows,
     // Few short rows: applied row by row; otherwise column by column.
     const bool serial = k <= small_serial_rows_ && k <= milp_kernels::kSmallRowsMax &&
                         entries <= milp_kernels::kSmallEntries;
-    if (!medium_ || serial) {
+    if (!medium_ || (serial && small_batch_)) {
       UpdateRowRowWiseSmall(filtered_rows, rho, algorithm, drop, entries, serial);
       return;
     }

@@ -309,7 +309,7 @@ void DeviceLp::PrepareTriContext(int slot, int rows, int pos) {
       c.stream = stream_;
     } else {
       hipStream_t st;
-      if (stream_priority_) {
+      if (stream_prioritized_) {
         int least = 0, greatest = 0;
         Check(hipDeviceGetStreamPriorityRange(&least, &greatest), "priority range");
         Check(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least), "hipStreamCreate");
@@ -449,6 +449,11 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
   if (tri_mode_ == 2) return false;
   const int nc = t.num_cols();
   if (tri_mode_ == 0 && nc < tri_min_rows_) return false;
+  // Medium LPs solved in a batch keep the host triangles: many LPs' level
+  // chains contend for the device queues, each hop pays the contended launch
+  // latency (ta041-shaped batch of 64, 16 in flight: 15.7 LPs/s with the
+  // device solves, 37.7 with the host's).
+  if (tri_mode_ == 0 && small_batch_ && medium_) return false;
   if (static_cast<int>(x->size()) < nc) return false;
   // The solver's thread (slot 0) or the factorization's tau worker (slot 1).
   const int slot = g_lu_slot == 0 ? 0 : 1;
