@@ -260,14 +260,18 @@ def test_small_lp_one_launch_update_row_parity(case, dual, fused, monkeypatch):
     assert st["update_row"]["launches"] + st["single_row"]["launches"] > 0
 
 
-@pytest.mark.parametrize("shape", [(6, 6), (10, 10)])
+@pytest.mark.parametrize("shape", [(6, 6), (10, 10), (25, 10)])
 def test_batched_children_parity(shape):
     """Config-4 batch: children of one search node (bounds of two order
     variables fixed), warm-started from the root basis, solved by 4 GPU
-    workers; each child must match the oracle solving it alone."""
+    workers; each child must match the oracle solving it alone. 25x10 has
+    N > 8192: the mid-size batched update row (kMediumRowWise) and the host
+    triangular solves of a batch."""
     import jobshop
     jobs = jobshop.FT06 if shape == (6, 6) else jobshop.random_instance(*shape, 3)
     lp, ycols = jobshop.relaxation(jobs)
+    if shape == (25, 10):
+        assert 8192 < lp.m + lp.n <= 65536
     root = engine.LpHandle(abi.default_params(use_dual_simplex=1))
     root.load(lp)
     assert root.solve().problem_status == abi.OPTIMAL
