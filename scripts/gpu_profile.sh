@@ -3,6 +3,7 @@
 # that per-kernel-id byte counts are not mixed:
 #   C2: scripts/probe.py --config c2        -> gpurun_out/prof_c2/{trace,fetch,write}
 #   C5: scripts/probe.py --config c5        -> gpurun_out/prof_c5/{trace,fetch,write}
+#   C4M: ta041-shaped mid-size batch (50x10, 16 children, 1 worker)
 #   C4: scripts/probe_batch.py (256 children, 1 worker: rocprofv3 crashed
 #       under 8 concurrent worker threads) -> gpurun_out/prof_c4/...
 # Kernel trace + stats in one run; FETCH_SIZE and WRITE_SIZE in runs of their
@@ -15,9 +16,10 @@ OUT=$R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 C2="python3 $R/scripts/probe.py --config c2 --warmup 3 --steps 64"
 C4="python3 $R/scripts/probe_batch.py --lps 256 --workers 1"
+C4M="python3 $R/scripts/probe_batch.py --jobs 50 --machines 10 --lps 16 --workers 1"
 C5="python3 $R/scripts/probe.py --config c5 --m 100000 --n 1000000 --warmup ${C5_WARMUP:-20000} --steps ${C5_STEPS:-1000}"
 for W in ${WORKLOADS:-c2 c5}; do
-  if [ "$W" = c2 ]; then CMD=$C2; elif [ "$W" = c4 ]; then CMD=$C4; else CMD=$C5; fi
+  if [ "$W" = c2 ]; then CMD=$C2; elif [ "$W" = c4 ]; then CMD=$C4; elif [ "$W" = c4m ]; then CMD=$C4M; else CMD=$C5; fi
   P=$OUT/prof_$W
   mkdir -p $P
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $P/trace -o run -- $CMD > $P/trace.log 2>&1 || { echo "$W trace failed"; tail -20 $P/trace.log; rm -rf $P; exit 1; }
