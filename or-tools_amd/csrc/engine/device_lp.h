@@ -411,14 +411,10 @@ class DeviceLp : public DeviceSolver {
   // 256 measured 4-5 % slower on the config-4 probe).
   int small_threads_ = 1024;
   // Medium LPs (kSmallLdsCols < N <= kMediumCols, MILP_MEDIUM=off disables)
-  // solved in a batch: the serial row-wise update row takes one batched launch with
-  // its accumulators in device memory (d_medium_acc_, valid where
-  // d_medium_touch_ holds the launch's epoch); everything else is generic.
+  // solved in a batch: the serial row-wise update row takes one batched launch
+  // (accumulators in an LDS hash table); everything else is generic.
   bool medium_enabled_ = true;
   bool medium_ = false;
-  double* d_medium_acc_ = nullptr;
-  uint32_t* d_medium_touch_ = nullptr;
-  uint32_t medium_epoch_ = 0;
   void* h_small_in_ = nullptr;
   int32_t* h_small_rows_ = nullptr;
   double* h_small_rho_ = nullptr;

@@ -691,13 +691,6 @@ void DeviceLp::UploadMatrix(const CompactSparseMatrix& csc, const CompactSparseM
   mask_dirty_ = false;
   medium_ = small_fused_enabled_ && medium_enabled_ && n_total_ > milp_kernels::kSmallLdsCols &&
             n_total_ <= milp_kernels::kMediumCols;
-  if (medium_) {
-    d_medium_acc_ = Alloc<double>(n_total_);
-    d_medium_touch_ = Alloc<uint32_t>(n_total_);
-    Check(hipMemsetAsync(d_medium_touch_, 0, size_t(n_total_) * sizeof(uint32_t), S(stream_)),
-          "touch init");
-    medium_epoch_ = 0;
-  }
   if (n_total_ <= milp_kernels::kSmallLdsCols || medium_) {
     const int cap = std::max(1, m_);  // filtered rows
     const size_t rho_off = (size_t(cap) * sizeof(int32_t) + 63) / 64 * 64;
@@ -1183,16 +1176,6 @@ void DeviceLp::UpdateRowRowWiseSmall(const std::vector<int>& filtered_rows,
   a.host_list = d_map_list_;
   a.host_vals = d_map_vals_;
   a.host_count = d_map_count_;
-  if (medium_) {
-    if (++medium_epoch_ == 0) {  // wrapped: stale tags could match again
-      Check(hipMemsetAsync(d_medium_touch_, 0, size_t(n_total_) * sizeof(uint32_t), S(stream_)),
-            "touch reset");
-      medium_epoch_ = 1;
-    }
-    a.acc = d_medium_acc_;
-    a.touch = d_medium_touch_;
-    a.epoch = medium_epoch_;
-  }
   BeginKernel(id);
   LaunchSmall(medium_ ? milp_kernels::kMediumRowWise : milp_kernels::kSmallRowWise, a);
   // Rows and multipliers, the CSR entries, N-sized flags/coefficients, the list.

@@ -161,11 +161,6 @@ struct RowWiseSmallArgs {
   int32_t* host_list;  // mapped host memory
   double* host_vals;
   int* host_count;
-  // Medium LPs (kSmallLdsCols < N <= kMediumCols): accumulators in global
-  // memory, a position's accumulator valid when touch[pos] == epoch.
-  double* acc;
-  uint32_t* touch;
-  uint32_t epoch;
 };
 constexpr int kMediumCols = 65536;
 

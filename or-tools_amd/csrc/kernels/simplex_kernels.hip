@@ -703,19 +703,42 @@ __global__ __launch_bounds__(THREADS) void row_wise_small_kernel(RowWiseSmallArg
 }
 
 // Medium LPs (N <= kMediumCols): row_wise_small_body's algorithm with the
-// accumulators in global memory (a.acc, valid where a.touch == a.epoch: no
-// clearing pass), read at agent scope after each row's barrier so a value
-// another wave stored is seen from L2. Same arithmetic, same order, same
-// write rules and the same list (increasing positions).
-__device__ __forceinline__ double medium_load(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// accumulators in an LDS hash table instead of an N-sized LDS array. A request
+// has at most kSmallEntries entries, so at most that many positions are
+// touched; kMediumSlots > kSmallEntries slots with linear probing always find
+// a free slot or the key. The slots are assigned before the row loop, so the
+// rows are applied in turn out of LDS with a barrier between rows, exactly as
+// the small kernel does (same arithmetic, order and first-write rule). The
+// epilogue looks positions up in the table: flags and coefficients
+// position-interleaved (coalesced), the listed bits into LDS, then thread t
+// compacts word t, so the list is in increasing position order.
+constexpr int kMediumSlots = 5120;
+static_assert(kMediumSlots > kSmallEntries, "the table must never fill");
+
+__device__ __forceinline__ int medium_hash(int pos) {
+  return static_cast<int>((static_cast<uint32_t>(pos) * 2654435761u) % kMediumSlots);
+}
+
+// Slot holding `pos`, or -1. Probes end at an empty slot or after every slot.
+__device__ __forceinline__ int medium_find(const int32_t* keys, int pos) {
+  int sl = medium_hash(pos);
+  for (int i = 0; i < kMediumSlots; ++i) {
+    const int k = keys[sl];
+    if (k == pos) return sl;
+    if (k < 0) return -1;
+    sl = sl + 1 == kMediumSlots ? 0 : sl + 1;
+  }
+  return -1;
 }
 
 __device__ __forceinline__ void row_wise_medium_body(const RowWiseSmallArgs& a) {
   constexpr int THREADS = kCompactThreads;
+  __shared__ int32_t keys[kMediumSlots];
+  __shared__ double acc[kMediumSlots];
+  __shared__ uint8_t written[kMediumSlots];
   __shared__ uint64_t rel[kMediumCols / 64];
   __shared__ unsigned long long listed_w[kMediumCols / 64];
-  __shared__ int32_t ent_pos[kSmallEntries];
+  __shared__ int16_t ent_slot[kSmallEntries];
   __shared__ double ent_val[kSmallEntries];
   __shared__ double s_rho[kSmallRowsMax];
   __shared__ int64_t s_off[kSmallRowsMax];
@@ -724,8 +747,14 @@ __device__ __forceinline__ void row_wise_medium_body(const RowWiseSmallArgs& a) 
   const int t = threadIdx.x;
   const int n = a.num_cols;
   const int k_rows = a.num_filtered;
-  const uint32_t epoch = a.epoch;
-  for (int w = t; w < (n + 63) / 64; w += THREADS) rel[w] = a.relevant[w];
+  for (int i = t; i < kMediumSlots; i += THREADS) {
+    keys[i] = -1;
+    written[i] = 0;
+  }
+  for (int w = t; w < (n + 63) / 64; w += THREADS) {
+    rel[w] = a.relevant[w];
+    listed_w[w] = 0;
+  }
   int len = 0;
   if (t < k_rows) {
     const int r = a.filtered_rows[t];
@@ -754,39 +783,38 @@ __device__ __forceinline__ void row_wise_medium_body(const RowWiseSmallArgs& a) 
       if (s_beg[mid] <= e) lo = mid; else hi = mid - 1;
     }
     const int64_t i = s_off[lo] + (e - s_beg[lo]);
-    ent_pos[e] = a.t_cols[i];
+    const int pos = a.t_cols[i];
     ent_val[e] = s_rho[lo] * a.t_vals[i];
+    int sl = medium_hash(pos);
+    for (int probe = 0; probe < kMediumSlots; ++probe) {
+      const int old = atomicCAS(&keys[sl], -1, pos);
+      if (old == -1 || old == pos) break;
+      sl = sl + 1 == kMediumSlots ? 0 : sl + 1;
+    }
+    ent_slot[e] = static_cast<int16_t>(sl);
   }
   __syncthreads();
   for (int k = 0; k < k_rows; ++k) {
     for (int e = s_beg[k] + t; e < s_beg[k + 1]; e += THREADS) {
-      const int pos = ent_pos[e];
+      const int sl = ent_slot[e];
       const double v = ent_val[e];
-      const bool first =
-          __hip_atomic_load(a.touch + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch;
       double out;
       if (a.algorithm == 0) {
         out = v;
-      } else if (first) {
+      } else if (!written[sl]) {
         out = a.algorithm == 2 ? 0.0 + v : v;
       } else {
-        out = medium_load(a.acc + pos) + v;
+        out = acc[sl] + v;
       }
-      a.acc[pos] = out;
-      a.touch[pos] = epoch;
+      acc[sl] = out;
+      written[sl] = 1;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // rows are applied in order
   }
-  // Epilogue in two passes: the flags and coefficients position-interleaved
-  // over the threads (coalesced), the listed bits into LDS; then thread t
-  // compacts word t (positions 64t..64t+63, n <= 64 * THREADS) in order.
-  for (int w = t; w < (n + 63) / 64; w += THREADS) listed_w[w] = 0;
-  __syncthreads();
   for (int pos = t; pos < n; pos += THREADS) {
-    const bool was_touched =
-        __hip_atomic_load(a.touch + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-    const double v = was_touched ? medium_load(a.acc + pos) : 0.0;
+    const int sl = medium_find(keys, pos);
+    const bool was_touched = sl >= 0 && written[sl] != 0;
+    const double v = was_touched ? acc[sl] : 0.0;
     const bool is_rel = (rel[pos >> 6] >> (pos & 63)) & 1ull;
     bool listed;
     if (a.algorithm == 0) {
@@ -816,7 +844,7 @@ __device__ __forceinline__ void row_wise_medium_body(const RowWiseSmallArgs& a) 
   int out_pos = sums[t] - c;
   for (uint64_t bits = mine; bits != 0; bits &= bits - 1) {
     const int pos = t * 64 + __builtin_ctzll(bits);
-    const double v = medium_load(a.acc + pos);  // a listed position was touched
+    const double v = acc[medium_find(keys, pos)];  // a listed position was touched
     a.list[out_pos] = pos;
     a.vals[out_pos] = v;
     a.host_list[out_pos] = pos;
@@ -1673,7 +1701,7 @@ hipError_t small_batch(int kind, const SmallBatchArgs& args, hipStream_t s) {
 
 hipError_t row_wise_update_medium(const RowWiseSmallArgs& args, hipStream_t s) {
   if (args.num_cols > kMediumCols || args.num_filtered > kSmallRowsMax ||
-      args.num_filtered < 0 || args.acc == nullptr || args.touch == nullptr) {
+      args.num_filtered < 0) {
     return hipErrorInvalidValue;
   }
   row_wise_medium_kernel<<<1, kCompactThreads, 0, s>>>(args);
