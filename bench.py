@@ -92,6 +92,22 @@ def kernel_roofline(stats, traffic_json=None):
             "ms_per_launch": ms_per_launch, "launches": ds["launches"]}
 
 
+def window_stats(ts, start, done, before, after):
+    """Per-iteration statistics of a timed window [start, start + done):
+    p50/p90/max of the iteration times (from the engine's per-iteration
+    timestamps) and the LU refactorizations that fell inside it, so that a
+    short window is interpretable (a refactorization costs many iterations)."""
+    out = {"refactorizations_in_window": after["factorizations"] - before["factorizations"],
+           "refactorization_ms_in_window": round(
+               1000.0 * (after["factorization_seconds"] - before["factorization_seconds"]), 3)}
+    if done > 0 and len(ts) >= start + done and start > 0:
+        per = np.diff(np.asarray(ts[start - 1:start + done])) * 1000.0
+        out.update(iteration_ms_p50=round(float(np.percentile(per, 50)), 4),
+                   iteration_ms_p90=round(float(np.percentile(per, 90)), 4),
+                   iteration_ms_max=round(float(per.max()), 4))
+    return out
+
+
 def kernel_table(stats):
     return {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
                 "call_ms": round(v["call_ms"], 3), "GB": round(v["bytes"] / 1e9, 4)}
@@ -108,6 +124,7 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     p = abi.default_params(use_dual_simplex=1)
     h = engine.LpHandle(p, device=local_rank)
     h.load(lp)
+    h.record_iteration_times(True)  # per-iteration timestamps (window statistics)
     t = time.perf_counter()
     start = args.c5_window + args.warmup
     h.begin(start)
@@ -115,6 +132,7 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     log(f"c5: solve ran to iteration {start} in {setup:.1f}s (untimed)")
     h.reset_kernel_stats()
     h.set_kernel_timing(True)
+    before = h.run_counters()
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -123,7 +141,9 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     barrier()
     elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
     stats = h.kernel_stats()
+    after = h.run_counters()
     done = it - start
+    window = window_stats(h.iteration_times(), start, done, before, after)
     total_done = distributed.sum_over_ranks(done, dist, "cuda")
     h.stop()
     h.finish()
@@ -141,6 +161,7 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
                                   / max(1, done), 3),
         "device_call_ms_per_step": round(sum(v["call_ms"] for v in stats.values())
                                          / max(1, done), 3),
+        "window": window,
     }
     if rank == 0 and world == 1 and not args.no_cpu and args.c5_cpu_steps > 0:
         import oracle_lib
@@ -175,12 +196,14 @@ def run_c2(args, rank, world, local_rank, dist, barrier, sync):
     params = abi.default_params()  # Glop defaults: primal simplex, steepest edge
     h = engine.LpHandle(params, device=local_rank)
     h.load(lp)
+    h.record_iteration_times(True)
     t_setup = time.perf_counter()
     h.begin(args.c2_warmup)  # load to HBM, factorize, first norms, warm-up iterations
     t_setup = time.perf_counter() - t_setup
     log(f"c2: warm-up done in {t_setup:.1f}s; timing {args.c2_steps} iterations")
     h.reset_kernel_stats()
     h.set_kernel_timing(True)
+    before = h.run_counters()
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -190,6 +213,7 @@ def run_c2(args, rank, world, local_rank, dist, barrier, sync):
     elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
     stats = h.kernel_stats()
     done = it - args.c2_warmup
+    window = window_stats(h.iteration_times(), args.c2_warmup, done, before, h.run_counters())
     total_done = distributed.sum_over_ranks(done, dist, "cuda")
     # A late window of the same length: the host LU solves grow as dense
     # columns enter the basis, so the early rate overstates the solve.
@@ -200,6 +224,7 @@ def run_c2(args, rank, world, local_rank, dist, barrier, sync):
         reach_s = time.perf_counter() - t
         if not fin_l:
             sync()
+            before_l = h.run_counters()
             t0l = time.perf_counter()
             fin_l, it_l2 = h.run_until(it_l + args.c2_steps)
             sync()
@@ -207,7 +232,9 @@ def run_c2(args, rank, world, local_rank, dist, barrier, sync):
             late = {"timed_iterations": [it_l, it_l2], "reached_in_s": round(reach_s, 2),
                     "value": distributed.sum_over_ranks(it_l2 - it_l, dist, "cuda") / el
                     if el > 0 else 0.0,
-                    "ms_per_step": 1000.0 * el / max(1, it_l2 - it_l)}
+                    "ms_per_step": 1000.0 * el / max(1, it_l2 - it_l),
+                    "window": window_stats(h.iteration_times(), it_l, it_l2 - it_l, before_l,
+                                           h.run_counters())}
             log(f"c2: late window {it_l}..{it_l2}: {late['value']:.1f} it/s")
     h.stop()
     h.finish()
@@ -225,6 +252,7 @@ def run_c2(args, rank, world, local_rank, dist, barrier, sync):
         "kernels": kernel_table(stats),
         "host_ms_per_step": round((1000.0 * elapsed - sum(v["call_ms"] for v in stats.values()))
                                   / max(1, done), 3),
+        "window": window,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         log("c2: cpu baseline (oracle)")
@@ -474,6 +502,7 @@ def main():
         "kernels": c5["kernels"],
         "host_ms_per_step": c5["host_ms_per_step"],
         "device_call_ms_per_step": c5["device_call_ms_per_step"],
+        "window": c5["window"],
         "cpu_baseline": c5.get("cpu_baseline"),
         "c2": c2,
         "c3": c3,

@@ -231,6 +231,9 @@ int mi_lp_notify_matrix_unchanged(mi_lp* h);
 int mi_lp_notify_matrix_changed(mi_lp* h);
 int mi_lp_set_starting_variable_values(mi_lp* h, const double* values, int32_t len);
 int mi_lp_set_integrality_scale(mi_lp* h, int32_t col, double scale);
+/* RevisedSimplex::ClearIntegralityScales (revised_simplex.h:236), called by
+ * sat/linear_programming_constraint.cc:424 before it sets the scales again. */
+int mi_lp_clear_integrality_scales(mi_lp* h);
 int mi_lp_objective_limit_reached(const mi_lp* h, int32_t* reached);
 int mi_lp_get_unit_row_left_inverse(mi_lp* h, int32_t row, double* values, int32_t* non_zeros,
                                     int32_t* num_non_zeros);
@@ -268,8 +271,26 @@ int mi_lp_stop(mi_lp* h);
 
 int mi_lp_get_kernel_stats(const mi_lp* h, mi_lp_kernel_stats* s);
 int mi_lp_reset_kernel_stats(mi_lp* h);
-/* enable != 0: bracket every hot kernel with HIP events (adds a sync). */
+/* enable != 0: bracket every hot kernel with HIP events. The events are
+ * read back when the stats are collected (or every 512 launches): timing adds
+ * no synchronization to the iteration it measures. */
 int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable);
+
+/* Window statistics for the benchmark harness (the reference keeps the same
+ * numbers in RevisedSimplex's stats, revised_simplex.h:717-760, and
+ * BasisFactorization's, basis_representation.h:359-373).
+ * mi_lp_record_iteration_times: enable a timestamp (seconds since Solve()
+ * started) per completed iteration; call before mi_lp_begin or while paused.
+ * mi_lp_get_iteration_times copies min(cap, count) of them and returns count
+ * (a negative error code when the solve is running). */
+typedef struct mi_lp_run_counters {
+  int64_t factorizations;       /* LU factorizations computed so far */
+  double factorization_seconds; /* host wall time spent in them */
+  int64_t iterations;           /* RevisedSimplex::GetNumberOfIterations */
+} mi_lp_run_counters;
+int mi_lp_record_iteration_times(mi_lp* h, int32_t enable);
+int64_t mi_lp_get_iteration_times(const mi_lp* h, double* out, int64_t cap);
+int mi_lp_get_run_counters(const mi_lp* h, mi_lp_run_counters* c);
 
 /* Batch API: solves count independent LPs already loaded in handles (all on
  * the same device) on num_threads host threads; each thread drives several

@@ -201,6 +201,7 @@ class DeviceLp : public DeviceSolver {
   template <typename Args>
   void LaunchSmall(int kind, const Args& args);
   void WaitSmallBatch();
+  void RestoreDevice();  // after a fiber yield
   bool small_batch_ = false;
   int batch_slot_ = -1;
   unsigned long long batch_seq_ = 0;

@@ -54,11 +54,15 @@ void ReleaseSmallBatchSlot(int device, int slot);  // below, with SmallBatcher
 
 DeviceLp::~DeviceLp() {
   if (device_ >= 0) (void)hipSetDevice(device_);
+  bool slot_idle = true;
   try {
     WaitSmallBatch();  // a batched request may still write this handle's buffers
   } catch (const std::exception&) {
+    // The request never completed: its slot is not returned to the pool (a
+    // later owner would take the stale sequence number for its own).
+    slot_idle = false;
   }
-  if (batch_slot_ >= 0) ReleaseSmallBatchSlot(device_, batch_slot_);
+  if (batch_slot_ >= 0 && slot_idle) ReleaseSmallBatchSlot(device_, batch_slot_);
   if (stream_ != nullptr) (void)hipStreamSynchronize(S(stream_));
   FreeTriBuffers();
   for (void* p : allocations_) (void)hipFree(p);
@@ -433,6 +437,7 @@ void DeviceLp::WaitSmallBatch() {
   while (b.done(batch_slot_) != batch_seq_) {
     if (InFiber()) {
       FiberYield();
+      RestoreDevice();
     } else {
       __builtin_ia32_pause();
     }
@@ -446,13 +451,25 @@ void DeviceLp::WaitSmallBatch() {
   batch_pending_ = false;
 }
 
+// Fibers of one host thread may belong to handles on different GPUs: the
+// thread's current device is whatever the last fiber set, so a fiber that
+// resumes makes its own handle's device current again before any HIP call
+// (allocations and launches use the current device).
+void DeviceLp::RestoreDevice() {
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != device_) Check(hipSetDevice(device_), "hipSetDevice");
+}
+
 // The stream wait of this handle. On a fiber of a batched solve (fibers.h)
 // the fiber yields while the stream is busy, so the thread runs another LP's
 // host work instead of spinning.
 void DeviceLp::WaitStream() {
   WaitSmallBatch();
   if (InFiber()) {
-    while (hipStreamQuery(S(stream_)) == hipErrorNotReady) FiberYield();
+    while (hipStreamQuery(S(stream_)) == hipErrorNotReady) {
+      FiberYield();
+      RestoreDevice();
+    }
   }
   Check(hipStreamSynchronize(S(stream_)), "sync");
 }

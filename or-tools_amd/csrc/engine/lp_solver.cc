@@ -339,6 +339,22 @@ void mi_lp_solver_params_default(mi_lp_solver_params* p) {
   p->max_valid_magnitude = 1e30;            // max_valid_magnitude default
 }
 
+}  // extern "C"
+
+namespace {
+// mi_lp_load's argument rule: every array an LP of this shape reads is given.
+bool LpArraysPresent(int32_t m, int32_t n, const int64_t* cs, const int32_t* ri,
+                     const double* vals, const double* clb, const double* cub, const double* rlb,
+                     const double* rub, const double* obj) {
+  if (cs[n] > 0 && (ri == nullptr || vals == nullptr)) return false;
+  if (n > 0 && (clb == nullptr || cub == nullptr || obj == nullptr)) return false;
+  if (m > 0 && (rlb == nullptr || rub == nullptr)) return false;
+  return true;
+}
+}  // namespace
+
+extern "C" {
+
 int mi_lp_scale(const mi_lp_solver_params* sp, int32_t m, int32_t n, const int64_t* cs,
                 const int32_t* ri, double* vals, double* clb, double* cub, double* rlb,
                 double* rub, double* obj, double* obj_offset, double* obj_scale,
@@ -349,6 +365,7 @@ int mi_lp_scale(const mi_lp_solver_params* sp, int32_t m, int32_t n, const int64
     return MI_LP_ERROR_NULL;
   }
   if (m < 0 || n < 0 || cs[0] != 0 || cs[n] < 0) return MI_LP_ERROR_INVALID_PROBLEM;
+  if (!LpArraysPresent(m, n, cs, ri, vals, clb, cub, rlb, rub, obj)) return MI_LP_ERROR_NULL;
   try {
     milp::ScaledLp lp;
     lp.m = m;
@@ -401,6 +418,7 @@ int mi_lp_solver_solve(mi_lp* h, const mi_lp_solver_params* sp, int32_t m, int32
   using milp::ScaledLp;
   if (h == nullptr || sp == nullptr || out == nullptr || cs == nullptr) return MI_LP_ERROR_NULL;
   if (m < 0 || n < 0 || cs[0] != 0 || cs[n] < 0) return MI_LP_ERROR_INVALID_PROBLEM;
+  if (!LpArraysPresent(m, n, cs, ri, vals, clb, cub, rlb, rub, obj)) return MI_LP_ERROR_NULL;
   std::memset(out, 0, sizeof(*out));
   try {
     const ScaledLp orig = [&] {

@@ -1,6 +1,8 @@
 // Host basis factorization of the MI355X simplex engine (see lu.h).
 #include "lu.h"
 
+#include <chrono>
+
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
@@ -1051,7 +1053,11 @@ Status BasisFactorization::ForceRefactorization() {
 
 Status BasisFactorization::ComputeFactorization() {
   CompactSparseMatrixView basis_matrix{&compact_matrix_, &basis_};
+  const auto t0 = std::chrono::steady_clock::now();
   const Status status = lu_factorization_.ComputeFactorization(basis_matrix);
+  ++num_factorizations_;
+  factorization_seconds_ +=
+      std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   last_factorization_deterministic_time_ =
       lu_factorization_.DeterministicTimeOfLastFactorization();
   deterministic_time_ += last_factorization_deterministic_time_;

@@ -1095,6 +1095,10 @@ class BasisFactorization {
   Fractional ComputeInfinityNormConditionNumberUpperBound() const;
   double DeterministicTime() const { return deterministic_time_; }
   int NumUpdates() const { return num_updates_; }
+  // Run counters (bench.py window statistics): LU factorizations computed
+  // by this object and the host wall time spent in them.
+  int64_t NumFactorizations() const { return num_factorizations_; }
+  double FactorizationSeconds() const { return factorization_seconds_; }
   int GetNumberOfRows() const { return compact_matrix_.num_rows(); }
   const std::vector<int>& GetColumnPermutation() const {
     return lu_factorization_.GetColumnPermutation();
@@ -1141,6 +1145,8 @@ class BasisFactorization {
   int max_num_updates_ = 64;
   bool dynamic_period_ = true;
   int num_updates_ = 0;
+  int64_t num_factorizations_ = 0;
+  double factorization_seconds_ = 0.0;
   mutable std::vector<int> left_pool_mapping_;
   mutable std::vector<int> right_pool_mapping_;
   mutable CompactSparseMatrix storage_;

@@ -2871,6 +2871,9 @@ class RevisedSimplex {
     variable_starting_values_ = values;
   }
   void SetIntegralityScale(int col, Fractional scale);
+  // revised_simplex.h:236 (called by sat/linear_programming_constraint.cc:424
+  // before the scales are set again).
+  void ClearIntegralityScales() { integrality_scale_.clear(); }
   bool objective_limit_reached() const { return objective_limit_reached_; }
   // revised_simplex.h:209-211 (UpdateRow::ComputeAndGetUnitRowLeftInverse).
   const ScatteredVector& GetUnitRowLeftInverse(int row) {
@@ -2921,6 +2924,8 @@ class RevisedSimplex {
   // Called after every completed iteration (benchmark slicing, mi_lp_begin).
   std::function<void(int64_t)> iteration_hook;
   DeviceLp& device() { return device_; }
+  int64_t NumFactorizations() const { return basis_factorization_.NumFactorizations(); }
+  double FactorizationSeconds() const { return basis_factorization_.FactorizationSeconds(); }
 
  private:
   enum class Phase { FEASIBILITY, OPTIMIZATION, PUSH };
@@ -5274,26 +5279,44 @@ int LoadLp(mi_lp* h, int32_t m, int32_t n, const int64_t* cs, const int32_t* ri,
   h->solved = false;
   return MI_LP_OK;
 }
+// No begun solve, or one that is parked (paused or finished): its state may
+// be read.
+bool SolveIsParked(const mi_lp* h) {
+  mi_lp* m = const_cast<mi_lp*>(h);
+  std::lock_guard<std::mutex> l(m->mu);
+  return !m->running || m->paused || m->finished;
+}
 }  // namespace
 
 extern "C" {
 
 int mi_lp_load_basis_state(mi_lp* h, const int8_t* st, int32_t len) {
   if (h == nullptr || (st == nullptr && len > 0)) return MI_LP_ERROR_NULL;
-  std::vector<milp::VariableStatus> s(len);
-  for (int i = 0; i < len; ++i) {
-    if (st[i] < 0 || st[i] > 4) return MI_LP_ERROR_INVALID_PROBLEM;
-    s[i] = static_cast<milp::VariableStatus>(st[i]);
+  if (len < 0) return MI_LP_ERROR_INVALID_PROBLEM;
+  try {
+    std::vector<milp::VariableStatus> s(len);
+    for (int i = 0; i < len; ++i) {
+      if (st[i] < 0 || st[i] > 4) return MI_LP_ERROR_INVALID_PROBLEM;
+      s[i] = static_cast<milp::VariableStatus>(st[i]);
+    }
+    h->simplex.LoadStateForNextSolve(s);
+  } catch (const std::exception& e) {
+    h->error = std::string("mi_lp_load_basis_state: ") + e.what();
+    return MI_LP_ERROR_INTERNAL;
   }
-  h->simplex.LoadStateForNextSolve(s);
   return MI_LP_OK;
 }
 
 int mi_lp_set_variable_bounds(mi_lp* h, const double* col_lb, const double* col_ub) {
   if (h == nullptr || col_lb == nullptr || col_ub == nullptr) return MI_LP_ERROR_NULL;
   if (!h->loaded) return MI_LP_ERROR_STATE;
-  h->lp.col_lb.assign(col_lb, col_lb + h->lp.n);
-  h->lp.col_ub.assign(col_ub, col_ub + h->lp.n);
+  try {
+    h->lp.col_lb.assign(col_lb, col_lb + h->lp.n);
+    h->lp.col_ub.assign(col_ub, col_ub + h->lp.n);
+  } catch (const std::exception& e) {
+    h->error = std::string("mi_lp_set_variable_bounds: ") + e.what();
+    return MI_LP_ERROR_INTERNAL;
+  }
   return MI_LP_OK;
 }
 
@@ -5336,6 +5359,12 @@ int mi_lp_set_integrality_scale(mi_lp* h, int32_t col, double scale) {
     h->error = e.what();
     return MI_LP_ERROR_INTERNAL;
   }
+  return MI_LP_OK;
+}
+
+int mi_lp_clear_integrality_scales(mi_lp* h) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  h->simplex.ClearIntegralityScales();
   return MI_LP_OK;
 }
 
@@ -5570,9 +5599,36 @@ int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable) {
   return MI_LP_OK;
 }
 
+int mi_lp_record_iteration_times(mi_lp* h, int32_t enable) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  if (!SolveIsParked(h)) return MI_LP_ERROR_STATE;
+  h->simplex.record_iteration_times = enable != 0;
+  return MI_LP_OK;
+}
+
+int64_t mi_lp_get_iteration_times(const mi_lp* h, double* out, int64_t cap) {
+  if (h == nullptr) return -MI_LP_ERROR_NULL;
+  if (!SolveIsParked(h)) return -MI_LP_ERROR_STATE;
+  const std::vector<double>& t = h->simplex.iteration_times;
+  const int64_t n = std::min<int64_t>(cap, static_cast<int64_t>(t.size()));
+  for (int64_t i = 0; out != nullptr && i < n; ++i) out[i] = t[i];
+  return static_cast<int64_t>(t.size());
+}
+
+int mi_lp_get_run_counters(const mi_lp* h, mi_lp_run_counters* c) {
+  if (h == nullptr || c == nullptr) return MI_LP_ERROR_NULL;
+  if (!SolveIsParked(h)) return MI_LP_ERROR_STATE;
+  std::memset(c, 0, sizeof(*c));
+  c->factorizations = h->simplex.NumFactorizations();
+  c->factorization_seconds = h->simplex.FactorizationSeconds();
+  c->iterations = h->simplex.GetNumberOfIterations();
+  return MI_LP_OK;
+}
+
 }  // extern "C"
 
 namespace {
+
 // Back to single launches after a batch call (a device error there is the
 // handle's next call's to report).
 void SetSmallBatchSafe(mi_lp* h, bool on) {

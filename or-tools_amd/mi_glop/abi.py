@@ -137,6 +137,15 @@ INVALID_PROBLEM = 10
 IMPRECISE = 11
 
 # Kernel ids (include/mi_lp.h MI_K_*)
+class MiLpRunCounters(ctypes.Structure):
+    """mi_lp_run_counters (include/mi_lp.h): window statistics."""
+    _fields_ = [
+        ("factorizations", ctypes.c_int64),
+        ("factorization_seconds", ctypes.c_double),
+        ("iterations", ctypes.c_int64),
+    ]
+
+
 KERNEL_NAMES = ["pricing", "update_row", "primal_norms", "rc_update", "tri_solve",
                 "col_norms", "spmv_rows", "single_row", "dual_ratio", "readback",
                 "tri_solve_tau", "tri_solve_l"]
@@ -160,6 +169,8 @@ EXPORTED_SYMBOLS = [
     "mi_mps_read_file", "mi_mps_parse_string", "mi_mps_error", "mi_mps_dims", "mi_mps_get",
     "mi_mps_name", "mi_mps_col_name", "mi_mps_row_name", "mi_mps_free",
     "mi_lp_solver_params_default", "mi_lp_scale", "mi_lp_solver_solve",
+    "mi_lp_clear_integrality_scales", "mi_lp_record_iteration_times",
+    "mi_lp_get_iteration_times", "mi_lp_get_run_counters",
 ]
 
 

@@ -70,6 +70,11 @@ def lib():
     L.mi_lp_notify_matrix_changed.argtypes = [vp]
     L.mi_lp_set_starting_variable_values.argtypes = [vp, vp, ctypes.c_int32]
     L.mi_lp_set_integrality_scale.argtypes = [vp, ctypes.c_int32, ctypes.c_double]
+    L.mi_lp_clear_integrality_scales.argtypes = [vp]
+    L.mi_lp_record_iteration_times.argtypes = [vp, ctypes.c_int32]
+    L.mi_lp_get_iteration_times.argtypes = [vp, vp, ctypes.c_int64]
+    L.mi_lp_get_iteration_times.restype = ctypes.c_int64
+    L.mi_lp_get_run_counters.argtypes = [vp, ctypes.POINTER(abi.MiLpRunCounters)]
     L.mi_lp_objective_limit_reached.argtypes = [vp, vp]
     L.mi_lp_get_unit_row_left_inverse.argtypes = [vp, ctypes.c_int32, vp, vp, vp]
     L.mi_lp_compute_dictionary.argtypes = [vp, vp, ctypes.c_int32, vp]
@@ -221,6 +226,27 @@ class LpHandle:
                            device_ms=s.device_ms[i], call_ms=s.call_ms[i])
                 for i, name in enumerate(abi.KERNEL_NAMES)}
 
+    def record_iteration_times(self, on=True):
+        self._check(self._L.mi_lp_record_iteration_times(self.h, int(on)),
+                    "mi_lp_record_iteration_times")
+
+    def iteration_times(self):
+        """Seconds since Solve() started at the end of every iteration."""
+        n = self._L.mi_lp_get_iteration_times(self.h, None, 0)
+        if n < 0:
+            raise RuntimeError(f"mi_lp_get_iteration_times failed ({-n})")
+        out = np.zeros(n)
+        self._L.mi_lp_get_iteration_times(self.h, _p(out), n)
+        return out
+
+    def run_counters(self):
+        c = abi.MiLpRunCounters()
+        self._check(self._L.mi_lp_get_run_counters(self.h, ctypes.byref(c)),
+                    "mi_lp_get_run_counters")
+        return {"factorizations": int(c.factorizations),
+                "factorization_seconds": float(c.factorization_seconds),
+                "iterations": int(c.iterations)}
+
     def reset_kernel_stats(self):
         self._L.mi_lp_reset_kernel_stats(self.h)
 
@@ -277,6 +303,9 @@ class LpHandle:
 
     def set_integrality_scale(self, col, scale):
         self._call("set_integrality_scale", int(col), ctypes.c_double(scale))
+
+    def clear_integrality_scales(self):
+        self._call("clear_integrality_scales")
 
     def objective_limit_reached(self):
         r = ctypes.c_int32()

@@ -320,6 +320,9 @@ class Solver:
         model = self.to_linear_program()
         p = params if params is not None else self._params
         if self._time_limit_ms:
+            # A copy: the caller's params (and the solver's own) keep their
+            # time limit, as MPSolver's do.
+            p = type(p).from_buffer_copy(p)
             p.max_time_in_seconds = self._time_limit_ms / 1000.0
         if self._handle is None:
             self._handle = engine.LpHandle(p, device=self._device)

@@ -2002,6 +2002,7 @@ class RevisedSimplex {
     variable_starting_values_ = values;
   }
   void SetIntegralityScale(int col, Fractional scale);
+  void ClearIntegralityScales() { integrality_scale_.clear(); }  // revised_simplex.h:236
   bool objective_limit_reached() const { return objective_limit_reached_; }
   // revised_simplex.h:209-211 (UpdateRow::ComputeAndGetUnitRowLeftInverse).
   const ScatteredVector& GetUnitRowLeftInverse(int row) {
@@ -3993,6 +3994,10 @@ int oracle_lp_set_starting_variable_values(void* hv, const double* values, int32
 }
 int oracle_lp_set_integrality_scale(void* hv, int32_t col, double scale) {
   static_cast<OracleHandle*>(hv)->simplex.SetIntegralityScale(col, scale);
+  return 0;
+}
+int oracle_lp_clear_integrality_scales(void* hv) {
+  static_cast<OracleHandle*>(hv)->simplex.ClearIntegralityScales();
   return 0;
 }
 int oracle_lp_objective_limit_reached(void* hv, int32_t* reached) {

@@ -53,6 +53,7 @@ def lib():
         L.oracle_lp_notify_matrix_changed.argtypes = [vp]
         L.oracle_lp_set_starting_variable_values.argtypes = [vp, vp, ctypes.c_int32]
         L.oracle_lp_set_integrality_scale.argtypes = [vp, ctypes.c_int32, ctypes.c_double]
+        L.oracle_lp_clear_integrality_scales.argtypes = [vp]
         L.oracle_lp_objective_limit_reached.argtypes = [vp, vp]
         L.oracle_lp_get_unit_row_left_inverse.argtypes = [vp, ctypes.c_int32, vp, vp, vp]
         L.oracle_lp_compute_dictionary.argtypes = [vp, vp, ctypes.c_int32, vp]
@@ -172,6 +173,9 @@ class OracleLp:
 
     def set_integrality_scale(self, col, scale):
         self._call("set_integrality_scale", int(col), ctypes.c_double(scale))
+
+    def clear_integrality_scales(self):
+        self._call("clear_integrality_scales")
 
     def objective_limit_reached(self):
         r = ctypes.c_int32()

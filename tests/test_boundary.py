@@ -173,3 +173,49 @@ def test_objective_limit_and_starting_values_parity():
     ro2 = o2.solve()
     rg2 = g2.solve()
     parity_util.compare(o2, ro2, g2, rg2, lp)
+
+
+def test_clear_integrality_scales_drops_polish():
+    """ClearIntegralityScales (revised_simplex.h:236): after the clear, a solve
+    is the plain solve (no Polish), as CP-SAT relies on when it resets the
+    scales (sat/linear_programming_constraint.cc:424-433)."""
+    lp = lp_gen.random_sparse_lp(50, 160, 0.1, 12)
+    plain, rp = _solved_oracle(lp)
+    o = oracle_lib.OracleLp(abi.default_params())
+    o.load(lp)
+    for col in range(lp.n):
+        o.set_integrality_scale(col, 1.0 + (col % 3))
+    o.clear_integrality_scales()
+    r = o.solve()
+    assert r.iterations == rp.iterations
+    np.testing.assert_array_equal(o.basis(), plain.basis())
+    np.testing.assert_array_equal(o.primal(), plain.primal())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [12, 13])
+def test_clear_integrality_scales_parity(seed):
+    """mi_lp_clear_integrality_scales: scales set, cleared, then a subset set
+    again (the CP-SAT sequence of linear_programming_constraint.cc:424-433);
+    the engine's solve equals the oracle's bit for bit."""
+    import parity_util
+    from mi_glop import engine
+    lp = lp_gen.random_sparse_lp(50, 160, 0.1, seed)
+    p = abi.default_params()
+    o = oracle_lib.OracleLp(p)
+    g = engine.LpHandle(p)
+    for h in (o, g):
+        h.load(lp)
+        for col in range(lp.n):
+            h.set_integrality_scale(col, 2.0)
+        h.clear_integrality_scales()
+        for col in range(0, lp.n, 2):
+            h.set_integrality_scale(col, 1.0 + (col % 3))
+    ro = o.solve()
+    rg = g.solve()
+    parity_util.compare(o, ro, g, rg, lp)
+    for h in (o, g):
+        h.clear_integrality_scales()
+    ro2 = o.solve()
+    rg2 = g.solve()
+    parity_util.compare(o, ro2, g, rg2, lp)

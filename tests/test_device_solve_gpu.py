@@ -67,9 +67,14 @@ def test_device_u_solve_parity(case, variant, monkeypatch):
     o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
     parity_util.compare(o, ro, g, rg, lp)
     assert rg.deterministic_time == r_host.deterministic_time
-    st = g.kernel_stats()["tri_solve"]
+    stats = g.kernel_stats()
+    st = stats["tri_solve"]
     if name.startswith("c5") or name.startswith("dense"):
         assert st["launches"] > 0, f"{name}: no dense U solve reached the device"
+    if name.startswith("dense"):
+        # Dense bases make every FTRAN's L solve dense too: the device L solve
+        # (LowerSolveStartingAt restated as a gather, MILP_TRI_LOWER) ran.
+        assert stats["tri_solve_l"]["launches"] > 0, f"{name}: no dense L solve on the device"
 
 
 @pytest.mark.parametrize("device_dual", ["off", "force"])

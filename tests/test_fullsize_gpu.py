@@ -8,6 +8,8 @@ values). The windows cover the iterations bench.py times:
     start of the timed window (20 000 + warm-up), with the device U solves
     and the dual device mode on (their default at this size);
   * config 2 (10k x 50k dense, primal simplex): the first 40 iterations
+    against the live oracle, and the ends of both timed windows (iterations
+    67 and 1564) against the oracle's digests in tests/golden/c2_windows.json
     (the oracle needs ~0.5 s per iteration here);
   * config 3: eleven members of the Netlib-shaped suite solved to the end,
     the largest included.
@@ -47,6 +49,43 @@ def test_config2_window_parity():
     o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
     assert rg.iterations == 40
     parity_util.compare(o, ro, g, rg, lp)
+    assert g.kernel_stats()["pricing"]["launches"] > 0
+
+
+def _c2_golden():
+    import json
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "c2_windows.json")
+    return json.load(open(path))
+
+
+@pytest.mark.parametrize("cap", [67, 1564])
+def test_config2_bench_windows_golden(cap):
+    """The iterations bench.py times on config 2: the early window ends at
+    67 and the late window at 1564. The oracle needs ~0.5 s per iteration
+    there, so its state at those caps was computed once on the CPU
+    (scripts/make_c2_window_golden.py) and is kept as sha256 digests of the
+    exact bytes; the engine must reproduce them."""
+    import hashlib
+    import numpy as np
+    gold = _c2_golden()["caps"][str(cap)]
+    lp = lp_gen.dense_box_lp(10000, 50000, SEED)
+    g = engine.LpHandle(abi.default_params(max_number_of_iterations=cap))
+    g.load(lp)
+    r = g.solve()
+
+    def digest(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    var, cons = g.statuses()
+    got = {"iterations": int(r.iterations), "problem_status": int(r.problem_status),
+           "error_code": int(r.error_code), "objective": float(r.objective).hex(),
+           "basis": digest(g.basis()), "state": digest(g.state()),
+           "var_status": digest(var), "cons_status": digest(cons),
+           "primal": digest(g.primal()), "duals": digest(g.duals()),
+           "reduced_costs": digest(g.reduced_costs())}
+    for k, v in got.items():
+        assert v == gold[k], (k, v, gold[k])
     assert g.kernel_stats()["pricing"]["launches"] > 0
 
 
