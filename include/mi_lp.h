@@ -179,7 +179,12 @@ enum {
   MI_K_TRI_SOLVE_TAU = 10, /* the same dense U solve for the tau FTRAN on the
                               factorization's worker thread (dual_edge_norms.cc:134-141) */
   MI_K_TRI_SOLVE_L = 11,   /* dense L solve of FTRAN (sparse.cc:793-812) on the device */
-  MI_K_COUNT = 12
+  MI_K_TRI_SOLVE_T = 12,   /* dense solves of BTRAN on the device: U^T (TransposeUpperSolve,
+                              sparse.cc:848-897), L^T (TransposeLowerSolve), the unit-row U^T
+                              (LowerSolveStartingAt, lu_factorization.cc:405-436) */
+  MI_K_TRI_SOLVE_UPPER = 13, /* dense UpperSolve (sparse.cc:814-846): the product-form and
+                                squared-norm FTRANs' U */
+  MI_K_COUNT = 14
 };
 
 void mi_glop_params_default(mi_glop_params* p);

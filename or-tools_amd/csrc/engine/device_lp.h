@@ -131,9 +131,9 @@ class DeviceLp : public DeviceSolver {
     kTriLevels, kTriRecRow, kTriRecN, kTriRecEntry, kTriRecValue, kTriDiag, kTriOvfPos,
     kTriOvfValue, kTriPosRow, kTriNumStaged
   };
-  // One triangular matrix's level schedule and records, rebuilt when the
-  // factorization key changes. 0: U (TransposeLowerSolve of U^T), 1: L.
-  enum TriMatrix { kTriU = 0, kTriL = 1, kTriNumMatrices = 2 };
+  // One triangular loop's level schedule and records (device_solver.h
+  // TriKind), rebuilt when the factorization key changes.
+  enum TriMatrix { kTriU = 0, kTriL = 1, kTriNumMatrices = kNumTriKinds };
   struct TriSchedule {
     uint64_t key = 0;
     bool ok = false;
@@ -155,8 +155,8 @@ class DeviceLp : public DeviceSolver {
     double* m_x = nullptr;       // its device-visible address
     size_t h_x_elems = 0;
     int* h_top = nullptr;        // pinned
-    void* graph_exec[kTriNumMatrices] = {nullptr, nullptr};  // hipGraphExec_t per matrix
-    uint64_t graph_key[kTriNumMatrices] = {0, 0};            // schedule captured for
+    void* graph_exec[kTriNumMatrices] = {};  // hipGraphExec_t per matrix
+    uint64_t graph_key[kTriNumMatrices] = {};  // schedule captured for
     void* ev[2] = {nullptr, nullptr};
   };
   // TriangularMatrix::TransposeLowerSolve (sparse.cc:899-955) on one CU,
@@ -165,6 +165,8 @@ class DeviceLp : public DeviceSolver {
                            std::vector<double>* x) override;
   bool LowerSolve(const TriangularMatrix& lower, uint64_t key,
                   std::vector<double>* x) override;
+  bool Solve(TriKind kind, const TriangularMatrix& t, uint64_t key, int start,
+             std::vector<double>* x) override;
 
   // Accounting (roofline): launches, algorithmic bytes, HIP-event time.
   void SetTiming(bool on);
@@ -275,6 +277,9 @@ class DeviceLp : public DeviceSolver {
                         const int64_t* st, const int32_t* idx, const double* val, bool reverse,
                         bool descending, bool sequential, uint64_t key, void* stream);
   bool TriSolve(int which, const TriangularMatrix& t, uint64_t key, std::vector<double>* x);
+  // Gather lists of a scatter loop: output r lists (column j, t[r, j]) for
+  // the columns j >= fni holding row r, by ascending j (or descending).
+  void TransposeColumns(const TriangularMatrix& t, bool descending);
   void TriReserve(TriBuffer* b, size_t bytes);
   void PrepareTriContext(int slot, int rows, int pos);
   milp_kernels::TriSolveArgs TriArgs(const TriSchedule& s, const TriContext& c) const;
@@ -489,10 +494,14 @@ class DeviceLp : public DeviceSolver {
   bool tri_syncfree_ = true;  // MILP_TRI_SYNCFREE: readiness-driven single launch
   int tri_syncfree_min_levels_ = 0;  // MILP_TRI_SYNCFREE_MIN_LEVELS: shallower -> level plan
   bool tri_fuse0_ = true;     // MILP_TRI_FUSE0: level 0 inside the gather kernel
+  int tri_poll_max_ = 1;      // MILP_TRI_POLL_MAX: sync-free poll backoff cap (s_sleep units)
+  int tri_persist_groups_ = 0;  // MILP_TRI_PERSIST: persistent sync-free workgroups (0: off)
+  int tri_xcd_stride_ = 1;    // MILP_TRI_XCD=1: the persistent ones on one XCD (stride 8)
   bool stream_priority_ = false;  // MILP_STREAM_PRIORITY=1: solver stream high, tau stream low
   bool stream_prioritized_ = false;  // stream_ was created at the highest priority
   void SetStreamPriority(bool high);
   bool tri_lower_ = true;     // MILP_TRI_LOWER: the L solves too
+  bool tri_btran_ = true;     // MILP_TRI_BTRAN: the other dense loops (BTRAN, UpperSolve) too
   int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
   uint64_t* d_tri_clock_ = nullptr;
   TriSchedule tri_sched_[kTriNumMatrices];

@@ -157,11 +157,17 @@ void DeviceLp::Init(int device) {
   if (const char* v = std::getenv("MILP_TRI_MAPPED")) tri_mapped_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_SYNCFREE")) tri_syncfree_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_LOWER")) tri_lower_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_TRI_BTRAN")) tri_btran_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_MIN_WIDTH")) tri_min_width_ = std::atoi(v);
   if (const char* v = std::getenv("MILP_TRI_SYNCFREE_MIN_LEVELS")) {
     tri_syncfree_min_levels_ = std::atoi(v);
   }
   if (const char* v = std::getenv("MILP_TRI_FUSE0")) tri_fuse0_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_TRI_POLL_MAX")) tri_poll_max_ = std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("MILP_TRI_PERSIST")) {
+    tri_persist_groups_ = std::max(0, std::min(256, std::atoi(v)));
+  }
+  if (const char* v = std::getenv("MILP_TRI_XCD")) tri_xcd_stride_ = std::atoi(v) != 0 ? 8 : 1;
   if (const char* v = std::getenv("MILP_SMALL_BATCH")) small_batch_ = std::atoi(v) != 0;
   CreateShards();
   StartWatchdog();

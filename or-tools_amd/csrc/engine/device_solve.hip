@@ -112,7 +112,6 @@ void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, cons
   s->sequential = sequential;
   const int64_t nnz = gst[nc] - gst[0];
   if (nnz >= (int64_t{1} << 31)) return;
-  if (sequential && !ones) return;  // LowerSolve's division order: host only
   std::vector<int32_t> level(nc, 0);
   int depth = 0;
   int num_work = 0;
@@ -370,6 +369,7 @@ milp_kernels::TriSolveArgs DeviceLp::TriArgs(const TriSchedule& s, const TriCont
   a.num_levels = s.levels;
   a.sequential = s.sequential ? 1 : 0;
   a.fuse_level0 = tri_fuse0_ ? 1 : 0;
+  a.poll_max = tri_poll_max_;
   a.clock = nullptr;
   return a;
 }
@@ -405,6 +405,13 @@ void DeviceLp::EnqueueTriKernels(const TriSchedule& s, const milp_kernels::TriSo
                                  void* stream) {
   // The single-launch kernel pays a cross-workgroup hand-off per level; a
   // shallow schedule runs faster as a few level launches.
+  if (tri_persist_groups_ > 0 && tri_syncfree_ && a.clock == nullptr &&
+      s.levels >= tri_syncfree_min_levels_) {
+    Check(milp_launch::tri_transpose_lower_persistent(a, tri_persist_groups_, tri_xcd_stride_,
+                                                      Stream(stream)),
+          "tri persistent");
+    return;
+  }
   if (tri_syncfree_ && a.clock == nullptr && a.num_work <= milp_kernels::kTriSyncFreeMaxWork &&
       s.levels >= tri_syncfree_min_levels_) {
     Check(milp_launch::tri_transpose_lower_syncfree(a, Stream(stream)), "tri syncfree");
@@ -444,6 +451,45 @@ bool DeviceLp::LowerSolve(const TriangularMatrix& lower, uint64_t key, std::vect
   return TriSolve(kTriL, lower, key, x);
 }
 
+bool DeviceLp::Solve(TriKind kind, const TriangularMatrix& t, uint64_t key, int /*start*/,
+                     std::vector<double>* x) {
+  // LowerSolveStartingAt(start): the loops below `start` only meet zeros in
+  // every caller (a unit row, or L's input below its first non-zero), which
+  // the gather computes as the loop leaves them.
+  if (kind != TriKind::kUpperT && !tri_btran_) return false;
+  if (kind == TriKind::kLower && !tri_lower_) return false;
+  return TriSolve(static_cast<int>(kind), t, key, x);
+}
+
+// Gather lists of a scatter loop over t's columns (LowerSolveStartingAt,
+// UpperSolve): output r lists the columns j >= fni whose column holds row r,
+// with t[r, j], by ascending j (LowerSolve's column order) or descending
+// (UpperSolve's). Built into tri_lt_* (a counting transpose).
+void DeviceLp::TransposeColumns(const TriangularMatrix& t, bool descending) {
+  const int nc = t.num_cols();
+  const int fni = t.GetFirstNonIdentityColumn();
+  tri_lt_starts_.assign(nc + 1, 0);
+  for (int j = fni; j < nc; ++j) {
+    for (int64_t i = t.starts_[j]; i < t.starts_[j + 1]; ++i) ++tri_lt_starts_[t.rows_[i] + 1];
+  }
+  for (int r = 0; r < nc; ++r) tri_lt_starts_[r + 1] += tri_lt_starts_[r];
+  tri_lt_idx_.resize(tri_lt_starts_[nc]);
+  tri_lt_val_.resize(tri_lt_starts_[nc]);
+  std::vector<int64_t> fill(tri_lt_starts_.begin(), tri_lt_starts_.end() - 1);
+  auto put = [&](int j) {
+    for (int64_t i = t.starts_[j]; i < t.starts_[j + 1]; ++i) {
+      const int64_t at = fill[t.rows_[i]]++;
+      tri_lt_idx_[at] = j;
+      tri_lt_val_[at] = t.coefficients_[i];
+    }
+  };
+  if (descending) {
+    for (int j = nc - 1; j >= fni; --j) put(j);
+  } else {
+    for (int j = fni; j < nc; ++j) put(j);
+  }
+}
+
 bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
                         std::vector<double>* x) {
   if (tri_mode_ == 2) return false;
@@ -458,8 +504,12 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
   // The solver's thread (slot 0) or the factorization's tau worker (slot 1).
   const int slot = g_lu_slot == 0 ? 0 : 1;
   if (slot != 0 && !tri_tau_) return false;
-  const int id = slot != 0 ? MI_K_TRI_SOLVE_TAU : which == kTriU ? MI_K_TRI_SOLVE
-                                                                 : MI_K_TRI_SOLVE_L;
+  const TriKind kind = static_cast<TriKind>(which);
+  const int id = slot != 0                       ? MI_K_TRI_SOLVE_TAU
+                 : kind == TriKind::kUpperT      ? MI_K_TRI_SOLVE
+                 : kind == TriKind::kLower       ? MI_K_TRI_SOLVE_L
+                 : kind == TriKind::kUpper       ? MI_K_TRI_SOLVE_UPPER
+                                                 : MI_K_TRI_SOLVE_T;
   SolveCallTimer timer(&stats_, id);
   DeviceOp(which == kTriU ? (slot == 0 ? "tri U enter" : "tri U enter (slot 1)")
                           : (slot == 0 ? "tri L enter" : "tri L enter (slot 1)"));
@@ -475,35 +525,44 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
     if (c.stream == nullptr) PrepareTriContext(slot, nc, 1);
     if (s.key != key) {
       DeviceOp("tri build");
-      if (which == kTriU) {
-        // Gather lists = the columns of U^T, evaluated from their ends.
-        BuildTriSchedule(&s, nc, t.GetFirstNonIdentityColumn(), t.all_diagonal_coefficients_are_one_,
-                         t.diagonal_coefficients_.data(), t.starts_.data(), t.rows_.data(),
-                         t.coefficients_.data(), /*reverse=*/true, /*descending=*/true,
-                         /*sequential=*/false, key, c.stream);
-      } else {
-        // Gather lists = the rows of L, ascending columns (a counting
-        // transpose of its columns, sparse.cc:793-812's scatter order).
-        const int fni = t.GetFirstNonIdentityColumn();
-        tri_lt_starts_.assign(nc + 1, 0);
-        for (int j = fni; j < nc; ++j) {
-          for (int64_t i = t.starts_[j]; i < t.starts_[j + 1]; ++i) ++tri_lt_starts_[t.rows_[i] + 1];
-        }
-        for (int r = 0; r < nc; ++r) tri_lt_starts_[r + 1] += tri_lt_starts_[r];
-        tri_lt_idx_.resize(tri_lt_starts_[nc]);
-        tri_lt_val_.resize(tri_lt_starts_[nc]);
-        std::vector<int64_t> fill(tri_lt_starts_.begin(), tri_lt_starts_.end() - 1);
-        for (int j = fni; j < nc; ++j) {
-          for (int64_t i = t.starts_[j]; i < t.starts_[j + 1]; ++i) {
-            const int64_t at = fill[t.rows_[i]]++;
-            tri_lt_idx_[at] = j;
-            tri_lt_val_[at] = t.coefficients_[i];
-          }
-        }
-        BuildTriSchedule(&s, nc, fni, t.all_diagonal_coefficients_are_one_,
-                         t.diagonal_coefficients_.data(), tri_lt_starts_.data(),
-                         tri_lt_idx_.data(), tri_lt_val_.data(), /*reverse=*/false,
-                         /*descending=*/false, /*sequential=*/true, key, c.stream);
+      const int fni = t.GetFirstNonIdentityColumn();
+      const bool ones = t.all_diagonal_coefficients_are_one_;
+      const double* diag = t.diagonal_coefficients_.data();
+      switch (kind) {
+        case TriKind::kUpperT:
+        case TriKind::kLowerT:
+          // TransposeLowerSolve (sparse.cc:899-955): gather lists = t's
+          // columns, evaluated from their ends; reads rows > c.
+          BuildTriSchedule(&s, nc, fni, ones, diag, t.starts_.data(), t.rows_.data(),
+                           t.coefficients_.data(), /*reverse=*/true, /*descending=*/true,
+                           /*sequential=*/false, key, c.stream);
+          break;
+        case TriKind::kUpperTUp:
+          // TransposeUpperSolve (sparse.cc:848-897): t's columns forward;
+          // reads rows < c, also rows below the first non-identity column
+          // (positions from row 0).
+          BuildTriSchedule(&s, nc, 0, ones, diag, t.starts_.data(), t.rows_.data(),
+                           t.coefficients_.data(), /*reverse=*/false, /*descending=*/false,
+                           /*sequential=*/false, key, c.stream);
+          break;
+        case TriKind::kLower:
+        case TriKind::kUnitRow:
+          // LowerSolveStartingAt (sparse.cc:792-812): a scatter by ascending
+          // columns, restated as a gather over t's rows in that order.
+          TransposeColumns(t, /*descending=*/false);
+          BuildTriSchedule(&s, nc, fni, ones, diag, tri_lt_starts_.data(), tri_lt_idx_.data(),
+                           tri_lt_val_.data(), /*reverse=*/false, /*descending=*/false,
+                           /*sequential=*/true, key, c.stream);
+          break;
+        case TriKind::kUpper:
+          // UpperSolve (sparse.cc:814-846): the scatter by descending columns;
+          // rows below the first non-identity column receive too (outputs
+          // from row 0; their own columns are identity, never divided).
+          TransposeColumns(t, /*descending=*/true);
+          BuildTriSchedule(&s, nc, 0, ones, diag, tri_lt_starts_.data(), tri_lt_idx_.data(),
+                           tri_lt_val_.data(), /*reverse=*/false, /*descending=*/true,
+                           /*sequential=*/true, key, c.stream);
+          break;
       }
       if (which == kTriU) {
         if (const char* d = std::getenv("MILP_TRI_DEBUG")) tri_debug_left_ = std::atoi(d);
@@ -521,14 +580,16 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
   // U (sparse.cc:908-912): the host loop starts at the last non-zero; the
   // L loop runs over every column (outputs below its start receive nothing).
   int top = nc - 1;
-  if (which == kTriU) {
+  if (kind == TriKind::kUpperT || kind == TriKind::kLowerT) {
     while (top >= fni && xv[top] == 0.0) --top;
     if (top < fni) return true;
   }
   if (s.rows_upto[top + 1] - s.rows_upto[fni] == 0) return true;  // identity part only
   // Outputs c >= fni read rows >= fni only: x[fni..nc) in and out.
   const size_t in = size_t(nc - fni);
+  FtranTimer ft(kFtDevCopyIn);
   CopyHost(c.h_x + fni, xv + fni, in * sizeof(double));
+  ft.Lap(kFtDevRun);
   *c.h_top = top;
   int* h_words = reinterpret_cast<int*>(c.h_x + nc);
   h_words[0] = top;  // zero-copy plan reads it here
@@ -622,6 +683,7 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
   if (*static_cast<volatile int*>(h_words + 1) != 0) {
     throw DeviceError("triangular solve: dependency wait timed out");
   }
+  ft.Lap(kFtDevCopyOut);
   CopyHost(xv + fni, c.h_x + fni, size_t(top - fni + 1) * sizeof(double));
   return true;
 }

@@ -14,9 +14,27 @@ namespace milp {
 
 class TriangularMatrix;
 
+// The dense loops of TriangularMatrix (sparse.cc:776-955) the device
+// replaces, by the matrix of the LU they run on:
+enum class TriKind {
+  kUpperT = 0,     // transpose_upper_.TransposeLowerSolve: FTRAN's U (gather from the end)
+  kLower = 1,      // lower_.LowerSolveStartingAt: FTRAN's L (column scatter)
+  kUpperTUp = 2,   // upper_.TransposeUpperSolve: BTRAN's U^T (forward gather)
+  kLowerT = 3,     // lower_.TransposeLowerSolve: BTRAN's L^T (gather from the end)
+  kUnitRow = 4,    // transpose_upper_.LowerSolveStartingAt: the unit-row BTRAN's U^T
+  kUpper = 5,      // upper_.UpperSolve: the product-form FTRAN's U (backward scatter)
+};
+constexpr int kNumTriKinds = 6;
+
 class DeviceSolver {
  public:
   virtual ~DeviceSolver() = default;
+  // x <- the result of the host loop `kind` on t, bit for bit (start: the
+  // first column of LowerSolveStartingAt; ignored by the other loops).
+  // Returns false, leaving x untouched, when the solve should run on the
+  // host (MILP_DEVICE_SOLVE and the size threshold decide).
+  virtual bool Solve(TriKind kind, const TriangularMatrix& t, uint64_t key, int start,
+                     std::vector<double>* x) = 0;
   // x <- the result of t.TransposeLowerSolve(x), bit for bit. `key`
   // identifies the matrix (its LU and the factorization that built it): the
   // device copy and its dependency schedule are rebuilt when it changes.

@@ -14,6 +14,9 @@
 
 namespace milp {
 
+double g_ftran_ms[kFtPieces] = {};
+const bool g_ftran_timing = std::getenv("MILP_PHASE_TIMING") != nullptr;
+
 // ---------------------------------------------------------------------------
 // Markowitz (markowitz.cc:14-494)
 Status Markowitz::ComputeRowAndColumnPermutation(const CompactSparseMatrixView& b,
@@ -488,13 +491,13 @@ Fractional LuFactorization::RightSolveSquaredNorm(const ColumnView& a) const {
   }
   lower_.ComputeRowsToConsiderInSortedOrder(&non_zero_rows_);
   if (non_zero_rows_.empty()) {
-    lower_.LowerSolve(&DenseZeroScratch());
+    DenseLowerSolve(0, &DenseZeroScratch());
   } else {
     lower_.HyperSparseSolve(&DenseZeroScratch(), &non_zero_rows_);
     upper_.ComputeRowsToConsiderInSortedOrder(&non_zero_rows_);
   }
   if (non_zero_rows_.empty()) {
-    upper_.UpperSolve(&DenseZeroScratch());
+    DenseSolve(TriKind::kUpper, upper_, 0, &DenseZeroScratch());
   } else {
     upper_.HyperSparseSolveWithReversedNonZeros(&DenseZeroScratch(),
                                                 &non_zero_rows_);
@@ -532,6 +535,31 @@ void LuFactorization::DenseLowerSolve(int start, std::vector<Fractional>* x) con
   if (device_solver_ == nullptr ||
       !device_solver_->LowerSolve(lower_, factorization_key_, x)) {
     lower_.LowerSolveStartingAt(start, x);
+  }
+}
+
+// Every other dense loop of the solves: on the device when it takes them
+// (same bits, device_solver.h), else the host loop.
+void LuFactorization::DenseSolve(TriKind kind, const TriangularMatrix& t, int start,
+                                 std::vector<Fractional>* x) const {
+  if (device_solver_ != nullptr && device_solver_->Solve(kind, t, factorization_key_, start, x)) {
+    return;
+  }
+  switch (kind) {
+    case TriKind::kUpperT:
+    case TriKind::kLowerT:
+      t.TransposeLowerSolve(x);
+      break;
+    case TriKind::kUpperTUp:
+      t.TransposeUpperSolve(x);
+      break;
+    case TriKind::kLower:
+    case TriKind::kUnitRow:
+      t.LowerSolveStartingAt(start, x);
+      break;
+    case TriKind::kUpper:
+      t.UpperSolve(x);
+      break;
   }
 }
 
@@ -640,7 +668,7 @@ void LuFactorization::LeftSolveUWithNonZeros(ScatteredVector* y) const {
   transpose_upper_.ComputeRowsToConsiderInSortedOrder(&y->non_zeros);
   y->non_zeros_are_sorted = true;
   if (y->non_zeros.empty()) {
-    upper_.TransposeUpperSolve(&y->values);
+    DenseSolve(TriKind::kUpperTUp, upper_, 0, &y->values);
   } else {
     upper_.TransposeHyperSparseSolve(&y->values, &y->non_zeros);
   }
@@ -674,7 +702,7 @@ bool LuFactorization::LeftSolveLWithNonZeros(
   transpose_lower_.ComputeRowsToConsiderInSortedOrder(nz);
   y->non_zeros_are_sorted = true;
   if (nz->empty()) {
-    lower_.TransposeLowerSolve(x);
+    DenseSolve(TriKind::kLowerT, lower_, 0, x);
   } else {
     lower_.TransposeHyperSparseSolveWithReversedNonZeros(x, nz);
   }
@@ -725,7 +753,7 @@ int LuFactorization::LeftSolveUForUnitRow(int col, ScatteredVector* y) const {
     transpose_upper_.ComputeRowsToConsiderInSortedOrder(&y->non_zeros);
     y->non_zeros_are_sorted = true;
     if (y->non_zeros.empty()) {
-      transpose_upper_.LowerSolveStartingAt(permuted_col, &y->values);
+      DenseSolve(TriKind::kUnitRow, transpose_upper_, permuted_col, &y->values);
     } else {
       transpose_upper_.HyperSparseSolve(&y->values, &y->non_zeros);
     }
@@ -771,16 +799,16 @@ void ApplyInversePermutationTo(const std::vector<int>& perm, const std::vector<F
 void LuFactorization::RightSolve(std::vector<Fractional>* x) const {
   if (is_identity_factorization_) return;
   ApplyPermutationTo(row_perm_, *x, &dense_column_scratchpad_);
-  lower_.LowerSolve(&dense_column_scratchpad_);
-  upper_.UpperSolve(&dense_column_scratchpad_);
+  DenseLowerSolve(0, &dense_column_scratchpad_);
+  DenseSolve(TriKind::kUpper, upper_, 0, &dense_column_scratchpad_);
   ApplyPermutationTo(inverse_col_perm_, dense_column_scratchpad_, x);
 }
 
 void LuFactorization::LeftSolve(std::vector<Fractional>* y) const {
   if (is_identity_factorization_) return;
   ApplyInversePermutationTo(inverse_col_perm_, *y, &dense_column_scratchpad_);
-  upper_.TransposeUpperSolve(&dense_column_scratchpad_);
-  lower_.TransposeLowerSolve(&dense_column_scratchpad_);
+  DenseSolve(TriKind::kUpperTUp, upper_, 0, &dense_column_scratchpad_);
+  DenseSolve(TriKind::kLowerT, lower_, 0, &dense_column_scratchpad_);
   ApplyInversePermutationTo(row_perm_, dense_column_scratchpad_, y);
 }
 
@@ -1148,8 +1176,11 @@ void BasisFactorization::RightSolve(ScatteredVector* d) const {
     BumpDeterministicTimeForSolve(static_cast<int64_t>(d->NumNonZerosEstimate()));
     return;
   }
+  FtranTimer t(kFtL);
   lu_factorization_.RightSolveLWithNonZeros(d);
+  t.Lap(kFtEtas);
   rank_one_factorization_.RightSolveWithNonZeros(d);
+  t.Lap(kFtU);
   lu_factorization_.RightSolveUWithNonZeros(d);
   d->SortNonZerosIfNeeded();
   BumpDeterministicTimeForSolve(static_cast<int64_t>(d->NumNonZerosEstimate()));
@@ -1249,8 +1280,11 @@ void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d)
     BumpDeterministicTimeForSolve(static_cast<int64_t>(d->NumNonZerosEstimate()));
     return;
   }
+  FtranTimer t(kFtL);
   lu_factorization_.RightSolveLForColumnView(compact_matrix_.column(col), d);
+  t.Lap(kFtEtas);
   rank_one_factorization_.RightSolveWithNonZeros(d);
+  t.Lap(kFtU);
   if (col >= static_cast<int>(right_pool_mapping_.size())) {
     right_pool_mapping_.resize(col + 1, kInvalidCol);
   }

@@ -21,6 +21,28 @@ namespace milp {
 // 1 on BasisFactorization's tau worker (the two run FTRANs concurrently).
 inline thread_local int g_lu_slot = 0;
 
+// Debug aid (MILP_PHASE_TIMING): host wall time of the pieces of the solver
+// thread's FTRANs (L, etas, U) and of the device U/L solve calls (copy-in,
+// launch + wait, copy-out). Printed with the phase timing.
+enum FtranPiece { kFtL, kFtEtas, kFtU, kFtDevCopyIn, kFtDevRun, kFtDevCopyOut, kFtPieces };
+extern double g_ftran_ms[kFtPieces];
+extern const bool g_ftran_timing;
+struct FtranTimer {
+  int p;
+  std::chrono::steady_clock::time_point t0;
+  explicit FtranTimer(int q) : p(q) {
+    if (g_ftran_timing && g_lu_slot == 0) t0 = std::chrono::steady_clock::now();
+  }
+  void Lap(int next) {
+    if (!g_ftran_timing || g_lu_slot != 0) return;
+    const auto now = std::chrono::steady_clock::now();
+    g_ftran_ms[p] += std::chrono::duration<double, std::milli>(now - t0).count();
+    t0 = now;
+    p = next;
+  }
+  ~FtranTimer() { Lap(p); }
+};
+
 // ---------------------------------------------------------------------------
 // TriangularMatrix (sparse.h:583-921).
 class TriangularMatrix : public CompactSparseMatrix {
@@ -827,6 +849,8 @@ class LuFactorization {
   void SetDeviceSolver(DeviceSolver* d) { device_solver_ = d; }
   // lower_.LowerSolveStartingAt(start, x), on the device when it takes it.
   void DenseLowerSolve(int start, std::vector<Fractional>* x) const;
+  void DenseSolve(TriKind kind, const TriangularMatrix& t, int start,
+                  std::vector<Fractional>* x) const;
 
   // Exposed for the factor-structure parity tests.
   const TriangularMatrix& lower() const { return lower_; }

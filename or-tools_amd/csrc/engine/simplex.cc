@@ -103,6 +103,7 @@ PhaseClock::PhaseClock(bool dual) : names(dual ? kDual : kPrimal) {
 
 void PhaseClock::Reset() {
   std::fill(ms, ms + kPhases, 0.0);
+  std::fill(g_ftran_ms, g_ftran_ms + kFtPieces, 0.0);
   std::fill(g_sub_ms, g_sub_ms + kNumSubPhases, 0.0);
   g_dual_candidates = g_dual_list = 0.0;
   window = 0;
@@ -118,6 +119,15 @@ void PhaseClock::Dump(long long iterations) {
   if (g_dual_list > 0.0) {
     std::fprintf(stderr, "  device ratio test: %.0f candidates from %.0f update-row positions\n",
                  g_dual_candidates, g_dual_list);
+  }
+  {
+    static const char* const kFt[kFtPieces] = {"ftran L", "ftran etas", "ftran U (call)",
+                                                "  U copy-in", "  U launch+wait",
+                                                "  U copy-out"};
+    for (int i = 0; i < kFtPieces; ++i) {
+      std::fprintf(stderr, "  %-22s %10.3f ms  (%.3f ms/it)\n", kFt[i], g_ftran_ms[i],
+                   iterations > 0 ? g_ftran_ms[i] / iterations : 0.0);
+    }
   }
   std::fprintf(stderr, "  -- sections:\n");
   for (int i = 0; i < kNumSubPhases; ++i) {
@@ -2337,6 +2347,8 @@ class VariableValues {
   }
 
  private:
+  std::vector<Fractional> price_scratch_;  // UpdateDualPrices' parallel pass
+  std::vector<uint8_t> price_keep_;
   Fractional GetUpperBoundInfeasibility(int col) const {
     return variable_values_[col] - variables_info_.GetVariableUpperBounds()[col];
   }
@@ -2534,6 +2546,41 @@ void VariableValues::UpdateDualPrices(const std::vector<int>& rows) {
   const Fractional* lb = variables_info_.GetVariableLowerBounds().data();
   const Fractional* ub = variables_info_.GetVariableUpperBounds().data();
   const size_t n = rows.size();
+  if (n >= 8192 && HostPool::Get().threads() > 1) {
+    // Long lists (a dense direction): the prices, element by element with the
+    // serial loop's expression, in parallel into scratch (-1: not a
+    // candidate); then AddOrUpdate / Remove in list order, so the top-k
+    // bookkeeping and its RNG draws are the serial loop's.
+    price_scratch_.resize(n);
+    price_keep_.resize(n);
+    Fractional* price = price_scratch_.data();
+    uint8_t* keep = price_keep_.data();
+    const int* basis = basis_.data();
+    const bool by_norm = put_more_importance_on_norm_;
+    ParallelRanges(static_cast<int64_t>(n), 8192, 64, [&](int, int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k) {
+        if (k + 16 < e) {
+          const int ahead = basis[rows[k + 16]];
+          __builtin_prefetch(x + ahead);
+          __builtin_prefetch(lb + ahead);
+          __builtin_prefetch(ub + ahead);
+        }
+        const int row = rows[k];
+        const int col = basis[row];
+        const Fractional inf = std::max(x[col] - ub[col], lb[col] - x[col]);
+        keep[k] = inf > tolerance ? 1 : 0;
+        if (keep[k]) price[k] = by_norm ? std::fabs(inf) / sn[row] : Square(inf) / sn[row];
+      }
+    });
+    for (size_t k = 0; k < n; ++k) {
+      if (keep[k]) {
+        dual_prices_->AddOrUpdate(rows[k], price[k]);
+      } else {
+        dual_prices_->Remove(rows[k]);
+      }
+    }
+    return;
+  }
   for (size_t k = 0; k < n; ++k) {
     if (k + 16 < n) {
       const int ahead = basis_[rows[k + 16]];

@@ -331,6 +331,9 @@ struct TriSolveArgs {
   // Level plan: 1 when level 0 (outputs without entries, only a division)
   // is computed inside the gather kernel instead of a launch of its own.
   int fuse_level0;
+  // Sync-free variants: a waiting lane's sleep between polls doubles from
+  // one s_sleep unit up to this many (MILP_TRI_POLL_MAX; 1 = fixed).
+  int poll_max;
 };
 // The sync-free variant needs every workgroup resident: at most this many
 // outputs (512 workgroups of 256 threads, 2 per CU).
@@ -417,6 +420,11 @@ hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, const int
 // The same solve driven by per-output readiness instead of levels (one
 // launch for the whole triangle; rec_row/x updated in place, no scatter).
 hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, hipStream_t s);
+// The same, persistent: `groups` workgroups of kTriThreads threads walk the
+// outputs in level order (thread t: t, t + T, ...); xcd_stride 8 keeps them
+// on one XCD under round-robin dealing (speed only, any placement is correct).
+hipError_t tri_transpose_lower_persistent(const milp_kernels::TriSolveArgs& args, int groups,
+                                          int xcd_stride, hipStream_t s);
 hipError_t column_squared_norms(const int64_t* starts, const double* vals,
                                 const uint64_t* relevant, int ncols, double* out,
                                 hipStream_t s);

@@ -109,6 +109,16 @@ __device__ __forceinline__ double subtract_sequential(const TriSolveArgs& a, con
   return sum;
 }
 
+// A scatter loop's own column (sparse.cc:792-846): a zero is skipped, so it
+// keeps its bits and is not divided; anything else is divided by the
+// diagonal (nothing to do for a unit one). Consumers skip the columns whose
+// final value is zero, as the loop does (bit-identical except where value /
+// diagonal underflows to zero, which the loop would still scatter).
+__device__ __forceinline__ double tri_sequential_divide(const TriSolveArgs& a, double sum,
+                                                        double d) {
+  return (a.diag != nullptr && sum != 0.0) ? sum / d : sum;
+}
+
 // The output's value from its input `sum` and its entries (final values).
 __device__ __forceinline__ double tri_apply(const TriSolveArgs& a, const double* y, double sum,
                                             const TriRec& r) {
@@ -126,7 +136,7 @@ __device__ __forceinline__ double tri_apply(const TriSolveArgs& a, const double*
     } else {
       sum = subtract_sequential(a, y, sum, r.e.x, r.e.x + r.n);
     }
-    return sum;  // unit diagonal (the schedule builder requires it)
+    return tri_sequential_divide(a, sum, r.d);
   }
   if (r.n <= 4) {
     const int n = r.n;
@@ -190,7 +200,9 @@ __global__ __launch_bounds__(256) void tri_gather_level0_kernel(TriSolveArgs a) 
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.num_pos;
        k += gridDim.x * blockDim.x) {
     double v = a.x[a.pos_row[k]];
-    if (k < l0_end && a.rec_row[k] <= top) v = v / a.diag[k];  // padding rows: INT32_MAX
+    if (k < l0_end && a.rec_row[k] <= top) {  // padding rows: INT32_MAX
+      v = a.sequential ? tri_sequential_divide(a, v, a.diag[k]) : v / a.diag[k];
+    }
     a.y[k] = v;
   }
 }
@@ -254,7 +266,7 @@ __device__ __forceinline__ double tri_apply_vals(const TriSolveArgs& a, const Va
         if (v != 0.0) sum -= v * a.ovf_value[e];
       }
     }
-    return sum;  // unit diagonal
+    return tri_sequential_divide(a, sum, r.d);
   }
   if (r.n <= 4) {
     const int n = r.n;
@@ -388,6 +400,13 @@ __global__ __launch_bounds__(256) void tri_init_kernel(TriSolveArgs a) {
   }
 }
 
+// Backoff between polls: `units` s_sleep(1) (64 clocks each), doubling up to
+// a.poll_max; fewer polls in flight leave the memory queues to the hand-offs.
+__device__ __forceinline__ void tri_backoff(const TriSolveArgs& a, int* units) {
+  for (int i = 0; i < *units; ++i) __builtin_amdgcn_s_sleep(1);
+  *units = min(*units * 2, a.poll_max);
+}
+
 __device__ __forceinline__ int tri_entry_pos(const TriSolveArgs& a, const int4& e, int n, int j) {
   if (n > 4) return a.ovf_pos[e.x + j];
   return j == 0 ? e.x : j == 1 ? e.y : j == 2 ? e.z : e.w;
@@ -402,7 +421,7 @@ __device__ __forceinline__ double tri_apply4(const TriSolveArgs& a, double sum, 
     if (y1 != 0.0) sum -= y1 * r.v[1];
     if (y2 != 0.0) sum -= y2 * r.v[2];
     if (y3 != 0.0) sum -= y3 * r.v[3];
-    return sum;
+    return tri_sequential_divide(a, sum, r.d);
   }
   if (n == 4) {
     sum -= r.v[0] * y0 + r.v[1] * y1 + r.v[2] * y2 + r.v[3] * y3;
@@ -414,16 +433,15 @@ __device__ __forceinline__ double tri_apply4(const TriSolveArgs& a, double sum, 
   return a.diag != nullptr ? sum / r.d : sum;
 }
 
-__global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= a.num_work) return;
-  const int top = *a.top;
+// Output k of the sync-free solve: wait for its entries, compute, store.
+__device__ __forceinline__ void tri_syncfree_output(const TriSolveArgs& a, int k, int top) {
   TriRec r;
   tri_load(a, k, a.num_work, top, &r);
   if (r.row > top) return;  // not computed: y[k] already holds x[row]
   double* y = a.y;
   const double in = a.x[r.row];
   bool done = false;
+  int backoff = 1;
   const uint64_t t0 = wall_clock64();  // 100 MHz
   if (r.n <= 4) {
     // One poll round loads all entries at once and keeps them: the values
@@ -447,7 +465,7 @@ __global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a) {
         if (a.fail != nullptr) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         done = true;
       } else {
-        __builtin_amdgcn_s_sleep(1);
+        tri_backoff(a, &backoff);
       }
     }
     return;
@@ -466,8 +484,34 @@ __global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a) {
       if (a.fail != nullptr) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       done = true;
     } else {
-      __builtin_amdgcn_s_sleep(2);
+      tri_backoff(a, &backoff);
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= a.num_work) return;
+  tri_syncfree_output(a, k, *a.top);
+}
+
+// Persistent form: the working workgroups' threads walk the outputs in level
+// order, thread t taking t, t + T, t + 2T, ... (T threads in all). Every wait
+// goes to a lower position; the thread owning it is at a position no higher
+// than the waiter's (same stride walk), so the lowest waiting output always
+// has its entries computed or computable: all waits end with every working
+// workgroup resident (a handful per XCD). With xcd_stride 8 only the blocks
+// b with b % 8 == 0 work: they share one XCD under the observed round-robin
+// dealing, so hand-offs stay in one L2 (speed only; the stores and loads are
+// agent scope, correct under any placement).
+__global__ __launch_bounds__(kTriThreads) void tri_syncfree_persistent_kernel(TriSolveArgs a,
+                                                                              int xcd_stride) {
+  if (blockIdx.x % xcd_stride != 0) return;
+  const int group = blockIdx.x / xcd_stride;
+  const int total = (gridDim.x / xcd_stride) * kTriThreads;
+  const int top = *a.top;
+  for (int k = group * kTriThreads + threadIdx.x; k < a.num_work; k += total) {
+    tri_syncfree_output(a, k, top);
   }
 }
 
@@ -492,6 +536,29 @@ hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, 
   // One thread per listed output: every workgroup resident (100k outputs =
   // 391 workgroups of 256 on 256 CUs).
   milp_kernels::tri_syncfree_kernel<<<(args.num_work + 255) / 256, 256, 0, s>>>(args);
+  e = hipGetLastError();
+  if (e != hipSuccess || args.host_x == nullptr) return e;
+  milp_kernels::tri_copy_out_kernel<<<row_blocks, 256, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t tri_transpose_lower_persistent(const milp_kernels::TriSolveArgs& args, int groups,
+                                          int xcd_stride, hipStream_t s) {
+  if (args.num_work <= 0) return hipSuccess;
+  const int row_blocks =
+      std::max(1, std::min(1024, (args.num_rows - args.first_col + 255) / 256));
+  hipError_t e;
+  if (args.host_x != nullptr) {
+    milp_kernels::tri_copy_in_kernel<<<row_blocks, 256, 0, s>>>(args);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const int pos_blocks = std::max(1, std::min(1024, (args.num_pos + 255) / 256));
+  milp_kernels::tri_init_kernel<<<pos_blocks, 256, 0, s>>>(args);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  milp_kernels::tri_syncfree_persistent_kernel<<<groups * xcd_stride, milp_kernels::kTriThreads,
+                                                 0, s>>>(args, xcd_stride);
   e = hipGetLastError();
   if (e != hipSuccess || args.host_x == nullptr) return e;
   milp_kernels::tri_copy_out_kernel<<<row_blocks, 256, 0, s>>>(args);

@@ -148,7 +148,7 @@ class MiLpRunCounters(ctypes.Structure):
 
 KERNEL_NAMES = ["pricing", "update_row", "primal_norms", "rc_update", "tri_solve",
                 "col_norms", "spmv_rows", "single_row", "dual_ratio", "readback",
-                "tri_solve_tau", "tri_solve_l"]
+                "tri_solve_tau", "tri_solve_l", "tri_solve_t", "tri_solve_upper"]
 
 # Names of every exported entry point of include/mi_lp.h (checked by tests).
 EXPORTED_SYMBOLS = [

@@ -219,3 +219,30 @@ def test_clear_integrality_scales_parity(seed):
     ro2 = o.solve()
     rg2 = g.solve()
     parity_util.compare(o, ro2, g, rg2, lp)
+
+
+@pytest.mark.gpu
+def test_iteration_times_and_run_counters():
+    """mi_lp_record_iteration_times / mi_lp_get_run_counters (bench.py's window
+    statistics): one timestamp per iteration, non-decreasing, readable while a
+    begun solve is parked; the factorization count grows across a window with
+    refactorizations and matches the oracle-independent bookkeeping."""
+    from mi_glop import engine
+    lp = lp_gen.random_sparse_lp(120, 400, 0.05, 16)
+    g = engine.LpHandle(abi.default_params(use_dual_simplex=1))
+    g.load(lp)
+    g.record_iteration_times(True)
+    g.begin(20)
+    c0 = g.run_counters()
+    assert c0["factorizations"] >= 1
+    assert c0["iterations"] == 20
+    ts = g.iteration_times()
+    assert len(ts) == 20 and np.all(np.diff(ts) >= 0.0)
+    fin, it = g.run_until(150)
+    c1 = g.run_counters()
+    assert c1["iterations"] == it
+    assert c1["factorizations"] >= c0["factorizations"]
+    assert c1["factorization_seconds"] >= c0["factorization_seconds"]
+    g.stop()
+    r = g.finish()
+    assert len(g.iteration_times()) == r.iterations

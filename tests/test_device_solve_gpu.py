@@ -42,6 +42,9 @@ VARIANTS = {
     "syncfree": {},
     "levels": {"MILP_TRI_SYNCFREE": "0"},
     "levels_copies": {"MILP_TRI_SYNCFREE": "0", "MILP_TRI_MAPPED": "0"},
+    "syncfree_copies": {"MILP_TRI_MAPPED": "0"},
+    "persistent_xcd": {"MILP_TRI_PERSIST": "32", "MILP_TRI_XCD": "1", "MILP_TRI_POLL_MAX": "8"},
+    "persistent_chip": {"MILP_TRI_PERSIST": "64", "MILP_TRI_POLL_MAX": "4"},
 }
 
 
@@ -49,7 +52,8 @@ VARIANTS = {
 # two (their kernels are shared, only the schedule walk differs).
 _PARAMS = [(c, "syncfree") for c in _cases()] + [
     (c, v) for c in _cases() if c[0] in ("c5_71", "dense_dual")
-    for v in ("levels", "levels_copies")]
+    for v in ("levels", "levels_copies", "syncfree_copies", "persistent_xcd",
+              "persistent_chip")]
 
 
 @pytest.mark.parametrize("case,variant", _PARAMS, ids=lambda x: x if isinstance(x, str) else x[0])
@@ -125,3 +129,35 @@ def test_device_u_solve_warm_started_children(monkeypatch):
         ro2 = o.solve()
         rg2 = g.solve()
         parity_util.compare(o, ro2, g, rg2, lp)
+
+
+@pytest.mark.parametrize("pfi", [0, 1], ids=["mpf", "product_form"])
+@pytest.mark.parametrize("dual", [0, 1])
+def test_device_btran_and_upper_solve_parity(pfi, dual, monkeypatch):
+    """Every dense loop of the factorization's solves on the device:
+    BTRAN's U^T (TransposeUpperSolve, sparse.cc:848-897), L^T
+    (TransposeLowerSolve), the unit-row U^T (LowerSolveStartingAt,
+    lu_factorization.cc:405-436), and with product-form etas the FTRAN's
+    UpperSolve (sparse.cc:814-846, a scatter restated as a gather with the
+    loop's zero skip and division). Forced onto the device at test size, the
+    engine must equal the oracle bit for bit and the device solves must run."""
+    monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
+    lp = lp_gen.dense_box_lp(90, 300, 81 + dual)
+    p = abi.default_params(use_dual_simplex=dual, use_middle_product_form_update=1 - pfi,
+                           max_number_of_iterations=600)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    st = g.kernel_stats()
+    assert st["tri_solve_t"]["launches"] > 0, "no dense BTRAN solve reached the device"
+    if pfi:
+        assert st["tri_solve_upper"]["launches"] > 0, "no dense UpperSolve on the device"
+
+
+def test_device_btran_sparse_dual_parity(monkeypatch):
+    """A sparse dual LP whose BTRANs turn dense late: forced device solves of
+    every kind against the oracle."""
+    monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
+    lp = lp_gen.sparse_c5_lp(700, 7000, 7, 83)
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1500)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
