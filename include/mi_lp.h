@@ -297,6 +297,25 @@ int mi_lp_record_iteration_times(mi_lp* h, int32_t enable);
 int64_t mi_lp_get_iteration_times(const mi_lp* h, double* out, int64_t cap);
 int mi_lp_get_run_counters(const mi_lp* h, mi_lp_run_counters* c);
 
+/* Cross-process split of ONE LP over `world` processes (the
+ * reference's sharding pattern is pdlp/sharder.h:34-160): every process loads
+ * the same LP into its handle and runs the same host control flow; process
+ * `rank` keeps column block `rank` of [A | I] (64-aligned blocks balanced by
+ * entries, as MILP_SHARDS cuts them) on its own GPU. Each per-column device
+ * operation runs on the owned block, and its results are joined in block
+ * order through `allgather`: the update row's list, the pricing reduced
+ * costs, the dual ratio test's filtered breakpoints (the all-reduce(min) of
+ * the bound is implicit: each block filters under its own bound, a superset
+ * of the joint filter) and the entering column's coefficient. Results are
+ * bit-identical to the unsplit engine. allgather(ctx, send, send_bytes, recv,
+ * recv_bytes) must place every rank's bytes in rank order (recv_bytes[r]
+ * bytes from rank r, all ranks' sizes known to the caller) and return 0.
+ * Call before mi_lp_load; world <= 1 or allgather == NULL turns it off. */
+typedef int (*mi_lp_allgather_fn)(void* ctx, const void* send, int64_t send_bytes, void* recv,
+                                  const int64_t* recv_bytes);
+int mi_lp_set_exchange(mi_lp* h, int32_t rank, int32_t world, void* ctx,
+                       mi_lp_allgather_fn allgather);
+
 /* Batch API: solves count independent LPs already loaded in handles (all on
  * the same device) on num_threads host threads; each thread drives several
  * LPs as fibers (MILP_BATCH_FIBERS, default 4) switching at device waits, and

@@ -185,6 +185,12 @@ class DeviceLp : public DeviceSolver {
   // shards, the candidates and update-row lists a concatenation. Row sums,
   // column norms and the triangular solves stay on this handle (full copy).
   int num_shards() const { return shards_.empty() ? 1 : static_cast<int>(shards_.size()); }
+  // Cross-process split (include/mi_lp.h mi_lp_set_exchange): this process
+  // owns block `rank` of `world`; fn all-gathers byte strings in rank order.
+  using ExchangeFn = int (*)(void* ctx, const void* send, int64_t send_bytes, void* recv,
+                             const int64_t* recv_bytes);
+  void SetExchange(int rank, int world, void* ctx, ExchangeFn fn);
+  bool IsLocalShard(int s) const { return shards_.empty() || shards_[s] != nullptr; }
   // Batched small-LP launches for this handle (the batch APIs turn it on for
   // their duration; MILP_SMALL_BATCH=1 turns it on everywhere, =0 nowhere).
   void SetSmallBatch(bool on);
@@ -249,7 +255,12 @@ class DeviceLp : public DeviceSolver {
   void ShardedStats();
   void FlushOwnMasks();
   bool is_shard_ = false;
-  std::vector<std::unique_ptr<DeviceLp>> shards_;
+  std::vector<std::unique_ptr<DeviceLp>> shards_;  // null: a block owned by another process
+  ExchangeFn exchange_fn_ = nullptr;
+  void* exchange_ctx_ = nullptr;
+  int exchange_rank_ = 0;
+  int exchange_world_ = 1;
+  void ExchangeParts(std::vector<std::string>* parts);
   std::vector<int> shard_begin_;
   bool own_mask_dirty_[kNumMasks] = {false, false, false};
   mi_lp_kernel_stats agg_stats_{};

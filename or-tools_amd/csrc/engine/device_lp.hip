@@ -491,13 +491,17 @@ void DeviceLp::Synchronize() {
   WaitStream();
   DeviceOp("Synchronize done");
   small_inflight_ = false;
-  for (auto& d : shards_) d->Synchronize();
+  for (auto& d : shards_) {
+    if (d) d->Synchronize();
+  }
 }
 
 void DeviceLp::ResetStats() {
   DrainTimings();
   std::memset(&stats_, 0, sizeof(stats_));
-  for (auto& d : shards_) d->ResetStats();
+  for (auto& d : shards_) {
+    if (d) d->ResetStats();
+  }
 }
 
 const mi_lp_kernel_stats& DeviceLp::stats() {

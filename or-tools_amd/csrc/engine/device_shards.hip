@@ -41,7 +41,97 @@ struct DeviceGuard {
   int device;
   ~DeviceGuard() { (void)hipSetDevice(device); }
 };
+// Shard results travel between processes as byte strings: vectors with a
+// count prefix, appended and read back in the same order.
+struct PartWriter {
+  std::string b;
+  template <typename T>
+  void Put(const std::vector<T>& v) {
+    const int64_t n = static_cast<int64_t>(v.size());
+    b.append(reinterpret_cast<const char*>(&n), sizeof(n));
+    if (n > 0) b.append(reinterpret_cast<const char*>(v.data()), size_t(n) * sizeof(T));
+  }
+  template <typename T>
+  void Put(T x) {
+    b.append(reinterpret_cast<const char*>(&x), sizeof(x));
+  }
+};
+struct PartReader {
+  const std::string& b;
+  size_t at = 0;
+  template <typename T>
+  void Get(std::vector<T>* v) {
+    int64_t n = 0;
+    Raw(&n, sizeof(n));
+    v->resize(size_t(n));
+    if (n > 0) Raw(v->data(), size_t(n) * sizeof(T));
+  }
+  template <typename T>
+  T Get() {
+    T x{};
+    Raw(&x, sizeof(x));
+    return x;
+  }
+  void Raw(void* dst, size_t bytes) {
+    if (at + bytes > b.size()) throw DeviceError("column split: short exchange message");
+    std::memcpy(dst, b.data() + at, bytes);
+    at += bytes;
+  }
+};
 }  // namespace
+
+// Cross-process split: `world` processes solve the same LP,
+// each with the same host control flow; process `rank` owns column block
+// `rank` on its own GPU. Every per-column operation runs on the owned block
+// only, and a join gathers the blocks' results in block order through the
+// caller's all-gather, so every process sees the joined vectors the
+// single-process split (and the unsplit engine) computes.
+void DeviceLp::SetExchange(int rank, int world, void* ctx, ExchangeFn fn) {
+  if (world <= 1 || fn == nullptr) {
+    exchange_fn_ = nullptr;
+    exchange_rank_ = 0;
+    exchange_world_ = 1;
+    return;
+  }
+  if (rank < 0 || rank >= world) throw DeviceError("column split: bad rank");
+  if (m_ > 0) throw DeviceError("column split: set the exchange before loading the LP");
+  exchange_fn_ = fn;
+  exchange_ctx_ = ctx;
+  exchange_rank_ = rank;
+  exchange_world_ = world;
+  DeviceGuard guard{device_};
+  shards_.clear();
+  shards_.resize(world);
+  auto shard = std::make_unique<DeviceLp>();
+  shard->is_shard_ = true;
+  shard->Init(device_);
+  shard->timing_ = timing_;
+  shards_[rank] = std::move(shard);
+}
+
+// Local shard results in, every shard's results out (block order).
+void DeviceLp::ExchangeParts(std::vector<std::string>* parts) {
+  if (exchange_fn_ == nullptr) return;
+  const int world = exchange_world_;
+  const std::string& mine = (*parts)[exchange_rank_];
+  int64_t n = static_cast<int64_t>(mine.size());
+  std::vector<int64_t> sizes(world, 0);
+  std::vector<int64_t> eight(world, int64_t{sizeof(int64_t)});
+  if (exchange_fn_(exchange_ctx_, &n, sizeof(n), sizes.data(), eight.data()) != 0) {
+    throw DeviceError("column split: exchange of sizes failed");
+  }
+  int64_t total = 0;
+  for (int64_t z : sizes) total += z;
+  std::string all(size_t(total), '\0');
+  if (exchange_fn_(exchange_ctx_, mine.data(), n, all.data(), sizes.data()) != 0) {
+    throw DeviceError("column split: exchange failed");
+  }
+  int64_t at = 0;
+  for (int r = 0; r < world; ++r) {
+    (*parts)[r].assign(all.data() + at, size_t(sizes[r]));
+    at += sizes[r];
+  }
+}
 
 void DeviceLp::CreateShards() {
   if (is_shard_) return;
@@ -99,6 +189,7 @@ void DeviceLp::ShardedUpload(const CompactSparseMatrix& csc) {
   }
   for (; s < ns; ++s) shard_begin_[s] = n;  // tiny LPs: empty trailing shards
   for (int k = 0; k < ns; ++k) {
+    if (!IsLocalShard(k)) continue;
     CompactSparseMatrix slice, slice_t;
     slice.PopulateColumnSlice(csc, shard_begin_[k], shard_begin_[k + 1]);
     slice_t.PopulateFromTranspose(slice);
@@ -109,13 +200,17 @@ void DeviceLp::ShardedUpload(const CompactSparseMatrix& csc) {
 uint64_t DeviceLp::list_epoch() const {
   if (shards_.empty()) return list_epoch_;
   uint64_t e = 0;
-  for (const auto& d : shards_) e += d->list_epoch_;
+  for (const auto& d : shards_) {
+    if (d) e += d->list_epoch_;
+  }
   return e;
 }
 
 void DeviceLp::SetTiming(bool on) {
   timing_ = on;
-  for (auto& d : shards_) d->timing_ = on;
+  for (auto& d : shards_) {
+    if (d) d->timing_ = on;
+  }
 }
 
 void DeviceLp::FlushOwnMasks() {
@@ -135,7 +230,7 @@ void DeviceLp::ShardedSetMask(Mask which, const uint64_t* words, int num_words) 
   DeviceGuard guard{device_};
   for (int s = 0; s < num_shards(); ++s) {
     const int b = shard_begin_[s], e = shard_begin_[s + 1];
-    if (e == b) continue;
+    if (e == b || !IsLocalShard(s)) continue;
     Shard(s).SetMask(which, words + b / 64, (e - b + 63) / 64);
   }
 }
@@ -145,6 +240,7 @@ void DeviceLp::ShardedUpdateRowColumnWise(const std::vector<double>& rho, double
                                           const std::vector<double>* w) {
   DeviceGuard guard{device_};
   for (int s = 0; s < num_shards(); ++s) {
+    if (!IsLocalShard(s)) continue;
     DeviceLp& d = Shard(s);
     if (d.n_total_ == 0) continue;
     // (byte accounting only) the shard's share of the relevant entries
@@ -158,6 +254,7 @@ void DeviceLp::ShardedUpdateRowRowWise(const std::vector<int>& filtered_rows,
                                        double drop) {
   DeviceGuard guard{device_};
   for (int s = 0; s < num_shards(); ++s) {
+    if (!IsLocalShard(s)) continue;
     DeviceLp& d = Shard(s);
     if (d.n_total_ > 0) d.UpdateRowRowWise(filtered_rows, rho, algorithm, drop);
   }
@@ -167,12 +264,26 @@ void DeviceLp::ShardedFetchUpdateRow(std::vector<int>* positions, std::vector<do
   DeviceGuard guard{device_};
   positions->clear();
   values->clear();
+  const int ns = num_shards();
+  std::vector<std::string> parts(ns);
+  for (int s = 0; s < ns; ++s) {
+    if (!IsLocalShard(s)) continue;
+    DeviceLp& d = Shard(s);
+    std::vector<int> p;
+    std::vector<double> v;
+    if (d.n_total_ > 0) d.FetchUpdateRow(&p, &v);
+    PartWriter w;
+    w.Put(p);
+    w.Put(v);
+    parts[s] = std::move(w.b);
+  }
+  ExchangeParts(&parts);
   std::vector<int> p;
   std::vector<double> v;
-  for (int s = 0; s < num_shards(); ++s) {
-    DeviceLp& d = Shard(s);
-    if (d.n_total_ == 0) continue;
-    d.FetchUpdateRow(&p, &v);
+  for (int s = 0; s < ns; ++s) {
+    PartReader r{parts[s]};
+    r.Get(&p);
+    r.Get(&v);
     for (int& c : p) c += shard_begin_[s];
     positions->insert(positions->end(), p.begin(), p.end());
     values->insert(values->end(), v.begin(), v.end());
@@ -183,18 +294,37 @@ void DeviceLp::ShardedFetchUpdateRow(std::vector<int>* positions, std::vector<do
 double DeviceLp::ShardedReadCoefficient(int col) {
   DeviceGuard guard{device_};
   const int s = ShardOf(col);
-  return Shard(s).ReadCoefficient(col - shard_begin_[s]);
+  if (exchange_fn_ == nullptr) return Shard(s).ReadCoefficient(col - shard_begin_[s]);
+  // The owner reads, everyone receives (a broadcast as an all-gather).
+  std::vector<std::string> parts(num_shards());
+  PartWriter w;
+  w.Put(IsLocalShard(s) ? Shard(s).ReadCoefficient(col - shard_begin_[s]) : 0.0);
+  parts[exchange_rank_] = std::move(w.b);
+  ExchangeParts(&parts);
+  PartReader r{parts[s]};
+  return r.Get<double>();
 }
 
 void DeviceLp::ShardedListDotsOverUpdateRow(const std::vector<double>& v,
                                             std::vector<double>* out) {
   DeviceGuard guard{device_};
   out->clear();
+  const int ns = num_shards();
+  std::vector<std::string> parts(ns);
   std::vector<double> part;
-  for (int s = 0; s < num_shards(); ++s) {
+  for (int s = 0; s < ns; ++s) {
+    if (!IsLocalShard(s)) continue;
     DeviceLp& d = Shard(s);
-    if (d.n_total_ == 0) continue;
-    d.ListDotsOverUpdateRow(v, &part);
+    part.clear();
+    if (d.n_total_ > 0) d.ListDotsOverUpdateRow(v, &part);
+    PartWriter w;
+    w.Put(part);
+    parts[s] = std::move(w.b);
+  }
+  ExchangeParts(&parts);
+  for (int s = 0; s < ns; ++s) {
+    PartReader r{parts[s]};
+    r.Get(&part);
     out->insert(out->end(), part.begin(), part.end());
   }
 }
@@ -210,11 +340,21 @@ void DeviceLp::ShardedListDots(const std::vector<int>& cols, const std::vector<d
     where[s].push_back(i);
   }
   out->assign(cols.size(), 0.0);
+  std::vector<std::string> parts(ns);
   std::vector<double> part;
   for (int s = 0; s < ns; ++s) {
-    if (sub[s].empty()) continue;
-    Shard(s).ListDots(sub[s], v, &part);
-    for (size_t k = 0; k < part.size(); ++k) (*out)[where[s][k]] = part[k];
+    if (!IsLocalShard(s)) continue;
+    part.clear();
+    if (!sub[s].empty()) Shard(s).ListDots(sub[s], v, &part);
+    PartWriter w;
+    w.Put(part);
+    parts[s] = std::move(w.b);
+  }
+  ExchangeParts(&parts);
+  for (int s = 0; s < ns; ++s) {
+    PartReader r{parts[s]};
+    r.Get(&part);
+    for (size_t k = 0; k < part.size() && k < where[s].size(); ++k) (*out)[where[s][k]] = part[k];
   }
 }
 
@@ -224,14 +364,30 @@ void DeviceLp::ShardedPricing(const std::vector<double>& c, const std::vector<do
   DeviceGuard guard{device_};
   rc->resize(n_total_);
   if (list_dots != nullptr) list_dots->clear();
+  const int ns = num_shards();
+  std::vector<std::string> parts(ns);
   std::vector<double> cs, part, dots;
-  for (int s = 0; s < num_shards(); ++s) {
+  for (int s = 0; s < ns; ++s) {
+    if (!IsLocalShard(s)) continue;
     DeviceLp& d = Shard(s);
-    if (d.n_total_ == 0) continue;
-    const int b = shard_begin_[s];
-    cs.assign(c.begin() + b, c.begin() + shard_begin_[s + 1]);
-    d.Pricing(cs, y, &part, w, w != nullptr ? &dots : nullptr);
-    std::copy(part.begin(), part.end(), rc->begin() + b);
+    part.clear();
+    dots.clear();
+    if (d.n_total_ > 0) {
+      const int b = shard_begin_[s];
+      cs.assign(c.begin() + b, c.begin() + shard_begin_[s + 1]);
+      d.Pricing(cs, y, &part, w, w != nullptr ? &dots : nullptr);
+    }
+    PartWriter pw;
+    pw.Put(part);
+    pw.Put(dots);
+    parts[s] = std::move(pw.b);
+  }
+  ExchangeParts(&parts);
+  for (int s = 0; s < ns; ++s) {
+    PartReader r{parts[s]};
+    r.Get(&part);
+    r.Get(&dots);
+    std::copy(part.begin(), part.end(), rc->begin() + shard_begin_[s]);
     if (w != nullptr) list_dots->insert(list_dots->end(), dots.begin(), dots.end());
   }
 }
@@ -241,6 +397,7 @@ void DeviceLp::ShardedDualBegin(const std::vector<double>& rc,
                                 const std::vector<double>& bound_diff) {
   DeviceGuard guard{device_};
   for (int s = 0; s < num_shards(); ++s) {
+    if (!IsLocalShard(s)) continue;
     DeviceLp& d = Shard(s);
     if (d.n_total_ == 0) continue;
     const int b = shard_begin_[s], e = shard_begin_[s + 1];
@@ -262,13 +419,14 @@ void DeviceLp::ShardedDualSetColBits(const std::vector<int32_t>& cols,
     sb[s].push_back(bits[i]);
   }
   for (int s = 0; s < ns; ++s) {
-    if (!sc[s].empty()) Shard(s).DualSetColBits(sc[s], sb[s]);
+    if (!sc[s].empty() && IsLocalShard(s)) Shard(s).DualSetColBits(sc[s], sb[s]);
   }
 }
 
 void DeviceLp::ShardedDualTakePricedReducedCosts() {
   DeviceGuard guard{device_};
   for (int s = 0; s < num_shards(); ++s) {
+    if (!IsLocalShard(s)) continue;
     DeviceLp& d = Shard(s);
     if (d.n_total_ > 0) d.DualTakePricedReducedCosts();
   }
@@ -277,11 +435,22 @@ void DeviceLp::ShardedDualTakePricedReducedCosts() {
 void DeviceLp::ShardedDualDownloadReducedCosts(std::vector<double>* rc) {
   DeviceGuard guard{device_};
   rc->resize(n_total_);
+  const int ns = num_shards();
+  std::vector<std::string> parts(ns);
   std::vector<double> part;
-  for (int s = 0; s < num_shards(); ++s) {
+  for (int s = 0; s < ns; ++s) {
+    if (!IsLocalShard(s)) continue;
     DeviceLp& d = Shard(s);
-    if (d.n_total_ == 0) continue;
-    d.DualDownloadReducedCosts(&part);
+    part.clear();
+    if (d.n_total_ > 0) d.DualDownloadReducedCosts(&part);
+    PartWriter w;
+    w.Put(part);
+    parts[s] = std::move(w.b);
+  }
+  ExchangeParts(&parts);
+  for (int s = 0; s < ns; ++s) {
+    PartReader r{parts[s]};
+    r.Get(&part);
     std::copy(part.begin(), part.end(), rc->begin() + shard_begin_[s]);
   }
 }
@@ -289,7 +458,7 @@ void DeviceLp::ShardedDualDownloadReducedCosts(std::vector<double>* rc) {
 void DeviceLp::ShardedDualSetReducedCost(int col, double value) {
   DeviceGuard guard{device_};
   const int s = ShardOf(col);
-  Shard(s).DualSetReducedCost(col - shard_begin_[s], value);
+  if (IsLocalShard(s)) Shard(s).DualSetReducedCost(col - shard_begin_[s], value);
 }
 
 void DeviceLp::ShardedDualRatioCandidates(double sign, double threshold,
@@ -300,12 +469,34 @@ void DeviceLp::ShardedDualRatioCandidates(double sign, double threshold,
   out->coeff.clear();
   out->rc.clear();
   out->list_count = 0;
+  const int ns = num_shards();
+  std::vector<std::string> parts(ns);
   DualCandidates part;
-  for (int s = 0; s < num_shards(); ++s) {
+  for (int s = 0; s < ns; ++s) {
+    if (!IsLocalShard(s)) continue;
     DeviceLp& d = Shard(s);
-    if (d.n_total_ == 0) continue;
-    d.DualRatioCandidates(sign, threshold, harris_tolerance, minimum_delta,
-                          variation_magnitude, &part);
+    part = DualCandidates();
+    if (d.n_total_ > 0) {
+      d.DualRatioCandidates(sign, threshold, harris_tolerance, minimum_delta,
+                            variation_magnitude, &part);
+    }
+    PartWriter w;
+    w.Put(part.col);
+    w.Put(part.coeff);
+    w.Put(part.rc);
+    w.Put(static_cast<int64_t>(part.list_count));
+    parts[s] = std::move(w.b);
+  }
+  // Across processes this is the reference's exchange: the blocks' filtered
+  // breakpoints (each a superset under its own bound, see the top of this
+  // file) gathered in block order.
+  ExchangeParts(&parts);
+  for (int s = 0; s < ns; ++s) {
+    PartReader r{parts[s]};
+    r.Get(&part.col);
+    r.Get(&part.coeff);
+    r.Get(&part.rc);
+    part.list_count = static_cast<int>(r.Get<int64_t>());
     for (int& c : part.col) c += shard_begin_[s];
     out->col.insert(out->col.end(), part.col.begin(), part.col.end());
     out->coeff.insert(out->coeff.end(), part.coeff.begin(), part.coeff.end());
@@ -319,6 +510,7 @@ void DeviceLp::ShardedDualUpdateReducedCosts(double mult, int leaving_col,
                                              double leaving_value, int entering_col) {
   DeviceGuard guard{device_};
   for (int s = 0; s < num_shards(); ++s) {
+    if (!IsLocalShard(s)) continue;
     DeviceLp& d = Shard(s);
     if (d.n_total_ == 0) continue;
     const int b = shard_begin_[s], e = shard_begin_[s + 1];
@@ -333,12 +525,22 @@ void DeviceLp::ShardedDualBoxedFlips(const std::vector<int>* cols, double thresh
   DeviceGuard guard{device_};
   const int ns = num_shards();
   std::vector<uint8_t> part;
+  std::vector<std::string> parts(ns);
   if (cols == nullptr) {
     flags->assign(n_total_, 0);
     for (int s = 0; s < ns; ++s) {
+      if (!IsLocalShard(s)) continue;
       DeviceLp& d = Shard(s);
-      if (d.n_total_ == 0) continue;
-      d.DualBoxedFlips(nullptr, threshold, &part);
+      part.clear();
+      if (d.n_total_ > 0) d.DualBoxedFlips(nullptr, threshold, &part);
+      PartWriter w;
+      w.Put(part);
+      parts[s] = std::move(w.b);
+    }
+    ExchangeParts(&parts);
+    for (int s = 0; s < ns; ++s) {
+      PartReader r{parts[s]};
+      r.Get(&part);
       std::copy(part.begin(), part.end(), flags->begin() + shard_begin_[s]);
     }
     return;
@@ -351,15 +553,25 @@ void DeviceLp::ShardedDualBoxedFlips(const std::vector<int>* cols, double thresh
   }
   flags->assign(cols->size(), 0);
   for (int s = 0; s < ns; ++s) {
-    if (sub[s].empty()) continue;
-    Shard(s).DualBoxedFlips(&sub[s], threshold, &part);
-    for (size_t k = 0; k < part.size(); ++k) (*flags)[where[s][k]] = part[k];
+    if (!IsLocalShard(s)) continue;
+    part.clear();
+    if (!sub[s].empty()) Shard(s).DualBoxedFlips(&sub[s], threshold, &part);
+    PartWriter w;
+    w.Put(part);
+    parts[s] = std::move(w.b);
+  }
+  ExchangeParts(&parts);
+  for (int s = 0; s < ns; ++s) {
+    PartReader r{parts[s]};
+    r.Get(&part);
+    for (size_t k = 0; k < part.size() && k < where[s].size(); ++k) (*flags)[where[s][k]] = part[k];
   }
 }
 
 void DeviceLp::ShardedStats() {
   agg_stats_ = stats_;
   for (auto& d : shards_) {
+    if (!d) continue;  // another process's block
     const mi_lp_kernel_stats& st = d->stats();
     for (int k = 0; k < MI_K_COUNT; ++k) {
       agg_stats_.launches[k] += st.launches[k];

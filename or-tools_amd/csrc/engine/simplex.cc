@@ -5646,6 +5646,23 @@ int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable) {
   return MI_LP_OK;
 }
 
+int mi_lp_set_exchange(mi_lp* h, int32_t rank, int32_t world, void* ctx,
+                       mi_lp_allgather_fn allgather) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  if (h->running) return MI_LP_ERROR_STATE;
+  try {
+    (void)hipSetDevice(h->device);
+    h->simplex.device().SetExchange(rank, world, ctx, allgather);
+  } catch (const milp::DeviceError& e) {
+    h->error = e.what();
+    return MI_LP_ERROR_DEVICE;
+  } catch (const std::exception& e) {
+    h->error = e.what();
+    return MI_LP_ERROR_INTERNAL;
+  }
+  return MI_LP_OK;
+}
+
 int mi_lp_record_iteration_times(mi_lp* h, int32_t enable) {
   if (h == nullptr) return MI_LP_ERROR_NULL;
   if (!SolveIsParked(h)) return MI_LP_ERROR_STATE;

@@ -170,7 +170,7 @@ EXPORTED_SYMBOLS = [
     "mi_mps_name", "mi_mps_col_name", "mi_mps_row_name", "mi_mps_free",
     "mi_lp_solver_params_default", "mi_lp_scale", "mi_lp_solver_solve",
     "mi_lp_clear_integrality_scales", "mi_lp_record_iteration_times",
-    "mi_lp_get_iteration_times", "mi_lp_get_run_counters",
+    "mi_lp_get_iteration_times", "mi_lp_get_run_counters", "mi_lp_set_exchange",
 ]
 
 

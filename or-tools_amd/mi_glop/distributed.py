@@ -77,13 +77,15 @@ def sum_over_ranks(x, dist=None, device=None):
 
 
 # --- single LP split across GPUs -----------------
-# The engine's column shards (DeviceLp MILP_SHARDS, engine/device_shards.hip)
-# join inside one process; across processes the same joins are these
-# collectives, one exchange step per dual iteration:
-#   * all-reduce(min) of the ratio test's Harris bound over the shards,
-#   * an all-gather of each shard's candidate breakpoints (few), concatenated
-#     in rank (= column block) order, the order the host replays them in,
-#   * a broadcast of the entering column a_q from the rank that owns it.
+# One LP over `world` processes: every process loads the same LP and runs the
+# same host control flow; process r keeps column block r of [A | I] on its
+# GPU (DeviceLp::SetExchange, engine/device_shards.hip). Each per-column
+# device operation's results are joined in block order by an all-gather of
+# byte strings: the update row's list, the pricing reduced costs, the dual
+# ratio test's filtered breakpoints (each block filtered under its own
+# bound: the all-reduce(min) of the reference's exchange is implicit in the
+# superset), the entering column's coefficient. The engine calls
+# allgather_bytes through mi_lp_set_exchange.
 
 def column_blocks(col_starts, world):
     """Column blocks of [A | I] per rank, as DeviceLp::ShardedUpload cuts
@@ -110,45 +112,27 @@ def owner_of(col, bounds):
     return bisect.bisect_right(bounds, col) - 1
 
 
-def min_bound(bound, dist=None, device=None):
-    """All-reduce(min) of the per-shard Harris bound (the filter key)."""
-    return share_bound(bound, dist, device)
-
-
-def gather_candidates(cols, coeffs, dist=None, device=None):
-    """All-gather of the per-rank candidate lists (global column ids and
-    their update-row coefficients), concatenated in rank order. Lists are
-    padded to the longest one for the fixed-size collective."""
+def allgather_bytes(data, sizes, dist, group=None):
+    """Every rank's `data` (sizes[r] bytes from rank r, known to all ranks),
+    concatenated in rank order: one all-gather of uint8 tensors padded to the
+    longest message. On a gloo group the tensors stay on the CPU."""
     import torch
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
-        return list(cols), list(coeffs)
-    world = dist.get_world_size()
-    n = torch.tensor([len(cols)], dtype=torch.int64, device=device or "cpu")
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    cap = max(int(s.item()) for s in sizes)
-    c = torch.full((max(cap, 1),), -1, dtype=torch.int64, device=device or "cpu")
-    v = torch.zeros((max(cap, 1),), dtype=torch.float64, device=device or "cpu")
-    if cols:
-        c[:len(cols)] = torch.tensor(list(cols), dtype=torch.int64)
-        v[:len(coeffs)] = torch.tensor(list(coeffs), dtype=torch.float64)
-    cs = [torch.empty_like(c) for _ in range(world)]
-    vs = [torch.empty_like(v) for _ in range(world)]
-    dist.all_gather(cs, c)
-    dist.all_gather(vs, v)
-    out_c, out_v = [], []
-    for r in range(world):
-        k = int(sizes[r].item())
-        out_c += [int(x) for x in cs[r][:k].tolist()]
-        out_v += [float(x) for x in vs[r][:k].tolist()]
-    return out_c, out_v
+    world = len(sizes)
+    cap = max(1, max(sizes))
+    buf = torch.zeros(cap, dtype=torch.uint8)
+    if data:
+        buf[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    outs = [torch.empty(cap, dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(outs, buf, group=group)
+    return b"".join(bytes(outs[r][:sizes[r]].numpy().tobytes()) for r in range(world))
 
 
-def broadcast_column(values, owner, dist=None, device=None):
-    """The entering column a_q (dense, m values) from the rank that owns it."""
-    import torch
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
-        return list(values)
-    t = torch.tensor(list(values), dtype=torch.float64, device=device or "cpu")
-    dist.broadcast(t, src=owner)
-    return [float(x) for x in t.tolist()]
+def attach_column_split(handle, dist, group=None):
+    """Makes `handle` (engine.LpHandle) this rank's block of one LP split over
+    the group (call before handle.load). The exchange runs on `group` (a gloo
+    group: the joined messages are host bytes the engine consumes)."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    handle.set_exchange(rank, world,
+                        lambda data, sizes: allgather_bytes(data, sizes, dist, group))
+    return rank, world

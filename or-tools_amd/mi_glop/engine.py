@@ -21,6 +21,11 @@ class EngineUnavailable(RuntimeError):
     pass
 
 
+# mi_lp_allgather_fn (include/mi_lp.h): ctx, send, send_bytes, recv, recv_bytes.
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64))
+
+
 def build(jobs=8):
     """Compiles the engine for gfx950 (hipcc cross-compiles without a GPU)."""
     subprocess.run(["make", "-s", f"-j{jobs}", "-C", PKG_DIR], check=True)
@@ -75,6 +80,7 @@ def lib():
     L.mi_lp_get_iteration_times.argtypes = [vp, vp, ctypes.c_int64]
     L.mi_lp_get_iteration_times.restype = ctypes.c_int64
     L.mi_lp_get_run_counters.argtypes = [vp, ctypes.POINTER(abi.MiLpRunCounters)]
+    L.mi_lp_set_exchange.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, ALLGATHER_FN]
     L.mi_lp_objective_limit_reached.argtypes = [vp, vp]
     L.mi_lp_get_unit_row_left_inverse.argtypes = [vp, ctypes.c_int32, vp, vp, vp]
     L.mi_lp_compute_dictionary.argtypes = [vp, vp, ctypes.c_int32, vp]
@@ -96,6 +102,25 @@ def device_count():
 
 def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def allgather_callback(world, allgather):
+    """A mi_lp_allgather_fn over a Python `allgather(data, sizes) -> bytes`.
+    Failures return 1 (no exception may cross the C ABI; the engine then
+    raises a DeviceError for the solve)."""
+    def cb(_ctx, send, send_bytes, recv, recv_bytes):
+        try:
+            sizes = [int(recv_bytes[r]) for r in range(world)]
+            data = ctypes.string_at(send, send_bytes) if send_bytes > 0 else b""
+            out = allgather(data, sizes)
+            if len(out) != sum(sizes):
+                return 1
+            if out:
+                ctypes.memmove(recv, out, len(out))
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+    return ALLGATHER_FN(cb)
 
 
 class LpHandle:
@@ -225,6 +250,14 @@ class LpHandle:
         return {name: dict(launches=s.launches[i], bytes=s.algorithmic_bytes[i],
                            device_ms=s.device_ms[i], call_ms=s.call_ms[i])
                 for i, name in enumerate(abi.KERNEL_NAMES)}
+
+    def set_exchange(self, rank, world, allgather):
+        """Cross-process column split (mi_lp_set_exchange): `allgather(data:
+        bytes, sizes: list[int]) -> bytes` returns every rank's bytes in rank
+        order. Call before load()."""
+        self._exchange_cb = allgather_callback(world, allgather)  # kept alive with the handle
+        self._check(self._L.mi_lp_set_exchange(self.h, int(rank), int(world), None,
+                                               self._exchange_cb), "mi_lp_set_exchange")
 
     def record_iteration_times(self, on=True):
         self._check(self._L.mi_lp_record_iteration_times(self.h, int(on)),

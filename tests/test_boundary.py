@@ -234,14 +234,16 @@ def test_iteration_times_and_run_counters():
     g.record_iteration_times(True)
     g.begin(20)
     c0 = g.run_counters()
-    assert c0["factorizations"] >= 1
     assert c0["iterations"] == 20
     ts = g.iteration_times()
     assert len(ts) == 20 and np.all(np.diff(ts) >= 0.0)
     fin, it = g.run_until(150)
     c1 = g.run_counters()
     assert c1["iterations"] == it
+    # The slack basis needs no factorization; 64 updates later one is made.
     assert c1["factorizations"] >= c0["factorizations"]
+    if it > 70:
+        assert c1["factorizations"] >= 1
     assert c1["factorization_seconds"] >= c0["factorization_seconds"]
     g.stop()
     r = g.finish()

@@ -111,62 +111,38 @@ def test_bound_share_world2(tmp_path):
     assert min(float(rows[0][2]), float(rows[1][2])) == best
 
 
-# --- single-LP column split: the exchange step ------
-
-def _split_problem():
-    """A config-5-shaped LP's [A | I] CSC, a rho, reduced costs: the inputs of
-    one dual ratio test (entering_variable.cc:37-130)."""
-    import numpy as np
-    import lp_gen
-    lp = lp_gen.sparse_c5_lp(300, 3000, 6, 123)
-    m, n = lp.m, lp.n
-    starts = np.concatenate([lp.col_starts, lp.col_starts[-1] + 1 + np.arange(m)])
-    rows = np.concatenate([lp.row_idx, np.arange(m)])
-    vals = np.concatenate([lp.vals, np.ones(m)])
-    rng = np.random.default_rng(7)
-    rho = rng.uniform(-1, 1, m) * (rng.random(m) < 0.2)
-    rc = np.abs(rng.normal(size=n + m))
-    return starts, rows, vals, rho, rc
-
-
-def _alpha(starts, rows, vals, rho, b, e):
-    import numpy as np
-    return np.array([float(np.dot(rho[rows[starts[c]:starts[c + 1]]],
-                                  vals[starts[c]:starts[c + 1]])) for c in range(b, e)])
-
-
-def _local_filter(alpha, rc, b, tol=1e-9):
-    """Harris bound of the block (min over its breakpoints of (|rc|+tol)/|alpha|)
-    and its breakpoints, as (column, alpha, ratio)."""
-    import numpy as np
-    nz = np.abs(alpha) > 1e-9
-    ratio = np.where(nz, rc / np.where(nz, np.abs(alpha), 1.0), np.inf)
-    harris = np.where(nz, (rc + tol) / np.where(nz, np.abs(alpha), 1.0), np.inf)
-    return float(harris.min()), [(b + i, float(alpha[i]), float(ratio[i]))
-                                 for i in range(len(alpha)) if nz[i]]
-
+# --- single-LP column split: the engine's exchange ---
 
 def _split_worker(rank, world, port, out_dir):
+    """Drives the engine's exchange callback (mi_lp_allgather_fn, built by
+    engine.allgather_callback over distributed.allgather_bytes) the way
+    DeviceLp::ExchangeParts does: sizes first (8 bytes per rank), then the
+    variable-size block messages, including an empty one."""
+    import ctypes
     sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "or-tools_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from mi_glop import distributed
-    starts, rows, vals, rho, rc = _split_problem()
-    bounds = distributed.column_blocks(starts, world)
-    b, e = bounds[rank], bounds[rank + 1]
-    bound, cands = _local_filter(_alpha(starts, rows, vals, rho, b, e), rc[b:e], b)
-    bound = distributed.min_bound(bound, dist)           # all-reduce(min)
-    keep = [(c, a) for c, a, r in cands if r <= bound * (1.0 + 1e-9)]
-    cols, coeffs = distributed.gather_candidates([c for c, _ in keep], [a for _, a in keep], dist)
-    q = cols[0] if cols else 0
-    owner = distributed.owner_of(q, bounds)
-    col = [0.0] * len(rho)
-    if owner == rank:
-        for k in range(starts[q], starts[q + 1]):
-            col[rows[k]] = float(vals[k])
-    col = distributed.broadcast_column(col, owner, dist)  # a_q from its owner
+    from mi_glop import distributed, engine
+    cb = engine.allgather_callback(world, lambda d, s: distributed.allgather_bytes(d, s, dist))
+    got = []
+    for msg in (b"", bytes(range(7)) * (rank + 1), bytes([rank]) * (1000 * rank)):
+        n = ctypes.c_int64(len(msg))
+        sizes = (ctypes.c_int64 * world)()
+        eight = (ctypes.c_int64 * world)(*([8] * world))
+        assert cb(None, ctypes.byref(n), 8, sizes, eight) == 0
+        total = sum(sizes)
+        recv = ctypes.create_string_buffer(max(1, total))
+        send = ctypes.create_string_buffer(msg, max(1, len(msg)))
+        assert cb(None, send, len(msg), recv, sizes) == 0
+        got.append((list(sizes), recv.raw[:total].hex()))
+    # A failing all-gather reports 1 instead of raising through the C ABI.
+    bad = engine.allgather_callback(world, lambda d, s: b"short")
+    n = ctypes.c_int64(3)
+    sizes = (ctypes.c_int64 * world)(3, 3)
+    recv = ctypes.create_string_buffer(6)
+    got.append(bad(None, ctypes.byref(n), 3, recv, sizes))
     with open(os.path.join(out_dir, f"s{rank}.txt"), "w") as f:
-        f.write(repr((b, e, bound, cols, coeffs, q, col)) + "\n")
+        f.write(repr(got) + "\n")
     dist.destroy_process_group()
 
 
@@ -182,26 +158,20 @@ def test_column_blocks_match_engine_rule():
 
 
 def test_column_split_exchange_world2(tmp_path):
-    """Two ranks each own a column block; after all-reduce(min) of the bound,
-    all-gather of the candidates and broadcast of a_q, every rank holds
-    exactly what the single-process join computes (the virtual-shard join of
-    engine/device_shards.hip, which the GPU tests pin to the oracle)."""
-    from mi_glop import distributed
+    """The byte all-gather the engine's column split calls (gloo, world 2):
+    every rank receives every rank's message in rank order, sizes included,
+    for empty and unequal messages; a broken collective returns an error
+    code. (The engine split itself needs a GPU: tests/test_split_gpu.py runs
+    it across two processes against the unsplit engine and the oracle.)"""
     port = _free_port()
     mp.start_processes(_split_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
                        start_method="spawn")
     import ast
     got = [ast.literal_eval(open(tmp_path / f"s{r}.txt").read()) for r in range(2)]
-    starts, rows, vals, rho, rc = _split_problem()
-    n_total = len(starts) - 1
-    bound, cands = _local_filter(_alpha(starts, rows, vals, rho, 0, n_total), rc, 0)
-    keep = [(c, a) for c, a, r in cands if r <= bound * (1.0 + 1e-9)]
-    assert got[0][1] == got[1][0]  # contiguous blocks
+    msgs = [[b"", bytes(range(7)) * (r + 1), bytes([r]) * (1000 * r)] for r in range(2)]
     for g in got:
-        assert g[2] == bound
-        assert g[3] == [c for c, _ in keep] and g[4] == [a for _, a in keep]
-    q = keep[0][0]
-    ref = [0.0] * len(rho)
-    for k in range(starts[q], starts[q + 1]):
-        ref[rows[k]] = float(vals[k])
-    assert got[0][6] == ref and got[1][6] == ref and got[0][5] == q
+        for k in range(3):
+            sizes, data = g[k]
+            assert sizes == [len(msgs[0][k]), len(msgs[1][k])]
+            assert bytes.fromhex(data) == msgs[0][k] + msgs[1][k]
+        assert g[3] == 1
