@@ -13,10 +13,13 @@ early phase), then W more warm-up iterations, then exactly K iterations are
 timed, bracketed by barrier + device synchronize, with HIP-event kernel
 timing on (events are collected after the window, no per-kernel sync).
 
-Multi-GPU: one process per GPU (torchrun). A single LP does not shard yet
-(DESIGN.md 8), so each rank solves its own replica LP (seed + rank):
-"replicas only", no collective in the data path; value = sum of iterations
-over ranks / max wall time over ranks.
+Multi-GPU: one process per GPU (torchrun). Config 5 is ONE LP split across
+the ranks by column blocks (mi_lp_set_exchange): every rank runs
+the same host control flow on the same LP, owns one block of [A | I] on its
+GPU, and the per-column results are joined through an all-gather every
+iteration; value = the LP's iterations / max wall time over ranks ("scaling":
+"strong"). --c5-replicas runs one independent LP per rank instead (weak
+scaling, no collective in the data path).
 """
 import argparse
 import json
@@ -120,9 +123,14 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     rank). The solve runs untimed to iteration c5_window + warmup; then
     exactly `steps` iterations are timed with the kernel timing on."""
     import lp_gen
-    lp = lp_gen.sparse_c5_lp(args.c5_m, args.c5_n, 10, args.seed + rank)
+    split = world > 1 and not args.c5_replicas
+    lp = lp_gen.sparse_c5_lp(args.c5_m, args.c5_n, 10, args.seed + (0 if split else rank))
     p = abi.default_params(use_dual_simplex=1)
     h = engine.LpHandle(p, device=local_rank)
+    if split:
+        # The exchange runs on a gloo group: the joined messages are host
+        # bytes the engine's host control flow consumes.
+        distributed.attach_column_split(h, dist, dist.new_group(backend="gloo"))
     h.load(lp)
     h.record_iteration_times(True)  # per-iteration timestamps (window statistics)
     t = time.perf_counter()
@@ -144,7 +152,8 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     after = h.run_counters()
     done = it - start
     window = window_stats(h.iteration_times(), start, done, before, after)
-    total_done = distributed.sum_over_ranks(done, dist, "cuda")
+    # Split: every rank ran the same iterations of one LP; replicas: sum.
+    total_done = done if split else distributed.sum_over_ranks(done, dist, "cuda")
     h.stop()
     h.finish()
     del h
@@ -162,6 +171,7 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
         "device_call_ms_per_step": round(sum(v["call_ms"] for v in stats.values())
                                          / max(1, done), 3),
         "window": window,
+        "split": split,
     }
     if rank == 0 and world == 1 and not args.no_cpu and args.c5_cpu_steps > 0:
         import oracle_lib
@@ -331,24 +341,33 @@ def run_c3(args, rank, world, local_rank, dist, barrier, sync):
 
 
 def run_batched(args, rank, world, local_rank, dist, barrier, sync):
-    """Config 4: children of one CP-SAT-style search node,
-    sharded across ranks (each rank its own children, weak scaling), solved
-    by `workers` GPU handles per rank with the dual simplex warm-started from
-    the root basis. The only collective: all-reduce(min) of the best child
-    bound (RCCL), the cross-GPU analogue of
-    SharedResponseManager::UpdateInnerObjectiveBounds."""
+    """Config 4: one CP-SAT search node's branching LPs
+    (mi_glop.cpsat: BranchOnVar, linear_programming_constraint.cc:485-584).
+    The node LP is solved, its fractional order variables (most fractional
+    first) each give a down branch (y <= floor) and an up branch (y >= ceil),
+    all warm-started from the node's basis state (SolveLpForBranching,
+    :443-464). The variables are sharded across ranks (both branches of a
+    variable on one rank, weak scaling: each rank batch_lps LPs), solved by
+    `workers` GPU handles per rank, and folded with BranchOnVar's decisions.
+    The only collective: all-reduce(max) of the node's objective lower bound
+    (each variable's min over its branches is a valid bound), the cross-GPU
+    analogue of SharedResponseManager::UpdateInnerObjectiveBounds."""
+    import math
     import jobshop
+    from mi_glop import cpsat
     jobs = jobshop.random_instance(args.batch_jobs, args.batch_machines, args.seed)
     lp, ycols = jobshop.relaxation(jobs)
     root = engine.LpHandle(abi.default_params(use_dual_simplex=1), device=local_rank)
     root.load(lp)
     root_res = root.solve()
     state = root.state()
-    # The node's children, sharded across ranks (each rank: batch_lps of them).
-    all_lbs, all_ubs = jobshop.child_bounds(lp, ycols, args.batch_lps * world, args.seed + 1000)
-    b, e = distributed.shard(args.batch_lps * world, rank, world)
-    lbs, ubs = all_lbs[b:e], all_ubs[b:e]
-    del all_lbs, all_ubs
+    x = root.primal()
+    node = cpsat.IntegerTrail(lp.col_lb, lp.col_ub,
+                              obj_lb=math.ceil(root_res.objective - cpsat.K_CP_EPSILON))
+    cols_all = cpsat.fractional_columns(x, ycols, limit=(args.batch_lps // 2) * world)
+    b, e = distributed.shard(len(cols_all), rank, world)
+    cols = cols_all[b:e]
+    lbs, ubs = cpsat.branch_lps(node, x, cols)
     p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
     workers = [engine.LpHandle(p, device=local_rank) for _ in range(args.batch_workers)]
     for w in workers:
@@ -359,21 +378,25 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     sync()
     t0 = time.perf_counter()
     res = engine.batch_solve_bounds(workers, lbs, ubs, state)
-    best = distributed.share_bound(distributed.best_bound(res, abi.OPTIMAL), dist, "cuda")
+    summary = cpsat.fold_node(cpsat.IntegerTrail(node.lb, node.ub, node.obj_lb), x, cols, res)
+    node_lb = -distributed.share_bound(-summary["obj_lb"], dist, "cuda")  # all-reduce(max)
     sync()
     barrier()
     elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
-    total = args.batch_lps * world
+    total = distributed.sum_over_ranks(len(lbs), dist, "cuda")
     out = {
         "metric": "batched LPs/sec", "value": total / elapsed, "unit": "LPs/s",
-        "lps": total, "seconds": elapsed, "workers_per_gpu": args.batch_workers,
+        "lps": int(total), "seconds": elapsed, "workers_per_gpu": args.batch_workers,
         "host_threads_per_gpu": min(args.batch_workers, 16),
-        "mean_iterations": float(np.mean([r.iterations for r in res])),
-        "best_bound": best, "root_iterations": int(root_res.iterations),
-        "workload": (f"config 4: job-shop {args.batch_jobs}x{args.batch_machines} "
-                     f"(seeded, ta041-shaped family) big-M LP relaxation, m={lp.m} n={lp.n}; "
-                     f"{args.batch_lps} children/GPU with two order variables fixed, dual "
-                     f"simplex warm-started from the root basis, cap 1000 iterations"),
+        "mean_iterations": float(np.mean([r.iterations for r in res])) if res else 0.0,
+        "root_objective": float(root_res.objective), "root_iterations": int(root_res.iterations),
+        "node_obj_lb": node_lb, "deductions": int(summary["deductions"]),
+        "speculative_lps": int(summary["speculative"]),
+        "workload": (f"config 4: job-shop {args.batch_jobs}x{args.batch_machines} (seeded, "
+                     f"ta041-shaped family) big-M LP relaxation, m={lp.m} n={lp.n}; one search "
+                     f"node's BranchOnVar LPs: {len(cols_all)} fractional order variables x 2 "
+                     f"branches, dual simplex warm-started from the node basis, cap 1000 "
+                     f"iterations"),
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_lib
@@ -386,7 +409,8 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = {
             "value": n_cpu / dt, "unit": "LPs/s", "cores": args.batch_cpu_threads, "kind": "port",
-            "sample": f"oracle, {args.batch_cpu_threads} threads, first {n_cpu} of the same children"}
+            "sample": f"oracle, {args.batch_cpu_threads} threads, the first {n_cpu} of the same "
+                      f"branch LPs"}
     return out
 
 
@@ -404,6 +428,8 @@ def main():
     ap.add_argument("--c5-window", type=int, default=20000,
                     help="config-5 iteration where the timed window starts")
     ap.add_argument("--c5-cpu-steps", type=int, default=300)
+    ap.add_argument("--c5-replicas", action="store_true",
+                    help="N > 1: one independent config-5 LP per rank instead of one split LP")
     ap.add_argument("--c5-traffic-json",
                     default=os.path.join(REPO, "profiles", "traffic_c5.json"),
                     help="per-launch HBM bytes of the config-5 kernels (profiles/)")
@@ -421,7 +447,7 @@ def main():
                     help="per-launch HBM bytes of the config-2 dominant kernel from a "
                          "separate rocprofv3 --pmc pass (profiles/)")
     ap.add_argument("--batch-lps", type=int, default=512,
-                    help="config-4 children per GPU (0 disables the batched section)")
+                    help="config-4 branch LPs per GPU (0 disables the batched section)")
     ap.add_argument("--batch-workers", type=int, default=128,
                     help="config-4 solver handles per GPU (LPs in flight); the engine runs "
                          "them on at most 16 host threads as fibers with batched launches")
@@ -484,7 +510,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": c5["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if c5["split"] else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded sparse LP, BASELINE.json config 5 generator, tests/lp_gen.py)",
@@ -496,7 +522,7 @@ def main():
             "timed_iterations": c5["timed_iterations"],
             "finished_early": c5["finished_early"],
             "setup_and_warmup_s": c5["setup_and_warmup_s"],
-            "parallelism": f"replicas{world}",
+            "parallelism": f"column_split{world}" if c5["split"] else f"replicas{world}",
         },
         "roofline": c5["roofline"],
         "kernels": c5["kernels"],
