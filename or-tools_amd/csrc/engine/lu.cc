@@ -123,16 +123,24 @@ struct MatrixEntry {
 void Markowitz::ExtractSingletonColumns(const CompactSparseMatrixView& b,
                                         std::vector<int>* row_perm,
                                         std::vector<int>* col_perm, int* index) {
-  std::vector<MatrixEntry> singleton_entries;
+  std::vector<MatrixEntry> collected;
   const int num_cols = b.num_cols();
+  const int num_rows = b.num_rows();
   for (int col = 0; col < num_cols; ++col) {
     const ColumnView c = b.column(col);
     if (c.n == 1) {
-      singleton_entries.push_back(
-          MatrixEntry{c.GetFirstRow(), col, c.GetFirstCoefficient()});
+      collected.push_back(MatrixEntry{c.GetFirstRow(), col, c.GetFirstCoefficient()});
     }
   }
-  std::sort(singleton_entries.begin(), singleton_entries.end());
+  // markowitz.cc sorts the entries by (row, col). The keys are distinct and
+  // the entries were collected by increasing column, so a stable counting
+  // sort by row gives that order in O(entries) instead of O(e log e) (a
+  // third of a config-5 refactorization).
+  std::vector<int> row_start(num_rows + 1, 0);
+  for (const MatrixEntry& e : collected) ++row_start[e.row + 1];
+  for (int r = 0; r < num_rows; ++r) row_start[r + 1] += row_start[r];
+  std::vector<MatrixEntry> singleton_entries(collected.size());
+  for (const MatrixEntry& e : collected) singleton_entries[row_start[e.row]++] = e;
   for (const MatrixEntry e : singleton_entries) {
     if ((*row_perm)[e.row] == kInvalidRow) {
       (*col_perm)[e.col] = *index;
