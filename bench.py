@@ -36,6 +36,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 from mi_glop import abi, distributed, engine  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+COLL_DEVICE = "cuda"  # RCCL collectives on device tensors ("cpu" under gloo)
 METRIC = "simplex iterations/sec + batched LPs/sec, 1/2/4/8 MI355X vs Glop CPU"
 
 
@@ -101,6 +102,8 @@ def window_stats(ts, start, done, before, after):
     timestamps) and the LU refactorizations that fell inside it, so that a
     short window is interpretable (a refactorization costs many iterations)."""
     out = {"refactorizations_in_window": after["factorizations"] - before["factorizations"],
+           "u_schedule_levels": after.get("u_levels", 0),
+           "u_schedule_outputs": after.get("u_outputs", 0),
            "refactorization_ms_in_window": round(
                1000.0 * (after["factorization_seconds"] - before["factorization_seconds"]), 3)}
     if done > 0 and len(ts) >= start + done and start > 0:
@@ -147,13 +150,21 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     fin, it = h.run_until(start + args.steps)
     sync()
     barrier()
-    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, COLL_DEVICE)
     stats = h.kernel_stats()
     after = h.run_counters()
     done = it - start
     window = window_stats(h.iteration_times(), start, done, before, after)
+    roof = kernel_roofline(stats, args.c5_traffic_json)
+    if roof["kernel"] in ("tri_solve", "tri_solve_tau") and after.get("u_levels", 0) > 0:
+        # The U solve is a dependency chain: each level is a hand-off between
+        # workgroups (MI355X_MICROARCH.md handoff-1to1: ~1 us idle, 2.5-5 us
+        # with the waves of a loaded CU). Time per level of the schedule in use.
+        roof["latency"] = {"levels": after["u_levels"],
+                           "us_per_level": 1000.0 * roof["ms_per_launch"] / after["u_levels"],
+                           "handoff_us_idle": 1.0}
     # Split: every rank ran the same iterations of one LP; replicas: sum.
-    total_done = done if split else distributed.sum_over_ranks(done, dist, "cuda")
+    total_done = done if split else distributed.sum_over_ranks(done, dist, COLL_DEVICE)
     h.stop()
     h.finish()
     del h
@@ -164,7 +175,7 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
         "timed_iterations": [start, start + done],
         "finished_early": bool(fin), "setup_and_warmup_s": round(setup, 2),
         "nnz": int(lp.nnz),
-        "roofline": kernel_roofline(stats, args.c5_traffic_json),
+        "roofline": roof,
         "kernels": kernel_table(stats),
         "host_ms_per_step": round((1000.0 * elapsed - sum(v["call_ms"] for v in stats.values()))
                                   / max(1, done), 3),
@@ -220,11 +231,11 @@ def run_c2(args, rank, world, local_rank, dist, barrier, sync):
     finished, it = h.run_until(args.c2_warmup + args.c2_steps)
     sync()
     barrier()
-    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, COLL_DEVICE)
     stats = h.kernel_stats()
     done = it - args.c2_warmup
     window = window_stats(h.iteration_times(), args.c2_warmup, done, before, h.run_counters())
-    total_done = distributed.sum_over_ranks(done, dist, "cuda")
+    total_done = distributed.sum_over_ranks(done, dist, COLL_DEVICE)
     # A late window of the same length: the host LU solves grow as dense
     # columns enter the basis, so the early rate overstates the solve.
     late = None
@@ -238,9 +249,9 @@ def run_c2(args, rank, world, local_rank, dist, barrier, sync):
             t0l = time.perf_counter()
             fin_l, it_l2 = h.run_until(it_l + args.c2_steps)
             sync()
-            el = distributed.max_over_ranks(time.perf_counter() - t0l, dist, "cuda")
+            el = distributed.max_over_ranks(time.perf_counter() - t0l, dist, COLL_DEVICE)
             late = {"timed_iterations": [it_l, it_l2], "reached_in_s": round(reach_s, 2),
-                    "value": distributed.sum_over_ranks(it_l2 - it_l, dist, "cuda") / el
+                    "value": distributed.sum_over_ranks(it_l2 - it_l, dist, COLL_DEVICE) / el
                     if el > 0 else 0.0,
                     "ms_per_step": 1000.0 * el / max(1, it_l2 - it_l),
                     "window": window_stats(h.iteration_times(), it_l, it_l2 - it_l, before_l,
@@ -305,7 +316,7 @@ def run_c3(args, rank, world, local_rank, dist, barrier, sync):
     res = engine.batch_solve(handles, num_threads=args.c3_workers)
     sync()
     barrier()
-    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, COLL_DEVICE)
     statuses = [r.problem_status for r in res]
     out = {
         "metric": "batched LPs/sec", "unit": "LPs/s", "scaling": "strong",
@@ -379,11 +390,11 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     t0 = time.perf_counter()
     res = engine.batch_solve_bounds(workers, lbs, ubs, state)
     summary = cpsat.fold_node(cpsat.IntegerTrail(node.lb, node.ub, node.obj_lb), x, cols, res)
-    node_lb = -distributed.share_bound(-summary["obj_lb"], dist, "cuda")  # all-reduce(max)
+    node_lb = -distributed.share_bound(-summary["obj_lb"], dist, COLL_DEVICE)  # all-reduce(max)
     sync()
     barrier()
-    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, "cuda")
-    total = distributed.sum_over_ranks(len(lbs), dist, "cuda")
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, COLL_DEVICE)
+    total = distributed.sum_over_ranks(len(lbs), dist, COLL_DEVICE)
     out = {
         "metric": "batched LPs/sec", "value": total / elapsed, "unit": "LPs/s",
         "lps": int(total), "seconds": elapsed, "workers_per_gpu": args.batch_workers,
@@ -464,12 +475,21 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the multi-rank path on a one-GPU box: every rank on GPU 0.
+    one_gpu = os.environ.get("MILP_BENCH_ONE_GPU") == "1"
+    if one_gpu:
+        local_rank = 0
     dist = None
     if world > 1:
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if one_gpu:  # RCCL refuses two ranks on one GPU: gloo for the rehearsal
+            global COLL_DEVICE
+            COLL_DEVICE = "cpu"
+            tdist.init_process_group("gloo")
+        else:
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         dist = tdist
 
     def barrier():

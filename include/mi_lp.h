@@ -292,6 +292,12 @@ typedef struct mi_lp_run_counters {
   int64_t factorizations;       /* LU factorizations computed so far */
   double factorization_seconds; /* host wall time spent in them */
   int64_t iterations;           /* RevisedSimplex::GetNumberOfIterations */
+  /* The device schedule of the current factorization's U (FTRAN's dense U
+   * solve, 0 when none was built): dependency levels, computed outputs,
+   * gather entries. A level is a dependency hop of the solve. */
+  int64_t u_levels;
+  int64_t u_outputs;
+  int64_t u_entries;
 } mi_lp_run_counters;
 int mi_lp_record_iteration_times(mi_lp* h, int32_t enable);
 int64_t mi_lp_get_iteration_times(const mi_lp* h, double* out, int64_t cap);
@@ -326,12 +332,20 @@ int mi_lp_set_exchange(mi_lp* h, int32_t rank, int32_t world, void* ctx,
  * error code) is in results[i]. No exception crosses this boundary. */
 int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
                       mi_lp_result* results);
+/* mi_lp_batch_solve over several GPUs of one process (SURVEY 8(b)
+ * mi_lp_batch_solve(hs, count, num_gpus, ...)): every handle's device must be
+ * in [0, num_gpus); each device's handles run on a pool of threads_per_gpu
+ * threads of their own, all devices at once. */
+int mi_lp_batch_solve_gpus(mi_lp* const* handles, int32_t count, int32_t num_gpus,
+                           int32_t threads_per_gpu, mi_lp_result* results);
 /* Batched children of one search node: count LPs that share
  * the workers' loaded matrix and differ in variable bounds (lbs/ubs are
  * count x n, row-major), each warm-started from warm_state (n+m statuses,
  * may be NULL, else warm_len must be n+m) like LoadStateForNextSolve. The
- * workers run on at most 16 host threads (MILP_BATCH_THREADS), a thread's
- * workers as fibers with batched small-LP launches (as mi_lp_batch_solve). A child whose bounds or state cannot be loaded is
+ * workers may be on several GPUs; they run on at most 16 host threads
+ * (MILP_BATCH_THREADS), dealt device by device, a thread's workers as fibers
+ * with batched small-LP launches (as mi_lp_batch_solve), every worker pulling
+ * the next child from one shared counter. A child whose bounds or state cannot be loaded is
  * not solved: results[i] = {ABNORMAL, that error code}. */
 int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t count,
                              const double* lbs, const double* ubs, const int8_t* warm_state,

@@ -167,6 +167,8 @@ class DeviceLp : public DeviceSolver {
                   std::vector<double>* x) override;
   bool Solve(TriKind kind, const TriangularMatrix& t, uint64_t key, int start,
              std::vector<double>* x) override;
+  bool SolvePair(TriKind kind, const TriangularMatrix& t, uint64_t key, std::vector<double>* x0,
+                 std::vector<double>* x1) override;
 
   // Accounting (roofline): launches, algorithmic bytes, HIP-event time.
   void SetTiming(bool on);
@@ -174,6 +176,13 @@ class DeviceLp : public DeviceSolver {
   void ResetStats();
   void Synchronize();
   int dense_columns() const { return nd_; }
+  // The U schedule in use (levels, listed outputs, entries; zeros if none).
+  void TriScheduleShape(int64_t* levels, int64_t* outputs, int64_t* entries) const {
+    const TriSchedule& s = tri_sched_[kTriU];
+    *levels = s.ok ? s.levels : 0;
+    *outputs = s.ok && !s.rows_upto.empty() ? s.rows_upto.back() : 0;
+    *entries = s.ok && !s.entries_upto.empty() ? s.entries_upto.back() : 0;
+  }
 
   // --- column shards ----------------------------------------
   // MILP_SHARDS=S > 1 splits the columns of [A | I] into S contiguous blocks
@@ -288,6 +297,8 @@ class DeviceLp : public DeviceSolver {
                         const int64_t* st, const int32_t* idx, const double* val, bool reverse,
                         bool descending, bool sequential, uint64_t key, void* stream);
   bool TriSolve(int which, const TriangularMatrix& t, uint64_t key, std::vector<double>* x);
+  bool TriPrepare(int which, const TriangularMatrix& t, uint64_t key, int slot,
+                  const std::vector<double>& x);
   // Gather lists of a scatter loop: output r lists (column j, t[r, j]) for
   // the columns j >= fni holding row r, by ascending j (or descending).
   void TransposeColumns(const TriangularMatrix& t, bool descending);
@@ -513,12 +524,14 @@ class DeviceLp : public DeviceSolver {
   void SetStreamPriority(bool high);
   bool tri_lower_ = true;     // MILP_TRI_LOWER: the L solves too
   bool tri_btran_ = true;     // MILP_TRI_BTRAN: the other dense loops (BTRAN, UpperSolve) too
+  bool tri_pair_ = true;      // MILP_TRI_PAIR: direction and tau U solves in one launch
   int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
   uint64_t* d_tri_clock_ = nullptr;
   TriSchedule tri_sched_[kTriNumMatrices];
   // Per solving thread: 0 = the solver's thread (the handle's stream),
-  // 1 = BasisFactorization's tau worker (its own stream).
-  TriContext tri_ctx_[2];
+  // 1 = BasisFactorization's tau worker (its own stream), 2 = the second
+  // vector of a pair solve (the solver's stream).
+  TriContext tri_ctx_[3];
   std::mutex tri_mu_;  // schedule (re)builds and graph captures
   void* h_tri_stage_ = nullptr;  // pinned staging of the schedule upload
   size_t tri_stage_bytes_ = 0;

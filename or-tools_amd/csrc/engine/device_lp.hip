@@ -158,6 +158,7 @@ void DeviceLp::Init(int device) {
   if (const char* v = std::getenv("MILP_TRI_SYNCFREE")) tri_syncfree_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_LOWER")) tri_lower_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_BTRAN")) tri_btran_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_TRI_PAIR")) tri_pair_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_MIN_WIDTH")) tri_min_width_ = std::atoi(v);
   if (const char* v = std::getenv("MILP_TRI_SYNCFREE_MIN_LEVELS")) {
     tri_syncfree_min_levels_ = std::atoi(v);

@@ -70,7 +70,7 @@ void DeviceLp::FreeTriBuffers() {
   }
   if (d_tri_clock_ != nullptr) (void)hipFree(d_tri_clock_);
   d_tri_clock_ = nullptr;
-  for (int slot = 0; slot < 2; ++slot) {
+  for (int slot = 0; slot < 3; ++slot) {
     TriContext& c = tri_ctx_[slot];
     for (void* g : c.graph_exec) {
       if (g != nullptr) (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(g));
@@ -304,7 +304,7 @@ void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, cons
 void DeviceLp::PrepareTriContext(int slot, int rows, int pos) {
   TriContext& c = tri_ctx_[slot];
   if (c.stream == nullptr) {
-    if (slot == 0) {
+    if (slot != 1) {  // the solver's thread: its own vector (0) or a pair's second (2)
       c.stream = stream_;
     } else {
       hipStream_t st;
@@ -371,6 +371,11 @@ milp_kernels::TriSolveArgs DeviceLp::TriArgs(const TriSchedule& s, const TriCont
   a.fuse_level0 = tri_fuse0_ ? 1 : 0;
   a.poll_max = tri_poll_max_;
   a.clock = nullptr;
+  a.x2 = nullptr;
+  a.y2 = nullptr;
+  a.host_x2 = nullptr;
+  a.top2 = nullptr;
+  a.fail2 = nullptr;
   return a;
 }
 
@@ -490,8 +495,10 @@ void DeviceLp::TransposeColumns(const TriangularMatrix& t, bool descending) {
   }
 }
 
-bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
-                        std::vector<double>* x) {
+// The schedule of `which` for this factorization and the solving context
+// (built and sized on first use). False: the solve should run on the host.
+bool DeviceLp::TriPrepare(int which, const TriangularMatrix& t, uint64_t key, int slot,
+                          const std::vector<double>& x) {
   if (tri_mode_ == 2) return false;
   const int nc = t.num_cols();
   if (tri_mode_ == 0 && nc < tri_min_rows_) return false;
@@ -500,20 +507,9 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
   // latency (ta041-shaped batch of 64, 16 in flight: 15.7 LPs/s with the
   // device solves, 37.7 with the host's).
   if (tri_mode_ == 0 && small_batch_ && medium_) return false;
-  if (static_cast<int>(x->size()) < nc) return false;
-  // The solver's thread (slot 0) or the factorization's tau worker (slot 1).
-  const int slot = g_lu_slot == 0 ? 0 : 1;
-  if (slot != 0 && !tri_tau_) return false;
+  if (static_cast<int>(x.size()) < nc) return false;
   const TriKind kind = static_cast<TriKind>(which);
-  const int id = slot != 0                       ? MI_K_TRI_SOLVE_TAU
-                 : kind == TriKind::kUpperT      ? MI_K_TRI_SOLVE
-                 : kind == TriKind::kLower       ? MI_K_TRI_SOLVE_L
-                 : kind == TriKind::kUpper       ? MI_K_TRI_SOLVE_UPPER
-                                                 : MI_K_TRI_SOLVE_T;
-  SolveCallTimer timer(&stats_, id);
-  DeviceOp(which == kTriU ? (slot == 0 ? "tri U enter" : "tri U enter (slot 1)")
-                          : (slot == 0 ? "tri L enter" : "tri L enter (slot 1)"));
-  if (slot != 0) Check(hipSetDevice(device_), "hipSetDevice");
+  if (slot == 1) Check(hipSetDevice(device_), "hipSetDevice");
   TriContext& c = tri_ctx_[slot];
   TriSchedule& s = tri_sched_[which];
   {
@@ -575,6 +571,27 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
     if (tri_mode_ == 0 && s.work < int64_t(s.levels) * tri_min_width_) return false;
     PrepareTriContext(slot, nc, s.pos);
   }
+  return true;
+}
+
+bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
+                        std::vector<double>* x) {
+  // The solver's thread (slot 0) or the factorization's tau worker (slot 1).
+  const int slot = g_lu_slot == 0 ? 0 : 1;
+  if (slot != 0 && !tri_tau_) return false;
+  const TriKind kind = static_cast<TriKind>(which);
+  const int id = slot != 0                       ? MI_K_TRI_SOLVE_TAU
+                 : kind == TriKind::kUpperT      ? MI_K_TRI_SOLVE
+                 : kind == TriKind::kLower       ? MI_K_TRI_SOLVE_L
+                 : kind == TriKind::kUpper       ? MI_K_TRI_SOLVE_UPPER
+                                                 : MI_K_TRI_SOLVE_T;
+  SolveCallTimer timer(&stats_, id);
+  DeviceOp(which == kTriU ? (slot == 0 ? "tri U enter" : "tri U enter (slot 1)")
+                          : (slot == 0 ? "tri L enter" : "tri L enter (slot 1)"));
+  if (!TriPrepare(which, t, key, slot, *x)) return false;
+  const int nc = t.num_cols();
+  TriContext& c = tri_ctx_[slot];
+  TriSchedule& s = tri_sched_[which];
   double* xv = x->data();
   const int fni = s.first_col;
   // U (sparse.cc:908-912): the host loop starts at the last non-zero; the
@@ -685,6 +702,82 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
   }
   ft.Lap(kFtDevCopyOut);
   CopyHost(xv + fni, c.h_x + fni, size_t(top - fni + 1) * sizeof(double));
+  return true;
+}
+
+// Two right-hand sides of the FTRAN's U solve in one launch (the direction
+// and the dual steepest-edge tau, dual_edge_norms.cc:134-141, both against
+// the same factorization): blockIdx.y picks the vector, each has its own
+// rows, positions, staging and top row, the schedule is shared. Each vector's
+// outputs are computed exactly as a single solve computes them.
+bool DeviceLp::SolvePair(TriKind kind, const TriangularMatrix& t, uint64_t key,
+                         std::vector<double>* x0, std::vector<double>* x1) {
+  if (kind != TriKind::kUpperT || !tri_pair_ || g_lu_slot != 0) return false;
+  if (!tri_syncfree_ || !tri_mapped_ || tri_graph_ || tri_persist_groups_ > 0) return false;
+  if (tri_debug_left_ > 0) return false;
+  SolveCallTimer timer(&stats_, MI_K_TRI_SOLVE);
+  DeviceOp("tri U pair enter");
+  if (!TriPrepare(kTriU, t, key, 0, *x0)) return false;
+  if (static_cast<int>(x1->size()) < t.num_cols()) return false;
+  TriSchedule& s = tri_sched_[kTriU];
+  // Both vectors' workgroups resident at once: 2 x 512 workgroups of 256
+  // at most, 4 per CU of the 8 the kernel's registers allow.
+  if (s.work > milp_kernels::kTriSyncFreeMaxWork || s.levels < tri_syncfree_min_levels_) {
+    return false;
+  }
+  const int nc = t.num_cols();
+  const int fni = s.first_col;
+  {
+    std::lock_guard<std::mutex> lock(tri_mu_);
+    PrepareTriContext(2, nc, s.pos);
+  }
+  TriContext& c0 = tri_ctx_[0];
+  TriContext& c1 = tri_ctx_[2];
+  std::vector<double>* xs[2] = {x0, x1};
+  TriContext* cs[2] = {&c0, &c1};
+  int tops[2];
+  double bytes = 0.0;
+  for (int v = 0; v < 2; ++v) {
+    const double* xv = xs[v]->data();
+    int top = nc - 1;
+    while (top >= fni && xv[top] == 0.0) --top;
+    // A vector with nothing to compute (only the identity part) is solved
+    // alone by the caller's single path.
+    if (top < fni || s.rows_upto[top + 1] - s.rows_upto[fni] == 0) return false;
+    tops[v] = top;
+    const double rows = s.rows_upto[top + 1] - s.rows_upto[fni];
+    const double entries = static_cast<double>(s.entries_upto[top + 1] - s.entries_upto[fni]);
+    bytes += rows * (24.0 + (s.ones ? 0.0 : 8.0)) + entries * 20.0 + double(s.pos) * 20.0 +
+             rows * 20.0;
+  }
+  const size_t in = size_t(nc - fni);
+  for (int v = 0; v < 2; ++v) {
+    TriContext& c = *cs[v];
+    CopyHost(c.h_x + fni, xs[v]->data() + fni, in * sizeof(double));
+    int* words = reinterpret_cast<int*>(c.h_x + nc);
+    words[0] = tops[v];
+    words[1] = 0;
+  }
+  milp_kernels::TriSolveArgs a = TriArgs(s, c0);
+  a.x2 = static_cast<double*>(c1.x.ptr);
+  a.y2 = static_cast<double*>(c1.y.ptr);
+  a.host_x2 = c1.m_x;
+  a.top2 = static_cast<int*>(c1.top.ptr);
+  a.fail2 = reinterpret_cast<int*>(c1.m_x + s.rows) + 1;
+  BeginKernel(MI_K_TRI_SOLVE);
+  Check(milp_launch::tri_transpose_lower_syncfree(a, Stream(c0.stream), 2), "tri pair");
+  EndKernel(MI_K_TRI_SOLVE, bytes);
+  DeviceOp("tri pair sync");
+  Check(hipStreamSynchronize(Stream(c0.stream)), "sync");
+  for (int v = 0; v < 2; ++v) {
+    const int* words = reinterpret_cast<const int*>(cs[v]->h_x + nc);
+    if (*static_cast<const volatile int*>(words + 1) != 0) {
+      throw DeviceError("triangular solve: dependency wait timed out");
+    }
+  }
+  for (int v = 0; v < 2; ++v) {
+    CopyHost(xs[v]->data() + fni, cs[v]->h_x + fni, size_t(tops[v] - fni + 1) * sizeof(double));
+  }
   return true;
 }
 

@@ -35,6 +35,13 @@ class DeviceSolver {
   // host (MILP_DEVICE_SOLVE and the size threshold decide).
   virtual bool Solve(TriKind kind, const TriangularMatrix& t, uint64_t key, int start,
                      std::vector<double>* x) = 0;
+  // Two right-hand sides of the same dense loop in one device launch (each
+  // vector's bits as its own Solve); false: solve them one by one.
+  virtual bool SolvePair(TriKind kind, const TriangularMatrix& t, uint64_t key,
+                         std::vector<double>* x0, std::vector<double>* x1) {
+    (void)kind, (void)t, (void)key, (void)x0, (void)x1;
+    return false;
+  }
   // x <- the result of t.TransposeLowerSolve(x), bit for bit. `key`
   // identifies the matrix (its LU and the factorization that built it): the
   // device copy and its dependency schedule are rebuilt when it changes.

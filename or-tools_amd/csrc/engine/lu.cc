@@ -682,11 +682,35 @@ void LuFactorization::LeftSolveUWithNonZeros(ScatteredVector* y) const {
   }
 }
 
+void LuFactorization::RightSolveUWithNonZerosPair(ScatteredVector* x,
+                                                  ScatteredVector* tau) const {
+  if (is_identity_factorization_) return;
+  upper_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
+  x->non_zeros_are_sorted = true;
+  {
+    LuSlotGuard slot(1);
+    upper_.ComputeRowsToConsiderInSortedOrder(&tau->non_zeros);
+    tau->non_zeros_are_sorted = true;
+  }
+  if (x->non_zeros.empty() && tau->non_zeros.empty() && device_solver_ != nullptr &&
+      device_solver_->SolvePair(TriKind::kUpperT, transpose_upper_, factorization_key_,
+                                &x->values, &tau->values)) {
+    return;
+  }
+  RightSolveUAfterRows(x);
+  LuSlotGuard slot(1);
+  RightSolveUAfterRows(tau);
+}
+
 // lu_factorization.cc:314-331
 void LuFactorization::RightSolveUWithNonZeros(ScatteredVector* x) const {
   if (is_identity_factorization_) return;
   upper_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
   x->non_zeros_are_sorted = true;
+  RightSolveUAfterRows(x);
+}
+
+void LuFactorization::RightSolveUAfterRows(ScatteredVector* x) const {
   if (x->non_zeros.empty()) {
     // The dense U solve: on the device (the solver's thread and the tau
     // worker each with its own stream), same result bits.
@@ -934,6 +958,7 @@ BasisFactorization::BasisFactorization(const CompactSparseMatrix* matrix,
     if (std::strcmp(e, "force") == 0) async_min_rows_ = 0;
   }
   if (const char* e = std::getenv("MILP_INLINE_TAU")) inline_tau_ = std::strcmp(e, "off") != 0;
+  if (const char* e = std::getenv("MILP_TRI_PAIR")) fuse_tau_ = std::atoi(e) != 0;
 }
 
 BasisFactorization::~BasisFactorization() {
@@ -956,7 +981,11 @@ uint64_t BasisFactorization::StartAsync(AsyncKind kind, std::function<void()> jo
 
 bool BasisFactorization::TakeAsync(uint64_t ticket) const {
   if (async_kind_ == AsyncKind::kNone || ticket != async_ticket_) return false;
-  if (async_) async_->Wait();
+  if (async_kind_ == AsyncKind::kTauDeferred) {
+    FinishDeferredTauU();
+  } else if (async_) {
+    async_->Wait();
+  }
   async_kind_ = AsyncKind::kNone;
   async_input_ = nullptr;
   // The worker's deterministic-time bumps land now, where the serial solve
@@ -969,7 +998,8 @@ bool BasisFactorization::TakeAsync(uint64_t ticket) const {
 
 void BasisFactorization::DropAsync() const {
   if (async_kind_ == AsyncKind::kNone) return;
-  if (async_) async_->Wait();
+  tau_u_pending_ = false;
+  if (async_ && async_kind_ != AsyncKind::kTauDeferred) async_->Wait();
   async_kind_ = AsyncKind::kNone;
   async_input_ = nullptr;
   rank_one_factorization_.TakeDeferredBumps(false);
@@ -977,7 +1007,9 @@ void BasisFactorization::DropAsync() const {
 }
 
 void BasisFactorization::WaitAsync() const {
-  if (async_kind_ != AsyncKind::kNone && async_) async_->Wait();
+  if (async_kind_ != AsyncKind::kNone && async_kind_ != AsyncKind::kTauDeferred && async_) {
+    async_->Wait();
+  }
 }
 
 // The body of RightSolveForTau (basis_representation.cc:374-398) into *out,
@@ -995,8 +1027,43 @@ void BasisFactorization::ComputeTauInto(bool can_be_optimized, const ScatteredVe
   BumpDeterministicTimeForSolve(static_cast<int64_t>(out->NumNonZerosEstimate()));
 }
 
+bool BasisFactorization::TauFusionEnabled() const {
+  return fuse_tau_ && AsyncEnabled() && lu_factorization_.HasDeviceSolver();
+}
+
+// tau's U solve, alone, on slot 1 (the pending half of a deferred tau), with
+// the bump ComputeTauInto makes after it (deferred like the others).
+void BasisFactorization::FinishDeferredTauU() const {
+  if (!tau_u_pending_) return;
+  LuSlotGuard slot(1);
+  lu_factorization_.RightSolveUWithNonZeros(&async_tau_);
+  BumpDeterministicTimeForSolve(static_cast<int64_t>(async_tau_.NumNonZerosEstimate()));
+  tau_u_pending_ = false;
+}
+
 void BasisFactorization::StartAsyncTau(const ScatteredVector& rho) const {
   DropAsync();
+  if (TauFusionEnabled()) {
+    // tau = B^-1 rho (dual_edge_norms.cc:134-141) against the factorization
+    // the direction is solved with next: L and the etas now (slot 1, bumps
+    // deferred), the U solve together with the direction's
+    // (RightSolveForProblemColumn), taken in RightSolveForTau.
+    const bool can_be_optimized = tau_computation_can_be_optimized_;
+    async_kind_ = AsyncKind::kTauDeferred;
+    tau_ticket_ = ++async_ticket_;
+    LuSlotGuard slot(1);
+    if (can_be_optimized) {
+      async_tau_ = tau_;
+      lu_factorization_.RightSolveLWithPermutedInput(rho.values, &async_tau_);
+    } else {
+      ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), &async_tau_);
+      lu_factorization_.RightSolveLForScatteredColumn(rho, &async_tau_);
+    }
+    rank_one_factorization_.RightSolveWithNonZeros(&async_tau_);
+    tau_u_pending_ = true;
+    async_input_ = &rho;
+    return;
+  }
   if (!AsyncEnabled()) return;
   const bool can_be_optimized = tau_computation_can_be_optimized_;
   tau_ticket_ = StartAsync(AsyncKind::kTau, [this, can_be_optimized, &rho]() {
@@ -1197,7 +1264,8 @@ void BasisFactorization::RightSolve(ScatteredVector* d) const {
 // basis_representation.cc:374-398
 const std::vector<Fractional>& BasisFactorization::RightSolveForTau(
     const ScatteredVector& a) const {
-  if (async_kind_ == AsyncKind::kTau && async_input_ == &a && TakeAsync(tau_ticket_)) {
+  if ((async_kind_ == AsyncKind::kTau || async_kind_ == AsyncKind::kTauDeferred) &&
+      async_input_ == &a && TakeAsync(tau_ticket_)) {
     std::swap(tau_, async_tau_);
     tau_computation_can_be_optimized_ = false;
     tau_is_computed_ = true;
@@ -1303,7 +1371,15 @@ void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d)
     right_pool_mapping_[col] =
         right_storage_.AddDenseColumnWithNonZeros(d->values, d->non_zeros);
   }
-  lu_factorization_.RightSolveUWithNonZeros(d);
+  if (async_kind_ == AsyncKind::kTauDeferred && tau_u_pending_) {
+    // The direction's and tau's U solves together; tau's bump deferred.
+    lu_factorization_.RightSolveUWithNonZerosPair(d, &async_tau_);
+    LuSlotGuard slot(1);
+    BumpDeterministicTimeForSolve(static_cast<int64_t>(async_tau_.NumNonZerosEstimate()));
+    tau_u_pending_ = false;
+  } else {
+    lu_factorization_.RightSolveUWithNonZeros(d);
+  }
   d->SortNonZerosIfNeeded();
   BumpDeterministicTimeForSolve(static_cast<int64_t>(d->NumNonZerosEstimate()));
 }

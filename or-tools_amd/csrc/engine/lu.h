@@ -20,6 +20,12 @@ namespace milp {
 // Which copy of the solve scratch a thread uses: 0 on the solver's thread,
 // 1 on BasisFactorization's tau worker (the two run FTRANs concurrently).
 inline thread_local int g_lu_slot = 0;
+// Runs a scope with another solve slot (scratch and deferred bookkeeping).
+struct LuSlotGuard {
+  int saved;
+  explicit LuSlotGuard(int slot) : saved(g_lu_slot) { g_lu_slot = slot; }
+  ~LuSlotGuard() { g_lu_slot = saved; }
+};
 
 // Debug aid (MILP_PHASE_TIMING): host wall time of the pieces of the solver
 // thread's FTRANs (L, etas, U) and of the device U/L solve calls (copy-in,
@@ -821,6 +827,11 @@ class LuFactorization {
                                      ScatteredVector* x) const;
   void LeftSolveUWithNonZeros(ScatteredVector* y) const;
   void RightSolveUWithNonZeros(ScatteredVector* x) const;
+  // The U solves of two vectors of the same factorization (the direction on
+  // this thread's scratch, tau on slot 1's), in one device launch when both
+  // take the dense path; else one after the other. Same bits as two calls.
+  void RightSolveUWithNonZerosPair(ScatteredVector* x, ScatteredVector* tau) const;
+  void RightSolveUAfterRows(ScatteredVector* x) const;
   bool LeftSolveLWithNonZeros(ScatteredVector* y,
                               ScatteredVector* result_before_permutation) const;
   int LeftSolveUForUnitRow(int col, ScatteredVector* y) const;
@@ -847,6 +858,7 @@ class LuFactorization {
   // Dense U solves of the solver's thread go to this device (engine
   // substitution, bit-identical; see device_solver.h).
   void SetDeviceSolver(DeviceSolver* d) { device_solver_ = d; }
+  bool HasDeviceSolver() const { return device_solver_ != nullptr; }
   // lower_.LowerSolveStartingAt(start, x), on the device when it takes it.
   void DenseLowerSolve(int start, std::vector<Fractional>* x) const;
   void DenseSolve(TriKind kind, const TriangularMatrix& t, int start,
@@ -1075,7 +1087,9 @@ class BasisFactorization {
   // factorization first waits for the worker and drops it. The solve is the
   // same code on a private scratch copy, and its deterministic-time bumps are
   // applied when it is taken, so results and timing match the serial order.
-  enum class AsyncKind { kNone, kTau, kLeftSolve };
+  // kTauDeferred: tau's L and etas are done, its U solve waits for the
+  // direction's (one two-vector device launch, MILP_TRI_PAIR).
+  enum class AsyncKind { kNone, kTau, kLeftSolve, kTauDeferred };
   void StartAsyncTau(const ScatteredVector& rho) const;
   // Small bases: tau on the calling thread, overlapped with the GPU update row.
   bool InlineTauEnabled() const;
@@ -1148,6 +1162,9 @@ class BasisFactorization {
   uint64_t StartAsync(AsyncKind kind, std::function<void()> job) const;
   void WaitAsync() const;
   void SyncForUnitRow() const;
+  bool TauFusionEnabled() const;
+  void FinishDeferredTauU() const;  // tau's U solve alone (slot 1), if still pending
+  mutable bool tau_u_pending_ = false;
   void ComputeTauInto(bool can_be_optimized, const ScatteredVector& a,
                       ScatteredVector* out) const;
 
@@ -1163,6 +1180,7 @@ class BasisFactorization {
   mutable std::vector<int64_t> deferred_solve_entries_;
   int async_min_rows_ = 16384;
   bool inline_tau_ = true;  // MILP_INLINE_TAU=off disables ComputeTauNow's use
+  bool fuse_tau_ = true;    // MILP_TRI_PAIR=0: tau's U solve on the worker, not with the direction's
   mutable bool tau_is_computed_ = false;
   mutable bool tau_computation_can_be_optimized_ = false;
   mutable ScatteredVector tau_;

@@ -5686,6 +5686,8 @@ int mi_lp_get_run_counters(const mi_lp* h, mi_lp_run_counters* c) {
   c->factorizations = h->simplex.NumFactorizations();
   c->factorization_seconds = h->simplex.FactorizationSeconds();
   c->iterations = h->simplex.GetNumberOfIterations();
+  const_cast<mi_lp*>(h)->simplex.device().TriScheduleShape(&c->u_levels, &c->u_outputs,
+                                                          &c->u_entries);
   return MI_LP_OK;
 }
 
@@ -5813,20 +5815,79 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
       RunSolve(h, nullptr, &results[i]);
     }
   };
+  // Workers are dealt to threads device by device (a thread's fibers never
+  // span two GPUs; each device's workers get a share of the threads in
+  // proportion to their number), all pulling children from one counter.
+  std::vector<int> order(num_workers);
+  for (int w = 0; w < num_workers; ++w) order[w] = w;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int a, int b) { return workers[a]->device < workers[b]->device; });
+  std::vector<std::vector<mi_lp*>> per_thread(threads);
+  {
+    int t = 0;
+    for (int w0 = 0; w0 < num_workers;) {
+      int w1 = w0;
+      while (w1 < num_workers && workers[order[w1]]->device == workers[order[w0]]->device) ++w1;
+      const int group = w1 - w0;
+      const int share = std::max(1, static_cast<int>(int64_t(group) * threads / num_workers));
+      for (int k = 0; k < group; ++k) per_thread[(t + k % share) % threads].push_back(workers[order[w0 + k]]);
+      t = (t + share) % threads;
+      w0 = w1;
+    }
+  }
   std::vector<std::thread> pool;
   for (int t = 0; t < threads; ++t) {
+    if (per_thread[t].empty()) continue;
     pool.emplace_back([&, t]() {
       std::vector<std::function<void()>> tasks;
-      for (int w = t; w < num_workers; w += threads) {
-        mi_lp* h = workers[w];
-        tasks.push_back([&worker_loop, h]() { worker_loop(h); });
-      }
+      for (mi_lp* h : per_thread[t]) tasks.push_back([&worker_loop, h]() { worker_loop(h); });
       milp::RunFibers(std::move(tasks));
     });
   }
   for (auto& th : pool) th.join();
   for (int w = 0; w < num_workers; ++w) SetSmallBatchSafe(workers[w], false);
   return MI_LP_OK;  // per-entry outcomes are in results[i]
+}
+
+// SURVEY 8(b) mi_lp_batch_solve(hs, count, num_gpus, ...): the handles'
+// devices must lie in [0, num_gpus); each device's handles are solved by a
+// pool of threads_per_gpu threads of their own (fibers per thread, batched
+// launches, largest LPs first), every device at once.
+int mi_lp_batch_solve_gpus(mi_lp* const* handles, int32_t count, int32_t num_gpus,
+                           int32_t threads_per_gpu, mi_lp_result* results) {
+  if (handles == nullptr || results == nullptr) return MI_LP_ERROR_NULL;
+  if (count < 0 || num_gpus < 1) return MI_LP_ERROR_INVALID_PROBLEM;
+  std::vector<std::vector<int>> by_device(num_gpus);
+  for (int i = 0; i < count; ++i) {
+    if (handles[i] == nullptr) return MI_LP_ERROR_NULL;
+    const int d = handles[i]->device;
+    if (d < 0 || d >= num_gpus) return MI_LP_ERROR_INVALID_PROBLEM;
+    by_device[d].push_back(i);
+  }
+  try {
+    std::vector<std::vector<mi_lp*>> hs(num_gpus);
+    std::vector<std::vector<mi_lp_result>> rs(num_gpus);
+    for (int d = 0; d < num_gpus; ++d) {
+      for (const int i : by_device[d]) hs[d].push_back(handles[i]);
+      rs[d].resize(hs[d].size());
+    }
+    std::vector<std::thread> per_device;
+    for (int d = 0; d < num_gpus; ++d) {
+      if (hs[d].empty()) continue;
+      per_device.emplace_back([&, d]() {
+        (void)hipSetDevice(d);
+        mi_lp_batch_solve(hs[d].data(), static_cast<int32_t>(hs[d].size()), threads_per_gpu,
+                          rs[d].data());
+      });
+    }
+    for (auto& th : per_device) th.join();
+    for (int d = 0; d < num_gpus; ++d) {
+      for (size_t k = 0; k < by_device[d].size(); ++k) results[by_device[d][k]] = rs[d][k];
+    }
+  } catch (const std::exception&) {
+    return MI_LP_ERROR_INTERNAL;
+  }
+  return MI_LP_OK;
 }
 
 }  // extern "C"

@@ -334,7 +334,26 @@ struct TriSolveArgs {
   // Sync-free variants: a waiting lane's sleep between polls doubles from
   // one s_sleep unit up to this many (MILP_TRI_POLL_MAX; 1 = fixed).
   int poll_max;
+  // A second right-hand side solved in the same launch (blockIdx.y == 1):
+  // its own rows, positions, staging, top row and failure word.
+  double* x2;
+  double* y2;
+  double* host_x2;
+  int* top2;
+  int* fail2;
 };
+// The argument set of right-hand side blockIdx.y (0 or 1).
+__host__ __device__ inline TriSolveArgs TriRhs(const TriSolveArgs& a, int rhs) {
+  TriSolveArgs b = a;
+  if (rhs == 1) {
+    b.x = a.x2;
+    b.y = a.y2;
+    b.host_x = a.host_x2;
+    b.top = a.top2;
+    b.fail = a.fail2;
+  }
+  return b;
+}
 // The sync-free variant needs every workgroup resident: at most this many
 // outputs (512 workgroups of 256 threads, 2 per CU).
 constexpr int kTriSyncFreeMaxWork = 512 * 256;
@@ -419,7 +438,8 @@ hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, const int
                                int num_segments, hipStream_t s);
 // The same solve driven by per-output readiness instead of levels (one
 // launch for the whole triangle; rec_row/x updated in place, no scatter).
-hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, hipStream_t s);
+hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, hipStream_t s,
+                                        int num_rhs = 1);
 // The same, persistent: `groups` workgroups of kTriThreads threads walk the
 // outputs in level order (thread t: t, t + T, ...); xcd_stride 8 keeps them
 // on one XCD under round-robin dealing (speed only, any placement is correct).

@@ -715,8 +715,12 @@ __global__ __launch_bounds__(THREADS) void row_wise_small_kernel(RowWiseSmallArg
 constexpr int kMediumSlots = 5120;
 static_assert(kMediumSlots > kSmallEntries, "the table must never fill");
 
+// Multiplicative hash, mapped to [0, kMediumSlots) by its high bits (a
+// modulo of the low bits would send positions equal mod 1024 to the same 5
+// home slots: long probe runs).
 __device__ __forceinline__ int medium_hash(int pos) {
-  return static_cast<int>((static_cast<uint32_t>(pos) * 2654435761u) % kMediumSlots);
+  const uint32_t h = static_cast<uint32_t>(pos) * 2654435761u;
+  return static_cast<int>((static_cast<uint64_t>(h) * kMediumSlots) >> 32);
 }
 
 // Slot holding `pos`, or -1. Probes end at an empty slot or after every slot.
@@ -738,6 +742,7 @@ __device__ __forceinline__ void row_wise_medium_body(const RowWiseSmallArgs& a) 
   __shared__ uint8_t written[kMediumSlots];
   __shared__ uint64_t rel[kMediumCols / 64];
   __shared__ unsigned long long listed_w[kMediumCols / 64];
+  __shared__ unsigned long long touched_w[kMediumCols / 64];  // positions in the table
   __shared__ int16_t ent_slot[kSmallEntries];
   __shared__ double ent_val[kSmallEntries];
   __shared__ double s_rho[kSmallRowsMax];
@@ -754,6 +759,7 @@ __device__ __forceinline__ void row_wise_medium_body(const RowWiseSmallArgs& a) 
   for (int w = t; w < (n + 63) / 64; w += THREADS) {
     rel[w] = a.relevant[w];
     listed_w[w] = 0;
+    touched_w[w] = 0;
   }
   int len = 0;
   if (t < k_rows) {
@@ -792,6 +798,7 @@ __device__ __forceinline__ void row_wise_medium_body(const RowWiseSmallArgs& a) 
       sl = sl + 1 == kMediumSlots ? 0 : sl + 1;
     }
     ent_slot[e] = static_cast<int16_t>(sl);
+    atomicOr(&touched_w[pos >> 6], 1ull << (pos & 63));
   }
   __syncthreads();
   for (int k = 0; k < k_rows; ++k) {
@@ -812,7 +819,10 @@ __device__ __forceinline__ void row_wise_medium_body(const RowWiseSmallArgs& a) 
     __syncthreads();  // rows are applied in order
   }
   for (int pos = t; pos < n; pos += THREADS) {
-    const int sl = medium_find(keys, pos);
+    // Only positions an entry touched are in the table: the others skip the
+    // probe (it would walk to an empty slot).
+    const bool in_table = (touched_w[pos >> 6] >> (pos & 63)) & 1ull;
+    const int sl = in_table ? medium_find(keys, pos) : -1;
     const bool was_touched = sl >= 0 && written[sl] != 0;
     const double v = was_touched ? acc[sl] : 0.0;
     const bool is_rel = (rel[pos >> 6] >> (pos & 63)) & 1ull;

@@ -165,7 +165,8 @@ __device__ __forceinline__ void tri_compute(const TriSolveArgs& a, double* y, in
 
 // Zero-copy staging in and out of device-visible host memory (coalesced
 // PCIe reads and writes, inside the captured plan: no copy engine calls).
-__global__ __launch_bounds__(256) void tri_copy_in_kernel(TriSolveArgs a) {
+__global__ __launch_bounds__(256) void tri_copy_in_kernel(TriSolveArgs a0) {
+  const TriSolveArgs a = TriRhs(a0, blockIdx.y);
   const int n = a.num_rows - a.first_col;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     a.x[a.first_col + i] = a.host_x[a.first_col + i];
@@ -175,7 +176,8 @@ __global__ __launch_bounds__(256) void tri_copy_in_kernel(TriSolveArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void tri_copy_out_kernel(TriSolveArgs a) {
+__global__ __launch_bounds__(256) void tri_copy_out_kernel(TriSolveArgs a0) {
+  const TriSolveArgs a = TriRhs(a0, blockIdx.y);
   const int end = *a.top + 1;
   for (int i = a.first_col + blockIdx.x * blockDim.x + threadIdx.x; i < end;
        i += gridDim.x * blockDim.x) {
@@ -385,7 +387,8 @@ __device__ __forceinline__ bool tri_pending(double v) {
 }
 
 // y[k] = x[row(k)], or "pending" for the outputs this solve computes.
-__global__ __launch_bounds__(256) void tri_init_kernel(TriSolveArgs a) {
+__global__ __launch_bounds__(256) void tri_init_kernel(TriSolveArgs a0) {
+  const TriSolveArgs a = TriRhs(a0, blockIdx.y);
   const int top = *a.top;
   const double pending = __longlong_as_double(static_cast<long long>(kTriPending));
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.num_pos;
@@ -489,7 +492,8 @@ __device__ __forceinline__ void tri_syncfree_output(const TriSolveArgs& a, int k
   }
 }
 
-__global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a) {
+__global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a0) {
+  const TriSolveArgs a = TriRhs(a0, blockIdx.y);
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= a.num_work) return;
   tri_syncfree_output(a, k, *a.top);
@@ -519,26 +523,28 @@ __global__ __launch_bounds__(kTriThreads) void tri_syncfree_persistent_kernel(Tr
 
 namespace milp_launch {
 
-hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, hipStream_t s) {
+hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, hipStream_t s,
+                                        int num_rhs) {
   if (args.num_work <= 0) return hipSuccess;
   const int row_blocks =
       std::max(1, std::min(1024, (args.num_rows - args.first_col + 255) / 256));
   hipError_t e;
   if (args.host_x != nullptr) {
-    milp_kernels::tri_copy_in_kernel<<<row_blocks, 256, 0, s>>>(args);
+    milp_kernels::tri_copy_in_kernel<<<dim3(row_blocks, num_rhs), 256, 0, s>>>(args);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   const int pos_blocks = std::max(1, std::min(1024, (args.num_pos + 255) / 256));
-  milp_kernels::tri_init_kernel<<<pos_blocks, 256, 0, s>>>(args);
+  milp_kernels::tri_init_kernel<<<dim3(pos_blocks, num_rhs), 256, 0, s>>>(args);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // One thread per listed output: every workgroup resident (100k outputs =
-  // 391 workgroups of 256 on 256 CUs).
-  milp_kernels::tri_syncfree_kernel<<<(args.num_work + 255) / 256, 256, 0, s>>>(args);
+  // One thread per listed output and right-hand side: every workgroup
+  // resident (100k outputs = 391 workgroups of 256 per vector on 256 CUs).
+  milp_kernels::tri_syncfree_kernel<<<dim3((args.num_work + 255) / 256, num_rhs), 256, 0, s>>>(
+      args);
   e = hipGetLastError();
   if (e != hipSuccess || args.host_x == nullptr) return e;
-  milp_kernels::tri_copy_out_kernel<<<row_blocks, 256, 0, s>>>(args);
+  milp_kernels::tri_copy_out_kernel<<<dim3(row_blocks, num_rhs), 256, 0, s>>>(args);
   return hipGetLastError();
 }
 

@@ -143,6 +143,9 @@ class MiLpRunCounters(ctypes.Structure):
         ("factorizations", ctypes.c_int64),
         ("factorization_seconds", ctypes.c_double),
         ("iterations", ctypes.c_int64),
+        ("u_levels", ctypes.c_int64),
+        ("u_outputs", ctypes.c_int64),
+        ("u_entries", ctypes.c_int64),
     ]
 
 
@@ -171,6 +174,7 @@ EXPORTED_SYMBOLS = [
     "mi_lp_solver_params_default", "mi_lp_scale", "mi_lp_solver_solve",
     "mi_lp_clear_integrality_scales", "mi_lp_record_iteration_times",
     "mi_lp_get_iteration_times", "mi_lp_get_run_counters", "mi_lp_set_exchange",
+    "mi_lp_batch_solve_gpus",
 ]
 
 

@@ -70,6 +70,8 @@ def lib():
     L.mi_lp_batch_solve.argtypes = [vp, ctypes.c_int32, ctypes.c_int32,
                                     ctypes.POINTER(abi.MiLpResult)]
     L.mi_lp_set_variable_bounds.argtypes = [vp, vp, vp]
+    L.mi_lp_batch_solve_gpus.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.POINTER(abi.MiLpResult)]
     L.mi_lp_batch_solve_bounds.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
                                            ctypes.c_int32, ctypes.POINTER(abi.MiLpResult)]
     L.mi_lp_notify_matrix_changed.argtypes = [vp]
@@ -278,7 +280,8 @@ class LpHandle:
                     "mi_lp_get_run_counters")
         return {"factorizations": int(c.factorizations),
                 "factorization_seconds": float(c.factorization_seconds),
-                "iterations": int(c.iterations)}
+                "iterations": int(c.iterations), "u_levels": int(c.u_levels),
+                "u_outputs": int(c.u_outputs), "u_entries": int(c.u_entries)}
 
     def reset_kernel_stats(self):
         self._L.mi_lp_reset_kernel_stats(self.h)
@@ -376,6 +379,20 @@ def batch_solve(handles, num_threads=4):
     arr = (ctypes.c_void_p * len(handles))(*[h.h.value for h in handles])
     res = (abi.MiLpResult * len(handles))()
     L.mi_lp_batch_solve(arr, len(handles), num_threads, res)
+    return list(res)
+
+
+def batch_solve_gpus(handles, num_gpus, threads_per_gpu=4):
+    """Loaded handles on devices [0, num_gpus) solved concurrently, one thread
+    pool per device (mi_lp_batch_solve_gpus)."""
+    L = lib()
+    for h in handles:
+        h._push_params()
+    arr = (ctypes.c_void_p * len(handles))(*[h.h.value for h in handles])
+    res = (abi.MiLpResult * len(handles))()
+    rc = L.mi_lp_batch_solve_gpus(arr, len(handles), num_gpus, threads_per_gpu, res)
+    if rc != 0:
+        raise RuntimeError(f"mi_lp_batch_solve_gpus failed ({rc})")
     return list(res)
 
 

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--lps", type=int, default=128)
     ap.add_argument("--workers", type=int, nargs="*", default=[1, 8])
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--node", action="store_true",
+                    help="the node's BranchOnVar LPs (bench.py config 4) instead of random fixings")
     a = ap.parse_args()
     jobs = jobshop.random_instance(a.jobs, a.machines, a.seed)
     lp, ycols = jobshop.relaxation(jobs)
@@ -32,7 +34,14 @@ def main():
     root.load(lp)
     root.solve()
     state = root.state()
-    lbs, ubs = jobshop.child_bounds(lp, ycols, a.lps, a.seed + 1000)
+    if a.node:
+        from mi_glop import cpsat
+        x = root.primal()
+        cols = cpsat.fractional_columns(x, ycols, limit=a.lps // 2)
+        lbs, ubs = cpsat.branch_lps(cpsat.IntegerTrail(lp.col_lb, lp.col_ub), x, cols)
+        a.lps = len(lbs)
+    else:
+        lbs, ubs = jobshop.child_bounds(lp, ycols, a.lps, a.seed + 1000)
     p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
     out = {"m": lp.m, "n": lp.n, "lps": a.lps}
     gpu_res = {}

@@ -248,3 +248,26 @@ def test_iteration_times_and_run_counters():
     g.stop()
     r = g.finish()
     assert len(g.iteration_times()) == r.iterations
+
+
+@pytest.mark.gpu
+def test_batch_solve_gpus_parity():
+    """mi_lp_batch_solve_gpus (SURVEY 8(b)'s batch entry with num_gpus): each
+    device's handles on a thread pool of their own; every LP equals the
+    oracle's solve bit for bit. A device outside [0, num_gpus) is refused."""
+    import parity_util
+    from mi_glop import engine
+    lps = [lp_gen.random_sparse_lp(40 + 7 * k, 120 + 20 * k, 0.08, 30 + k) for k in range(6)]
+    p = abi.default_params(use_dual_simplex=1)
+    hs = []
+    for lp in lps:
+        h = engine.LpHandle(p)
+        h.load(lp)
+        hs.append(h)
+    res = engine.batch_solve_gpus(hs, num_gpus=engine.device_count(), threads_per_gpu=2)
+    for lp, h, r in zip(lps, hs, res):
+        o = oracle_lib.OracleLp(p)
+        o.load(lp)
+        parity_util.compare(o, o.solve(), h, r, lp)
+    with pytest.raises(RuntimeError):
+        engine.batch_solve_gpus(hs, num_gpus=0)
