@@ -403,8 +403,8 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
         "root_objective": float(root_res.objective), "root_iterations": int(root_res.iterations),
         "node_obj_lb": node_lb, "deductions": int(summary["deductions"]),
         "speculative_lps": int(summary["speculative"]),
-        "workload": (f"config 4: job-shop {args.batch_jobs}x{args.batch_machines} (seeded, "
-                     f"ta041-shaped family) big-M LP relaxation, m={lp.m} n={lp.n}; one search "
+        "workload": (f"config 4: job-shop {args.batch_jobs}x{args.batch_machines} (seeded "
+                     f"Taillard-style instance; ta041 itself is 50x10) big-M LP relaxation, m={lp.m} n={lp.n}; one search "
                      f"node's BranchOnVar LPs: {len(cols_all)} fractional order variables x 2 "
                      f"branches, dual simplex warm-started from the node basis, cap 1000 "
                      f"iterations"),
@@ -457,9 +457,9 @@ def main():
                     default=os.path.join(REPO, "profiles", "traffic_c2.json"),
                     help="per-launch HBM bytes of the config-2 dominant kernel from a "
                          "separate rocprofv3 --pmc pass (profiles/)")
-    ap.add_argument("--batch-lps", type=int, default=512,
+    ap.add_argument("--batch-lps", type=int, default=1024,
                     help="config-4 branch LPs per GPU (0 disables the batched section)")
-    ap.add_argument("--batch-workers", type=int, default=128,
+    ap.add_argument("--batch-workers", type=int, default=256,
                     help="config-4 solver handles per GPU (LPs in flight); the engine runs "
                          "them on at most 16 host threads as fibers with batched launches")
     ap.add_argument("--batch-cpu-threads", type=int, default=16)

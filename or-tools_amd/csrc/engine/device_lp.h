@@ -147,6 +147,11 @@ class DeviceLp : public DeviceSolver {
     std::vector<int64_t> entries_upto;  // their entries
     int max_entries = 0;
     int rows_over[3] = {0, 0, 0};     // outputs with > 4, 16, 64 entries
+    int64_t late_entries = 0;         // long outputs: entries from the deepest input on
+    // Sync-free launch segments: (first position, end position, narrow) triples.
+    std::vector<int> runs;
+    int chain_levels = 0;             // levels in narrow segments
+    int max_wide_run = 0;             // positions of the largest chip-wide segment
   };
   struct TriContext {  // one solving thread's stream, values and graphs
     void* stream = nullptr;
@@ -526,6 +531,12 @@ class DeviceLp : public DeviceSolver {
   bool tri_btran_ = true;     // MILP_TRI_BTRAN: the other dense loops (BTRAN, UpperSolve) too
   bool tri_pair_ = true;      // MILP_TRI_PAIR: direction and tau U solves in one launch
   int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
+  // MILP_TRI_CHAIN=0: no single-workgroup segments; a narrow segment is a
+  // run of at least MILP_TRI_CHAIN_MIN_LEVELS levels of at most
+  // MILP_TRI_CHAIN_WIDTH outputs each (tri_chain_kernel).
+  bool tri_chain_ = true;
+  int tri_chain_width_ = 1024;
+  int tri_chain_min_levels_ = 4;
   uint64_t* d_tri_clock_ = nullptr;
   TriSchedule tri_sched_[kTriNumMatrices];
   // Per solving thread: 0 = the solver's thread (the handle's stream),

@@ -160,6 +160,11 @@ void DeviceLp::Init(int device) {
   if (const char* v = std::getenv("MILP_TRI_BTRAN")) tri_btran_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_PAIR")) tri_pair_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_MIN_WIDTH")) tri_min_width_ = std::atoi(v);
+  if (const char* v = std::getenv("MILP_TRI_CHAIN")) tri_chain_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_TRI_CHAIN_WIDTH")) tri_chain_width_ = std::atoi(v);
+  if (const char* v = std::getenv("MILP_TRI_CHAIN_MIN_LEVELS")) {
+    tri_chain_min_levels_ = std::max(1, std::atoi(v));
+  }
   if (const char* v = std::getenv("MILP_TRI_SYNCFREE_MIN_LEVELS")) {
     tri_syncfree_min_levels_ = std::atoi(v);
   }

@@ -134,9 +134,56 @@ void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, cons
   for (int c = fni; c < nc; ++c) {
     if (level[c] > 0 || !ones) ++level_count[level[c]];
   }
+  // Narrow segments (sync-free plans only): runs of at least
+  // tri_chain_min_levels_ levels of at most tri_chain_width_ outputs each,
+  // cut where the chain kernel's LDS is full, solved by one workgroup; their
+  // levels are not padded. The rest run chip-wide.
+  std::vector<int> seg_level;  // (first level, end level, narrow) triples
+  if (tri_chain_ && tri_syncfree_ && tri_persist_groups_ == 0) {
+    int wide_from = 0;
+    int l = 0;
+    while (l <= depth) {
+      if (level_count[l] > tri_chain_width_) {
+        ++l;
+        continue;
+      }
+      int e = l;
+      int held = 0;
+      while (e <= depth && level_count[e] <= tri_chain_width_ &&
+             held + level_count[e] <= milp_kernels::kTriChainVals) {
+        held += level_count[e];
+        ++e;
+      }
+      if (e - l >= tri_chain_min_levels_) {
+        if (l > wide_from) seg_level.insert(seg_level.end(), {wide_from, l, 0});
+        seg_level.insert(seg_level.end(), {l, e, 1});
+        wide_from = e;
+      }
+      l = e;
+    }
+    if (wide_from <= depth) seg_level.insert(seg_level.end(), {wide_from, depth + 1, 0});
+  } else {
+    seg_level = {0, depth + 1, 0};
+  }
+  std::vector<char> narrow(depth + 1, 0);
+  s->chain_levels = 0;
+  for (size_t i = 0; i < seg_level.size(); i += 3) {
+    if (seg_level[i + 2] == 0) continue;
+    for (int l = seg_level[i]; l < seg_level[i + 1]; ++l) narrow[l] = 1;
+    s->chain_levels += seg_level[i + 1] - seg_level[i];
+  }
   std::vector<int32_t> level_start(depth + 2, 0);
   for (int l = 0; l <= depth; ++l) {
-    level_start[l + 1] = level_start[l] + (level_count[l] + 63) / 64 * 64;
+    level_start[l + 1] =
+        level_start[l] + (narrow[l] ? level_count[l] : (level_count[l] + 63) / 64 * 64);
+  }
+  s->runs.clear();
+  s->max_wide_run = 0;
+  for (size_t i = 0; i < seg_level.size(); i += 3) {
+    const int b = level_start[seg_level[i]], e = level_start[seg_level[i + 1]];
+    if (e <= b) continue;
+    s->runs.insert(s->runs.end(), {b, e, seg_level[i + 2]});
+    if (seg_level[i + 2] == 0) s->max_wide_run = std::max(s->max_wide_run, e - b);
   }
   num_work = level_start[depth + 1];  // listed outputs + padding
   const int num_pos = num_work + (nc - fni);  // + every row, read-only copies
@@ -196,10 +243,25 @@ void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, cons
   int64_t num_ovf = 0;
   s->max_entries = 0;
   s->rows_over[0] = s->rows_over[1] = s->rows_over[2] = 0;
+  s->late_entries = 0;
   for (int k = 0; k < num_work; ++k) {
     if (is_pad[k]) continue;
     const int c = pos_row[k];
     const int64_t n = gst[c + 1] - gst[c];
+    if (n > 4) {
+      // Entries evaluated at or after the first one of the deepest level:
+      // what is left to fold once the last input arrives.
+      int deepest = -1;
+      int64_t first = 0;
+      for (int64_t j = 0; j < n; ++j) {
+        const int l = level[gidx[reverse ? gst[c + 1] - 1 - j : gst[c] + j]];
+        if (l > deepest) {
+          deepest = l;
+          first = j;
+        }
+      }
+      s->late_entries += n - first;
+    }
     if (n > 4) num_ovf += n;
     s->max_entries = std::max<int>(s->max_entries, static_cast<int>(n));
     s->rows_over[0] += n > 4;
@@ -376,6 +438,8 @@ milp_kernels::TriSolveArgs DeviceLp::TriArgs(const TriSchedule& s, const TriCont
   a.host_x2 = nullptr;
   a.top2 = nullptr;
   a.fail2 = nullptr;
+  a.seg_begin = 0;
+  a.seg_end = s.work;
   return a;
 }
 
@@ -417,9 +481,12 @@ void DeviceLp::EnqueueTriKernels(const TriSchedule& s, const milp_kernels::TriSo
           "tri persistent");
     return;
   }
-  if (tri_syncfree_ && a.clock == nullptr && a.num_work <= milp_kernels::kTriSyncFreeMaxWork &&
+  if (tri_syncfree_ && a.clock == nullptr && s.max_wide_run <= milp_kernels::kTriSyncFreeMaxWork &&
       s.levels >= tri_syncfree_min_levels_) {
-    Check(milp_launch::tri_transpose_lower_syncfree(a, Stream(stream)), "tri syncfree");
+    Check(milp_launch::tri_transpose_lower_syncfree(a, s.runs.data(),
+                                                    static_cast<int>(s.runs.size() / 3),
+                                                    Stream(stream)),
+          "tri syncfree");
     return;
   }
   Check(milp_launch::tri_transpose_lower(a, s.segments.data(),
@@ -563,12 +630,38 @@ bool DeviceLp::TriPrepare(int which, const TriangularMatrix& t, uint64_t key, in
       if (which == kTriU) {
         if (const char* d = std::getenv("MILP_TRI_DEBUG")) tri_debug_left_ = std::atoi(d);
       }
+      if (s.ok && std::getenv("MILP_TRI_SCHED") != nullptr) {
+        // Shape of each schedule as built: how many levels are narrow, and
+        // how much of the long outputs' work waits for their deepest input.
+        int narrow64 = 0, narrow1024 = 0;
+        for (int w : s.level_width) {
+          narrow64 += w <= 64;
+          narrow1024 += w <= 1024;
+        }
+        int64_t long_entries = 0;
+        for (int c = 0; c < nc; ++c) {
+          const int64_t n = s.entries_upto[c + 1] - s.entries_upto[c];
+          if (n > 4) long_entries += n;
+        }
+        std::fprintf(stderr,
+                     "[tri sched] kind %d rows %d first %d work %d levels %d (<=64: %d, "
+                     "<=1024: %d) long outputs %d entries %lld late %lld; segments %zu, "
+                     "%d levels narrow\n",
+                     which, nc, s.first_col, s.work, s.levels, narrow64, narrow1024,
+                     s.rows_over[0], static_cast<long long>(long_entries),
+                     static_cast<long long>(s.late_entries), s.runs.size() / 3,
+                     s.chain_levels);
+      }
     }
     if (!s.ok) return false;
     // Auto mode: the device pays a dependency hop per level, the host loop a
     // few ns per entry; a triangle without enough outputs per level stays on
     // the host (MILP_TRI_MIN_WIDTH, outputs per level on average).
-    if (tri_mode_ == 0 && s.work < int64_t(s.levels) * tri_min_width_) return false;
+    // The narrow segments' levels cost an LDS hand-off each, not a trip
+    // between XCDs: only the chip-wide levels count.
+    if (tri_mode_ == 0 && s.work < int64_t(s.levels - s.chain_levels) * tri_min_width_) {
+      return false;
+    }
     PrepareTriContext(slot, nc, s.pos);
   }
   return true;
@@ -722,7 +815,7 @@ bool DeviceLp::SolvePair(TriKind kind, const TriangularMatrix& t, uint64_t key,
   TriSchedule& s = tri_sched_[kTriU];
   // Both vectors' workgroups resident at once: 2 x 512 workgroups of 256
   // at most, 4 per CU of the 8 the kernel's registers allow.
-  if (s.work > milp_kernels::kTriSyncFreeMaxWork || s.levels < tri_syncfree_min_levels_) {
+  if (s.max_wide_run > milp_kernels::kTriSyncFreeMaxWork || s.levels < tri_syncfree_min_levels_) {
     return false;
   }
   const int nc = t.num_cols();
@@ -765,7 +858,10 @@ bool DeviceLp::SolvePair(TriKind kind, const TriangularMatrix& t, uint64_t key,
   a.top2 = static_cast<int*>(c1.top.ptr);
   a.fail2 = reinterpret_cast<int*>(c1.m_x + s.rows) + 1;
   BeginKernel(MI_K_TRI_SOLVE);
-  Check(milp_launch::tri_transpose_lower_syncfree(a, Stream(c0.stream), 2), "tri pair");
+  Check(milp_launch::tri_transpose_lower_syncfree(a, s.runs.data(),
+                                                  static_cast<int>(s.runs.size() / 3),
+                                                  Stream(c0.stream), 2),
+        "tri pair");
   EndKernel(MI_K_TRI_SOLVE, bytes);
   DeviceOp("tri pair sync");
   Check(hipStreamSynchronize(Stream(c0.stream)), "sync");

@@ -981,11 +981,8 @@ uint64_t BasisFactorization::StartAsync(AsyncKind kind, std::function<void()> jo
 
 bool BasisFactorization::TakeAsync(uint64_t ticket) const {
   if (async_kind_ == AsyncKind::kNone || ticket != async_ticket_) return false;
-  if (async_kind_ == AsyncKind::kTauDeferred) {
-    FinishDeferredTauU();
-  } else if (async_) {
-    async_->Wait();
-  }
+  if (async_) async_->Wait();
+  if (async_kind_ == AsyncKind::kTauDeferred) FinishDeferredTauU();
   async_kind_ = AsyncKind::kNone;
   async_input_ = nullptr;
   // The worker's deterministic-time bumps land now, where the serial solve
@@ -998,8 +995,8 @@ bool BasisFactorization::TakeAsync(uint64_t ticket) const {
 
 void BasisFactorization::DropAsync() const {
   if (async_kind_ == AsyncKind::kNone) return;
+  if (async_) async_->Wait();
   tau_u_pending_ = false;
-  if (async_ && async_kind_ != AsyncKind::kTauDeferred) async_->Wait();
   async_kind_ = AsyncKind::kNone;
   async_input_ = nullptr;
   rank_one_factorization_.TakeDeferredBumps(false);
@@ -1007,9 +1004,7 @@ void BasisFactorization::DropAsync() const {
 }
 
 void BasisFactorization::WaitAsync() const {
-  if (async_kind_ != AsyncKind::kNone && async_kind_ != AsyncKind::kTauDeferred && async_) {
-    async_->Wait();
-  }
+  if (async_kind_ != AsyncKind::kNone && async_) async_->Wait();
 }
 
 // The body of RightSolveForTau (basis_representation.cc:374-398) into *out,
@@ -1045,22 +1040,21 @@ void BasisFactorization::StartAsyncTau(const ScatteredVector& rho) const {
   DropAsync();
   if (TauFusionEnabled()) {
     // tau = B^-1 rho (dual_edge_norms.cc:134-141) against the factorization
-    // the direction is solved with next: L and the etas now (slot 1, bumps
-    // deferred), the U solve together with the direction's
+    // the direction is solved with next: L and the etas on the worker (slot
+    // 1, bumps deferred), the U solve together with the direction's
     // (RightSolveForProblemColumn), taken in RightSolveForTau.
     const bool can_be_optimized = tau_computation_can_be_optimized_;
-    async_kind_ = AsyncKind::kTauDeferred;
-    tau_ticket_ = ++async_ticket_;
-    LuSlotGuard slot(1);
-    if (can_be_optimized) {
-      async_tau_ = tau_;
-      lu_factorization_.RightSolveLWithPermutedInput(rho.values, &async_tau_);
-    } else {
-      ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), &async_tau_);
-      lu_factorization_.RightSolveLForScatteredColumn(rho, &async_tau_);
-    }
-    rank_one_factorization_.RightSolveWithNonZeros(&async_tau_);
-    tau_u_pending_ = true;
+    tau_ticket_ = StartAsync(AsyncKind::kTauDeferred, [this, can_be_optimized, &rho]() {
+      if (can_be_optimized) {
+        async_tau_ = tau_;
+        lu_factorization_.RightSolveLWithPermutedInput(rho.values, &async_tau_);
+      } else {
+        ClearAndResizeVectorWithNonZeros(compact_matrix_.num_rows(), &async_tau_);
+        lu_factorization_.RightSolveLForScatteredColumn(rho, &async_tau_);
+      }
+      rank_one_factorization_.RightSolveWithNonZeros(&async_tau_);
+      tau_u_pending_ = true;  // read by the solver's thread after Wait
+    });
     async_input_ = &rho;
     return;
   }
@@ -1371,6 +1365,7 @@ void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d)
     right_pool_mapping_[col] =
         right_storage_.AddDenseColumnWithNonZeros(d->values, d->non_zeros);
   }
+  if (async_kind_ == AsyncKind::kTauDeferred && async_) async_->Wait();  // tau's L, etas
   if (async_kind_ == AsyncKind::kTauDeferred && tau_u_pending_) {
     // The direction's and tau's U solves together; tau's bump deferred.
     lu_factorization_.RightSolveUWithNonZerosPair(d, &async_tau_);

@@ -1087,8 +1087,8 @@ class BasisFactorization {
   // factorization first waits for the worker and drops it. The solve is the
   // same code on a private scratch copy, and its deterministic-time bumps are
   // applied when it is taken, so results and timing match the serial order.
-  // kTauDeferred: tau's L and etas are done, its U solve waits for the
-  // direction's (one two-vector device launch, MILP_TRI_PAIR).
+  // kTauDeferred: the worker does tau's L and etas only; its U solve waits
+  // for the direction's (one two-vector device launch, MILP_TRI_PAIR).
   enum class AsyncKind { kNone, kTau, kLeftSolve, kTauDeferred };
   void StartAsyncTau(const ScatteredVector& rho) const;
   // Small bases: tau on the calling thread, overlapped with the GPU update row.

@@ -341,6 +341,14 @@ struct TriSolveArgs {
   double* host_x2;
   int* top2;
   int* fail2;
+  // Sync-free plans run the schedule as segments of consecutive levels, one
+  // launch each, in order: this launch's positions are [seg_begin, seg_end).
+  // A chip-wide segment (tri_syncfree_kernel) hands values between
+  // workgroups through y; a narrow one (tri_chain_kernel, unpadded levels)
+  // runs on one workgroup per right-hand side with its values in LDS.
+  // Earlier segments are final in y when a launch starts.
+  int seg_begin;
+  int seg_end;
 };
 // The argument set of right-hand side blockIdx.y (0 or 1).
 __host__ __device__ inline TriSolveArgs TriRhs(const TriSolveArgs& a, int rhs) {
@@ -357,6 +365,8 @@ __host__ __device__ inline TriSolveArgs TriRhs(const TriSolveArgs& a, int rhs) {
 // The sync-free variant needs every workgroup resident: at most this many
 // outputs (512 workgroups of 256 threads, 2 per CU).
 constexpr int kTriSyncFreeMaxWork = 512 * 256;
+// Values the chain kernel keeps in LDS (96 KB): a tail never holds more.
+constexpr int kTriChainVals = 12288;
 }  // namespace milp_kernels
 
 namespace milp_launch {
@@ -436,9 +446,12 @@ hipError_t boxed_flips(const int32_t* cols, int n, const double* rc, const uint8
 // one CU; (-level - 1, blocks) = one wide level over `blocks` workgroups.
 hipError_t tri_transpose_lower(const milp_kernels::TriSolveArgs& args, const int* segments,
                                int num_segments, hipStream_t s);
-// The same solve driven by per-output readiness instead of levels (one
-// launch for the whole triangle; rec_row/x updated in place, no scatter).
-hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, hipStream_t s,
+// The same solve driven by per-output readiness instead of levels
+// (rec_row/x updated in place, no scatter): one launch per segment, segs =
+// num_segs triples (first position, end position, 1 = narrow segment on one
+// workgroup / 0 = chip-wide).
+hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args,
+                                        const int* segs, int num_segs, hipStream_t s,
                                         int num_rhs = 1);
 // The same, persistent: `groups` workgroups of kTriThreads threads walk the
 // outputs in level order (thread t: t, t + T, ...); xcd_stride 8 keeps them

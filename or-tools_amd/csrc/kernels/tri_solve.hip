@@ -473,17 +473,74 @@ __device__ __forceinline__ void tri_syncfree_output(const TriSolveArgs& a, int k
     }
     return;
   }
-  int ready = 0;  // entries [0, ready) are known final
+  // A long output folds its entries in evaluation order as they become final
+  // (the same operations as subtract_overflow / subtract_sequential, so the
+  // same bits): by the time its last input arrives only the groups after the
+  // last stall are left, and a deep chain of long outputs advances by one
+  // group fold per hop instead of one whole sum. The wait bound restarts on
+  // progress (a stall detector, not a budget for the whole chain).
+  double sum = in;
+  int e = r.e.x;
+  const int end = r.e.x + r.n;
+  uint64_t t_progress = t0;
   while (!done) {
-    for (; ready < r.n; ++ready) {
-      if (tri_pending(load_final(y, tri_entry_pos(a, r.e, r.n, ready)))) break;
+    const int e0 = e;
+    while (e < end) {
+      // Up to 8 values per round, their loads in flight together.
+      double v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = e + i < end ? load_final(y, a.ovf_pos[e + i]) : 0.0;
+      int took = 0;
+      if (a.sequential) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (took != i || e + i >= end || tri_pending(v[i])) continue;
+          if (v[i] != 0.0) sum -= v[i] * a.ovf_value[e + i];
+          took = i + 1;
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 8; g += 4) {
+          if (took != g || e + g + 3 >= end) continue;
+          if (tri_pending(v[g]) || tri_pending(v[g + 1]) || tri_pending(v[g + 2]) ||
+              tri_pending(v[g + 3])) {
+            continue;
+          }
+          sum -= a.ovf_value[e + g] * v[g] + a.ovf_value[e + g + 1] * v[g + 1] +
+                 a.ovf_value[e + g + 2] * v[g + 2] + a.ovf_value[e + g + 3] * v[g + 3];
+          took = g + 4;
+        }
+        // The tail (fewer than 4 left), one subtraction per entry, all final.
+        const int left = end - e - took;
+        if (took < 8 && left > 0 && left < 4) {
+          const int t = took;
+          bool ready = true;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            if (i < left && t + i < 8) ready = ready && !tri_pending(v[t + i]);
+          }
+          if (ready && t + left <= 8) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+              if (i < left) sum -= a.ovf_value[e + t + i] * v[t + i];
+            }
+            took = t + left;
+          }
+        }
+      }
+      e += took;
+      if (took < 8) break;  // a pending value, or the end
     }
-    if (ready == r.n) {
-      const double out = tri_apply(a, y, in, r);
+    if (e == end) {
+      const double out = a.sequential ? tri_sequential_divide(a, sum, r.d)
+                                      : (a.diag != nullptr ? sum / r.d : sum);
       a.x[r.row] = out;  // the scatter, fused
       __hip_atomic_store(y + k, out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       done = true;
-    } else if (wall_clock64() - t0 > kTriMaxWaitTicks) {
+    } else if (e != e0) {
+      t_progress = wall_clock64();
+      backoff = 1;
+    } else if (wall_clock64() - t_progress > kTriMaxWaitTicks) {
       if (a.fail != nullptr) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       done = true;
     } else {
@@ -494,8 +551,8 @@ __device__ __forceinline__ void tri_syncfree_output(const TriSolveArgs& a, int k
 
 __global__ __launch_bounds__(256) void tri_syncfree_kernel(TriSolveArgs a0) {
   const TriSolveArgs a = TriRhs(a0, blockIdx.y);
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= a.num_work) return;
+  const int k = a.seg_begin + blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= a.seg_end) return;
   tri_syncfree_output(a, k, *a.top);
 }
 
@@ -519,11 +576,165 @@ __global__ __launch_bounds__(kTriThreads) void tri_syncfree_persistent_kernel(Tr
   }
 }
 
+// A narrow segment of the schedule (positions [seg_begin, seg_end), levels
+// unpadded) on one workgroup per right-hand side: a hand-off between two of
+// its outputs is an LDS store and load inside one CU (a fraction of a
+// microsecond) instead of a trip through the L2s of two XCDs. Thread t walks
+// the segment's positions t, t + T, ... in order; every output reads lower
+// positions only, so the lowest unfinished output is always computable and
+// all waits end (one workgroup, all its waves resident). Each output is
+// evaluated exactly as tri_syncfree_output evaluates it (same operations in
+// the same order, long outputs folding as their inputs arrive); earlier
+// segments are final in y, and the outputs go to y for later ones.
+__device__ __forceinline__ double tri_chain_load(const TriSolveArgs& a, const double* vals,
+                                                 int p) {
+  if (p >= a.seg_begin && p < a.seg_end) {
+    return __hip_atomic_load(vals + (p - a.seg_begin), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  return load_final(a.y, p);
+}
+
+__global__ __launch_bounds__(kTriThreads) void tri_chain_kernel(TriSolveArgs a0) {
+  const TriSolveArgs a = TriRhs(a0, blockIdx.y);
+  __shared__ double vals[kTriChainVals];
+  const int cs = a.seg_begin;
+  const int ce = a.seg_end;
+  const int top = *a.top;
+  const double pending = __longlong_as_double(static_cast<long long>(kTriPending));
+  for (int k = cs + threadIdx.x; k < ce; k += kTriThreads) {
+    const int row = a.rec_row[k];
+    vals[k - cs] = row <= top ? pending : a.x[min(row, a.num_rows - 1)];
+  }
+  __syncthreads();
+  int k = cs + threadIdx.x;
+  TriRec r;
+  bool have = false;
+  double sum = 0.0;
+  int e = 0, end = 0;
+  int wpos[8];
+  double wval[8];
+  uint64_t t_progress = wall_clock64();
+  int polls = 0;
+  while (true) {
+    if (!have) {
+      if (k >= ce) break;
+      tri_load(a, k, ce, top, &r);
+      if (r.row > top) {  // not computed: vals holds x[row]
+        k += kTriThreads;
+        continue;
+      }
+      sum = a.x[r.row];
+      have = true;
+      if (r.n > 4) {
+        e = r.e.x;
+        end = r.e.x + r.n;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          wpos[i] = e + i < end ? a.ovf_pos[e + i] : 0;
+          wval[i] = e + i < end ? a.ovf_value[e + i] : 0.0;
+        }
+      }
+    }
+    bool finished = false;
+    bool progress = false;
+    double out = 0.0;
+    if (r.n <= 4) {
+      const int n = r.n;
+      const double y0 = n > 0 ? tri_chain_load(a, vals, r.e.x) : 0.0;
+      const double y1 = n > 1 ? tri_chain_load(a, vals, r.e.y) : 0.0;
+      const double y2 = n > 2 ? tri_chain_load(a, vals, r.e.z) : 0.0;
+      const double y3 = n > 3 ? tri_chain_load(a, vals, r.e.w) : 0.0;
+      if (!(tri_pending(y0) || tri_pending(y1) || tri_pending(y2) || tri_pending(y3))) {
+        out = tri_apply4(a, sum, r, y0, y1, y2, y3);
+        finished = true;
+      }
+    } else {
+      // The window [e, e + 8) of entries sits in registers; a poll reloads
+      // only the values.
+      double v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = e + i < end ? tri_chain_load(a, vals, wpos[i]) : 0.0;
+      int took = 0;
+      if (a.sequential) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (took != i || e + i >= end || tri_pending(v[i])) continue;
+          if (v[i] != 0.0) sum -= v[i] * wval[i];
+          took = i + 1;
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 8; g += 4) {
+          if (took != g || e + g + 3 >= end) continue;
+          if (tri_pending(v[g]) || tri_pending(v[g + 1]) || tri_pending(v[g + 2]) ||
+              tri_pending(v[g + 3])) {
+            continue;
+          }
+          sum -= wval[g] * v[g] + wval[g + 1] * v[g + 1] + wval[g + 2] * v[g + 2] +
+                 wval[g + 3] * v[g + 3];
+          took = g + 4;
+        }
+        const int left = end - e - took;
+        if (took < 8 && left > 0 && left < 4) {
+          const int t = took;
+          bool ready = true;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            if (i < left && t + i < 8) ready = ready && !tri_pending(v[t + i]);
+          }
+          if (ready && t + left <= 8) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+              if (i < left) sum -= wval[t + i] * v[t + i];
+            }
+            took = t + left;
+          }
+        }
+      }
+      if (took > 0) {
+        e += took;
+        progress = true;
+        if (e == end) {
+          out = a.sequential ? tri_sequential_divide(a, sum, r.d)
+                             : (a.diag != nullptr ? sum / r.d : sum);
+          finished = true;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            wpos[i] = e + i < end ? a.ovf_pos[e + i] : 0;
+            wval[i] = e + i < end ? a.ovf_value[e + i] : 0.0;
+          }
+        }
+      }
+    }
+    if (finished) {
+      __hip_atomic_store(vals + (k - cs), out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(a.y + k, out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.x[r.row] = out;  // the scatter, fused
+      have = false;
+      k += kTriThreads;
+      progress = true;
+    }
+    if (progress) {
+      polls = 0;
+    } else if (++polls % 64 == 0) {
+      const uint64_t now = wall_clock64();
+      if (polls == 64) t_progress = now;  // first stalled check of this wait
+      if (now - t_progress > kTriMaxWaitTicks) {
+        if (a.fail != nullptr) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+}
+
 }  // namespace milp_kernels
 
 namespace milp_launch {
 
-hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, hipStream_t s,
+hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args,
+                                        const int* segs, int num_segs, hipStream_t s,
                                         int num_rhs) {
   if (args.num_work <= 0) return hipSuccess;
   const int row_blocks =
@@ -538,12 +749,23 @@ hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args, 
   milp_kernels::tri_init_kernel<<<dim3(pos_blocks, num_rhs), 256, 0, s>>>(args);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // One thread per listed output and right-hand side: every workgroup
-  // resident (100k outputs = 391 workgroups of 256 per vector on 256 CUs).
-  milp_kernels::tri_syncfree_kernel<<<dim3((args.num_work + 255) / 256, num_rhs), 256, 0, s>>>(
-      args);
-  e = hipGetLastError();
-  if (e != hipSuccess || args.host_x == nullptr) return e;
+  milp_kernels::TriSolveArgs a = args;
+  for (int i = 0; i < num_segs; ++i) {
+    a.seg_begin = segs[3 * i];
+    a.seg_end = segs[3 * i + 1];
+    if (a.seg_end <= a.seg_begin) continue;
+    if (segs[3 * i + 2] != 0) {
+      milp_kernels::tri_chain_kernel<<<dim3(1, num_rhs), milp_kernels::kTriThreads, 0, s>>>(a);
+    } else {
+      // One thread per listed output and right-hand side: every workgroup
+      // resident (100k outputs = 391 workgroups of 256 per vector on 256 CUs).
+      milp_kernels::tri_syncfree_kernel<<<dim3((a.seg_end - a.seg_begin + 255) / 256, num_rhs),
+                                          256, 0, s>>>(a);
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (args.host_x == nullptr) return hipSuccess;
   milp_kernels::tri_copy_out_kernel<<<dim3(row_blocks, num_rhs), 256, 0, s>>>(args);
   return hipGetLastError();
 }

@@ -80,7 +80,13 @@ def main():
                           for k, v in st.items() if v["launches"] or v["call_ms"]}
         log(f"gpu: {done} iterations in {dt:.3f}s ({res['gpu_it_per_s']} it/s)")
         h.stop()
-        h.finish()
+        r = h.finish()
+        res["status"] = int(r.problem_status)
+        res["error_code"] = int(r.error_code)
+        res["iterations_total"] = int(r.iterations)
+        if fin or fin2:
+            log(f"solve ended early: status {r.problem_status} error {r.error_code} after {r.iterations} iterations, "
+                f"error: {h.last_error() if hasattr(h, 'last_error') else ''}")
         del h
         for k in env:
             os.environ.pop(k, None)

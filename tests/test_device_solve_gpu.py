@@ -35,6 +35,9 @@ def _cases():
     cases.append(("sparse_primal", lambda: lp_gen.random_sparse_lp(200, 900, 0.04, 75), 0))
     cases.append(("dense_primal", lambda: lp_gen.dense_box_lp(97, 400, 76), 0))
     cases.append(("dense_dual", lambda: lp_gen.dense_box_lp(120, 600, 77), 1))
+    # A deep chain of long outputs (a dense bump of a few hundred columns):
+    # each output folds its groups as its inputs arrive.
+    cases.append(("dense_deep", lambda: lp_gen.dense_box_lp(320, 1280, 78), 1))
     return cases
 
 
@@ -45,6 +48,10 @@ VARIANTS = {
     "syncfree_copies": {"MILP_TRI_MAPPED": "0"},
     "persistent_xcd": {"MILP_TRI_PERSIST": "32", "MILP_TRI_XCD": "1", "MILP_TRI_POLL_MAX": "8"},
     "persistent_chip": {"MILP_TRI_PERSIST": "64", "MILP_TRI_POLL_MAX": "4"},
+    # Every level chip-wide (no single-workgroup narrow segments), and
+    # narrow segments of any width (long runs cut at the LDS capacity).
+    "no_chain": {"MILP_TRI_CHAIN": "0"},
+    "wide_chain": {"MILP_TRI_CHAIN_WIDTH": "100000", "MILP_TRI_CHAIN_MIN_LEVELS": "1"},
 }
 
 
@@ -53,7 +60,7 @@ VARIANTS = {
 _PARAMS = [(c, "syncfree") for c in _cases()] + [
     (c, v) for c in _cases() if c[0] in ("c5_71", "dense_dual")
     for v in ("levels", "levels_copies", "syncfree_copies", "persistent_xcd",
-              "persistent_chip")]
+              "persistent_chip", "no_chain", "wide_chain")]
 
 
 @pytest.mark.parametrize("case,variant", _PARAMS, ids=lambda x: x if isinstance(x, str) else x[0])
