@@ -1,0 +1,1706 @@
+// Device-resident dual simplex segment: the algorithms.
+//
+// One restatement, compiled twice: by g++ into the host engine (the CPU
+// checks and MILP_SDUAL=host) and by hipcc into the gfx950 kernel
+// (sdual_kernel.hip). Each function follows the Glop function named in its
+// comment with the same floating-point evaluation order, so the device run is
+// bit-identical to the host engine and to the oracle. Compiled with
+// -ffp-contract=off everywhere.
+#ifndef MILP_SDUAL_CORE_H_
+#define MILP_SDUAL_CORE_H_
+
+#include "sdual_state.h"
+
+#if !defined(__HIPCC__)
+#include <cmath>
+#endif
+
+namespace sdual {
+
+constexpr int kInvalid = -1;
+// lp_types.h VariableStatus / VariableType
+constexpr int8_t kBasic = 0, kFixedValue = 1, kAtLower = 2, kAtUpper = 3, kFree = 4;
+constexpr int8_t kUnconstrained = 0, kLowerBounded = 1, kUpperBounded = 2, kBoxed = 3,
+                 kFixedVariable = 4;
+
+SD_INLINE f64 sd_inf() { return __builtin_inf(); }
+SD_INLINE f64 sd_dbl_max() { return 1.7976931348623157e308; }
+SD_INLINE f64 sd_fabs(f64 v) { return __builtin_fabs(v); }
+SD_INLINE f64 sd_sqrt(f64 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_sqrt(v);
+#else
+  return std::sqrt(v);
+#endif
+}
+// std::max / std::min exactly (NaN and signed-zero behaviour included).
+SD_INLINE f64 sd_max(f64 a, f64 b) { return (a < b) ? b : a; }
+SD_INLINE f64 sd_min(f64 a, f64 b) { return (b < a) ? b : a; }
+SD_INLINE f64 sq(f64 v) { return v * v; }
+SD_INLINE f64 dt_ops(int64_t n) { return 2e-9 * static_cast<f64>(n); }
+
+// ---- Bitset64 ----
+SD_INLINE bool bit_get(const uint64_t* w, int i) { return (w[i >> 6] >> (i & 63)) & 1; }
+SD_INLINE void bit_set(uint64_t* w, int i) { w[i >> 6] |= (1ull << (i & 63)); }
+SD_INLINE void bit_clear(uint64_t* w, int i) { w[i >> 6] &= ~(1ull << (i & 63)); }
+SD_INLINE void bit_put(uint64_t* w, int i, bool v) {
+  if (v) bit_set(w, i); else bit_clear(w, i);
+}
+SD_INLINE int sd_ctz(uint64_t v) { return __builtin_ctzll(v); }
+
+// ---- std::mt19937_64, libstdc++ state layout ----
+SD_INLINE uint64_t mt_next(Lp& s) {
+  const int n = 312, mm = 156;
+  const uint64_t upper = ~((1ull << 31) - 1), lower = (1ull << 31) - 1;
+  if (s.mti >= 312) {
+    for (int k = 0; k < n - mm; ++k) {
+      const uint64_t y = (s.mt[k] & upper) | (s.mt[k + 1] & lower);
+      s.mt[k] = s.mt[k + mm] ^ (y >> 1) ^ ((y & 1) ? 0xb5026f5aa96619e9ull : 0);
+    }
+    for (int k = n - mm; k < n - 1; ++k) {
+      const uint64_t y = (s.mt[k] & upper) | (s.mt[k + 1] & lower);
+      s.mt[k] = s.mt[k + (mm - n)] ^ (y >> 1) ^ ((y & 1) ? 0xb5026f5aa96619e9ull : 0);
+    }
+    const uint64_t y = (s.mt[n - 1] & upper) | (s.mt[0] & lower);
+    s.mt[n - 1] = s.mt[mm - 1] ^ (y >> 1) ^ ((y & 1) ? 0xb5026f5aa96619e9ull : 0);
+    s.mti = 0;
+  }
+  uint64_t z = s.mt[s.mti++];
+  z ^= (z >> 29) & 0x5555555555555555ull;
+  z ^= (z << 17) & 0x71d67fffeda60000ull;
+  z ^= (z << 37) & 0xfff7eee000000000ull;
+  z ^= (z >> 43);
+  return z;
+}
+
+SD_INLINE void mul64(uint64_t a, uint64_t b, uint64_t* hi, uint64_t* lo) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  *hi = __umul64hi(a, b);
+  *lo = a * b;
+#else
+  const unsigned __int128 p = static_cast<unsigned __int128>(a) * b;
+  *hi = static_cast<uint64_t>(p >> 64);
+  *lo = static_cast<uint64_t>(p);
+#endif
+}
+
+// std::uniform_int_distribution<int>(0, hi)(mt19937_64): libstdc++ (GCC 11)
+// takes _S_nd<unsigned __int128> (Lemire) for a full 64-bit generator.
+SD_INLINE int uniform_int(Lp& s, int hi) {
+  const uint64_t range = static_cast<uint64_t>(hi) + 1;
+  uint64_t ph, pl;
+  mul64(mt_next(s), range, &ph, &pl);
+  if (pl < range) {
+    const uint64_t threshold = (0ull - range) % range;
+    while (pl < threshold) mul64(mt_next(s), range, &ph, &pl);
+  }
+  return static_cast<int>(ph);
+}
+
+// absl::Bernoulli as restated by the oracle (oracle_simplex.h AbslBernoulli).
+SD_INLINE bool bernoulli(Lp& s, f64 p) {
+  const f64 kP32 = 4294967296.0;
+  while (true) {
+    const uint64_t c = static_cast<uint64_t>(static_cast<int64_t>(p * kP32));
+    const uint32_t v = static_cast<uint32_t>(mt_next(s));
+    if (v != c) return v < c;
+    const f64 q = static_cast<f64>(c) / kP32;
+    const f64 here = (p - q) * kP32;
+    if (here == 0) return false;
+    p = here;
+  }
+}
+
+// std::sort of distinct-or-not ints: any correct sort gives the same result.
+SD_INLINE void sort_ints(int32_t* a, int n) {
+  if (n < 2) return;
+  if (n <= 24) {
+    for (int i = 1; i < n; ++i) {
+      const int32_t v = a[i];
+      int j = i - 1;
+      while (j >= 0 && a[j] > v) {
+        a[j + 1] = a[j];
+        --j;
+      }
+      a[j + 1] = v;
+    }
+    return;
+  }
+  // heap sort
+  for (int start = (n - 2) / 2; start >= 0; --start) {
+    int root = start;
+    while (2 * root + 1 < n) {
+      int child = 2 * root + 1;
+      if (child + 1 < n && a[child] < a[child + 1]) ++child;
+      if (a[root] < a[child]) {
+        const int32_t t = a[root]; a[root] = a[child]; a[child] = t;
+        root = child;
+      } else {
+        break;
+      }
+    }
+  }
+  for (int end = n - 1; end > 0; --end) {
+    const int32_t t = a[0]; a[0] = a[end]; a[end] = t;
+    int root = 0;
+    while (2 * root + 1 < end) {
+      int child = 2 * root + 1;
+      if (child + 1 < end && a[child] < a[child + 1]) ++child;
+      if (a[root] < a[child]) {
+        const int32_t u = a[root]; a[root] = a[child]; a[child] = u;
+        root = child;
+      } else {
+        break;
+      }
+    }
+  }
+}
+
+// ---- ScatteredVector helpers (scattered_vector.h, lp_utils.h) ----
+SD_INLINE bool vec_dense(const Vec& v, f64 ratio) {
+  if (v.nnz == 0) return true;
+  return static_cast<f64>(v.nnz) > ratio * static_cast<f64>(v.size);
+}
+SD_INLINE void vec_clear_mask(Vec& v) {
+  if (vec_dense(v, 0.8)) {
+    for (int i = 0; i < v.size; ++i) v.mask[i] = 0;
+  } else {
+    for (int k = 0; k < v.nnz; ++k) v.mask[v.nz[k]] = 0;
+  }
+}
+SD_INLINE void vec_repopulate_mask(Vec& v) {
+  vec_clear_mask(v);
+  for (int k = 0; k < v.nnz; ++k) v.mask[v.nz[k]] = 1;
+}
+SD_INLINE void vec_clear_nz_if_too_dense(Vec& v, f64 ratio) {
+  if (vec_dense(v, ratio)) {
+    vec_clear_mask(v);
+    v.nnz = 0;
+  }
+}
+SD_INLINE void vec_add(Vec& v, int i, f64 value) {
+  v.values[i] += value;
+  if (!v.mask[i] && value != 0.0) {
+    v.mask[i] = 1;
+    v.nz[v.nnz++] = i;
+    v.sorted = 0;
+  }
+}
+SD_INLINE void vec_sort_if_needed(Vec& v) {
+  if (!v.sorted) {
+    sort_ints(v.nz, v.nnz);
+    v.sorted = 1;
+  }
+}
+SD_INLINE int64_t vec_nnz_estimate(const Vec& v) { return v.nnz == 0 ? v.size : v.nnz; }
+// lp_utils.h:281-299 (the size is always m here).
+SD_INLINE void vec_clear_and_resize(Vec& v, int size) {
+  if (v.nnz != 0 && static_cast<f64>(v.nnz) < 0.05 * static_cast<f64>(size)) {
+    for (int k = 0; k < v.nnz; ++k) v.values[v.nz[k]] = 0.0;
+    for (int i = v.size; i < size; ++i) v.values[i] = 0.0;
+  } else {
+    for (int i = 0; i < size; ++i) v.values[i] = 0.0;
+  }
+  v.size = size;
+  v.nnz = 0;
+}
+SD_INLINE void vec_copy(Vec& dst, const Vec& src) {  // *x = b
+  for (int i = 0; i < src.size; ++i) dst.values[i] = src.values[i];
+  dst.size = src.size;
+  for (int k = 0; k < src.nnz; ++k) dst.nz[k] = src.nz[k];
+  dst.nnz = src.nnz;
+  dst.sorted = src.sorted;
+  for (int i = 0; i < src.size; ++i) dst.mask[i] = src.mask[i];
+}
+// lp_utils.cc:62-75 and :46-54
+SD_INLINE f64 dense_squared_norm(const f64* c, int n) {
+  f64 sum = 0.0;
+  int r = 0;
+  const int blocks = n / 4;
+  for (int b = 0; b < blocks; ++b) {
+    sum += sq(c[r]) + sq(c[r + 1]) + sq(c[r + 2]) + sq(c[r + 3]);
+    r += 4;
+  }
+  while (r < n) {
+    sum += sq(c[r]);
+    ++r;
+  }
+  return sum;
+}
+SD_INLINE f64 vec_squared_norm(const Vec& v) {
+  if (vec_dense(v, 0.8)) return dense_squared_norm(v.values, v.size);
+  f64 sum = 0.0;
+  for (int k = 0; k < v.nnz; ++k) sum += sq(v.values[v.nz[k]]);
+  return sum;
+}
+
+// ---- CompactSparseMatrix column ops ----
+// sparse.h:514-542
+template <typename M>
+SD_INLINE f64 col_dot(const M& a, int col, const f64* v) {
+  int64_t i = a.starts[col];
+  const int64_t end = a.starts[col + 1];
+  const int64_t shifted_end = end - 3;
+  f64 r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0;
+  for (; i < shifted_end; i += 4) {
+    r1 += a.coefs[i] * v[a.rows[i]];
+    r2 += a.coefs[i + 1] * v[a.rows[i + 1]];
+    r3 += a.coefs[i + 2] * v[a.rows[i + 2]];
+    r4 += a.coefs[i + 3] * v[a.rows[i + 3]];
+  }
+  f64 result = r1 + r2 + r3 + r4;
+  if (i < end) {
+    result += a.coefs[i] * v[a.rows[i]];
+    if (i + 1 < end) {
+      result += a.coefs[i + 1] * v[a.rows[i + 1]];
+      if (i + 2 < end) result += a.coefs[i + 2] * v[a.rows[i + 2]];
+    }
+  }
+  return result;
+}
+template <typename M>
+SD_INLINE int64_t col_entries(const M& a, int col) {
+  return a.starts[col + 1] - a.starts[col];
+}
+// sparse.h:389-399
+template <typename M>
+SD_INLINE void col_add_dense(const M& a, int col, f64 mult, f64* dense) {
+  if (mult == 0.0) return;
+  for (int64_t i = a.starts[col]; i < a.starts[col + 1]; ++i)
+    dense[a.rows[i]] += mult * a.coefs[i];
+}
+// sparse.h:403-413
+template <typename M>
+SD_INLINE void col_add_scattered(const M& a, int col, f64 mult, Vec& c) {
+  if (mult == 0.0) return;
+  for (int64_t i = a.starts[col]; i < a.starts[col + 1]; ++i)
+    vec_add(c, a.rows[i], mult * a.coefs[i]);
+}
+
+// ---- growing storage (sparse.cc:576-623) ----
+SD_INLINE int store_add_dense_prefix(Store& st, const f64* d, int n, int start) {
+  int64_t e = st.starts[st.num_cols];
+  for (int r = start; r < n; ++r) {
+    if (d[r] != 0.0) {
+      st.rows[e] = r;
+      st.coefs[e] = d[r];
+      ++e;
+    }
+  }
+  st.starts[st.num_cols + 1] = e;
+  return st.num_cols++;
+}
+SD_INLINE int store_add_dense_nz(Store& st, const f64* d, int n, const int32_t* nz, int nnz) {
+  if (nnz == 0) return store_add_dense_prefix(st, d, n, 0);
+  int64_t e = st.starts[st.num_cols];
+  for (int k = 0; k < nnz; ++k) {
+    const int r = nz[k];
+    if (d[r] != 0.0) {
+      st.rows[e] = r;
+      st.coefs[e] = d[r];
+      ++e;
+    }
+  }
+  st.starts[st.num_cols + 1] = e;
+  return st.num_cols++;
+}
+SD_INLINE int store_add_and_clear(Store& st, f64* col, int32_t* nz, int* nnz) {
+  int64_t e = st.starts[st.num_cols];
+  for (int k = 0; k < *nnz; ++k) {
+    const int r = nz[k];
+    const f64 v = col[r];
+    if (v != 0.0) {
+      st.rows[e] = r;
+      st.coefs[e] = v;
+      col[r] = 0.0;
+      ++e;
+    }
+  }
+  *nnz = 0;
+  st.starts[st.num_cols + 1] = e;
+  return st.num_cols++;
+}
+// ColumnCopyToClearedDenseColumnWithNonZeros (sparse.h:440-455)
+SD_INLINE void store_copy_to_vec(const Store& st, int col, Vec& v) {
+  v.nnz = 0;
+  for (int64_t i = st.starts[col]; i < st.starts[col + 1]; ++i) {
+    v.values[st.rows[i]] = st.coefs[i];
+    v.nz[v.nnz++] = st.rows[i];
+  }
+}
+
+// ---- TriangularMatrix solves (sparse.cc:776-1128) ----
+SD_INLINE void tri_lower_solve_from(const Tri& t, int start, f64* x) {
+  const int begin = start > t.first_non_identity ? start : t.first_non_identity;
+  const int end = t.num_cols;
+  const bool ones = t.all_ones;
+  for (int col = begin; col < end; ++col) {
+    const f64 value = x[col];
+    if (value == 0.0) continue;
+    const f64 coeff = ones ? value : value / t.diag[col];
+    if (!ones) x[col] = coeff;
+    for (int64_t i = t.starts[col]; i < t.starts[col + 1]; ++i)
+      x[t.rows[i]] -= coeff * t.coefs[i];
+  }
+}
+SD_INLINE void tri_upper_solve(const Tri& t, f64* x) {
+  const int end = t.first_non_identity;
+  const bool ones = t.all_ones;
+  for (int col = t.num_cols - 1; col >= end; --col) {
+    const f64 value = x[col];
+    if (value == 0.0) continue;
+    const f64 coeff = ones ? value : value / t.diag[col];
+    if (!ones) x[col] = coeff;
+    for (int64_t i = t.starts[col + 1] - 1; i >= t.starts[col]; --i)
+      x[t.rows[i]] -= coeff * t.coefs[i];
+  }
+}
+SD_INLINE void tri_transpose_upper_solve(const Tri& t, f64* x) {
+  const int end = t.num_cols;
+  const bool ones = t.all_ones;
+  int64_t i = t.starts[t.first_non_identity];
+  for (int col = t.first_non_identity; col < end; ++col) {
+    f64 sum = x[col];
+    const int64_t i_end = t.starts[col + 1];
+    const int64_t shifted_end = i_end - 3;
+    for (; i < shifted_end; i += 4) {
+      sum -= t.coefs[i] * x[t.rows[i]] + t.coefs[i + 1] * x[t.rows[i + 1]] +
+             t.coefs[i + 2] * x[t.rows[i + 2]] + t.coefs[i + 3] * x[t.rows[i + 3]];
+    }
+    if (i < i_end) {
+      sum -= t.coefs[i] * x[t.rows[i]];
+      if (i + 1 < i_end) {
+        sum -= t.coefs[i + 1] * x[t.rows[i + 1]];
+        if (i + 2 < i_end) sum -= t.coefs[i + 2] * x[t.rows[i + 2]];
+      }
+      i = i_end;
+    }
+    x[col] = ones ? sum : sum / t.diag[col];
+  }
+}
+SD_INLINE void tri_transpose_lower_solve(const Tri& t, f64* x) {
+  const int end = t.first_non_identity;
+  int col = t.num_cols - 1;
+  while (col >= end && x[col] == 0.0) --col;
+  const bool ones = t.all_ones;
+  int64_t i = t.starts[col + 1] - 1;
+  for (; col >= end; --col) {
+    f64 sum = x[col];
+    const int64_t i_end = t.starts[col];
+    const int64_t shifted_end = i_end + 3;
+    for (; i >= shifted_end; i -= 4) {
+      sum -= t.coefs[i] * x[t.rows[i]] + t.coefs[i - 1] * x[t.rows[i - 1]] +
+             t.coefs[i - 2] * x[t.rows[i - 2]] + t.coefs[i - 3] * x[t.rows[i - 3]];
+    }
+    if (i >= i_end) {
+      sum -= t.coefs[i] * x[t.rows[i]];
+      if (i >= i_end + 1) {
+        sum -= t.coefs[i - 1] * x[t.rows[i - 1]];
+        if (i >= i_end + 2) sum -= t.coefs[i - 2] * x[t.rows[i - 2]];
+      }
+      i = i_end - 1;
+    }
+    x[col] = ones ? sum : sum / t.diag[col];
+  }
+}
+SD_INLINE void tri_hyper_solve(const Tri& t, f64* x, int32_t* nz, int* nnz) {
+  const bool ones = t.all_ones;
+  int new_size = 0;
+  for (int k = 0; k < *nnz; ++k) {
+    const int row = nz[k];
+    if (x[row] == 0.0) continue;
+    const f64 coeff = ones ? x[row] : x[row] / t.diag[row];
+    x[row] = coeff;
+    for (int64_t i = t.starts[row]; i < t.starts[row + 1]; ++i)
+      x[t.rows[i]] -= coeff * t.coefs[i];
+    nz[new_size++] = row;
+  }
+  *nnz = new_size;
+}
+SD_INLINE void erase_prefix(int32_t* nz, int* nnz, int new_start) {
+  const int n = *nnz - new_start;
+  for (int k = 0; k < n; ++k) nz[k] = nz[new_start + k];
+  *nnz = n;
+}
+SD_INLINE void tri_hyper_solve_rev(const Tri& t, f64* x, int32_t* nz, int* nnz) {
+  const bool ones = t.all_ones;
+  int new_start = *nnz;
+  for (int k = *nnz - 1; k >= 0; --k) {
+    const int row = nz[k];
+    if (x[row] == 0.0) continue;
+    const f64 coeff = ones ? x[row] : x[row] / t.diag[row];
+    x[row] = coeff;
+    for (int64_t i = t.starts[row]; i < t.starts[row + 1]; ++i)
+      x[t.rows[i]] -= coeff * t.coefs[i];
+    nz[--new_start] = row;
+  }
+  erase_prefix(nz, nnz, new_start);
+}
+SD_INLINE void tri_transpose_hyper_solve(const Tri& t, f64* x, int32_t* nz, int* nnz) {
+  const bool ones = t.all_ones;
+  int new_size = 0;
+  for (int k = 0; k < *nnz; ++k) {
+    const int row = nz[k];
+    f64 sum = x[row];
+    int64_t i = t.starts[row];
+    const int64_t i_end = t.starts[row + 1];
+    const int64_t shifted_end = i_end - 3;
+    for (; i < shifted_end; i += 4) {
+      sum -= t.coefs[i] * x[t.rows[i]] + t.coefs[i + 1] * x[t.rows[i + 1]] +
+             t.coefs[i + 2] * x[t.rows[i + 2]] + t.coefs[i + 3] * x[t.rows[i + 3]];
+    }
+    if (i < i_end) {
+      sum -= t.coefs[i] * x[t.rows[i]];
+      if (i + 1 < i_end) {
+        sum -= t.coefs[i + 1] * x[t.rows[i + 1]];
+        if (i + 2 < i_end) sum -= t.coefs[i + 2] * x[t.rows[i + 2]];
+      }
+    }
+    x[row] = ones ? sum : sum / t.diag[row];
+    if (sum != 0.0) nz[new_size++] = row;
+  }
+  *nnz = new_size;
+}
+SD_INLINE void tri_transpose_hyper_solve_rev(const Tri& t, f64* x, int32_t* nz, int* nnz) {
+  const bool ones = t.all_ones;
+  int new_start = *nnz;
+  for (int k = *nnz - 1; k >= 0; --k) {
+    const int row = nz[k];
+    f64 sum = x[row];
+    int64_t i = t.starts[row + 1] - 1;
+    const int64_t i_end = t.starts[row];
+    const int64_t shifted_end = i_end + 3;
+    for (; i >= shifted_end; i -= 4) {
+      sum -= t.coefs[i] * x[t.rows[i]] + t.coefs[i - 1] * x[t.rows[i - 1]] +
+             t.coefs[i - 2] * x[t.rows[i - 2]] + t.coefs[i - 3] * x[t.rows[i - 3]];
+    }
+    if (i >= i_end) {
+      sum -= t.coefs[i] * x[t.rows[i]];
+      if (i >= i_end + 1) {
+        sum -= t.coefs[i - 1] * x[t.rows[i - 1]];
+        if (i >= i_end + 2) sum -= t.coefs[i - 2] * x[t.rows[i - 2]];
+      }
+    }
+    x[row] = ones ? sum : sum / t.diag[row];
+    if (sum != 0.0) nz[--new_start] = row;
+  }
+  erase_prefix(nz, nnz, new_start);
+}
+// sparse.cc:1445-1492 (ComputeRowsToConsiderInSortedOrder; the ratio
+// arguments are ignored upstream).
+SD_INLINE void tri_rows_to_consider(const Tri& t, int32_t* nz, int* nnz, char* stored) {
+  if (*nnz == 0) return;
+  const int sparsity_threshold = static_cast<int>(0.025 * t.num_rows);
+  const int num_ops_threshold = static_cast<int>(0.05 * t.num_rows);
+  int num_ops = *nnz;
+  if (num_ops > sparsity_threshold) {
+    *nnz = 0;
+    return;
+  }
+  for (int k = 0; k < *nnz; ++k) stored[nz[k]] = 1;
+  for (int k = 0; k < *nnz; ++k) {
+    const int row = nz[k];
+    for (int64_t i = t.starts[row]; i < t.starts[row + 1]; ++i) {
+      ++num_ops;
+      const int er = t.rows[i];
+      if (!stored[er]) {
+        nz[(*nnz)++] = er;
+        stored[er] = 1;
+      }
+    }
+    if (num_ops > num_ops_threshold) break;
+  }
+  for (int k = 0; k < *nnz; ++k) stored[nz[k]] = 0;
+  if (num_ops > num_ops_threshold) {
+    *nnz = 0;
+  } else {
+    sort_ints(nz, *nnz);
+  }
+}
+SD_INLINE int64_t tri_num_entries(const Tri& t) {
+  return static_cast<int64_t>(t.num_cols) + t.ncoefs;
+}
+
+// ---- LuFactorization (lu_factorization.cc:200-454) ----
+// lp_utils.h:240-277. `values` and the zero scratchpad swap buffers.
+SD_INLINE void permute_with_scratchpad(Lp& s, const int32_t* perm, Vec& io) {
+  f64* old = io.values;
+  io.values = s.zero_scratch;
+  s.zero_scratch = old;
+  const int size = io.size;
+  for (int i = 0; i < size; ++i) io.values[i] = 0.0;  // resize(size, 0.0) of an all-zero buffer
+  for (int i = 0; i < size; ++i) {
+    const f64 v = s.zero_scratch[i];
+    if (v != 0.0) io.values[perm[i]] = v;
+  }
+  for (int i = 0; i < size; ++i) s.zero_scratch[i] = 0.0;
+}
+SD_INLINE void permute_with_known_nz(Lp& s, const int32_t* perm, Vec& io) {
+  f64* old = io.values;
+  io.values = s.zero_scratch;
+  s.zero_scratch = old;
+  for (int k = 0; k < io.nnz; ++k) {
+    const int ref = io.nz[k];
+    const f64 v = s.zero_scratch[ref];
+    s.zero_scratch[ref] = 0.0;
+    const int p = perm[ref];
+    io.values[p] = v;
+    io.nz[k] = p;
+  }
+}
+SD_INLINE void lu_right_solve_l_permuted_input(Lp& s, Vec& x) {
+  if (s.is_identity) return;
+  tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored);
+  if (x.nnz == 0) {
+    tri_lower_solve_from(s.lower, 0, x.values);
+  } else {
+    tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz);
+  }
+}
+// RightSolveLInternal (lu_factorization.cc:214-243); the rhs is a matrix
+// column (rows/coefs/n) or a scattered vector's list.
+SD_INLINE void lu_right_solve_l_internal(Lp& s, const int32_t* brows, const f64* bcoefs,
+                                          const f64* bvalues, int bn, Vec& x) {
+  int first = x.size;
+  const int limit = s.lower.first_non_identity;
+  for (int k = 0; k < bn; ++k) {
+    const int r = brows[k];
+    const int permuted_row = s.row_perm[r];
+    x.values[permuted_row] = bcoefs != nullptr ? bcoefs[k] : bvalues[r];
+    x.nz[x.nnz++] = permuted_row;
+    const int col = permuted_row;
+    if (col < limit || s.lower.starts[col + 1] == s.lower.starts[col]) continue;
+    first = first < col ? first : col;
+  }
+  tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored);
+  x.sorted = 1;
+  if (x.nnz == 0) {
+    tri_lower_solve_from(s.lower, first, x.values);
+  } else {
+    tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz);
+  }
+}
+SD_INLINE void lu_right_solve_l_for_column(Lp& s, int col, Vec& x) {
+  x.nnz = 0;
+  const int64_t b = s.A.starts[col], e = s.A.starts[col + 1];
+  if (s.is_identity) {
+    for (int64_t i = b; i < e; ++i) {
+      x.values[s.A.rows[i]] = s.A.coefs[i];
+      x.nz[x.nnz++] = s.A.rows[i];
+    }
+    return;
+  }
+  lu_right_solve_l_internal(s, s.A.rows + b, s.A.coefs + b, nullptr, static_cast<int>(e - b), x);
+}
+SD_INLINE void lu_right_solve_l_with_nz(Lp& s, Vec& x) {
+  if (s.is_identity) return;
+  if (x.nnz == 0) {
+    permute_with_scratchpad(s, s.row_perm, x);
+    tri_lower_solve_from(s.lower, 0, x.values);
+    return;
+  }
+  permute_with_known_nz(s, s.row_perm, x);
+  tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored);
+  x.sorted = 1;
+  if (x.nnz == 0) {
+    tri_lower_solve_from(s.lower, 0, x.values);
+  } else {
+    tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz);
+  }
+}
+SD_INLINE void lu_right_solve_l_for_scattered(Lp& s, const Vec& b, Vec& x) {
+  x.nnz = 0;
+  if (s.is_identity) {
+    vec_copy(x, b);
+    return;
+  }
+  if (b.nnz == 0) {
+    vec_copy(x, b);
+    lu_right_solve_l_with_nz(s, x);
+    return;
+  }
+  lu_right_solve_l_internal(s, b.nz, nullptr, b.values, b.nnz, x);
+}
+SD_INLINE void lu_right_solve_u_with_nz(Lp& s, Vec& x) {
+  if (s.is_identity) return;
+  tri_rows_to_consider(s.upper, x.nz, &x.nnz, s.stored);
+  x.sorted = 1;
+  if (x.nnz == 0) {
+    tri_transpose_lower_solve(s.tupper, x.values);
+  } else {
+    tri_transpose_hyper_solve_rev(s.tupper, x.values, x.nz, &x.nnz);
+  }
+}
+// LeftSolveLWithNonZeros (lu_factorization.cc:333-399); `before` is tau_
+// (result_before_permutation) or null. Returns true when `before` was filled.
+SD_INLINE bool lu_left_solve_l_with_nz(Lp& s, Vec& y, Vec* before) {
+  if (s.is_identity) return false;
+  tri_rows_to_consider(s.tlower, y.nz, &y.nnz, s.stored);
+  y.sorted = 1;
+  if (y.nnz == 0) {
+    tri_transpose_lower_solve(s.lower, y.values);
+  } else {
+    tri_transpose_hyper_solve_rev(s.lower, y.values, y.nz, &y.nnz);
+  }
+  if (before == nullptr) {
+    if (y.nnz == 0) {
+      permute_with_scratchpad(s, s.inv_row_perm, y);
+    } else {
+      permute_with_known_nz(s, s.inv_row_perm, y);
+    }
+    return false;
+  }
+  vec_clear_and_resize(*before, y.size);
+  {  // x->swap(result_before_permutation->values)
+    f64* t = y.values;
+    y.values = before->values;
+    before->values = t;
+    const int sz = y.size;
+    y.size = before->size;
+    before->size = sz;
+  }
+  if (y.nnz == 0) {
+    for (int row = 0; row < s.m; ++row) {
+      const f64 value = before->values[row];
+      if (value != 0.0) y.values[s.inv_row_perm[row]] = value;
+    }
+  } else {
+    {  // nz->swap(result_before_permutation->non_zeros)
+      int32_t* t = y.nz;
+      y.nz = before->nz;
+      before->nz = t;
+      const int n = y.nnz;
+      y.nnz = before->nnz;
+      before->nnz = n;
+    }
+    y.nnz = 0;  // nz is the cleared list of `before` (vec_clear_and_resize)
+    for (int k = 0; k < before->nnz; ++k) {
+      const int row = before->nz[k];
+      const f64 value = before->values[row];
+      const int permuted_row = s.inv_row_perm[row];
+      y.values[permuted_row] = value;
+      y.nz[y.nnz++] = permuted_row;
+    }
+    y.sorted = 0;
+  }
+  return true;
+}
+// LeftSolveUForUnitRow (lu_factorization.cc:405-436)
+SD_INLINE int lu_left_solve_u_unit_row(Lp& s, int col, Vec& y) {
+  if (s.is_identity) {
+    y.values[col] = 1.0;
+    y.nz[y.nnz++] = col;
+    return col;
+  }
+  const int pc = s.col_perm_empty ? col : s.col_perm[col];
+  y.values[pc] = 1.0;
+  y.nz[y.nnz++] = pc;
+  if (s.tupper.starts[pc + 1] == s.tupper.starts[pc]) {
+    y.values[pc] /= s.tupper.diag[pc];
+  } else {
+    tri_rows_to_consider(s.tupper, y.nz, &y.nnz, s.stored);
+    y.sorted = 1;
+    if (y.nnz == 0) {
+      tri_lower_solve_from(s.tupper, pc, y.values);
+    } else {
+      tri_hyper_solve(s.tupper, y.values, y.nz, &y.nnz);
+    }
+  }
+  return pc;
+}
+// GetColumnOfU (lu_factorization.cc:438-447) with SparseVector::CleanUp.
+SD_INLINE void lu_column_of_u(Lp& s, int col) {
+  s.n_col_u = 0;
+  if (s.is_identity) {
+    s.col_u_rows[0] = col;
+    s.col_u_coefs[0] = 1.0;
+    s.n_col_u = 1;
+    return;
+  }
+  const int c = s.col_perm_empty ? col : s.col_perm[col];
+  const Tri& u = s.upper;
+  int n = 0;
+  for (int64_t i = u.starts[c]; i < u.starts[c + 1]; ++i) {
+    s.col_u_rows[n] = u.rows[i];
+    s.col_u_coefs[n] = u.coefs[i];
+    ++n;
+  }
+  s.col_u_rows[n] = c;
+  s.col_u_coefs[n] = u.diag[c];
+  ++n;
+  // stable insertion sort by row
+  for (int i = 1; i < n; ++i) {
+    const int32_t r = s.col_u_rows[i];
+    const f64 v = s.col_u_coefs[i];
+    int j = i - 1;
+    while (j >= 0 && s.col_u_rows[j] > r) {
+      s.col_u_rows[j + 1] = s.col_u_rows[j];
+      s.col_u_coefs[j + 1] = s.col_u_coefs[j];
+      --j;
+    }
+    s.col_u_rows[j + 1] = r;
+    s.col_u_coefs[j + 1] = v;
+  }
+  int out = 0;
+  for (int i = 0; i < n; ++i) {
+    if (s.col_u_coefs[i] == 0.0) continue;
+    if (i + 1 == n || s.col_u_rows[i] != s.col_u_rows[i + 1]) {
+      s.col_u_rows[out] = s.col_u_rows[i];
+      s.col_u_coefs[out] = s.col_u_coefs[i];
+      ++out;
+    }
+  }
+  s.n_col_u = out;
+}
+SD_INLINE int64_t lu_number_of_entries(const Lp& s) {
+  return s.is_identity ? 0 : tri_num_entries(s.lower) + tri_num_entries(s.upper);
+}
+
+// ---- RankOneUpdateFactorization (rank_one_update.h:30-246) ----
+SD_INLINE void r1_right_solve_dense(Lp& s, f64* x) {
+  for (int i = 0; i < s.r1_count; ++i) {
+    const f64 mult = -col_dot(s.storage, s.r1_v[i], x) / s.r1_mu[i];
+    col_add_dense(s.storage, s.r1_u[i], mult, x);
+  }
+  s.r1_dtime += dt_ops(s.r1_num_entries);
+}
+SD_INLINE void r1_right_solve_nz(Lp& s, Vec& d) {
+  if (d.nnz == 0) {
+    r1_right_solve_dense(s, d.values);
+    return;
+  }
+  vec_repopulate_mask(d);
+  bool use_dense = vec_dense(d, 0.05);
+  for (int i = 0; i < s.r1_count; ++i) {
+    if (use_dense) {
+      const f64 mult = -col_dot(s.storage, s.r1_v[i], d.values) / s.r1_mu[i];
+      col_add_dense(s.storage, s.r1_u[i], mult, d.values);
+    } else {
+      const f64 mult = -col_dot(s.storage, s.r1_v[i], d.values) / s.r1_mu[i];
+      if (mult != 0.0) col_add_scattered(s.storage, s.r1_u[i], mult, d);
+      use_dense = vec_dense(d, 0.05);
+    }
+  }
+  vec_clear_mask(d);
+  vec_clear_nz_if_too_dense(d, 0.05);
+  s.r1_dtime += dt_ops(s.r1_num_entries);
+}
+SD_INLINE void r1_left_solve_dense(Lp& s, f64* y) {
+  for (int i = s.r1_count - 1; i >= 0; --i) {
+    const f64 mult = -col_dot(s.storage, s.r1_u[i], y) / s.r1_mu[i];
+    col_add_dense(s.storage, s.r1_v[i], mult, y);
+  }
+  s.r1_dtime += dt_ops(s.r1_num_entries);
+}
+SD_INLINE void r1_left_solve_nz(Lp& s, Vec& y) {
+  if (y.nnz == 0) {
+    r1_left_solve_dense(s, y.values);
+    return;
+  }
+  vec_repopulate_mask(y);
+  bool use_dense = vec_dense(y, 0.05);
+  for (int i = s.r1_count - 1; i >= 0; --i) {
+    if (use_dense) {
+      const f64 mult = -col_dot(s.storage, s.r1_u[i], y.values) / s.r1_mu[i];
+      col_add_dense(s.storage, s.r1_v[i], mult, y.values);
+    } else {
+      const f64 mult = -col_dot(s.storage, s.r1_u[i], y.values) / s.r1_mu[i];
+      if (mult != 0.0) col_add_scattered(s.storage, s.r1_v[i], mult, y);
+      use_dense = vec_dense(y, 0.05);
+    }
+  }
+  vec_clear_mask(y);
+  vec_clear_nz_if_too_dense(y, 0.05);
+  s.r1_dtime += dt_ops(s.r1_num_entries);
+}
+
+// ---- BasisFactorization (basis_representation.cc:304-624, MPF path) ----
+SD_INLINE void bf_bump(Lp& s, int64_t num_entries) {
+  if (s.m == 0) return;
+  const f64 density = static_cast<f64>(num_entries) / static_cast<f64>(s.m);
+  s.bf_dtime += density * dt_ops(lu_number_of_entries(s)) + dt_ops(s.r1_num_entries);
+}
+SD_INLINE void bf_right_solve(Lp& s, Vec& d) {
+  lu_right_solve_l_with_nz(s, d);
+  r1_right_solve_nz(s, d);
+  lu_right_solve_u_with_nz(s, d);
+  vec_sort_if_needed(d);
+  bf_bump(s, vec_nnz_estimate(d));
+}
+SD_INLINE const f64* bf_right_solve_for_tau(Lp& s, const Vec& a) {
+  if (s.tau_can_opt) {
+    s.tau_can_opt = 0;
+    lu_right_solve_l_permuted_input(s, s.tau);
+  } else {
+    vec_clear_and_resize(s.tau, s.m);
+    lu_right_solve_l_for_scattered(s, a, s.tau);
+  }
+  r1_right_solve_nz(s, s.tau);
+  lu_right_solve_u_with_nz(s, s.tau);
+  s.tau_is_computed = 1;
+  bf_bump(s, vec_nnz_estimate(s.tau));
+  return s.tau.values;
+}
+SD_INLINE void bf_left_solve_for_unit_row(Lp& s, int j, Vec& y) {
+  vec_clear_and_resize(y, s.m);
+  if (s.left_pool[j] == kInvalid) {
+    const int start = lu_left_solve_u_unit_row(s, j, y);
+    if (y.nnz == 0) {
+      s.left_pool[j] = store_add_dense_prefix(s.storage, y.values, y.size, start);
+    } else {
+      s.left_pool[j] = store_add_dense_nz(s.storage, y.values, y.size, y.nz, y.nnz);
+    }
+  } else {
+    store_copy_to_vec(s.storage, s.left_pool[j], y);
+  }
+  r1_left_solve_nz(s, y);
+  if (s.tau_is_computed) {
+    s.tau_can_opt = lu_left_solve_l_with_nz(s, y, &s.tau) ? 1 : 0;
+  } else {
+    s.tau_can_opt = 0;
+    lu_left_solve_l_with_nz(s, y, nullptr);
+  }
+  s.tau_is_computed = 0;
+  vec_sort_if_needed(y);
+  bf_bump(s, vec_nnz_estimate(y));
+}
+SD_INLINE void bf_right_solve_for_column(Lp& s, int col, Vec& d) {
+  vec_clear_and_resize(d, s.m);
+  lu_right_solve_l_for_column(s, col, d);
+  r1_right_solve_nz(s, d);
+  if (d.nnz == 0) {
+    s.right_pool[col] = store_add_dense_prefix(s.right_storage, d.values, d.size, 0);
+  } else {
+    sort_ints(d.nz, d.nnz);
+    s.right_pool[col] = store_add_dense_nz(s.right_storage, d.values, d.size, d.nz, d.nnz);
+  }
+  lu_right_solve_u_with_nz(s, d);
+  vec_sort_if_needed(d);
+  bf_bump(s, vec_nnz_estimate(d));
+}
+
+// ---- DynamicMaximum (pricing.h:152-345) ----
+// HeapLess: a.value > b.value (min-heap); libstdc++ make_heap restated.
+SD_INLINE void dp_push_heap(Lp& s, int hole, int top, int vi, f64 vv) {
+  int parent = (hole - 1) / 2;
+  while (hole > top && s.dp_tops_val[parent] > vv) {
+    s.dp_tops_idx[hole] = s.dp_tops_idx[parent];
+    s.dp_tops_val[hole] = s.dp_tops_val[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  s.dp_tops_idx[hole] = vi;
+  s.dp_tops_val[hole] = vv;
+}
+SD_INLINE void dp_adjust_heap(Lp& s, int hole, int len, int vi, f64 vv) {
+  const int top = hole;
+  int second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (s.dp_tops_val[second] > s.dp_tops_val[second - 1]) second--;
+    s.dp_tops_idx[hole] = s.dp_tops_idx[second];
+    s.dp_tops_val[hole] = s.dp_tops_val[second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    s.dp_tops_idx[hole] = s.dp_tops_idx[second - 1];
+    s.dp_tops_val[hole] = s.dp_tops_val[second - 1];
+    hole = second - 1;
+  }
+  dp_push_heap(s, hole, top, vi, vv);
+}
+SD_INLINE void dp_make_heap(Lp& s) {
+  const int len = s.dp_ntops;
+  if (len < 2) return;
+  int parent = (len - 2) / 2;
+  while (true) {
+    const int vi = s.dp_tops_idx[parent];
+    const f64 vv = s.dp_tops_val[parent];
+    dp_adjust_heap(s, parent, len, vi, vv);
+    if (parent == 0) return;
+    parent--;
+  }
+}
+SD_INLINE void dp_update_top_k(Lp& s, int position, f64 value) {
+  const int k = 31;
+  if (s.dp_ntops < k) {
+    s.dp_tops_idx[s.dp_ntops] = position;
+    s.dp_tops_val[s.dp_ntops] = value;
+    ++s.dp_ntops;
+    if (s.dp_ntops == k) {
+      dp_make_heap(s);
+      s.dp_threshold = s.dp_tops_val[0];
+    }
+    return;
+  }
+  if (value == s.dp_tops_val[0]) {
+    if (bernoulli(s, 0.5)) s.dp_tops_idx[0] = position;
+    return;
+  }
+  int i = 0;
+  const int limit = k / 2;
+  for (; i < limit;) {
+    const int left = 2 * i + 1;
+    const int right = left + 1;
+    const f64 lv = s.dp_tops_val[left];
+    const f64 rv = s.dp_tops_val[right];
+    if (lv > rv) {
+      if (value <= rv) break;
+      s.dp_tops_idx[i] = s.dp_tops_idx[right];
+      s.dp_tops_val[i] = s.dp_tops_val[right];
+      i = right;
+    } else {
+      if (value <= lv) break;
+      s.dp_tops_idx[i] = s.dp_tops_idx[left];
+      s.dp_tops_val[i] = s.dp_tops_val[left];
+      i = left;
+    }
+  }
+  s.dp_tops_idx[i] = position;
+  s.dp_tops_val[i] = value;
+  s.dp_threshold = s.dp_tops_val[0];
+}
+SD_INLINE void dp_clear_and_resize(Lp& s, int n) {
+  s.dp_ntops = 0;
+  s.dp_threshold = -sd_inf();
+  for (int i = s.dp_size; i < n; ++i) s.dp_values[i] = 0.0;
+  s.dp_size = n;
+  const int words = (n + 63) / 64;
+  for (int w = 0; w < words; ++w) s.dp_cand[w] = 0;
+}
+SD_INLINE void dp_start_dense_updates(Lp& s) {
+  s.dp_ntops = 0;
+  s.dp_threshold = sd_inf();
+}
+SD_INLINE void dp_dense_add_or_update(Lp& s, int position, f64 value) {
+  bit_set(s.dp_cand, position);
+  s.dp_values[position] = value;
+}
+SD_INLINE void dp_add_or_update(Lp& s, int position, f64 value) {
+  bit_set(s.dp_cand, position);
+  s.dp_values[position] = value;
+  if (value >= s.dp_threshold) dp_update_top_k(s, position, value);
+}
+SD_INLINE void dp_remove(Lp& s, int position) { bit_clear(s.dp_cand, position); }
+SD_INLINE int dp_randomize(Lp& s, int best, int n_equiv) {
+  if (n_equiv == 0) return best;
+  s.dp_equiv[n_equiv++] = best;
+  return s.dp_equiv[uniform_int(s, n_equiv - 1)];
+}
+SD_INLINE int dp_get_maximum(Lp& s) {
+  f64 best_value = -sd_inf();
+  int best_position = -1;
+  int n_equiv = 0;
+  if (s.dp_ntops != 0) {
+    // iterate over a copy of tops_ (the loop compacts in place)
+    int32_t cidx[32];
+    f64 cval[32];
+    const int n = s.dp_ntops;
+    for (int k = 0; k < n; ++k) {
+      cidx[k] = s.dp_tops_idx[k];
+      cval[k] = s.dp_tops_val[k];
+    }
+    int new_size = 0;
+    for (int k = 0; k < n; ++k) {
+      const int idx = cidx[k];
+      const f64 val = cval[k];
+      if (!bit_get(s.dp_cand, idx)) continue;
+      if (s.dp_values[idx] != val) continue;
+      s.dp_tops_idx[new_size] = idx;
+      s.dp_tops_val[new_size] = val;
+      ++new_size;
+      if (val >= best_value) {
+        if (val == best_value) {
+          s.dp_equiv[n_equiv++] = idx;
+          continue;
+        }
+        n_equiv = 0;
+        best_value = val;
+        best_position = idx;
+      }
+    }
+    s.dp_ntops = new_size;
+    if (new_size != 0) return dp_randomize(s, best_position, n_equiv);
+  }
+  s.dp_threshold = -sd_inf();
+  const int words = (s.dp_size + 63) / 64;
+  for (int w = 0; w < words; ++w) {
+    uint64_t word = s.dp_cand[w];
+    while (word) {
+      const int position = w * 64 + sd_ctz(word);
+      word &= word - 1;
+      if (position >= s.dp_size) break;
+      const f64 value = s.dp_values[position];
+      if (value < s.dp_threshold) continue;
+      dp_update_top_k(s, position, value);
+      if (value >= best_value) {
+        if (value == best_value) {
+          s.dp_equiv[n_equiv++] = position;
+          continue;
+        }
+        n_equiv = 0;
+        best_value = value;
+        best_position = position;
+      }
+    }
+  }
+  return dp_randomize(s, best_position, n_equiv);
+}
+
+// ---- VariableValues (variable_values.cc) ----
+SD_INLINE f64 row_infeasibility(const Lp& s, int col) {
+  return sd_max(s.x[col] - s.ub[col], s.lb[col] - s.x[col]);
+}
+SD_INLINE void vv_recompute_dual_prices(Lp& s, int put_more_importance_on_norm) {
+  dp_clear_and_resize(s, s.m);
+  dp_start_dense_updates(s);
+  s.put_more_importance_on_norm = put_more_importance_on_norm;
+  const f64 tol = s.primal_feasibility_tolerance;
+  for (int row = 0; row < s.m; ++row) {
+    const int col = s.basis[row];
+    const f64 inf = row_infeasibility(s, col);
+    if (inf > tol) {
+      dp_dense_add_or_update(s, row, s.put_more_importance_on_norm
+                                         ? sd_fabs(inf) / s.norms[row]
+                                         : sq(inf) / s.norms[row]);
+    }
+  }
+}
+SD_INLINE void vv_update_dual_price(Lp& s, int row) {
+  const int col = s.basis[row];
+  const f64 inf = row_infeasibility(s, col);
+  if (inf > s.primal_feasibility_tolerance) {
+    dp_add_or_update(s, row, s.put_more_importance_on_norm ? sd_fabs(inf) / s.norms[row]
+                                                           : sq(inf) / s.norms[row]);
+  } else {
+    dp_remove(s, row);
+  }
+}
+// UpdateDualPrices(rows); the caller guarantees the norms are current.
+SD_INLINE void vv_update_dual_prices(Lp& s, const int32_t* rows, int n) {
+  if (s.dp_size != s.m) {
+    vv_recompute_dual_prices(s, s.put_more_importance_on_norm);
+    return;
+  }
+  for (int k = 0; k < n; ++k) vv_update_dual_price(s, rows[k]);
+}
+SD_INLINE void vv_set_nonbasic_from_status(Lp& s, int col) {
+  switch (s.vstatus[col]) {
+    case kFixedValue:
+    case kAtLower:
+      s.x[col] = s.lb[col];
+      break;
+    case kAtUpper:
+      s.x[col] = s.ub[col];
+      break;
+    default:
+      break;
+  }
+}
+// UpdateGivenNonBasicVariables(cols, update_basic = true) (:179-227)
+SD_INLINE void vv_update_given_nonbasic(Lp& s, const int32_t* cols, int n) {
+  Vec& v = s.ia0;
+  for (int i = v.size; i < s.m; ++i) v.values[i] = 0.0;  // resize(num_rows, 0.0)
+  v.size = s.m;
+  vec_clear_mask(v);
+  bool use_dense = false;
+  for (int k = 0; k < n; ++k) {
+    const int col = cols[k];
+    const f64 old_value = s.x[col];
+    vv_set_nonbasic_from_status(s, col);
+    if (use_dense) {
+      col_add_dense(s.A, col, s.x[col] - old_value, v.values);
+    } else {
+      col_add_scattered(s.A, col, s.x[col] - old_value, v);
+      use_dense = vec_dense(v, 0.8);
+    }
+  }
+  vec_clear_mask(v);
+  vec_clear_nz_if_too_dense(v, 0.8);
+  bf_right_solve(s, v);
+  if (v.nnz == 0) {
+    for (int row = 0; row < s.m; ++row) s.x[s.basis[row]] -= v.values[row];
+    for (int row = 0; row < s.m; ++row) v.values[row] = 0.0;
+    v.size = s.m;
+    vv_recompute_dual_prices(s, 0);  // RecomputeDualPrices() default argument
+    return;
+  }
+  for (int k = 0; k < v.nnz; ++k) {
+    const int row = v.nz[k];
+    s.x[s.basis[row]] -= v.values[row];
+    v.values[row] = 0.0;
+  }
+  vv_update_dual_prices(s, v.nz, v.nnz);
+  v.nnz = 0;
+}
+
+// ---- VariablesInfo (variables_info.cc) ----
+SD_INLINE void vi_set_relevance(Lp& s, int col, bool relevance) {
+  if (bit_get(s.relevant, col) == relevance) return;
+  if (relevance) {
+    bit_set(s.relevant, col);
+    s.num_entries_relevant += col_entries(s.A, col);
+  } else {
+    bit_clear(s.relevant, col);
+    s.num_entries_relevant -= col_entries(s.A, col);
+  }
+}
+SD_INLINE void vi_to_basic(Lp& s, int col) {
+  s.vstatus[col] = kBasic;
+  bit_set(s.is_basic, col);
+  bit_clear(s.not_basic, col);
+  bit_clear(s.can_inc, col);
+  bit_clear(s.can_dec, col);
+  bit_clear(s.boxed, col);
+  vi_set_relevance(s, col, false);
+}
+SD_INLINE void vi_to_nonbasic(Lp& s, int col, int8_t status) {
+  s.vstatus[col] = status;
+  bit_clear(s.is_basic, col);
+  bit_set(s.not_basic, col);
+  bit_put(s.can_inc, col, status == kAtLower || status == kFree);
+  bit_put(s.can_dec, col, status == kAtUpper || status == kFree);
+  const bool boxed = s.vtype[col] == kBoxed;
+  bit_put(s.boxed, col, boxed);
+  const bool relevance = status != kFixedValue && (s.boxed_relevant || !boxed);
+  vi_set_relevance(s, col, relevance);
+}
+
+// ---- UpdateRow (update_row.cc:60-306) ----
+SD_INLINE void ur_invalidate(Lp& s) {
+  s.left_inv_for = kInvalid;
+  s.urow_for = kInvalid;
+}
+SD_INLINE void ur_compute_unit_row_left_inverse(Lp& s, int leaving_row) {
+  if (s.left_inv_for == leaving_row) return;
+  s.left_inv_for = leaving_row;
+  bf_left_solve_for_unit_row(s, leaving_row, s.rho);
+}
+SD_INLINE void ur_row_wise(Lp& s) {
+  for (int c = 0; c < s.N; ++c) s.coeff[c] = 0.0;
+  for (int k = 0; k < s.n_rho_filtered; ++k) {
+    const int col = s.rho_filtered[k];
+    const f64 mult = s.rho.values[col];
+    for (int64_t i = s.At.starts[col]; i < s.At.starts[col + 1]; ++i)
+      s.coeff[s.At.rows[i]] += mult * s.At.coefs[i];
+  }
+  s.n_nzpos = 0;
+  const f64 drop = s.drop_tolerance;
+  for (int w = 0; w < s.nwords; ++w) {
+    uint64_t word = s.relevant[w];
+    while (word) {
+      const int col = w * 64 + sd_ctz(word);
+      word &= word - 1;
+      if (col >= s.N) break;
+      if (sd_fabs(s.coeff[col]) > drop) s.nzpos[s.n_nzpos++] = col;
+    }
+  }
+}
+SD_INLINE void ur_row_wise_hypersparse(Lp& s) {
+  for (int w = 0; w < s.nwords; ++w) s.nzset[w] = 0;
+  for (int k = 0; k < s.n_rho_filtered; ++k) {
+    const int col = s.rho_filtered[k];
+    const f64 mult = s.rho.values[col];
+    for (int64_t i = s.At.starts[col]; i < s.At.starts[col + 1]; ++i) {
+      const int pos = s.At.rows[i];
+      const f64 v = mult * s.At.coefs[i];
+      if (!bit_get(s.nzset, pos)) {
+        s.coeff[pos] = v;
+        bit_set(s.nzset, pos);
+      } else {
+        s.coeff[pos] += v;
+      }
+    }
+  }
+  for (int w = 0; w < s.nwords; ++w) s.nzset[w] &= s.relevant[w];
+  s.n_nzpos = 0;
+  const f64 drop = s.drop_tolerance;
+  for (int w = 0; w < s.nwords; ++w) {
+    uint64_t word = s.nzset[w];
+    while (word) {
+      const int col = w * 64 + sd_ctz(word);
+      word &= word - 1;
+      if (col >= s.N) break;
+      if (sd_fabs(s.coeff[col]) > drop) s.nzpos[s.n_nzpos++] = col;
+    }
+  }
+}
+SD_INLINE void ur_single_row(Lp& s, int row_as_col) {
+  s.n_nzpos = 0;
+  const f64 drop = s.drop_tolerance;
+  const f64 mult = s.rho.values[row_as_col];
+  for (int64_t i = s.At.starts[row_as_col]; i < s.At.starts[row_as_col + 1]; ++i) {
+    const int pos = s.At.rows[i];
+    if (!bit_get(s.relevant, pos)) continue;
+    const f64 v = mult * s.At.coefs[i];
+    if (sd_fabs(v) > drop) {
+      s.coeff[pos] = v;
+      s.nzpos[s.n_nzpos++] = pos;
+    }
+  }
+}
+SD_INLINE void ur_column_wise(Lp& s) {
+  s.n_nzpos = 0;
+  const f64 drop = s.drop_tolerance;
+  for (int w = 0; w < s.nwords; ++w) {
+    uint64_t word = s.relevant[w];
+    while (word) {
+      const int col = w * 64 + sd_ctz(word);
+      word &= word - 1;
+      if (col >= s.N) break;
+      const f64 c = col_dot(s.A, col, s.rho.values);
+      if (sd_fabs(c) > drop) {
+        s.nzpos[s.n_nzpos++] = col;
+        s.coeff[col] = c;
+      }
+    }
+  }
+}
+SD_INLINE void ur_compute_update_row(Lp& s, int leaving_row) {
+  if (s.urow_for == leaving_row) return;
+  s.urow_for = leaving_row;
+  ur_compute_unit_row_left_inverse(s, leaving_row);
+  if (s.use_transposed_matrix) {
+    int64_t num_row_wise_entries = 0;
+    const f64 drop = s.drop_tolerance;
+    s.n_rho_filtered = 0;
+    if (s.rho.nnz == 0) {
+      for (int col = 0; col < s.rho.size; ++col) {
+        if (sd_fabs(s.rho.values[col]) > drop) {
+          s.rho_filtered[s.n_rho_filtered++] = col;
+          num_row_wise_entries += col_entries(s.At, col);
+        }
+      }
+    } else {
+      for (int k = 0; k < s.rho.nnz; ++k) {
+        const int col = s.rho.nz[k];
+        if (sd_fabs(s.rho.values[col]) > drop) {
+          s.rho_filtered[s.n_rho_filtered++] = col;
+          num_row_wise_entries += col_entries(s.At, col);
+        }
+      }
+    }
+    if (s.n_rho_filtered == 1) {
+      ur_single_row(s, s.rho_filtered[0]);
+      s.ur_ops += num_row_wise_entries;
+      s.last_alg = 0;
+      return;
+    }
+    const int64_t num_col_wise_entries = s.num_entries_relevant;
+    const f64 row_wise = static_cast<f64>(num_row_wise_entries);
+    if (row_wise < 0.5 * static_cast<f64>(num_col_wise_entries)) {
+      if (row_wise < 1.1 * static_cast<f64>(s.N)) {
+        ur_row_wise_hypersparse(s);
+        s.ur_ops += 5 * num_row_wise_entries + s.N / 64;
+        s.last_alg = 1;
+      } else {
+        ur_row_wise(s);
+        s.ur_ops += num_row_wise_entries + s.m;
+        s.last_alg = 2;
+      }
+    } else {
+      ur_column_wise(s);
+      s.ur_ops += num_col_wise_entries + s.N;
+      s.last_alg = 3;
+    }
+  } else {
+    ur_column_wise(s);
+    s.ur_ops += s.num_entries_relevant + s.N;
+    s.last_alg = 3;
+  }
+}
+
+// ---- EnteringVariable::DualChooseEnteringColumn (entering_variable.cc:37-239) ----
+// ColWithRatio order: a < b iff (a.ratio == b.ratio ? (a.mag == b.mag ? a.col > b.col
+// : a.mag < b.mag) : a.ratio > b.ratio). std::make_heap/pop_heap pop the
+// greatest first; the order is total, so any max-heap pops the same sequence.
+SD_INLINE bool bp_less(const Lp& s, int a, int b) {
+  if (s.bp_ratio[a] == s.bp_ratio[b]) {
+    if (s.bp_mag[a] == s.bp_mag[b]) return s.bp_col[a] > s.bp_col[b];
+    return s.bp_mag[a] < s.bp_mag[b];
+  }
+  return s.bp_ratio[a] > s.bp_ratio[b];
+}
+SD_INLINE void bp_swap(Lp& s, int a, int b) {
+  const int32_t c = s.bp_col[a]; s.bp_col[a] = s.bp_col[b]; s.bp_col[b] = c;
+  const f64 r = s.bp_ratio[a]; s.bp_ratio[a] = s.bp_ratio[b]; s.bp_ratio[b] = r;
+  const f64 g = s.bp_mag[a]; s.bp_mag[a] = s.bp_mag[b]; s.bp_mag[b] = g;
+}
+SD_INLINE void bp_sift_down(Lp& s, int i, int n) {
+  while (true) {
+    const int l = 2 * i + 1;
+    if (l >= n) return;
+    int c = l;
+    if (l + 1 < n && bp_less(s, l, l + 1)) c = l + 1;
+    if (!bp_less(s, i, c)) return;
+    bp_swap(s, i, c);
+    i = c;
+  }
+}
+SD_INLINE void ent_dual_choose(Lp& s, bool nothing_to_recompute, f64 cost_variation,
+                               int* entering_col) {
+  const f64 threshold =
+      nothing_to_recompute ? s.minimum_acceptable_pivot : s.ratio_test_zero_threshold;
+  f64 variation_magnitude = sd_fabs(cost_variation) - threshold;
+  const f64 harris_tolerance = s.harris_tolerance_ratio * s.dual_tol;
+  f64 harris_ratio = sd_dbl_max();
+  const f64 minimum_delta = s.degenerate_ministep_factor * s.dual_tol;
+  s.ent_ops += 10 * static_cast<int64_t>(s.n_nzpos);
+  int nbp = 0;
+  for (int k = 0; k < s.n_nzpos; ++k) {
+    const int col = s.nzpos[k];
+    const f64 coeff = (cost_variation > 0.0) ? s.coeff[col] : -s.coeff[col];
+    f64 ratio, mag;
+    if (bit_get(s.can_dec, col) && coeff > threshold) {
+      if (-s.rc[col] > harris_ratio * coeff) continue;
+      ratio = -s.rc[col] / coeff;
+      mag = coeff;
+    } else if (bit_get(s.can_inc, col) && coeff < -threshold) {
+      if (s.rc[col] > harris_ratio * -coeff) continue;
+      ratio = s.rc[col] / -coeff;
+      mag = -coeff;
+    } else {
+      continue;
+    }
+    const f64 hr = sd_max(minimum_delta / mag, ratio + harris_tolerance / mag);
+    if (hr < harris_ratio) {
+      if (bit_get(s.boxed, col)) {
+        const f64 delta = (s.ub[col] - s.lb[col]) * mag;
+        if (delta >= variation_magnitude) harris_ratio = hr;
+      } else {
+        harris_ratio = hr;
+      }
+    }
+    s.bp_col[nbp] = col;
+    s.bp_ratio[nbp] = ratio;
+    s.bp_mag[nbp] = mag;
+    ++nbp;
+  }
+  for (int i = nbp / 2 - 1; i >= 0; --i) bp_sift_down(s, i, nbp);
+  harris_ratio = sd_dbl_max();
+  *entering_col = kInvalid;
+  s.n_flips = 0;
+  f64 step = 0.0;
+  f64 best_coeff = -1.0;
+  int n_equiv = 0;
+  while (nbp > 0) {
+    const int tcol = s.bp_col[0];
+    const f64 tratio = s.bp_ratio[0];
+    const f64 tmag = s.bp_mag[0];
+    if (tratio > harris_ratio) break;
+    bool popped = false;
+    if (variation_magnitude > 0.0) {
+      if (bit_get(s.boxed, tcol)) {
+        variation_magnitude -= (s.ub[tcol] - s.lb[tcol]) * tmag;
+        if (variation_magnitude > 0.0) {
+          s.flips[s.n_flips++] = tcol;
+          popped = true;
+        }
+      }
+    }
+    if (!popped) {
+      if (tmag >= best_coeff) {
+        harris_ratio =
+            sd_min(harris_ratio, sd_max(minimum_delta / tmag, tratio + harris_tolerance / tmag));
+        if (tmag == best_coeff && tratio == step) {
+          s.ent_equiv[n_equiv++] = tcol;
+        } else {
+          n_equiv = 0;
+          best_coeff = tmag;
+          *entering_col = tcol;
+          step = tratio;
+        }
+      }
+    }
+    --nbp;
+    if (nbp > 0) {
+      bp_swap(s, 0, nbp);
+      bp_sift_down(s, 0, nbp);
+    }
+  }
+  if (n_equiv != 0) {
+    s.ent_equiv[n_equiv++] = *entering_col;
+    *entering_col = s.ent_equiv[uniform_int(s, n_equiv - 1)];
+  }
+  if (*entering_col == kInvalid) return;
+  const f64 pivot_limit = s.minimum_acceptable_pivot;
+  if (best_coeff < pivot_limit && s.n_flips != 0) {
+    for (int i = s.n_flips - 1; i >= 0; --i) {
+      const int col = s.flips[i];
+      if (sd_fabs(s.coeff[col]) < pivot_limit) continue;
+      *entering_col = col;
+      break;
+    }
+  }
+}
+
+// ---- DualEdgeNorms (dual_edge_norms.cc:49-118) ----
+SD_INLINE bool den_test_precision(Lp& s, int leaving_row) {
+  if (s.norms_recompute) return true;
+  const f64 leaving = vec_squared_norm(s.rho);
+  const f64 old = s.norms[leaving_row];
+  const f64 acc = (sd_sqrt(leaving) - sd_sqrt(old)) / sd_sqrt(leaving);
+  if (sd_fabs(acc) > s.recompute_edges_norm_threshold) s.norms_recompute = 1;
+  s.norms[leaving_row] = leaving;
+  return old > 0.25 * leaving;
+}
+SD_INLINE void den_update_before_pivot(Lp& s, int leaving_row) {
+  if (s.norms_recompute) return;
+  const f64* tau = bf_right_solve_for_tau(s, s.rho);
+  const f64 pivot = s.dir.values[leaving_row];
+  const f64 new_leaving = s.norms[leaving_row] / sq(pivot);
+  for (int k = 0; k < s.dir.nnz; ++k) {
+    const int row = s.dir.nz[k];
+    const f64 c = s.dir.values[row];
+    s.norms[row] += c * (c * new_leaving - 2.0 / pivot * tau[row]);
+    const f64 kLowerBound = 1e-4;
+    if (s.norms[row] < kLowerBound) {
+      if (row == leaving_row) continue;
+      s.norms[row] = kLowerBound;
+    }
+  }
+  s.norms[leaving_row] = new_leaving;
+}
+
+// ---- ReducedCosts (reduced_costs.cc:172-488) ----
+SD_INLINE void rc_shift_cost_if_needed(Lp& s, bool increasing_rc_is_needed, int col) {
+  const f64 minimum_delta = s.degenerate_ministep_factor * s.dual_tol;
+  if (increasing_rc_is_needed && s.rc[col] <= -minimum_delta) return;
+  if (!increasing_rc_is_needed && s.rc[col] >= minimum_delta) return;
+  const f64 delta = increasing_rc_is_needed ? minimum_delta : -minimum_delta;
+  s.cost_pert[col] -= s.rc[col] + delta;
+  s.rc[col] = -delta;
+  s.has_cost_shift = 1;
+}
+SD_INLINE void rc_update_before_pivot(Lp& s, int entering_col, int leaving_row) {
+  const int leaving_col = s.basis[leaving_row];
+  if (!s.recompute_rc) {
+    const f64 entering_rc = s.rc[entering_col];
+    if (entering_rc == 0.0) {
+      s.rc_precise = 0;
+    } else {
+      s.rc_recomputed = 0;
+      s.rc_precise = 0;
+      ur_compute_update_row(s, leaving_row);
+      const f64 new_leaving_rc = entering_rc / -s.dir.values[leaving_row];
+      for (int k = 0; k < s.n_nzpos; ++k) {
+        const int col = s.nzpos[k];
+        s.rc[col] += new_leaving_rc * s.coeff[col];
+      }
+      s.rc[leaving_col] = new_leaving_rc;
+      s.rc[entering_col] = 0.0;
+    }
+  }
+  s.basic_obj[leaving_row] = s.objective[entering_col] + s.cost_pert[entering_col];
+  s.recompute_bo_left_inverse = 1;
+}
+
+// ---- RevisedSimplex ----
+SD_INLINE f64 rs_deterministic_time(const Lp& s) {
+  return dt_ops(s.num_update_price_ops) + s.bf_dtime + dt_ops(s.ur_ops) + dt_ops(s.ent_ops) +
+         s.rc_dtime + s.primal_norms_dtime;
+}
+SD_INLINE void rs_advance_deterministic_time(Lp& s) {
+  const f64 cur = rs_deterministic_time(s);
+  s.tl_det_elapsed += cur - s.last_det_update;
+  s.last_det_update = cur;
+}
+SD_INLINE void rs_compute_direction(Lp& s, int col) {
+  bf_right_solve_for_column(s, col, s.dir);
+  s.dir_inf_norm = 0.0;
+  if (s.dir.nnz == 0) {
+    for (int row = 0; row < s.m; ++row) {
+      const f64 value = s.dir.values[row];
+      if (value != 0.0) {
+        s.dir.nz[s.dir.nnz++] = row;
+        s.dir_inf_norm = sd_max(s.dir_inf_norm, sd_fabs(value));
+      }
+    }
+  } else {
+    for (int k = 0; k < s.dir.nnz; ++k)
+      s.dir_inf_norm = sd_max(s.dir_inf_norm, sd_fabs(s.dir.values[s.dir.nz[k]]));
+  }
+}
+SD_INLINE void rs_make_boxed_dual_feasible(Lp& s) {
+  int n_changed = 0;
+  const f64 threshold = s.dual_tol;
+  for (int k = 0; k < s.n_flips; ++k) {
+    const int col = s.flips[k];
+    const f64 rc = s.rc[col];
+    const int8_t status = s.vstatus[col];
+    if (rc > threshold && status == kAtUpper) {
+      vi_to_nonbasic(s, col, kAtLower);
+      s.changed_cols[n_changed++] = col;
+    } else if (rc < -threshold && status == kAtLower) {
+      vi_to_nonbasic(s, col, kAtUpper);
+      s.changed_cols[n_changed++] = col;
+    }
+  }
+  if (n_changed != 0) vv_update_given_nonbasic(s, s.changed_cols, n_changed);
+}
+
+// Room for one more iteration in every fixed-capacity array.
+SD_INLINE bool sd_room_for_iteration(const Lp& s) {
+  const int64_t need = static_cast<int64_t>(s.m) + 1;
+  if (s.storage.num_cols + 3 > s.storage.cap_cols) return false;
+  if (s.right_storage.num_cols + 2 > s.right_storage.cap_cols) return false;
+  if (s.storage.starts[s.storage.num_cols] + 2 * need > s.storage.cap_entries) return false;
+  if (s.right_storage.starts[s.right_storage.num_cols] + need > s.right_storage.cap_entries)
+    return false;
+  if (s.r1_count + 1 > s.r1_cap) return false;
+  return true;
+}
+
+// The phase-II dual loop (revised_simplex.cc:3058-3367) from the point after
+// the loop-top block, until the host is needed. Returns the exit code.
+SD_INLINE int32_t sd_run(Lp& s) {
+  s.exit_code = kExitNone;
+  s.iterations_done = 0;
+  bool at_top = false;  // false: enter after the loop-top block
+  while (true) {
+    if (at_top) {
+      // Loop top (refactorize == false here).
+      if (s.must_refactorize || s.norms_recompute || s.num_updates == 0 ||
+          (s.iteration_cap > 0 && s.iterations_done >= s.iteration_cap) ||
+          !sd_room_for_iteration(s)) {
+        s.refactorize = 0;
+        return s.exit_code = kExitLoopTop;
+      }
+      // !IsRefactorized(), !feasibility_phase:
+      rs_make_boxed_dual_feasible(s);
+      s.n_flips = 0;
+      vv_update_dual_prices(s, s.dir.nz, s.dir.nnz);
+    }
+    at_top = true;
+    // DualChooseLeavingVariableRow (:2148-2181)
+    if (s.dp_size == 0) vv_recompute_dual_prices(s, s.dual_price_prioritize_norm);
+    const int leaving_row = dp_get_maximum(s);
+    if (leaving_row == kInvalid) {
+      s.exit_row = kInvalid;
+      return s.exit_code = kExitNoLeaving;
+    }
+    const int lcol = s.basis[leaving_row];
+    const f64 value = s.x[lcol];
+    f64 cost_variation, target_bound;
+    if (value < s.lb[lcol]) {
+      cost_variation = s.lb[lcol] - value;
+      target_bound = s.lb[lcol];
+    } else {
+      cost_variation = s.ub[lcol] - value;
+      target_bound = s.ub[lcol];
+    }
+    s.exit_row = leaving_row;
+    s.exit_cost_variation = cost_variation;
+    s.exit_target_bound = target_bound;
+
+    ur_compute_unit_row_left_inverse(s, leaving_row);
+    if (!den_test_precision(s, leaving_row)) {
+      if (s.norms_recompute) return s.exit_code = kExitPrecision;  // host recomputes norms
+      const int32_t one = leaving_row;
+      vv_update_dual_prices(s, &one, 1);
+      continue;
+    }
+    ur_compute_update_row(s, leaving_row);
+
+    int entering_col;
+    ent_dual_choose(s, s.rc_precise != 0, cost_variation, &entering_col);
+    if (entering_col == kInvalid) {
+      if (!s.rc_precise) {
+        s.refactorize = 1;
+        return s.exit_code = kExitLoopTop;
+      }
+      return s.exit_code = kExitNoEntering;
+    }
+    const f64 entering_coeff = s.coeff[entering_col];
+    if (sd_fabs(entering_coeff) < s.dual_small_pivot_threshold && !s.rc_precise) {
+      s.refactorize = 1;
+      return s.exit_code = kExitLoopTop;
+    }
+    rs_compute_direction(s, entering_col);
+    if (sd_fabs(s.dir.values[leaving_row]) < s.small_pivot_threshold * s.dir_inf_norm) {
+      if (!s.rc_precise) {
+        s.refactorize = 1;
+        return s.exit_code = kExitLoopTop;
+      }
+    }
+    rs_advance_deterministic_time(s);
+    if (s.num_iterations == s.max_number_of_iterations || s.tl_det_elapsed > s.tl_det_max) {
+      return s.exit_code = kExitReturnOk;
+    }
+    const bool increasing_rc_is_needed = (cost_variation > 0.0) == (entering_coeff > 0.0);
+    rc_shift_cost_if_needed(s, increasing_rc_is_needed, entering_col);
+    rc_update_before_pivot(s, entering_col, leaving_row);
+    den_update_before_pivot(s, leaving_row);
+    // ComputeStepToMoveBasicVariableToBound + UpdateOnPivoting
+    const f64 primal_step = (s.x[lcol] - target_bound) / s.dir.values[leaving_row];
+    for (int k = 0; k < s.dir.nnz; ++k) {
+      const int row = s.dir.nz[k];
+      s.x[s.basis[row]] -= s.dir.values[row] * primal_step;
+    }
+    s.x[entering_col] += primal_step;
+    // UpdateAndPivot (:2504-2575)
+    const f64 pivot_from_update_row = s.coeff[entering_col];  // IsComputedFor(leaving_row)
+    const int8_t leaving_status = s.lb[lcol] == s.ub[lcol] ? kFixedValue
+                                  : target_bound == s.lb[lcol] ? kAtLower
+                                                               : kAtUpper;
+    vi_to_nonbasic(s, lcol, leaving_status);  // UpdateBasis
+    s.basis[leaving_row] = entering_col;
+    vi_to_basic(s, entering_col);
+    ur_invalidate(s);
+    const f64 pivot_from_direction = s.dir.values[leaving_row];
+    const f64 diff = sd_fabs(pivot_from_update_row - pivot_from_direction);
+    s.exit_col = lcol;
+    if (diff > s.refactorization_threshold *
+                   (1.0 + sd_min(sd_fabs(pivot_from_update_row), sd_fabs(pivot_from_direction)))) {
+      s.exit_lu_bump = s.num_updates < 10 ? 1 : 0;
+      return s.exit_code = kExitPivotRefactor;
+    }
+    // BasisFactorization::Update (:304-340)
+    if (s.num_updates >= s.max_updates) {
+      if (!s.dynamic_period || s.last_fact_dtime < s.r1_dtime) {
+        s.exit_lu_bump = 0;
+        return s.exit_code = kExitPivotRefactor;
+      }
+    }
+    const int right_index = s.right_pool[entering_col];
+    const int left_index = s.left_pool[leaving_row];
+    if (right_index == kInvalid || left_index == kInvalid) {
+      s.exit_lu_bump = 0;
+      return s.exit_code = kExitPivotRefactor;
+    }
+    ++s.num_updates;
+    // MiddleProductFormUpdate (:258-302)
+    {
+      for (int64_t i = s.right_storage.starts[right_index];
+           i < s.right_storage.starts[right_index + 1]; ++i) {
+        s.mpf_scratch[s.right_storage.rows[i]] = s.right_storage.coefs[i];
+        s.mpf_scratch_nz[s.n_mpf_scratch_nz++] = s.right_storage.rows[i];
+      }
+      lu_column_of_u(s, leaving_row);
+      for (int k = 0; k < s.n_col_u; ++k) {
+        s.mpf_scratch[s.col_u_rows[k]] -= s.col_u_coefs[k];
+        s.mpf_scratch_nz[s.n_mpf_scratch_nz++] = s.col_u_rows[k];
+      }
+      const f64 scalar_product = col_dot(s.storage, left_index, s.mpf_scratch);
+      const int u_index =
+          store_add_and_clear(s.storage, s.mpf_scratch, s.mpf_scratch_nz, &s.n_mpf_scratch_nz);
+      const f64 mu = 1.0 + scalar_product;
+      if (mu == 0.0) return s.exit_code = kExitLuError;
+      s.r1_u[s.r1_count] = u_index;
+      s.r1_v[s.r1_count] = left_index;
+      s.r1_mu[s.r1_count] = mu;
+      ++s.r1_count;
+      s.r1_num_entries += col_entries(s.storage, u_index) + col_entries(s.storage, left_index);
+    }
+    s.tau_can_opt = 0;
+    // IsRefactorized() is false here: no PermuteBasis.
+    vv_set_nonbasic_from_status(s, lcol);
+    ++s.num_iterations;  // OnIterationDone
+    ++s.iterations_done;
+  }
+}
+
+}  // namespace sdual
+
+#endif  // MILP_SDUAL_CORE_H_

@@ -1,0 +1,255 @@
+// Device-resident dual simplex segment ("sdual"): the state of one LP.
+//
+// Glop's dual simplex iteration (revised_simplex.cc:3058-3367, the phase-II
+// loop body and its helpers) runs as one workgroup per LP on the GPU. The host
+// engine keeps everything that is not a plain iteration: Markowitz
+// factorizations, the recomputations after them, phase changes, status
+// decisions. At a segment boundary the host packs its state into this flat
+// structure (sdual_bridge.inc), the device runs iterations until the loop needs
+// the host again, and the host unpacks the state and continues at the
+// matching point of its own loop (SdExit).
+//
+// Every array lives in one arena per LP (device memory on the GPU, host
+// memory in the host build used by the CPU checks); the struct itself is the
+// arena's header. Sizes: m rows, N = n + m columns. Glop's std::vector
+// capacities become fixed capacities here; the host never starts a segment
+// that could overflow them (sd_can_start).
+#ifndef MILP_SDUAL_STATE_H_
+#define MILP_SDUAL_STATE_H_
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define SD_HD __host__ __device__
+#define SD_INLINE __host__ __device__ inline
+#else
+#define SD_HD
+#define SD_INLINE inline
+#endif
+
+namespace sdual {
+
+using f64 = double;
+
+// ScatteredVector (lp_data/scattered_vector.h:61-177). `size` is
+// values.size(); is_non_zero is all false between uses (as upstream).
+struct Vec {
+  f64* values;
+  int size;
+  int* nz;
+  int nnz;
+  int sorted;
+  char* mask;
+};
+
+// CompactSparseMatrix read-only view (sparse.h:291-512).
+struct Csc {
+  const int64_t* starts;
+  const int32_t* rows;
+  const f64* coefs;
+  int num_rows;
+  int num_cols;
+};
+
+// TriangularMatrix (sparse.h:583-921): L, U and their transposes.
+struct Tri {
+  int64_t* starts;  // num_cols + 1
+  int32_t* rows;
+  f64* coefs;
+  f64* diag;  // diagonal_coefficients_, size num_cols
+  int num_rows;
+  int num_cols;
+  int first_non_identity;
+  int all_ones;
+  int64_t ncoefs;  // coefficients_.size() (num_entries() = num_cols + ncoefs)
+};
+
+// Growing CompactSparseMatrix (the MPF storages, basis_representation.h).
+struct Store {
+  int64_t* starts;  // cap_cols + 1
+  int32_t* rows;
+  f64* coefs;
+  int num_rows;
+  int num_cols;
+  int cap_cols;
+  int64_t cap_entries;
+};
+
+// Why the device handed the LP back, and where the host loop resumes
+// (RevisedSimplex::DualMinimize, engine/simplex.cc).
+enum SdExit : int32_t {
+  kExitNone = 0,
+  kExitLoopTop = 1,        // `refactorize = exit_refactorize; continue;`
+  kExitNoLeaving = 2,      // leaving_row == kInvalidRow block
+  kExitPrecision = 3,      // TestPrecision failed: UpdateDualPrices({row}); continue
+  kExitNoEntering = 4,     // entering_col == kInvalidCol block
+  kExitReturnOk = 5,       // iteration or deterministic limit: return OK
+  kExitPivotRefactor = 6,  // UpdateAndPivot must refactorize (host Markowitz)
+  kExitLuError = 7,        // MiddleProductFormUpdate: degenerate rank-one update
+  kExitCapacity = 8,       // a fixed capacity would overflow: resume at loop top
+};
+
+struct Lp {
+  // ---- problem (read-only during a segment) ----
+  int m;  // rows
+  int N;  // columns of [A | I]
+  Csc A;  // compact_matrix_
+  Csc At; // transposed_matrix_ (num_cols = m)
+  const f64* objective;
+
+  // ---- parameters (GlopParameters subset) ----
+  f64 drop_tolerance;
+  f64 primal_feasibility_tolerance;
+  f64 recompute_edges_norm_threshold;
+  f64 minimum_acceptable_pivot;
+  f64 ratio_test_zero_threshold;
+  f64 harris_tolerance_ratio;
+  f64 degenerate_ministep_factor;
+  f64 dual_small_pivot_threshold;
+  f64 small_pivot_threshold;
+  f64 refactorization_threshold;
+  f64 lu_factorization_pivot_threshold;
+  int use_transposed_matrix;
+  int put_more_importance_on_norm;  // VariableValues::put_more_importance_on_norm_
+  int dual_price_prioritize_norm;   // GlopParameters
+  int64_t max_number_of_iterations;
+
+  // ---- VariablesInfo ----
+  f64* lb;
+  f64* ub;
+  int8_t* vtype;
+  int8_t* vstatus;
+  uint64_t* can_inc;
+  uint64_t* can_dec;
+  uint64_t* relevant;
+  uint64_t* is_basic;
+  uint64_t* not_basic;
+  uint64_t* boxed;
+  int nwords;  // (N + 63) / 64
+  int64_t num_entries_relevant;
+  int boxed_relevant;
+
+  int32_t* basis;
+  f64* x;  // VariableValues::variable_values_
+
+  // ---- ReducedCosts ----
+  f64* rc;
+  f64* cost_pert;
+  f64* basic_obj;
+  int must_refactorize;
+  int recompute_bo_left_inverse;
+  int recompute_bo;
+  int recompute_rc;
+  int rc_precise;
+  int rc_recomputed;
+  int has_cost_shift;
+  f64 dual_tol;
+  f64 rc_dtime;
+
+  // ---- DualEdgeNorms ----
+  f64* norms;
+  int norms_recompute;
+
+  // ---- DynamicMaximum dual_prices_ (pricing.h:58-345) ----
+  f64* dp_values;
+  uint64_t* dp_cand;
+  int dp_size;  // values_.size()
+  f64 dp_threshold;
+  int dp_ntops;
+  int32_t dp_tops_idx[32];
+  f64 dp_tops_val[32];
+  int32_t* dp_equiv;  // equivalent_choices_ scratch (m + 1)
+
+  // ---- UpdateRow ----
+  Vec rho;
+  int32_t* rho_filtered;
+  int n_rho_filtered;
+  int32_t* nzpos;  // non_zero_position_list_
+  int n_nzpos;
+  uint64_t* nzset;  // non_zero_position_set_ (nwords)
+  f64* coeff;       // coefficient_ (N)
+  int left_inv_for;
+  int urow_for;
+  int64_t ur_ops;
+  int last_alg;
+
+  // ---- EnteringVariable ----
+  int64_t ent_ops;
+  int32_t* bp_col;  // breakpoints_ heap (N)
+  f64* bp_ratio;
+  f64* bp_mag;
+  int32_t* ent_equiv;  // equivalent_entering_choices_ (N + 1)
+
+  // ---- RevisedSimplex ----
+  Vec dir;
+  f64 dir_inf_norm;
+  int32_t* flips;  // bound_flip_candidates_ (N)
+  int n_flips;
+  int32_t* changed_cols;  // MakeBoxedVariableDualFeasible scratch (N)
+  Vec ia0;                // VariableValues::initially_all_zero_scratchpad_
+  int64_t num_iterations;
+  int64_t num_update_price_ops;
+  f64 primal_norms_dtime;  // PrimalEdgeNorms::DeterministicTime() (constant here)
+  f64 last_det_update;     // last_deterministic_time_update_
+  f64 tl_det_elapsed;      // TimeLimit deterministic elapsed
+  f64 tl_det_max;          // max_deterministic_time
+
+  // ---- LuFactorization ----
+  Tri lower, upper, tupper, tlower;
+  int32_t* col_perm;  // empty when col_perm_empty
+  int32_t* inv_col_perm;
+  int32_t* row_perm;
+  int32_t* inv_row_perm;
+  int col_perm_empty;
+  int is_identity;
+  f64* zero_scratch;  // dense_zero_scratchpad_ (zero between uses)
+  char* stored;       // TriangularMatrix::stored_ (false between uses)
+  int32_t* col_u_rows;  // column_of_upper_ (m + 1)
+  f64* col_u_coefs;
+  int n_col_u;
+
+  // ---- BasisFactorization (MPF) ----
+  int num_updates;
+  int max_updates;
+  int dynamic_period;
+  int tau_is_computed;
+  int tau_can_opt;
+  Vec tau;
+  f64 last_fact_dtime;
+  f64 bf_dtime;
+  int32_t* left_pool;   // left_pool_mapping_ (m, -1 = none)
+  int32_t* right_pool;  // right_pool_mapping_ (N, -1 = none)
+  Store storage;
+  Store right_storage;
+  f64* mpf_scratch;  // scratchpad_ (m, zero between uses)
+  int32_t* mpf_scratch_nz;  // scratchpad_non_zeros_ (2m)
+  int n_mpf_scratch_nz;
+
+  // ---- RankOneUpdateFactorization ----
+  int32_t* r1_u;
+  int32_t* r1_v;
+  f64* r1_mu;
+  int r1_count;
+  int r1_cap;
+  int64_t r1_num_entries;
+  f64 r1_dtime;
+
+  // ---- std::mt19937_64 (libstdc++ layout: _M_x[312], _M_p) ----
+  uint64_t mt[312];
+  uint64_t mti;
+
+  // ---- loop carry and exit ----
+  int refactorize;  // the host loop's `refactorize` flag
+  int32_t exit_code;
+  int32_t exit_row;       // leaving_row at the exit
+  int32_t exit_col;       // leaving_col (kExitPivotRefactor) / entering_col
+  int32_t exit_lu_bump;   // UpdateAndPivot raised the LU pivot threshold
+  f64 exit_cost_variation;
+  f64 exit_target_bound;
+  int64_t iterations_done;  // this segment
+  int64_t iteration_cap;    // stop after this many (0 = no cap)
+};
+
+}  // namespace sdual
+
+#endif  // MILP_SDUAL_STATE_H_

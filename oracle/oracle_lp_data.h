@@ -22,6 +22,10 @@
 
 namespace oracle {
 
+// Test build only (-DORACLE_SDUAL): the host bridge of the device dual
+// segment (or-tools_amd/csrc/sdual) reads these classes' members.
+struct SdualBridge;
+
 using Fractional = double;
 using RowIndex = int32_t;
 using ColIndex = int32_t;
@@ -120,6 +124,8 @@ class Bitset {
     for (size_t i = k; i < w_.size(); ++i) w_[i] = 0;
   }
   uint64_t Word(int b) const { return w_[b]; }
+  const uint64_t* data() const { return w_.data(); }
+  uint64_t* mutable_data() { return w_.data(); }
   int NumWords() const { return static_cast<int>(w_.size()); }
   template <typename F>
   void ForEach(F&& f) const {

@@ -774,6 +774,8 @@ class Markowitz {
 
 // lu_factorization.{h,cc}
 class LuFactorization {
+  friend struct SdualBridge;
+
  public:
   void Clear();
   Status ComputeFactorization(const CompactSparseMatrixView& b);
@@ -847,6 +849,8 @@ class LuFactorization {
 
 // rank_one_update.h:30-148
 class RankOneUpdateElementaryMatrix {
+  friend struct SdualBridge;
+
  public:
   RankOneUpdateElementaryMatrix(const CompactSparseMatrix* storage, int u_index,
                                 int v_index, Fractional u_dot_v)
@@ -892,6 +896,8 @@ class RankOneUpdateElementaryMatrix {
 
 // rank_one_update.h:150-246
 class RankOneUpdateFactorization {
+  friend struct SdualBridge;
+
  public:
   void Clear() {
     elementary_matrices_.clear();
@@ -1003,6 +1009,8 @@ class EtaFactorization {
 };
 
 class BasisFactorization {
+  friend struct SdualBridge;
+
  public:
   BasisFactorization(const CompactSparseMatrix* matrix, const std::vector<int>* basis)
       : compact_matrix_(*matrix), basis_(*basis) {}

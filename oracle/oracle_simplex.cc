@@ -416,6 +416,8 @@ void VariablesInfo::EndDualPhaseI(Fractional tol, const std::vector<Fractional>&
 // ---------------------------------------------------------------------------
 // DualEdgeNorms (dual_edge_norms.cc)
 class DualEdgeNorms {
+  friend struct SdualBridge;
+
  public:
   explicit DualEdgeNorms(const BasisFactorization& bf) : bf_(bf) {}
   void SetParameters(const GlopParameters& p) { params_ = p; }
@@ -479,6 +481,8 @@ class DualEdgeNorms {
 // ---------------------------------------------------------------------------
 // UpdateRow (update_row.cc)
 class UpdateRow {
+  friend struct SdualBridge;
+
  public:
   UpdateRow(const CompactSparseMatrix& m, const CompactSparseMatrix& t,
             const VariablesInfo& vi, const std::vector<int>& basis,
@@ -889,6 +893,8 @@ void PrimalEdgeNorms::UpdateDevexWeights(int /*entering_col*/, int leaving_col,
 // ---------------------------------------------------------------------------
 // ReducedCosts (reduced_costs.cc:24-510)
 class ReducedCosts {
+  friend struct SdualBridge;
+
  public:
   ReducedCosts(const CompactSparseMatrix& m, const std::vector<Fractional>& obj,
                const std::vector<int>& basis, const VariablesInfo& vi,
@@ -1252,6 +1258,8 @@ class PrimalPrices {
 // ---------------------------------------------------------------------------
 // EnteringVariable (entering_variable.cc)
 class EnteringVariable {
+  friend struct SdualBridge;
+
  public:
   EnteringVariable(const VariablesInfo& vi, Rng* random, ReducedCosts* rc)
       : variables_info_(vi), random_(random), reduced_costs_(rc) {}
@@ -1462,6 +1470,8 @@ Status EnteringVariable::DualPhaseIChooseEnteringColumn(bool nothing_to_recomput
 // ---------------------------------------------------------------------------
 // VariableValues (variable_values.cc)
 class VariableValues {
+  friend struct SdualBridge;
+
  public:
   VariableValues(const GlopParameters& p, const CompactSparseMatrix& m,
                  const std::vector<int>& basis, const VariablesInfo& vi,
@@ -1977,6 +1987,8 @@ void CompleteBixbyBasis(const CompactSparseMatrix& matrix, const std::vector<Fra
 // ---------------------------------------------------------------------------
 // RevisedSimplex (revised_simplex.cc)
 class RevisedSimplex {
+  friend struct SdualBridge;
+
  public:
   RevisedSimplex();
   void SetParameters(const GlopParameters& p) {  // revised_simplex.cc:3586-3593
@@ -2257,7 +2269,29 @@ class RevisedSimplex {
   bool objective_limit_reached_ = false;
   SparseColumn leaving_candidates_;
   std::vector<int> equivalent_leaving_choices_;
+#ifdef ORACLE_SDUAL
+  std::vector<char> sdual_buffer_;
+#endif
 };
+
+#ifdef ORACLE_SDUAL
+// Test build only: the device dual segment's host restatement runs inside
+// the oracle's own loop, so the CPU checks can require it to change nothing.
+}  // namespace oracle
+#include <cstring>
+#include "sdual_core.h"
+namespace oracle {
+std::atomic<int64_t> g_sdual_segments{0}, g_sdual_iterations{0};
+struct SdualHooks {
+  static bool Supported(const RevisedSimplex&) { return true; }
+  static void PrepareForPack(RevisedSimplex&) {}
+  static void AfterUnpack(RevisedSimplex&, const sdual::Lp& s) {
+    ++g_sdual_segments;
+    g_sdual_iterations += s.iterations_done;
+  }
+};
+#include "sdual_bridge.inc"
+#endif
 
 RevisedSimplex::RevisedSimplex()
     : random_(42),
@@ -3572,6 +3606,16 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
       }
     }
 
+#ifdef ORACLE_SDUAL
+    if (!feasibility_phase && SdualBridge::Supported(*this, time_limit)) {
+      Status st;
+      bool keep_looping = true;
+      SdualBridge::RunOnHost(*this, time_limit, &refactorize, &st, &keep_looping,
+                             &sdual_buffer_);
+      if (!keep_looping) return st;
+      continue;
+    }
+#endif
     if (feasibility_phase) {
       ORACLE_RETURN_IF_ERROR(
           DualPhaseIChooseLeavingVariableRow(&leaving_row, &cost_variation, &target_bound));
@@ -3938,6 +3982,13 @@ extern "C" {
 
 void* oracle_lp_create() { return new OracleHandle(); }
 void oracle_lp_destroy(void* h) { delete static_cast<OracleHandle*>(h); }
+
+#ifdef ORACLE_SDUAL
+// Segments / iterations the sdual restatement ran in this process.
+int64_t oracle_sdual_counter(int32_t which) {
+  return which == 0 ? oracle::g_sdual_segments.load() : oracle::g_sdual_iterations.load();
+}
+#endif
 
 int oracle_lp_set_params(void* hv, const mi_glop_params* p) {
   auto* h = static_cast<OracleHandle*>(hv);

@@ -14,19 +14,22 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
 ORACLE_SO = os.path.join(ORACLE_DIR, "build", "liboracle_glop.so")
 
-_lib = None
+_libs = {}
 
 
 def build():
     subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(ORACLE_SO):
+def lib(variant="glop"):
+    """variant "glop": the oracle. "sdual": the same oracle with the device
+    dual segment's host restatement (or-tools_amd/csrc/sdual) in its dual loop,
+    a test-only build that the CPU checks compare with the oracle."""
+    if variant not in _libs:
+        path = os.path.join(ORACLE_DIR, "build", f"liboracle_{variant}.so")
+        if not os.path.exists(path):
             build()
-        L = ctypes.CDLL(ORACLE_SO)
+        L = ctypes.CDLL(path)
         L.oracle_lp_create.restype = ctypes.c_void_p
         L.oracle_lp_destroy.argtypes = [ctypes.c_void_p]
         vp = ctypes.c_void_p
@@ -58,8 +61,8 @@ def lib():
         L.oracle_lp_get_unit_row_left_inverse.argtypes = [vp, ctypes.c_int32, vp, vp, vp]
         L.oracle_lp_compute_dictionary.argtypes = [vp, vp, ctypes.c_int32, vp]
         L.oracle_lp_get_dictionary.argtypes = [vp, vp, vp, vp]
-        _lib = L
-    return _lib
+        _libs[variant] = L
+    return _libs[variant]
 
 
 def _p(a):
@@ -69,8 +72,8 @@ def _p(a):
 class OracleLp:
     """Same surface as mi_glop.engine.LpHandle, CPU restatement behind it."""
 
-    def __init__(self, params=None):
-        self._L = lib()
+    def __init__(self, params=None, variant="glop"):
+        self._L = lib(variant)
         self.h = ctypes.c_void_p(self._L.oracle_lp_create())
         self.params = params or abi.default_params()
         self.lp = None
@@ -208,7 +211,7 @@ class OracleLp:
 def batch_solve_bounds(workers, lbs, ubs, warm_state=None):
     """CPU baseline / checker of engine.batch_solve_bounds (one thread per
     oracle worker, shared LP counter)."""
-    L = lib()
+    L = workers[0]._L
     for w in workers:
         L.oracle_lp_set_params(w.h, ctypes.byref(w.params))
     lbs = np.ascontiguousarray(lbs, dtype=np.float64)
