@@ -184,7 +184,10 @@ enum {
                               (LowerSolveStartingAt, lu_factorization.cc:405-436) */
   MI_K_TRI_SOLVE_UPPER = 13, /* dense UpperSolve (sparse.cc:814-846): the product-form and
                                 squared-norm FTRANs' U */
-  MI_K_COUNT = 14
+  MI_K_SDUAL = 14,      /* device dual simplex segment: whole phase-II dual iterations of one
+                           LP on one workgroup (revised_simplex.cc:3058-3367); bytes = the
+                           state arena moved in and out */
+  MI_K_COUNT = 15
 };
 
 void mi_glop_params_default(mi_glop_params* p);
@@ -298,6 +301,10 @@ typedef struct mi_lp_run_counters {
   int64_t u_levels;
   int64_t u_outputs;
   int64_t u_entries;
+  /* Device dual simplex segments (MILP_SDUAL; phase-II dual iterations run
+   * whole on one workgroup) and the iterations they ran, since creation. */
+  int64_t sdual_segments;
+  int64_t sdual_iterations;
 } mi_lp_run_counters;
 int mi_lp_record_iteration_times(mi_lp* h, int32_t enable);
 int64_t mi_lp_get_iteration_times(const mi_lp* h, double* out, int64_t cap);

@@ -20,6 +20,9 @@ namespace milp_kernels {
 struct TriSolveArgs;
 struct ScanState;
 }
+namespace sdual {
+struct Mailbox;
+}
 
 namespace milp {
 
@@ -211,6 +214,28 @@ class DeviceLp : public DeviceSolver {
   bool small_batch() const { return small_batch_; }
   int shard_begin(int s) const { return shard_begin_[s]; }
 
+  // --- device dual simplex segment (csrc/sdual) ----------------------------
+  // A device arena and a pinned staging image of at least `bytes`; the
+  // RevisedSimplex side packs into sdual_staging() with pointers into
+  // sdual_arena(), SdualRun moves [0, bytes) in, runs the segment on one
+  // workgroup and moves it back (fiber-aware wait).
+  // The mailbox (pinned, coherent, mapped) carries the segment's
+  // factorization requests: rows basis entries and an LuImage of lu_cap.
+  void SdualReserve(size_t bytes, int rows, int64_t lu_cap);
+  void SdualFree();
+  char* sdual_staging() const { return static_cast<char*>(sdual_staging_); }
+  uintptr_t sdual_arena() const { return reinterpret_cast<uintptr_t>(sdual_arena_); }
+  // serve(ctx) answers a request (the mailbox flag is 1) by writing an
+  // LuImage into sdual_mailbox_image(); SdualRun then raises the flag to 2.
+  void SdualRun(size_t bytes, const double* arena_coeff, int n, void (*serve)(void*), void* ctx);
+  sdual::Mailbox* sdual_mailbox() const { return sdual_mb_; }
+  const int32_t* sdual_mailbox_basis() const { return sdual_mb_basis_; }
+  char* sdual_mailbox_image() const { return sdual_mb_image_; }
+  void SdualMailboxDevice(sdual::Mailbox** mb, int32_t** basis, char** image) const;
+  void SdualMatrix(const int64_t** starts, const int32_t** rows, const double** vals,
+                   const int64_t** t_starts, const int32_t** t_cols,
+                   const double** t_vals) const;
+
  private:
   template <typename T>
   T* Alloc(size_t n);
@@ -316,6 +341,16 @@ class DeviceLp : public DeviceSolver {
                          void* stream);
   void CaptureTriGraph(int which, TriContext* c);
   void FreeTriBuffers();
+
+  void* sdual_arena_ = nullptr;
+  void* sdual_staging_ = nullptr;
+  size_t sdual_cap_ = 0;
+  void* sdual_mb_block_ = nullptr;  // pinned: Mailbox | basis | LuImage
+  size_t sdual_mb_cap_ = 0;
+  sdual::Mailbox* sdual_mb_ = nullptr;
+  int32_t* sdual_mb_basis_ = nullptr;
+  char* sdual_mb_image_ = nullptr;
+  void* sdual_mb_device_ = nullptr;
 
   int device_ = -1;
   void* stream_ = nullptr;  // hipStream_t

@@ -64,6 +64,7 @@ DeviceLp::~DeviceLp() {
   }
   if (batch_slot_ >= 0 && slot_idle) ReleaseSmallBatchSlot(device_, batch_slot_);
   if (stream_ != nullptr) (void)hipStreamSynchronize(S(stream_));
+  SdualFree();
   FreeTriBuffers();
   for (void* p : allocations_) (void)hipFree(p);
   if (h_pin_i_) (void)hipHostFree(h_pin_i_);

@@ -20,6 +20,10 @@
 
 namespace milp {
 
+// Host bridge of the device dual segment (csrc/sdual/sdual_bridge.inc).
+struct SdualBridge;
+struct SdualHooks;
+
 using Fractional = double;
 using RowIndex = int32_t;
 using ColIndex = int32_t;

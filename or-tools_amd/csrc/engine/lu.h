@@ -809,6 +809,8 @@ class Markowitz {
 
 // lu_factorization.{h,cc}
 class LuFactorization {
+  friend struct SdualBridge;
+
  public:
   void Clear();
   Status ComputeFactorization(const CompactSparseMatrixView& b);
@@ -902,6 +904,8 @@ class LuFactorization {
 
 // rank_one_update.h:30-148
 class RankOneUpdateElementaryMatrix {
+  friend struct SdualBridge;
+
  public:
   RankOneUpdateElementaryMatrix(const CompactSparseMatrix* storage, int u_index,
                                 int v_index, Fractional u_dot_v)
@@ -947,6 +951,8 @@ class RankOneUpdateElementaryMatrix {
 
 // rank_one_update.h:150-246
 class RankOneUpdateFactorization {
+  friend struct SdualBridge;
+
  public:
   void Clear() {
     elementary_matrices_.clear();
@@ -1073,6 +1079,9 @@ class EtaFactorization {
 };
 
 class BasisFactorization {
+  friend struct SdualBridge;
+  friend struct SdualHooks;
+
  public:
   BasisFactorization(const CompactSparseMatrix* matrix, const std::vector<int>* basis);
   ~BasisFactorization();

@@ -534,6 +534,9 @@ void VariablesInfo::EndDualPhaseI(Fractional tol, const std::vector<Fractional>&
 // ---------------------------------------------------------------------------
 // DualEdgeNorms (dual_edge_norms.cc)
 class DualEdgeNorms {
+  friend struct SdualBridge;
+  friend struct SdualHooks;
+
  public:
   explicit DualEdgeNorms(const BasisFactorization& bf) : bf_(bf) {}
   void SetParameters(const GlopParameters& p) { params_ = p; }
@@ -605,6 +608,9 @@ class DualEdgeNorms {
 // ---------------------------------------------------------------------------
 // UpdateRow (update_row.cc)
 class UpdateRow {
+  friend struct SdualBridge;
+  friend struct SdualHooks;
+
  public:
   UpdateRow(const CompactSparseMatrix& m, const CompactSparseMatrix& t,
             const VariablesInfo& vi, const std::vector<int>& basis,
@@ -1290,6 +1296,9 @@ void PrimalEdgeNorms::UpdateDevexWeights(int /*entering_col*/, int leaving_col,
 // ---------------------------------------------------------------------------
 // ReducedCosts (reduced_costs.cc:24-510)
 class ReducedCosts {
+  friend struct SdualBridge;
+  friend struct SdualHooks;
+
  public:
   ReducedCosts(const CompactSparseMatrix& m, const std::vector<Fractional>& obj,
                const std::vector<int>& basis, const VariablesInfo& vi,
@@ -1939,6 +1948,9 @@ class PrimalPrices {
 // ---------------------------------------------------------------------------
 // EnteringVariable (entering_variable.cc)
 class EnteringVariable {
+  friend struct SdualBridge;
+  friend struct SdualHooks;
+
  public:
   EnteringVariable(const VariablesInfo& vi, Rng* random, ReducedCosts* rc)
       : variables_info_(vi), random_(random), reduced_costs_(rc) {}
@@ -2293,6 +2305,9 @@ Status EnteringVariable::DualPhaseIChooseEnteringColumn(bool nothing_to_recomput
 // ---------------------------------------------------------------------------
 // VariableValues (variable_values.cc)
 class VariableValues {
+  friend struct SdualBridge;
+  friend struct SdualHooks;
+
  public:
   VariableValues(const GlopParameters& p, const CompactSparseMatrix& m,
                  const std::vector<int>& basis, const VariablesInfo& vi,
@@ -2893,6 +2908,9 @@ void CompleteBixbyBasis(const CompactSparseMatrix& matrix, const std::vector<Fra
 // ---------------------------------------------------------------------------
 // RevisedSimplex (revised_simplex.cc)
 class RevisedSimplex {
+  friend struct SdualBridge;
+  friend struct SdualHooks;
+
  public:
   RevisedSimplex();
   void SetParameters(const GlopParameters& p) {  // revised_simplex.cc:3586-3593
@@ -3124,6 +3142,24 @@ class RevisedSimplex {
                  static_cast<unsigned long long>(HashBits(reduced_costs_.RawReducedCosts())),
                  static_cast<unsigned long long>(HashBits(primal_edge_norms_.RawEdgeNorms())),
                  ComputeObjectiveValue());
+    // MILP_TRACE_DUMP=k: raw x, rc and basis at iterations k-1 and k.
+    static const char* dump = std::getenv("MILP_TRACE_DUMP");
+    if (dump != nullptr && num_iterations_ + 1 >= std::atoll(dump) &&
+        num_iterations_ <= std::atoll(dump)) {
+      const std::string base = std::string(prefix) + ".it" + std::to_string(num_iterations_) +
+                               ".%s";
+      auto put = [&](const char* what, const void* p, size_t bytes) {
+        char name[512];
+        std::snprintf(name, sizeof(name), base.c_str(), what);
+        if (FILE* d = std::fopen((std::string(name) + ".device").c_str(), "wb")) {
+          std::fwrite(p, 1, bytes, d);
+          std::fclose(d);
+        }
+      };
+      put("x", variable_values_.GetDenseRow().data(), sizeof(Fractional) * num_cols_);
+      put("rc", reduced_costs_.RawReducedCosts().data(), sizeof(Fractional) * num_cols_);
+      put("basis", basis_.data(), sizeof(int) * num_rows_);
+    }
     if (num_cols_ <= 64) {
       const std::vector<Fractional>* vs[3] = {&variable_values_.GetDenseRow(),
                                               &reduced_costs_.RawReducedCosts(),
@@ -3202,7 +3238,64 @@ class RevisedSimplex {
   std::vector<int> flush_cols_;
   std::vector<uint8_t> flush_bits_;
   std::vector<uint8_t> flip_flags_;
+  // Device dual segment (csrc/sdual): 0 off, 1 on the host (the same
+  // restatement compiled for the CPU, a debugging aid), 2 on the device.
+  int sdual_mode_ = 0;
+  std::vector<char> sdual_buffer_;
+  int64_t sdual_segments_ = 0;
+  int64_t sdual_iterations_ = 0;
+  // -1: no segment (the host runs the iteration), else SdualBridge::Continue's
+  // answer: kReturn (DualMinimize returns *status), kLoopTop, kBody.
+  int RunSdualSegment(TimeLimit* tl, bool* refactorize, Status* status);
+
+ public:
+  void SdualCounters(int64_t* segments, int64_t* iterations) const {
+    *segments = sdual_segments_;
+    *iterations = sdual_iterations_;
+  }
 };
+
+// ---------------------------------------------------------------------------
+// Device dual simplex segment: the engine's side of csrc/sdual.
+}  // namespace milp
+#include "../sdual/sdual_core.h"
+namespace milp {
+struct SdualHooks {
+  static bool Supported(const RevisedSimplex& rs) {
+    return rs.sdual_mode_ != 0 && !rs.dual_device_mode_ && !rs.iteration_hook &&
+           rs.device_.num_shards() == 1 && !rs.basis_factorization_.tau_u_pending_;
+  }
+  // Engine-only deferred work must be settled before the state is read: a
+  // pending tau on the worker (dropped, as any other use of the factorization
+  // would), a deferred column-wise update row, the host mirror of the row.
+  static void PrepareForPack(RevisedSimplex& rs) {
+    rs.basis_factorization_.DropAsync();
+    rs.update_row_.Materialize();
+    rs.update_row_.EnsureHost();
+  }
+  static void AfterUnpack(RevisedSimplex& rs, const sdual::Lp& s) {
+    UpdateRow& ur = rs.update_row_;
+    ur.listed_.assign(rs.num_cols_, 0);
+    for (const int pos : ur.non_zero_position_list_) ur.listed_[pos] = 1;
+    ur.host_stale_ = false;
+    ur.known_col_ = -1;
+    ur.pending_column_wise_ = false;
+    ++ur.epoch_;
+    ++rs.sdual_segments_;
+    rs.sdual_iterations_ += s.iterations_done;
+  }
+};
+#define SDUAL_DEVICE_RUNNER 1
+#include "../sdual/sdual_bridge.inc"
+
+// One segment (MILP_SDUAL=host: the host build of the same code).
+int RevisedSimplex::RunSdualSegment(TimeLimit* tl, bool* refactorize, Status* status) {
+  if (!SdualBridge::Supported(*this, tl)) return -1;
+  if (sdual_mode_ == 1) {
+    return SdualBridge::RunOnHost(*this, tl, refactorize, status, &sdual_buffer_);
+  }
+  return SdualBridge::RunOnDevice(*this, tl, refactorize, status);
+}
 
 RevisedSimplex::RevisedSimplex()
     : random_(42),
@@ -3222,6 +3315,10 @@ RevisedSimplex::RevisedSimplex()
   reduced_costs_.SetDeferredNorms(&primal_edge_norms_);
   basis_factorization_.SetDeviceSolver(&device_);
   SetParameters(parameters_);
+  if (const char* e = std::getenv("MILP_SDUAL")) {
+    if (std::strcmp(e, "host") == 0) sdual_mode_ = 1;
+    if (std::strcmp(e, "device") == 0 || std::strcmp(e, "on") == 0) sdual_mode_ = 2;
+  }
 }
 
 // revised_simplex.cc:139-635
@@ -4658,6 +4755,15 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     }
     clock.Mark(0);
 
+    if (!feasibility_phase && sdual_mode_ != 0) {
+      Status sd_status;
+      int sd;
+      do {
+        sd = RunSdualSegment(time_limit, &refactorize, &sd_status);
+      } while (sd == SdualBridge::kBody);
+      if (sd == SdualBridge::kLoopTop) continue;
+      if (sd == SdualBridge::kReturn) return sd_status;
+    }
     if (feasibility_phase) {
       MILP_RETURN_IF_ERROR(
           DualPhaseIChooseLeavingVariableRow(&leaving_row, &cost_variation, &target_bound));
@@ -5688,6 +5794,7 @@ int mi_lp_get_run_counters(const mi_lp* h, mi_lp_run_counters* c) {
   c->iterations = h->simplex.GetNumberOfIterations();
   const_cast<mi_lp*>(h)->simplex.device().TriScheduleShape(&c->u_levels, &c->u_outputs,
                                                           &c->u_entries);
+  h->simplex.SdualCounters(&c->sdual_segments, &c->sdual_iterations);
   return MI_LP_OK;
 }
 

@@ -125,6 +125,8 @@ inline int UniformInt(Rng& g, int hi) {  // std::uniform_int_distribution<int>(0
 
 // pricing.h:58-345 DynamicMaximum.
 class DynamicMaximum {
+  friend struct SdualBridge;
+
  public:
   explicit DynamicMaximum(Rng* random) : random_(random) {}
   void ClearAndResize(int n) {
@@ -188,6 +190,8 @@ class DynamicMaximum {
 
 // variables_info.{h,cc}
 class VariablesInfo {
+  friend struct SdualBridge;
+
  public:
   explicit VariablesInfo(const CompactSparseMatrix& m) : matrix_(m) {}
   bool LoadBoundsAndReturnTrueIfUnchanged(const std::vector<double>& vlb,

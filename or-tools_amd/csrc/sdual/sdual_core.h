@@ -827,6 +827,60 @@ SD_INLINE void bf_right_solve(Lp& s, Vec& d) {
   vec_sort_if_needed(d);
   bf_bump(s, vec_nnz_estimate(d));
 }
+// LeftSolveUWithNonZeros (lu_factorization.cc:298-312)
+SD_INLINE void lu_left_solve_u_with_nz(Lp& s, Vec& y) {
+  if (s.is_identity) return;
+  tri_rows_to_consider(s.tupper, y.nz, &y.nnz, s.stored);
+  y.sorted = 1;
+  if (y.nnz == 0) {
+    tri_transpose_upper_solve(s.upper, y.values);
+  } else {
+    tri_transpose_hyper_solve(s.upper, y.values, y.nz, &y.nnz);
+  }
+}
+// BasisFactorization::LeftSolve (basis_representation.cc:342-356, MPF)
+SD_INLINE void bf_left_solve(Lp& s, Vec& y) {
+  lu_left_solve_u_with_nz(s, y);
+  r1_left_solve_nz(s, y);
+  lu_left_solve_l_with_nz(s, y, nullptr);
+  vec_sort_if_needed(y);
+  bf_bump(s, vec_nnz_estimate(y));
+}
+// LuFactorization::DualEdgeSquaredNorm (lu_factorization.cc:158-186) with
+// BasisFactorization's bump (basis_representation.cc).
+SD_INLINE f64 bf_dual_edge_squared_norm(Lp& s, int row) {
+  bf_bump(s, 1);
+  if (s.is_identity) return 1.0;
+  const int pr = s.col_perm_empty ? row : s.col_perm[row];
+  int32_t* nz = s.dp_equiv;  // non_zero_rows_ scratch
+  int nnz = 0;
+  f64* z = s.zero_scratch;
+  z[pr] = 1.0;
+  nz[nnz++] = pr;
+  tri_rows_to_consider(s.tupper, nz, &nnz, s.stored);
+  if (nnz == 0) {
+    tri_lower_solve_from(s.tupper, pr, z);
+  } else {
+    tri_hyper_solve(s.tupper, z, nz, &nnz);
+    tri_rows_to_consider(s.tlower, nz, &nnz, s.stored);
+  }
+  if (nnz == 0) {
+    tri_upper_solve(s.tlower, z);
+  } else {
+    tri_hyper_solve_rev(s.tlower, z, nz, &nnz);
+  }
+  f64 sum = 0.0;
+  if (nnz == 0) {
+    sum = dense_squared_norm(z, s.m);
+    for (int i = 0; i < s.m; ++i) z[i] = 0.0;
+  } else {
+    for (int k = 0; k < nnz; ++k) {
+      sum += sq(z[nz[k]]);
+      z[nz[k]] = 0.0;
+    }
+  }
+  return sum;
+}
 SD_INLINE const f64* bf_right_solve_for_tau(Lp& s, const Vec& a) {
   if (s.tau_can_opt) {
     s.tau_can_opt = 0;
@@ -1048,6 +1102,15 @@ SD_INLINE int dp_get_maximum(Lp& s) {
   return dp_randomize(s, best_position, n_equiv);
 }
 
+// DualEdgeNorms::GetEdgeSquaredNorms (dual_edge_norms.cc:120-132)
+SD_INLINE const f64* norms_get(Lp& s) {
+  if (s.norms_recompute) {
+    for (int row = 0; row < s.m; ++row) s.norms[row] = bf_dual_edge_squared_norm(s, row);
+    s.norms_recompute = 0;
+  }
+  return s.norms;
+}
+
 // ---- VariableValues (variable_values.cc) ----
 SD_INLINE f64 row_infeasibility(const Lp& s, int col) {
   return sd_max(s.x[col] - s.ub[col], s.lb[col] - s.x[col]);
@@ -1057,6 +1120,7 @@ SD_INLINE void vv_recompute_dual_prices(Lp& s, int put_more_importance_on_norm) 
   dp_start_dense_updates(s);
   s.put_more_importance_on_norm = put_more_importance_on_norm;
   const f64 tol = s.primal_feasibility_tolerance;
+  norms_get(s);
   for (int row = 0; row < s.m; ++row) {
     const int col = s.basis[row];
     const f64 inf = row_infeasibility(s, col);
@@ -1083,6 +1147,7 @@ SD_INLINE void vv_update_dual_prices(Lp& s, const int32_t* rows, int n) {
     vv_recompute_dual_prices(s, s.put_more_importance_on_norm);
     return;
   }
+  norms_get(s);
   for (int k = 0; k < n; ++k) vv_update_dual_price(s, rows[k]);
 }
 SD_INLINE void vv_set_nonbasic_from_status(Lp& s, int col) {
@@ -1540,6 +1605,227 @@ SD_INLINE void rs_make_boxed_dual_feasible(Lp& s) {
   if (n_changed != 0) vv_update_given_nonbasic(s, s.changed_cols, n_changed);
 }
 
+// ---- ReducedCosts recomputation (reduced_costs.cc:303-439) ----
+SD_INLINE void rc_set_recompute_and_notify(Lp& s) {
+  s.recompute_rc = 1;
+  s.rc_notify = 1;
+}
+SD_INLINE void rc_make_precise(Lp& s) {
+  if (s.rc_precise) return;
+  s.must_refactorize = 1;
+  s.recompute_bo_left_inverse = 1;
+  rc_set_recompute_and_notify(s);
+}
+SD_INLINE void rc_clear_and_remove_cost_shifts(Lp& s) {
+  s.has_cost_shift = 0;
+  for (int c = 0; c < s.N; ++c) s.cost_pert[c] = 0.0;
+  s.recompute_bo = 1;
+  s.recompute_bo_left_inverse = 1;
+  s.rc_precise = 0;
+  rc_set_recompute_and_notify(s);
+}
+SD_INLINE void rc_compute_basic_objective(Lp& s) {
+  for (int row = 0; row < s.m; ++row) {
+    const int bc = s.basis[row];
+    s.basic_obj[row] = s.objective[bc] + s.cost_pert[bc];
+  }
+  s.recompute_bo = 0;
+  s.recompute_bo_left_inverse = 1;
+}
+SD_INLINE void rc_compute_basic_objective_left_inverse(Lp& s) {
+  if (s.recompute_bo) rc_compute_basic_objective(s);
+  Vec& y = s.bolinv;
+  for (int row = 0; row < s.m; ++row) y.values[row] = s.basic_obj[row];
+  y.size = s.m;
+  y.nnz = 0;
+  bf_left_solve(s, y);
+  s.recompute_bo_left_inverse = 0;
+}
+SD_INLINE void rc_compute_reduced_costs(Lp& s) {
+  if (s.recompute_bo_left_inverse) rc_compute_basic_objective_left_inverse(s);
+  f64 dual_residual_error = 0.0;
+  const f64* y = s.bolinv.values;
+  for (int col = 0; col < s.N; ++col) {
+    s.rc[col] = s.objective[col] + s.cost_pert[col] - col_dot(s.A, col, y);
+    if (bit_get(s.is_basic, col)) {
+      dual_residual_error = sd_max(dual_residual_error, sd_fabs(s.rc[col]));
+    }
+  }
+  s.rc_dtime += dt_ops(s.a_num_entries);
+  s.recompute_rc = 0;
+  s.rc_recomputed = 1;
+  s.rc_precise = s.num_updates == 0 ? 1 : 0;
+  s.dual_tol = s.dual_feasibility_tolerance;
+  if (dual_residual_error > s.dual_tol) s.dual_tol = dual_residual_error;
+}
+// GetReducedCosts() side effects.
+SD_INLINE void rc_get(Lp& s) {
+  if (s.num_updates == 0) s.must_refactorize = 0;
+  if (s.recompute_rc) rc_compute_reduced_costs(s);
+}
+
+// ---- factorization (host Markowitz through the mailbox) ----
+// Points the LU fields at an image installed at address `b` (`im` is a
+// readable copy of its header).
+SD_INLINE void sd_install_lu(Lp& s, const LuImage* im, uintptr_t b) {
+  auto fix = [&](Tri* t, const Tri& src) {
+    *t = src;
+    t->starts = reinterpret_cast<int64_t*>(b + reinterpret_cast<uintptr_t>(src.starts));
+    t->rows = reinterpret_cast<int32_t*>(b + reinterpret_cast<uintptr_t>(src.rows));
+    t->coefs = reinterpret_cast<f64*>(b + reinterpret_cast<uintptr_t>(src.coefs));
+    t->diag = reinterpret_cast<f64*>(b + reinterpret_cast<uintptr_t>(src.diag));
+  };
+  fix(&s.lower, im->lower);
+  fix(&s.upper, im->upper);
+  fix(&s.tupper, im->tupper);
+  fix(&s.tlower, im->tlower);
+  s.is_identity = im->is_identity;
+  s.col_perm_empty = im->col_perm_empty;
+  s.col_perm = reinterpret_cast<int32_t*>(b + im->off_col_perm);
+  s.inv_col_perm = reinterpret_cast<int32_t*>(b + im->off_inv_col_perm);
+  s.row_perm = reinterpret_cast<int32_t*>(b + im->off_row_perm);
+  s.inv_row_perm = reinterpret_cast<int32_t*>(b + im->off_inv_row_perm);
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ inline int32_t sd_mb_load(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline void sd_mb_store(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#endif
+
+// ForceRefactorization (basis_representation.cc:228-238): Clear() and a new
+// factorization of the current basis. Markowitz runs on the host (the
+// mailbox); this side mirrors Clear()'s and ComputeFactorization()'s effects.
+// Returns the image status: 0 installed, 1 LU error, 2 computed but too
+// large for the arena (the caller hands the LP back).
+SD_INLINE int sd_refactorize(Lp& s, int bump) {
+  int status;
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (int r = 0; r < s.m; ++r) s.mb_basis[r] = s.basis[r];
+  s.mb->bump = bump;
+  __threadfence_system();
+  sd_mb_store(&s.mb->flag, 1);
+  while (sd_mb_load(&s.mb->flag) != 2) __builtin_amdgcn_s_sleep(8);
+  const LuImage* im = reinterpret_cast<const LuImage*>(s.mb_image);
+  status = im->status;
+  const f64 dtime = im->last_fact_dtime;
+  if (status == 0) {
+    const int64_t words = (im->bytes + 7) / 8;
+    const volatile uint64_t* src = reinterpret_cast<const volatile uint64_t*>(s.mb_image);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(s.lu_region);
+    for (int64_t w = 0; w < words; ++w) dst[w] = src[w];
+  }
+  sd_mb_store(&s.mb->flag, 0);
+#else
+  status = s.lu_service(s.lu_ctx, &s, bump);
+  const f64 dtime = reinterpret_cast<const LuImage*>(s.lu_region)->last_fact_dtime;
+#endif
+  if (bump) {
+    f64 t = s.lu_factorization_pivot_threshold * 1.5;
+    s.lu_factorization_pivot_threshold = t < 0.9 ? t : 0.9;
+  }
+  // Clear()
+  s.num_updates = 0;
+  s.tau_can_opt = 0;
+  s.r1_count = 0;
+  s.r1_num_entries = 0;
+  s.storage.num_cols = 0;
+  s.storage.starts[0] = 0;
+  s.right_storage.num_cols = 0;
+  s.right_storage.starts[0] = 0;
+  for (int r = 0; r < s.m; ++r) s.left_pool[r] = kInvalid;
+  for (int c = 0; c < s.N; ++c) s.right_pool[c] = kInvalid;
+  // ComputeFactorization()
+  s.last_fact_dtime = dtime;
+  s.bf_dtime += dtime;
+  s.r1_dtime = 0.0;
+  ++s.factorizations;
+  // Not installed: the host's factorization (and its column permutation) is
+  // newer than anything this side holds.
+  if (status == 2) s.col_perm_empty = 0;
+  if (status == 0) {
+    sd_install_lu(s, reinterpret_cast<const LuImage*>(s.lu_region),
+                  reinterpret_cast<uintptr_t>(s.lu_region));
+  }
+  return status;
+}
+
+// PermuteBasis (revised_simplex.cc:2475-2502)
+SD_INLINE void rs_permute_basis(Lp& s) {
+  if (s.col_perm_empty) return;
+  int32_t* tmp = s.changed_cols;
+  for (int i = 0; i < s.m; ++i) tmp[s.col_perm[i]] = s.basis[i];
+  for (int i = 0; i < s.m; ++i) s.basis[i] = tmp[i];
+  f64* ftmp = s.bp_ratio;
+  if (s.dpv_size != 0) {
+    for (int i = 0; i < s.m; ++i) ftmp[s.col_perm[i]] = s.dpv[i];
+    for (int i = 0; i < s.m; ++i) s.dpv[i] = ftmp[i];
+  }
+  s.recompute_bo = 1;
+  s.recompute_bo_left_inverse = 1;
+  if (!s.norms_recompute) {
+    for (int i = 0; i < s.m; ++i) ftmp[s.col_perm[i]] = s.norms[i];
+    for (int i = 0; i < s.m; ++i) s.norms[i] = ftmp[i];
+  }
+  s.col_perm_empty = 1;
+}
+
+// MakeBoxedVariableDualFeasible(GetNonBasicBoxedVariables(), false)
+SD_INLINE void rs_make_boxed_dual_feasible_all(Lp& s) {
+  const f64 threshold = s.dual_tol;
+  rc_get(s);
+  for (int w = 0; w < s.nwords; ++w) {
+    uint64_t word = s.boxed[w];
+    while (word) {
+      const int col = w * 64 + sd_ctz(word);
+      word &= word - 1;
+      if (col >= s.N) break;
+      const f64 rc = s.rc[col];
+      const int8_t status = s.vstatus[col];
+      if (rc > threshold && status == kAtUpper) {
+        vi_to_nonbasic(s, col, kAtLower);
+        vv_set_nonbasic_from_status(s, col);
+      } else if (rc < -threshold && status == kAtLower) {
+        vi_to_nonbasic(s, col, kAtUpper);
+        vv_set_nonbasic_from_status(s, col);
+      }
+    }
+  }
+}
+// RecomputeBasicVariableValues (variable_values.cc:101-118)
+SD_INLINE void vv_recompute_basic_values(Lp& s) {
+  Vec& v = s.vv_scratch;
+  v.nnz = 0;
+  for (int r = 0; r < s.m; ++r) v.values[r] = 0.0;
+  v.size = s.m;
+  for (int w = 0; w < s.nwords; ++w) {
+    uint64_t word = s.not_basic[w];
+    while (word) {
+      const int col = w * 64 + sd_ctz(word);
+      word &= word - 1;
+      if (col >= s.N) break;
+      col_add_dense(s.A, col, -s.x[col], v.values);
+    }
+  }
+  bf_right_solve(s, v);
+  for (int row = 0; row < s.m; ++row) s.x[s.basis[row]] = v.values[row];
+  dp_clear_and_resize(s, 0);  // dual_prices_->Clear()
+}
+// PreciseScalarProduct(objective_, variable_values_) (lp_utils.h:106-114)
+SD_INLINE f64 rs_objective_value(const Lp& s) {
+  f64 sum = 0.0, err = 0.0;
+  for (int c = 0; c < s.N; ++c) {
+    err += s.objective[c] * s.x[c];
+    const f64 new_sum = sum + err;
+    err += sum - new_sum;
+    sum = new_sum;
+  }
+  return sum;
+}
+
 // Room for one more iteration in every fixed-capacity array.
 SD_INLINE bool sd_room_for_iteration(const Lp& s) {
   const int64_t need = static_cast<int64_t>(s.m) + 1;
@@ -1552,33 +1838,61 @@ SD_INLINE bool sd_room_for_iteration(const Lp& s) {
   return true;
 }
 
-// The phase-II dual loop (revised_simplex.cc:3058-3367) from the point after
-// the loop-top block, until the host is needed. Returns the exit code.
+// The phase-II dual loop (revised_simplex.cc:3058-3367), entered after the
+// loop-top block, until the loop returns or needs the host. Returns the exit.
 SD_INLINE int32_t sd_run(Lp& s) {
   s.exit_code = kExitNone;
   s.iterations_done = 0;
   bool at_top = false;  // false: enter after the loop-top block
   while (true) {
     if (at_top) {
-      // Loop top (refactorize == false here).
-      if (s.must_refactorize || s.norms_recompute || s.num_updates == 0 ||
-          (s.iteration_cap > 0 && s.iterations_done >= s.iteration_cap) ||
+      if ((s.iteration_cap > 0 && s.iterations_done >= s.iteration_cap) ||
           !sd_room_for_iteration(s)) {
-        s.refactorize = 0;
-        return s.exit_code = kExitLoopTop;
+        return s.exit_code = kExitLoopTop;  // s.refactorize carries the flag
       }
-      // !IsRefactorized(), !feasibility_phase:
-      rs_make_boxed_dual_feasible(s);
-      s.n_flips = 0;
-      vv_update_dual_prices(s, s.dir.nz, s.dir.nnz);
+      const int old_refactorize = s.refactorize;
+      if (!s.refactorize && s.must_refactorize) s.refactorize = 1;
+      if (!s.refactorize && s.norms_recompute) s.refactorize = 1;
+      // RefactorizeBasisIfNeeded
+      if (s.refactorize && s.num_updates != 0) {
+        const int st = sd_refactorize(s, 0);
+        if (st == 1) return s.exit_code = kExitLuError;
+        if (st == 2) {
+          s.refactorize = old_refactorize;
+          return s.exit_code = kExitResumeTop;
+        }
+        ur_invalidate(s);
+        rs_permute_basis(s);
+      }
+      s.refactorize = 0;
+      if (s.num_updates == 0) {
+        if (old_refactorize) rc_make_precise(s);
+        rs_make_boxed_dual_feasible_all(s);
+        vv_recompute_basic_values(s);
+        vv_recompute_dual_prices(s, s.dual_price_prioritize_norm);
+        if (s.phase_optimization && s.dual_objective_limit != sd_inf() &&
+            rs_objective_value(s) > s.dual_objective_limit) {
+          s.objective_limit_reached = 1;
+          return s.exit_code = kExitObjectiveLimit;
+        }
+      } else {
+        rs_make_boxed_dual_feasible(s);
+        s.n_flips = 0;
+        vv_update_dual_prices(s, s.dir.nz, s.dir.nnz);
+      }
     }
     at_top = true;
     // DualChooseLeavingVariableRow (:2148-2181)
     if (s.dp_size == 0) vv_recompute_dual_prices(s, s.dual_price_prioritize_norm);
     const int leaving_row = dp_get_maximum(s);
     if (leaving_row == kInvalid) {
+      if (s.num_updates != 0 || s.has_cost_shift) {
+        rc_clear_and_remove_cost_shifts(s);
+        s.refactorize = 1;
+        continue;
+      }
       s.exit_row = kInvalid;
-      return s.exit_code = kExitNoLeaving;
+      return s.exit_code = kExitOptimal;
     }
     const int lcol = s.basis[leaving_row];
     const f64 value = s.x[lcol];
@@ -1596,7 +1910,6 @@ SD_INLINE int32_t sd_run(Lp& s) {
 
     ur_compute_unit_row_left_inverse(s, leaving_row);
     if (!den_test_precision(s, leaving_row)) {
-      if (s.norms_recompute) return s.exit_code = kExitPrecision;  // host recomputes norms
       const int32_t one = leaving_row;
       vv_update_dual_prices(s, &one, 1);
       continue;
@@ -1608,20 +1921,20 @@ SD_INLINE int32_t sd_run(Lp& s) {
     if (entering_col == kInvalid) {
       if (!s.rc_precise) {
         s.refactorize = 1;
-        return s.exit_code = kExitLoopTop;
+        continue;
       }
       return s.exit_code = kExitNoEntering;
     }
     const f64 entering_coeff = s.coeff[entering_col];
     if (sd_fabs(entering_coeff) < s.dual_small_pivot_threshold && !s.rc_precise) {
       s.refactorize = 1;
-      return s.exit_code = kExitLoopTop;
+      continue;
     }
     rs_compute_direction(s, entering_col);
     if (sd_fabs(s.dir.values[leaving_row]) < s.small_pivot_threshold * s.dir_inf_norm) {
       if (!s.rc_precise) {
         s.refactorize = 1;
-        return s.exit_code = kExitLoopTop;
+        continue;
       }
     }
     rs_advance_deterministic_time(s);
@@ -1651,51 +1964,54 @@ SD_INLINE int32_t sd_run(Lp& s) {
     const f64 pivot_from_direction = s.dir.values[leaving_row];
     const f64 diff = sd_fabs(pivot_from_update_row - pivot_from_direction);
     s.exit_col = lcol;
+    int refactor = 0;  // 1: ForceRefactorization, 2: the same after the LU threshold bump
     if (diff > s.refactorization_threshold *
                    (1.0 + sd_min(sd_fabs(pivot_from_update_row), sd_fabs(pivot_from_direction)))) {
-      s.exit_lu_bump = s.num_updates < 10 ? 1 : 0;
-      return s.exit_code = kExitPivotRefactor;
-    }
-    // BasisFactorization::Update (:304-340)
-    if (s.num_updates >= s.max_updates) {
-      if (!s.dynamic_period || s.last_fact_dtime < s.r1_dtime) {
-        s.exit_lu_bump = 0;
-        return s.exit_code = kExitPivotRefactor;
+      refactor = s.num_updates < 10 ? 2 : 1;
+    } else if (s.num_updates >= s.max_updates &&
+               (!s.dynamic_period || s.last_fact_dtime < s.r1_dtime)) {
+      refactor = 1;  // BasisFactorization::Update (:304-340)
+    } else {
+      const int right_index = s.right_pool[entering_col];
+      const int left_index = s.left_pool[leaving_row];
+      ++s.num_updates;
+      if (right_index == kInvalid || left_index == kInvalid) {
+        refactor = 1;
+      } else {
+        // MiddleProductFormUpdate (:258-302)
+        for (int64_t i = s.right_storage.starts[right_index];
+             i < s.right_storage.starts[right_index + 1]; ++i) {
+          s.mpf_scratch[s.right_storage.rows[i]] = s.right_storage.coefs[i];
+          s.mpf_scratch_nz[s.n_mpf_scratch_nz++] = s.right_storage.rows[i];
+        }
+        lu_column_of_u(s, leaving_row);
+        for (int k = 0; k < s.n_col_u; ++k) {
+          s.mpf_scratch[s.col_u_rows[k]] -= s.col_u_coefs[k];
+          s.mpf_scratch_nz[s.n_mpf_scratch_nz++] = s.col_u_rows[k];
+        }
+        const f64 scalar_product = col_dot(s.storage, left_index, s.mpf_scratch);
+        const int u_index =
+            store_add_and_clear(s.storage, s.mpf_scratch, s.mpf_scratch_nz, &s.n_mpf_scratch_nz);
+        const f64 mu = 1.0 + scalar_product;
+        if (mu == 0.0) return s.exit_code = kExitLuError;
+        s.r1_u[s.r1_count] = u_index;
+        s.r1_v[s.r1_count] = left_index;
+        s.r1_mu[s.r1_count] = mu;
+        ++s.r1_count;
+        s.r1_num_entries += col_entries(s.storage, u_index) + col_entries(s.storage, left_index);
+        s.tau_can_opt = 0;
       }
     }
-    const int right_index = s.right_pool[entering_col];
-    const int left_index = s.left_pool[leaving_row];
-    if (right_index == kInvalid || left_index == kInvalid) {
-      s.exit_lu_bump = 0;
-      return s.exit_code = kExitPivotRefactor;
+    if (refactor != 0) {
+      const int st = sd_refactorize(s, refactor == 2 ? 1 : 0);
+      if (st == 1) return s.exit_code = kExitLuError;
+      if (st == 2) return s.exit_code = kExitResumePivot;
+      rs_permute_basis(s);  // IsRefactorized() holds after a factorization
     }
-    ++s.num_updates;
-    // MiddleProductFormUpdate (:258-302)
-    {
-      for (int64_t i = s.right_storage.starts[right_index];
-           i < s.right_storage.starts[right_index + 1]; ++i) {
-        s.mpf_scratch[s.right_storage.rows[i]] = s.right_storage.coefs[i];
-        s.mpf_scratch_nz[s.n_mpf_scratch_nz++] = s.right_storage.rows[i];
-      }
-      lu_column_of_u(s, leaving_row);
-      for (int k = 0; k < s.n_col_u; ++k) {
-        s.mpf_scratch[s.col_u_rows[k]] -= s.col_u_coefs[k];
-        s.mpf_scratch_nz[s.n_mpf_scratch_nz++] = s.col_u_rows[k];
-      }
-      const f64 scalar_product = col_dot(s.storage, left_index, s.mpf_scratch);
-      const int u_index =
-          store_add_and_clear(s.storage, s.mpf_scratch, s.mpf_scratch_nz, &s.n_mpf_scratch_nz);
-      const f64 mu = 1.0 + scalar_product;
-      if (mu == 0.0) return s.exit_code = kExitLuError;
-      s.r1_u[s.r1_count] = u_index;
-      s.r1_v[s.r1_count] = left_index;
-      s.r1_mu[s.r1_count] = mu;
-      ++s.r1_count;
-      s.r1_num_entries += col_entries(s.storage, u_index) + col_entries(s.storage, left_index);
-    }
-    s.tau_can_opt = 0;
-    // IsRefactorized() is false here: no PermuteBasis.
     vv_set_nonbasic_from_status(s, lcol);
+#if !defined(__HIP_DEVICE_COMPILE__)
+    if (s.trace != nullptr) s.trace(&s);
+#endif
     ++s.num_iterations;  // OnIterationDone
     ++s.iterations_done;
   }

@@ -85,8 +85,36 @@ enum SdExit : int32_t {
   kExitNoEntering = 4,     // entering_col == kInvalidCol block
   kExitReturnOk = 5,       // iteration or deterministic limit: return OK
   kExitPivotRefactor = 6,  // UpdateAndPivot must refactorize (host Markowitz)
-  kExitLuError = 7,        // MiddleProductFormUpdate: degenerate rank-one update
+  kExitLuError = 7,        // degenerate rank-one update / LU failure: return error
   kExitCapacity = 8,       // a fixed capacity would overflow: resume at loop top
+  kExitOptimal = 9,        // no leaving row on a fresh factorization: OPTIMAL
+  kExitObjectiveLimit = 10,  // DUAL_FEASIBLE, objective limit reached
+  // The host already refactorized (its LU did not fit the arena): resume
+  // after RefactorizeBasisIfNeeded's factorization with old_refactorize =
+  // exit_refactorize, or after UpdateAndPivot's.
+  kExitResumeTop = 11,
+  kExitResumePivot = 12,
+};
+
+// The factorization as the device stores it: a header followed by its arrays;
+// array pointers are offsets from the header until installed (sd_install_lu).
+struct LuImage {
+  int64_t bytes;
+  int32_t status;  // 0 OK, 1 LU error, 2 did not fit
+  int32_t is_identity;
+  int32_t col_perm_empty;
+  int32_t pad;
+  double last_fact_dtime;
+  Tri lower, upper, tupper, tlower;
+  int64_t off_col_perm, off_inv_col_perm, off_row_perm, off_inv_row_perm;
+};
+
+// Host <-> running kernel requests (pinned, mapped): the device asks for a
+// Markowitz factorization of its basis; the host answers with an LuImage.
+struct Mailbox {
+  int32_t flag;  // 0 idle, 1 request, 2 answer ready
+  int32_t bump;  // UpdateAndPivot raised the LU pivot threshold first
+  int64_t image_cap;
 };
 
 struct Lp {
@@ -237,6 +265,32 @@ struct Lp {
   // ---- std::mt19937_64 (libstdc++ layout: _M_x[312], _M_p) ----
   uint64_t mt[312];
   uint64_t mti;
+
+  // ---- refactorization service ----
+  char* lu_region;  // installed LuImage (arena)
+  int64_t lu_cap;
+  Mailbox* mb;       // mapped host memory (device mode)
+  int32_t* mb_basis; // m entries
+  char* mb_image;    // LuImage written by the host
+  // Host mode: computes the factorization of s->basis into s->lu_region;
+  // returns the LuImage status.
+  int (*lu_service)(void* ctx, Lp* s, int bump);
+  void* lu_ctx;
+  // Host mode debugging aid: called at OnIterationDone.
+  void (*trace)(const Lp* s);
+
+  // ---- state the post-factorization block uses ----
+  Vec bolinv;     // ReducedCosts::basic_objective_left_inverse_
+  Vec vv_scratch; // VariableValues::scratchpad_
+  f64 dual_feasibility_tolerance;
+  int64_t a_num_entries;
+  f64* dpv;  // dual_pricing_vector_ (phase I leftovers, permuted with the basis)
+  int dpv_size;
+  int phase_optimization;
+  f64 dual_objective_limit;
+  int objective_limit_reached;
+  int rc_notify;  // SetRecomputeReducedCostsAndNotifyWatchers ran
+  int64_t factorizations;  // served during the segment
 
   // ---- loop carry and exit ----
   int refactorize;  // the host loop's `refactorize` flag

@@ -146,12 +146,14 @@ class MiLpRunCounters(ctypes.Structure):
         ("u_levels", ctypes.c_int64),
         ("u_outputs", ctypes.c_int64),
         ("u_entries", ctypes.c_int64),
+        ("sdual_segments", ctypes.c_int64),
+        ("sdual_iterations", ctypes.c_int64),
     ]
 
 
 KERNEL_NAMES = ["pricing", "update_row", "primal_norms", "rc_update", "tri_solve",
                 "col_norms", "spmv_rows", "single_row", "dual_ratio", "readback",
-                "tri_solve_tau", "tri_solve_l", "tri_solve_t", "tri_solve_upper"]
+                "tri_solve_tau", "tri_solve_l", "tri_solve_t", "tri_solve_upper", "sdual"]
 
 # Names of every exported entry point of include/mi_lp.h (checked by tests).
 EXPORTED_SYMBOLS = [

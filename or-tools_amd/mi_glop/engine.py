@@ -281,7 +281,9 @@ class LpHandle:
         return {"factorizations": int(c.factorizations),
                 "factorization_seconds": float(c.factorization_seconds),
                 "iterations": int(c.iterations), "u_levels": int(c.u_levels),
-                "u_outputs": int(c.u_outputs), "u_entries": int(c.u_entries)}
+                "u_outputs": int(c.u_outputs), "u_entries": int(c.u_entries),
+                "sdual_segments": int(c.sdual_segments),
+                "sdual_iterations": int(c.sdual_iterations)}
 
     def reset_kernel_stats(self):
         self._L.mi_lp_reset_kernel_stats(self.h)

@@ -2199,6 +2199,24 @@ class RevisedSimplex {
                  static_cast<unsigned long long>(HashBits(reduced_costs_.RawReducedCosts())),
                  static_cast<unsigned long long>(HashBits(primal_edge_norms_.RawEdgeNorms())),
                  ComputeObjectiveValue());
+    // MILP_TRACE_DUMP=k: raw x, rc and basis at iterations k-1 and k.
+    static const char* dump = std::getenv("MILP_TRACE_DUMP");
+    if (dump != nullptr && num_iterations_ + 1 >= std::atoll(dump) &&
+        num_iterations_ <= std::atoll(dump)) {
+      const std::string base = std::string(prefix) + ".it" + std::to_string(num_iterations_) +
+                               ".%s";
+      auto put = [&](const char* what, const void* p, size_t bytes) {
+        char name[512];
+        std::snprintf(name, sizeof(name), base.c_str(), what);
+        if (FILE* d = std::fopen((std::string(name) + ".oracle").c_str(), "wb")) {
+          std::fwrite(p, 1, bytes, d);
+          std::fclose(d);
+        }
+      };
+      put("x", variable_values_.GetDenseRow().data(), sizeof(Fractional) * num_cols_);
+      put("rc", reduced_costs_.RawReducedCosts().data(), sizeof(Fractional) * num_cols_);
+      put("basis", basis_.data(), sizeof(int) * num_rows_);
+    }
     if (num_cols_ <= 64) {
       const std::vector<Fractional>* vs[3] = {&variable_values_.GetDenseRow(),
                                               &reduced_costs_.RawReducedCosts(),
@@ -3609,11 +3627,12 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
 #ifdef ORACLE_SDUAL
     if (!feasibility_phase && SdualBridge::Supported(*this, time_limit)) {
       Status st;
-      bool keep_looping = true;
-      SdualBridge::RunOnHost(*this, time_limit, &refactorize, &st, &keep_looping,
-                             &sdual_buffer_);
-      if (!keep_looping) return st;
-      continue;
+      int next;
+      do {
+        next = SdualBridge::RunOnHost(*this, time_limit, &refactorize, &st, &sdual_buffer_);
+      } while (next == SdualBridge::kBody && SdualBridge::Supported(*this, time_limit));
+      if (next == SdualBridge::kReturn) return st;
+      if (next == SdualBridge::kLoopTop) continue;
     }
 #endif
     if (feasibility_phase) {

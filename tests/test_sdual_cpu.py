@@ -1,0 +1,137 @@
+"""CPU checks of the device dual simplex segment's restatement
+(or-tools_amd/csrc/sdual/sdual_core.h). The oracle's test build
+liboracle_sdual.so runs the same restatement, compiled for the host, inside
+the oracle's own dual loop (revised_simplex.cc:3058-3367 from the leaving-row
+choice on); every result must equal the plain oracle's bit for bit, and the
+segments must actually have run."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+
+from mi_glop import abi, cpsat
+import jobshop
+import kat_lps
+import lp_gen
+import oracle_lib
+
+
+def _counters():
+    L = oracle_lib.lib("sdual")
+    L.oracle_sdual_counter.restype = ctypes.c_int64
+    return L.oracle_sdual_counter(0), L.oracle_sdual_counter(1)
+
+
+def _full(o, r):
+    var, cons = o.statuses()
+    return dict(err=r.error_code, status=r.problem_status, it=r.iterations,
+                obj=float(r.objective).hex(), x=o.primal().tobytes(),
+                rc=o.reduced_costs().tobytes(), y=o.duals().tobytes(),
+                basis=o.basis().tobytes(), var=var.tobytes(), cons=cons.tobytes(),
+                state=o.state().tobytes())
+
+
+def _both(lp, p, state=None, bounds=None):
+    out = []
+    for variant in ("glop", "sdual"):
+        o = oracle_lib.OracleLp(p, variant=variant)
+        o.load(lp)
+        if bounds is not None:
+            o.set_variable_bounds(*bounds)
+        if state is not None:
+            o.load_basis_state(state)
+        out.append(_full(o, o.solve()))
+    return out
+
+
+def _assert_same(a, b, tag):
+    bad = [k for k in a if a[k] != b[k]]
+    assert not bad, (tag, bad, a["it"], b["it"], a["obj"], b["obj"])
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_sdual_restatement_sparse(seed):
+    seg0, it0 = _counters()
+    m, n = 40 + 25 * seed, 150 + 60 * seed
+    lp = lp_gen.random_sparse_lp(m, n, 0.06 if seed % 2 else 0.03, 700 + seed,
+                                 maximize=bool(seed % 3 == 0))
+    a, b = _both(lp, abi.default_params(use_dual_simplex=1))
+    _assert_same(a, b, seed)
+    seg1, it1 = _counters()
+    assert seg1 > seg0 and it1 > it0
+
+
+def test_sdual_restatement_kats():
+    for lp, expect in (kat_lps.tiny_lp(),):
+        a, b = _both(lp, abi.default_params(use_dual_simplex=1))
+        _assert_same(a, b, "tiny")
+
+
+@pytest.mark.parametrize("shape", [(6, 6), (10, 5)])
+def test_sdual_restatement_children(shape):
+    """Config-4 children (CP-SAT BranchOnVar LPs, warm-started dual simplex
+    with an iteration cap, linear_programming_constraint.cc:485-584)."""
+    jobs = jobshop.FT06 if shape == (6, 6) else jobshop.random_instance(*shape, 5)
+    lp, ycols = jobshop.relaxation(jobs)
+    root = oracle_lib.OracleLp(abi.default_params(use_dual_simplex=1))
+    root.load(lp)
+    rr = root.solve()
+    state, x = root.state(), root.primal()
+    node = cpsat.IntegerTrail(lp.col_lb, lp.col_ub,
+                              obj_lb=math.ceil(rr.objective - cpsat.K_CP_EPSILON))
+    cols = cpsat.fractional_columns(x, ycols, limit=12)
+    lbs, ubs = cpsat.branch_lps(node, x, cols)
+    seg0, _ = _counters()
+    for cap in (1000, 7):
+        p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=cap)
+        for i in range(len(lbs)):
+            a, b = _both(lp, p, state=state, bounds=(lbs[i], ubs[i]))
+            _assert_same(a, b, (cap, i))
+    seg1, _ = _counters()
+    assert seg1 > seg0
+
+
+def test_sdual_restatement_c5_shape():
+    """A config-5-shaped LP (sparse, dual steepest edge) at small size."""
+    lp = lp_gen.sparse_c5_lp(300, 3000, 6, 41)
+    a, b = _both(lp, abi.default_params(use_dual_simplex=1))
+    _assert_same(a, b, "c5")
+
+
+def test_uniform_int_matches_libstdcxx():
+    """The restatement's std::uniform_int_distribution<int> over mt19937_64
+    (libstdc++ Lemire path) draws what the oracle draws: exercised through
+    tie-heavy LPs (equal costs give equal prices and ratios)."""
+    m, n = 60, 200
+    rng = np.random.default_rng(5)
+    lp = lp_gen.random_sparse_lp(m, n, 0.05, 77)
+    lp.obj = np.round(rng.uniform(-1, 1, lp.n) * 2) / 2  # many ties
+    a, b = _both(lp, abi.default_params(use_dual_simplex=1))
+    _assert_same(a, b, "ties")
+
+
+def test_sdual_restatement_resume_paths():
+    """With almost no room for later factorizations in the arena
+    (MILP_SDUAL_LU_SLACK), every refactorization inside a segment hands the
+    LP back through the resume exits (kExitResumeTop / kExitResumePivot);
+    results must not change. Runs in a child process (the cap is read once)."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path[:0] = %r\n"
+        "import test_sdual_cpu as t, lp_gen\n"
+        "from mi_glop import abi\n"
+        "for seed in range(3):\n"
+        "    lp = lp_gen.random_sparse_lp(80 + 30 * seed, 300, 0.05, 40 + seed)\n"
+        "    a, b = t._both(lp, abi.default_params(use_dual_simplex=1))\n"
+        "    t._assert_same(a, b, seed)\n"
+        "lp = lp_gen.sparse_c5_lp(300, 3000, 6, 41)\n"
+        "a, b = t._both(lp, abi.default_params(use_dual_simplex=1))\n"
+        "t._assert_same(a, b, 'c5')\n"
+        "print('ok')\n") % (sys.path[:6],)
+    env = dict(os.environ, MILP_SDUAL_LU_SLACK="64")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
