@@ -228,6 +228,8 @@ class DeviceLp : public DeviceSolver {
   // serve(ctx) answers a request (the mailbox flag is 1) by writing an
   // LuImage into sdual_mailbox_image(); SdualRun then raises the flag to 2.
   void SdualRun(size_t bytes, const double* arena_coeff, int n, void (*serve)(void*), void* ctx);
+  void SdualRunPooled(size_t bytes, const double* arena_coeff, int n, void (*serve)(void*),
+                      void* ctx);
   sdual::Mailbox* sdual_mailbox() const { return sdual_mb_; }
   const int32_t* sdual_mailbox_basis() const { return sdual_mb_basis_; }
   char* sdual_mailbox_image() const { return sdual_mb_image_; }
@@ -344,6 +346,7 @@ class DeviceLp : public DeviceSolver {
 
   void* sdual_arena_ = nullptr;
   void* sdual_staging_ = nullptr;
+  void* sdual_staging_dev_ = nullptr;
   size_t sdual_cap_ = 0;
   void* sdual_mb_block_ = nullptr;  // pinned: Mailbox | basis | LuImage
   size_t sdual_mb_cap_ = 0;

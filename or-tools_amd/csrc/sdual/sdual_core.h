@@ -39,6 +39,38 @@ SD_INLINE f64 sd_min(f64 a, f64 b) { return (b < a) ? b : a; }
 SD_INLINE f64 sq(f64 v) { return v * v; }
 SD_INLINE f64 dt_ops(int64_t n) { return 2e-9 * static_cast<f64>(n); }
 
+// ---- the wave ----
+// On the device all 64 lanes of the workgroup's single wave walk the loop
+// together: scalar work is executed redundantly (same addresses, same values,
+// so the memory system serves them once), and loops whose iterations are
+// independent are split over the lanes, followed by sd_sync(). On the host
+// there is one lane.
+SD_INLINE int sd_lane() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return static_cast<int>(threadIdx.x);
+#else
+  return 0;
+#endif
+}
+SD_INLINE int sd_lanes() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return static_cast<int>(blockDim.x);
+#else
+  return 1;
+#endif
+}
+SD_INLINE void sd_sync() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __threadfence_block();
+  __syncthreads();
+#endif
+}
+template <typename T>
+SD_INLINE void sd_fill(T* p, int64_t n, T v) {
+  for (int64_t i = sd_lane(); i < n; i += sd_lanes()) p[i] = v;
+  sd_sync();
+}
+
 // ---- Bitset64 ----
 SD_INLINE bool bit_get(const uint64_t* w, int i) { return (w[i >> 6] >> (i & 63)) & 1; }
 SD_INLINE void bit_set(uint64_t* w, int i) { w[i >> 6] |= (1ull << (i & 63)); }
@@ -163,7 +195,7 @@ SD_INLINE bool vec_dense(const Vec& v, f64 ratio) {
 }
 SD_INLINE void vec_clear_mask(Vec& v) {
   if (vec_dense(v, 0.8)) {
-    for (int i = 0; i < v.size; ++i) v.mask[i] = 0;
+    sd_fill<char>(v.mask, v.size, 0);
   } else {
     for (int k = 0; k < v.nnz; ++k) v.mask[v.nz[k]] = 0;
   }
@@ -199,7 +231,7 @@ SD_INLINE void vec_clear_and_resize(Vec& v, int size) {
     for (int k = 0; k < v.nnz; ++k) v.values[v.nz[k]] = 0.0;
     for (int i = v.size; i < size; ++i) v.values[i] = 0.0;
   } else {
-    for (int i = 0; i < size; ++i) v.values[i] = 0.0;
+    sd_fill<f64>(v.values, size, 0.0);
   }
   v.size = size;
   v.nnz = 0;
@@ -528,12 +560,13 @@ SD_INLINE void permute_with_scratchpad(Lp& s, const int32_t* perm, Vec& io) {
   io.values = s.zero_scratch;
   s.zero_scratch = old;
   const int size = io.size;
-  for (int i = 0; i < size; ++i) io.values[i] = 0.0;  // resize(size, 0.0) of an all-zero buffer
-  for (int i = 0; i < size; ++i) {
+  sd_fill<f64>(io.values, size, 0.0);  // resize(size, 0.0) of an all-zero buffer
+  for (int i = sd_lane(); i < size; i += sd_lanes()) {
     const f64 v = s.zero_scratch[i];
-    if (v != 0.0) io.values[perm[i]] = v;
+    if (v != 0.0) io.values[perm[i]] = v;  // a permutation: distinct targets
   }
-  for (int i = 0; i < size; ++i) s.zero_scratch[i] = 0.0;
+  sd_sync();
+  sd_fill<f64>(s.zero_scratch, size, 0.0);
 }
 SD_INLINE void permute_with_known_nz(Lp& s, const int32_t* perm, Vec& io) {
   f64* old = io.values;
@@ -660,10 +693,11 @@ SD_INLINE bool lu_left_solve_l_with_nz(Lp& s, Vec& y, Vec* before) {
     before->size = sz;
   }
   if (y.nnz == 0) {
-    for (int row = 0; row < s.m; ++row) {
+    for (int row = sd_lane(); row < s.m; row += sd_lanes()) {
       const f64 value = before->values[row];
       if (value != 0.0) y.values[s.inv_row_perm[row]] = value;
     }
+    sd_sync();
   } else {
     {  // nz->swap(result_before_permutation->non_zeros)
       int32_t* t = y.nz;
@@ -1243,12 +1277,15 @@ SD_INLINE void ur_compute_unit_row_left_inverse(Lp& s, int leaving_row) {
   bf_left_solve_for_unit_row(s, leaving_row, s.rho);
 }
 SD_INLINE void ur_row_wise(Lp& s) {
-  for (int c = 0; c < s.N; ++c) s.coeff[c] = 0.0;
+  sd_fill<f64>(s.coeff, s.N, 0.0);
+  // Rows in list order; a row's entries are distinct positions, so they are
+  // split over the lanes (each position keeps its row-by-row order).
   for (int k = 0; k < s.n_rho_filtered; ++k) {
     const int col = s.rho_filtered[k];
     const f64 mult = s.rho.values[col];
-    for (int64_t i = s.At.starts[col]; i < s.At.starts[col + 1]; ++i)
+    for (int64_t i = s.At.starts[col] + sd_lane(); i < s.At.starts[col + 1]; i += sd_lanes())
       s.coeff[s.At.rows[i]] += mult * s.At.coefs[i];
+    sd_sync();
   }
   s.n_nzpos = 0;
   const f64 drop = s.drop_tolerance;
@@ -1308,7 +1345,9 @@ SD_INLINE void ur_single_row(Lp& s, int row_as_col) {
 SD_INLINE void ur_column_wise(Lp& s) {
   s.n_nzpos = 0;
   const f64 drop = s.drop_tolerance;
-  for (int w = 0; w < s.nwords; ++w) {
+  // The dots, one column per lane (a word of the relevance mask per lane);
+  // then the list in increasing position order.
+  for (int w = sd_lane(); w < s.nwords; w += sd_lanes()) {
     uint64_t word = s.relevant[w];
     while (word) {
       const int col = w * 64 + sd_ctz(word);
@@ -1316,11 +1355,24 @@ SD_INLINE void ur_column_wise(Lp& s) {
       if (col >= s.N) break;
       const f64 c = col_dot(s.A, col, s.rho.values);
       if (sd_fabs(c) > drop) {
-        s.nzpos[s.n_nzpos++] = col;
         s.coeff[col] = c;
+        s.col_flag[col] = 1;
       }
     }
   }
+  sd_sync();
+  for (int w = 0; w < s.nwords; ++w) {
+    uint64_t word = s.relevant[w];
+    while (word) {
+      const int col = w * 64 + sd_ctz(word);
+      word &= word - 1;
+      if (col >= s.N) break;
+      if (s.col_flag[col]) s.nzpos[s.n_nzpos++] = col;
+    }
+  }
+  sd_sync();
+  for (int k = sd_lane(); k < s.n_nzpos; k += sd_lanes()) s.col_flag[s.nzpos[k]] = 0;
+  sd_sync();
 }
 SD_INLINE void ur_compute_update_row(Lp& s, int leaving_row) {
   if (s.urow_for == leaving_row) return;
@@ -1618,7 +1670,7 @@ SD_INLINE void rc_make_precise(Lp& s) {
 }
 SD_INLINE void rc_clear_and_remove_cost_shifts(Lp& s) {
   s.has_cost_shift = 0;
-  for (int c = 0; c < s.N; ++c) s.cost_pert[c] = 0.0;
+  sd_fill<f64>(s.cost_pert, s.N, 0.0);
   s.recompute_bo = 1;
   s.recompute_bo_left_inverse = 1;
   s.rc_precise = 0;
@@ -1645,8 +1697,11 @@ SD_INLINE void rc_compute_reduced_costs(Lp& s) {
   if (s.recompute_bo_left_inverse) rc_compute_basic_objective_left_inverse(s);
   f64 dual_residual_error = 0.0;
   const f64* y = s.bolinv.values;
-  for (int col = 0; col < s.N; ++col) {
+  for (int col = sd_lane(); col < s.N; col += sd_lanes()) {
     s.rc[col] = s.objective[col] + s.cost_pert[col] - col_dot(s.A, col, y);
+  }
+  sd_sync();
+  for (int col = 0; col < s.N; ++col) {
     if (bit_get(s.is_basic, col)) {
       dual_residual_error = sd_max(dual_residual_error, sd_fabs(s.rc[col]));
     }
@@ -1704,7 +1759,8 @@ __device__ inline void sd_mb_store(int32_t* p, int32_t v) {
 SD_INLINE int sd_refactorize(Lp& s, int bump) {
   int status;
 #if defined(__HIP_DEVICE_COMPILE__)
-  for (int r = 0; r < s.m; ++r) s.mb_basis[r] = s.basis[r];
+  for (int r = sd_lane(); r < s.m; r += sd_lanes()) s.mb_basis[r] = s.basis[r];
+  sd_sync();
   s.mb->bump = bump;
   __threadfence_system();
   sd_mb_store(&s.mb->flag, 1);
@@ -1716,7 +1772,8 @@ SD_INLINE int sd_refactorize(Lp& s, int bump) {
     const int64_t words = (im->bytes + 7) / 8;
     const volatile uint64_t* src = reinterpret_cast<const volatile uint64_t*>(s.mb_image);
     uint64_t* dst = reinterpret_cast<uint64_t*>(s.lu_region);
-    for (int64_t w = 0; w < words; ++w) dst[w] = src[w];
+    for (int64_t w = sd_lane(); w < words; w += sd_lanes()) dst[w] = src[w];
+    sd_sync();
   }
   sd_mb_store(&s.mb->flag, 0);
 #else
@@ -1736,8 +1793,8 @@ SD_INLINE int sd_refactorize(Lp& s, int bump) {
   s.storage.starts[0] = 0;
   s.right_storage.num_cols = 0;
   s.right_storage.starts[0] = 0;
-  for (int r = 0; r < s.m; ++r) s.left_pool[r] = kInvalid;
-  for (int c = 0; c < s.N; ++c) s.right_pool[c] = kInvalid;
+  sd_fill<int32_t>(s.left_pool, s.m, kInvalid);
+  sd_fill<int32_t>(s.right_pool, s.N, kInvalid);
   // ComputeFactorization()
   s.last_fact_dtime = dtime;
   s.bf_dtime += dtime;
@@ -1799,17 +1856,22 @@ SD_INLINE void rs_make_boxed_dual_feasible_all(Lp& s) {
 SD_INLINE void vv_recompute_basic_values(Lp& s) {
   Vec& v = s.vv_scratch;
   v.nnz = 0;
-  for (int r = 0; r < s.m; ++r) v.values[r] = 0.0;
   v.size = s.m;
-  for (int w = 0; w < s.nwords; ++w) {
-    uint64_t word = s.not_basic[w];
-    while (word) {
-      const int col = w * 64 + sd_ctz(word);
-      word &= word - 1;
-      if (col >= s.N) break;
-      col_add_dense(s.A, col, -s.x[col], v.values);
+  // sum over non-basic columns in increasing order of -x_j a_j: per row over
+  // the transpose (its entries are in increasing column order), zero
+  // multipliers skipped as ColumnAddMultipleToDenseColumn does.
+  for (int r = sd_lane(); r < s.m; r += sd_lanes()) {
+    f64 acc = 0.0;
+    for (int64_t i = s.At.starts[r]; i < s.At.starts[r + 1]; ++i) {
+      const int col = s.At.rows[i];
+      if (!bit_get(s.not_basic, col)) continue;
+      const f64 mult = -s.x[col];
+      if (mult == 0.0) continue;
+      acc += mult * s.At.coefs[i];
     }
+    v.values[r] = acc;
   }
+  sd_sync();
   bf_right_solve(s, v);
   for (int row = 0; row < s.m; ++row) s.x[s.basis[row]] = v.values[row];
   dp_clear_and_resize(s, 0);  // dual_prices_->Clear()
@@ -1840,11 +1902,38 @@ SD_INLINE bool sd_room_for_iteration(const Lp& s) {
 
 // The phase-II dual loop (revised_simplex.cc:3058-3367), entered after the
 // loop-top block, until the loop returns or needs the host. Returns the exit.
+// Phase timer (device only): 0 loop top, 1 leaving row, 2 BTRAN, 3 update
+// row, 4 ratio test, 5 FTRAN, 6 rc and norm updates with tau, 7 pivot (x,
+// basis, MPF), 8 factorization requests.
+SD_INLINE uint64_t sd_now() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return wall_clock64();
+#else
+  return 0;
+#endif
+}
+#define SD_PHASE(k)                          \
+  do {                                       \
+    const uint64_t now_ = sd_now();          \
+    s.phase_ticks[phase_] += now_ - mark_;   \
+    mark_ = now_;                            \
+    phase_ = (k);                            \
+  } while (0)
+
 SD_INLINE int32_t sd_run(Lp& s) {
   s.exit_code = kExitNone;
   s.iterations_done = 0;
   bool at_top = false;  // false: enter after the loop-top block
+  uint64_t mark_ = sd_now();
+  int phase_ = 0;
+  struct Flush {
+    Lp& s;
+    uint64_t& mark;
+    int& phase;
+    SD_HD ~Flush() { s.phase_ticks[phase] += sd_now() - mark; }
+  } flush_{s, mark_, phase_};
   while (true) {
+    SD_PHASE(0);
     if (at_top) {
       if ((s.iteration_cap > 0 && s.iterations_done >= s.iteration_cap) ||
           !sd_room_for_iteration(s)) {
@@ -1855,7 +1944,9 @@ SD_INLINE int32_t sd_run(Lp& s) {
       if (!s.refactorize && s.norms_recompute) s.refactorize = 1;
       // RefactorizeBasisIfNeeded
       if (s.refactorize && s.num_updates != 0) {
+        SD_PHASE(8);
         const int st = sd_refactorize(s, 0);
+        SD_PHASE(0);
         if (st == 1) return s.exit_code = kExitLuError;
         if (st == 2) {
           s.refactorize = old_refactorize;
@@ -1882,6 +1973,7 @@ SD_INLINE int32_t sd_run(Lp& s) {
       }
     }
     at_top = true;
+    SD_PHASE(1);
     // DualChooseLeavingVariableRow (:2148-2181)
     if (s.dp_size == 0) vv_recompute_dual_prices(s, s.dual_price_prioritize_norm);
     const int leaving_row = dp_get_maximum(s);
@@ -1908,14 +2000,17 @@ SD_INLINE int32_t sd_run(Lp& s) {
     s.exit_cost_variation = cost_variation;
     s.exit_target_bound = target_bound;
 
+    SD_PHASE(2);
     ur_compute_unit_row_left_inverse(s, leaving_row);
     if (!den_test_precision(s, leaving_row)) {
       const int32_t one = leaving_row;
       vv_update_dual_prices(s, &one, 1);
       continue;
     }
+    SD_PHASE(3);
     ur_compute_update_row(s, leaving_row);
 
+    SD_PHASE(4);
     int entering_col;
     ent_dual_choose(s, s.rc_precise != 0, cost_variation, &entering_col);
     if (entering_col == kInvalid) {
@@ -1930,6 +2025,7 @@ SD_INLINE int32_t sd_run(Lp& s) {
       s.refactorize = 1;
       continue;
     }
+    SD_PHASE(5);
     rs_compute_direction(s, entering_col);
     if (sd_fabs(s.dir.values[leaving_row]) < s.small_pivot_threshold * s.dir_inf_norm) {
       if (!s.rc_precise) {
@@ -1942,9 +2038,11 @@ SD_INLINE int32_t sd_run(Lp& s) {
       return s.exit_code = kExitReturnOk;
     }
     const bool increasing_rc_is_needed = (cost_variation > 0.0) == (entering_coeff > 0.0);
+    SD_PHASE(6);
     rc_shift_cost_if_needed(s, increasing_rc_is_needed, entering_col);
     rc_update_before_pivot(s, entering_col, leaving_row);
     den_update_before_pivot(s, leaving_row);
+    SD_PHASE(7);
     // ComputeStepToMoveBasicVariableToBound + UpdateOnPivoting
     const f64 primal_step = (s.x[lcol] - target_bound) / s.dir.values[leaving_row];
     for (int k = 0; k < s.dir.nnz; ++k) {
@@ -2003,6 +2101,7 @@ SD_INLINE int32_t sd_run(Lp& s) {
       }
     }
     if (refactor != 0) {
+      SD_PHASE(8);
       const int st = sd_refactorize(s, refactor == 2 ? 1 : 0);
       if (st == 1) return s.exit_code = kExitLuError;
       if (st == 2) return s.exit_code = kExitResumePivot;

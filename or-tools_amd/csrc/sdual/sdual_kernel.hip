@@ -5,8 +5,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
+#include <vector>
 
 #include "../engine/device_lp.h"
 #include "../engine/fibers.h"
@@ -19,8 +22,183 @@ inline hipStream_t Stream(void* p) { return reinterpret_cast<hipStream_t>(p); }
 
 // One thread walks Glop's loop; the header lives in the arena.
 __global__ __launch_bounds__(64) void sdual_segment_kernel(sdual::Lp* lp) {
-  if (threadIdx.x == 0) sdual::sd_run(*lp);
+  sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
 }
+
+// ---------------------------------------------------------------------------
+// Persistent segment pool (the batch APIs): one launch per device keeps
+// kPoolGroups workgroups resident; each claims the next queue index, waits
+// for the host to publish an LP arena there, runs its segment and raises the
+// LP's mailbox flag to 3. Queue and flags live in coherent mapped memory.
+// Every workgroup exits on the stop word or after kIdleSpins polls without
+// work, so the grid always drains.
+struct SdQueue {
+  static constexpr int kCap = 1 << 14;
+  int64_t tail;  // entries [0, tail) published
+  int32_t stop;
+  int32_t pad;
+  uint64_t entry[kCap];  // sdual::Lp* (device address of the arena header)
+};
+constexpr int kPoolGroups = 1024;
+constexpr int64_t kIdleSpins = 1 << 22;  // ~2-8 s of s_sleep polling
+
+// Cooperative copy by the workgroup (16-byte words; regions are 256-byte
+// aligned and padded).
+__device__ inline void team_copy(char* dst, const char* src, int64_t bytes) {
+  const int64_t words = (bytes + 15) / 16;
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  for (int64_t w = threadIdx.x; w < words; w += blockDim.x) d[w] = s[w];
+}
+__device__ inline void team_copy_store_prefix(const sdual::Store& st, const char* from_base,
+                                              char* to_base, uint64_t arena, bool out) {
+  // st's pointers are arena addresses; its starts are readable at from_base.
+  const int64_t* starts = reinterpret_cast<const int64_t*>(
+      from_base + (reinterpret_cast<uint64_t>(st.starts) - arena));
+  const int64_t used = starts[st.num_cols];
+  const uint64_t r = reinterpret_cast<uint64_t>(st.rows) - arena;
+  const uint64_t c = reinterpret_cast<uint64_t>(st.coefs) - arena;
+  team_copy(to_base + r, from_base + r, used * 4);
+  team_copy(to_base + c, from_base + c, used * 8);
+  (void)out;
+}
+
+__global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, unsigned long long* head) {
+  __shared__ sdual::Lp* lp_shared;
+  __shared__ int quit;
+  while (true) {
+    if (threadIdx.x == 0) {
+      quit = 0;
+      lp_shared = nullptr;
+      const unsigned long long idx = atomicAdd(head, 1ull);
+      int64_t spins = 0;
+      while (true) {
+        const int64_t tail =
+            __hip_atomic_load(&q->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (static_cast<int64_t>(idx) < tail) {
+          lp_shared = reinterpret_cast<sdual::Lp*>(__hip_atomic_load(
+              &q->entry[idx % SdQueue::kCap], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+          break;
+        }
+        if (__hip_atomic_load(&q->stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+            ++spins > kIdleSpins) {
+          quit = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(32);
+      }
+    }
+    __syncthreads();
+    if (quit) return;
+    // The entry is the staging image (device view of pinned host memory):
+    // move it into the arena, run, move the mutable part back.
+    const sdual::Lp* sh = lp_shared;
+    const char* stage = reinterpret_cast<const char*>(sh);
+    char* arena = reinterpret_cast<char*>(sh->arena_dev);
+    const uint64_t arena_addr = sh->arena_dev;
+    team_copy(arena, stage, sh->fixed_end);
+    team_copy_store_prefix(sh->storage, stage, arena, arena_addr, false);
+    team_copy_store_prefix(sh->right_storage, stage, arena, arena_addr, false);
+    __threadfence();
+    __syncthreads();
+    sdual::Lp* lp = reinterpret_cast<sdual::Lp*>(arena);
+    sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
+    __threadfence();
+    __syncthreads();
+    char* stage_out = const_cast<char*>(stage);
+    team_copy(stage_out, arena, lp->mutable_end);
+    team_copy_store_prefix(lp->storage, arena, stage_out, arena_addr, true);
+    team_copy_store_prefix(lp->right_storage, arena, stage_out, arena_addr, true);
+    if (lp->coeff_out != nullptr) {
+      for (int c = threadIdx.x; c < lp->N; c += blockDim.x) lp->coeff_out[c] = lp->coeff[c];
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&lp->mb->flag, 3, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+namespace {
+// One pool per device. Never destroyed (like SmallBatcher): the runtime may
+// be gone at process exit; the kernel drains on its idle limit.
+class SdualPool {
+ public:
+  static SdualPool& Get(int device) {
+    static std::mutex mu;
+    static std::vector<SdualPool*>* all = new std::vector<SdualPool*>();
+    std::lock_guard<std::mutex> lock(mu);
+    if (static_cast<int>(all->size()) <= device) all->resize(device + 1, nullptr);
+    if ((*all)[device] == nullptr) (*all)[device] = new SdualPool(device);
+    return *(*all)[device];
+  }
+  // Publishes one arena; (re)launches the kernel when it is not running.
+  void Enqueue(void* lp) {
+    std::lock_guard<std::mutex> lock(mu_);
+    if (!running_ || hipStreamQuery(stream_) == hipSuccess) Launch();
+    const int64_t t = q_->tail;
+    if (t - head_base_ >= SdQueue::kCap) {
+      throw DeviceError("sdual pool: queue full");
+    }
+    __atomic_store_n(&q_->entry[t % SdQueue::kCap], reinterpret_cast<uint64_t>(lp),
+                     __ATOMIC_RELEASE);
+    __atomic_store_n(&q_->tail, t + 1, __ATOMIC_RELEASE);
+  }
+  // False when the kernel is gone (idle limit) before serving a request.
+  bool Alive() {
+    std::lock_guard<std::mutex> lock(mu_);
+    return running_ && hipStreamQuery(stream_) == hipErrorNotReady;
+  }
+
+ private:
+  explicit SdualPool(int device) : device_(device) {
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    if (hipHostMalloc(reinterpret_cast<void**>(&q_), sizeof(SdQueue),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_q_), q_, 0) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_head_), sizeof(unsigned long long)) != hipSuccess ||
+        hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipSetDevice(prev);
+      throw DeviceError("sdual pool: allocation failed");
+    }
+    std::memset(q_, 0, sizeof(SdQueue));
+    (void)hipSetDevice(prev);
+  }
+  // Called with mu_ held and the previous grid (if any) drained: the queue
+  // restarts at the current tail.
+  void Launch() {
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device_);
+    if (running_) (void)hipStreamSynchronize(stream_);
+    head_base_ = q_->tail;
+    const unsigned long long h = static_cast<unsigned long long>(head_base_);
+    if (hipMemcpyAsync(d_head_, &h, sizeof(h), hipMemcpyHostToDevice, stream_) != hipSuccess) {
+      (void)hipSetDevice(prev);
+      throw DeviceError("sdual pool: head reset failed");
+    }
+    __atomic_store_n(&q_->stop, 0, __ATOMIC_RELEASE);
+    hipLaunchKernelGGL(sdual_pool_kernel, dim3(kPoolGroups), dim3(64), 0, stream_, d_q_, d_head_);
+    const hipError_t e = hipGetLastError();
+    (void)hipStreamSynchronize(nullptr);  // the head reset is a pageable copy
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) throw DeviceError("sdual pool: launch failed");
+    running_ = true;
+  }
+
+  int device_;
+  std::mutex mu_;
+  SdQueue* q_ = nullptr;
+  SdQueue* d_q_ = nullptr;
+  unsigned long long* d_head_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  bool running_ = false;
+  int64_t head_base_ = 0;
+};
+}  // namespace
 
 void DeviceLp::SdualReserve(size_t bytes, int rows, int64_t lu_cap) {
   if (bytes > sdual_cap_) {
@@ -33,7 +211,9 @@ void DeviceLp::SdualReserve(size_t bytes, int rows, int64_t lu_cap) {
       sdual_staging_ = nullptr;
     }
     Check(hipMalloc(&sdual_arena_, cap), "hipMalloc sdual arena");
-    Check(hipHostMalloc(&sdual_staging_, cap, hipHostMallocDefault), "hipHostMalloc sdual");
+    Check(hipHostMalloc(&sdual_staging_, cap, hipHostMallocMapped | hipHostMallocCoherent),
+          "hipHostMalloc sdual");
+    Check(hipHostGetDevicePointer(&sdual_staging_dev_, sdual_staging_, 0), "staging pointer");
     sdual_cap_ = cap;
   }
   const size_t basis_off = 256;
@@ -90,6 +270,14 @@ void DeviceLp::SdualMatrix(const int64_t** starts, const int32_t** rows, const d
 
 void DeviceLp::SdualRun(size_t bytes, const double* arena_coeff, int n, void (*serve)(void*),
                         void* ctx) {
+  static const bool pool = [] {
+    const char* e = std::getenv("MILP_SDUAL_POOL");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  if (pool) {
+    SdualRunPooled(bytes, arena_coeff, n, serve, ctx);
+    return;
+  }
   DeviceOp("sdual segment");
   if (batch_pending_) WaitSmallBatch();
   BeginKernel(MI_K_SDUAL);
@@ -131,6 +319,50 @@ void DeviceLp::SdualRun(size_t bytes, const double* arena_coeff, int n, void (*s
     }
   }
   DeviceOp("sdual segment done");
+}
+
+// The same segment through the device's persistent pool kernel: a resident
+// workgroup moves the staging image in and out itself (no stream work, so
+// nothing queues behind the resident grid), and signals completion through
+// the mailbox flag (3). Many LPs' segments run at once.
+void DeviceLp::SdualRunPooled(size_t bytes, const double* arena_coeff, int n,
+                              void (*serve)(void*), void* ctx) {
+  (void)bytes;
+  (void)arena_coeff;
+  (void)n;
+  DeviceOp("sdual pooled segment");
+  if (batch_pending_) WaitSmallBatch();
+  sdual::Lp* hs = reinterpret_cast<sdual::Lp*>(sdual_staging_);
+  hs->staging_dev = reinterpret_cast<uint64_t>(sdual_staging_dev_);
+  hs->coeff_out = d_coeff_;
+  int32_t* flag = &sdual_mb_->flag;
+  __atomic_store_n(flag, 0, __ATOMIC_RELEASE);
+  SdualPool& pool = SdualPool::Get(device_);
+  pool.Enqueue(sdual_staging_dev_);
+  int64_t polls = 0;
+  while (true) {
+    const int32_t f = __atomic_load_n(flag, __ATOMIC_ACQUIRE);
+    if (f == 3) break;
+    if (f == 1) {
+      DeviceOp("sdual factorization request");
+      serve(ctx);
+      __atomic_store_n(flag, 2, __ATOMIC_RELEASE);
+      continue;
+    }
+    if ((++polls & 1023) == 0 && !pool.Alive() && __atomic_load_n(flag, __ATOMIC_ACQUIRE) == 0) {
+      // The grid drained (idle limit) before claiming this entry: publish it
+      // again on a new grid.
+      pool.Enqueue(sdual_staging_dev_);
+    }
+    if (InFiber()) {
+      FiberYield();
+      RestoreDevice();
+    } else {
+      std::this_thread::yield();
+    }
+  }
+  ++stats_.launches[MI_K_SDUAL];
+  DeviceOp("sdual pooled segment done");
 }
 
 }  // namespace milp

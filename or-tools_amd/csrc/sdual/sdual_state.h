@@ -196,6 +196,7 @@ struct Lp {
   int n_nzpos;
   uint64_t* nzset;  // non_zero_position_set_ (nwords)
   f64* coeff;       // coefficient_ (N)
+  char* col_flag;   // column-wise pass scratch (N, zero between uses)
   int left_inv_for;
   int urow_for;
   int64_t ur_ops;
@@ -291,6 +292,15 @@ struct Lp {
   int objective_limit_reached;
   int rc_notify;  // SetRecomputeReducedCostsAndNotifyWatchers ran
   int64_t factorizations;  // served during the segment
+
+  // ---- transfers of the pooled path (the workgroup moves its own arena) ----
+  uint64_t arena_dev;    // device address of this header's arena
+  uint64_t staging_dev;  // device view of the pinned staging image
+  int64_t fixed_end;     // [0, fixed_end) moves in
+  int64_t mutable_end;   // [0, mutable_end) moves out
+  f64* coeff_out;        // DeviceLp's update-row coefficients (N), refreshed at the end
+  // Device time per loop phase (wall_clock64 ticks, 100 MHz): see sd_run.
+  uint64_t phase_ticks[12];
 
   // ---- loop carry and exit ----
   int refactorize;  // the host loop's `refactorize` flag

@@ -1,16 +1,18 @@
 #!/bin/bash
-# Round 3: device dual segments with the mailbox factorization service
-# (tests/test_sdual_gpu.py), the config-2 dump at iteration 454, and config-4
-# children with segments on vs off.
+# Round 3: device dual segments (tests/test_sdual_gpu.py) with per-LP launches
+# and with the persistent pool kernel, config-4 children with segments on vs
+# off, then the config-2 dump at iteration 454.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r03_sdual2
 mkdir -p $OUT
-timeout -k 10 400 python3 -u -m pytest $R/tests/test_sdual_gpu.py -x -v --timeout 300 \
-  --timeout-method thread -m gpu > $OUT/tests.log 2>&1
-rc=$?
-tail -5 $OUT/tests.log
-if [ $rc -ne 0 ]; then grep -E "Error|assert" $OUT/tests.log | head -20; exit $rc; fi
+for P in 0 1; do
+  MILP_SDUAL_POOL=$P timeout -k 10 240 python3 -u -m pytest $R/tests/test_sdual_gpu.py -x -v \
+    --timeout 120 --timeout-method thread -m gpu > $OUT/tests_pool$P.log 2>&1
+  rc=$?
+  echo "== tests pool=$P rc=$rc"; tail -3 $OUT/tests_pool$P.log
+  if [ $rc -ne 0 ]; then grep -E "Error|assert|Timeout" $OUT/tests_pool$P.log | head -20; exit $rc; fi
+done
 for V in off device; do
   MILP_SDUAL=$V timeout -k 10 300 python3 -u $R/scripts/probe_batch.py --node --lps 512 \
     --workers 64 256 > $OUT/c4_$V.json 2> $OUT/c4_$V.err || { tail -20 $OUT/c4_$V.err; exit 1; }
