@@ -96,7 +96,14 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, unsigned lon
     const char* stage = reinterpret_cast<const char*>(sh);
     char* arena = reinterpret_cast<char*>(sh->arena_dev);
     const uint64_t arena_addr = sh->arena_dev;
-    team_copy(arena, stage, sh->fixed_end);
+    team_copy(arena, stage, sizeof(sdual::Lp));
+    team_copy(arena + sh->mutable_begin, stage + sh->mutable_begin,
+              sh->fixed_end - sh->mutable_begin);
+    {
+      uint4* z = reinterpret_cast<uint4*>(arena + sh->scratch_begin);
+      const int64_t words = (sh->scratch_end - sh->scratch_begin + 15) / 16;
+      for (int64_t w = threadIdx.x; w < words; w += blockDim.x) z[w] = make_uint4(0, 0, 0, 0);
+    }
     team_copy_store_prefix(sh->storage, stage, arena, arena_addr, false);
     team_copy_store_prefix(sh->right_storage, stage, arena, arena_addr, false);
     __threadfence();
@@ -106,7 +113,9 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, unsigned lon
     __threadfence();
     __syncthreads();
     char* stage_out = const_cast<char*>(stage);
-    team_copy(stage_out, arena, lp->mutable_end);
+    team_copy(stage_out, arena, sizeof(sdual::Lp));
+    team_copy(stage_out + lp->mutable_begin, arena + lp->mutable_begin,
+              lp->mutable_end - lp->mutable_begin);
     team_copy_store_prefix(lp->storage, arena, stage_out, arena_addr, true);
     team_copy_store_prefix(lp->right_storage, arena, stage_out, arena_addr, true);
     if (lp->coeff_out != nullptr) {

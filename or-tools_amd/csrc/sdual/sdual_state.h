@@ -296,8 +296,15 @@ struct Lp {
   // ---- transfers of the pooled path (the workgroup moves its own arena) ----
   uint64_t arena_dev;    // device address of this header's arena
   uint64_t staging_dev;  // device view of the pinned staging image
-  int64_t fixed_end;     // [0, fixed_end) moves in
-  int64_t mutable_end;   // [0, mutable_end) moves out
+  // Arena layout: [header][scratch][mutable][read-only][LU image][storages]:
+  // the header and [mutable_begin, in_end) move in, the scratch is zeroed on
+  // the device, the header and [mutable_begin, mutable_end) move out (plus
+  // the storages' used prefixes both ways).
+  int64_t scratch_begin;
+  int64_t scratch_end;
+  int64_t mutable_begin;
+  int64_t fixed_end;     // in_end: the LU image's last used byte
+  int64_t mutable_end;
   f64* coeff_out;        // DeviceLp's update-row coefficients (N), refreshed at the end
   // Device time per loop phase (wall_clock64 ticks, 100 MHz): see sd_run.
   uint64_t phase_ticks[12];
