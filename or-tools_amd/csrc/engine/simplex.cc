@@ -3241,6 +3241,7 @@ class RevisedSimplex {
   // Device dual segment (csrc/sdual): 0 off, 1 on the host (the same
   // restatement compiled for the CPU, a debugging aid), 2 on the device.
   int sdual_mode_ = 0;
+  int saved_sdual_mode_ = 0;
   std::vector<char> sdual_buffer_;
   int64_t sdual_segments_ = 0;
   int64_t sdual_iterations_ = 0;
@@ -3249,6 +3250,23 @@ class RevisedSimplex {
   int RunSdualSegment(TimeLimit* tl, bool* refactorize, Status* status);
 
  public:
+  // The batch APIs run the phase-II dual loop of their LPs on the device
+  // (one workgroup per LP) unless MILP_SDUAL says otherwise.
+  void SetBatchMode(bool on) {
+    static const int batch_mode = [] {
+      const char* e = std::getenv("MILP_SDUAL");
+      if (e == nullptr) return 2;
+      if (std::strcmp(e, "host") == 0) return 1;
+      if (std::strcmp(e, "device") == 0 || std::strcmp(e, "on") == 0) return 2;
+      return 0;
+    }();
+    if (on) {
+      saved_sdual_mode_ = sdual_mode_;
+      sdual_mode_ = batch_mode;
+    } else {
+      sdual_mode_ = saved_sdual_mode_;
+    }
+  }
   void SdualCounters(int64_t* segments, int64_t* iterations) const {
     *segments = sdual_segments_;
     *iterations = sdual_iterations_;
@@ -5805,6 +5823,7 @@ namespace {
 // Back to single launches after a batch call (a device error there is the
 // handle's next call's to report).
 void SetSmallBatchSafe(mi_lp* h, bool on) {
+  h->simplex.SetBatchMode(on);
   try {
     h->simplex.device().SetSmallBatch(on);
   } catch (const std::exception& e) {
@@ -5829,7 +5848,10 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
   // MILP_BATCH_FIBERS=k (default 4), MILP_SMALL_BATCH=0 turns batching off.
   int fibers = 4;
   if (const char* e = std::getenv("MILP_BATCH_FIBERS")) fibers = std::max(1, std::atoi(e));
-  for (int i = 0; i < count; ++i) handles[i]->simplex.device().SetSmallBatch(true);
+  for (int i = 0; i < count; ++i) {
+    handles[i]->simplex.SetBatchMode(true);
+    handles[i]->simplex.device().SetSmallBatch(true);
+  }
   // Largest LPs first (LPT order, weight (nnz + m) * m as in the multi-GPU
   // partition of mi_glop.distributed): the long solves start early instead of
   // forming the tail of the batch.
@@ -5900,7 +5922,10 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
   if (const char* e = std::getenv("MILP_BATCH_THREADS")) {
     threads = std::max(1, std::min(num_workers, std::atoi(e)));
   }
-  for (int w = 0; w < num_workers; ++w) workers[w]->simplex.device().SetSmallBatch(true);
+  for (int w = 0; w < num_workers; ++w) {
+    workers[w]->simplex.SetBatchMode(true);
+    workers[w]->simplex.device().SetSmallBatch(true);
+  }
   std::atomic<int> next(0);
   auto worker_loop = [&](mi_lp* h) {
     (void)hipSetDevice(h->device);

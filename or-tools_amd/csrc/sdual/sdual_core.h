@@ -65,6 +65,42 @@ SD_INLINE void sd_sync() {
   __syncthreads();
 #endif
 }
+// Maximum over the lanes (exact: no rounding; values are finite).
+SD_INLINE f64 sd_wave_max(f64 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (int off = 32; off > 0; off >>= 1) {
+    const f64 o = __shfl_xor(v, off, 64);
+    v = (v < o) ? o : v;
+  }
+#endif
+  return v;
+}
+// Positions i in [0, n) with keep(i), in increasing order, into out; returns
+// the count (ballot + prefix popcount per 64-wide chunk).
+template <typename Keep>
+SD_INLINE int sd_ordered_compact(int n, int32_t* out, Keep keep) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  int count = 0;
+  const int lane = sd_lane();
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const bool k = i < n && keep(i);
+    const uint64_t mask = __ballot(k);
+    if (k) out[count + __popcll(mask & below)] = i;
+    count += __popcll(mask);
+  }
+  sd_sync();
+  return count;
+#else
+  int count = 0;
+  for (int i = 0; i < n; ++i) {
+    if (keep(i)) out[count++] = i;
+  }
+  return count;
+#endif
+}
+
 template <typename T>
 SD_INLINE void sd_fill(T* p, int64_t n, T v) {
   for (int64_t i = sd_lane(); i < n; i += sd_lanes()) p[i] = v;
@@ -1567,7 +1603,8 @@ SD_INLINE void den_update_before_pivot(Lp& s, int leaving_row) {
   const f64* tau = bf_right_solve_for_tau(s, s.rho);
   const f64 pivot = s.dir.values[leaving_row];
   const f64 new_leaving = s.norms[leaving_row] / sq(pivot);
-  for (int k = 0; k < s.dir.nnz; ++k) {
+  // Element-wise over the direction's distinct rows: split over the lanes.
+  for (int k = sd_lane(); k < s.dir.nnz; k += sd_lanes()) {
     const int row = s.dir.nz[k];
     const f64 c = s.dir.values[row];
     s.norms[row] += c * (c * new_leaving - 2.0 / pivot * tau[row]);
@@ -1577,6 +1614,7 @@ SD_INLINE void den_update_before_pivot(Lp& s, int leaving_row) {
       s.norms[row] = kLowerBound;
     }
   }
+  sd_sync();
   s.norms[leaving_row] = new_leaving;
 }
 
@@ -1601,10 +1639,11 @@ SD_INLINE void rc_update_before_pivot(Lp& s, int entering_col, int leaving_row) 
       s.rc_precise = 0;
       ur_compute_update_row(s, leaving_row);
       const f64 new_leaving_rc = entering_rc / -s.dir.values[leaving_row];
-      for (int k = 0; k < s.n_nzpos; ++k) {
+      for (int k = sd_lane(); k < s.n_nzpos; k += sd_lanes()) {  // distinct positions
         const int col = s.nzpos[k];
         s.rc[col] += new_leaving_rc * s.coeff[col];
       }
+      sd_sync();
       s.rc[leaving_col] = new_leaving_rc;
       s.rc[entering_col] = 0.0;
     }
@@ -1625,19 +1664,19 @@ SD_INLINE void rs_advance_deterministic_time(Lp& s) {
 }
 SD_INLINE void rs_compute_direction(Lp& s, int col) {
   bf_right_solve_for_column(s, col, s.dir);
-  s.dir_inf_norm = 0.0;
+  // The list of a dense result in increasing row order and the infinity norm
+  // (a maximum of absolute values: exact in any order).
+  f64 norm = 0.0;
   if (s.dir.nnz == 0) {
-    for (int row = 0; row < s.m; ++row) {
-      const f64 value = s.dir.values[row];
-      if (value != 0.0) {
-        s.dir.nz[s.dir.nnz++] = row;
-        s.dir_inf_norm = sd_max(s.dir_inf_norm, sd_fabs(value));
-      }
-    }
+    const f64* v = s.dir.values;
+    s.dir.nnz = sd_ordered_compact(s.m, s.dir.nz, [&](int r) { return v[r] != 0.0; });
+    for (int k = sd_lane(); k < s.dir.nnz; k += sd_lanes())
+      norm = sd_max(norm, sd_fabs(v[s.dir.nz[k]]));
   } else {
-    for (int k = 0; k < s.dir.nnz; ++k)
-      s.dir_inf_norm = sd_max(s.dir_inf_norm, sd_fabs(s.dir.values[s.dir.nz[k]]));
+    for (int k = sd_lane(); k < s.dir.nnz; k += sd_lanes())
+      norm = sd_max(norm, sd_fabs(s.dir.values[s.dir.nz[k]]));
   }
+  s.dir_inf_norm = sd_wave_max(norm);
 }
 SD_INLINE void rs_make_boxed_dual_feasible(Lp& s) {
   int n_changed = 0;
@@ -1743,8 +1782,10 @@ SD_INLINE void sd_install_lu(Lp& s, const LuImage* im, uintptr_t b) {
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
+// Polls are relaxed (the polled word bypasses the caches, nothing else is
+// invalidated); the caller fences once the value changed.
 __device__ inline int32_t sd_mb_load(const int32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ inline void sd_mb_store(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1765,6 +1806,7 @@ SD_INLINE int sd_refactorize(Lp& s, int bump) {
   __threadfence_system();
   sd_mb_store(&s.mb->flag, 1);
   while (sd_mb_load(&s.mb->flag) != 2) __builtin_amdgcn_s_sleep(8);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const LuImage* im = reinterpret_cast<const LuImage*>(s.mb_image);
   status = im->status;
   const f64 dtime = im->last_fact_dtime;
@@ -2045,10 +2087,11 @@ SD_INLINE int32_t sd_run(Lp& s) {
     SD_PHASE(7);
     // ComputeStepToMoveBasicVariableToBound + UpdateOnPivoting
     const f64 primal_step = (s.x[lcol] - target_bound) / s.dir.values[leaving_row];
-    for (int k = 0; k < s.dir.nnz; ++k) {
+    for (int k = sd_lane(); k < s.dir.nnz; k += sd_lanes()) {  // distinct basic columns
       const int row = s.dir.nz[k];
       s.x[s.basis[row]] -= s.dir.values[row] * primal_step;
     }
+    sd_sync();
     s.x[entering_col] += primal_step;
     // UpdateAndPivot (:2504-2575)
     const f64 pivot_from_update_row = s.coeff[entering_col];  // IsComputedFor(leaving_row)

@@ -5,6 +5,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -27,20 +30,33 @@ __global__ __launch_bounds__(64) void sdual_segment_kernel(sdual::Lp* lp) {
 
 // ---------------------------------------------------------------------------
 // Persistent segment pool (the batch APIs): one launch per device keeps
-// kPoolGroups workgroups resident; each claims the next queue index, waits
-// for the host to publish an LP arena there, runs its segment and raises the
-// LP's mailbox flag to 3. Queue and flags live in coherent mapped memory.
-// Every workgroup exits on the stop word or after kIdleSpins polls without
-// work, so the grid always drains.
+// kPoolGroups workgroups resident. Workgroup 0 is the dispatcher: it alone
+// polls the host queue (coherent mapped memory, ~4 us between polls, so the
+// PCIe link stays free) and republishes new entries in device memory. The
+// others claim the next index, wait on the device-side tail, move the LP's
+// staging image in, run its segment, move it out and raise the LP's mailbox
+// flag to 3. The dispatcher stops on the stop word or after kIdleSpins polls
+// without work; the workers follow, so the grid always drains.
 struct SdQueue {
   static constexpr int kCap = 1 << 14;
   int64_t tail;  // entries [0, tail) published
   int32_t stop;
   int32_t pad;
-  uint64_t entry[kCap];  // sdual::Lp* (device address of the arena header)
+  int64_t dbg[8];  // MILP_SDUAL_DEBUG progress words
+  uint64_t entry[kCap];  // device view of an LP's staging image
+};
+__device__ inline void pool_dbg(SdQueue* q, int k, int64_t v) {
+  __hip_atomic_store(&q->dbg[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+struct SdRing {
+  unsigned long long head;  // next index a worker claims
+  long long tail;           // entries [0, tail) republished
+  int quit;
+  int pad;
+  uint64_t entry[SdQueue::kCap];
 };
 constexpr int kPoolGroups = 1024;
-constexpr int64_t kIdleSpins = 1 << 22;  // ~2-8 s of s_sleep polling
+constexpr int64_t kIdleSpins = 1 << 20;  // ~4 s of dispatcher polls
 
 // Cooperative copy by the workgroup (16-byte words; regions are 256-byte
 // aligned and padded).
@@ -51,7 +67,7 @@ __device__ inline void team_copy(char* dst, const char* src, int64_t bytes) {
   for (int64_t w = threadIdx.x; w < words; w += blockDim.x) d[w] = s[w];
 }
 __device__ inline void team_copy_store_prefix(const sdual::Store& st, const char* from_base,
-                                              char* to_base, uint64_t arena, bool out) {
+                                              char* to_base, uint64_t arena) {
   // st's pointers are arena addresses; its starts are readable at from_base.
   const int64_t* starts = reinterpret_cast<const int64_t*>(
       from_base + (reinterpret_cast<uint64_t>(st.starts) - arena));
@@ -60,39 +76,65 @@ __device__ inline void team_copy_store_prefix(const sdual::Store& st, const char
   const uint64_t c = reinterpret_cast<uint64_t>(st.coefs) - arena;
   team_copy(to_base + r, from_base + r, used * 4);
   team_copy(to_base + c, from_base + c, used * 8);
-  (void)out;
 }
 
-__global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, unsigned long long* head) {
-  __shared__ sdual::Lp* lp_shared;
+__global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring,
+                                                        long long head_base) {
+  if (blockIdx.x == 0) {
+    if (threadIdx.x != 0) return;
+    long long seen = head_base;
+    int64_t idle = 0;
+    while (true) {
+      // Relaxed polls bypass the caches for the polled word only; the acquire
+      // fence (one cache invalidation) follows a change.
+      const long long t = static_cast<long long>(
+          __hip_atomic_load(&q->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      if (t > seen) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        for (long long k = seen; k < t; ++k) {
+          ring->entry[k % SdQueue::kCap] = __hip_atomic_load(
+              &q->entry[k % SdQueue::kCap], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __hip_atomic_store(&ring->tail, t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        seen = t;
+        idle = 0;
+        pool_dbg(q, 0, seen);
+      } else if (__hip_atomic_load(&q->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+                 ++idle > kIdleSpins) {
+        __hip_atomic_store(&ring->quit, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(127);
+    }
+  }
+  __shared__ uint64_t entry_shared;
   __shared__ int quit;
   while (true) {
     if (threadIdx.x == 0) {
       quit = 0;
-      lp_shared = nullptr;
-      const unsigned long long idx = atomicAdd(head, 1ull);
-      int64_t spins = 0;
+      const unsigned long long idx = atomicAdd(&ring->head, 1ull);
       while (true) {
-        const int64_t tail =
-            __hip_atomic_load(&q->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (static_cast<int64_t>(idx) < tail) {
-          lp_shared = reinterpret_cast<sdual::Lp*>(__hip_atomic_load(
-              &q->entry[idx % SdQueue::kCap], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+        if (static_cast<long long>(idx) <
+            __hip_atomic_load(&ring->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          entry_shared = __hip_atomic_load(&ring->entry[idx % SdQueue::kCap], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+          pool_dbg(q, 1, static_cast<int64_t>(idx) + 1);
+          pool_dbg(q, 2, 1);
           break;
         }
-        if (__hip_atomic_load(&q->stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
-            ++spins > kIdleSpins) {
+        if (__hip_atomic_load(&ring->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
           quit = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(32);
+        __builtin_amdgcn_s_sleep(64);
       }
     }
     __syncthreads();
     if (quit) return;
     // The entry is the staging image (device view of pinned host memory):
     // move it into the arena, run, move the mutable part back.
-    const sdual::Lp* sh = lp_shared;
+    const sdual::Lp* sh = reinterpret_cast<const sdual::Lp*>(entry_shared);
     const char* stage = reinterpret_cast<const char*>(sh);
     char* arena = reinterpret_cast<char*>(sh->arena_dev);
     const uint64_t arena_addr = sh->arena_dev;
@@ -104,32 +146,64 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, unsigned lon
       const int64_t words = (sh->scratch_end - sh->scratch_begin + 15) / 16;
       for (int64_t w = threadIdx.x; w < words; w += blockDim.x) z[w] = make_uint4(0, 0, 0, 0);
     }
-    team_copy_store_prefix(sh->storage, stage, arena, arena_addr, false);
-    team_copy_store_prefix(sh->right_storage, stage, arena, arena_addr, false);
+    team_copy_store_prefix(sh->storage, stage, arena, arena_addr);
+    team_copy_store_prefix(sh->right_storage, stage, arena, arena_addr);
     __threadfence();
     __syncthreads();
+    if (threadIdx.x == 0) pool_dbg(q, 2, 2);
     sdual::Lp* lp = reinterpret_cast<sdual::Lp*>(arena);
     sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
+    if (threadIdx.x == 0) {
+      pool_dbg(q, 2, 3);
+      pool_dbg(q, 3, lp->num_iterations);
+    }
     __threadfence();
     __syncthreads();
     char* stage_out = const_cast<char*>(stage);
+    if (threadIdx.x == 0) {
+      pool_dbg(q, 4, lp->mutable_end - lp->mutable_begin);
+      pool_dbg(q, 5, reinterpret_cast<int64_t>(stage_out));
+    }
     team_copy(stage_out, arena, sizeof(sdual::Lp));
+    if (threadIdx.x == 0) pool_dbg(q, 2, 31);
     team_copy(stage_out + lp->mutable_begin, arena + lp->mutable_begin,
               lp->mutable_end - lp->mutable_begin);
-    team_copy_store_prefix(lp->storage, arena, stage_out, arena_addr, true);
-    team_copy_store_prefix(lp->right_storage, arena, stage_out, arena_addr, true);
+    if (threadIdx.x == 0) pool_dbg(q, 2, 32);
+    team_copy_store_prefix(lp->storage, arena, stage_out, arena_addr);
+    team_copy_store_prefix(lp->right_storage, arena, stage_out, arena_addr);
+    if (threadIdx.x == 0) pool_dbg(q, 2, 33);
     if (lp->coeff_out != nullptr) {
       for (int c = threadIdx.x; c < lp->N; c += blockDim.x) lp->coeff_out[c] = lp->coeff[c];
     }
-    __threadfence_system();
+    if (threadIdx.x == 0) pool_dbg(q, 2, 34);
+    __threadfence();
+    if (threadIdx.x == 0) pool_dbg(q, 2, 35);
     __syncthreads();
+    if (threadIdx.x == 0) pool_dbg(q, 2, 36);
+    __threadfence_system();
     if (threadIdx.x == 0) {
+      pool_dbg(q, 2, 4);
       __hip_atomic_store(&lp->mb->flag, 3, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
 
 namespace {
+// A stream with a CU mask gets a hardware queue of its own: the resident grid
+// never sits in front of another stream's work (streams otherwise share the
+// GPU_MAX_HW_QUEUES queues round-robin, in order).
+bool CreateOwnQueueStream(int device, hipStream_t* s) {
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      cus <= 0) {
+    return false;
+  }
+  std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
+  if (cus % 32 != 0) mask.back() = (1u << (cus % 32)) - 1;
+  return hipExtStreamCreateWithCUMask(s, static_cast<uint32_t>(mask.size()), mask.data()) ==
+         hipSuccess;
+}
+
 // One pool per device. Never destroyed (like SmallBatcher): the runtime may
 // be gone at process exit; the kernel drains on its idle limit.
 class SdualPool {
@@ -154,6 +228,8 @@ class SdualPool {
                      __ATOMIC_RELEASE);
     __atomic_store_n(&q_->tail, t + 1, __ATOMIC_RELEASE);
   }
+  int64_t Tail() const { return q_->tail; }
+  const int64_t* Dbg() const { return q_->dbg; }
   // False when the kernel is gone (idle limit) before serving a request.
   bool Alive() {
     std::lock_guard<std::mutex> lock(mu_);
@@ -168,8 +244,10 @@ class SdualPool {
     if (hipHostMalloc(reinterpret_cast<void**>(&q_), sizeof(SdQueue),
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void**>(&d_q_), q_, 0) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&d_head_), sizeof(unsigned long long)) != hipSuccess ||
-        hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+        hipMalloc(reinterpret_cast<void**>(&d_ring_), sizeof(SdRing)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&h_ring_), sizeof(SdRing),
+                      hipHostMallocDefault) != hipSuccess ||
+        !CreateOwnQueueStream(device, &stream_)) {
       (void)hipSetDevice(prev);
       throw DeviceError("sdual pool: allocation failed");
     }
@@ -184,15 +262,20 @@ class SdualPool {
     (void)hipSetDevice(device_);
     if (running_) (void)hipStreamSynchronize(stream_);
     head_base_ = q_->tail;
-    const unsigned long long h = static_cast<unsigned long long>(head_base_);
-    if (hipMemcpyAsync(d_head_, &h, sizeof(h), hipMemcpyHostToDevice, stream_) != hipSuccess) {
+    // The grid claims queue indices from head_base_ on (a synchronous copy:
+    // the launch below must see it).
+    std::memset(h_ring_, 0, offsetof(SdRing, entry));
+    h_ring_->head = static_cast<unsigned long long>(head_base_);
+    h_ring_->tail = head_base_;
+    if (hipMemcpy(d_ring_, h_ring_, offsetof(SdRing, entry), hipMemcpyHostToDevice) !=
+        hipSuccess) {
       (void)hipSetDevice(prev);
-      throw DeviceError("sdual pool: head reset failed");
+      throw DeviceError("sdual pool: ring reset failed");
     }
     __atomic_store_n(&q_->stop, 0, __ATOMIC_RELEASE);
-    hipLaunchKernelGGL(sdual_pool_kernel, dim3(kPoolGroups), dim3(64), 0, stream_, d_q_, d_head_);
+    hipLaunchKernelGGL(sdual_pool_kernel, dim3(kPoolGroups), dim3(64), 0, stream_, d_q_, d_ring_,
+                       static_cast<long long>(head_base_));
     const hipError_t e = hipGetLastError();
-    (void)hipStreamSynchronize(nullptr);  // the head reset is a pageable copy
     (void)hipSetDevice(prev);
     if (e != hipSuccess) throw DeviceError("sdual pool: launch failed");
     running_ = true;
@@ -202,7 +285,8 @@ class SdualPool {
   std::mutex mu_;
   SdQueue* q_ = nullptr;
   SdQueue* d_q_ = nullptr;
-  unsigned long long* d_head_ = nullptr;
+  SdRing* d_ring_ = nullptr;
+  SdRing* h_ring_ = nullptr;
   hipStream_t stream_ = nullptr;
   bool running_ = false;
   int64_t head_base_ = 0;
@@ -340,7 +424,7 @@ void DeviceLp::SdualRunPooled(size_t bytes, const double* arena_coeff, int n,
   (void)arena_coeff;
   (void)n;
   DeviceOp("sdual pooled segment");
-  if (batch_pending_) WaitSmallBatch();
+  WaitStream();  // nothing of this handle's may still write d_coeff_
   sdual::Lp* hs = reinterpret_cast<sdual::Lp*>(sdual_staging_);
   hs->staging_dev = reinterpret_cast<uint64_t>(sdual_staging_dev_);
   hs->coeff_out = d_coeff_;
@@ -349,8 +433,26 @@ void DeviceLp::SdualRunPooled(size_t bytes, const double* arena_coeff, int n,
   SdualPool& pool = SdualPool::Get(device_);
   pool.Enqueue(sdual_staging_dev_);
   int64_t polls = 0;
+  static const bool debug = std::getenv("MILP_SDUAL_DEBUG") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  int64_t next_report = 1;
   while (true) {
     const int32_t f = __atomic_load_n(flag, __ATOMIC_ACQUIRE);
+    if (debug) {
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (s > next_report) {
+        const volatile int64_t* d = pool.Dbg();
+        std::fprintf(stderr,
+                     "sdual pooled: %.0fs flag=%d alive=%d tail=%lld seen=%lld claimed=%lld "
+                     "stage=%lld iterations=%lld out=%lld stage_ptr=%llx staging_dev=%p\n",
+                     s, f, pool.Alive() ? 1 : 0, static_cast<long long>(pool.Tail()),
+                     static_cast<long long>(d[0]), static_cast<long long>(d[1]),
+                     static_cast<long long>(d[2]), static_cast<long long>(d[3]),
+                     static_cast<long long>(d[4]), static_cast<unsigned long long>(d[5]),
+                     sdual_staging_dev_);
+        next_report += 1;
+      }
+    }
     if (f == 3) break;
     if (f == 1) {
       DeviceOp("sdual factorization request");

@@ -6,7 +6,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r03_sdual2
 mkdir -p $OUT
-for P in 0 1; do
+for P in ${POOLS:-0 1}; do
   MILP_SDUAL_POOL=$P timeout -k 10 240 python3 -u -m pytest $R/tests/test_sdual_gpu.py -x -v \
     --timeout 120 --timeout-method thread -m gpu > $OUT/tests_pool$P.log 2>&1
   rc=$?
