@@ -75,10 +75,20 @@ SD_INLINE f64 sd_wave_max(f64 v) {
 #endif
   return v;
 }
+SD_INLINE int sd_wave_min_int(int v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (int off = 32; off > 0; off >>= 1) {
+    const int o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+#endif
+  return v;
+}
 // Positions i in [0, n) with keep(i), in increasing order, into out; returns
 // the count (ballot + prefix popcount per 64-wide chunk).
-template <typename Keep>
-SD_INLINE int sd_ordered_compact(int n, int32_t* out, Keep keep) {
+// sd_ordered_compact_map: the values map(i) of those positions instead.
+template <typename Keep, typename Map>
+SD_INLINE int sd_ordered_compact_map(int n, int32_t* out, Keep keep, Map map) {
 #if defined(__HIP_DEVICE_COMPILE__)
   int count = 0;
   const int lane = sd_lane();
@@ -87,7 +97,7 @@ SD_INLINE int sd_ordered_compact(int n, int32_t* out, Keep keep) {
     const int i = base + lane;
     const bool k = i < n && keep(i);
     const uint64_t mask = __ballot(k);
-    if (k) out[count + __popcll(mask & below)] = i;
+    if (k) out[count + __popcll(mask & below)] = map(i);
     count += __popcll(mask);
   }
   sd_sync();
@@ -95,10 +105,20 @@ SD_INLINE int sd_ordered_compact(int n, int32_t* out, Keep keep) {
 #else
   int count = 0;
   for (int i = 0; i < n; ++i) {
-    if (keep(i)) out[count++] = i;
+    if (keep(i)) out[count++] = map(i);
   }
   return count;
 #endif
+}
+template <typename Keep>
+SD_INLINE int sd_ordered_compact(int n, int32_t* out, Keep keep) {
+  return sd_ordered_compact_map(n, out, keep, [](int i) { return i; });
+}
+SD_INLINE int64_t sd_wave_sum_i64(int64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+#endif
+  return v;
 }
 
 template <typename T>
@@ -229,16 +249,19 @@ SD_INLINE bool vec_dense(const Vec& v, f64 ratio) {
   if (v.nnz == 0) return true;
   return static_cast<f64>(v.nnz) > ratio * static_cast<f64>(v.size);
 }
+// The list holds distinct positions: loops over it split over the lanes.
 SD_INLINE void vec_clear_mask(Vec& v) {
   if (vec_dense(v, 0.8)) {
     sd_fill<char>(v.mask, v.size, 0);
   } else {
-    for (int k = 0; k < v.nnz; ++k) v.mask[v.nz[k]] = 0;
+    for (int k = sd_lane(); k < v.nnz; k += sd_lanes()) v.mask[v.nz[k]] = 0;
+    sd_sync();
   }
 }
 SD_INLINE void vec_repopulate_mask(Vec& v) {
   vec_clear_mask(v);
-  for (int k = 0; k < v.nnz; ++k) v.mask[v.nz[k]] = 1;
+  for (int k = sd_lane(); k < v.nnz; k += sd_lanes()) v.mask[v.nz[k]] = 1;
+  sd_sync();
 }
 SD_INLINE void vec_clear_nz_if_too_dense(Vec& v, f64 ratio) {
   if (vec_dense(v, ratio)) {
@@ -264,8 +287,9 @@ SD_INLINE int64_t vec_nnz_estimate(const Vec& v) { return v.nnz == 0 ? v.size : 
 // lp_utils.h:281-299 (the size is always m here).
 SD_INLINE void vec_clear_and_resize(Vec& v, int size) {
   if (v.nnz != 0 && static_cast<f64>(v.nnz) < 0.05 * static_cast<f64>(size)) {
-    for (int k = 0; k < v.nnz; ++k) v.values[v.nz[k]] = 0.0;
-    for (int i = v.size; i < size; ++i) v.values[i] = 0.0;
+    for (int k = sd_lane(); k < v.nnz; k += sd_lanes()) v.values[v.nz[k]] = 0.0;
+    for (int i = v.size + sd_lane(); i < size; i += sd_lanes()) v.values[i] = 0.0;
+    sd_sync();
   } else {
     sd_fill<f64>(v.values, size, 0.0);
   }
@@ -273,12 +297,15 @@ SD_INLINE void vec_clear_and_resize(Vec& v, int size) {
   v.nnz = 0;
 }
 SD_INLINE void vec_copy(Vec& dst, const Vec& src) {  // *x = b
-  for (int i = 0; i < src.size; ++i) dst.values[i] = src.values[i];
+  for (int i = sd_lane(); i < src.size; i += sd_lanes()) {
+    dst.values[i] = src.values[i];
+    dst.mask[i] = src.mask[i];
+  }
+  for (int k = sd_lane(); k < src.nnz; k += sd_lanes()) dst.nz[k] = src.nz[k];
+  sd_sync();
   dst.size = src.size;
-  for (int k = 0; k < src.nnz; ++k) dst.nz[k] = src.nz[k];
   dst.nnz = src.nnz;
   dst.sorted = src.sorted;
-  for (int i = 0; i < src.size; ++i) dst.mask[i] = src.mask[i];
 }
 // lp_utils.cc:62-75 and :46-54
 SD_INLINE f64 dense_squared_norm(const f64* c, int n) {
@@ -330,72 +357,175 @@ template <typename M>
 SD_INLINE int64_t col_entries(const M& a, int col) {
   return a.starts[col + 1] - a.starts[col];
 }
+// col_dot with the products on the lanes: lane j < 4 keeps accumulator
+// r_{j+1} and adds the products of entries j, j + 4, j + 8, ... in order, so
+// the sums round exactly as the sequential loop's.
+template <typename M>
+SD_INLINE f64 col_dot_par(const M& a, int col, const f64* v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int64_t b = a.starts[col], e = a.starts[col + 1];
+  const int64_t body = (e - b) & ~int64_t{3};  // the four-accumulator loop's entries
+  const int lane = sd_lane();
+  const int j = lane & 3;
+  f64 acc = 0.0;
+  for (int64_t base = 0; base < body; base += 64) {
+    const int64_t k = base + lane;
+    f64 p = 0.0;
+    if (k < body) p = a.coefs[b + k] * v[a.rows[b + k]];
+    const int groups = static_cast<int>((body - base < 64 ? body - base : 64) >> 2);
+    for (int g = 0; g < groups; ++g) acc += __shfl(p, j + 4 * g, 64);
+  }
+  const f64 r1 = __shfl(acc, 0, 64), r2 = __shfl(acc, 1, 64);
+  const f64 r3 = __shfl(acc, 2, 64), r4 = __shfl(acc, 3, 64);
+  f64 result = r1 + r2 + r3 + r4;
+  for (int64_t i = b + body; i < e; ++i) result += a.coefs[i] * v[a.rows[i]];
+  return result;
+#else
+  return col_dot(a, col, v);
+#endif
+}
 // sparse.h:389-399
 template <typename M>
 SD_INLINE void col_add_dense(const M& a, int col, f64 mult, f64* dense) {
   if (mult == 0.0) return;
-  for (int64_t i = a.starts[col]; i < a.starts[col + 1]; ++i)
+  // A column's rows are distinct: the lanes split it.
+  for (int64_t i = a.starts[col] + sd_lane(); i < a.starts[col + 1]; i += sd_lanes())
     dense[a.rows[i]] += mult * a.coefs[i];
+  sd_sync();
 }
 // sparse.h:403-413
+// The lanes take 64 entries at a time (a column's rows are distinct); the new
+// positions join the list in entry order (ballot prefix counts).
 template <typename M>
 SD_INLINE void col_add_scattered(const M& a, int col, f64 mult, Vec& c) {
   if (mult == 0.0) return;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int64_t e = a.starts[col + 1];
+  const int lane = sd_lane();
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int nnz = c.nnz;
+  for (int64_t base = a.starts[col]; base < e; base += 64) {
+    const int64_t i = base + lane;
+    bool fresh = false;
+    int row = 0;
+    if (i < e) {
+      row = a.rows[i];
+      const f64 value = mult * a.coefs[i];
+      c.values[row] += value;
+      fresh = !c.mask[row] && value != 0.0;
+      if (fresh) c.mask[row] = 1;
+    }
+    const uint64_t fresh_mask = __ballot(fresh);
+    if (fresh) c.nz[nnz + __popcll(fresh_mask & below)] = row;
+    nnz += __popcll(fresh_mask);
+  }
+  sd_sync();
+  if (nnz != c.nnz) c.sorted = 0;
+  c.nnz = nnz;
+#else
   for (int64_t i = a.starts[col]; i < a.starts[col + 1]; ++i)
     vec_add(c, a.rows[i], mult * a.coefs[i]);
+#endif
 }
 
 // ---- growing storage (sparse.cc:576-623) ----
-SD_INLINE int store_add_dense_prefix(Store& st, const f64* d, int n, int start) {
+// Appends the nonzeros among positions pos(k), k < count, in k order as a
+// new column (ballot prefix counts give each lane its slot); clear: zero the
+// appended values in d. `pos` null: position k itself. A list that may
+// repeat a position (the MPF scratch) goes through the sequential loop: its
+// first occurrence takes the value and clears it.
+SD_INLINE int store_append(Store& st, f64* d, const int32_t* pos, int first, int count, bool clear) {
   int64_t e = st.starts[st.num_cols];
-  for (int r = start; r < n; ++r) {
-    if (d[r] != 0.0) {
-      st.rows[e] = r;
-      st.coefs[e] = d[r];
-      ++e;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (clear) {
+    for (int k = first; k < count; ++k) {
+      const int r = pos != nullptr ? pos[k] : k;
+      const f64 v = d[r];
+      if (v != 0.0) {
+        st.rows[e] = r;
+        st.coefs[e] = v;
+        d[r] = 0.0;
+        ++e;
+      }
     }
+    st.starts[st.num_cols + 1] = e;
+    return st.num_cols++;
   }
-  st.starts[st.num_cols + 1] = e;
-  return st.num_cols++;
-}
-SD_INLINE int store_add_dense_nz(Store& st, const f64* d, int n, const int32_t* nz, int nnz) {
-  if (nnz == 0) return store_add_dense_prefix(st, d, n, 0);
-  int64_t e = st.starts[st.num_cols];
-  for (int k = 0; k < nnz; ++k) {
-    const int r = nz[k];
-    if (d[r] != 0.0) {
-      st.rows[e] = r;
-      st.coefs[e] = d[r];
-      ++e;
+  const int lane = sd_lane();
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int base = first; base < count; base += 64) {
+    const int k = base + lane;
+    int r = 0;
+    f64 v = 0.0;
+    if (k < count) {
+      r = pos != nullptr ? pos[k] : k;
+      v = d[r];
     }
+    const bool keep = v != 0.0;
+    const uint64_t mask = __ballot(keep);
+    if (keep) {
+      const int64_t at = e + __popcll(mask & below);
+      st.rows[at] = r;
+      st.coefs[at] = v;
+    }
+    e += __popcll(mask);
   }
-  st.starts[st.num_cols + 1] = e;
-  return st.num_cols++;
-}
-SD_INLINE int store_add_and_clear(Store& st, f64* col, int32_t* nz, int* nnz) {
-  int64_t e = st.starts[st.num_cols];
-  for (int k = 0; k < *nnz; ++k) {
-    const int r = nz[k];
-    const f64 v = col[r];
+  sd_sync();
+#else
+  for (int k = first; k < count; ++k) {
+    const int r = pos != nullptr ? pos[k] : k;
+    const f64 v = d[r];
     if (v != 0.0) {
       st.rows[e] = r;
       st.coefs[e] = v;
-      col[r] = 0.0;
+      if (clear) d[r] = 0.0;
       ++e;
     }
   }
-  *nnz = 0;
+#endif
   st.starts[st.num_cols + 1] = e;
   return st.num_cols++;
 }
+SD_INLINE int store_add_dense_prefix(Store& st, const f64* d, int n, int start) {
+  return store_append(st, const_cast<f64*>(d), nullptr, start, n, false);
+}
+SD_INLINE int store_add_dense_nz(Store& st, const f64* d, int n, const int32_t* nz, int nnz) {
+  if (nnz == 0) return store_add_dense_prefix(st, d, n, 0);
+  return store_append(st, const_cast<f64*>(d), nz, 0, nnz, false);
+}
+SD_INLINE int store_add_and_clear(Store& st, f64* col, int32_t* nz, int* nnz) {
+  const int index = store_append(st, col, nz, 0, *nnz, true);
+  *nnz = 0;
+  return index;
+}
 // ColumnCopyToClearedDenseColumnWithNonZeros (sparse.h:440-455)
 SD_INLINE void store_copy_to_vec(const Store& st, int col, Vec& v) {
-  v.nnz = 0;
-  for (int64_t i = st.starts[col]; i < st.starts[col + 1]; ++i) {
-    v.values[st.rows[i]] = st.coefs[i];
-    v.nz[v.nnz++] = st.rows[i];
+  const int64_t b = st.starts[col];
+  const int count = static_cast<int>(st.starts[col + 1] - b);
+  for (int k = sd_lane(); k < count; k += sd_lanes()) {
+    v.values[st.rows[b + k]] = st.coefs[b + k];
+    v.nz[k] = st.rows[b + k];
   }
+  sd_sync();
+  v.nnz = count;
 }
+
+SD_INLINE uint64_t sd_now() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return wall_clock64();
+#else
+  return 0;
+#endif
+}
+// Sub-phase timers (MILP_SDUAL_PROFILE): slots 9-11 count the dense
+// triangular scatters, the dense transposed gathers and the rank-one
+// products inside the loop phases that call them.
+struct SdSubTimer {
+  uint64_t* slot;
+  uint64_t t0;
+  SD_HD explicit SdSubTimer(uint64_t* p) : slot(p), t0(sd_now()) {}
+  SD_HD ~SdSubTimer() { *slot += sd_now() - t0; }
+};
 
 // ---- TriangularMatrix solves (sparse.cc:776-1128) ----
 SD_INLINE void tri_lower_solve_from(const Tri& t, int start, f64* x) {
@@ -423,53 +553,102 @@ SD_INLINE void tri_upper_solve(const Tri& t, f64* x) {
       x[t.rows[i]] -= coeff * t.coefs[i];
   }
 }
-SD_INLINE void tri_transpose_upper_solve(const Tri& t, f64* x) {
-  const int end = t.num_cols;
-  const bool ones = t.all_ones;
-  int64_t i = t.starts[t.first_non_identity];
-  for (int col = t.first_non_identity; col < end; ++col) {
-    f64 sum = x[col];
-    const int64_t i_end = t.starts[col + 1];
-    const int64_t shifted_end = i_end - 3;
-    for (; i < shifted_end; i += 4) {
-      sum -= t.coefs[i] * x[t.rows[i]] + t.coefs[i + 1] * x[t.rows[i + 1]] +
-             t.coefs[i + 2] * x[t.rows[i + 2]] + t.coefs[i + 3] * x[t.rows[i + 3]];
-    }
-    if (i < i_end) {
-      sum -= t.coefs[i] * x[t.rows[i]];
-      if (i + 1 < i_end) {
-        sum -= t.coefs[i + 1] * x[t.rows[i + 1]];
-        if (i + 2 < i_end) sum -= t.coefs[i + 2] * x[t.rows[i + 2]];
-      }
-      i = i_end;
-    }
-    x[col] = ones ? sum : sum / t.diag[col];
+// One column of TransposeUpperSolve / TransposeLowerSolve
+// (sparse.cc:872-947): the entries in the sequential code's order and
+// grouping of four, so that a column computes the same value wherever it runs.
+SD_INLINE f64 tri_tu_column(const Tri& t, const f64* x, int col) {
+  f64 sum = x[col];
+  int64_t i = t.starts[col];
+  const int64_t i_end = t.starts[col + 1];
+  const int64_t shifted_end = i_end - 3;
+  for (; i < shifted_end; i += 4) {
+    sum -= t.coefs[i] * x[t.rows[i]] + t.coefs[i + 1] * x[t.rows[i + 1]] +
+           t.coefs[i + 2] * x[t.rows[i + 2]] + t.coefs[i + 3] * x[t.rows[i + 3]];
   }
+  if (i < i_end) {
+    sum -= t.coefs[i] * x[t.rows[i]];
+    if (i + 1 < i_end) {
+      sum -= t.coefs[i + 1] * x[t.rows[i + 1]];
+      if (i + 2 < i_end) sum -= t.coefs[i + 2] * x[t.rows[i + 2]];
+    }
+  }
+  return t.all_ones ? sum : sum / t.diag[col];
+}
+SD_INLINE f64 tri_tl_column(const Tri& t, const f64* x, int col) {
+  f64 sum = x[col];
+  int64_t i = t.starts[col + 1] - 1;
+  const int64_t i_end = t.starts[col];
+  const int64_t shifted_end = i_end + 3;
+  for (; i >= shifted_end; i -= 4) {
+    sum -= t.coefs[i] * x[t.rows[i]] + t.coefs[i - 1] * x[t.rows[i - 1]] +
+           t.coefs[i - 2] * x[t.rows[i - 2]] + t.coefs[i - 3] * x[t.rows[i - 3]];
+  }
+  if (i >= i_end) {
+    sum -= t.coefs[i] * x[t.rows[i]];
+    if (i >= i_end + 1) {
+      sum -= t.coefs[i - 1] * x[t.rows[i - 1]];
+      if (i >= i_end + 2) sum -= t.coefs[i - 2] * x[t.rows[i - 2]];
+    }
+  }
+  return t.all_ones ? sum : sum / t.diag[col];
+}
+// A level schedule pays when the levels are few against the columns.
+SD_INLINE bool tri_use_levels(const Tri& t) {
+  return t.num_levels >= 0 && 4 * t.num_levels <= t.num_cols - t.first_non_identity;
+}
+// Columns of each level split over the lanes, a barrier between levels:
+// every column reads only finished columns, so the results are those of the
+// sequential sweep.
+SD_INLINE void tri_level_sweep_upper(const Tri& t, f64* x) {
+  for (int l = 0; l < t.num_levels; ++l) {
+    for (int k = t.lv_starts[l] + sd_lane(); k < t.lv_starts[l + 1]; k += sd_lanes()) {
+      const int col = t.lv_order[k];
+      x[col] = tri_tu_column(t, x, col);
+    }
+    sd_sync();
+  }
+}
+SD_INLINE void tri_level_sweep_lower(const Tri& t, f64* x, int last) {
+  for (int l = 0; l < t.num_levels; ++l) {
+    for (int k = t.lv_starts[l] + sd_lane(); k < t.lv_starts[l + 1]; k += sd_lanes()) {
+      const int col = t.lv_order[k];
+      if (col <= last) x[col] = tri_tl_column(t, x, col);
+    }
+    sd_sync();
+  }
+}
+SD_INLINE void tri_transpose_upper_solve(const Tri& t, f64* x) {
+  if (tri_use_levels(t)) {
+    tri_level_sweep_upper(t, x);
+    return;
+  }
+  for (int col = t.first_non_identity; col < t.num_cols; ++col) x[col] = tri_tu_column(t, x, col);
+}
+// The last column with a nonzero value (the sequential code's skip of the
+// trailing zeros), end - 1 when there is none.
+SD_INLINE int tri_last_nonzero(const f64* x, int end, int num_cols) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (int top = num_cols - 1; top >= end; top -= 64) {
+    const int col = top - sd_lane();
+    const uint64_t mask = __ballot(col >= end && x[col] != 0.0);
+    if (mask != 0) return top - (__builtin_ctzll(mask));
+  }
+  return end - 1;
+#else
+  int col = num_cols - 1;
+  while (col >= end && x[col] == 0.0) --col;
+  return col;
+#endif
 }
 SD_INLINE void tri_transpose_lower_solve(const Tri& t, f64* x) {
   const int end = t.first_non_identity;
-  int col = t.num_cols - 1;
-  while (col >= end && x[col] == 0.0) --col;
-  const bool ones = t.all_ones;
-  int64_t i = t.starts[col + 1] - 1;
-  for (; col >= end; --col) {
-    f64 sum = x[col];
-    const int64_t i_end = t.starts[col];
-    const int64_t shifted_end = i_end + 3;
-    for (; i >= shifted_end; i -= 4) {
-      sum -= t.coefs[i] * x[t.rows[i]] + t.coefs[i - 1] * x[t.rows[i - 1]] +
-             t.coefs[i - 2] * x[t.rows[i - 2]] + t.coefs[i - 3] * x[t.rows[i - 3]];
-    }
-    if (i >= i_end) {
-      sum -= t.coefs[i] * x[t.rows[i]];
-      if (i >= i_end + 1) {
-        sum -= t.coefs[i - 1] * x[t.rows[i - 1]];
-        if (i >= i_end + 2) sum -= t.coefs[i - 2] * x[t.rows[i - 2]];
-      }
-      i = i_end - 1;
-    }
-    x[col] = ones ? sum : sum / t.diag[col];
+  const int last = tri_last_nonzero(x, end, t.num_cols);
+  if (last < end) return;
+  if (tri_use_levels(t)) {
+    tri_level_sweep_lower(t, x, last);
+    return;
   }
+  for (int col = last; col >= end; --col) x[col] = tri_tl_column(t, x, col);
 }
 SD_INLINE void tri_hyper_solve(const Tri& t, f64* x, int32_t* nz, int* nnz) {
   const bool ones = t.all_ones;
@@ -608,7 +787,7 @@ SD_INLINE void permute_with_known_nz(Lp& s, const int32_t* perm, Vec& io) {
   f64* old = io.values;
   io.values = s.zero_scratch;
   s.zero_scratch = old;
-  for (int k = 0; k < io.nnz; ++k) {
+  for (int k = sd_lane(); k < io.nnz; k += sd_lanes()) {  // distinct positions
     const int ref = io.nz[k];
     const f64 v = s.zero_scratch[ref];
     s.zero_scratch[ref] = 0.0;
@@ -616,12 +795,16 @@ SD_INLINE void permute_with_known_nz(Lp& s, const int32_t* perm, Vec& io) {
     io.values[p] = v;
     io.nz[k] = p;
   }
+  sd_sync();
 }
 SD_INLINE void lu_right_solve_l_permuted_input(Lp& s, Vec& x) {
   if (s.is_identity) return;
   tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored);
   if (x.nnz == 0) {
-    tri_lower_solve_from(s.lower, 0, x.values);
+    {
+      SdSubTimer t_(&s.phase_ticks[9]);
+      tri_lower_solve_from(s.lower, 0, x.values);
+    }
   } else {
     tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz);
   }
@@ -632,19 +815,26 @@ SD_INLINE void lu_right_solve_l_internal(Lp& s, const int32_t* brows, const f64*
                                           const f64* bvalues, int bn, Vec& x) {
   int first = x.size;
   const int limit = s.lower.first_non_identity;
-  for (int k = 0; k < bn; ++k) {
+  const int base = x.nnz;
+  for (int k = sd_lane(); k < bn; k += sd_lanes()) {  // distinct rows
     const int r = brows[k];
     const int permuted_row = s.row_perm[r];
     x.values[permuted_row] = bcoefs != nullptr ? bcoefs[k] : bvalues[r];
-    x.nz[x.nnz++] = permuted_row;
+    x.nz[base + k] = permuted_row;
     const int col = permuted_row;
     if (col < limit || s.lower.starts[col + 1] == s.lower.starts[col]) continue;
     first = first < col ? first : col;
   }
+  first = sd_wave_min_int(first);
+  x.nnz = base + bn;
+  sd_sync();
   tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored);
   x.sorted = 1;
   if (x.nnz == 0) {
-    tri_lower_solve_from(s.lower, first, x.values);
+    {
+      SdSubTimer t_(&s.phase_ticks[9]);
+      tri_lower_solve_from(s.lower, first, x.values);
+    }
   } else {
     tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz);
   }
@@ -665,14 +855,20 @@ SD_INLINE void lu_right_solve_l_with_nz(Lp& s, Vec& x) {
   if (s.is_identity) return;
   if (x.nnz == 0) {
     permute_with_scratchpad(s, s.row_perm, x);
-    tri_lower_solve_from(s.lower, 0, x.values);
+    {
+      SdSubTimer t_(&s.phase_ticks[9]);
+      tri_lower_solve_from(s.lower, 0, x.values);
+    }
     return;
   }
   permute_with_known_nz(s, s.row_perm, x);
   tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored);
   x.sorted = 1;
   if (x.nnz == 0) {
-    tri_lower_solve_from(s.lower, 0, x.values);
+    {
+      SdSubTimer t_(&s.phase_ticks[9]);
+      tri_lower_solve_from(s.lower, 0, x.values);
+    }
   } else {
     tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz);
   }
@@ -695,7 +891,10 @@ SD_INLINE void lu_right_solve_u_with_nz(Lp& s, Vec& x) {
   tri_rows_to_consider(s.upper, x.nz, &x.nnz, s.stored);
   x.sorted = 1;
   if (x.nnz == 0) {
-    tri_transpose_lower_solve(s.tupper, x.values);
+    {
+      SdSubTimer t_(&s.phase_ticks[10]);
+      tri_transpose_lower_solve(s.tupper, x.values);
+    }
   } else {
     tri_transpose_hyper_solve_rev(s.tupper, x.values, x.nz, &x.nnz);
   }
@@ -707,7 +906,10 @@ SD_INLINE bool lu_left_solve_l_with_nz(Lp& s, Vec& y, Vec* before) {
   tri_rows_to_consider(s.tlower, y.nz, &y.nnz, s.stored);
   y.sorted = 1;
   if (y.nnz == 0) {
-    tri_transpose_lower_solve(s.lower, y.values);
+    {
+      SdSubTimer t_(&s.phase_ticks[10]);
+      tri_transpose_lower_solve(s.lower, y.values);
+    }
   } else {
     tri_transpose_hyper_solve_rev(s.lower, y.values, y.nz, &y.nnz);
   }
@@ -743,14 +945,16 @@ SD_INLINE bool lu_left_solve_l_with_nz(Lp& s, Vec& y, Vec* before) {
       y.nnz = before->nnz;
       before->nnz = n;
     }
-    y.nnz = 0;  // nz is the cleared list of `before` (vec_clear_and_resize)
-    for (int k = 0; k < before->nnz; ++k) {
+    // nz is the cleared list of `before` (vec_clear_and_resize)
+    for (int k = sd_lane(); k < before->nnz; k += sd_lanes()) {  // distinct rows
       const int row = before->nz[k];
       const f64 value = before->values[row];
       const int permuted_row = s.inv_row_perm[row];
       y.values[permuted_row] = value;
-      y.nz[y.nnz++] = permuted_row;
+      y.nz[k] = permuted_row;
     }
+    sd_sync();
+    y.nnz = before->nnz;
     y.sorted = 0;
   }
   return true;
@@ -771,7 +975,10 @@ SD_INLINE int lu_left_solve_u_unit_row(Lp& s, int col, Vec& y) {
     tri_rows_to_consider(s.tupper, y.nz, &y.nnz, s.stored);
     y.sorted = 1;
     if (y.nnz == 0) {
-      tri_lower_solve_from(s.tupper, pc, y.values);
+      {
+        SdSubTimer t_(&s.phase_ticks[9]);
+        tri_lower_solve_from(s.tupper, pc, y.values);
+      }
     } else {
       tri_hyper_solve(s.tupper, y.values, y.nz, &y.nnz);
     }
@@ -829,12 +1036,13 @@ SD_INLINE int64_t lu_number_of_entries(const Lp& s) {
 // ---- RankOneUpdateFactorization (rank_one_update.h:30-246) ----
 SD_INLINE void r1_right_solve_dense(Lp& s, f64* x) {
   for (int i = 0; i < s.r1_count; ++i) {
-    const f64 mult = -col_dot(s.storage, s.r1_v[i], x) / s.r1_mu[i];
+    const f64 mult = -col_dot_par(s.storage, s.r1_v[i], x) / s.r1_mu[i];
     col_add_dense(s.storage, s.r1_u[i], mult, x);
   }
   s.r1_dtime += dt_ops(s.r1_num_entries);
 }
 SD_INLINE void r1_right_solve_nz(Lp& s, Vec& d) {
+  SdSubTimer t_(&s.phase_ticks[11]);
   if (d.nnz == 0) {
     r1_right_solve_dense(s, d.values);
     return;
@@ -843,10 +1051,10 @@ SD_INLINE void r1_right_solve_nz(Lp& s, Vec& d) {
   bool use_dense = vec_dense(d, 0.05);
   for (int i = 0; i < s.r1_count; ++i) {
     if (use_dense) {
-      const f64 mult = -col_dot(s.storage, s.r1_v[i], d.values) / s.r1_mu[i];
+      const f64 mult = -col_dot_par(s.storage, s.r1_v[i], d.values) / s.r1_mu[i];
       col_add_dense(s.storage, s.r1_u[i], mult, d.values);
     } else {
-      const f64 mult = -col_dot(s.storage, s.r1_v[i], d.values) / s.r1_mu[i];
+      const f64 mult = -col_dot_par(s.storage, s.r1_v[i], d.values) / s.r1_mu[i];
       if (mult != 0.0) col_add_scattered(s.storage, s.r1_u[i], mult, d);
       use_dense = vec_dense(d, 0.05);
     }
@@ -857,12 +1065,13 @@ SD_INLINE void r1_right_solve_nz(Lp& s, Vec& d) {
 }
 SD_INLINE void r1_left_solve_dense(Lp& s, f64* y) {
   for (int i = s.r1_count - 1; i >= 0; --i) {
-    const f64 mult = -col_dot(s.storage, s.r1_u[i], y) / s.r1_mu[i];
+    const f64 mult = -col_dot_par(s.storage, s.r1_u[i], y) / s.r1_mu[i];
     col_add_dense(s.storage, s.r1_v[i], mult, y);
   }
   s.r1_dtime += dt_ops(s.r1_num_entries);
 }
 SD_INLINE void r1_left_solve_nz(Lp& s, Vec& y) {
+  SdSubTimer t_(&s.phase_ticks[11]);
   if (y.nnz == 0) {
     r1_left_solve_dense(s, y.values);
     return;
@@ -871,10 +1080,10 @@ SD_INLINE void r1_left_solve_nz(Lp& s, Vec& y) {
   bool use_dense = vec_dense(y, 0.05);
   for (int i = s.r1_count - 1; i >= 0; --i) {
     if (use_dense) {
-      const f64 mult = -col_dot(s.storage, s.r1_u[i], y.values) / s.r1_mu[i];
+      const f64 mult = -col_dot_par(s.storage, s.r1_u[i], y.values) / s.r1_mu[i];
       col_add_dense(s.storage, s.r1_v[i], mult, y.values);
     } else {
-      const f64 mult = -col_dot(s.storage, s.r1_u[i], y.values) / s.r1_mu[i];
+      const f64 mult = -col_dot_par(s.storage, s.r1_u[i], y.values) / s.r1_mu[i];
       if (mult != 0.0) col_add_scattered(s.storage, s.r1_v[i], mult, y);
       use_dense = vec_dense(y, 0.05);
     }
@@ -903,7 +1112,10 @@ SD_INLINE void lu_left_solve_u_with_nz(Lp& s, Vec& y) {
   tri_rows_to_consider(s.tupper, y.nz, &y.nnz, s.stored);
   y.sorted = 1;
   if (y.nnz == 0) {
-    tri_transpose_upper_solve(s.upper, y.values);
+    {
+      SdSubTimer t_(&s.phase_ticks[10]);
+      tri_transpose_upper_solve(s.upper, y.values);
+    }
   } else {
     tri_transpose_hyper_solve(s.upper, y.values, y.nz, &y.nnz);
   }
@@ -929,13 +1141,19 @@ SD_INLINE f64 bf_dual_edge_squared_norm(Lp& s, int row) {
   nz[nnz++] = pr;
   tri_rows_to_consider(s.tupper, nz, &nnz, s.stored);
   if (nnz == 0) {
-    tri_lower_solve_from(s.tupper, pr, z);
+    {
+      SdSubTimer t_(&s.phase_ticks[9]);
+      tri_lower_solve_from(s.tupper, pr, z);
+    }
   } else {
     tri_hyper_solve(s.tupper, z, nz, &nnz);
     tri_rows_to_consider(s.tlower, nz, &nnz, s.stored);
   }
   if (nnz == 0) {
-    tri_upper_solve(s.tlower, z);
+    {
+      SdSubTimer t_(&s.phase_ticks[9]);
+      tri_upper_solve(s.tlower, z);
+    }
   } else {
     tri_hyper_solve_rev(s.tlower, z, nz, &nnz);
   }
@@ -1323,60 +1541,79 @@ SD_INLINE void ur_row_wise(Lp& s) {
       s.coeff[s.At.rows[i]] += mult * s.At.coefs[i];
     sd_sync();
   }
-  s.n_nzpos = 0;
   const f64 drop = s.drop_tolerance;
-  for (int w = 0; w < s.nwords; ++w) {
-    uint64_t word = s.relevant[w];
-    while (word) {
-      const int col = w * 64 + sd_ctz(word);
-      word &= word - 1;
-      if (col >= s.N) break;
-      if (sd_fabs(s.coeff[col]) > drop) s.nzpos[s.n_nzpos++] = col;
-    }
-  }
+  const uint64_t* relevant = s.relevant;
+  const f64* coeff = s.coeff;
+  s.n_nzpos = sd_ordered_compact(s.N, s.nzpos, [&](int col) {
+    return bit_get(relevant, col) && sd_fabs(coeff[col]) > drop;
+  });
 }
+// The first touch of a position sets it, later ones add (row by row, a
+// row's positions over the lanes); touched positions are flagged in col_flag
+// (bytes, so that lanes never share a word) and cleared after the list.
 SD_INLINE void ur_row_wise_hypersparse(Lp& s) {
-  for (int w = 0; w < s.nwords; ++w) s.nzset[w] = 0;
   for (int k = 0; k < s.n_rho_filtered; ++k) {
     const int col = s.rho_filtered[k];
     const f64 mult = s.rho.values[col];
-    for (int64_t i = s.At.starts[col]; i < s.At.starts[col + 1]; ++i) {
+    for (int64_t i = s.At.starts[col] + sd_lane(); i < s.At.starts[col + 1]; i += sd_lanes()) {
       const int pos = s.At.rows[i];
       const f64 v = mult * s.At.coefs[i];
-      if (!bit_get(s.nzset, pos)) {
+      if (!s.col_flag[pos]) {
         s.coeff[pos] = v;
-        bit_set(s.nzset, pos);
+        s.col_flag[pos] = 1;
       } else {
         s.coeff[pos] += v;
       }
     }
+    sd_sync();
   }
-  for (int w = 0; w < s.nwords; ++w) s.nzset[w] &= s.relevant[w];
-  s.n_nzpos = 0;
-  const f64 drop = s.drop_tolerance;
+  // non_zero_position_set_: the touched positions, relevant ones only.
   for (int w = 0; w < s.nwords; ++w) {
-    uint64_t word = s.nzset[w];
-    while (word) {
-      const int col = w * 64 + sd_ctz(word);
-      word &= word - 1;
-      if (col >= s.N) break;
-      if (sd_fabs(s.coeff[col]) > drop) s.nzpos[s.n_nzpos++] = col;
-    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int col = w * 64 + sd_lane();
+    const uint64_t touched = __ballot(col < s.N && s.col_flag[col]);
+#else
+    uint64_t touched = 0;
+    for (int b = 0; b < 64 && w * 64 + b < s.N; ++b)
+      if (s.col_flag[w * 64 + b]) touched |= 1ull << b;
+#endif
+    s.nzset[w] = touched & s.relevant[w];
   }
+  sd_sync();
+  const f64 drop = s.drop_tolerance;
+  const uint64_t* nzset = s.nzset;
+  const f64* coeff = s.coeff;
+  s.n_nzpos = sd_ordered_compact(s.N, s.nzpos, [&](int col) {
+    return bit_get(nzset, col) && sd_fabs(coeff[col]) > drop;
+  });
+  for (int k = 0; k < s.n_rho_filtered; ++k) {
+    const int col = s.rho_filtered[k];
+    for (int64_t i = s.At.starts[col] + sd_lane(); i < s.At.starts[col + 1]; i += sd_lanes())
+      s.col_flag[s.At.rows[i]] = 0;
+  }
+  sd_sync();
 }
 SD_INLINE void ur_single_row(Lp& s, int row_as_col) {
-  s.n_nzpos = 0;
   const f64 drop = s.drop_tolerance;
   const f64 mult = s.rho.values[row_as_col];
-  for (int64_t i = s.At.starts[row_as_col]; i < s.At.starts[row_as_col + 1]; ++i) {
-    const int pos = s.At.rows[i];
-    if (!bit_get(s.relevant, pos)) continue;
-    const f64 v = mult * s.At.coefs[i];
-    if (sd_fabs(v) > drop) {
-      s.coeff[pos] = v;
-      s.nzpos[s.n_nzpos++] = pos;
-    }
-  }
+  const int64_t b = s.At.starts[row_as_col];
+  const int len = static_cast<int>(s.At.starts[row_as_col + 1] - b);
+  const int32_t* rows = s.At.rows + b;
+  const f64* coefs = s.At.coefs + b;
+  const uint64_t* relevant = s.relevant;
+  f64* coeff = s.coeff;
+  // Entries in row order; a kept entry also writes its product.
+  s.n_nzpos = sd_ordered_compact_map(
+      len, s.nzpos,
+      [&](int k) {
+        const int pos = rows[k];
+        if (!bit_get(relevant, pos)) return false;
+        const f64 v = mult * coefs[k];
+        if (!(sd_fabs(v) > drop)) return false;
+        coeff[pos] = v;
+        return true;
+      },
+      [&](int k) { return rows[k]; });
 }
 SD_INLINE void ur_column_wise(Lp& s) {
   s.n_nzpos = 0;
@@ -1397,16 +1634,11 @@ SD_INLINE void ur_column_wise(Lp& s) {
     }
   }
   sd_sync();
-  for (int w = 0; w < s.nwords; ++w) {
-    uint64_t word = s.relevant[w];
-    while (word) {
-      const int col = w * 64 + sd_ctz(word);
-      word &= word - 1;
-      if (col >= s.N) break;
-      if (s.col_flag[col]) s.nzpos[s.n_nzpos++] = col;
-    }
-  }
-  sd_sync();
+  const uint64_t* relevant = s.relevant;
+  const char* flag = s.col_flag;
+  s.n_nzpos = sd_ordered_compact(s.N, s.nzpos, [&](int col) {
+    return flag[col] && bit_get(relevant, col);
+  });
   for (int k = sd_lane(); k < s.n_nzpos; k += sd_lanes()) s.col_flag[s.nzpos[k]] = 0;
   sd_sync();
 }
@@ -1415,25 +1647,21 @@ SD_INLINE void ur_compute_update_row(Lp& s, int leaving_row) {
   s.urow_for = leaving_row;
   ur_compute_unit_row_left_inverse(s, leaving_row);
   if (s.use_transposed_matrix) {
-    int64_t num_row_wise_entries = 0;
     const f64 drop = s.drop_tolerance;
-    s.n_rho_filtered = 0;
+    const f64* rho = s.rho.values;
+    const int32_t* rho_nz = s.rho.nz;
     if (s.rho.nnz == 0) {
-      for (int col = 0; col < s.rho.size; ++col) {
-        if (sd_fabs(s.rho.values[col]) > drop) {
-          s.rho_filtered[s.n_rho_filtered++] = col;
-          num_row_wise_entries += col_entries(s.At, col);
-        }
-      }
+      s.n_rho_filtered = sd_ordered_compact(
+          s.rho.size, s.rho_filtered, [&](int col) { return sd_fabs(rho[col]) > drop; });
     } else {
-      for (int k = 0; k < s.rho.nnz; ++k) {
-        const int col = s.rho.nz[k];
-        if (sd_fabs(s.rho.values[col]) > drop) {
-          s.rho_filtered[s.n_rho_filtered++] = col;
-          num_row_wise_entries += col_entries(s.At, col);
-        }
-      }
+      s.n_rho_filtered = sd_ordered_compact_map(
+          s.rho.nnz, s.rho_filtered, [&](int k) { return sd_fabs(rho[rho_nz[k]]) > drop; },
+          [&](int k) { return rho_nz[k]; });
     }
+    int64_t num_row_wise_entries = 0;  // an integer sum: any order
+    for (int k = sd_lane(); k < s.n_rho_filtered; k += sd_lanes())
+      num_row_wise_entries += col_entries(s.At, s.rho_filtered[k]);
+    num_row_wise_entries = sd_wave_sum_i64(num_row_wise_entries);
     if (s.n_rho_filtered == 1) {
       ur_single_row(s, s.rho_filtered[0]);
       s.ur_ops += num_row_wise_entries;
@@ -1768,6 +1996,10 @@ SD_INLINE void sd_install_lu(Lp& s, const LuImage* im, uintptr_t b) {
     t->rows = reinterpret_cast<int32_t*>(b + reinterpret_cast<uintptr_t>(src.rows));
     t->coefs = reinterpret_cast<f64*>(b + reinterpret_cast<uintptr_t>(src.coefs));
     t->diag = reinterpret_cast<f64*>(b + reinterpret_cast<uintptr_t>(src.diag));
+    if (src.num_levels >= 0) {
+      t->lv_order = reinterpret_cast<int32_t*>(b + reinterpret_cast<uintptr_t>(src.lv_order));
+      t->lv_starts = reinterpret_cast<int32_t*>(b + reinterpret_cast<uintptr_t>(src.lv_starts));
+    }
   };
   fix(&s.lower, im->lower);
   fix(&s.upper, im->upper);
@@ -1947,13 +2179,6 @@ SD_INLINE bool sd_room_for_iteration(const Lp& s) {
 // Phase timer (device only): 0 loop top, 1 leaving row, 2 BTRAN, 3 update
 // row, 4 ratio test, 5 FTRAN, 6 rc and norm updates with tau, 7 pivot (x,
 // basis, MPF), 8 factorization requests.
-SD_INLINE uint64_t sd_now() {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return wall_clock64();
-#else
-  return 0;
-#endif
-}
 #define SD_PHASE(k)                          \
   do {                                       \
     const uint64_t now_ = sd_now();          \

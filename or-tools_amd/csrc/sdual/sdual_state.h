@@ -62,6 +62,13 @@ struct Tri {
   int first_non_identity;
   int all_ones;
   int64_t ncoefs;  // coefficients_.size() (num_entries() = num_cols + ncoefs)
+  // Level schedule of the transposed (gather) solve over this matrix: the
+  // columns of level k are lv_order[lv_starts[k] .. lv_starts[k + 1]) and
+  // read only columns of earlier levels. num_levels < 0: no schedule.
+  int32_t* lv_order;
+  int32_t* lv_starts;
+  int32_t num_levels;
+  int32_t lv_pad;
 };
 
 // Growing CompactSparseMatrix (the MPF storages, basis_representation.h).

@@ -5,7 +5,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r03_c4small
 mkdir -p $OUT
-for P in 0 1; do
+for P in ${POOLS:-0 1}; do
   echo "== pool=$P $(date +%T)"
   MILP_SDUAL=device MILP_SDUAL_POOL=$P MILP_SDUAL_PROFILE=1 timeout -k 10 150 python3 -u \
     $R/scripts/probe_batch.py --node --lps ${LPS:-32} --workers ${W:-16} > $OUT/c4_pool$P.json \
