@@ -2037,16 +2037,37 @@ SD_INLINE int sd_refactorize(Lp& s, int bump) {
   s.mb->bump = bump;
   __threadfence_system();
   sd_mb_store(&s.mb->flag, 1);
-  while (sd_mb_load(&s.mb->flag) != 2) __builtin_amdgcn_s_sleep(8);
+  // The flag sits in host memory: every poll is a PCIe read. One lane polls,
+  // backing off from ~3 us to ~27 us (a Markowitz answer takes ~100 us), so
+  // that hundreds of waiting waves leave the link to the image copies.
+  for (int polls = 0;; ++polls) {
+    int32_t f = 0;
+    if (sd_lane() == 0) f = sd_mb_load(&s.mb->flag);
+    if (__shfl(f, 0, 64) == 2) break;
+    const int reps = polls < 4 ? 1 : polls < 12 ? 3 : 8;
+    for (int r = 0; r < reps; ++r) __builtin_amdgcn_s_sleep(127);
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const LuImage* im = reinterpret_cast<const LuImage*>(s.mb_image);
   status = im->status;
   const f64 dtime = im->last_fact_dtime;
   if (status == 0) {
-    const int64_t words = (im->bytes + 7) / 8;
-    const volatile uint64_t* src = reinterpret_cast<const volatile uint64_t*>(s.mb_image);
-    uint64_t* dst = reinterpret_cast<uint64_t*>(s.lu_region);
-    for (int64_t w = sd_lane(); w < words; w += sd_lanes()) dst[w] = src[w];
+    // Over PCIe: 16-byte words, eight reads in flight per lane.
+    SdSubTimer t_(&s.phase_ticks[12]);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const int64_t words = (im->bytes + 15) / 16;
+    const u32x4* src = reinterpret_cast<const u32x4*>(s.mb_image);
+    u32x4* dst = reinterpret_cast<u32x4*>(s.lu_region);
+    const int lane = sd_lane();
+    int64_t w = 0;
+    for (; w + 8 * 64 <= words; w += 8 * 64) {
+      u32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(src + w + u * 64 + lane);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) dst[w + u * 64 + lane] = v[u];
+    }
+    for (w += lane; w < words; w += 64) dst[w] = src[w];
     sd_sync();
   }
   sd_mb_store(&s.mb->flag, 0);

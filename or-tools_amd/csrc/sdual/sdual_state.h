@@ -314,7 +314,7 @@ struct Lp {
   int64_t mutable_end;
   f64* coeff_out;        // DeviceLp's update-row coefficients (N), refreshed at the end
   // Device time per loop phase (wall_clock64 ticks, 100 MHz): see sd_run.
-  uint64_t phase_ticks[12];
+  uint64_t phase_ticks[16];
 
   // ---- loop carry and exit ----
   int refactorize;  // the host loop's `refactorize` flag

@@ -53,8 +53,10 @@ def main():
         for h in hs:
             h.reset_kernel_stats()
         t = time.perf_counter()
+        c0 = time.process_time()
         res = engine.batch_solve_bounds(hs, lbs, ubs, state)
         dt = time.perf_counter() - t
+        cpu = time.process_time() - c0
         gpu_res[w] = res
         its = sum(r.iterations for r in res)
         agg = {}
@@ -64,6 +66,7 @@ def main():
                 d["launches"] += v["launches"]
                 d["call_ms"] += v["call_ms"]
         out[f"gpu_w{w}"] = {"lps_per_s": a.lps / dt, "iterations": its,
+                            "wall_s": dt, "host_cpu_s": cpu,
                             "us_per_iteration_per_worker": 1e6 * dt * w / max(1, its),
                             "kernels": {k: v for k, v in agg.items() if v["launches"] or v["call_ms"]}}
         print(f"[probe] w={w}: {a.lps / dt:.1f} LPs/s", file=sys.stderr, flush=True)
