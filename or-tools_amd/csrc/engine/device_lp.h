@@ -25,6 +25,8 @@ struct Mailbox;
 }
 
 namespace milp {
+// Zeroes the MILP_SDUAL_PROFILE host counters (sdual_kernel.hip).
+void SdualProfileReset();
 
 class CompactSparseMatrix;
 
@@ -211,6 +213,12 @@ class DeviceLp : public DeviceSolver {
   // Batched small-LP launches for this handle (the batch APIs turn it on for
   // their duration; MILP_SMALL_BATCH=1 turns it on everywhere, =0 nowhere).
   void SetSmallBatch(bool on);
+  // Batched small LPs whose dual loop runs as a device segment (csrc/sdual):
+  // the once-per-solve row sums and column dots outside the loop run on the
+  // host thread that owns the LP (Glop's order, the kernels' bits) instead of
+  // as single launches that queue behind hundreds of other LPs' work.
+  void SetHostSmallOps(bool on) { host_small_ops_ = on; }
+  bool host_small_ops() const { return host_small_ops_; }
   bool small_batch() const { return small_batch_; }
   int shard_begin(int s) const { return shard_begin_[s]; }
 
@@ -252,6 +260,7 @@ class DeviceLp : public DeviceSolver {
   void WaitSmallBatch();
   void RestoreDevice();  // after a fiber yield
   bool small_batch_ = false;
+  bool host_small_ops_ = false;
   int batch_slot_ = -1;
   unsigned long long batch_seq_ = 0;
   bool batch_pending_ = false;

@@ -449,7 +449,7 @@ void DeviceLp::WaitSmallBatch() {
   int spins = 0;
   while (b.done(batch_slot_) != batch_seq_) {
     if (InFiber()) {
-      FiberYield();
+      FiberYield(spins > 0);
       RestoreDevice();
     } else {
       __builtin_ia32_pause();
@@ -479,8 +479,10 @@ void DeviceLp::RestoreDevice() {
 void DeviceLp::WaitStream() {
   WaitSmallBatch();
   if (InFiber()) {
+    bool polled = false;  // later rounds of this wait only poll
     while (hipStreamQuery(S(stream_)) == hipErrorNotReady) {
-      FiberYield();
+      FiberYield(polled);
+      polled = true;
       RestoreDevice();
     }
   }

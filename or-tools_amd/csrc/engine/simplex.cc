@@ -24,6 +24,45 @@
 #include "../../../include/mi_lp.h"
 #include "device_lp.h"
 #include "fibers.h"
+
+// fibers.h's context switch (x86-64 SysV). The frame it pushes and pops:
+// [control words][r15][r14][r13][r12][rbx][rbp][return address].
+asm(R"(
+  .text
+  .globl milp_fiber_switch
+  .type milp_fiber_switch, @function
+milp_fiber_switch:
+  pushq %rbp
+  pushq %rbx
+  pushq %r12
+  pushq %r13
+  pushq %r14
+  pushq %r15
+  subq $8, %rsp
+  stmxcsr (%rsp)
+  fnstcw 4(%rsp)
+  movq %rsp, (%rdi)
+  movq %rsi, %rsp
+  ldmxcsr (%rsp)
+  fldcw 4(%rsp)
+  addq $8, %rsp
+  popq %r15
+  popq %r14
+  popq %r13
+  popq %r12
+  popq %rbx
+  popq %rbp
+  ret
+  .size milp_fiber_switch, .-milp_fiber_switch
+
+  .globl milp_fiber_trampoline
+  .type milp_fiber_trampoline, @function
+milp_fiber_trampoline:
+  movq %r12, %rdi
+  callq *%r13
+  ud2
+  .size milp_fiber_trampoline, .-milp_fiber_trampoline
+)");
 #include "host_pool.h"
 
 #include <chrono>
@@ -1507,7 +1546,12 @@ Fractional ReducedCosts::ComputeMaximumDualResidual() {
   Fractional err = 0.0;
   const int num_rows = matrix_.num_rows();
   const std::vector<Fractional>& y = GetDualValues();
-  dev_->ListDots(basis_, y, &dots_);  // a_{B(r)} . y on the GPU
+  if (dev_->host_small_ops()) {
+    dots_.resize(num_rows);
+    for (int row = 0; row < num_rows; ++row) dots_[row] = matrix_.ColumnScalarProduct(basis_[row], y);
+  } else {
+    dev_->ListDots(basis_, y, &dots_);  // a_{B(r)} . y on the GPU
+  }
   for (int row = 0; row < num_rows; ++row) {
     const int basic_col = basis_[row];
     const Fractional residual =
@@ -1633,6 +1677,10 @@ void ReducedCosts::ComputeReducedCosts() {
       deferred_norms_->FlushPendingUpdate();
       dev_->Pricing(shifted_objective_, y, &reduced_costs_);
     }
+  } else if (dev_->host_small_ops() && !device_mode_) {
+    reduced_costs_.resize(num_cols);
+    for (int col = 0; col < num_cols; ++col)
+      reduced_costs_[col] = shifted_objective_[col] - matrix_.ColumnScalarProduct(col, y);
   } else {
     dev_->Pricing(shifted_objective_, y, &reduced_costs_);
   }
@@ -2425,15 +2473,34 @@ void VariableValues::ResetAllNonBasicVariableValues(const std::vector<Fractional
   }
 }
 
+// Host forms of DeviceLp::RowSums / ListDots / Pricing for the sdual batch
+// mode (DeviceLp::SetHostSmallOps): sparse.h's ColumnAddMultipleToDenseColumn
+// and ColumnScalarProduct in column order, as the kernels sum.
+namespace {
+void HostRowSums(const CompactSparseMatrix& a, const std::vector<Fractional>& x,
+                 const Bitset* skip, Fractional sign, std::vector<Fractional>* out) {
+  out->assign(a.num_rows(), 0.0);
+  for (int col = 0; col < a.num_cols(); ++col) {
+    if (skip != nullptr && skip->IsSet(col)) continue;
+    a.ColumnAddMultipleToDenseColumn(col, sign * x[col], out->data());
+  }
+}
+}  // namespace
+
 // variable_values.cc:101-118
 void VariableValues::RecomputeBasicVariableValues() {
   SubTimer timer(kSubRecomputeValues);
   const int num_rows = matrix_.num_rows();
   scratchpad_.non_zeros.clear();
   // -sum over non-basic columns of x_j a_j, per row in column order (GPU).
-  dev_->SetMask(DeviceLp::kBasic, variables_info_.GetIsBasicBitRow().data(),
-                variables_info_.GetIsBasicBitRow().NumWords());
-  dev_->RowSums(variable_values_, /*skip_basic=*/true, -1.0, &scratchpad_.values);
+  if (dev_->host_small_ops()) {
+    HostRowSums(matrix_, variable_values_, &variables_info_.GetIsBasicBitRow(), -1.0,
+                &scratchpad_.values);
+  } else {
+    dev_->SetMask(DeviceLp::kBasic, variables_info_.GetIsBasicBitRow().data(),
+                  variables_info_.GetIsBasicBitRow().NumWords());
+    dev_->RowSums(variable_values_, /*skip_basic=*/true, -1.0, &scratchpad_.values);
+  }
   bf_.RightSolve(&scratchpad_);
   for (int row = 0; row < num_rows; ++row) variable_values_[basis_[row]] = scratchpad_[row];
   dual_prices_->Clear();
@@ -2442,7 +2509,11 @@ void VariableValues::RecomputeBasicVariableValues() {
 // variable_values.cc:120-131
 Fractional VariableValues::ComputeMaximumPrimalResidual() const {
   scratchpad_.non_zeros.clear();
-  dev_->RowSums(variable_values_, /*skip_basic=*/false, 1.0, &scratchpad_.values);
+  if (dev_->host_small_ops()) {
+    HostRowSums(matrix_, variable_values_, nullptr, 1.0, &scratchpad_.values);
+  } else {
+    dev_->RowSums(variable_values_, /*skip_basic=*/false, 1.0, &scratchpad_.values);
+  }
   return InfinityNorm(scratchpad_.values);
 }
 
@@ -3260,12 +3331,17 @@ class RevisedSimplex {
       if (std::strcmp(e, "device") == 0 || std::strcmp(e, "on") == 0) return 2;
       return 0;
     }();
+    static const bool host_ops = [] {
+      const char* e = std::getenv("MILP_SDUAL_HOSTOPS");
+      return e == nullptr || std::atoi(e) != 0;
+    }();
     if (on) {
       saved_sdual_mode_ = sdual_mode_;
       sdual_mode_ = batch_mode;
     } else {
       sdual_mode_ = saved_sdual_mode_;
     }
+    device_.SetHostSmallOps(on && sdual_mode_ == 2 && host_ops);
   }
   void SdualCounters(int64_t* segments, int64_t* iterations) const {
     *segments = sdual_segments_;
@@ -3977,7 +4053,11 @@ void RevisedSimplex::CorrectErrorsOnVariableValues() {
 }
 
 void RevisedSimplex::ComputeVariableValuesError() {
-  device_.RowSums(variable_values_.GetDenseRow(), /*skip_basic=*/false, -1.0, &error_);
+  if (device_.host_small_ops()) {
+    HostRowSums(compact_matrix_, variable_values_.GetDenseRow(), nullptr, -1.0, &error_);
+  } else {
+    device_.RowSums(variable_values_.GetDenseRow(), /*skip_basic=*/false, -1.0, &error_);
+  }
 }
 
 // revised_simplex.cc:1695-1720
@@ -6023,3 +6103,10 @@ int mi_lp_batch_solve_gpus(mi_lp* const* handles, int32_t count, int32_t num_gpu
 }
 
 }  // extern "C"
+
+// Development aid (scripts/probe_batch.py): zero the MILP_SDUAL_PROFILE
+// counters after a warm-up batch.
+extern "C" void milp_sdual_profile_reset() {
+  milp::SdualBridge::ResetProfile();
+  milp::SdualProfileReset();
+}

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstddef>
 #include <chrono>
 #include <cstdio>
@@ -136,6 +137,7 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring
     // move it into the arena, run, move the mutable part back.
     const sdual::Lp* sh = reinterpret_cast<const sdual::Lp*>(entry_shared);
     const char* stage = reinterpret_cast<const char*>(sh);
+    const uint64_t t_claim = wall_clock64();
     char* arena = reinterpret_cast<char*>(sh->arena_dev);
     const uint64_t arena_addr = sh->arena_dev;
     team_copy(arena, stage, sizeof(sdual::Lp));
@@ -152,7 +154,9 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring
     __syncthreads();
     if (threadIdx.x == 0) pool_dbg(q, 2, 2);
     sdual::Lp* lp = reinterpret_cast<sdual::Lp*>(arena);
+    lp->phase_ticks[13] += wall_clock64() - t_claim;  // staging image in
     sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
+    const uint64_t t_out = wall_clock64();
     if (threadIdx.x == 0) {
       pool_dbg(q, 2, 3);
       pool_dbg(q, 3, lp->num_iterations);
@@ -177,6 +181,11 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring
     }
     if (threadIdx.x == 0) pool_dbg(q, 2, 34);
     __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      reinterpret_cast<sdual::Lp*>(stage_out)->phase_ticks[14] =
+          lp->phase_ticks[14] + (wall_clock64() - t_out);  // staging image out
+    }
     if (threadIdx.x == 0) pool_dbg(q, 2, 35);
     __syncthreads();
     if (threadIdx.x == 0) pool_dbg(q, 2, 36);
@@ -293,9 +302,83 @@ class SdualPool {
 };
 }  // namespace
 
+// MILP_SDUAL_PROFILE: reallocations of the arena / mailbox and their time.
+namespace {
+// How long pooled-segment fibers were away between their polls.
+struct GapSum {
+  std::atomic<int64_t> total_ns{0}, last_ns{0}, max_ns{0}, polls{0}, segments{0};
+  ~GapSum() {
+    std::fprintf(stderr,
+                 "  host fiber polls %lld, away %.1f us total, max %.1f us; last gap %.1f us "
+                 "over %lld segments\n",
+                 static_cast<long long>(polls.load()), total_ns.load() / 1e3, max_ns.load() / 1e3,
+                 last_ns.load() / 1e3, static_cast<long long>(segments.load()));
+    std::fprintf(stderr, "  host fiber slices > 1 ms: %lld, %.1f us; longest %.1f us\n",
+                 static_cast<long long>(fiber_detail::g_slices.long_count.load()),
+                 fiber_detail::g_slices.long_ns.load() / 1e3,
+                 fiber_detail::g_slices.max_ns.load() / 1e3);
+  }
+};
+GapSum gaps;
+// When the pooled segments were enqueued and seen done (ns since the last
+// profile reset): the batch's ramp and tail.
+struct Timeline {
+  std::mutex mu;
+  std::chrono::steady_clock::time_point epoch = std::chrono::steady_clock::now();
+  std::vector<int64_t> enq, done;
+  int64_t Now() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                epoch).count();
+  }
+  static void Print(const char* what, std::vector<int64_t> v) {
+    if (v.empty()) return;
+    std::sort(v.begin(), v.end());
+    auto q = [&](double f) { return v[std::min(v.size() - 1, static_cast<size_t>(f * v.size()))] / 1e6; };
+    std::fprintf(stderr, "  host %s ms: p0 %.1f p10 %.1f p50 %.1f p90 %.1f p100 %.1f\n", what,
+                 q(0.0), q(0.1), q(0.5), q(0.9), q(1.0));
+  }
+  ~Timeline() {
+    if (std::getenv("MILP_SDUAL_PROFILE") == nullptr) return;
+    Print("segment enqueued at", enq);
+    Print("segment done at", done);
+  }
+};
+Timeline timeline;
+
+struct ReserveStats {
+  std::atomic<int64_t> reallocs{0}, ns{0};
+  ~ReserveStats() {
+    if (std::getenv("MILP_SDUAL_PROFILE") == nullptr) return;
+    std::fprintf(stderr, "  host reserve reallocs %lld, %.1f us\n",
+                 static_cast<long long>(reallocs.load()), ns.load() / 1e3);
+  }
+};
+ReserveStats g_reserve_stats;
+}  // namespace
+
+void SdualProfileReset() {
+  {
+    std::lock_guard<std::mutex> lock(timeline.mu);
+    timeline.epoch = std::chrono::steady_clock::now();
+    timeline.enq.clear();
+    timeline.done.clear();
+  }
+  for (auto* a : {&gaps.total_ns, &gaps.last_ns, &gaps.max_ns, &gaps.polls, &gaps.segments,
+                  &g_reserve_stats.reallocs, &g_reserve_stats.ns, &fiber_detail::g_slices.long_ns,
+                  &fiber_detail::g_slices.long_count, &fiber_detail::g_slices.max_ns}) {
+    a->store(0);
+  }
+}
+
+// The arena and staging image grow to twice the first request (a later
+// segment's LU or rank-one storage may need more); a reallocation frees the
+// old buffers, which waits on the device.
 void DeviceLp::SdualReserve(size_t bytes, int rows, int64_t lu_cap) {
+  const auto t0 = std::chrono::steady_clock::now();
+  bool realloc = false;
   if (bytes > sdual_cap_) {
-    const size_t cap = std::max(bytes + bytes / 4, static_cast<size_t>(1) << 20);
+    realloc = true;
+    const size_t cap = std::max(2 * bytes, static_cast<size_t>(1) << 20);
     if (sdual_arena_ != nullptr) {
       Check(hipStreamSynchronize(Stream(stream_)), "sdual sync");
       Check(hipFree(sdual_arena_), "hipFree");
@@ -313,8 +396,9 @@ void DeviceLp::SdualReserve(size_t bytes, int rows, int64_t lu_cap) {
   const size_t image_off = basis_off + ((sizeof(int32_t) * static_cast<size_t>(rows) + 255) & ~size_t{255});
   const size_t mb_bytes = image_off + static_cast<size_t>(lu_cap);
   if (mb_bytes > sdual_mb_cap_) {
+    realloc = true;
     if (sdual_mb_block_ != nullptr) Check(hipHostFree(sdual_mb_block_), "hipHostFree mailbox");
-    const size_t cap = mb_bytes + mb_bytes / 4;
+    const size_t cap = 2 * mb_bytes;
     Check(hipHostMalloc(&sdual_mb_block_, cap, hipHostMallocMapped | hipHostMallocCoherent),
           "hipHostMalloc mailbox");
     Check(hipHostGetDevicePointer(&sdual_mb_device_, sdual_mb_block_, 0), "mailbox pointer");
@@ -326,6 +410,11 @@ void DeviceLp::SdualReserve(size_t bytes, int rows, int64_t lu_cap) {
   sdual_mb_image_ = base + image_off;
   std::memset(base, 0, sizeof(sdual::Mailbox));
   sdual_mb_->image_cap = lu_cap;
+  if (realloc) {
+    ++g_reserve_stats.reallocs;
+    g_reserve_stats.ns += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now() - t0).count();
+  }
 }
 
 void DeviceLp::SdualMailboxDevice(sdual::Mailbox** mb, int32_t** basis, char** image) const {
@@ -394,18 +483,21 @@ void DeviceLp::SdualRun(size_t bytes, const double* arena_coeff, int n, void (*s
   EndKernel(MI_K_SDUAL, 2.0 * static_cast<double>(bytes));
   // Answer factorization requests until the stream (kernel, copies) is done.
   int32_t* flag = &sdual_mb_->flag;
+  bool idle = false;  // the slice since the last resume found nothing to do
   while (true) {
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == 1) {
       DeviceOp("sdual factorization request");
       serve(ctx);
       __atomic_store_n(flag, 2, __ATOMIC_RELEASE);
+      idle = false;
       continue;
     }
     const hipError_t q = hipStreamQuery(Stream(stream_));
     if (q == hipSuccess) break;
     if (q != hipErrorNotReady) Check(q, "sdual segment");
     if (InFiber()) {
-      FiberYield();
+      FiberYield(idle);
+      idle = true;
       RestoreDevice();
     } else {
       std::this_thread::yield();
@@ -413,6 +505,104 @@ void DeviceLp::SdualRun(size_t bytes, const double* arena_coeff, int n, void (*s
   }
   DeviceOp("sdual segment done");
 }
+
+// ---------------------------------------------------------------------------
+// LU servers: with hundreds of LPs on a few host threads' fibers, a fiber sees
+// its segment's factorization request only when the round robin comes back to
+// it (a whole cycle of other LPs' host work). Server threads
+// (MILP_SDUAL_SERVERS, default 4; 0 = the fibers alone) scan the mailboxes of
+// the running pooled segments and answer at once. The mailbox flag arbitrates:
+// whoever moves it 1 -> 4 serves, then stores 2. The requesting LP's host
+// objects are idle meanwhile (its fiber waits in SdualRunPooled), and the
+// answer is published by the release store of 2.
+class LuServers {
+ public:
+  static constexpr int kSlots = 8192;
+  static LuServers* Get() {
+    static LuServers* s = new LuServers();  // never destroyed (detached threads)
+    return s;
+  }
+  bool enabled() const { return threads_ > 0; }
+  int Register(int32_t* flag, void (*serve)(void*), void* ctx) {
+    std::lock_guard<std::mutex> lock(mu_);
+    int slot;
+    if (!free_.empty()) {
+      slot = free_.back();
+      free_.pop_back();
+    } else {
+      if (used_ >= kSlots) return -1;
+      slot = used_++;
+    }
+    Slot& sl = slots_[slot];
+    sl.serve = serve;
+    sl.ctx = ctx;
+    sl.flag.store(flag, std::memory_order_release);
+    if (slot + 1 > hi_.load(std::memory_order_relaxed)) hi_.store(slot + 1, std::memory_order_release);
+    return slot;
+  }
+  // Returns once no server is inside this slot's service.
+  void Unregister(int slot) {
+    if (slot < 0) return;
+    Slot& sl = slots_[slot];
+    sl.flag.store(nullptr, std::memory_order_seq_cst);
+    while (sl.busy.load(std::memory_order_seq_cst)) std::this_thread::yield();
+    std::lock_guard<std::mutex> lock(mu_);
+    free_.push_back(slot);
+  }
+  // Claims a pending request of `flag` (1 -> 4) for the caller to serve.
+  static bool Claim(int32_t* flag) {
+    int32_t expected = 1;
+    return __atomic_compare_exchange_n(flag, &expected, 4, false, __ATOMIC_ACQ_REL,
+                                       __ATOMIC_ACQUIRE);
+  }
+
+ private:
+  struct Slot {
+    std::atomic<int32_t*> flag{nullptr};
+    std::atomic<bool> busy{false};
+    void (*serve)(void*) = nullptr;
+    void* ctx = nullptr;
+  };
+  LuServers() {
+    int n = 4;
+    if (const char* e = std::getenv("MILP_SDUAL_SERVERS")) n = std::max(0, std::atoi(e));
+    threads_ = n;
+    for (int t = 0; t < n; ++t) std::thread([this, t, n] { Loop(t, n); }).detach();
+  }
+  void Loop(int t, int n) {
+    int idle = 0;
+    while (true) {
+      bool served = false;
+      const int hi = hi_.load(std::memory_order_acquire);
+      for (int i = t; i < hi; i += n) {
+        Slot& sl = slots_[i];
+        int32_t* flag = sl.flag.load(std::memory_order_acquire);
+        if (flag == nullptr || __atomic_load_n(flag, __ATOMIC_ACQUIRE) != 1) continue;
+        sl.busy.store(true, std::memory_order_seq_cst);
+        // Re-read after raising busy: Unregister clears the flag pointer first.
+        if (sl.flag.load(std::memory_order_seq_cst) == flag && Claim(flag)) {
+          sl.serve(sl.ctx);
+          __atomic_store_n(flag, 2, __ATOMIC_RELEASE);
+          served = true;
+        }
+        sl.busy.store(false, std::memory_order_release);
+      }
+      if (served) {
+        idle = 0;
+      } else if (++idle > 64) {
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+      } else {
+        std::this_thread::yield();
+      }
+    }
+  }
+  int threads_ = 0;
+  std::mutex mu_;
+  std::vector<int> free_;
+  int used_ = 0;
+  std::atomic<int> hi_{0};
+  Slot slots_[kSlots];
+};
 
 // The same segment through the device's persistent pool kernel: a resident
 // workgroup moves the staging image in and out itself (no stream work, so
@@ -431,9 +621,25 @@ void DeviceLp::SdualRunPooled(size_t bytes, const double* arena_coeff, int n,
   int32_t* flag = &sdual_mb_->flag;
   __atomic_store_n(flag, 0, __ATOMIC_RELEASE);
   SdualPool& pool = SdualPool::Get(device_);
+  LuServers* servers = LuServers::Get();
+  const int slot = servers->enabled() ? servers->Register(flag, serve, ctx) : -1;
+  struct Unreg {
+    LuServers* s;
+    int slot;
+    ~Unreg() { s->Unregister(slot); }
+  } unreg{servers, slot};
+  if (std::getenv("MILP_SDUAL_PROFILE") != nullptr) {
+    std::lock_guard<std::mutex> lock(timeline.mu);
+    timeline.enq.push_back(timeline.Now());
+  }
   pool.Enqueue(sdual_staging_dev_);
   int64_t polls = 0;
   static const bool debug = std::getenv("MILP_SDUAL_DEBUG") != nullptr;
+  // MILP_SDUAL_PROFILE: how long the fiber was away between its polls (the
+  // last gap bounds the delay in seeing the segment done).
+  static const bool prof = std::getenv("MILP_SDUAL_PROFILE") != nullptr;
+  int64_t gap_ns = 0;
+  bool idle = false;  // the slice since the last resume found nothing to do
   const auto t0 = std::chrono::steady_clock::now();
   int64_t next_report = 1;
   while (true) {
@@ -453,11 +659,20 @@ void DeviceLp::SdualRunPooled(size_t bytes, const double* arena_coeff, int n,
         next_report += 1;
       }
     }
-    if (f == 3) break;
-    if (f == 1) {
+    if (f == 3) {
+      if (prof) {
+        gaps.last_ns += gap_ns;
+        ++gaps.segments;
+        std::lock_guard<std::mutex> lock(timeline.mu);
+        timeline.done.push_back(timeline.Now());
+      }
+      break;
+    }
+    if (f == 1 && LuServers::Claim(flag)) {
       DeviceOp("sdual factorization request");
       serve(ctx);
       __atomic_store_n(flag, 2, __ATOMIC_RELEASE);
+      idle = false;
       continue;
     }
     if ((++polls & 1023) == 0 && !pool.Alive() && __atomic_load_n(flag, __ATOMIC_ACQUIRE) == 0) {
@@ -465,11 +680,22 @@ void DeviceLp::SdualRunPooled(size_t bytes, const double* arena_coeff, int n,
       // again on a new grid.
       pool.Enqueue(sdual_staging_dev_);
     }
+    const auto y0 = prof ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
     if (InFiber()) {
-      FiberYield();
+      FiberYield(idle);
+      idle = true;
       RestoreDevice();
     } else {
       std::this_thread::yield();
+    }
+    if (prof) {
+      gap_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now() - y0).count();
+      gaps.total_ns += gap_ns;
+      ++gaps.polls;
+      int64_t m = gaps.max_ns.load();
+      while (gap_ns > m && !gaps.max_ns.compare_exchange_weak(m, gap_ns)) {
+      }
     }
   }
   ++stats_.launches[MI_K_SDUAL];

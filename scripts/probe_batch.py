@@ -52,6 +52,7 @@ def main():
         engine.batch_solve_bounds(hs, lbs[:w], ubs[:w], state)  # warm-up
         for h in hs:
             h.reset_kernel_stats()
+        engine.lib().milp_sdual_profile_reset()
         t = time.perf_counter()
         c0 = time.process_time()
         res = engine.batch_solve_bounds(hs, lbs, ubs, state)
