@@ -617,8 +617,25 @@ SD_INLINE void tri_level_sweep_lower(const Tri& t, f64* x, int last) {
     sd_sync();
   }
 }
-SD_INLINE void tri_transpose_upper_solve(const Tri& t, f64* x) {
+// The dense vector of a level sweep in LDS when it fits: each level then
+// waits on one round trip (its entries) instead of three.
+SD_INLINE f64* sd_stage_in(f64* lds, int cap, const f64* x, int n) {
+  if (lds == nullptr || n > cap) return nullptr;
+  for (int i = sd_lane(); i < n; i += sd_lanes()) lds[i] = x[i];
+  sd_sync();
+  return lds;
+}
+SD_INLINE void sd_stage_out(const f64* lds, f64* x, int n) {
+  for (int i = sd_lane(); i < n; i += sd_lanes()) x[i] = lds[i];
+  sd_sync();
+}
+SD_INLINE void tri_transpose_upper_solve(const Tri& t, f64* x, f64* lds = nullptr, int cap = 0) {
   if (tri_use_levels(t)) {
+    if (f64* v = sd_stage_in(lds, cap, x, t.num_cols)) {
+      tri_level_sweep_upper(t, v);
+      sd_stage_out(v, x, t.num_cols);
+      return;
+    }
     tri_level_sweep_upper(t, x);
     return;
   }
@@ -640,11 +657,17 @@ SD_INLINE int tri_last_nonzero(const f64* x, int end, int num_cols) {
   return col;
 #endif
 }
-SD_INLINE void tri_transpose_lower_solve(const Tri& t, f64* x) {
+SD_INLINE void tri_transpose_lower_solve(const Tri& t, f64* x, f64* lds = nullptr, int cap = 0) {
   const int end = t.first_non_identity;
   const int last = tri_last_nonzero(x, end, t.num_cols);
   if (last < end) return;
   if (tri_use_levels(t)) {
+    // Columns above `last` are read (zeros of either sign) but not written.
+    if (f64* v = sd_stage_in(lds, cap, x, t.num_cols)) {
+      tri_level_sweep_lower(t, v, last);
+      sd_stage_out(v, x, last + 1);
+      return;
+    }
     tri_level_sweep_lower(t, x, last);
     return;
   }
@@ -893,7 +916,7 @@ SD_INLINE void lu_right_solve_u_with_nz(Lp& s, Vec& x) {
   if (x.nnz == 0) {
     {
       SdSubTimer t_(&s.phase_ticks[10]);
-      tri_transpose_lower_solve(s.tupper, x.values);
+      tri_transpose_lower_solve(s.tupper, x.values, s.lds, s.lds_doubles);
     }
   } else {
     tri_transpose_hyper_solve_rev(s.tupper, x.values, x.nz, &x.nnz);
@@ -908,7 +931,7 @@ SD_INLINE bool lu_left_solve_l_with_nz(Lp& s, Vec& y, Vec* before) {
   if (y.nnz == 0) {
     {
       SdSubTimer t_(&s.phase_ticks[10]);
-      tri_transpose_lower_solve(s.lower, y.values);
+      tri_transpose_lower_solve(s.lower, y.values, s.lds, s.lds_doubles);
     }
   } else {
     tri_transpose_hyper_solve_rev(s.lower, y.values, y.nz, &y.nnz);
@@ -1034,11 +1057,91 @@ SD_INLINE int64_t lu_number_of_entries(const Lp& s) {
 }
 
 // ---- RankOneUpdateFactorization (rank_one_update.h:30-246) ----
-SD_INLINE void r1_right_solve_dense(Lp& s, f64* x) {
-  for (int i = 0; i < s.r1_count; ++i) {
-    const f64 mult = -col_dot_par(s.storage, s.r1_v[i], x) / s.r1_mu[i];
-    col_add_dense(s.storage, s.r1_u[i], mult, x);
+#if defined(__HIP_DEVICE_COMPILE__)
+// Dense steps k = 0 .. count-1 of a solve: update i = first + k (right
+// solves) or first - k (left solves), x += mult * add_col with
+// mult = -(dot_col . x) / mu (right: dot v_i, add u_i; left: dot u_i, add
+// v_i). Lane k of a 64-step chunk loads step k's columns' bounds and mu
+// first; a step loads the first 64 entries of both columns and the add
+// column's current values together (the dot leaves x unchanged), so it waits
+// on two round trips to memory instead of eight. The dot keeps
+// ColumnScalarProduct's four chains and tail (col_dot_par).
+SD_INLINE void r1_dense_steps(Lp& s, f64* x, int first, int count, bool left) {
+  const Store& st = s.storage;
+  const int lane = sd_lane();
+  const int j = lane & 3;
+  for (int c0 = 0; c0 < count; c0 += 64) {
+    int64_t m_db = 0, m_de = 0, m_ab = 0, m_ae = 0;
+    f64 m_mu = 1.0;
+    if (c0 + lane < count) {
+      const int i = left ? first - (c0 + lane) : first + (c0 + lane);
+      const int dcol = left ? s.r1_u[i] : s.r1_v[i];
+      const int acol = left ? s.r1_v[i] : s.r1_u[i];
+      m_db = st.starts[dcol];
+      m_de = st.starts[dcol + 1];
+      m_ab = st.starts[acol];
+      m_ae = st.starts[acol + 1];
+      m_mu = s.r1_mu[i];
+    }
+    const int steps = count - c0 < 64 ? count - c0 : 64;
+    for (int k = 0; k < steps; ++k) {
+      const int64_t db = __shfl(m_db, k, 64), de = __shfl(m_de, k, 64);
+      const int64_t ab = __shfl(m_ab, k, 64), ae = __shfl(m_ae, k, 64);
+      const f64 mu = __shfl(m_mu, k, 64);
+      const int64_t di = db + lane, ai = ab + lane;
+      int dr = 0, ar = 0;
+      f64 dc = 0.0, ac = 0.0;
+      if (di < de) {
+        dr = st.rows[di];
+        dc = st.coefs[di];
+      }
+      if (ai < ae) {
+        ar = st.rows[ai];
+        ac = st.coefs[ai];
+      }
+      const f64 dx = di < de ? x[dr] : 0.0;
+      const f64 ax = ai < ae ? x[ar] : 0.0;
+      const f64 p0 = dc * dx;  // entry `lane` of the dot column's first chunk
+      const int64_t len = de - db;
+      const int64_t body = len & ~int64_t{3};
+      f64 acc = 0.0;
+      for (int64_t base = 0; base < body; base += 64) {
+        f64 p;
+        if (base == 0) {
+          p = lane < body ? p0 : 0.0;
+        } else {
+          const int64_t e = db + base + lane;
+          p = base + lane < body ? st.coefs[e] * x[st.rows[e]] : 0.0;
+        }
+        const int groups = static_cast<int>((body - base < 64 ? body - base : 64) >> 2);
+        for (int g = 0; g < groups; ++g) acc += __shfl(p, j + 4 * g, 64);
+      }
+      f64 dot = __shfl(acc, 0, 64) + __shfl(acc, 1, 64) + __shfl(acc, 2, 64) + __shfl(acc, 3, 64);
+      for (int64_t t = body; t < len; ++t) {
+        dot += t < 64 ? __shfl(p0, static_cast<int>(t), 64) : st.coefs[db + t] * x[st.rows[db + t]];
+      }
+      const f64 mult = -dot / mu;
+      if (mult != 0.0) {  // col_add_dense: a column's rows are distinct
+        if (ai < ae) x[ar] = ax + mult * ac;
+        for (int64_t e = ab + 64 + lane; e < ae; e += 64) x[st.rows[e]] += mult * st.coefs[e];
+      }
+      sd_sync();
+    }
   }
+}
+#else
+SD_INLINE void r1_dense_steps(Lp& s, f64* x, int first, int count, bool left) {
+  for (int k = 0; k < count; ++k) {
+    const int i = left ? first - k : first + k;
+    const int dcol = left ? s.r1_u[i] : s.r1_v[i];
+    const int acol = left ? s.r1_v[i] : s.r1_u[i];
+    const f64 mult = -col_dot(s.storage, dcol, x) / s.r1_mu[i];
+    col_add_dense(s.storage, acol, mult, x);
+  }
+}
+#endif
+SD_INLINE void r1_right_solve_dense(Lp& s, f64* x) {
+  r1_dense_steps(s, x, 0, s.r1_count, false);
   s.r1_dtime += dt_ops(s.r1_num_entries);
 }
 SD_INLINE void r1_right_solve_nz(Lp& s, Vec& d) {
@@ -1050,24 +1153,20 @@ SD_INLINE void r1_right_solve_nz(Lp& s, Vec& d) {
   vec_repopulate_mask(d);
   bool use_dense = vec_dense(d, 0.05);
   for (int i = 0; i < s.r1_count; ++i) {
-    if (use_dense) {
-      const f64 mult = -col_dot_par(s.storage, s.r1_v[i], d.values) / s.r1_mu[i];
-      col_add_dense(s.storage, s.r1_u[i], mult, d.values);
-    } else {
-      const f64 mult = -col_dot_par(s.storage, s.r1_v[i], d.values) / s.r1_mu[i];
-      if (mult != 0.0) col_add_scattered(s.storage, s.r1_u[i], mult, d);
-      use_dense = vec_dense(d, 0.05);
+    if (use_dense) {  // stays dense for the remaining updates
+      r1_dense_steps(s, d.values, i, s.r1_count - i, false);
+      break;
     }
+    const f64 mult = -col_dot_par(s.storage, s.r1_v[i], d.values) / s.r1_mu[i];
+    if (mult != 0.0) col_add_scattered(s.storage, s.r1_u[i], mult, d);
+    use_dense = vec_dense(d, 0.05);
   }
   vec_clear_mask(d);
   vec_clear_nz_if_too_dense(d, 0.05);
   s.r1_dtime += dt_ops(s.r1_num_entries);
 }
 SD_INLINE void r1_left_solve_dense(Lp& s, f64* y) {
-  for (int i = s.r1_count - 1; i >= 0; --i) {
-    const f64 mult = -col_dot_par(s.storage, s.r1_u[i], y) / s.r1_mu[i];
-    col_add_dense(s.storage, s.r1_v[i], mult, y);
-  }
+  r1_dense_steps(s, y, s.r1_count - 1, s.r1_count, true);
   s.r1_dtime += dt_ops(s.r1_num_entries);
 }
 SD_INLINE void r1_left_solve_nz(Lp& s, Vec& y) {
@@ -1079,14 +1178,13 @@ SD_INLINE void r1_left_solve_nz(Lp& s, Vec& y) {
   vec_repopulate_mask(y);
   bool use_dense = vec_dense(y, 0.05);
   for (int i = s.r1_count - 1; i >= 0; --i) {
-    if (use_dense) {
-      const f64 mult = -col_dot_par(s.storage, s.r1_u[i], y.values) / s.r1_mu[i];
-      col_add_dense(s.storage, s.r1_v[i], mult, y.values);
-    } else {
-      const f64 mult = -col_dot_par(s.storage, s.r1_u[i], y.values) / s.r1_mu[i];
-      if (mult != 0.0) col_add_scattered(s.storage, s.r1_v[i], mult, y);
-      use_dense = vec_dense(y, 0.05);
+    if (use_dense) {  // stays dense for the remaining updates
+      r1_dense_steps(s, y.values, i, i + 1, true);
+      break;
     }
+    const f64 mult = -col_dot_par(s.storage, s.r1_u[i], y.values) / s.r1_mu[i];
+    if (mult != 0.0) col_add_scattered(s.storage, s.r1_v[i], mult, y);
+    use_dense = vec_dense(y, 0.05);
   }
   vec_clear_mask(y);
   vec_clear_nz_if_too_dense(y, 0.05);
@@ -1114,7 +1212,7 @@ SD_INLINE void lu_left_solve_u_with_nz(Lp& s, Vec& y) {
   if (y.nnz == 0) {
     {
       SdSubTimer t_(&s.phase_ticks[10]);
-      tri_transpose_upper_solve(s.upper, y.values);
+      tri_transpose_upper_solve(s.upper, y.values, s.lds, s.lds_doubles);
     }
   } else {
     tri_transpose_hyper_solve(s.upper, y.values, y.nz, &y.nnz);

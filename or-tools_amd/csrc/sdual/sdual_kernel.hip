@@ -24,8 +24,16 @@ namespace {
 inline hipStream_t Stream(void* p) { return reinterpret_cast<hipStream_t>(p); }
 }  // namespace
 
+// Dynamic LDS of a segment workgroup: the staged dense vector of the
+// triangular sweeps (32 KB: five workgroups per CU keep the 1 024-group pool
+// resident).
+constexpr int kLdsDoubles = 4096;
+extern __shared__ double sd_lds[];
+
 // One thread walks Glop's loop; the header lives in the arena.
 __global__ __launch_bounds__(64) void sdual_segment_kernel(sdual::Lp* lp) {
+  lp->lds = sd_lds;
+  lp->lds_doubles = kLdsDoubles;
   sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
 }
 
@@ -155,6 +163,8 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring
     if (threadIdx.x == 0) pool_dbg(q, 2, 2);
     sdual::Lp* lp = reinterpret_cast<sdual::Lp*>(arena);
     lp->phase_ticks[13] += wall_clock64() - t_claim;  // staging image in
+    lp->lds = sd_lds;
+    lp->lds_doubles = kLdsDoubles;
     sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
     const uint64_t t_out = wall_clock64();
     if (threadIdx.x == 0) {
@@ -282,7 +292,7 @@ class SdualPool {
       throw DeviceError("sdual pool: ring reset failed");
     }
     __atomic_store_n(&q_->stop, 0, __ATOMIC_RELEASE);
-    hipLaunchKernelGGL(sdual_pool_kernel, dim3(kPoolGroups), dim3(64), 0, stream_, d_q_, d_ring_,
+    hipLaunchKernelGGL(sdual_pool_kernel, dim3(kPoolGroups), dim3(64), kLdsDoubles * sizeof(double), stream_, d_q_, d_ring_,
                        static_cast<long long>(head_base_));
     const hipError_t e = hipGetLastError();
     (void)hipSetDevice(prev);
@@ -466,7 +476,7 @@ void DeviceLp::SdualRun(size_t bytes, const double* arena_coeff, int n, void (*s
   Check(hipMemcpyAsync(sdual_arena_, sdual_staging_, bytes, hipMemcpyHostToDevice,
                        Stream(stream_)),
         "sdual H2D");
-  hipLaunchKernelGGL(sdual_segment_kernel, dim3(1), dim3(64), 0, Stream(stream_),
+  hipLaunchKernelGGL(sdual_segment_kernel, dim3(1), dim3(64), kLdsDoubles * sizeof(double), Stream(stream_),
                      reinterpret_cast<sdual::Lp*>(sdual_arena_));
   Check(hipGetLastError(), "sdual launch");
   // The segment's last update row becomes the device copy that later device

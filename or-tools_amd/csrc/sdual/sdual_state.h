@@ -315,6 +315,11 @@ struct Lp {
   f64* coeff_out;        // DeviceLp's update-row coefficients (N), refreshed at the end
   // Device time per loop phase (wall_clock64 ticks, 100 MHz): see sd_run.
   uint64_t phase_ticks[16];
+  // The workgroup's LDS scratch (set by the kernel before sd_run; null on the
+  // host): dense vectors of the triangular sweeps are staged there.
+  f64* lds;
+  int32_t lds_doubles;
+  int32_t lds_pad;
 
   // ---- loop carry and exit ----
   int refactorize;  // the host loop's `refactorize` flag
