@@ -4046,10 +4046,16 @@ Status RevisedSimplex::Initialize(const LinearProgram& lp) {
 // revised_simplex.cc:1663-1693
 void RevisedSimplex::CorrectErrorsOnVariableValues() {
   const Fractional primal_residual = variable_values_.ComputeMaximumPrimalResidual();
-  if (primal_residual >=
-      parameters_.harris_tolerance_ratio * parameters_.primal_feasibility_tolerance) {
-    variable_values_.RecomputeBasicVariableValues();
+  const bool recompute = primal_residual >= parameters_.harris_tolerance_ratio *
+                                                parameters_.primal_feasibility_tolerance;
+  if (const char* e = std::getenv("MILP_TRACE_RESIDUAL")) {  // debugging aid
+    if (FILE* f = std::fopen(e, "a")) {
+      std::fprintf(f, "it=%lld residual=%a recompute=%d\n", static_cast<long long>(num_iterations_),
+                   primal_residual, recompute ? 1 : 0);
+      std::fclose(f);
+    }
   }
+  if (recompute) variable_values_.RecomputeBasicVariableValues();
 }
 
 void RevisedSimplex::ComputeVariableValuesError() {

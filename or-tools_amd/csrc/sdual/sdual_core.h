@@ -673,6 +673,12 @@ SD_INLINE void tri_transpose_lower_solve(const Tri& t, f64* x, f64* lds = nullpt
   }
   for (int col = last; col >= end; --col) x[col] = tri_tl_column(t, x, col);
 }
+// A column's scatter over its (distinct) rows is split over the lanes.
+SD_INLINE void tri_scatter_column(const Tri& t, int col, f64 coeff, f64* x) {
+  for (int64_t i = t.starts[col] + sd_lane(); i < t.starts[col + 1]; i += sd_lanes())
+    x[t.rows[i]] -= coeff * t.coefs[i];
+  sd_sync();
+}
 SD_INLINE void tri_hyper_solve(const Tri& t, f64* x, int32_t* nz, int* nnz) {
   const bool ones = t.all_ones;
   int new_size = 0;
@@ -681,8 +687,7 @@ SD_INLINE void tri_hyper_solve(const Tri& t, f64* x, int32_t* nz, int* nnz) {
     if (x[row] == 0.0) continue;
     const f64 coeff = ones ? x[row] : x[row] / t.diag[row];
     x[row] = coeff;
-    for (int64_t i = t.starts[row]; i < t.starts[row + 1]; ++i)
-      x[t.rows[i]] -= coeff * t.coefs[i];
+    tri_scatter_column(t, row, coeff, x);
     nz[new_size++] = row;
   }
   *nnz = new_size;
@@ -700,8 +705,7 @@ SD_INLINE void tri_hyper_solve_rev(const Tri& t, f64* x, int32_t* nz, int* nnz) 
     if (x[row] == 0.0) continue;
     const f64 coeff = ones ? x[row] : x[row] / t.diag[row];
     x[row] = coeff;
-    for (int64_t i = t.starts[row]; i < t.starts[row + 1]; ++i)
-      x[t.rows[i]] -= coeff * t.coefs[i];
+    tri_scatter_column(t, row, coeff, x);
     nz[--new_start] = row;
   }
   erase_prefix(nz, nnz, new_start);
