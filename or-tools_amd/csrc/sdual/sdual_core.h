@@ -244,6 +244,62 @@ SD_INLINE void sort_ints(int32_t* a, int n) {
   }
 }
 
+// Sorts n distinct values of [0, range) in increasing order (the result of
+// any correct sort). flags: `range` bytes, zero on entry and on exit. On the
+// device: up to 128 values by rank (each lane counts the smaller values via
+// shuffles), more by marking the flags and compacting [0, range) in order
+// (ballot prefix counts, four 64-position chunks per round).
+SD_INLINE void sort_distinct(int32_t* a, int n, int range, char* flags) {
+  if (n < 2) return;
+#if defined(__HIP_DEVICE_COMPILE__)
+  sd_sync();  // the list and the flags were last written by every lane
+  const int lane = sd_lane();
+  if (n <= 128) {
+    const int32_t kNone = 0x7fffffff;
+    const int32_t v0 = lane < n ? a[lane] : kNone;
+    const int32_t v1 = lane + 64 < n ? a[lane + 64] : kNone;
+    int r0 = 0, r1 = 0;
+    for (int j = 0; j < 64; ++j) {
+      const int32_t x0 = __shfl(v0, j, 64), x1 = __shfl(v1, j, 64);
+      r0 += (x0 < v0) + (x1 < v0);
+      r1 += (x0 < v1) + (x1 < v1);
+    }
+    sd_sync();
+    if (lane < n) a[r0] = v0;
+    if (lane + 64 < n) a[r1] = v1;
+    sd_sync();
+    return;
+  }
+  for (int k = lane; k < n; k += 64) flags[a[k]] = 1;
+  sd_sync();
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int count = 0;
+  for (int base = 0; base < range; base += 256) {
+    bool f[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = base + 64 * u + lane;
+      f[u] = i < range && flags[i] != 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = base + 64 * u + lane;
+      const uint64_t m = __ballot(f[u]);
+      if (f[u]) {
+        a[count + __popcll(m & below)] = i;
+        flags[i] = 0;
+      }
+      count += __popcll(m);
+    }
+  }
+  sd_sync();
+#else
+  (void)range;
+  (void)flags;
+  sort_ints(a, n);
+#endif
+}
+
 // ---- ScatteredVector helpers (scattered_vector.h, lp_utils.h) ----
 SD_INLINE bool vec_dense(const Vec& v, f64 ratio) {
   if (v.nnz == 0) return true;
@@ -277,9 +333,9 @@ SD_INLINE void vec_add(Vec& v, int i, f64 value) {
     v.sorted = 0;
   }
 }
-SD_INLINE void vec_sort_if_needed(Vec& v) {
+SD_INLINE void vec_sort_if_needed(Vec& v, char* flags) {
   if (!v.sorted) {
-    sort_ints(v.nz, v.nnz);
+    sort_distinct(v.nz, v.nnz, v.size, flags);
     v.sorted = 1;
   }
 }
@@ -788,7 +844,7 @@ SD_INLINE void tri_rows_to_consider(const Tri& t, int32_t* nz, int* nnz, char* s
   if (num_ops > num_ops_threshold) {
     *nnz = 0;
   } else {
-    sort_ints(nz, *nnz);
+    sort_distinct(nz, *nnz, t.num_rows, stored);
   }
 }
 SD_INLINE int64_t tri_num_entries(const Tri& t) {
@@ -1205,7 +1261,7 @@ SD_INLINE void bf_right_solve(Lp& s, Vec& d) {
   lu_right_solve_l_with_nz(s, d);
   r1_right_solve_nz(s, d);
   lu_right_solve_u_with_nz(s, d);
-  vec_sort_if_needed(d);
+  vec_sort_if_needed(d, s.stored);
   bf_bump(s, vec_nnz_estimate(d));
 }
 // LeftSolveUWithNonZeros (lu_factorization.cc:298-312)
@@ -1227,7 +1283,7 @@ SD_INLINE void bf_left_solve(Lp& s, Vec& y) {
   lu_left_solve_u_with_nz(s, y);
   r1_left_solve_nz(s, y);
   lu_left_solve_l_with_nz(s, y, nullptr);
-  vec_sort_if_needed(y);
+  vec_sort_if_needed(y, s.stored);
   bf_bump(s, vec_nnz_estimate(y));
 }
 // LuFactorization::DualEdgeSquaredNorm (lu_factorization.cc:158-186) with
@@ -1305,7 +1361,7 @@ SD_INLINE void bf_left_solve_for_unit_row(Lp& s, int j, Vec& y) {
     lu_left_solve_l_with_nz(s, y, nullptr);
   }
   s.tau_is_computed = 0;
-  vec_sort_if_needed(y);
+  vec_sort_if_needed(y, s.stored);
   bf_bump(s, vec_nnz_estimate(y));
 }
 SD_INLINE void bf_right_solve_for_column(Lp& s, int col, Vec& d) {
@@ -1315,11 +1371,11 @@ SD_INLINE void bf_right_solve_for_column(Lp& s, int col, Vec& d) {
   if (d.nnz == 0) {
     s.right_pool[col] = store_add_dense_prefix(s.right_storage, d.values, d.size, 0);
   } else {
-    sort_ints(d.nz, d.nnz);
+    sort_distinct(d.nz, d.nnz, d.size, s.stored);
     s.right_pool[col] = store_add_dense_nz(s.right_storage, d.values, d.size, d.nz, d.nnz);
   }
   lu_right_solve_u_with_nz(s, d);
-  vec_sort_if_needed(d);
+  vec_sort_if_needed(d, s.stored);
   bf_bump(s, vec_nnz_estimate(d));
 }
 
@@ -1411,7 +1467,8 @@ SD_INLINE void dp_clear_and_resize(Lp& s, int n) {
   for (int i = s.dp_size; i < n; ++i) s.dp_values[i] = 0.0;
   s.dp_size = n;
   const int words = (n + 63) / 64;
-  for (int w = 0; w < words; ++w) s.dp_cand[w] = 0;
+  for (int w = sd_lane(); w < words; w += sd_lanes()) s.dp_cand[w] = 0;
+  sd_sync();
 }
 SD_INLINE void dp_start_dense_updates(Lp& s) {
   s.dp_ntops = 0;
@@ -1511,6 +1568,24 @@ SD_INLINE void vv_recompute_dual_prices(Lp& s, int put_more_importance_on_norm) 
   s.put_more_importance_on_norm = put_more_importance_on_norm;
   const f64 tol = s.primal_feasibility_tolerance;
   norms_get(s);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // Row chunk c is candidate word c (cleared above): its bits are the ballot.
+  for (int base = 0; base < s.m; base += 64) {
+    const int row = base + sd_lane();
+    bool keep = false;
+    if (row < s.m) {
+      const f64 inf = row_infeasibility(s, s.basis[row]);
+      if (inf > tol) {
+        keep = true;
+        s.dp_values[row] = s.put_more_importance_on_norm ? sd_fabs(inf) / s.norms[row]
+                                                         : sq(inf) / s.norms[row];
+      }
+    }
+    const uint64_t word = __ballot(keep);
+    if (sd_lane() == 0) s.dp_cand[base >> 6] = word;
+  }
+  sd_sync();
+#else
   for (int row = 0; row < s.m; ++row) {
     const int col = s.basis[row];
     const f64 inf = row_infeasibility(s, col);
@@ -1520,6 +1595,7 @@ SD_INLINE void vv_recompute_dual_prices(Lp& s, int put_more_importance_on_norm) 
                                          : sq(inf) / s.norms[row]);
     }
   }
+#endif
 }
 SD_INLINE void vv_update_dual_price(Lp& s, int row) {
   const int col = s.basis[row];
@@ -1538,7 +1614,45 @@ SD_INLINE void vv_update_dual_prices(Lp& s, const int32_t* rows, int n) {
     return;
   }
   norms_get(s);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // 64 rows at a time: the prices, values and candidate bits on the lanes
+  // (distinct rows; words shared by lanes take atomic or/and), then the rows
+  // that can enter the top-k (price >= the threshold at the chunk's start:
+  // the threshold never decreases) replay dp_update_top_k in list order.
+  const int lane = sd_lane();
+  const f64 tol = s.primal_feasibility_tolerance;
+  for (int base = 0; base < n; base += 64) {
+    const int k = base + lane;
+    int row = 0;
+    f64 price = 0.0;
+    bool cand = false;
+    if (k < n) {
+      row = rows[k];
+      const f64 inf = row_infeasibility(s, s.basis[row]);
+      unsigned long long* word = reinterpret_cast<unsigned long long*>(s.dp_cand + (row >> 6));
+      const unsigned long long bit = 1ull << (row & 63);
+      if (inf > tol) {
+        price = s.put_more_importance_on_norm ? sd_fabs(inf) / s.norms[row] : sq(inf) / s.norms[row];
+        s.dp_values[row] = price;
+        atomicOr(word, bit);
+        cand = price >= s.dp_threshold;
+      } else {
+        atomicAnd(word, ~bit);
+      }
+    }
+    uint64_t mask = __ballot(cand);
+    while (mask != 0) {
+      const int l = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const int r = __shfl(row, l, 64);
+      const f64 p = __shfl(price, l, 64);
+      if (p >= s.dp_threshold) dp_update_top_k(s, r, p);
+    }
+  }
+  sd_sync();
+#else
   for (int k = 0; k < n; ++k) vv_update_dual_price(s, rows[k]);
+#endif
 }
 SD_INLINE void vv_set_nonbasic_from_status(Lp& s, int col) {
   switch (s.vstatus[col]) {

@@ -318,6 +318,7 @@ namespace {
 struct GapSum {
   std::atomic<int64_t> total_ns{0}, last_ns{0}, max_ns{0}, polls{0}, segments{0};
   ~GapSum() {
+    if (std::getenv("MILP_SDUAL_PROFILE") == nullptr) return;
     std::fprintf(stderr,
                  "  host fiber polls %lld, away %.1f us total, max %.1f us; last gap %.1f us "
                  "over %lld segments\n",
