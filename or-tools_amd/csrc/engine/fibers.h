@@ -77,8 +77,9 @@ inline void FiberYield(bool idle = false) {
 
 // Runs every task as a fiber on the calling thread, round robin at the
 // yields, until all have returned. Tasks must not throw (RunSolve catches).
-// After two rounds in which every fiber only polled, the thread sleeps ~20 us
-// per round instead of spinning (CPU quota stays with the threads that work).
+// After two rounds in which every fiber only polled the thread yields its CPU
+// between rounds; after 4 096 such rounds (a long device wait) it sleeps ~20 us
+// per round, so the CPU quota stays with the threads that work.
 inline void RunFibers(std::vector<std::function<void()>> tasks, size_t stack_bytes = 4u << 20) {
   using namespace fiber_detail;
   if (tasks.size() == 1) {  // nothing to interleave
@@ -137,7 +138,11 @@ inline void RunFibers(std::vector<std::function<void()>> tasks, size_t stack_byt
       if (f->done) --remaining;
     }
     idle_rounds = all_idle ? idle_rounds + 1 : 0;
-    if (idle_rounds >= 2) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    if (idle_rounds >= 4096) {
+      std::this_thread::sleep_for(std::chrono::microseconds(20));  // long device waits
+    } else if (idle_rounds >= 2) {
+      std::this_thread::yield();
+    }
   }
   t_sched_sp = saved_sched;
   t_current = saved_current;
