@@ -827,6 +827,40 @@ SD_INLINE void tri_rows_to_consider(const Tri& t, int32_t* nz, int* nnz, char* s
     *nnz = 0;
     return;
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // A column's entries (distinct rows) on the lanes; its new rows join the
+  // list in entry order (ballot prefix counts), as the sequential loop appends.
+  const int lane = sd_lane();
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int n = *nnz;
+  for (int k = lane; k < n; k += 64) stored[nz[k]] = 1;
+  sd_sync();
+  for (int k = 0; k < n; ++k) {
+    const int row = nz[k];
+    const int64_t b = t.starts[row], e = t.starts[row + 1];
+    for (int64_t base = b; base < e; base += 64) {
+      const int64_t i = base + lane;
+      bool fresh = false;
+      int er = 0;
+      if (i < e) {
+        er = t.rows[i];
+        fresh = !stored[er];
+      }
+      const uint64_t m = __ballot(fresh);
+      if (fresh) {
+        nz[n + __popcll(m & below)] = er;
+        stored[er] = 1;
+      }
+      n += __popcll(m);
+    }
+    num_ops += static_cast<int>(e - b);
+    sd_sync();
+    if (num_ops > num_ops_threshold) break;
+  }
+  *nnz = n;
+  for (int k = lane; k < n; k += 64) stored[nz[k]] = 0;
+  sd_sync();
+#else
   for (int k = 0; k < *nnz; ++k) stored[nz[k]] = 1;
   for (int k = 0; k < *nnz; ++k) {
     const int row = nz[k];
@@ -841,6 +875,7 @@ SD_INLINE void tri_rows_to_consider(const Tri& t, int32_t* nz, int* nnz, char* s
     if (num_ops > num_ops_threshold) break;
   }
   for (int k = 0; k < *nnz; ++k) stored[nz[k]] = 0;
+#endif
   if (num_ops > num_ops_threshold) {
     *nnz = 0;
   } else {
