@@ -329,6 +329,7 @@ def run_c3(args, rank, world, local_rank, dist, barrier, sync):
                      f"m 27..{args.c3_max_rows}, 1.5-4 columns per row, all bound types), "
                      f"primal simplex, Glop defaults, solved from scratch"),
     }
+    out["roofline"] = batched_roofline(handles)
     for h in handles:
         h.close()
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -349,6 +350,35 @@ def run_c3(args, rank, world, local_rank, dist, barrier, sync):
             "kind": "port",
             "sample": f"oracle, {args.c3_cpu_threads} threads, the same {len(suite)} LPs"}
     return out
+
+
+def batched_roofline(handles):
+    """Roofline of the batch's dominant kernel kind, summed over the handles
+    of the timed batch: algorithmic bytes (the engine's per-kind formulas,
+    DESIGN.md section 4) over that kind's measured time. Kinds launched in
+    batched form are timed by their callers' waits (call_ms, which includes
+    queueing: a lower bound on the achieved bandwidth) when no device time was
+    recorded."""
+    try:
+        agg = {}
+        for h in handles:
+            for k, v in h.kernel_stats().items():
+                a = agg.setdefault(k, {"launches": 0, "bytes": 0.0, "device_ms": 0.0, "call_ms": 0.0})
+                for f in a:
+                    a[f] += v[f]
+        kind, a = max(agg.items(), key=lambda kv: max(kv[1]["device_ms"], kv[1]["call_ms"]))
+        timed_ms = a["device_ms"] if a["device_ms"] > 0 else a["call_ms"]
+        if a["launches"] == 0 or timed_ms <= 0:
+            return None
+        achieved = a["bytes"] / (timed_ms * 1e-3) / 1e9
+        return {"kernel": kind, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "launches": int(a["launches"]), "bytes_per_launch": a["bytes"] / a["launches"],
+                "ms_per_launch": timed_ms / a["launches"],
+                "timing": "device" if a["device_ms"] > 0 else "call"}
+    except Exception as e:  # the roofline is a report, never a reason to fail the bench
+        log(f"batched roofline unavailable: {e}")
+        return None
 
 
 def run_batched(args, rank, world, local_rank, dist, barrier, sync):
@@ -385,6 +415,8 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
         w.load(lp)
     # Warm-up batch (not timed): first-touch allocations on every worker.
     engine.batch_solve_bounds(workers, lbs[:args.batch_workers], ubs[:args.batch_workers], state)
+    for w in workers:
+        w.reset_kernel_stats()
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -409,6 +441,7 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
                      f"branches, dual simplex warm-started from the node basis, cap 1000 "
                      f"iterations"),
     }
+    out["roofline"] = batched_roofline(workers)
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_lib
         ows = [oracle_lib.OracleLp(p) for _ in range(args.batch_cpu_threads)]
