@@ -366,7 +366,10 @@ def batched_roofline(handles):
                 a = agg.setdefault(k, {"launches": 0, "bytes": 0.0, "device_ms": 0.0, "call_ms": 0.0})
                 for f in a:
                     a[f] += v[f]
-        kind, a = max(agg.items(), key=lambda kv: max(kv[1]["device_ms"], kv[1]["call_ms"]))
+        timed = {k: a for k, a in agg.items() if a["launches"] > 0 and a["bytes"] > 0}
+        if not timed:
+            return None
+        kind, a = max(timed.items(), key=lambda kv: max(kv[1]["device_ms"], kv[1]["call_ms"]))
         timed_ms = a["device_ms"] if a["device_ms"] > 0 else a["call_ms"]
         if a["launches"] == 0 or timed_ms <= 0:
             return None
@@ -492,7 +495,7 @@ def main():
                          "separate rocprofv3 --pmc pass (profiles/)")
     ap.add_argument("--batch-lps", type=int, default=1024,
                     help="config-4 branch LPs per GPU (0 disables the batched section)")
-    ap.add_argument("--batch-workers", type=int, default=256,
+    ap.add_argument("--batch-workers", type=int, default=1024,
                     help="config-4 solver handles per GPU (LPs in flight); the engine runs "
                          "them on at most 16 host threads as fibers with batched launches")
     ap.add_argument("--batch-cpu-threads", type=int, default=16)
