@@ -495,7 +495,7 @@ def main():
                          "separate rocprofv3 --pmc pass (profiles/)")
     ap.add_argument("--batch-lps", type=int, default=1024,
                     help="config-4 branch LPs per GPU (0 disables the batched section)")
-    ap.add_argument("--batch-workers", type=int, default=256,
+    ap.add_argument("--batch-workers", type=int, default=1024,
                     help="config-4 solver handles per GPU (LPs in flight); the engine runs "
                          "them on at most 16 host threads as fibers with batched launches")
     ap.add_argument("--batch-cpu-threads", type=int, default=16)

@@ -3321,14 +3321,13 @@ class RevisedSimplex {
   int RunSdualSegment(TimeLimit* tl, bool* refactorize, Status* status);
 
  public:
-  // MILP_SDUAL=device: the batch APIs run the phase-II dual loop of their
-  // LPs as device segments (one workgroup per LP, csrc/sdual).
-  // Off by default this round: the full GPU suite has not yet run with it as
-  // the default.
+  // The batch APIs run the phase-II dual loop of their LPs as device
+  // segments (one workgroup per LP, csrc/sdual);
+  // MILP_SDUAL=off keeps the batched-launch path.
   void SetBatchMode(bool on) {
     const int batch_mode = [] {  // read per batch call (tests switch it)
       const char* e = std::getenv("MILP_SDUAL");
-      if (e == nullptr) return 0;
+      if (e == nullptr) return 2;
       if (std::strcmp(e, "host") == 0) return 1;
       if (std::strcmp(e, "device") == 0 || std::strcmp(e, "on") == 0) return 2;
       return 0;
