@@ -1,13 +1,15 @@
 #!/bin/bash
-# Round 3: sdual GPU tests, the config-4 probe through the device segments, and
-# the default bench (bench2.json).
+# Round 3, last check of the committed tree: the whole GPU suite, smoke() and the
+# default bench, each under its own time limit; stops at the first failure.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-mkdir -p $R/gpurun_out/r03_final
-timeout -k 10 300 python3 -u -m pytest $R/tests/test_sdual_gpu.py -x -q --timeout 120 \
-  --timeout-method thread > $R/gpurun_out/r03_final/sdual_tests.log 2>&1
-rc=$?; tail -1 $R/gpurun_out/r03_final/sdual_tests.log; [ $rc -eq 0 ] || exit $rc
-WS=1024 bash $R/scripts/gpu_r03_c4scale.sh || exit 1
-timeout -k 10 800 python3 -u $R/bench.py > $R/gpurun_out/r03_final/bench2.json \
-  2> $R/gpurun_out/r03_final/bench2.log
-echo "bench rc=$?"
+O=$R/gpurun_out/r03_last
+mkdir -p $O
+timeout -k 10 660 python3 -u -m pytest $R/tests -m gpu -x -q --timeout 200 --timeout-method thread \
+  > $O/gpu_tests.log 2>&1
+rc=$?; tail -1 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 180 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
+  > $O/smoke.log 2>&1
+rc=$?; tail -1 $O/smoke.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -u $R/bench.py > $O/bench.json 2> $O/bench.log
+rc=$?; echo "bench rc=$rc"; exit $rc
