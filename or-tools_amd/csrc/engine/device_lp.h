@@ -27,6 +27,9 @@ struct Mailbox;
 namespace milp {
 // Zeroes the MILP_SDUAL_PROFILE host counters (sdual_kernel.hip).
 void SdualProfileReset();
+// A batch call on `device` starts (begin) or ends using the device's segment
+// pool; when the last one ends, the resident pool grid is told to stop.
+void SdualPoolScope(int device, bool begin);
 
 class CompactSparseMatrix;
 

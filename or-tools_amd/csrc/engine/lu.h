@@ -9,6 +9,7 @@
 
 #include <cstdint>
 #include <functional>
+#include <cstring>
 #include <memory>
 #include <string>
 
@@ -16,6 +17,22 @@
 #include "lp_data.h"
 
 namespace milp {
+
+// Debug aid (MILP_TRACE): bit-hashes of the last problem-column FTRAN's
+// stages (after L, after the rank-one etas, after U), printed with the
+// per-iteration trace line so engine and oracle divergences can be located.
+inline bool g_trace_ftran = false;
+inline uint64_t g_ftran_hash[3] = {0, 0, 0};
+inline uint64_t TraceHashVector(const std::vector<Fractional>& v, const std::vector<int>& nz) {
+  uint64_t h = 1469598103934665603ull;
+  for (const Fractional x : v) {
+    uint64_t b;
+    std::memcpy(&b, &x, sizeof(b));
+    h = (h ^ b) * 1099511628211ull;
+  }
+  for (const int r : nz) h = (h ^ static_cast<uint32_t>(r)) * 1099511628211ull;
+  return h;
+}
 
 // Which copy of the solve scratch a thread uses: 0 on the solver's thread,
 // 1 on BasisFactorization's tau worker (the two run FTRANs concurrently).

@@ -3206,13 +3206,20 @@ class RevisedSimplex {
     const std::string path = std::string(prefix) + ".device";
     FILE* f = std::fopen(path.c_str(), "a");
     if (f == nullptr) return;
-    std::fprintf(f, "it=%lld phase=%d basis=%016llx x=%016llx rc=%016llx se=%016llx obj=%a\n",
+    std::fprintf(f, "it=%lld phase=%d basis=%016llx x=%016llx rc=%016llx se=%016llx obj=%a"
+                 " ent=%d lr=%d step=%a rcq=%a d=%016llx/%016llx/%016llx\n",
                  static_cast<long long>(num_iterations_), static_cast<int>(phase_),
                  static_cast<unsigned long long>(HashInts(basis_)),
                  static_cast<unsigned long long>(HashBits(variable_values_.GetDenseRow())),
                  static_cast<unsigned long long>(HashBits(reduced_costs_.RawReducedCosts())),
                  static_cast<unsigned long long>(HashBits(primal_edge_norms_.RawEdgeNorms())),
-                 ComputeObjectiveValue());
+                 ComputeObjectiveValue(), trace_entering_, trace_leaving_row_, trace_step_,
+                 trace_reduced_cost_, static_cast<unsigned long long>(g_ftran_hash[0]),
+                 static_cast<unsigned long long>(g_ftran_hash[1]),
+                 static_cast<unsigned long long>(g_ftran_hash[2]));
+    trace_entering_ = trace_leaving_row_ = -1;
+    trace_step_ = trace_reduced_cost_ = 0.0;
+    g_ftran_hash[0] = g_ftran_hash[1] = g_ftran_hash[2] = 0;
     // MILP_TRACE_DUMP=k: raw x, rc and basis at iterations k-1 and k.
     static const char* dump = std::getenv("MILP_TRACE_DUMP");
     if (dump != nullptr && num_iterations_ + 1 >= std::atoll(dump) &&
@@ -3230,6 +3237,7 @@ class RevisedSimplex {
       put("x", variable_values_.GetDenseRow().data(), sizeof(Fractional) * num_cols_);
       put("rc", reduced_costs_.RawReducedCosts().data(), sizeof(Fractional) * num_cols_);
       put("basis", basis_.data(), sizeof(int) * num_rows_);
+      put("d", direction_.values.data(), sizeof(Fractional) * direction_.values.size());
     }
     if (num_cols_ <= 64) {
       const std::vector<Fractional>* vs[3] = {&variable_values_.GetDenseRow(),
@@ -3244,6 +3252,10 @@ class RevisedSimplex {
     }
     std::fclose(f);
   }
+  int trace_entering_ = -1;
+  int trace_leaving_row_ = -1;
+  Fractional trace_step_ = 0.0;
+  Fractional trace_reduced_cost_ = 0.0;
   void OnIterationDone(TimeLimit* tl) {
     TraceIteration();
     ++num_iterations_;
@@ -3313,6 +3325,7 @@ class RevisedSimplex {
   // restatement compiled for the CPU, a debugging aid), 2 on the device.
   int sdual_mode_ = 0;
   int saved_sdual_mode_ = 0;
+  int batch_depth_ = 0;
   std::vector<char> sdual_buffer_;
   int64_t sdual_segments_ = 0;
   int64_t sdual_iterations_ = 0;
@@ -3336,14 +3349,20 @@ class RevisedSimplex {
       const char* e = std::getenv("MILP_SDUAL_HOSTOPS");
       return e == nullptr || std::atoi(e) != 0;
     }();
+    // A handle may be passed more than once to one batch call: only the
+    // outermost on/off pair saves and restores the mode.
     if (on) {
-      saved_sdual_mode_ = sdual_mode_;
-      sdual_mode_ = batch_mode;
-    } else {
+      if (batch_depth_++ == 0) {
+        saved_sdual_mode_ = sdual_mode_;
+        sdual_mode_ = batch_mode;
+      }
+    } else if (batch_depth_ > 0 && --batch_depth_ == 0) {
       sdual_mode_ = saved_sdual_mode_;
     }
-    device_.SetHostSmallOps(on && sdual_mode_ == 2 && host_ops);
+    device_.SetHostSmallOps(batch_depth_ > 0 && sdual_mode_ == 2 && host_ops);
   }
+  // Whether this handle's batch solves use the device's segment pool.
+  bool UsesSdualPool() const { return batch_depth_ > 0 && sdual_mode_ == 2; }
   void SdualCounters(int64_t* segments, int64_t* iterations) const {
     *segments = sdual_segments_;
     *iterations = sdual_iterations_;
@@ -4551,6 +4570,7 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
     int64_t first;
     ~DumpAtExit() { c->Dump(static_cast<long long>(*it - first)); }
   } dump{&clock, &num_iterations_, first_iteration};
+  g_trace_ftran = std::getenv("MILP_TRACE") != nullptr;
   bool refactorize = false;
   primal_prices_.ForceRecomputation();
   if (phase_ == Phase::FEASIBILITY) {
@@ -4669,6 +4689,10 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
     if (phase_ == Phase::FEASIBILITY && leaving_row != kInvalidRow) {
       step = ComputeStepToMoveBasicVariableToBound(leaving_row, target_bound);
     }
+    trace_entering_ = entering_col;
+    trace_leaving_row_ = leaving_row;
+    trace_step_ = step;
+    trace_reduced_cost_ = reduced_cost;
     const int leaving_col = (leaving_row == kInvalidRow) ? kInvalidCol : basis_[leaving_row];
     bool is_degenerate = false;
     if (leaving_row != kInvalidRow) {
@@ -5917,6 +5941,32 @@ void SetSmallBatchSafe(mi_lp* h, bool on) {
     h->error = e.what();
   }
 }
+// The devices whose segment pool a batch call uses: when the last batch
+// call on a device ends, its resident pool grid is told to stop.
+struct PoolScope {
+  std::vector<int> devices;
+  PoolScope(mi_lp* const* hs, int count) {
+    for (int i = 0; i < count; ++i) {
+      if (!hs[i]->simplex.UsesSdualPool()) continue;
+      const int d = hs[i]->device;
+      if (std::find(devices.begin(), devices.end(), d) != devices.end()) continue;
+      devices.push_back(d);
+      try {
+        milp::SdualPoolScope(d, true);
+      } catch (const std::exception&) {
+        devices.pop_back();  // the segment itself reports the device error
+      }
+    }
+  }
+  ~PoolScope() {
+    for (const int d : devices) {
+      try {
+        milp::SdualPoolScope(d, false);
+      } catch (const std::exception&) {
+      }
+    }
+  }
+};
 }  // namespace
 
 extern "C" {
@@ -5939,6 +5989,7 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
     handles[i]->simplex.SetBatchMode(true);
     handles[i]->simplex.device().SetSmallBatch(true);
   }
+  PoolScope pool_scope(handles, count);
   // Largest LPs first (LPT order, weight (nnz + m) * m as in the multi-GPU
   // partition of mi_glop.distributed): the long solves start early instead of
   // forming the tail of the batch.
@@ -6013,6 +6064,7 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
     workers[w]->simplex.SetBatchMode(true);
     workers[w]->simplex.device().SetSmallBatch(true);
   }
+  PoolScope pool_scope(workers, num_workers);
   std::atomic<int> next(0);
   auto worker_loop = [&](mi_lp* h) {
     (void)hipSetDevice(h->device);

@@ -46,9 +46,23 @@ __global__ __launch_bounds__(64) void sdual_segment_kernel(sdual::Lp* lp) {
 // staging image in, run its segment, move it out and raise the LP's mailbox
 // flag to 3. The dispatcher stops on the stop word or after kIdleSpins polls
 // without work; the workers follow, so the grid always drains.
+//
+// Both queues are rings of `cap` slots (kCap, or less for the wrap-around
+// test: MILP_SDUAL_QUEUE_CAP) indexed by a running count:
+//  * the host publishes entry t into q->entry[t % cap] only while
+//    t - q->seen < cap, i.e. the dispatcher has copied the slot's previous
+//    occupant;
+//  * the dispatcher republishes entry k into ring->entry[k % cap] only when
+//    the slot's previous occupant (k - cap) was read: ring->ack[slot] holds
+//    the last index read from the slot + 1 (slots last used by an earlier
+//    grid are free: that grid read everything it republished before it quit);
+//  * a worker that claimed index idx reads it once ring->tail > idx.
+// A grid that drained leaves q->seen behind: the next launch starts there, so
+// an entry published while the old grid was quitting is served, once.
 struct SdQueue {
   static constexpr int kCap = 1 << 14;
-  int64_t tail;  // entries [0, tail) published
+  int64_t tail;  // entries [0, tail) published (host)
+  int64_t seen;  // entries [0, seen) copied into the device ring (dispatcher)
   int32_t stop;
   int32_t pad;
   int64_t dbg[8];  // MILP_SDUAL_DEBUG progress words
@@ -63,6 +77,7 @@ struct SdRing {
   int quit;
   int pad;
   uint64_t entry[SdQueue::kCap];
+  long long ack[SdQueue::kCap];  // per slot: last index read from it + 1
 };
 constexpr int kPoolGroups = 1024;
 constexpr int64_t kIdleSpins = 1 << 20;  // ~4 s of dispatcher polls
@@ -88,10 +103,12 @@ __device__ inline void team_copy_store_prefix(const sdual::Store& st, const char
 }
 
 __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring,
-                                                        long long head_base) {
+                                                        long long head_base, long long cap) {
   if (blockIdx.x == 0) {
     if (threadIdx.x != 0) return;
     long long seen = head_base;
+    __hip_atomic_store(&q->seen, static_cast<int64_t>(seen), __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
     int64_t idle = 0;
     while (true) {
       // Relaxed polls bypass the caches for the polled word only; the acquire
@@ -100,14 +117,26 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring
           __hip_atomic_load(&q->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
       if (t > seen) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        for (long long k = seen; k < t; ++k) {
-          ring->entry[k % SdQueue::kCap] = __hip_atomic_load(
-              &q->entry[k % SdQueue::kCap], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        long long k = seen;
+        for (; k < t; ++k) {
+          const long long slot = k % cap;
+          // The slot's previous occupant must have been read (see above).
+          if (k - cap >= head_base &&
+              __hip_atomic_load(&ring->ack[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                  k - cap + 1) {
+            break;
+          }
+          ring->entry[slot] = __hip_atomic_load(&q->entry[slot], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        __hip_atomic_store(&ring->tail, t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        seen = t;
-        idle = 0;
-        pool_dbg(q, 0, seen);
+        if (k > seen) {
+          __hip_atomic_store(&ring->tail, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          seen = k;
+          __hip_atomic_store(&q->seen, static_cast<int64_t>(seen), __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+          pool_dbg(q, 0, seen);
+        }
+        idle = 0;  // entries wait (a full ring waits for the workers)
       } else if (__hip_atomic_load(&q->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
                  ++idle > kIdleSpins) {
         __hip_atomic_store(&ring->quit, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -126,8 +155,11 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring
         if (static_cast<long long>(idx) <
             __hip_atomic_load(&ring->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          entry_shared = __hip_atomic_load(&ring->entry[idx % SdQueue::kCap], __ATOMIC_RELAXED,
+          const long long slot = static_cast<long long>(idx) % cap;
+          entry_shared = __hip_atomic_load(&ring->entry[slot], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ring->ack[slot], static_cast<long long>(idx) + 1, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_AGENT);
           pool_dbg(q, 1, static_cast<int64_t>(idx) + 1);
           pool_dbg(q, 2, 1);
           break;
@@ -235,17 +267,27 @@ class SdualPool {
     if ((*all)[device] == nullptr) (*all)[device] = new SdualPool(device);
     return *(*all)[device];
   }
-  // Publishes one arena; (re)launches the kernel when it is not running.
+  // Publishes one arena; (re)launches the kernel when it is not running. A
+  // full host ring (kCap entries the dispatcher has not copied yet) waits.
   void Enqueue(void* lp) {
-    std::lock_guard<std::mutex> lock(mu_);
-    if (!running_ || hipStreamQuery(stream_) == hipSuccess) Launch();
-    const int64_t t = q_->tail;
-    if (t - head_base_ >= SdQueue::kCap) {
-      throw DeviceError("sdual pool: queue full");
+    while (true) {
+      {
+        std::lock_guard<std::mutex> lock(mu_);
+        if (!running_ || hipStreamQuery(stream_) == hipSuccess) Launch();
+        const int64_t t = q_->tail;
+        if (t - __atomic_load_n(&q_->seen, __ATOMIC_ACQUIRE) < cap_) {
+          __atomic_store_n(&q_->entry[t % cap_], reinterpret_cast<uint64_t>(lp),
+                           __ATOMIC_RELEASE);
+          __atomic_store_n(&q_->tail, t + 1, __ATOMIC_RELEASE);
+          return;
+        }
+      }
+      if (InFiber()) {
+        FiberYield(false);
+      } else {
+        std::this_thread::yield();
+      }
     }
-    __atomic_store_n(&q_->entry[t % SdQueue::kCap], reinterpret_cast<uint64_t>(lp),
-                     __ATOMIC_RELEASE);
-    __atomic_store_n(&q_->tail, t + 1, __ATOMIC_RELEASE);
   }
   int64_t Tail() const { return q_->tail; }
   const int64_t* Dbg() const { return q_->dbg; }
@@ -253,6 +295,24 @@ class SdualPool {
   bool Alive() {
     std::lock_guard<std::mutex> lock(mu_);
     return running_ && hipStreamQuery(stream_) == hipErrorNotReady;
+  }
+  // A published entry waits for a grid: relaunch one if the last drained
+  // (idle limit or stop word) before copying it. The new grid starts at the
+  // old one's seen, so the entry is served once.
+  void EnsureRunning() {
+    std::lock_guard<std::mutex> lock(mu_);
+    if (!running_ || hipStreamQuery(stream_) == hipSuccess) Launch();
+  }
+  // The batch calls in progress on this device (BatchScope): the last one to
+  // end raises the stop word, so the resident grid leaves the CUs to single
+  // solves instead of spinning out its idle limit.
+  void Acquire() {
+    std::lock_guard<std::mutex> lock(mu_);
+    if (users_++ == 0) __atomic_store_n(&q_->stop, 0, __ATOMIC_RELEASE);
+  }
+  void Release() {
+    std::lock_guard<std::mutex> lock(mu_);
+    if (--users_ == 0 && running_) __atomic_store_n(&q_->stop, 1, __ATOMIC_RELEASE);
   }
 
  private:
@@ -271,16 +331,23 @@ class SdualPool {
       throw DeviceError("sdual pool: allocation failed");
     }
     std::memset(q_, 0, sizeof(SdQueue));
+    if (hipMemset(d_ring_, 0, sizeof(SdRing)) != hipSuccess) {
+      (void)hipSetDevice(prev);
+      throw DeviceError("sdual pool: ring clear failed");
+    }
+    if (const char* e = std::getenv("MILP_SDUAL_QUEUE_CAP")) {  // wrap-around tests
+      cap_ = std::max<int64_t>(2, std::min<int64_t>(SdQueue::kCap, std::atoll(e)));
+    }
     (void)hipSetDevice(prev);
   }
-  // Called with mu_ held and the previous grid (if any) drained: the queue
-  // restarts at the current tail.
+  // Called with mu_ held: waits for the previous grid (if any) to drain; the
+  // new one starts at the first entry the old dispatcher did not copy.
   void Launch() {
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(device_);
     if (running_) (void)hipStreamSynchronize(stream_);
-    head_base_ = q_->tail;
+    head_base_ = __atomic_load_n(&q_->seen, __ATOMIC_ACQUIRE);
     // The grid claims queue indices from head_base_ on (a synchronous copy:
     // the launch below must see it).
     std::memset(h_ring_, 0, offsetof(SdRing, entry));
@@ -293,7 +360,7 @@ class SdualPool {
     }
     __atomic_store_n(&q_->stop, 0, __ATOMIC_RELEASE);
     hipLaunchKernelGGL(sdual_pool_kernel, dim3(kPoolGroups), dim3(64), kLdsDoubles * sizeof(double), stream_, d_q_, d_ring_,
-                       static_cast<long long>(head_base_));
+                       static_cast<long long>(head_base_), static_cast<long long>(cap_));
     const hipError_t e = hipGetLastError();
     (void)hipSetDevice(prev);
     if (e != hipSuccess) throw DeviceError("sdual pool: launch failed");
@@ -309,8 +376,19 @@ class SdualPool {
   hipStream_t stream_ = nullptr;
   bool running_ = false;
   int64_t head_base_ = 0;
+  int64_t cap_ = SdQueue::kCap;
+  int users_ = 0;
 };
 }  // namespace
+
+void SdualPoolScope(int device, bool begin) {
+  SdualPool& pool = SdualPool::Get(device);
+  if (begin) {
+    pool.Acquire();
+  } else {
+    pool.Release();
+  }
+}
 
 // MILP_SDUAL_PROFILE: reallocations of the arena / mailbox and their time.
 namespace {
@@ -686,10 +764,10 @@ void DeviceLp::SdualRunPooled(size_t bytes, const double* arena_coeff, int n,
       idle = false;
       continue;
     }
-    if ((++polls & 1023) == 0 && !pool.Alive() && __atomic_load_n(flag, __ATOMIC_ACQUIRE) == 0) {
-      // The grid drained (idle limit) before claiming this entry: publish it
-      // again on a new grid.
-      pool.Enqueue(sdual_staging_dev_);
+    if ((++polls & 1023) == 0 && __atomic_load_n(flag, __ATOMIC_ACQUIRE) == 0) {
+      // The grid may have drained (idle limit, stop word) before copying this
+      // entry: a new grid starts from the first uncopied entry.
+      pool.EnsureRunning();
     }
     const auto y0 = prof ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
     if (InFiber()) {

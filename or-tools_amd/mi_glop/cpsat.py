@@ -11,7 +11,12 @@ CPU oracle):
 * AnalyzeLp (:762-860): a DUAL_UNBOUNDED LP is a conflict; an OPTIMAL or
   DUAL_FEASIBLE one pushes the objective lower bound ceil(obj - kCpEpsilon)
   and the reduced-cost strengthening deductions (:2367-2408).
-* UpdateSimplexIterationLimit (:1665-1695) for linearization level 2.
+* CalculateDegeneracy (:2351-2365) and UpdateSimplexIterationLimit
+  (:1665-1695) for linearization level 2; Propagate (:1697-1806): the root
+  cap root_lp_iterations = 2000 (sat_parameters.proto:899) at level 0, else
+  next_simplex_iter_, then SolveLp and AnalyzeLp. Cut generation and the
+  constraint manager's LP changes are CP-SAT search, out of scope: with no
+  cut generators ChangeLp adds nothing, so one round ends the loop.
 * BranchOnVar (:485-584) with SolveLpForBranching (:443-464): both branches of
   a fractional variable solved from the node's basis state, deductions from
   infeasible branches, the node's objective bound from the two branch bounds.
@@ -29,15 +34,22 @@ Bounds are plain floats (the CP integer bounds); the LP carries the CP
 variables unscaled, so the scaler's factors (scaler_.VariableScalingFactor)
 are 1 and the objective scaling factor is the LP's obj_scale.
 """
+import ctypes
 import math
 
 import numpy as np
 
 from . import abi
 
+
+def ctypes_copy(dst, src):
+    ctypes.memmove(ctypes.addressof(dst), ctypes.addressof(src), ctypes.sizeof(src))
+
 K_CP_EPSILON = 1e-4  # linear_programming_constraint.h:407
 K_LP_EPSILON = 1e-6  # linear_programming_constraint.h:410
 KEEP_STATUSES = (abi.OPTIMAL, abi.DUAL_FEASIBLE)
+ROOT_LP_ITERATIONS = 2000  # sat_parameters.proto:899
+BASIC = 0  # glop::VariableStatus::BASIC (lp_types.h), the state() encoding
 
 
 class IntegerTrail:
@@ -95,7 +107,9 @@ class LpConstraint:
         self.h = handle
         self.h.load(lp)
         self.linearization_level = linearization_level
-        self.next_simplex_iter = 500  # sat_parameters' starting limit
+        self.next_simplex_iter = 500  # linear_programming_constraint.h:548
+        self.is_degenerate = False
+        self.lp_at_level_zero_is_final = False
         self.lp_solution = None
         self.lp_objective = math.nan
         self.reduced_costs = None
@@ -119,13 +133,51 @@ class LpConstraint:
         self.num_solves += 1
         if r.problem_status == abi.OPTIMAL:
             self.lp_solution = self.h.primal()
-            self.lp_objective = float(r.objective)
-            self.reduced_costs = self.h.reduced_costs()
         return True
+
+    # -- Propagate (:1697-1806) ----------------------------------------------
+    def set_iteration_cap(self, level):
+        """The simplex iteration cap Propagate sets (:1716-1723)."""
+        cap = ROOT_LP_ITERATIONS if level == 0 else self.next_simplex_iter
+        p = type(self.h.params)()
+        ctypes_copy(p, self.h.params)
+        p.max_number_of_iterations = int(cap)
+        self.h.set_params(p)
+        return cap
+
+    def propagate(self, trail, level=0):
+        """One Propagate call at decision level `level`. Returns False on a
+        conflict. The cut loop (:1731-1806) adds nothing here (no cut
+        generators), which ends it after the first round; at level 0 that
+        marks the level-zero LP final (:1797-1800)."""
+        self.set_iteration_cap(level)
+        if not self.solve_lp(trail):
+            return True
+        if not self.analyze_lp(trail):
+            return False
+        if self.last.problem_status == abi.OPTIMAL and level == 0:
+            self.lp_at_level_zero_is_final = True
+        return True
+
+    def calculate_degeneracy(self):
+        """CalculateDegeneracy (:2351-2365): non-basic columns (slacks
+        included: RevisedSimplex's num_cols_) with a zero reduced cost; a slack's
+        reduced cost is minus its row's dual value."""
+        state = np.asarray(self.h.state())
+        n = self.lp.n
+        zero = np.concatenate([np.asarray(self.h.reduced_costs())[:n] == 0.0,
+                               np.asarray(self.h.duals()) == 0.0])
+        count = int(np.count_nonzero(zero & (state != BASIC)))
+        self.is_degenerate = count >= 0.3 * len(state)
+        return count
 
     # -- AnalyzeLp (:762-860) ------------------------------------------------
     def analyze_lp(self, trail):
-        """Returns False on a conflict (infeasible LP, or a bound crossing)."""
+        """Returns False on a conflict (infeasible LP, or a bound crossing).
+        The deductions read the simplex's current reduced costs and values
+        (GetReducedCost / GetVariableValue, :2380-2381) for OPTIMAL and
+        DUAL_FEASIBLE alike; the objective bound is pushed before them
+        (:817-837)."""
         r = self.last
         if r.problem_status == abi.DUAL_UNBOUNDED:
             trail.conflict = True
@@ -133,25 +185,31 @@ class LpConstraint:
         self.update_iteration_limit(r.problem_status)
         if r.problem_status in KEEP_STATUSES:
             obj = float(r.objective)
-            for col, kind, value in self.reduced_cost_deductions(trail, trail.obj_ub - obj):
-                ok = trail.enqueue_le(col, value) if kind == "le" else trail.enqueue_ge(col, value)
-                if not ok:
-                    return False
+            rc = np.asarray(self.h.reduced_costs())
+            x = np.asarray(self.h.primal())
+            deductions = self.reduced_cost_deductions(trail, trail.obj_ub - obj, rc, x)
             new_lb = float(math.ceil(obj - K_CP_EPSILON))
             if new_lb > trail.obj_lb and not trail.enqueue_obj_ge(new_lb):
                 return False
+            for col, kind, value in deductions:
+                ok = trail.enqueue_le(col, value) if kind == "le" else trail.enqueue_ge(col, value)
+                if not ok:
+                    return False
+        if r.problem_status == abi.OPTIMAL:
+            self.lp_objective = float(r.objective)
+            self.reduced_costs = np.asarray(self.h.reduced_costs())
         return True
 
-    def reduced_cost_deductions(self, trail, cp_objective_delta):
+    def reduced_cost_deductions(self, trail, cp_objective_delta, rc=None, x=None):
         """ReducedCostStrengtheningDeductions (:2367-2408): a column moved off
         its bound by more than objective slack / |rc| would cross the
-        incumbent."""
+        incumbent. rc and x default to the handle's current values."""
         out = []
-        if not math.isfinite(cp_objective_delta) or self.reduced_costs is None:
+        if not math.isfinite(cp_objective_delta):
             return out
         lp_delta = cp_objective_delta / self.lp.obj_scale
-        rc = self.reduced_costs
-        x = self.lp_solution
+        rc = np.asarray(self.h.reduced_costs()) if rc is None else rc
+        x = np.asarray(self.h.primal()) if x is None else x
         for col in self.int_cols:
             c = float(rc[col])
             if c == 0.0:
@@ -167,16 +225,16 @@ class LpConstraint:
                     out.append((int(col), "ge", float(new_lb)))
         return out
 
-    def update_iteration_limit(self, status, num_degenerate_columns=0, min_iter=10,
-                               max_iter=1000):
+    def update_iteration_limit(self, status, min_iter=10, max_iter=1000):
         """UpdateSimplexIterationLimit (:1665-1695); level < 2 keeps it."""
         if self.linearization_level < 2:
             return
-        num_cols = self.lp.n
+        num_degenerate_columns = self.calculate_degeneracy()
+        num_cols = self.lp.n + self.lp.m  # GetProblemNumCols (slacks included)
         if num_cols <= 0:
             return
         decrease = (10 * num_degenerate_columns) // num_cols
-        degenerate = num_degenerate_columns > 0
+        degenerate = self.is_degenerate
         if status == abi.DUAL_FEASIBLE:
             if degenerate:
                 self.next_simplex_iter //= max(1, decrease)

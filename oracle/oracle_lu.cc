@@ -1034,7 +1034,9 @@ void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d)
     return;
   }
   lu_factorization_.RightSolveLForColumnView(compact_matrix_.column(col), d);
+  if (g_trace_ftran) g_ftran_hash[0] = TraceHashVector(d->values, d->non_zeros);
   rank_one_factorization_.RightSolveWithNonZeros(d);
+  if (g_trace_ftran) g_ftran_hash[1] = TraceHashVector(d->values, d->non_zeros);
   if (col >= static_cast<int>(right_pool_mapping_.size())) {
     right_pool_mapping_.resize(col + 1, kInvalidCol);
   }
@@ -1047,6 +1049,7 @@ void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d)
   }
   lu_factorization_.RightSolveUWithNonZeros(d);
   d->SortNonZerosIfNeeded();
+  if (g_trace_ftran) g_ftran_hash[2] = TraceHashVector(d->values, d->non_zeros);
   BumpDeterministicTimeForSolve(static_cast<int64_t>(d->NumNonZerosEstimate()));
 }
 

@@ -9,12 +9,29 @@
 #ifndef ORACLE_LU_H_
 #define ORACLE_LU_H_
 
+#include <cstring>
 #include <memory>
 #include <string>
 
 #include "oracle_lp_data.h"
 
 namespace oracle {
+
+// Debug aid (MILP_TRACE): bit-hashes of the last problem-column FTRAN's
+// stages (after L, after the rank-one etas, after U), printed with the
+// per-iteration trace line so engine and oracle divergences can be located.
+inline bool g_trace_ftran = false;
+inline uint64_t g_ftran_hash[3] = {0, 0, 0};
+inline uint64_t TraceHashVector(const std::vector<Fractional>& v, const std::vector<int>& nz) {
+  uint64_t h = 1469598103934665603ull;
+  for (const Fractional x : v) {
+    uint64_t b;
+    std::memcpy(&b, &x, sizeof(b));
+    h = (h ^ b) * 1099511628211ull;
+  }
+  for (const int r : nz) h = (h ^ static_cast<uint32_t>(r)) * 1099511628211ull;
+  return h;
+}
 
 // ---------------------------------------------------------------------------
 // TriangularMatrix (sparse.h:583-921).

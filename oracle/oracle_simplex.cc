@@ -2192,13 +2192,20 @@ class RevisedSimplex {
     const std::string path = std::string(prefix) + ".oracle";
     FILE* f = std::fopen(path.c_str(), "a");
     if (f == nullptr) return;
-    std::fprintf(f, "it=%lld phase=%d basis=%016llx x=%016llx rc=%016llx se=%016llx obj=%a\n",
+    std::fprintf(f, "it=%lld phase=%d basis=%016llx x=%016llx rc=%016llx se=%016llx obj=%a"
+                 " ent=%d lr=%d step=%a rcq=%a d=%016llx/%016llx/%016llx\n",
                  static_cast<long long>(num_iterations_), static_cast<int>(phase_),
                  static_cast<unsigned long long>(HashInts(basis_)),
                  static_cast<unsigned long long>(HashBits(variable_values_.GetDenseRow())),
                  static_cast<unsigned long long>(HashBits(reduced_costs_.RawReducedCosts())),
                  static_cast<unsigned long long>(HashBits(primal_edge_norms_.RawEdgeNorms())),
-                 ComputeObjectiveValue());
+                 ComputeObjectiveValue(), trace_entering_, trace_leaving_row_, trace_step_,
+                 trace_reduced_cost_, static_cast<unsigned long long>(g_ftran_hash[0]),
+                 static_cast<unsigned long long>(g_ftran_hash[1]),
+                 static_cast<unsigned long long>(g_ftran_hash[2]));
+    trace_entering_ = trace_leaving_row_ = -1;
+    trace_step_ = trace_reduced_cost_ = 0.0;
+    g_ftran_hash[0] = g_ftran_hash[1] = g_ftran_hash[2] = 0;
     // MILP_TRACE_DUMP=k: raw x, rc and basis at iterations k-1 and k.
     static const char* dump = std::getenv("MILP_TRACE_DUMP");
     if (dump != nullptr && num_iterations_ + 1 >= std::atoll(dump) &&
@@ -2216,6 +2223,7 @@ class RevisedSimplex {
       put("x", variable_values_.GetDenseRow().data(), sizeof(Fractional) * num_cols_);
       put("rc", reduced_costs_.RawReducedCosts().data(), sizeof(Fractional) * num_cols_);
       put("basis", basis_.data(), sizeof(int) * num_rows_);
+      put("d", direction_.values.data(), sizeof(Fractional) * direction_.values.size());
     }
     if (num_cols_ <= 64) {
       const std::vector<Fractional>* vs[3] = {&variable_values_.GetDenseRow(),
@@ -2230,6 +2238,10 @@ class RevisedSimplex {
     }
     std::fclose(f);
   }
+  int trace_entering_ = -1;
+  int trace_leaving_row_ = -1;
+  Fractional trace_step_ = 0.0;
+  Fractional trace_reduced_cost_ = 0.0;
   void OnIterationDone(TimeLimit* tl) {
     TraceIteration();
     ++num_iterations_;
@@ -3441,6 +3453,7 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
     std::function<void()> f;
     ~Cleanup() { f(); }
   } cleanup{[this, time_limit]() { AdvanceDeterministicTime(time_limit); }};
+  g_trace_ftran = std::getenv("MILP_TRACE") != nullptr;
   bool refactorize = false;
   primal_prices_.ForceRecomputation();
   if (phase_ == Phase::FEASIBILITY) {
@@ -3554,6 +3567,10 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
     if (phase_ == Phase::FEASIBILITY && leaving_row != kInvalidRow) {
       step = ComputeStepToMoveBasicVariableToBound(leaving_row, target_bound);
     }
+    trace_entering_ = entering_col;
+    trace_leaving_row_ = leaving_row;
+    trace_step_ = step;
+    trace_reduced_cost_ = reduced_cost;
     const int leaving_col = (leaving_row == kInvalidRow) ? kInvalidCol : basis_[leaving_row];
     bool is_degenerate = false;
     if (leaving_row != kInvalidRow) {

@@ -146,3 +146,69 @@ def test_node_branch_lps_parity():
     s1 = cpsat.fold_node(cpsat.IntegerTrail(t.lb, t.ub, t.obj_lb), c.lp_solution, cols, got)
     s2 = cpsat.fold_node(cpsat.IntegerTrail(t.lb, t.ub, t.obj_lb), c.lp_solution, cols, ref)
     assert s1 == s2
+
+
+def test_analyze_dual_feasible_reads_current_values():
+    """AnalyzeLp on a DUAL_FEASIBLE result (the iteration cap hit by the dual
+    simplex) deduces from the simplex's current reduced costs and values
+    (linear_programming_constraint.cc:2380-2381), not from an earlier OPTIMAL
+    solve, and pushes the objective bound first (:817-837)."""
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
+    lp, ycols, o, c, t = _node(jobshop.random_instance(6, 4, 3), p)
+    stale_rc = c.reduced_costs.copy()
+    cols = cpsat.fractional_columns(c.lp_solution, ycols, limit=1)
+    assert cols
+    lbs, ubs = cpsat.branch_lps(t, c.lp_solution, cols)
+    trail = cpsat.IntegerTrail(lbs[0], ubs[0], obj_lb=t.obj_lb, obj_ub=t.obj_lb + 40.0)
+    capped = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1)
+    o.set_params(capped)
+    assert c.solve_lp(trail)
+    assert c.last.problem_status == abi.DUAL_FEASIBLE, abi.PROBLEM_STATUS[c.last.problem_status]
+    rc, x = o.reduced_costs(), o.primal()
+    assert not (np.array_equal(rc, stale_rc) and np.array_equal(x, c.lp_solution))
+    want = []
+    delta = (trail.obj_ub - c.last.objective) / lp.obj_scale
+    for col in ycols:
+        r = float(rc[col])
+        if r == 0.0:
+            continue
+        other = float(x[col]) + delta / r
+        if r > cpsat.K_LP_EPSILON and math.floor(other + cpsat.K_CP_EPSILON) < trail.ub[col]:
+            want.append((int(col), "le", float(math.floor(other + cpsat.K_CP_EPSILON))))
+        elif r < -cpsat.K_LP_EPSILON and math.ceil(other - cpsat.K_CP_EPSILON) > trail.lb[col]:
+            want.append((int(col), "ge", float(math.ceil(other - cpsat.K_CP_EPSILON))))
+    assert c.reduced_cost_deductions(trail, trail.obj_ub - c.last.objective) == want
+    before_lb = trail.obj_lb
+    ok = c.analyze_lp(trail)
+    new_lb = math.ceil(c.last.objective - cpsat.K_CP_EPSILON)
+    if ok:
+        assert trail.obj_lb == max(before_lb, new_lb)
+        for col, kind, v in want:
+            assert (trail.ub[col] <= v) if kind == "le" else (trail.lb[col] >= v)
+
+
+def test_propagate_iteration_caps_and_degeneracy():
+    """Propagate's simplex caps (:1716-1723): root_lp_iterations at level 0,
+    next_simplex_iter_ below; at linearization level 2 the limit follows
+    UpdateSimplexIterationLimit with CalculateDegeneracy's count (:2351-2365)."""
+    p = abi.default_params(use_dual_simplex=1)
+    lp, ycols = jobshop.relaxation(jobshop.FT06)
+    o = oracle_lib.OracleLp(p)
+    c = cpsat.LpConstraint(lp, ycols, o, linearization_level=2)
+    t = cpsat.IntegerTrail(lp.col_lb, lp.col_ub)
+    assert c.propagate(t, level=0)
+    assert o.params.max_number_of_iterations == cpsat.ROOT_LP_ITERATIONS
+    assert c.last.problem_status == abi.OPTIMAL and c.lp_at_level_zero_is_final
+    state = o.state()
+    zero = np.concatenate([o.reduced_costs() == 0.0, o.duals() == 0.0])
+    count = int(np.count_nonzero(zero & (np.asarray(state) != cpsat.BASIC)))
+    assert c.calculate_degeneracy() == count
+    assert c.is_degenerate == (count >= 0.3 * (lp.n + lp.m))
+    cols = lp.n + lp.m
+    if c.is_degenerate:
+        expect = max(10, min(1000, 500 // max(1, 2 * ((10 * count) // cols))))
+    else:
+        expect = max(10, min(1000, cols // 40))
+    assert c.next_simplex_iter == expect
+    assert c.propagate(t, level=3)
+    assert o.params.max_number_of_iterations == expect

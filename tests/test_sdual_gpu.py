@@ -88,3 +88,68 @@ def test_sdual_child_full_state(sdual_mode):
         o.load_basis_state(state)
         ro = o.solve()
         parity_util.compare(o, ro, g, rg, lp)
+
+
+def test_sdual_pool_at_bench_scale():
+    """The pool at the benchmark's scale (bench.py's config-4 section runs
+    1 024 handles): 512 children of the 15x10 node with 256 LPs in flight,
+    each equal to the oracle solving it alone."""
+    lp, state, lbs, ubs = _children((15, 10), 512)
+    assert len(lbs) >= 256
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
+    workers = [engine.LpHandle(p) for _ in range(256)]
+    for w in workers:
+        w.load(lp)
+    got = engine.batch_solve_bounds(workers, lbs, ubs, state)
+    ows = [oracle_lib.OracleLp(p) for _ in range(8)]
+    for w in ows:
+        w.load(lp)
+    ref = oracle_lib.batch_solve_bounds(ows, lbs, ubs, state)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        assert (a.error_code, a.problem_status, a.iterations) == \
+            (b.error_code, b.problem_status, b.iterations), i
+        assert a.objective == b.objective, (i, a.objective, b.objective)
+    assert sum(w.run_counters()["sdual_segments"] for w in workers) > 0
+
+
+_WRAP = r"""
+import sys
+sys.path[:0] = ["tests", "or-tools_amd"]
+from mi_glop import abi, engine
+import oracle_lib
+import test_sdual_gpu as t
+lp, state, lbs, ubs = t._children((10, 5), 40, seed=11)
+p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
+workers = [engine.LpHandle(p) for _ in range(16)]
+for w in workers:
+    w.load(lp)
+ows = [oracle_lib.OracleLp(p) for _ in range(4)]
+for w in ows:
+    w.load(lp)
+ref = oracle_lib.batch_solve_bounds(ows, lbs, ubs, state)
+for call in range(3):
+    got = engine.batch_solve_bounds(workers, lbs, ubs, state)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        assert (a.error_code, a.problem_status, a.iterations, a.objective) == \
+            (b.error_code, b.problem_status, b.iterations, b.objective), (call, i)
+segs = sum(w.run_counters()["sdual_segments"] for w in workers)
+print("OK segments", segs)
+"""
+
+
+def test_sdual_pool_queue_wraparound():
+    """More segments than the queue's slots through the pool: the rings are
+    cut to 8 slots (MILP_SDUAL_QUEUE_CAP, read when the pool is created, so
+    in a fresh process), three batch calls back to back (the last batch call
+    stops the grid, the next relaunches it from the first uncopied entry);
+    every child still equals the oracle."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MILP_SDUAL_QUEUE_CAP="8", MILP_SDUAL="device")
+    r = subprocess.run([sys.executable, "-c", _WRAP], cwd=repo, env=env, timeout=240,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    segs = int(r.stdout.split("OK segments")[1].split()[0])
+    assert segs > 3 * 8, segs
