@@ -29,6 +29,11 @@ def digest(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+def lp_digest(lp):
+    """The LP the digests describe (the GPU test checks it builds the same)."""
+    return {k: digest(getattr(lp, k)) for k in ("row_lb", "row_ub", "obj", "vals")}
+
+
 def state_digests(o, r):
     var, cons = o.statuses()
     return {"iterations": int(r.iterations), "problem_status": int(r.problem_status),
@@ -46,6 +51,7 @@ def main():
     lp = lp_gen.dense_box_lp(10000, 50000, seed)
     print(f"generated in {time.time() - t:.1f}s", flush=True)
     out = {"lp": "lp_gen.dense_box_lp(10000, 50000, 20261015)",
+           "lp_digest": lp_digest(lp),
            "params": "abi.default_params(max_number_of_iterations=cap)",
            "generator": "scripts/make_c2_window_golden.py", "caps": {}}
     path = os.path.join(REPO, "tests", "golden", "c2_windows.json")

@@ -59,6 +59,19 @@ def random_sparse_lp(m, n, density, seed, eq_frac=0.2, free_frac=0.05,
                          0.0, 1.0, maximize, f"sparse_{m}x{n}_s{seed}")
 
 
+def fixed_order_matvec(At, x):
+    """A @ x from the rows of At = A^T, summed column by column in index
+    order with one rounding per multiply and per add. BLAS (`A @ x`) picks
+    its kernel and thread split by CPU, so its last bits differ between this
+    container and the GPU box: an LP built with it is not the same LP on both
+    machines, and golden fixtures made here would not describe the LP the GPU
+    test builds there."""
+    acc = np.zeros(At.shape[1])
+    for j in range(At.shape[0]):
+        acc += At[j] * x[j]
+    return acc
+
+
 def dense_box_lp(m, n, seed, maximize=True):
     """Config 2 generator: A_ij ~ U(-1,1) dense,
     x0 ~ U(0,1), rows A x <= A x0 + U(0,1), 0 <= x <= 10, c ~ U(-1,1)."""
@@ -66,10 +79,12 @@ def dense_box_lp(m, n, seed, maximize=True):
     A = rng.uniform(-1.0, 1.0, size=(m, n))
     A[A == 0.0] = 0.5
     x0 = rng.uniform(0.0, 1.0, size=n)
-    rhs = A @ x0 + rng.uniform(0.0, 1.0, size=m)
+    At = np.ascontiguousarray(A.T)
+    del A
+    rhs = fixed_order_matvec(At, x0) + rng.uniform(0.0, 1.0, size=m)
     cs = np.arange(0, (n + 1) * m, m, dtype=np.int64)
     ri = np.tile(np.arange(m, dtype=np.int32), n)
-    va = np.ascontiguousarray(A.T).reshape(-1)
+    va = At.reshape(-1)
     obj = rng.uniform(-1.0, 1.0, size=n)
     return LinearProgram(m, n, cs, ri, va, np.zeros(n), np.full(n, 10.0),
                          np.full(m, -INF), rhs, obj, 0.0, 1.0, maximize,
@@ -111,7 +126,7 @@ def from_dense_box(A, rng, maximize=True):
     and bound construction as dense_box_lp, explicit zeros dropped."""
     m, n = A.shape
     x0 = rng.uniform(0.0, 1.0, size=n)
-    rhs = A @ x0 + rng.uniform(0.0, 1.0, size=m)
+    rhs = fixed_order_matvec(np.ascontiguousarray(A.T), x0) + rng.uniform(0.0, 1.0, size=m)
     cols = [np.nonzero(A[:, j])[0] for j in range(n)]
     cs = np.zeros(n + 1, dtype=np.int64)
     cs[1:] = np.cumsum([len(c) for c in cols])
