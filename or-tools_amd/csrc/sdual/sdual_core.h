@@ -127,6 +127,70 @@ SD_INLINE void sd_fill(T* p, int64_t n, T v) {
   sd_sync();
 }
 
+// The workgroup's LDS scratch (sdual_kernel.hip: after the staging area):
+// 256 products or chain sums, then one chunk of rank-one step metadata.
+struct SdScratch {
+  f64 red[256];
+  int64_t meta[64 * 4];
+  f64 mu[64];
+};
+constexpr int kSdScratchDoubles = static_cast<int>(sizeof(SdScratch) / sizeof(f64));
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// Explicit address spaces for the hot loops: the arena's arrays are global
+// memory (AS 1), the workgroup's scratch LDS (AS 3). Typed pointers let the
+// compiler issue global_load / ds_read (partial waits, several loads in
+// flight) instead of flat accesses, and know that the two never alias.
+#define SD_G(T, p) ((__attribute__((address_space(1))) T*)(p))
+#define SD_L(T, p) ((__attribute__((address_space(3))) T*)(p))
+typedef __attribute__((address_space(1))) f64 g_f64;
+typedef __attribute__((address_space(3))) f64 l_f64;
+typedef __attribute__((address_space(1))) const int32_t gc_i32;
+typedef __attribute__((address_space(1))) const int64_t gc_i64;
+typedef __attribute__((address_space(1))) const f64 gc_f64;
+typedef __attribute__((address_space(3))) int64_t l_i64;
+
+
+// ColumnScalarProduct (sparse.h:514-542) of entries [b, e) of a column
+// (rows/coefs) against x, on the lanes: up to 256 products are computed
+// together (their loads in flight at once) and written to LDS, then lane
+// j < 4 adds the products of entries j, j + 4, ... in order (Glop's
+// accumulator r_{j+1}); the four sums are folded as ((r1 + r2) + r3) + r4
+// and the tail entries added in order. Same roundings as the sequential loop.
+template <typename XP>
+__device__ inline f64 sd_ordered_dot(gc_i32* rows, gc_f64* coefs, int64_t b, int64_t e, XP x,
+                                     l_f64* red) {
+  const int lane = sd_lane();
+  const int64_t len = e - b;
+  const int64_t body = len & ~int64_t{3};
+  f64 acc = 0.0;
+  for (int64_t base = 0; base < body; base += 256) {
+    const int64_t n = body - base < 256 ? body - base : 256;
+    f64 p[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t k = base + u * 64 + lane;
+      p[u] = 0.0;
+      if (u * 64 + lane < n) p[u] = coefs[b + k] * x[rows[b + k]];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) red[u * 64 + lane] = p[u];
+    sd_sync();
+    if (lane < 4) {
+      const int groups = static_cast<int>(n >> 2);
+      for (int g = 0; g < groups; ++g) acc += red[lane + 4 * g];
+    }
+    sd_sync();
+  }
+  if (lane < 4) red[lane] = acc;
+  sd_sync();
+  f64 result = red[0] + red[1] + red[2] + red[3];
+  sd_sync();
+  for (int64_t t = body; t < len; ++t) result += coefs[b + t] * x[rows[b + t]];
+  return result;
+}
+#endif
+
 // ---- Bitset64 ----
 SD_INLINE bool bit_get(const uint64_t* w, int i) { return (w[i >> 6] >> (i & 63)) & 1; }
 SD_INLINE void bit_set(uint64_t* w, int i) { w[i >> 6] |= (1ull << (i & 63)); }
@@ -417,26 +481,13 @@ SD_INLINE int64_t col_entries(const M& a, int col) {
 // r_{j+1} and adds the products of entries j, j + 4, j + 8, ... in order, so
 // the sums round exactly as the sequential loop's.
 template <typename M>
-SD_INLINE f64 col_dot_par(const M& a, int col, const f64* v) {
+SD_INLINE f64 col_dot_par(const M& a, int col, const f64* v, f64* lds_scratch) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  const int64_t b = a.starts[col], e = a.starts[col + 1];
-  const int64_t body = (e - b) & ~int64_t{3};  // the four-accumulator loop's entries
-  const int lane = sd_lane();
-  const int j = lane & 3;
-  f64 acc = 0.0;
-  for (int64_t base = 0; base < body; base += 64) {
-    const int64_t k = base + lane;
-    f64 p = 0.0;
-    if (k < body) p = a.coefs[b + k] * v[a.rows[b + k]];
-    const int groups = static_cast<int>((body - base < 64 ? body - base : 64) >> 2);
-    for (int g = 0; g < groups; ++g) acc += __shfl(p, j + 4 * g, 64);
-  }
-  const f64 r1 = __shfl(acc, 0, 64), r2 = __shfl(acc, 1, 64);
-  const f64 r3 = __shfl(acc, 2, 64), r4 = __shfl(acc, 3, 64);
-  f64 result = r1 + r2 + r3 + r4;
-  for (int64_t i = b + body; i < e; ++i) result += a.coefs[i] * v[a.rows[i]];
-  return result;
+  return sd_ordered_dot(SD_G(const int32_t, a.rows), SD_G(const f64, a.coefs), a.starts[col],
+                        a.starts[col + 1], SD_G(const f64, v),
+                        SD_L(f64, reinterpret_cast<SdScratch*>(lds_scratch)->red));
 #else
+  (void)lds_scratch;
   return col_dot(a, col, v);
 #endif
 }
@@ -652,6 +703,87 @@ SD_INLINE f64 tri_tl_column(const Tri& t, const f64* x, int col) {
 SD_INLINE bool tri_use_levels(const Tri& t) {
   return t.num_levels >= 0 && 4 * t.num_levels <= t.num_cols - t.first_non_identity;
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+// One column of tri_tu_column (kUpper) / tri_tl_column with typed pointers:
+// the four entries of a group load together.
+template <bool kUpper, typename XP>
+__device__ inline f64 tri_column_dev(gc_i32* rows, gc_f64* coefs, int64_t b, int64_t e, XP x,
+                                     int col) {
+  f64 sum = x[col];
+  if (kUpper) {
+    int64_t i = b;
+    for (; i < e - 3; i += 4) {
+      sum -= coefs[i] * x[rows[i]] + coefs[i + 1] * x[rows[i + 1]] +
+             coefs[i + 2] * x[rows[i + 2]] + coefs[i + 3] * x[rows[i + 3]];
+    }
+    if (i < e) {
+      sum -= coefs[i] * x[rows[i]];
+      if (i + 1 < e) {
+        sum -= coefs[i + 1] * x[rows[i + 1]];
+        if (i + 2 < e) sum -= coefs[i + 2] * x[rows[i + 2]];
+      }
+    }
+  } else {
+    int64_t i = e - 1;
+    for (; i >= b + 3; i -= 4) {
+      sum -= coefs[i] * x[rows[i]] + coefs[i - 1] * x[rows[i - 1]] +
+             coefs[i - 2] * x[rows[i - 2]] + coefs[i - 3] * x[rows[i - 3]];
+    }
+    if (i >= b) {
+      sum -= coefs[i] * x[rows[i]];
+      if (i >= b + 1) {
+        sum -= coefs[i - 1] * x[rows[i - 1]];
+        if (i >= b + 2) sum -= coefs[i - 2] * x[rows[i - 2]];
+      }
+    }
+  }
+  return sum;
+}
+// The level sweep with the next level's bounds, first columns and their
+// entry ranges loaded while the current level computes (read-only schedule
+// data), so a level waits on its entries and x only.
+template <bool kUpper, typename XP>
+__device__ inline void tri_level_sweep_dev(const Tri& t, XP x, int last) {
+  gc_i64* starts = SD_G(const int64_t, t.starts);
+  gc_i32* rows = SD_G(const int32_t, t.rows);
+  gc_f64* coefs = SD_G(const f64, t.coefs);
+  gc_f64* diag = SD_G(const f64, t.diag);
+  gc_i32* order = SD_G(const int32_t, t.lv_order);
+  gc_i32* lvs = SD_G(const int32_t, t.lv_starts);
+  const bool ones = t.all_ones;
+  const int lane = sd_lane();
+  const int levels = t.num_levels;
+  if (levels <= 0) return;
+  int le = lvs[1];
+  int k = lvs[0] + lane;
+  int col = k < le ? order[k] : 0;
+  int64_t cb = k < le ? starts[col] : 0, ce = k < le ? starts[col + 1] : 0;
+  for (int l = 0; l < levels; ++l) {
+    const int le2 = l + 1 < levels ? lvs[l + 2] : le;
+    const int k2 = le + lane;
+    const int col2 = k2 < le2 ? order[k2] : 0;
+    const int64_t cb2 = k2 < le2 ? starts[col2] : 0, ce2 = k2 < le2 ? starts[col2 + 1] : 0;
+    for (; k < le;) {
+      if (kUpper || col <= last) {
+        const f64 sum = tri_column_dev<kUpper>(rows, coefs, cb, ce, x, col);
+        x[col] = ones ? sum : sum / diag[col];
+      }
+      k += 64;
+      if (k < le) {
+        col = order[k];
+        cb = starts[col];
+        ce = starts[col + 1];
+      }
+    }
+    sd_sync();
+    le = le2;
+    k = k2;
+    col = col2;
+    cb = cb2;
+    ce = ce2;
+  }
+}
+#endif
 // Columns of each level split over the lanes, a barrier between levels:
 // every column reads only finished columns, so the results are those of the
 // sequential sweep.
@@ -677,18 +809,36 @@ SD_INLINE void tri_level_sweep_lower(const Tri& t, f64* x, int last) {
 // waits on one round trip (its entries) instead of three.
 SD_INLINE f64* sd_stage_in(f64* lds, int cap, const f64* x, int n) {
   if (lds == nullptr || n > cap) return nullptr;
+#if defined(__HIP_DEVICE_COMPILE__)
+  l_f64* l = SD_L(f64, lds);
+  gc_f64* g = SD_G(const f64, x);
+#pragma unroll 8
+  for (int i = sd_lane(); i < n; i += 64) l[i] = g[i];
+#else
   for (int i = sd_lane(); i < n; i += sd_lanes()) lds[i] = x[i];
+#endif
   sd_sync();
   return lds;
 }
 SD_INLINE void sd_stage_out(const f64* lds, f64* x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __attribute__((address_space(3))) f64* l = SD_L(const f64, lds);
+  g_f64* g = SD_G(f64, x);
+#pragma unroll 8
+  for (int i = sd_lane(); i < n; i += 64) g[i] = l[i];
+#else
   for (int i = sd_lane(); i < n; i += sd_lanes()) x[i] = lds[i];
+#endif
   sd_sync();
 }
 SD_INLINE void tri_transpose_upper_solve(const Tri& t, f64* x, f64* lds = nullptr, int cap = 0) {
   if (tri_use_levels(t)) {
     if (f64* v = sd_stage_in(lds, cap, x, t.num_cols)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      tri_level_sweep_dev<true>(t, SD_L(f64, v), t.num_cols);
+#else
       tri_level_sweep_upper(t, v);
+#endif
       sd_stage_out(v, x, t.num_cols);
       return;
     }
@@ -720,7 +870,11 @@ SD_INLINE void tri_transpose_lower_solve(const Tri& t, f64* x, f64* lds = nullpt
   if (tri_use_levels(t)) {
     // Columns above `last` are read (zeros of either sign) but not written.
     if (f64* v = sd_stage_in(lds, cap, x, t.num_cols)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      tri_level_sweep_dev<false>(t, SD_L(f64, v), last);
+#else
       tri_level_sweep_lower(t, v, last);
+#endif
       sd_stage_out(v, x, last + 1);
       return;
     }
@@ -894,10 +1048,33 @@ SD_INLINE void permute_with_scratchpad(Lp& s, const int32_t* perm, Vec& io) {
   s.zero_scratch = old;
   const int size = io.size;
   sd_fill<f64>(io.values, size, 0.0);  // resize(size, 0.0) of an all-zero buffer
+#if defined(__HIP_DEVICE_COMPILE__)
+  {
+    gc_f64* src = SD_G(const f64, s.zero_scratch);
+    gc_i32* pg = SD_G(const int32_t, perm);
+    g_f64* dst = SD_G(f64, io.values);
+    // Eight chunks at a time, every load before any store.
+    for (int i0 = sd_lane(); i0 < size; i0 += 512) {
+      f64 v[8];
+      int p[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 64 * u;
+        v[u] = i < size ? src[i] : 0.0;
+        p[u] = i < size ? pg[i] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (v[u] != 0.0) dst[p[u]] = v[u];  // a permutation: distinct targets
+      }
+    }
+  }
+#else
   for (int i = sd_lane(); i < size; i += sd_lanes()) {
     const f64 v = s.zero_scratch[i];
     if (v != 0.0) io.values[perm[i]] = v;  // a permutation: distinct targets
   }
+#endif
   sd_sync();
   sd_fill<f64>(s.zero_scratch, size, 0.0);
 }
@@ -905,6 +1082,37 @@ SD_INLINE void permute_with_known_nz(Lp& s, const int32_t* perm, Vec& io) {
   f64* old = io.values;
   io.values = s.zero_scratch;
   s.zero_scratch = old;
+#if defined(__HIP_DEVICE_COMPILE__)
+  {
+    g_f64* zs = SD_G(f64, s.zero_scratch);
+    gc_i32* pg = SD_G(const int32_t, perm);
+    g_f64* dst = SD_G(f64, io.values);
+    __attribute__((address_space(1))) int32_t* nz = SD_G(int32_t, io.nz);
+    const int n = io.nnz;
+    // Four chunks at a time, every load before any store (distinct positions).
+    for (int k0 = sd_lane(); k0 < n; k0 += 256) {
+      int ref[4], p[4];
+      f64 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ref[u] = k0 + 64 * u < n ? nz[k0 + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (ref[u] >= 0) {
+          v[u] = zs[ref[u]];
+          p[u] = pg[ref[u]];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (ref[u] >= 0) {
+          zs[ref[u]] = 0.0;
+          dst[p[u]] = v[u];
+          nz[k0 + 64 * u] = p[u];
+        }
+      }
+    }
+  }
+#else
   for (int k = sd_lane(); k < io.nnz; k += sd_lanes()) {  // distinct positions
     const int ref = io.nz[k];
     const f64 v = s.zero_scratch[ref];
@@ -913,18 +1121,19 @@ SD_INLINE void permute_with_known_nz(Lp& s, const int32_t* perm, Vec& io) {
     io.values[p] = v;
     io.nz[k] = p;
   }
+#endif
   sd_sync();
 }
 SD_INLINE void lu_right_solve_l_permuted_input(Lp& s, Vec& x) {
   if (s.is_identity) return;
-  tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored);
+  { SdSubTimer t_x_(&s.phase_ticks[16]); tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored); }
   if (x.nnz == 0) {
     {
       SdSubTimer t_(&s.phase_ticks[9]);
       tri_lower_solve_from(s.lower, 0, x.values);
     }
   } else {
-    tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz);
+    { SdSubTimer t_x_(&s.phase_ticks[17]); tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz); }
   }
 }
 // RightSolveLInternal (lu_factorization.cc:214-243); the rhs is a matrix
@@ -946,7 +1155,7 @@ SD_INLINE void lu_right_solve_l_internal(Lp& s, const int32_t* brows, const f64*
   first = sd_wave_min_int(first);
   x.nnz = base + bn;
   sd_sync();
-  tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored);
+  { SdSubTimer t_x_(&s.phase_ticks[16]); tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored); }
   x.sorted = 1;
   if (x.nnz == 0) {
     {
@@ -954,7 +1163,7 @@ SD_INLINE void lu_right_solve_l_internal(Lp& s, const int32_t* brows, const f64*
       tri_lower_solve_from(s.lower, first, x.values);
     }
   } else {
-    tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz);
+    { SdSubTimer t_x_(&s.phase_ticks[17]); tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz); }
   }
 }
 SD_INLINE void lu_right_solve_l_for_column(Lp& s, int col, Vec& x) {
@@ -972,15 +1181,15 @@ SD_INLINE void lu_right_solve_l_for_column(Lp& s, int col, Vec& x) {
 SD_INLINE void lu_right_solve_l_with_nz(Lp& s, Vec& x) {
   if (s.is_identity) return;
   if (x.nnz == 0) {
-    permute_with_scratchpad(s, s.row_perm, x);
+    { SdSubTimer t_x_(&s.phase_ticks[22]); permute_with_scratchpad(s, s.row_perm, x); }
     {
       SdSubTimer t_(&s.phase_ticks[9]);
       tri_lower_solve_from(s.lower, 0, x.values);
     }
     return;
   }
-  permute_with_known_nz(s, s.row_perm, x);
-  tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored);
+  { SdSubTimer t_x_(&s.phase_ticks[22]); permute_with_known_nz(s, s.row_perm, x); }
+  { SdSubTimer t_x_(&s.phase_ticks[16]); tri_rows_to_consider(s.lower, x.nz, &x.nnz, s.stored); }
   x.sorted = 1;
   if (x.nnz == 0) {
     {
@@ -988,7 +1197,7 @@ SD_INLINE void lu_right_solve_l_with_nz(Lp& s, Vec& x) {
       tri_lower_solve_from(s.lower, 0, x.values);
     }
   } else {
-    tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz);
+    { SdSubTimer t_x_(&s.phase_ticks[17]); tri_hyper_solve(s.lower, x.values, x.nz, &x.nnz); }
   }
 }
 SD_INLINE void lu_right_solve_l_for_scattered(Lp& s, const Vec& b, Vec& x) {
@@ -1006,7 +1215,7 @@ SD_INLINE void lu_right_solve_l_for_scattered(Lp& s, const Vec& b, Vec& x) {
 }
 SD_INLINE void lu_right_solve_u_with_nz(Lp& s, Vec& x) {
   if (s.is_identity) return;
-  tri_rows_to_consider(s.upper, x.nz, &x.nnz, s.stored);
+  { SdSubTimer t_x_(&s.phase_ticks[16]); tri_rows_to_consider(s.upper, x.nz, &x.nnz, s.stored); }
   x.sorted = 1;
   if (x.nnz == 0) {
     {
@@ -1014,14 +1223,14 @@ SD_INLINE void lu_right_solve_u_with_nz(Lp& s, Vec& x) {
       tri_transpose_lower_solve(s.tupper, x.values, s.lds, s.lds_doubles);
     }
   } else {
-    tri_transpose_hyper_solve_rev(s.tupper, x.values, x.nz, &x.nnz);
+    { SdSubTimer t_x_(&s.phase_ticks[17]); tri_transpose_hyper_solve_rev(s.tupper, x.values, x.nz, &x.nnz); }
   }
 }
 // LeftSolveLWithNonZeros (lu_factorization.cc:333-399); `before` is tau_
 // (result_before_permutation) or null. Returns true when `before` was filled.
 SD_INLINE bool lu_left_solve_l_with_nz(Lp& s, Vec& y, Vec* before) {
   if (s.is_identity) return false;
-  tri_rows_to_consider(s.tlower, y.nz, &y.nnz, s.stored);
+  { SdSubTimer t_x_(&s.phase_ticks[16]); tri_rows_to_consider(s.tlower, y.nz, &y.nnz, s.stored); }
   y.sorted = 1;
   if (y.nnz == 0) {
     {
@@ -1029,13 +1238,13 @@ SD_INLINE bool lu_left_solve_l_with_nz(Lp& s, Vec& y, Vec* before) {
       tri_transpose_lower_solve(s.lower, y.values, s.lds, s.lds_doubles);
     }
   } else {
-    tri_transpose_hyper_solve_rev(s.lower, y.values, y.nz, &y.nnz);
+    { SdSubTimer t_x_(&s.phase_ticks[17]); tri_transpose_hyper_solve_rev(s.lower, y.values, y.nz, &y.nnz); }
   }
   if (before == nullptr) {
     if (y.nnz == 0) {
-      permute_with_scratchpad(s, s.inv_row_perm, y);
+      { SdSubTimer t_x_(&s.phase_ticks[22]); permute_with_scratchpad(s, s.inv_row_perm, y); }
     } else {
-      permute_with_known_nz(s, s.inv_row_perm, y);
+      { SdSubTimer t_x_(&s.phase_ticks[22]); permute_with_known_nz(s, s.inv_row_perm, y); }
     }
     return false;
   }
@@ -1090,7 +1299,7 @@ SD_INLINE int lu_left_solve_u_unit_row(Lp& s, int col, Vec& y) {
   if (s.tupper.starts[pc + 1] == s.tupper.starts[pc]) {
     y.values[pc] /= s.tupper.diag[pc];
   } else {
-    tri_rows_to_consider(s.tupper, y.nz, &y.nnz, s.stored);
+    { SdSubTimer t_x_(&s.phase_ticks[16]); tri_rows_to_consider(s.tupper, y.nz, &y.nnz, s.stored); }
     y.sorted = 1;
     if (y.nnz == 0) {
       {
@@ -1098,7 +1307,7 @@ SD_INLINE int lu_left_solve_u_unit_row(Lp& s, int col, Vec& y) {
         tri_lower_solve_from(s.tupper, pc, y.values);
       }
     } else {
-      tri_hyper_solve(s.tupper, y.values, y.nz, &y.nnz);
+      { SdSubTimer t_x_(&s.phase_ticks[17]); tri_hyper_solve(s.tupper, y.values, y.nz, &y.nnz); }
     }
   }
   return pc;
@@ -1156,72 +1365,66 @@ SD_INLINE int64_t lu_number_of_entries(const Lp& s) {
 // Dense steps k = 0 .. count-1 of a solve: update i = first + k (right
 // solves) or first - k (left solves), x += mult * add_col with
 // mult = -(dot_col . x) / mu (right: dot v_i, add u_i; left: dot u_i, add
-// v_i). Lane k of a 64-step chunk loads step k's columns' bounds and mu
-// first; a step loads the first 64 entries of both columns and the add
-// column's current values together (the dot leaves x unchanged), so it waits
-// on two round trips to memory instead of eight. The dot keeps
-// ColumnScalarProduct's four chains and tail (col_dot_par).
-SD_INLINE void r1_dense_steps(Lp& s, f64* x, int first, int count, bool left) {
+// v_i). Lane k of a 64-step chunk stages step k's column bounds and mu in
+// LDS; a step prefetches the add column's first 64 entries, takes the dot
+// with ColumnScalarProduct's chains (sd_ordered_dot) and scatters the add
+// column (its rows are distinct) over the lanes. x is staged in LDS for the
+// whole solve when it fits.
+template <typename XP>
+__device__ inline void r1_dense_run(const Lp& s, XP x, int first, int count, bool left) {
   const Store& st = s.storage;
   const int lane = sd_lane();
-  const int j = lane & 3;
+  SdScratch* sc = reinterpret_cast<SdScratch*>(s.lds_scratch);
+  l_f64* red = SD_L(f64, sc->red);
+  l_i64* meta = SD_L(int64_t, sc->meta);
+  l_f64* mus = SD_L(f64, sc->mu);
+  gc_i64* starts = SD_G(const int64_t, st.starts);
+  gc_i32* rows = SD_G(const int32_t, st.rows);
+  gc_f64* coefs = SD_G(const f64, st.coefs);
+  gc_i32* ru = SD_G(const int32_t, s.r1_u);
+  gc_i32* rv = SD_G(const int32_t, s.r1_v);
+  gc_f64* rmu = SD_G(const f64, s.r1_mu);
   for (int c0 = 0; c0 < count; c0 += 64) {
-    int64_t m_db = 0, m_de = 0, m_ab = 0, m_ae = 0;
-    f64 m_mu = 1.0;
     if (c0 + lane < count) {
       const int i = left ? first - (c0 + lane) : first + (c0 + lane);
-      const int dcol = left ? s.r1_u[i] : s.r1_v[i];
-      const int acol = left ? s.r1_v[i] : s.r1_u[i];
-      m_db = st.starts[dcol];
-      m_de = st.starts[dcol + 1];
-      m_ab = st.starts[acol];
-      m_ae = st.starts[acol + 1];
-      m_mu = s.r1_mu[i];
+      const int dcol = left ? ru[i] : rv[i];
+      const int acol = left ? rv[i] : ru[i];
+      meta[4 * lane + 0] = starts[dcol];
+      meta[4 * lane + 1] = starts[dcol + 1];
+      meta[4 * lane + 2] = starts[acol];
+      meta[4 * lane + 3] = starts[acol + 1];
+      mus[lane] = rmu[i];
     }
+    sd_sync();
     const int steps = count - c0 < 64 ? count - c0 : 64;
     for (int k = 0; k < steps; ++k) {
-      const int64_t db = __shfl(m_db, k, 64), de = __shfl(m_de, k, 64);
-      const int64_t ab = __shfl(m_ab, k, 64), ae = __shfl(m_ae, k, 64);
-      const f64 mu = __shfl(m_mu, k, 64);
-      const int64_t di = db + lane, ai = ab + lane;
-      int dr = 0, ar = 0;
-      f64 dc = 0.0, ac = 0.0;
-      if (di < de) {
-        dr = st.rows[di];
-        dc = st.coefs[di];
-      }
+      const int64_t db = meta[4 * k], de = meta[4 * k + 1];
+      const int64_t ab = meta[4 * k + 2], ae = meta[4 * k + 3];
+      const f64 mu = mus[k];
+      const int64_t ai = ab + lane;
+      int ar = 0;
+      f64 ac = 0.0;
       if (ai < ae) {
-        ar = st.rows[ai];
-        ac = st.coefs[ai];
+        ar = rows[ai];
+        ac = coefs[ai];
       }
-      const f64 dx = di < de ? x[dr] : 0.0;
-      const f64 ax = ai < ae ? x[ar] : 0.0;
-      const f64 p0 = dc * dx;  // entry `lane` of the dot column's first chunk
-      const int64_t len = de - db;
-      const int64_t body = len & ~int64_t{3};
-      f64 acc = 0.0;
-      for (int64_t base = 0; base < body; base += 64) {
-        f64 p;
-        if (base == 0) {
-          p = lane < body ? p0 : 0.0;
-        } else {
-          const int64_t e = db + base + lane;
-          p = base + lane < body ? st.coefs[e] * x[st.rows[e]] : 0.0;
-        }
-        const int groups = static_cast<int>((body - base < 64 ? body - base : 64) >> 2);
-        for (int g = 0; g < groups; ++g) acc += __shfl(p, j + 4 * g, 64);
-      }
-      f64 dot = __shfl(acc, 0, 64) + __shfl(acc, 1, 64) + __shfl(acc, 2, 64) + __shfl(acc, 3, 64);
-      for (int64_t t = body; t < len; ++t) {
-        dot += t < 64 ? __shfl(p0, static_cast<int>(t), 64) : st.coefs[db + t] * x[st.rows[db + t]];
-      }
+      const f64 dot = sd_ordered_dot(rows, coefs, db, de, x, red);
       const f64 mult = -dot / mu;
       if (mult != 0.0) {  // col_add_dense: a column's rows are distinct
-        if (ai < ae) x[ar] = ax + mult * ac;
-        for (int64_t e = ab + 64 + lane; e < ae; e += 64) x[st.rows[e]] += mult * st.coefs[e];
+        if (ai < ae) x[ar] += mult * ac;
+        for (int64_t e = ai + 64; e < ae; e += 64) x[rows[e]] += mult * coefs[e];
       }
       sd_sync();
     }
+  }
+}
+SD_INLINE void r1_dense_steps(Lp& s, f64* x, int first, int count, bool left) {
+  if (count <= 0) return;
+  if (f64* staged = sd_stage_in(s.lds, s.lds_doubles, x, s.m)) {
+    r1_dense_run(s, SD_L(f64, staged), first, count, left);
+    sd_stage_out(staged, x, s.m);
+  } else {
+    r1_dense_run(s, SD_G(f64, x), first, count, left);
   }
 }
 #else
@@ -1252,7 +1455,7 @@ SD_INLINE void r1_right_solve_nz(Lp& s, Vec& d) {
       r1_dense_steps(s, d.values, i, s.r1_count - i, false);
       break;
     }
-    const f64 mult = -col_dot_par(s.storage, s.r1_v[i], d.values) / s.r1_mu[i];
+    const f64 mult = -col_dot_par(s.storage, s.r1_v[i], d.values, s.lds_scratch) / s.r1_mu[i];
     if (mult != 0.0) col_add_scattered(s.storage, s.r1_u[i], mult, d);
     use_dense = vec_dense(d, 0.05);
   }
@@ -1277,7 +1480,7 @@ SD_INLINE void r1_left_solve_nz(Lp& s, Vec& y) {
       r1_dense_steps(s, y.values, i, i + 1, true);
       break;
     }
-    const f64 mult = -col_dot_par(s.storage, s.r1_u[i], y.values) / s.r1_mu[i];
+    const f64 mult = -col_dot_par(s.storage, s.r1_u[i], y.values, s.lds_scratch) / s.r1_mu[i];
     if (mult != 0.0) col_add_scattered(s.storage, s.r1_v[i], mult, y);
     use_dense = vec_dense(y, 0.05);
   }
@@ -1302,7 +1505,7 @@ SD_INLINE void bf_right_solve(Lp& s, Vec& d) {
 // LeftSolveUWithNonZeros (lu_factorization.cc:298-312)
 SD_INLINE void lu_left_solve_u_with_nz(Lp& s, Vec& y) {
   if (s.is_identity) return;
-  tri_rows_to_consider(s.tupper, y.nz, &y.nnz, s.stored);
+  { SdSubTimer t_x_(&s.phase_ticks[16]); tri_rows_to_consider(s.tupper, y.nz, &y.nnz, s.stored); }
   y.sorted = 1;
   if (y.nnz == 0) {
     {
@@ -1310,7 +1513,7 @@ SD_INLINE void lu_left_solve_u_with_nz(Lp& s, Vec& y) {
       tri_transpose_upper_solve(s.upper, y.values, s.lds, s.lds_doubles);
     }
   } else {
-    tri_transpose_hyper_solve(s.upper, y.values, y.nz, &y.nnz);
+    { SdSubTimer t_x_(&s.phase_ticks[17]); tri_transpose_hyper_solve(s.upper, y.values, y.nz, &y.nnz); }
   }
 }
 // BasisFactorization::LeftSolve (basis_representation.cc:342-356, MPF)
@@ -1332,15 +1535,15 @@ SD_INLINE f64 bf_dual_edge_squared_norm(Lp& s, int row) {
   f64* z = s.zero_scratch;
   z[pr] = 1.0;
   nz[nnz++] = pr;
-  tri_rows_to_consider(s.tupper, nz, &nnz, s.stored);
+  { SdSubTimer t_x_(&s.phase_ticks[16]); tri_rows_to_consider(s.tupper, nz, &nnz, s.stored); }
   if (nnz == 0) {
     {
       SdSubTimer t_(&s.phase_ticks[9]);
       tri_lower_solve_from(s.tupper, pr, z);
     }
   } else {
-    tri_hyper_solve(s.tupper, z, nz, &nnz);
-    tri_rows_to_consider(s.tlower, nz, &nnz, s.stored);
+    { SdSubTimer t_x_(&s.phase_ticks[17]); tri_hyper_solve(s.tupper, z, nz, &nnz); }
+    { SdSubTimer t_x_(&s.phase_ticks[16]); tri_rows_to_consider(s.tlower, nz, &nnz, s.stored); }
   }
   if (nnz == 0) {
     {
@@ -1348,7 +1551,7 @@ SD_INLINE f64 bf_dual_edge_squared_norm(Lp& s, int row) {
       tri_upper_solve(s.tlower, z);
     }
   } else {
-    tri_hyper_solve_rev(s.tlower, z, nz, &nnz);
+    { SdSubTimer t_x_(&s.phase_ticks[17]); tri_hyper_solve_rev(s.tlower, z, nz, &nnz); }
   }
   f64 sum = 0.0;
   if (nnz == 0) {
@@ -1363,6 +1566,7 @@ SD_INLINE f64 bf_dual_edge_squared_norm(Lp& s, int row) {
   return sum;
 }
 SD_INLINE const f64* bf_right_solve_for_tau(Lp& s, const Vec& a) {
+  SdSubTimer t_sub_(&s.phase_ticks[30]);
   if (s.tau_can_opt) {
     s.tau_can_opt = 0;
     lu_right_solve_l_permuted_input(s, s.tau);
@@ -1381,9 +1585,9 @@ SD_INLINE void bf_left_solve_for_unit_row(Lp& s, int j, Vec& y) {
   if (s.left_pool[j] == kInvalid) {
     const int start = lu_left_solve_u_unit_row(s, j, y);
     if (y.nnz == 0) {
-      s.left_pool[j] = store_add_dense_prefix(s.storage, y.values, y.size, start);
+      { SdSubTimer t_x_(&s.phase_ticks[18]); s.left_pool[j] = store_add_dense_prefix(s.storage, y.values, y.size, start); }
     } else {
-      s.left_pool[j] = store_add_dense_nz(s.storage, y.values, y.size, y.nz, y.nnz);
+      { SdSubTimer t_x_(&s.phase_ticks[18]); s.left_pool[j] = store_add_dense_nz(s.storage, y.values, y.size, y.nz, y.nnz); }
     }
   } else {
     store_copy_to_vec(s.storage, s.left_pool[j], y);
@@ -1404,10 +1608,10 @@ SD_INLINE void bf_right_solve_for_column(Lp& s, int col, Vec& d) {
   lu_right_solve_l_for_column(s, col, d);
   r1_right_solve_nz(s, d);
   if (d.nnz == 0) {
-    s.right_pool[col] = store_add_dense_prefix(s.right_storage, d.values, d.size, 0);
+    { SdSubTimer t_x_(&s.phase_ticks[18]); s.right_pool[col] = store_add_dense_prefix(s.right_storage, d.values, d.size, 0); }
   } else {
     sort_distinct(d.nz, d.nnz, d.size, s.stored);
-    s.right_pool[col] = store_add_dense_nz(s.right_storage, d.values, d.size, d.nz, d.nnz);
+    { SdSubTimer t_x_(&s.phase_ticks[18]); s.right_pool[col] = store_add_dense_nz(s.right_storage, d.values, d.size, d.nz, d.nnz); }
   }
   lu_right_solve_u_with_nz(s, d);
   vec_sort_if_needed(d, s.stored);
@@ -1499,7 +1703,7 @@ SD_INLINE void dp_update_top_k(Lp& s, int position, f64 value) {
 SD_INLINE void dp_clear_and_resize(Lp& s, int n) {
   s.dp_ntops = 0;
   s.dp_threshold = -sd_inf();
-  for (int i = s.dp_size; i < n; ++i) s.dp_values[i] = 0.0;
+  for (int i = s.dp_size + sd_lane(); i < n; i += sd_lanes()) s.dp_values[i] = 0.0;
   s.dp_size = n;
   const int words = (n + 63) / 64;
   for (int w = sd_lane(); w < words; w += sd_lanes()) s.dp_cand[w] = 0;
@@ -1525,6 +1729,7 @@ SD_INLINE int dp_randomize(Lp& s, int best, int n_equiv) {
   return s.dp_equiv[uniform_int(s, n_equiv - 1)];
 }
 SD_INLINE int dp_get_maximum(Lp& s) {
+  SdSubTimer t_sub_(&s.phase_ticks[27]);
   f64 best_value = -sd_inf();
   int best_position = -1;
   int n_equiv = 0;
@@ -1644,6 +1849,7 @@ SD_INLINE void vv_update_dual_price(Lp& s, int row) {
 }
 // UpdateDualPrices(rows); the caller guarantees the norms are current.
 SD_INLINE void vv_update_dual_prices(Lp& s, const int32_t* rows, int n) {
+  SdSubTimer t_sub_(&s.phase_ticks[19]);
   if (s.dp_size != s.m) {
     vv_recompute_dual_prices(s, s.put_more_importance_on_norm);
     return;
@@ -1724,17 +1930,21 @@ SD_INLINE void vv_update_given_nonbasic(Lp& s, const int32_t* cols, int n) {
   vec_clear_nz_if_too_dense(v, 0.8);
   bf_right_solve(s, v);
   if (v.nnz == 0) {
-    for (int row = 0; row < s.m; ++row) s.x[s.basis[row]] -= v.values[row];
-    for (int row = 0; row < s.m; ++row) v.values[row] = 0.0;
+    for (int row = sd_lane(); row < s.m; row += sd_lanes()) {  // distinct basic columns
+      s.x[s.basis[row]] -= v.values[row];
+      v.values[row] = 0.0;
+    }
+    sd_sync();
     v.size = s.m;
     vv_recompute_dual_prices(s, 0);  // RecomputeDualPrices() default argument
     return;
   }
-  for (int k = 0; k < v.nnz; ++k) {
+  for (int k = sd_lane(); k < v.nnz; k += sd_lanes()) {  // distinct rows
     const int row = v.nz[k];
     s.x[s.basis[row]] -= v.values[row];
     v.values[row] = 0.0;
   }
+  sd_sync();
   vv_update_dual_prices(s, v.nz, v.nnz);
   v.nnz = 0;
 }
@@ -1782,6 +1992,7 @@ SD_INLINE void ur_compute_unit_row_left_inverse(Lp& s, int leaving_row) {
   bf_left_solve_for_unit_row(s, leaving_row, s.rho);
 }
 SD_INLINE void ur_row_wise(Lp& s) {
+  SdSubTimer t_sub_(&s.phase_ticks[28]);
   sd_fill<f64>(s.coeff, s.N, 0.0);
   // Rows in list order; a row's entries are distinct positions, so they are
   // split over the lanes (each position keeps its row-by-row order).
@@ -1803,6 +2014,7 @@ SD_INLINE void ur_row_wise(Lp& s) {
 // row's positions over the lanes); touched positions are flagged in col_flag
 // (bytes, so that lanes never share a word) and cleared after the list.
 SD_INLINE void ur_row_wise_hypersparse(Lp& s) {
+  SdSubTimer t_sub_(&s.phase_ticks[28]);
   for (int k = 0; k < s.n_rho_filtered; ++k) {
     const int col = s.rho_filtered[k];
     const f64 mult = s.rho.values[col];
@@ -1845,6 +2057,7 @@ SD_INLINE void ur_row_wise_hypersparse(Lp& s) {
   sd_sync();
 }
 SD_INLINE void ur_single_row(Lp& s, int row_as_col) {
+  SdSubTimer t_sub_(&s.phase_ticks[28]);
   const f64 drop = s.drop_tolerance;
   const f64 mult = s.rho.values[row_as_col];
   const int64_t b = s.At.starts[row_as_col];
@@ -1867,6 +2080,7 @@ SD_INLINE void ur_single_row(Lp& s, int row_as_col) {
       [&](int k) { return rows[k]; });
 }
 SD_INLINE void ur_column_wise(Lp& s) {
+  SdSubTimer t_sub_(&s.phase_ticks[28]);
   s.n_nzpos = 0;
   const f64 drop = s.drop_tolerance;
   // The dots, one column per lane (a word of the relevance mask per lane);
@@ -1898,6 +2112,7 @@ SD_INLINE void ur_compute_update_row(Lp& s, int leaving_row) {
   s.urow_for = leaving_row;
   ur_compute_unit_row_left_inverse(s, leaving_row);
   if (s.use_transposed_matrix) {
+    SdSubTimer t_x_(&s.phase_ticks[29]);
     const f64 drop = s.drop_tolerance;
     const f64* rho = s.rho.values;
     const int32_t* rho_nz = s.rho.nz;
@@ -2070,7 +2285,11 @@ SD_INLINE void ent_dual_choose(Lp& s, bool nothing_to_recompute, f64 cost_variat
 // ---- DualEdgeNorms (dual_edge_norms.cc:49-118) ----
 SD_INLINE bool den_test_precision(Lp& s, int leaving_row) {
   if (s.norms_recompute) return true;
-  const f64 leaving = vec_squared_norm(s.rho);
+  f64 leaving;
+  {
+    SdSubTimer t_x_(&s.phase_ticks[21]);
+    leaving = vec_squared_norm(s.rho);
+  }
   const f64 old = s.norms[leaving_row];
   const f64 acc = (sd_sqrt(leaving) - sd_sqrt(old)) / sd_sqrt(leaving);
   if (sd_fabs(acc) > s.recompute_edges_norm_threshold) s.norms_recompute = 1;
@@ -2082,6 +2301,7 @@ SD_INLINE void den_update_before_pivot(Lp& s, int leaving_row) {
   const f64* tau = bf_right_solve_for_tau(s, s.rho);
   const f64 pivot = s.dir.values[leaving_row];
   const f64 new_leaving = s.norms[leaving_row] / sq(pivot);
+  SdSubTimer t_x_(&s.phase_ticks[24]);
   // Element-wise over the direction's distinct rows: split over the lanes.
   for (int k = sd_lane(); k < s.dir.nnz; k += sd_lanes()) {
     const int row = s.dir.nz[k];
@@ -2118,6 +2338,7 @@ SD_INLINE void rc_update_before_pivot(Lp& s, int entering_col, int leaving_row) 
       s.rc_precise = 0;
       ur_compute_update_row(s, leaving_row);
       const f64 new_leaving_rc = entering_rc / -s.dir.values[leaving_row];
+      SdSubTimer t_x_(&s.phase_ticks[23]);
       for (int k = sd_lane(); k < s.n_nzpos; k += sd_lanes()) {  // distinct positions
         const int col = s.nzpos[k];
         s.rc[col] += new_leaving_rc * s.coeff[col];
@@ -2158,6 +2379,7 @@ SD_INLINE void rs_compute_direction(Lp& s, int col) {
   s.dir_inf_norm = sd_wave_max(norm);
 }
 SD_INLINE void rs_make_boxed_dual_feasible(Lp& s) {
+  SdSubTimer t_sub_(&s.phase_ticks[31]);
   int n_changed = 0;
   const f64 threshold = s.dual_tol;
   for (int k = 0; k < s.n_flips; ++k) {
@@ -2195,17 +2417,19 @@ SD_INLINE void rc_clear_and_remove_cost_shifts(Lp& s) {
   rc_set_recompute_and_notify(s);
 }
 SD_INLINE void rc_compute_basic_objective(Lp& s) {
-  for (int row = 0; row < s.m; ++row) {
+  for (int row = sd_lane(); row < s.m; row += sd_lanes()) {
     const int bc = s.basis[row];
     s.basic_obj[row] = s.objective[bc] + s.cost_pert[bc];
   }
+  sd_sync();
   s.recompute_bo = 0;
   s.recompute_bo_left_inverse = 1;
 }
 SD_INLINE void rc_compute_basic_objective_left_inverse(Lp& s) {
   if (s.recompute_bo) rc_compute_basic_objective(s);
   Vec& y = s.bolinv;
-  for (int row = 0; row < s.m; ++row) y.values[row] = s.basic_obj[row];
+  for (int row = sd_lane(); row < s.m; row += sd_lanes()) y.values[row] = s.basic_obj[row];
+  sd_sync();
   y.size = s.m;
   y.nnz = 0;
   bf_left_solve(s, y);
@@ -2219,11 +2443,13 @@ SD_INLINE void rc_compute_reduced_costs(Lp& s) {
     s.rc[col] = s.objective[col] + s.cost_pert[col] - col_dot(s.A, col, y);
   }
   sd_sync();
-  for (int col = 0; col < s.N; ++col) {
+  // A maximum of absolute values: exact in any order.
+  for (int col = sd_lane(); col < s.N; col += sd_lanes()) {
     if (bit_get(s.is_basic, col)) {
       dual_residual_error = sd_max(dual_residual_error, sd_fabs(s.rc[col]));
     }
   }
+  dual_residual_error = sd_wave_max(dual_residual_error);
   s.rc_dtime += dt_ops(s.a_num_entries);
   s.recompute_rc = 0;
   s.rc_recomputed = 1;
@@ -2358,20 +2584,28 @@ SD_INLINE int sd_refactorize(Lp& s, int bump) {
 
 // PermuteBasis (revised_simplex.cc:2475-2502)
 SD_INLINE void rs_permute_basis(Lp& s) {
+  SdSubTimer t_sub_(&s.phase_ticks[22]);
   if (s.col_perm_empty) return;
+  // col_perm is a permutation: every loop writes distinct positions.
   int32_t* tmp = s.changed_cols;
-  for (int i = 0; i < s.m; ++i) tmp[s.col_perm[i]] = s.basis[i];
-  for (int i = 0; i < s.m; ++i) s.basis[i] = tmp[i];
+  for (int i = sd_lane(); i < s.m; i += sd_lanes()) tmp[s.col_perm[i]] = s.basis[i];
+  sd_sync();
+  for (int i = sd_lane(); i < s.m; i += sd_lanes()) s.basis[i] = tmp[i];
+  sd_sync();
   f64* ftmp = s.bp_ratio;
   if (s.dpv_size != 0) {
-    for (int i = 0; i < s.m; ++i) ftmp[s.col_perm[i]] = s.dpv[i];
-    for (int i = 0; i < s.m; ++i) s.dpv[i] = ftmp[i];
+    for (int i = sd_lane(); i < s.m; i += sd_lanes()) ftmp[s.col_perm[i]] = s.dpv[i];
+    sd_sync();
+    for (int i = sd_lane(); i < s.m; i += sd_lanes()) s.dpv[i] = ftmp[i];
+    sd_sync();
   }
   s.recompute_bo = 1;
   s.recompute_bo_left_inverse = 1;
   if (!s.norms_recompute) {
-    for (int i = 0; i < s.m; ++i) ftmp[s.col_perm[i]] = s.norms[i];
-    for (int i = 0; i < s.m; ++i) s.norms[i] = ftmp[i];
+    for (int i = sd_lane(); i < s.m; i += sd_lanes()) ftmp[s.col_perm[i]] = s.norms[i];
+    sd_sync();
+    for (int i = sd_lane(); i < s.m; i += sd_lanes()) s.norms[i] = ftmp[i];
+    sd_sync();
   }
   s.col_perm_empty = 1;
 }
@@ -2419,7 +2653,8 @@ SD_INLINE void vv_recompute_basic_values(Lp& s) {
   }
   sd_sync();
   bf_right_solve(s, v);
-  for (int row = 0; row < s.m; ++row) s.x[s.basis[row]] = v.values[row];
+  for (int row = sd_lane(); row < s.m; row += sd_lanes()) s.x[s.basis[row]] = v.values[row];
+  sd_sync();
   dp_clear_and_resize(s, 0);  // dual_prices_->Clear()
 }
 // PreciseScalarProduct(objective_, variable_values_) (lp_utils.h:106-114)
@@ -2496,6 +2731,7 @@ SD_INLINE int32_t sd_run(Lp& s) {
       }
       s.refactorize = 0;
       if (s.num_updates == 0) {
+        SdSubTimer t_x_(&s.phase_ticks[20]);
         if (old_refactorize) rc_make_precise(s);
         rs_make_boxed_dual_feasible_all(s);
         vv_recompute_basic_values(s);
@@ -2584,11 +2820,14 @@ SD_INLINE int32_t sd_run(Lp& s) {
     SD_PHASE(7);
     // ComputeStepToMoveBasicVariableToBound + UpdateOnPivoting
     const f64 primal_step = (s.x[lcol] - target_bound) / s.dir.values[leaving_row];
-    for (int k = sd_lane(); k < s.dir.nnz; k += sd_lanes()) {  // distinct basic columns
-      const int row = s.dir.nz[k];
-      s.x[s.basis[row]] -= s.dir.values[row] * primal_step;
+    {
+      SdSubTimer t_x_(&s.phase_ticks[25]);
+      for (int k = sd_lane(); k < s.dir.nnz; k += sd_lanes()) {  // distinct basic columns
+        const int row = s.dir.nz[k];
+        s.x[s.basis[row]] -= s.dir.values[row] * primal_step;
+      }
+      sd_sync();
     }
-    sd_sync();
     s.x[entering_col] += primal_step;
     // UpdateAndPivot (:2504-2575)
     const f64 pivot_from_update_row = s.coeff[entering_col];  // IsComputedFor(leaving_row)
@@ -2617,17 +2856,32 @@ SD_INLINE int32_t sd_run(Lp& s) {
         refactor = 1;
       } else {
         // MiddleProductFormUpdate (:258-302)
-        for (int64_t i = s.right_storage.starts[right_index];
-             i < s.right_storage.starts[right_index + 1]; ++i) {
-          s.mpf_scratch[s.right_storage.rows[i]] = s.right_storage.coefs[i];
-          s.mpf_scratch_nz[s.n_mpf_scratch_nz++] = s.right_storage.rows[i];
+        SdSubTimer t_x_(&s.phase_ticks[26]);
+        // Each column's rows are distinct: the lanes split them; the list
+        // entries keep their positions (right column, then U's column).
+        {
+          const int64_t rb = s.right_storage.starts[right_index];
+          const int rn = static_cast<int>(s.right_storage.starts[right_index + 1] - rb);
+          const int base = s.n_mpf_scratch_nz;
+          for (int k = sd_lane(); k < rn; k += sd_lanes()) {
+            const int r = s.right_storage.rows[rb + k];
+            s.mpf_scratch[r] = s.right_storage.coefs[rb + k];
+            s.mpf_scratch_nz[base + k] = r;
+          }
+          sd_sync();
+          s.n_mpf_scratch_nz = base + rn;
         }
         lu_column_of_u(s, leaving_row);
-        for (int k = 0; k < s.n_col_u; ++k) {
-          s.mpf_scratch[s.col_u_rows[k]] -= s.col_u_coefs[k];
-          s.mpf_scratch_nz[s.n_mpf_scratch_nz++] = s.col_u_rows[k];
+        {
+          const int base = s.n_mpf_scratch_nz;
+          for (int k = sd_lane(); k < s.n_col_u; k += sd_lanes()) {
+            s.mpf_scratch[s.col_u_rows[k]] -= s.col_u_coefs[k];
+            s.mpf_scratch_nz[base + k] = s.col_u_rows[k];
+          }
+          sd_sync();
+          s.n_mpf_scratch_nz = base + s.n_col_u;
         }
-        const f64 scalar_product = col_dot(s.storage, left_index, s.mpf_scratch);
+        const f64 scalar_product = col_dot_par(s.storage, left_index, s.mpf_scratch, s.lds_scratch);
         const int u_index =
             store_add_and_clear(s.storage, s.mpf_scratch, s.mpf_scratch_nz, &s.n_mpf_scratch_nz);
         const f64 mu = 1.0 + scalar_product;

@@ -25,15 +25,18 @@ inline hipStream_t Stream(void* p) { return reinterpret_cast<hipStream_t>(p); }
 }  // namespace
 
 // Dynamic LDS of a segment workgroup: the staged dense vector of the
-// triangular sweeps (32 KB: five workgroups per CU keep the 1 024-group pool
-// resident).
+// triangular sweeps and rank-one products (32 KB), then the reduction and
+// metadata scratch (SdScratch, 4.5 KB): four workgroups per CU keep the
+// 1 024-group pool resident.
 constexpr int kLdsDoubles = 4096;
+constexpr int kLdsTotalDoubles = kLdsDoubles + sdual::kSdScratchDoubles;
 extern __shared__ double sd_lds[];
 
 // One thread walks Glop's loop; the header lives in the arena.
 __global__ __launch_bounds__(64) void sdual_segment_kernel(sdual::Lp* lp) {
   lp->lds = sd_lds;
   lp->lds_doubles = kLdsDoubles;
+  lp->lds_scratch = sd_lds + kLdsDoubles;
   sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
 }
 
@@ -197,6 +200,7 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring
     lp->phase_ticks[13] += wall_clock64() - t_claim;  // staging image in
     lp->lds = sd_lds;
     lp->lds_doubles = kLdsDoubles;
+    lp->lds_scratch = sd_lds + kLdsDoubles;
     sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
     const uint64_t t_out = wall_clock64();
     if (threadIdx.x == 0) {
@@ -359,7 +363,7 @@ class SdualPool {
       throw DeviceError("sdual pool: ring reset failed");
     }
     __atomic_store_n(&q_->stop, 0, __ATOMIC_RELEASE);
-    hipLaunchKernelGGL(sdual_pool_kernel, dim3(kPoolGroups), dim3(64), kLdsDoubles * sizeof(double), stream_, d_q_, d_ring_,
+    hipLaunchKernelGGL(sdual_pool_kernel, dim3(kPoolGroups), dim3(64), kLdsTotalDoubles * sizeof(double), stream_, d_q_, d_ring_,
                        static_cast<long long>(head_base_), static_cast<long long>(cap_));
     const hipError_t e = hipGetLastError();
     (void)hipSetDevice(prev);
@@ -555,7 +559,7 @@ void DeviceLp::SdualRun(size_t bytes, const double* arena_coeff, int n, void (*s
   Check(hipMemcpyAsync(sdual_arena_, sdual_staging_, bytes, hipMemcpyHostToDevice,
                        Stream(stream_)),
         "sdual H2D");
-  hipLaunchKernelGGL(sdual_segment_kernel, dim3(1), dim3(64), kLdsDoubles * sizeof(double), Stream(stream_),
+  hipLaunchKernelGGL(sdual_segment_kernel, dim3(1), dim3(64), kLdsTotalDoubles * sizeof(double), Stream(stream_),
                      reinterpret_cast<sdual::Lp*>(sdual_arena_));
   Check(hipGetLastError(), "sdual launch");
   // The segment's last update row becomes the device copy that later device

@@ -313,13 +313,16 @@ struct Lp {
   int64_t fixed_end;     // in_end: the LU image's last used byte
   int64_t mutable_end;
   f64* coeff_out;        // DeviceLp's update-row coefficients (N), refreshed at the end
-  // Device time per loop phase (wall_clock64 ticks, 100 MHz): see sd_run.
-  uint64_t phase_ticks[16];
+  // Device time per loop phase (wall_clock64 ticks, 100 MHz): see sd_run
+  // (0-8 loop phases, 9-15 sub-phases and transfers, 16-31 finer
+  // sub-phases, sdual_bridge.inc names them).
+  uint64_t phase_ticks[32];
   // The workgroup's LDS scratch (set by the kernel before sd_run; null on the
   // host): dense vectors of the triangular sweeps are staged there.
   f64* lds;
   int32_t lds_doubles;
   int32_t lds_pad;
+  f64* lds_scratch;  // SdScratch after the staging area (device only)
 
   // ---- loop carry and exit ----
   int refactorize;  // the host loop's `refactorize` flag
