@@ -563,8 +563,24 @@ def main():
     ap.add_argument("--c3-cpu-threads", type=int, default=16)
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` on its own: start the N ranks (one process
+        # per GPU, torch.distributed.run) before anything touches a GPU, as a
+        # child process, and exit with its status.
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+               f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # Rehearsal of the multi-rank path on a one-GPU box: every rank on GPU 0.
     one_gpu = os.environ.get("MILP_BENCH_ONE_GPU") == "1"

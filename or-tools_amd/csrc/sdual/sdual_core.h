@@ -149,6 +149,9 @@ typedef __attribute__((address_space(1))) const int32_t gc_i32;
 typedef __attribute__((address_space(1))) const int64_t gc_i64;
 typedef __attribute__((address_space(1))) const f64 gc_f64;
 typedef __attribute__((address_space(3))) int64_t l_i64;
+// Whether a generic pointer addresses the workgroup's LDS (the solves'
+// working vector lives there, SdLdsVec).
+__device__ inline bool sd_is_lds(const void* p) { return __builtin_amdgcn_is_shared(p); }
 
 
 // ColumnScalarProduct (sparse.h:514-542) of entries [b, e) of a column
@@ -164,8 +167,11 @@ __device__ inline f64 sd_ordered_dot(gc_i32* rows, gc_f64* coefs, int64_t b, int
   const int64_t len = e - b;
   const int64_t body = len & ~int64_t{3};
   f64 acc = 0.0;
-  for (int64_t base = 0; base < body; base += 256) {
-    const int64_t n = body - base < 256 ? body - base : 256;
+  f64 tail[3] = {0.0, 0.0, 0.0};
+  // Rounds of up to 256 entries cover the body and the (up to three) tail
+  // entries; the tail products are read back before the chain sums reuse red.
+  for (int64_t base = 0; base < len; base += 256) {
+    const int64_t n = len - base < 256 ? len - base : 256;
     f64 p[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -176,17 +182,19 @@ __device__ inline f64 sd_ordered_dot(gc_i32* rows, gc_f64* coefs, int64_t b, int
 #pragma unroll
     for (int u = 0; u < 4; ++u) red[u * 64 + lane] = p[u];
     sd_sync();
+    const int64_t nb = body - base < n ? (body - base > 0 ? body - base : 0) : n;
     if (lane < 4) {
-      const int groups = static_cast<int>(n >> 2);
+      const int groups = static_cast<int>(nb >> 2);
       for (int g = 0; g < groups; ++g) acc += red[lane + 4 * g];
     }
+    for (int64_t t = body > base ? body : base; t < base + n; ++t) tail[t - body] = red[t - base];
     sd_sync();
   }
   if (lane < 4) red[lane] = acc;
   sd_sync();
   f64 result = red[0] + red[1] + red[2] + red[3];
   sd_sync();
-  for (int64_t t = body; t < len; ++t) result += coefs[b + t] * x[rows[b + t]];
+  for (int64_t t = body; t < len; ++t) result += tail[t - body];
   return result;
 }
 #endif
@@ -483,9 +491,13 @@ SD_INLINE int64_t col_entries(const M& a, int col) {
 template <typename M>
 SD_INLINE f64 col_dot_par(const M& a, int col, const f64* v, f64* lds_scratch) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  l_f64* red = SD_L(f64, reinterpret_cast<SdScratch*>(lds_scratch)->red);
+  if (sd_is_lds(v)) {
+    return sd_ordered_dot(SD_G(const int32_t, a.rows), SD_G(const f64, a.coefs), a.starts[col],
+                          a.starts[col + 1], SD_L(const f64, v), red);
+  }
   return sd_ordered_dot(SD_G(const int32_t, a.rows), SD_G(const f64, a.coefs), a.starts[col],
-                        a.starts[col + 1], SD_G(const f64, v),
-                        SD_L(f64, reinterpret_cast<SdScratch*>(lds_scratch)->red));
+                        a.starts[col + 1], SD_G(const f64, v), red);
 #else
   (void)lds_scratch;
   return col_dot(a, col, v);
@@ -808,6 +820,9 @@ SD_INLINE void tri_level_sweep_lower(const Tri& t, f64* x, int last) {
 // The dense vector of a level sweep in LDS when it fits: each level then
 // waits on one round trip (its entries) instead of three.
 SD_INLINE f64* sd_stage_in(f64* lds, int cap, const f64* x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (sd_is_lds(x)) return const_cast<f64*>(x);  // already the LDS working vector
+#endif
   if (lds == nullptr || n > cap) return nullptr;
 #if defined(__HIP_DEVICE_COMPILE__)
   l_f64* l = SD_L(f64, lds);
@@ -821,11 +836,16 @@ SD_INLINE f64* sd_stage_in(f64* lds, int cap, const f64* x, int n) {
   return lds;
 }
 SD_INLINE void sd_stage_out(const f64* lds, f64* x, int n) {
+  if (lds == x) return;
 #if defined(__HIP_DEVICE_COMPILE__)
-  const __attribute__((address_space(3))) f64* l = SD_L(const f64, lds);
+  // The staging area is left all zero (the LDS working vector's invariant).
+  l_f64* l = SD_L(f64, const_cast<f64*>(lds));
   g_f64* g = SD_G(f64, x);
 #pragma unroll 8
-  for (int i = sd_lane(); i < n; i += 64) g[i] = l[i];
+  for (int i = sd_lane(); i < n; i += 64) {
+    g[i] = l[i];
+    l[i] = 0.0;
+  }
 #else
   for (int i = sd_lane(); i < n; i += sd_lanes()) x[i] = lds[i];
 #endif
@@ -876,6 +896,10 @@ SD_INLINE void tri_transpose_lower_solve(const Tri& t, f64* x, f64* lds = nullpt
       tri_level_sweep_lower(t, v, last);
 #endif
       sd_stage_out(v, x, last + 1);
+      if (v != x) {  // entries above `last` were read only: clear their staged copies
+        for (int i = last + 1 + sd_lane(); i < t.num_cols; i += sd_lanes()) v[i] = 0.0;
+        sd_sync();
+      }
       return;
     }
     tri_level_sweep_lower(t, x, last);
@@ -1043,6 +1067,41 @@ SD_INLINE int64_t tri_num_entries(const Tri& t) {
 // ---- LuFactorization (lu_factorization.cc:200-454) ----
 // lp_utils.h:240-277. `values` and the zero scratchpad swap buffers.
 SD_INLINE void permute_with_scratchpad(Lp& s, const int32_t* perm, Vec& io) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (sd_is_lds(io.values)) {
+    // The working vector stays in LDS: its values go through the (all-zero)
+    // global scratchpad and come back permuted; the scratchpad ends zero.
+    l_f64* w = SD_L(f64, io.values);
+    g_f64* z = SD_G(f64, s.zero_scratch);
+    gc_i32* pg = SD_G(const int32_t, perm);
+    const int size = io.size;
+    for (int i = sd_lane(); i < size; i += 64) {
+      z[i] = w[i];
+      w[i] = 0.0;
+    }
+    sd_sync();
+    for (int i0 = sd_lane(); i0 < size; i0 += 512) {
+      f64 v[8];
+      int p[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 64 * u;
+        v[u] = i < size ? z[i] : 0.0;
+        p[u] = i < size ? pg[i] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 64 * u;
+        if (v[u] != 0.0) {
+          w[p[u]] = v[u];  // a permutation: distinct targets
+          z[i] = 0.0;
+        }
+      }
+    }
+    sd_sync();
+    return;
+  }
+#endif
   f64* old = io.values;
   io.values = s.zero_scratch;
   s.zero_scratch = old;
@@ -1079,6 +1138,46 @@ SD_INLINE void permute_with_scratchpad(Lp& s, const int32_t* perm, Vec& io) {
   sd_fill<f64>(s.zero_scratch, size, 0.0);
 }
 SD_INLINE void permute_with_known_nz(Lp& s, const int32_t* perm, Vec& io) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (sd_is_lds(io.values)) {
+    // In LDS: every listed value is read (into the global scratchpad, at its
+    // position) and cleared before any is written at its permuted position.
+    l_f64* w = SD_L(f64, io.values);
+    g_f64* z = SD_G(f64, s.zero_scratch);
+    gc_i32* pg = SD_G(const int32_t, perm);
+    __attribute__((address_space(1))) int32_t* nz = SD_G(int32_t, io.nz);
+    const int n = io.nnz;
+    for (int k = sd_lane(); k < n; k += 64) {
+      const int ref = nz[k];
+      z[ref] = w[ref];
+      w[ref] = 0.0;
+    }
+    sd_sync();
+    for (int k0 = sd_lane(); k0 < n; k0 += 256) {
+      int ref[4], p[4];
+      f64 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ref[u] = k0 + 64 * u < n ? nz[k0 + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (ref[u] >= 0) {
+          v[u] = z[ref[u]];
+          p[u] = pg[ref[u]];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (ref[u] >= 0) {
+          z[ref[u]] = 0.0;
+          w[p[u]] = v[u];
+          nz[k0 + 64 * u] = p[u];
+        }
+      }
+    }
+    sd_sync();
+    return;
+  }
+#endif
   f64* old = io.values;
   io.values = s.zero_scratch;
   s.zero_scratch = old;
@@ -1362,18 +1461,84 @@ SD_INLINE int64_t lu_number_of_entries(const Lp& s) {
 
 // ---- RankOneUpdateFactorization (rank_one_update.h:30-246) ----
 #if defined(__HIP_DEVICE_COMPILE__)
-// Dense steps k = 0 .. count-1 of a solve: update i = first + k (right
-// solves) or first - k (left solves), x += mult * add_col with
-// mult = -(dot_col . x) / mu (right: dot v_i, add u_i; left: dot u_i, add
-// v_i). Lane k of a 64-step chunk stages step k's column bounds and mu in
-// LDS; a step prefetches the add column's first 64 entries, takes the dot
-// with ColumnScalarProduct's chains (sd_ordered_dot) and scatters the add
-// column (its rows are distinct) over the lanes. x is staged in LDS for the
-// whole solve when it fits.
+// ColumnScalarProduct as sd_ordered_dot, with the column's first 256
+// entries already in registers (pr/pc: entry base + 64u + lane).
 template <typename XP>
-__device__ inline void r1_dense_run(const Lp& s, XP x, int first, int count, bool left) {
+__device__ inline f64 sd_ordered_dot_pf(gc_i32* rows, gc_f64* coefs, int64_t b, int64_t e, XP x,
+                                        l_f64* red, const int* pr, const f64* pc) {
+  const int lane = sd_lane();
+  const int64_t len = e - b;
+  const int64_t body = len & ~int64_t{3};
+  f64 acc = 0.0;
+  f64 tail[3] = {0.0, 0.0, 0.0};
+  for (int64_t base = 0; base < len; base += 256) {
+    const int64_t n = len - base < 256 ? len - base : 256;
+    f64 p[4];
+    if (base == 0) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p[u] = u * 64 + lane < n ? pc[u] * x[pr[u]] : 0.0;
+    } else {
+      int r[4];
+      f64 c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t k = b + base + u * 64 + lane;
+        const bool in = u * 64 + lane < n;
+        r[u] = in ? rows[k] : 0;
+        c[u] = in ? coefs[k] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p[u] = u * 64 + lane < n ? c[u] * x[r[u]] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) red[u * 64 + lane] = p[u];
+    sd_sync();
+    const int64_t nb = body - base < n ? (body - base > 0 ? body - base : 0) : n;
+    if (lane < 4) {
+      const int groups = static_cast<int>(nb >> 2);
+      for (int g = 0; g < groups; ++g) acc += red[lane + 4 * g];
+    }
+    for (int64_t t = body > base ? body : base; t < base + n; ++t) tail[t - body] = red[t - base];
+    sd_sync();
+  }
+  if (lane < 4) red[lane] = acc;
+  sd_sync();
+  f64 result = red[0] + red[1] + red[2] + red[3];
+  sd_sync();
+  for (int64_t t = body; t < len; ++t) result += tail[t - body];
+  return result;
+}
+// The first entries of step k's columns (k's bounds staged in meta).
+__device__ inline void r1_fetch(l_i64* meta, int k, gc_i32* rows, gc_f64* coefs, int* pr, f64* pc,
+                                int* ar, f64* ac) {
+  const int lane = sd_lane();
+  const int64_t db = meta[4 * k], de = meta[4 * k + 1];
+  const int64_t ab = meta[4 * k + 2], ae = meta[4 * k + 3];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = db + 64 * u + lane;
+    pr[u] = i < de ? rows[i] : 0;
+    pc[u] = i < de ? coefs[i] : 0.0;
+  }
+  *ar = ab + lane < ae ? rows[ab + lane] : 0;
+  *ac = ab + lane < ae ? coefs[ab + lane] : 0.0;
+}
+// Steps k = 0 .. count-1 of a rank-one solve (RankOneUpdateFactorization::
+// RightSolveWithNonZeros / LeftSolveWithNonZeros, rank_one_update.h:196-246):
+// update i = first + k (right) or first - k (left), x += mult * add_col with
+// mult = -(dot_col . x) / mu (right: dot v_i, add u_i; left: dot u_i, add
+// v_i). While the vector is sparse (dense == false) the add is Glop's
+// scattered add (new positions join the list in entry order, the mask marks
+// them) and the 5% density test follows every step; once dense, plain adds
+// for the remaining steps. A 64-step chunk's column bounds and mu are staged
+// in LDS; the next step's first 256 dot entries and 64 add entries are
+// loaded while the current step computes.
+template <typename XP>
+__device__ inline void r1_run_dev(Lp& s, Vec& d, XP x, int first, int count, bool left,
+                                  bool dense) {
   const Store& st = s.storage;
   const int lane = sd_lane();
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   SdScratch* sc = reinterpret_cast<SdScratch*>(s.lds_scratch);
   l_f64* red = SD_L(f64, sc->red);
   l_i64* meta = SD_L(int64_t, sc->meta);
@@ -1397,34 +1562,75 @@ __device__ inline void r1_dense_run(const Lp& s, XP x, int first, int count, boo
     }
     sd_sync();
     const int steps = count - c0 < 64 ? count - c0 : 64;
+    int pr[4], ar;
+    f64 pc[4], ac;
+    r1_fetch(meta, 0, rows, coefs, pr, pc, &ar, &ac);
     for (int k = 0; k < steps; ++k) {
       const int64_t db = meta[4 * k], de = meta[4 * k + 1];
       const int64_t ab = meta[4 * k + 2], ae = meta[4 * k + 3];
       const f64 mu = mus[k];
-      const int64_t ai = ab + lane;
-      int ar = 0;
-      f64 ac = 0.0;
-      if (ai < ae) {
-        ar = rows[ai];
-        ac = coefs[ai];
-      }
-      const f64 dot = sd_ordered_dot(rows, coefs, db, de, x, red);
+      int nr[4] = {0, 0, 0, 0}, nar = 0;
+      f64 nc[4] = {0.0, 0.0, 0.0, 0.0}, nac = 0.0;
+      if (k + 1 < steps) r1_fetch(meta, k + 1, rows, coefs, nr, nc, &nar, &nac);
+      const f64 dot = sd_ordered_dot_pf(rows, coefs, db, de, x, red, pr, pc);
       const f64 mult = -dot / mu;
-      if (mult != 0.0) {  // col_add_dense: a column's rows are distinct
-        if (ai < ae) x[ar] += mult * ac;
-        for (int64_t e = ai + 64; e < ae; e += 64) x[rows[e]] += mult * coefs[e];
+      if (mult != 0.0) {
+        if (dense) {  // col_add_dense: a column's rows are distinct
+          if (ab + lane < ae) x[ar] += mult * ac;
+          for (int64_t e0 = ab + 64 + lane; e0 < ae; e0 += 256) {
+            int r[4];
+            f64 c[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int64_t e = e0 + 64 * u;
+              r[u] = e < ae ? rows[e] : 0;
+              c[u] = e < ae ? coefs[e] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (e0 + 64 * u < ae) x[r[u]] += mult * c[u];
+            }
+          }
+        } else {  // col_add_scattered (sparse.h:403-413)
+          int nnz = d.nnz;
+          for (int64_t base = ab; base < ae; base += 64) {
+            const int64_t i = base + lane;
+            bool fresh = false;
+            int row = 0;
+            if (i < ae) {
+              row = base == ab ? ar : rows[i];
+              const f64 value = mult * (base == ab ? ac : coefs[i]);
+              x[row] += value;
+              fresh = !d.mask[row] && value != 0.0;
+              if (fresh) d.mask[row] = 1;
+            }
+            const uint64_t fresh_mask = __ballot(fresh);
+            if (fresh) d.nz[nnz + __popcll(fresh_mask & below)] = row;
+            nnz += __popcll(fresh_mask);
+          }
+          sd_sync();
+          if (nnz != d.nnz) d.sorted = 0;
+          d.nnz = nnz;
+        }
       }
+      if (!dense) dense = vec_dense(d, 0.05);
       sd_sync();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        pr[u] = nr[u];
+        pc[u] = nc[u];
+      }
+      ar = nar;
+      ac = nac;
     }
   }
 }
-SD_INLINE void r1_dense_steps(Lp& s, f64* x, int first, int count, bool left) {
+SD_INLINE void r1_run(Lp& s, Vec& d, int first, int count, bool left, bool dense) {
   if (count <= 0) return;
-  if (f64* staged = sd_stage_in(s.lds, s.lds_doubles, x, s.m)) {
-    r1_dense_run(s, SD_L(f64, staged), first, count, left);
-    sd_stage_out(staged, x, s.m);
+  if (sd_is_lds(d.values)) {
+    r1_run_dev(s, d, SD_L(f64, d.values), first, count, left, dense);
   } else {
-    r1_dense_run(s, SD_G(f64, x), first, count, left);
+    r1_run_dev(s, d, SD_G(f64, d.values), first, count, left, dense);
   }
 }
 #else
@@ -1438,6 +1644,32 @@ SD_INLINE void r1_dense_steps(Lp& s, f64* x, int first, int count, bool left) {
   }
 }
 #endif
+#if defined(__HIP_DEVICE_COMPILE__)
+SD_INLINE void r1_right_solve_nz(Lp& s, Vec& d) {
+  SdSubTimer t_(&s.phase_ticks[11]);
+  if (d.nnz == 0) {
+    r1_run(s, d, 0, s.r1_count, false, true);
+  } else {
+    vec_repopulate_mask(d);
+    r1_run(s, d, 0, s.r1_count, false, vec_dense(d, 0.05));
+    vec_clear_mask(d);
+    vec_clear_nz_if_too_dense(d, 0.05);
+  }
+  s.r1_dtime += dt_ops(s.r1_num_entries);
+}
+SD_INLINE void r1_left_solve_nz(Lp& s, Vec& y) {
+  SdSubTimer t_(&s.phase_ticks[11]);
+  if (y.nnz == 0) {
+    r1_run(s, y, s.r1_count - 1, s.r1_count, true, true);
+  } else {
+    vec_repopulate_mask(y);
+    r1_run(s, y, s.r1_count - 1, s.r1_count, true, vec_dense(y, 0.05));
+    vec_clear_mask(y);
+    vec_clear_nz_if_too_dense(y, 0.05);
+  }
+  s.r1_dtime += dt_ops(s.r1_num_entries);
+}
+#else
 SD_INLINE void r1_right_solve_dense(Lp& s, f64* x) {
   r1_dense_steps(s, x, 0, s.r1_count, false);
   s.r1_dtime += dt_ops(s.r1_num_entries);
@@ -1489,6 +1721,60 @@ SD_INLINE void r1_left_solve_nz(Lp& s, Vec& y) {
   s.r1_dtime += dt_ops(s.r1_num_entries);
 }
 
+#endif
+// The working vector of one BasisFactorization solve in LDS (device, when
+// m fits the workgroup's staging area): the vector's values are moved into
+// the LDS buffer for the solve (copy_in) and back into its global buffer at
+// the end, so that every step of the solve (L, rank-one updates, U, their
+// permutes and level sweeps) reads and writes LDS. The solve may hand the
+// buffer to tau (LeftSolveLWithNonZeros' swap) or to the zero scratchpad (a
+// permute's swap); whoever holds it at the end gets the saved global buffer
+// with the same contents. The LDS buffer is all zero between solves.
+struct SdLdsVec {
+  Lp& s;
+  Vec& v;
+  f64* saved = nullptr;
+  SD_HD SdLdsVec(Lp& lp, Vec& vec, bool copy_in) : s(lp), v(vec) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (s.lds == nullptr || s.lds_busy || s.m > s.lds_doubles) return;
+    s.lds_busy = 1;
+    saved = v.values;
+    l_f64* w = SD_L(f64, s.lds);
+    if (copy_in) {
+      gc_f64* g = SD_G(const f64, saved);
+#pragma unroll 8
+      for (int i = sd_lane(); i < s.m; i += 64) w[i] = g[i];
+      sd_sync();
+    }
+    v.values = s.lds;
+#else
+    (void)copy_in;
+#endif
+  }
+  SD_HD ~SdLdsVec() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (saved == nullptr) return;
+    f64* w = s.lds;
+    l_f64* wl = SD_L(f64, w);
+    g_f64* g = SD_G(f64, saved);
+    const int m = s.m;
+    if (s.zero_scratch == w) {  // the buffer is zero (a permute cleared it)
+      for (int i = sd_lane(); i < m; i += 64) g[i] = 0.0;
+      s.zero_scratch = saved;
+    } else {
+      f64** owner = v.values == w ? &v.values : &s.tau.values;
+      for (int i = sd_lane(); i < m; i += 64) {
+        g[i] = wl[i];
+        wl[i] = 0.0;
+      }
+      *owner = saved;
+    }
+    sd_sync();
+    s.lds_busy = 0;
+#endif
+  }
+};
+
 // ---- BasisFactorization (basis_representation.cc:304-624, MPF path) ----
 SD_INLINE void bf_bump(Lp& s, int64_t num_entries) {
   if (s.m == 0) return;
@@ -1496,6 +1782,7 @@ SD_INLINE void bf_bump(Lp& s, int64_t num_entries) {
   s.bf_dtime += density * dt_ops(lu_number_of_entries(s)) + dt_ops(s.r1_num_entries);
 }
 SD_INLINE void bf_right_solve(Lp& s, Vec& d) {
+  SdLdsVec lds_(s, d, true);
   lu_right_solve_l_with_nz(s, d);
   r1_right_solve_nz(s, d);
   lu_right_solve_u_with_nz(s, d);
@@ -1518,6 +1805,7 @@ SD_INLINE void lu_left_solve_u_with_nz(Lp& s, Vec& y) {
 }
 // BasisFactorization::LeftSolve (basis_representation.cc:342-356, MPF)
 SD_INLINE void bf_left_solve(Lp& s, Vec& y) {
+  SdLdsVec lds_(s, y, true);
   lu_left_solve_u_with_nz(s, y);
   r1_left_solve_nz(s, y);
   lu_left_solve_l_with_nz(s, y, nullptr);
@@ -1567,6 +1855,8 @@ SD_INLINE f64 bf_dual_edge_squared_norm(Lp& s, int row) {
 }
 SD_INLINE const f64* bf_right_solve_for_tau(Lp& s, const Vec& a) {
   SdSubTimer t_sub_(&s.phase_ticks[30]);
+  {
+  SdLdsVec lds_(s, s.tau, s.tau_can_opt != 0);
   if (s.tau_can_opt) {
     s.tau_can_opt = 0;
     lu_right_solve_l_permuted_input(s, s.tau);
@@ -1576,11 +1866,13 @@ SD_INLINE const f64* bf_right_solve_for_tau(Lp& s, const Vec& a) {
   }
   r1_right_solve_nz(s, s.tau);
   lu_right_solve_u_with_nz(s, s.tau);
+  }
   s.tau_is_computed = 1;
   bf_bump(s, vec_nnz_estimate(s.tau));
   return s.tau.values;
 }
 SD_INLINE void bf_left_solve_for_unit_row(Lp& s, int j, Vec& y) {
+  SdLdsVec lds_(s, y, false);
   vec_clear_and_resize(y, s.m);
   if (s.left_pool[j] == kInvalid) {
     const int start = lu_left_solve_u_unit_row(s, j, y);
@@ -1604,6 +1896,7 @@ SD_INLINE void bf_left_solve_for_unit_row(Lp& s, int j, Vec& y) {
   bf_bump(s, vec_nnz_estimate(y));
 }
 SD_INLINE void bf_right_solve_for_column(Lp& s, int col, Vec& d) {
+  SdLdsVec lds_(s, d, false);
   vec_clear_and_resize(d, s.m);
   lu_right_solve_l_for_column(s, col, d);
   r1_right_solve_nz(s, d);
@@ -1991,8 +2284,80 @@ SD_INLINE void ur_compute_unit_row_left_inverse(Lp& s, int leaving_row) {
   s.left_inv_for = leaving_row;
   bf_left_solve_for_unit_row(s, leaving_row, s.rho);
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+// The rows of rho_filtered[c0, c0 + 64) staged in LDS for the row-wise
+// update rows: the entry range of row k at meta[4k], meta[4k + 1], its
+// multiplier rho[col] at mus[k].
+__device__ inline int ur_stage_rows(const Lp& s, int c0, l_i64* meta, l_f64* mus) {
+  const int lane = sd_lane();
+  const int n = s.n_rho_filtered - c0 < 64 ? s.n_rho_filtered - c0 : 64;
+  if (lane < n) {
+    const int col = SD_G(const int32_t, s.rho_filtered)[c0 + lane];
+    gc_i64* st = SD_G(const int64_t, s.At.starts);
+    meta[4 * lane] = st[col];
+    meta[4 * lane + 1] = st[col + 1];
+    mus[lane] = SD_G(const f64, s.rho.values)[col];
+  }
+  sd_sync();
+  return n;
+}
+// ComputeUpdatesRowWise (update_row.cc:196-216) with the accumulator in
+// LDS (when N fits the staging area and no solve holds it): zero, then each
+// filtered row's products added in row order (a row's positions are
+// distinct, split over the lanes; the next row's first 64 entries load
+// while the current one adds), then the list and the coefficients out.
+__device__ inline bool ur_row_wise_lds(Lp& s) {
+  if (s.lds == nullptr || s.lds_busy || s.N > s.lds_doubles) return false;
+  SdScratch* sc = reinterpret_cast<SdScratch*>(s.lds_scratch);
+  l_i64* meta = SD_L(int64_t, sc->meta);
+  l_f64* mus = SD_L(f64, sc->mu);
+  l_f64* acc = SD_L(f64, s.lds);  // all zero between uses
+  gc_i32* rows = SD_G(const int32_t, s.At.rows);
+  gc_f64* coefs = SD_G(const f64, s.At.coefs);
+  const int lane = sd_lane();
+  for (int c0 = 0; c0 < s.n_rho_filtered; c0 += 64) {
+    const int n = ur_stage_rows(s, c0, meta, mus);
+    int pr = 0;
+    f64 pc = 0.0;
+    if (meta[0] + lane < meta[1]) {
+      pr = rows[meta[0] + lane];
+      pc = coefs[meta[0] + lane];
+    }
+    for (int k = 0; k < n; ++k) {
+      const int64_t b = meta[4 * k], e = meta[4 * k + 1];
+      const f64 mult = mus[k];
+      int nr = 0;
+      f64 nc = 0.0;
+      if (k + 1 < n && meta[4 * k + 4] + lane < meta[4 * k + 5]) {
+        nr = rows[meta[4 * k + 4] + lane];
+        nc = coefs[meta[4 * k + 4] + lane];
+      }
+      if (b + lane < e) acc[pr] += mult * pc;
+      for (int64_t i = b + 64 + lane; i < e; i += 64) acc[rows[i]] += mult * coefs[i];
+      sd_sync();
+      pr = nr;
+      pc = nc;
+    }
+  }
+  const f64 drop = s.drop_tolerance;
+  const uint64_t* relevant = s.relevant;
+  s.n_nzpos = sd_ordered_compact(s.N, s.nzpos, [&](int col) {
+    return bit_get(relevant, col) && sd_fabs(acc[col]) > drop;
+  });
+  g_f64* coeff = SD_G(f64, s.coeff);
+  for (int i = lane; i < s.N; i += 64) {
+    coeff[i] = acc[i];
+    acc[i] = 0.0;
+  }
+  sd_sync();
+  return true;
+}
+#endif
 SD_INLINE void ur_row_wise(Lp& s) {
   SdSubTimer t_sub_(&s.phase_ticks[28]);
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (ur_row_wise_lds(s)) return;
+#endif
   sd_fill<f64>(s.coeff, s.N, 0.0);
   // Rows in list order; a row's entries are distinct positions, so they are
   // split over the lanes (each position keeps its row-by-row order).
@@ -2013,8 +2378,85 @@ SD_INLINE void ur_row_wise(Lp& s) {
 // The first touch of a position sets it, later ones add (row by row, a
 // row's positions over the lanes); touched positions are flagged in col_flag
 // (bytes, so that lanes never share a word) and cleared after the list.
+#if defined(__HIP_DEVICE_COMPILE__)
+// ComputeUpdatesRowWiseHypersparse (update_row.cc:220-259) with the
+// accumulator and the touch flags in LDS: the first touch of a position
+// sets it, later ones add; only touched positions are written back (the
+// others keep their stale values, as upstream).
+__device__ inline bool ur_row_wise_hyper_lds(Lp& s) {
+  if (s.lds == nullptr || s.lds_busy ||
+      static_cast<int64_t>(s.N) * 9 > static_cast<int64_t>(s.lds_doubles) * 8) {
+    return false;
+  }
+  SdScratch* sc = reinterpret_cast<SdScratch*>(s.lds_scratch);
+  l_i64* meta = SD_L(int64_t, sc->meta);
+  l_f64* mus = SD_L(f64, sc->mu);
+  l_f64* acc = SD_L(f64, s.lds);  // all zero between uses
+  __attribute__((address_space(3))) char* flag = SD_L(char, s.lds + s.N);
+  gc_i32* rows = SD_G(const int32_t, s.At.rows);
+  gc_f64* coefs = SD_G(const f64, s.At.coefs);
+  const int lane = sd_lane();
+  for (int c0 = 0; c0 < s.n_rho_filtered; c0 += 64) {
+    const int n = ur_stage_rows(s, c0, meta, mus);
+    int pr = 0;
+    f64 pc = 0.0;
+    if (meta[0] + lane < meta[1]) {
+      pr = rows[meta[0] + lane];
+      pc = coefs[meta[0] + lane];
+    }
+    for (int k = 0; k < n; ++k) {
+      const int64_t b = meta[4 * k], e = meta[4 * k + 1];
+      const f64 mult = mus[k];
+      int nr = 0;
+      f64 nc = 0.0;
+      if (k + 1 < n && meta[4 * k + 4] + lane < meta[4 * k + 5]) {
+        nr = rows[meta[4 * k + 4] + lane];
+        nc = coefs[meta[4 * k + 4] + lane];
+      }
+      for (int64_t i = b + lane; i < e; i += 64) {
+        const int pos = i == b + lane ? pr : rows[i];
+        const f64 v = mult * (i == b + lane ? pc : coefs[i]);
+        if (!flag[pos]) {
+          acc[pos] = v;
+          flag[pos] = 1;
+        } else {
+          acc[pos] += v;
+        }
+      }
+      sd_sync();
+      pr = nr;
+      pc = nc;
+    }
+  }
+  // non_zero_position_set_: the touched positions, relevant ones only.
+  for (int w = 0; w < s.nwords; ++w) {
+    const int col = w * 64 + lane;
+    const uint64_t touched = __ballot(col < s.N && flag[col]);
+    if (lane == 0) s.nzset[w] = touched & s.relevant[w];
+  }
+  sd_sync();
+  const f64 drop = s.drop_tolerance;
+  const uint64_t* nzset = s.nzset;
+  s.n_nzpos = sd_ordered_compact(s.N, s.nzpos, [&](int col) {
+    return bit_get(nzset, col) && sd_fabs(acc[col]) > drop;
+  });
+  g_f64* coeff = SD_G(f64, s.coeff);
+  for (int i = lane; i < s.N; i += 64) {
+    if (flag[i]) {
+      coeff[i] = acc[i];
+      acc[i] = 0.0;
+      flag[i] = 0;
+    }
+  }
+  sd_sync();
+  return true;
+}
+#endif
 SD_INLINE void ur_row_wise_hypersparse(Lp& s) {
   SdSubTimer t_sub_(&s.phase_ticks[28]);
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (ur_row_wise_hyper_lds(s)) return;
+#endif
   for (int k = 0; k < s.n_rho_filtered; ++k) {
     const int col = s.rho_filtered[k];
     const f64 mult = s.rho.values[col];

@@ -37,6 +37,9 @@ __global__ __launch_bounds__(64) void sdual_segment_kernel(sdual::Lp* lp) {
   lp->lds = sd_lds;
   lp->lds_doubles = kLdsDoubles;
   lp->lds_scratch = sd_lds + kLdsDoubles;
+  lp->lds_busy = 0;
+  for (int i = threadIdx.x; i < kLdsDoubles; i += blockDim.x) sd_lds[i] = 0.0;  // SdLdsVec
+  __syncthreads();
   sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
 }
 
@@ -201,6 +204,9 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring
     lp->lds = sd_lds;
     lp->lds_doubles = kLdsDoubles;
     lp->lds_scratch = sd_lds + kLdsDoubles;
+    lp->lds_busy = 0;
+    for (int i = threadIdx.x; i < kLdsDoubles; i += blockDim.x) sd_lds[i] = 0.0;  // SdLdsVec
+    __syncthreads();
     sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
     const uint64_t t_out = wall_clock64();
     if (threadIdx.x == 0) {

@@ -323,6 +323,8 @@ struct Lp {
   int32_t lds_doubles;
   int32_t lds_pad;
   f64* lds_scratch;  // SdScratch after the staging area (device only)
+  int32_t lds_busy;  // a solve's working vector occupies the staging area
+  int32_t lds_pad2;
 
   // ---- loop carry and exit ----
   int refactorize;  // the host loop's `refactorize` flag
