@@ -326,6 +326,33 @@ SD_INLINE void sort_distinct(int32_t* a, int n, int range, char* flags) {
 #if defined(__HIP_DEVICE_COMPILE__)
   sd_sync();  // the list and the flags were last written by every lane
   const int lane = sd_lane();
+  if (__builtin_amdgcn_is_shared(flags) && range <= 64 * 256) {
+    // Flags in LDS: mark, then lane j scans its block of range / 64
+    // positions, counts, takes its offset from a wave prefix sum and writes
+    // its positions in order (clearing the flags).
+    __attribute__((address_space(3))) char* f = SD_L(char, flags);
+    for (int k = lane; k < n; k += 64) f[a[k]] = 1;
+    sd_sync();
+    const int per = (range + 63) / 64;
+    const int lo = lane * per;
+    const int hi = lo + per < range ? lo + per : range;
+    int count = 0;
+    for (int i = lo; i < hi; ++i) count += f[i] != 0;
+    int incl = count;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += t;
+    }
+    int pos = incl - count;
+    for (int i = lo; i < hi; ++i) {
+      if (f[i] != 0) {
+        a[pos++] = i;
+        f[i] = 0;
+      }
+    }
+    sd_sync();
+    return;
+  }
   if (n <= 128) {
     const int32_t kNone = 0x7fffffff;
     const int32_t v0 = lane < n ? a[lane] : kNone;
@@ -450,6 +477,52 @@ SD_INLINE f64 dense_squared_norm(const f64* c, int n) {
   }
   return sum;
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+// SquaredNorm of a ScatteredVector (lp_utils.h: blocks of four in order for
+// a dense vector, the listed entries in order otherwise) on the lanes: up to
+// 256 terms (a block's ((a + b) + c) + d, or one square) are computed
+// together and lane 0 adds them in order; the result is broadcast.
+__device__ inline f64 vec_squared_norm_dev(const Vec& v, f64* lds_scratch) {
+  l_f64* red = SD_L(f64, reinterpret_cast<SdScratch*>(lds_scratch)->red);
+  const int lane = sd_lane();
+  const bool dense = vec_dense(v, 0.8);
+  const f64* c = v.values;
+  const int n = dense ? v.size / 4 : v.nnz;
+  f64 sum = 0.0;
+  for (int base = 0; base < n; base += 256) {
+    const int cnt = n - base < 256 ? n - base : 256;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = base + 64 * u + lane;
+      f64 term = 0.0;
+      if (64 * u + lane < cnt) {
+        if (dense) {
+          const int r = 4 * j;
+          term = sq(c[r]) + sq(c[r + 1]) + sq(c[r + 2]) + sq(c[r + 3]);
+        } else {
+          term = sq(c[v.nz[j]]);
+        }
+      }
+      red[64 * u + lane] = term;
+    }
+    sd_sync();
+    if (lane == 0) {
+      for (int j = 0; j < cnt; ++j) sum += red[j];
+    }
+    sd_sync();
+  }
+  if (lane == 0) {
+    if (dense) {
+      for (int r = 4 * n; r < v.size; ++r) sum += sq(c[r]);
+    }
+    red[0] = sum;
+  }
+  sd_sync();
+  const f64 result = red[0];
+  sd_sync();
+  return result;
+}
+#endif
 SD_INLINE f64 vec_squared_norm(const Vec& v) {
   if (vec_dense(v, 0.8)) return dense_squared_norm(v.values, v.size);
   f64 sum = 0.0;
@@ -751,9 +824,80 @@ __device__ inline f64 tri_column_dev(gc_i32* rows, gc_f64* coefs, int64_t b, int
   }
   return sum;
 }
-// The level sweep with the next level's bounds, first columns and their
-// entry ranges loaded while the current level computes (read-only schedule
-// data), so a level waits on its entries and x only.
+// A lane's next column of a level sweep, fetched ahead: its entry range,
+// the first group of four entries in the order tri_column_dev takes them
+// (from the start for kUpper, from the end otherwise) and the diagonal.
+struct SdColPf {
+  int col;
+  int64_t b, e;
+  int r[4];
+  f64 c[4];
+  f64 diag;
+};
+template <bool kUpper>
+__device__ inline void tri_fetch_col(gc_i32* order, gc_i64* starts, gc_i32* rows, gc_f64* coefs,
+                                     gc_f64* diag, bool ones, int k, SdColPf* p) {
+  p->col = order[k];
+  p->b = starts[p->col];
+  p->e = starts[p->col + 1];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = kUpper ? p->b + u : p->e - 1 - u;
+    const bool in = kUpper ? i < p->e : i >= p->b;
+    p->r[u] = in ? rows[i] : 0;
+    p->c[u] = in ? coefs[i] : 0.0;
+  }
+  p->diag = ones ? 1.0 : diag[p->col];
+}
+// tri_column_dev with the first group of entries from a prefetch.
+template <bool kUpper, typename XP>
+__device__ inline f64 tri_column_pf(gc_i32* rows, gc_f64* coefs, const SdColPf& p, XP x) {
+  const int64_t b = p.b, e = p.e;
+  f64 sum = x[p.col];
+  if (e - b >= 4) {
+    sum -= p.c[0] * x[p.r[0]] + p.c[1] * x[p.r[1]] + p.c[2] * x[p.r[2]] + p.c[3] * x[p.r[3]];
+    if (kUpper) {
+      int64_t i = b + 4;
+      for (; i < e - 3; i += 4) {
+        sum -= coefs[i] * x[rows[i]] + coefs[i + 1] * x[rows[i + 1]] +
+               coefs[i + 2] * x[rows[i + 2]] + coefs[i + 3] * x[rows[i + 3]];
+      }
+      if (i < e) {
+        sum -= coefs[i] * x[rows[i]];
+        if (i + 1 < e) {
+          sum -= coefs[i + 1] * x[rows[i + 1]];
+          if (i + 2 < e) sum -= coefs[i + 2] * x[rows[i + 2]];
+        }
+      }
+    } else {
+      int64_t i = e - 5;
+      for (; i >= b + 3; i -= 4) {
+        sum -= coefs[i] * x[rows[i]] + coefs[i - 1] * x[rows[i - 1]] +
+               coefs[i - 2] * x[rows[i - 2]] + coefs[i - 3] * x[rows[i - 3]];
+      }
+      if (i >= b) {
+        sum -= coefs[i] * x[rows[i]];
+        if (i >= b + 1) {
+          sum -= coefs[i - 1] * x[rows[i - 1]];
+          if (i >= b + 2) sum -= coefs[i - 2] * x[rows[i - 2]];
+        }
+      }
+    }
+  } else {
+    const int64_t len = e - b;
+    if (len > 0) {
+      sum -= p.c[0] * x[p.r[0]];
+      if (len > 1) {
+        sum -= p.c[1] * x[p.r[1]];
+        if (len > 2) sum -= p.c[2] * x[p.r[2]];
+      }
+    }
+  }
+  return sum;
+}
+// The level sweep with each lane's next-level column (bounds, first four
+// entries, diagonal: read-only schedule and factor data) loaded while the
+// current level computes, so a level mostly waits on x in LDS.
 template <bool kUpper, typename XP>
 __device__ inline void tri_level_sweep_dev(const Tri& t, XP x, int last) {
   gc_i64* starts = SD_G(const int64_t, t.starts);
@@ -768,31 +912,25 @@ __device__ inline void tri_level_sweep_dev(const Tri& t, XP x, int last) {
   if (levels <= 0) return;
   int le = lvs[1];
   int k = lvs[0] + lane;
-  int col = k < le ? order[k] : 0;
-  int64_t cb = k < le ? starts[col] : 0, ce = k < le ? starts[col + 1] : 0;
+  SdColPf cur;
+  if (k < le) tri_fetch_col<kUpper>(order, starts, rows, coefs, diag, ones, k, &cur);
   for (int l = 0; l < levels; ++l) {
     const int le2 = l + 1 < levels ? lvs[l + 2] : le;
     const int k2 = le + lane;
-    const int col2 = k2 < le2 ? order[k2] : 0;
-    const int64_t cb2 = k2 < le2 ? starts[col2] : 0, ce2 = k2 < le2 ? starts[col2 + 1] : 0;
-    for (; k < le;) {
-      if (kUpper || col <= last) {
-        const f64 sum = tri_column_dev<kUpper>(rows, coefs, cb, ce, x, col);
-        x[col] = ones ? sum : sum / diag[col];
+    SdColPf nxt;
+    if (k2 < le2) tri_fetch_col<kUpper>(order, starts, rows, coefs, diag, ones, k2, &nxt);
+    while (k < le) {
+      if (kUpper || cur.col <= last) {
+        const f64 sum = tri_column_pf<kUpper>(rows, coefs, cur, x);
+        x[cur.col] = ones ? sum : sum / cur.diag;
       }
       k += 64;
-      if (k < le) {
-        col = order[k];
-        cb = starts[col];
-        ce = starts[col + 1];
-      }
+      if (k < le) tri_fetch_col<kUpper>(order, starts, rows, coefs, diag, ones, k, &cur);
     }
     sd_sync();
     le = le2;
     k = k2;
-    col = col2;
-    cb = cb2;
-    ce = ce2;
+    cur = nxt;
   }
 }
 #endif
@@ -907,6 +1045,114 @@ SD_INLINE void tri_transpose_lower_solve(const Tri& t, f64* x, f64* lds = nullpt
   }
   for (int col = last; col >= end; --col) x[col] = tri_tl_column(t, x, col);
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+// Hypersparse solves over a non-zero list (sparse.cc:957-1128) on the
+// device: the next listed column's bounds, first entries and diagonal load
+// while the current one computes (read-only factor data; the list entries
+// ahead of the loop are never rewritten before they are read).
+// kScatter: HyperSparseSolve / ...WithReversedNonZeros (a column scatter,
+// split over the lanes); else TransposeHyperSparseSolve / ...Reversed (a
+// grouped dot, tri_column_pf's order). kRev: the list from its end, kept rows
+// gathered at its end and moved to the front (erase_prefix).
+struct SdHyperPf {
+  int row;
+  int64_t b, e;
+  int r;
+  f64 c;
+  f64 diag;
+};
+template <bool kScatter, bool kRev, typename XP>
+__device__ inline void tri_hyper_dev(const Tri& t, XP x, int32_t* nz, int* nnz) {
+  gc_i64* starts = SD_G(const int64_t, t.starts);
+  gc_i32* rows = SD_G(const int32_t, t.rows);
+  gc_f64* coefs = SD_G(const f64, t.coefs);
+  gc_f64* diag = SD_G(const f64, t.diag);
+  __attribute__((address_space(1))) int32_t* nzg = SD_G(int32_t, nz);
+  const bool ones = t.all_ones;
+  const int lane = sd_lane();
+  const int n = *nnz;
+  int out = kRev ? n : 0;
+  if (kScatter) {
+    auto fetch = [&](int k, SdHyperPf* p) {
+      p->row = nzg[k];
+      p->b = starts[p->row];
+      p->e = starts[p->row + 1];
+      const int64_t i = p->b + lane;
+      p->r = i < p->e ? rows[i] : 0;
+      p->c = i < p->e ? coefs[i] : 0.0;
+      p->diag = ones ? 1.0 : diag[p->row];
+    };
+    SdHyperPf cur;
+    if (n > 0) fetch(kRev ? n - 1 : 0, &cur);
+    for (int j = 0; j < n; ++j) {
+      const int k = kRev ? n - 1 - j : j;
+      SdHyperPf nxt;
+      if (j + 1 < n) fetch(kRev ? k - 1 : k + 1, &nxt);
+      const f64 v = x[cur.row];
+      if (v != 0.0) {
+        const f64 coeff = ones ? v : v / cur.diag;
+        x[cur.row] = coeff;
+        if (cur.b + lane < cur.e) x[cur.r] -= coeff * cur.c;
+        for (int64_t i = cur.b + 64 + lane; i < cur.e; i += 64) x[rows[i]] -= coeff * coefs[i];
+        sd_sync();
+        if (kRev) {
+          nzg[--out] = cur.row;
+        } else {
+          nzg[out++] = cur.row;
+        }
+      }
+      cur = nxt;
+    }
+  } else {
+    // transposed: kRev walks the list backwards with the lower-triangle
+    // (backward) grouping, as TransposeHyperSparseSolveWithReversedNonZeros.
+    constexpr bool kForward = !kRev;
+    gc_i32* order = nzg;
+    SdColPf cur;
+    if (n > 0) tri_fetch_col<kForward>(order, starts, rows, coefs, diag, ones, kRev ? n - 1 : 0, &cur);
+    for (int j = 0; j < n; ++j) {
+      const int k = kRev ? n - 1 - j : j;
+      SdColPf nxt;
+      if (j + 1 < n) tri_fetch_col<kForward>(order, starts, rows, coefs, diag, ones, kRev ? k - 1 : k + 1, &nxt);
+      const f64 sum = tri_column_pf<kForward>(rows, coefs, cur, x);
+      x[cur.col] = ones ? sum : sum / cur.diag;
+      sd_sync();
+      if (sum != 0.0) {
+        if (kRev) {
+          nzg[--out] = cur.col;
+        } else {
+          nzg[out++] = cur.col;
+        }
+      }
+      cur = nxt;
+    }
+  }
+  sd_sync();
+  if (kRev) {
+    // erase_prefix: the kept rows [out, n) to the front, chunk by chunk in
+    // increasing order (a chunk's sources lie at or after its targets).
+    const int cnt = n - out;
+    for (int c0 = 0; c0 < cnt; c0 += 64) {
+      const int k = c0 + lane;
+      const int v = k < cnt ? nzg[out + k] : 0;
+      sd_sync();
+      if (k < cnt) nzg[k] = v;
+      sd_sync();
+    }
+    *nnz = cnt;
+  } else {
+    *nnz = out;
+  }
+}
+template <bool kScatter, bool kRev>
+__device__ inline void tri_hyper_dispatch(const Tri& t, f64* x, int32_t* nz, int* nnz) {
+  if (sd_is_lds(x)) {
+    tri_hyper_dev<kScatter, kRev>(t, SD_L(f64, x), nz, nnz);
+  } else {
+    tri_hyper_dev<kScatter, kRev>(t, SD_G(f64, x), nz, nnz);
+  }
+}
+#endif
 // A column's scatter over its (distinct) rows is split over the lanes.
 SD_INLINE void tri_scatter_column(const Tri& t, int col, f64 coeff, f64* x) {
   for (int64_t i = t.starts[col] + sd_lane(); i < t.starts[col + 1]; i += sd_lanes())
@@ -914,6 +1160,10 @@ SD_INLINE void tri_scatter_column(const Tri& t, int col, f64 coeff, f64* x) {
   sd_sync();
 }
 SD_INLINE void tri_hyper_solve(const Tri& t, f64* x, int32_t* nz, int* nnz) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  tri_hyper_dispatch<true, false>(t, x, nz, nnz);
+  return;
+#endif
   const bool ones = t.all_ones;
   int new_size = 0;
   for (int k = 0; k < *nnz; ++k) {
@@ -932,6 +1182,10 @@ SD_INLINE void erase_prefix(int32_t* nz, int* nnz, int new_start) {
   *nnz = n;
 }
 SD_INLINE void tri_hyper_solve_rev(const Tri& t, f64* x, int32_t* nz, int* nnz) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  tri_hyper_dispatch<true, true>(t, x, nz, nnz);
+  return;
+#endif
   const bool ones = t.all_ones;
   int new_start = *nnz;
   for (int k = *nnz - 1; k >= 0; --k) {
@@ -945,6 +1199,10 @@ SD_INLINE void tri_hyper_solve_rev(const Tri& t, f64* x, int32_t* nz, int* nnz) 
   erase_prefix(nz, nnz, new_start);
 }
 SD_INLINE void tri_transpose_hyper_solve(const Tri& t, f64* x, int32_t* nz, int* nnz) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  tri_hyper_dispatch<false, false>(t, x, nz, nnz);
+  return;
+#endif
   const bool ones = t.all_ones;
   int new_size = 0;
   for (int k = 0; k < *nnz; ++k) {
@@ -970,6 +1228,10 @@ SD_INLINE void tri_transpose_hyper_solve(const Tri& t, f64* x, int32_t* nz, int*
   *nnz = new_size;
 }
 SD_INLINE void tri_transpose_hyper_solve_rev(const Tri& t, f64* x, int32_t* nz, int* nnz) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  tri_hyper_dispatch<false, true>(t, x, nz, nnz);
+  return;
+#endif
   const bool ones = t.all_ones;
   int new_start = *nnz;
   for (int k = *nnz - 1; k >= 0; --k) {
@@ -1008,20 +1270,50 @@ SD_INLINE void tri_rows_to_consider(const Tri& t, int32_t* nz, int* nnz, char* s
 #if defined(__HIP_DEVICE_COMPILE__)
   // A column's entries (distinct rows) on the lanes; its new rows join the
   // list in entry order (ballot prefix counts), as the sequential loop appends.
+  // The next listed row's bounds and first 64 entries load while the current
+  // one is expanded (when it is already listed).
   const int lane = sd_lane();
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  gc_i64* tst = SD_G(const int64_t, t.starts);
+  gc_i32* trows = SD_G(const int32_t, t.rows);
   int n = *nnz;
+  {
+    // The listed rows are expanded first, in order: if their entries alone
+    // take the count past the threshold, so does the sequential loop (the
+    // list is then dropped: the caller takes the dense path).
+    int64_t entries = 0;
+    for (int k = lane; k < n; k += 64) entries += tst[nz[k] + 1] - tst[nz[k]];
+    entries = sd_wave_sum_i64(entries);
+    if (num_ops + entries > num_ops_threshold) {
+      *nnz = 0;
+      return;
+    }
+  }
   for (int k = lane; k < n; k += 64) stored[nz[k]] = 1;
   sd_sync();
-  for (int k = 0; k < n; ++k) {
+  int64_t pb = 0, pe = 0;
+  int per = 0;
+  bool have = false;
+  auto fetch = [&](int k) {
     const int row = nz[k];
-    const int64_t b = t.starts[row], e = t.starts[row + 1];
+    pb = tst[row];
+    pe = tst[row + 1];
+    per = pb + lane < pe ? trows[pb + lane] : 0;
+    have = true;
+  };
+  if (n > 0) fetch(0);
+  for (int k = 0; k < n; ++k) {
+    if (!have) fetch(k);
+    const int64_t b = pb, e = pe;
+    const int first_er = per;
+    have = false;
+    if (k + 1 < n) fetch(k + 1);
     for (int64_t base = b; base < e; base += 64) {
       const int64_t i = base + lane;
       bool fresh = false;
       int er = 0;
       if (i < e) {
-        er = t.rows[i];
+        er = base == b ? first_er : trows[i];
         fresh = !stored[er];
       }
       const uint64_t m = __ballot(fresh);
@@ -2026,6 +2318,79 @@ SD_INLINE int dp_get_maximum(Lp& s) {
   f64 best_value = -sd_inf();
   int best_position = -1;
   int n_equiv = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int lane = sd_lane();
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  if (s.dp_ntops != 0) {
+    // The tops on the lanes (at most 31): the kept ones (still candidates
+    // with an unchanged value) compacted in order; the maximum's first
+    // occurrence is the best position, its later ones the equivalent
+    // choices in order (the sequential loop's result).
+    const int n = s.dp_ntops;
+    int idx = 0;
+    f64 val = -sd_inf();
+    bool kept = false;
+    if (lane < n) {
+      idx = s.dp_tops_idx[lane];
+      val = s.dp_tops_val[lane];
+      kept = bit_get(s.dp_cand, idx) && s.dp_values[idx] == val;
+    }
+    const uint64_t kmask = __ballot(kept);
+    const int new_size = __popcll(kmask);
+    sd_sync();
+    if (kept) {
+      const int pos = __popcll(kmask & below);
+      s.dp_tops_idx[pos] = idx;
+      s.dp_tops_val[pos] = val;
+    }
+    s.dp_ntops = new_size;
+    if (new_size != 0) {
+      const f64 top = sd_wave_max(kept ? val : -sd_inf());
+      const uint64_t emask = __ballot(kept && val == top);
+      const int first = __builtin_ctzll(emask);
+      best_position = __shfl(idx, first, 64);
+      n_equiv = __popcll(emask) - 1;
+      if (((emask >> lane) & 1) && lane != first) {
+        s.dp_equiv[__popcll(emask & below) - 1] = idx;
+      }
+      sd_sync();
+      return dp_randomize(s, best_position, n_equiv);
+    }
+    sd_sync();
+  }
+  // Rescan: 64 positions at a time, candidates below the threshold at the
+  // chunk's start skipped on the lanes (the threshold never decreases), the
+  // others replayed in order.
+  s.dp_threshold = -sd_inf();
+  for (int base = 0; base < s.dp_size; base += 64) {
+    const int position = base + lane;
+    f64 value = 0.0;
+    bool cand = false;
+    if (position < s.dp_size && bit_get(s.dp_cand, position)) {
+      value = s.dp_values[position];
+      cand = value >= s.dp_threshold;
+    }
+    uint64_t mask = __ballot(cand);
+    while (mask != 0) {
+      const int l = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const f64 v = __shfl(value, l, 64);
+      if (v < s.dp_threshold) continue;
+      dp_update_top_k(s, base + l, v);
+      if (v >= best_value) {
+        if (v == best_value) {
+          s.dp_equiv[n_equiv++] = base + l;
+          continue;
+        }
+        n_equiv = 0;
+        best_value = v;
+        best_position = base + l;
+      }
+    }
+  }
+  sd_sync();
+  return dp_randomize(s, best_position, n_equiv);
+#endif
   if (s.dp_ntops != 0) {
     // iterate over a copy of tops_ (the loop compacts in place)
     int32_t cidx[32];
@@ -2730,7 +3095,11 @@ SD_INLINE bool den_test_precision(Lp& s, int leaving_row) {
   f64 leaving;
   {
     SdSubTimer t_x_(&s.phase_ticks[21]);
+#if defined(__HIP_DEVICE_COMPILE__)
+    leaving = vec_squared_norm_dev(s.rho, s.lds_scratch);
+#else
     leaving = vec_squared_norm(s.rho);
+#endif
   }
   const f64 old = s.norms[leaving_row];
   const f64 acc = (sd_sqrt(leaving) - sd_sqrt(old)) / sd_sqrt(leaving);

@@ -29,18 +29,36 @@ inline hipStream_t Stream(void* p) { return reinterpret_cast<hipStream_t>(p); }
 // metadata scratch (SdScratch, 4.5 KB): four workgroups per CU keep the
 // 1 024-group pool resident.
 constexpr int kLdsDoubles = 4096;
-constexpr int kLdsTotalDoubles = kLdsDoubles + sdual::kSdScratchDoubles;
 extern __shared__ double sd_lds[];
-
-// One thread walks Glop's loop; the header lives in the arena.
-__global__ __launch_bounds__(64) void sdual_segment_kernel(sdual::Lp* lp) {
+// TriangularMatrix::stored_ (m flags, zero between uses) in LDS for m up to
+// this many rows.
+constexpr int kLdsStoredBytes = 2560;
+constexpr int kLdsTotalDoubles = kLdsDoubles + sdual::kSdScratchDoubles + kLdsStoredBytes / 8;
+// The segment's LDS: the staging / working vector area (zeroed), the stored
+// flags when they fit (zeroed; the arena pointer is put back before the
+// header leaves), the scratch.
+__device__ inline char* sd_lds_enter(sdual::Lp* lp) {
   lp->lds = sd_lds;
   lp->lds_doubles = kLdsDoubles;
   lp->lds_scratch = sd_lds + kLdsDoubles;
   lp->lds_busy = 0;
   for (int i = threadIdx.x; i < kLdsDoubles; i += blockDim.x) sd_lds[i] = 0.0;  // SdLdsVec
+  char* saved = lp->stored;
+  if (lp->m <= kLdsStoredBytes) {
+    char* st = reinterpret_cast<char*>(sd_lds + kLdsDoubles + sdual::kSdScratchDoubles);
+    for (int i = threadIdx.x; i < kLdsStoredBytes; i += blockDim.x) st[i] = 0;
+    lp->stored = st;
+  }
   __syncthreads();
+  return saved;
+}
+
+// One thread walks Glop's loop; the header lives in the arena.
+__global__ __launch_bounds__(64) void sdual_segment_kernel(sdual::Lp* lp) {
+  char* stored = sd_lds_enter(lp);
   sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
+  __syncthreads();
+  lp->stored = stored;
 }
 
 // ---------------------------------------------------------------------------
@@ -201,13 +219,10 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring
     if (threadIdx.x == 0) pool_dbg(q, 2, 2);
     sdual::Lp* lp = reinterpret_cast<sdual::Lp*>(arena);
     lp->phase_ticks[13] += wall_clock64() - t_claim;  // staging image in
-    lp->lds = sd_lds;
-    lp->lds_doubles = kLdsDoubles;
-    lp->lds_scratch = sd_lds + kLdsDoubles;
-    lp->lds_busy = 0;
-    for (int i = threadIdx.x; i < kLdsDoubles; i += blockDim.x) sd_lds[i] = 0.0;  // SdLdsVec
+    char* stored = sd_lds_enter(lp);
+    sdual::sd_run(*lp);
     __syncthreads();
-    sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
+    lp->stored = stored;  // every lane (sdual_core.h: the wave)
     const uint64_t t_out = wall_clock64();
     if (threadIdx.x == 0) {
       pool_dbg(q, 2, 3);
