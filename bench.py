@@ -133,7 +133,10 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     if split:
         # The exchange runs on a gloo group: the joined messages are host
         # bytes the engine's host control flow consumes.
-        distributed.attach_column_split(h, dist, dist.new_group(backend="gloo"))
+        # The joins run through the engine's C++ same-node exchange
+        # (engine/exchange.cc); a gloo group only distributes its name.
+        _, _, xchg = distributed.attach_column_split(h, dist, dist.new_group(backend="gloo"),
+                                                     transport=args.c5_transport)
     h.load(lp)
     h.record_iteration_times(True)  # per-iteration timestamps (window statistics)
     t = time.perf_counter()
@@ -210,6 +213,12 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
         "amortized": amortized,
         "split": split,
     }
+    if split:
+        ex = stats.get("exchange", {})
+        out["exchange"] = {"transport": args.c5_transport,
+                           "allgathers_per_step": ex.get("launches", 0) / max(1, done),
+                           "us_per_step": 1000.0 * ex.get("call_ms", 0.0) / max(1, done),
+                           "bytes_per_step": ex.get("bytes", 0.0) / max(1, done)}
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_lib
         # The oracle runs the same solve to the end of the amortized window;
@@ -530,6 +539,8 @@ def main():
     ap.add_argument("--c5-amortized", type=int, default=1000,
                     help="config-5 iterations of the refactorization-amortized window "
                          "(starts with the headline window)")
+    ap.add_argument("--c5-transport", default="shm", choices=["shm", "gloo"],
+                    help="N > 1: the split's join transport (C++ shared memory, or gloo)")
     ap.add_argument("--c5-replicas", action="store_true",
                     help="N > 1: one independent config-5 LP per rank instead of one split LP")
     ap.add_argument("--c5-traffic-json",
@@ -658,6 +669,7 @@ def main():
         "window": c5["window"],
         "cpu_baseline": c5.get("cpu_baseline"),
         "amortized": c5.get("amortized"),
+        "exchange": c5.get("exchange"),
         "c2": c2,
         "c3": c3,
         "batched": batched,

@@ -187,7 +187,9 @@ enum {
   MI_K_SDUAL = 14,      /* device dual simplex segment: whole phase-II dual iterations of one
                            LP on one workgroup (revised_simplex.cc:3058-3367); bytes = the
                            state arena moved in and out */
-  MI_K_COUNT = 15
+  MI_K_EXCHANGE = 15,   /* cross-process split joins (mi_lp_set_exchange): all-gathers, host
+                           wall time, bytes gathered */
+  MI_K_COUNT = 16
 };
 
 void mi_glop_params_default(mi_glop_params* p);
@@ -328,6 +330,22 @@ typedef int (*mi_lp_allgather_fn)(void* ctx, const void* send, int64_t send_byte
                                   const int64_t* recv_bytes);
 int mi_lp_set_exchange(mi_lp* h, int32_t rank, int32_t world, void* ctx,
                        mi_lp_allgather_fn allgather);
+
+/* Same-node exchange for mi_lp_set_exchange (engine/exchange.cc): an
+ * all-gather of host bytes through one POSIX shared-memory segment, so the
+ * split's per-iteration joins run in C++ with no Python and no socket on the
+ * path (the joined messages are consumed by every rank's host control flow).
+ * Rank 0 creates `name` (a fresh shm name, e.g. "/mi_lp_<uuid>", distributed
+ * by the caller), the others attach; the name is unlinked once all `world`
+ * ranks attached. Messages longer than slot_bytes go in several rounds.
+ * Pass (ctx = the exchange, allgather = mi_exchange_allgather) to
+ * mi_lp_set_exchange; close after the handle is done with it. */
+typedef struct mi_exchange mi_exchange;
+int mi_exchange_open(const char* name, int32_t rank, int32_t world, int64_t slot_bytes,
+                     mi_exchange** out);
+int mi_exchange_allgather(void* ctx, const void* send, int64_t send_bytes, void* recv,
+                          const int64_t* recv_bytes);
+void mi_exchange_close(mi_exchange* x);
 
 /* Batch API: solves count independent LPs already loaded in handles (all on
  * the same device) on num_threads host threads; each thread drives several

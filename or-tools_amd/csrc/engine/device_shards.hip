@@ -23,6 +23,8 @@
 // host memory.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -112,6 +114,18 @@ void DeviceLp::SetExchange(int rank, int world, void* ctx, ExchangeFn fn) {
 // Local shard results in, every shard's results out (block order).
 void DeviceLp::ExchangeParts(std::vector<std::string>* parts) {
   if (exchange_fn_ == nullptr) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Account {
+    mi_lp_kernel_stats& st;
+    std::chrono::steady_clock::time_point t0;
+    int64_t bytes = 0;
+    ~Account() {
+      st.launches[MI_K_EXCHANGE] += 2;  // sizes, then the messages
+      st.algorithmic_bytes[MI_K_EXCHANGE] += static_cast<double>(bytes);
+      st.call_ms[MI_K_EXCHANGE] += std::chrono::duration<double, std::milli>(
+                                       std::chrono::steady_clock::now() - t0).count();
+    }
+  } account{stats_, t0};
   const int world = exchange_world_;
   const std::string& mine = (*parts)[exchange_rank_];
   int64_t n = static_cast<int64_t>(mine.size());
@@ -122,6 +136,7 @@ void DeviceLp::ExchangeParts(std::vector<std::string>* parts) {
   }
   int64_t total = 0;
   for (int64_t z : sizes) total += z;
+  account.bytes = total;
   std::string all(size_t(total), '\0');
   if (exchange_fn_(exchange_ctx_, mine.data(), n, all.data(), sizes.data()) != 0) {
     throw DeviceError("column split: exchange failed");

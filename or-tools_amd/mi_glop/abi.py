@@ -153,7 +153,8 @@ class MiLpRunCounters(ctypes.Structure):
 
 KERNEL_NAMES = ["pricing", "update_row", "primal_norms", "rc_update", "tri_solve",
                 "col_norms", "spmv_rows", "single_row", "dual_ratio", "readback",
-                "tri_solve_tau", "tri_solve_l", "tri_solve_t", "tri_solve_upper", "sdual"]
+                "tri_solve_tau", "tri_solve_l", "tri_solve_t", "tri_solve_upper", "sdual",
+                "exchange"]
 
 # Names of every exported entry point of include/mi_lp.h (checked by tests).
 EXPORTED_SYMBOLS = [
@@ -176,6 +177,7 @@ EXPORTED_SYMBOLS = [
     "mi_lp_solver_params_default", "mi_lp_scale", "mi_lp_solver_solve",
     "mi_lp_clear_integrality_scales", "mi_lp_record_iteration_times",
     "mi_lp_get_iteration_times", "mi_lp_get_run_counters", "mi_lp_set_exchange",
+    "mi_exchange_open", "mi_exchange_allgather", "mi_exchange_close",
     "mi_lp_batch_solve_gpus",
 ]
 

@@ -127,12 +127,30 @@ def allgather_bytes(data, sizes, dist, group=None):
     return b"".join(bytes(outs[r][:sizes[r]].numpy().tobytes()) for r in range(world))
 
 
-def attach_column_split(handle, dist, group=None):
+def shm_name(dist, group=None):
+    """A fresh shared-memory name chosen by rank 0 and broadcast to the group
+    (the only use of the process group on the split's path: setup)."""
+    import uuid
+    obj = [f"/mi_lp_{uuid.uuid4().hex}" if dist.get_rank(group) == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return obj[0]
+
+
+def attach_column_split(handle, dist, group=None, transport="shm"):
     """Makes `handle` (engine.LpHandle) this rank's block of one LP split over
-    the group (call before handle.load). The exchange runs on `group` (a gloo
-    group: the joined messages are host bytes the engine consumes)."""
+    the group (call before handle.load). transport "shm": the joins go through
+    the engine's C++ same-node exchange (engine.ShmExchange; the group only
+    distributes its name); "gloo": through allgather_bytes on `group` (a
+    gloo group: the joined messages are host bytes the engine consumes).
+    Returns (rank, world, exchange or None); keep the exchange open while the
+    handle solves."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
+    if transport == "shm":
+        from . import engine
+        x = engine.ShmExchange(shm_name(dist, group), rank, world)
+        handle.set_exchange_native(rank, world, x)
+        return rank, world, x
     handle.set_exchange(rank, world,
                         lambda data, sizes: allgather_bytes(data, sizes, dist, group))
-    return rank, world
+    return rank, world, None

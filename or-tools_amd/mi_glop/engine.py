@@ -83,6 +83,10 @@ def lib():
     L.mi_lp_get_iteration_times.restype = ctypes.c_int64
     L.mi_lp_get_run_counters.argtypes = [vp, ctypes.POINTER(abi.MiLpRunCounters)]
     L.mi_lp_set_exchange.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, ALLGATHER_FN]
+    L.mi_exchange_open.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
+                                   ctypes.c_int64, ctypes.POINTER(vp)]
+    L.mi_exchange_allgather.argtypes = [vp, vp, ctypes.c_int64, vp, ctypes.POINTER(ctypes.c_int64)]
+    L.mi_exchange_close.argtypes = [vp]
     L.mi_lp_objective_limit_reached.argtypes = [vp, vp]
     L.mi_lp_get_unit_row_left_inverse.argtypes = [vp, ctypes.c_int32, vp, vp, vp]
     L.mi_lp_compute_dictionary.argtypes = [vp, vp, ctypes.c_int32, vp]
@@ -123,6 +127,49 @@ def allgather_callback(world, allgather):
         except Exception:  # noqa: BLE001
             return 1
     return ALLGATHER_FN(cb)
+
+
+class ShmExchange:
+    """Same-node all-gather of host bytes in C++ (mi_exchange_open, engine/
+    exchange.cc): the split's joins run without Python. Rank 0 creates the
+    segment `name`, the other ranks attach (the call returns once all
+    `world` ranks are attached). Needs no GPU."""
+
+    def __init__(self, name, rank, world, slot_bytes=8 << 20):
+        self._L = lib()
+        x = ctypes.c_void_p()
+        rc = self._L.mi_exchange_open(name.encode(), int(rank), int(world), int(slot_bytes),
+                                      ctypes.byref(x))
+        if rc != 0:
+            raise RuntimeError(f"mi_exchange_open({name!r}, rank {rank}/{world}) failed with {rc}")
+        self.x = x
+        self.rank, self.world = int(rank), int(world)
+
+    def allgather(self, data, sizes):
+        """Every rank's bytes in rank order (sizes[r] from rank r)."""
+        send = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+        recv = ctypes.create_string_buffer(max(1, sum(sizes)))
+        arr = (ctypes.c_int64 * self.world)(*sizes)
+        rc = self._L.mi_exchange_allgather(self.x, send, len(data), recv, arr)
+        if rc != 0:
+            raise RuntimeError(f"mi_exchange_allgather failed with {rc}")
+        return recv.raw[:sum(sizes)]
+
+    def function(self):
+        """(ctx, mi_lp_allgather_fn) for mi_lp_set_exchange: the C function."""
+        addr = ctypes.cast(self._L.mi_exchange_allgather, ctypes.c_void_p).value
+        return self.x, ALLGATHER_FN(addr)
+
+    def close(self):
+        if getattr(self, "x", None):
+            self._L.mi_exchange_close(self.x)
+            self.x = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class LpHandle:
@@ -260,6 +307,14 @@ class LpHandle:
         self._exchange_cb = allgather_callback(world, allgather)  # kept alive with the handle
         self._check(self._L.mi_lp_set_exchange(self.h, int(rank), int(world), None,
                                                self._exchange_cb), "mi_lp_set_exchange")
+
+    def set_exchange_native(self, rank, world, exchange):
+        """Cross-process split with a C++ exchange (ShmExchange): the engine
+        calls mi_exchange_allgather directly. Call before load()."""
+        ctx, fn = exchange.function()
+        self._exchange_keep = (exchange, fn)
+        self._check(self._L.mi_lp_set_exchange(self.h, int(rank), int(world), ctx, fn),
+                    "mi_lp_set_exchange")
 
     def record_iteration_times(self, on=True):
         self._check(self._L.mi_lp_record_iteration_times(self.h, int(on)),
