@@ -746,6 +746,14 @@ void DeviceLp::SdualRunPooled(size_t bytes, const double* arena_coeff, int n,
     std::lock_guard<std::mutex> lock(timeline.mu);
     timeline.enq.push_back(timeline.Now());
   }
+  // Algorithmic work of the segment: Glop's own operation counts (the
+  // deterministic-time counters, 2e-9 s per operation, lp_types.h:421-424),
+  // 12 bytes per operation (an 8-byte value and a 4-byte index), plus the
+  // arena bytes the workgroup moves in and out.
+  const double dt_before = sdual::rs_deterministic_time(*hs);
+  const double moved = 2.0 * sizeof(sdual::Lp) +
+                       static_cast<double>(hs->fixed_end - hs->mutable_begin) +
+                       static_cast<double>(hs->scratch_end - hs->scratch_begin);
   pool.Enqueue(sdual_staging_dev_);
   int64_t polls = 0;
   static const bool debug = std::getenv("MILP_SDUAL_DEBUG") != nullptr;
@@ -813,6 +821,16 @@ void DeviceLp::SdualRunPooled(size_t bytes, const double* arena_coeff, int n,
     }
   }
   ++stats_.launches[MI_K_SDUAL];
+  {
+    const double ops = (sdual::rs_deterministic_time(*hs) - dt_before) / 2e-9;
+    stats_.algorithmic_bytes[MI_K_SDUAL] +=
+        12.0 * ops + moved + static_cast<double>(hs->mutable_end - hs->mutable_begin);
+    // The workgroup's own time (wall_clock64, 100 MHz): the loop phases and
+    // the arena transfers.
+    uint64_t ticks = 0;
+    for (int k : {0, 1, 2, 3, 4, 5, 6, 7, 8, 13, 14}) ticks += hs->phase_ticks[k];
+    stats_.device_ms[MI_K_SDUAL] += static_cast<double>(ticks) / 1e5;
+  }
   DeviceOp("sdual pooled segment done");
 }
 
