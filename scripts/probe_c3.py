@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--max-rows", type=int, default=1000)
     ap.add_argument("--workers", type=int, nargs="*", default=[8])
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--single", type=int, nargs="*", default=[],
+                    help="suite indices solved one at a time (GPU alone, then the oracle)")
     a = ap.parse_args()
     lps = netlib_suite.suite(max_rows=a.max_rows)
     p = abi.default_params()
@@ -30,6 +32,31 @@ def main():
     warm.load(lp_gen.random_sparse_lp(40, 100, 0.1, 1))
     warm.solve()
     out = {"lps": len(lps), "max_n": max(lp.n + lp.m for lp in lps)}
+    for i in a.single:
+        # The suite's critical path: one LP alone, per-iteration latency.
+        lp = lps[i]
+        h = engine.LpHandle(p)
+        h.load(lp)
+        t = time.perf_counter()
+        r = h.solve()
+        dt = time.perf_counter() - t
+        ks = {k: {"launches": v["launches"], "call_ms": round(v["call_ms"], 3)}
+              for k, v in h.kernel_stats().items() if v["launches"] or v["call_ms"]}
+        h.close()
+        rec = {"m": lp.m, "n": lp.n, "nnz": int(lp.nnz), "iterations": int(r.iterations),
+               "gpu_s": dt, "gpu_us_per_iteration": 1e6 * dt / max(1, r.iterations),
+               "kernels": ks}
+        if a.cpu:
+            import oracle_lib
+            o = oracle_lib.OracleLp(p)
+            o.load(lp)
+            t = time.perf_counter()
+            ro = o.solve()
+            dt = time.perf_counter() - t
+            rec.update(cpu_s=dt, cpu_us_per_iteration=1e6 * dt / max(1, ro.iterations),
+                       same_iterations=int(ro.iterations) == int(r.iterations))
+        out[f"single_{i}"] = rec
+        print(f"[probe] single {i}: {rec}", file=sys.stderr, flush=True)
     for w in a.workers:
         hs = []
         for lp in lps:
