@@ -30,9 +30,13 @@ CPU oracle):
   branch BranchOnVar would skip (lower branch not usable, or not improving)
   is solved anyway and counted as speculative.
 
-Bounds are plain floats (the CP integer bounds); the LP carries the CP
-variables unscaled, so the scaler's factors (scaler_.VariableScalingFactor)
-are 1 and the objective scaling factor is the LP's obj_scale.
+Bounds are plain floats (the CP integer bounds). With scaling=False the LP
+carries the CP variables unscaled (every scaler factor 1, the objective
+scaling factor the LP's obj_scale). With scaling=True the LP is scaled once,
+with its level-zero bounds, by LpScalingHelper (:417, scaling.py) under
+CP-SAT's simplex parameters (MEAN_COST_SCALING, :234); the LP then sees bounds
+times VariableScalingFactor (:699-707, :505-509), and the solution, reduced
+costs and deductions are unscaled as at :685, :849 and :2367-2408.
 """
 import ctypes
 import math
@@ -40,6 +44,7 @@ import math
 import numpy as np
 
 from . import abi
+from .scaling import LpScalingHelper
 
 
 def ctypes_copy(dst, src):
@@ -101,11 +106,18 @@ class LpConstraint:
     (integer variables) of `lp`, solved by `handle` (engine.LpHandle or a
     handle with the same surface)."""
 
-    def __init__(self, lp, int_cols, handle, linearization_level=1):
+    def __init__(self, lp, int_cols, handle, linearization_level=1, scaling=False):
         self.lp = lp
         self.int_cols = np.asarray(int_cols, dtype=np.int64)
         self.h = handle
-        self.h.load(lp)
+        self.scaler = LpScalingHelper()
+        self.lp_data = lp  # what the simplex holds (lp_data_)
+        if scaling:
+            self.lp_data = self.scaler.scale(
+                lp, abi.default_solver_params(cost_scaling=abi.MEAN_COST_SCALING))
+        # VariableScalingFactor of every column (1 without scaling).
+        self.factor = np.array([self.scaler.variable_scaling_factor(c) for c in range(lp.n)])
+        self.h.load(self.lp_data)
         self.linearization_level = linearization_level
         self.next_simplex_iter = 500  # linear_programming_constraint.h:548
         self.is_degenerate = False
@@ -117,9 +129,14 @@ class LpConstraint:
         self.total_iterations = 0
 
     # -- SolveLp (:709-760) -------------------------------------------------
+    def scale_bounds(self, lbs, ubs):
+        """CP bounds -> the LP's (times VariableScalingFactor, :704-705); rows
+        of a 2-D array are independent bound sets (branch_lps)."""
+        return np.asarray(lbs) * self.factor, np.asarray(ubs) * self.factor
+
     def update_bounds(self, trail):
         """UpdateBoundsOfLpVariables (:699-707)."""
-        self.h.set_variable_bounds(trail.lb, trail.ub)
+        self.h.set_variable_bounds(*self.scale_bounds(trail.lb, trail.ub))
 
     def solve_lp(self, trail):
         self.update_bounds(trail)
@@ -132,7 +149,8 @@ class LpConstraint:
         self.h.notify_matrix_unchanged()
         self.num_solves += 1
         if r.problem_status == abi.OPTIMAL:
-            self.lp_solution = self.h.primal()
+            # GetVariableValueAtCpScale (:683-686)
+            self.lp_solution = self.scaler.unscale_variable_values(self.h.primal())
         return True
 
     # -- Propagate (:1697-1806) ----------------------------------------------
@@ -197,7 +215,7 @@ class LpConstraint:
                     return False
         if r.problem_status == abi.OPTIMAL:
             self.lp_objective = float(r.objective)
-            self.reduced_costs = np.asarray(self.h.reduced_costs())
+            self.reduced_costs = self.scaler.unscale_reduced_costs(self.h.reduced_costs())
         return True
 
     def reduced_cost_deductions(self, trail, cp_objective_delta, rc=None, x=None):
@@ -207,14 +225,16 @@ class LpConstraint:
         out = []
         if not math.isfinite(cp_objective_delta):
             return out
-        lp_delta = cp_objective_delta / self.lp.obj_scale
+        # TRICKY (:2370-2374): only the objective value carries the LP's
+        # objective scaling factor; rc and x are the simplex's own.
+        lp_delta = cp_objective_delta / self.lp_data.obj_scale
         rc = np.asarray(self.h.reduced_costs()) if rc is None else rc
         x = np.asarray(self.h.primal()) if x is None else x
         for col in self.int_cols:
             c = float(rc[col])
             if c == 0.0:
                 continue
-            other = float(x[col]) + lp_delta / c
+            other = self.scaler.unscale_variable_value(int(col), float(x[col]) + lp_delta / c)
             if c > K_LP_EPSILON:
                 new_ub = math.floor(other + K_CP_EPSILON)
                 if new_ub < trail.ub[col]:
@@ -270,14 +290,14 @@ class LpConstraint:
         lbs = trail.lb.copy()
         ubs = trail.ub.copy()
         ubs[col] = math.floor(value)
-        self.h.set_variable_bounds(lbs, ubs)
+        self.h.set_variable_bounds(*self.scale_bounds(lbs, ubs))
         lower = self.solve_lp_for_branching()
         ubs[col] = ub
         lbs[col] = math.ceil(value)
         upper = None
         if _usable(lower) and not (lower.status != abi.DUAL_UNBOUNDED and
                                    lower.new_obj_bound <= trail.obj_lb):
-            self.h.set_variable_bounds(lbs, ubs)
+            self.h.set_variable_bounds(*self.scale_bounds(lbs, ubs))
             upper = self.solve_lp_for_branching()
         self.update_bounds(trail)
         return fold_branch(col, value, lower, upper, trail)
