@@ -160,6 +160,7 @@ class DeviceLp : public DeviceSolver {
     std::vector<int> runs;
     int chain_levels = 0;             // levels in narrow segments
     int max_wide_run = 0;             // positions of the largest chip-wide segment
+    int level0_end = 0;               // positions of a chip-wide level 0 (the init fuses it)
   };
   struct TriContext {  // one solving thread's stream, values and graphs
     void* stream = nullptr;

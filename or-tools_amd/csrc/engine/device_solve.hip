@@ -185,6 +185,9 @@ void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, cons
     s->runs.insert(s->runs.end(), {b, e, seg_level[i + 2]});
     if (seg_level[i + 2] == 0) s->max_wide_run = std::max(s->max_wide_run, e - b);
   }
+  // Level 0 on the chip (not in a narrow run): its outputs are a division of
+  // their input, done by the init kernel of a sync-free solve.
+  s->level0_end = (!narrow[0] && depth >= 0) ? level_start[1] : 0;
   num_work = level_start[depth + 1];  // listed outputs + padding
   const int num_pos = num_work + (nc - fni);  // + every row, read-only copies
   s->work = num_work;
@@ -440,6 +443,7 @@ milp_kernels::TriSolveArgs DeviceLp::TriArgs(const TriSchedule& s, const TriCont
   a.fail2 = nullptr;
   a.seg_begin = 0;
   a.seg_end = s.work;
+  a.level0_end = tri_fuse0_ ? s.level0_end : 0;
   return a;
 }
 

@@ -952,6 +952,8 @@ void UpdateRow::ComputeFullUpdateRow(int leaving_row,
 // ---------------------------------------------------------------------------
 // PrimalEdgeNorms (primal_edge_norms.cc)
 class PrimalEdgeNorms {
+  friend struct SdualBridge;
+
  public:
   PrimalEdgeNorms(const CompactSparseMatrix& m, const VariablesInfo& vi,
                   const BasisFactorization& bf, DeviceLp* dev)
@@ -1750,6 +1752,8 @@ void ReducedCosts::UpdateReducedCosts(int entering_col, int leaving_col, int lea
 // ---------------------------------------------------------------------------
 // PrimalPrices (reduced_costs.cc:512-600)
 class PrimalPrices {
+  friend struct SdualBridge;
+
  public:
   PrimalPrices(Rng* random, const VariablesInfo& vi, PrimalEdgeNorms* pen,
                ReducedCosts* rc)

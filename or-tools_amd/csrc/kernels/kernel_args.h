@@ -349,6 +349,9 @@ struct TriSolveArgs {
   // Earlier segments are final in y when a launch starts.
   int seg_begin;
   int seg_end;
+  // Sync-free plans: positions [0, level0_end) are level 0 (no entries, a
+  // division at most), computed by tri_init_kernel; 0 = not fused.
+  int level0_end;
 };
 // The argument set of right-hand side blockIdx.y (0 or 1).
 __host__ __device__ inline TriSolveArgs TriRhs(const TriSolveArgs& a, int rhs) {

@@ -386,7 +386,9 @@ __device__ __forceinline__ bool tri_pending(double v) {
   return static_cast<unsigned long long>(__double_as_longlong(v)) == kTriPending;
 }
 
-// y[k] = x[row(k)], or "pending" for the outputs this solve computes.
+// y[k] = x[row(k)], or "pending" for the outputs this solve computes; the
+// outputs of a fused level 0 (k < level0_end: no entries) are computed here,
+// their input divided as tri_apply divides it, and scattered to x.
 __global__ __launch_bounds__(256) void tri_init_kernel(TriSolveArgs a0) {
   const TriSolveArgs a = TriRhs(a0, blockIdx.y);
   const int top = *a.top;
@@ -394,12 +396,24 @@ __global__ __launch_bounds__(256) void tri_init_kernel(TriSolveArgs a0) {
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.num_pos;
        k += gridDim.x * blockDim.x) {
     const int row = a.pos_row[k];
+    double v;
+    if (k < a.level0_end) {
+      const int rrow = a.rec_row[k];  // INT32_MAX for padding
+      v = a.x[row];
+      if (rrow <= top) {
+        if (a.diag != nullptr) {
+          v = a.sequential ? tri_sequential_divide(a, v, a.diag[k]) : v / a.diag[k];
+        }
+        a.x[row] = v;  // the scatter, fused
+      }
+    } else {
+      v = (k < a.num_work && row <= top) ? pending : a.x[row];
+    }
     // Write-through (sc1) stores: a plain store would leave the line valid in
     // this XCD's L2, and a reader on this XCD would then poll that stale copy
     // (pending) until the line is evicted, long after its producer on
     // another XCD stored the final value.
-    __hip_atomic_store(a.y + k, (k < a.num_work && row <= top) ? pending : a.x[row],
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.y + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -447,15 +461,19 @@ __device__ __forceinline__ void tri_syncfree_output(const TriSolveArgs& a, int k
   int backoff = 1;
   const uint64_t t0 = wall_clock64();  // 100 MHz
   if (r.n <= 4) {
-    // One poll round loads all entries at once and keeps them: the values
-    // that end the wait are the ones the output is computed from (a hop is
-    // one round trip, not a readiness walk plus a reload).
+    // One poll round loads the entries still pending at once and keeps them:
+    // the values that end the wait are the ones the output is computed from
+    // (a hop is one round trip, not a readiness walk plus a reload), and a
+    // final value is never loaded twice.
     const int n = r.n;
+    const double pend = __longlong_as_double(static_cast<long long>(kTriPending));
+    double y0 = n > 0 ? pend : 0.0, y1 = n > 1 ? pend : 0.0;
+    double y2 = n > 2 ? pend : 0.0, y3 = n > 3 ? pend : 0.0;
     while (!done) {
-      const double y0 = n > 0 ? load_final(y, r.e.x) : 0.0;
-      const double y1 = n > 1 ? load_final(y, r.e.y) : 0.0;
-      const double y2 = n > 2 ? load_final(y, r.e.z) : 0.0;
-      const double y3 = n > 3 ? load_final(y, r.e.w) : 0.0;
+      if (tri_pending(y0)) y0 = load_final(y, r.e.x);
+      if (tri_pending(y1)) y1 = load_final(y, r.e.y);
+      if (tri_pending(y2)) y2 = load_final(y, r.e.z);
+      if (tri_pending(y3)) y3 = load_final(y, r.e.w);
       const bool pending = tri_pending(y0) || tri_pending(y1) || tri_pending(y2) ||
                            tri_pending(y3);
       if (!pending) {
@@ -572,7 +590,7 @@ __global__ __launch_bounds__(kTriThreads) void tri_syncfree_persistent_kernel(Tr
   const int total = (gridDim.x / xcd_stride) * kTriThreads;
   const int top = *a.top;
   for (int k = group * kTriThreads + threadIdx.x; k < a.num_work; k += total) {
-    tri_syncfree_output(a, k, top);
+    if (k >= a.level0_end) tri_syncfree_output(a, k, top);  // level 0: the init's
   }
 }
 
@@ -586,144 +604,203 @@ __global__ __launch_bounds__(kTriThreads) void tri_syncfree_persistent_kernel(Tr
 // evaluated exactly as tri_syncfree_output evaluates it (same operations in
 // the same order, long outputs folding as their inputs arrive); earlier
 // segments are final in y, and the outputs go to y for later ones.
+//
+// The segment's inputs x[row] are loaded into LDS by the whole workgroup
+// first, with a ready word per position (1: final -- an output of this
+// segment once computed, or a position it does not compute), so an output's
+// input comes from LDS and only its record from global memory. A value is
+// stored before its ready word (workgroup release / acquire).
 __device__ __forceinline__ double tri_chain_load(const TriSolveArgs& a, const double* vals,
-                                                 int p) {
+                                                 const int* ready, int p) {
   if (p >= a.seg_begin && p < a.seg_end) {
-    return __hip_atomic_load(vals + (p - a.seg_begin), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__hip_atomic_load(ready + (p - a.seg_begin), __ATOMIC_ACQUIRE,
+                          __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+      return __longlong_as_double(static_cast<long long>(kTriPending));
+    }
+    return vals[p - a.seg_begin];
   }
   return load_final(a.y, p);
+}
+
+// An entry's value when an output starts: earlier segments' values are final
+// in y (loaded once, kept in registers), this segment's come from LDS when
+// ready, else the pending mark; polls then re-read only pending entries,
+// from LDS.
+__device__ __forceinline__ double tri_chain_first(const TriSolveArgs& a, const double* vals,
+                                                  const int* ready, int p) {
+  if (p >= a.seg_begin && p < a.seg_end) return tri_chain_load(a, vals, ready, p);
+  return load_final(a.y, p);
+}
+__device__ __forceinline__ double tri_chain_refresh(const TriSolveArgs& a, const double* vals,
+                                                    const int* ready, int p, double cur) {
+  return tri_pending(cur) ? tri_chain_load(a, vals, ready, p) : cur;
 }
 
 __global__ __launch_bounds__(kTriThreads) void tri_chain_kernel(TriSolveArgs a0) {
   const TriSolveArgs a = TriRhs(a0, blockIdx.y);
   __shared__ double vals[kTriChainVals];
+  __shared__ int ready[kTriChainVals];
   const int cs = a.seg_begin;
   const int ce = a.seg_end;
   const int top = *a.top;
-  const double pending = __longlong_as_double(static_cast<long long>(kTriPending));
-  for (int k = cs + threadIdx.x; k < ce; k += kTriThreads) {
-    const int row = a.rec_row[k];
-    vals[k - cs] = row <= top ? pending : a.x[min(row, a.num_rows - 1)];
-  }
-  __syncthreads();
-  int k = cs + threadIdx.x;
-  TriRec r;
-  bool have = false;
-  double sum = 0.0;
-  int e = 0, end = 0;
-  int wpos[8];
-  double wval[8];
-  uint64_t t_progress = wall_clock64();
-  int polls = 0;
-  while (true) {
-    if (!have) {
-      if (k >= ce) break;
-      tri_load(a, k, ce, top, &r);
-      if (r.row > top) {  // not computed: vals holds x[row]
-        k += kTriThreads;
-        continue;
-      }
-      sum = a.x[r.row];
-      have = true;
-      if (r.n > 4) {
-        e = r.e.x;
-        end = r.e.x + r.n;
+  {
+    // Eight positions per thread in flight: the rows, then their inputs.
+    for (int k0 = cs + threadIdx.x; k0 < ce; k0 += 8 * kTriThreads) {
+      int row[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          wpos[i] = e + i < end ? a.ovf_pos[e + i] : 0;
-          wval[i] = e + i < end ? a.ovf_value[e + i] : 0.0;
-        }
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u * kTriThreads;
+        row[u] = k < ce ? a.rec_row[k] : INT32_MAX;
       }
-    }
-    bool finished = false;
-    bool progress = false;
-    double out = 0.0;
-    if (r.n <= 4) {
-      const int n = r.n;
-      const double y0 = n > 0 ? tri_chain_load(a, vals, r.e.x) : 0.0;
-      const double y1 = n > 1 ? tri_chain_load(a, vals, r.e.y) : 0.0;
-      const double y2 = n > 2 ? tri_chain_load(a, vals, r.e.z) : 0.0;
-      const double y3 = n > 3 ? tri_chain_load(a, vals, r.e.w) : 0.0;
-      if (!(tri_pending(y0) || tri_pending(y1) || tri_pending(y2) || tri_pending(y3))) {
-        out = tri_apply4(a, sum, r, y0, y1, y2, y3);
-        finished = true;
-      }
-    } else {
-      // The window [e, e + 8) of entries sits in registers; a poll reloads
-      // only the values.
       double v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = e + i < end ? tri_chain_load(a, vals, wpos[i]) : 0.0;
-      int took = 0;
-      if (a.sequential) {
+      for (int u = 0; u < 8; ++u) {
+        v[u] = row[u] < a.num_rows ? a.x[row[u]] : 0.0;
+      }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (took != i || e + i >= end || tri_pending(v[i])) continue;
-          if (v[i] != 0.0) sum -= v[i] * wval[i];
-          took = i + 1;
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u * kTriThreads;
+        if (k < ce) {
+          vals[k - cs] = v[u];
+          ready[k - cs] = row[u] <= top ? 0 : 1;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // Thread t's outputs are positions t, t + T, ... of the segment, taken in
+  // that order by a uniform outer loop: every lane of a wave loads its
+  // output's record and entries (global loads) together, then the wave polls
+  // LDS only until all its lanes are done. A lane waiting on LDS is never held
+  // behind another lane's global load (a hand-off costs an LDS round trip).
+  // Long outputs fold their entries by windows of 8 as they become final.
+  uint64_t t_progress = wall_clock64();
+  bool failed = false;
+  for (int k = cs + threadIdx.x; k < ce && !failed; k += kTriThreads) {
+    if (ready[k - cs] != 0) continue;  // not computed: keeps its input
+    TriRec r;
+    tri_load(a, k, ce, top, &r);
+    double sum = vals[k - cs];
+    int e = 0, end = 0;
+    int wpos[8];
+    double wval[8];
+    double v[8];  // entry values, the pending mark until final
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = 0.0;
+    if (r.n > 4) {
+      e = r.e.x;
+      end = r.e.x + r.n;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        wpos[u] = e + u < end ? a.ovf_pos[e + u] : 0;
+        wval[u] = e + u < end ? a.ovf_value[e + u] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = e + u < end ? tri_chain_first(a, vals, ready, wpos[u]) : 0.0;
+    } else {
+      const int n = r.n;
+      v[0] = n > 0 ? tri_chain_first(a, vals, ready, r.e.x) : 0.0;
+      v[1] = n > 1 ? tri_chain_first(a, vals, ready, r.e.y) : 0.0;
+      v[2] = n > 2 ? tri_chain_first(a, vals, ready, r.e.z) : 0.0;
+      v[3] = n > 3 ? tri_chain_first(a, vals, ready, r.e.w) : 0.0;
+    }
+    int polls = 0;
+    while (true) {
+      bool finished = false;
+      bool progress = false;
+      double out = 0.0;
+      if (r.n <= 4) {
+        if (!(tri_pending(v[0]) || tri_pending(v[1]) || tri_pending(v[2]) || tri_pending(v[3]))) {
+          out = tri_apply4(a, sum, r, v[0], v[1], v[2], v[3]);
+          finished = true;
         }
       } else {
+        int took = 0;
+        if (a.sequential) {
 #pragma unroll
-        for (int g = 0; g < 8; g += 4) {
-          if (took != g || e + g + 3 >= end) continue;
-          if (tri_pending(v[g]) || tri_pending(v[g + 1]) || tri_pending(v[g + 2]) ||
-              tri_pending(v[g + 3])) {
-            continue;
+          for (int u = 0; u < 8; ++u) {
+            if (took != u || e + u >= end || tri_pending(v[u])) continue;
+            if (v[u] != 0.0) sum -= v[u] * wval[u];
+            took = u + 1;
           }
-          sum -= wval[g] * v[g] + wval[g + 1] * v[g + 1] + wval[g + 2] * v[g + 2] +
-                 wval[g + 3] * v[g + 3];
-          took = g + 4;
-        }
-        const int left = end - e - took;
-        if (took < 8 && left > 0 && left < 4) {
-          const int t = took;
-          bool ready = true;
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            if (i < left && t + i < 8) ready = ready && !tri_pending(v[t + i]);
-          }
-          if (ready && t + left <= 8) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-              if (i < left) sum -= wval[t + i] * v[t + i];
-            }
-            took = t + left;
-          }
-        }
-      }
-      if (took > 0) {
-        e += took;
-        progress = true;
-        if (e == end) {
-          out = a.sequential ? tri_sequential_divide(a, sum, r.d)
-                             : (a.diag != nullptr ? sum / r.d : sum);
-          finished = true;
         } else {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            wpos[i] = e + i < end ? a.ovf_pos[e + i] : 0;
-            wval[i] = e + i < end ? a.ovf_value[e + i] : 0.0;
+          for (int g = 0; g < 8; g += 4) {
+            if (took != g || e + g + 3 >= end) continue;
+            if (tri_pending(v[g]) || tri_pending(v[g + 1]) || tri_pending(v[g + 2]) ||
+                tri_pending(v[g + 3])) {
+              continue;
+            }
+            sum -= wval[g] * v[g] + wval[g + 1] * v[g + 1] + wval[g + 2] * v[g + 2] +
+                   wval[g + 3] * v[g + 3];
+            took = g + 4;
+          }
+          const int left = end - e - took;
+          if (took < 8 && left > 0 && left < 4) {
+            const int t = took;
+            bool all_final = true;
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+              if (u < left && t + u < 8) all_final = all_final && !tri_pending(v[t + u]);
+            }
+            if (all_final && t + left <= 8) {
+#pragma unroll
+              for (int u = 0; u < 3; ++u) {
+                if (u < left) sum -= wval[t + u] * v[t + u];
+              }
+              took = t + left;
+            }
+          }
+        }
+        if (took > 0) {
+          e += took;
+          progress = true;
+          if (e == end) {
+            out = a.sequential ? tri_sequential_divide(a, sum, r.d)
+                               : (a.diag != nullptr ? sum / r.d : sum);
+            finished = true;
+          } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              wpos[u] = e + u < end ? a.ovf_pos[e + u] : 0;
+              wval[u] = e + u < end ? a.ovf_value[e + u] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              v[u] = e + u < end ? tri_chain_first(a, vals, ready, wpos[u]) : 0.0;
+            }
           }
         }
       }
-    }
-    if (finished) {
-      __hip_atomic_store(vals + (k - cs), out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_store(a.y + k, out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      a.x[r.row] = out;  // the scatter, fused
-      have = false;
-      k += kTriThreads;
-      progress = true;
-    }
-    if (progress) {
-      polls = 0;
-    } else if (++polls % 64 == 0) {
-      const uint64_t now = wall_clock64();
-      if (polls == 64) t_progress = now;  // first stalled check of this wait
-      if (now - t_progress > kTriMaxWaitTicks) {
-        if (a.fail != nullptr) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (finished) {
+        vals[k - cs] = out;
+        __hip_atomic_store(ready + (k - cs), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(a.y + k, out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.x[r.row] = out;  // the scatter, fused
         break;
+      }
+      // A wave none of whose lanes moved yields its issue slots for a moment
+      // (the LDS polls of 16 waves would otherwise crowd the producers).
+      if (__ballot(progress) == 0) __builtin_amdgcn_s_sleep(1);
+      if (progress) {
+        polls = 0;
+      } else if (++polls % 64 == 0) {
+        const uint64_t now = wall_clock64();
+        if (polls == 64) t_progress = now;  // first stalled check of this wait
+        if (now - t_progress > kTriMaxWaitTicks) {
+          if (a.fail != nullptr) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          failed = true;
+          break;
+        }
+      }
+      if (r.n <= 4) {
+        v[0] = tri_chain_refresh(a, vals, ready, r.e.x, v[0]);
+        v[1] = tri_chain_refresh(a, vals, ready, r.e.y, v[1]);
+        v[2] = tri_chain_refresh(a, vals, ready, r.e.z, v[2]);
+        v[3] = tri_chain_refresh(a, vals, ready, r.e.w, v[3]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = tri_chain_refresh(a, vals, ready, wpos[u], v[u]);
       }
     }
   }
@@ -751,7 +828,8 @@ hipError_t tri_transpose_lower_syncfree(const milp_kernels::TriSolveArgs& args,
   if (e != hipSuccess) return e;
   milp_kernels::TriSolveArgs a = args;
   for (int i = 0; i < num_segs; ++i) {
-    a.seg_begin = segs[3 * i];
+    // Positions of a fused level 0 were computed by the init kernel.
+    a.seg_begin = std::max(segs[3 * i], args.level0_end);
     a.seg_end = segs[3 * i + 1];
     if (a.seg_end <= a.seg_begin) continue;
     if (segs[3 * i + 2] != 0) {

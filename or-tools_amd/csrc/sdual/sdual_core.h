@@ -2110,7 +2110,7 @@ SD_INLINE f64 bf_dual_edge_squared_norm(Lp& s, int row) {
   bf_bump(s, 1);
   if (s.is_identity) return 1.0;
   const int pr = s.col_perm_empty ? row : s.col_perm[row];
-  int32_t* nz = s.dp_equiv;  // non_zero_rows_ scratch
+  int32_t* nz = s.dp.equiv;  // non_zero_rows_ scratch
   int nnz = 0;
   f64* z = s.zero_scratch;
   z[pr] = 1.0;
@@ -2205,61 +2205,61 @@ SD_INLINE void bf_right_solve_for_column(Lp& s, int col, Vec& d) {
 
 // ---- DynamicMaximum (pricing.h:152-345) ----
 // HeapLess: a.value > b.value (min-heap); libstdc++ make_heap restated.
-SD_INLINE void dp_push_heap(Lp& s, int hole, int top, int vi, f64 vv) {
+SD_INLINE void dp_push_heap(Lp& s, DynMax& d, int hole, int top, int vi, f64 vv) {
   int parent = (hole - 1) / 2;
-  while (hole > top && s.dp_tops_val[parent] > vv) {
-    s.dp_tops_idx[hole] = s.dp_tops_idx[parent];
-    s.dp_tops_val[hole] = s.dp_tops_val[parent];
+  while (hole > top && d.tops_val[parent] > vv) {
+    d.tops_idx[hole] = d.tops_idx[parent];
+    d.tops_val[hole] = d.tops_val[parent];
     hole = parent;
     parent = (hole - 1) / 2;
   }
-  s.dp_tops_idx[hole] = vi;
-  s.dp_tops_val[hole] = vv;
+  d.tops_idx[hole] = vi;
+  d.tops_val[hole] = vv;
 }
-SD_INLINE void dp_adjust_heap(Lp& s, int hole, int len, int vi, f64 vv) {
+SD_INLINE void dp_adjust_heap(Lp& s, DynMax& d, int hole, int len, int vi, f64 vv) {
   const int top = hole;
   int second = hole;
   while (second < (len - 1) / 2) {
     second = 2 * (second + 1);
-    if (s.dp_tops_val[second] > s.dp_tops_val[second - 1]) second--;
-    s.dp_tops_idx[hole] = s.dp_tops_idx[second];
-    s.dp_tops_val[hole] = s.dp_tops_val[second];
+    if (d.tops_val[second] > d.tops_val[second - 1]) second--;
+    d.tops_idx[hole] = d.tops_idx[second];
+    d.tops_val[hole] = d.tops_val[second];
     hole = second;
   }
   if ((len & 1) == 0 && second == (len - 2) / 2) {
     second = 2 * (second + 1);
-    s.dp_tops_idx[hole] = s.dp_tops_idx[second - 1];
-    s.dp_tops_val[hole] = s.dp_tops_val[second - 1];
+    d.tops_idx[hole] = d.tops_idx[second - 1];
+    d.tops_val[hole] = d.tops_val[second - 1];
     hole = second - 1;
   }
-  dp_push_heap(s, hole, top, vi, vv);
+  dp_push_heap(s, d, hole, top, vi, vv);
 }
-SD_INLINE void dp_make_heap(Lp& s) {
-  const int len = s.dp_ntops;
+SD_INLINE void dp_make_heap(Lp& s, DynMax& d) {
+  const int len = d.ntops;
   if (len < 2) return;
   int parent = (len - 2) / 2;
   while (true) {
-    const int vi = s.dp_tops_idx[parent];
-    const f64 vv = s.dp_tops_val[parent];
-    dp_adjust_heap(s, parent, len, vi, vv);
+    const int vi = d.tops_idx[parent];
+    const f64 vv = d.tops_val[parent];
+    dp_adjust_heap(s, d, parent, len, vi, vv);
     if (parent == 0) return;
     parent--;
   }
 }
-SD_INLINE void dp_update_top_k(Lp& s, int position, f64 value) {
+SD_INLINE void dp_update_top_k(Lp& s, DynMax& d, int position, f64 value) {
   const int k = 31;
-  if (s.dp_ntops < k) {
-    s.dp_tops_idx[s.dp_ntops] = position;
-    s.dp_tops_val[s.dp_ntops] = value;
-    ++s.dp_ntops;
-    if (s.dp_ntops == k) {
-      dp_make_heap(s);
-      s.dp_threshold = s.dp_tops_val[0];
+  if (d.ntops < k) {
+    d.tops_idx[d.ntops] = position;
+    d.tops_val[d.ntops] = value;
+    ++d.ntops;
+    if (d.ntops == k) {
+      dp_make_heap(s, d);
+      d.threshold = d.tops_val[0];
     }
     return;
   }
-  if (value == s.dp_tops_val[0]) {
-    if (bernoulli(s, 0.5)) s.dp_tops_idx[0] = position;
+  if (value == d.tops_val[0]) {
+    if (bernoulli(s, 0.5)) d.tops_idx[0] = position;
     return;
   }
   int i = 0;
@@ -2267,53 +2267,53 @@ SD_INLINE void dp_update_top_k(Lp& s, int position, f64 value) {
   for (; i < limit;) {
     const int left = 2 * i + 1;
     const int right = left + 1;
-    const f64 lv = s.dp_tops_val[left];
-    const f64 rv = s.dp_tops_val[right];
+    const f64 lv = d.tops_val[left];
+    const f64 rv = d.tops_val[right];
     if (lv > rv) {
       if (value <= rv) break;
-      s.dp_tops_idx[i] = s.dp_tops_idx[right];
-      s.dp_tops_val[i] = s.dp_tops_val[right];
+      d.tops_idx[i] = d.tops_idx[right];
+      d.tops_val[i] = d.tops_val[right];
       i = right;
     } else {
       if (value <= lv) break;
-      s.dp_tops_idx[i] = s.dp_tops_idx[left];
-      s.dp_tops_val[i] = s.dp_tops_val[left];
+      d.tops_idx[i] = d.tops_idx[left];
+      d.tops_val[i] = d.tops_val[left];
       i = left;
     }
   }
-  s.dp_tops_idx[i] = position;
-  s.dp_tops_val[i] = value;
-  s.dp_threshold = s.dp_tops_val[0];
+  d.tops_idx[i] = position;
+  d.tops_val[i] = value;
+  d.threshold = d.tops_val[0];
 }
-SD_INLINE void dp_clear_and_resize(Lp& s, int n) {
-  s.dp_ntops = 0;
-  s.dp_threshold = -sd_inf();
-  for (int i = s.dp_size + sd_lane(); i < n; i += sd_lanes()) s.dp_values[i] = 0.0;
-  s.dp_size = n;
+SD_INLINE void dp_clear_and_resize(Lp& s, DynMax& d, int n) {
+  d.ntops = 0;
+  d.threshold = -sd_inf();
+  for (int i = d.size + sd_lane(); i < n; i += sd_lanes()) d.values[i] = 0.0;
+  d.size = n;
   const int words = (n + 63) / 64;
-  for (int w = sd_lane(); w < words; w += sd_lanes()) s.dp_cand[w] = 0;
+  for (int w = sd_lane(); w < words; w += sd_lanes()) d.cand[w] = 0;
   sd_sync();
 }
-SD_INLINE void dp_start_dense_updates(Lp& s) {
-  s.dp_ntops = 0;
-  s.dp_threshold = sd_inf();
+SD_INLINE void dp_start_dense_updates(Lp& s, DynMax& d) {
+  d.ntops = 0;
+  d.threshold = sd_inf();
 }
-SD_INLINE void dp_dense_add_or_update(Lp& s, int position, f64 value) {
-  bit_set(s.dp_cand, position);
-  s.dp_values[position] = value;
+SD_INLINE void dp_dense_add_or_update(Lp& s, DynMax& d, int position, f64 value) {
+  bit_set(d.cand, position);
+  d.values[position] = value;
 }
-SD_INLINE void dp_add_or_update(Lp& s, int position, f64 value) {
-  bit_set(s.dp_cand, position);
-  s.dp_values[position] = value;
-  if (value >= s.dp_threshold) dp_update_top_k(s, position, value);
+SD_INLINE void dp_add_or_update(Lp& s, DynMax& d, int position, f64 value) {
+  bit_set(d.cand, position);
+  d.values[position] = value;
+  if (value >= d.threshold) dp_update_top_k(s, d, position, value);
 }
-SD_INLINE void dp_remove(Lp& s, int position) { bit_clear(s.dp_cand, position); }
-SD_INLINE int dp_randomize(Lp& s, int best, int n_equiv) {
+SD_INLINE void dp_remove(Lp& s, DynMax& d, int position) { bit_clear(d.cand, position); }
+SD_INLINE int dp_randomize(Lp& s, DynMax& d, int best, int n_equiv) {
   if (n_equiv == 0) return best;
-  s.dp_equiv[n_equiv++] = best;
-  return s.dp_equiv[uniform_int(s, n_equiv - 1)];
+  d.equiv[n_equiv++] = best;
+  return d.equiv[uniform_int(s, n_equiv - 1)];
 }
-SD_INLINE int dp_get_maximum(Lp& s) {
+SD_INLINE int dp_get_maximum(Lp& s, DynMax& d) {
   SdSubTimer t_sub_(&s.phase_ticks[27]);
   f64 best_value = -sd_inf();
   int best_position = -1;
@@ -2321,29 +2321,29 @@ SD_INLINE int dp_get_maximum(Lp& s) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const int lane = sd_lane();
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  if (s.dp_ntops != 0) {
+  if (d.ntops != 0) {
     // The tops on the lanes (at most 31): the kept ones (still candidates
     // with an unchanged value) compacted in order; the maximum's first
     // occurrence is the best position, its later ones the equivalent
     // choices in order (the sequential loop's result).
-    const int n = s.dp_ntops;
+    const int n = d.ntops;
     int idx = 0;
     f64 val = -sd_inf();
     bool kept = false;
     if (lane < n) {
-      idx = s.dp_tops_idx[lane];
-      val = s.dp_tops_val[lane];
-      kept = bit_get(s.dp_cand, idx) && s.dp_values[idx] == val;
+      idx = d.tops_idx[lane];
+      val = d.tops_val[lane];
+      kept = bit_get(d.cand, idx) && d.values[idx] == val;
     }
     const uint64_t kmask = __ballot(kept);
     const int new_size = __popcll(kmask);
     sd_sync();
     if (kept) {
       const int pos = __popcll(kmask & below);
-      s.dp_tops_idx[pos] = idx;
-      s.dp_tops_val[pos] = val;
+      d.tops_idx[pos] = idx;
+      d.tops_val[pos] = val;
     }
-    s.dp_ntops = new_size;
+    d.ntops = new_size;
     if (new_size != 0) {
       const f64 top = sd_wave_max(kept ? val : -sd_inf());
       const uint64_t emask = __ballot(kept && val == top);
@@ -2351,35 +2351,35 @@ SD_INLINE int dp_get_maximum(Lp& s) {
       best_position = __shfl(idx, first, 64);
       n_equiv = __popcll(emask) - 1;
       if (((emask >> lane) & 1) && lane != first) {
-        s.dp_equiv[__popcll(emask & below) - 1] = idx;
+        d.equiv[__popcll(emask & below) - 1] = idx;
       }
       sd_sync();
-      return dp_randomize(s, best_position, n_equiv);
+      return dp_randomize(s, d, best_position, n_equiv);
     }
     sd_sync();
   }
   // Rescan: 64 positions at a time, candidates below the threshold at the
   // chunk's start skipped on the lanes (the threshold never decreases), the
   // others replayed in order.
-  s.dp_threshold = -sd_inf();
-  for (int base = 0; base < s.dp_size; base += 64) {
+  d.threshold = -sd_inf();
+  for (int base = 0; base < d.size; base += 64) {
     const int position = base + lane;
     f64 value = 0.0;
     bool cand = false;
-    if (position < s.dp_size && bit_get(s.dp_cand, position)) {
-      value = s.dp_values[position];
-      cand = value >= s.dp_threshold;
+    if (position < d.size && bit_get(d.cand, position)) {
+      value = d.values[position];
+      cand = value >= d.threshold;
     }
     uint64_t mask = __ballot(cand);
     while (mask != 0) {
       const int l = __builtin_ctzll(mask);
       mask &= mask - 1;
       const f64 v = __shfl(value, l, 64);
-      if (v < s.dp_threshold) continue;
-      dp_update_top_k(s, base + l, v);
+      if (v < d.threshold) continue;
+      dp_update_top_k(s, d, base + l, v);
       if (v >= best_value) {
         if (v == best_value) {
-          s.dp_equiv[n_equiv++] = base + l;
+          d.equiv[n_equiv++] = base + l;
           continue;
         }
         n_equiv = 0;
@@ -2389,29 +2389,29 @@ SD_INLINE int dp_get_maximum(Lp& s) {
     }
   }
   sd_sync();
-  return dp_randomize(s, best_position, n_equiv);
+  return dp_randomize(s, d, best_position, n_equiv);
 #endif
-  if (s.dp_ntops != 0) {
+  if (d.ntops != 0) {
     // iterate over a copy of tops_ (the loop compacts in place)
     int32_t cidx[32];
     f64 cval[32];
-    const int n = s.dp_ntops;
+    const int n = d.ntops;
     for (int k = 0; k < n; ++k) {
-      cidx[k] = s.dp_tops_idx[k];
-      cval[k] = s.dp_tops_val[k];
+      cidx[k] = d.tops_idx[k];
+      cval[k] = d.tops_val[k];
     }
     int new_size = 0;
     for (int k = 0; k < n; ++k) {
       const int idx = cidx[k];
       const f64 val = cval[k];
-      if (!bit_get(s.dp_cand, idx)) continue;
-      if (s.dp_values[idx] != val) continue;
-      s.dp_tops_idx[new_size] = idx;
-      s.dp_tops_val[new_size] = val;
+      if (!bit_get(d.cand, idx)) continue;
+      if (d.values[idx] != val) continue;
+      d.tops_idx[new_size] = idx;
+      d.tops_val[new_size] = val;
       ++new_size;
       if (val >= best_value) {
         if (val == best_value) {
-          s.dp_equiv[n_equiv++] = idx;
+          d.equiv[n_equiv++] = idx;
           continue;
         }
         n_equiv = 0;
@@ -2419,23 +2419,23 @@ SD_INLINE int dp_get_maximum(Lp& s) {
         best_position = idx;
       }
     }
-    s.dp_ntops = new_size;
-    if (new_size != 0) return dp_randomize(s, best_position, n_equiv);
+    d.ntops = new_size;
+    if (new_size != 0) return dp_randomize(s, d, best_position, n_equiv);
   }
-  s.dp_threshold = -sd_inf();
-  const int words = (s.dp_size + 63) / 64;
+  d.threshold = -sd_inf();
+  const int words = (d.size + 63) / 64;
   for (int w = 0; w < words; ++w) {
-    uint64_t word = s.dp_cand[w];
+    uint64_t word = d.cand[w];
     while (word) {
       const int position = w * 64 + sd_ctz(word);
       word &= word - 1;
-      if (position >= s.dp_size) break;
-      const f64 value = s.dp_values[position];
-      if (value < s.dp_threshold) continue;
-      dp_update_top_k(s, position, value);
+      if (position >= d.size) break;
+      const f64 value = d.values[position];
+      if (value < d.threshold) continue;
+      dp_update_top_k(s, d, position, value);
       if (value >= best_value) {
         if (value == best_value) {
-          s.dp_equiv[n_equiv++] = position;
+          d.equiv[n_equiv++] = position;
           continue;
         }
         n_equiv = 0;
@@ -2444,7 +2444,7 @@ SD_INLINE int dp_get_maximum(Lp& s) {
       }
     }
   }
-  return dp_randomize(s, best_position, n_equiv);
+  return dp_randomize(s, d, best_position, n_equiv);
 }
 
 // DualEdgeNorms::GetEdgeSquaredNorms (dual_edge_norms.cc:120-132)
@@ -2461,8 +2461,8 @@ SD_INLINE f64 row_infeasibility(const Lp& s, int col) {
   return sd_max(s.x[col] - s.ub[col], s.lb[col] - s.x[col]);
 }
 SD_INLINE void vv_recompute_dual_prices(Lp& s, int put_more_importance_on_norm) {
-  dp_clear_and_resize(s, s.m);
-  dp_start_dense_updates(s);
+  dp_clear_and_resize(s, s.dp, s.m);
+  dp_start_dense_updates(s, s.dp);
   s.put_more_importance_on_norm = put_more_importance_on_norm;
   const f64 tol = s.primal_feasibility_tolerance;
   norms_get(s);
@@ -2475,12 +2475,12 @@ SD_INLINE void vv_recompute_dual_prices(Lp& s, int put_more_importance_on_norm) 
       const f64 inf = row_infeasibility(s, s.basis[row]);
       if (inf > tol) {
         keep = true;
-        s.dp_values[row] = s.put_more_importance_on_norm ? sd_fabs(inf) / s.norms[row]
+        s.dp.values[row] = s.put_more_importance_on_norm ? sd_fabs(inf) / s.norms[row]
                                                          : sq(inf) / s.norms[row];
       }
     }
     const uint64_t word = __ballot(keep);
-    if (sd_lane() == 0) s.dp_cand[base >> 6] = word;
+    if (sd_lane() == 0) s.dp.cand[base >> 6] = word;
   }
   sd_sync();
 #else
@@ -2488,7 +2488,7 @@ SD_INLINE void vv_recompute_dual_prices(Lp& s, int put_more_importance_on_norm) 
     const int col = s.basis[row];
     const f64 inf = row_infeasibility(s, col);
     if (inf > tol) {
-      dp_dense_add_or_update(s, row, s.put_more_importance_on_norm
+      dp_dense_add_or_update(s, s.dp, row, s.put_more_importance_on_norm
                                          ? sd_fabs(inf) / s.norms[row]
                                          : sq(inf) / s.norms[row]);
     }
@@ -2499,16 +2499,16 @@ SD_INLINE void vv_update_dual_price(Lp& s, int row) {
   const int col = s.basis[row];
   const f64 inf = row_infeasibility(s, col);
   if (inf > s.primal_feasibility_tolerance) {
-    dp_add_or_update(s, row, s.put_more_importance_on_norm ? sd_fabs(inf) / s.norms[row]
+    dp_add_or_update(s, s.dp, row, s.put_more_importance_on_norm ? sd_fabs(inf) / s.norms[row]
                                                            : sq(inf) / s.norms[row]);
   } else {
-    dp_remove(s, row);
+    dp_remove(s, s.dp, row);
   }
 }
 // UpdateDualPrices(rows); the caller guarantees the norms are current.
 SD_INLINE void vv_update_dual_prices(Lp& s, const int32_t* rows, int n) {
   SdSubTimer t_sub_(&s.phase_ticks[19]);
-  if (s.dp_size != s.m) {
+  if (s.dp.size != s.m) {
     vv_recompute_dual_prices(s, s.put_more_importance_on_norm);
     return;
   }
@@ -2528,13 +2528,13 @@ SD_INLINE void vv_update_dual_prices(Lp& s, const int32_t* rows, int n) {
     if (k < n) {
       row = rows[k];
       const f64 inf = row_infeasibility(s, s.basis[row]);
-      unsigned long long* word = reinterpret_cast<unsigned long long*>(s.dp_cand + (row >> 6));
+      unsigned long long* word = reinterpret_cast<unsigned long long*>(s.dp.cand + (row >> 6));
       const unsigned long long bit = 1ull << (row & 63);
       if (inf > tol) {
         price = s.put_more_importance_on_norm ? sd_fabs(inf) / s.norms[row] : sq(inf) / s.norms[row];
-        s.dp_values[row] = price;
+        s.dp.values[row] = price;
         atomicOr(word, bit);
-        cand = price >= s.dp_threshold;
+        cand = price >= s.dp.threshold;
       } else {
         atomicAnd(word, ~bit);
       }
@@ -2545,7 +2545,7 @@ SD_INLINE void vv_update_dual_prices(Lp& s, const int32_t* rows, int n) {
       mask &= mask - 1;
       const int r = __shfl(row, l, 64);
       const f64 p = __shfl(price, l, 64);
-      if (p >= s.dp_threshold) dp_update_top_k(s, r, p);
+      if (p >= s.dp.threshold) dp_update_top_k(s, s.dp, r, p);
     }
   }
   sd_sync();
@@ -3212,6 +3212,7 @@ SD_INLINE void rs_make_boxed_dual_feasible(Lp& s) {
 SD_INLINE void rc_set_recompute_and_notify(Lp& s) {
   s.recompute_rc = 1;
   s.rc_notify = 1;
+  s.pp_recompute = 1;  // PrimalPrices::recompute_ watches the reduced costs
 }
 SD_INLINE void rc_make_precise(Lp& s) {
   if (s.rc_precise) return;
@@ -3466,7 +3467,7 @@ SD_INLINE void vv_recompute_basic_values(Lp& s) {
   bf_right_solve(s, v);
   for (int row = sd_lane(); row < s.m; row += sd_lanes()) s.x[s.basis[row]] = v.values[row];
   sd_sync();
-  dp_clear_and_resize(s, 0);  // dual_prices_->Clear()
+  dp_clear_and_resize(s, s.dp, 0);  // dual_prices_->Clear()
 }
 // PreciseScalarProduct(objective_, variable_values_) (lp_utils.h:106-114)
 SD_INLINE f64 rs_objective_value(const Lp& s) {
@@ -3490,6 +3491,88 @@ SD_INLINE bool sd_room_for_iteration(const Lp& s) {
     return false;
   if (s.r1_count + 1 > s.r1_cap) return false;
   return true;
+}
+
+// UpdateAndPivot (revised_simplex.cc:2504-2575) up to the factorization:
+// the pivot from the update row (or its ColumnScalarProduct with rho when the
+// row is not computed for leaving_row), UpdateBasis, the precision test, then
+// the MPF update (basis_representation.cc:258-340) or *refactor = 1
+// (ForceRefactorization) / 2 (the same after the LU threshold bump). Returns
+// kExitLuError for a degenerate rank-one update, else kExitNone.
+SD_INLINE int32_t sd_pivot(Lp& s, int entering_col, int leaving_row, f64 target_bound,
+                           int* refactor) {
+  *refactor = 0;
+  f64 pivot_from_update_row;
+  if (s.urow_for == leaving_row) {  // update_row_.IsComputedFor(leaving_row)
+    pivot_from_update_row = s.coeff[entering_col];
+  } else {
+    ur_compute_unit_row_left_inverse(s, leaving_row);
+    pivot_from_update_row = col_dot_par(s.A, entering_col, s.rho.values, s.lds_scratch);
+  }
+  const int lcol = s.basis[leaving_row];
+  const int8_t leaving_status = s.lb[lcol] == s.ub[lcol] ? kFixedValue
+                                : target_bound == s.lb[lcol] ? kAtLower
+                                                             : kAtUpper;
+  vi_to_nonbasic(s, lcol, leaving_status);  // UpdateBasis
+  s.basis[leaving_row] = entering_col;
+  vi_to_basic(s, entering_col);
+  ur_invalidate(s);
+  const f64 pivot_from_direction = s.dir.values[leaving_row];
+  const f64 diff = sd_fabs(pivot_from_update_row - pivot_from_direction);
+  s.exit_col = lcol;
+  if (diff > s.refactorization_threshold *
+                 (1.0 + sd_min(sd_fabs(pivot_from_update_row), sd_fabs(pivot_from_direction)))) {
+    *refactor = s.num_updates < 10 ? 2 : 1;
+  } else if (s.num_updates >= s.max_updates &&
+             (!s.dynamic_period || s.last_fact_dtime < s.r1_dtime)) {
+    *refactor = 1;  // BasisFactorization::Update (:304-340)
+  } else {
+    const int right_index = s.right_pool[entering_col];
+    const int left_index = s.left_pool[leaving_row];
+    ++s.num_updates;
+    if (right_index == kInvalid || left_index == kInvalid) {
+      *refactor = 1;
+    } else {
+      // MiddleProductFormUpdate (:258-302)
+      SdSubTimer t_x_(&s.phase_ticks[26]);
+      // Each column's rows are distinct: the lanes split them; the list
+      // entries keep their positions (right column, then U's column).
+      {
+        const int64_t rb = s.right_storage.starts[right_index];
+        const int rn = static_cast<int>(s.right_storage.starts[right_index + 1] - rb);
+        const int base = s.n_mpf_scratch_nz;
+        for (int k = sd_lane(); k < rn; k += sd_lanes()) {
+          const int r = s.right_storage.rows[rb + k];
+          s.mpf_scratch[r] = s.right_storage.coefs[rb + k];
+          s.mpf_scratch_nz[base + k] = r;
+        }
+        sd_sync();
+        s.n_mpf_scratch_nz = base + rn;
+      }
+      lu_column_of_u(s, leaving_row);
+      {
+        const int base = s.n_mpf_scratch_nz;
+        for (int k = sd_lane(); k < s.n_col_u; k += sd_lanes()) {
+          s.mpf_scratch[s.col_u_rows[k]] -= s.col_u_coefs[k];
+          s.mpf_scratch_nz[base + k] = s.col_u_rows[k];
+        }
+        sd_sync();
+        s.n_mpf_scratch_nz = base + s.n_col_u;
+      }
+      const f64 scalar_product = col_dot_par(s.storage, left_index, s.mpf_scratch, s.lds_scratch);
+      const int u_index =
+          store_add_and_clear(s.storage, s.mpf_scratch, s.mpf_scratch_nz, &s.n_mpf_scratch_nz);
+      const f64 mu = 1.0 + scalar_product;
+      if (mu == 0.0) return kExitLuError;
+      s.r1_u[s.r1_count] = u_index;
+      s.r1_v[s.r1_count] = left_index;
+      s.r1_mu[s.r1_count] = mu;
+      ++s.r1_count;
+      s.r1_num_entries += col_entries(s.storage, u_index) + col_entries(s.storage, left_index);
+      s.tau_can_opt = 0;
+    }
+  }
+  return kExitNone;
 }
 
 // The phase-II dual loop (revised_simplex.cc:3058-3367), entered after the
@@ -3561,8 +3644,8 @@ SD_INLINE int32_t sd_run(Lp& s) {
     at_top = true;
     SD_PHASE(1);
     // DualChooseLeavingVariableRow (:2148-2181)
-    if (s.dp_size == 0) vv_recompute_dual_prices(s, s.dual_price_prioritize_norm);
-    const int leaving_row = dp_get_maximum(s);
+    if (s.dp.size == 0) vv_recompute_dual_prices(s, s.dual_price_prioritize_norm);
+    const int leaving_row = dp_get_maximum(s, s.dp);
     if (leaving_row == kInvalid) {
       if (s.num_updates != 0 || s.has_cost_shift) {
         rc_clear_and_remove_cost_shifts(s);
@@ -3641,69 +3724,9 @@ SD_INLINE int32_t sd_run(Lp& s) {
     }
     s.x[entering_col] += primal_step;
     // UpdateAndPivot (:2504-2575)
-    const f64 pivot_from_update_row = s.coeff[entering_col];  // IsComputedFor(leaving_row)
-    const int8_t leaving_status = s.lb[lcol] == s.ub[lcol] ? kFixedValue
-                                  : target_bound == s.lb[lcol] ? kAtLower
-                                                               : kAtUpper;
-    vi_to_nonbasic(s, lcol, leaving_status);  // UpdateBasis
-    s.basis[leaving_row] = entering_col;
-    vi_to_basic(s, entering_col);
-    ur_invalidate(s);
-    const f64 pivot_from_direction = s.dir.values[leaving_row];
-    const f64 diff = sd_fabs(pivot_from_update_row - pivot_from_direction);
-    s.exit_col = lcol;
     int refactor = 0;  // 1: ForceRefactorization, 2: the same after the LU threshold bump
-    if (diff > s.refactorization_threshold *
-                   (1.0 + sd_min(sd_fabs(pivot_from_update_row), sd_fabs(pivot_from_direction)))) {
-      refactor = s.num_updates < 10 ? 2 : 1;
-    } else if (s.num_updates >= s.max_updates &&
-               (!s.dynamic_period || s.last_fact_dtime < s.r1_dtime)) {
-      refactor = 1;  // BasisFactorization::Update (:304-340)
-    } else {
-      const int right_index = s.right_pool[entering_col];
-      const int left_index = s.left_pool[leaving_row];
-      ++s.num_updates;
-      if (right_index == kInvalid || left_index == kInvalid) {
-        refactor = 1;
-      } else {
-        // MiddleProductFormUpdate (:258-302)
-        SdSubTimer t_x_(&s.phase_ticks[26]);
-        // Each column's rows are distinct: the lanes split them; the list
-        // entries keep their positions (right column, then U's column).
-        {
-          const int64_t rb = s.right_storage.starts[right_index];
-          const int rn = static_cast<int>(s.right_storage.starts[right_index + 1] - rb);
-          const int base = s.n_mpf_scratch_nz;
-          for (int k = sd_lane(); k < rn; k += sd_lanes()) {
-            const int r = s.right_storage.rows[rb + k];
-            s.mpf_scratch[r] = s.right_storage.coefs[rb + k];
-            s.mpf_scratch_nz[base + k] = r;
-          }
-          sd_sync();
-          s.n_mpf_scratch_nz = base + rn;
-        }
-        lu_column_of_u(s, leaving_row);
-        {
-          const int base = s.n_mpf_scratch_nz;
-          for (int k = sd_lane(); k < s.n_col_u; k += sd_lanes()) {
-            s.mpf_scratch[s.col_u_rows[k]] -= s.col_u_coefs[k];
-            s.mpf_scratch_nz[base + k] = s.col_u_rows[k];
-          }
-          sd_sync();
-          s.n_mpf_scratch_nz = base + s.n_col_u;
-        }
-        const f64 scalar_product = col_dot_par(s.storage, left_index, s.mpf_scratch, s.lds_scratch);
-        const int u_index =
-            store_add_and_clear(s.storage, s.mpf_scratch, s.mpf_scratch_nz, &s.n_mpf_scratch_nz);
-        const f64 mu = 1.0 + scalar_product;
-        if (mu == 0.0) return s.exit_code = kExitLuError;
-        s.r1_u[s.r1_count] = u_index;
-        s.r1_v[s.r1_count] = left_index;
-        s.r1_mu[s.r1_count] = mu;
-        ++s.r1_count;
-        s.r1_num_entries += col_entries(s.storage, u_index) + col_entries(s.storage, left_index);
-        s.tau_can_opt = 0;
-      }
+    if (sd_pivot(s, entering_col, leaving_row, target_bound, &refactor) != kExitNone) {
+      return s.exit_code = kExitLuError;
     }
     if (refactor != 0) {
       SD_PHASE(8);
@@ -3722,5 +3745,7 @@ SD_INLINE int32_t sd_run(Lp& s) {
 }
 
 }  // namespace sdual
+
+#include "sprimal_core.h"
 
 #endif  // MILP_SDUAL_CORE_H_

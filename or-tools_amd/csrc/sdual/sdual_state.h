@@ -42,6 +42,20 @@ struct Vec {
   char* mask;
 };
 
+// DynamicMaximum<Index> (glop/pricing.h:58-345): values, the candidate
+// bitset, the top-k cache with its threshold, and the equivalent-choices
+// scratch (size + 1 entries).
+struct DynMax {
+  f64* values;
+  uint64_t* cand;
+  int size;  // values_.size()
+  int ntops;
+  f64 threshold;
+  int32_t tops_idx[32];
+  f64 tops_val[32];
+  int32_t* equiv;
+};
+
 // CompactSparseMatrix read-only view (sparse.h:291-512).
 struct Csc {
   const int64_t* starts;
@@ -101,6 +115,10 @@ enum SdExit : int32_t {
   // exit_refactorize, or after UpdateAndPivot's.
   kExitResumeTop = 11,
   kExitResumePivot = 12,
+  // Primal segment: a final status (exit_status: ProblemStatus), and an
+  // unbounded ray (the host builds it from the direction).
+  kExitStatus = 13,
+  kExitUnbounded = 14,
 };
 
 // The factorization as the device stores it: a header followed by its arrays;
@@ -130,7 +148,7 @@ struct Lp {
   int N;  // columns of [A | I]
   Csc A;  // compact_matrix_
   Csc At; // transposed_matrix_ (num_cols = m)
-  const f64* objective;
+  f64* objective;  // objective_ (rewritten by the primal phase-I costs)
 
   // ---- parameters (GlopParameters subset) ----
   f64 drop_tolerance;
@@ -185,15 +203,8 @@ struct Lp {
   f64* norms;
   int norms_recompute;
 
-  // ---- DynamicMaximum dual_prices_ (pricing.h:58-345) ----
-  f64* dp_values;
-  uint64_t* dp_cand;
-  int dp_size;  // values_.size()
-  f64 dp_threshold;
-  int dp_ntops;
-  int32_t dp_tops_idx[32];
-  f64 dp_tops_val[32];
-  int32_t* dp_equiv;  // equivalent_choices_ scratch (m + 1)
+  // ---- DynamicMaximum dual_prices_ (pricing.h:58-345) over the rows ----
+  DynMax dp;
 
   // ---- UpdateRow ----
   Vec rho;
@@ -325,6 +336,32 @@ struct Lp {
   f64* lds_scratch;  // SdScratch after the staging area (device only)
   int32_t lds_busy;  // a solve's working vector occupies the staging area
   int32_t lds_pad2;
+
+  // ---- primal segment (PrimalMinimize, revised_simplex.cc:2751-3045) ----
+  int primal;             // the segment runs the primal loop (sp_run)
+  int phase_feasibility;  // phase_ == FEASIBILITY: phase-I costs
+  f64 primal_objective_limit;
+  f64 recompute_reduced_costs_threshold;
+  // PrimalPrices (reduced_costs.cc:512-600): a DynamicMaximum over columns.
+  DynMax pp;
+  int pp_recompute;
+  // PrimalEdgeNorms (primal_edge_norms.cc), steepest edge.
+  int pen_recompute;  // recompute_edge_squared_norms_
+  int pen_pad;
+  f64* pen_norms;     // edge_squared_norms_ (N)
+  int64_t pen_ops;    // num_operations_
+  Vec dli;            // direction_left_inverse_
+  // Ratio-test scratch: Harris leaving candidates (m), phase-I breakpoints
+  // (2m + 2: row, ratio, magnitude, target bound).
+  int32_t* lc_row;
+  f64* lc_ratio;
+  int32_t* bp1_row;
+  f64* bp1_ratio;
+  f64* bp1_mag;
+  f64* bp1_target;
+  int32_t exit_status;  // kExitStatus: the ProblemStatus
+  int32_t exit_entering;
+  f64 exit_reduced_cost;
 
   // ---- loop carry and exit ----
   int refactorize;  // the host loop's `refactorize` flag

@@ -693,6 +693,8 @@ void UpdateRow::ComputeFullUpdateRow(int leaving_row,
 // ---------------------------------------------------------------------------
 // PrimalEdgeNorms (primal_edge_norms.cc)
 class PrimalEdgeNorms {
+  friend struct SdualBridge;
+
  public:
   PrimalEdgeNorms(const CompactSparseMatrix& m, const VariablesInfo& vi,
                   const BasisFactorization& bf)
@@ -1190,6 +1192,8 @@ void ReducedCosts::UpdateReducedCosts(int entering_col, int leaving_col, int lea
 // ---------------------------------------------------------------------------
 // PrimalPrices (reduced_costs.cc:512-600)
 class PrimalPrices {
+  friend struct SdualBridge;
+
  public:
   PrimalPrices(Rng* random, const VariablesInfo& vi, PrimalEdgeNorms* pen,
                ReducedCosts* rc)
@@ -2312,10 +2316,16 @@ class RevisedSimplex {
 #include "sdual_core.h"
 namespace oracle {
 std::atomic<int64_t> g_sdual_segments{0}, g_sdual_iterations{0};
+std::atomic<int64_t> g_sprimal_segments{0}, g_sprimal_iterations{0};
 struct SdualHooks {
   static bool Supported(const RevisedSimplex&) { return true; }
   static void PrepareForPack(RevisedSimplex&) {}
   static void AfterUnpack(RevisedSimplex&, const sdual::Lp& s) {
+    if (s.primal) {
+      ++g_sprimal_segments;
+      g_sprimal_iterations += s.iterations_done;
+      return;
+    }
     ++g_sdual_segments;
     g_sdual_iterations += s.iterations_done;
   }
@@ -3488,6 +3498,17 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
       }
     }
 
+#ifdef ORACLE_SDUAL
+    if (SdualBridge::SupportedPrimal(*this, time_limit)) {
+      Status st;
+      int next;
+      do {
+        next = SdualBridge::RunOnHostPrimal(*this, time_limit, &refactorize, &st, &sdual_buffer_);
+      } while (next == SdualBridge::kBody && SdualBridge::SupportedPrimal(*this, time_limit));
+      if (next == SdualBridge::kReturn) return st;
+      if (next == SdualBridge::kLoopTop) continue;
+    }
+#endif
     const int entering_col = primal_prices_.GetBestEnteringColumn();
     if (entering_col == kInvalidCol) {
       if (reduced_costs_.AreReducedCostsPrecise() && basis_factorization_.IsRefactorized()) {
@@ -4028,7 +4049,12 @@ void oracle_lp_destroy(void* h) { delete static_cast<OracleHandle*>(h); }
 #ifdef ORACLE_SDUAL
 // Segments / iterations the sdual restatement ran in this process.
 int64_t oracle_sdual_counter(int32_t which) {
-  return which == 0 ? oracle::g_sdual_segments.load() : oracle::g_sdual_iterations.load();
+  switch (which) {
+    case 0: return oracle::g_sdual_segments.load();
+    case 1: return oracle::g_sdual_iterations.load();
+    case 2: return oracle::g_sprimal_segments.load();
+    default: return oracle::g_sprimal_iterations.load();
+  }
 }
 #endif
 

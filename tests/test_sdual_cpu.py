@@ -1,9 +1,10 @@
-"""CPU checks of the device dual simplex segment's restatement
-(or-tools_amd/csrc/sdual/sdual_core.h). The oracle's test build
-liboracle_sdual.so runs the same restatement, compiled for the host, inside
-the oracle's own dual loop (revised_simplex.cc:3058-3367 from the leaving-row
-choice on); every result must equal the plain oracle's bit for bit, and the
-segments must actually have run."""
+"""CPU checks of the device simplex segments' restatement
+(or-tools_amd/csrc/sdual/sdual_core.h, sprimal_core.h). The oracle's test
+build liboracle_sdual.so runs the same restatement, compiled for the host,
+inside the oracle's own loops -- the dual loop (revised_simplex.cc:3058-3367
+from the leaving-row choice on) and the primal loop (:2751-3045 from the
+entering-column choice on, phases I and II); every result must equal the
+plain oracle's bit for bit, and the segments must actually have run."""
 import ctypes
 import math
 
@@ -17,10 +18,11 @@ import lp_gen
 import oracle_lib
 
 
-def _counters():
+def _counters(primal=False):
     L = oracle_lib.lib("sdual")
     L.oracle_sdual_counter.restype = ctypes.c_int64
-    return L.oracle_sdual_counter(0), L.oracle_sdual_counter(1)
+    k = 2 if primal else 0
+    return L.oracle_sdual_counter(k), L.oracle_sdual_counter(k + 1)
 
 
 def _full(o, r):
@@ -130,6 +132,72 @@ def test_sdual_restatement_resume_paths():
         "lp = lp_gen.sparse_c5_lp(300, 3000, 6, 41)\n"
         "a, b = t._both(lp, abi.default_params(use_dual_simplex=1))\n"
         "t._assert_same(a, b, 'c5')\n"
+        "print('ok')\n") % (sys.path[:6],)
+    env = dict(os.environ, MILP_SDUAL_LU_SLACK="64")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_sprimal_restatement_sparse(seed):
+    """Primal simplex (Glop's default), phase I and II in segments."""
+    seg0, it0 = _counters(primal=True)
+    m, n = 30 + 20 * seed, 90 + 50 * seed
+    lp = lp_gen.random_sparse_lp(m, n, 0.06 if seed % 2 else 0.03, 900 + seed,
+                                 maximize=bool(seed % 3 == 0))
+    a, b = _both(lp, abi.default_params())
+    _assert_same(a, b, seed)
+    seg1, it1 = _counters(primal=True)
+    assert seg1 > seg0 and it1 > it0
+
+
+def test_sprimal_restatement_netlib_shaped():
+    """The config-3 stand-in suite up to 300 rows, every LP bit-identical."""
+    import netlib_suite
+    seg0, it0 = _counters(primal=True)
+    for i, lp in enumerate(netlib_suite.suite(max_rows=300)):
+        a, b = _both(lp, abi.default_params())
+        _assert_same(a, b, i)
+    seg1, it1 = _counters(primal=True)
+    assert it1 - it0 > 10000
+
+
+def test_sprimal_restatement_kats():
+    """Known-answer LPs (optimal, infeasible, unbounded) on both loops."""
+    for builder in kat_lps.ALL:
+        lp, _ = builder()
+        for dual in (0, 1):
+            a, b = _both(lp, abi.default_params(use_dual_simplex=dual))
+            _assert_same(a, b, (builder.__name__, dual))
+
+
+@pytest.mark.parametrize("cap", [1, 5, 40])
+def test_sprimal_restatement_iteration_cap(cap):
+    """An iteration cap ends a segment (kExitReturnOk) at the same point."""
+    lp = lp_gen.random_sparse_lp(120, 300, 0.04, 77)
+    a, b = _both(lp, abi.default_params(max_number_of_iterations=cap))
+    _assert_same(a, b, cap)
+
+
+def test_sprimal_restatement_resume_paths():
+    """Primal segments with almost no room for later factorizations
+    (MILP_SDUAL_LU_SLACK): every refactorization hands the LP back through the
+    resume exits; results must not change. Runs in a child process (the cap
+    is read once)."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path[:0] = %r\n"
+        "import test_sdual_cpu as t, lp_gen\n"
+        "from mi_glop import abi\n"
+        "s0 = t._counters(primal=True)\n"
+        "for seed in range(3):\n"
+        "    lp = lp_gen.random_sparse_lp(80 + 30 * seed, 300, 0.05, 60 + seed)\n"
+        "    a, b = t._both(lp, abi.default_params())\n"
+        "    t._assert_same(a, b, seed)\n"
+        "assert t._counters(primal=True)[1] > s0[1]\n"
         "print('ok')\n") % (sys.path[:6],)
     env = dict(os.environ, MILP_SDUAL_LU_SLACK="64")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
