@@ -3336,6 +3336,10 @@ class RevisedSimplex {
   // -1: no segment (the host runs the iteration), else SdualBridge::Continue's
   // answer: kReturn (DualMinimize returns *status), kLoopTop, kBody.
   int RunSdualSegment(TimeLimit* tl, bool* refactorize, Status* status);
+  // The same for the primal loop (csrc/sdual/sprimal_core.h): batch solves
+  // with MILP_SPRIMAL=on (device) or host; MILP_SDUAL=host runs it on the host.
+  int sprimal_mode_ = 0;
+  int RunSprimalSegment(TimeLimit* tl, bool* refactorize, Status* status);
 
  public:
   // The batch APIs run the phase-II dual loop of their LPs as device
@@ -3359,11 +3363,20 @@ class RevisedSimplex {
       if (batch_depth_++ == 0) {
         saved_sdual_mode_ = sdual_mode_;
         sdual_mode_ = batch_mode;
+        sprimal_mode_ = SprimalMode();
       }
     } else if (batch_depth_ > 0 && --batch_depth_ == 0) {
       sdual_mode_ = saved_sdual_mode_;
+      sprimal_mode_ = SprimalMode();
     }
     device_.SetHostSmallOps(batch_depth_ > 0 && sdual_mode_ == 2 && host_ops);
+  }
+  // Primal segments run where the dual ones do, when MILP_SPRIMAL is "on"
+  // (read per call; tests switch it).
+  int SprimalMode() const {
+    const char* e = std::getenv("MILP_SPRIMAL");
+    if (e == nullptr || std::strcmp(e, "on") != 0) return 0;
+    return sdual_mode_;
   }
   // Whether this handle's batch solves use the device's segment pool.
   bool UsesSdualPool() const { return batch_depth_ > 0 && sdual_mode_ == 2; }
@@ -3387,6 +3400,10 @@ struct SdualHooks {
   // pending tau on the worker (dropped, as any other use of the factorization
   // would), a deferred column-wise update row, the host mirror of the row.
   static void PrepareForPack(RevisedSimplex& rs) {
+    // A parked edge-norm update completes first (it reads the update row the
+    // next lines may rebuild); its queued price updates replay with it.
+    rs.primal_edge_norms_.FlushPendingUpdate();
+    rs.primal_edge_norms_.DropDirectionLeftInverse();
     rs.basis_factorization_.DropAsync();
     rs.update_row_.Materialize();
     rs.update_row_.EnsureHost();
@@ -3415,6 +3432,14 @@ int RevisedSimplex::RunSdualSegment(TimeLimit* tl, bool* refactorize, Status* st
   return SdualBridge::RunOnDevice(*this, tl, refactorize, status);
 }
 
+int RevisedSimplex::RunSprimalSegment(TimeLimit* tl, bool* refactorize, Status* status) {
+  if (sprimal_mode_ == 0 || !SdualBridge::SupportedPrimal(*this, tl)) return -1;
+  if (sprimal_mode_ == 1) {
+    return SdualBridge::RunOnHostPrimal(*this, tl, refactorize, status, &sdual_buffer_);
+  }
+  return SdualBridge::RunOnDevice(*this, tl, refactorize, status, /*primal=*/true);
+}
+
 RevisedSimplex::RevisedSimplex()
     : random_(42),
       basis_factorization_(&compact_matrix_, &basis_),
@@ -3437,6 +3462,7 @@ RevisedSimplex::RevisedSimplex()
     if (std::strcmp(e, "host") == 0) sdual_mode_ = 1;
     if (std::strcmp(e, "device") == 0 || std::strcmp(e, "on") == 0) sdual_mode_ = 2;
   }
+  sprimal_mode_ = SprimalMode();
 }
 
 // revised_simplex.cc:139-635
@@ -4609,6 +4635,15 @@ Status RevisedSimplex::PrimalMinimize(TimeLimit* time_limit) {
       }
     }
 
+    if (sprimal_mode_ != 0) {
+      Status sp_status;
+      int sp;
+      do {
+        sp = RunSprimalSegment(time_limit, &refactorize, &sp_status);
+      } while (sp == SdualBridge::kBody);
+      if (sp == SdualBridge::kLoopTop) continue;
+      if (sp == SdualBridge::kReturn) return sp_status;
+    }
     clock.Mark(0);
     const int entering_col = primal_prices_.GetBestEnteringColumn();
     clock.Mark(1);

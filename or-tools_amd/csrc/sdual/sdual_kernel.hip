@@ -1,6 +1,6 @@
-// Device dual simplex segment on gfx950: one workgroup runs the phase-II dual
-// loop of one LP (sdual_core.h) over its arena in HBM until the loop needs the
-// host (SdExit). DeviceLp owns the arena, a pinned staging image and the
+// Device simplex segment on gfx950: one workgroup runs the phase-II dual loop
+// (sdual_core.h) or the primal loop (sprimal_core.h) of one LP over its arena
+// in HBM until the loop needs the host (SdExit). DeviceLp owns the arena, a pinned staging image and the
 // transfers; RevisedSimplex (engine/simplex.cc) packs and unpacks.
 #include <hip/hip_runtime.h>
 
@@ -56,7 +56,12 @@ __device__ inline char* sd_lds_enter(sdual::Lp* lp) {
 // One thread walks Glop's loop; the header lives in the arena.
 __global__ __launch_bounds__(64) void sdual_segment_kernel(sdual::Lp* lp) {
   char* stored = sd_lds_enter(lp);
-  sdual::sd_run(*lp);  // every lane (sdual_core.h: the wave)
+  // every lane (sdual_core.h: the wave); primal segments: sprimal_core.h
+  if (lp->primal) {
+    sdual::sp_run(*lp);
+  } else {
+    sdual::sd_run(*lp);
+  }
   __syncthreads();
   lp->stored = stored;
 }
@@ -220,7 +225,11 @@ __global__ __launch_bounds__(64) void sdual_pool_kernel(SdQueue* q, SdRing* ring
     sdual::Lp* lp = reinterpret_cast<sdual::Lp*>(arena);
     lp->phase_ticks[13] += wall_clock64() - t_claim;  // staging image in
     char* stored = sd_lds_enter(lp);
-    sdual::sd_run(*lp);
+    if (lp->primal) {
+      sdual::sp_run(*lp);
+    } else {
+      sdual::sd_run(*lp);
+    }
     __syncthreads();
     lp->stored = stored;  // every lane (sdual_core.h: the wave)
     const uint64_t t_out = wall_clock64();
