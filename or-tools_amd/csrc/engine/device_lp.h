@@ -29,7 +29,7 @@ namespace milp {
 void SdualProfileReset();
 // A batch call on `device` starts (begin) or ends using the device's segment
 // pool; when the last one ends, the resident pool grid is told to stop.
-void SdualPoolScope(int device, bool begin);
+void SdualPoolScope(int device, bool begin, int lps);
 
 class CompactSparseMatrix;
 

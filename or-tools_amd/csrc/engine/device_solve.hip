@@ -159,7 +159,7 @@ void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, cons
         seg_level.insert(seg_level.end(), {l, e, 1});
         wide_from = e;
       }
-      l = e;
+      l = std::max(e, l + 1);  // a level alone larger than the LDS stays wide
     }
     if (wide_from <= depth) seg_level.insert(seg_level.end(), {wide_from, depth + 1, 0});
   } else {

@@ -5984,23 +5984,34 @@ void SetSmallBatchSafe(mi_lp* h, bool on) {
 // call on a device ends, its resident pool grid is told to stop.
 struct PoolScope {
   std::vector<int> devices;
+  std::vector<int> lps;  // handles of this call on devices[i]
   PoolScope(mi_lp* const* hs, int count) {
+    std::vector<int> all, n;
     for (int i = 0; i < count; ++i) {
       if (!hs[i]->simplex.UsesSdualPool()) continue;
       const int d = hs[i]->device;
-      if (std::find(devices.begin(), devices.end(), d) != devices.end()) continue;
-      devices.push_back(d);
+      const auto it = std::find(all.begin(), all.end(), d);
+      if (it != all.end()) {
+        ++n[it - all.begin()];
+        continue;
+      }
+      all.push_back(d);
+      n.push_back(1);
+    }
+    for (size_t k = 0; k < all.size(); ++k) {
       try {
-        milp::SdualPoolScope(d, true);
+        milp::SdualPoolScope(all[k], true, n[k]);
+        devices.push_back(all[k]);
+        lps.push_back(n[k]);
       } catch (const std::exception&) {
-        devices.pop_back();  // the segment itself reports the device error
+        // the segment itself reports the device error
       }
     }
   }
   ~PoolScope() {
-    for (const int d : devices) {
+    for (size_t k = 0; k < devices.size(); ++k) {
       try {
-        milp::SdualPoolScope(d, false);
+        milp::SdualPoolScope(devices[k], false, lps[k]);
       } catch (const std::exception&) {
       }
     }

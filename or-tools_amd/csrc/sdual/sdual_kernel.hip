@@ -1,7 +1,8 @@
 // Device simplex segment on gfx950: one workgroup runs the phase-II dual loop
 // (sdual_core.h) or the primal loop (sprimal_core.h) of one LP over its arena
-// in HBM until the loop needs the host (SdExit). DeviceLp owns the arena, a pinned staging image and the
-// transfers; RevisedSimplex (engine/simplex.cc) packs and unpacks.
+// in HBM until the loop needs the host (SdExit). DeviceLp owns the arena, a
+// pinned staging image and the transfers; RevisedSimplex (engine/simplex.cc)
+// packs and unpacks.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -109,6 +110,7 @@ struct SdRing {
   long long ack[SdQueue::kCap];  // per slot: last index read from it + 1
 };
 constexpr int kPoolGroups = 1024;
+constexpr int kMinPoolGroups = 33;
 constexpr int64_t kIdleSpins = 1 << 20;  // ~4 s of dispatcher polls
 
 // Cooperative copy by the workgroup (16-byte words; regions are 256-byte
@@ -340,12 +342,18 @@ class SdualPool {
   // The batch calls in progress on this device (BatchScope): the last one to
   // end raises the stop word, so the resident grid leaves the CUs to single
   // solves instead of spinning out its idle limit.
-  void Acquire() {
+  // `lps`: the LPs the batch call may have in flight on this device; a grid
+  // launched meanwhile has one workgroup per LP (plus the dispatcher), up to
+  // kPoolGroups. A pool wave holds a whole SIMD's registers, so a grid larger
+  // than the work would lock the engine's other kernels out of the CUs.
+  void Acquire(int lps) {
     std::lock_guard<std::mutex> lock(mu_);
+    lps_ += lps;
     if (users_++ == 0) __atomic_store_n(&q_->stop, 0, __ATOMIC_RELEASE);
   }
-  void Release() {
+  void Release(int lps) {
     std::lock_guard<std::mutex> lock(mu_);
+    lps_ -= lps;
     if (--users_ == 0 && running_) __atomic_store_n(&q_->stop, 1, __ATOMIC_RELEASE);
   }
 
@@ -393,7 +401,9 @@ class SdualPool {
       throw DeviceError("sdual pool: ring reset failed");
     }
     __atomic_store_n(&q_->stop, 0, __ATOMIC_RELEASE);
-    hipLaunchKernelGGL(sdual_pool_kernel, dim3(kPoolGroups), dim3(64), kLdsTotalDoubles * sizeof(double), stream_, d_q_, d_ring_,
+    // Outside batch calls (single solves): a few dozen workers.
+    const int groups = std::max(kMinPoolGroups, std::min(kPoolGroups, lps_ + 1));
+    hipLaunchKernelGGL(sdual_pool_kernel, dim3(groups), dim3(64), kLdsTotalDoubles * sizeof(double), stream_, d_q_, d_ring_,
                        static_cast<long long>(head_base_), static_cast<long long>(cap_));
     const hipError_t e = hipGetLastError();
     (void)hipSetDevice(prev);
@@ -412,15 +422,16 @@ class SdualPool {
   int64_t head_base_ = 0;
   int64_t cap_ = SdQueue::kCap;
   int users_ = 0;
+  int lps_ = 0;
 };
 }  // namespace
 
-void SdualPoolScope(int device, bool begin) {
+void SdualPoolScope(int device, bool begin, int lps) {
   SdualPool& pool = SdualPool::Get(device);
   if (begin) {
-    pool.Acquire();
+    pool.Acquire(lps);
   } else {
-    pool.Release();
+    pool.Release(lps);
   }
 }
 
