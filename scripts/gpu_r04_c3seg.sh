@@ -14,4 +14,7 @@ MILP_SPRIMAL=on MILP_SDUAL=device MILP_SDUAL_PROFILE=1 timeout -k 10 300 python3
   --single 89 93 86 --workers > $OUT/c3_single_on.json 2> $OUT/c3_single_on.err || exit 1
 timeout -k 10 200 python3 -u scripts/probe_batch.py --node --lps 1024 --workers 1024 \
   > $OUT/c4.json 2> $OUT/c4.err || exit 1
+# Config 2's late window (iterations 1500..1564): primal loop phase split.
+MILP_PHASE_TIMING=1 MILP_PHASE_TIMING_EVERY=64 timeout -k 10 300 python3 -u scripts/probe.py \
+  --config c2 --warmup 1500 --steps 64 > $OUT/c2_late.json 2> $OUT/c2_late.err || exit 1
 grep -h "LPs/s\|us/it\|gpu_us" $OUT/*.err | head -20
