@@ -778,6 +778,7 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
       Check(hipEventRecord(reinterpret_cast<hipEvent_t>(c.ev[1]), Stream(c.stream)), "ev");
     }
     TriCopyOut(s, c);
+    if (slot == 0) g_overlap.Run();  // host work behind the device's
     DeviceOp("tri sync");
     Check(hipStreamSynchronize(Stream(c.stream)), "sync");
     DeviceOp("tri sync done");
@@ -867,6 +868,7 @@ bool DeviceLp::SolvePair(TriKind kind, const TriangularMatrix& t, uint64_t key,
                                                   Stream(c0.stream), 2),
         "tri pair");
   EndKernel(MI_K_TRI_SOLVE, bytes);
+  g_overlap.Run();  // host work behind the device's
   DeviceOp("tri pair sync");
   Check(hipStreamSynchronize(Stream(c0.stream)), "sync");
   for (int v = 0; v < 2; ++v) {

@@ -8,6 +8,7 @@
 #define MILP_DEVICE_SOLVER_H_
 
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 namespace milp {
@@ -25,6 +26,23 @@ enum class TriKind {
   kUpper = 5,      // upper_.UpperSolve: the product-form FTRAN's U (backward scatter)
 };
 constexpr int kNumTriKinds = 6;
+
+// Host work the solving thread may do while a device triangular solve is in
+// flight: set by the caller, run once -- by the device solve between its
+// launch and its wait, or else by the caller before any host loop touches
+// the vector the work reads. (The MPF right-pool append of a dense FTRAN
+// column, basis_representation.cc:468-501, reads the vector the U solve then
+// overwrites; the device solve has copied it by then.)
+struct OverlapWork {
+  std::function<void()> f;
+  void Run() {
+    if (!f) return;
+    std::function<void()> g = std::move(f);
+    f = nullptr;
+    g();
+  }
+};
+extern thread_local OverlapWork g_overlap;
 
 class DeviceSolver {
  public:

@@ -222,6 +222,12 @@ inline void ClearAndResizeVectorWithNonZeros(int size, ScatteredVector* v) {
       v->non_zeros.size() < kSparseThreshold * size) {
     for (const int index : v->non_zeros) v->values[index] = 0.0;
     v->values.resize(size, 0.0);
+  } else if (size >= (1 << 16) && static_cast<int>(v->values.size()) == size) {
+    // A long dense vector: zeroed by the host pool (the same bits).
+    double* p = v->values.data();
+    ParallelRanges(size, 1 << 16, 4096, [p](int, int64_t b, int64_t e) {
+      std::fill(p + b, p + e, 0.0);
+    });
   } else {
     v->values.assign(size, 0.0);
   }

@@ -717,9 +717,11 @@ void LuFactorization::RightSolveUAfterRows(ScatteredVector* x) const {
     if (device_solver_ == nullptr ||
         !device_solver_->TransposeLowerSolve(transpose_upper_, factorization_key_,
                                              &x->values)) {
+      g_overlap.Run();
       transpose_upper_.TransposeLowerSolve(&x->values);
     }
   } else {
+    g_overlap.Run();
     transpose_upper_.TransposeHyperSparseSolveWithReversedNonZeros(
         &x->values, &x->non_zeros);
   }
@@ -1236,6 +1238,8 @@ void BasisFactorization::LeftSolve(ScatteredVector* y) const {
   BumpDeterministicTimeForSolve(static_cast<int64_t>(y->NumNonZerosEstimate()));
 }
 
+thread_local OverlapWork g_overlap;
+
 // basis_representation.cc:358-372
 void BasisFactorization::RightSolve(ScatteredVector* d) const {
   if (!use_middle_product_form_update_) {
@@ -1360,8 +1364,17 @@ void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d)
   if (col >= static_cast<int>(right_pool_mapping_.size())) {
     right_pool_mapping_.resize(col + 1, kInvalidCol);
   }
+  // A thrown device error must not leave the append armed for a later solve.
+  struct Disarm {
+    ~Disarm() { g_overlap.f = nullptr; }
+  } disarm;
   if (d->non_zeros.empty()) {
-    right_pool_mapping_[col] = right_storage_.AddDenseColumn(d->values);
+    // Appended while the device solves U (the column is the vector before U;
+    // g_overlap runs before anything overwrites it).
+    const int slot_col = col;
+    g_overlap.f = [this, slot_col, d]() {
+      right_pool_mapping_[slot_col] = right_storage_.AddDenseColumn(d->values);
+    };
   } else {
     std::sort(d->non_zeros.begin(), d->non_zeros.end());
     right_pool_mapping_[col] =
@@ -1377,6 +1390,7 @@ void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d)
   } else {
     lu_factorization_.RightSolveUWithNonZeros(d);
   }
+  g_overlap.Run();  // nothing solved U (identity factorization)
   d->SortNonZerosIfNeeded();
   if (g_trace_ftran) g_ftran_hash[2] = TraceHashVector(d->values, d->non_zeros);
   BumpDeterministicTimeForSolve(static_cast<int64_t>(d->NumNonZerosEstimate()));

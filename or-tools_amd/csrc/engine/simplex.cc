@@ -3465,8 +3465,11 @@ RevisedSimplex::RevisedSimplex()
   sprimal_mode_ = SprimalMode();
 }
 
+void SamplerAttachThread();  // engine/sampler.cc (MILP_SAMPLE_WALL)
+
 // revised_simplex.cc:139-635
 Status RevisedSimplex::Solve(const LinearProgram& lp, TimeLimit* time_limit) {
+  SamplerAttachThread();
   struct Cleanup {
     std::function<void()> f;
     ~Cleanup() { f(); }

@@ -65,11 +65,16 @@ def main():
         # Timing brackets every kernel with events (one sync each); the rate
         # is measured with it off, then the kernel split with it on.
         t = time.perf_counter()
+        clk0 = {"monotonic": time.monotonic_ns(), "boottime": time.clock_gettime_ns(time.CLOCK_BOOTTIME)}
         fin, it = h.run_until(a.warmup + a.steps)
         dt = time.perf_counter() - t
+        clk1 = {"monotonic": time.monotonic_ns(), "boottime": time.clock_gettime_ns(time.CLOCK_BOOTTIME)}
+        # The engine's host sampler (MILP_SAMPLE_PROFILE) reports this window.
+        os.environ["MILP_SAMPLE_WINDOW"] = f"{clk0['monotonic']},{clk1['monotonic']}"
         done = it - a.warmup
         res.update(gpu_iterations=done, gpu_s=round(dt, 4),
-                   gpu_it_per_s=done / dt if dt > 0 else None, finished=fin)
+                   gpu_it_per_s=done / dt if dt > 0 else None, finished=fin,
+                   window_clock_ns={k: [clk0[k], clk1[k]] for k in clk0})
         h.reset_kernel_stats()
         h.set_kernel_timing(True)
         fin2, it2 = h.run_until(it + a.steps)
