@@ -222,6 +222,10 @@ class DeviceLp : public DeviceSolver {
   // host thread that owns the LP (Glop's order, the kernels' bits) instead of
   // as single launches that queue behind hundreds of other LPs' work.
   void SetHostSmallOps(bool on) { host_small_ops_ = on; }
+  // Whether a chip-wide update-row compaction also writes the list into
+  // mapped host memory (off in dual device mode: the host reads the list
+  // rarely, and then downloads it).
+  void SetListMirror(bool on) { list_mirror_ = on; }
   bool host_small_ops() const { return host_small_ops_; }
   bool small_batch() const { return small_batch_; }
   int shard_begin(int s) const { return shard_begin_[s]; }
@@ -481,6 +485,7 @@ class DeviceLp : public DeviceSolver {
   int* d_map_count_ = nullptr;
   int32_t* d_map_list_ = nullptr;
   double* d_map_vals_ = nullptr;
+  bool list_mirror_ = true;
   bool mapped_result_ = false;  // the last Compact wrote to h_map_
   // Small LPs (N <= kSmallLdsCols): the row-wise update row is one launch
   // (row_wise_small_kernel) reading its inputs, including the relevant mask,

@@ -937,10 +937,12 @@ void DeviceLp::Compact(int n) {
     // Ordered single-pass compaction over the chip, the list also into
     // mapped host memory.
     Check(milp_launch::compact_flags(d_flags_, n, d_coeff_, d_list_, d_out_list_, d_count_,
-                                     d_map_list_, d_map_vals_, d_map_count_, NextScan(),
+                                     list_mirror_ ? d_map_list_ : nullptr,
+                                     list_mirror_ ? d_map_vals_ : nullptr,
+                                     list_mirror_ ? d_map_count_ : nullptr, NextScan(),
                                      S(stream_)),
           "compact");
-    mapped_result_ = true;
+    mapped_result_ = list_mirror_;
   }
   list_count_ = -1;  // known after FetchUpdateRow
   ++list_epoch_;

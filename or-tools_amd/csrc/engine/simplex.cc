@@ -4795,6 +4795,7 @@ void RevisedSimplex::BeginDualDeviceMode() {
   device_.DualBegin(reduced_costs_.RawReducedCosts(), bits, bound_diff);
   reduced_costs_.EnterDeviceMode();
   update_row_.SetLazyFetch(true);
+  device_.SetListMirror(false);
   status_log_.clear();
   variables_info_.SetChangeLog(&status_log_);
   dual_device_mode_ = true;
@@ -4805,6 +4806,7 @@ void RevisedSimplex::EndDualDeviceMode() {
   variables_info_.SetChangeLog(nullptr);
   status_log_.clear();
   update_row_.SetLazyFetch(false);
+  device_.SetListMirror(true);
   // Bring the last update row to the host while the device list is intact
   // (later ListDots calls reuse the list-value buffer).
   update_row_.GetNonZeroPositions();
