@@ -591,7 +591,7 @@ class DeviceLp : public DeviceSolver {
   // run of at least MILP_TRI_CHAIN_MIN_LEVELS levels of at most
   // MILP_TRI_CHAIN_WIDTH outputs each (tri_chain_kernel).
   bool tri_chain_ = true;
-  int tri_chain_width_ = 1024;
+  int tri_chain_width_ = 512;
   int tri_chain_min_levels_ = 4;
   uint64_t* d_tri_clock_ = nullptr;
   TriSchedule tri_sched_[kTriNumMatrices];
