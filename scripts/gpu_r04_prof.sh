@@ -5,8 +5,8 @@
 # the config-4 pool batch (the persistent sdual kernel), last.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-WORKLOADS="c5 c2" TAG=r04 bash $R/scripts/gpu_profile.sh || exit 1
-OUT=$R/gpurun_out/profiles/r04_c4
+WORKLOADS="c5 c2" TAG=${TAG:-r04} bash $R/scripts/gpu_profile.sh || exit 1
+OUT=$R/gpurun_out/profiles/${TAG:-r04}_c4
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- \
