@@ -193,32 +193,46 @@ template <typename Real>
 void ParallelAppendNonZeros(const Real* v, int64_t begin, int64_t n, std::vector<int>* rows,
                             std::vector<Real>* vals, Real* max_abs = nullptr) {
   constexpr int kMaxParts = 16;
-  std::vector<int> part_rows[kMaxParts];
+  int64_t part_count[kMaxParts] = {};
   Real part_max[kMaxParts] = {};
   const int64_t len = n > begin ? n - begin : 0;
+  // Pass 1: count (and the largest magnitude) per part; pass 2: each part
+  // writes its entries at its offset. Both passes split [begin, n) the same
+  // way (same length, threshold and alignment).
   const int parts = ParallelRanges(len, 65536, 64, [&](int p, int64_t b, int64_t e) {
-    std::vector<int>& out = part_rows[p];
+    int64_t c = 0;
     Real m = 0;
     for (int64_t i = begin + b; i < begin + e; ++i) {
       if (v[i] != 0.0) {
-        out.push_back(static_cast<int>(i));
+        ++c;
         m = std::max(m, std::fabs(v[i]));
       }
     }
+    part_count[p] = c;
     part_max[p] = m;
   });
-  size_t total = rows->size();
-  for (int p = 0; p < parts; ++p) total += part_rows[p].size();
-  rows->reserve(total);
-  if (vals != nullptr) vals->reserve(vals->size() + (total - rows->size()));
-  Real m = max_abs != nullptr ? *max_abs : Real(0);
-  for (int p = 0; p < parts; ++p) {
-    for (const int r : part_rows[p]) {
-      rows->push_back(r);
-      if (vals != nullptr) vals->push_back(v[r]);
+  const size_t base = rows->size();
+  const size_t vbase = vals != nullptr ? vals->size() : 0;
+  int64_t offset[kMaxParts + 1];
+  offset[0] = 0;
+  for (int p = 0; p < parts; ++p) offset[p + 1] = offset[p] + part_count[p];
+  rows->resize(base + static_cast<size_t>(offset[parts]));
+  if (vals != nullptr) vals->resize(vbase + static_cast<size_t>(offset[parts]));
+  int* out_rows = rows->data() + base;
+  Real* out_vals = vals != nullptr ? vals->data() + vbase : nullptr;
+  const int parts2 = ParallelRanges(len, 65536, 64, [&](int p, int64_t b, int64_t e) {
+    int64_t at = offset[p];
+    for (int64_t i = begin + b; i < begin + e; ++i) {
+      if (v[i] != 0.0) {
+        out_rows[at] = static_cast<int>(i);
+        if (out_vals != nullptr) out_vals[at] = v[i];
+        ++at;
+      }
     }
-    m = std::max(m, part_max[p]);
-  }
+  });
+  (void)parts2;
+  Real m = max_abs != nullptr ? *max_abs : Real(0);
+  for (int p = 0; p < parts; ++p) m = std::max(m, part_max[p]);
   if (max_abs != nullptr) *max_abs = m;
 }
 
