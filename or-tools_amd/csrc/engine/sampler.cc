@@ -87,6 +87,8 @@ std::string Name(void* pc) {
 
 int g_interval_us = 0;
 std::atomic<bool> g_attached{false};
+timer_t g_timer;
+bool g_timer_set = false;
 
 struct Sampler {
   Sampler() {
@@ -162,20 +164,50 @@ Sampler g_sampler;
 
 }  // namespace
 
+namespace {
+bool WallMode(bool batch) {
+  const char* w = std::getenv("MILP_SAMPLE_WALL");
+  if (g_samples == nullptr || w == nullptr) return false;
+  return (std::strcmp(w, "batch") == 0) == batch;
+}
+void AttachCaller();
+}  // namespace
+
+// MILP_SAMPLE_WALL=1: the first thread entering RevisedSimplex::Solve;
+// MILP_SAMPLE_WALL=batch: the first batch worker thread (its fibers).
 void SamplerAttachThread() {
-  if (g_samples == nullptr || std::getenv("MILP_SAMPLE_WALL") == nullptr) return;
+  if (WallMode(false)) AttachCaller();
+}
+void SamplerAttachBatchThread() {
+  if (WallMode(true)) AttachCaller();
+}
+// A batch call starts: its first worker thread is the one sampled (the
+// previous call's workers have exited).
+void SamplerBatchCallBegin() {
+  if (!WallMode(true)) return;
+  if (g_timer_set) {
+    timer_delete(g_timer);
+    g_timer_set = false;
+  }
+  g_attached.store(false);
+}
+
+namespace {
+void AttachCaller() {
   if (g_attached.exchange(true)) return;
   sigevent ev;
   std::memset(&ev, 0, sizeof(ev));
   ev.sigev_notify = SIGEV_THREAD_ID;
   ev.sigev_signo = SIGPROF;
   ev._sigev_un._tid = static_cast<pid_t>(syscall(SYS_gettid));
-  timer_t timer;
+  timer_t& timer = g_timer;
   if (timer_create(CLOCK_MONOTONIC, &ev, &timer) != 0) return;
+  g_timer_set = true;
   itimerspec its;
   its.it_interval.tv_sec = 0;
   its.it_interval.tv_nsec = static_cast<long>(g_interval_us) * 1000;
   its.it_value = its.it_interval;
   timer_settime(timer, 0, &its, nullptr);
 }
+}  // namespace
 }  // namespace milp

@@ -3465,7 +3465,9 @@ RevisedSimplex::RevisedSimplex()
   sprimal_mode_ = SprimalMode();
 }
 
-void SamplerAttachThread();  // engine/sampler.cc (MILP_SAMPLE_WALL)
+void SamplerAttachThread();       // engine/sampler.cc (MILP_SAMPLE_WALL)
+void SamplerAttachBatchThread();  // (MILP_SAMPLE_WALL=batch)
+void SamplerBatchCallBegin();
 
 // revised_simplex.cc:139-635
 Status RevisedSimplex::Solve(const LinearProgram& lp, TimeLimit* time_limit) {
@@ -6028,6 +6030,7 @@ extern "C" {
 
 int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
                       mi_lp_result* results) {
+  milp::SamplerBatchCallBegin();
   if (handles == nullptr || results == nullptr) return MI_LP_ERROR_NULL;
   if (count < 0) return MI_LP_ERROR_INVALID_PROBLEM;
   for (int i = 0; i < count; ++i) {
@@ -6061,6 +6064,7 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
   std::vector<std::thread> pool;
   for (int t = 0; t < num_threads; ++t) {
     pool.emplace_back([&]() {
+      milp::SamplerAttachBatchThread();
       std::vector<std::function<void()>> tasks;
       for (int f = 0; f < fibers; ++f) {
         tasks.push_back([&]() {
@@ -6090,6 +6094,7 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
 int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t count,
                              const double* lbs, const double* ubs, const int8_t* warm_state,
                              int32_t warm_len, mi_lp_result* results) {
+  milp::SamplerBatchCallBegin();
   if (workers == nullptr || lbs == nullptr || ubs == nullptr || results == nullptr) {
     return MI_LP_ERROR_NULL;
   }
@@ -6165,6 +6170,7 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
   for (int t = 0; t < threads; ++t) {
     if (per_thread[t].empty()) continue;
     pool.emplace_back([&, t]() {
+      milp::SamplerAttachBatchThread();
       std::vector<std::function<void()>> tasks;
       for (mi_lp* h : per_thread[t]) tasks.push_back([&worker_loop, h]() { worker_loop(h); });
       milp::RunFibers(std::move(tasks));

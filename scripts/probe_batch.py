@@ -55,8 +55,11 @@ def main():
         engine.lib().milp_sdual_profile_reset()
         t = time.perf_counter()
         c0 = time.process_time()
+        m0 = time.monotonic_ns()
         res = engine.batch_solve_bounds(hs, lbs, ubs, state)
         dt = time.perf_counter() - t
+        # The engine's host sampler (MILP_SAMPLE_PROFILE) reports this call.
+        os.environ["MILP_SAMPLE_WINDOW"] = f"{m0},{time.monotonic_ns()}"
         cpu = time.process_time() - c0
         gpu_res[w] = res
         its = sum(r.iterations for r in res)
