@@ -584,8 +584,11 @@ class DeviceLp : public DeviceSolver {
   bool stream_prioritized_ = false;  // stream_ was created at the highest priority
   void SetStreamPriority(bool high);
   bool tri_lower_ = true;     // MILP_TRI_LOWER: the L solves too
-  bool tri_btran_ = true;     // MILP_TRI_BTRAN: the other dense loops (BTRAN, UpperSolve) too
-  bool tri_pair_ = true;      // MILP_TRI_PAIR: direction and tau U solves in one launch
+  // Off by default since round 4: with the host's dense loops faster (the
+  // parallel non-zero appends), config 5's window runs 3 % faster without the
+  // device BTRAN loops and 5 % faster without either (scripts/gpu_r04_ab2.sh).
+  bool tri_btran_ = false;    // MILP_TRI_BTRAN=1: the other dense loops (BTRAN, UpperSolve) too
+  bool tri_pair_ = false;     // MILP_TRI_PAIR=1: direction and tau U solves in one launch
   int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
   // MILP_TRI_CHAIN=0: no single-workgroup segments; a narrow segment is a
   // run of at least MILP_TRI_CHAIN_MIN_LEVELS levels of at most

@@ -52,6 +52,8 @@ VARIANTS = {
     # narrow segments of any width (long runs cut at the LDS capacity).
     "no_chain": {"MILP_TRI_CHAIN": "0"},
     "wide_chain": {"MILP_TRI_CHAIN_WIDTH": "100000", "MILP_TRI_CHAIN_MIN_LEVELS": "1"},
+    # The two-vector U launch and the device BTRAN loops (off by default).
+    "pair_btran": {"MILP_TRI_PAIR": "1", "MILP_TRI_BTRAN": "1"},
 }
 
 
@@ -60,7 +62,7 @@ VARIANTS = {
 _PARAMS = [(c, "syncfree") for c in _cases()] + [
     (c, v) for c in _cases() if c[0] in ("c5_71", "dense_dual")
     for v in ("levels", "levels_copies", "syncfree_copies", "persistent_xcd",
-              "persistent_chip", "no_chain", "wide_chain")]
+              "persistent_chip", "no_chain", "wide_chain", "pair_btran")]
 
 
 @pytest.mark.parametrize("case,variant", _PARAMS, ids=lambda x: x if isinstance(x, str) else x[0])
@@ -98,6 +100,7 @@ def test_device_u_solve_with_async_tau_and_device_dual(device_dual, async_solves
     monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
     monkeypatch.setenv("MILP_DEVICE_DUAL", device_dual)
     monkeypatch.setenv("MILP_ASYNC_SOLVES", async_solves)
+    monkeypatch.setenv("MILP_TRI_PAIR", "1")  # the two-vector launch where it applies
     lp = lp_gen.sparse_c5_lp(600, 6000, 6, 78)
     # Capped: forced onto the device, the deep L and U of this small LP take
     # a dependency hop per level (milliseconds per solve, where the host loop
@@ -149,6 +152,7 @@ def test_device_btran_and_upper_solve_parity(pfi, dual, monkeypatch):
     loop's zero skip and division). Forced onto the device at test size, the
     engine must equal the oracle bit for bit and the device solves must run."""
     monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
+    monkeypatch.setenv("MILP_TRI_BTRAN", "1")
     lp = lp_gen.dense_box_lp(90, 300, 81 + dual)
     p = abi.default_params(use_dual_simplex=dual, use_middle_product_form_update=1 - pfi,
                            max_number_of_iterations=600)
@@ -164,6 +168,7 @@ def test_device_btran_sparse_dual_parity(monkeypatch):
     """A sparse dual LP whose BTRANs turn dense late: forced device solves of
     every kind against the oracle."""
     monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
+    monkeypatch.setenv("MILP_TRI_BTRAN", "1")
     lp = lp_gen.sparse_c5_lp(700, 7000, 7, 83)
     p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1500)
     o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
