@@ -4,7 +4,7 @@
 # exchange; gloo for the barrier/max, every rank on GPU 0).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/r04_final
+OUT=$R/gpurun_out/${OUTDIR:-r04_final}
 mkdir -p $OUT
 cd $R
 timeout -k 10 1500 python3 -u -m pytest -x -v --timeout 600 --timeout-method thread \
