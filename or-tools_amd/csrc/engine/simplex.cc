@@ -213,7 +213,7 @@ int DynamicMaximum::GetMaximum() {
     if (new_size != 0) return RandomizeIfManyChoices(best_position);
   }
   threshold_ = -kInfinity;
-  is_candidate_.ForEach([&](int position) {
+  auto visit = [&](int position) {
     const Fractional value = values_[position];
     if (value < threshold_) return;
     UpdateTopK(position, value);
@@ -226,8 +226,96 @@ int DynamicMaximum::GetMaximum() {
       best_value = value;
       best_position = position;
     }
-  });
+  };
+  std::vector<int> processed;
+  if (ScanCandidatesInParallel(&processed)) {
+    for (const int position : processed) visit(position);
+  } else {
+    is_candidate_.ForEach(visit);
+  }
   return RandomizeIfManyChoices(best_position);
+}
+
+// The full scan above only acts on the candidates that are not below the
+// threshold when the scan reaches them, and that threshold is the 31st
+// largest value seen so far (UpdateTopK keeps the 31 largest values; an equal
+// value only swaps an index). The host pool finds those candidates: pass 1
+// gives each part its 31 largest values, pass 2 scans each part from the
+// 31 largest of the parts before it, keeping the same multiset the heap
+// would hold. The serial replay of the found candidates then makes the same
+// UpdateTopK calls, RNG draws and tie lists as the plain scan.
+bool DynamicMaximum::ScanCandidatesInParallel(std::vector<int>* processed) const {
+  constexpr int k = 31;
+  const int n = is_candidate_.size();
+  if (n < (1 << 16) || HostPool::Get().threads() <= 1) return false;
+  const uint64_t* words = is_candidate_.data();
+  const int num_words = (n + 63) / 64;
+  const Fractional* values = values_.data();
+  constexpr int kMaxParts = 16;
+  std::vector<Fractional> tops[kMaxParts];
+  bool has_nan[kMaxParts] = {};
+  auto offer = [](std::vector<Fractional>* h, Fractional v) {
+    // Min-heap of the k largest values (multiset).
+    if (static_cast<int>(h->size()) < k) {
+      h->push_back(v);
+      std::push_heap(h->begin(), h->end(), std::greater<Fractional>());
+    } else if (v > h->front()) {
+      std::pop_heap(h->begin(), h->end(), std::greater<Fractional>());
+      h->back() = v;
+      std::push_heap(h->begin(), h->end(), std::greater<Fractional>());
+    }
+  };
+  const int parts = ParallelRanges(num_words, 1024, 1, [&](int p, int64_t w0, int64_t w1) {
+    std::vector<Fractional>& h = tops[p];
+    h.clear();
+    for (int64_t w = w0; w < w1; ++w) {
+      uint64_t bits = words[w];
+      while (bits) {
+        const int i = static_cast<int>(w * 64 + __builtin_ctzll(bits));
+        bits &= bits - 1;
+        if (i >= n) break;
+        const Fractional v = values[i];
+        if (v != v) has_nan[p] = true;
+        offer(&h, v);
+      }
+    }
+  });
+  if (parts > kMaxParts) return false;
+  for (int p = 0; p < parts; ++p) {
+    if (has_nan[p]) return false;  // the plain scan's comparisons, not these
+  }
+  std::vector<Fractional> incoming[kMaxParts];
+  {
+    std::vector<Fractional> running;
+    for (int p = 0; p < parts; ++p) {
+      incoming[p] = running;
+      for (const Fractional v : tops[p]) offer(&running, v);
+    }
+  }
+  std::vector<int> found[kMaxParts];
+  const int parts2 = ParallelRanges(num_words, 1024, 1, [&](int p, int64_t w0, int64_t w1) {
+    std::vector<Fractional> h = incoming[p];
+    std::vector<int>& out = found[p];
+    out.clear();
+    Fractional threshold = static_cast<int>(h.size()) < k ? -kInfinity : h.front();
+    for (int64_t w = w0; w < w1; ++w) {
+      uint64_t bits = words[w];
+      while (bits) {
+        const int i = static_cast<int>(w * 64 + __builtin_ctzll(bits));
+        bits &= bits - 1;
+        if (i >= n) break;
+        const Fractional v = values[i];
+        if (v < threshold) continue;
+        out.push_back(i);
+        offer(&h, v);
+        threshold = static_cast<int>(h.size()) < k ? -kInfinity : h.front();
+      }
+    }
+  });
+  if (parts2 != parts) return false;
+  processed->clear();
+  for (int p = 0; p < parts; ++p) processed->insert(processed->end(), found[p].begin(), found[p].end());
+  return true;
 }
 
 void DynamicMaximum::UpdateTopK(int position, Fractional value) {

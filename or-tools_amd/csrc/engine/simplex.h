@@ -179,6 +179,9 @@ class DynamicMaximum {
   };
   void UpdateTopK(int position, Fractional value);
   int RandomizeIfManyChoices(int best);
+  // GetMaximum's full scan: the candidates it acts on, found by the host
+  // pool (false: scan serially).
+  bool ScanCandidatesInParallel(std::vector<int>* processed) const;
 
   Rng* random_;
   std::vector<int> equivalent_choices_;
