@@ -236,6 +236,95 @@ int DynamicMaximum::GetMaximum() {
   return RandomizeIfManyChoices(best_position);
 }
 
+void DynamicMaximum::BulkAddOrUpdate(const int* pos, const Fractional* value,
+                                     const uint8_t* keep, size_t n) {
+  constexpr int k = 31;
+  constexpr int kMaxParts = 16;
+  const bool parallel = n >= 8192 && HostPool::Get().threads() > 1 &&
+                        static_cast<int>(tops_.size()) == k;
+  if (!parallel) {
+    for (size_t i = 0; i < n; ++i) {
+      if (keep[i]) {
+        AddOrUpdate(pos[i], value[i]);
+      } else {
+        Remove(pos[i]);
+      }
+    }
+    return;
+  }
+  // The heap is full, so threshold_ is its minimum and an AddOrUpdate reaches
+  // UpdateTopK iff its value is not below the minimum of the 31 largest
+  // values so far (the heap's multiset). Pass 1: the writes (distinct
+  // positions, whole candidate words per part are not needed: Set/Clear of
+  // one bit is made atomic) and each part's 31 largest kept values; pass 2:
+  // each part's acting entries from the multiset of the heap and the parts
+  // before it.
+  auto offer = [](std::vector<Fractional>* h, Fractional v) {
+    if (static_cast<int>(h->size()) < k) {
+      h->push_back(v);
+      std::push_heap(h->begin(), h->end(), std::greater<Fractional>());
+    } else if (v > h->front()) {
+      std::pop_heap(h->begin(), h->end(), std::greater<Fractional>());
+      h->back() = v;
+      std::push_heap(h->begin(), h->end(), std::greater<Fractional>());
+    }
+  };
+  std::vector<Fractional> tops[kMaxParts];
+  bool has_nan[kMaxParts] = {};
+  Fractional* values = values_.data();
+  uint64_t* words = is_candidate_.mutable_data();
+  const int parts = ParallelRanges(static_cast<int64_t>(n), 8192, 1,
+                                   [&](int p, int64_t b, int64_t e) {
+    std::vector<Fractional>& h = tops[p];
+    h.clear();
+    for (int64_t i = b; i < e; ++i) {
+      const int q = pos[i];
+      uint64_t* w = words + (q >> 6);
+      const uint64_t bit = uint64_t{1} << (q & 63);
+      if (keep[i]) {
+        __atomic_fetch_or(w, bit, __ATOMIC_RELAXED);
+        values[q] = value[i];
+        if (value[i] != value[i]) has_nan[p] = true;
+        offer(&h, value[i]);
+      } else {
+        __atomic_fetch_and(w, ~bit, __ATOMIC_RELAXED);
+      }
+    }
+  });
+  bool nan = parts > kMaxParts;
+  for (int p = 0; p < parts && !nan; ++p) nan = has_nan[p];
+  std::vector<int> acting;
+  if (!nan) {
+    std::vector<Fractional> incoming[kMaxParts];
+    std::vector<Fractional> running;
+    for (const HeapElement& e : tops_) offer(&running, e.value);
+    for (int p = 0; p < parts; ++p) {
+      incoming[p] = running;
+      for (const Fractional v : tops[p]) offer(&running, v);
+    }
+    std::vector<int> found[kMaxParts];
+    ParallelRanges(static_cast<int64_t>(n), 8192, 1, [&](int p, int64_t b, int64_t e) {
+      std::vector<Fractional> h = incoming[p];
+      std::vector<int>& out = found[p];
+      out.clear();
+      for (int64_t i = b; i < e; ++i) {
+        if (!keep[i] || value[i] < h.front()) continue;
+        out.push_back(static_cast<int>(i));
+        offer(&h, value[i]);
+      }
+    });
+    for (int p = 0; p < parts; ++p) acting.insert(acting.end(), found[p].begin(), found[p].end());
+  } else {
+    for (size_t i = 0; i < n; ++i) {
+      if (keep[i]) acting.push_back(static_cast<int>(i));
+    }
+  }
+  // The values and bits are final; the top-k sees the acting entries in order.
+  for (const int i : acting) {
+    if (value[i] >= threshold_) UpdateTopK(pos[i], value[i]);
+  }
+}
+
 // The full scan above only acts on the candidates that are not below the
 // threshold when the scan reaches them, and that threshold is the 31st
 // largest value seen so far (UpdateTopK keeps the 31 largest values; an equal
@@ -2750,13 +2839,7 @@ void VariableValues::UpdateDualPrices(const std::vector<int>& rows) {
         if (keep[k]) price[k] = by_norm ? std::fabs(inf) / sn[row] : Square(inf) / sn[row];
       }
     });
-    for (size_t k = 0; k < n; ++k) {
-      if (keep[k]) {
-        dual_prices_->AddOrUpdate(rows[k], price[k]);
-      } else {
-        dual_prices_->Remove(rows[k]);
-      }
-    }
+    dual_prices_->BulkAddOrUpdate(rows.data(), price, keep, n);
     return;
   }
   for (size_t k = 0; k < n; ++k) {

@@ -183,6 +183,15 @@ class DynamicMaximum {
   // pool (false: scan serially).
   bool ScanCandidatesInParallel(std::vector<int>* processed) const;
 
+ public:
+  // For k in [0, n): keep[k] ? AddOrUpdate(pos[k], value[k]) : Remove(pos[k]),
+  // the positions distinct. Long lists on a full top-k run the writes in
+  // parallel and replay only the AddOrUpdates that reach UpdateTopK, in
+  // order (the same heap operations and RNG draws as the loop).
+  void BulkAddOrUpdate(const int* pos, const Fractional* value, const uint8_t* keep, size_t n);
+
+ private:
+
   Rng* random_;
   std::vector<int> equivalent_choices_;
   std::vector<Fractional> values_;

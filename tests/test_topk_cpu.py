@@ -13,6 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROG = r"""
 #include "simplex.h"
 #include <cstdio>
+#include <algorithm>
 #include <random>
 #include <vector>
 // The serial scan of an empty top-k (GetMaximum's second half and UpdateTopK,
@@ -79,6 +80,48 @@ int main() {
     }
     if (got != want || r1() != r2()) {
       std::printf("mismatch trial %d: got %d want %d\n", trial, got, want);
+      return 1;
+    }
+  }
+  // BulkAddOrUpdate against the AddOrUpdate / Remove loop, round after round
+  // (GetMaximum between rounds keeps the top-k full and prunes it).
+  for (int trial = 0; trial < 12; ++trial) {
+    const int n = 90000;
+    const int levels = trial % 3 == 0 ? 4 : trial % 3 == 1 ? 40 : 1000000;
+    milp::Rng r1(7 + trial), r2(7 + trial);
+    milp::DynamicMaximum a(&r1), b(&r2);
+    a.ClearAndResize(n);
+    b.ClearAndResize(n);
+    a.StartDenseUpdates();
+    b.StartDenseUpdates();
+    for (int i = 0; i < n; ++i) {
+      if (gen() % 2) {
+        const double v = static_cast<double>(gen() % levels) * 0.5;
+        a.DenseAddOrUpdate(i, v);
+        b.DenseAddOrUpdate(i, v);
+      }
+    }
+    for (int round = 0; round < 6; ++round) {
+      const int ga = a.GetMaximum(), gb = b.GetMaximum();
+      if (ga != gb) { std::printf("bulk mismatch before round %d trial %d\n", round, trial); return 1; }
+      std::vector<int> perm(n);
+      for (int i = 0; i < n; ++i) perm[i] = i;
+      std::shuffle(perm.begin(), perm.end(), gen);
+      const int m = 10000 + static_cast<int>(gen() % 60000);
+      std::vector<int> pos(perm.begin(), perm.begin() + m);
+      std::vector<double> val(m);
+      std::vector<uint8_t> keep(m);
+      for (int k = 0; k < m; ++k) {
+        keep[k] = gen() % 4 != 0;
+        val[k] = static_cast<double>(gen() % levels) * 0.5 + (round % 2 ? 0.25 : 0.0);
+      }
+      a.BulkAddOrUpdate(pos.data(), val.data(), keep.data(), m);
+      for (int k = 0; k < m; ++k) {
+        if (keep[k]) b.AddOrUpdate(pos[k], val[k]); else b.Remove(pos[k]);
+      }
+    }
+    if (a.GetMaximum() != b.GetMaximum() || r1() != r2()) {
+      std::printf("bulk mismatch trial %d\n", trial);
       return 1;
     }
   }
