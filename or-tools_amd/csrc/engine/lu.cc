@@ -1240,6 +1240,121 @@ void BasisFactorization::LeftSolve(ScatteredVector* y) const {
 
 thread_local OverlapWork g_overlap;
 
+bool TriangularMatrix::ParallelTransposeSolve(bool forward, std::vector<Fractional>* rhs) const {
+  static const bool enabled = [] {
+    const char* e = std::getenv("MILP_HOST_TRI_PAR");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  constexpr int kMinRun = 2048;
+  const int n = num_cols_;
+  const int fni = first_non_identity_column_;
+  if (!enabled || n - fni < kMinRun || HostPool::Get().threads() <= 1) return false;
+  const int d = forward ? 0 : 1;
+  if (!par_ready_[d]) {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!par_ready_[d]) {
+      std::vector<int>& runs = par_runs_[d];
+      runs.clear();
+      int64_t long_entries = 0;
+      if (forward) {
+        // Column c reads rows r < c (and rows below fni, final): a run
+        // [a, b) reads no row of its own iff every column's largest row < a.
+        int a = fni;
+        while (a < n) {
+          int b = a + 1;
+          while (b < n) {
+            int mx = -1;
+            for (int64_t i = starts_[b]; i < starts_[b + 1]; ++i) mx = std::max(mx, rows_[i]);
+            if (mx >= a) break;
+            ++b;
+          }
+          if (b - a >= kMinRun) {
+            runs.push_back(a);
+            runs.push_back(b);
+            long_entries += starts_[b] - starts_[a];
+          }
+          a = b;
+        }
+      } else {
+        // Column c reads rows r > c: a run from a down to b reads no row of
+        // its own iff every column's smallest row > a.
+        int a = n - 1;
+        while (a >= fni) {
+          int b = a - 1;
+          while (b >= fni) {
+            int mn = n;
+            for (int64_t i = starts_[b]; i < starts_[b + 1]; ++i) mn = std::min(mn, rows_[i]);
+            if (mn <= a) break;
+            --b;
+          }
+          if (a - b >= kMinRun) {
+            runs.push_back(b + 1);  // [b + 1, a + 1)
+            runs.push_back(a + 1);
+            long_entries += starts_[a + 1] - starts_[b + 1];
+          }
+          a = b;
+        }
+      }
+      if (long_entries < (1 << 16)) runs.clear();
+      static const bool debug = std::getenv("MILP_HOST_TRI_PAR_DEBUG") != nullptr;
+      if (debug) {
+        int cols = 0;
+        for (size_t r = 0; r < runs.size(); r += 2) cols += runs[r + 1] - runs[r];
+        std::fprintf(stderr, "[tri par] %s n %d fni %d: %zu runs, %d columns, %lld entries\n",
+                     forward ? "forward" : "backward", n, fni, runs.size() / 2, cols,
+                     static_cast<long long>(long_entries));
+      }
+      par_ready_[d] = true;
+    }
+  }
+  const std::vector<int>& runs = par_runs_[d];
+  if (runs.empty()) return false;
+  Fractional* x = rhs->data();
+  auto run_parallel = [&](int b, int e) {
+    ParallelRanges(e - b, 512, 1, [&](int, int64_t lo, int64_t hi) {
+      for (int64_t k = lo; k < hi; ++k) {
+        const int col = b + static_cast<int>(k);
+        x[col] = forward ? TransposeUpperOutput(x, col) : TransposeLowerOutput(x, col);
+      }
+    });
+  };
+  if (forward) {
+    size_t r = 0;
+    int col = fni;
+    while (col < n) {
+      if (r < runs.size() && runs[r] == col) {
+        run_parallel(runs[r], runs[r + 1]);
+        col = runs[r + 1];
+        r += 2;
+      } else {
+        x[col] = TransposeUpperOutput(x, col);
+        ++col;
+      }
+    }
+    return true;
+  }
+  // Backward: the loop starts at the last non-zero input (the columns above
+  // it keep their zero).
+  int col = n - 1;
+  while (col >= fni && x[col] == 0.0) --col;
+  size_t r = 0;
+  while (r < runs.size() && runs[r] > col) r += 2;  // runs entirely above the start
+  while (col >= fni) {
+    if (r < runs.size() && runs[r + 1] - 1 >= col && runs[r] <= col) {
+      const int lo = runs[r];
+      run_parallel(lo, col + 1);  // the part of the run at or below col
+      col = lo - 1;
+      r += 2;
+    } else {
+      x[col] = TransposeLowerOutput(x, col);
+      --col;
+      while (r < runs.size() && runs[r] > col) r += 2;
+    }
+  }
+  return true;
+}
+
 // basis_representation.cc:358-372
 void BasisFactorization::RightSolve(ScatteredVector* d) const {
   if (!use_middle_product_form_update_) {

@@ -77,6 +77,7 @@ class TriangularMatrix : public CompactSparseMatrix {
   }
   // sparse.cc:562-572
   void Reset(int num_rows, int col_capacity) {
+    par_ready_[0] = par_ready_[1] = false;
     CompactSparseMatrix::Reset(num_rows);
     first_non_identity_column_ = 0;
     all_diagonal_coefficients_are_one_ = true;
@@ -86,6 +87,8 @@ class TriangularMatrix : public CompactSparseMatrix {
     starts_[0] = 0;
   }
   void Swap(TriangularMatrix* o) {
+    par_ready_[0] = par_ready_[1] = false;
+    o->par_ready_[0] = o->par_ready_[1] = false;
     std::swap(num_rows_, o->num_rows_);
     std::swap(num_cols_, o->num_cols_);
     coefficients_.swap(o->coefficients_);
@@ -98,6 +101,7 @@ class TriangularMatrix : public CompactSparseMatrix {
   }
   // sparse.cc:530-552
   void PopulateFromTranspose(const TriangularMatrix& input) {
+    par_ready_[0] = par_ready_[1] = false;
     CompactSparseMatrix::PopulateFromTranspose(input);
     diagonal_coefficients_ = input.diagonal_coefficients_;
     all_diagonal_coefficients_are_one_ = input.all_diagonal_coefficients_are_one_;
@@ -113,6 +117,7 @@ class TriangularMatrix : public CompactSparseMatrix {
   }
   // sparse.cc:651-672
   void CloseCurrentColumn(Fractional diagonal_value) {
+    par_ready_[0] = par_ready_[1] = false;
     diagonal_coefficients_[num_cols_] = diagonal_value;
     pruned_ends_[num_cols_] = coefficients_.size();
     ++num_cols_;
@@ -163,6 +168,7 @@ class TriangularMatrix : public CompactSparseMatrix {
   }
   // sparse.cc:749-755
   void ApplyRowPermutationToNonDiagonalEntries(const std::vector<int>& perm) {
+    par_ready_[0] = par_ready_[1] = false;
     for (auto& r : rows_) r = perm[r];
   }
   bool IsUpperTriangular() const {  // sparse.cc:739-747
@@ -216,8 +222,53 @@ class TriangularMatrix : public CompactSparseMatrix {
         x[rows_[i]] -= coeff * coefficients_[i];
     }
   }
+  // One output of TransposeUpperSolve / TransposeLowerSolve, the loops' own
+  // operations in their order (entries from the start / from the end).
+  Fractional TransposeUpperOutput(const Fractional* x, int col) const {
+    Fractional sum = x[col];
+    int64_t i = starts_[col];
+    const int64_t i_end = starts_[col + 1];
+    const int64_t shifted_end = i_end - 3;
+    for (; i < shifted_end; i += 4) {
+      sum -= coefficients_[i] * x[rows_[i]] + coefficients_[i + 1] * x[rows_[i + 1]] +
+             coefficients_[i + 2] * x[rows_[i + 2]] + coefficients_[i + 3] * x[rows_[i + 3]];
+    }
+    if (i < i_end) {
+      sum -= coefficients_[i] * x[rows_[i]];
+      if (i + 1 < i_end) {
+        sum -= coefficients_[i + 1] * x[rows_[i + 1]];
+        if (i + 2 < i_end) sum -= coefficients_[i + 2] * x[rows_[i + 2]];
+      }
+    }
+    return all_diagonal_coefficients_are_one_ ? sum : sum / diagonal_coefficients_[col];
+  }
+  Fractional TransposeLowerOutput(const Fractional* x, int col) const {
+    Fractional sum = x[col];
+    int64_t i = starts_[col + 1] - 1;
+    const int64_t i_end = starts_[col];
+    const int64_t shifted_end = i_end + 3;
+    for (; i >= shifted_end; i -= 4) {
+      sum -= coefficients_[i] * x[rows_[i]] + coefficients_[i - 1] * x[rows_[i - 1]] +
+             coefficients_[i - 2] * x[rows_[i - 2]] + coefficients_[i - 3] * x[rows_[i - 3]];
+    }
+    if (i >= i_end) {
+      sum -= coefficients_[i] * x[rows_[i]];
+      if (i >= i_end + 1) {
+        sum -= coefficients_[i - 1] * x[rows_[i - 1]];
+        if (i >= i_end + 2) sum -= coefficients_[i - 2] * x[rows_[i - 2]];
+      }
+    }
+    return all_diagonal_coefficients_are_one_ ? sum : sum / diagonal_coefficients_[col];
+  }
+  // Runs of consecutive columns that read no row of their own run, in the
+  // loop's order (forward: TransposeUpperSolve; backward: TransposeLowerSolve):
+  // a long run's outputs are independent, the host pool computes them
+  // (MILP_HOST_TRI_PAR=0: never). Built on first use after a change.
+  bool ParallelTransposeSolve(bool forward, std::vector<Fractional>* rhs) const;
+
   // sparse.cc:848-897 (grouped 4-term subtraction)
   void TransposeUpperSolve(std::vector<Fractional>* rhs) const {
+    if (ParallelTransposeSolve(true, rhs)) return;
     Fractional* x = rhs->data();
     const int end = num_cols_;
     const bool ones = all_diagonal_coefficients_are_one_;
@@ -245,6 +296,7 @@ class TriangularMatrix : public CompactSparseMatrix {
   }
   // sparse.cc:899-955
   void TransposeLowerSolve(std::vector<Fractional>* rhs) const {
+    if (ParallelTransposeSolve(false, rhs)) return;
     Fractional* x = rhs->data();
     const int end = first_non_identity_column_;
     int col = num_cols_ - 1;
@@ -525,6 +577,10 @@ class TriangularMatrix : public CompactSparseMatrix {
   std::vector<int64_t> pruned_ends_;
 
  private:
+  // ParallelTransposeSolve's runs per direction (0 forward, 1 backward):
+  // [begin, end) column ranges of the long independent runs, in loop order.
+  mutable bool par_ready_[2] = {false, false};
+  mutable std::vector<int> par_runs_[2];
   mutable std::vector<char> stored_slots_[2];
   std::vector<char> marked_;
   std::vector<int> nodes_to_explore_;

@@ -1,0 +1,106 @@
+"""TriangularMatrix's TransposeUpperSolve / TransposeLowerSolve (sparse.cc:
+848-955) with long independent runs of columns computed by the host pool
+(engine/lu.cc ParallelTransposeSolve) must give the serial loops' bits. The
+engine library is linked (host code only); MILP_HOST_TRI_PAR=0 is the serial
+reference."""
+import os
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+PROG = r"""
+#include "lu.h"
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+// Columns: a chain, a long run reading only the chain, a chain again, a run,
+// a few identity columns first. upper: rows < col; else rows > col.
+static void Build(milp::TriangularMatrix* t, int n, bool upper, std::mt19937_64& g, bool ones) {
+  t->Reset(n, n);
+  std::vector<int> rows;
+  std::vector<double> coefs;
+  std::uniform_real_distribution<double> u(-2, 2);
+  const int ident = 7;
+  for (int k = 0; k < n; ++k) {
+    const int col = k;
+    rows.clear();
+    coefs.clear();
+    const int pos = upper ? col : n - 1 - col;  // position in the loop order
+    if (pos >= ident) {
+      const bool chain = (pos / 3000) % 2 == 0 && pos % 3000 < 400;
+      const int base = (pos / 3000) * 3000;  // the previous block's end
+      const int cnt = 1 + static_cast<int>(g() % 30);
+      for (int e = 0; e < cnt; ++e) {
+        int src_pos;
+        if (chain) {
+          src_pos = pos - 1 - static_cast<int>(g() % std::max(1, std::min(pos, 50)));
+        } else {
+          // A run column reads only positions before its block's run start.
+          const int lim = std::max(1, base + 400);
+          src_pos = static_cast<int>(g() % std::min(lim, pos));
+        }
+        if (src_pos < 0 || src_pos >= pos) continue;
+        const int r = upper ? src_pos : n - 1 - src_pos;
+        bool dup = false;
+        for (int q : rows) dup = dup || q == r;
+        if (dup) continue;
+        rows.push_back(r);
+        coefs.push_back(u(g));
+      }
+    }
+    rows.push_back(col);
+    coefs.push_back(ones ? 1.0 : 0.5 + (g() % 100) / 50.0);
+    milp::ColumnView v;
+    v.rows = rows.data();
+    v.coefs = coefs.data();
+    v.n = static_cast<int64_t>(rows.size());
+    t->AddTriangularColumn(v, col);
+  }
+}
+int main(int argc, char** argv) {
+  const bool dump = argc > 1 && std::strcmp(argv[1], "dump") == 0;
+  std::mt19937_64 g(5);
+  unsigned long long h = 1469598103934665603ull;
+  for (int trial = 0; trial < 6; ++trial) {
+    const int n = 9000 + 1500 * trial;
+    for (int upper = 0; upper < 2; ++upper) {
+      milp::TriangularMatrix t;
+      Build(&t, n, upper == 1, g, trial % 2 == 0);
+      for (int rep = 0; rep < 3; ++rep) {
+        std::vector<double> x(n, 0.0);
+        const int zeros_top = rep == 2 ? 1000 : 0;  // the backward loop's skip
+        for (int i = 0; i < n - zeros_top; ++i) x[i] = (g() % 5 == 0) ? 0.0 : std::uniform_real_distribution<double>(-1, 1)(g);
+        if (upper) t.TransposeUpperSolve(&x); else t.TransposeLowerSolve(&x);
+        for (double v : x) { unsigned long long b; std::memcpy(&b, &v, 8); h = (h ^ b) * 1099511628211ull; }
+      }
+    }
+  }
+  std::printf("%016llx\n", h);
+  return 0;
+}
+"""
+
+
+def test_parallel_transpose_solves_match_serial(tmp_path):
+    src = tmp_path / "tp.cc"
+    src.write_text(PROG)
+    exe = tmp_path / "tp"
+    lib = os.path.join(REPO, "or-tools_amd", "lib")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-ffp-contract=off",
+                    "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include",
+                    "-I", os.path.join(REPO, "or-tools_amd", "csrc", "engine"), str(src),
+                    "-o", str(exe), "-L", lib, "-lmi_lp", f"-Wl,-rpath,{lib}"], check=True)
+    out = {}
+    for par, threads in (("0", "8"), ("1", "8"), ("1", "3")):
+        env = dict(os.environ, MILP_HOST_TRI_PAR=par, MILP_HOST_THREADS=threads,
+                   MILP_HOST_TRI_PAR_DEBUG="1")
+        r = subprocess.run([str(exe)], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        if par == "1":  # the parallel runs were found in both directions
+            assert "forward" in r.stderr and "backward" in r.stderr, r.stderr
+            assert " 0 runs" not in r.stderr, r.stderr
+        out[(par, threads)] = r.stdout.strip()
+    assert len(set(out.values())) == 1, out
