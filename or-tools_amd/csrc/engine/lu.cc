@@ -1276,6 +1276,41 @@ bool TriangularMatrix::ParallelTransposeSolve(bool forward, std::vector<Fraction
           }
           a = b;
         }
+        // A dense tail: the trailing columns holding at least n/4 entries
+        // each. Their leading groups of four that read rows below the tail
+        // only are final when the tail starts: that part of each column's
+        // subtraction chain is computed for all tail columns at once.
+        par_tail_ = -1;
+        int t = n;
+        while (t > fni && starts_[t] - starts_[t - 1] >= n / 4) --t;
+        if (n - t >= 64) {
+          par_split_.assign(n - t, 0);
+          int64_t pre = 0;
+          for (int c = t; c < n; ++c) {
+            const int64_t i0 = starts_[c], i1 = starts_[c + 1];
+            int64_t i = i0;
+            while (i + 3 < i1 && rows_[i] < t && rows_[i + 1] < t && rows_[i + 2] < t &&
+                   rows_[i + 3] < t) {
+              i += 4;
+            }
+            par_split_[c - t] = i;
+            pre += i - i0;
+          }
+          if (pre >= (1 << 16)) {
+            par_tail_ = t;
+            // Runs past the tail's start would race with it: cut them there.
+            std::vector<int> kept;
+            for (size_t r = 0; r < runs.size(); r += 2) {
+              const int rb = runs[r], re = std::min(runs[r + 1], t);
+              if (re - rb >= kMinRun) {
+                kept.push_back(rb);
+                kept.push_back(re);
+              }
+            }
+            runs.swap(kept);
+            long_entries = std::max<int64_t>(long_entries, 1 << 16);  // the tail pays
+          }
+        }
       } else {
         // Column c reads rows r > c: a run from a down to b reads no row of
         // its own iff every column's smallest row > a.
@@ -1301,15 +1336,15 @@ bool TriangularMatrix::ParallelTransposeSolve(bool forward, std::vector<Fraction
       if (debug) {
         int cols = 0;
         for (size_t r = 0; r < runs.size(); r += 2) cols += runs[r + 1] - runs[r];
-        std::fprintf(stderr, "[tri par] %s n %d fni %d: %zu runs, %d columns, %lld entries\n",
+        std::fprintf(stderr, "[tri par] %s n %d fni %d: %zu runs, %d columns, %lld entries, tail %d\n",
                      forward ? "forward" : "backward", n, fni, runs.size() / 2, cols,
-                     static_cast<long long>(long_entries));
+                     static_cast<long long>(long_entries), forward ? par_tail_ : -1);
       }
       par_ready_[d] = true;
     }
   }
   const std::vector<int>& runs = par_runs_[d];
-  if (runs.empty()) return false;
+  if (runs.empty() && !(forward && par_tail_ >= fni)) return false;
   Fractional* x = rhs->data();
   auto run_parallel = [&](int b, int e) {
     ParallelRanges(e - b, 512, 1, [&](int, int64_t lo, int64_t hi) {
@@ -1322,7 +1357,8 @@ bool TriangularMatrix::ParallelTransposeSolve(bool forward, std::vector<Fraction
   if (forward) {
     size_t r = 0;
     int col = fni;
-    while (col < n) {
+    const int tail = par_tail_ >= fni ? par_tail_ : n;
+    while (col < tail) {
       if (r < runs.size() && runs[r] == col) {
         run_parallel(runs[r], runs[r + 1]);
         col = runs[r + 1];
@@ -1330,6 +1366,44 @@ bool TriangularMatrix::ParallelTransposeSolve(bool forward, std::vector<Fraction
       } else {
         x[col] = TransposeUpperOutput(x, col);
         ++col;
+      }
+    }
+    if (tail < n) {
+      // The chains' final-only prefixes (sum = x[c], then the loop's own
+      // grouped subtractions up to the split), in parallel; then each column
+      // in order continues its chain exactly where the loop would be.
+      par_prefix_.resize(n - tail);
+      Fractional* pre = par_prefix_.data();
+      ParallelRanges(n - tail, 64, 1, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi; ++k) {
+          const int c = tail + static_cast<int>(k);
+          Fractional sum = x[c];
+          const int64_t split = par_split_[k];
+          for (int64_t i = starts_[c]; i < split; i += 4) {
+            sum -= coefficients_[i] * x[rows_[i]] + coefficients_[i + 1] * x[rows_[i + 1]] +
+                   coefficients_[i + 2] * x[rows_[i + 2]] +
+                   coefficients_[i + 3] * x[rows_[i + 3]];
+          }
+          pre[k] = sum;
+        }
+      });
+      for (int c = tail; c < n; ++c) {
+        Fractional sum = pre[c - tail];
+        int64_t i = par_split_[c - tail];
+        const int64_t i_end = starts_[c + 1];
+        const int64_t shifted_end = i_end - 3;
+        for (; i < shifted_end; i += 4) {
+          sum -= coefficients_[i] * x[rows_[i]] + coefficients_[i + 1] * x[rows_[i + 1]] +
+                 coefficients_[i + 2] * x[rows_[i + 2]] + coefficients_[i + 3] * x[rows_[i + 3]];
+        }
+        if (i < i_end) {
+          sum -= coefficients_[i] * x[rows_[i]];
+          if (i + 1 < i_end) {
+            sum -= coefficients_[i + 1] * x[rows_[i + 1]];
+            if (i + 2 < i_end) sum -= coefficients_[i + 2] * x[rows_[i + 2]];
+          }
+        }
+        x[c] = all_diagonal_coefficients_are_one_ ? sum : sum / diagonal_coefficients_[c];
       }
     }
     return true;

@@ -581,6 +581,11 @@ class TriangularMatrix : public CompactSparseMatrix {
   // [begin, end) column ranges of the long independent runs, in loop order.
   mutable bool par_ready_[2] = {false, false};
   mutable std::vector<int> par_runs_[2];
+  // Forward solve's dense tail [par_tail_, n): per column, the end of its
+  // leading groups of four that read rows < par_tail_ only (-1: no tail).
+  mutable int par_tail_ = -1;
+  mutable std::vector<int64_t> par_split_;
+  mutable std::vector<Fractional> par_prefix_;
   mutable std::vector<char> stored_slots_[2];
   std::vector<char> marked_;
   std::vector<int> nodes_to_explore_;

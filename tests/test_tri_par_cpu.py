@@ -13,6 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROG = r"""
 #include "lu.h"
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <random>
 #include <vector>
@@ -60,6 +61,37 @@ static void Build(milp::TriangularMatrix* t, int n, bool upper, std::mt19937_64&
     t->AddTriangularColumn(v, col);
   }
 }
+// A dense tail (upper, forward solve): the last `tail` columns read most of
+// the rows below the tail (in increasing row order) and then the tail's own
+// earlier columns, like a Markowitz U over a dense kernel.
+static void BuildTail(milp::TriangularMatrix* t, int n, int tail, std::mt19937_64& g, bool sorted) {
+  t->Reset(n, n);
+  std::vector<int> rows;
+  std::vector<double> coefs;
+  std::uniform_real_distribution<double> u(-1, 1);
+  for (int col = 0; col < n; ++col) {
+    rows.clear();
+    coefs.clear();
+    if (col >= n - tail) {
+      for (int r = 0; r < col; ++r) {
+        if (r < n - tail && g() % 5 == 0) continue;
+        rows.push_back(r);
+        coefs.push_back(u(g) * 0.01);
+      }
+      if (!sorted) std::shuffle(rows.begin(), rows.end(), g);
+    } else if (col > 3 && g() % 2) {
+      rows.push_back(static_cast<int>(g() % col));
+      coefs.push_back(u(g));
+    }
+    rows.push_back(col);
+    coefs.push_back(1.0 + (g() % 7) * 0.1);
+    milp::ColumnView v;
+    v.rows = rows.data();
+    v.coefs = coefs.data();
+    v.n = static_cast<int64_t>(rows.size());
+    t->AddTriangularColumn(v, col);
+  }
+}
 int main(int argc, char** argv) {
   const bool dump = argc > 1 && std::strcmp(argv[1], "dump") == 0;
   std::mt19937_64 g(5);
@@ -76,6 +108,16 @@ int main(int argc, char** argv) {
         if (upper) t.TransposeUpperSolve(&x); else t.TransposeLowerSolve(&x);
         for (double v : x) { unsigned long long b; std::memcpy(&b, &v, 8); h = (h ^ b) * 1099511628211ull; }
       }
+    }
+  }
+  for (int trial = 0; trial < 4; ++trial) {
+    milp::TriangularMatrix t;
+    BuildTail(&t, 3000 + 500 * trial, 200 + 100 * trial, g, trial != 3);
+    for (int rep = 0; rep < 2; ++rep) {
+      std::vector<double> x(t.num_cols());
+      for (auto& v : x) v = (g() % 4 == 0) ? 0.0 : std::uniform_real_distribution<double>(-1, 1)(g);
+      t.TransposeUpperSolve(&x);
+      for (double v : x) { unsigned long long b; std::memcpy(&b, &v, 8); h = (h ^ b) * 1099511628211ull; }
     }
   }
   std::printf("%016llx\n", h);
@@ -99,8 +141,10 @@ def test_parallel_transpose_solves_match_serial(tmp_path):
                    MILP_HOST_TRI_PAR_DEBUG="1")
         r = subprocess.run([str(exe)], env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr
-        if par == "1":  # the parallel runs were found in both directions
-            assert "forward" in r.stderr and "backward" in r.stderr, r.stderr
-            assert " 0 runs" not in r.stderr, r.stderr
+        if par == "1":  # runs in both directions and a dense tail were found
+            lines = [ln for ln in r.stderr.splitlines() if ln.startswith("[tri par]")]
+            assert any("forward" in ln and " 0 runs" not in ln for ln in lines), r.stderr
+            assert any("backward" in ln and " 0 runs" not in ln for ln in lines), r.stderr
+            assert any("forward" in ln and "tail -1" not in ln for ln in lines), r.stderr
         out[(par, threads)] = r.stdout.strip()
     assert len(set(out.values())) == 1, out
