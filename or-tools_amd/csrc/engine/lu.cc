@@ -1248,7 +1248,9 @@ bool TriangularMatrix::ParallelTransposeSolve(bool forward, std::vector<Fraction
   constexpr int kMinRun = 2048;
   const int n = num_cols_;
   const int fni = first_non_identity_column_;
-  if (!enabled || n - fni < kMinRun || HostPool::Get().threads() <= 1) return false;
+  // (A dense tail can be short: a kernel of a few hundred columns behind
+  // thousands of identity columns.)
+  if (!enabled || n - fni < 64 || HostPool::Get().threads() <= 1) return false;
   const int d = forward ? 0 : 1;
   if (!par_ready_[d]) {
     static std::mutex mu;

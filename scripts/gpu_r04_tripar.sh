@@ -14,7 +14,7 @@ rc=$?; echo "tests rc=$rc"; tail -3 $OUT/tests.log
 MILP_HOST_TRI_PAR_DEBUG=1 timeout -k 10 500 python3 -u scripts/probe.py --config c2 --warmup 1500 --steps 64 \
   --variants "" MILP_HOST_TRI_PAR=0 > $OUT/c2_late.json 2> $OUT/c2_late.err || exit 1
 grep -h "variant\|it/s" $OUT/c2_late.err
-grep -h "tri par" $OUT/c2_late.err | sort | uniq -c | sort -rn | head -8
+grep -h "tri par" $OUT/c2_late.err | sort | uniq -c | sort -rn | head -4; grep -h "tri par\] forward" $OUT/c2_late.err | tail -3
 timeout -k 10 300 python3 -u scripts/probe.py --config c5 --m 100000 --n 1000000 --warmup 20020 \
   --steps 1000 --variants "" MILP_HOST_TRI_PAR=0 > $OUT/c5.json 2> $OUT/c5.err || exit 1
 grep -h "variant\|it/s" $OUT/c5.err
