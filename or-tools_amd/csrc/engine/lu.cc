@@ -1241,9 +1241,12 @@ void BasisFactorization::LeftSolve(ScatteredVector* y) const {
 thread_local OverlapWork g_overlap;
 
 bool TriangularMatrix::ParallelTransposeSolve(bool forward, std::vector<Fractional>* rhs) const {
+  // Opt-in (MILP_HOST_TRI_PAR=1): on the MI355X box the gain on config 2's
+  // late window stayed within the noise and config 5's window read -9 % / +3 %
+  // in two A/Bs (scripts/gpu_r04_tripar.sh).
   static const bool enabled = [] {
     const char* e = std::getenv("MILP_HOST_TRI_PAR");
-    return e == nullptr || std::atoi(e) != 0;
+    return e != nullptr && std::atoi(e) != 0;
   }();
   constexpr int kMinRun = 2048;
   const int n = num_cols_;
