@@ -74,6 +74,23 @@ def cpu_baseline(lp, warm, iters):
                       timed_iterations=iters, warm_iterations=warm)
 
 
+def _solution_digests(h, r):
+    """sha256 of everything the drop-in contract names, from an engine handle
+    or an oracle handle after a solve (same getters on both)."""
+    import hashlib
+
+    def digest(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    var, cons = h.statuses()
+    return {"iterations": str(int(r.iterations)), "problem_status": str(int(r.problem_status)),
+            "error_code": str(int(r.error_code)), "objective": float(r.objective).hex(),
+            "basis": digest(h.basis()), "state": digest(h.state()),
+            "var_status": digest(var), "cons_status": digest(cons),
+            "primal": digest(h.primal()), "duals": digest(h.duals()),
+            "reduced_costs": digest(h.reduced_costs())}
+
+
 def kernel_roofline(stats, traffic_json=None):
     """Roofline of the dominant kernel id of a timed window: algorithmic bytes
     per launch / HIP-event time per launch, against the HBM peak."""
@@ -128,7 +145,11 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     import lp_gen
     split = world > 1 and not args.c5_replicas
     lp = lp_gen.sparse_c5_lp(args.c5_m, args.c5_n, 10, args.seed + (0 if split else rank))
-    p = abi.default_params(use_dual_simplex=1)
+    start = args.c5_window + args.warmup
+    # The solve is capped where the timed windows end, so that its final
+    # state is the one the oracle reaches with the same cap (oracle_check).
+    end = start + max(args.steps, args.c5_amortized)
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=end)
     h = engine.LpHandle(p, device=local_rank)
     if split:
         # The exchange runs on a gloo group: the joined messages are host
@@ -140,7 +161,6 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     h.load(lp)
     h.record_iteration_times(True)  # per-iteration timestamps (window statistics)
     t = time.perf_counter()
-    start = args.c5_window + args.warmup
     h.begin(start)
     setup = time.perf_counter() - t
     log(f"c5: solve ran to iteration {start} in {setup:.1f}s (untimed)")
@@ -194,8 +214,11 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
         amortized = {"timed_iterations": [start, start + done], "value": total_done / elapsed
                      if elapsed > 0 else 0.0, "ms_per_step": 1000.0 * elapsed / max(1, done),
                      "window": window}
-    h.stop()
-    h.finish()
+    # Run on to the cap (untimed): the final state is compared with the
+    # oracle's at the same iteration below.
+    h.run_until(end + 1)
+    final = h.finish()
+    digests = _solution_digests(h, final) if rank == 0 and world == 1 else None
     del h
     out = {
         "value": total_done / elapsed if elapsed > 0 else 0.0,
@@ -221,18 +244,26 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
                            "bytes_per_step": ex.get("bytes", 0.0) / max(1, done)}
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_lib
-        # The oracle runs the same solve to the end of the amortized window;
-        # its per-iteration timestamps give its rate on exactly the GPU's
-        # headline window and on the amortized window.
-        end = start + max(done, span if amortized else done)
+        # The oracle runs the same solve with the same cap; its per-iteration
+        # timestamps give its rate on exactly the GPU's headline window and
+        # on the amortized window, and its final state must equal the
+        # engine's bit for bit (oracle_check).
         log(f"c5: cpu baseline (oracle) to iteration {end}")
         po = abi.default_params(use_dual_simplex=1, max_number_of_iterations=end)
         o = oracle_lib.OracleLp(po)
         o.record_iteration_times(True)
         o.load(lp)
         t = time.perf_counter()
-        o.solve()
+        ro = o.solve()
         wall = time.perf_counter() - t
+        ref = _solution_digests(o, ro)
+        bad = sorted(k for k in ref if ref[k] != digests[k])
+        out["oracle_check"] = {"iteration": int(ro.iterations), "fields": sorted(ref),
+                               "mismatches": len(bad), "differing": bad,
+                               "digest": ref["primal"][:16]}
+        if bad:
+            FAILURES.append(f"config 5 at iteration {ro.iterations}: {bad} differ from the oracle")
+        log(f"c5: oracle_check at iteration {ro.iterations}: {len(bad)} mismatches")
         ts = o.iteration_times()
         if len(ts) >= start + done and done > 0:
             dt = ts[start + done - 1] - ts[start - 1]
@@ -351,10 +382,20 @@ def run_c3(args, rank, world, local_rank, dist, barrier, sync):
         h = engine.LpHandle(p, device=local_rank)
         h.load(lp)
         handles.append(h)
+    log(f"c3: {len(lps)} LPs loaded (largest {max(lp.m for lp in lps)} rows)")
+
+    def progress(done, elapsed):
+        # Per-LP progress on stderr: a long or stuck member shows by name.
+        left = [lps[i] for i in range(len(lps)) if i not in set(done)]
+        big = ", ".join(f"{lp.m}x{lp.n}" for lp in sorted(left, key=lambda q: -q.m)[:3])
+        log(f"c3: {len(done)}/{len(lps)} LPs done after {elapsed:.1f}s"
+            + (f"; largest running: {big}" if left else ""))
+
     barrier()
     sync()
     t0 = time.perf_counter()
-    res = engine.batch_solve(handles, num_threads=args.c3_workers)
+    res = engine.batch_solve(handles, num_threads=args.c3_workers, progress=progress,
+                             progress_s=10.0)
     sync()
     barrier()
     elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, COLL_DEVICE)
@@ -494,7 +535,8 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     first) each give a down branch (y <= floor) and an up branch (y >= ceil),
     all warm-started from the node's basis state (SolveLpForBranching,
     :443-464). The variables are sharded across ranks (both branches of a
-    variable on one rank, weak scaling: each rank batch_lps LPs), solved by
+    variable on one rank; strong scaling by default: the node's batch_lps
+    LPs split over the ranks, --batch-scaling weak: batch_lps per rank), solved by
     `workers` GPU handles per rank, and folded with BranchOnVar's decisions.
     The only collective: all-reduce(max) of the node's objective lower bound
     (each variable's min over its branches is a valid bound), the cross-GPU
@@ -511,16 +553,21 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     x = root.primal()
     node = cpsat.IntegerTrail(lp.col_lb, lp.col_ub,
                               obj_lb=math.ceil(root_res.objective - cpsat.K_CP_EPSILON))
-    cols_all = cpsat.fractional_columns(x, ycols, limit=(args.batch_lps // 2) * world)
+    # Strong scaling (BASELINE config 4: one node's ~1k LPs sharded over the
+    # GPUs): --batch-lps is the node's total; weak: --batch-lps per GPU.
+    strong = args.batch_scaling == "strong"
+    per_node = args.batch_lps // 2 if strong else (args.batch_lps // 2) * world
+    cols_all = cpsat.fractional_columns(x, ycols, limit=per_node)
     b, e = distributed.shard(len(cols_all), rank, world)
     cols = cols_all[b:e]
     lbs, ubs = cpsat.branch_lps(node, x, cols)
     p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
-    workers = [engine.LpHandle(p, device=local_rank) for _ in range(args.batch_workers)]
+    n_workers = max(1, min(args.batch_workers, len(lbs)))
+    workers = [engine.LpHandle(p, device=local_rank) for _ in range(n_workers)]
     for w in workers:
         w.load(lp)
     # Warm-up batch (not timed): first-touch allocations on every worker.
-    engine.batch_solve_bounds(workers, lbs[:args.batch_workers], ubs[:args.batch_workers], state)
+    engine.batch_solve_bounds(workers, lbs[:n_workers], ubs[:n_workers], state)
     for w in workers:
         w.reset_kernel_stats()
     barrier()
@@ -535,8 +582,9 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     total = distributed.sum_over_ranks(len(lbs), dist, COLL_DEVICE)
     out = {
         "metric": "batched LPs/sec", "value": total / elapsed, "unit": "LPs/s",
-        "lps": int(total), "seconds": elapsed, "workers_per_gpu": args.batch_workers,
-        "host_threads_per_gpu": min(args.batch_workers, 16),
+        "scaling": args.batch_scaling, "lps_this_rank": len(lbs),
+        "lps": int(total), "seconds": elapsed, "workers_per_gpu": n_workers,
+        "host_threads_per_gpu": min(n_workers, 16),
         "mean_iterations": float(np.mean([r.iterations for r in res])) if res else 0.0,
         "root_objective": float(root_res.objective), "root_iterations": int(root_res.iterations),
         "node_obj_lb": node_lb, "deductions": int(summary["deductions"]),
@@ -602,7 +650,11 @@ def main():
                     help="per-launch HBM bytes of the config-2 dominant kernel from a "
                          "separate rocprofv3 --pmc pass (profiles/)")
     ap.add_argument("--batch-lps", type=int, default=1024,
-                    help="config-4 branch LPs per GPU (0 disables the batched section)")
+                    help="config-4 branch LPs of the search node (strong) or per GPU (weak); "
+                         "0 disables the batched section")
+    ap.add_argument("--batch-scaling", default="strong", choices=["strong", "weak"],
+                    help="config 4 over N GPUs: one node's LPs split over the ranks (strong, "
+                         "BASELINE config 4) or --batch-lps per rank (weak)")
     ap.add_argument("--batch-workers", type=int, default=1024,
                     help="config-4 solver handles per GPU (LPs in flight); the engine runs "
                          "them on at most 16 host threads as fibers with batched launches")
@@ -611,7 +663,8 @@ def main():
     ap.add_argument("--batch-machines", type=int, default=10)
     ap.add_argument("--batch-cpu-lps", type=int, default=512)
     ap.add_argument("--no-c3", action="store_true", help="skip the config-3 section")
-    ap.add_argument("--c3-max-rows", type=int, default=1000)
+    ap.add_argument("--c3-max-rows", type=int, default=16000,
+                    help="largest config-3 member (SURVEY 8(c): m from 27 to ~16k)")
     ap.add_argument("--c3-workers", type=int, default=16)
     ap.add_argument("--c3-cpu-threads", type=int, default=16)
     args = ap.parse_args()
@@ -676,7 +729,7 @@ def main():
         log(f"c3: {c3['value']:.1f} LPs/s")
     batched = None
     if args.batch_lps > 0:
-        log(f"batched section: {args.batch_lps} children per GPU")
+        log(f"batched section: {args.batch_lps} children ({args.batch_scaling} scaling)")
         batched = run_batched(args, rank, world, local_rank, dist, barrier, sync)
         log(f"batched: {batched['value']:.1f} LPs/s")
     if rank != 0:

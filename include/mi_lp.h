@@ -196,6 +196,13 @@ void mi_glop_params_default(mi_glop_params* p);
 
 /* Returns the number of visible GPUs (0 on a host without one). */
 int mi_lp_device_count(void);
+/* Process teardown: drains the persistent batched-segment grids and joins the
+ * engine's service threads (LU servers, batched-launch launchers) while the
+ * HIP runtime is still up. Registered with atexit when the first such object
+ * is created; hosts whose own teardown runs earlier (Python atexit, a plugin
+ * unload) call it explicitly. Idempotent; later solves restart what they need.
+ * (No Glop counterpart: Glop owns no threads or device state.) */
+int mi_lp_shutdown(void);
 
 int mi_lp_create(int device, mi_lp** out);
 int mi_lp_destroy(mi_lp* h);

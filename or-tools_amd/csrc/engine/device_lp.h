@@ -30,6 +30,13 @@ void SdualProfileReset();
 // A batch call on `device` starts (begin) or ends using the device's segment
 // pool; when the last one ends, the resident pool grid is told to stop.
 void SdualPoolScope(int device, bool begin, int lps);
+// Process teardown of the engine's long-lived device objects (sdual pool
+// grids, LU server threads, small-batch launcher threads), before the HIP
+// runtime's own: mi_lp_shutdown, and an atexit handler registered when the
+// first such object is created (RegisterDeviceShutdown). Idempotent.
+void ShutdownDevices();
+void SdualShutdown();
+void RegisterDeviceShutdown();
 
 class CompactSparseMatrix;
 

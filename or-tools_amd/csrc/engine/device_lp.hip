@@ -245,14 +245,23 @@ class SmallBatcher {
  public:
   static constexpr int kMaxSlots = 2048;
   static SmallBatcher& Get(int device) {
-    // Never destroyed: the launcher thread sleeps in its wait at process
-    // exit, after the HIP runtime may already be gone.
-    static std::mutex mu;
-    static std::vector<SmallBatcher*>* all = new std::vector<SmallBatcher*>();
-    std::lock_guard<std::mutex> lock(mu);
-    if (static_cast<int>(all->size()) <= device) all->resize(device + 1, nullptr);
-    if ((*all)[device] == nullptr) (*all)[device] = new SmallBatcher(device);
-    return *(*all)[device];
+    // Never destroyed: the launcher thread is stopped and joined by
+    // ShutdownAll (mi_lp_shutdown / the atexit handler) before the HIP
+    // runtime goes away.
+    std::lock_guard<std::mutex> lock(RegistryMutex());
+    std::vector<SmallBatcher*>& all = Registry();
+    if (static_cast<int>(all.size()) <= device) all.resize(device + 1, nullptr);
+    if (all[device] == nullptr) {
+      all[device] = new SmallBatcher(device);
+      RegisterDeviceShutdown();
+    }
+    return *all[device];
+  }
+  static void ShutdownAll() {
+    std::lock_guard<std::mutex> lock(RegistryMutex());
+    for (SmallBatcher* b : Registry()) {
+      if (b != nullptr) b->Stop();
+    }
   }
   int AddSlot() {
     std::lock_guard<std::mutex> lock(mu_);
@@ -279,11 +288,17 @@ class SmallBatcher {
       std::lock_guard<std::mutex> lock(mu_);
       pending_[kind].push_back(id);
       ++num_pending_;
+      if (!launcher_.joinable()) {  // stopped by ShutdownAll: start again
+        stop_ = false;
+        launcher_ = std::thread([this] { LauncherLoop(); });
+      }
     }
     cv_.notify_one();
   }
 
-  ~SmallBatcher() {
+  ~SmallBatcher() { Stop(); }
+  // The launcher finishes the requests already pending, then exits.
+  void Stop() {
     {
       std::lock_guard<std::mutex> lock(mu_);
       stop_ = true;
@@ -293,6 +308,14 @@ class SmallBatcher {
   }
 
  private:
+  static std::mutex& RegistryMutex() {
+    static std::mutex* mu = new std::mutex();
+    return *mu;
+  }
+  static std::vector<SmallBatcher*>& Registry() {
+    static std::vector<SmallBatcher*>* all = new std::vector<SmallBatcher*>();
+    return *all;
+  }
   // The launcher: takes every pending request, launches one kernel per kind
   // (a workgroup per request), waits for it, repeats. With one batch in
   // flight the requests of the other LPs gather while it runs, so a batch
@@ -386,6 +409,22 @@ void SetSlotArgs(milp_kernels::SmallSlot* s, const milp_kernels::RowWiseSmallCol
 }  // namespace
 
 void ReleaseSmallBatchSlot(int device, int slot) { SmallBatcher::Get(device).FreeSlot(slot); }
+
+void ShutdownDevices() {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  SdualShutdown();
+  SmallBatcher::ShutdownAll();
+}
+
+// std::atexit from the first long-lived device object: registered after the
+// HIP runtime initialized, so it runs before the runtime's own exit-time
+// teardown (atexit handlers and static destructors run in reverse order of
+// registration).
+void RegisterDeviceShutdown() {
+  static std::once_flag once;
+  std::call_once(once, [] { std::atexit([] { ShutdownDevices(); }); });
+}
 
 template <typename Args>
 void DeviceLp::LaunchSmall(int kind, const Args& args) {

@@ -732,6 +732,9 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
     EnqueueTriKernels(s, a, c.stream);
     EndKernel(id, bytes);
     TriCopyOut(s, c);
+    // The armed MPF right-pool append reads the FTRAN vector before it is
+    // overwritten below, as on the normal path.
+    g_overlap.Run();
     Synchronize();
     --tri_debug_left_;
     std::vector<uint64_t> clk(s.levels + 1);

@@ -13,8 +13,10 @@
 // chunks out. Two banks suffice: a rank can start round seq + 1 only after
 // every rank started round seq, i.e. finished reading round seq - 1's bank.
 // Messages longer than a slot go in several rounds.
+#include <errno.h>
 #include <fcntl.h>
 #include <sched.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -22,6 +24,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -46,26 +49,48 @@ struct Header {
   std::atomic<int32_t> attached;
   int32_t pad;
   SeqWord seq[kMaxWorld];
+  std::atomic<int32_t> pid[kMaxWorld];  // each rank's process, for liveness checks
 };
+
+// MILP_EXCHANGE_TIMEOUT_S: how long a rank waits for its peers in one
+// all-gather round (default 0 = as long as every peer process is alive: a
+// long refactorization or a slow first segment on one rank is not an error).
+// Attaching waits at most MILP_EXCHANGE_ATTACH_S (default 120) seconds.
+double EnvSeconds(const char* name, double fallback) {
+  const char* e = std::getenv(name);
+  return e != nullptr ? std::atof(e) : fallback;
+}
+
+bool PeerAlive(int32_t pid) { return pid <= 0 || kill(pid, 0) == 0 || errno != ESRCH; }
 
 size_t SegmentBytes(int world, int64_t slot_bytes) {
   return sizeof(Header) + 2 * static_cast<size_t>(world) * static_cast<size_t>(slot_bytes);
 }
 
-// Waits until pred() or the timeout (seconds); spins, then yields.
-template <typename Pred>
-bool WaitFor(Pred pred, double timeout_s) {
+// Waits until pred() or the timeout (seconds; <= 0: none) or alive()
+// returns false (checked about once a second); spins, then yields.
+template <typename Pred, typename Alive>
+bool WaitFor(Pred pred, double timeout_s, Alive alive) {
   for (int i = 0; i < 4096; ++i) {
     if (pred()) return true;
   }
   const auto t0 = std::chrono::steady_clock::now();
+  double next_check = 1.0;
   while (!pred()) {
     std::this_thread::yield();
-    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
-      return false;
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_s > 0 && s > timeout_s) return false;
+    if (s > next_check) {
+      if (!alive()) return false;
+      next_check = s + 1.0;
     }
   }
   return true;
+}
+
+template <typename Pred>
+bool WaitFor(Pred pred, double timeout_s) {
+  return WaitFor(pred, timeout_s, [] { return true; });
 }
 
 }  // namespace
@@ -75,7 +100,7 @@ struct mi_exchange {
   int world = 1;
   int64_t slot_bytes = 0;
   uint64_t seq = 0;
-  double timeout_s = 120.0;
+  double timeout_s = 0.0;
   Header* header = nullptr;
   char* slots = nullptr;
   size_t bytes = 0;
@@ -111,7 +136,7 @@ int mi_exchange_open(const char* name, int32_t rank, int32_t world, int64_t slot
       if (fd < 0) return false;
       struct stat st;
       return fstat(fd, &st) == 0 && static_cast<size_t>(st.st_size) >= bytes;
-    }, 120.0);
+    }, EnvSeconds("MILP_EXCHANGE_ATTACH_S", 120.0));
     if (!ok) {
       if (fd >= 0) close(fd);
       return MI_LP_ERROR_STATE;
@@ -128,18 +153,23 @@ int mi_exchange_open(const char* name, int32_t rank, int32_t world, int64_t slot
     h->world = world;
     h->slot_bytes = slot_bytes;
     h->attached.store(0, std::memory_order_relaxed);
-    for (int r = 0; r < kMaxWorld; ++r) h->seq[r].v.store(0, std::memory_order_relaxed);
+    for (int r = 0; r < kMaxWorld; ++r) {
+      h->seq[r].v.store(0, std::memory_order_relaxed);
+      h->pid[r].store(0, std::memory_order_relaxed);
+    }
     h->magic.store(kMagic, std::memory_order_release);
   } else if (!WaitFor([&]() { return h->magic.load(std::memory_order_acquire) == kMagic; },
-                      120.0) ||
+                      EnvSeconds("MILP_EXCHANGE_ATTACH_S", 120.0)) ||
              h->world != world || h->slot_bytes != slot_bytes) {
     munmap(p, bytes);
     return MI_LP_ERROR_INVALID_PROBLEM;
   }
+  h->pid[rank].store(static_cast<int32_t>(getpid()), std::memory_order_release);
   h->attached.fetch_add(1, std::memory_order_acq_rel);
   // Everyone attached: the name can go (nothing is left in /dev/shm if a
   // rank dies later).
-  if (!WaitFor([&]() { return h->attached.load(std::memory_order_acquire) == world; }, 120.0)) {
+  if (!WaitFor([&]() { return h->attached.load(std::memory_order_acquire) == world; },
+               EnvSeconds("MILP_EXCHANGE_ATTACH_S", 120.0))) {
     munmap(p, bytes);
     if (rank == 0) shm_unlink(name);
     return MI_LP_ERROR_STATE;
@@ -156,6 +186,7 @@ int mi_exchange_open(const char* name, int32_t rank, int32_t world, int64_t slot
   x->header = h;
   x->slots = static_cast<char*>(p) + sizeof(Header);
   x->bytes = bytes;
+  x->timeout_s = EnvSeconds("MILP_EXCHANGE_TIMEOUT_S", 0.0);
   *out = x;
   return MI_LP_OK;
 }
@@ -188,7 +219,8 @@ int mi_exchange_allgather(void* ctx, const void* send, int64_t send_bytes, void*
     x->header->seq[x->rank].v.store(s, std::memory_order_release);
     for (int r = 0; r < x->world; ++r) {
       if (!WaitFor([&]() { return x->header->seq[r].v.load(std::memory_order_acquire) >= s; },
-                   x->timeout_s)) {
+                   x->timeout_s,
+                   [&]() { return PeerAlive(x->header->pid[r].load(std::memory_order_acquire)); })) {
         return MI_LP_ERROR_STATE;
       }
     }

@@ -159,8 +159,15 @@ inline int64_t ParallelMinOverride() {
   return e != nullptr ? std::atoll(e) : -1;
 }
 
-template <typename F>
-int ParallelRanges(int64_t n, int64_t min_parallel, int64_t align, F&& fn) {
+// The split of [0, n) ParallelRanges uses: `parts` parts of `per` elements
+// (the last one shorter). Two-pass callers plan once and run both passes on
+// the same plan, whatever MILP_HOST_THREADS reads between them.
+struct RangePlan {
+  int parts = 1;
+  int64_t per = 0;
+};
+
+inline RangePlan PlanRanges(int64_t n, int64_t min_parallel, int64_t align) {
   HostPool& pool = HostPool::Get();
   const int64_t override_min = ParallelMinOverride();
   if (override_min >= 0) min_parallel = override_min;
@@ -168,19 +175,35 @@ int ParallelRanges(int64_t n, int64_t min_parallel, int64_t align, F&& fn) {
   if (const char* cap = std::getenv("MILP_HOST_THREADS")) {  // read per call: probes vary it
     parts = std::max(1, std::min(parts, std::atoi(cap)));
   }
+  RangePlan plan;
   if (parts <= 1) {
+    plan.per = n;
+    return plan;
+  }
+  plan.per = ((n + parts - 1) / parts + align - 1) / align * align;
+  plan.parts = static_cast<int>((n + plan.per - 1) / plan.per);
+  return plan;
+}
+
+template <typename F>
+int RunRanges(const RangePlan& plan, int64_t n, F&& fn) {
+  if (plan.parts <= 1) {
     fn(0, int64_t{0}, n);
     return 1;
   }
-  const int64_t per = ((n + parts - 1) / parts + align - 1) / align * align;
-  parts = static_cast<int>((n + per - 1) / per);
+  const int64_t per = plan.per;
   const std::function<void(int)> job = [&](int p) {
     const int64_t b = p * per;
     const int64_t e = std::min(n, b + per);
     fn(p, b, e);
   };
-  pool.Run(parts, job);
-  return parts;
+  HostPool::Get().Run(plan.parts, job);
+  return plan.parts;
+}
+
+template <typename F>
+int ParallelRanges(int64_t n, int64_t min_parallel, int64_t align, F&& fn) {
+  return RunRanges(PlanRanges(n, min_parallel, align), n, std::forward<F>(fn));
 }
 
 // Appends to *rows the indices r in [begin, n) with v[r] != 0 in increasing
@@ -197,9 +220,9 @@ void ParallelAppendNonZeros(const Real* v, int64_t begin, int64_t n, std::vector
   Real part_max[kMaxParts] = {};
   const int64_t len = n > begin ? n - begin : 0;
   // Pass 1: count (and the largest magnitude) per part; pass 2: each part
-  // writes its entries at its offset. Both passes split [begin, n) the same
-  // way (same length, threshold and alignment).
-  const int parts = ParallelRanges(len, 65536, 64, [&](int p, int64_t b, int64_t e) {
+  // writes its entries at its offset. Both passes run on one plan.
+  const RangePlan plan = PlanRanges(len, 65536, 64);
+  const int parts = RunRanges(plan, len, [&](int p, int64_t b, int64_t e) {
     int64_t c = 0;
     Real m = 0;
     for (int64_t i = begin + b; i < begin + e; ++i) {
@@ -220,7 +243,7 @@ void ParallelAppendNonZeros(const Real* v, int64_t begin, int64_t n, std::vector
   if (vals != nullptr) vals->resize(vbase + static_cast<size_t>(offset[parts]));
   int* out_rows = rows->data() + base;
   Real* out_vals = vals != nullptr ? vals->data() + vbase : nullptr;
-  const int parts2 = ParallelRanges(len, 65536, 64, [&](int p, int64_t b, int64_t e) {
+  RunRanges(plan, len, [&](int p, int64_t b, int64_t e) {
     int64_t at = offset[p];
     for (int64_t i = begin + b; i < begin + e; ++i) {
       if (v[i] != 0.0) {
@@ -230,7 +253,6 @@ void ParallelAppendNonZeros(const Real* v, int64_t begin, int64_t n, std::vector
       }
     }
   });
-  (void)parts2;
   Real m = max_abs != nullptr ? *max_abs : Real(0);
   for (int p = 0; p < parts; ++p) m = std::max(m, part_max[p]);
   if (max_abs != nullptr) *max_abs = m;

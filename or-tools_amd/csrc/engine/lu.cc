@@ -1377,8 +1377,10 @@ bool TriangularMatrix::ParallelTransposeSolve(bool forward, std::vector<Fraction
       // The chains' final-only prefixes (sum = x[c], then the loop's own
       // grouped subtractions up to the split), in parallel; then each column
       // in order continues its chain exactly where the loop would be.
-      par_prefix_.resize(n - tail);
-      Fractional* pre = par_prefix_.data();
+      // Per thread: the solver thread and the tau worker solve concurrently.
+      thread_local std::vector<Fractional> prefix;
+      prefix.resize(n - tail);
+      Fractional* pre = prefix.data();
       ParallelRanges(n - tail, 64, 1, [&](int, int64_t lo, int64_t hi) {
         for (int64_t k = lo; k < hi; ++k) {
           const int c = tail + static_cast<int>(k);

@@ -7,6 +7,7 @@
 #ifndef MILP_LU_H_
 #define MILP_LU_H_
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <cstring>
@@ -579,13 +580,29 @@ class TriangularMatrix : public CompactSparseMatrix {
  private:
   // ParallelTransposeSolve's runs per direction (0 forward, 1 backward):
   // [begin, end) column ranges of the long independent runs, in loop order.
-  mutable bool par_ready_[2] = {false, false};
+  // Built once per factorization under a lock by the first solve that needs
+  // them; read without it by the solver thread and the tau worker, so the
+  // ready flag is an acquire/release atomic (copies start not ready).
+  struct ReadyFlag {
+    std::atomic<bool> v{false};
+    ReadyFlag() = default;
+    ReadyFlag(const ReadyFlag&) {}
+    ReadyFlag& operator=(const ReadyFlag&) {
+      v.store(false, std::memory_order_release);
+      return *this;
+    }
+    ReadyFlag& operator=(bool b) {
+      v.store(b, std::memory_order_release);
+      return *this;
+    }
+    operator bool() const { return v.load(std::memory_order_acquire); }
+  };
+  mutable ReadyFlag par_ready_[2];
   mutable std::vector<int> par_runs_[2];
   // Forward solve's dense tail [par_tail_, n): per column, the end of its
   // leading groups of four that read rows < par_tail_ only (-1: no tail).
   mutable int par_tail_ = -1;
   mutable std::vector<int64_t> par_split_;
-  mutable std::vector<Fractional> par_prefix_;
   mutable std::vector<char> stored_slots_[2];
   std::vector<char> marked_;
   std::vector<int> nodes_to_explore_;

@@ -273,8 +273,10 @@ void DynamicMaximum::BulkAddOrUpdate(const int* pos, const Fractional* value,
   bool has_nan[kMaxParts] = {};
   Fractional* values = values_.data();
   uint64_t* words = is_candidate_.mutable_data();
-  const int parts = ParallelRanges(static_cast<int64_t>(n), 8192, 1,
-                                   [&](int p, int64_t b, int64_t e) {
+  // One plan for both passes (pass 2 indexes pass 1's per-part results).
+  const RangePlan plan = PlanRanges(static_cast<int64_t>(n), 8192, 1);
+  const int parts = RunRanges(plan, static_cast<int64_t>(n),
+                              [&](int p, int64_t b, int64_t e) {
     std::vector<Fractional>& h = tops[p];
     h.clear();
     for (int64_t i = b; i < e; ++i) {
@@ -303,7 +305,7 @@ void DynamicMaximum::BulkAddOrUpdate(const int* pos, const Fractional* value,
       for (const Fractional v : tops[p]) offer(&running, v);
     }
     std::vector<int> found[kMaxParts];
-    ParallelRanges(static_cast<int64_t>(n), 8192, 1, [&](int p, int64_t b, int64_t e) {
+    RunRanges(plan, static_cast<int64_t>(n), [&](int p, int64_t b, int64_t e) {
       std::vector<Fractional> h = incoming[p];
       std::vector<int>& out = found[p];
       out.clear();
@@ -5456,6 +5458,10 @@ Status RevisedSimplex::PrimalPush(TimeLimit* time_limit) {
 #include <mutex>
 #include <thread>
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+
 #include <hip/hip_runtime_api.h>
 
 struct mi_lp {
@@ -5676,6 +5682,47 @@ void mi_glop_params_default(mi_glop_params* p) {
   p->relative_max_cost_perturbation = 1e-7;
   p->initial_condition_number_threshold = 1e50;
   p->crossover_bound_snapping_distance = milp::kInfinity;
+}
+
+// MILP_CRASH_REPORT=1: a SIGSEGV/SIGBUS/SIGABRT handler that prints each
+// frame as library+offset (dladdr), so a crash inside another library's
+// teardown can be attributed, then re-raises with the default action.
+namespace {
+void CrashReport(int sig, siginfo_t* info, void*) {
+  void* frames[48];
+  const int n = backtrace(frames, 48);
+  std::fprintf(stderr, "[mi_lp crash report] signal %d, fault address %p, %d frames\n", sig,
+               info != nullptr ? info->si_addr : nullptr, n);
+  for (int i = 0; i < n; ++i) {
+    Dl_info d{};
+    if (dladdr(frames[i], &d) != 0 && d.dli_fname != nullptr) {
+      std::fprintf(stderr, "  #%02d %p %s+0x%lx (%s)\n", i, frames[i], d.dli_fname,
+                   static_cast<unsigned long>(reinterpret_cast<uintptr_t>(frames[i]) -
+                                              reinterpret_cast<uintptr_t>(d.dli_fbase)),
+                   d.dli_sname != nullptr ? d.dli_sname : "?");
+    } else {
+      std::fprintf(stderr, "  #%02d %p (no mapping)\n", i, frames[i]);
+    }
+  }
+  std::fflush(stderr);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+__attribute__((constructor)) void InstallCrashReport() {
+  const char* e = std::getenv("MILP_CRASH_REPORT");
+  if (e == nullptr || std::atoi(e) == 0) return;
+  struct sigaction sa {};
+  sa.sa_sigaction = CrashReport;
+  sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+  sigemptyset(&sa.sa_mask);
+  for (int sig : {SIGSEGV, SIGBUS, SIGABRT}) sigaction(sig, &sa, nullptr);
+}
+}  // namespace
+
+int mi_lp_shutdown(void) {
+  milp::ShutdownDevices();
+  return MI_LP_OK;
 }
 
 int mi_lp_device_count(void) {

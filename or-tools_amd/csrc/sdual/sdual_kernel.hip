@@ -296,12 +296,38 @@ bool CreateOwnQueueStream(int device, hipStream_t* s) {
 class SdualPool {
  public:
   static SdualPool& Get(int device) {
-    static std::mutex mu;
-    static std::vector<SdualPool*>* all = new std::vector<SdualPool*>();
-    std::lock_guard<std::mutex> lock(mu);
-    if (static_cast<int>(all->size()) <= device) all->resize(device + 1, nullptr);
-    if ((*all)[device] == nullptr) (*all)[device] = new SdualPool(device);
-    return *(*all)[device];
+    std::lock_guard<std::mutex> lock(RegistryMutex());
+    std::vector<SdualPool*>& all = Registry();
+    if (static_cast<int>(all.size()) <= device) all.resize(device + 1, nullptr);
+    if (all[device] == nullptr) {
+      all[device] = new SdualPool(device);
+      RegisterDeviceShutdown();
+    }
+    return *all[device];
+  }
+  // Process teardown (mi_lp_shutdown, or the atexit handler registered with
+  // the first pool): the resident grid drains on the stop word before the HIP
+  // runtime, and any profiler hooked into it, goes away. Waits at most ~10 s.
+  static void ShutdownAll() {
+    std::lock_guard<std::mutex> lock(RegistryMutex());
+    for (SdualPool* p : Registry()) {
+      if (p != nullptr) p->Shutdown();
+    }
+  }
+  void Shutdown() {
+    std::lock_guard<std::mutex> lock(mu_);
+    if (!running_) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device_);
+    __atomic_store_n(&q_->stop, 1, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hipStreamQuery(stream_) == hipErrorNotReady &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10)) {
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    running_ = false;
+    (void)hipSetDevice(prev);
   }
   // Publishes one arena; (re)launches the kernel when it is not running. A
   // full host ring (kCap entries the dispatcher has not copied yet) waits.
@@ -309,9 +335,22 @@ class SdualPool {
     while (true) {
       {
         std::lock_guard<std::mutex> lock(mu_);
+        if (running_ && inflight_ == 0 && launched_groups_ < GroupsFor(lps_) &&
+            hipStreamQuery(stream_) == hipErrorNotReady) {
+          // A grid launched for fewer LPs (a single solve's few dozen
+          // workers) would serve a batch on too few workgroups: stop it (no
+          // entry can be published while mu_ is held, so its dispatcher goes
+          // idle and quits) and relaunch at the batch's size; Launch waits
+          // for the old grid and starts at the first uncopied entry. Only
+          // with no segment in flight: one could wait for a factorization
+          // this thread's fibers would serve.
+          __atomic_store_n(&q_->stop, 1, __ATOMIC_RELEASE);
+          Launch();
+        }
         if (!running_ || hipStreamQuery(stream_) == hipSuccess) Launch();
         const int64_t t = q_->tail;
         if (t - __atomic_load_n(&q_->seen, __ATOMIC_ACQUIRE) < cap_) {
+          ++inflight_;
           __atomic_store_n(&q_->entry[t % cap_], reinterpret_cast<uint64_t>(lp),
                            __ATOMIC_RELEASE);
           __atomic_store_n(&q_->tail, t + 1, __ATOMIC_RELEASE);
@@ -324,6 +363,11 @@ class SdualPool {
         std::this_thread::yield();
       }
     }
+  }
+  // A segment published by Enqueue has completed (its mailbox flag read 3).
+  void Done() {
+    std::lock_guard<std::mutex> lock(mu_);
+    --inflight_;
   }
   int64_t Tail() const { return q_->tail; }
   const int64_t* Dbg() const { return q_->dbg; }
@@ -402,13 +446,24 @@ class SdualPool {
     }
     __atomic_store_n(&q_->stop, 0, __ATOMIC_RELEASE);
     // Outside batch calls (single solves): a few dozen workers.
-    const int groups = std::max(kMinPoolGroups, std::min(kPoolGroups, lps_ + 1));
+    const int groups = GroupsFor(lps_);
+    launched_groups_ = groups;
     hipLaunchKernelGGL(sdual_pool_kernel, dim3(groups), dim3(64), kLdsTotalDoubles * sizeof(double), stream_, d_q_, d_ring_,
                        static_cast<long long>(head_base_), static_cast<long long>(cap_));
     const hipError_t e = hipGetLastError();
     (void)hipSetDevice(prev);
     if (e != hipSuccess) throw DeviceError("sdual pool: launch failed");
     running_ = true;
+  }
+
+  static int GroupsFor(int lps) { return std::max(kMinPoolGroups, std::min(kPoolGroups, lps + 1)); }
+  static std::mutex& RegistryMutex() {
+    static std::mutex* mu = new std::mutex();
+    return *mu;
+  }
+  static std::vector<SdualPool*>& Registry() {
+    static std::vector<SdualPool*>* all = new std::vector<SdualPool*>();
+    return *all;
   }
 
   int device_;
@@ -423,6 +478,8 @@ class SdualPool {
   int64_t cap_ = SdQueue::kCap;
   int users_ = 0;
   int lps_ = 0;
+  int launched_groups_ = 0;
+  int inflight_ = 0;
 };
 }  // namespace
 
@@ -653,10 +710,27 @@ class LuServers {
  public:
   static constexpr int kSlots = 8192;
   static LuServers* Get() {
-    static LuServers* s = new LuServers();  // never destroyed (detached threads)
+    static LuServers* s = [] {
+      LuServers* created = new LuServers();  // never destroyed; threads joined by Shutdown
+      g_instance.store(created, std::memory_order_release);
+      RegisterDeviceShutdown();
+      return created;
+    }();
     return s;
   }
-  bool enabled() const { return threads_ > 0; }
+  // Process teardown: the server threads stop polling the mailboxes (mapped
+  // host memory the HIP runtime frees at exit) and are joined; later
+  // segments are served by their own fibers.
+  static void ShutdownAll() {
+    LuServers* s = g_instance.load(std::memory_order_acquire);
+    if (s == nullptr) return;
+    s->stop_.store(true, std::memory_order_release);
+    for (std::thread& t : s->workers_) {
+      if (t.joinable()) t.join();
+    }
+    s->threads_ = 0;
+  }
+  bool enabled() const { return threads_ > 0 && !stop_.load(std::memory_order_acquire); }
   int Register(int32_t* flag, void (*serve)(void*), void* ctx) {
     std::lock_guard<std::mutex> lock(mu_);
     int slot;
@@ -701,11 +775,11 @@ class LuServers {
     int n = 4;
     if (const char* e = std::getenv("MILP_SDUAL_SERVERS")) n = std::max(0, std::atoi(e));
     threads_ = n;
-    for (int t = 0; t < n; ++t) std::thread([this, t, n] { Loop(t, n); }).detach();
+    for (int t = 0; t < n; ++t) workers_.emplace_back([this, t, n] { Loop(t, n); });
   }
   void Loop(int t, int n) {
     int idle = 0;
-    while (true) {
+    while (!stop_.load(std::memory_order_acquire)) {
       bool served = false;
       const int hi = hi_.load(std::memory_order_acquire);
       for (int i = t; i < hi; i += n) {
@@ -730,13 +804,23 @@ class LuServers {
       }
     }
   }
+  static std::atomic<LuServers*> g_instance;
   int threads_ = 0;
+  std::atomic<bool> stop_{false};
+  std::vector<std::thread> workers_;
   std::mutex mu_;
   std::vector<int> free_;
   int used_ = 0;
   std::atomic<int> hi_{0};
   Slot slots_[kSlots];
 };
+
+std::atomic<LuServers*> LuServers::g_instance{nullptr};
+
+void SdualShutdown() {
+  LuServers::ShutdownAll();
+  SdualPool::ShutdownAll();
+}
 
 // The same segment through the device's persistent pool kernel: a resident
 // workgroup moves the staging image in and out itself (no stream work, so
@@ -802,6 +886,7 @@ void DeviceLp::SdualRunPooled(size_t bytes, const double* arena_coeff, int n,
       }
     }
     if (f == 3) {
+      pool.Done();
       if (prof) {
         gaps.last_ns += gap_ns;
         ++gaps.segments;

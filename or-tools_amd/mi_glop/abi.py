@@ -158,7 +158,7 @@ KERNEL_NAMES = ["pricing", "update_row", "primal_norms", "rc_update", "tri_solve
 
 # Names of every exported entry point of include/mi_lp.h (checked by tests).
 EXPORTED_SYMBOLS = [
-    "mi_glop_params_default", "mi_lp_device_count", "mi_lp_create",
+    "mi_glop_params_default", "mi_lp_device_count", "mi_lp_shutdown", "mi_lp_create",
     "mi_lp_destroy", "mi_lp_last_error", "mi_lp_set_params", "mi_lp_load",
     "mi_lp_load_basis_state", "mi_lp_clear_basis_state",
     "mi_lp_notify_matrix_unchanged", "mi_lp_solve", "mi_lp_get_primal",

@@ -42,6 +42,12 @@ def lib():
     vp = ctypes.c_void_p
     L.mi_glop_params_default.argtypes = [ctypes.POINTER(abi.MiGlopParams)]
     L.mi_lp_device_count.restype = ctypes.c_int
+    L.mi_lp_shutdown.restype = ctypes.c_int
+    # Drain the engine's resident grids and join its service threads while
+    # the HIP runtime is still up: Python's atexit runs before the C exit
+    # handlers (the runtime's and a profiler's own teardown).
+    import atexit
+    atexit.register(L.mi_lp_shutdown)
     L.mi_lp_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.mi_lp_destroy.argtypes = [vp]
     L.mi_lp_last_error.argtypes = [vp]
@@ -428,14 +434,33 @@ class LpHandle:
         return starts, cols[:nnz.value], vals[:nnz.value]
 
 
-def batch_solve(handles, num_threads=4):
-    """Solves already-loaded handles concurrently (mi_lp_batch_solve)."""
+def batch_solve(handles, num_threads=4, progress=None, progress_s=15.0):
+    """Solves already-loaded handles concurrently (mi_lp_batch_solve).
+
+    progress: optional callable(done_indices, elapsed_s), called every
+    progress_s seconds while the batch runs and once at the end with the
+    indices whose results have landed (each result is written when its LP
+    finishes; unfinished ones keep the -1 iteration sentinel)."""
     L = lib()
     for h in handles:
         h._push_params()
     arr = (ctypes.c_void_p * len(handles))(*[h.h.value for h in handles])
     res = (abi.MiLpResult * len(handles))()
-    L.mi_lp_batch_solve(arr, len(handles), num_threads, res)
+    if progress is None:
+        L.mi_lp_batch_solve(arr, len(handles), num_threads, res)
+        return list(res)
+    import threading
+    import time
+    for r in res:
+        r.iterations = -1
+    t0 = time.perf_counter()
+    th = threading.Thread(target=L.mi_lp_batch_solve,
+                          args=(arr, len(handles), num_threads, res), daemon=True)
+    th.start()
+    while th.is_alive():
+        th.join(progress_s)
+        progress([i for i, r in enumerate(res) if r.iterations >= 0],
+                 time.perf_counter() - t0)
     return list(res)
 
 

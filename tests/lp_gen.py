@@ -27,6 +27,13 @@ def random_sparse_lp(m, n, density, seed, eq_frac=0.2, free_frac=0.05,
     cs = np.asarray(starts, np.int64)
     ri = np.asarray(rows, np.int32)
     va = np.asarray(vals, np.float64)
+    return _mixed_bounds_lp(rng, m, n, cs, ri, va, eq_frac, free_frac, boxed_frac, maximize,
+                            f"sparse_{m}x{n}_s{seed}")
+
+
+def _mixed_bounds_lp(rng, m, n, cs, ri, va, eq_frac, free_frac, boxed_frac, maximize, name):
+    """Row/column bounds and costs of random_sparse_lp around a feasible
+    point x0 (every bound type of lp_types.h), for the CSC (cs, ri, va)."""
     x0 = rng.uniform(0.0, 1.0, size=n)
     ax = np.zeros(m)
     for c in range(n):
@@ -56,7 +63,41 @@ def random_sparse_lp(m, n, density, seed, eq_frac=0.2, free_frac=0.05,
     col_ub[unb] = 10.0 + rng.uniform(0, 5, size=unb.sum())
     col_lb[free] = -10.0 - rng.uniform(0, 5, size=free.sum())
     return LinearProgram(m, n, cs, ri, va, col_lb, col_ub, row_lb, row_ub, obj,
-                         0.0, 1.0, maximize, f"sparse_{m}x{n}_s{seed}")
+                         0.0, 1.0, maximize, name)
+
+
+def staircase_lp(m, n, seed, block_rows=50, link_frac=0.2, eq_frac=0.1, free_frac=0.05,
+                 boxed_frac=0.5, maximize=False):
+    """Multi-period ("staircase") LP, the shape of Netlib's large models
+    (scfxm, sctap, stocfor, pilot families): the rows form periods of about
+    `block_rows` rows, each column has 2-7 non-zeros in its own period and,
+    with probability `link_frac`, one in the next period (the carry-over of
+    a multi-period model). The basis then factors with fill limited to the
+    periods, as on the real models, instead of the dense fill of a uniformly
+    random matrix. Bounds, row types and costs as in random_sparse_lp."""
+    rng = np.random.default_rng(seed)
+    periods = max(1, m // block_rows)
+    edges = np.linspace(0, m, periods + 1).astype(np.int64)
+    col_period = np.sort(rng.integers(0, periods, size=n))
+    starts = [0]
+    rows, vals = [], []
+    for c in range(n):
+        t = col_period[c]
+        lo, hi = edges[t], edges[t + 1]
+        k = int(min(hi - lo, rng.integers(2, 8)))
+        r = rng.choice(np.arange(lo, hi), size=k, replace=False)
+        if t + 1 < periods and rng.uniform() < link_frac:
+            r = np.append(r, rng.integers(edges[t + 1], edges[t + 2]))
+        r = np.sort(r)
+        v = rng.uniform(0.1, 1.0, size=r.size) * rng.choice([-1.0, 1.0], size=r.size)
+        rows.extend(r.tolist())
+        vals.extend(v.tolist())
+        starts.append(len(rows))
+    cs = np.asarray(starts, np.int64)
+    ri = np.asarray(rows, np.int32)
+    va = np.asarray(vals, np.float64)
+    return _mixed_bounds_lp(rng, m, n, cs, ri, va, eq_frac, free_frac, boxed_frac, maximize,
+                            f"staircase_{m}x{n}_s{seed}")
 
 
 def fixed_order_matvec(At, x):

@@ -11,8 +11,9 @@ values). The windows cover the iterations bench.py times:
     against the live oracle, and the ends of both timed windows (iterations
     67 and 1564) against the oracle's digests in tests/golden/c2_windows.json
     (the oracle needs ~0.5 s per iteration here);
-  * config 3: eleven members of the Netlib-shaped suite solved to the end,
-    the largest included.
+  * config 3: eleven members of the m <= 1000 suite solved to the end, and
+    bench.py's suite itself (m from 27 to 16 000): its two
+    largest members one by one and a third of it through the batch API.
 """
 import pytest
 
@@ -127,3 +128,50 @@ def test_config3_batched_suite_parity():
         o.load(lps[i])
         ro = o.solve()
         parity_util.compare(o, ro, handles[k], res[k], lps[i])
+
+
+C3_MAX_ROWS = 16000  # bench.py's --c3-max-rows default
+
+
+def _c3_big(indices):
+    shapes = netlib_suite.suite_shapes(max_rows=C3_MAX_ROWS)
+    return [(i, netlib_suite.member(*shapes[i])) for i in indices]
+
+
+@pytest.mark.parametrize("index", [92, 93])
+def test_config3_largest_members_parity(index):
+    """The two largest members of the config-3 suite bench.py times
+    (14 938 and 16 000 rows, staircase LPs), solved to the end by one
+    handle, against the oracle bit for bit."""
+    (_, lp), = _c3_big([index])
+    assert lp.m >= 14000
+    o, ro, g, rg = parity_util.solve_both(lp, abi.default_params(), _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    assert ro.problem_status == abi.OPTIMAL
+
+
+def test_config3_fullsize_batched_parity():
+    """bench.py's config-3 path at full size: every third member of the
+    16 000-row suite plus the largest, through mi_lp_batch_solve (fibers,
+    batched launches, LPT order) on 16 threads, each LP against the oracle
+    bit for bit."""
+    import concurrent.futures
+    picks = sorted(set(range(1, 94, 3)) | {93})
+    members = _c3_big(picks)
+    handles = []
+    for _, lp in members:
+        h = engine.LpHandle(abi.default_params())
+        h.load(lp)
+        handles.append(h)
+    res = engine.batch_solve(handles, num_threads=16)
+
+    def oracle(lp):
+        o = oracle_lib.OracleLp(abi.default_params())
+        o.load(lp)
+        return o, o.solve()
+
+    with concurrent.futures.ThreadPoolExecutor(8) as ex:
+        refs = list(ex.map(oracle, [lp for _, lp in members]))
+    for k, (i, lp) in enumerate(members):
+        o, ro = refs[k]
+        parity_util.compare(o, ro, handles[k], res[k], lp)
