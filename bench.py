@@ -763,6 +763,7 @@ def main():
         "device_call_ms_per_step": c5["device_call_ms_per_step"],
         "window": c5["window"],
         "cpu_baseline": c5.get("cpu_baseline"),
+        "oracle_check": c5.get("oracle_check"),
         "amortized": c5.get("amortized"),
         "exchange": c5.get("exchange"),
         "c2": c2,

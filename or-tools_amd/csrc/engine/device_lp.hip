@@ -290,6 +290,7 @@ class SmallBatcher {
       ++num_pending_;
       if (!launcher_.joinable()) {  // stopped by ShutdownAll: start again
         stop_ = false;
+        CreateStreams();
         launcher_ = std::thread([this] { LauncherLoop(); });
       }
     }
@@ -305,9 +306,23 @@ class SmallBatcher {
     }
     cv_.notify_one();
     if (launcher_.joinable()) launcher_.join();
+    for (hipStream_t& st : streams_) {
+      if (st != nullptr) (void)hipStreamDestroy(st);
+      st = nullptr;
+    }
   }
 
  private:
+  void CreateStreams() {
+    (void)hipSetDevice(device_);
+    for (int i = 0; i < kStreams; ++i) {
+      hipStream_t st;
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        throw DeviceError("small batch: stream");
+      }
+      streams_[i] = st;
+    }
+  }
   static std::mutex& RegistryMutex() {
     static std::mutex* mu = new std::mutex();
     return *mu;
@@ -355,14 +370,7 @@ class SmallBatcher {
 
  private:
   explicit SmallBatcher(int device) : device_(device) {
-    (void)hipSetDevice(device);
-    for (int i = 0; i < kStreams; ++i) {
-      hipStream_t s;
-      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
-        throw DeviceError("small batch: stream");
-      }
-      streams_[i] = s;
-    }
+    CreateStreams();
     void* p = nullptr;
     void* d = nullptr;
     if (hipHostMalloc(&p, sizeof(milp_kernels::SmallSlot) * kMaxSlots, hipHostMallocMapped) !=

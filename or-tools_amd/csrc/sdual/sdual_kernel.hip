@@ -327,6 +327,12 @@ class SdualPool {
       std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
     running_ = false;
+    // The CU-masked queue goes too: left to the runtime's exit-time teardown,
+    // a profiler's own teardown (rocprofiler-sdk's static destructors) later
+    // calls into HSA on it and faults (symbolized with MILP_CRASH_REPORT,
+    // profiles/r05_pmc). Launch creates a new one when needed.
+    (void)hipStreamDestroy(stream_);
+    stream_ = nullptr;
     (void)hipSetDevice(prev);
   }
   // Publishes one arena; (re)launches the kernel when it is not running. A
@@ -433,6 +439,10 @@ class SdualPool {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(device_);
     if (running_) (void)hipStreamSynchronize(stream_);
+    if (stream_ == nullptr && !CreateOwnQueueStream(device_, &stream_)) {
+      (void)hipSetDevice(prev);
+      throw DeviceError("sdual pool: stream");
+    }
     head_base_ = __atomic_load_n(&q_->seen, __ATOMIC_ACQUIRE);
     // The grid claims queue indices from head_base_ on (a synchronous copy:
     // the launch below must see it).

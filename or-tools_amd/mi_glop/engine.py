@@ -439,8 +439,8 @@ def batch_solve(handles, num_threads=4, progress=None, progress_s=15.0):
 
     progress: optional callable(done_indices, elapsed_s), called every
     progress_s seconds while the batch runs and once at the end with the
-    indices whose results have landed (each result is written when its LP
-    finishes; unfinished ones keep the -1 iteration sentinel)."""
+    indices whose results have landed (a finished solve writes its positive
+    solve_seconds or an error code; the entry is zeroed when it starts)."""
     L = lib()
     for h in handles:
         h._push_params()
@@ -451,15 +451,13 @@ def batch_solve(handles, num_threads=4, progress=None, progress_s=15.0):
         return list(res)
     import threading
     import time
-    for r in res:
-        r.iterations = -1
     t0 = time.perf_counter()
     th = threading.Thread(target=L.mi_lp_batch_solve,
                           args=(arr, len(handles), num_threads, res), daemon=True)
     th.start()
     while th.is_alive():
         th.join(progress_s)
-        progress([i for i, r in enumerate(res) if r.iterations >= 0],
+        progress([i for i, r in enumerate(res) if r.solve_seconds > 0 or r.error_code != 0],
                  time.perf_counter() - t0)
     return list(res)
 

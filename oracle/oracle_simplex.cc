@@ -2050,6 +2050,8 @@ class RevisedSimplex {
   }
   const std::vector<VariableStatus>& GetState() const { return solution_state_; }
   int GetBasis(int row) const { return basis_[row]; }
+  // revised_simplex.h GetBasisFactorization (test analysis of the factors).
+  const BasisFactorization& GetBasisFactorization() const { return basis_factorization_; }
   const std::vector<Fractional>& GetPrimalRay() const { return solution_primal_ray_; }
   const std::vector<Fractional>& GetDualRay() const { return solution_dual_ray_; }
   const std::vector<Fractional>& GetDualRayRowCombination() const {
@@ -4261,6 +4263,32 @@ int oracle_lp_get_basis(void* hv, int32_t* b) {
   for (int r = 0; r < h->lp.m; ++r) b[r] = h->simplex.GetBasis(r);
   return 0;
 }
+// Test analysis only: the current LU's U factor (CSC, diagonal apart) and
+// row permutation. Call with null arrays for the sizes (sizes[0] = columns,
+// sizes[1] = entries), then with arrays of those sizes.
+int oracle_lp_debug_upper(void* hv, int64_t* sizes, int64_t* starts, int32_t* rows, double* vals,
+                          double* diag) {
+  auto* h = static_cast<OracleHandle*>(hv);
+  const auto& u = h->simplex.GetBasisFactorization().lu().upper();
+  const int n = u.num_cols();
+  sizes[0] = n;
+  sizes[1] = u.num_entries() - n;
+  if (starts == nullptr) return 0;
+  int64_t at = 0;
+  for (int c = 0; c < n; ++c) {
+    starts[c] = at;
+    const auto col = u.column(c);
+    for (int64_t i = 0; i < col.n; ++i) {
+      rows[at] = col.rows[i];
+      vals[at] = col.coefs[i];
+      ++at;
+    }
+    diag[c] = u.GetDiagonalCoefficient(c);
+  }
+  starts[n] = at;
+  return 0;
+}
+
 int oracle_lp_get_state(void* hv, int8_t* st) {
   auto* h = static_cast<OracleHandle*>(hv);
   const auto& s = h->simplex.GetState();
