@@ -597,10 +597,13 @@ class DeviceLp : public DeviceSolver {
   bool tri_btran_ = false;    // MILP_TRI_BTRAN=1: the other dense loops (BTRAN, UpperSolve) too
   bool tri_pair_ = false;     // MILP_TRI_PAIR=1: direction and tau U solves in one launch
   int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
-  // MILP_TRI_CHAIN=0: no single-workgroup segments; a narrow segment is a
-  // run of at least MILP_TRI_CHAIN_MIN_LEVELS levels of at most
-  // MILP_TRI_CHAIN_WIDTH outputs each (tri_chain_kernel).
-  bool tri_chain_ = true;
+  // MILP_TRI_CHAIN=1: single-workgroup segments; a narrow segment is a run
+  // of at least MILP_TRI_CHAIN_MIN_LEVELS levels of at most
+  // MILP_TRI_CHAIN_WIDTH outputs each (tri_chain_kernel). Off by default
+  // since round 5: with the sync-free stores kept inside the wait loop one
+  // chip-wide launch is faster (config-5 window 668 -> 713 it/s,
+  // profiles/r05_tri).
+  bool tri_chain_ = false;
   int tri_chain_width_ = 512;
   int tri_chain_min_levels_ = 4;
   uint64_t* d_tri_clock_ = nullptr;

@@ -451,25 +451,41 @@ __device__ __forceinline__ double tri_apply4(const TriSolveArgs& a, double sum, 
 }
 
 // Output k of the sync-free solve: wait for its entries, compute, store.
+//
+// The wait loop's exit is wave-uniform (`__ballot` over the lanes still
+// waiting): a lane that finishes stores inside the loop body, the same pass.
+// With a per-lane exit the compiler sinks the division and the stores below
+// the loop, so a wave published its 64 outputs only when its slowest lane was
+// done: every level paid the wave's slowest input, not each output's own.
 __device__ __forceinline__ void tri_syncfree_output(const TriSolveArgs& a, int k, int top) {
   TriRec r;
   tri_load(a, k, a.num_work, top, &r);
-  if (r.row > top) return;  // not computed: y[k] already holds x[row]
+  bool done = r.row > top;  // not computed: y[k] already holds x[row]
   double* y = a.y;
-  const double in = a.x[r.row];
-  bool done = false;
+  const double in = done ? 0.0 : a.x[r.row];
   int backoff = 1;
   const uint64_t t0 = wall_clock64();  // 100 MHz
-  if (r.n <= 4) {
-    // One poll round loads the entries still pending at once and keeps them:
-    // the values that end the wait are the ones the output is computed from
-    // (a hop is one round trip, not a readiness walk plus a reload), and a
-    // final value is never loaded twice.
-    const int n = r.n;
-    const double pend = __longlong_as_double(static_cast<long long>(kTriPending));
-    double y0 = n > 0 ? pend : 0.0, y1 = n > 1 ? pend : 0.0;
-    double y2 = n > 2 ? pend : 0.0, y3 = n > 3 ? pend : 0.0;
-    while (!done) {
+  const double pend = __longlong_as_double(static_cast<long long>(kTriPending));
+  // n <= 4: one poll round loads the entries still pending at once and keeps
+  // them: the values that end the wait are the ones the output is computed
+  // from (a hop is one round trip, not a readiness walk plus a reload), and a
+  // final value is never loaded twice.
+  const int n = r.n;
+  double y0 = n > 0 ? pend : 0.0, y1 = n > 1 ? pend : 0.0;
+  double y2 = n > 2 ? pend : 0.0, y3 = n > 3 ? pend : 0.0;
+  // n > 4: the output folds its entries in evaluation order as they become
+  // final (the same operations as subtract_overflow / subtract_sequential,
+  // so the same bits): by the time its last input arrives only the groups
+  // after the last stall are left, and a deep chain of long outputs advances
+  // by one group fold per hop instead of one whole sum. The wait bound
+  // restarts on progress (a stall detector, not a budget for the chain).
+  double sum = in;
+  int e = r.e.x;
+  const int end = r.e.x + r.n;
+  uint64_t t_progress = t0;
+  while (__ballot(!done) != 0) {
+    if (done) continue;
+    if (n <= 4) {
       if (tri_pending(y0)) y0 = load_final(y, r.e.x);
       if (tri_pending(y1)) y1 = load_final(y, r.e.y);
       if (tri_pending(y2)) y2 = load_final(y, r.e.z);
@@ -488,20 +504,8 @@ __device__ __forceinline__ void tri_syncfree_output(const TriSolveArgs& a, int k
       } else {
         tri_backoff(a, &backoff);
       }
+      continue;
     }
-    return;
-  }
-  // A long output folds its entries in evaluation order as they become final
-  // (the same operations as subtract_overflow / subtract_sequential, so the
-  // same bits): by the time its last input arrives only the groups after the
-  // last stall are left, and a deep chain of long outputs advances by one
-  // group fold per hop instead of one whole sum. The wait bound restarts on
-  // progress (a stall detector, not a budget for the whole chain).
-  double sum = in;
-  int e = r.e.x;
-  const int end = r.e.x + r.n;
-  uint64_t t_progress = t0;
-  while (!done) {
     const int e0 = e;
     while (e < end) {
       // Up to 8 values per round, their loads in flight together.

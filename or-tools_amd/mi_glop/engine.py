@@ -47,7 +47,7 @@ def lib():
     # the HIP runtime is still up: Python's atexit runs before the C exit
     # handlers (the runtime's and a profiler's own teardown).
     import atexit
-    atexit.register(L.mi_lp_shutdown)
+    atexit.register(_shutdown, L)
     L.mi_lp_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.mi_lp_destroy.argtypes = [vp]
     L.mi_lp_last_error.argtypes = [vp]
@@ -106,6 +106,22 @@ def lib():
         ctypes.POINTER(abi.MiLpResult)] + [vp] * 6
     _lib = L
     return L
+
+
+_open_handles = None  # weakref.WeakSet of LpHandle, created with the first
+
+
+def _shutdown(L):
+    """Python exit: destroy the handles still open (their streams and device
+    memory) and then the engine's shared device objects, before the HIP
+    runtime and any profiler attached to it tear down."""
+    if _open_handles is not None:
+        for h in list(_open_handles):
+            try:
+                h.close()
+            except Exception:  # noqa: BLE001 (exit path)
+                pass
+    L.mi_lp_shutdown()
 
 
 def device_count():
@@ -191,6 +207,11 @@ class LpHandle:
         self.h = h
         self.params = params or abi.default_params()
         self.lp = None
+        global _open_handles
+        if _open_handles is None:
+            import weakref
+            _open_handles = weakref.WeakSet()
+        _open_handles.add(self)
 
     def close(self):
         if getattr(self, "h", None):

@@ -71,7 +71,13 @@ __device__ __forceinline__ void output(const Sched& s, int k) {
   int e = e0;
   int backoff = 1;
   uint64_t t_prog = wall_clock64();
-  while (true) {
+  // The loop's exit is wave-uniform (every lane stays until all are done):
+  // the store of a finished lane then sits inside the loop body and cannot be
+  // sunk below the loop, where a waiting lane of the same wave would never
+  // let the wave reach it.
+  bool done = false;
+  while (__ballot(!done) != 0) {
+    if (done) continue;
     const int before = e;
     while (e < end) {
       double v[8];
@@ -113,14 +119,15 @@ __device__ __forceinline__ void output(const Sched& s, int k) {
     }
     if (e == end) {
       st(s.y + k, sum / d);
-      return;
+      done = true;
+      continue;
     }
     if (e != before) {
       t_prog = wall_clock64();
       backoff = 1;
     } else if (wall_clock64() - t_prog > kMaxWait) {
       atomicExch(s.fail, 1);
-      return;
+      done = true;
     } else {
       for (int i = 0; i < backoff; ++i) __builtin_amdgcn_s_sleep(1);
       backoff = min(backoff * 2, s.poll_max);
@@ -141,7 +148,14 @@ __global__ __launch_bounds__(256) void stride_kernel(Sched s, int xcd) {
   if (blockIdx.x % xcd != 0) return;
   const int g = blockIdx.x / xcd;
   const int T = (gridDim.x / xcd) * blockDim.x;
-  for (int k = s.l0_end + g * blockDim.x + threadIdx.x; k < s.num_pos; k += T) output(s, k);
+  // Every lane of a wave holds positions of the same round: the for loop's
+  // trip count is wave-uniform up to the last round, where output() keeps
+  // the exit uniform itself.
+  for (int k0 = s.l0_end + g * blockDim.x; k0 < s.num_pos; k0 += T) {
+    const int k = k0 + threadIdx.x;
+    if (__ballot(k < s.num_pos) == 0) break;
+    if (k < s.num_pos) output(s, k);
+  }
 }
 
 // A: over a position range [lo, hi) only (the wide levels).
@@ -228,8 +242,10 @@ __global__ __launch_bounds__(kE) void chain_lds_kernel(Sched s, int lo, int hi) 
   }
   uint64_t t_prog = wall_clock64();
   // One loop body polls, folds and stores, so a lane whose output another
-  // lane of its wave waits for stores before the wave polls again.
-  while (active) {
+  // lane of its wave waits for stores before the wave polls again; the loop
+  // exit is wave-uniform so that no store can be sunk below it.
+  while (__ballot(active) != 0) {
+    if (!active) continue;
     const int n = cur.n;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -463,6 +479,11 @@ int main(int argc, char** argv) {
     launch();
     CHECK(hipStreamSynchronize(st));
     const bool ok = check(name);
+    if (!ok && std::strcmp(name, "init only") != 0) {
+      std::printf("%-40s WRONG (not timed)\n", name);
+      CHECK(hipMemset(s.fail, 0, 4));
+      return;
+    }
     CHECK(hipEventRecord(e0, st));
     for (int r = 0; r < reps; ++r) {
       init_kernel<<<init_blocks, 256, 0, st>>>(s);
