@@ -165,7 +165,10 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     setup = time.perf_counter() - t
     log(f"c5: solve ran to iteration {start} in {setup:.1f}s (untimed)")
     h.reset_kernel_stats()
-    h.set_kernel_timing(True)
+    # HIP events bracket the dominant kernels only (two event records per
+    # launch of every other kernel cost ~9 % of the window, profiles/r05_tri).
+    timed = None if args.c5_timed_kernels == "all" else args.c5_timed_kernels.split(",")
+    h.set_kernel_timing(True, kernels=timed)
     before = h.run_counters()
     barrier()
     sync()
@@ -235,6 +238,7 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
         "window": window,
         "amortized": amortized,
         "split": split,
+        "event_timed_kernels": timed or "all",
     }
     if split:
         ex = stats.get("exchange", {})
@@ -629,6 +633,9 @@ def main():
     ap.add_argument("--c5-amortized", type=int, default=1000,
                     help="config-5 iterations of the refactorization-amortized window "
                          "(starts with the headline window)")
+    ap.add_argument("--c5-timed-kernels", default="tri_solve,tri_solve_tau",
+                    help="kernel ids bracketed with HIP events in the config-5 windows "
+                         "(comma-separated, or 'all')")
     ap.add_argument("--c5-transport", default="shm", choices=["shm", "gloo"],
                     help="N > 1: the split's join transport (C++ shared memory, or gloo)")
     ap.add_argument("--c5-replicas", action="store_true",
@@ -759,6 +766,7 @@ def main():
         },
         "roofline": c5["roofline"],
         "kernels": c5["kernels"],
+        "event_timed_kernels": c5["event_timed_kernels"],
         "host_ms_per_step": c5["host_ms_per_step"],
         "device_call_ms_per_step": c5["device_call_ms_per_step"],
         "window": c5["window"],

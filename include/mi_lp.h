@@ -292,6 +292,10 @@ int mi_lp_reset_kernel_stats(mi_lp* h);
  * read back when the stats are collected (or every 512 launches): timing adds
  * no synchronization to the iteration it measures. */
 int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable);
+/* The same for the kernel ids whose bits are set in id_mask (bit k = id k of
+ * mi_lp_kernel_stats; 0 = off): a benchmark times its dominant kernel
+ * without paying two event records on every other launch. */
+int mi_lp_set_kernel_timing_ids(mi_lp* h, uint32_t id_mask);
 
 /* Window statistics for the benchmark harness (the reference keeps the same
  * numbers in RevisedSimplex's stats, revised_simplex.h:717-760, and

@@ -192,7 +192,8 @@ class DeviceLp : public DeviceSolver {
                  std::vector<double>* x1) override;
 
   // Accounting (roofline): launches, algorithmic bytes, HIP-event time.
-  void SetTiming(bool on);
+  void SetTiming(bool on, uint32_t id_mask = ~0u);
+  bool Timed(int id) const { return timing_ && (timing_ids_ >> (id & 31) & 1u) != 0; }
   const mi_lp_kernel_stats& stats();  // collects the pending event timings
   void ResetStats();
   void Synchronize();
@@ -384,6 +385,7 @@ class DeviceLp : public DeviceSolver {
   void* ev_start_ = nullptr;
   void* ev_stop_ = nullptr;
   bool timing_ = false;
+  uint32_t timing_ids_ = ~0u;  // kernel ids bracketed with events while timing_
   struct PendingTiming {
     void* start;  // hipEvent_t
     void* stop;
@@ -595,7 +597,12 @@ class DeviceLp : public DeviceSolver {
   // parallel non-zero appends), config 5's window runs 3 % faster without the
   // device BTRAN loops and 5 % faster without either (scripts/gpu_r04_ab2.sh).
   bool tri_btran_ = false;    // MILP_TRI_BTRAN=1: the other dense loops (BTRAN, UpperSolve) too
-  bool tri_pair_ = false;     // MILP_TRI_PAIR=1: direction and tau U solves in one launch
+  bool tri_pair_ = false;
+  // MILP_TRI_PAD=1: every chip-wide level starts on a wave boundary (empty
+  // padding records). Needed while the sync-free stores sat below the wait
+  // loop (a wave holding an output and its reader deadlocked); since the
+  // loop exit is wave-uniform a reader may share its producer's wave.
+  bool tri_pad_ = false;     // MILP_TRI_PAIR=1: direction and tau U solves in one launch
   int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
   // MILP_TRI_CHAIN=1: single-workgroup segments; a narrow segment is a run
   // of at least MILP_TRI_CHAIN_MIN_LEVELS levels of at most

@@ -160,6 +160,7 @@ void DeviceLp::Init(int device) {
   if (const char* v = std::getenv("MILP_TRI_LOWER")) tri_lower_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_BTRAN")) tri_btran_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_PAIR")) tri_pair_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_TRI_PAD")) tri_pad_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_MIN_WIDTH")) tri_min_width_ = std::atoi(v);
   if (const char* v = std::getenv("MILP_TRI_CHAIN")) tri_chain_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_CHAIN_WIDTH")) tri_chain_width_ = std::atoi(v);
@@ -603,7 +604,7 @@ void DeviceLp::BeginKernel(int id) {
                                        "?", "?", "?", "?"};
   DeviceOp(kNames[id & 15]);
   if (batch_pending_) WaitSmallBatch();  // kernels after a batched request see its results
-  if (!timing_) return;
+  if (!Timed(id)) return;
   if (ev_open_ == nullptr) ev_open_ = TakeEvent();
   Check(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_open_), S(stream_)), "ev");
 }
@@ -612,7 +613,7 @@ void DeviceLp::EndKernel(int id, double bytes, bool count_launch) {
   Check(hipGetLastError(), "kernel launch");
   if (count_launch) stats_.launches[id] += 1;
   stats_.algorithmic_bytes[id] += bytes;
-  if (timing_ && ev_open_ != nullptr) {
+  if (Timed(id) && ev_open_ != nullptr) {
     void* stop = TakeEvent();
     Check(hipEventRecord(reinterpret_cast<hipEvent_t>(stop), S(stream_)), "ev");
     ev_pending_.push_back(PendingTiming{ev_open_, stop, id});

@@ -221,10 +221,14 @@ uint64_t DeviceLp::list_epoch() const {
   return e;
 }
 
-void DeviceLp::SetTiming(bool on) {
+void DeviceLp::SetTiming(bool on, uint32_t id_mask) {
   timing_ = on;
+  timing_ids_ = id_mask;
   for (auto& d : shards_) {
-    if (d) d->timing_ = on;
+    if (d) {
+      d->timing_ = on;
+      d->timing_ids_ = id_mask;
+    }
   }
 }
 

@@ -127,9 +127,10 @@ void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, cons
   } else {
     for (int c = fni; c < nc; ++c) visit(c);
   }
-  // Counting sort by level. Each level starts on a wave boundary (empty
-  // padding records fill the gap): a wave of the sync-free kernel then never
-  // holds both an output and one of its readers.
+  // Counting sort by level. With MILP_TRI_PAD each chip-wide level starts on
+  // a wave boundary (empty padding records fill the gap), so that a wave of
+  // the sync-free kernel never holds both an output and one of its readers;
+  // the level plan's kernels always pad.
   std::vector<int32_t> level_count(depth + 1, 0);
   for (int c = fni; c < nc; ++c) {
     if (level[c] > 0 || !ones) ++level_count[level[c]];
@@ -174,8 +175,8 @@ void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, cons
   }
   std::vector<int32_t> level_start(depth + 2, 0);
   for (int l = 0; l <= depth; ++l) {
-    level_start[l + 1] =
-        level_start[l] + (narrow[l] ? level_count[l] : (level_count[l] + 63) / 64 * 64);
+    const bool pad = !narrow[l] && (tri_pad_ || !tri_syncfree_);
+    level_start[l + 1] = level_start[l] + (pad ? (level_count[l] + 63) / 64 * 64 : level_count[l]);
   }
   s->runs.clear();
   s->max_wide_run = 0;
@@ -765,7 +766,7 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
     TriCopyIn(s, c);
     if (slot == 0) {
       BeginKernel(id);  // events around the graph: the kernels only
-    } else if (timing_) {
+    } else if (Timed(id)) {
       Check(hipEventRecord(reinterpret_cast<hipEvent_t>(c.ev[0]), Stream(c.stream)), "ev");
     }
     if (tri_graph_) {
@@ -777,7 +778,7 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
     }
     if (slot == 0) {
       EndKernel(id, bytes);
-    } else if (timing_) {
+    } else if (Timed(id)) {
       Check(hipEventRecord(reinterpret_cast<hipEvent_t>(c.ev[1]), Stream(c.stream)), "ev");
     }
     TriCopyOut(s, c);
@@ -789,7 +790,7 @@ bool DeviceLp::TriSolve(int which, const TriangularMatrix& t, uint64_t key,
       // The worker's own counters (its id is written by this thread only).
       stats_.launches[id] += 1;
       stats_.algorithmic_bytes[id] += bytes;
-      if (timing_) {
+      if (Timed(id)) {
         float ms = 0.0f;
         Check(hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(c.ev[0]),
                                   reinterpret_cast<hipEvent_t>(c.ev[1])),

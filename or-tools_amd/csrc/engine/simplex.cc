@@ -5722,6 +5722,27 @@ __attribute__((constructor)) void InstallCrashReport() {
 
 int mi_lp_shutdown(void) {
   milp::ShutdownDevices();
+  // MILP_DEVICE_RESET_AT_EXIT=1 (profiling runs only): release every HIP
+  // resource of every device through the runtime, so that a profiler's own
+  // exit-time teardown finds nothing left to release. Under rocprofv3 --pmc
+  // a run that executed the device dual segments otherwise ends in a SIGSEGV
+  // inside rocprofiler-sdk's static destructors (calling into HSA) after the
+  // counters are written (scripts/pmc_teardown_probe.py bisects it: a torch
+  // kernel, a single engine solve, a batch with MILP_SDUAL=off and a
+  // scratch-using kernel all exit 0).
+  if (const char* e = std::getenv("MILP_DEVICE_RESET_AT_EXIT")) {
+    if (std::atoi(e) != 0) {
+      int n = 0;
+      if (hipGetDeviceCount(&n) == hipSuccess) {
+        for (int d = 0; d < n; ++d) {
+          if (hipSetDevice(d) == hipSuccess) {
+            (void)hipDeviceSynchronize();
+            (void)hipDeviceReset();
+          }
+        }
+      }
+    }
+  }
   return MI_LP_OK;
 }
 
@@ -6137,6 +6158,11 @@ int mi_lp_get_kernel_stats(const mi_lp* h, mi_lp_kernel_stats* s) {
 int mi_lp_reset_kernel_stats(mi_lp* h) {
   if (h == nullptr) return MI_LP_ERROR_NULL;
   h->simplex.device().ResetStats();
+  return MI_LP_OK;
+}
+int mi_lp_set_kernel_timing_ids(mi_lp* h, uint32_t id_mask) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  h->simplex.device().SetTiming(id_mask != 0, id_mask);
   return MI_LP_OK;
 }
 int mi_lp_set_kernel_timing(mi_lp* h, int32_t enable) {

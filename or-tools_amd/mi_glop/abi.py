@@ -167,7 +167,7 @@ EXPORTED_SYMBOLS = [
     "mi_lp_get_primal_ray", "mi_lp_get_dual_ray",
     "mi_lp_get_dual_ray_row_combination", "mi_lp_begin", "mi_lp_run_until",
     "mi_lp_finish", "mi_lp_stop", "mi_lp_get_kernel_stats", "mi_lp_reset_kernel_stats",
-    "mi_lp_set_kernel_timing", "mi_lp_batch_solve", "mi_lp_set_variable_bounds",
+    "mi_lp_set_kernel_timing", "mi_lp_set_kernel_timing_ids", "mi_lp_batch_solve", "mi_lp_set_variable_bounds",
     "mi_lp_batch_solve_bounds", "mi_lp_notify_matrix_changed",
     "mi_lp_set_starting_variable_values", "mi_lp_set_integrality_scale",
     "mi_lp_objective_limit_reached", "mi_lp_get_unit_row_left_inverse",

@@ -73,6 +73,7 @@ def lib():
     L.mi_lp_get_kernel_stats.argtypes = [vp, ctypes.POINTER(abi.MiLpKernelStats)]
     L.mi_lp_reset_kernel_stats.argtypes = [vp]
     L.mi_lp_set_kernel_timing.argtypes = [vp, ctypes.c_int32]
+    L.mi_lp_set_kernel_timing_ids.argtypes = [vp, ctypes.c_uint32]
     L.mi_lp_batch_solve.argtypes = [vp, ctypes.c_int32, ctypes.c_int32,
                                     ctypes.POINTER(abi.MiLpResult)]
     L.mi_lp_set_variable_bounds.argtypes = [vp, vp, vp]
@@ -370,8 +371,16 @@ class LpHandle:
     def reset_kernel_stats(self):
         self._L.mi_lp_reset_kernel_stats(self.h)
 
-    def set_kernel_timing(self, on=True):
-        self._L.mi_lp_set_kernel_timing(self.h, int(on))
+    def set_kernel_timing(self, on=True, kernels=None):
+        """HIP-event timing of the kernel ids in `kernels` (names of
+        abi.KERNEL_NAMES; None: all) while on."""
+        if kernels is None:
+            self._L.mi_lp_set_kernel_timing(self.h, int(on))
+            return
+        mask = 0
+        for k in kernels:
+            mask |= 1 << abi.KERNEL_NAMES.index(k)
+        self._L.mi_lp_set_kernel_timing_ids(self.h, mask if on else 0)
 
     def _get(self, fn, n, dtype):
         out = np.zeros(n, dtype=dtype)
