@@ -597,7 +597,10 @@ class DeviceLp : public DeviceSolver {
   // parallel non-zero appends), config 5's window runs 3 % faster without the
   // device BTRAN loops and 5 % faster without either (scripts/gpu_r04_ab2.sh).
   bool tri_btran_ = false;    // MILP_TRI_BTRAN=1: the other dense loops (BTRAN, UpperSolve) too
-  bool tri_pair_ = false;
+  // MILP_TRI_PAIR=0: the direction's and tau's U solves as two launches on
+  // two streams. On by default since round 5 (config-5 window 724/759 ->
+  // 773/827 it/s, profiles/r05_tri).
+  bool tri_pair_ = true;
   // MILP_TRI_PAD=1: every chip-wide level starts on a wave boundary (empty
   // padding records). Needed while the sync-free stores sat below the wait
   // loop (a wave holding an output and its reader deadlocked); since the

@@ -48,12 +48,16 @@ VARIANTS = {
     "syncfree_copies": {"MILP_TRI_MAPPED": "0"},
     "persistent_xcd": {"MILP_TRI_PERSIST": "32", "MILP_TRI_XCD": "1", "MILP_TRI_POLL_MAX": "8"},
     "persistent_chip": {"MILP_TRI_PERSIST": "64", "MILP_TRI_POLL_MAX": "4"},
-    # Every level chip-wide (no single-workgroup narrow segments), and
+    # Single-workgroup narrow segments (off by default since round 5), and
     # narrow segments of any width (long runs cut at the LDS capacity).
-    "no_chain": {"MILP_TRI_CHAIN": "0"},
-    "wide_chain": {"MILP_TRI_CHAIN_WIDTH": "100000", "MILP_TRI_CHAIN_MIN_LEVELS": "1"},
-    # The two-vector U launch and the device BTRAN loops (off by default).
-    "pair_btran": {"MILP_TRI_PAIR": "1", "MILP_TRI_BTRAN": "1"},
+    "chain": {"MILP_TRI_CHAIN": "1"},
+    "wide_chain": {"MILP_TRI_CHAIN": "1", "MILP_TRI_CHAIN_WIDTH": "100000",
+                   "MILP_TRI_CHAIN_MIN_LEVELS": "1"},
+    # Levels padded to wave boundaries (off by default since round 5).
+    "padded": {"MILP_TRI_PAD": "1"},
+    # The two U solves as separate launches (the two-vector launch is the
+    # default since round 5), and the device BTRAN loops (off by default).
+    "no_pair_btran": {"MILP_TRI_PAIR": "0", "MILP_TRI_BTRAN": "1"},
 }
 
 
@@ -62,7 +66,7 @@ VARIANTS = {
 _PARAMS = [(c, "syncfree") for c in _cases()] + [
     (c, v) for c in _cases() if c[0] in ("c5_71", "dense_dual")
     for v in ("levels", "levels_copies", "syncfree_copies", "persistent_xcd",
-              "persistent_chip", "no_chain", "wide_chain", "pair_btran")]
+              "persistent_chip", "chain", "wide_chain", "padded", "no_pair_btran")]
 
 
 @pytest.mark.parametrize("case,variant", _PARAMS, ids=lambda x: x if isinstance(x, str) else x[0])
