@@ -359,7 +359,8 @@ def run_c2(args, rank, world, local_rank, dist, barrier, sync):
             "sample": (f"oracle (C++ restatement of Glop, -O3, 1 thread) on the same "
                        f"{args.m}x{args.n} LP: iterations {args.cpu_warmup}.."
                        f"{args.cpu_warmup + args.cpu_iters} timed "
-                       f"({info['wall_s']:.1f}s wall incl. setup)")}
+                       f"({info['wall_s']:.1f}s wall incl. setup)"),
+            "late_window": "not timed: the oracle needs ~10 min to reach iteration 1500"}
     return out
 
 
@@ -422,6 +423,8 @@ def run_c3(args, rank, world, local_rank, dist, barrier, sync):
     # dominant kind's device time (the timed pass above runs without events).
     timed_pass = None
     try:
+        if args.profile_batch:
+            raise RuntimeError("skipped (--profile-batch)")
         th = []
         for lp in lps:
             h = engine.LpHandle(p, device=local_rank)
@@ -434,7 +437,10 @@ def run_c3(args, rank, world, local_rank, dist, barrier, sync):
             h.close()
     except Exception as e:  # a report, never a reason to fail the bench
         log(f"c3: event-timed pass unavailable: {e}")
-    out["roofline"] = batched_roofline_from(stats, elapsed, timed_pass)
+    out["roofline"] = batched_roofline_from(stats, elapsed, timed_pass, args.c3_traffic_json,
+                                            len(lps))
+    if args.profile_batch:
+        log(f"c3: LPs solved in this process: {len(lps) + 1}")
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_lib
         log("c3: cpu baseline (oracle)")
@@ -485,11 +491,24 @@ def _agg_stats(handles):
     return agg
 
 
-def batched_roofline(handles, wall_s, timed_pass=None):
-    return batched_roofline_from(_agg_stats(handles), wall_s, timed_pass)
+def batched_roofline(handles, wall_s, timed_pass=None, traffic_json=None, lps=0):
+    return batched_roofline_from(_agg_stats(handles), wall_s, timed_pass, traffic_json, lps)
 
 
-def batched_roofline_from(agg, wall_s, timed_pass=None):
+def batch_traffic(traffic_json, lps):
+    """HBM bytes of a batch of `lps` LPs from a profiled run of the same
+    section (scripts/profile_bench.sh: FETCH_SIZE x2 + WRITE_SIZE of every
+    engine kernel of the run, per LP solved in it), or (None, None)."""
+    if not traffic_json or not os.path.exists(traffic_json) or lps <= 0:
+        return None, None
+    tj = json.load(open(traffic_json))
+    b = tj.get("_batch")
+    if not b:
+        return None, None
+    return b["bytes_per_lp"] * lps, tj.get("_source", traffic_json)
+
+
+def batched_roofline_from(agg, wall_s, timed_pass=None, traffic_json=None, lps=0):
     """Roofline of the batch's dominant kernel kind, summed over the handles
     of the timed batch: algorithmic bytes (the engine's per-kind formulas,
     DESIGN.md section 4; for the device dual segments 12 bytes per operation
@@ -520,8 +539,11 @@ def batched_roofline_from(agg, wall_s, timed_pass=None):
                           key=lambda kv: max(kv[1]["device_ms"], kv[1]["call_ms"]))
         per_lp_ms = a["device_ms"] if a["device_ms"] > 0 else a["call_ms"]
         achieved = a["bytes"] / wall_s / 1e9
+        traffic, traffic_src = batch_traffic(traffic_json, lps)
         return {"kernel": kind, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_unit": "HBM bytes of the whole batch (all engine kernels)",
+                "traffic_source": traffic_src, "algorithmic_bytes": a["bytes"],
                 "launches": int(a["launches"]), "bytes_per_launch": a["bytes"] / a["launches"],
                 "timing": "batch wall", "wall_s": wall_s,
                 "summed_kind_ms": per_lp_ms,
@@ -571,7 +593,10 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     for w in workers:
         w.load(lp)
     # Warm-up batch (not timed): first-touch allocations on every worker.
-    engine.batch_solve_bounds(workers, lbs[:n_workers], ubs[:n_workers], state)
+    if not args.profile_batch:
+        engine.batch_solve_bounds(workers, lbs[:n_workers], ubs[:n_workers], state)
+    else:
+        log(f"batched: LPs solved in this process: {len(lbs) + 1}")
     for w in workers:
         w.reset_kernel_stats()
     barrier()
@@ -599,7 +624,7 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
                      f"branches, dual simplex warm-started from the node basis, cap 1000 "
                      f"iterations"),
     }
-    out["roofline"] = batched_roofline(workers, elapsed)
+    out["roofline"] = batched_roofline(workers, elapsed, None, args.c4_traffic_json, len(lbs))
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_lib
         ows = [oracle_lib.OracleLp(p) for _ in range(args.batch_cpu_threads)]
@@ -650,8 +675,10 @@ def main():
     ap.add_argument("--c2-warmup", type=int, default=3)
     ap.add_argument("--c2-late", type=int, default=1500,
                     help="config-2 iteration where a second (late) window starts (0: none)")
-    ap.add_argument("--cpu-iters", type=int, default=6)
-    ap.add_argument("--cpu-warmup", type=int, default=2)
+    ap.add_argument("--cpu-iters", type=int, default=None,
+                    help="config-2 CPU baseline iterations (default: the GPU's --c2-steps)")
+    ap.add_argument("--cpu-warmup", type=int, default=None,
+                    help="config-2 CPU baseline start (default: the GPU's --c2-warmup)")
     ap.add_argument("--traffic-json",
                     default=os.path.join(REPO, "profiles", "traffic_c2.json"),
                     help="per-launch HBM bytes of the config-2 dominant kernel from a "
@@ -670,11 +697,22 @@ def main():
     ap.add_argument("--batch-machines", type=int, default=10)
     ap.add_argument("--batch-cpu-lps", type=int, default=512)
     ap.add_argument("--no-c3", action="store_true", help="skip the config-3 section")
+    ap.add_argument("--profile-batch", action="store_true",
+                    help="profiling runs (scripts/profile_bench.sh): config 3 without its "
+                         "event-timed second pass, config 4 without its warm-up batch, so "
+                         "that the process solves each batch once")
+    ap.add_argument("--c3-traffic-json", default=os.path.join(REPO, "profiles", "traffic_c3.json"))
+    ap.add_argument("--c4-traffic-json", default=os.path.join(REPO, "profiles", "traffic_c4.json"))
     ap.add_argument("--c3-max-rows", type=int, default=16000,
                     help="largest config-3 member (SURVEY 8(c): m from 27 to ~16k)")
     ap.add_argument("--c3-workers", type=int, default=16)
     ap.add_argument("--c3-cpu-threads", type=int, default=16)
     args = ap.parse_args()
+    # The config-2 CPU baseline times the GPU's own early window by default.
+    if args.cpu_iters is None:
+        args.cpu_iters = args.c2_steps
+    if args.cpu_warmup is None:
+        args.cpu_warmup = args.c2_warmup
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` on its own: start the N ranks (one process

@@ -72,7 +72,7 @@ def group_of(name):
     return None
 
 
-def main(src, tag, workload):
+def main(src, tag, workload, lps=0):
     root = os.environ.get("PROFILE_OUT_ROOT") or os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
     out = os.path.join(root, tag)
@@ -125,12 +125,24 @@ def main(src, tag, workload):
     traffic = {g: {"traffic_bytes_per_launch": v[0] / max(1, logical_launches(g, v)),
                    "anchor_kernel": v[2], "launches": logical_launches(g, v)}
                for g, v in groups.items()}
+    if lps > 0:
+        # Batched sections: every engine kernel of the run (the persistent
+        # sdual pool kernel is one dispatch for the whole batch), per LP.
+        total = sum(v[0] for v in groups.values())
+        total += sum(c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)
+                     for name, c in counters.items() if "sdual" in name or "sprimal" in name)
+        traffic["_batch"] = {"bytes_total": total, "lps_in_run": lps,
+                             "bytes_per_lp": total / lps}
     json.dump(traffic, open(os.path.join(out, "traffic.json"), "w"), indent=1)
     latest = dict(traffic, _source=f"profiles/{tag}")
     json.dump(latest, open(os.path.join(os.path.dirname(out), f"traffic_{workload}.json"), "w"),
               indent=1)
     lines += ["", "Per engine kernel id (bytes per logical launch, all HIP kernels of the id):", ""]
     for g, v in traffic.items():
+        if g == "_batch":
+            lines.append(f"- batch: {v['bytes_total'] / 1e9:.3f} GB over {v['lps_in_run']} LPs = "
+                         f"{v['bytes_per_lp'] / 1e6:.3f} MB per LP")
+            continue
         lines.append(f"- {g}: {v['traffic_bytes_per_launch'] / 1e9:.3f} GB/launch "
                      f"(anchor `{v['anchor_kernel'][:60]}`, {v['launches']} launches)")
     open(os.path.join(out, "summary.md"), "w").write("\n".join(lines) + "\n")
@@ -138,4 +150,5 @@ def main(src, tag, workload):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "c2")
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "c2",
+         int(sys.argv[4]) if len(sys.argv) > 4 else 0)
