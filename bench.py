@@ -668,6 +668,8 @@ def main():
     ap.add_argument("--c5-traffic-json",
                     default=os.path.join(REPO, "profiles", "traffic_c5.json"),
                     help="per-launch HBM bytes of the config-5 kernels (profiles/)")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the config-5 headline (profiling runs of the other sections)")
     ap.add_argument("--no-c2", action="store_true", help="skip the config-2 section")
     ap.add_argument("--m", type=int, default=10000, help="config-2 rows")
     ap.add_argument("--n", type=int, default=50000, help="config-2 columns")
@@ -759,9 +761,15 @@ def main():
             import torch
             torch.cuda.synchronize()
 
-    log(f"config-5 headline: {args.c5_m}x{args.c5_n}")
-    c5 = run_c5(args, rank, world, local_rank, dist, barrier, sync)
-    log(f"c5: {c5['value']:.1f} iterations/s")
+    if args.no_c5:  # profiling runs of the other sections only
+        c5 = {"value": 0.0, "ms_per_step": 0.0, "timed_iterations": [0, 0], "finished_early": False,
+              "setup_and_warmup_s": 0.0, "nnz": 0, "roofline": None, "kernels": {},
+              "event_timed_kernels": None, "host_ms_per_step": None,
+              "device_call_ms_per_step": None, "window": None, "split": False}
+    else:
+        log(f"config-5 headline: {args.c5_m}x{args.c5_n}")
+        c5 = run_c5(args, rank, world, local_rank, dist, barrier, sync)
+        log(f"c5: {c5['value']:.1f} iterations/s")
     c2 = None
     if not args.no_c2:
         log(f"config-2 section: {args.m}x{args.n} dense")
