@@ -20,7 +20,7 @@ for P in "$P1" "$P2" "$P3"; do
   Q=""
   for c in $P; do if grep -qx "$c" $OUT/sq_counters.txt; then Q="$Q $c"; else echo "missing $c"; fi; done
   [ -n "$Q" ] || { echo "pass $n skipped"; n=$((n+1)); continue; }
-  MILP_SDUAL_POOL=0 MILP_CRASH_REPORT=1 timeout -s KILL 240 rocprofv3 --pmc $Q -d $OUT/p$n -o p$n \
+  MILP_SDUAL_POOL=0 MILP_CRASH_REPORT=1 MILP_DEVICE_RESET_AT_EXIT=1 timeout -s KILL 240 rocprofv3 --pmc $Q -d $OUT/p$n -o p$n \
     --output-format csv -- python3 $R/scripts/probe_batch.py --node --lps 64 --workers 64 \
     > $OUT/p$n.log 2>&1
   rc=$?; echo "pass $n rc=$rc"
