@@ -25,3 +25,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
     python3 $R/bench.py "$@" > $OUT/$p.log 2>&1 || { echo "$c pass failed"; exit 1; }
 done
 cd $R && PROFILE_OUT_ROOT=$R/gpurun_out/profiles python3 scripts/profile_summary.py $OUT $tag $workload ${PROFILE_LPS:-0}
+# The per-dispatch traces and counter rows (hundreds of MB over a config-5
+# solve) stay on the box: gpurun copies back at most 64 MiB.
+rm -f $OUT/trace/run_kernel_trace.csv $OUT/*/run_counter_collection.csv $OUT/*/*.db
