@@ -605,7 +605,7 @@ class DeviceLp : public DeviceSolver {
   // padding records). Needed while the sync-free stores sat below the wait
   // loop (a wave holding an output and its reader deadlocked); since the
   // loop exit is wave-uniform a reader may share its producer's wave.
-  bool tri_pad_ = false;     // MILP_TRI_PAIR=1: direction and tau U solves in one launch
+  bool tri_pad_ = false;
   int tri_min_width_ = 128;   // MILP_TRI_MIN_WIDTH (auto mode)
   // MILP_TRI_CHAIN=1: single-workgroup segments; a narrow segment is a run
   // of at least MILP_TRI_CHAIN_MIN_LEVELS levels of at most
@@ -617,6 +617,28 @@ class DeviceLp : public DeviceSolver {
   int tri_chain_width_ = 512;
   int tri_chain_min_levels_ = 4;
   uint64_t* d_tri_clock_ = nullptr;
+  // Dense tail of BTRAN's forward U^T solve (dense_tail.hip): the last
+  // factorization's tail columns on the device, rebuilt when its key changes.
+  // MILP_DENSE_TAIL=0 keeps the host loop; MILP_DENSE_TAIL_MIN_ENTRIES (default
+  // 2^20) and MILP_DENSE_TAIL_MIN_COLS (default 128) decide when it pays.
+  struct DenseTail {
+    uint64_t key = ~0ull;
+    bool ok = false;
+    int n = 0, fni = 0, t = 0;
+    int64_t entries = 0;
+    TriBuffer starts, split, rows, vals, diag, x, pre;
+    double* h_in = nullptr;    // pinned, mapped: x in (n values), then the fail word
+    double* m_in = nullptr;
+    double* h_out = nullptr;   // pinned, mapped: x[t, n) out
+    double* m_out = nullptr;
+    int cap_n = 0, cap_t = 0;
+  };
+  DenseTail dense_tail_;
+  int dense_tail_mode_ = 1;
+  int64_t dense_tail_min_entries_ = int64_t{1} << 20;
+  int dense_tail_min_cols_ = 128;
+  bool DenseTailSolve(const TriangularMatrix& t, uint64_t key, std::vector<double>* x);
+  void FreeDenseTail();
   TriSchedule tri_sched_[kTriNumMatrices];
   // Per solving thread: 0 = the solver's thread (the handle's stream),
   // 1 = BasisFactorization's tau worker (its own stream), 2 = the second

@@ -161,6 +161,13 @@ void DeviceLp::Init(int device) {
   if (const char* v = std::getenv("MILP_TRI_BTRAN")) tri_btran_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_PAIR")) tri_pair_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_PAD")) tri_pad_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_DENSE_TAIL")) dense_tail_mode_ = std::atoi(v);
+  if (const char* v = std::getenv("MILP_DENSE_TAIL_MIN_ENTRIES")) {
+    dense_tail_min_entries_ = std::atoll(v);
+  }
+  if (const char* v = std::getenv("MILP_DENSE_TAIL_MIN_COLS")) {
+    dense_tail_min_cols_ = std::max(1, std::atoi(v));
+  }
   if (const char* v = std::getenv("MILP_TRI_MIN_WIDTH")) tri_min_width_ = std::atoi(v);
   if (const char* v = std::getenv("MILP_TRI_CHAIN")) tri_chain_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_CHAIN_WIDTH")) tri_chain_width_ = std::atoi(v);

@@ -64,6 +64,7 @@ void DeviceLp::TriReserve(TriBuffer* b, size_t bytes) {
 }
 
 void DeviceLp::FreeTriBuffers() {
+  FreeDenseTail();
   for (TriSchedule& s : tri_sched_) {
     for (TriBuffer& b : s.buf) FreeBuffer(&b);
     s = TriSchedule();
@@ -528,8 +529,162 @@ bool DeviceLp::LowerSolve(const TriangularMatrix& lower, uint64_t key, std::vect
   return TriSolve(kTriL, lower, key, x);
 }
 
+void DeviceLp::FreeDenseTail() {
+  DenseTail& d = dense_tail_;
+  for (TriBuffer* b : {&d.starts, &d.split, &d.rows, &d.vals, &d.diag, &d.x, &d.pre}) {
+    FreeBuffer(b);
+  }
+  if (d.h_in != nullptr) (void)hipHostFree(d.h_in);
+  if (d.h_out != nullptr) (void)hipHostFree(d.h_out);
+  d = DenseTail();
+}
+
+// BTRAN's forward U^T solve (TriangularMatrix::TransposeUpperSolve,
+// sparse.cc:848-897) with its dense tail on the device (dense_tail.hip).
+// Columns [fni, t) run the host loop here, unchanged; columns [t, n) -- the
+// trailing columns holding at least n / 8 entries each -- on the device: the
+// leading groups of four that read rows < t only, for all tail columns at
+// once, then the tail's own dependency walk on one workgroup. Every output
+// is evaluated with the loop's operations in the loop's order (same bits).
+// False: the host loop runs the whole solve.
+bool DeviceLp::DenseTailSolve(const TriangularMatrix& u, uint64_t key, std::vector<double>* xv) {
+  if (dense_tail_mode_ == 0 || g_lu_slot != 0) return false;
+  const int n = u.num_cols();
+  if (static_cast<int>(xv->size()) < n) return false;
+  DenseTail& d = dense_tail_;
+  const int64_t* st = u.starts_.data();
+  if (d.key != key) {
+    DeviceOp("dense tail build");
+    d.key = key;
+    d.ok = false;
+    d.n = n;
+    d.fni = u.GetFirstNonIdentityColumn();
+    int t = n;
+    const int64_t dense = std::max<int64_t>(16, n / 8);
+    while (t > d.fni && st[t] - st[t - 1] >= dense) --t;
+    const int T = n - t;
+    const int64_t entries = st[n] - st[t];
+    if (T < dense_tail_min_cols_ || T > milp_kernels::kTailMaxCols ||
+        entries < dense_tail_min_entries_) {
+      return false;
+    }
+    d.t = t;
+    d.entries = entries;
+    // Per tail column: the end of its leading groups of four whose rows are
+    // all below t (final when the tail starts).
+    std::vector<int64_t> rel(T + 1), split(T);
+    const int32_t* rows = u.rows_.data();
+    for (int c = t; c < n; ++c) {
+      const int64_t i0 = st[c], i1 = st[c + 1];
+      int64_t i = i0;
+      while (i + 3 < i1 && rows[i] < t && rows[i + 1] < t && rows[i + 2] < t && rows[i + 3] < t) {
+        i += 4;
+      }
+      rel[c - t] = i0 - st[t];
+      split[c - t] = i - st[t];
+    }
+    rel[T] = entries;
+    TriReserve(&d.starts, sizeof(int64_t) * (T + 1));
+    TriReserve(&d.split, sizeof(int64_t) * T);
+    TriReserve(&d.rows, sizeof(int32_t) * entries);
+    TriReserve(&d.vals, sizeof(double) * entries);
+    TriReserve(&d.x, sizeof(double) * n);
+    TriReserve(&d.pre, sizeof(double) * T);
+    hipStream_t s = Stream(stream_);
+    Check(hipMemcpyAsync(d.starts.ptr, rel.data(), sizeof(int64_t) * (T + 1),
+                         hipMemcpyHostToDevice, s), "dense tail upload");
+    Check(hipMemcpyAsync(d.split.ptr, split.data(), sizeof(int64_t) * T, hipMemcpyHostToDevice, s),
+          "dense tail upload");
+    Check(hipMemcpyAsync(d.rows.ptr, rows + st[t], sizeof(int32_t) * entries,
+                         hipMemcpyHostToDevice, s), "dense tail upload");
+    Check(hipMemcpyAsync(d.vals.ptr, u.coefficients_.data() + st[t], sizeof(double) * entries,
+                         hipMemcpyHostToDevice, s), "dense tail upload");
+    if (!u.all_diagonal_coefficients_are_one_) {
+      TriReserve(&d.diag, sizeof(double) * T);
+      Check(hipMemcpyAsync(d.diag.ptr, u.diagonal_coefficients_.data() + t, sizeof(double) * T,
+                           hipMemcpyHostToDevice, s), "dense tail upload");
+    }
+    if (d.cap_n < n) {
+      if (d.h_in != nullptr) (void)hipHostFree(d.h_in);
+      Check(hipHostMalloc(reinterpret_cast<void**>(&d.h_in), sizeof(double) * (n + 1),
+                          hipHostMallocMapped), "dense tail staging");
+      Check(hipHostGetDevicePointer(reinterpret_cast<void**>(&d.m_in), d.h_in, 0), "mapped");
+      d.cap_n = n;
+    }
+    if (d.cap_t < T) {
+      if (d.h_out != nullptr) (void)hipHostFree(d.h_out);
+      Check(hipHostMalloc(reinterpret_cast<void**>(&d.h_out), sizeof(double) * T,
+                          hipHostMallocMapped), "dense tail staging");
+      Check(hipHostGetDevicePointer(reinterpret_cast<void**>(&d.m_out), d.h_out, 0), "mapped");
+      d.cap_t = T;
+    }
+    Check(hipStreamSynchronize(s), "dense tail upload");  // rel/split are freed below
+    d.ok = true;
+  }
+  if (!d.ok) return false;
+  SolveCallTimer timer(&stats_, MI_K_TRI_SOLVE_T);
+  const int t = d.t;
+  const int T = n - t;
+  double* x = xv->data();
+  // Columns [fni, t): the host loop (sparse.cc:848-897), as it runs them.
+  {
+    const int32_t* rows = u.rows_.data();
+    const double* coefs = u.coefficients_.data();
+    const bool ones = u.all_diagonal_coefficients_are_one_;
+    int64_t i = st[d.fni];
+    for (int col = d.fni; col < t; ++col) {
+      double sum = x[col];
+      const int64_t i_end = st[col + 1];
+      const int64_t shifted_end = i_end - 3;
+      for (; i < shifted_end; i += 4) {
+        sum -= coefs[i] * x[rows[i]] + coefs[i + 1] * x[rows[i + 1]] +
+               coefs[i + 2] * x[rows[i + 2]] + coefs[i + 3] * x[rows[i + 3]];
+      }
+      if (i < i_end) {
+        sum -= coefs[i] * x[rows[i]];
+        if (i + 1 < i_end) {
+          sum -= coefs[i + 1] * x[rows[i + 1]];
+          if (i + 2 < i_end) sum -= coefs[i + 2] * x[rows[i + 2]];
+        }
+        i = i_end;
+      }
+      x[col] = ones ? sum : sum / u.diagonal_coefficients_[col];
+    }
+  }
+  DeviceOp("dense tail solve");
+  CopyHost(d.h_in, x, sizeof(double) * n);
+  int* fail = reinterpret_cast<int*>(d.h_in + n);
+  *fail = 0;
+  milp_kernels::DenseTailArgs a{};
+  a.starts = static_cast<const int64_t*>(d.starts.ptr);
+  a.split = static_cast<const int64_t*>(d.split.ptr);
+  a.rows = static_cast<const int32_t*>(d.rows.ptr);
+  a.vals = static_cast<const double*>(d.vals.ptr);
+  a.diag = u.all_diagonal_coefficients_are_one_ ? nullptr : static_cast<const double*>(d.diag.ptr);
+  a.x = static_cast<double*>(d.x.ptr);
+  a.pre = static_cast<double*>(d.pre.ptr);
+  a.host_x = d.m_in;
+  a.host_out = d.m_out;
+  a.n = n;
+  a.t = t;
+  a.fail = reinterpret_cast<int*>(d.m_in + n);
+  // Algorithmic bytes: per entry its row and value (12 B) and the value it
+  // reads (8 B); per tail output its prefix, diagonal, value in and out.
+  const double bytes = 20.0 * static_cast<double>(d.entries) + 40.0 * T + 16.0 * n;
+  BeginKernel(MI_K_TRI_SOLVE_T);
+  Check(milp_launch::dense_tail_upper_solve(a, Stream(stream_)), "dense tail solve");
+  EndKernel(MI_K_TRI_SOLVE_T, bytes);
+  Check(hipStreamSynchronize(Stream(stream_)), "dense tail sync");
+  if (*static_cast<volatile int*>(fail) != 0) {
+    throw DeviceError("dense tail solve: dependency wait timed out");
+  }
+  CopyHost(x + t, d.h_out, sizeof(double) * T);
+  return true;
+}
+
 bool DeviceLp::Solve(TriKind kind, const TriangularMatrix& t, uint64_t key, int /*start*/,
                      std::vector<double>* x) {
+  if (kind == TriKind::kUpperTUp && DenseTailSolve(t, key, x)) return true;
   // LowerSolveStartingAt(start): the loops below `start` only meet zeros in
   // every caller (a unit row, or L's input below its first non-zero), which
   // the gather computes as the loop leaves them.
