@@ -584,6 +584,7 @@ bool DeviceLp::DenseTailSolve(const TriangularMatrix& u, uint64_t key, std::vect
       split[c - t] = i - st[t];
     }
     rel[T] = entries;
+    d.split_host = split;
     TriReserve(&d.starts, sizeof(int64_t) * (T + 1));
     TriReserve(&d.split, sizeof(int64_t) * T);
     TriReserve(&d.rows, sizeof(int32_t) * entries);
@@ -671,14 +672,47 @@ bool DeviceLp::DenseTailSolve(const TriangularMatrix& u, uint64_t key, std::vect
   // Algorithmic bytes: per entry its row and value (12 B) and the value it
   // reads (8 B); per tail output its prefix, diagonal, value in and out.
   const double bytes = 20.0 * static_cast<double>(d.entries) + 40.0 * T + 16.0 * n;
+  // MILP_DENSE_TAIL=2: only the leading groups on the device; the tail's
+  // own triangle runs the host loop from the prefixes (same operations).
+  const bool walk = dense_tail_mode_ != 2;
   BeginKernel(MI_K_TRI_SOLVE_T);
-  Check(milp_launch::dense_tail_upper_solve(a, Stream(stream_)), "dense tail solve");
+  if (walk) {
+    Check(milp_launch::dense_tail_upper_solve(a, Stream(stream_)), "dense tail solve");
+  } else {
+    Check(milp_launch::dense_tail_prefix(a, Stream(stream_)), "dense tail prefix");
+  }
   EndKernel(MI_K_TRI_SOLVE_T, bytes);
   Check(hipStreamSynchronize(Stream(stream_)), "dense tail sync");
   if (*static_cast<volatile int*>(fail) != 0) {
     throw DeviceError("dense tail solve: dependency wait timed out");
   }
-  CopyHost(x + t, d.h_out, sizeof(double) * T);
+  if (walk) {
+    CopyHost(x + t, d.h_out, sizeof(double) * T);
+    return true;
+  }
+  // The host walk: each tail column continues its chain where the prefix
+  // stopped (sparse.cc:848-897 from there on).
+  const int32_t* rows = u.rows_.data();
+  const double* coefs = u.coefficients_.data();
+  const bool ones = u.all_diagonal_coefficients_are_one_;
+  for (int col = t; col < n; ++col) {
+    double sum = d.h_out[col - t];
+    int64_t i = st[t] + d.split_host[col - t];
+    const int64_t i_end = st[col + 1];
+    const int64_t shifted_end = i_end - 3;
+    for (; i < shifted_end; i += 4) {
+      sum -= coefs[i] * x[rows[i]] + coefs[i + 1] * x[rows[i + 1]] +
+             coefs[i + 2] * x[rows[i + 2]] + coefs[i + 3] * x[rows[i + 3]];
+    }
+    if (i < i_end) {
+      sum -= coefs[i] * x[rows[i]];
+      if (i + 1 < i_end) {
+        sum -= coefs[i + 1] * x[rows[i + 1]];
+        if (i + 2 < i_end) sum -= coefs[i + 2] * x[rows[i + 2]];
+      }
+    }
+    x[col] = ones ? sum : sum / u.diagonal_coefficients_[col];
+  }
   return true;
 }
 

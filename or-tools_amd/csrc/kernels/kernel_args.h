@@ -380,7 +380,7 @@ constexpr int kTriChainVals = 12288;
 // computed before the tail), then one workgroup walks the tail's own
 // dependencies with the tail's values in LDS.
 constexpr int kTailThreads = 1024;
-constexpr int kTailMaxCols = 16384;  // tail values held in LDS (128 KB)
+constexpr int kTailMaxCols = 4096;  // tail columns held in LDS (values, sums, cursors: 80 KB)
 struct DenseTailArgs {
   const int64_t* starts;  // [T + 1] entry ranges of the tail columns (relative)
   const int64_t* split;   // [T] end of each column's leading groups (relative)
@@ -493,6 +493,9 @@ hipError_t column_squared_norms(const int64_t* starts, const double* vals,
 // groups of every tail column (one workgroup per column), the tail's own
 // dependency walk (one workgroup), copy-out of x[t, n) to host_out.
 hipError_t dense_tail_upper_solve(const milp_kernels::DenseTailArgs& args, hipStream_t s);
+// Only the leading groups: copy-in, the prefixes, and the prefixes out to
+// host_out (T values); the caller walks the tail on the host.
+hipError_t dense_tail_prefix(const milp_kernels::DenseTailArgs& args, hipStream_t s);
 }  // namespace milp_launch
 
 #endif  // MILP_KERNEL_ARGS_H_
