@@ -626,11 +626,10 @@ class DeviceLp : public DeviceSolver {
     bool ok = false;
     int n = 0, fni = 0, t = 0;
     int64_t entries = 0;
-    TriBuffer starts, split, rows, vals, diag, x, pre;
+    TriBuffer starts, cur, rows, vals, diag, x, pre;
     double* h_in = nullptr;    // pinned, mapped: x in (n values), then the fail word
     double* m_in = nullptr;
-    double* h_out = nullptr;   // pinned, mapped: x[t, n) out (or the prefixes)
-    std::vector<int64_t> split_host;  // per tail column, relative to the tail's first entry
+    double* h_out = nullptr;   // pinned, mapped: x[t, n) out
     double* m_out = nullptr;
     int cap_n = 0, cap_t = 0;
   };

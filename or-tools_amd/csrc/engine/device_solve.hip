@@ -531,7 +531,7 @@ bool DeviceLp::LowerSolve(const TriangularMatrix& lower, uint64_t key, std::vect
 
 void DeviceLp::FreeDenseTail() {
   DenseTail& d = dense_tail_;
-  for (TriBuffer* b : {&d.starts, &d.split, &d.rows, &d.vals, &d.diag, &d.x, &d.pre}) {
+  for (TriBuffer* b : {&d.starts, &d.cur, &d.rows, &d.vals, &d.diag, &d.x, &d.pre}) {
     FreeBuffer(b);
   }
   if (d.h_in != nullptr) (void)hipHostFree(d.h_in);
@@ -584,9 +584,21 @@ bool DeviceLp::DenseTailSolve(const TriangularMatrix& u, uint64_t key, std::vect
       split[c - t] = i - st[t];
     }
     rel[T] = entries;
-    d.split_host = split;
+    if (std::getenv("MILP_DENSE_TAIL_DEBUG") != nullptr) {
+      int64_t prefix = 0, unsorted = 0;
+      for (int c = t; c < n; ++c) {
+        prefix += split[c - t] - rel[c - t];
+        for (int64_t i = st[c]; i + 1 < st[c + 1]; ++i) unsorted += rows[i] > rows[i + 1];
+      }
+      std::fprintf(stderr,
+                   "[dense tail] n %d fni %d t %d T %d entries %lld prefix %lld triangle %lld "
+                   "unsorted pairs %lld, columns [fni, t) entries %lld\n",
+                   n, d.fni, t, T, static_cast<long long>(entries), static_cast<long long>(prefix),
+                   static_cast<long long>(entries - prefix), static_cast<long long>(unsorted),
+                   static_cast<long long>(st[t] - st[d.fni]));
+    }
     TriReserve(&d.starts, sizeof(int64_t) * (T + 1));
-    TriReserve(&d.split, sizeof(int64_t) * T);
+    TriReserve(&d.cur, sizeof(int64_t) * T);
     TriReserve(&d.rows, sizeof(int32_t) * entries);
     TriReserve(&d.vals, sizeof(double) * entries);
     TriReserve(&d.x, sizeof(double) * n);
@@ -594,8 +606,6 @@ bool DeviceLp::DenseTailSolve(const TriangularMatrix& u, uint64_t key, std::vect
     hipStream_t s = Stream(stream_);
     Check(hipMemcpyAsync(d.starts.ptr, rel.data(), sizeof(int64_t) * (T + 1),
                          hipMemcpyHostToDevice, s), "dense tail upload");
-    Check(hipMemcpyAsync(d.split.ptr, split.data(), sizeof(int64_t) * T, hipMemcpyHostToDevice, s),
-          "dense tail upload");
     Check(hipMemcpyAsync(d.rows.ptr, rows + st[t], sizeof(int32_t) * entries,
                          hipMemcpyHostToDevice, s), "dense tail upload");
     Check(hipMemcpyAsync(d.vals.ptr, u.coefficients_.data() + st[t], sizeof(double) * entries,
@@ -658,7 +668,7 @@ bool DeviceLp::DenseTailSolve(const TriangularMatrix& u, uint64_t key, std::vect
   *fail = 0;
   milp_kernels::DenseTailArgs a{};
   a.starts = static_cast<const int64_t*>(d.starts.ptr);
-  a.split = static_cast<const int64_t*>(d.split.ptr);
+  a.cur = static_cast<int64_t*>(d.cur.ptr);
   a.rows = static_cast<const int32_t*>(d.rows.ptr);
   a.vals = static_cast<const double*>(d.vals.ptr);
   a.diag = u.all_diagonal_coefficients_are_one_ ? nullptr : static_cast<const double*>(d.diag.ptr);
@@ -670,49 +680,17 @@ bool DeviceLp::DenseTailSolve(const TriangularMatrix& u, uint64_t key, std::vect
   a.t = t;
   a.fail = reinterpret_cast<int*>(d.m_in + n);
   // Algorithmic bytes: per entry its row and value (12 B) and the value it
-  // reads (8 B); per tail output its prefix, diagonal, value in and out.
+  // reads (8 B); per tail output its running sum, cursor, diagonal, value in
+  // and out.
   const double bytes = 20.0 * static_cast<double>(d.entries) + 40.0 * T + 16.0 * n;
-  // MILP_DENSE_TAIL=2: only the leading groups on the device; the tail's
-  // own triangle runs the host loop from the prefixes (same operations).
-  const bool walk = dense_tail_mode_ != 2;
   BeginKernel(MI_K_TRI_SOLVE_T);
-  if (walk) {
-    Check(milp_launch::dense_tail_upper_solve(a, Stream(stream_)), "dense tail solve");
-  } else {
-    Check(milp_launch::dense_tail_prefix(a, Stream(stream_)), "dense tail prefix");
-  }
+  Check(milp_launch::dense_tail_upper_solve(a, Stream(stream_)), "dense tail solve");
   EndKernel(MI_K_TRI_SOLVE_T, bytes);
   Check(hipStreamSynchronize(Stream(stream_)), "dense tail sync");
   if (*static_cast<volatile int*>(fail) != 0) {
     throw DeviceError("dense tail solve: dependency wait timed out");
   }
-  if (walk) {
-    CopyHost(x + t, d.h_out, sizeof(double) * T);
-    return true;
-  }
-  // The host walk: each tail column continues its chain where the prefix
-  // stopped (sparse.cc:848-897 from there on).
-  const int32_t* rows = u.rows_.data();
-  const double* coefs = u.coefficients_.data();
-  const bool ones = u.all_diagonal_coefficients_are_one_;
-  for (int col = t; col < n; ++col) {
-    double sum = d.h_out[col - t];
-    int64_t i = st[t] + d.split_host[col - t];
-    const int64_t i_end = st[col + 1];
-    const int64_t shifted_end = i_end - 3;
-    for (; i < shifted_end; i += 4) {
-      sum -= coefs[i] * x[rows[i]] + coefs[i + 1] * x[rows[i + 1]] +
-             coefs[i + 2] * x[rows[i + 2]] + coefs[i + 3] * x[rows[i + 3]];
-    }
-    if (i < i_end) {
-      sum -= coefs[i] * x[rows[i]];
-      if (i + 1 < i_end) {
-        sum -= coefs[i + 1] * x[rows[i + 1]];
-        if (i + 2 < i_end) sum -= coefs[i + 2] * x[rows[i + 2]];
-      }
-    }
-    x[col] = ones ? sum : sum / u.diagonal_coefficients_[col];
-  }
+  CopyHost(x + t, d.h_out, sizeof(double) * T);
   return true;
 }
 

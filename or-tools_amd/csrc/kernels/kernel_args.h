@@ -373,22 +373,17 @@ constexpr int kTriChainVals = 12288;
 
 // Dense tail of BTRAN's forward U^T solve (dense_tail.hip): upper_.
 // TransposeUpperSolve (sparse.cc:848-897) when the last columns of U hold
-// most of its entries (config 2's dense kernel: ~1 500 columns, each reading
-// ~8 500 slack rows before the kernel's own rows). Columns [t, n) are the
-// tail; each tail column's leading groups of four that read rows < t only
-// are folded first, for all tail columns at once (final values: rows < t are
-// computed before the tail), then one workgroup walks the tail's own
-// dependencies with the tail's values in LDS.
-constexpr int kTailThreads = 1024;
-constexpr int kTailMaxCols = 4096;  // tail columns held in LDS (values, sums, cursors: 80 KB)
+// most of its entries (config 2's dense kernel). Columns [t, n) are the tail,
+// solved by blocks of 64 columns (advance over the chip, finish on one wave).
+constexpr int kTailMaxCols = 16384;
 struct DenseTailArgs {
   const int64_t* starts;  // [T + 1] entry ranges of the tail columns (relative)
-  const int64_t* split;   // [T] end of each column's leading groups (relative)
   const int32_t* rows;    // entries: rows (< the column)
   const double* vals;
   const double* diag;     // [T], nullptr when all are 1
   double* x;              // [n] the vector, in and out
-  double* pre;            // [T] each column's running sum after its leading groups
+  double* pre;            // [T] each column's running sum
+  int64_t* cur;           // [T] each column's chain cursor (relative entry index)
   const double* host_x;   // device view of the pinned staging copy (n values)
   double* host_out;       // device view of the pinned output (x[t, n))
   int n;
@@ -489,13 +484,10 @@ hipError_t tri_transpose_lower_persistent(const milp_kernels::TriSolveArgs& args
 hipError_t column_squared_norms(const int64_t* starts, const double* vals,
                                 const uint64_t* relevant, int ncols, double* out,
                                 hipStream_t s);
-// Dense-tail TransposeUpperSolve: copy-in of x from host_x, the leading
-// groups of every tail column (one workgroup per column), the tail's own
-// dependency walk (one workgroup), copy-out of x[t, n) to host_out.
+// Dense-tail TransposeUpperSolve: copy-in of x from host_x, the blocks of
+// 64 tail columns (advance + finish launches), copy-out of x[t, n) to host_out.
 hipError_t dense_tail_upper_solve(const milp_kernels::DenseTailArgs& args, hipStream_t s);
-// Only the leading groups: copy-in, the prefixes, and the prefixes out to
-// host_out (T values); the caller walks the tail on the host.
-hipError_t dense_tail_prefix(const milp_kernels::DenseTailArgs& args, hipStream_t s);
+
 }  // namespace milp_launch
 
 #endif  // MILP_KERNEL_ARGS_H_

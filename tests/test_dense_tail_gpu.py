@@ -26,13 +26,9 @@ def _cases():
     ]
 
 
-@pytest.mark.parametrize("mode", ["1", "2"], ids=["device_walk", "host_walk"])
 @pytest.mark.parametrize("case", _cases(), ids=lambda c: c[0])
-def test_dense_tail_parity(case, mode, monkeypatch):
-    """Mode 1: the tail's triangle on the device; mode 2: the leading groups
-    on the device, the triangle by the host loop from them."""
+def test_dense_tail_parity(case, monkeypatch):
     name, build, dual, cap = case
-    monkeypatch.setenv("MILP_DENSE_TAIL", mode)
     monkeypatch.setenv("MILP_DENSE_TAIL_MIN_ENTRIES", "2000")
     monkeypatch.setenv("MILP_DENSE_TAIL_MIN_COLS", "8")
     lp = build()
