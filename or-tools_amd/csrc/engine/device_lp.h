@@ -619,8 +619,12 @@ class DeviceLp : public DeviceSolver {
   uint64_t* d_tri_clock_ = nullptr;
   // Dense tail of BTRAN's forward U^T solve (dense_tail.hip): the last
   // factorization's tail columns on the device, rebuilt when its key changes.
-  // MILP_DENSE_TAIL=0 keeps the host loop; MILP_DENSE_TAIL_MIN_ENTRIES (default
-  // 2^20) and MILP_DENSE_TAIL_MIN_COLS (default 128) decide when it pays.
+  // Opt-in (MILP_DENSE_TAIL=1): on config 2's late bases each tail column's
+  // entries are ~10 ascending runs of rows, so its chain stalls on the first
+  // tail row of its order and most of it folds only after the previous
+  // column -- a sequential chain the device runs slower than the host loop
+  // (late window 17 vs 53 it/s). MILP_DENSE_TAIL_MIN_ENTRIES
+  // (default 2^20) and MILP_DENSE_TAIL_MIN_COLS (default 128) gate it.
   struct DenseTail {
     uint64_t key = ~0ull;
     bool ok = false;
@@ -634,7 +638,7 @@ class DeviceLp : public DeviceSolver {
     int cap_n = 0, cap_t = 0;
   };
   DenseTail dense_tail_;
-  int dense_tail_mode_ = 1;
+  int dense_tail_mode_ = 0;
   int64_t dense_tail_min_entries_ = int64_t{1} << 20;
   int dense_tail_min_cols_ = 128;
   bool DenseTailSolve(const TriangularMatrix& t, uint64_t key, std::vector<double>* x);

@@ -29,6 +29,7 @@ def _cases():
 @pytest.mark.parametrize("case", _cases(), ids=lambda c: c[0])
 def test_dense_tail_parity(case, monkeypatch):
     name, build, dual, cap = case
+    monkeypatch.setenv("MILP_DENSE_TAIL", "1")
     monkeypatch.setenv("MILP_DENSE_TAIL_MIN_ENTRIES", "2000")
     monkeypatch.setenv("MILP_DENSE_TAIL_MIN_COLS", "8")
     lp = build()
