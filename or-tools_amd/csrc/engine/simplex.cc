@@ -5103,7 +5103,7 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     }
     clock.Mark(0);
 
-    if (!feasibility_phase && sdual_mode_ != 0) {
+    if (sdual_mode_ != 0) {  // phase II, or dual phase I (sd_run's dual_phase1)
       Status sd_status;
       int sd;
       do {

@@ -3275,6 +3275,287 @@ SD_INLINE void rc_get(Lp& s) {
   if (s.recompute_rc) rc_compute_reduced_costs(s);
 }
 
+// ---- Dual phase I (revised_simplex.cc:2198-2388, entering_variable.cc:241-355) ----
+// Glop's dedicated dual feasibility algorithm: the leaving row maximizes
+// price^2 / norm over the phase-I prices (dual_pricing_vector_, the right
+// solve of the sum of the dual-infeasible columns signed by the direction
+// that improves them), the entering column is the phase-I breakpoint test,
+// and the prices follow the pivot instead of the primal values.
+SD_INLINE bool dp1_is_candidate(f64 price, int8_t type, f64 threshold) {
+  if (price == 0.0) return false;
+  return type == kBoxed || type == kFixedVariable ||
+         (type == kUpperBounded && price < -threshold) ||
+         (type == kLowerBounded && price > threshold);
+}
+// OnDualPriceChange (:2198-2215) for distinct rows in list order: `upd(row,
+// &type)` applies the row's price change and names the basic type. On the
+// device 64 rows at a time: prices, values and candidate bits on the lanes,
+// then the rows that can enter the top-k (value >= the threshold at the
+// chunk's start: the threshold never decreases) replay dp_update_top_k in
+// list order, as the sequential AddOrUpdate calls do.
+template <typename Upd>
+SD_INLINE void dp1_rows_changed(Lp& s, const int32_t* rows, int n, const f64* sn, Upd upd) {
+  const f64 threshold = s.ratio_test_zero_threshold;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int lane = sd_lane();
+  for (int base = 0; base < n; base += 64) {
+    const int k = base + lane;
+    int row = 0;
+    f64 value = 0.0;
+    bool cand = false;
+    if (k < n) {
+      row = rows[k];
+      int8_t type;
+      upd(row, &type);
+      const f64 price = s.dpv[row];
+      unsigned long long* word = reinterpret_cast<unsigned long long*>(s.dp.cand + (row >> 6));
+      const unsigned long long bit = 1ull << (row & 63);
+      if (dp1_is_candidate(price, type, threshold)) {
+        value = sq(price) / sn[row];
+        s.dp.values[row] = value;
+        atomicOr(word, bit);
+        cand = value >= s.dp.threshold;
+      } else {
+        atomicAnd(word, ~bit);
+      }
+    }
+    uint64_t mask = __ballot(cand);
+    while (mask != 0) {
+      const int l = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const int r = __shfl(row, l, 64);
+      const f64 v = __shfl(value, l, 64);
+      if (v >= s.dp.threshold) dp_update_top_k(s, s.dp, r, v);
+    }
+  }
+  sd_sync();
+#else
+  for (int k = 0; k < n; ++k) {
+    const int row = rows[k];
+    int8_t type;
+    upd(row, &type);
+    const f64 price = s.dpv[row];
+    if (dp1_is_candidate(price, type, threshold)) {
+      dp_add_or_update(s, s.dp, row, sq(price) / sn[row]);
+    } else {
+      dp_remove(s, s.dp, row);
+    }
+  }
+#endif
+}
+// DualPhaseIUpdatePrice (:2217-2267), before UpdateAndPivot.
+// AreReducedCostsRecomputed(): recomputed, or about to be (reduced_costs.h).
+SD_INLINE bool rc_are_recomputed(const Lp& s) { return s.recompute_rc || s.rc_recomputed; }
+SD_INLINE void dp1_update_price(Lp& s, int leaving_row, int entering_col) {
+  if (rc_are_recomputed(s) || s.norms_recompute || s.dpv_size == 0) return;
+  const f64* sn = norms_get(s);
+  const f64 step = s.dpv[leaving_row] / s.dir.values[leaving_row];
+  dp1_rows_changed(s, s.dir.nz, s.dir.nnz, sn, [&](int row, int8_t* type) {
+    s.dpv[row] -= s.dir.values[row] * step;
+    *type = s.vtype[s.basis[row]];
+  });
+  s.dpv[leaving_row] = step;
+  s.dpv[leaving_row] -= s.diid[entering_col];
+  if (s.diid[entering_col] != 0.0) --s.n_dual_inf;
+  s.diid[entering_col] = 0.0;
+  s.diid[s.basis[leaving_row]] = 0.0;
+  const int32_t one = leaving_row;
+  dp1_rows_changed(s, &one, 1, sn, [&](int, int8_t* type) { *type = s.vtype[entering_col]; });
+}
+// DualPhaseIUpdatePriceOnReducedCostChange (:2269-2333) over `cols` (null:
+// the relevant columns in increasing order). The changed columns' signed
+// sum is scattered in order into the zero scratchpad (ia0: the host's two
+// initially-all-zero scratchpads are both zero between uses), solved with
+// B and added to the prices.
+SD_INLINE void dp1_update_price_on_rc_change(Lp& s, const int32_t* cols, int n) {
+  rc_get(s);  // GetReducedCosts()
+  const f64 tol = s.dual_tol;
+  Vec& v = s.ia0;
+  bool something_to_do = false;
+  auto change = [&](int col, f64 sign) {
+    const f64 old = s.diid[col];
+    if (sign == 0.0) {
+      --s.n_dual_inf;
+    } else if (old == 0.0) {
+      ++s.n_dual_inf;
+    }
+    if (!something_to_do) {
+      for (int i = v.size + sd_lane(); i < s.m; i += sd_lanes()) v.values[i] = 0.0;
+      sd_sync();
+      v.size = s.m;
+      vec_clear_mask(v);
+      v.nnz = 0;
+      something_to_do = true;
+    }
+    s.num_update_price_ops += 10 * col_entries(s.A, col);
+    col_add_scattered(s.A, col, sign - old, v);
+    s.diid[col] = sign;
+  };
+  auto sign_of = [&](int col) -> f64 {
+    const f64 rc = s.rc[col];
+    return (bit_get(s.can_inc, col) && rc < -tol)   ? 1.0
+           : (bit_get(s.can_dec, col) && rc > tol) ? -1.0
+                                                   : 0.0;
+  };
+  const int count = cols != nullptr ? n : s.N;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // 64 positions at a time: the signs on the lanes, the changed columns
+  // replayed in order (their scatters are order-dependent).
+  for (int base = 0; base < count; base += 64) {
+    const int k = base + sd_lane();
+    int col = -1;
+    f64 sign = 0.0;
+    if (k < count) {
+      col = cols != nullptr ? cols[k] : (bit_get(s.relevant, k) ? k : -1);
+      if (col >= 0) sign = sign_of(col);
+    }
+    uint64_t mask = __ballot(col >= 0 && sign != s.diid[col >= 0 ? col : 0]);
+    while (mask != 0) {
+      const int l = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      change(__shfl(col, l, 64), __shfl(sign, l, 64));
+    }
+  }
+#else
+  for (int k = 0; k < count; ++k) {
+    const int col = cols != nullptr ? cols[k] : k;
+    if (cols == nullptr && !bit_get(s.relevant, col)) continue;
+    const f64 sign = sign_of(col);
+    if (sign != s.diid[col]) change(col, sign);
+  }
+#endif
+  if (!something_to_do) return;
+  vec_clear_nz_if_too_dense(v, 0.8);  // ClearNonZerosIfTooDense()
+  vec_clear_mask(v);                  // ClearSparseMask()
+  const f64* sn = norms_get(s);
+  bf_right_solve(s, v);
+  if (v.nnz == 0) {
+    // DenseAddOrUpdate over the rows with a change (no top-k maintenance).
+    dp_start_dense_updates(s, s.dp);
+    const f64 threshold = s.ratio_test_zero_threshold;
+#if defined(__HIP_DEVICE_COMPILE__)
+    for (int base = 0; base < s.m; base += 64) {
+      const int row = base + sd_lane();
+      bool touched = false, cand = false;
+      if (row < s.m && v.values[row] != 0.0) {
+        touched = true;
+        s.dpv[row] += v.values[row];
+        const f64 price = s.dpv[row];
+        if (dp1_is_candidate(price, s.vtype[s.basis[row]], threshold)) {
+          cand = true;
+          s.dp.values[row] = sq(price) / sn[row];
+        }
+      }
+      const uint64_t tmask = __ballot(touched);
+      const uint64_t cmask = __ballot(cand);
+      if (sd_lane() == 0 && tmask != 0) {
+        s.dp.cand[base >> 6] = (s.dp.cand[base >> 6] & ~tmask) | cmask;
+      }
+    }
+    sd_sync();
+#else
+    for (int row = 0; row < s.m; ++row) {
+      if (v.values[row] == 0.0) continue;
+      s.dpv[row] += v.values[row];
+      const f64 price = s.dpv[row];
+      if (dp1_is_candidate(price, s.vtype[s.basis[row]], threshold)) {
+        dp_dense_add_or_update(s, s.dp, row, sq(price) / sn[row]);
+      } else {
+        dp_remove(s, s.dp, row);
+      }
+    }
+#endif
+    sd_fill<f64>(v.values, s.m, 0.0);
+  } else {
+    dp1_rows_changed(s, v.nz, v.nnz, sn, [&](int row, int8_t* type) {
+      s.dpv[row] += v.values[row];
+      v.values[row] = 0.0;
+      *type = s.vtype[s.basis[row]];
+    });
+  }
+  v.nnz = 0;
+}
+// DualPhaseIChooseLeavingVariableRow (:2335-2388); kInvalid when none.
+SD_INLINE int dp1_choose_leaving(Lp& s, f64* cost_variation, f64* target_bound) {
+  if (rc_are_recomputed(s) || s.norms_recompute || s.dpv_size == 0) {
+    s.n_dual_inf = 0;
+    sd_fill<f64>(s.dpv, s.m, 0.0);
+    s.dpv_size = s.m;
+    dp_clear_and_resize(s, s.dp, s.m);
+    sd_fill<f64>(s.diid, s.N, 0.0);
+    s.diid_size = s.N;
+    dp1_update_price_on_rc_change(s, nullptr, 0);
+  } else {
+    dp1_update_price_on_rc_change(s, s.nzpos, s.n_nzpos);
+  }
+  if (s.n_dual_inf == 0) return kInvalid;
+  const int row = dp_get_maximum(s, s.dp);
+  if (row == kInvalid) return kInvalid;
+  *cost_variation = s.dpv[row];
+  const int col = s.basis[row];
+  *target_bound = *cost_variation < 0.0 ? s.ub[col] : s.lb[col];
+  return row;
+}
+// EnteringVariable::DualPhaseIChooseEnteringColumn (entering_variable.cc:241-355).
+SD_INLINE void ent_dual_phase1_choose(Lp& s, bool nothing_to_recompute, f64 cost_variation,
+                                      int* entering_col) {
+  rc_get(s);  // GetReducedCosts()
+  const f64 threshold =
+      nothing_to_recompute ? s.minimum_acceptable_pivot : s.ratio_test_zero_threshold;
+  const f64 dual_tol = s.dual_tol;
+  const f64 harris_tolerance = s.harris_tolerance_ratio * dual_tol;
+  const f64 minimum_delta = s.degenerate_ministep_factor * dual_tol;
+  s.ent_ops += 10 * static_cast<int64_t>(s.n_nzpos);
+  int nbp = 0;
+  for (int k = 0; k < s.n_nzpos; ++k) {
+    const int col = s.nzpos[k];
+    if (sd_fabs(s.coeff[col]) < threshold) continue;
+    const f64 coeff = (cost_variation > 0.0) ? s.coeff[col] : -s.coeff[col];
+    const f64 rc = s.rc[col];
+    f64 ratio;  // the ColWithRatio's reduced_cost argument
+    if (sd_fabs(rc) <= dual_tol) {
+      if (coeff > 0 && !bit_get(s.can_dec, col)) continue;
+      if (coeff < 0 && !bit_get(s.can_inc, col)) continue;
+      ratio = coeff * rc > 0.0 ? sd_max(minimum_delta, harris_tolerance - sd_fabs(rc))
+                               : sd_fabs(rc) + harris_tolerance;
+    } else {
+      if (coeff * rc > 0.0) continue;
+      ratio = sd_fabs(rc) + harris_tolerance;
+    }
+    // ColWithRatio(col, reduced_cost, coeff_m): ratio = reduced_cost / coeff_m.
+    const f64 mag = sd_fabs(coeff);
+    s.bp_col[nbp] = col;
+    s.bp_ratio[nbp] = ratio / mag;
+    s.bp_mag[nbp] = mag;
+    ++nbp;
+  }
+  for (int i = nbp / 2 - 1; i >= 0; --i) bp_sift_down(s, i, nbp);
+  f64 pivot_magnitude = 0.0;
+  *entering_col = kInvalid;
+  f64 step = -1.0;
+  f64 improvement = sd_fabs(cost_variation);
+  while (nbp > 0) {
+    const int tcol = s.bp_col[0];
+    const f64 tratio = s.bp_ratio[0];
+    const f64 tmag = s.bp_mag[0];
+    if (tratio > step && tmag >= pivot_magnitude) {
+      *entering_col = tcol;
+      step = tratio;
+      pivot_magnitude = tmag;
+    }
+    improvement -= tmag;
+    if (bit_get(s.can_dec, tcol) && bit_get(s.can_inc, tcol) && sd_fabs(s.rc[tcol]) > threshold) {
+      improvement -= tmag;
+    }
+    if (improvement <= 0.0) break;
+    --nbp;
+    if (nbp > 0) {
+      bp_swap(s, 0, nbp);
+      bp_sift_down(s, 0, nbp);
+    }
+  }
+}
+
 // ---- factorization (host Markowitz through the mailbox) ----
 // Points the LU fields at an image installed at address `b` (`im` is a
 // readable copy of its header).
@@ -3624,7 +3905,10 @@ SD_INLINE int32_t sd_run(Lp& s) {
         rs_permute_basis(s);
       }
       s.refactorize = 0;
-      if (s.num_updates == 0) {
+      if (s.dual_phase1) {
+        // Phase I: only MakeReducedCostsPrecise after a factorization.
+        if (s.num_updates == 0) rc_make_precise(s);
+      } else if (s.num_updates == 0) {
         SdSubTimer t_x_(&s.phase_ticks[20]);
         if (old_refactorize) rc_make_precise(s);
         rs_make_boxed_dual_feasible_all(s);
@@ -3643,9 +3927,15 @@ SD_INLINE int32_t sd_run(Lp& s) {
     }
     at_top = true;
     SD_PHASE(1);
-    // DualChooseLeavingVariableRow (:2148-2181)
-    if (s.dp.size == 0) vv_recompute_dual_prices(s, s.dual_price_prioritize_norm);
-    const int leaving_row = dp_get_maximum(s, s.dp);
+    // DualChooseLeavingVariableRow (:2148-2181) / DualPhaseIChooseLeavingVariableRow
+    f64 cost_variation = 0.0, target_bound = 0.0;
+    int leaving_row;
+    if (s.dual_phase1) {
+      leaving_row = dp1_choose_leaving(s, &cost_variation, &target_bound);
+    } else {
+      if (s.dp.size == 0) vv_recompute_dual_prices(s, s.dual_price_prioritize_norm);
+      leaving_row = dp_get_maximum(s, s.dp);
+    }
     if (leaving_row == kInvalid) {
       if (s.num_updates != 0 || s.has_cost_shift) {
         rc_clear_and_remove_cost_shifts(s);
@@ -3653,17 +3943,19 @@ SD_INLINE int32_t sd_run(Lp& s) {
         continue;
       }
       s.exit_row = kInvalid;
+      // Phase I: DUAL_FEASIBLE / DUAL_INFEASIBLE from n_dual_inf (the bridge).
       return s.exit_code = kExitOptimal;
     }
     const int lcol = s.basis[leaving_row];
-    const f64 value = s.x[lcol];
-    f64 cost_variation, target_bound;
-    if (value < s.lb[lcol]) {
-      cost_variation = s.lb[lcol] - value;
-      target_bound = s.lb[lcol];
-    } else {
-      cost_variation = s.ub[lcol] - value;
-      target_bound = s.ub[lcol];
+    if (!s.dual_phase1) {
+      const f64 value = s.x[lcol];
+      if (value < s.lb[lcol]) {
+        cost_variation = s.lb[lcol] - value;
+        target_bound = s.lb[lcol];
+      } else {
+        cost_variation = s.ub[lcol] - value;
+        target_bound = s.ub[lcol];
+      }
     }
     s.exit_row = leaving_row;
     s.exit_cost_variation = cost_variation;
@@ -3672,8 +3964,14 @@ SD_INLINE int32_t sd_run(Lp& s) {
     SD_PHASE(2);
     ur_compute_unit_row_left_inverse(s, leaving_row);
     if (!den_test_precision(s, leaving_row)) {
-      const int32_t one = leaving_row;
-      vv_update_dual_prices(s, &one, 1);
+      if (s.dual_phase1) {
+        const f64 price = s.dpv[leaving_row];
+        const f64* sn = norms_get(s);
+        dp_add_or_update(s, s.dp, leaving_row, sq(price) / sn[leaving_row]);
+      } else {
+        const int32_t one = leaving_row;
+        vv_update_dual_prices(s, &one, 1);
+      }
       continue;
     }
     SD_PHASE(3);
@@ -3681,13 +3979,17 @@ SD_INLINE int32_t sd_run(Lp& s) {
 
     SD_PHASE(4);
     int entering_col;
-    ent_dual_choose(s, s.rc_precise != 0, cost_variation, &entering_col);
+    if (s.dual_phase1) {
+      ent_dual_phase1_choose(s, s.rc_precise != 0, cost_variation, &entering_col);
+    } else {
+      ent_dual_choose(s, s.rc_precise != 0, cost_variation, &entering_col);
+    }
     if (entering_col == kInvalid) {
       if (!s.rc_precise) {
         s.refactorize = 1;
         continue;
       }
-      return s.exit_code = kExitNoEntering;
+      return s.exit_code = kExitNoEntering;  // phase I: ABNORMAL (the bridge)
     }
     const f64 entering_coeff = s.coeff[entering_col];
     if (sd_fabs(entering_coeff) < s.dual_small_pivot_threshold && !s.rc_precise) {
@@ -3712,17 +4014,21 @@ SD_INLINE int32_t sd_run(Lp& s) {
     rc_update_before_pivot(s, entering_col, leaving_row);
     den_update_before_pivot(s, leaving_row);
     SD_PHASE(7);
-    // ComputeStepToMoveBasicVariableToBound + UpdateOnPivoting
-    const f64 primal_step = (s.x[lcol] - target_bound) / s.dir.values[leaving_row];
-    {
-      SdSubTimer t_x_(&s.phase_ticks[25]);
-      for (int k = sd_lane(); k < s.dir.nnz; k += sd_lanes()) {  // distinct basic columns
-        const int row = s.dir.nz[k];
-        s.x[s.basis[row]] -= s.dir.values[row] * primal_step;
+    if (s.dual_phase1) {
+      dp1_update_price(s, leaving_row, entering_col);
+    } else {
+      // ComputeStepToMoveBasicVariableToBound + UpdateOnPivoting
+      const f64 primal_step = (s.x[lcol] - target_bound) / s.dir.values[leaving_row];
+      {
+        SdSubTimer t_x_(&s.phase_ticks[25]);
+        for (int k = sd_lane(); k < s.dir.nnz; k += sd_lanes()) {  // distinct basic columns
+          const int row = s.dir.nz[k];
+          s.x[s.basis[row]] -= s.dir.values[row] * primal_step;
+        }
+        sd_sync();
       }
-      sd_sync();
+      s.x[entering_col] += primal_step;
     }
-    s.x[entering_col] += primal_step;
     // UpdateAndPivot (:2504-2575)
     int refactor = 0;  // 1: ForceRefactorization, 2: the same after the LU threshold bump
     if (sd_pivot(s, entering_col, leaving_row, target_bound, &refactor) != kExitNone) {

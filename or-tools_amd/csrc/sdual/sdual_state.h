@@ -303,9 +303,15 @@ struct Lp {
   Vec vv_scratch; // VariableValues::scratchpad_
   f64 dual_feasibility_tolerance;
   int64_t a_num_entries;
-  f64* dpv;  // dual_pricing_vector_ (phase I leftovers, permuted with the basis)
+  f64* dpv;  // dual_pricing_vector_ (the phase-I prices, permuted with the basis)
   int dpv_size;
   int phase_optimization;
+  // ---- dual phase I (DualMinimize(feasibility_phase = true)) ----
+  int dual_phase1;  // the segment runs the phase-I loop (revised_simplex.cc:2198-2388)
+  int n_dual_inf;   // num_dual_infeasible_positions_
+  int diid_size;    // dual_infeasibility_improvement_direction_.size(): 0 or N
+  int dp1_pad;
+  f64* diid;        // dual_infeasibility_improvement_direction_ (N)
   f64 dual_objective_limit;
   int objective_limit_reached;
   int rc_notify;  // SetRecomputeReducedCostsAndNotifyWatchers ran

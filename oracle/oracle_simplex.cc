@@ -3671,7 +3671,7 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     }
 
 #ifdef ORACLE_SDUAL
-    if (!feasibility_phase && SdualBridge::Supported(*this, time_limit)) {
+    if (SdualBridge::Supported(*this, time_limit)) {
       Status st;
       int next;
       do {

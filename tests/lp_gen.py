@@ -100,6 +100,64 @@ def staircase_lp(m, n, seed, block_rows=50, link_frac=0.2, eq_frac=0.1, free_fra
                             f"staircase_{m}x{n}_s{seed}")
 
 
+def dual_phase1_lp(m, n, seed, density=0.05, unbounded_cols=0):
+    """An LP whose slack basis is dual infeasible on unboxed columns, so that
+    Glop's dual simplex from scratch runs its dedicated phase I
+    (revised_simplex.cc:2198-2388) for many iterations: maximize c.x with c
+    mostly > 0 over lower-bounded columns (x >= 0, no upper bound) with
+    non-negative entries, upper-bounded columns (x <= u) with non-positive
+    entries and c < 0, a few boxed and fixed columns, and <= / ranged rows
+    with b > 0 (x = 0 is feasible, every improving ray meets a row).
+    `unbounded_cols` trailing lower-bounded columns with a positive cost get
+    no entries: the LP is then dual infeasible (phase I ends DUAL_INFEASIBLE)."""
+    rng = np.random.default_rng(seed)
+    nnz_per_col = max(1, int(round(density * m)))
+    kinds = rng.uniform(size=n)  # < 0.6 lower, < 0.8 upper, < 0.95 boxed, else fixed
+    starts = [0]
+    rows, vals = [], []
+    for c in range(n):
+        if c >= n - unbounded_cols:
+            starts.append(len(rows))
+            continue
+        k = max(1, min(m, rng.binomial(2 * nnz_per_col, 0.5)))
+        r = np.sort(rng.choice(m, size=k, replace=False))
+        v = rng.uniform(0.1, 1.0, size=k)
+        if kinds[c] >= 0.6 and kinds[c] < 0.8:
+            v = -v
+        elif kinds[c] >= 0.8:
+            v = v * rng.choice([-1.0, 1.0], size=k)
+        rows.extend(r.tolist())
+        vals.extend(v.tolist())
+        starts.append(len(rows))
+    cs = np.asarray(starts, np.int64)
+    ri = np.asarray(rows, np.int32)
+    va = np.asarray(vals, np.float64)
+    col_lb = np.zeros(n)
+    col_ub = np.full(n, INF)
+    obj = rng.uniform(0.1, 1.0, size=n)
+    upper = (kinds >= 0.6) & (kinds < 0.8)
+    col_lb[upper] = -INF
+    col_ub[upper] = rng.uniform(0.0, 1.0, size=upper.sum())
+    obj[upper] = -obj[upper]
+    boxed = (kinds >= 0.8) & (kinds < 0.95)
+    col_ub[boxed] = 1.0 + rng.uniform(0, 2, size=boxed.sum())
+    obj[boxed] *= rng.choice([-1.0, 1.0], size=boxed.sum())
+    fixed = kinds >= 0.95
+    col_ub[fixed] = 0.0
+    if unbounded_cols:
+        col_lb[n - unbounded_cols:] = 0.0
+        col_ub[n - unbounded_cols:] = INF
+        obj[n - unbounded_cols:] = rng.uniform(0.1, 1.0, size=unbounded_cols)
+    # Row activity at x = 0 is the upper-bounded columns' contribution at
+    # their bounds at most: b covers it.
+    row_ub = rng.uniform(1.0, 2.0, size=m)
+    row_lb = np.full(m, -INF)
+    ranged = rng.uniform(size=m) < 0.2
+    row_lb[ranged] = -1.0 - rng.uniform(0.0, 1.0, size=ranged.sum())
+    return LinearProgram(m, n, cs, ri, va, col_lb, col_ub, row_lb, row_ub, obj,
+                         0.0, 1.0, True, f"dual_phase1_{m}x{n}_s{seed}")
+
+
 def fixed_order_matvec(At, x):
     """A @ x from the rows of At = A^T, summed column by column in index
     order with one rounding per multiply and per add. BLAS (`A @ x`) picks

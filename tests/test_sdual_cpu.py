@@ -139,6 +139,70 @@ def test_sdual_restatement_resume_paths():
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
+def _segment_iterations(lp, p, phase1):
+    """Iterations the oracle's sdual variant ran inside segments, with dual
+    phase I in segments (MILP_SDUAL_PHASE1 unset) or on the host loop."""
+    import os
+    old = os.environ.pop("MILP_SDUAL_PHASE1", None)
+    if not phase1:
+        os.environ["MILP_SDUAL_PHASE1"] = "0"
+    try:
+        _, it0 = _counters()
+        o = oracle_lib.OracleLp(p, variant="sdual")
+        o.load(lp)
+        out = _full(o, o.solve())
+        _, it1 = _counters()
+    finally:
+        os.environ.pop("MILP_SDUAL_PHASE1", None)
+        if old is not None:
+            os.environ["MILP_SDUAL_PHASE1"] = old
+    return out, it1 - it0
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_sdual_restatement_dual_phase1(seed):
+    """Glop's dedicated dual phase I (revised_simplex.cc:2198-2388,
+    entering_variable.cc:241-355) in segments: LPs whose slack basis is dual
+    infeasible on unboxed columns, so that DualMinimize(feasibility_phase)
+    runs many iterations; seed 5 is dual infeasible (phase I ends
+    DUAL_INFEASIBLE). Equal to the plain oracle bit for bit, and the segments
+    ran phase-I iterations (more than with phase I kept on the host)."""
+    m, n = 60 + 40 * seed, 200 + 100 * seed
+    lp = lp_gen.dual_phase1_lp(m, n, 900 + seed, unbounded_cols=2 if seed == 5 else 0)
+    p = abi.default_params(use_dual_simplex=1)
+    o = oracle_lib.OracleLp(p)
+    o.load(lp)
+    plain = _full(o, o.solve())
+    seg, it_on = _segment_iterations(lp, p, True)
+    host_p1, it_off = _segment_iterations(lp, p, False)
+    _assert_same(plain, seg, seed)
+    _assert_same(plain, host_p1, seed)
+    assert it_on > it_off, (it_on, it_off)
+    if seed == 5:
+        assert plain["status"] == seg["status"]
+
+
+def test_sdual_restatement_dual_phase1_resume_paths():
+    """Dual phase I through the resume exits (MILP_SDUAL_LU_SLACK: every
+    refactorization inside a segment hands the LP back), in a child process."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path[:0] = %r\n"
+        "import test_sdual_cpu as t, lp_gen\n"
+        "from mi_glop import abi\n"
+        "for seed in range(3):\n"
+        "    lp = lp_gen.dual_phase1_lp(100 + 40 * seed, 400, 950 + seed)\n"
+        "    a, b = t._both(lp, abi.default_params(use_dual_simplex=1))\n"
+        "    t._assert_same(a, b, seed)\n"
+        "print('ok')\n") % (sys.path[:6],)
+    env = dict(os.environ, MILP_SDUAL_LU_SLACK="64")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_sprimal_restatement_sparse(seed):
     """Primal simplex (Glop's default), phase I and II in segments."""

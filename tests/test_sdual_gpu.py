@@ -35,6 +35,46 @@ def test_sdual_single_lp_parity(seed, sdual_mode):
         assert g.kernel_stats()["sdual"]["launches"] == c["sdual_segments"]
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_sdual_dual_phase1_parity(seed, sdual_mode, monkeypatch):
+    """Glop's dedicated dual phase I (revised_simplex.cc:2198-2388,
+    entering_variable.cc:241-355) in segments: LPs whose slack basis is dual
+    infeasible on unboxed columns (seed 3 is dual infeasible), from scratch.
+    The whole final state equals the oracle's, and the segments ran more
+    iterations than with phase I on the host (MILP_SDUAL_PHASE1=0)."""
+    m, n = 80 + 60 * seed, 300 + 200 * seed
+    lp = lp_gen.dual_phase1_lp(m, n, 910 + seed, unbounded_cols=2 if seed == 3 else 0)
+    p = abi.default_params(use_dual_simplex=1)
+    counters = []
+    for phase1 in ("1", "0"):
+        monkeypatch.setenv("MILP_SDUAL_PHASE1", phase1)
+        o, ro, g, rg = parity_util.solve_both(lp, p, lambda q: engine.LpHandle(q, 0))
+        parity_util.compare(o, ro, g, rg, lp)
+        counters.append(g.run_counters())
+    assert counters[0]["sdual_iterations"] > counters[1]["sdual_iterations"], counters
+
+
+def test_sdual_dual_phase1_batch():
+    """Phase-I LPs through the batch API (the pool kernel on the device, 4
+    workers): each result equals the oracle solving it alone."""
+    lps = [lp_gen.dual_phase1_lp(70 + 30 * k, 260 + 90 * k, 930 + k) for k in range(8)]
+    p = abi.default_params(use_dual_simplex=1)
+    handles = []
+    for lp in lps:
+        h = engine.LpHandle(p)
+        h.load(lp)
+        handles.append(h)
+    res = engine.batch_solve(handles, 4)
+    for k, (lp, r) in enumerate(zip(lps, res)):
+        o = oracle_lib.OracleLp(p)
+        o.load(lp)
+        ro = o.solve()
+        assert (r.error_code, r.problem_status, r.iterations) == \
+            (ro.error_code, ro.problem_status, ro.iterations), k
+        assert r.objective == ro.objective, (k, r.objective, ro.objective)
+    assert sum(h.run_counters()["sdual_iterations"] for h in handles) > 0
+
+
 def _children(shape, count, seed=3):
     jobs = jobshop.FT06 if shape == (6, 6) else jobshop.random_instance(*shape, seed)
     lp, ycols = jobshop.relaxation(jobs)
