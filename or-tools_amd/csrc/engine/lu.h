@@ -1137,6 +1137,8 @@ class RankOneUpdateFactorization {
 // used instead of the middle-product form when
 // use_middle_product_form_update is false.
 class EtaMatrix {
+  friend struct SdualBridge;
+
  public:
   EtaMatrix(int eta_col, const ScatteredVector& direction);
   void LeftSolve(std::vector<Fractional>* y) const;
@@ -1148,9 +1150,12 @@ class EtaMatrix {
   Fractional eta_col_coefficient_;
   std::vector<Fractional> eta_coeff_;
   SparseColumn sparse_eta_coeff_;  // entries in direction.non_zeros order
+  EtaMatrix() = default;  // the device segment's etas (sdual_bridge.inc)
 };
 
 class EtaFactorization {
+  friend struct SdualBridge;
+
  public:
   void Clear() { eta_matrix_.clear(); }
   void Update(int /*entering_col*/, int leaving_variable_row,

@@ -2067,6 +2067,126 @@ struct SdLdsVec {
   }
 };
 
+// ---- EtaFactorization (basis_representation.cc:25-176, PFI path) ----
+// The loops are sequential in Glop's order (a running sum, or scatters
+// whose order fixes nothing but are kept), on every lane of the wave.
+SD_INLINE void eta_left_solve_one(const Lp& s, int k, f64* y) {
+  const int c = s.eta_col[k];
+  f64 y_value = y[c];
+  const int64_t b = s.eta_sp_starts[k], e = s.eta_sp_starts[k + 1];
+  if (b != e) {
+    for (int64_t i = b; i < e; ++i) y_value -= y[s.eta_sp_rows[i]] * s.eta_sp_coefs[i];
+  } else {
+    const f64* coeff = s.eta_dense + static_cast<int64_t>(k) * s.m;
+    for (int row = 0; row < s.m; ++row) y_value -= y[row] * coeff[row];
+  }
+  sd_sync();
+  y[c] = y_value / s.eta_piv[k];
+  sd_sync();
+}
+SD_INLINE void eta_right_solve_one(const Lp& s, int k, f64* d) {
+  const int c = s.eta_col[k];
+  if (d[c] == 0.0) return;
+  const f64 coeff = d[c] / s.eta_piv[k];
+  const int64_t b = s.eta_sp_starts[k], e = s.eta_sp_starts[k + 1];
+  sd_sync();
+  // The rows of one eta are distinct (and differ from its column): the
+  // lanes split them.
+  if (b != e) {
+    for (int64_t i = b + sd_lane(); i < e; i += sd_lanes()) {
+      d[s.eta_sp_rows[i]] -= s.eta_sp_coefs[i] * coeff;
+    }
+  } else {
+    const f64* ec = s.eta_dense + static_cast<int64_t>(k) * s.m;
+    for (int row = sd_lane(); row < s.m; row += sd_lanes()) d[row] -= ec[row] * coeff;
+  }
+  sd_sync();
+  d[c] = coeff;
+  sd_sync();
+}
+SD_INLINE void eta_left_solve(const Lp& s, f64* y) {
+  for (int k = s.eta_count - 1; k >= 0; --k) eta_left_solve_one(s, k, y);
+}
+SD_INLINE void eta_right_solve(const Lp& s, f64* d) {
+  for (int k = 0; k < s.eta_count; ++k) eta_right_solve_one(s, k, d);
+}
+// SparseLeftSolve: y's positions in `pos` (the eta column joins the list).
+SD_INLINE void eta_sparse_left_solve(const Lp& s, f64* y, int32_t* pos, int* npos) {
+  for (int k = s.eta_count - 1; k >= 0; --k) {
+    const int c = s.eta_col[k];
+    const f64* coeff = s.eta_dense + static_cast<int64_t>(k) * s.m;
+    f64 y_value = y[c];
+    bool in_pos = false;
+    const int size = *npos;
+    for (int i = 0; i < size; ++i) {
+      const int col = pos[i];
+      if (col == c) {
+        in_pos = true;
+        continue;
+      }
+      y_value -= y[col] * coeff[col];
+    }
+    sd_sync();
+    y[c] = y_value / s.eta_piv[k];
+    if (!in_pos) pos[(*npos)++] = c;
+    sd_sync();
+  }
+}
+// EtaFactorization::Update: EtaMatrix(leaving_row, direction).
+SD_INLINE void eta_update(Lp& s, int leaving_row, const Vec& dir) {
+  const int k = s.eta_count;
+  f64* ec = s.eta_dense + static_cast<int64_t>(k) * s.m;
+  for (int row = sd_lane(); row < s.m; row += sd_lanes()) ec[row] = dir.values[row];
+  sd_sync();
+  s.eta_col[k] = leaving_row;
+  s.eta_piv[k] = dir.values[leaving_row];
+  ec[leaving_row] = 0.0;
+  int64_t e = s.eta_sp_starts[k];
+  if (static_cast<f64>(dir.nnz) < 0.5 * static_cast<f64>(s.m)) {
+    for (int i = 0; i < dir.nnz; ++i) {
+      const int row = dir.nz[i];
+      if (row == leaving_row) continue;
+      s.eta_sp_rows[e] = row;
+      s.eta_sp_coefs[e] = ec[row];
+      ++e;
+    }
+  }
+  s.eta_sp_starts[k + 1] = e;
+  s.eta_count = k + 1;
+  sd_sync();
+}
+// LuFactorization::RightSolve / LeftSolve on dense vectors
+// (lu_factorization.cc:135-156): permute into the scratchpad, the two
+// triangular loops, permute back.
+SD_INLINE void lu_right_solve_dense(Lp& s, f64* x) {
+  if (s.is_identity) return;
+  f64* t = s.pfi_scratch;
+  for (int i = sd_lane(); i < s.m; i += sd_lanes()) t[s.row_perm[i]] = x[i];
+  sd_sync();
+  tri_lower_solve_from(s.lower, 0, t);
+  sd_sync();
+  tri_upper_solve(s.upper, t);
+  sd_sync();
+  for (int i = sd_lane(); i < s.m; i += sd_lanes()) {
+    x[s.col_perm_empty ? i : s.inv_col_perm[i]] = t[i];
+  }
+  sd_sync();
+}
+SD_INLINE void lu_left_solve_dense(Lp& s, f64* y) {
+  if (s.is_identity) return;
+  f64* t = s.pfi_scratch;
+  for (int i = sd_lane(); i < s.m; i += sd_lanes()) {
+    t[i] = y[s.col_perm_empty ? i : s.inv_col_perm[i]];
+  }
+  sd_sync();
+  tri_transpose_upper_solve(s.upper, t);
+  sd_sync();
+  tri_transpose_lower_solve(s.lower, t);
+  sd_sync();
+  for (int i = sd_lane(); i < s.m; i += sd_lanes()) y[i] = t[s.row_perm[i]];
+  sd_sync();
+}
+
 // ---- BasisFactorization (basis_representation.cc:304-624, MPF path) ----
 SD_INLINE void bf_bump(Lp& s, int64_t num_entries) {
   if (s.m == 0) return;
@@ -2074,6 +2194,13 @@ SD_INLINE void bf_bump(Lp& s, int64_t num_entries) {
   s.bf_dtime += density * dt_ops(lu_number_of_entries(s)) + dt_ops(s.r1_num_entries);
 }
 SD_INLINE void bf_right_solve(Lp& s, Vec& d) {
+  if (!s.mpf) {  // RightSolve, PFI (basis_representation.cc:358-372)
+    d.nnz = 0;
+    lu_right_solve_dense(s, d.values);
+    eta_right_solve(s, d.values);
+    bf_bump(s, vec_nnz_estimate(d));
+    return;
+  }
   SdLdsVec lds_(s, d, true);
   lu_right_solve_l_with_nz(s, d);
   r1_right_solve_nz(s, d);
@@ -2097,6 +2224,13 @@ SD_INLINE void lu_left_solve_u_with_nz(Lp& s, Vec& y) {
 }
 // BasisFactorization::LeftSolve (basis_representation.cc:342-356, MPF)
 SD_INLINE void bf_left_solve(Lp& s, Vec& y) {
+  if (!s.mpf) {  // LeftSolve, PFI (:342-356)
+    y.nnz = 0;
+    eta_left_solve(s, y.values);
+    lu_left_solve_dense(s, y.values);
+    bf_bump(s, vec_nnz_estimate(y));
+    return;
+  }
   SdLdsVec lds_(s, y, true);
   lu_left_solve_u_with_nz(s, y);
   r1_left_solve_nz(s, y);
@@ -2147,6 +2281,17 @@ SD_INLINE f64 bf_dual_edge_squared_norm(Lp& s, int row) {
 }
 SD_INLINE const f64* bf_right_solve_for_tau(Lp& s, const Vec& a) {
   SdSubTimer t_sub_(&s.phase_ticks[30]);
+  if (!s.mpf) {  // RightSolveForTau, PFI (:374-398)
+    s.tau.nnz = 0;
+    for (int i = sd_lane(); i < a.size; i += sd_lanes()) s.tau.values[i] = a.values[i];
+    sd_sync();
+    s.tau.size = a.size;
+    lu_right_solve_dense(s, s.tau.values);
+    eta_right_solve(s, s.tau.values);
+    s.tau_is_computed = 1;
+    bf_bump(s, vec_nnz_estimate(s.tau));
+    return s.tau.values;
+  }
   {
   SdLdsVec lds_(s, s.tau, s.tau_can_opt != 0);
   if (s.tau_can_opt) {
@@ -2164,6 +2309,15 @@ SD_INLINE const f64* bf_right_solve_for_tau(Lp& s, const Vec& a) {
   return s.tau.values;
 }
 SD_INLINE void bf_left_solve_for_unit_row(Lp& s, int j, Vec& y) {
+  if (!s.mpf) {  // LeftSolveForUnitRow, PFI (:400-453)
+    vec_clear_and_resize(y, s.m);
+    y.values[j] = 1.0;
+    y.nz[y.nnz++] = j;
+    eta_sparse_left_solve(s, y.values, y.nz, &y.nnz);
+    lu_left_solve_dense(s, y.values);
+    bf_bump(s, vec_nnz_estimate(y));
+    return;
+  }
   SdLdsVec lds_(s, y, false);
   vec_clear_and_resize(y, s.m);
   if (s.left_pool[j] == kInvalid) {
@@ -2188,6 +2342,17 @@ SD_INLINE void bf_left_solve_for_unit_row(Lp& s, int j, Vec& y) {
   bf_bump(s, vec_nnz_estimate(y));
 }
 SD_INLINE void bf_right_solve_for_column(Lp& s, int col, Vec& d) {
+  if (!s.mpf) {  // RightSolveForProblemColumn, PFI (:468-501)
+    vec_clear_and_resize(d, s.m);
+    for (int64_t i = s.A.starts[col] + sd_lane(); i < s.A.starts[col + 1]; i += sd_lanes()) {
+      d.values[s.A.rows[i]] = s.A.coefs[i];
+    }
+    sd_sync();
+    lu_right_solve_dense(s, d.values);
+    eta_right_solve(s, d.values);
+    bf_bump(s, vec_nnz_estimate(d));
+    return;
+  }
   SdLdsVec lds_(s, d, false);
   vec_clear_and_resize(d, s.m);
   lu_right_solve_l_for_column(s, col, d);
@@ -3654,6 +3819,7 @@ SD_INLINE int sd_refactorize(Lp& s, int bump) {
   s.tau_can_opt = 0;
   s.r1_count = 0;
   s.r1_num_entries = 0;
+  s.eta_count = 0;  // eta_factorization_.Clear()
   s.storage.num_cols = 0;
   s.storage.starts[0] = 0;
   s.right_storage.num_cols = 0;
@@ -3771,6 +3937,10 @@ SD_INLINE bool sd_room_for_iteration(const Lp& s) {
   if (s.right_storage.starts[s.right_storage.num_cols] + need > s.right_storage.cap_entries)
     return false;
   if (s.r1_count + 1 > s.r1_cap) return false;
+  if (!s.mpf) {  // one more eta, dense and possibly sparse
+    if (s.eta_count + 1 > s.eta_cap) return false;
+    if (s.eta_sp_starts[s.eta_count] + s.m / 2 + 1 > s.eta_sp_cap) return false;
+  }
   return true;
 }
 
@@ -3807,6 +3977,10 @@ SD_INLINE int32_t sd_pivot(Lp& s, int entering_col, int leaving_row, f64 target_
   } else if (s.num_updates >= s.max_updates &&
              (!s.dynamic_period || s.last_fact_dtime < s.r1_dtime)) {
     *refactor = 1;  // BasisFactorization::Update (:304-340)
+  } else if (!s.mpf) {
+    ++s.num_updates;  // EtaFactorization::Update (PFI)
+    eta_update(s, leaving_row, s.dir);
+    s.tau_can_opt = 0;
   } else {
     const int right_index = s.right_pool[entering_col];
     const int left_index = s.left_pool[leaving_row];

@@ -272,6 +272,24 @@ struct Lp {
   int32_t* mpf_scratch_nz;  // scratchpad_non_zeros_ (2m)
   int n_mpf_scratch_nz;
 
+  // ---- EtaFactorization (basis_representation.cc:25-176): the product-form
+  // updates used instead of the MPF when use_middle_product_form_update is
+  // false (mpf == 0). Eta k: its column (the leaving row), the pivot, the
+  // dense coefficients (m, eta column zeroed) and, when the direction was
+  // sparse (< 0.5 m non-zeros), its entries in list order.
+  int mpf;
+  int eta_count;
+  int eta_cap;
+  int eta_pad;
+  int32_t* eta_col;
+  f64* eta_piv;
+  f64* eta_dense;          // eta_cap x m
+  int64_t* eta_sp_starts;  // eta_cap + 1; an empty range = the dense loops
+  int32_t* eta_sp_rows;
+  f64* eta_sp_coefs;
+  int64_t eta_sp_cap;
+  f64* pfi_scratch;        // LuFactorization::dense_column_scratchpad_ (m)
+
   // ---- RankOneUpdateFactorization ----
   int32_t* r1_u;
   int32_t* r1_v;

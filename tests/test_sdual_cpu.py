@@ -182,8 +182,33 @@ def test_sdual_restatement_dual_phase1(seed):
         assert plain["status"] == seg["status"]
 
 
+@pytest.mark.parametrize("kind", ["sparse", "phase1", "suite"])
+def test_sdual_restatement_pfi(kind):
+    """The product-form updates (use_middle_product_form_update = false:
+    EtaFactorization, basis_representation.cc:25-176, and the dense LU
+    solves around it) in segments. The suite member runs hundreds of
+    iterations, so segments also end at the eta room and repack the host's
+    etas."""
+    import netlib_suite
+    if kind == "sparse":
+        lps = [lp_gen.random_sparse_lp(60 + 30 * k, 240 + 80 * k, 0.05, 720 + k) for k in range(3)]
+    elif kind == "phase1":
+        lps = [lp_gen.dual_phase1_lp(80 + 40 * k, 300 + 100 * k, 960 + k) for k in range(3)]
+    else:
+        lps = [netlib_suite.suite(max_rows=1500)[63]]
+    p = abi.default_params(use_dual_simplex=1, use_middle_product_form_update=0)
+    for k, lp in enumerate(lps):
+        seg0, it0 = _counters()
+        a, b = _both(lp, p)
+        _assert_same(a, b, (kind, k))
+        seg1, it1 = _counters()
+        assert it1 - it0 > 0
+    if kind == "suite":
+        assert seg1 - seg0 > 8  # the eta room ended segments
+
+
 def test_sdual_restatement_dual_phase1_resume_paths():
-    """Dual phase I through the resume exits (MILP_SDUAL_LU_SLACK: every
+    """Dual phase I (and the PFI updates) through the resume exits (MILP_SDUAL_LU_SLACK: every
     refactorization inside a segment hands the LP back), in a child process."""
     import os
     import subprocess
@@ -196,6 +221,9 @@ def test_sdual_restatement_dual_phase1_resume_paths():
         "    lp = lp_gen.dual_phase1_lp(100 + 40 * seed, 400, 950 + seed)\n"
         "    a, b = t._both(lp, abi.default_params(use_dual_simplex=1))\n"
         "    t._assert_same(a, b, seed)\n"
+        "    p = abi.default_params(use_dual_simplex=1, use_middle_product_form_update=0)\n"
+        "    a, b = t._both(lp, p)\n"
+        "    t._assert_same(a, b, ('pfi', seed))\n"
         "print('ok')\n") % (sys.path[:6],)
     env = dict(os.environ, MILP_SDUAL_LU_SLACK="64")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,

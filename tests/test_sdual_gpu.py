@@ -54,6 +54,22 @@ def test_sdual_dual_phase1_parity(seed, sdual_mode, monkeypatch):
     assert counters[0]["sdual_iterations"] > counters[1]["sdual_iterations"], counters
 
 
+@pytest.mark.parametrize("kind", ["sparse", "phase1"])
+def test_sdual_pfi_parity(kind, sdual_mode):
+    """The product-form (eta) updates, use_middle_product_form_update = false
+    (basis_representation.cc:25-176), in segments on one workgroup: the
+    whole final state equals the oracle's."""
+    if kind == "sparse":
+        lp = lp_gen.random_sparse_lp(160, 600, 0.04, 731)
+    else:
+        lp = lp_gen.dual_phase1_lp(200, 700, 961)
+    p = abi.default_params(use_dual_simplex=1, use_middle_product_form_update=0)
+    o, ro, g, rg = parity_util.solve_both(lp, p, lambda q: engine.LpHandle(q, 0))
+    parity_util.compare(o, ro, g, rg, lp)
+    c = g.run_counters()
+    assert c["sdual_segments"] > 0 and c["sdual_iterations"] > 0, c
+
+
 def test_sdual_dual_phase1_batch():
     """Phase-I LPs through the batch API (the pool kernel on the device, 4
     workers): each result equals the oracle solving it alone."""
