@@ -182,7 +182,7 @@ def test_sdual_restatement_dual_phase1(seed):
         assert plain["status"] == seg["status"]
 
 
-@pytest.mark.parametrize("kind", ["sparse", "phase1", "suite"])
+@pytest.mark.parametrize("kind", ["sparse", "phase1", "suite", "primal"])
 def test_sdual_restatement_pfi(kind):
     """The product-form updates (use_middle_product_form_update = false:
     EtaFactorization, basis_representation.cc:25-176, and the dense LU
@@ -194,14 +194,17 @@ def test_sdual_restatement_pfi(kind):
         lps = [lp_gen.random_sparse_lp(60 + 30 * k, 240 + 80 * k, 0.05, 720 + k) for k in range(3)]
     elif kind == "phase1":
         lps = [lp_gen.dual_phase1_lp(80 + 40 * k, 300 + 100 * k, 960 + k) for k in range(3)]
-    else:
+    elif kind == "suite":
         lps = [netlib_suite.suite(max_rows=1500)[63]]
-    p = abi.default_params(use_dual_simplex=1, use_middle_product_form_update=0)
+    else:  # the primal loop's segments (Glop's default algorithm)
+        lps = [lp_gen.random_sparse_lp(90, 320, 0.05, 721), netlib_suite.suite(max_rows=1500)[45]]
+    p = abi.default_params(use_dual_simplex=0 if kind == "primal" else 1,
+                           use_middle_product_form_update=0)
     for k, lp in enumerate(lps):
-        seg0, it0 = _counters()
+        seg0, it0 = _counters(primal=kind == "primal")
         a, b = _both(lp, p)
         _assert_same(a, b, (kind, k))
-        seg1, it1 = _counters()
+        seg1, it1 = _counters(primal=kind == "primal")
         assert it1 - it0 > 0
     if kind == "suite":
         assert seg1 - seg0 > 8  # the eta room ended segments

@@ -41,6 +41,16 @@ def test_sprimal_single_lp_parity(seed, sprimal_mode):
     _check_ran(g, sprimal_mode)
 
 
+def test_sprimal_pfi_parity(sprimal_mode):
+    """The primal loop with product-form (eta) updates,
+    use_middle_product_form_update = false (basis_representation.cc:25-176)."""
+    lp = lp_gen.random_sparse_lp(150, 500, 0.04, 733)
+    p = abi.default_params(use_middle_product_form_update=0)
+    o, ro, g, rg = parity_util.solve_both(lp, p, lambda q: engine.LpHandle(q, 0))
+    parity_util.compare(o, ro, g, rg, lp)
+    _check_ran(g, sprimal_mode)
+
+
 def test_sprimal_kats(sprimal_mode):
     """Known-answer LPs (optimal, infeasible, unbounded) through the primal
     loop with segments on."""
