@@ -6287,11 +6287,23 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
   // MILP_BATCH_FIBERS=k (default 4), MILP_SMALL_BATCH=0 turns batching off.
   int fibers = 4;
   if (const char* e = std::getenv("MILP_BATCH_FIBERS")) fibers = std::max(1, std::atoi(e));
+  // MILP_BATCH_TRACE: the batch call's phases on stderr (setup, last solve
+  // done, threads joined, teardown).
+  static const bool trace = std::getenv("MILP_BATCH_TRACE") != nullptr;
+  const auto t_start = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!trace) return;
+    std::fprintf(stderr, "[batch] %-22s %9.3f s\n", what,
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
+  };
+  std::atomic<int> solved(0);
   for (int i = 0; i < count; ++i) {
     handles[i]->simplex.SetBatchMode(true);
     handles[i]->simplex.device().SetSmallBatch(true);
   }
-  PoolScope pool_scope(handles, count);
+  mark("batch mode on");
+  auto pool_scope = std::make_unique<PoolScope>(handles, count);
+  mark("pool scope");
   // Largest LPs first (LPT order, weight (nnz + m) * m as in the multi-GPU
   // partition of mi_glop.distributed): the long solves start early instead of
   // forming the tail of the batch.
@@ -6318,6 +6330,7 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
             const int i = order[at];
             (void)hipSetDevice(handles[i]->device);
             RunSolve(handles[i], nullptr, &results[i]);
+            if (solved.fetch_add(1) + 1 == count) mark("last solve done");
           }
         });
       }
@@ -6325,7 +6338,11 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
     });
   }
   for (auto& th : pool) th.join();
+  mark("threads joined");
   for (int i = 0; i < count; ++i) SetSmallBatchSafe(handles[i], false);
+  mark("batch mode off");
+  pool_scope.reset();
+  mark("pool scope closed");
   return MI_LP_OK;  // per-entry outcomes are in results[i]
 }
 
