@@ -405,6 +405,9 @@ def run_c3(args, rank, world, local_rank, dist, barrier, sync):
     barrier()
     elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, COLL_DEVICE)
     statuses = [r.problem_status for r in res]
+    slow = sorted(range(len(lps)), key=lambda i: -res[i].solve_seconds)[:5]
+    log("c3: slowest LPs: " + ", ".join(
+        f"{lps[i].m}x{lps[i].n} {res[i].iterations} it {res[i].solve_seconds:.2f}s" for i in slow))
     out = {
         "metric": "batched LPs/sec", "unit": "LPs/s", "scaling": "strong",
         "value": len(suite) / elapsed, "lps": len(suite), "lps_this_rank": len(lps),
@@ -454,6 +457,10 @@ def run_c3(args, rank, world, local_rank, dist, barrier, sync):
         with concurrent.futures.ThreadPoolExecutor(args.c3_cpu_threads) as ex:
             ref = list(ex.map(solve_one, suite))
         dt = time.perf_counter() - t
+        slow = sorted(range(len(suite)), key=lambda i: -ref[i].solve_seconds)[:5]
+        log("c3: oracle's slowest LPs: " + ", ".join(
+            f"{suite[i].m}x{suite[i].n} {ref[i].iterations} it {ref[i].solve_seconds:.2f}s"
+            for i in slow))
         if world == 1:
             out["oracle_check"] = oracle_check(res, [ref[i] for i in mine])
         out["cpu_baseline"] = {

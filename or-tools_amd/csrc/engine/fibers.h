@@ -37,6 +37,7 @@ struct Fiber {
   std::function<void()> fn;
   std::unique_ptr<char[]> stack;
   bool done = false;
+  double weight = 0.0;  // SetFiberWeight: the scheduler favours the heaviest
 };
 inline thread_local void** t_sched_sp = nullptr;  // where the scheduler's sp is saved
 inline thread_local Fiber* t_current = nullptr;
@@ -62,6 +63,21 @@ extern "C" inline void milp_fiber_entry(Fiber* f) {
 
 // True inside a fiber of a running pool.
 inline bool InFiber() { return fiber_detail::t_current != nullptr; }
+
+// The current fiber's work estimate (0 = none). A pool gives its heaviest
+// fiber every other slice: a large LP is host-bound and would otherwise get
+// a 1/k share of its thread while the light LPs it shares the thread with
+// mostly wait for the device; the light ones now run in its device waits.
+inline void SetFiberWeight(double w) {
+  if (fiber_detail::t_current != nullptr) fiber_detail::t_current->weight = w;
+}
+inline bool FiberPriorityEnabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MILP_BATCH_PRIORITY");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
 
 // Gives the thread to the next fiber of the pool; returns when this fiber is
 // scheduled again. A no-op outside a pool. idle: the slice since the last
@@ -113,11 +129,11 @@ inline void RunFibers(std::vector<std::function<void()>> tasks, size_t stack_byt
   t_sched_sp = &sched_sp;
   size_t remaining = fibers.size();
   int idle_rounds = 0;
+  const bool priority = FiberPriorityEnabled();
   while (remaining > 0) {
     bool all_idle = true;
-    for (auto& f : fibers) {
-      if (f->done) continue;
-      t_current = f.get();
+    auto run_slice = [&](Fiber* f) {
+      t_current = f;
       t_slice_idle = false;
       const bool prof = SliceProfile();
       const auto s0 = prof ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
@@ -136,7 +152,23 @@ inline void RunFibers(std::vector<std::function<void()>> tasks, size_t stack_byt
       t_current = nullptr;
       if (!t_slice_idle) all_idle = false;
       if (f->done) --remaining;
+    };
+    // The heaviest running fiber (weights are set by the tasks) runs before
+    // every other fiber's slice.
+    Fiber* heavy = nullptr;
+    if (priority) {
+      for (auto& f : fibers) {
+        if (!f->done && f->weight > 0.0 && (heavy == nullptr || f->weight > heavy->weight)) {
+          heavy = f.get();
+        }
+      }
     }
+    for (auto& f : fibers) {
+      if (f->done || f.get() == heavy) continue;
+      if (heavy != nullptr && !heavy->done) run_slice(heavy);
+      run_slice(f.get());
+    }
+    if (heavy != nullptr && !heavy->done) run_slice(heavy);
     idle_rounds = all_idle ? idle_rounds + 1 : 0;
     if (idle_rounds >= 4096) {
       std::this_thread::sleep_for(std::chrono::microseconds(20));  // long device waits

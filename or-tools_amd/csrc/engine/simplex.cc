@@ -6329,7 +6329,9 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
             if (at >= count) break;
             const int i = order[at];
             (void)hipSetDevice(handles[i]->device);
+            milp::SetFiberWeight(weight(i));
             RunSolve(handles[i], nullptr, &results[i]);
+            milp::SetFiberWeight(0.0);
             if (solved.fetch_add(1) + 1 == count) mark("last solve done");
           }
         });
