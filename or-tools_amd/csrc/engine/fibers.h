@@ -170,10 +170,18 @@ inline void RunFibers(std::vector<std::function<void()>> tasks, size_t stack_byt
     }
     if (heavy != nullptr && !heavy->done) run_slice(heavy);
     idle_rounds = all_idle ? idle_rounds + 1 : 0;
+    static const int idle_us = [] {  // MILP_FIBER_IDLE_US=k: sleep k us per idle round
+      const char* e = std::getenv("MILP_FIBER_IDLE_US");
+      return e != nullptr ? std::atoi(e) : 0;
+    }();
     if (idle_rounds >= 4096) {
       std::this_thread::sleep_for(std::chrono::microseconds(20));  // long device waits
     } else if (idle_rounds >= 2) {
-      std::this_thread::yield();
+      if (idle_us > 0) {
+        std::this_thread::sleep_for(std::chrono::microseconds(idle_us));
+      } else {
+        std::this_thread::yield();
+      }
     }
   }
   t_sched_sp = saved_sched;

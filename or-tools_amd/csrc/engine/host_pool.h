@@ -26,17 +26,28 @@
 
 namespace milp {
 
+// A thread that runs one LP of a batch (mi_lp_batch_solve's workers): the
+// batch already keeps every core busy, so its loops run serially instead of
+// waking the pool (whose spinning workers would take cores from the other
+// LPs). The results are the same either way.
+inline thread_local bool t_host_serial = false;
+struct HostSerialScope {
+  bool saved;
+  explicit HostSerialScope(bool on) : saved(t_host_serial) { t_host_serial = on; }
+  ~HostSerialScope() { t_host_serial = saved; }
+};
+
 class HostPool {
  public:
   static HostPool& Get() {
     static HostPool pool;
     return pool;
   }
-  int threads() const { return num_threads_; }
+  int threads() const { return t_host_serial ? 1 : num_threads_; }
 
   // fn(part) for part in [0, parts); part 0 runs on the caller.
   void Run(int parts, const std::function<void(int)>& fn) {
-    if (parts <= 1 || num_threads_ <= 1) {
+    if (parts <= 1 || threads() <= 1) {
       for (int p = 0; p < parts; ++p) fn(p);
       return;
     }

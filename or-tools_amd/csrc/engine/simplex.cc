@@ -6318,9 +6318,15 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
                    [&](int a, int b) { return weight(a) > weight(b); });
   std::atomic<int> next(0);
   std::vector<std::thread> pool;
+  // MILP_BATCH_HOST_POOL=1: the batch's LPs may also use the host pool.
+  static const bool batch_pool = [] {
+    const char* e = std::getenv("MILP_BATCH_HOST_POOL");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
   for (int t = 0; t < num_threads; ++t) {
     pool.emplace_back([&]() {
       milp::SamplerAttachBatchThread();
+      milp::HostSerialScope serial(!batch_pool && num_threads > 1);
       std::vector<std::function<void()>> tasks;
       for (int f = 0; f < fibers; ++f) {
         tasks.push_back([&]() {
