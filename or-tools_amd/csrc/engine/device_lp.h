@@ -225,6 +225,11 @@ class DeviceLp : public DeviceSolver {
   // Batched small-LP launches for this handle (the batch APIs turn it on for
   // their duration; MILP_SMALL_BATCH=1 turns it on everywhere, =0 nowhere).
   void SetSmallBatch(bool on);
+  // A batch's few heaviest LPs take a high-priority stream, so their device
+  // round trips do not queue behind the light LPs' kernels (the suite's wall
+  // is their chain); applied now if the matrix is on the device, else at
+  // its upload. false restores the process default (MILP_STREAM_PRIORITY).
+  void SetBatchPriority(bool high);
   // Batched small LPs whose dual loop runs as a device segment (csrc/sdual):
   // the once-per-solve row sums and column dots outside the loop run on the
   // host thread that owns the LP (Glop's order, the kernels' bits) instead of
@@ -590,6 +595,7 @@ class DeviceLp : public DeviceSolver {
   int tri_persist_groups_ = 0;  // MILP_TRI_PERSIST: persistent sync-free workgroups (0: off)
   int tri_xcd_stride_ = 1;    // MILP_TRI_XCD=1: the persistent ones on one XCD (stride 8)
   bool stream_priority_ = false;  // MILP_STREAM_PRIORITY=1: solver stream high, tau stream low
+  bool stream_priority_env_ = false;  // the process default above, for SetBatchPriority(false)
   bool stream_prioritized_ = false;  // stream_ was created at the highest priority
   void SetStreamPriority(bool high);
   bool tri_lower_ = true;     // MILP_TRI_LOWER: the L solves too

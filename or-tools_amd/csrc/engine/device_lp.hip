@@ -112,6 +112,7 @@ void DeviceLp::Init(int device) {
   // The stream starts at the default priority; UploadMatrix sets it
   // (SetStreamPriority).
   if (const char* v = std::getenv("MILP_STREAM_PRIORITY")) stream_priority_ = std::atoi(v) != 0;
+  stream_priority_env_ = stream_priority_;
   hipStream_t s;
   Check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
   stream_ = s;
@@ -495,6 +496,19 @@ void DeviceLp::SetSmallBatch(bool on) {
   if (!on) WaitSmallBatch();  // the last request completes before single launches resume
   if (const char* v = std::getenv("MILP_SMALL_BATCH")) on = std::atoi(v) != 0;
   small_batch_ = on;
+}
+
+void DeviceLp::SetBatchPriority(bool high) {
+  stream_priority_ = high || stream_priority_env_;
+  if (m_ > 0) SetStreamPriority(stream_priority_);
+  // A prioritized LP launches its own kernels on its stream instead of
+  // joining the batched launches (whose cycle is set by the light LPs'
+  // requests); MILP_BATCH_PRIORITY_DIRECT=0 keeps it in the batches.
+  static const bool direct = [] {
+    const char* e = std::getenv("MILP_BATCH_PRIORITY_DIRECT");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  if (high && direct) SetSmallBatch(false);
 }
 
 void DeviceLp::WaitSmallBatch() {

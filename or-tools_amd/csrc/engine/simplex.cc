@@ -6316,6 +6316,20 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
   };
   std::stable_sort(order.begin(), order.end(),
                    [&](int a, int b) { return weight(a) > weight(b); });
+  // The heaviest LPs (MILP_BATCH_PRIORITY_LPS, default 4) on high-priority
+  // streams: their chains set the batch's wall.
+  static const int priority_lps = [] {
+    const char* e = std::getenv("MILP_BATCH_PRIORITY_LPS");
+    return e != nullptr ? std::max(0, std::atoi(e)) : 4;
+  }();
+  const int prioritized = count > num_threads ? std::min(priority_lps, count) : 0;
+  for (int k = 0; k < prioritized; ++k) {
+    try {
+      handles[order[k]]->simplex.device().SetBatchPriority(true);
+    } catch (const std::exception& e) {
+      handles[order[k]]->error = e.what();
+    }
+  }
   std::atomic<int> next(0);
   std::vector<std::thread> pool;
   // MILP_BATCH_HOST_POOL=1: the batch's LPs may also use the host pool.
@@ -6347,6 +6361,13 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
   }
   for (auto& th : pool) th.join();
   mark("threads joined");
+  for (int k = 0; k < prioritized; ++k) {
+    try {
+      handles[order[k]]->simplex.device().SetBatchPriority(false);
+    } catch (const std::exception& e) {
+      handles[order[k]]->error = e.what();
+    }
+  }
   for (int i = 0; i < count; ++i) SetSmallBatchSafe(handles[i], false);
   mark("batch mode off");
   pool_scope.reset();
