@@ -467,6 +467,10 @@ void DeviceLp::LaunchSmall(int kind, const Args& args) {
         e = milp_launch::list_dots_small(
             reinterpret_cast<const milp_kernels::ListDotsSmallArgs&>(args), S(stream_));
         break;
+      case milp_kernels::kMediumListDots:
+        e = milp_launch::list_dots_medium(
+            reinterpret_cast<const milp_kernels::ListDotsSmallArgs&>(args), S(stream_));
+        break;
       default:
         e = milp_launch::row_wise_update_small_by_column(
             reinterpret_cast<const milp_kernels::RowWiseSmallColArgs&>(args), S(stream_));
@@ -1411,8 +1415,9 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
   }
   fused_ready_ = false;
   if (small_fused_enabled_ && h_small_in_ != nullptr && nd_ == 0 &&
-      m_ <= milp_kernels::kSmallLdsCols) {
-    // Small LP: one launch, v in and the dots out through mapped host memory.
+      (m_ <= milp_kernels::kSmallLdsCols || (medium_ && m_ <= milp_kernels::kMediumListRows))) {
+    // Small or mid-size LP: one launch, v in and the dots out through mapped
+    // host memory.
     if (small_inflight_) Synchronize();
     std::memcpy(h_small_y_, v.data(), m_ * sizeof(double));
     milp_kernels::ListDotsSmallArgs a{};
@@ -1425,7 +1430,9 @@ void DeviceLp::ListDotsOverUpdateRow(const std::vector<double>& v, std::vector<d
     a.n = n;
     a.out = d_small_out_;
     BeginKernel(MI_K_PRIMAL_NORMS);
-    LaunchSmall(milp_kernels::kSmallListDots, a);
+    LaunchSmall(m_ <= milp_kernels::kSmallLdsCols ? milp_kernels::kSmallListDots
+                                                  : milp_kernels::kMediumListDots,
+                a);
     EndKernel(MI_K_PRIMAL_NORMS, 12.0 * double(list_entries_) + 8.0 * m_ + 4.0 * n + 8.0 * n);
     Synchronize();
     std::memcpy(out->data(), h_small_out_, n * sizeof(double));

@@ -272,7 +272,11 @@ struct RowSumArgs {
 // Batched small-LP launches (simplex_kernels.hip small_batch_kernel): one
 // request per LP in a slot of mapped host memory.
 enum SmallKind { kSmallRowWise = 0, kSmallColWise = 1, kSmallListDots = 2,
-                 kSmallRowWiseByColumn = 3, kMediumRowWise = 4, kSmallKinds = 5 };
+                 kSmallRowWiseByColumn = 3, kMediumRowWise = 4, kMediumListDots = 5,
+                 kSmallKinds = 6 };
+// The list dots of mid-size LPs (kMediumListDots): y (m <= kMediumListRows,
+// 128 KB) staged in LDS as the small kind does.
+constexpr int kMediumListRows = 16384;
 struct SmallSlot {
   unsigned long long seq;  // published to done[slot] when the request is finished
   int kind;
@@ -423,6 +427,7 @@ hipError_t row_wise_update_small(const milp_kernels::RowWiseSmallArgs& args, int
 hipError_t row_wise_update_medium(const milp_kernels::RowWiseSmallArgs& args, hipStream_t s);
 hipError_t small_batch(int kind, const milp_kernels::SmallBatchArgs& args, hipStream_t s);
 hipError_t list_dots_small(const milp_kernels::ListDotsSmallArgs& args, hipStream_t s);
+hipError_t list_dots_medium(const milp_kernels::ListDotsSmallArgs& args, hipStream_t s);
 hipError_t row_wise_update_small_by_column(const milp_kernels::RowWiseSmallColArgs& args,
                                            hipStream_t s);
 hipError_t column_wise_update_small(const milp_kernels::ColWiseSmallArgs& args, hipStream_t s);

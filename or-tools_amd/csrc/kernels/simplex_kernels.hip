@@ -941,9 +941,10 @@ __global__ __launch_bounds__(kCompactThreads) void column_wise_small_kernel(ColW
 }
 
 // Small LPs: the primal edge-norm dots over the update-row list in one launch
-// (ListDotsSmallArgs), one thread per listed column.
-__device__ __forceinline__ void list_dots_small_body(const ListDotsSmallArgs& a) {
-  __shared__ double s_y[kSmallLdsCols];
+// (ListDotsSmallArgs), one thread per listed column; y (m <= kRows) in LDS.
+template <int kRows>
+__device__ __forceinline__ void list_dots_body(const ListDotsSmallArgs& a) {
+  __shared__ double s_y[kRows];
   const int t = threadIdx.x;
   for (int i = t; i < a.m; i += kCompactThreads) s_y[i] = a.y[i];
   __syncthreads();
@@ -954,7 +955,12 @@ __device__ __forceinline__ void list_dots_small_body(const ListDotsSmallArgs& a)
 }
 
 __global__ __launch_bounds__(kCompactThreads) void list_dots_small_kernel(ListDotsSmallArgs a) {
-  list_dots_small_body(a);
+  list_dots_body<kSmallLdsCols>(a);
+}
+
+// Mid-size LPs (kSmallLdsCols < m <= kMediumListRows): the same with 128 KB of y.
+__global__ __launch_bounds__(kCompactThreads) void list_dots_medium_kernel(ListDotsSmallArgs a) {
+  list_dots_body<kMediumListRows>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -1162,7 +1168,10 @@ __global__ __launch_bounds__(kCompactThreads) void small_batch_kernel(SmallBatch
     row_wise_medium_body(a);
   } else if constexpr (KIND == kSmallListDots) {
     const ListDotsSmallArgs a = s_slot.ld;
-    list_dots_small_body(a);
+    list_dots_body<kSmallLdsCols>(a);
+  } else if constexpr (KIND == kMediumListDots) {
+    const ListDotsSmallArgs a = s_slot.ld;
+    list_dots_body<kMediumListRows>(a);
   } else {
     const RowWiseSmallColArgs a = s_slot.rc;
     row_wise_small_by_column_body(a);
@@ -1703,6 +1712,9 @@ hipError_t small_batch(int kind, const SmallBatchArgs& args, hipStream_t s) {
     case kMediumRowWise:
       small_batch_kernel<kMediumRowWise><<<args.count, kCompactThreads, 0, s>>>(args);
       break;
+    case kMediumListDots:
+      small_batch_kernel<kMediumListDots><<<args.count, kCompactThreads, 0, s>>>(args);
+      break;
     default:
       return hipErrorInvalidValue;
   }
@@ -1721,6 +1733,12 @@ hipError_t row_wise_update_medium(const RowWiseSmallArgs& args, hipStream_t s) {
 hipError_t list_dots_small(const ListDotsSmallArgs& args, hipStream_t s) {
   if (args.m > kSmallLdsCols || args.n < 1) return hipErrorInvalidValue;
   list_dots_small_kernel<<<1, kCompactThreads, 0, s>>>(args);
+  return hipGetLastError();
+}
+
+hipError_t list_dots_medium(const ListDotsSmallArgs& args, hipStream_t s) {
+  if (args.m > kMediumListRows || args.n < 1) return hipErrorInvalidValue;
+  list_dots_medium_kernel<<<1, kCompactThreads, 0, s>>>(args);
   return hipGetLastError();
 }
 
