@@ -324,12 +324,20 @@ class SmallBatcher {
  private:
   void CreateStreams() {
     (void)hipSetDevice(device_);
+    if (const char* e = std::getenv("MILP_SMALL_BATCH_STREAMS")) {
+      streams_used_ = std::max(1, std::min(kStreams, std::atoi(e)));
+    }
     for (int i = 0; i < kStreams; ++i) {
       hipStream_t st;
       if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
         throw DeviceError("small batch: stream");
       }
       streams_[i] = st;
+      if (events_[i] == nullptr &&
+          hipEventCreateWithFlags(&events_[i], hipEventDisableTiming) != hipSuccess) {
+        throw DeviceError("small batch: event");
+      }
+      in_flight_[i] = false;
     }
   }
   static std::mutex& RegistryMutex() {
@@ -341,17 +349,32 @@ class SmallBatcher {
     return *all;
   }
   // The launcher: takes every pending request, launches one kernel per kind
-  // (a workgroup per request), waits for it, repeats. With one batch in
-  // flight the requests of the other LPs gather while it runs, so a batch
-  // holds as many requests as LPs that reached their update row meanwhile.
+  // (a workgroup per request) on one of its streams, repeats. Up to
+  // `streams_used_` batches are in flight (MILP_SMALL_BATCH_STREAMS, default
+  // 4): a request that arrives while batches run is launched at once on a
+  // free stream instead of waiting for the running batch (whose time is its
+  // slowest request: the mid-size LPs' update rows made every small LP wait
+  // for them). With every stream busy the launcher waits for the oldest
+  // batch; meanwhile the other LPs' requests gather into the next one.
   void LauncherLoop() {
     (void)hipSetDevice(device_);
     std::vector<int> batch[milp_kernels::kSmallKinds];
+    int next = 0;
     while (true) {
       {
         std::unique_lock<std::mutex> lock(mu_);
         cv_.wait(lock, [&] { return stop_ || num_pending_ > 0; });
-        if (stop_ && num_pending_ == 0) return;
+        if (stop_ && num_pending_ == 0) break;
+      }
+      // A free stream: the next in turn, once its last batch has completed.
+      const int s = next;
+      next = (next + 1) % streams_used_;
+      if (in_flight_[s]) {
+        (void)hipEventSynchronize(events_[s]);
+        in_flight_[s] = false;
+      }
+      {
+        std::lock_guard<std::mutex> lock(mu_);
         for (int k = 0; k < milp_kernels::kSmallKinds; ++k) {
           batch[k].swap(pending_[k]);
           pending_[k].clear();
@@ -367,13 +390,21 @@ class SmallBatcher {
           a.count = static_cast<int>(
               std::min<size_t>(milp_kernels::kSmallBatchMax, batch[k].size() - at));
           for (int i = 0; i < a.count; ++i) a.ids[i] = batch[k][at + i];
-          if (milp_launch::small_batch(k, a, streams_[0]) != hipSuccess) failed = true;
+          if (milp_launch::small_batch(k, a, streams_[s]) != hipSuccess) failed = true;
         }
         batch[k].clear();
       }
       // A failed launch leaves its requests without a done word: their
       // owners time out and report a DeviceError.
-      (void)hipStreamSynchronize(streams_[0]);
+      if (hipEventRecord(events_[s], streams_[s]) == hipSuccess) {
+        in_flight_[s] = true;
+      } else {
+        (void)hipStreamSynchronize(streams_[s]);
+      }
+    }
+    for (int s = 0; s < streams_used_; ++s) {
+      if (in_flight_[s]) (void)hipEventSynchronize(events_[s]);
+      in_flight_[s] = false;
     }
   }
 
@@ -401,8 +432,11 @@ class SmallBatcher {
     launcher_ = std::thread([this] { LauncherLoop(); });
   }
   int device_;
-  static constexpr int kStreams = 1;
+  static constexpr int kStreams = 8;
+  int streams_used_ = 4;
   hipStream_t streams_[kStreams] = {};
+  hipEvent_t events_[kStreams] = {};  // each stream's last batch
+  bool in_flight_[kStreams] = {};
   std::mutex mu_;
   std::condition_variable cv_;
   std::thread launcher_;
