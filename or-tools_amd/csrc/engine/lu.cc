@@ -1597,6 +1597,22 @@ Fractional BasisFactorization::RightSolveSquaredNorm(const ColumnView& a) const 
   return lu_factorization_.RightSolveSquaredNorm(a);
 }
 
+uint64_t BasisFactorization::FactorizationContentKey() const {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+  mix(static_cast<uint64_t>(compact_matrix_.num_rows()));
+  mix(static_cast<uint64_t>(compact_matrix_.num_cols()));
+  for (const int c : basis_) mix(static_cast<uint32_t>(c));
+  const LuFactorization& lu = lu_factorization_;
+  mix(lu.IsIdentityFactorization() ? 1 : 0);
+  mix(static_cast<uint64_t>(lu.NumberOfEntries()));
+  mix(0x9e3779b97f4a7c15ull);
+  for (const int c : lu.row_perm()) mix(static_cast<uint32_t>(c));
+  mix(0x9e3779b97f4a7c15ull);
+  for (const int c : lu.GetColumnPermutation()) mix(static_cast<uint32_t>(c));
+  return h;
+}
+
 Fractional BasisFactorization::DualEdgeSquaredNorm(int row) const {
   BumpDeterministicTimeForSolve(1);
   return lu_factorization_.DualEdgeSquaredNorm(row);

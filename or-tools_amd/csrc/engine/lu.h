@@ -961,6 +961,7 @@ class LuFactorization {
   void DenseSolve(TriKind kind, const TriangularMatrix& t, int start,
                   std::vector<Fractional>* x) const;
 
+  const std::vector<int>& inverse_col_perm() const { return inverse_col_perm_; }
   // Exposed for the factor-structure parity tests.
   const TriangularMatrix& lower() const { return lower_; }
   const TriangularMatrix& upper() const { return upper_; }
@@ -1263,6 +1264,11 @@ class BasisFactorization {
 
   // basis_representation.cc:607-624 (public: replayed by the GPU paths).
   void BumpDeterministicTimeForSolve(int64_t num_entries) const;
+  // A content key of the current factorization: the basis, the LU's
+  // permutations and entry counts (engine, no Glop counterpart). Handles
+  // that loaded the same matrix with the same LU parameters and hold equal
+  // keys hold the same factorization (Markowitz is deterministic).
+  uint64_t FactorizationContentKey() const;
 
  private:
   Status ComputeFactorization();

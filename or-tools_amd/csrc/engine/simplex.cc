@@ -66,6 +66,7 @@ milp_fiber_trampoline:
 #include "host_pool.h"
 
 #include <chrono>
+#include <mutex>
 
 namespace milp {
 namespace {
@@ -750,6 +751,34 @@ void VariablesInfo::EndDualPhaseI(Fractional tol, const std::vector<Fractional>&
 }
 
 // ---------------------------------------------------------------------------
+// Dual edge norms shared by the handles of one batch call
+// (mi_lp_batch_solve_bounds): the children of a search node start from the
+// same basis of the same matrix, so the first child's norm recompute after
+// the first factorization is every child's. Keyed by the factorization's
+// content; a hit copies the values and replays the loop's deterministic-time
+// bumps, so every result is the one a solve computing its own norms gets.
+struct DualNormCache {
+  std::mutex mu;
+  std::vector<std::pair<uint64_t, std::shared_ptr<const std::vector<Fractional>>>> entries;
+  static constexpr size_t kMaxEntries = 8;
+  std::shared_ptr<const std::vector<Fractional>> Find(uint64_t key) {
+    std::lock_guard<std::mutex> l(mu);
+    for (const auto& e : entries) {
+      if (e.first == key) return e.second;
+    }
+    return nullptr;
+  }
+  void Insert(uint64_t key, const std::vector<Fractional>& v) {
+    std::lock_guard<std::mutex> l(mu);
+    if (entries.size() >= kMaxEntries) return;
+    for (const auto& e : entries) {
+      if (e.first == key) return;
+    }
+    entries.emplace_back(key, std::make_shared<const std::vector<Fractional>>(v));
+  }
+};
+
+// ---------------------------------------------------------------------------
 // DualEdgeNorms (dual_edge_norms.cc)
 class DualEdgeNorms {
   friend struct SdualBridge;
@@ -813,10 +842,27 @@ class DualEdgeNorms {
  private:
   void ComputeEdgeSquaredNorms() {  // dual_edge_norms.cc:120-132
     const int num_rows = bf_.GetNumberOfRows();
+    uint64_t key = 0;
+    if (cache_ != nullptr && bf_.NumUpdates() == 0) {
+      key = bf_.FactorizationContentKey();
+      const auto hit = cache_->Find(key);
+      if (hit != nullptr && static_cast<int>(hit->size()) == num_rows) {
+        norms_ = *hit;
+        for (int row = 0; row < num_rows; ++row) bf_.BumpDeterministicTimeForSolve(1);
+        recompute_ = false;
+        return;
+      }
+    }
     norms_.resize(num_rows, 0.0);
     for (int row = 0; row < num_rows; ++row) norms_[row] = bf_.DualEdgeSquaredNorm(row);
     recompute_ = false;
+    if (key != 0) cache_->Insert(key, norms_);
   }
+ public:
+  void SetCache(DualNormCache* cache) { cache_ = cache; }
+
+ private:
+  DualNormCache* cache_ = nullptr;
   const BasisFactorization& bf_;
   GlopParameters params_;
   bool recompute_ = true;
@@ -3553,6 +3599,8 @@ class RevisedSimplex {
   }
   // Whether this handle's batch solves use the device's segment pool.
   bool UsesSdualPool() const { return batch_depth_ > 0 && sdual_mode_ == 2; }
+  // The batch's shared dual edge norms (DualNormCache), or none.
+  void SetDualNormCache(DualNormCache* cache) { dual_edge_norms_.SetCache(cache); }
   void SdualCounters(int64_t* segments, int64_t* iterations) const {
     *segments = sdual_segments_;
     *iterations = sdual_iterations_;
@@ -6410,9 +6458,17 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
   if (const char* e = std::getenv("MILP_BATCH_THREADS")) {
     threads = std::max(1, std::min(num_workers, std::atoi(e)));
   }
+  // The children share one basis: its dual edge norms are computed once
+  // (MILP_BATCH_SHARED_NORMS=0 lets every child compute its own).
+  static const bool shared_norms = [] {
+    const char* e = std::getenv("MILP_BATCH_SHARED_NORMS");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  milp::DualNormCache norm_cache;
   for (int w = 0; w < num_workers; ++w) {
     workers[w]->simplex.SetBatchMode(true);
     workers[w]->simplex.device().SetSmallBatch(true);
+    if (shared_norms && warm_state != nullptr) workers[w]->simplex.SetDualNormCache(&norm_cache);
   }
   PoolScope pool_scope(workers, num_workers);
   std::atomic<int> next(0);
@@ -6467,7 +6523,10 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
     });
   }
   for (auto& th : pool) th.join();
-  for (int w = 0; w < num_workers; ++w) SetSmallBatchSafe(workers[w], false);
+  for (int w = 0; w < num_workers; ++w) {
+    workers[w]->simplex.SetDualNormCache(nullptr);
+    SetSmallBatchSafe(workers[w], false);
+  }
   return MI_LP_OK;  // per-entry outcomes are in results[i]
 }
 
