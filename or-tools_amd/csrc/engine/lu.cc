@@ -407,6 +407,20 @@ Status LuFactorization::ComputeFactorization(const CompactSparseMatrixView& b) {
   return Status::OK();
 }
 
+void LuFactorization::AdoptFactorizationOf(const LuFactorization& o) {
+  Clear();  // a fresh factorization key
+  is_identity_factorization_ = o.is_identity_factorization_;
+  lower_ = o.lower_;
+  upper_ = o.upper_;
+  transpose_upper_ = o.transpose_upper_;
+  transpose_lower_ = o.transpose_lower_;
+  col_perm_ = o.col_perm_;
+  inverse_col_perm_ = o.inverse_col_perm_;
+  row_perm_ = o.row_perm_;
+  inverse_row_perm_ = o.inverse_row_perm_;
+  markowitz_.CopyStatsFrom(o.markowitz_);
+}
+
 std::vector<int> LuFactorization::ComputeInitialBasis(
     const CompactSparseMatrix& matrix, const std::vector<int>& candidates) {
   CompactSparseMatrixView view{&matrix, &candidates};
@@ -1153,7 +1167,31 @@ Status BasisFactorization::ForceRefactorization() {
 Status BasisFactorization::ComputeFactorization() {
   CompactSparseMatrixView basis_matrix{&compact_matrix_, &basis_};
   const auto t0 = std::chrono::steady_clock::now();
-  const Status status = lu_factorization_.ComputeFactorization(basis_matrix);
+  uint64_t share_key = 0;
+  std::shared_ptr<const LuFactorization> shared;
+  if (lu_share_ != nullptr) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+    mix(static_cast<uint64_t>(compact_matrix_.num_rows()));
+    mix(static_cast<uint64_t>(compact_matrix_.num_cols()));
+    for (const int c : basis_) mix(static_cast<uint32_t>(c));
+    const LuParameters& p = lu_factorization_.parameters();
+    uint64_t bits;
+    std::memcpy(&bits, &p.lu_factorization_pivot_threshold, 8);
+    mix(bits);
+    std::memcpy(&bits, &p.markowitz_singularity_threshold, 8);
+    mix(bits);
+    mix(static_cast<uint64_t>(p.markowitz_zlatev_parameter));
+    share_key = h | 1;
+    shared = lu_share_->Find(share_key);
+  }
+  Status status;
+  if (shared != nullptr) {
+    lu_factorization_.AdoptFactorizationOf(*shared);
+  } else {
+    status = lu_factorization_.ComputeFactorization(basis_matrix);
+    if (share_key != 0 && status.ok()) lu_share_->Insert(share_key, lu_factorization_);
+  }
   ++num_factorizations_;
   factorization_seconds_ +=
       std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

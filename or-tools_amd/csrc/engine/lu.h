@@ -12,6 +12,7 @@
 #include <functional>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 
 #include "device_solver.h"
@@ -868,6 +869,10 @@ class Markowitz {
     return DeterministicTimeForFpOperations(num_fp_operations_);
   }
   void SetParameters(const LuParameters& p) { parameters_ = p; }
+  const LuParameters& parameters() const { return parameters_; }
+  // The operation count of another object's last factorization (an adopted
+  // factorization reports the same deterministic time).
+  void CopyStatsFrom(const Markowitz& o) { num_fp_operations_ = o.num_fp_operations_; }
 
  private:
   void ExtractSingletonColumns(const CompactSparseMatrixView& b,
@@ -951,7 +956,13 @@ class LuFactorization {
     inverse_col_perm_.clear();
   }
   void SetParameters(const LuParameters& p) { markowitz_.SetParameters(p); }
+  const LuParameters& parameters() const { return markowitz_.parameters(); }
   bool IsIdentityFactorization() const { return is_identity_factorization_; }
+  // This object becomes a copy of o's factorization (the factors, their
+  // transposes, the permutations and the last factorization's operation
+  // count) under a fresh factorization key: what ComputeFactorization of
+  // the same basis matrix with the same parameters would have produced.
+  void AdoptFactorizationOf(const LuFactorization& o);
   // Dense U solves of the solver's thread go to this device (engine
   // substitution, bit-identical; see device_solver.h).
   void SetDeviceSolver(DeviceSolver* d) { device_solver_ = d; }
@@ -1269,6 +1280,10 @@ class BasisFactorization {
   // that loaded the same matrix with the same LU parameters and hold equal
   // keys hold the same factorization (Markowitz is deterministic).
   uint64_t FactorizationContentKey() const;
+  // Factorizations shared by the handles of one batch call (LuShareCache,
+  // engine only): a fresh factorization of a basis the cache holds adopts
+  // the cached factors instead of running Markowitz.
+  void SetLuShareCache(struct LuShareCache* c) { lu_share_ = c; }
 
  private:
   Status ComputeFactorization();
@@ -1316,6 +1331,36 @@ class BasisFactorization {
   LuFactorization lu_factorization_;
   double last_factorization_deterministic_time_ = 0.0;
   mutable double deterministic_time_ = 0.0;
+  struct LuShareCache* lu_share_ = nullptr;
+};
+
+// Factorizations of one batch call's handles (mi_lp_batch_solve_bounds: the
+// children of a node load the same matrix and start from the same basis),
+// keyed by the basis matrix's columns, its size and the LU parameters.
+struct LuShareCache {
+  std::mutex mu;
+  std::vector<std::pair<uint64_t, std::shared_ptr<const LuFactorization>>> entries;
+  static constexpr size_t kMaxEntries = 4;
+  std::shared_ptr<const LuFactorization> Find(uint64_t key) {
+    std::lock_guard<std::mutex> l(mu);
+    for (const auto& e : entries) {
+      if (e.first == key) return e.second;
+    }
+    return nullptr;
+  }
+  void Insert(uint64_t key, const LuFactorization& lu) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (entries.size() >= kMaxEntries) return;
+      for (const auto& e : entries) {
+        if (e.first == key) return;
+      }
+    }
+    auto copy = std::make_shared<LuFactorization>();
+    copy->AdoptFactorizationOf(lu);
+    std::lock_guard<std::mutex> l(mu);
+    if (entries.size() < kMaxEntries) entries.emplace_back(key, std::move(copy));
+  }
 };
 
 }  // namespace milp

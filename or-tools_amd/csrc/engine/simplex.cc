@@ -3601,6 +3601,8 @@ class RevisedSimplex {
   bool UsesSdualPool() const { return batch_depth_ > 0 && sdual_mode_ == 2; }
   // The batch's shared dual edge norms (DualNormCache), or none.
   void SetDualNormCache(DualNormCache* cache) { dual_edge_norms_.SetCache(cache); }
+  // The batch's shared factorizations (LuShareCache), or none.
+  void SetLuShareCache(LuShareCache* cache) { basis_factorization_.SetLuShareCache(cache); }
   void SdualCounters(int64_t* segments, int64_t* iterations) const {
     *segments = sdual_segments_;
     *iterations = sdual_iterations_;
@@ -6464,11 +6466,19 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
     const char* e = std::getenv("MILP_BATCH_SHARED_NORMS");
     return e == nullptr || std::atoi(e) != 0;
   }();
+  // ... and its factorization once (MILP_BATCH_SHARED_LU=0: every child runs
+  // Markowitz on it).
+  static const bool shared_lu = [] {
+    const char* e = std::getenv("MILP_BATCH_SHARED_LU");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
   milp::DualNormCache norm_cache;
+  milp::LuShareCache lu_cache;
   for (int w = 0; w < num_workers; ++w) {
     workers[w]->simplex.SetBatchMode(true);
     workers[w]->simplex.device().SetSmallBatch(true);
     if (shared_norms && warm_state != nullptr) workers[w]->simplex.SetDualNormCache(&norm_cache);
+    if (shared_lu && warm_state != nullptr) workers[w]->simplex.SetLuShareCache(&lu_cache);
   }
   PoolScope pool_scope(workers, num_workers);
   std::atomic<int> next(0);
@@ -6525,6 +6535,7 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
   for (auto& th : pool) th.join();
   for (int w = 0; w < num_workers; ++w) {
     workers[w]->simplex.SetDualNormCache(nullptr);
+    workers[w]->simplex.SetLuShareCache(nullptr);
     SetSmallBatchSafe(workers[w], false);
   }
   return MI_LP_OK;  // per-entry outcomes are in results[i]
