@@ -5153,7 +5153,11 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     }
     clock.Mark(0);
 
-    if (sdual_mode_ != 0) {  // phase II, or dual phase I (sd_run's dual_phase1)
+    // Phase II, or dual phase I (sd_run's dual_phase1) once its prices exist:
+    // a warm start that is dual feasible ends phase I at its first leaving
+    // choice, which stays on the host (a segment would be one more round
+    // trip per child for that one scan).
+    if (sdual_mode_ != 0 && (!feasibility_phase || !dual_pricing_vector_.empty())) {
       Status sd_status;
       int sd;
       do {
