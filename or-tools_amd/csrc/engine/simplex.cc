@@ -6464,17 +6464,17 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
   if (const char* e = std::getenv("MILP_BATCH_THREADS")) {
     threads = std::max(1, std::min(num_workers, std::atoi(e)));
   }
-  // The children share one basis: its dual edge norms are computed once
-  // (MILP_BATCH_SHARED_NORMS=0 lets every child compute its own).
+  // The children share one basis: MILP_BATCH_SHARED_NORMS=1 computes its
+  // dual edge norms once, MILP_BATCH_SHARED_LU=1 its factorization once
+  // (opt-in until measured on the GPU; every child computes its own by
+  // default).
   static const bool shared_norms = [] {
     const char* e = std::getenv("MILP_BATCH_SHARED_NORMS");
-    return e == nullptr || std::atoi(e) != 0;
+    return e != nullptr && std::atoi(e) != 0;
   }();
-  // ... and its factorization once (MILP_BATCH_SHARED_LU=0: every child runs
-  // Markowitz on it).
   static const bool shared_lu = [] {
     const char* e = std::getenv("MILP_BATCH_SHARED_LU");
-    return e == nullptr || std::atoi(e) != 0;
+    return e != nullptr && std::atoi(e) != 0;
   }();
   milp::DualNormCache norm_cache;
   milp::LuShareCache lu_cache;
