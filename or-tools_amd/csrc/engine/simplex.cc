@@ -6467,15 +6467,13 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
   // The children share one basis: MILP_BATCH_SHARED_NORMS=1 computes its
   // dual edge norms once, MILP_BATCH_SHARED_LU=1 its factorization once
   // (opt-in until measured on the GPU; every child computes its own by
-  // default).
-  static const bool shared_norms = [] {
-    const char* e = std::getenv("MILP_BATCH_SHARED_NORMS");
+  // default). Read per call (tests switch them).
+  auto env_on = [](const char* name) {
+    const char* e = std::getenv(name);
     return e != nullptr && std::atoi(e) != 0;
-  }();
-  static const bool shared_lu = [] {
-    const char* e = std::getenv("MILP_BATCH_SHARED_LU");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
+  };
+  const bool shared_norms = env_on("MILP_BATCH_SHARED_NORMS");
+  const bool shared_lu = env_on("MILP_BATCH_SHARED_LU");
   milp::DualNormCache norm_cache;
   milp::LuShareCache lu_cache;
   for (int w = 0; w < num_workers; ++w) {
