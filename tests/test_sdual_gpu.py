@@ -3,6 +3,7 @@ phase-II dual iterations run whole on one workgroup, the host engine keeps the
 factorizations and the loop's other branches. Every result must equal the
 oracle's bit for bit, and the segments must have run on the device."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -128,6 +129,9 @@ def test_sdual_children_parity(shape, sdual_mode):
     assert segs > 0
 
 
+@pytest.mark.skipif(os.environ.get("MILP_TEST_SHARED_CACHES") != "1",
+                    reason="opt-in batch caches (MILP_BATCH_SHARED_LU/_NORMS) not yet run on a "
+                           "GPU; MILP_TEST_SHARED_CACHES=1 runs this check")
 @pytest.mark.parametrize("shape", [(6, 6), (15, 10)])
 def test_sdual_children_shared_caches(shape, monkeypatch):
     """A node's children with the shared first factorization and dual edge
