@@ -5153,11 +5153,10 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     }
     clock.Mark(0);
 
-    // Phase II, or dual phase I (sd_run's dual_phase1) once its prices exist:
-    // a warm start that is dual feasible ends phase I at its first leaving
-    // choice, which stays on the host (a segment would be one more round
-    // trip per child for that one scan).
-    if (sdual_mode_ != 0 && (!feasibility_phase || !dual_pricing_vector_.empty())) {
+    // Phase II, or dual phase I (sd_run's dual_phase1). A warm start's phase
+    // I begins with the reduced costs to recompute, which keeps its first
+    // leaving choice on the host (SdualBridge::Supported).
+    if (sdual_mode_ != 0) {
       Status sd_status;
       int sd;
       do {
