@@ -182,6 +182,24 @@ def test_sdual_restatement_dual_phase1(seed):
         assert plain["status"] == seg["status"]
 
 
+@pytest.mark.parametrize("cap", [1, 5, 37])
+def test_sdual_restatement_dual_phase1_caps(cap):
+    """Dual phase I stopped by an iteration cap inside a segment
+    (kExitReturnOk in the phase-I loop) and the solve's status after it,
+    for the MPF and the PFI updates; a minimization with the costs negated
+    runs the same phase from the other side."""
+    lp = lp_gen.dual_phase1_lp(120, 420, 977)
+    flipped = lp_gen.dual_phase1_lp(120, 420, 977)
+    flipped.obj = -flipped.obj
+    flipped.maximize = False
+    for case, q in (("max", lp), ("min", flipped)):
+        for mpf in (1, 0):
+            p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=cap,
+                                   use_middle_product_form_update=mpf)
+            a, b = _both(q, p)
+            _assert_same(a, b, (case, mpf, cap))
+
+
 @pytest.mark.parametrize("kind", ["sparse", "phase1", "suite", "primal"])
 def test_sdual_restatement_pfi(kind):
     """The product-form updates (use_middle_product_form_update = false:
