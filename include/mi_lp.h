@@ -438,6 +438,18 @@ typedef struct mi_lp_solver_params {
   int32_t cost_scaling;                     /* 60, CONTAIN_ONE_COST_SCALING */
   int32_t provide_strong_optimal_guarantee; /* 24, true */
   double max_valid_magnitude;               /* 199, 1e30 */
+  /* Presolve: MainLpPreprocessor's passes (preprocessor.cc:76-147). Glop's
+   * default for use_preprocessing is true; this layer's default is 0 (scaling
+   * only) until the presolve path has run on the GPU box, see DESIGN.md §4e. */
+  int32_t use_preprocessing;                /* 34 */
+  int32_t use_implied_free_preprocessor;    /* 67, true */
+  int32_t solve_dual_problem;               /* 20, LET_SOLVER_DECIDE (ALWAYS_DO 0,
+                                               NEVER_DO 1, LET_SOLVER_DECIDE 2) */
+  int32_t reserved0;
+  double dualizer_threshold;                /* 21, 1.5 */
+  double preprocessor_zero_tolerance;       /* 39, 1e-9 */
+  double solution_feasibility_tolerance;    /* 22, 1e-6 */
+  double drop_tolerance;                    /* 52, 1e-14 */
 } mi_lp_solver_params;
 void mi_lp_solver_params_default(mi_lp_solver_params* p);
 /* ScalingPreprocessor::Run alone, in place on the caller's arrays (no device
@@ -457,6 +469,61 @@ int mi_lp_solver_solve(mi_lp* h, const mi_lp_solver_params* sp, int32_t m, int32
                        double obj_scale, int32_t maximize, const volatile int32_t* interrupt,
                        mi_lp_result* out, double* primal, double* duals, double* reduced_costs,
                        double* activities, int8_t* var_status, int8_t* cons_status);
+
+/* The same LPSolver flow with the simplex supplied by the caller
+ * (LPSolver::RunRevisedSimplexIfNeeded, lp_solver.cc:591-658, is the call
+ * site): fn receives the presolved and scaled LP, fills out (problem_status,
+ * iterations, error_code) and the solution arrays (n primal values, m dual
+ * values, n variable and m constraint statuses) and returns MI_LP_OK or an
+ * error code, which is passed through. mi_lp_solver_solve is this with the
+ * engine's handle behind fn. */
+typedef int (*mi_lp_simplex_fn)(void* user, int32_t m, int32_t n, const int64_t* col_starts,
+                                const int32_t* row_idx, const double* vals,
+                                const double* col_lb, const double* col_ub,
+                                const double* row_lb, const double* row_ub, const double* obj,
+                                double obj_offset, double obj_scale, int32_t maximize,
+                                mi_lp_result* out, double* primal, double* duals,
+                                int8_t* var_status, int8_t* cons_status);
+int mi_lp_solver_solve_with(mi_lp_simplex_fn fn, void* user, const mi_lp_solver_params* sp,
+                            int32_t m, int32_t n, const int64_t* col_starts,
+                            const int32_t* row_idx, const double* vals, const double* col_lb,
+                            const double* col_ub, const double* row_lb, const double* row_ub,
+                            const double* obj, double obj_offset, double obj_scale,
+                            int32_t maximize, mi_lp_result* out, double* primal, double* duals,
+                            double* reduced_costs, double* activities, int8_t* var_status,
+                            int8_t* cons_status);
+
+/* Presolve alone (host only, no device needed): MainLpPreprocessor's passes
+ * (glop/preprocessor.cc:76-147, without the scaling) on a copy of the LP, and
+ * DestructiveRecoverSolution (:203-209) for a solution of the presolved LP.
+ *   mi_presolve_run       *status = Glop's status after presolve (MI_LP_INIT:
+ *                         the simplex must run on the presolved LP)
+ *   mi_presolve_dims      presolved sizes and direction (the dualizer turns
+ *                         the LP into a maximization)
+ *   mi_presolve_get       the presolved LP (any pointer may be NULL)
+ *   mi_presolve_recover   solution of the presolved LP (its sizes) -> solution
+ *                         of the original LP (original sizes); *status in/out
+ *                         (the dualizer maps primal/dual statuses); once only
+ *   mi_presolve_pass_name the passes that changed the LP, in order */
+typedef struct mi_presolve mi_presolve;
+mi_presolve* mi_presolve_create(void);
+void mi_presolve_destroy(mi_presolve* ps);
+int mi_presolve_run(mi_presolve* ps, const mi_lp_solver_params* sp, int32_t m, int32_t n,
+                    const int64_t* col_starts, const int32_t* row_idx, const double* vals,
+                    const double* col_lb, const double* col_ub, const double* row_lb,
+                    const double* row_ub, const double* obj, double obj_offset, double obj_scale,
+                    int32_t maximize, int32_t* status);
+int mi_presolve_dims(const mi_presolve* ps, int32_t* m, int32_t* n, int64_t* nnz,
+                     int32_t* maximize);
+int mi_presolve_get(const mi_presolve* ps, int64_t* col_starts, int32_t* row_idx, double* vals,
+                    double* col_lb, double* col_ub, double* row_lb, double* row_ub, double* obj,
+                    double* obj_offset, double* obj_scale);
+int mi_presolve_recover(mi_presolve* ps, int32_t* status, const double* primal,
+                        const double* duals, const int8_t* var_status, const int8_t* cons_status,
+                        double* primal_out, double* duals_out, int8_t* var_status_out,
+                        int8_t* cons_status_out);
+int32_t mi_presolve_num_passes(const mi_presolve* ps);
+const char* mi_presolve_pass_name(const mi_presolve* ps, int32_t i);
 
 #ifdef __cplusplus
 }

@@ -23,10 +23,12 @@
 #include <cstring>
 #include <exception>
 #include <limits>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../../include/mi_lp.h"
+#include "presolve.h"
 
 namespace milp {
 namespace {
@@ -324,6 +326,182 @@ bool IsValid(const ScaledLp& lp, double max_magnitude) {
   return true;
 }
 
+// LPSolver::IsProblemSolutionConsistent (lp_solver.cc:679-790).
+bool IsSolutionConsistent(const ScaledLp& lp, const presolve::Solution& s) {
+  if (s.status != MI_LP_OPTIMAL && s.status != MI_LP_PRIMAL_FEASIBLE &&
+      s.status != MI_LP_DUAL_FEASIBLE) {
+    return true;
+  }
+  auto within = [](double x, double y, double tol) {  // AreWithinAbsoluteTolerance
+    if (std::isinf(x) || std::isinf(y)) return x == y;
+    return std::fabs(x - y) <= tol;
+  };
+  int64_t num_basic = 0;
+  for (int c = 0; c < lp.n; ++c) {
+    const double value = s.primal[c];
+    const double lb = lp.col_lb[c];
+    const double ub = lp.col_ub[c];
+    switch (s.vstat[c]) {
+      case MI_LP_BASIC:
+        ++num_basic;
+        break;
+      case MI_LP_FIXED_VALUE:
+        if (value != ub && value != lb) return false;
+        break;
+      case MI_LP_AT_LOWER_BOUND:
+        if (value != lb || lb == ub) return false;
+        break;
+      case MI_LP_AT_UPPER_BOUND:
+        if (!within(value, ub, 1e-7) || lb == ub) return false;
+        break;
+      case MI_LP_FREE:
+        if (lb != -kInf || ub != kInf || value != 0.0) return false;
+        break;
+      default:
+        return false;
+    }
+  }
+  for (int r = 0; r < lp.m; ++r) {
+    const double dual = s.dual[r];
+    const double lb = lp.row_lb[r];
+    const double ub = lp.row_ub[r];
+    switch (s.cstat[r]) {
+      case MI_LP_BASIC:
+        if (dual != 0.0) return false;
+        ++num_basic;
+        break;
+      case MI_LP_FIXED_VALUE:
+        if (ub - lb > 1e-12) return false;
+        break;
+      case MI_LP_AT_LOWER_BOUND:
+        if (lb == -kInf) return false;
+        break;
+      case MI_LP_AT_UPPER_BOUND:
+        if (ub == kInf) return false;
+        break;
+      case MI_LP_FREE:
+        if (dual != 0.0) return false;
+        if (lb != -kInf || ub != kInf) return false;
+        break;
+      default:
+        return false;
+    }
+  }
+  return num_basic == lp.m;
+}
+
+presolve::Params PresolveParamsOf(const mi_lp_solver_params& sp) {
+  presolve::Params p;
+  p.use_preprocessing = sp.use_preprocessing != 0;
+  p.use_implied_free_preprocessor = sp.use_implied_free_preprocessor != 0;
+  p.solve_dual_problem = sp.solve_dual_problem;
+  p.dualizer_threshold = sp.dualizer_threshold;
+  p.preprocessor_zero_tolerance = sp.preprocessor_zero_tolerance;
+  p.solution_feasibility_tolerance = sp.solution_feasibility_tolerance;
+  p.drop_tolerance = sp.drop_tolerance;
+  return p;
+}
+
+presolve::Lp ToPresolveLp(const ScaledLp& s, bool maximize) {
+  presolve::Lp lp;
+  lp.num_rows = s.m;
+  lp.cols.resize(s.n);
+  for (int c = 0; c < s.n; ++c) {
+    for (int64_t k = s.starts[c]; k < s.starts[c + 1]; ++k) {
+      lp.cols[c].push_back({s.rows[k], s.vals[k]});
+    }
+  }
+  lp.col_lb = s.col_lb;
+  lp.col_ub = s.col_ub;
+  lp.obj = s.obj;
+  lp.row_lb = s.row_lb;
+  lp.row_ub = s.row_ub;
+  lp.offset = s.offset;
+  lp.scale = s.scale;
+  lp.maximize = maximize;
+  return lp;
+}
+
+ScaledLp FromPresolveLp(const presolve::Lp& p) {
+  ScaledLp s;
+  s.m = p.num_rows;
+  s.n = p.num_cols();
+  s.starts.assign(s.n + 1, 0);
+  for (int c = 0; c < s.n; ++c) {
+    s.starts[c + 1] = s.starts[c] + static_cast<int64_t>(p.cols[c].size());
+    for (const presolve::Entry& e : p.cols[c]) {
+      s.rows.push_back(e.index);
+      s.vals.push_back(e.coeff);
+    }
+  }
+  s.col_lb = p.col_lb;
+  s.col_ub = p.col_ub;
+  s.obj = p.obj;
+  s.row_lb = p.row_lb;
+  s.row_ub = p.row_ub;
+  s.offset = p.offset;
+  s.scale = p.scale;
+  return s;
+}
+
+ScaledLp CopyLp(int32_t m, int32_t n, const int64_t* cs, const int32_t* ri, const double* vals,
+                const double* clb, const double* cub, const double* rlb, const double* rub,
+                const double* obj, double obj_offset, double obj_scale) {
+  ScaledLp lp;
+  lp.m = m;
+  lp.n = n;
+  lp.starts.assign(cs, cs + n + 1);
+  lp.rows.assign(ri, ri + cs[n]);
+  lp.vals.assign(vals, vals + cs[n]);
+  lp.col_lb.assign(clb, clb + n);
+  lp.col_ub.assign(cub, cub + n);
+  lp.row_lb.assign(rlb, rlb + m);
+  lp.row_ub.assign(rub, rub + m);
+  lp.obj.assign(obj, obj + n);
+  lp.offset = obj_offset;
+  lp.scale = obj_scale;
+  return lp;
+}
+
+// IsCleanedUp (lp_solver.cc:185-191): rows strictly increasing per column, no
+// explicit zeros, rows in range.
+bool IsCleanedUp(const ScaledLp& lp) {
+  for (int c = 0; c < lp.n; ++c) {
+    if (lp.starts[c + 1] < lp.starts[c]) return false;
+    for (int64_t k = lp.starts[c]; k < lp.starts[c + 1]; ++k) {
+      const int r = lp.rows[k];
+      if (r < 0 || r >= lp.m || lp.vals[k] == 0.0) return false;
+      if (k > lp.starts[c] && lp.rows[k - 1] >= r) return false;
+    }
+  }
+  return true;
+}
+
+// The engine as the LPSolver's simplex (RunRevisedSimplexIfNeeded,
+// lp_solver.cc:591-658): load, solve, and read back the solution.
+struct EngineSimplex {
+  mi_lp* h;
+  const volatile int32_t* interrupt;
+};
+
+int EngineSimplexSolve(void* user, int32_t m, int32_t n, const int64_t* cs, const int32_t* ri,
+                       const double* vals, const double* clb, const double* cub,
+                       const double* rlb, const double* rub, const double* obj, double offset,
+                       double scale, int32_t maximize, mi_lp_result* out, double* primal,
+                       double* duals, int8_t* vstat, int8_t* cstat) {
+  const EngineSimplex* e = static_cast<const EngineSimplex*>(user);
+  const int rc_load =
+      mi_lp_load(e->h, m, n, cs, ri, vals, clb, cub, rlb, rub, obj, offset, scale, maximize);
+  if (rc_load != MI_LP_OK) return rc_load;
+  const int rc_solve = mi_lp_solve(e->h, e->interrupt, out);
+  if (rc_solve != MI_LP_OK) return rc_solve;
+  if (out->error_code != MI_LP_OK) return MI_LP_OK;
+  mi_lp_get_primal(e->h, primal);
+  mi_lp_get_duals(e->h, duals);
+  mi_lp_get_statuses(e->h, vstat, cstat);
+  return MI_LP_OK;
+}
+
 }  // namespace
 }  // namespace milp
 
@@ -337,6 +515,13 @@ void mi_lp_solver_params_default(mi_lp_solver_params* p) {
   p->cost_scaling = MI_LP_CONTAIN_ONE_COST_SCALING;  // :209-210
   p->provide_strong_optimal_guarantee = 1;  // :271
   p->max_valid_magnitude = 1e30;            // max_valid_magnitude default
+  p->use_preprocessing = 0;                 // Glop: true (:326); see mi_lp.h
+  p->use_implied_free_preprocessor = 1;     // :473
+  p->solve_dual_problem = 2;                // :236, LET_SOLVER_DECIDE
+  p->dualizer_threshold = 1.5;              // :241
+  p->preprocessor_zero_tolerance = 1e-9;    // :356
+  p->solution_feasibility_tolerance = 1e-6; // :251
+  p->drop_tolerance = 1e-14;                // :183
 }
 
 }  // extern "C"
@@ -353,6 +538,14 @@ bool LpArraysPresent(int32_t m, int32_t n, const int64_t* cs, const int32_t* ri,
 }
 }  // namespace
 
+// Opaque presolve object of the C ABI.
+struct mi_presolve {
+  std::unique_ptr<milp::presolve::MainPresolve> pre;
+  milp::presolve::Lp lp;
+  int32_t m0 = 0, n0 = 0;
+  bool ran = false, recovered = false, post = false;
+};
+
 extern "C" {
 
 int mi_lp_scale(const mi_lp_solver_params* sp, int32_t m, int32_t n, const int64_t* cs,
@@ -367,22 +560,11 @@ int mi_lp_scale(const mi_lp_solver_params* sp, int32_t m, int32_t n, const int64
   if (m < 0 || n < 0 || cs[0] != 0 || cs[n] < 0) return MI_LP_ERROR_INVALID_PROBLEM;
   if (!LpArraysPresent(m, n, cs, ri, vals, clb, cub, rlb, rub, obj)) return MI_LP_ERROR_NULL;
   try {
-    milp::ScaledLp lp;
-    lp.m = m;
-    lp.n = n;
-    lp.starts.assign(cs, cs + n + 1);
-    lp.rows.assign(ri, ri + cs[n]);
+    milp::ScaledLp lp = milp::CopyLp(m, n, cs, ri, vals, clb, cub, rlb, rub, obj, *obj_offset,
+                                     *obj_scale);
     for (int32_t r : lp.rows) {
       if (r < 0 || r >= m) return MI_LP_ERROR_INVALID_PROBLEM;
     }
-    lp.vals.assign(vals, vals + cs[n]);
-    lp.col_lb.assign(clb, clb + n);
-    lp.col_ub.assign(cub, cub + n);
-    lp.row_lb.assign(rlb, rlb + m);
-    lp.row_ub.assign(rub, rub + m);
-    lp.obj.assign(obj, obj + n);
-    lp.offset = *obj_offset;
-    lp.scale = *obj_scale;
     milp::MatrixScaler scaler;
     scaler.Init(&lp);
     *cost_factor = 1.0;
@@ -408,93 +590,107 @@ int mi_lp_scale(const mi_lp_solver_params* sp, int32_t m, int32_t n, const int64
   }
 }
 
-int mi_lp_solver_solve(mi_lp* h, const mi_lp_solver_params* sp, int32_t m, int32_t n,
-                       const int64_t* cs, const int32_t* ri, const double* vals,
-                       const double* clb, const double* cub, const double* rlb,
-                       const double* rub, const double* obj, double obj_offset,
-                       double obj_scale, int32_t maximize, const volatile int32_t* interrupt,
-                       mi_lp_result* out, double* primal, double* duals, double* rc,
-                       double* act, int8_t* vstat, int8_t* cstat) {
+int mi_lp_solver_solve_with(mi_lp_simplex_fn fn, void* user, const mi_lp_solver_params* sp,
+                            int32_t m, int32_t n, const int64_t* cs, const int32_t* ri,
+                            const double* vals, const double* clb, const double* cub,
+                            const double* rlb, const double* rub, const double* obj,
+                            double obj_offset, double obj_scale, int32_t maximize,
+                            mi_lp_result* out, double* primal, double* duals, double* rc,
+                            double* act, int8_t* vstat, int8_t* cstat) {
   using milp::ScaledLp;
-  if (h == nullptr || sp == nullptr || out == nullptr || cs == nullptr) return MI_LP_ERROR_NULL;
+  namespace ps = milp::presolve;
+  if (fn == nullptr || sp == nullptr || out == nullptr || cs == nullptr) return MI_LP_ERROR_NULL;
   if (m < 0 || n < 0 || cs[0] != 0 || cs[n] < 0) return MI_LP_ERROR_INVALID_PROBLEM;
   if (!LpArraysPresent(m, n, cs, ri, vals, clb, cub, rlb, rub, obj)) return MI_LP_ERROR_NULL;
   std::memset(out, 0, sizeof(*out));
   try {
-    const ScaledLp orig = [&] {
-      ScaledLp lp;
-      lp.m = m;
-      lp.n = n;
-      lp.starts.assign(cs, cs + n + 1);
-      lp.rows.assign(ri, ri + cs[n]);
-      lp.vals.assign(vals, vals + cs[n]);
-      lp.col_lb.assign(clb, clb + n);
-      lp.col_ub.assign(cub, cub + n);
-      lp.row_lb.assign(rlb, rlb + m);
-      lp.row_ub.assign(rub, rub + m);
-      lp.obj.assign(obj, obj + n);
-      lp.offset = obj_offset;
-      lp.scale = obj_scale;
-      return lp;
-    }();
-    // IsCleanedUp (lp_solver.cc:185-191): rows strictly increasing per
-    // column, no explicit zeros, rows in range.
-    for (int c = 0; c < n; ++c) {
-      if (orig.starts[c + 1] < orig.starts[c]) return MI_LP_ERROR_INVALID_PROBLEM;
-      for (int64_t k = orig.starts[c]; k < orig.starts[c + 1]; ++k) {
-        const int r = orig.rows[k];
-        if (r < 0 || r >= m || orig.vals[k] == 0.0) return MI_LP_ERROR_INVALID_PROBLEM;
-        if (k > orig.starts[c] && orig.rows[k - 1] >= r) return MI_LP_ERROR_INVALID_PROBLEM;
-      }
-    }
+    const ScaledLp orig =
+        milp::CopyLp(m, n, cs, ri, vals, clb, cub, rlb, rub, obj, obj_offset, obj_scale);
+    if (!milp::IsCleanedUp(orig)) return MI_LP_ERROR_INVALID_PROBLEM;
     if (!milp::IsValid(orig, sp->max_valid_magnitude)) {
       out->problem_status = MI_LP_INVALID_PROBLEM;
       return MI_LP_OK;
     }
-    ScaledLp lp = orig;
+    // MainLpPreprocessor::Run (preprocessor.cc:76-147): the presolve passes,
+    // then the ScalingPreprocessor through RunAndPushIfRelevant (:152-194).
+    ps::MainPresolve pre(milp::PresolveParamsOf(*sp));
+    ps::Lp plp = milp::ToPresolveLp(orig, maximize != 0);
+    const bool postsolve = pre.Run(&plp);
+    int32_t status = pre.status();
+    const bool inner_max = plp.maximize;
+    const ScaledLp inner = milp::FromPresolveLp(plp);
+    plp = ps::Lp();
+    ScaledLp lp = inner;
     milp::MatrixScaler scaler;
     double cost_factor = 1.0, bound_factor = 1.0;
-    if (sp->use_scaling) {
-      milp::ScaleLp(&lp, &scaler);
-      cost_factor = milp::ScaleObjective(&lp, sp->cost_scaling);
-      bound_factor = milp::ScaleBounds(&lp);
+    bool scaled = false;
+    if (status == MI_LP_INIT) {
+      if (lp.m == 0 && lp.n == 0) {
+        status = MI_LP_OPTIMAL;
+      } else if (sp->use_scaling) {
+        milp::ScaleLp(&lp, &scaler);
+        cost_factor = milp::ScaleObjective(&lp, sp->cost_scaling);
+        bound_factor = milp::ScaleBounds(&lp);
+        scaled = true;
+      }
     }
-    int rc_load = mi_lp_load(h, m, n, lp.starts.data(), lp.rows.data(), lp.vals.data(),
-                             lp.col_lb.data(), lp.col_ub.data(), lp.row_lb.data(),
-                             lp.row_ub.data(), lp.obj.data(), lp.offset, lp.scale, maximize);
-    if (rc_load != MI_LP_OK) return rc_load;
+    // LPSolver::SolveWithTimeLimit (lp_solver.cc:226-247).
+    ps::Solution sol(lp.m, lp.n);
+    sol.status = status;
     mi_lp_result r;
-    const int rc_solve = mi_lp_solve(h, interrupt, &r);
-    if (rc_solve != MI_LP_OK) return rc_solve;
-    *out = r;
-    std::vector<double> x(n), y(m);
-    std::vector<int8_t> vs(n), cstats(m);
-    if (r.error_code != MI_LP_OK) return MI_LP_OK;
-    mi_lp_get_primal(h, x.data());
-    mi_lp_get_duals(h, y.data());
-    mi_lp_get_statuses(h, vs.data(), cstats.data());
+    std::memset(&r, 0, sizeof(r));
+    if (status == MI_LP_INIT) {
+      const int rc_fn = fn(user, lp.m, lp.n, lp.starts.data(), lp.rows.data(), lp.vals.data(),
+                           lp.col_lb.data(), lp.col_ub.data(), lp.row_lb.data(),
+                           lp.row_ub.data(), lp.obj.data(), lp.offset, lp.scale,
+                           inner_max ? 1 : 0, &r, sol.primal.data(), sol.dual.data(),
+                           sol.vstat.data(), sol.cstat.data());
+      if (rc_fn != MI_LP_OK) return rc_fn;
+      if (r.error_code != MI_LP_OK) {
+        *out = r;
+        return MI_LP_OK;
+      }
+      sol.status = r.problem_status;
+    }
     // ScalingPreprocessor::RecoverSolution (preprocessor.cc:3878-3912).
-    if (sp->use_scaling) {
-      for (int c = 0; c < n; ++c) x[c] /= scaler.col_scale[c];
-      for (int c = 0; c < n; ++c) x[c] *= bound_factor;
-      for (int row = 0; row < m; ++row) y[row] /= scaler.row_scale[row];
-      for (int row = 0; row < m; ++row) y[row] *= cost_factor;
-      for (int c = 0; c < n; ++c) {
-        switch (vs[c]) {
+    if (scaled) {
+      for (int c = 0; c < lp.n; ++c) sol.primal[c] /= scaler.col_scale[c];
+      for (int c = 0; c < lp.n; ++c) sol.primal[c] *= bound_factor;
+      for (int row = 0; row < lp.m; ++row) sol.dual[row] /= scaler.row_scale[row];
+      for (int row = 0; row < lp.m; ++row) sol.dual[row] *= cost_factor;
+      for (int c = 0; c < lp.n; ++c) {
+        switch (sol.vstat[c]) {
           case MI_LP_AT_UPPER_BOUND:
           case MI_LP_FIXED_VALUE:
-            x[c] = orig.col_ub[c];
+            sol.primal[c] = inner.col_ub[c];
             break;
           case MI_LP_AT_LOWER_BOUND:
-            x[c] = orig.col_lb[c];
+            sol.primal[c] = inner.col_lb[c];
             break;
           default:
             break;
         }
       }
     }
-    // LoadAndVerifySolution (lp_solver.cc:334-367), value part.
-    const bool strong = sp->provide_strong_optimal_guarantee && r.problem_status == MI_LP_OPTIMAL;
+    // MainLpPreprocessor::DestructiveRecoverSolution (preprocessor.cc:203-209).
+    if (postsolve) pre.Recover(&sol);
+    *out = r;
+    // LoadAndVerifySolution (lp_solver.cc:323-367).
+    if (!milp::IsSolutionConsistent(orig, sol)) {
+      out->problem_status = MI_LP_ABNORMAL;
+      out->objective = 0.0;
+      if (primal != nullptr) std::fill(primal, primal + n, 0.0);
+      if (duals != nullptr) std::fill(duals, duals + m, 0.0);
+      if (rc != nullptr) std::fill(rc, rc + n, 0.0);
+      if (act != nullptr) std::fill(act, act + m, 0.0);
+      if (vstat != nullptr) std::fill(vstat, vstat + n, static_cast<int8_t>(MI_LP_FREE));
+      if (cstat != nullptr) std::fill(cstat, cstat + m, static_cast<int8_t>(MI_LP_FREE));
+      return MI_LP_OK;
+    }
+    out->problem_status = sol.status;
+    std::vector<double>& x = sol.primal;
+    std::vector<double>& y = sol.dual;
+    const bool strong = sp->provide_strong_optimal_guarantee && sol.status == MI_LP_OPTIMAL;
     if (strong) {
       for (int c = 0; c < n; ++c) {  // MovePrimalValuesWithinBounds (:540-555)
         x[c] = std::min(x[c], orig.col_ub[c]);
@@ -531,12 +727,147 @@ int mi_lp_solver_solve(mi_lp* h, const mi_lp_solver_params* sp, int32_t m, int32
     }
     if (primal != nullptr) std::copy(x.begin(), x.end(), primal);
     if (duals != nullptr) std::copy(y.begin(), y.end(), duals);
-    if (vstat != nullptr) std::copy(vs.begin(), vs.end(), vstat);
-    if (cstat != nullptr) std::copy(cstats.begin(), cstats.end(), cstat);
+    if (vstat != nullptr) std::copy(sol.vstat.begin(), sol.vstat.end(), vstat);
+    if (cstat != nullptr) std::copy(sol.cstat.begin(), sol.cstat.end(), cstat);
     return MI_LP_OK;
   } catch (const std::exception&) {
     return MI_LP_ERROR_INTERNAL;
   }
+}
+
+int mi_lp_solver_solve(mi_lp* h, const mi_lp_solver_params* sp, int32_t m, int32_t n,
+                       const int64_t* cs, const int32_t* ri, const double* vals,
+                       const double* clb, const double* cub, const double* rlb,
+                       const double* rub, const double* obj, double obj_offset,
+                       double obj_scale, int32_t maximize, const volatile int32_t* interrupt,
+                       mi_lp_result* out, double* primal, double* duals, double* rc,
+                       double* act, int8_t* vstat, int8_t* cstat) {
+  if (h == nullptr) return MI_LP_ERROR_NULL;
+  milp::EngineSimplex engine{h, interrupt};
+  return mi_lp_solver_solve_with(milp::EngineSimplexSolve, &engine, sp, m, n, cs, ri, vals, clb,
+                                 cub, rlb, rub, obj, obj_offset, obj_scale, maximize, out,
+                                 primal, duals, rc, act, vstat, cstat);
+}
+
+// --- presolve alone -------------------------------------------------------------
+mi_presolve* mi_presolve_create(void) {
+  try {
+    return new mi_presolve();
+  } catch (const std::exception&) {
+    return nullptr;
+  }
+}
+
+void mi_presolve_destroy(mi_presolve* ps) { delete ps; }
+
+int mi_presolve_run(mi_presolve* ps, const mi_lp_solver_params* sp, int32_t m, int32_t n,
+                    const int64_t* cs, const int32_t* ri, const double* vals, const double* clb,
+                    const double* cub, const double* rlb, const double* rub, const double* obj,
+                    double obj_offset, double obj_scale, int32_t maximize, int32_t* status) {
+  if (ps == nullptr || sp == nullptr || cs == nullptr || status == nullptr) {
+    return MI_LP_ERROR_NULL;
+  }
+  if (ps->ran) return MI_LP_ERROR_STATE;
+  if (m < 0 || n < 0 || cs[0] != 0 || cs[n] < 0) return MI_LP_ERROR_INVALID_PROBLEM;
+  if (!LpArraysPresent(m, n, cs, ri, vals, clb, cub, rlb, rub, obj)) return MI_LP_ERROR_NULL;
+  try {
+    const milp::ScaledLp orig =
+        milp::CopyLp(m, n, cs, ri, vals, clb, cub, rlb, rub, obj, obj_offset, obj_scale);
+    if (!milp::IsCleanedUp(orig)) return MI_LP_ERROR_INVALID_PROBLEM;
+    ps->pre = std::make_unique<milp::presolve::MainPresolve>(milp::PresolveParamsOf(*sp));
+    ps->lp = milp::ToPresolveLp(orig, maximize != 0);
+    ps->m0 = m;
+    ps->n0 = n;
+    ps->post = ps->pre->Run(&ps->lp);
+    ps->ran = true;
+    *status = ps->pre->status();
+    return MI_LP_OK;
+  } catch (const std::exception&) {
+    return MI_LP_ERROR_INTERNAL;
+  }
+}
+
+int mi_presolve_dims(const mi_presolve* ps, int32_t* m, int32_t* n, int64_t* nnz,
+                     int32_t* maximize) {
+  if (ps == nullptr) return MI_LP_ERROR_NULL;
+  if (!ps->ran) return MI_LP_ERROR_STATE;
+  if (m != nullptr) *m = ps->lp.num_rows;
+  if (n != nullptr) *n = ps->lp.num_cols();
+  if (nnz != nullptr) *nnz = ps->lp.num_entries();
+  if (maximize != nullptr) *maximize = ps->lp.maximize ? 1 : 0;
+  return MI_LP_OK;
+}
+
+int mi_presolve_get(const mi_presolve* ps, int64_t* cs, int32_t* ri, double* vals, double* clb,
+                    double* cub, double* rlb, double* rub, double* obj, double* obj_offset,
+                    double* obj_scale) {
+  if (ps == nullptr) return MI_LP_ERROR_NULL;
+  if (!ps->ran) return MI_LP_ERROR_STATE;
+  const milp::ScaledLp s = milp::FromPresolveLp(ps->lp);
+  if (cs != nullptr) std::copy(s.starts.begin(), s.starts.end(), cs);
+  if (ri != nullptr) std::copy(s.rows.begin(), s.rows.end(), ri);
+  if (vals != nullptr) std::copy(s.vals.begin(), s.vals.end(), vals);
+  if (clb != nullptr) std::copy(s.col_lb.begin(), s.col_lb.end(), clb);
+  if (cub != nullptr) std::copy(s.col_ub.begin(), s.col_ub.end(), cub);
+  if (rlb != nullptr) std::copy(s.row_lb.begin(), s.row_lb.end(), rlb);
+  if (rub != nullptr) std::copy(s.row_ub.begin(), s.row_ub.end(), rub);
+  if (obj != nullptr) std::copy(s.obj.begin(), s.obj.end(), obj);
+  if (obj_offset != nullptr) *obj_offset = s.offset;
+  if (obj_scale != nullptr) *obj_scale = s.scale;
+  return MI_LP_OK;
+}
+
+int mi_presolve_recover(mi_presolve* ps, int32_t* status, const double* primal,
+                        const double* duals, const int8_t* vstat, const int8_t* cstat,
+                        double* primal_out, double* duals_out, int8_t* vstat_out,
+                        int8_t* cstat_out) {
+  if (ps == nullptr || status == nullptr) return MI_LP_ERROR_NULL;
+  if (!ps->ran || ps->recovered) return MI_LP_ERROR_STATE;
+  const int32_t m = ps->lp.num_rows;
+  const int32_t n = ps->lp.num_cols();
+  if ((n > 0 && (primal == nullptr || vstat == nullptr)) ||
+      (m > 0 && (duals == nullptr || cstat == nullptr))) {
+    return MI_LP_ERROR_NULL;
+  }
+  try {
+    milp::presolve::Solution s(m, n);
+    s.status = *status;
+    if (n > 0) {
+      std::copy(primal, primal + n, s.primal.begin());
+      std::copy(vstat, vstat + n, s.vstat.begin());
+    }
+    if (m > 0) {
+      std::copy(duals, duals + m, s.dual.begin());
+      std::copy(cstat, cstat + m, s.cstat.begin());
+    }
+    if (ps->post) ps->pre->Recover(&s);
+    ps->recovered = true;
+    if (static_cast<int32_t>(s.primal.size()) != ps->n0 ||
+        static_cast<int32_t>(s.dual.size()) != ps->m0) {
+      return MI_LP_ERROR_INTERNAL;
+    }
+    *status = s.status;
+    if (primal_out != nullptr) std::copy(s.primal.begin(), s.primal.end(), primal_out);
+    if (duals_out != nullptr) std::copy(s.dual.begin(), s.dual.end(), duals_out);
+    if (vstat_out != nullptr) std::copy(s.vstat.begin(), s.vstat.end(), vstat_out);
+    if (cstat_out != nullptr) std::copy(s.cstat.begin(), s.cstat.end(), cstat_out);
+    return MI_LP_OK;
+  } catch (const std::exception&) {
+    return MI_LP_ERROR_INTERNAL;
+  }
+}
+
+int32_t mi_presolve_num_passes(const mi_presolve* ps) {
+  if (ps == nullptr || !ps->ran) return 0;
+  return static_cast<int32_t>(ps->pre->applied().size());
+}
+
+const char* mi_presolve_pass_name(const mi_presolve* ps, int32_t i) {
+  if (ps == nullptr || !ps->ran || i < 0 ||
+      i >= static_cast<int32_t>(ps->pre->applied().size())) {
+    return nullptr;
+  }
+  return ps->pre->applied()[i].c_str();
 }
 
 }  // extern "C"

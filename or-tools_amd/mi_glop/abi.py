@@ -128,13 +128,18 @@ PROBLEM_STATUS = [
 OPTIMAL = 0
 PRIMAL_INFEASIBLE = 1
 DUAL_INFEASIBLE = 2
+INFEASIBLE_OR_UNBOUNDED = 3
 PRIMAL_UNBOUNDED = 4
 DUAL_UNBOUNDED = 5
+INIT = 6
 PRIMAL_FEASIBLE = 7
 DUAL_FEASIBLE = 8
 ABNORMAL = 9
 INVALID_PROBLEM = 10
 IMPRECISE = 11
+
+# glop::VariableStatus / ConstraintStatus (lp_data/lp_types.h:188-219)
+BASIC, FIXED_VALUE, AT_LOWER_BOUND, AT_UPPER_BOUND, FREE = 0, 1, 2, 3, 4
 
 # Kernel ids (include/mi_lp.h MI_K_*)
 class MiLpRunCounters(ctypes.Structure):
@@ -178,32 +183,48 @@ EXPORTED_SYMBOLS = [
     "mi_lp_clear_integrality_scales", "mi_lp_record_iteration_times",
     "mi_lp_get_iteration_times", "mi_lp_get_run_counters", "mi_lp_set_exchange",
     "mi_exchange_open", "mi_exchange_allgather", "mi_exchange_close",
-    "mi_lp_batch_solve_gpus",
+    "mi_lp_batch_solve_gpus", "mi_lp_solver_solve_with",
+    "mi_presolve_create", "mi_presolve_destroy", "mi_presolve_run", "mi_presolve_dims",
+    "mi_presolve_get", "mi_presolve_recover", "mi_presolve_num_passes", "mi_presolve_pass_name",
 ]
 
 
 class MiLpSolverParams(ctypes.Structure):
     """include/mi_lp.h mi_lp_solver_params: the GlopParameters fields that
-    glop::LPSolver reads around the simplex (parameters.proto field numbers
-    16, 57, 60, 24, 199)."""
+    glop::LPSolver and its presolve read around the simplex (parameters.proto
+    field numbers 16, 57, 60, 24, 199; presolve 34, 67, 20, 21, 39, 22, 52)."""
     _fields_ = [
         ("use_scaling", ctypes.c_int32),
         ("scaling_method", ctypes.c_int32),
         ("cost_scaling", ctypes.c_int32),
         ("provide_strong_optimal_guarantee", ctypes.c_int32),
         ("max_valid_magnitude", ctypes.c_double),
+        ("use_preprocessing", ctypes.c_int32),
+        ("use_implied_free_preprocessor", ctypes.c_int32),
+        ("solve_dual_problem", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("dualizer_threshold", ctypes.c_double),
+        ("preprocessor_zero_tolerance", ctypes.c_double),
+        ("solution_feasibility_tolerance", ctypes.c_double),
+        ("drop_tolerance", ctypes.c_double),
     ]
 
 
 # GlopParameters::ScalingAlgorithm / CostScalingAlgorithm (parameters.proto:34-36, 194-210)
 SCALING_DEFAULT, EQUILIBRATION, LINEAR_PROGRAM = 0, 1, 2
 NO_COST_SCALING, CONTAIN_ONE_COST_SCALING, MEAN_COST_SCALING, MEDIAN_COST_SCALING = 0, 1, 2, 3
+# GlopParameters::SolverBehavior (parameters.proto:42-46)
+ALWAYS_DO, NEVER_DO, LET_SOLVER_DECIDE = 0, 1, 2
 
 
 def default_solver_params(**overrides):
     p = MiLpSolverParams(use_scaling=1, scaling_method=EQUILIBRATION,
                          cost_scaling=CONTAIN_ONE_COST_SCALING,
-                         provide_strong_optimal_guarantee=1, max_valid_magnitude=1e30)
+                         provide_strong_optimal_guarantee=1, max_valid_magnitude=1e30,
+                         use_preprocessing=0, use_implied_free_preprocessor=1,
+                         solve_dual_problem=LET_SOLVER_DECIDE, dualizer_threshold=1.5,
+                         preprocessor_zero_tolerance=1e-9, solution_feasibility_tolerance=1e-6,
+                         drop_tolerance=1e-14)
     for k, v in overrides.items():
         if k not in dict(MiLpSolverParams._fields_):
             raise KeyError(f"unknown LPSolver parameter {k!r}")

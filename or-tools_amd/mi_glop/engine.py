@@ -24,6 +24,10 @@ class EngineUnavailable(RuntimeError):
 # mi_lp_allgather_fn (include/mi_lp.h): ctx, send, send_bytes, recv, recv_bytes.
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64))
+# include/mi_lp.h mi_lp_simplex_fn: the LPSolver's simplex, supplied by the caller.
+SIMPLEX_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                              *([ctypes.c_void_p] * 8), ctypes.c_double, ctypes.c_double,
+                              ctypes.c_int32, ctypes.c_void_p, *([ctypes.c_void_p] * 4))
 
 
 def build(jobs=8):
@@ -105,6 +109,22 @@ def lib():
                                      ctypes.c_int32] + [vp] * 8 + [
         ctypes.c_double, ctypes.c_double, ctypes.c_int32, vp,
         ctypes.POINTER(abi.MiLpResult)] + [vp] * 6
+    L.mi_lp_solver_solve_with.argtypes = [SIMPLEX_FN, vp, ctypes.POINTER(abi.MiLpSolverParams),
+                                          ctypes.c_int32, ctypes.c_int32] + [vp] * 8 + [
+        ctypes.c_double, ctypes.c_double, ctypes.c_int32, ctypes.POINTER(abi.MiLpResult)] + \
+        [vp] * 6
+    L.mi_presolve_create.restype = vp
+    L.mi_presolve_destroy.argtypes = [vp]
+    L.mi_presolve_run.argtypes = [vp, ctypes.POINTER(abi.MiLpSolverParams), ctypes.c_int32,
+                                  ctypes.c_int32] + [vp] * 8 + [
+        ctypes.c_double, ctypes.c_double, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
+    L.mi_presolve_dims.argtypes = [vp] + [vp] * 4
+    L.mi_presolve_get.argtypes = [vp] + [vp] * 10
+    L.mi_presolve_recover.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)] + [vp] * 8
+    L.mi_presolve_num_passes.argtypes = [vp]
+    L.mi_presolve_num_passes.restype = ctypes.c_int32
+    L.mi_presolve_pass_name.argtypes = [vp, ctypes.c_int32]
+    L.mi_presolve_pass_name.restype = ctypes.c_char_p
     _lib = L
     return L
 
@@ -565,3 +585,129 @@ def scale_lp(lp, solver_params=None):
                               sc.value, lp.maximize, lp.name)
     return out, {"row_scale": rs, "col_scale": cl, "cost_factor": cf.value,
                  "bound_factor": bf.value}
+
+
+def _lp_arrays(lp):
+    return [np.ascontiguousarray(x, dtype=t) for x, t in (
+        (lp.col_starts, np.int64), (lp.row_idx, np.int32), (lp.vals, np.float64),
+        (lp.col_lb, np.float64), (lp.col_ub, np.float64), (lp.row_lb, np.float64),
+        (lp.row_ub, np.float64), (lp.obj, np.float64))]
+
+
+class Presolve:
+    """Glop's MainLpPreprocessor passes and their postsolve (mi_presolve_*,
+    host only): run(lp) -> Glop's status after presolve; presolved() -> the
+    reduced LinearProgram; recover(...) -> the solution of the original LP."""
+
+    def __init__(self, solver_params=None):
+        self._L = lib()
+        self.sp = solver_params or abi.default_solver_params(use_preprocessing=1)
+        self.h = ctypes.c_void_p(self._L.mi_presolve_create())
+        if not self.h:
+            raise MemoryError("mi_presolve_create")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self._L.mi_presolve_destroy(self.h)
+            self.h = None
+
+    def run(self, lp):
+        self.lp = lp
+        keep = _lp_arrays(lp)
+        st = ctypes.c_int32()
+        rc = self._L.mi_presolve_run(self.h, ctypes.byref(self.sp), lp.m, lp.n,
+                                     *[_p(a) for a in keep], lp.obj_offset, lp.obj_scale,
+                                     int(lp.maximize), ctypes.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"mi_presolve_run failed ({rc})")
+        return st.value
+
+    def passes(self):
+        return [self._L.mi_presolve_pass_name(self.h, i).decode()
+                for i in range(self._L.mi_presolve_num_passes(self.h))]
+
+    def presolved(self):
+        from . import lp as lpmod
+        m, n, mx = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        nnz = ctypes.c_int64()
+        self._L.mi_presolve_dims(self.h, ctypes.byref(m), ctypes.byref(n), ctypes.byref(nnz),
+                                 ctypes.byref(mx))
+        m, n, nnz = m.value, n.value, nnz.value
+        cs = np.zeros(n + 1, np.int64)
+        ri = np.zeros(nnz, np.int32)
+        arrs = [np.zeros(k) for k in (nnz, n, n, m, m, n)]
+        off, sc = ctypes.c_double(), ctypes.c_double()
+        self._L.mi_presolve_get(self.h, _p(cs), _p(ri), *[_p(a) for a in arrs],
+                                ctypes.byref(off), ctypes.byref(sc))
+        v, clb, cub, rlb, rub, ob = arrs
+        return lpmod.LinearProgram(m, n, cs, ri, v, clb, cub, rlb, rub, ob, off.value,
+                                   sc.value, bool(mx.value), "presolved")
+
+    def recover(self, status, primal, duals, vstat, cstat):
+        p = np.ascontiguousarray(primal, np.float64)
+        d = np.ascontiguousarray(duals, np.float64)
+        vs = np.ascontiguousarray(vstat, np.int8)
+        cst = np.ascontiguousarray(cstat, np.int8)
+        n0, m0 = self.lp.n, self.lp.m
+        out = {"x": np.zeros(n0), "y": np.zeros(m0), "vstat": np.zeros(n0, np.int8),
+               "cstat": np.zeros(m0, np.int8)}
+        st = ctypes.c_int32(status)
+        rc = self._L.mi_presolve_recover(self.h, ctypes.byref(st), _p(p), _p(d), _p(vs), _p(cst),
+                                         *[_p(out[k]) for k in ("x", "y", "vstat", "cstat")])
+        if rc != 0:
+            raise RuntimeError(f"mi_presolve_recover failed ({rc})")
+        return st.value, out
+
+
+def solve_lp_with(lp, simplex, solver_params=None):
+    """mi_lp_solver_solve_with: Glop's LPSolver flow (presolve, scaling, the
+    caller's simplex, postsolve, LoadAndVerifySolution) with `simplex(inner_lp)`
+    returning (mi_lp_result, primal, duals, vstat, cstat) for the presolved,
+    scaled LP. Returns (result, dict of the original LP's solution arrays)."""
+    from . import lp as lpmod
+    L = lib()
+    sp = solver_params or abi.default_solver_params()
+    keep = _lp_arrays(lp)
+    errors = []
+
+    def cb(user, m, n, cs, ri, v, clb, cub, rlb, rub, ob, off, sc, mx, out, x, y, vs, cst):
+        try:
+            nnz = ctypes.cast(cs, ctypes.POINTER(ctypes.c_int64))[n] if n >= 0 else 0
+
+            def arr(ptr, k, t):
+                if k == 0:
+                    return np.zeros(0, t)
+                c = {np.float64: ctypes.c_double, np.int64: ctypes.c_int64,
+                     np.int32: ctypes.c_int32}[t]
+                return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(c)), (k,)).copy()
+            inner = lpmod.LinearProgram(
+                m, n, arr(cs, n + 1, np.int64), arr(ri, nnz, np.int32), arr(v, nnz, np.float64),
+                arr(clb, n, np.float64), arr(cub, n, np.float64), arr(rlb, m, np.float64),
+                arr(rub, m, np.float64), arr(ob, n, np.float64), off, sc, bool(mx), "inner")
+            r, px, dy, pvs, pcs = simplex(inner)
+            ctypes.memmove(out, ctypes.byref(r), ctypes.sizeof(abi.MiLpResult))
+            for ptr, a, t in ((x, px, np.float64), (y, dy, np.float64), (vs, pvs, np.int8),
+                              (cst, pcs, np.int8)):
+                a = np.ascontiguousarray(a, t)
+                if a.size:
+                    ctypes.memmove(ptr, a.ctypes.data, a.nbytes)
+            return 0
+        except Exception as exc:  # noqa: BLE001 (reported after the call)
+            errors.append(exc)
+            return 102
+
+    fn = SIMPLEX_FN(cb)
+    out = {"x": np.zeros(lp.n), "y": np.zeros(lp.m), "rc": np.zeros(lp.n),
+           "act": np.zeros(lp.m), "vstat": np.zeros(lp.n, np.int8),
+           "cstat": np.zeros(lp.m, np.int8)}
+    r = abi.MiLpResult()
+    rc = L.mi_lp_solver_solve_with(fn, None, ctypes.byref(sp), lp.m, lp.n,
+                                   *[_p(a) for a in keep], lp.obj_offset, lp.obj_scale,
+                                   int(lp.maximize), ctypes.byref(r),
+                                   *[_p(out[k]) for k in ("x", "y", "rc", "act", "vstat",
+                                                          "cstat")])
+    if errors:
+        raise errors[0]
+    if rc != 0:
+        raise RuntimeError(f"mi_lp_solver_solve_with failed ({rc})")
+    return r, out

@@ -264,3 +264,150 @@ def to_scipy(lp):
         return res.status, None
     val = res.fun + lp.obj_offset * (1 if not lp.maximize else -1)
     return 0, (-val if lp.maximize else val)
+
+
+def presolve_lp(m, n, seed, maximize=False, tall=False):
+    """Feasible LP around a point x0 carrying every structure Glop's presolve
+    passes act on (glop/preprocessor.cc): fixed, empty, singleton and free
+    doubleton columns, proportional columns and rows, empty, singleton,
+    forcing and doubleton-equality rows, implied-free bounds, one-sided and
+    free rows. tall=True makes rows >= 1.5 x columns (the dualizer's case)."""
+    rng = np.random.default_rng(seed)
+    if tall:
+        m = max(m, int(1.8 * n))
+    cols = []          # per column: dict row -> coeff
+    x0 = []
+    lb, ub, cost = [], [], []
+
+    def add_col(entries, lo, hi, c, x):
+        cols.append(dict(entries))
+        lb.append(lo)
+        ub.append(hi)
+        cost.append(c)
+        x0.append(x)
+        return len(cols) - 1
+
+    per_col = max(1, int(round(0.06 * m)))
+    for _ in range(n):
+        k = max(1, min(m, rng.binomial(2 * per_col, 0.5)))
+        rows = rng.choice(m, size=k, replace=False)
+        ent = {int(r): float(rng.uniform(0.2, 1.0) * rng.choice([-1.0, 1.0])) for r in rows}
+        kind = rng.uniform()
+        if kind < 0.55:
+            lo, hi = 0.0, float(1.0 + rng.uniform(0, 2))
+        elif kind < 0.75:
+            lo, hi = 0.0, INF
+        elif kind < 0.85:
+            lo, hi = float(-rng.uniform(1, 3)), float(rng.uniform(1, 3))
+        elif kind < 0.93:
+            lo, hi = float(rng.uniform(0.5, 2.0)), float(rng.uniform(3.0, 5.0))  # shifted
+        else:
+            lo, hi = -INF, float(rng.uniform(1, 3))
+        x = float(rng.uniform(max(lo, -1.0) if np.isfinite(lo) else -1.0,
+                              min(hi, 3.0) if np.isfinite(hi) else 3.0))
+        add_col(ent, lo, hi, float(rng.uniform(-1, 1)), x)
+    base = len(cols)
+    # fixed columns
+    for _ in range(max(1, n // 20)):
+        c = int(rng.integers(base))
+        v = float(rng.uniform(-1, 2))
+        add_col({int(r): float(rng.uniform(-1, 1)) for r in rng.choice(m, 3, replace=False)},
+                v, v, float(rng.uniform(-1, 1)), v)
+    # empty columns: cost pushes to a finite bound, or zero cost
+    for k in range(3):
+        c = [1.0, -1.0, 0.0][k]
+        add_col({}, 0.0 if c >= 0 else -INF, 2.0 if c <= 0 else INF, c, 0.0)
+    # proportional columns (copies of base columns, scaled), x0 = 0 in [.,.]
+    for _ in range(max(1, n // 25)):
+        src = int(rng.integers(base))
+        f = float(rng.choice([-2.0, 0.5, 3.0]))
+        same_cost = rng.uniform() < 0.6
+        c = cost[src] * f if same_cost else float(rng.uniform(-1, 1))
+        add_col({r: v * f for r, v in cols[src].items()}, 0.0, float(rng.uniform(1, 2)), c, 0.0)
+    # singleton columns (slacks), some with cost
+    for _ in range(max(1, n // 15)):
+        r = int(rng.integers(m))
+        add_col({r: float(rng.choice([-1.0, 1.0]) * rng.uniform(0.5, 2))}, 0.0,
+                float(rng.choice([2.0, INF])), float(rng.choice([0.0, rng.uniform(-1, 1)])), 0.0)
+    # free doubleton columns, zero cost
+    for _ in range(2):
+        r1, r2 = (int(v) for v in rng.choice(m, 2, replace=False))
+        add_col({r1: float(rng.uniform(0.5, 1.5)), r2: float(-rng.uniform(0.5, 1.5))},
+                -INF, INF, 0.0, float(rng.uniform(-1, 1)))
+    nrows = m
+    extra_rows = []    # (entries dict col -> coeff, kind)
+    # doubleton equality rows
+    for _ in range(max(1, m // 15)):
+        i, j = (int(v) for v in rng.choice(base, 2, replace=False))
+        extra_rows.append(({i: float(rng.uniform(0.5, 2)), j: float(-rng.uniform(0.5, 2))}, "eq"))
+    # singleton rows (tighten a variable)
+    for _ in range(max(1, m // 20)):
+        c = int(rng.integers(base))
+        extra_rows.append(({c: float(rng.choice([-1.0, 1.0]) * rng.uniform(0.5, 2))}, "rng"))
+    # forcing row: positive coefficients on boxed columns at their upper bound
+    boxed = [c for c in range(base) if lb[c] == 0.0 and np.isfinite(ub[c])]
+    if len(boxed) >= 3:
+        pick = [int(v) for v in rng.choice(boxed, 3, replace=False)]
+        for c in pick:
+            x0[c] = ub[c]
+        extra_rows.append(({c: float(rng.uniform(0.5, 1.5)) for c in pick}, "forcing"))
+    # proportional rows: scaled copies of the first rows (their entries)
+    col_rows = [dict() for _ in range(m)]
+    for c, ent in enumerate(cols):
+        for r, v in ent.items():
+            col_rows[r][c] = v
+    for r in range(min(3, m)):
+        if col_rows[r]:
+            f = float(rng.choice([-1.5, 2.0]))
+            extra_rows.append(({c: v * f for c, v in col_rows[r].items()}, "any"))
+    extra_rows.append(({}, "empty"))
+    for ent, kind in extra_rows:
+        for c, v in ent.items():
+            cols[c][nrows] = v
+        nrows += 1
+    ncols = len(cols)
+    x0 = np.asarray(x0)
+    ax = np.zeros(nrows)
+    for c, ent in enumerate(cols):
+        for r, v in ent.items():
+            ax[r] += v * x0[c]
+    row_lb = np.full(nrows, -INF)
+    row_ub = np.full(nrows, INF)
+    kinds = [None] * m + [k for _, k in extra_rows]
+    for r in range(nrows):
+        k = kinds[r]
+        u = rng.uniform()
+        if k == "eq" or (k is None and u < 0.2):
+            row_lb[r] = row_ub[r] = ax[r]
+        elif k == "forcing":
+            row_lb[r] = ax[r]
+        elif k == "empty":
+            row_lb[r], row_ub[r] = -1.0, 1.0
+        elif k == "rng" or u < 0.35:
+            row_lb[r], row_ub[r] = ax[r] - rng.uniform(0, 1), ax[r] + rng.uniform(0, 1)
+        elif u < 0.65:
+            row_ub[r] = ax[r] + rng.uniform(0, 1)
+        elif u < 0.97:
+            row_lb[r] = ax[r] - rng.uniform(0, 1)
+        # else free row
+    cs = [0]
+    ri, va = [], []
+    for ent in cols:
+        for r in sorted(ent):
+            ri.append(r)
+            va.append(ent[r])
+        cs.append(len(ri))
+    # keep bounded: cap infinite sides that the cost pushes towards
+    col_lb = np.asarray(lb, float)
+    col_ub = np.asarray(ub, float)
+    obj = np.asarray(cost, float)
+    sgn = -1.0 if maximize else 1.0
+    push_up = sgn * obj < 0
+    cap = ~np.isfinite(col_ub) & push_up
+    col_ub[cap] = 20.0
+    push_dn = sgn * obj > 0
+    capl = ~np.isfinite(col_lb) & push_dn
+    col_lb[capl] = -20.0
+    return LinearProgram(nrows, ncols, np.asarray(cs, np.int64), np.asarray(ri, np.int32),
+                         np.asarray(va, float), col_lb, col_ub, row_lb, row_ub, obj, 0.5, 1.0,
+                         maximize, f"presolve_{nrows}x{ncols}_s{seed}")

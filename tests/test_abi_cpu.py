@@ -16,7 +16,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_loads_and_exports_header_symbols():
     L = engine.lib()
     header = open(os.path.join(REPO, "include", "mi_lp.h")).read()
-    declared = sorted(set(re.findall(r"\b(mi_(?:lp|glop|mps|exchange)_[a-z_]+)\(", header)))
+    declared = sorted(set(re.findall(r"\b(mi_(?:lp|glop|mps|exchange|presolve)_[a-z_]+)\(", header)))
     assert declared == sorted(abi.EXPORTED_SYMBOLS)
     for name in declared:
         assert hasattr(L, name), name

@@ -95,6 +95,47 @@ def test_scale_rejects_bad_rows():
         engine.scale_lp(bad)
 
 
+@pytest.mark.parametrize("dual", [0, 1])
+@pytest.mark.parametrize("case", _cases(), ids=lambda c: c[0])
+def test_lp_solver_flow_cpu(case, dual):
+    """mi_lp_solver_solve's flow (mi_lp_solver_solve_with: validity checks,
+    presolve off, scaling, simplex, RecoverSolution, IsProblemSolutionConsistent,
+    LoadAndVerifySolution's values) with the oracle as its simplex equals the
+    numpy restatement bit for bit; test_lp_solver_parity runs the same flow
+    with the engine behind it on the GPU."""
+    lp, expect = case[1]()
+    p = abi.default_params(use_dual_simplex=dual)
+
+    def simplex(inner):
+        o = oracle_lib.OracleLp(p)
+        o.load(inner)
+        r = o.solve()
+        v, c = o.statuses()
+        return r, o.primal(), o.duals(), v, c
+
+    rg, sol = engine.solve_lp_with(lp, simplex)
+    arr, fac = oracle_scaling.scale_lp(lp)
+    slp = LinearProgram(lp.m, lp.n, lp.col_starts, lp.row_idx, arr["vals"], arr["col_lb"],
+                        arr["col_ub"], arr["row_lb"], arr["row_ub"], arr["obj"],
+                        arr["obj_offset"], arr["obj_scale"], lp.maximize, lp.name)
+    o = oracle_lib.OracleLp(p)
+    o.load(slp)
+    ro = o.solve()
+    assert rg.problem_status == ro.problem_status
+    assert rg.iterations == ro.iterations
+    if ro.problem_status == abi.INVALID_PROBLEM:
+        return
+    vs, cs = o.statuses()
+    np.testing.assert_array_equal(sol["vstat"], vs)
+    np.testing.assert_array_equal(sol["cstat"], cs)
+    want = oracle_scaling.recover_and_verify(lp, fac, o.primal(), o.duals(), vs,
+                                             ro.problem_status == abi.OPTIMAL)
+    for k in ("x", "y", "rc", "act"):
+        np.testing.assert_array_equal(sol[k], want[k], err_msg=k)
+    if ro.problem_status == abi.OPTIMAL:
+        assert rg.objective == want["objective"]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dual", [0, 1])
 @pytest.mark.parametrize("case", _cases(), ids=lambda c: c[0])
