@@ -14,7 +14,7 @@ holds no presolve fixtures. The checks are the size-independent properties
 of a correct presolve + postsolve on every LP of tests/lp_gen.presolve_lp
 (which makes each of the 14 passes fire) and of the known-answer LPs:
 - the same status and optimal objective as the unpresolved flow (1e-9
-  relative; measured 1e-13),
+  relative; measured 8.7e-14),
 - a postsolved solution that passes LPSolver's own IsProblemSolutionConsistent
   (lp_solver.cc:679-790: statuses at their bounds, exactly m basic), else the
   flow reports ABNORMAL,
