@@ -340,6 +340,16 @@ class Solver:
             self._sol["cstat"] = [self._BASIS[int(s)] for s in sol["cstat"]]
         return status
 
+    # GlopParameters enum value names (parameters.proto:34-92, 194-210, 42-46).
+    _ENUM_VALUES = {
+        "DANTZIG": 0, "STEEPEST_EDGE": 1, "DEVEX": 2,
+        "NONE": 0, "BIXBY": 1, "TRIANGULAR": 2, "MAROS": 3,
+        "DEFAULT": 0, "EQUILIBRATION": 1, "LINEAR_PROGRAM": 2,
+        "NO_COST_SCALING": 0, "CONTAIN_ONE_COST_SCALING": 1, "MEAN_COST_SCALING": 2,
+        "MEDIAN_COST_SCALING": 3,
+        "ALWAYS_DO": 0, "NEVER_DO": 1, "LET_SOLVER_DECIDE": 2,
+    }
+
     def SetSolverSpecificParametersAsString(self, text):
         """GLOPInterface::SetSolverSpecificParametersAsString (glop_interface.cc:
         397-411) reads a GlopParameters text proto; the fields of mi_glop_params
@@ -353,6 +363,8 @@ class Solver:
             value = tokens[i + 2]
             i += 3
             v = {"true": 1, "false": 0}.get(value.lower(), None)
+            if v is None:
+                v = self._ENUM_VALUES.get(value)
             if v is None:
                 try:
                     v = float(value) if any(ch in value for ch in ".eE") else int(value)

@@ -167,3 +167,22 @@ def test_infeasible_and_unbounded_status_maps():
     c2 = s2.Constraint(0, INF)
     c2.SetCoefficient(y, 1)
     assert s2.Solve() == linear_solver.Solver.UNBOUNDED
+
+
+def test_solver_specific_parameters_text():
+    """GLOPInterface::SetSolverSpecificParametersAsString (glop_interface.cc:
+    397-411): GlopParameters text, enum values by name, LPSolver and presolve
+    fields included."""
+    s = linear_solver.Solver("p")
+    assert s.SetSolverSpecificParametersAsString(
+        "use_preprocessing: true solve_dual_problem: ALWAYS_DO "
+        "feasibility_rule: DANTZIG initial_basis: MAROS cost_scaling: MEAN_COST_SCALING "
+        "preprocessor_zero_tolerance: 1e-10 use_dual_simplex: true")
+    assert s._solver_params.use_preprocessing == 1
+    assert s._solver_params.solve_dual_problem == 0
+    assert s._solver_params.cost_scaling == 2
+    assert s._solver_params.preprocessor_zero_tolerance == 1e-10
+    assert s._params.feasibility_rule == 0 and s._params.initial_basis == 3
+    assert s._params.use_dual_simplex == 1
+    assert not s.SetSolverSpecificParametersAsString("no_such_field: 3")
+    assert not s.SetSolverSpecificParametersAsString("solve_dual_problem: SOMETIMES")
