@@ -445,7 +445,8 @@ typedef struct mi_lp_solver_params {
   int32_t use_implied_free_preprocessor;    /* 67, true */
   int32_t solve_dual_problem;               /* 20, LET_SOLVER_DECIDE (ALWAYS_DO 0,
                                                NEVER_DO 1, LET_SOLVER_DECIDE 2) */
-  int32_t reserved0;
+  int32_t change_status_to_imprecise;       /* 58, true: LoadAndVerifySolution may
+                                               report IMPRECISE */
   double dualizer_threshold;                /* 21, 1.5 */
   double preprocessor_zero_tolerance;       /* 39, 1e-9 */
   double solution_feasibility_tolerance;    /* 22, 1e-6 */

@@ -516,6 +516,7 @@ void mi_lp_solver_params_default(mi_lp_solver_params* p) {
   p->provide_strong_optimal_guarantee = 1;  // :271
   p->max_valid_magnitude = 1e30;            // max_valid_magnitude default
   p->use_preprocessing = 0;                 // Glop: true (:326); see mi_lp.h
+  p->change_status_to_imprecise = 1;        // :275
   p->use_implied_free_preprocessor = 1;     // :473
   p->solve_dual_problem = 2;                // :236, LET_SOLVER_DECIDE
   p->dualizer_threshold = 1.5;              // :241
@@ -687,44 +688,150 @@ int mi_lp_solver_solve_with(mi_lp_simplex_fn fn, void* user, const mi_lp_solver_
       if (cstat != nullptr) std::fill(cstat, cstat + m, static_cast<int8_t>(MI_LP_FREE));
       return MI_LP_OK;
     }
-    out->problem_status = sol.status;
+    int32_t verified = sol.status;
     std::vector<double>& x = sol.primal;
     std::vector<double>& y = sol.dual;
-    const bool strong = sp->provide_strong_optimal_guarantee && sol.status == MI_LP_OPTIMAL;
-    if (strong) {
-      for (int c = 0; c < n; ++c) {  // MovePrimalValuesWithinBounds (:540-555)
-        x[c] = std::min(x[c], orig.col_ub[c]);
-        x[c] = std::max(x[c], orig.col_lb[c]);
-      }
-      const double sign = maximize ? -1.0 : 1.0;  // MoveDualValuesWithinBounds (:557-579)
-      for (int row = 0; row < m; ++row) {
-        double d = sign * y[row];
-        if (orig.row_lb[row] == -milp::kInf && d > 0.0) d = 0.0;
-        if (orig.row_ub[row] == milp::kInf && d < 0.0) d = 0.0;
-        y[row] = sign * d;
-      }
-    }
-    milp::KahanSum sum;  // ComputeObjective (:888-896)
-    for (int c = 0; c < n; ++c) sum.Add(orig.obj[c] * x[c]);
-    out->objective = orig.scale * (sum.sum + orig.offset);  // ProblemObjectiveValue (:306-308)
-    if (rc != nullptr) {  // ComputeReducedCosts (:877-886)
+    const double optimization_sign = maximize ? -1.0 : 1.0;
+    const double tolerance = sp->solution_feasibility_tolerance;
+    auto allowed_error = [tolerance](double value) {  // AllowedError (:316-318)
+      return tolerance * std::max(1.0, std::fabs(value));
+    };
+    std::vector<double> reduced(n, 0.0);
+    auto compute_reduced_costs = [&]() {  // ComputeReducedCosts (:877-886)
       for (int c = 0; c < n; ++c) {
         double dot = 0.0;
         for (int64_t k = orig.starts[c]; k < orig.starts[c + 1]; ++k) {
           dot += y[orig.rows[k]] * orig.vals[k];
         }
-        rc[c] = orig.obj[c] - dot;
+        reduced[c] = orig.obj[c] - dot;
       }
-    }
-    if (act != nullptr) {  // ComputeConstraintActivities (:866-875)
-      std::fill(act, act + m, 0.0);
+    };
+    auto compute_objective = [&]() {  // ComputeObjective (:888-896)
+      milp::KahanSum sum;
+      for (int c = 0; c < n; ++c) sum.Add(orig.obj[c] * x[c]);
+      return sum.sum;
+    };
+    compute_reduced_costs();
+    const double primal_objective = compute_objective();
+    double dual_objective;
+    {  // ComputeDualObjective (:914-975)
+      milp::KahanSum sum;
+      for (int row = 0; row < m; ++row) {
+        const double corrected = optimization_sign * y[row];
+        if (corrected > 0.0 && orig.row_lb[row] != -milp::kInf) sum.Add(y[row] * orig.row_lb[row]);
+        if (corrected < 0.0 && orig.row_ub[row] != milp::kInf) sum.Add(y[row] * orig.row_ub[row]);
+      }
       for (int c = 0; c < n; ++c) {
-        if (x[c] == 0.0) continue;
-        for (int64_t k = orig.starts[c]; k < orig.starts[c + 1]; ++k) {
-          act[orig.rows[k]] += x[c] * orig.vals[k];
+        const double rcm = optimization_sign * reduced[c];
+        double correction = 0.0;
+        if (sol.vstat[c] == MI_LP_AT_LOWER_BOUND && rcm > 0.0) {
+          correction = rcm * orig.col_lb[c];
+        } else if (sol.vstat[c] == MI_LP_AT_UPPER_BOUND && rcm < 0.0) {
+          correction = rcm * orig.col_ub[c];
+        } else if (sol.vstat[c] == MI_LP_FIXED_VALUE) {
+          correction = rcm * orig.col_ub[c];
         }
+        sum.Add(optimization_sign * correction);
+      }
+      dual_objective = sum.sum;
+    }
+    const bool strong = sp->provide_strong_optimal_guarantee && verified == MI_LP_OPTIMAL;
+    if (strong) {
+      for (int c = 0; c < n; ++c) {  // MovePrimalValuesWithinBounds (:540-555)
+        x[c] = std::min(x[c], orig.col_ub[c]);
+        x[c] = std::max(x[c], orig.col_lb[c]);
+      }
+      for (int row = 0; row < m; ++row) {  // MoveDualValuesWithinBounds (:557-579)
+        double d = optimization_sign * y[row];
+        if (orig.row_lb[row] == -milp::kInf && d > 0.0) d = 0.0;
+        if (orig.row_ub[row] == milp::kInf && d < 0.0) d = 0.0;
+        y[row] = optimization_sign * d;
       }
     }
+    // ProblemObjectiveValue (:306-312).
+    out->objective = orig.scale * (compute_objective() + orig.offset);
+    compute_reduced_costs();
+    std::vector<double> activity(m, 0.0);  // ComputeConstraintActivities (:866-875)
+    for (int c = 0; c < n; ++c) {
+      if (x[c] == 0.0) continue;
+      for (int64_t k = orig.starts[c]; k < orig.starts[c + 1]; ++k) {
+        activity[orig.rows[k]] += x[c] * orig.vals[k];
+      }
+    }
+    // The precision checks of LoadAndVerifySolution (:369-472).
+    bool rhs_too_large = false, cost_too_large = false, primal_inf_too_large = false,
+         dual_inf_too_large = false, primal_res_too_large = false, dual_res_too_large = false;
+    for (int row = 0; row < m; ++row) {  // ComputeMaxRhsPerturbation... (:838-864)
+      const double lb = orig.row_lb[row], ub = orig.row_ub[row], a = activity[row];
+      double err = 0.0, ok = 0.0;
+      if (sol.cstat[row] == MI_LP_AT_LOWER_BOUND || a < lb) {
+        err = std::fabs(a - lb);
+        ok = allowed_error(lb);
+      } else if (sol.cstat[row] == MI_LP_AT_UPPER_BOUND || a > ub) {
+        err = std::fabs(a - ub);
+        ok = allowed_error(ub);
+      }
+      rhs_too_large |= err > ok;
+    }
+    for (int c = 0; c < n; ++c) {  // ComputeMaxCostPerturbation... (:810-834)
+      const double rcm = optimization_sign * reduced[c];
+      const int8_t st = sol.vstat[c];
+      if (st == MI_LP_BASIC || st == MI_LP_FREE || (st == MI_LP_AT_UPPER_BOUND && rcm > 0.0) ||
+          (st == MI_LP_AT_LOWER_BOUND && rcm < 0.0)) {
+        cost_too_large |= std::fabs(rcm) > allowed_error(orig.obj[c]);
+      }
+    }
+    for (int c = 0; c < n; ++c) {  // ComputePrimalValueInfeasibility (:992-1020)
+      const double lb = orig.col_lb[c], ub = orig.col_ub[c];
+      if (lb == ub) {
+        primal_inf_too_large |= std::fabs(x[c] - ub) > allowed_error(ub);
+        continue;
+      }
+      if (x[c] > ub) primal_inf_too_large |= x[c] - ub > allowed_error(ub);
+      if (x[c] < lb) primal_inf_too_large |= lb - x[c] > allowed_error(lb);
+    }
+    for (int row = 0; row < m; ++row) {  // ComputeDualValueInfeasibility (:1073-1095)
+      const double d = optimization_sign * y[row];
+      if (orig.row_lb[row] == -milp::kInf) dual_inf_too_large |= d > tolerance;
+      if (orig.row_ub[row] == milp::kInf) dual_inf_too_large |= -d > tolerance;
+    }
+    for (int row = 0; row < m; ++row) {  // ComputeActivityInfeasibility (:1022-1071)
+      const double lb = orig.row_lb[row], ub = orig.row_ub[row], a = activity[row];
+      if (lb == ub) {
+        primal_res_too_large |= std::fabs(a - ub) > allowed_error(ub);
+        continue;
+      }
+      if (a > ub) primal_res_too_large |= a - ub > allowed_error(ub);
+      if (a < lb) primal_res_too_large |= lb - a > allowed_error(lb);
+    }
+    for (int c = 0; c < n; ++c) {  // ComputeReducedCostInfeasibility (:1097-1122)
+      const double rcm = optimization_sign * reduced[c];
+      const double ok = allowed_error(orig.obj[c]);
+      if (orig.col_lb[c] == -milp::kInf) dual_res_too_large |= rcm > ok;
+      if (orig.col_ub[c] == milp::kInf) dual_res_too_large |= -rcm > ok;
+    }
+    double objective_error_ub = 0.0;  // ComputeMaxExpectedObjectiveError (:977-990)
+    for (int c = 0; c < n; ++c) {
+      objective_error_ub += std::fabs(orig.obj[c]) * allowed_error(x[c]);
+    }
+    if (sp->change_status_to_imprecise) {
+      if (strong && (rhs_too_large || cost_too_large)) verified = MI_LP_IMPRECISE;
+      if (verified == MI_LP_OPTIMAL &&
+          std::fabs(primal_objective - dual_objective) > objective_error_ub) {
+        verified = MI_LP_IMPRECISE;
+      }
+      if ((verified == MI_LP_OPTIMAL || verified == MI_LP_PRIMAL_FEASIBLE) &&
+          (primal_res_too_large || primal_inf_too_large)) {
+        verified = MI_LP_IMPRECISE;
+      }
+      if ((verified == MI_LP_OPTIMAL || verified == MI_LP_DUAL_FEASIBLE) &&
+          (dual_res_too_large || dual_inf_too_large)) {
+        verified = MI_LP_IMPRECISE;
+      }
+    }
+    out->problem_status = verified;
+    if (rc != nullptr) std::copy(reduced.begin(), reduced.end(), rc);
+    if (act != nullptr) std::copy(activity.begin(), activity.end(), act);
     if (primal != nullptr) std::copy(x.begin(), x.end(), primal);
     if (duals != nullptr) std::copy(y.begin(), y.end(), duals);
     if (vstat != nullptr) std::copy(sol.vstat.begin(), sol.vstat.end(), vstat);

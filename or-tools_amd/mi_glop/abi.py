@@ -202,7 +202,7 @@ class MiLpSolverParams(ctypes.Structure):
         ("use_preprocessing", ctypes.c_int32),
         ("use_implied_free_preprocessor", ctypes.c_int32),
         ("solve_dual_problem", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("change_status_to_imprecise", ctypes.c_int32),
         ("dualizer_threshold", ctypes.c_double),
         ("preprocessor_zero_tolerance", ctypes.c_double),
         ("solution_feasibility_tolerance", ctypes.c_double),
@@ -224,7 +224,7 @@ def default_solver_params(**overrides):
                          use_preprocessing=0, use_implied_free_preprocessor=1,
                          solve_dual_problem=LET_SOLVER_DECIDE, dualizer_threshold=1.5,
                          preprocessor_zero_tolerance=1e-9, solution_feasibility_tolerance=1e-6,
-                         drop_tolerance=1e-14)
+                         drop_tolerance=1e-14, change_status_to_imprecise=1)
     for k, v in overrides.items():
         if k not in dict(MiLpSolverParams._fields_):
             raise KeyError(f"unknown LPSolver parameter {k!r}")

@@ -177,3 +177,25 @@ def test_lp_solver_invalid_problem():
                         lp.col_ub, lp.row_lb, lp.row_ub, lp.obj)
     rg, _ = engine.LpHandle().solve_lp(bad)
     assert rg.problem_status == abi.INVALID_PROBLEM
+
+
+@pytest.mark.parametrize("imprecise", [1, 0])
+def test_load_and_verify_flags_imprecise(imprecise):
+    """LoadAndVerifySolution's precision checks (lp_solver.cc:369-472): a
+    simplex answer whose basic values miss the rows by 1e-3 is IMPRECISE when
+    change_status_to_imprecise is set, OPTIMAL otherwise."""
+    lp, _ = kat_lps.test_lp()
+    p = abi.default_params(use_dual_simplex=1)
+
+    def simplex(inner):
+        o = oracle_lib.OracleLp(p)
+        o.load(inner)
+        r = o.solve()
+        v, c = o.statuses()
+        x = o.primal().copy()
+        x[v == abi.BASIC] += 1e-3
+        return r, x, o.duals(), v, c
+
+    r, _ = engine.solve_lp_with(lp, simplex, abi.default_solver_params(
+        change_status_to_imprecise=imprecise))
+    assert r.problem_status == (abi.IMPRECISE if imprecise else abi.OPTIMAL)
