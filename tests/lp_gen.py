@@ -411,3 +411,32 @@ def presolve_lp(m, n, seed, maximize=False, tall=False):
     return LinearProgram(nrows, ncols, np.asarray(cs, np.int64), np.asarray(ri, np.int32),
                          np.asarray(va, float), col_lb, col_ub, row_lb, row_ub, obj, 0.5, 1.0,
                          maximize, f"presolve_{nrows}x{ncols}_s{seed}")
+
+
+def tiny_mixed_lp(rng, max_dim=7):
+    """Small integer-coefficient LP with every bound type (free, one-sided,
+    boxed, fixed, crossing-free), sometimes a duplicated column and row; about
+    a third end optimal, the rest infeasible or unbounded (presolve fuzzing)."""
+    m = int(rng.integers(1, max_dim))
+    n = int(rng.integers(1, max_dim + 1))
+    a = rng.integers(-3, 4, size=(m, n)).astype(float) * (rng.uniform(size=(m, n)) < 0.5)
+    if rng.uniform() < 0.3:
+        if n > 1:
+            a[:, n - 1] = a[:, 0] * rng.choice([-2.0, 0.5, 1.0])
+        if m > 1:
+            a[m - 1, :] = a[0, :] * rng.choice([-1.0, 2.0])
+
+    def bounds(k):
+        lb, ub = np.zeros(k), np.zeros(k)
+        for i in range(k):
+            lo = float(rng.integers(-3, 4))
+            hi = lo + float(rng.integers(0, 4))
+            lb[i], ub[i] = [(lo, hi), (-INF, hi), (lo, INF), (-INF, INF), (lo, lo),
+                            (lo, hi)][int(rng.integers(6))]
+        return lb, ub
+
+    clb, cub = bounds(n)
+    rlb, rub = bounds(m)
+    obj = rng.integers(-3, 4, size=n).astype(float)
+    return LinearProgram.from_dense(a, clb, cub, rlb, rub, obj, float(rng.integers(-2, 3)),
+                                    maximize=bool(rng.integers(2)))
