@@ -45,3 +45,45 @@ def test_solve_cli_on_gpu(tmp_path, capsys, params):
     assert abs(value - 3.236842105263158) <= 1e-9
     assert sol.read_text().startswith("=obj= ")
     assert len(csv.read_text().splitlines()) == 8
+
+
+class _OracleHandle:
+    """Test double for engine.LpHandle: the same LPSolver flow
+    (mi_lp_solver_solve_with) with the CPU oracle as the simplex."""
+
+    def __init__(self, params, device=0):
+        self.params = params
+
+    def set_params(self, p):
+        self.params = p
+
+    def solve_lp(self, model, sp):
+        import oracle_lib
+        from mi_glop import engine
+
+        def simplex(inner):
+            o = oracle_lib.OracleLp(self.params)
+            o.load(inner)
+            r = o.solve()
+            v, c = o.statuses()
+            return r, o.primal(), o.duals(), v, c
+        return engine.solve_lp_with(model, simplex, sp)
+
+
+@pytest.mark.parametrize("params", ["", "use_preprocessing: true",
+                                    "use_preprocessing: true solve_dual_problem: ALWAYS_DO"])
+def test_solve_cli_with_oracle_simplex(tmp_path, capsys, monkeypatch, params):
+    from mi_glop import linear_solver
+    monkeypatch.setattr(linear_solver.engine, "LpHandle", _OracleHandle)
+    sol = tmp_path / "out.sol"
+    csv = tmp_path / "out.csv"
+    rc = solve.main(["--input", os.path.join(GOLDEN, "test2.mps"), "--params", params,
+                     "--sol_file", str(sol), "--output_csv", str(csv)])
+    out = capsys.readouterr().out
+    assert rc == 0, out
+    assert "Status      : MPSOLVER_OPTIMAL" in out and "Dimension   : 5 x 8" in out
+    value = float(out.split("Objective   :")[1].split()[0])
+    assert abs(value - 3.236842105263158) <= 1e-9
+    lines = sol.read_text().splitlines()
+    assert lines[0].startswith("=obj= ") and len(lines) == 9
+    assert len(csv.read_text().splitlines()) == 8
