@@ -286,3 +286,30 @@ def test_presolve_fuzz_statuses(seed):
             elif abi.PRIMAL_UNBOUNDED in base:
                 assert b in (abi.DUAL_INFEASIBLE, abi.INFEASIBLE_OR_UNBOUNDED,
                              abi.PRIMAL_UNBOUNDED), (t, dual, a, b)
+
+
+_SLACK_OF = {abi.BASIC: abi.BASIC, abi.FIXED_VALUE: abi.FIXED_VALUE,
+             abi.AT_LOWER_BOUND: abi.AT_UPPER_BOUND, abi.AT_UPPER_BOUND: abi.AT_LOWER_BOUND,
+             abi.FREE: abi.FREE}
+
+
+@pytest.mark.parametrize("scaling", [0, 1])
+@pytest.mark.parametrize("seed", range(8))
+def test_postsolved_basis_is_an_optimal_basis(seed, scaling):
+    """The postsolved statuses, loaded as a warm start into the simplex on the
+    original LP (constraint -> slack status as LPSolver::SetInitialBasis,
+    lp_solver.cc:268-299), are a nonsingular, primal and dual feasible basis:
+    the simplex stops after 0 iterations at the same objective."""
+    for tall in (False, True):
+        lp = lp_gen.presolve_lp(40 + seed, 90 + 2 * seed, 1200 + seed,
+                                maximize=bool(seed % 2), tall=tall)
+        p = abi.default_params(use_dual_simplex=1)
+        r, sol = _solve(lp, True, 1, use_scaling=scaling)
+        assert r.problem_status == abi.OPTIMAL
+        state = np.concatenate([sol["vstat"], [_SLACK_OF[int(c)] for c in sol["cstat"]]])
+        o = oracle_lib.OracleLp(p)
+        o.load(lp)
+        o.load_basis_state(state.astype(np.int8))
+        ro = o.solve()
+        assert (ro.problem_status, ro.iterations) == (abi.OPTIMAL, 0), (seed, tall)
+        assert abs(ro.objective - r.objective) <= 1e-9 * max(1.0, abs(r.objective))
