@@ -498,7 +498,8 @@ int mi_lp_solver_solve_with(mi_lp_simplex_fn fn, void* user, const mi_lp_solver_
  * (glop/preprocessor.cc:76-147, without the scaling) on a copy of the LP, and
  * DestructiveRecoverSolution (:203-209) for a solution of the presolved LP.
  *   mi_presolve_run       *status = Glop's status after presolve (MI_LP_INIT:
- *                         the simplex must run on the presolved LP)
+ *                         the simplex must run on the presolved LP;
+ *                         MI_LP_INVALID_PROBLEM: IsValid failed, nothing ran)
  *   mi_presolve_dims      presolved sizes and direction (the dualizer turns
  *                         the LP into a maximization)
  *   mi_presolve_get       the presolved LP (any pointer may be NULL)

@@ -885,8 +885,12 @@ int mi_presolve_run(mi_presolve* ps, const mi_lp_solver_params* sp, int32_t m, i
     ps->lp = milp::ToPresolveLp(orig, maximize != 0);
     ps->m0 = m;
     ps->n0 = n;
-    ps->post = ps->pre->Run(&ps->lp);
     ps->ran = true;
+    if (!milp::IsValid(orig, sp->max_valid_magnitude)) {  // lp_solver.cc:196-202
+      *status = MI_LP_INVALID_PROBLEM;
+      return MI_LP_OK;
+    }
+    ps->post = ps->pre->Run(&ps->lp);
     *status = ps->pre->status();
     return MI_LP_OK;
   } catch (const std::exception&) {

@@ -313,3 +313,12 @@ def test_postsolved_basis_is_an_optimal_basis(seed, scaling):
         ro = o.solve()
         assert (ro.problem_status, ro.iterations) == (abi.OPTIMAL, 0), (seed, tall)
         assert abs(ro.objective - r.objective) <= 1e-9 * max(1.0, abs(r.objective))
+
+
+def test_presolve_rejects_invalid_lp():
+    """LPSolver checks IsValid before presolve (lp_solver.cc:196-202)."""
+    lp = _lp([[1, 1]], [0, 2], [1, 1], [0], [1], [1, 1])  # x1 has lb > ub
+    ps = engine.Presolve()
+    assert ps.run(lp) == abi.INVALID_PROBLEM and ps.passes() == []
+    r, _ = _solve(lp, True)
+    assert r.problem_status == abi.INVALID_PROBLEM
