@@ -65,6 +65,11 @@ def _assert_feasible(lp, sol, tol=1e-9):
     above_lb = x > lp.col_lb + tol
     below_ub = x < lp.col_ub - tol
     assert np.all(rc[above_lb] <= tol) and np.all(rc[below_ub] >= -tol)
+    # Complementary slackness on the rows (minimization sense): a row strictly
+    # above its lower bound has dual <= 0, strictly below its upper bound >= 0.
+    y = sign * sol["y"]
+    assert np.all(y[act > lp.row_lb + tol * scale(lp.row_lb)] <= tol)
+    assert np.all(y[act < lp.row_ub - tol * scale(lp.row_ub)] >= -tol)
 
 
 @pytest.mark.parametrize("tall", [False, True], ids=["wide", "tall"])
