@@ -652,7 +652,7 @@ class ProportionalColumnPass : public Pass {
         } else {
           s->primal[col] = to_upper ? ubs_[col] - scaled_distance : lbs_[col] + scaled_distance;
           s->vstat[col] = rep_basic[rep]
-                              ? kBasic
+                              ? static_cast<int8_t>(kBasic)
                               : ComputeVariableStatus(s->primal[col], lbs_[col], ubs_[col]);
           distance[rep] = 0.0;
           rep_basic[rep] = false;
