@@ -1,0 +1,108 @@
+// Memory/UB check of the LPSolver flow (or-tools_amd/csrc/engine/lp_solver.cc:
+// presolve, scaling, postsolve, LoadAndVerifySolution) through
+// mi_lp_solver_solve_with, with a fake simplex that returns arbitrary
+// statuses and values of the right sizes. Built and run by
+// tests/test_presolve_native.py with ASan + UBSan; the engine entry points
+// that mi_lp_solver_solve uses are link stubs here (never called).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <random>
+#include <vector>
+
+#include "../../include/mi_lp.h"
+
+extern "C" {
+int mi_lp_load(mi_lp*, int32_t, int32_t, const int64_t*, const int32_t*, const double*,
+               const double*, const double*, const double*, const double*, const double*,
+               double, double, int32_t) { return MI_LP_ERROR_DEVICE; }
+int mi_lp_solve(mi_lp*, const volatile int32_t*, mi_lp_result*) { return MI_LP_ERROR_DEVICE; }
+int mi_lp_get_primal(const mi_lp*, double*) { return MI_LP_ERROR_DEVICE; }
+int mi_lp_get_duals(const mi_lp*, double*) { return MI_LP_ERROR_DEVICE; }
+int mi_lp_get_statuses(const mi_lp*, int8_t*, int8_t*) { return MI_LP_ERROR_DEVICE; }
+}
+
+static std::mt19937_64 rng(11);
+static int I(int a, int b) { return std::uniform_int_distribution<int>(a, b)(rng); }
+
+static int FakeSimplex(void*, int32_t m, int32_t n, const int64_t* cs, const int32_t* ri,
+                       const double*, const double* clb, const double* cub, const double*,
+                       const double*, const double*, double, double, int32_t,
+                       mi_lp_result* out, double* x, double* y, int8_t* vs, int8_t* cst) {
+  if (cs[0] != 0) return MI_LP_ERROR_INTERNAL;
+  for (int64_t k = 0; k < cs[n]; ++k) {
+    if (ri[k] < 0 || ri[k] >= m) return MI_LP_ERROR_INTERNAL;
+  }
+  std::memset(out, 0, sizeof(*out));
+  out->problem_status = I(0, 11);
+  out->iterations = I(0, 50);
+  for (int j = 0; j < n; ++j) {
+    vs[j] = static_cast<int8_t>(I(0, 4));
+    x[j] = std::isfinite(clb[j]) ? clb[j] : (std::isfinite(cub[j]) ? cub[j] : 0.0);
+  }
+  for (int i = 0; i < m; ++i) {
+    cst[i] = static_cast<int8_t>(I(0, 4));
+    y[i] = I(-2, 2);
+  }
+  return MI_LP_OK;
+}
+
+int main(int argc, char** argv) {
+  const int N = argc > 1 ? atoi(argv[1]) : 2000;
+  const double inf = std::numeric_limits<double>::infinity();
+  int statuses[12] = {0};
+  for (int t = 0; t < N; ++t) {
+    const int m = I(0, 10), n = I(0, 12);
+    std::vector<int64_t> cs(1, 0);
+    std::vector<int32_t> ri;
+    std::vector<double> v;
+    for (int c = 0; c < n; ++c) {
+      for (int r = 0; r < m; ++r) {
+        if (I(0, 2) == 0) {
+          const int a = I(-3, 3);
+          if (a != 0) {
+            ri.push_back(r);
+            v.push_back(a);
+          }
+        }
+      }
+      cs.push_back(static_cast<int64_t>(ri.size()));
+    }
+    auto bounds = [&](std::vector<double>& lb, std::vector<double>& ub, int k) {
+      lb.resize(k);
+      ub.resize(k);
+      for (int i = 0; i < k; ++i) {
+        const double a = I(-3, 3), b = a + I(0, 3);
+        const int ty = I(0, 5);
+        lb[i] = (ty == 1 || ty == 3) ? -inf : a;
+        ub[i] = (ty == 2 || ty == 3) ? inf : (ty == 4 ? a : b);
+      }
+    };
+    std::vector<double> clb, cub, rlb, rub, obj(n);
+    bounds(clb, cub, n);
+    bounds(rlb, rub, m);
+    for (auto& o : obj) o = I(-3, 3);
+    mi_lp_solver_params sp;
+    mi_lp_solver_params_default(&sp);
+    sp.use_preprocessing = I(0, 1);
+    sp.use_scaling = I(0, 1);
+    sp.solve_dual_problem = I(0, 2);
+    mi_lp_result r;
+    std::vector<double> x(n), y(m), rc(n), act(m);
+    std::vector<int8_t> vs(n), cst(m);
+    const int rc_flow = mi_lp_solver_solve_with(
+        FakeSimplex, nullptr, &sp, m, n, cs.data(), ri.data(), v.data(), clb.data(), cub.data(),
+        rlb.data(), rub.data(), obj.data(), 0.5, 1.0, I(0, 1), &r, x.data(), y.data(), rc.data(),
+        act.data(), vs.data(), cst.data());
+    if (rc_flow != MI_LP_OK) {
+      printf("flow error %d at %d\n", rc_flow, t);
+      return 1;
+    }
+    statuses[r.problem_status]++;
+  }
+  printf("ok %d LPs; statuses", N);
+  for (int s = 0; s < 12; ++s) printf(" %d", statuses[s]);
+  printf("\n");
+  return 0;
+}
