@@ -31,22 +31,6 @@ def test_model_extraction_is_the_mps_lp():
     assert [x.name() for x in xs] == lp.col_names
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("params", ["", "use_preprocessing: true"])
-def test_solve_cli_on_gpu(tmp_path, capsys, params):
-    sol = tmp_path / "out.sol"
-    csv = tmp_path / "out.csv"
-    rc = solve.main(["--input", os.path.join(GOLDEN, "test2.mps"), "--params", params,
-                     "--sol_file", str(sol), "--output_csv", str(csv)])
-    out = capsys.readouterr().out
-    assert rc == 0
-    assert "Status      : MPSOLVER_OPTIMAL" in out
-    value = float(out.split("Objective   :")[1].split()[0])
-    assert abs(value - 3.236842105263158) <= 1e-9
-    assert sol.read_text().startswith("=obj= ")
-    assert len(csv.read_text().splitlines()) == 8
-
-
 class _OracleHandle:
     """Test double for engine.LpHandle: the same LPSolver flow
     (mi_lp_solver_solve_with) with the CPU oracle as the simplex."""
