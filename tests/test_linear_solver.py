@@ -186,3 +186,17 @@ def test_solver_specific_parameters_text():
     assert s._params.use_dual_simplex == 1
     assert not s.SetSolverSpecificParametersAsString("no_such_field: 3")
     assert not s.SetSolverSpecificParametersAsString("solve_dual_problem: SOMETIMES")
+
+
+def test_mpsolver_path_with_oracle_simplex(monkeypatch):
+    """The GPU tests above, with the engine handle replaced by the same
+    LPSolver flow over the CPU oracle (test_solve_cli._OracleHandle): the
+    MPSolver mirror's extraction, parameters, status map and solution
+    accessors on CPU."""
+    import test_solve_cli
+    monkeypatch.setattr(linear_solver.engine, "LpHandle", test_solve_cli._OracleHandle)
+    test_solve_through_engine(lp_test_model, dict(objective=34.0, primal=[6, 4]))
+    test_solve_through_engine(simple_glop_model, dict(objective=4.0, primal=[1, 1]))
+    test_solve_through_engine(model_builder_model, dict(objective=733.3333333333334 - 5.5,
+                                                        primal=[100.0 / 3, 200.0 / 3, 0.0]))
+    test_infeasible_and_unbounded_status_maps()
