@@ -606,12 +606,27 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
         log(f"batched: LPs solved in this process: {len(lbs) + 1}")
     for w in workers:
         w.reset_kernel_stats()
+    # The bound share goes through the engine's C ABI (mi_lp_share_bound:
+    # ncclAllReduce on a device buffer, engine/comm.hip), as a C++ CP-SAT host
+    # would call it; the unique id travels over the process group. Rehearsals
+    # with every rank on one GPU (RCCL refuses that) use the process group.
+    comm, share = None, "torch.distributed all_reduce (" + ("gloo" if COLL_DEVICE == "cpu"
+                                                            else "rccl") + ")"
+    if COLL_DEVICE != "cpu":
+        try:
+            comm = distributed.NativeComm(rank, world, local_rank, dist=dist)
+            share = "mi_lp_share_bound (RCCL ncclAllReduce max, float64, device buffer)"
+        except Exception as e:  # reported in the line, never a reason to fail
+            log(f"batched: native RCCL communicator unavailable: {e}")
     barrier()
     sync()
     t0 = time.perf_counter()
     res = engine.batch_solve_bounds(workers, lbs, ubs, state)
     summary = cpsat.fold_node(cpsat.IntegerTrail(node.lb, node.ub, node.obj_lb), x, cols, res)
-    node_lb = -distributed.share_bound(-summary["obj_lb"], dist, COLL_DEVICE)  # all-reduce(max)
+    if comm is not None:
+        node_lb = comm.share_bound(summary["obj_lb"], distributed.NativeComm.MAX)
+    else:
+        node_lb = -distributed.share_bound(-summary["obj_lb"], dist, COLL_DEVICE)
     sync()
     barrier()
     elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dist, COLL_DEVICE)
@@ -623,7 +638,7 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
         "host_threads_per_gpu": min(n_workers, 16),
         "mean_iterations": float(np.mean([r.iterations for r in res])) if res else 0.0,
         "root_objective": float(root_res.objective), "root_iterations": int(root_res.iterations),
-        "node_obj_lb": node_lb, "deductions": int(summary["deductions"]),
+        "node_obj_lb": node_lb, "bound_share": share, "deductions": int(summary["deductions"]),
         "speculative_lps": int(summary["speculative"]),
         "workload": (f"config 4: job-shop {args.batch_jobs}x{args.batch_machines} (seeded "
                      f"Taillard-style instance; ta041 itself is 50x10) big-M LP relaxation, m={lp.m} n={lp.n}; one search "
@@ -632,6 +647,8 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
                      f"iterations"),
     }
     out["roofline"] = batched_roofline(workers, elapsed, None, args.c4_traffic_json, len(lbs))
+    if comm is not None:
+        comm.close()
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_lib
         ows = [oracle_lib.OracleLp(p) for _ in range(args.batch_cpu_threads)]

@@ -387,6 +387,38 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
                              const double* lbs, const double* ubs, const int8_t* warm_state,
                              int32_t warm_len, mi_lp_result* results);
 
+/* Multi-GPU bound sharing over RCCL: the batched LPs are
+ * sharded across GPUs with no data-path collective; the one exchange is the
+ * search's objective bound, an all-reduce(min) of one float64 over xGMI —
+ * the cross-GPU analogue of SharedResponseManager::UpdateInnerObjectiveBounds
+ * (ortools/sat/synchronization.h:306), which a CP-SAT worker thread calls
+ * with its LP's bound. One communicator per rank (process or thread), bound
+ * to a GPU; its unique id is created once (mi_lp_comm_get_unique_id, rank 0)
+ * and handed to every rank out of band, as ncclGetUniqueId's. RCCL is ROCm's
+ * librccl.so.1, opened privately (dlopen RTLD_LOCAL). Errors: MI_LP_ERROR_DEVICE
+ * (message in mi_lp_comm_last_error; with c == NULL, why RCCL is unusable). */
+typedef struct mi_lp_comm mi_lp_comm;
+enum { MI_LP_COMM_ID_BYTES = 128 };
+enum { MI_LP_BOUND_MIN = 0, MI_LP_BOUND_MAX = 1 };
+int mi_lp_comm_get_unique_id(uint8_t* id /* MI_LP_COMM_ID_BYTES */);
+/* Collective over the nranks ranks (ncclCommInitRank): blocks until all join. */
+int mi_lp_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device,
+                      mi_lp_comm** out);
+int32_t mi_lp_comm_rank(const mi_lp_comm* c);
+int32_t mi_lp_comm_size(const mi_lp_comm* c);
+/* *bound <- min (MI_LP_BOUND_MIN) or max over the ranks of *bound: the value
+ * goes through an 8-byte device buffer and one ncclAllReduce(ncclFloat64);
+ * returns once the result is on the host. Every rank must call it. */
+int mi_lp_share_bound(mi_lp_comm* c, double* bound, int32_t op);
+/* The same reduction in place on a caller's device buffer of count doubles,
+ * and an all-gather of bytes_per_rank bytes per rank between device buffers
+ * (recv holds nranks blocks in rank order). Synchronous. */
+int mi_lp_comm_allreduce_device(mi_lp_comm* c, double* d_values, int64_t count, int32_t op);
+int mi_lp_comm_allgather_device(mi_lp_comm* c, const void* d_send, void* d_recv,
+                                int64_t bytes_per_rank);
+const char* mi_lp_comm_last_error(const mi_lp_comm* c);
+void mi_lp_comm_destroy(mi_lp_comm* c);
+
 /* MPS ingestion: the reader that fills the
  * LinearProgram handed to mi_lp_load, replacing
  *   glop::MPSReader::ParseFile / ParseString   (ortools/lp_data/mps_reader.h:39-60,
@@ -422,8 +454,11 @@ void mi_mps_free(mi_mps_model* m);
  * ScaleBounds, lp_data.cc:1190-1258), the engine solve on handle h, then
  * ScalingPreprocessor::RecoverSolution (preprocessor.cc:3878-3912) and the
  * value part of LoadAndVerifySolution (lp_solver.cc:334-367: reduced costs,
- * Kahan objective, strong-optimal moves, activities). Presolve passes other
- * than the scaling (use_preprocessing) are not built. out->objective is the
+ * Kahan objective, strong-optimal moves, activities). With use_preprocessing
+ * (the default, as in Glop) MainLpPreprocessor's passes run before the
+ * scaling and their postsolve after it (engine/presolve.cc),
+ * and the postsolved solution goes through IsProblemSolutionConsistent
+ * (lp_solver.cc:679-790; inconsistent = ABNORMAL). out->objective is the
  * unscaled problem objective; the arrays (n / m entries, any may be NULL)
  * are the unscaled solution. An invalid LP gives MI_LP_OK with
  * problem_status MI_LP_INVALID_PROBLEM, as LPSolver returns it. */
@@ -438,10 +473,9 @@ typedef struct mi_lp_solver_params {
   int32_t cost_scaling;                     /* 60, CONTAIN_ONE_COST_SCALING */
   int32_t provide_strong_optimal_guarantee; /* 24, true */
   double max_valid_magnitude;               /* 199, 1e30 */
-  /* Presolve: MainLpPreprocessor's passes (preprocessor.cc:76-147). Glop's
-   * default for use_preprocessing is true; this layer's default is 0 (scaling
-   * only) until the presolve path has run on the GPU box, see DESIGN.md §4e. */
-  int32_t use_preprocessing;                /* 34 */
+  /* Presolve: MainLpPreprocessor's passes (preprocessor.cc:76-147), on by
+   * default as in Glop (parameters.proto:326); 0 = scaling only. DESIGN.md §6a. */
+  int32_t use_preprocessing;                /* 34, true */
   int32_t use_implied_free_preprocessor;    /* 67, true */
   int32_t solve_dual_problem;               /* 20, LET_SOLVER_DECIDE (ALWAYS_DO 0,
                                                NEVER_DO 1, LET_SOLVER_DECIDE 2) */

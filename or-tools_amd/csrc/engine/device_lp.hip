@@ -294,7 +294,10 @@ class SmallBatcher {
   }
   void Submit(int kind, int id) {
     {
-      std::lock_guard<std::mutex> lock(mu_);
+      std::unique_lock<std::mutex> lock(mu_);
+      // A Stop() in progress owns the launcher and the streams until it has
+      // joined the one and destroyed the others; a restart waits for it.
+      stopped_cv_.wait(lock, [&] { return !stopping_; });
       pending_[kind].push_back(id);
       ++num_pending_;
       if (!launcher_.joinable()) {  // stopped by ShutdownAll: start again
@@ -307,18 +310,30 @@ class SmallBatcher {
   }
 
   ~SmallBatcher() { Stop(); }
-  // The launcher finishes the requests already pending, then exits.
+  // The launcher finishes the requests already pending, then exits. The
+  // thread object moves out under the lock and `stopping_` holds off
+  // restarts (Submit) and other Stop() calls until the streams are gone.
   void Stop() {
+    std::thread launcher;
     {
-      std::lock_guard<std::mutex> lock(mu_);
+      std::unique_lock<std::mutex> lock(mu_);
+      stopped_cv_.wait(lock, [&] { return !stopping_; });
+      if (!launcher_.joinable()) return;  // never started, or already stopped
       stop_ = true;
+      stopping_ = true;
+      launcher = std::move(launcher_);
     }
     cv_.notify_one();
-    if (launcher_.joinable()) launcher_.join();
-    for (hipStream_t& st : streams_) {
-      if (st != nullptr) (void)hipStreamDestroy(st);
-      st = nullptr;
+    launcher.join();
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      for (hipStream_t& st : streams_) {
+        if (st != nullptr) (void)hipStreamDestroy(st);
+        st = nullptr;
+      }
+      stopping_ = false;
     }
+    stopped_cv_.notify_all();
   }
 
  private:
@@ -439,6 +454,8 @@ class SmallBatcher {
   bool in_flight_[kStreams] = {};
   std::mutex mu_;
   std::condition_variable cv_;
+  std::condition_variable stopped_cv_;  // a Stop() in progress has finished
+  bool stopping_ = false;
   std::thread launcher_;
   bool stop_ = false;
   int num_pending_ = 0;

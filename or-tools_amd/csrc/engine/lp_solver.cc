@@ -328,6 +328,11 @@ bool IsValid(const ScaledLp& lp, double max_magnitude) {
 
 // LPSolver::IsProblemSolutionConsistent (lp_solver.cc:679-790).
 bool IsSolutionConsistent(const ScaledLp& lp, const presolve::Solution& s) {
+  // The size checks come first (:683-686): a postsolve or a caller-supplied
+  // simplex that returned a wrong-sized solution is ABNORMAL, never indexed.
+  const size_t n = static_cast<size_t>(lp.n), m = static_cast<size_t>(lp.m);
+  if (s.vstat.size() != n || s.cstat.size() != m) return false;
+  if (s.primal.size() != n || s.dual.size() != m) return false;
   if (s.status != MI_LP_OPTIMAL && s.status != MI_LP_PRIMAL_FEASIBLE &&
       s.status != MI_LP_DUAL_FEASIBLE) {
     return true;
@@ -515,7 +520,7 @@ void mi_lp_solver_params_default(mi_lp_solver_params* p) {
   p->cost_scaling = MI_LP_CONTAIN_ONE_COST_SCALING;  // :209-210
   p->provide_strong_optimal_guarantee = 1;  // :271
   p->max_valid_magnitude = 1e30;            // max_valid_magnitude default
-  p->use_preprocessing = 0;                 // Glop: true (:326); see mi_lp.h
+  p->use_preprocessing = 1;                 // :326
   p->change_status_to_imprecise = 1;        // :275
   p->use_implied_free_preprocessor = 1;     // :473
   p->solve_dual_problem = 2;                // :236, LET_SOLVER_DECIDE
@@ -523,6 +528,31 @@ void mi_lp_solver_params_default(mi_lp_solver_params* p) {
   p->preprocessor_zero_tolerance = 1e-9;    // :356
   p->solution_feasibility_tolerance = 1e-6; // :251
   p->drop_tolerance = 1e-14;                // :183
+}
+
+// Test hook (tests/native/lp_solver_asan.cc): IsProblemSolutionConsistent
+// on an m x n LP with no constraints on its values and a solution whose
+// vectors have the given lengths: free columns at 0, basic slacks (the slack
+// basis, consistent when the sizes are right). Returns 1 when
+// consistent; a wrong-sized solution must be 0 (and must not be indexed).
+int milp_test_solution_consistent(int32_t m, int32_t n, int32_t status, int64_t primal_len,
+                                  int64_t dual_len, int64_t vstat_len, int64_t cstat_len) {
+  milp::ScaledLp lp;
+  lp.m = m;
+  lp.n = n;
+  lp.starts.assign(static_cast<size_t>(n) + 1, 0);
+  lp.col_lb.assign(n, -milp::kInf);
+  lp.col_ub.assign(n, milp::kInf);
+  lp.obj.assign(n, 0.0);
+  lp.row_lb.assign(m, -milp::kInf);
+  lp.row_ub.assign(m, milp::kInf);
+  milp::presolve::Solution s;
+  s.status = status;
+  s.primal.assign(primal_len, 0.0);
+  s.dual.assign(dual_len, 0.0);
+  s.vstat.assign(vstat_len, static_cast<int8_t>(MI_LP_FREE));
+  s.cstat.assign(cstat_len, static_cast<int8_t>(MI_LP_BASIC));
+  return milp::IsSolutionConsistent(lp, s) ? 1 : 0;
 }
 
 }  // extern "C"
@@ -954,7 +984,9 @@ int mi_presolve_recover(mi_presolve* ps, int32_t* status, const double* primal,
     if (ps->post) ps->pre->Recover(&s);
     ps->recovered = true;
     if (static_cast<int32_t>(s.primal.size()) != ps->n0 ||
-        static_cast<int32_t>(s.dual.size()) != ps->m0) {
+        static_cast<int32_t>(s.dual.size()) != ps->m0 ||
+        static_cast<int32_t>(s.vstat.size()) != ps->n0 ||
+        static_cast<int32_t>(s.cstat.size()) != ps->m0) {
       return MI_LP_ERROR_INTERNAL;
     }
     *status = s.status;

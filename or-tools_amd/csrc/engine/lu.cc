@@ -1183,14 +1183,14 @@ Status BasisFactorization::ComputeFactorization() {
     mix(bits);
     mix(static_cast<uint64_t>(p.markowitz_zlatev_parameter));
     share_key = h | 1;
-    shared = lu_share_->Find(share_key);
+    shared = lu_share_->Find(share_key, basis_);
   }
   Status status;
   if (shared != nullptr) {
     lu_factorization_.AdoptFactorizationOf(*shared);
   } else {
     status = lu_factorization_.ComputeFactorization(basis_matrix);
-    if (share_key != 0 && status.ok()) lu_share_->Insert(share_key, lu_factorization_);
+    if (share_key != 0 && status.ok()) lu_share_->Insert(share_key, basis_, lu_factorization_);
   }
   ++num_factorizations_;
   factorization_seconds_ +=

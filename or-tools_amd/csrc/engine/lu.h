@@ -1280,6 +1280,7 @@ class BasisFactorization {
   // that loaded the same matrix with the same LU parameters and hold equal
   // keys hold the same factorization (Markowitz is deterministic).
   uint64_t FactorizationContentKey() const;
+  const std::vector<int>& basis() const { return basis_; }
   // Factorizations shared by the handles of one batch call (LuShareCache,
   // engine only): a fresh factorization of a basis the cache holds adopts
   // the cached factors instead of running Markowitz.
@@ -1337,29 +1338,37 @@ class BasisFactorization {
 // Factorizations of one batch call's handles (mi_lp_batch_solve_bounds: the
 // children of a node load the same matrix and start from the same basis),
 // keyed by the basis matrix's columns, its size and the LU parameters.
+// An entry also keeps its basis, compared exactly on a hit (the key is a
+// hash); the batch call shares the cache only between handles whose loaded
+// matrices have the same fingerprint.
 struct LuShareCache {
+  struct Entry {
+    uint64_t key;
+    std::vector<int> basis;
+    std::shared_ptr<const LuFactorization> lu;
+  };
   std::mutex mu;
-  std::vector<std::pair<uint64_t, std::shared_ptr<const LuFactorization>>> entries;
+  std::vector<Entry> entries;
   static constexpr size_t kMaxEntries = 4;
-  std::shared_ptr<const LuFactorization> Find(uint64_t key) {
+  std::shared_ptr<const LuFactorization> Find(uint64_t key, const std::vector<int>& basis) {
     std::lock_guard<std::mutex> l(mu);
     for (const auto& e : entries) {
-      if (e.first == key) return e.second;
+      if (e.key == key && e.basis == basis) return e.lu;
     }
     return nullptr;
   }
-  void Insert(uint64_t key, const LuFactorization& lu) {
+  void Insert(uint64_t key, const std::vector<int>& basis, const LuFactorization& lu) {
     {
       std::lock_guard<std::mutex> l(mu);
       if (entries.size() >= kMaxEntries) return;
       for (const auto& e : entries) {
-        if (e.first == key) return;
+        if (e.key == key && e.basis == basis) return;
       }
     }
     auto copy = std::make_shared<LuFactorization>();
     copy->AdoptFactorizationOf(lu);
     std::lock_guard<std::mutex> l(mu);
-    if (entries.size() < kMaxEntries) entries.emplace_back(key, std::move(copy));
+    if (entries.size() < kMaxEntries) entries.push_back(Entry{key, basis, std::move(copy)});
   }
 };
 

@@ -758,23 +758,34 @@ void VariablesInfo::EndDualPhaseI(Fractional tol, const std::vector<Fractional>&
 // content; a hit copies the values and replays the loop's deterministic-time
 // bumps, so every result is the one a solve computing its own norms gets.
 struct DualNormCache {
+  struct Entry {
+    uint64_t key;
+    std::vector<int> basis, row_perm, col_perm;  // compared exactly on a hit
+    std::shared_ptr<const std::vector<Fractional>> norms;
+  };
   std::mutex mu;
-  std::vector<std::pair<uint64_t, std::shared_ptr<const std::vector<Fractional>>>> entries;
+  std::vector<Entry> entries;
   static constexpr size_t kMaxEntries = 8;
-  std::shared_ptr<const std::vector<Fractional>> Find(uint64_t key) {
+  std::shared_ptr<const std::vector<Fractional>> Find(uint64_t key, const std::vector<int>& basis,
+                                                      const std::vector<int>& row_perm,
+                                                      const std::vector<int>& col_perm) {
     std::lock_guard<std::mutex> l(mu);
     for (const auto& e : entries) {
-      if (e.first == key) return e.second;
+      if (e.key == key && e.basis == basis && e.row_perm == row_perm && e.col_perm == col_perm) {
+        return e.norms;
+      }
     }
     return nullptr;
   }
-  void Insert(uint64_t key, const std::vector<Fractional>& v) {
+  void Insert(uint64_t key, const std::vector<int>& basis, const std::vector<int>& row_perm,
+              const std::vector<int>& col_perm, const std::vector<Fractional>& v) {
     std::lock_guard<std::mutex> l(mu);
     if (entries.size() >= kMaxEntries) return;
     for (const auto& e : entries) {
-      if (e.first == key) return;
+      if (e.key == key && e.basis == basis) return;
     }
-    entries.emplace_back(key, std::make_shared<const std::vector<Fractional>>(v));
+    entries.push_back(
+        Entry{key, basis, row_perm, col_perm, std::make_shared<const std::vector<Fractional>>(v)});
   }
 };
 
@@ -845,7 +856,8 @@ class DualEdgeNorms {
     uint64_t key = 0;
     if (cache_ != nullptr && bf_.NumUpdates() == 0) {
       key = bf_.FactorizationContentKey();
-      const auto hit = cache_->Find(key);
+      const auto hit = cache_->Find(key, bf_.basis(), bf_.lu().row_perm(),
+                                    bf_.lu().GetColumnPermutation());
       if (hit != nullptr && static_cast<int>(hit->size()) == num_rows) {
         norms_ = *hit;
         for (int row = 0; row < num_rows; ++row) bf_.BumpDeterministicTimeForSolve(1);
@@ -856,7 +868,10 @@ class DualEdgeNorms {
     norms_.resize(num_rows, 0.0);
     for (int row = 0; row < num_rows; ++row) norms_[row] = bf_.DualEdgeSquaredNorm(row);
     recompute_ = false;
-    if (key != 0) cache_->Insert(key, norms_);
+    if (key != 0) {
+      cache_->Insert(key, bf_.basis(), bf_.lu().row_perm(), bf_.lu().GetColumnPermutation(),
+                     norms_);
+    }
   }
  public:
   void SetCache(DualNormCache* cache) { cache_ = cache; }
@@ -5895,6 +5910,21 @@ int LoadLp(mi_lp* h, int32_t m, int32_t n, const int64_t* cs, const int32_t* ri,
   lp.obj_offset = obj_offset;
   lp.obj_scale = obj_scale;
   lp.maximize = maximize != 0;
+  {
+    // 64-bit multiply-xor over the matrix words (a few GB/s; once per load).
+    uint64_t f = 0x243f6a8885a308d3ull ^ (static_cast<uint64_t>(m) << 32 | static_cast<uint32_t>(n));
+    auto mix = [&f](uint64_t v) {
+      f ^= v + 0x9e3779b97f4a7c15ull + (f << 6) + (f >> 2);
+      f *= 0xff51afd7ed558ccdull;
+    };
+    for (const int64_t v : lp.col_starts) mix(static_cast<uint64_t>(v));
+    for (int64_t k = 0; k < nnz; ++k) {
+      uint64_t bits;
+      std::memcpy(&bits, &lp.vals[k], 8);
+      mix(bits ^ (static_cast<uint64_t>(static_cast<uint32_t>(lp.row_idx[k])) << 1));
+    }
+    lp.matrix_fingerprint = f;
+  }
   h->loaded = true;
   h->solved = false;
   return MI_LP_OK;
@@ -6471,8 +6501,16 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
     const char* e = std::getenv(name);
     return e != nullptr && std::atoi(e) != 0;
   };
-  const bool shared_norms = env_on("MILP_BATCH_SHARED_NORMS");
-  const bool shared_lu = env_on("MILP_BATCH_SHARED_LU");
+  // Only between handles that loaded the same matrix (fingerprint at load;
+  // the cache entries also compare their basis exactly on a hit).
+  bool same_matrix = true;
+  for (int w = 1; w < num_workers; ++w) {
+    same_matrix = same_matrix &&
+                  workers[w]->lp.matrix_fingerprint == workers[0]->lp.matrix_fingerprint &&
+                  workers[w]->lp.col_starts.back() == workers[0]->lp.col_starts.back();
+  }
+  const bool shared_norms = same_matrix && env_on("MILP_BATCH_SHARED_NORMS");
+  const bool shared_lu = same_matrix && env_on("MILP_BATCH_SHARED_LU");
   milp::DualNormCache norm_cache;
   milp::LuShareCache lu_cache;
   for (int w = 0; w < num_workers; ++w) {

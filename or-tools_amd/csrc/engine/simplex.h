@@ -80,6 +80,9 @@ struct LinearProgram {
   double obj_offset = 0.0;
   double obj_scale = 1.0;
   bool maximize = false;
+  // Hash of (m, n, col_starts, row_idx, vals) set at load: the batch caches
+  // are shared only between handles whose matrices hash alike.
+  uint64_t matrix_fingerprint = 0;
 };
 
 // util/time_limit.h subset: wall clock + deterministic time + interrupt.

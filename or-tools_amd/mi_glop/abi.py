@@ -186,6 +186,9 @@ EXPORTED_SYMBOLS = [
     "mi_lp_batch_solve_gpus", "mi_lp_solver_solve_with",
     "mi_presolve_create", "mi_presolve_destroy", "mi_presolve_run", "mi_presolve_dims",
     "mi_presolve_get", "mi_presolve_recover", "mi_presolve_num_passes", "mi_presolve_pass_name",
+    "mi_lp_comm_get_unique_id", "mi_lp_comm_create", "mi_lp_comm_rank", "mi_lp_comm_size",
+    "mi_lp_share_bound", "mi_lp_comm_allreduce_device", "mi_lp_comm_allgather_device",
+    "mi_lp_comm_last_error", "mi_lp_comm_destroy",
 ]
 
 
@@ -221,7 +224,7 @@ def default_solver_params(**overrides):
     p = MiLpSolverParams(use_scaling=1, scaling_method=EQUILIBRATION,
                          cost_scaling=CONTAIN_ONE_COST_SCALING,
                          provide_strong_optimal_guarantee=1, max_valid_magnitude=1e30,
-                         use_preprocessing=0, use_implied_free_preprocessor=1,
+                         use_preprocessing=1, use_implied_free_preprocessor=1,
                          solve_dual_problem=LET_SOLVER_DECIDE, dualizer_threshold=1.5,
                          preprocessor_zero_tolerance=1e-9, solution_feasibility_tolerance=1e-6,
                          drop_tolerance=1e-14, change_status_to_imprecise=1)

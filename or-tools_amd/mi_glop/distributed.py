@@ -56,6 +56,72 @@ def share_bound(best, dist=None, device=None):
     return float(t.item())
 
 
+class NativeComm:
+    """The engine's RCCL communicator (mi_lp_comm_*, engine/comm.hip): the
+    C-ABI path a C++ CP-SAT host uses to share its bound across GPUs
+    (sat/synchronization.h:306) without Python. Here the unique id travels
+    over an existing process group (any backend); the all-reduce itself is
+    ncclAllReduce(ncclFloat64, min/max) on the engine's device buffer."""
+
+    MIN, MAX = 0, 1
+
+    def __init__(self, rank, world, device, uid=None, dist=None):
+        import ctypes
+        from . import engine
+        self._L = L = engine.lib()
+        if uid is None:
+            buf = (ctypes.c_uint8 * 128)()
+            if rank == 0 and L.mi_lp_comm_get_unique_id(buf) != 0:
+                raise RuntimeError("mi_lp_comm_get_unique_id: " +
+                                   (L.mi_lp_comm_last_error(None) or b"").decode())
+            uid = bytes(buf)
+            if dist is not None and world > 1:
+                box = [uid]
+                dist.broadcast_object_list(box, src=0)
+                uid = box[0]
+        self._buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        self._h = ctypes.c_void_p()
+        rc = L.mi_lp_comm_create(self._buf, world, rank, device, ctypes.byref(self._h))
+        if rc != 0:
+            raise RuntimeError(f"mi_lp_comm_create failed ({rc}): " +
+                               (L.mi_lp_comm_last_error(None) or b"").decode())
+
+    @staticmethod
+    def unique_id():
+        import ctypes
+        from . import engine
+        buf = (ctypes.c_uint8 * 128)()
+        if engine.lib().mi_lp_comm_get_unique_id(buf) != 0:
+            raise RuntimeError("mi_lp_comm_get_unique_id failed")
+        return bytes(buf)
+
+    def rank(self):
+        return self._L.mi_lp_comm_rank(self._h)
+
+    def size(self):
+        return self._L.mi_lp_comm_size(self._h)
+
+    def share_bound(self, value, op=MIN):
+        import ctypes
+        v = ctypes.c_double(value)
+        rc = self._L.mi_lp_share_bound(self._h, ctypes.byref(v), op)
+        if rc != 0:
+            raise RuntimeError(f"mi_lp_share_bound failed ({rc}): " +
+                               self._L.mi_lp_comm_last_error(self._h).decode())
+        return v.value
+
+    def close(self):
+        if self._h:
+            self._L.mi_lp_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def max_over_ranks(x, dist=None, device=None):
     """Wall time of the slowest rank (the bench contract's MAX over ranks)."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:

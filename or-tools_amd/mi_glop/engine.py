@@ -52,6 +52,18 @@ def lib():
     # handlers (the runtime's and a profiler's own teardown).
     import atexit
     atexit.register(_shutdown, L)
+    # RCCL bound sharing (engine/comm.hip).
+    L.mi_lp_comm_get_unique_id.argtypes = [vp]
+    L.mi_lp_comm_create.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.POINTER(vp)]
+    L.mi_lp_comm_rank.argtypes = [vp]
+    L.mi_lp_comm_size.argtypes = [vp]
+    L.mi_lp_share_bound.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int32]
+    L.mi_lp_comm_allreduce_device.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int32]
+    L.mi_lp_comm_allgather_device.argtypes = [vp, vp, vp, ctypes.c_int64]
+    L.mi_lp_comm_last_error.argtypes = [vp]
+    L.mi_lp_comm_last_error.restype = ctypes.c_char_p
+    L.mi_lp_comm_destroy.argtypes = [vp]
     L.mi_lp_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.mi_lp_destroy.argtypes = [vp]
     L.mi_lp_last_error.argtypes = [vp]

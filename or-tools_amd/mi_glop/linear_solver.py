@@ -18,11 +18,10 @@ CleanUp: one coefficient per (row, column), the last SetCoefficient wins as in
 MPConstraint; entries of a column sorted by row, zeros dropped (the
 IsCleanedUp precondition of lp_solver.cc:185-191).
 Status maps are glop_utils.cc:18-125. Solve() goes through the engine's
-LPSolver layer (mi_lp_solver_solve: Glop's scaling preprocessor, the simplex
-on the scaled LP, RecoverSolution and the value part of
-LoadAndVerifySolution, lp_solver.cc:150-367). Presolve passes other than
-the scaling (use_preprocessing) are not built, so bases on degenerate LPs
-may differ from upstream MPSolver+GLOP; objectives agree.
+LPSolver layer (mi_lp_solver_solve: Glop's presolve passes and scaling
+preprocessor, the simplex on the presolved and scaled LP, RecoverSolution,
+the postsolve and LoadAndVerifySolution, lp_solver.cc:150-790), with Glop's
+defaults (use_preprocessing on, parameters.proto:326).
 Integer variables are rejected (GLOP is an LP solver: IsMIP() is false).
 """
 import math

@@ -29,7 +29,7 @@ for step in "$@"; do
   rc=$?
   echo "[gpu_run] $(date +%T) step $name rc=$rc in $(( $(date +%s) - t0 ))s"
   echo "$name rc=$rc s=$(( $(date +%s) - t0 ))" >> "$out/steps.txt"
-  tail -3 "$out/$name.out" "$out/$name.err"
+  tail -n 3 "$out/$name.out" "$out/$name.err"
   if [ $rc -ne 0 ]; then
     echo "[gpu_run] stopping after $name (rc=$rc)"
     exit $rc

@@ -1,0 +1,12 @@
+set -u
+cd $GRAFT_REPO_ROOT
+export MILP_SDUAL=device
+P="python3 -u scripts/probe_batch.py --node --lps 1024"
+scripts/gpu_run.sh gpurun_out/r06_b \
+ "shp@200=python3 -u scripts/probe_shared.py 6,6" \
+ "shp2@200=python3 -u scripts/probe_shared.py 15,10" \
+ "base@200=MILP_SDUAL_PROFILE=1 $P --workers 1024" \
+ "sh@200=MILP_SDUAL_PROFILE=1 MILP_BATCH_SHARED_LU=1 MILP_BATCH_SHARED_NORMS=1 $P --workers 1024" \
+ "srv8@200=MILP_SDUAL_PROFILE=1 MILP_SDUAL_SERVERS=8 $P --workers 1024" \
+ "w128@200=MILP_SDUAL_PROFILE=1 $P --workers 128" \
+ "w128sh@200=MILP_SDUAL_PROFILE=1 MILP_BATCH_SHARED_LU=1 MILP_BATCH_SHARED_NORMS=1 $P --workers 128"

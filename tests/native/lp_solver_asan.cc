@@ -23,6 +23,27 @@ int mi_lp_get_duals(const mi_lp*, double*) { return MI_LP_ERROR_DEVICE; }
 int mi_lp_get_statuses(const mi_lp*, int8_t*, int8_t*) { return MI_LP_ERROR_DEVICE; }
 }
 
+extern "C" int milp_test_solution_consistent(int32_t m, int32_t n, int32_t status,
+                                             int64_t primal_len, int64_t dual_len,
+                                             int64_t vstat_len, int64_t cstat_len);
+
+// IsProblemSolutionConsistent's size checks (glop/lp_solver.cc:683-686): a
+// solution with any vector of the wrong length is inconsistent (ABNORMAL)
+// and is never indexed; ASan reports any read past a short vector.
+static int CheckSolutionSizes() {
+  const int m = 3, n = 5, optimal = MI_LP_OPTIMAL;
+  if (milp_test_solution_consistent(m, n, optimal, n, m, n, m) != 1) return 1;
+  const int64_t bad[][4] = {{n - 1, m, n, m}, {n, m - 1, n, m}, {n, m, n - 1, m},
+                            {n, m, n, m - 1}, {0, 0, 0, 0},    {n + 4, m, n, m},
+                            {n, m + 2, n, m}, {n, m, n + 1, m}, {n, m, n, m + 3}};
+  for (const auto& b : bad) {
+    for (int status : {optimal, static_cast<int>(MI_LP_PRIMAL_INFEASIBLE)}) {
+      if (milp_test_solution_consistent(m, n, status, b[0], b[1], b[2], b[3]) != 0) return 1;
+    }
+  }
+  return 0;
+}
+
 static std::mt19937_64 rng(11);
 static int I(int a, int b) { return std::uniform_int_distribution<int>(a, b)(rng); }
 
@@ -50,6 +71,10 @@ static int FakeSimplex(void*, int32_t m, int32_t n, const int64_t* cs, const int
 
 int main(int argc, char** argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 2000;
+  if (CheckSolutionSizes() != 0) {
+    printf("wrong-sized solution accepted\n");
+    return 1;
+  }
   const double inf = std::numeric_limits<double>::infinity();
   int statuses[12] = {0};
   for (int t = 0; t < N; ++t) {

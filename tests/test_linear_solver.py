@@ -13,7 +13,7 @@ import math
 import numpy as np
 import pytest
 
-from mi_glop import abi, linear_solver
+from mi_glop import abi, engine, linear_solver
 
 import os
 import sys
@@ -120,29 +120,51 @@ def test_cleanup_merges_and_drops():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("presolve", [True, False])
 @pytest.mark.parametrize("model,expect", [
     (lp_test_model, dict(objective=34.0, primal=[6, 4])),
     (simple_glop_model, dict(objective=4.0, primal=[1, 1])),
     (model_builder_model, dict(objective=733.3333333333334 - 5.5,
                                primal=[100.0 / 3, 200.0 / 3, 0.0]))])
-def test_solve_through_engine(model, expect):
+def test_solve_through_engine(model, expect, presolve):
+    _check_solve(model, expect, presolve)
+
+
+def _check_solve(model, expect, presolve):
     solver, xs, cons = model()
+    if not presolve:
+        assert solver.SetSolverSpecificParametersAsString("use_preprocessing: false")
     assert solver.Solve() == linear_solver.Solver.OPTIMAL
     assert abs(solver.Objective().Value() - expect["objective"]) <= 1e-6 * abs(expect["objective"])
     np.testing.assert_allclose([v.solution_value() for v in xs], expect["primal"], atol=1e-7)
-    # Oracle: the simplex restatement on the scaling restatement's LP, then
-    # the restated recovery (Solve() runs the LPSolver layer, lp_solver.cc).
     lp = solver.to_linear_program()
-    arr, fac = oracle_scaling.scale_lp(lp)
-    slp = LinearProgram(lp.m, lp.n, lp.col_starts, lp.row_idx, arr["vals"], arr["col_lb"],
-                        arr["col_ub"], arr["row_lb"], arr["row_ub"], arr["obj"],
-                        arr["obj_offset"], arr["obj_scale"], lp.maximize)
-    o = oracle_lib.OracleLp(abi.default_params())
-    o.load(slp)
-    ro = o.solve()
-    ov, oc = o.statuses()
-    want = oracle_scaling.recover_and_verify(lp, fac, o.primal(), o.duals(), ov,
-                                             ro.problem_status == abi.OPTIMAL)
+    p = abi.default_params()
+    if presolve:
+        # Glop's default LPSolver flow (presolve on): the same flow with the
+        # oracle simplex behind it (mi_lp_solver_solve_with) is the check.
+        def simplex(inner):
+            o = oracle_lib.OracleLp(p)
+            o.load(inner)
+            r = o.solve()
+            v, c = o.statuses()
+            return r, o.primal(), o.duals(), v, c
+
+        rw, sol = engine.solve_lp_with(lp, simplex)
+        want = {"x": sol["x"], "rc": sol["rc"], "y": sol["y"], "objective": rw.objective}
+        ov, oc = sol["vstat"], sol["cstat"]
+    else:
+        # Presolve off: the simplex restatement on the scaling restatement's
+        # LP, then the restated recovery (lp_solver.cc:150-367).
+        arr, fac = oracle_scaling.scale_lp(lp)
+        slp = LinearProgram(lp.m, lp.n, lp.col_starts, lp.row_idx, arr["vals"], arr["col_lb"],
+                            arr["col_ub"], arr["row_lb"], arr["row_ub"], arr["obj"],
+                            arr["obj_offset"], arr["obj_scale"], lp.maximize)
+        o = oracle_lib.OracleLp(p)
+        o.load(slp)
+        ro = o.solve()
+        ov, oc = o.statuses()
+        want = oracle_scaling.recover_and_verify(lp, fac, o.primal(), o.duals(), ov,
+                                                 ro.problem_status == abi.OPTIMAL)
     np.testing.assert_array_equal([v.solution_value() for v in xs], want["x"])
     np.testing.assert_array_equal([v.reduced_cost() for v in xs], want["rc"])
     np.testing.assert_array_equal([c.dual_value() for c in cons], want["y"])
@@ -160,13 +182,21 @@ def test_infeasible_and_unbounded_status_maps():
     c = s.Constraint(2, INF)
     c.SetCoefficient(x, 1)
     assert s.Solve() == linear_solver.Solver.INFEASIBLE
-    s2 = linear_solver.Solver.CreateSolver("GLOP")
-    y = s2.NumVar(0, INF, "y")
-    s2.Objective().SetCoefficient(y, 1)
-    s2.Objective().SetMaximization()
-    c2 = s2.Constraint(0, INF)
-    c2.SetCoefficient(y, 1)
-    assert s2.Solve() == linear_solver.Solver.UNBOUNDED
+    for presolve in (False, True):
+        s2 = linear_solver.Solver.CreateSolver("GLOP")
+        if not presolve:
+            assert s2.SetSolverSpecificParametersAsString("use_preprocessing: false")
+        y = s2.NumVar(0, INF, "y")
+        s2.Objective().SetCoefficient(y, 1)
+        s2.Objective().SetMaximization()
+        c2 = s2.Constraint(0, INF)
+        c2.SetCoefficient(y, 1)
+        # The simplex proves the ray (DUAL_INFEASIBLE -> UNBOUNDED); Glop's
+        # default presolve stops first at the empty column with an infinite
+        # target (INFEASIBLE_OR_UNBOUNDED), which MPSolver reports as
+        # INFEASIBLE (glop_utils.cc:25-38).
+        want = linear_solver.Solver.INFEASIBLE if presolve else linear_solver.Solver.UNBOUNDED
+        assert s2.Solve() == want
 
 
 def test_solver_specific_parameters_text():
@@ -195,8 +225,9 @@ def test_mpsolver_path_with_oracle_simplex(monkeypatch):
     accessors on CPU."""
     import test_solve_cli
     monkeypatch.setattr(linear_solver.engine, "LpHandle", test_solve_cli._OracleHandle)
-    test_solve_through_engine(lp_test_model, dict(objective=34.0, primal=[6, 4]))
-    test_solve_through_engine(simple_glop_model, dict(objective=4.0, primal=[1, 1]))
-    test_solve_through_engine(model_builder_model, dict(objective=733.3333333333334 - 5.5,
-                                                        primal=[100.0 / 3, 200.0 / 3, 0.0]))
+    for presolve in (True, False):
+        _check_solve(lp_test_model, dict(objective=34.0, primal=[6, 4]), presolve)
+        _check_solve(simple_glop_model, dict(objective=4.0, primal=[1, 1]), presolve)
+        _check_solve(model_builder_model, dict(objective=733.3333333333334 - 5.5,
+                                               primal=[100.0 / 3, 200.0 / 3, 0.0]), presolve)
     test_infeasible_and_unbounded_status_maps()

@@ -113,7 +113,9 @@ def test_lp_solver_flow_cpu(case, dual):
         v, c = o.statuses()
         return r, o.primal(), o.duals(), v, c
 
-    rg, sol = engine.solve_lp_with(lp, simplex)
+    # Presolve off: the numpy restatement covers the scaling layer only
+    # (tests/test_presolve.py and test_validate_presolve_gpu.py cover presolve).
+    rg, sol = engine.solve_lp_with(lp, simplex, abi.default_solver_params(use_preprocessing=0))
     arr, fac = oracle_scaling.scale_lp(lp)
     slp = LinearProgram(lp.m, lp.n, lp.col_starts, lp.row_idx, arr["vals"], arr["col_lb"],
                         arr["col_ub"], arr["row_lb"], arr["row_ub"], arr["obj"],
@@ -143,7 +145,7 @@ def test_lp_solver_parity(case, dual):
     lp, expect = case[1]()
     p = abi.default_params(use_dual_simplex=dual)
     g = engine.LpHandle(p)
-    rg, sol = g.solve_lp(lp)
+    rg, sol = g.solve_lp(lp, abi.default_solver_params(use_preprocessing=0))
     # Oracle: the simplex restatement on the restatement's scaled LP.
     arr, fac = oracle_scaling.scale_lp(lp)
     slp = LinearProgram(lp.m, lp.n, lp.col_starts, lp.row_idx, arr["vals"], arr["col_lb"],
@@ -197,5 +199,5 @@ def test_load_and_verify_flags_imprecise(imprecise):
         return r, x, o.duals(), v, c
 
     r, _ = engine.solve_lp_with(lp, simplex, abi.default_solver_params(
-        change_status_to_imprecise=imprecise))
+        change_status_to_imprecise=imprecise, use_preprocessing=0))
     assert r.problem_status == (abi.IMPRECISE if imprecise else abi.OPTIMAL)
