@@ -13,13 +13,15 @@ early phase), then W more warm-up iterations, then exactly K iterations are
 timed, bracketed by barrier + device synchronize, with HIP-event kernel
 timing on (events are collected after the window, no per-kernel sync).
 
-Multi-GPU: one process per GPU (torchrun). Config 5 is ONE LP split across
-the ranks by column blocks (mi_lp_set_exchange): every rank runs
-the same host control flow on the same LP, owns one block of [A | I] on its
-GPU, and the per-column results are joined through an all-gather every
-iteration; value = the LP's iterations / max wall time over ranks ("scaling":
-"strong"). --c5-replicas runs one independent LP per rank instead (weak
-scaling, no collective in the data path).
+Multi-GPU: one process per GPU (torchrun). Config 5 runs one independent LP
+per rank (seed + rank; replicas, "scaling": "weak", no collective in the data
+path): value = all ranks' iterations / max wall time over ranks. One LP does
+not divide usefully: its iteration is a chain of dependent host decisions and
+triangular solves that every rank would replicate.
+--c5-split runs ONE LP split across the ranks by column blocks instead (SURVEY
+8(e), mi_lp_set_exchange): every rank runs the same host control flow, owns
+one block of [A | I] on its GPU, and the per-column results are joined through
+an all-gather every iteration ("scaling": "strong").
 """
 import argparse
 import json
@@ -143,7 +145,7 @@ def run_c5(args, rank, world, local_rank, dist, barrier, sync):
     rank). The solve runs untimed to iteration c5_window + warmup; then
     exactly `steps` iterations are timed with the kernel timing on."""
     import lp_gen
-    split = world > 1 and not args.c5_replicas
+    split = world > 1 and args.c5_split
     lp = lp_gen.sparse_c5_lp(args.c5_m, args.c5_n, 10, args.seed + (0 if split else rank))
     start = args.c5_window + args.warmup
     # The solve is capped where the timed windows end, so that its final
@@ -545,10 +547,20 @@ def batched_roofline_from(agg, wall_s, timed_pass=None, traffic_json=None, lps=0
             kind, a = max(timed.items(),
                           key=lambda kv: max(kv[1]["device_ms"], kv[1]["call_ms"]))
         per_lp_ms = a["device_ms"] if a["device_ms"] > 0 else a["call_ms"]
-        achieved = a["bytes"] / wall_s / 1e9
         traffic, traffic_src = batch_traffic(traffic_json, lps)
+        # The segment's op-count model (12 B per Glop operation) also counts
+        # operands that stay in LDS or L2; when the profiled HBM bytes of the
+        # whole batch are below it, the counters are the honest numerator.
+        basis = "algorithmic bytes (engine per-kind model)"
+        numerator = a["bytes"]
+        if traffic is not None and traffic < numerator:
+            numerator = traffic
+            basis = ("HBM counter bytes of the batch (FETCH_SIZE + WRITE_SIZE, "
+                     f"{traffic_src}): the op-count model ({a['bytes'] / 1e9:.2f} GB) exceeds them")
+        achieved = numerator / wall_s / 1e9
         return {"kernel": kind, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "achieved_basis": basis,
+                "traffic": traffic,
                 "traffic_unit": "HBM bytes of the whole batch (all engine kernels)",
                 "traffic_source": traffic_src, "algorithmic_bytes": a["bytes"],
                 "launches": int(a["launches"]), "bytes_per_launch": a["bytes"] / a["launches"],
@@ -649,6 +661,17 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
     out["roofline"] = batched_roofline(workers, elapsed, None, args.c4_traffic_json, len(lbs))
     if comm is not None:
         comm.close()
+    if rank == 0 and world == 1 and args.batch_share_lps > 0:
+        # One GPU's share of an 8-way split of the node (BASELINE config 4 at
+        # 8 GPUs): the first batch_share_lps children on as many handles.
+        k = min(args.batch_share_lps, len(lbs))
+        sub = workers[:k]
+        t1 = time.perf_counter()
+        res_k = engine.batch_solve_bounds(sub, lbs[:k], ubs[:k], state)
+        dt_k = time.perf_counter() - t1
+        out["share_8way"] = {"lps": k, "workers": len(sub), "value": k / dt_k, "seconds": dt_k,
+                             "unit": "LPs/s"}
+        log(f"batched: {k} LPs on {len(sub)} handles: {k / dt_k:.1f} LPs/s")
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_lib
         ows = [oracle_lib.OracleLp(p) for _ in range(args.batch_cpu_threads)]
@@ -659,6 +682,16 @@ def run_batched(args, rank, world, local_rank, dist, barrier, sync):
         ref = oracle_lib.batch_solve_bounds(ows, lbs[:n_cpu], ubs[:n_cpu], state)
         dt = time.perf_counter() - t0
         out["oracle_check"] = oracle_check(res[:n_cpu], ref)
+        if "share_8way" in out:
+            k = out["share_8way"]["lps"]
+            out["share_8way"]["oracle_check"] = oracle_check(res_k, ref[:k]) if k <= n_cpu \
+                else None
+            t1 = time.perf_counter()
+            oracle_lib.batch_solve_bounds(ows, lbs[:k], ubs[:k], state)
+            out["share_8way"]["cpu_baseline"] = {
+                "value": k / (time.perf_counter() - t1), "unit": "LPs/s",
+                "cores": args.batch_cpu_threads, "kind": "port",
+                "sample": f"oracle, {args.batch_cpu_threads} threads, the same {k} LPs"}
         out["cpu_baseline"] = {
             "value": n_cpu / dt, "unit": "LPs/s", "cores": args.batch_cpu_threads, "kind": "port",
             "sample": f"oracle, {args.batch_cpu_threads} threads, the first {n_cpu} of the same "
@@ -687,8 +720,11 @@ def main():
                          "(comma-separated, or 'all')")
     ap.add_argument("--c5-transport", default="shm", choices=["shm", "gloo"],
                     help="N > 1: the split's join transport (C++ shared memory, or gloo)")
+    ap.add_argument("--c5-split", action="store_true",
+                    help="N > 1: one config-5 LP split by column blocks over the ranks "
+                         "(strong scaling) instead of one independent LP per rank")
     ap.add_argument("--c5-replicas", action="store_true",
-                    help="N > 1: one independent config-5 LP per rank instead of one split LP")
+                    help="N > 1: one independent config-5 LP per rank (the default)")
     ap.add_argument("--c5-traffic-json",
                     default=os.path.join(REPO, "profiles", "traffic_c5.json"),
                     help="per-launch HBM bytes of the config-5 kernels (profiles/)")
@@ -722,6 +758,9 @@ def main():
     ap.add_argument("--batch-jobs", type=int, default=15)
     ap.add_argument("--batch-machines", type=int, default=10)
     ap.add_argument("--batch-cpu-lps", type=int, default=512)
+    ap.add_argument("--batch-share-lps", type=int, default=128,
+                    help="N=1: also time this many children on as many handles (one GPU's "
+                         "share of an 8-way split of the node); 0 disables")
     ap.add_argument("--no-c3", action="store_true", help="skip the config-3 section")
     ap.add_argument("--profile-batch", action="store_true",
                     help="profiling runs (scripts/profile_bench.sh): config 3 without its "

@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""Whole solves on the MI355X (GetNumberOfIterations() / wall
+time of the simplex solve): config 5 (sparse 100k x 1M, dual simplex) and
+config 2 (dense 10k x 50k, primal simplex) run from the loaded LP to their
+final status with no iteration cap, timed from the first iteration to the
+last (load to HBM excluded, as bench.py's windows exclude it).
+
+Checks, per LP:
+  - KKT of the returned basic solution, computed here in numpy from the LP
+    and the engine's primal values, duals and reduced costs (a property of
+    the answer, no oracle): bound and row violations, rc = c - A^T y, the
+    sign of every reduced cost and dual against its variable's status;
+  - config 5 only: the final state's digests against tests/golden/
+    c5_whole.json (the CPU oracle's own whole solve, scripts/
+    make_c5_whole_golden.py), when that file is present.
+Prints one JSON line per config. Development aid: the driver's bench.py
+keeps its windows; this is the whole-solve leg the windows are judged by."""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "or-tools_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+from mi_glop import abi, engine  # noqa: E402
+import lp_gen  # noqa: E402
+
+BASIC, FIXED, AT_LOWER, AT_UPPER, FREE = 0, 1, 2, 3, 4  # VariableStatus (lp_types.h:192-219)
+
+
+def log(msg):
+    print(f"[whole {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def digest(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def kkt(lp, x, y, rc, vstat, cstat, maximize=False):
+    """Max violations of the optimality conditions of min/max c.x s.t.
+    row_lb <= A x <= row_ub, col_lb <= x <= col_ub (Glop's sign rules:
+    rc = c - A^T y; for a minimization a column at its lower bound has
+    rc >= 0, at its upper bound rc <= 0, basic rc = 0; rows alike with y)."""
+    n, m = lp.n, lp.m
+    cs = np.asarray(lp.col_starts)
+    cols = np.repeat(np.arange(n), np.diff(cs))
+    rows = np.asarray(lp.row_idx)
+    vals = np.asarray(lp.vals)
+    ax = np.zeros(m)
+    np.add.at(ax, rows, vals * x[cols])
+    aty = np.zeros(n)
+    np.add.at(aty, cols, vals * y[rows])
+    obj = np.asarray(lp.obj)
+    scale = max(1.0, float(np.abs(x).max(initial=0.0)))
+    out = {
+        "primal_bound_violation": float(max(np.max(lp.col_lb - x, initial=0.0),
+                                            np.max(x - lp.col_ub, initial=0.0))),
+        "row_violation": float(max(np.max(lp.row_lb - ax, initial=0.0),
+                                   np.max(ax - lp.row_ub, initial=0.0))) / scale,
+        "rc_identity": float(np.max(np.abs(rc - (obj - aty)), initial=0.0)),
+    }
+    sgn = -1.0 if maximize else 1.0
+    r = sgn * rc
+    bad_col = np.zeros(n)
+    bad_col[vstat == AT_LOWER] = np.maximum(0.0, -r[vstat == AT_LOWER])
+    bad_col[vstat == AT_UPPER] = np.maximum(0.0, r[vstat == AT_UPPER])
+    bad_col[vstat == BASIC] = np.abs(r[vstat == BASIC])
+    bad_col[vstat == FREE] = np.abs(r[vstat == FREE])
+    yy = sgn * y
+    bad_row = np.zeros(m)
+    # A row's slack status is the constraint status (GetConstraintStatus):
+    # at its lower bound the dual is >= 0, at its upper bound <= 0.
+    bad_row[cstat == AT_LOWER] = np.maximum(0.0, -yy[cstat == AT_LOWER])
+    bad_row[cstat == AT_UPPER] = np.maximum(0.0, yy[cstat == AT_UPPER])
+    bad_row[cstat == BASIC] = np.abs(yy[cstat == BASIC])
+    out["dual_sign_violation_cols"] = float(bad_col.max(initial=0.0))
+    out["dual_sign_violation_rows"] = float(bad_row.max(initial=0.0))
+    out["primal_objective"] = float(obj @ x)
+    return out
+
+
+def whole(name, lp, params, golden=None, limit_s=900.0):
+    h = engine.LpHandle(params)
+    h.load(lp)
+    h.record_iteration_times(True)
+    t0 = time.perf_counter()
+    h.begin(1)  # upload, first factorization, iteration 1
+    setup = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    fin, it = h.run_until(10 ** 9)
+    r = h.finish()
+    wall = time.perf_counter() - t1
+    ts = h.iteration_times()
+    var, cons = h.statuses()
+    x, y, rc = h.primal(), h.duals(), h.reduced_costs()
+    out = {"config": name, "m": lp.m, "n": lp.n, "nnz": int(lp.nnz),
+           "status": int(r.problem_status), "iterations": int(r.iterations),
+           "objective": float(r.objective), "setup_s": round(setup, 2),
+           "solve_s": round(setup + wall, 2),
+           "it_per_s_whole": r.iterations / (setup + wall),
+           "kkt": kkt(lp, x, y, rc, var, cons, bool(lp.maximize))}
+    if len(ts) >= 10:
+        marks = {}
+        for k in (1000, 5000, 10000, 20000, 40000, 80000, 160000):
+            if k <= len(ts):
+                marks[str(k)] = round(ts[k - 1], 3)
+        out["engine_iteration_time_at"] = marks
+    digests = {"iterations": int(r.iterations), "problem_status": int(r.problem_status),
+               "error_code": int(r.error_code), "objective": float(r.objective).hex(),
+               "basis": digest(h.basis()), "state": digest(h.state()),
+               "var_status": digest(var), "cons_status": digest(cons),
+               "primal": digest(x), "duals": digest(y), "reduced_costs": digest(rc)}
+    if golden is not None:
+        g = golden["final"]
+        bad = sorted(k for k in g if g[k] != digests[k])
+        out["oracle_check"] = {"fields": sorted(g), "mismatches": len(bad), "differing": bad,
+                               "oracle_it_per_s": golden.get("oracle_it_per_s"),
+                               "oracle_solve_s": golden.get("oracle_solve_s"),
+                               "oracle_host": golden.get("oracle_host")}
+    out["digests"] = digests
+    h.close()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", nargs="*", default=["c5", "c2"])
+    ap.add_argument("--seed", type=int, default=20261015)
+    a = ap.parse_args()
+    for c in a.configs:
+        if c == "c5":
+            lp = lp_gen.sparse_c5_lp(100000, 1000000, 10, a.seed)
+            gp = os.path.join(REPO, "tests", "golden", "c5_whole.json")
+            golden = json.load(open(gp)) if os.path.exists(gp) else None
+            log("c5: solving to the end")
+            out = whole("config 5", lp, abi.default_params(use_dual_simplex=1), golden)
+        else:
+            lp = lp_gen.dense_box_lp(10000, 50000, a.seed)
+            log("c2: solving to the end")
+            out = whole("config 2", lp, abi.default_params())
+        log(f"{c}: {out['iterations']} iterations, status {out['status']}, "
+            f"{out['it_per_s_whole']:.1f} it/s")
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

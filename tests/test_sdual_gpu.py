@@ -129,37 +129,39 @@ def test_sdual_children_parity(shape, sdual_mode):
     assert segs > 0
 
 
-@pytest.mark.skipif(os.environ.get("MILP_TEST_SHARED_CACHES") != "1",
-                    reason="opt-in batch caches (MILP_BATCH_SHARED_LU/_NORMS) not yet run on a "
-                           "GPU; MILP_TEST_SHARED_CACHES=1 runs this check")
 @pytest.mark.parametrize("shape", [(6, 6), (15, 10)])
 def test_sdual_children_shared_caches(shape, monkeypatch):
-    """A node's children with the shared first factorization and dual edge
-    norms (MILP_BATCH_SHARED_LU=1, MILP_BATCH_SHARED_NORMS=1): every child
-    equals the oracle solving it alone, and the same batch without the
-    caches (deterministic time included: a cache hit replays the bumps)."""
+    """A node's children with and without the shared first factorization and
+    dual edge norms (MILP_BATCH_SHARED_LU, MILP_BATCH_SHARED_NORMS): every
+    child equals the oracle solving it alone. The deterministic time is
+    cumulative per handle (as Glop's RevisedSimplex keeps it), so it is
+    compared on one worker, whose children run in order like the oracle's
+    reused handle: equal to the oracle's with the caches on or off (a cache
+    hit replays the bumps)."""
     monkeypatch.setenv("MILP_SDUAL", "device")
     lp, state, lbs, ubs = _children(shape, 24)
     p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1000)
-    runs = {}
+    o = oracle_lib.OracleLp(p)
+    o.load(lp)
+    ref = []
+    for i in range(len(lbs)):
+        o.set_variable_bounds(lbs[i], ubs[i])
+        o.load_basis_state(state)
+        ref.append(o.solve())
     for shared in ("0", "1"):
         monkeypatch.setenv("MILP_BATCH_SHARED_LU", shared)
         monkeypatch.setenv("MILP_BATCH_SHARED_NORMS", shared)
-        workers = [engine.LpHandle(p) for _ in range(8)]
-        for w in workers:
-            w.load(lp)
-        runs[shared] = engine.batch_solve_bounds(workers, lbs, ubs, state)
-    o = oracle_lib.OracleLp(p)
-    o.load(lp)
-    for i, (r, r0) in enumerate(zip(runs["1"], runs["0"])):
-        o.set_variable_bounds(lbs[i], ubs[i])
-        o.load_basis_state(state)
-        ro = o.solve()
-        assert (r.error_code, r.problem_status, r.iterations) == \
-            (ro.error_code, ro.problem_status, ro.iterations), i
-        assert r.objective == ro.objective, (i, r.objective, ro.objective)
-        assert (r.iterations, r.objective, r.deterministic_time) == \
-            (r0.iterations, r0.objective, r0.deterministic_time), i
+        for nw in (8, 1):
+            workers = [engine.LpHandle(p) for _ in range(nw)]
+            for w in workers:
+                w.load(lp)
+            res = engine.batch_solve_bounds(workers, lbs, ubs, state)
+            for i, (r, ro) in enumerate(zip(res, ref)):
+                assert (r.error_code, r.problem_status, r.iterations) == \
+                    (ro.error_code, ro.problem_status, ro.iterations), (shared, nw, i)
+                assert r.objective == ro.objective, (shared, nw, i, r.objective, ro.objective)
+                if nw == 1:
+                    assert r.deterministic_time == ro.deterministic_time, (shared, i)
 
 
 def test_sdual_child_full_state(sdual_mode):
