@@ -3577,12 +3577,22 @@ class RevisedSimplex {
 
  public:
   // The batch APIs run the phase-II dual loop of their LPs as device
-  // segments (one workgroup per LP, csrc/sdual);
-  // MILP_SDUAL=off keeps the batched-launch path.
-  void SetBatchMode(bool on) {
-    const int batch_mode = [] {  // read per batch call (tests switch it)
+  // segments (one workgroup per LP, csrc/sdual) when many LPs
+  // are in flight, and the batched-launch path (host loop, batched small
+  // kernels) when few are: a segment iteration is a chain of dependent
+  // memory round trips on one wave (~0.4-0.5 ms at m = 2 250), so segments
+  // only win by numbers (measured: 128 children 760 LPs/s on segments
+  // against 2 009 batched-launch; 1 024 children 4 650 against 3 359).
+  // MILP_SDUAL=off / host / device forces a mode; MILP_SDUAL_MIN_LPS sets
+  // the in-flight count from which segments are the default (512).
+  void SetBatchMode(bool on, int lps_in_flight = 1 << 30) {
+    const int batch_mode = [lps_in_flight] {  // read per batch call (tests switch it)
       const char* e = std::getenv("MILP_SDUAL");
-      if (e == nullptr) return 2;
+      if (e == nullptr) {
+        int min_lps = 512;
+        if (const char* v = std::getenv("MILP_SDUAL_MIN_LPS")) min_lps = std::atoi(v);
+        return lps_in_flight >= min_lps ? 2 : 0;
+      }
       if (std::strcmp(e, "host") == 0) return 1;
       if (std::strcmp(e, "device") == 0 || std::strcmp(e, "on") == 0) return 2;
       return 0;
@@ -6380,8 +6390,9 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
                  std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
   };
   std::atomic<int> solved(0);
+  const int in_flight = static_cast<int>(std::min<int64_t>(count, int64_t(num_threads) * fibers));
   for (int i = 0; i < count; ++i) {
-    handles[i]->simplex.SetBatchMode(true);
+    handles[i]->simplex.SetBatchMode(true, in_flight);
     handles[i]->simplex.device().SetSmallBatch(true);
   }
   mark("batch mode on");
@@ -6493,13 +6504,15 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
   if (const char* e = std::getenv("MILP_BATCH_THREADS")) {
     threads = std::max(1, std::min(num_workers, std::atoi(e)));
   }
-  // The children share one basis: MILP_BATCH_SHARED_NORMS=1 computes its
-  // dual edge norms once, MILP_BATCH_SHARED_LU=1 its factorization once
-  // (opt-in until measured on the GPU; every child computes its own by
-  // default). Read per call (tests switch them).
+  // The children share one basis: its dual edge norms and its factorization
+  // are computed once for the call (DualNormCache, LuShareCache; a hit
+  // replays the deterministic-time bumps, so every result and every
+  // handle's deterministic time are those of a child computing its own).
+  // MILP_BATCH_SHARED_NORMS=0 / MILP_BATCH_SHARED_LU=0 turn them off. Read
+  // per call (tests switch them).
   auto env_on = [](const char* name) {
     const char* e = std::getenv(name);
-    return e != nullptr && std::atoi(e) != 0;
+    return e == nullptr || std::atoi(e) != 0;
   };
   // Only between handles that loaded the same matrix (fingerprint at load;
   // the cache entries also compare their basis exactly on a hit).
@@ -6513,8 +6526,9 @@ int mi_lp_batch_solve_bounds(mi_lp* const* workers, int32_t num_workers, int32_t
   const bool shared_lu = same_matrix && env_on("MILP_BATCH_SHARED_LU");
   milp::DualNormCache norm_cache;
   milp::LuShareCache lu_cache;
+  const int in_flight = std::min(num_workers, count);
   for (int w = 0; w < num_workers; ++w) {
-    workers[w]->simplex.SetBatchMode(true);
+    workers[w]->simplex.SetBatchMode(true, in_flight);
     workers[w]->simplex.device().SetSmallBatch(true);
     if (shared_norms && warm_state != nullptr) workers[w]->simplex.SetDualNormCache(&norm_cache);
     if (shared_lu && warm_state != nullptr) workers[w]->simplex.SetLuShareCache(&lu_cache);

@@ -93,12 +93,22 @@ SD_INLINE int sd_ordered_compact_map(int n, int32_t* out, Keep keep, Map map) {
   int count = 0;
   const int lane = sd_lane();
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int base = 0; base < n; base += 64) {
-    const int i = base + lane;
-    const bool k = i < n && keep(i);
-    const uint64_t mask = __ballot(k);
-    if (k) out[count + __popcll(mask & below)] = map(i);
-    count += __popcll(mask);
+  // Four chunks per round: their keep() tests (loads) are all issued before
+  // the first write, so a round waits on one memory trip instead of four;
+  // the chunks are then written in order.
+  for (int base = 0; base < n; base += 256) {
+    bool k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = base + 64 * u + lane;
+      k[u] = i < n && keep(i);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t mask = __ballot(k[u]);
+      if (k[u]) out[count + __popcll(mask & below)] = map(base + 64 * u + lane);
+      count += __popcll(mask);
+    }
   }
   sd_sync();
   return count;
@@ -154,6 +164,36 @@ typedef __attribute__((address_space(3))) int64_t l_i64;
 __device__ inline bool sd_is_lds(const void* p) { return __builtin_amdgcn_is_shared(p); }
 
 
+// Lane j's accumulator chain of an ordered dot: acc += red[j], red[j + 4],
+// ... (groups terms, in order). The LDS reads go out eight at a time ahead of
+// the additions (a plain loop waits on each read before its add); the
+// additions keep their order, so the sum is bit for bit the loop's.
+__device__ inline f64 sd_chain_sum(l_f64* red, int lane, int groups, f64 acc) {
+  int g = 0;
+  for (; g + 8 <= groups; g += 8) {
+    f64 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = red[lane + 4 * (g + u)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; g < groups; ++g) acc += red[lane + 4 * g];
+  return acc;
+}
+// red[0 .. cnt) added in order onto sum (one lane), the reads eight ahead.
+__device__ inline f64 sd_seq_sum(l_f64* red, int cnt, f64 sum) {
+  int j = 0;
+  for (; j + 8 <= cnt; j += 8) {
+    f64 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = red[j + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) sum += v[u];
+  }
+  for (; j < cnt; ++j) sum += red[j];
+  return sum;
+}
+
 // ColumnScalarProduct (sparse.h:514-542) of entries [b, e) of a column
 // (rows/coefs) against x, on the lanes: up to 256 products are computed
 // together (their loads in flight at once) and written to LDS, then lane
@@ -183,10 +223,7 @@ __device__ inline f64 sd_ordered_dot(gc_i32* rows, gc_f64* coefs, int64_t b, int
     for (int u = 0; u < 4; ++u) red[u * 64 + lane] = p[u];
     sd_sync();
     const int64_t nb = body - base < n ? (body - base > 0 ? body - base : 0) : n;
-    if (lane < 4) {
-      const int groups = static_cast<int>(nb >> 2);
-      for (int g = 0; g < groups; ++g) acc += red[lane + 4 * g];
-    }
+    if (lane < 4) acc = sd_chain_sum(red, lane, static_cast<int>(nb >> 2), acc);
     for (int64_t t = body > base ? body : base; t < base + n; ++t) tail[t - body] = red[t - base];
     sd_sync();
   }
@@ -506,9 +543,7 @@ __device__ inline f64 vec_squared_norm_dev(const Vec& v, f64* lds_scratch) {
       red[64 * u + lane] = term;
     }
     sd_sync();
-    if (lane == 0) {
-      for (int j = 0; j < cnt; ++j) sum += red[j];
-    }
+    if (lane == 0) sum = sd_seq_sum(red, cnt, sum);
     sd_sync();
   }
   if (lane == 0) {
@@ -858,9 +893,33 @@ __device__ inline f64 tri_column_pf(gc_i32* rows, gc_f64* coefs, const SdColPf& 
     sum -= p.c[0] * x[p.r[0]] + p.c[1] * x[p.r[1]] + p.c[2] * x[p.r[2]] + p.c[3] * x[p.r[3]];
     if (kUpper) {
       int64_t i = b + 4;
-      for (; i < e - 3; i += 4) {
-        sum -= coefs[i] * x[rows[i]] + coefs[i + 1] * x[rows[i + 1]] +
-               coefs[i + 2] * x[rows[i + 2]] + coefs[i + 3] * x[rows[i + 3]];
+      // Whole groups with the next group's entries loaded while the current
+      // one is subtracted (same expression and order per group).
+      if (i < e - 3) {
+        int r[4];
+        f64 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          r[u] = rows[i + u];
+          c[u] = coefs[i + u];
+        }
+        for (; i < e - 3; i += 4) {
+          int nr[4] = {0, 0, 0, 0};
+          f64 nc[4] = {0.0, 0.0, 0.0, 0.0};
+          if (i + 4 < e - 3) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              nr[u] = rows[i + 4 + u];
+              nc[u] = coefs[i + 4 + u];
+            }
+          }
+          sum -= c[0] * x[r[0]] + c[1] * x[r[1]] + c[2] * x[r[2]] + c[3] * x[r[3]];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            r[u] = nr[u];
+            c[u] = nc[u];
+          }
+        }
       }
       if (i < e) {
         sum -= coefs[i] * x[rows[i]];
@@ -871,9 +930,31 @@ __device__ inline f64 tri_column_pf(gc_i32* rows, gc_f64* coefs, const SdColPf& 
       }
     } else {
       int64_t i = e - 5;
-      for (; i >= b + 3; i -= 4) {
-        sum -= coefs[i] * x[rows[i]] + coefs[i - 1] * x[rows[i - 1]] +
-               coefs[i - 2] * x[rows[i - 2]] + coefs[i - 3] * x[rows[i - 3]];
+      if (i >= b + 3) {
+        int r[4];
+        f64 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          r[u] = rows[i - u];
+          c[u] = coefs[i - u];
+        }
+        for (; i >= b + 3; i -= 4) {
+          int nr[4] = {0, 0, 0, 0};
+          f64 nc[4] = {0.0, 0.0, 0.0, 0.0};
+          if (i - 4 >= b + 3) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              nr[u] = rows[i - 4 - u];
+              nc[u] = coefs[i - 4 - u];
+            }
+          }
+          sum -= c[0] * x[r[0]] + c[1] * x[r[1]] + c[2] * x[r[2]] + c[3] * x[r[3]];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            r[u] = nr[u];
+            c[u] = nc[u];
+          }
+        }
       }
       if (i >= b) {
         sum -= coefs[i] * x[rows[i]];
@@ -1093,7 +1174,21 @@ __device__ inline void tri_hyper_dev(const Tri& t, XP x, int32_t* nz, int* nnz) 
         const f64 coeff = ones ? v : v / cur.diag;
         x[cur.row] = coeff;
         if (cur.b + lane < cur.e) x[cur.r] -= coeff * cur.c;
-        for (int64_t i = cur.b + 64 + lane; i < cur.e; i += 64) x[rows[i]] -= coeff * coefs[i];
+        // The rest of the column (distinct rows): four chunks' loads at once.
+        for (int64_t i0 = cur.b + 64 + lane; i0 < cur.e; i0 += 256) {
+          int r[4];
+          f64 c[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int64_t i = i0 + 64 * u;
+            r[u] = i < cur.e ? rows[i] : 0;
+            c[u] = i < cur.e ? coefs[i] : 0.0;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (i0 + 64 * u < cur.e) x[r[u]] -= coeff * c[u];
+          }
+        }
         sd_sync();
         if (kRev) {
           nzg[--out] = cur.row;
@@ -1786,10 +1881,7 @@ __device__ inline f64 sd_ordered_dot_pf(gc_i32* rows, gc_f64* coefs, int64_t b, 
     for (int u = 0; u < 4; ++u) red[u * 64 + lane] = p[u];
     sd_sync();
     const int64_t nb = body - base < n ? (body - base > 0 ? body - base : 0) : n;
-    if (lane < 4) {
-      const int groups = static_cast<int>(nb >> 2);
-      for (int g = 0; g < groups; ++g) acc += red[lane + 4 * g];
-    }
+    if (lane < 4) acc = sd_chain_sum(red, lane, static_cast<int>(nb >> 2), acc);
     for (int64_t t = body > base ? body : base; t < base + n; ++t) tail[t - body] = red[t - base];
     sd_sync();
   }

@@ -17,6 +17,14 @@ import parity_util
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _segments_on(monkeypatch):
+    """Segments in every batch call of this file: by default a batch with
+    fewer than MILP_SDUAL_MIN_LPS (512) LPs in flight takes the
+    batched-launch path (simplex.cc SetBatchMode)."""
+    monkeypatch.setenv("MILP_SDUAL", "device")
+
+
 @pytest.fixture(params=["device", "host"])
 def sdual_mode(request, monkeypatch):
     monkeypatch.setenv("MILP_SDUAL", request.param)
