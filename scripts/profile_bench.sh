@@ -17,8 +17,13 @@ cd /tmp && export TMPDIR=/tmp
 # A profiled run releases every HIP resource at exit (mi_lp_shutdown), so
 # that rocprofiler-sdk's own teardown finds nothing left.
 export MILP_DEVICE_RESET_AT_EXIT=1 MILP_CRASH_REPORT=1
+# TRACE_EXTRA: arguments appended to the trace pass only (argparse keeps the
+# last occurrence), e.g. "--c3-workers 2": the kernel trace of the 16-thread
+# config-3 batch faults inside rocprofiler-sdk (profiles/r06_c3trace), the
+# counter passes below run the benched arguments. trace.log (with the engine's
+# MILP_CRASH_REPORT frames) stays in $OUT on failure.
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-  python3 $R/bench.py "$@" > $OUT/trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
+  python3 $R/bench.py "$@" ${TRACE_EXTRA:-} > $OUT/trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE; do
   p=$(echo $c | tr A-Z a-z | cut -d_ -f1)
   timeout -k 10 600 rocprofv3 --pmc $c -d $OUT/$p -o run --output-format csv -- \

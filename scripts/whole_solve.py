@@ -93,7 +93,16 @@ def whole(name, lp, params, golden=None, limit_s=900.0):
     h.begin(1)  # upload, first factorization, iteration 1
     setup = time.perf_counter() - t0
     t1 = time.perf_counter()
-    fin, it = h.run_until(10 ** 9)
+    fin, it = False, 1
+    next_log = t1 + 30.0
+    while not fin and time.perf_counter() - t1 < limit_s:
+        fin, it = h.run_until(it + 500)
+        if time.perf_counter() > next_log:
+            log(f"{name}: {it} iterations after {time.perf_counter() - t1:.0f}s")
+            next_log += 30.0
+    capped = not fin
+    if capped:
+        h.stop()
     r = h.finish()
     wall = time.perf_counter() - t1
     ts = h.iteration_times()
@@ -103,7 +112,7 @@ def whole(name, lp, params, golden=None, limit_s=900.0):
            "status": int(r.problem_status), "iterations": int(r.iterations),
            "objective": float(r.objective), "setup_s": round(setup, 2),
            "solve_s": round(setup + wall, 2),
-           "it_per_s_whole": r.iterations / (setup + wall),
+           "it_per_s_whole": r.iterations / (setup + wall), "capped_at_s": limit_s if capped else None,
            "kkt": kkt(lp, x, y, rc, var, cons, bool(lp.maximize))}
     if len(ts) >= 10:
         marks = {}
@@ -132,18 +141,23 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", nargs="*", default=["c5", "c2"])
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--limit-s", type=float, default=900.0,
+                    help="wall-clock cap per solve (the result then says capped_at_s)")
+    ap.add_argument("--c5-m", type=int, default=100000)
+    ap.add_argument("--c5-n", type=int, default=1000000)
     a = ap.parse_args()
     for c in a.configs:
         if c == "c5":
-            lp = lp_gen.sparse_c5_lp(100000, 1000000, 10, a.seed)
-            gp = os.path.join(REPO, "tests", "golden", "c5_whole.json")
+            lp = lp_gen.sparse_c5_lp(a.c5_m, a.c5_n, 10, a.seed)
+            gp = os.path.join(REPO, "tests", "golden", f"c5_whole_{a.c5_m}.json")
             golden = json.load(open(gp)) if os.path.exists(gp) else None
-            log("c5: solving to the end")
-            out = whole("config 5", lp, abi.default_params(use_dual_simplex=1), golden)
+            log(f"c5: {a.c5_m}x{a.c5_n} solving to the end")
+            out = whole(f"config 5 shape {a.c5_m}x{a.c5_n}", lp,
+                        abi.default_params(use_dual_simplex=1), golden, a.limit_s)
         else:
             lp = lp_gen.dense_box_lp(10000, 50000, a.seed)
             log("c2: solving to the end")
-            out = whole("config 2", lp, abi.default_params())
+            out = whole("config 2", lp, abi.default_params(), None, a.limit_s)
         log(f"{c}: {out['iterations']} iterations, status {out['status']}, "
             f"{out['it_per_s_whole']:.1f} it/s")
         print(json.dumps(out), flush=True)
