@@ -545,10 +545,6 @@ class DeviceLp : public DeviceSolver {
   uint8_t* d_slot_flags_ = nullptr;
   int32_t* d_slots_ = nullptr;
   int* d_num_slots_ = nullptr;
-  int* d_sel_next_ = nullptr;  // the select kernel's running candidate count
-  int32_t* h_cand_slot_ = nullptr;  // candidates' list slots (mapped)
-  int32_t* m_cand_slot_ = nullptr;
-  std::vector<int> cand_order_;     // host: candidates in list order
   int32_t* d_cand_col_ = nullptr;
   double* d_cand_coeff_ = nullptr;
   double* d_cand_rc_ = nullptr;

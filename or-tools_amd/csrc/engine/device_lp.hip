@@ -76,8 +76,7 @@ DeviceLp::~DeviceLp() {
   if (h_map_) (void)hipHostFree(h_map_);
   if (h_small_in_) (void)hipHostFree(h_small_in_);
   if (h_scan_fail_) (void)hipHostFree(h_scan_fail_);
-  for (void* p : {static_cast<void*>(h_cand_slot_), static_cast<void*>(h_cand_col_),
-                  static_cast<void*>(h_cand_coeff_),
+  for (void* p : {static_cast<void*>(h_cand_col_), static_cast<void*>(h_cand_coeff_),
                   static_cast<void*>(h_cand_rc_), static_cast<void*>(h_dual_counts_),
                   static_cast<void*>(h_cb_cols_), static_cast<void*>(h_cb_bits_),
                   static_cast<void*>(h_flip_cols_), static_cast<void*>(h_flip_flags_)}) {
@@ -1658,8 +1657,6 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
     d_slot_flags_ = Alloc<uint8_t>(n_total_);
     d_slots_ = Alloc<int32_t>(n_total_);
     d_num_slots_ = Alloc<int>(1);
-    d_sel_next_ = Alloc<int>(1);
-    Check(hipMemsetAsync(d_sel_next_, 0, sizeof(int), S(stream_)), "memset");
     d_cand_col_ = Alloc<int32_t>(n_total_);
     d_cand_coeff_ = Alloc<double>(n_total_);
     d_cand_rc_ = Alloc<double>(n_total_);
@@ -1676,7 +1673,6 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
           "radix sizing");
     d_sort_temp_ = Alloc<uint8_t>(sort_temp_bytes_);
     Synchronize();  // the pinned buffers below may still feed earlier copies
-    MappedResize(&h_cand_slot_, &m_cand_slot_, n_total_);
     MappedResize(&h_cand_col_, &m_cand_col_, n_total_);
     MappedResize(&h_cand_coeff_, &m_cand_coeff_, n_total_);
     MappedResize(&h_cand_rc_, &m_cand_rc_, n_total_);
@@ -1791,8 +1787,6 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
   milp_kernels::DualSelectOut sel{};
   sel.slots = d_slots_;
   sel.num_slots = d_num_slots_;
-  sel.cand_slot = m_cand_slot_;
-  sel.next = d_sel_next_;
   sel.cand_col = m_cand_col_;
   sel.cand_coeff = m_cand_coeff_;
   sel.cand_rc = m_cand_rc_;
@@ -1833,21 +1827,9 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
   const bool tightened = k1 > tighten_min_candidates_;
   stats_.algorithmic_bytes[MI_K_DUAL_RATIO] +=
       (tightened ? 3.0 : 2.0) * 29.0 * count + 20.0 * k + (tightened ? 20.0 * k1 + 36.0 * k1 : 0.0);
-  // The select kernel writes its candidates in no particular order: list
-  // order (= slot order, what Glop's loops iterate) is restored here.
-  cand_order_.resize(k);
-  for (int i = 0; i < k; ++i) cand_order_[i] = i;
-  std::sort(cand_order_.begin(), cand_order_.end(),
-            [this](int x, int y) { return h_cand_slot_[x] < h_cand_slot_[y]; });
-  out->col.resize(k);
-  out->coeff.resize(k);
-  out->rc.resize(k);
-  for (int i = 0; i < k; ++i) {
-    const int j = cand_order_[i];
-    out->col[i] = h_cand_col_[j];
-    out->coeff[i] = h_cand_coeff_[j];
-    out->rc[i] = h_cand_rc_[j];
-  }
+  out->col.assign(h_cand_col_, h_cand_col_ + k);
+  out->coeff.assign(h_cand_coeff_, h_cand_coeff_ + k);
+  out->rc.assign(h_cand_rc_, h_cand_rc_ + k);
   out->list_count = count;
 }
 

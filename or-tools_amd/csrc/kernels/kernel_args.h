@@ -249,14 +249,12 @@ struct ScanState {
 
 // The fused dual ratio filter + compaction writes here (mapped host memory).
 struct DualSelectOut {
-  int32_t* slots;      // device: kept list slots, in no particular order
+  int32_t* slots;      // device: kept list slots, in list order
   int* num_slots;      // device
-  int32_t* cand_slot;  // host-visible: each candidate's list slot (the host sorts by it)
   int32_t* cand_col;   // host-visible
   double* cand_coeff;  // host-visible
   double* cand_rc;     // host-visible
   int* counts;         // host-visible: [0] kept, [1] list length
-  int* next;           // device: the running candidate count (0 between launches)
 };
 
 struct RowSumArgs {

@@ -456,31 +456,23 @@ __device__ __forceinline__ void scan_finish(const ScanState& st) {
   }
 }
 
-// kCompactItems flag bytes per thread (32: two 16-byte loads), so an
-// N-sized flag array is 4x fewer tiles than kScanItems would cut: the
-// look-back chain across tiles, not the bytes, bounds this kernel.
-constexpr int kCompactItems = 32;
-constexpr int kCompactTile = kScanThreads * kCompactItems;
-
 __global__ __launch_bounds__(kScanThreads) void compact_flags_kernel(
     const uint8_t* flags, int n, const double* coeff, int32_t* list, double* vals, int* count,
     int32_t* host_list, double* host_vals, int* host_count, ScanState st) {
   __shared__ int lds_tile, lds_prefix;
   __shared__ int lds_waves[kScanThreads / kWave];
   const int tile = scan_take_tile(st, &lds_tile);
-  const int base = tile * kCompactTile + threadIdx.x * kCompactItems;
+  const int base = tile * kScanTile + threadIdx.x * kScanItems;
+  // Eight flag bytes per thread in one load when the slice is whole.
   unsigned keep = 0;
-  if (base + kCompactItems <= n) {
-    const uint4 f0 = *reinterpret_cast<const uint4*>(flags + base);
-    const uint4 f1 = *reinterpret_cast<const uint4*>(flags + base + 16);
-    const unsigned w[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+  if (base + kScanItems <= n) {
+    const uint2 f = *reinterpret_cast<const uint2*>(flags + base);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int i = 0; i < 4; ++i) keep |= ((f.x >> (8 * i)) & 0xff) ? (1u << i) : 0u;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) keep |= ((w[j] >> (8 * i)) & 0xff) ? (1u << (4 * j + i)) : 0u;
-    }
+    for (int i = 0; i < 4; ++i) keep |= ((f.y >> (8 * i)) & 0xff) ? (1u << (4 + i)) : 0u;
   } else {
-    for (int i = 0; i < kCompactItems; ++i) {
+    for (int i = 0; i < kScanItems; ++i) {
       if (base + i < n && flags[base + i] != 0) keep |= 1u << i;
     }
   }
@@ -1324,18 +1316,17 @@ __global__ __launch_bounds__(256) void dual_ratio_bound_kernel(DualRatioArgs a) 
   }
 }
 
-// Pass 2: the kept slots of every tile go out at positions taken with one
-// atomic per workgroup, in no particular order (no tile waits on another);
-// the host puts the candidates in list order by their slots (few: ~10^2 out
-// of ~10^5 list slots). The last workgroup to finish writes the counts and
-// rewinds the counters for the next launch.
+// Pass 2 with its compaction: the kept slots come out in list order, their
+// candidates go straight to host memory; the workgroup of the last list tile
+// writes the counts. Grid: scan_tiles(max_count) tiles, those past the list
+// length only take their ticket.
 __global__ __launch_bounds__(kScanThreads) void dual_ratio_select_kernel(DualRatioArgs a,
                                                                          DualSelectOut out,
                                                                          ScanState st) {
-  __shared__ int lds_base;
+  __shared__ int lds_tile, lds_prefix;
   __shared__ int lds_waves[kScanThreads / kWave];
   const int n = *a.count;
-  const int tile = blockIdx.x;
+  const int tile = scan_take_tile(st, &lds_tile);
   const int last_tile = n > 0 ? (n - 1) / kScanTile : 0;
   if (tile <= last_tile) {
     const unsigned long long best = *a.bound;
@@ -1354,39 +1345,28 @@ __global__ __launch_bounds__(kScanThreads) void dual_ratio_select_kernel(DualRat
     }
     int total;
     const int excl = scan_block_exclusive(__popc(keep), &total, lds_waves);
-    if (threadIdx.x == 0) lds_base = total > 0 ? atomicAdd(out.next, total) : 0;
+    if (threadIdx.x == 0) lds_prefix = scan_look_back(st, tile, total);
     __syncthreads();
-    int pos = lds_base + excl;
+    int pos = lds_prefix + excl;
     while (keep != 0) {
       const int i = __ffs(keep) - 1;
       keep &= keep - 1;
       const int slot = base + i;
       const int col = a.list[slot];
       out.slots[pos] = slot;
-      out.cand_slot[pos] = slot;
       out.cand_col[pos] = col;
       out.cand_coeff[pos] = a.list_coeff[slot];
       out.cand_rc[pos] = a.rc[col];
       ++pos;
     }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // No fences: thread 0's count add returned (its result was used) before
-    // this arrival add is issued, and both are device-scope atomics at L2, so
-    // the last arrival reads every count. The candidate stores only need to
-    // be complete at the kernel's end (the host syncs, later kernels follow).
-    const unsigned int done = atomicAdd(st.ticket + 1, 1u);
-    if (done == gridDim.x - 1) {
-      const int all = atomicAdd(out.next, 0);
+    if (tile == last_tile && threadIdx.x == 0) {
+      const int all = lds_prefix + total;
       *out.num_slots = all;
       out.counts[0] = all;
       out.counts[1] = n;
-      __hip_atomic_store(out.next, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(st.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(st.ticket + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  scan_finish(st);
 }
 
 __device__ __forceinline__ unsigned long long order_bits(double x) {
@@ -1679,8 +1659,7 @@ hipError_t gather(const int32_t* list, int n, const double* src, double* dst, hi
 hipError_t compact_flags(const uint8_t* flags, int n, const double* coeff, int32_t* list,
                          double* vals, int* count, int32_t* host_list, double* host_vals,
                          int* host_count, const ScanState& st, hipStream_t s) {
-  const int tiles = n <= 0 ? 1 : div_up(n, kCompactTile);
-  compact_flags_kernel<<<tiles, kScanThreads, 0, s>>>(
+  compact_flags_kernel<<<scan_tiles(n), kScanThreads, 0, s>>>(
       flags, n, coeff, list, vals, count, host_list, host_vals, host_count, st);
   return hipGetLastError();
 }
