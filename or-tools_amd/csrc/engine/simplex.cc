@@ -6425,14 +6425,31 @@ int mi_lp_batch_solve(mi_lp* const* handles, int32_t count, int32_t num_threads,
       handles[order[k]]->error = e.what();
     }
   }
-  std::atomic<int> next(0);
+  // MILP_BATCH_DEDICATED=k: the k heaviest LPs each on a thread of their
+  // own (no fibers), the rest on num_threads - k pooled threads.
+  const int dedicated = [&] {
+    const char* e = std::getenv("MILP_BATCH_DEDICATED");
+    const int k = e != nullptr ? std::max(0, std::atoi(e)) : 0;
+    return count > num_threads ? std::min({k, count, num_threads - 1}) : 0;
+  }();
+  std::atomic<int> next(dedicated);
   std::vector<std::thread> pool;
   // MILP_BATCH_HOST_POOL=1: the batch's LPs may also use the host pool.
   static const bool batch_pool = [] {
     const char* e = std::getenv("MILP_BATCH_HOST_POOL");
     return e != nullptr && std::atoi(e) != 0;
   }();
-  for (int t = 0; t < num_threads; ++t) {
+  for (int k = 0; k < dedicated; ++k) {
+    pool.emplace_back([&, k]() {
+      milp::SamplerAttachBatchThread();
+      milp::HostSerialScope serial(!batch_pool);
+      const int i = order[k];
+      (void)hipSetDevice(handles[i]->device);
+      RunSolve(handles[i], nullptr, &results[i]);
+      if (solved.fetch_add(1) + 1 == count) mark("last solve done");
+    });
+  }
+  for (int t = 0; t < num_threads - dedicated; ++t) {
     pool.emplace_back([&]() {
       milp::SamplerAttachBatchThread();
       milp::HostSerialScope serial(!batch_pool && num_threads > 1);
