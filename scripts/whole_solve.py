@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 from mi_glop import abi, engine  # noqa: E402
 import lp_gen  # noqa: E402
 
-BASIC, FIXED, AT_LOWER, AT_UPPER, FREE = 0, 1, 2, 3, 4  # VariableStatus (lp_types.h:192-219)
+from kkt import kkt  # noqa: E402  (tests/kkt.py)
 
 
 def log(msg):
@@ -40,49 +40,6 @@ def log(msg):
 
 def digest(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
-
-
-def kkt(lp, x, y, rc, vstat, cstat, maximize=False):
-    """Max violations of the optimality conditions of min/max c.x s.t.
-    row_lb <= A x <= row_ub, col_lb <= x <= col_ub (Glop's sign rules:
-    rc = c - A^T y; for a minimization a column at its lower bound has
-    rc >= 0, at its upper bound rc <= 0, basic rc = 0; rows alike with y)."""
-    n, m = lp.n, lp.m
-    cs = np.asarray(lp.col_starts)
-    cols = np.repeat(np.arange(n), np.diff(cs))
-    rows = np.asarray(lp.row_idx)
-    vals = np.asarray(lp.vals)
-    ax = np.zeros(m)
-    np.add.at(ax, rows, vals * x[cols])
-    aty = np.zeros(n)
-    np.add.at(aty, cols, vals * y[rows])
-    obj = np.asarray(lp.obj)
-    scale = max(1.0, float(np.abs(x).max(initial=0.0)))
-    out = {
-        "primal_bound_violation": float(max(np.max(lp.col_lb - x, initial=0.0),
-                                            np.max(x - lp.col_ub, initial=0.0))),
-        "row_violation": float(max(np.max(lp.row_lb - ax, initial=0.0),
-                                   np.max(ax - lp.row_ub, initial=0.0))) / scale,
-        "rc_identity": float(np.max(np.abs(rc - (obj - aty)), initial=0.0)),
-    }
-    sgn = -1.0 if maximize else 1.0
-    r = sgn * rc
-    bad_col = np.zeros(n)
-    bad_col[vstat == AT_LOWER] = np.maximum(0.0, -r[vstat == AT_LOWER])
-    bad_col[vstat == AT_UPPER] = np.maximum(0.0, r[vstat == AT_UPPER])
-    bad_col[vstat == BASIC] = np.abs(r[vstat == BASIC])
-    bad_col[vstat == FREE] = np.abs(r[vstat == FREE])
-    yy = sgn * y
-    bad_row = np.zeros(m)
-    # A row's slack status is the constraint status (GetConstraintStatus):
-    # at its lower bound the dual is >= 0, at its upper bound <= 0.
-    bad_row[cstat == AT_LOWER] = np.maximum(0.0, -yy[cstat == AT_LOWER])
-    bad_row[cstat == AT_UPPER] = np.maximum(0.0, yy[cstat == AT_UPPER])
-    bad_row[cstat == BASIC] = np.abs(yy[cstat == BASIC])
-    out["dual_sign_violation_cols"] = float(bad_col.max(initial=0.0))
-    out["dual_sign_violation_rows"] = float(bad_row.max(initial=0.0))
-    out["primal_objective"] = float(obj @ x)
-    return out
 
 
 def whole(name, lp, params, golden=None, limit_s=900.0):
