@@ -8,7 +8,8 @@
 //
 // One process-wide pool. A caller that finds it busy (another handle's loop)
 // runs all parts itself. MILP_HOST_THREADS sets the thread count (caller
-// included, default 8; 1 disables the pool).
+// included, default 16 and at most the hardware's threads; 1 disables the
+// pool).
 #ifndef MILP_HOST_POOL_H_
 #define MILP_HOST_POOL_H_
 
@@ -96,7 +97,7 @@ class HostPool {
 
  private:
   HostPool() {
-    int n = 8;
+    int n = 16;  // the GPU box's CPU share per GPU
     if (const char* e = std::getenv("MILP_HOST_THREADS")) n = std::atoi(e);
     const int hw = static_cast<int>(std::thread::hardware_concurrency());
     if (hw > 0) n = std::min(n, hw);

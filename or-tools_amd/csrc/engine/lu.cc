@@ -699,7 +699,10 @@ void LuFactorization::LeftSolveUWithNonZeros(ScatteredVector* y) const {
 void LuFactorization::RightSolveUWithNonZerosPair(ScatteredVector* x,
                                                   ScatteredVector* tau) const {
   if (is_identity_factorization_) return;
-  upper_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
+  {
+    FtranTimer t(kFtURows);
+    upper_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
+  }
   x->non_zeros_are_sorted = true;
   {
     LuSlotGuard slot(1);
@@ -719,7 +722,10 @@ void LuFactorization::RightSolveUWithNonZerosPair(ScatteredVector* x,
 // lu_factorization.cc:314-331
 void LuFactorization::RightSolveUWithNonZeros(ScatteredVector* x) const {
   if (is_identity_factorization_) return;
-  upper_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
+  {
+    FtranTimer t(kFtURows);
+    upper_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
+  }
   x->non_zeros_are_sorted = true;
   RightSolveUAfterRows(x);
 }
@@ -732,10 +738,12 @@ void LuFactorization::RightSolveUAfterRows(ScatteredVector* x) const {
         !device_solver_->TransposeLowerSolve(transpose_upper_, factorization_key_,
                                              &x->values)) {
       g_overlap.Run();
+      FtranTimer t(kFtUHost);
       transpose_upper_.TransposeLowerSolve(&x->values);
     }
   } else {
     g_overlap.Run();
+    FtranTimer t(kFtUHost);
     transpose_upper_.TransposeHyperSparseSolveWithReversedNonZeros(
         &x->values, &x->non_zeros);
   }
@@ -1610,6 +1618,7 @@ void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d)
       right_pool_mapping_[slot_col] = right_storage_.AddDenseColumn(d->values);
     };
   } else {
+    FtranTimer pool_timer(kFtUPool);
     std::sort(d->non_zeros.begin(), d->non_zeros.end());
     right_pool_mapping_[col] =
         right_storage_.AddDenseColumnWithNonZeros(d->values, d->non_zeros);

@@ -49,7 +49,10 @@ struct LuSlotGuard {
 // Debug aid (MILP_PHASE_TIMING): host wall time of the pieces of the solver
 // thread's FTRANs (L, etas, U) and of the device U/L solve calls (copy-in,
 // launch + wait, copy-out). Printed with the phase timing.
-enum FtranPiece { kFtL, kFtEtas, kFtU, kFtDevCopyIn, kFtDevRun, kFtDevCopyOut, kFtPieces };
+enum FtranPiece {
+  kFtL, kFtEtas, kFtU, kFtDevCopyIn, kFtDevRun, kFtDevCopyOut,
+  kFtURows, kFtUHost, kFtUPool, kFtPieces
+};
 extern double g_ftran_ms[kFtPieces];
 extern const bool g_ftran_timing;
 struct FtranTimer {

@@ -112,13 +112,14 @@ enum SubPhase {
   kSubBtranY, kSubPricingCall, kSubCandidatesFull, kSubGetMaximum, kSubBtranW,
   kSubUpdateRowCall, kSubNormLoop, kSubQueue, kSubLuUpdate, kSubRefactorize,
   kSubBoxedScan, kSubFlipFtran, kSubRecomputeValues, kSubDualPrices, kSubFtranDirection,
-  kSubTau, kNumSubPhases
+  kSubTau, kSubFlipScatter, kSubFlipSolve, kSubFlipPrices, kNumSubPhases
 };
 const char* const kSubPhaseNames[kNumSubPhases] = {
     "btran y (c_B B^-1)", "pricing device call", "prices full rebuild", "GetMaximum",
     "btran w (B^-T d)",   "update-row device",   "norm update loop",    "price queue/replay",
     "basis update (MPF)", "refactorize (LU)", "boxed dual-feas scan", "flip update (FTRAN)",
-    "recompute x_B",      "dual prices",       "ftran direction",   "tau ftran"};
+    "recompute x_B",      "dual prices",       "ftran direction",   "tau ftran",
+    "  flip: column scatter", "  flip: RightSolve", "  flip: x_B + prices"};
 double g_sub_ms[kNumSubPhases] = {};
 double g_dual_candidates = 0.0;  // device ratio test: candidates returned
 double g_dual_list = 0.0;        // update-row positions they were filtered from
@@ -126,15 +127,18 @@ const bool g_sub_on = std::getenv("MILP_PHASE_TIMING") != nullptr;
 struct SubTimer {
   SubPhase p;
   std::chrono::steady_clock::time_point t0;
+  bool stopped = false;
   explicit SubTimer(SubPhase q) : p(q) {
     if (g_sub_on) t0 = std::chrono::steady_clock::now();
   }
-  ~SubTimer() {
-    if (g_sub_on) {
+  void Stop() {
+    if (g_sub_on && !stopped) {
       g_sub_ms[p] += std::chrono::duration<double, std::milli>(
                          std::chrono::steady_clock::now() - t0).count();
     }
+    stopped = true;
   }
+  ~SubTimer() { Stop(); }
 };
 
 PhaseClock::PhaseClock(bool dual) : names(dual ? kDual : kPrimal) {
@@ -163,7 +167,8 @@ void PhaseClock::Dump(long long iterations) {
   {
     static const char* const kFt[kFtPieces] = {"ftran L", "ftran etas", "ftran U (call)",
                                                 "  U copy-in", "  U launch+wait",
-                                                "  U copy-out"};
+                                                "  U copy-out", "  U rows to consider",
+                                                "  U host solve", "  U right-pool append"};
     for (int i = 0; i < kFtPieces; ++i) {
       std::fprintf(stderr, "  %-22s %10.3f ms  (%.3f ms/it)\n", kFt[i], g_ftran_ms[i],
                    iterations > 0 ? g_ftran_ms[i] / iterations : 0.0);
@@ -2783,6 +2788,7 @@ void VariableValues::UpdateGivenNonBasicVariables(const std::vector<int>& cols,
   initially_all_zero_scratchpad_.values.resize(num_rows, 0.0);
   initially_all_zero_scratchpad_.ClearSparseMask();
   bool use_dense = false;
+  SubTimer scatter_timer(kSubFlipScatter);
   for (const int col : cols) {
     const Fractional old_value = variable_values_[col];
     SetNonBasicVariableValueFromStatus(col);
@@ -2797,7 +2803,12 @@ void VariableValues::UpdateGivenNonBasicVariables(const std::vector<int>& cols,
   }
   initially_all_zero_scratchpad_.ClearSparseMask();
   initially_all_zero_scratchpad_.ClearNonZerosIfTooDense();
-  bf_.RightSolve(&initially_all_zero_scratchpad_);
+  scatter_timer.Stop();
+  {
+    SubTimer solve_timer(kSubFlipSolve);
+    bf_.RightSolve(&initially_all_zero_scratchpad_);
+  }
+  SubTimer prices_timer(kSubFlipPrices);
   if (initially_all_zero_scratchpad_.non_zeros.empty()) {
     // x_B update, scratch reset and RecomputeDualPrices() in one pass: a
     // row's price reads only its own basic variable, so the three loops of

@@ -1,0 +1,5 @@
+set -u
+cd $GRAFT_REPO_ROOT
+C5="python3 -u scripts/probe.py --config c5 --m 100000 --n 1000000 --warmup 20000 --steps 1000"
+scripts/gpu_run.sh gpurun_out/r06_o \
+ "ph@300=MILP_PHASE_TIMING=1 MILP_PHASE_TIMING_EVERY=1000 $C5"
