@@ -19,6 +19,7 @@
 namespace milp_kernels {
 struct TriSolveArgs;
 struct ScanState;
+struct TightenState;
 }
 namespace sdual {
 struct Mailbox;
@@ -574,6 +575,8 @@ class DeviceLp : public DeviceSolver {
   // tightens it on the device (MILP_DUAL_TIGHTEN_MIN).
   int tighten_min_candidates_ = 512;
   unsigned long long* d_best2_ = nullptr;
+  milp_kernels::TightenState* d_tighten_ = nullptr;
+  bool tighten_sort_ = false;  // MILP_DUAL_TIGHTEN_SORT=1: the full radix sort + walk
   unsigned long long* d_keys_in_ = nullptr;
   unsigned long long* d_keys_out_ = nullptr;
   int32_t* d_sorted_slots_ = nullptr;

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <limits>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -134,6 +135,7 @@ void DeviceLp::Init(int device) {
   if (const char* t = std::getenv("MILP_DUAL_TIGHTEN_MIN")) {
     tighten_min_candidates_ = std::atoi(t);
   }
+  if (const char* t = std::getenv("MILP_DUAL_TIGHTEN_SORT")) tighten_sort_ = std::atoi(t) != 0;
   if (const char* r = std::getenv("MILP_ROWWISE_CHUNK_MAX_ROWS")) {
     rowwise_chunk_max_rows_ = std::atoi(r);
   }
@@ -1662,7 +1664,8 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
     d_cand_rc_ = Alloc<double>(n_total_);
     d_small_cols_ = Alloc<int32_t>(n_total_);
     d_small_bits_ = Alloc<uint8_t>(n_total_);
-    d_best2_ = Alloc<unsigned long long>(1);
+    d_best2_ = Alloc<unsigned long long>(2);
+    d_tighten_ = Alloc<milp_kernels::TightenState>(1);
     d_keys_in_ = Alloc<unsigned long long>(n_total_);
     d_keys_out_ = Alloc<unsigned long long>(n_total_);
     d_sorted_slots_ = Alloc<int32_t>(n_total_);
@@ -1759,6 +1762,32 @@ void DeviceLp::CheckScan() {
 // compaction and the candidate gather into mapped host memory; one stream
 // synchronization, no copies. Only a large pass-2 set (rare) adds the
 // tightening round (keys, radix sort, walk, pass 2 again).
+// MILP_TIGHTEN_STATS=1: at exit, how many breakpoints the tightening passes
+// sorted (k1) and how far the walk went, by powers of two.
+struct TightenStats {
+  static inline const bool on = std::getenv("MILP_TIGHTEN_STATS") != nullptr;
+  std::mutex mu;
+  int64_t calls = 0, no_accept = 0, k1_hist[32] = {}, walk_hist[32] = {};
+  void Add(int k1, int walk, bool none) {
+    std::lock_guard<std::mutex> l(mu);
+    ++calls;
+    no_accept += none ? 1 : 0;
+    ++k1_hist[std::min(31, 32 - __builtin_clz(static_cast<unsigned>(std::max(k1, 1))))];
+    ++walk_hist[std::min(31, 32 - __builtin_clz(static_cast<unsigned>(std::max(walk, 1))))];
+  }
+  ~TightenStats() {
+    if (!on || calls == 0) return;
+    std::fprintf(stderr, "[tighten] calls %lld, walks without acceptance %lld\n",
+                 static_cast<long long>(calls), static_cast<long long>(no_accept));
+    for (int b = 0; b < 32; ++b) {
+      if (k1_hist[b] == 0 && walk_hist[b] == 0) continue;
+      std::fprintf(stderr, "[tighten] < 2^%2d: k1 %lld walk %lld\n", b,
+                   static_cast<long long>(k1_hist[b]), static_cast<long long>(walk_hist[b]));
+    }
+  }
+};
+TightenStats g_tighten_stats;
+
 void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_tolerance,
                                    double minimum_delta, double variation_magnitude,
                                    DualCandidates* out) {
@@ -1791,6 +1820,9 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
   sel.cand_coeff = m_cand_coeff_;
   sel.cand_rc = m_cand_rc_;
   sel.counts = m_dual_counts_;
+  // Past tighten_min_candidates_ a second pass follows and writes the host
+  // copy: this one keeps its candidates on the device.
+  sel.host_cap = std::max(0, tighten_min_candidates_);
   BeginKernel(MI_K_DUAL_RATIO);
   Check(milp_launch::dual_ratio_bound(a, S(stream_)), "dual ratio bound");
   Check(milp_launch::dual_ratio_select(a, sel, NextScan(), S(stream_)), "dual ratio select");
@@ -1802,17 +1834,29 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
   if (k1 > tighten_min_candidates_) {
     if (k1 > n_total_) throw DeviceError("dual ratio test: bad counts");
     BeginKernel(MI_K_DUAL_RATIO);
-    Check(milp_launch::dual_ratio_keys(a, d_slots_, k1, d_keys_in_, S(stream_)), "keys");
-    size_t bytes = sort_temp_bytes_;
-    Check(rocprim::radix_sort_pairs(d_sort_temp_, bytes, d_keys_in_, d_keys_out_, d_slots_,
-                                    d_sorted_slots_, k1, 0, 64, S(stream_)),
-          "radix sort");
-    Check(milp_launch::dual_flip_walk(a, d_sorted_slots_, k1, d_best2_, S(stream_)), "walk");
+    if (tighten_sort_) {
+      Check(milp_launch::dual_ratio_keys(a, d_slots_, k1, d_keys_in_, S(stream_)), "keys");
+      size_t bytes = sort_temp_bytes_;
+      Check(rocprim::radix_sort_pairs(d_sort_temp_, bytes, d_keys_in_, d_keys_out_, d_slots_,
+                                      d_sorted_slots_, k1, 0, 64, S(stream_)),
+            "radix sort");
+      Check(milp_launch::dual_flip_walk(a, d_sorted_slots_, k1, d_best2_, S(stream_)), "walk");
+    } else {
+      Check(milp_launch::dual_tighten(a, d_slots_, k1, d_keys_in_, d_tighten_, d_best2_,
+                                      S(stream_)),
+            "tighten");
+    }
     a.bound = d_best2_;
+    sel.host_cap = std::numeric_limits<int>::max();
     Check(milp_launch::dual_ratio_select(a, sel, NextScan(), S(stream_)), "dual ratio select");
     EndKernel(MI_K_DUAL_RATIO, 0.0, /*count_launch=*/false);  // same logical launch
     Synchronize();
     CheckScan();
+    if (TightenStats::on) {
+      unsigned long long w = 0;
+      Check(hipMemcpy(&w, d_best2_ + 1, sizeof(w), hipMemcpyDeviceToHost), "walk length");
+      g_tighten_stats.Add(k1, static_cast<int>(w & 0xffffffffull), (w >> 40) != 0);
+    }
   }
   const int k = h_dual_counts_[0];
   const int count = h_dual_counts_[1];

@@ -255,6 +255,23 @@ struct DualSelectOut {
   double* cand_coeff;  // host-visible
   double* cand_rc;     // host-visible
   int* counts;         // host-visible: [0] kept, [1] list length
+  int host_cap;        // candidates at positions >= host_cap skip the host copy
+};
+
+// Tightening by selection (dual_tighten below): histogram passes over the
+// sort keys' top 12 bits, then the next 12 within the chosen top bin, find a
+// threshold with at least min(kTightenTarget, k1) keys at or below it; one
+// workgroup sorts those (at most kTightenCap) in LDS and walks them.
+constexpr int kTightenTarget = 512;
+constexpr int kTightenCap = 2048;
+constexpr int kTightenBins = 4096;
+struct TightenState {
+  unsigned int hist[2][kTightenBins];
+  unsigned int ticket;
+  unsigned int bin0;       // pass 0: the top-12-bit bin the target falls in
+  unsigned int below0;     // keys in the bins below it
+  unsigned int count;      // pass 1: keys <= threshold
+  unsigned long long threshold;
 };
 
 struct RowSumArgs {
@@ -453,6 +470,13 @@ hipError_t dual_ratio_keys(const milp_kernels::DualRatioArgs& args, const int32_
 // on a ratio tie, where the pop order also depends on magnitudes).
 hipError_t dual_flip_walk(const milp_kernels::DualRatioArgs& args, const int32_t* sorted_slots,
                           int num_slots, unsigned long long* bound2, hipStream_t s);
+// The same bound from the smallest keys only (keys, two histogram passes,
+// one sort-and-walk workgroup): bound2[0] is the full walk's result, or B
+// when the walk leaves the gathered prefix; bound2[1] the walk length
+// (statistics). Uses `keys` (num_slots entries) and `st` as scratch.
+hipError_t dual_tighten(const milp_kernels::DualRatioArgs& args, const int32_t* slots,
+                        int num_slots, unsigned long long* keys, milp_kernels::TightenState* st,
+                        unsigned long long* bound2, hipStream_t s);
 // rc[list[i]] += mult * list_coeff[i] (reduced_costs.cc:466-470), then
 // rc[leaving] = leaving_value, rc[entering] = 0.
 hipError_t update_reduced_costs(const int32_t* list, const double* list_coeff, const int* count,

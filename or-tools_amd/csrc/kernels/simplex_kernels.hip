@@ -1354,9 +1354,11 @@ __global__ __launch_bounds__(kScanThreads) void dual_ratio_select_kernel(DualRat
       const int slot = base + i;
       const int col = a.list[slot];
       out.slots[pos] = slot;
-      out.cand_col[pos] = col;
-      out.cand_coeff[pos] = a.list_coeff[slot];
-      out.cand_rc[pos] = a.rc[col];
+      if (pos < out.host_cap) {
+        out.cand_col[pos] = col;
+        out.cand_coeff[pos] = a.list_coeff[slot];
+        out.cand_rc[pos] = a.rc[col];
+      }
       ++pos;
     }
     if (tile == last_tile && threadIdx.x == 0) {
@@ -1412,9 +1414,243 @@ __global__ void dual_flip_walk_kernel(DualRatioArgs a, const int32_t* sorted_slo
     // harris_ratio <= min(B, its Harris ratio) from here on (B: pass 1).
     const unsigned long long h = static_cast<unsigned long long>(__double_as_longlong(harris));
     *bound2 = h < *a.best ? h : *a.best;
+    bound2[1] = static_cast<unsigned long long>(i + 1);  // walk length (statistics)
     return;
   }
   *bound2 = *a.best;
+  bound2[1] = static_cast<unsigned long long>(num_slots) | (1ull << 40);
+}
+
+// ---------------------------------------------------------------------------
+// Tightening by selection. The walk above pops only the smallest few hundred
+// breakpoints (MILP_TIGHTEN_STATS on config 5: walks of 4-255 steps over
+// k1 = 512-300 000 candidates), so instead of sorting all k1 keys, two
+// histogram passes find a threshold T with at least min(kTightenTarget, k1)
+// keys <= T, and one workgroup gathers those (at most kTightenCap), sorts
+// them in LDS and walks them as dual_flip_walk_kernel walks the whole sorted
+// list. Its first steps see the same keys in the same order (equal keys end
+// both walks at the same step whatever their order), so the bound is the
+// full walk's -- unless the walk runs off the gathered prefix or accepts its
+// last element (whose successor it cannot compare): then the bound stays B,
+// and the second pass hands the host every candidate, as without tightening.
+
+// Keys of the pass-2 slots; the state's histograms, ticket and results zeroed.
+__global__ __launch_bounds__(256) void dual_tighten_keys_kernel(DualRatioArgs a,
+                                                                const int32_t* slots,
+                                                                int num_slots,
+                                                                unsigned long long* keys,
+                                                                TightenState* st) {
+  const int stride = gridDim.x * blockDim.x;
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned int* words = reinterpret_cast<unsigned int*>(st);
+  constexpr int kWords = static_cast<int>(sizeof(TightenState) / sizeof(unsigned int));
+  for (int w = tid; w < kWords; w += stride) words[w] = 0u;
+  for (int i = tid; i < num_slots; i += stride) {
+    double ratio = 0.0, harris;
+    bool sets_bound;
+    dual_breakpoint(a, slots[i], &ratio, &harris, &sets_bound);
+    keys[i] = order_bits(ratio);
+  }
+}
+
+// Pass 0: histogram of the keys' top 12 bits; pass 1: of bits 40-51 of the
+// keys in the bin pass 0 chose. The last workgroup finds the bin where the
+// count from below reaches min(kTightenTarget, n).
+__global__ __launch_bounds__(256) void dual_tighten_hist_kernel(const unsigned long long* keys,
+                                                                int n, TightenState* st,
+                                                                int pass) {
+  __shared__ unsigned int h[kTightenBins];
+  __shared__ int lds_waves[256 / kWave];
+  __shared__ bool last;
+  for (int b = threadIdx.x; b < kTightenBins; b += blockDim.x) h[b] = 0u;
+  __syncthreads();
+  const unsigned long long bin0 = pass == 0 ? 0ull : st->bin0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const unsigned long long k = keys[i];
+    if (pass == 0) {
+      atomicAdd(&h[k >> 52], 1u);
+    } else if ((k >> 52) == bin0) {
+      atomicAdd(&h[(k >> 40) & 0xfffull], 1u);
+    }
+  }
+  __syncthreads();
+  unsigned int* global = st->hist[pass];
+  for (int b = threadIdx.x; b < kTightenBins; b += blockDim.x) {
+    if (h[b] != 0u) atomicAdd(global + b, h[b]);
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&st->ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // Thread t owns bins [16t, 16t + 16).
+  constexpr int kPer = kTightenBins / 256;
+  unsigned int mine[kPer];
+  int sum = 0;
+  for (int j = 0; j < kPer; ++j) {
+    mine[j] = __hip_atomic_load(global + threadIdx.x * kPer + j, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    sum += static_cast<int>(mine[j]);
+  }
+  int total;
+  const int excl = scan_block_exclusive(sum, &total, lds_waves);
+  const int target = n < kTightenTarget ? n : kTightenTarget;
+  const int base = pass == 0 ? 0 : static_cast<int>(st->below0);
+  int cum = base + excl;
+  if (cum < target && target <= cum + sum) {
+    for (int j = 0; j < kPer; ++j) {
+      const int before = cum;
+      cum += static_cast<int>(mine[j]);
+      if (cum >= target) {
+        const unsigned int b = threadIdx.x * kPer + j;
+        if (pass == 0) {
+          st->bin0 = b;
+          st->below0 = static_cast<unsigned int>(before);
+        } else {
+          st->threshold = (bin0 << 52) | (static_cast<unsigned long long>(b) << 40) |
+                          ((1ull << 40) - 1ull);
+          st->count = static_cast<unsigned int>(cum);
+        }
+        break;
+      }
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&st->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(1024) void dual_tighten_walk_kernel(DualRatioArgs a,
+                                                                 const int32_t* slots,
+                                                                 const unsigned long long* keys,
+                                                                 int num_slots,
+                                                                 const TightenState* st,
+                                                                 unsigned long long* bound2) {
+  __shared__ unsigned long long s_key[kTightenCap];
+  __shared__ int s_slot[kTightenCap];
+  __shared__ double s_ratio[1024], s_harris[1024], s_delta[1024];
+  __shared__ int s_n, s_done;
+  const int tid = threadIdx.x;
+  const unsigned long long best = *a.best;
+  const unsigned long long threshold = st->threshold;
+  const int count = static_cast<int>(st->count);
+  if (count > kTightenCap) {
+    if (tid == 0) {
+      bound2[0] = best;
+      bound2[1] = static_cast<unsigned long long>(count) | (2ull << 40);
+    }
+    return;
+  }
+  if (tid == 0) {
+    s_n = 0;
+    s_done = 0;
+  }
+  __syncthreads();
+  for (int i = tid; i < num_slots; i += blockDim.x) {
+    const unsigned long long k = keys[i];
+    if (k <= threshold) {
+      const int p = atomicAdd(&s_n, 1);
+      if (p < kTightenCap) {
+        s_key[p] = k;
+        s_slot[p] = slots[i];
+      }
+    }
+  }
+  __syncthreads();
+  const int n = s_n;
+  if (n > kTightenCap) {  // never expected: the histograms counted these keys
+    if (tid == 0) {
+      bound2[0] = best;
+      bound2[1] = static_cast<unsigned long long>(n) | (2ull << 40);
+    }
+    return;
+  }
+  int size = 1;
+  while (size < n) size <<= 1;
+  for (int i = n + tid; i < size; i += blockDim.x) {
+    s_key[i] = ~0ull;
+    s_slot[i] = -1;
+  }
+  __syncthreads();
+  // Bitonic sort by key (ascending).
+  for (int k = 2; k <= size; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < size; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const unsigned long long ki = s_key[i], kj = s_key[ixj];
+          if ((ki > kj) == up) {
+            s_key[i] = kj;
+            s_key[ixj] = ki;
+            const int t = s_slot[i];
+            s_slot[i] = s_slot[ixj];
+            s_slot[ixj] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // The walk (dual_flip_walk_kernel's loop), 1024 breakpoints per round.
+  double variation = a.variation_magnitude;
+  double prev_ratio = 0.0;
+  unsigned long long result = best;
+  int steps = 0;
+  for (int c0 = 0; c0 < n; c0 += 1024) {
+    if (c0 + tid < n) {
+      double r = 0.0, h = 0.0, d = 0.0;
+      bool sb;
+      dual_breakpoint(a, s_slot[c0 + tid], &r, &h, &sb, &d);
+      s_ratio[tid] = r;
+      s_harris[tid] = h;
+      s_delta[tid] = d;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int jj = 0; jj < 1024 && c0 + jj < n; ++jj) {
+        const int i = c0 + jj;
+        const double ratio = s_ratio[jj];
+        steps = i + 1;
+        if (i > 0 && ratio == prev_ratio) {  // tie: B, as the full walk
+          s_done = 1;
+          break;
+        }
+        prev_ratio = ratio;
+        const double delta = s_delta[jj];
+        if (variation > 0.0 && delta > 0.0) {
+          variation -= delta;
+          if (variation > 0.0) continue;  // flipped
+        }
+        // First accepted breakpoint.
+        s_done = 1;
+        if (i + 1 < n) {
+          double next_ratio;
+          if (jj + 1 < 1024) {
+            next_ratio = s_ratio[jj + 1];
+          } else {
+            double h2, d2;
+            bool s2;
+            dual_breakpoint(a, s_slot[i + 1], &next_ratio, &h2, &s2, &d2);
+          }
+          if (next_ratio == ratio) break;  // tie: B
+        } else if (n < num_slots) {
+          break;  // its successor lies past the gathered keys: B
+        }
+        const unsigned long long h =
+            static_cast<unsigned long long>(__double_as_longlong(s_harris[jj]));
+        result = h < best ? h : best;
+        break;
+      }
+    }
+    __syncthreads();
+    if (s_done) break;
+  }
+  // A walk through every gathered key without acceptance: B (the full walk
+  // ends the same way when nothing lies past them, and is not known otherwise).
+  if (tid == 0) {
+    bound2[0] = result;
+    bound2[1] = static_cast<unsigned long long>(steps) | (s_done ? 0ull : (1ull << 40));
+  }
 }
 
 __global__ void update_reduced_costs_kernel(const int32_t* list, const double* list_coeff,
@@ -1800,6 +2036,20 @@ hipError_t dual_ratio_keys(const DualRatioArgs& args, const int32_t* slots, int 
 hipError_t dual_flip_walk(const DualRatioArgs& args, const int32_t* sorted_slots,
                           int num_slots, unsigned long long* bound2, hipStream_t s) {
   dual_flip_walk_kernel<<<1, 64, 0, s>>>(args, sorted_slots, num_slots, bound2);
+  return hipGetLastError();
+}
+
+hipError_t dual_tighten(const DualRatioArgs& args, const int32_t* slots, int num_slots,
+                        unsigned long long* keys, TightenState* st, unsigned long long* bound2,
+                        hipStream_t s) {
+  if (num_slots <= 0) return hipSuccess;
+  constexpr int kStateWords = static_cast<int>(sizeof(TightenState) / sizeof(unsigned int));
+  const int key_blocks = std::max(grid_for(num_slots), div_up(kStateWords, 256));
+  dual_tighten_keys_kernel<<<key_blocks, 256, 0, s>>>(args, slots, num_slots, keys, st);
+  const int hist_blocks = std::max(1, std::min(256, div_up(num_slots, 256 * 8)));
+  dual_tighten_hist_kernel<<<hist_blocks, 256, 0, s>>>(keys, num_slots, st, 0);
+  dual_tighten_hist_kernel<<<hist_blocks, 256, 0, s>>>(keys, num_slots, st, 1);
+  dual_tighten_walk_kernel<<<1, 1024, 0, s>>>(args, slots, keys, num_slots, st, bound2);
   return hipGetLastError();
 }
 
