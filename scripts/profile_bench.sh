@@ -22,6 +22,11 @@ export MILP_DEVICE_RESET_AT_EXIT=1 MILP_CRASH_REPORT=1
 # config-3 batch faults inside rocprofiler-sdk (profiles/r06_c3trace), the
 # counter passes below run the benched arguments. trace.log (with the engine's
 # MILP_CRASH_REPORT frames) stays in $OUT on failure.
+# The per-dispatch traces and counter rows (hundreds of MB over a config-5
+# solve) stay on the box, also when a pass fails: gpurun copies back at most
+# 64 MiB.
+cleanup() { rm -f $OUT/trace/run_kernel_trace.csv $OUT/*/run_counter_collection.csv $OUT/*/*.db; }
+trap cleanup EXIT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
   python3 $R/bench.py "$@" ${TRACE_EXTRA:-} > $OUT/trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE; do
@@ -30,6 +35,3 @@ for c in FETCH_SIZE WRITE_SIZE; do
     python3 $R/bench.py "$@" > $OUT/$p.log 2>&1 || { echo "$c pass failed"; exit 1; }
 done
 cd $R && PROFILE_OUT_ROOT=$R/gpurun_out/profiles python3 scripts/profile_summary.py $OUT $tag $workload ${PROFILE_LPS:-0}
-# The per-dispatch traces and counter rows (hundreds of MB over a config-5
-# solve) stay on the box: gpurun copies back at most 64 MiB.
-rm -f $OUT/trace/run_kernel_trace.csv $OUT/*/run_counter_collection.csv $OUT/*/*.db
