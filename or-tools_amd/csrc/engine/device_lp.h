@@ -577,6 +577,7 @@ class DeviceLp : public DeviceSolver {
   unsigned long long* d_best2_ = nullptr;
   milp_kernels::TightenState* d_tighten_ = nullptr;
   bool tighten_sort_ = false;  // MILP_DUAL_TIGHTEN_SORT=1: the full radix sort + walk
+  int tighten_target_ = 512;   // MILP_TIGHTEN_TARGET: keys the selection keeps (tests go small)
   unsigned long long* d_keys_in_ = nullptr;
   unsigned long long* d_keys_out_ = nullptr;
   int32_t* d_sorted_slots_ = nullptr;

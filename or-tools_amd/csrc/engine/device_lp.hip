@@ -136,6 +136,8 @@ void DeviceLp::Init(int device) {
     tighten_min_candidates_ = std::atoi(t);
   }
   if (const char* t = std::getenv("MILP_DUAL_TIGHTEN_SORT")) tighten_sort_ = std::atoi(t) != 0;
+  tighten_target_ = milp_kernels::kTightenTarget;
+  if (const char* t = std::getenv("MILP_TIGHTEN_TARGET")) tighten_target_ = std::atoi(t);
   if (const char* r = std::getenv("MILP_ROWWISE_CHUNK_MAX_ROWS")) {
     rowwise_chunk_max_rows_ = std::atoi(r);
   }
@@ -1843,7 +1845,7 @@ void DeviceLp::DualRatioCandidates(double sign, double threshold, double harris_
       Check(milp_launch::dual_flip_walk(a, d_sorted_slots_, k1, d_best2_, S(stream_)), "walk");
     } else {
       Check(milp_launch::dual_tighten(a, d_slots_, k1, d_keys_in_, d_tighten_, d_best2_,
-                                      S(stream_)),
+                                      tighten_target_, S(stream_)),
             "tighten");
     }
     a.bound = d_best2_;

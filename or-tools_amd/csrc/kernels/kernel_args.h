@@ -260,7 +260,8 @@ struct DualSelectOut {
 
 // Tightening by selection (dual_tighten below): histogram passes over the
 // sort keys' top 12 bits, then the next 12 within the chosen top bin, find a
-// threshold with at least min(kTightenTarget, k1) keys at or below it; one
+// threshold with at least min(target, k1) keys at or below it (target
+// kTightenTarget, MILP_TIGHTEN_TARGET in tests); one
 // workgroup sorts those (at most kTightenCap) in LDS and walks them.
 constexpr int kTightenTarget = 512;
 constexpr int kTightenCap = 2048;
@@ -476,7 +477,7 @@ hipError_t dual_flip_walk(const milp_kernels::DualRatioArgs& args, const int32_t
 // (statistics). Uses `keys` (num_slots entries) and `st` as scratch.
 hipError_t dual_tighten(const milp_kernels::DualRatioArgs& args, const int32_t* slots,
                         int num_slots, unsigned long long* keys, milp_kernels::TightenState* st,
-                        unsigned long long* bound2, hipStream_t s);
+                        unsigned long long* bound2, int target_keys, hipStream_t s);
 // rc[list[i]] += mult * list_coeff[i] (reduced_costs.cc:466-470), then
 // rc[leaving] = leaving_value, rc[entering] = 0.
 hipError_t update_reduced_costs(const int32_t* list, const double* list_coeff, const int* count,

@@ -1425,7 +1425,7 @@ __global__ void dual_flip_walk_kernel(DualRatioArgs a, const int32_t* sorted_slo
 // Tightening by selection. The walk above pops only the smallest few hundred
 // breakpoints (MILP_TIGHTEN_STATS on config 5: walks of 4-255 steps over
 // k1 = 512-300 000 candidates), so instead of sorting all k1 keys, two
-// histogram passes find a threshold T with at least min(kTightenTarget, k1)
+// histogram passes find a threshold T with at least min(target, k1)
 // keys <= T, and one workgroup gathers those (at most kTightenCap), sorts
 // them in LDS and walks them as dual_flip_walk_kernel walks the whole sorted
 // list. Its first steps see the same keys in the same order (equal keys end
@@ -1455,10 +1455,10 @@ __global__ __launch_bounds__(256) void dual_tighten_keys_kernel(DualRatioArgs a,
 
 // Pass 0: histogram of the keys' top 12 bits; pass 1: of bits 40-51 of the
 // keys in the bin pass 0 chose. The last workgroup finds the bin where the
-// count from below reaches min(kTightenTarget, n).
+// count from below reaches min(target_keys, n).
 __global__ __launch_bounds__(256) void dual_tighten_hist_kernel(const unsigned long long* keys,
                                                                 int n, TightenState* st,
-                                                                int pass) {
+                                                                int pass, int target_keys) {
   __shared__ unsigned int h[kTightenBins];
   __shared__ int lds_waves[256 / kWave];
   __shared__ bool last;
@@ -1495,7 +1495,7 @@ __global__ __launch_bounds__(256) void dual_tighten_hist_kernel(const unsigned l
   }
   int total;
   const int excl = scan_block_exclusive(sum, &total, lds_waves);
-  const int target = n < kTightenTarget ? n : kTightenTarget;
+  const int target = n < target_keys ? n : target_keys;
   const int base = pass == 0 ? 0 : static_cast<int>(st->below0);
   int cum = base + excl;
   if (cum < target && target <= cum + sum) {
@@ -2041,14 +2041,15 @@ hipError_t dual_flip_walk(const DualRatioArgs& args, const int32_t* sorted_slots
 
 hipError_t dual_tighten(const DualRatioArgs& args, const int32_t* slots, int num_slots,
                         unsigned long long* keys, TightenState* st, unsigned long long* bound2,
-                        hipStream_t s) {
+                        int target_keys, hipStream_t s) {
   if (num_slots <= 0) return hipSuccess;
   constexpr int kStateWords = static_cast<int>(sizeof(TightenState) / sizeof(unsigned int));
   const int key_blocks = std::max(grid_for(num_slots), div_up(kStateWords, 256));
   dual_tighten_keys_kernel<<<key_blocks, 256, 0, s>>>(args, slots, num_slots, keys, st);
   const int hist_blocks = std::max(1, std::min(256, div_up(num_slots, 256 * 8)));
-  dual_tighten_hist_kernel<<<hist_blocks, 256, 0, s>>>(keys, num_slots, st, 0);
-  dual_tighten_hist_kernel<<<hist_blocks, 256, 0, s>>>(keys, num_slots, st, 1);
+  target_keys = std::max(1, std::min(target_keys, kTightenCap));
+  dual_tighten_hist_kernel<<<hist_blocks, 256, 0, s>>>(keys, num_slots, st, 0, target_keys);
+  dual_tighten_hist_kernel<<<hist_blocks, 256, 0, s>>>(keys, num_slots, st, 1, target_keys);
   dual_tighten_walk_kernel<<<1, 1024, 0, s>>>(args, slots, keys, num_slots, st, bound2);
   return hipGetLastError();
 }

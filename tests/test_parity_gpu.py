@@ -323,6 +323,23 @@ def test_device_dual_mode_parity(case, tighten, monkeypatch):
     parity_util.compare(o, ro, g, rg, lp)
 
 
+@pytest.mark.parametrize("target", ["1", "3"])
+@pytest.mark.parametrize("case", _device_dual_cases(), ids=lambda c: c[0])
+def test_device_dual_mode_parity_small_selection(case, target, monkeypatch):
+    """The tightening walk over the smallest keys only (simplex_kernels.hip
+    dual_tighten) with the selection cut to 1 or 3 keys, so that its walks
+    leave the gathered prefix or accept its last key: the bound must then
+    stay B (the host gets every candidate) and every result equal the
+    oracle's."""
+    monkeypatch.setenv("MILP_DEVICE_DUAL", "force")
+    monkeypatch.setenv("MILP_DUAL_TIGHTEN_MIN", "0")
+    monkeypatch.setenv("MILP_TIGHTEN_TARGET", target)
+    lp = case[1]()
+    p = abi.default_params(use_dual_simplex=1)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+
+
 def test_device_dual_mode_warm_start_and_children(monkeypatch):
     """CP-SAT-style re-solves in dual device mode: bound change + warm start."""
     monkeypatch.setenv("MILP_DEVICE_DUAL", "force")
