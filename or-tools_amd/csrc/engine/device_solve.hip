@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -101,6 +102,31 @@ void DeviceLp::FreeTriBuffers() {
 // entries and a unit diagonal keep their input and are not listed.
 // Positions: the listed outputs by level, then the other rows >= fni (read,
 // never written). Entries refer to positions, in evaluation order.
+// MILP_LU_TIMING=1: the device solve schedules built after refactorizations
+// (host wall time, printed at exit with the factorization's stages).
+namespace {
+struct ScheduleBuildTotals {
+  static inline const bool on = std::getenv("MILP_LU_TIMING") != nullptr;
+  std::atomic<int64_t> ns{0}, builds{0};
+  ~ScheduleBuildTotals() {
+    if (!on || builds.load() == 0) return;
+    std::fprintf(stderr, "[lu timing] tri schedule builds %lld, %.3f ms total, %.3f ms each\n",
+                 static_cast<long long>(builds.load()), ns.load() / 1e6,
+                 ns.load() / 1e6 / builds.load());
+  }
+};
+ScheduleBuildTotals g_schedule_build;
+}  // namespace
+struct ScheduleBuildTimer {
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  ~ScheduleBuildTimer() {
+    if (!ScheduleBuildTotals::on) return;
+    g_schedule_build.ns += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::steady_clock::now() - t0).count();
+    ++g_schedule_build.builds;
+  }
+};
+
 void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, const double* diag,
                                 const int64_t* gst, const int32_t* gidx, const double* gval,
                                 bool reverse, bool descending, bool sequential, uint64_t key,
@@ -760,6 +786,7 @@ bool DeviceLp::TriPrepare(int which, const TriangularMatrix& t, uint64_t key, in
     if (c.stream == nullptr) PrepareTriContext(slot, nc, 1);
     if (s.key != key) {
       DeviceOp("tri build");
+      ScheduleBuildTimer build_timer;
       const int fni = t.GetFirstNonIdentityColumn();
       const bool ones = t.all_diagonal_coefficients_are_one_;
       const double* diag = t.diagonal_coefficients_.data();

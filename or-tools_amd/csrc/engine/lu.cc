@@ -19,6 +19,38 @@ const bool g_ftran_timing = std::getenv("MILP_PHASE_TIMING") != nullptr;
 
 // ---------------------------------------------------------------------------
 // Markowitz (markowitz.cc:14-494)
+// MILP_LU_TIMING=1: wall time of the factorization's stages, summed over the
+// process and printed at exit.
+namespace {
+struct LuStageTimes {
+  static inline const bool on = std::getenv("MILP_LU_TIMING") != nullptr;
+  static constexpr int kStages = 6;
+  double ms[kStages] = {};
+  int64_t count = 0;
+  ~LuStageTimes() {
+    if (!on || count == 0) return;
+    static const char* const kNames[kStages] = {"singleton columns", "residual singletons",
+                                                "residual matrix init", "markowitz loop",
+                                                "row permutation", "transposes"};
+    std::fprintf(stderr, "[lu timing] %lld factorizations\n", static_cast<long long>(count));
+    for (int i = 0; i < kStages; ++i) {
+      std::fprintf(stderr, "[lu timing]   %-22s %9.3f ms total, %.3f ms each\n", kNames[i], ms[i],
+                   ms[i] / count);
+    }
+  }
+};
+LuStageTimes g_lu_times;
+struct LuLap {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void Lap(int stage) {
+    if (!LuStageTimes::on) return;
+    const auto now = std::chrono::steady_clock::now();
+    g_lu_times.ms[stage] += std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  }
+};
+}  // namespace
+
 Status Markowitz::ComputeRowAndColumnPermutation(const CompactSparseMatrixView& b,
                                                  std::vector<int>* row_perm,
                                                  std::vector<int>* col_perm) {
@@ -37,10 +69,14 @@ Status Markowitz::ComputeRowAndColumnPermutation(const CompactSparseMatrixView& 
   contains_only_singleton_columns_ = true;
 
   int index = 0;
+  LuLap lap;
   ExtractSingletonColumns(b, row_perm, col_perm, &index);
+  lap.Lap(0);
   ExtractResidualSingletonColumns(b, row_perm, col_perm, &index);
+  lap.Lap(1);
   residual_matrix_non_zero_.InitializeFromMatrixSubset(
       b, *row_perm, *col_perm, &singleton_column_, &singleton_row_);
+  lap.Lap(2);
 
   const int end_index = std::min(num_rows, num_cols);
   const Fractional singularity_threshold =
@@ -83,6 +119,7 @@ Status Markowitz::ComputeRowAndColumnPermutation(const CompactSparseMatrixView& 
   }
   num_fp_operations_ += 10 * lower_.num_entries();
   num_fp_operations_ += 10 * upper_.num_entries();
+  lap.Lap(3);
   return Status::OK();
 }
 
@@ -92,8 +129,10 @@ Status Markowitz::ComputeLU(const CompactSparseMatrixView& b,
   lower_.Swap(lower);
   upper_.Swap(upper);
   MILP_RETURN_IF_ERROR(ComputeRowAndColumnPermutation(b, row_perm, col_perm));
+  LuLap lap;
   lower_.ApplyRowPermutationToNonDiagonalEntries(*row_perm);
   upper_.ApplyRowPermutationToNonDiagonalEntries(*row_perm);
+  lap.Lap(4);
   lower_.Swap(lower);
   upper_.Swap(upper);
   return Status::OK();
@@ -399,10 +438,13 @@ Status LuFactorization::ComputeFactorization(const CompactSparseMatrixView& b) {
   }
   MILP_RETURN_IF_ERROR(
       markowitz_.ComputeLU(b, &row_perm_, &col_perm_, &lower_, &upper_));
+  LuLap lap;
   PopulateFromInverse(col_perm_, &inverse_col_perm_);
   PopulateFromInverse(row_perm_, &inverse_row_perm_);
   ComputeTransposeUpper();
   ComputeTransposeLower();
+  lap.Lap(5);
+  if (LuStageTimes::on) ++g_lu_times.count;
   is_identity_factorization_ = false;
   return Status::OK();
 }
