@@ -191,6 +191,10 @@ class DeviceLp : public DeviceSolver {
              std::vector<double>* x) override;
   bool SolvePair(TriKind kind, const TriangularMatrix& t, uint64_t key, std::vector<double>* x0,
                  std::vector<double>* x1) override;
+  bool StartAsyncU(const TriangularMatrix& t, uint64_t key, const std::vector<double>& x) override;
+  void FinishAsyncU(std::vector<double>* x) override;
+  void DropAsyncU() override;
+  bool SpecFlipEnabled() const { return spec_flip_ && tri_mapped_ && !tri_graph_; }
 
   // Accounting (roofline): launches, algorithmic bytes, HIP-event time.
   void SetTiming(bool on, uint32_t id_mask = ~0u);
@@ -656,8 +660,25 @@ class DeviceLp : public DeviceSolver {
   TriSchedule tri_sched_[kTriNumMatrices];
   // Per solving thread: 0 = the solver's thread (the handle's stream),
   // 1 = BasisFactorization's tau worker (its own stream), 2 = the second
-  // vector of a pair solve (the solver's stream).
-  TriContext tri_ctx_[3];
+  // vector of a pair solve (the solver's stream), 3 = the solver's
+  // asynchronous U solve (StartAsyncU, its own stream).
+  static constexpr int kTriSlots = 4;
+  TriContext tri_ctx_[kTriSlots];
+  // The one asynchronous U solve (slot 3): launched, or trivial (nothing to
+  // compute: the input is the result).
+  struct AsyncU {
+    bool active = false;
+    bool trivial = false;
+    bool timed = false;  // events recorded around the launch
+    int rows = 0;
+    int first = 0;
+    int top = 0;
+    double bytes = 0.0;
+  };
+  AsyncU async_u_;
+  // MILP_SPEC_FLIP=0 turns the speculative flip FTRAN (lu.h) off; read by the
+  // dual loop through SpecFlipEnabled().
+  bool spec_flip_ = true;
   std::mutex tri_mu_;  // schedule (re)builds and graph captures
   void* h_tri_stage_ = nullptr;  // pinned staging of the schedule upload
   size_t tri_stage_bytes_ = 0;

@@ -165,6 +165,7 @@ void DeviceLp::Init(int device) {
   if (const char* v = std::getenv("MILP_TRI_LOWER")) tri_lower_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_BTRAN")) tri_btran_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_PAIR")) tri_pair_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_SPEC_FLIP")) spec_flip_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_PAD")) tri_pad_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_DENSE_TAIL")) dense_tail_mode_ = std::atoi(v);
   if (const char* v = std::getenv("MILP_DENSE_TAIL_MIN_ENTRIES")) {

@@ -72,7 +72,8 @@ void DeviceLp::FreeTriBuffers() {
   }
   if (d_tri_clock_ != nullptr) (void)hipFree(d_tri_clock_);
   d_tri_clock_ = nullptr;
-  for (int slot = 0; slot < 3; ++slot) {
+  DropAsyncU();
+  for (int slot = 0; slot < kTriSlots; ++slot) {
     TriContext& c = tri_ctx_[slot];
     for (void* g : c.graph_exec) {
       if (g != nullptr) (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(g));
@@ -85,7 +86,7 @@ void DeviceLp::FreeTriBuffers() {
     for (void* e : c.ev) {
       if (e != nullptr) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e));
     }
-    if (slot == 1 && c.stream != nullptr) {
+    if ((slot == 1 || slot == 3) && c.stream != nullptr) {
       (void)hipStreamSynchronize(Stream(c.stream));
       (void)hipStreamDestroy(Stream(c.stream));
     }
@@ -397,7 +398,7 @@ void DeviceLp::BuildTriSchedule(TriSchedule* s, int nc, int fni, bool ones, cons
 void DeviceLp::PrepareTriContext(int slot, int rows, int pos) {
   TriContext& c = tri_ctx_[slot];
   if (c.stream == nullptr) {
-    if (slot != 1) {  // the solver's thread: its own vector (0) or a pair's second (2)
+    if (slot == 0 || slot == 2) {  // the solver's thread: its own vector (0) or a pair's second (2)
       c.stream = stream_;
     } else {
       hipStream_t st;
@@ -785,6 +786,10 @@ bool DeviceLp::TriPrepare(int which, const TriangularMatrix& t, uint64_t key, in
     DeviceOp("tri lock held");
     if (c.stream == nullptr) PrepareTriContext(slot, nc, 1);
     if (s.key != key) {
+      // An asynchronous U solve reads the schedule being replaced.
+      if (which == kTriU && async_u_.active && !async_u_.trivial) {
+        (void)hipStreamSynchronize(Stream(tri_ctx_[3].stream));
+      }
       DeviceOp("tri build");
       ScheduleBuildTimer build_timer;
       const int fni = t.GetFirstNonIdentityColumn();
@@ -1079,6 +1084,79 @@ bool DeviceLp::SolvePair(TriKind kind, const TriangularMatrix& t, uint64_t key,
     CopyHost(xs[v]->data() + fni, cs[v]->h_x + fni, size_t(tops[v] - fni + 1) * sizeof(double));
   }
   return true;
+}
+
+// The dense U solve of the speculative flip FTRAN (device_solver.h
+// StartAsyncU): TriSolve's staging and launch plan on slot 3's stream, with
+// no wait; FinishAsyncU waits and copies the result back as TriSolve does.
+bool DeviceLp::StartAsyncU(const TriangularMatrix& t, uint64_t key, const std::vector<double>& x) {
+  if (g_lu_slot != 0 || !spec_flip_ || !tri_mapped_ || tri_graph_ || tri_debug_left_ > 0) {
+    return false;
+  }
+  DropAsyncU();
+  if (!TriPrepare(kTriU, t, key, 3, x)) return false;
+  const int nc = t.num_cols();
+  TriContext& c = tri_ctx_[3];
+  TriSchedule& s = tri_sched_[kTriU];
+  const int fni = s.first_col;
+  int top = nc - 1;
+  while (top >= fni && x[top] == 0.0) --top;
+  async_u_.active = true;
+  async_u_.trivial = top < fni || s.rows_upto[top + 1] - s.rows_upto[fni] == 0;
+  if (async_u_.trivial) return true;
+  DeviceOp("tri U async enter");
+  CopyHost(c.h_x + fni, x.data() + fni, size_t(nc - fni) * sizeof(double));
+  int* h_words = reinterpret_cast<int*>(c.h_x + nc);
+  h_words[0] = top;
+  h_words[1] = 0;
+  const double rows = s.rows_upto[top + 1] - s.rows_upto[fni];
+  const double entries = static_cast<double>(s.entries_upto[top + 1] - s.entries_upto[fni]);
+  async_u_.bytes = rows * (24.0 + (s.ones ? 0.0 : 8.0)) + entries * 20.0 +
+                   double(s.pos) * 20.0 + rows * 20.0;
+  async_u_.rows = nc;
+  async_u_.first = fni;
+  async_u_.top = top;
+  async_u_.timed = Timed(MI_K_TRI_SOLVE);
+  if (async_u_.timed) {
+    Check(hipEventRecord(reinterpret_cast<hipEvent_t>(c.ev[0]), Stream(c.stream)), "ev");
+  }
+  EnqueueTriKernels(s, TriArgs(s, c), c.stream);
+  if (async_u_.timed) {
+    Check(hipEventRecord(reinterpret_cast<hipEvent_t>(c.ev[1]), Stream(c.stream)), "ev");
+  }
+  return true;
+}
+
+void DeviceLp::FinishAsyncU(std::vector<double>* x) {
+  if (!async_u_.active) throw DeviceError("asynchronous U solve: none in flight");
+  async_u_.active = false;
+  if (async_u_.trivial) return;
+  TriContext& c = tri_ctx_[3];
+  DeviceOp("tri U async sync");
+  Check(hipStreamSynchronize(Stream(c.stream)), "sync");
+  stats_.launches[MI_K_TRI_SOLVE] += 1;
+  stats_.algorithmic_bytes[MI_K_TRI_SOLVE] += async_u_.bytes;
+  if (async_u_.timed && Timed(MI_K_TRI_SOLVE)) {
+    float ms = 0.0f;
+    Check(hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(c.ev[0]),
+                              reinterpret_cast<hipEvent_t>(c.ev[1])),
+          "ev time");
+    stats_.device_ms[MI_K_TRI_SOLVE] += ms;
+  }
+  const int nc = async_u_.rows;
+  if (*reinterpret_cast<volatile int*>(reinterpret_cast<int*>(c.h_x + nc) + 1) != 0) {
+    throw DeviceError("triangular solve: dependency wait timed out");
+  }
+  const int fni = async_u_.first;
+  CopyHost(x->data() + fni, c.h_x + fni, size_t(async_u_.top - fni + 1) * sizeof(double));
+}
+
+void DeviceLp::DropAsyncU() {
+  if (!async_u_.active) return;
+  async_u_.active = false;
+  if (!async_u_.trivial && tri_ctx_[3].stream != nullptr) {
+    (void)hipStreamSynchronize(Stream(tri_ctx_[3].stream));
+  }
 }
 
 }  // namespace milp

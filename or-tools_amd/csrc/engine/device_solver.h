@@ -60,6 +60,17 @@ class DeviceSolver {
     (void)kind, (void)t, (void)key, (void)x0, (void)x1;
     return false;
   }
+  // The dense U solve (TransposeLowerSolve) of a vector needed later: staged
+  // now and launched on a stream of its own, so it runs behind the caller's
+  // other work (engine: the speculative flip FTRAN, lu.h). FinishAsyncU
+  // waits and writes the result into x (the vector given to StartAsyncU,
+  // kept by the caller); DropAsyncU waits and discards it. One at a time.
+  virtual bool StartAsyncU(const TriangularMatrix& t, uint64_t key, const std::vector<double>& x) {
+    (void)t, (void)key, (void)x;
+    return false;
+  }
+  virtual void FinishAsyncU(std::vector<double>* x) { (void)x; }
+  virtual void DropAsyncU() {}
   // x <- the result of t.TransposeLowerSolve(x), bit for bit. `key`
   // identifies the matrix (its LU and the factorization that built it): the
   // device copy and its dependency schedule are rebuilt when it changes.

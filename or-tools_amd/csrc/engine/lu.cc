@@ -791,6 +791,29 @@ void LuFactorization::RightSolveUAfterRows(ScatteredVector* x) const {
   }
 }
 
+int LuFactorization::StartRightSolveUAsync(ScatteredVector* x) const {
+  if (is_identity_factorization_) return 0;
+  upper_.ComputeRowsToConsiderInSortedOrder(&x->non_zeros);
+  x->non_zeros_are_sorted = true;
+  if (!x->non_zeros.empty()) {
+    transpose_upper_.TransposeHyperSparseSolveWithReversedNonZeros(&x->values, &x->non_zeros);
+    return 0;
+  }
+  if (device_solver_ != nullptr &&
+      device_solver_->StartAsyncU(transpose_upper_, factorization_key_, x->values)) {
+    return 1;
+  }
+  return -1;
+}
+
+void LuFactorization::FinishRightSolveUAsync(ScatteredVector* x) const {
+  device_solver_->FinishAsyncU(&x->values);
+}
+
+void LuFactorization::DropRightSolveUAsync() const {
+  if (device_solver_ != nullptr) device_solver_->DropAsyncU();
+}
+
 // lu_factorization.cc:333-399
 bool LuFactorization::LeftSolveLWithNonZeros(
     ScatteredVector* y, ScatteredVector* result_before_permutation) const {
@@ -1176,6 +1199,7 @@ void BasisFactorization::SyncForUnitRow() const {
 
 void BasisFactorization::Clear() {
   DropAsync();
+  SpecFlipDrop();
   num_updates_ = 0;
   tau_computation_can_be_optimized_ = false;
   lu_factorization_.Clear();
@@ -1265,28 +1289,118 @@ Status BasisFactorization::MiddleProductFormUpdate(int entering_col,
   if (right_index == kInvalidCol || left_index == kInvalidCol) {
     return ForceRefactorization();
   }
-  scratchpad_.resize(right_storage_.num_rows(), 0.0);
-  const ColumnView rc = right_storage_.column(right_index);
-  for (int64_t i = 0; i < rc.n; ++i) {
-    scratchpad_[rc.rows[i]] = rc.coefs[i];
-    scratchpad_non_zeros_.push_back(rc.rows[i]);
-  }
-  const SparseColumn& column_of_u =
-      lu_factorization_.GetColumnOfU(leaving_variable_row);
-  for (int64_t k = 0; k < column_of_u.num_entries(); ++k) {
-    scratchpad_[column_of_u.rows[k]] -= column_of_u.coefs[k];
-    scratchpad_non_zeros_.push_back(column_of_u.rows[k]);
-  }
+  int u_index = 0;
   const Fractional scalar_product =
-      storage_.ColumnScalarProduct(left_index, scratchpad_.data());
-  const int u_index =
-      storage_.AddAndClearColumnWithNonZeros(&scratchpad_, &scratchpad_non_zeros_);
+      MpfColumn(right_index, leaving_variable_row, left_index, &scratchpad_,
+                &scratchpad_non_zeros_, &storage_, &u_index);
   RankOneUpdateElementaryMatrix m(&storage_, u_index, left_index, scalar_product);
   if (m.IsSingular()) {
     return Status(Status::ERROR_LU, "Degenerate rank-one update.");
   }
   rank_one_factorization_.Update(m);
   return Status::OK();
+}
+
+Fractional BasisFactorization::MpfColumn(int right_index, int leaving_row, int left_index,
+                                         std::vector<Fractional>* scratch,
+                                         std::vector<int>* scratch_nz, CompactSparseMatrix* out,
+                                         int* u_index) const {
+  scratch->resize(right_storage_.num_rows(), 0.0);
+  const ColumnView rc = right_storage_.column(right_index);
+  for (int64_t i = 0; i < rc.n; ++i) {
+    (*scratch)[rc.rows[i]] = rc.coefs[i];
+    scratch_nz->push_back(rc.rows[i]);
+  }
+  const SparseColumn& column_of_u = lu_factorization_.GetColumnOfU(leaving_row);
+  for (int64_t k = 0; k < column_of_u.num_entries(); ++k) {
+    (*scratch)[column_of_u.rows[k]] -= column_of_u.coefs[k];
+    scratch_nz->push_back(column_of_u.rows[k]);
+  }
+  const Fractional scalar_product = storage_.ColumnScalarProduct(left_index, scratch->data());
+  *u_index = out->AddAndClearColumnWithNonZeros(scratch, scratch_nz);
+  return scalar_product;
+}
+
+// ---- speculative flip FTRAN (lu.h, BasisFactorization::SpecFlipBegin) ----
+bool BasisFactorization::SpecFlipBegin(ScatteredVector* f, int entering_col,
+                                       int leaving_row) const {
+  SpecFlipDrop();
+  if (!use_middle_product_form_update_) return false;
+  std::swap(spec_vec_, *f);  // *f gets the idle (all-zero) vector
+  // RightSolve (basis_representation.cc:358-372) up to the etas it has now.
+  lu_factorization_.RightSolveLWithNonZeros(&spec_vec_);
+  rank_one_factorization_.RightSolveBegin(&spec_vec_, &spec_split_);
+  spec_entering_ = entering_col;
+  spec_leaving_ = leaving_row;
+  spec_updates_ = num_updates_;
+  spec_factorizations_ = num_factorizations_;
+  spec_state_ = SpecState::kArmed;
+  return true;
+}
+
+// Inside the direction's FTRAN (after its right-pool append, while its U
+// solve runs on the device): the update UpdateAndPivot will make, applied
+// to the flip vector, then the flip vector's U solve.
+void BasisFactorization::SpecFlipLaunch() const {
+  if (spec_state_ != SpecState::kArmed) return;
+  const int right_index = spec_entering_ < static_cast<int>(right_pool_mapping_.size())
+                              ? right_pool_mapping_[spec_entering_]
+                              : kInvalidCol;
+  const int left_index = spec_leaving_ < static_cast<int>(left_pool_mapping_.size())
+                             ? left_pool_mapping_[spec_leaving_]
+                             : kInvalidCol;
+  if (right_index == kInvalidCol || left_index == kInvalidCol) {
+    SpecFlipDrop();
+    return;
+  }
+  spec_storage_.Reset(compact_matrix_.num_rows());
+  int u_index = 0;
+  const Fractional dot = MpfColumn(right_index, spec_leaving_, left_index, &spec_scratch_,
+                                   &spec_scratch_nz_, &spec_storage_, &u_index);
+  const RankOneUpdateElementaryMatrix next(&storage_, u_index, left_index, dot, &spec_storage_);
+  if (next.IsSingular()) {
+    SpecFlipDrop();
+    return;
+  }
+  rank_one_factorization_.RightSolveEnd(&spec_vec_, spec_split_, next);
+  const int r = lu_factorization_.StartRightSolveUAsync(&spec_vec_);
+  if (r < 0) {
+    SpecFlipDrop();
+    return;
+  }
+  spec_state_ = r == 1 ? SpecState::kInflight : SpecState::kDone;
+}
+
+bool BasisFactorization::SpecFlipTake(ScatteredVector* out) const {
+  if (spec_state_ != SpecState::kInflight && spec_state_ != SpecState::kDone) {
+    SpecFlipDrop();
+    return false;
+  }
+  if (num_factorizations_ != spec_factorizations_ || num_updates_ != spec_updates_ + 1) {
+    SpecFlipDrop();
+    return false;
+  }
+  if (spec_state_ == SpecState::kInflight) {
+    spec_state_ = SpecState::kDone;
+    lu_factorization_.FinishRightSolveUAsync(&spec_vec_);
+  }
+  spec_state_ = SpecState::kIdle;
+  std::swap(*out, spec_vec_);  // spec_vec_ takes the caller's all-zero vector
+  out->SortNonZerosIfNeeded();
+  // RightSolve's bumps, in its order: the etas', then the solve's.
+  rank_one_factorization_.BumpTime();
+  BumpDeterministicTimeForSolve(static_cast<int64_t>(out->NumNonZerosEstimate()));
+  return true;
+}
+
+void BasisFactorization::SpecFlipDrop() const {
+  if (spec_state_ == SpecState::kIdle) return;
+  if (spec_state_ == SpecState::kInflight) lu_factorization_.DropRightSolveUAsync();
+  spec_state_ = SpecState::kIdle;
+  std::fill(spec_vec_.values.begin(), spec_vec_.values.end(), 0.0);
+  spec_vec_.non_zeros.clear();
+  spec_vec_.non_zeros_are_sorted = false;
+  spec_vec_.is_non_zero.assign(spec_vec_.values.size(), false);
 }
 
 // basis_representation.cc:304-340
@@ -1652,18 +1766,24 @@ void BasisFactorization::RightSolveForProblemColumn(int col, ScatteredVector* d)
   struct Disarm {
     ~Disarm() { g_overlap.f = nullptr; }
   } disarm;
+  // The speculative flip FTRAN of this pivot (SpecFlipBegin) takes the
+  // update built from this column: it runs right after the append.
+  const bool spec = spec_state_ == SpecState::kArmed && spec_entering_ == col;
+  if (spec_state_ == SpecState::kArmed && !spec) SpecFlipDrop();
   if (d->non_zeros.empty()) {
     // Appended while the device solves U (the column is the vector before U;
     // g_overlap runs before anything overwrites it).
     const int slot_col = col;
-    g_overlap.f = [this, slot_col, d]() {
+    g_overlap.f = [this, slot_col, d, spec]() {
       right_pool_mapping_[slot_col] = right_storage_.AddDenseColumn(d->values);
+      if (spec) SpecFlipLaunch();
     };
   } else {
     FtranTimer pool_timer(kFtUPool);
     std::sort(d->non_zeros.begin(), d->non_zeros.end());
     right_pool_mapping_[col] =
         right_storage_.AddDenseColumnWithNonZeros(d->values, d->non_zeros);
+    if (spec) g_overlap.f = [this]() { SpecFlipLaunch(); };
   }
   if (async_kind_ == AsyncKind::kTauDeferred && async_) async_->Wait();  // tau's L, etas
   if (async_kind_ == AsyncKind::kTauDeferred && tau_u_pending_) {

@@ -937,6 +937,14 @@ class LuFactorization {
   // take the dense path; else one after the other. Same bits as two calls.
   void RightSolveUWithNonZerosPair(ScatteredVector* x, ScatteredVector* tau) const;
   void RightSolveUAfterRows(ScatteredVector* x) const;
+  // The speculative flip FTRAN's U solve (engine, BasisFactorization::
+  // SpecFlipLaunch): RightSolveUWithNonZeros' steps with the dense solve
+  // launched on the device's own stream for it. 1: launched (Finish
+  // completes x), 0: solved here (identity or hypersparse), -1: the device
+  // declined a dense solve (x is not solved; the caller drops it).
+  int StartRightSolveUAsync(ScatteredVector* x) const;
+  void FinishRightSolveUAsync(ScatteredVector* x) const;
+  void DropRightSolveUAsync() const;
   bool LeftSolveLWithNonZeros(ScatteredVector* y,
                               ScatteredVector* result_before_permutation) const;
   int LeftSolveUForUnitRow(int col, ScatteredVector* y) const;
@@ -1017,35 +1025,38 @@ class RankOneUpdateElementaryMatrix {
   friend struct SdualBridge;
 
  public:
+  // u_storage: where u lives when not in `storage` (engine: the speculative
+  // flip FTRAN's copy of the next update, BasisFactorization::SpecFlipLaunch).
   RankOneUpdateElementaryMatrix(const CompactSparseMatrix* storage, int u_index,
-                                int v_index, Fractional u_dot_v)
-      : storage_(storage), u_index_(u_index), v_index_(v_index),
-        mu_(1.0 + u_dot_v) {}
+                                int v_index, Fractional u_dot_v,
+                                const CompactSparseMatrix* u_storage = nullptr)
+      : storage_(storage), u_storage_(u_storage != nullptr ? u_storage : storage),
+        u_index_(u_index), v_index_(v_index), mu_(1.0 + u_dot_v) {}
   bool IsSingular() const { return mu_ == 0.0; }
   void RightSolve(std::vector<Fractional>* x) const {
     const Fractional multiplier =
         -storage_->ColumnScalarProduct(v_index_, x->data()) / mu_;
-    storage_->ColumnAddMultipleToDenseColumn(u_index_, multiplier, x->data());
+    u_storage_->ColumnAddMultipleToDenseColumn(u_index_, multiplier, x->data());
   }
   void RightSolveWithNonZeros(ScatteredVector* x) const {
     const Fractional multiplier =
         -storage_->ColumnScalarProduct(v_index_, x->values.data()) / mu_;
     if (multiplier != 0.0)
-      storage_->ColumnAddMultipleToSparseScatteredColumn(u_index_, multiplier, x);
+      u_storage_->ColumnAddMultipleToSparseScatteredColumn(u_index_, multiplier, x);
   }
   void LeftSolve(std::vector<Fractional>* y) const {
     const Fractional multiplier =
-        -storage_->ColumnScalarProduct(u_index_, y->data()) / mu_;
+        -u_storage_->ColumnScalarProduct(u_index_, y->data()) / mu_;
     storage_->ColumnAddMultipleToDenseColumn(v_index_, multiplier, y->data());
   }
   void LeftSolveWithNonZeros(ScatteredVector* y) const {
     const Fractional multiplier =
-        -storage_->ColumnScalarProduct(u_index_, y->values.data()) / mu_;
+        -u_storage_->ColumnScalarProduct(u_index_, y->values.data()) / mu_;
     if (multiplier != 0.0)
       storage_->ColumnAddMultipleToSparseScatteredColumn(v_index_, multiplier, y);
   }
   int64_t num_entries() const {
-    return storage_->ColumnNumEntries(u_index_) +
+    return u_storage_->ColumnNumEntries(u_index_) +
            storage_->ColumnNumEntries(v_index_);
   }
   int u_index() const { return u_index_; }
@@ -1054,6 +1065,7 @@ class RankOneUpdateElementaryMatrix {
 
  private:
   const CompactSparseMatrix* storage_;
+  const CompactSparseMatrix* u_storage_;
   int u_index_;
   int v_index_;
   Fractional mu_;
@@ -1119,6 +1131,47 @@ class RankOneUpdateFactorization {
     d->ClearSparseMask();
     d->ClearNonZerosIfTooDense(hypersparse_ratio_);
     BumpTime();
+  }
+  // RightSolveWithNonZeros split in two calls (engine: the speculative flip
+  // FTRAN applies the matrix of the next update later, once it is known):
+  // Begin applies the current matrices, End one more and finishes as the
+  // loop above finishes. Same steps in the same order, so the same bits as
+  // RightSolveWithNonZeros over all of them; neither call bumps (the caller
+  // applies BumpTime() where the serial solve would have).
+  struct SplitSolve {
+    bool dense = false;      // d->non_zeros was empty: RightSolve's dense loop
+    bool use_dense = false;  // the sparse loop's state after Begin
+  };
+  void RightSolveBegin(ScatteredVector* d, SplitSolve* st) const {
+    st->dense = d->non_zeros.empty();
+    if (st->dense) {
+      for (const auto& m : elementary_matrices_) m.RightSolve(&d->values);
+      return;
+    }
+    d->RepopulateSparseMask();
+    st->use_dense = d->ShouldUseDenseIteration(hypersparse_ratio_);
+    for (const auto& m : elementary_matrices_) {
+      if (st->use_dense) {
+        m.RightSolve(&d->values);
+      } else {
+        m.RightSolveWithNonZeros(d);
+        st->use_dense = d->ShouldUseDenseIteration(hypersparse_ratio_);
+      }
+    }
+  }
+  void RightSolveEnd(ScatteredVector* d, const SplitSolve& st,
+                     const RankOneUpdateElementaryMatrix& last) const {
+    if (st.dense) {
+      last.RightSolve(&d->values);
+      return;
+    }
+    if (st.use_dense) {
+      last.RightSolve(&d->values);
+    } else {
+      last.RightSolveWithNonZeros(d);
+    }
+    d->ClearSparseMask();
+    d->ClearNonZerosIfTooDense(hypersparse_ratio_);
   }
   int64_t num_entries() const { return num_entries_; }
   // A solve on the tau worker defers its bump; the solver's thread applies
@@ -1289,9 +1342,47 @@ class BasisFactorization {
   // the cached factors instead of running Markowitz.
   void SetLuShareCache(struct LuShareCache* c) { lu_share_ = c; }
 
+  // Speculative flip FTRAN (engine scheduling, no Glop counterpart). The
+  // next iteration's MakeBoxedVariableDualFeasible (revised_simplex.cc:
+  // 2391-2437) RightSolves the bound flips' value changes against the basis
+  // after this iteration's pivot. The dual loop predicts the flips right
+  // after the ratio test and hands their scattered changes to SpecFlipBegin,
+  // which runs L and the current etas on them. The direction's FTRAN then
+  // builds the MPF update the pivot will make (its u column exactly as
+  // MiddleProductFormUpdate builds it, into a scratch storage), applies it
+  // and launches the U solve on a stream of its own, behind the rest of the
+  // iteration (SpecFlipLaunch). SpecFlipTake hands the result over at the
+  // next iteration's top when the factorization is the one it was computed
+  // for (one more update, no refactorization), with the deterministic-time
+  // bumps RightSolve makes there; the caller has checked the flips. The
+  // vector it returns in *out is RightSolve's, bit for bit. Begin takes *f
+  // (leaving an all-zero vector there) unless it returns false (PFI path).
+  bool SpecFlipBegin(ScatteredVector* f, int entering_col, int leaving_row) const;
+  bool SpecFlipTake(ScatteredVector* out) const;
+  void SpecFlipDrop() const;  // waits for a launched solve; no-op when idle
+  bool SpecFlipPending() const { return spec_state_ != SpecState::kIdle; }
+
  private:
   Status ComputeFactorization();
   Status MiddleProductFormUpdate(int entering_col, int leaving_variable_row);
+  // MiddleProductFormUpdate's u column (basis_representation.cc:272-293):
+  // the right pool's column minus U's column of the leaving row, appended to
+  // *out through the all-zero scratch; returns u.v (v: the left pool's column).
+  Fractional MpfColumn(int right_index, int leaving_row, int left_index,
+                       std::vector<Fractional>* scratch, std::vector<int>* scratch_nz,
+                       CompactSparseMatrix* out, int* u_index) const;
+  void SpecFlipLaunch() const;
+  enum class SpecState { kIdle, kArmed, kInflight, kDone };
+  mutable SpecState spec_state_ = SpecState::kIdle;
+  mutable ScatteredVector spec_vec_;  // all zero when idle
+  mutable RankOneUpdateFactorization::SplitSolve spec_split_;
+  mutable int spec_entering_ = -1;
+  mutable int spec_leaving_ = -1;
+  mutable int spec_updates_ = 0;
+  mutable int64_t spec_factorizations_ = 0;
+  mutable CompactSparseMatrix spec_storage_;
+  mutable std::vector<Fractional> spec_scratch_;
+  mutable std::vector<int> spec_scratch_nz_;
 
   uint64_t StartAsync(AsyncKind kind, std::function<void()> job) const;
   void WaitAsync() const;

@@ -13,6 +13,7 @@
 // produces. Basis factorization and FTRAN/BTRAN stay on the host in round 1.
 #include "simplex.h"
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -2271,6 +2272,9 @@ class EnteringVariable {
   double DeterministicTime() const {
     return DeterministicTimeForFpOperations(num_operations_);
   }
+  // The last device ratio test's candidates (their update-row coefficients
+  // and reduced costs): the speculative flip FTRAN's prediction reads them.
+  const DeviceLp::DualCandidates& LastDeviceCandidates() const { return candidates_; }
 
  private:
   struct ColWithRatio {  // entering_variable.h:118-139
@@ -2635,6 +2639,15 @@ class VariableValues {
     variable_values_[entering_col] += step;
   }
   void UpdateGivenNonBasicVariables(const std::vector<int>& cols, bool update_basic);
+  // Speculative flip FTRAN (engine; BasisFactorization::SpecFlipBegin): the
+  // flips `cols` with value changes `deltas` the next iteration's
+  // MakeBoxedVariableDualFeasible is expected to make, scattered as
+  // UpdateGivenNonBasicVariables scatters them and solved ahead. That call
+  // uses the result when it flips exactly these columns by exactly these
+  // changes; SpecFlipDone drops a speculation nothing used.
+  void SpecFlipBegin(const std::vector<int>& cols, const std::vector<Fractional>& deltas,
+                     int entering_col, int leaving_row);
+  void SpecFlipDone();
   void RecomputeDualPrices(bool put_more_importance_on_norm = false);
   void RecomputeDualPricesImpl(bool put_more_importance_on_norm, Fractional* delta);
   void UpdateDualPrices(const std::vector<int>& rows);
@@ -2676,9 +2689,20 @@ class VariableValues {
   DualEdgeNorms* dual_edge_norms_;
   DynamicMaximum* dual_prices_;
   DeviceLp* dev_;
+  // UpdateGivenNonBasicVariables' scatter of the flips' value changes.
+  void ScatterFlipChanges(const std::vector<int>& cols, const Fractional* deltas,
+                          ScatteredVector* v) const;
   std::vector<Fractional> variable_values_;
   mutable ScatteredVector scratchpad_;
   ScatteredVector initially_all_zero_scratchpad_;
+  std::vector<Fractional> flip_deltas_;
+  bool spec_armed_ = false;
+  std::vector<int> spec_cols_;
+  std::vector<Fractional> spec_deltas_;
+  ScatteredVector spec_scratch_;  // all zero between uses
+ public:
+  // MILP_SPEC_FLIP_STATS=1: speculations used / dropped, printed at exit.
+  static std::atomic<int64_t> spec_used, spec_missed, spec_started;
 };
 
 void VariableValues::SetNonBasicVariableValueFromStatus(int col) {
@@ -2778,33 +2802,93 @@ Fractional VariableValues::ComputeMaximumPrimalInfeasibility() const {
 }
 
 // variable_values.cc:179-227
+std::atomic<int64_t> VariableValues::spec_used{0}, VariableValues::spec_missed{0},
+    VariableValues::spec_started{0};
+namespace {
+struct SpecFlipStatsAtExit {
+  ~SpecFlipStatsAtExit() {
+    if (std::getenv("MILP_SPEC_FLIP_STATS") == nullptr) return;
+    std::fprintf(stderr, "[spec flip] started %lld used %lld dropped %lld\n",
+                 static_cast<long long>(VariableValues::spec_started.load()),
+                 static_cast<long long>(VariableValues::spec_used.load()),
+                 static_cast<long long>(VariableValues::spec_missed.load()));
+  }
+} g_spec_flip_stats_at_exit;
+}  // namespace
+
+void VariableValues::ScatterFlipChanges(const std::vector<int>& cols, const Fractional* deltas,
+                                        ScatteredVector* v) const {
+  v->values.resize(matrix_.num_rows(), 0.0);
+  v->ClearSparseMask();
+  bool use_dense = false;
+  for (size_t i = 0; i < cols.size(); ++i) {
+    if (use_dense) {
+      matrix_.ColumnAddMultipleToDenseColumn(cols[i], deltas[i], v->values.data());
+    } else {
+      matrix_.ColumnAddMultipleToSparseScatteredColumn(cols[i], deltas[i], v);
+      use_dense = v->ShouldUseDenseIteration();
+    }
+  }
+  v->ClearSparseMask();
+  v->ClearNonZerosIfTooDense();
+}
+
+void VariableValues::SpecFlipBegin(const std::vector<int>& cols,
+                                   const std::vector<Fractional>& deltas, int entering_col,
+                                   int leaving_row) {
+  SpecFlipDone();
+  ScatterFlipChanges(cols, deltas.data(), &spec_scratch_);
+  if (!bf_.SpecFlipBegin(&spec_scratch_, entering_col, leaving_row)) {
+    std::fill(spec_scratch_.values.begin(), spec_scratch_.values.end(), 0.0);
+    spec_scratch_.non_zeros.clear();
+    spec_scratch_.ClearSparseMask();
+    return;
+  }
+  spec_cols_ = cols;
+  spec_deltas_ = deltas;
+  spec_armed_ = true;
+  ++spec_started;
+}
+
+void VariableValues::SpecFlipDone() {
+  if (!spec_armed_) return;
+  spec_armed_ = false;
+  bf_.SpecFlipDrop();
+  ++spec_missed;
+}
+
 void VariableValues::UpdateGivenNonBasicVariables(const std::vector<int>& cols,
                                                   bool update_basic) {
   if (!update_basic) {
     for (const int col : cols) SetNonBasicVariableValueFromStatus(col);
     return;
   }
-  const int num_rows = matrix_.num_rows();
-  initially_all_zero_scratchpad_.values.resize(num_rows, 0.0);
-  initially_all_zero_scratchpad_.ClearSparseMask();
-  bool use_dense = false;
   SubTimer scatter_timer(kSubFlipScatter);
-  for (const int col : cols) {
-    const Fractional old_value = variable_values_[col];
-    SetNonBasicVariableValueFromStatus(col);
-    if (use_dense) {
-      matrix_.ColumnAddMultipleToDenseColumn(col, variable_values_[col] - old_value,
-                                             initially_all_zero_scratchpad_.values.data());
-    } else {
-      matrix_.ColumnAddMultipleToSparseScatteredColumn(
-          col, variable_values_[col] - old_value, &initially_all_zero_scratchpad_);
-      use_dense = initially_all_zero_scratchpad_.ShouldUseDenseIteration();
-    }
+  flip_deltas_.resize(cols.size());
+  for (size_t i = 0; i < cols.size(); ++i) {
+    const Fractional old_value = variable_values_[cols[i]];
+    SetNonBasicVariableValueFromStatus(cols[i]);
+    flip_deltas_[i] = variable_values_[cols[i]] - old_value;
   }
-  initially_all_zero_scratchpad_.ClearSparseMask();
-  initially_all_zero_scratchpad_.ClearNonZerosIfTooDense();
-  scatter_timer.Stop();
-  {
+  // The speculative solve is RightSolve's result for the same flips and
+  // changes (same columns in the same order, the same bits).
+  bool solved = false;
+  if (spec_armed_) {
+    scatter_timer.Stop();
+    spec_armed_ = false;
+    if (cols == spec_cols_ &&
+        std::memcmp(flip_deltas_.data(), spec_deltas_.data(),
+                    cols.size() * sizeof(Fractional)) == 0) {
+      SubTimer solve_timer(kSubFlipSolve);
+      solved = bf_.SpecFlipTake(&initially_all_zero_scratchpad_);
+    } else {
+      bf_.SpecFlipDrop();
+    }
+    ++(solved ? spec_used : spec_missed);
+  }
+  if (!solved) {
+    ScatterFlipChanges(cols, flip_deltas_.data(), &initially_all_zero_scratchpad_);
+    scatter_timer.Stop();
     SubTimer solve_timer(kSubFlipSolve);
     bf_.RightSolve(&initially_all_zero_scratchpad_);
   }
@@ -3388,6 +3472,8 @@ class RevisedSimplex {
   void FlushColumnBits();
   // MakeBoxedVariableDualFeasible with the decisions taken on the device;
   // cols == nullptr: every non-basic boxed column.
+  void SpeculateFlips(int entering_col, int leaving_row, Fractional entering_coeff,
+                      Fractional entering_rc);
   void MakeBoxedVariableDualFeasibleOnDevice(const std::vector<int>* cols,
                                              bool update_basic_values);
   Fractional ComputeStepToMoveBasicVariableToBound(int leaving_row, Fractional target_bound) {
@@ -3570,6 +3656,9 @@ class RevisedSimplex {
   std::vector<int> flush_cols_;
   std::vector<uint8_t> flush_bits_;
   std::vector<uint8_t> flip_flags_;
+  std::vector<int> spec_pos_;  // SpeculateFlips: candidate index by column (-1)
+  std::vector<int> spec_cols_;
+  std::vector<Fractional> spec_deltas_;
   // Device dual segment (csrc/sdual): 0 off, 1 on the host (the same
   // restatement compiled for the CPU, a debugging aid), 2 on the device.
   int sdual_mode_ = 0;
@@ -5089,6 +5178,43 @@ void RevisedSimplex::FlushColumnBits() {
 
 // revised_simplex.cc:2391-2437. The per-column decisions do not depend on
 // each other, so they are taken in one device pass and applied in order.
+// Speculative flip FTRAN (VariableValues::SpecFlipBegin): the flips the
+// next iteration's MakeBoxedVariableDualFeasible(bound_flip_candidates_)
+// (revised_simplex.cc:2391-2437) is expected to make, predicted from the
+// candidates' reduced costs after this pivot's update (reduced_costs.cc:
+// 444-488, with the update row's entering coefficient for the pivot). A
+// wrong prediction costs the speculative solve only: the next iteration
+// uses it only for exactly the flips and value changes it makes.
+void RevisedSimplex::SpeculateFlips(int entering_col, int leaving_row, Fractional entering_coeff,
+                                    Fractional entering_rc) {
+  const DeviceLp::DualCandidates& cand = entering_variable_.LastDeviceCandidates();
+  const int n = static_cast<int>(cand.col.size());
+  spec_pos_.resize(variables_info_.GetStatusRow().size(), -1);
+  for (int k = 0; k < n; ++k) spec_pos_[cand.col[k]] = k;
+  const Fractional threshold = reduced_costs_.GetDualFeasibilityTolerance();
+  const Fractional step = entering_rc == 0.0 ? 0.0 : entering_rc / -entering_coeff;
+  const std::vector<VariableStatus>& status = variables_info_.GetStatusRow();
+  const std::vector<Fractional>& lb = variables_info_.GetVariableLowerBounds();
+  const std::vector<Fractional>& ub = variables_info_.GetVariableUpperBounds();
+  spec_cols_.clear();
+  spec_deltas_.clear();
+  for (const int col : bound_flip_candidates_) {
+    const int k = spec_pos_[col];
+    if (col == entering_col || k < 0) continue;
+    const Fractional rc = cand.rc[k] + step * cand.coeff[k];
+    if (rc > threshold && status[col] == VariableStatus::AT_UPPER_BOUND) {
+      spec_cols_.push_back(col);
+      spec_deltas_.push_back(lb[col] - variable_values_.Get(col));
+    } else if (rc < -threshold && status[col] == VariableStatus::AT_LOWER_BOUND) {
+      spec_cols_.push_back(col);
+      spec_deltas_.push_back(ub[col] - variable_values_.Get(col));
+    }
+  }
+  for (int k = 0; k < n; ++k) spec_pos_[cand.col[k]] = -1;
+  if (spec_cols_.empty()) return;
+  variable_values_.SpecFlipBegin(spec_cols_, spec_deltas_, entering_col, leaving_row);
+}
+
 void RevisedSimplex::MakeBoxedVariableDualFeasibleOnDevice(const std::vector<int>* cols,
                                                            bool update_basic_values) {
   std::vector<int> changed_cols;
@@ -5145,6 +5271,19 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
       }
     }
   } end_device_mode{this, device_mode};
+  // A speculative flip FTRAN still pending when the loop leaves is dropped
+  // (its device solve waited for).
+  struct DropSpec {
+    VariableValues* v;
+    ~DropSpec() {
+      try {
+        v->SpecFlipDone();
+      } catch (const DeviceError&) {
+      }
+    }
+  } drop_spec{&variable_values_};
+  const bool spec_flip = device_mode && device_.SpecFlipEnabled() &&
+                         parameters_.use_middle_product_form_update;
   bool refactorize = false;
   bound_flip_candidates_.clear();
   int leaving_row;
@@ -5187,6 +5326,7 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
         variable_values_.UpdateDualPrices(direction_.non_zeros);
       }
     }
+    variable_values_.SpecFlipDone();  // a speculation the flips did not use
     clock.Mark(0);
 
     // Phase II, or dual phase I (sd_run's dual_phase1). A warm start's phase
@@ -5272,6 +5412,9 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
       if (entering_col != kInvalidCol) {
         update_row_.SetKnownCoefficient(entering_col, coeff);
         reduced_costs_.SetKnownReducedCost(entering_col, rc);
+        if (spec_flip && !bound_flip_candidates_.empty()) {
+          SpeculateFlips(entering_col, leaving_row, coeff, rc);
+        }
       }
     } else {
       MILP_RETURN_IF_ERROR(entering_variable_.DualChooseEnteringColumn(
@@ -6671,4 +6814,12 @@ int mi_lp_batch_solve_gpus(mi_lp* const* handles, int32_t count, int32_t num_gpu
 extern "C" void milp_sdual_profile_reset() {
   milp::SdualBridge::ResetProfile();
   milp::SdualProfileReset();
+}
+
+// Speculative flip FTRAN counters (process-wide): out[0] started, out[1]
+// used by the next iteration, out[2] dropped. Read by the GPU tests.
+extern "C" void milp_spec_flip_stats(int64_t* out) {
+  out[0] = milp::VariableValues::spec_started.load();
+  out[1] = milp::VariableValues::spec_used.load();
+  out[2] = milp::VariableValues::spec_missed.load();
 }

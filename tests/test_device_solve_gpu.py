@@ -115,6 +115,38 @@ def test_device_u_solve_with_async_tau_and_device_dual(device_dual, async_solves
     assert g.kernel_stats()["tri_solve"]["launches"] > 0
 
 
+def _spec_flip_stats():
+    import ctypes
+    out = (ctypes.c_int64 * 3)()
+    engine.lib().milp_spec_flip_stats(out)
+    return list(out)
+
+
+@pytest.mark.parametrize("seed", [78, 79, 80])
+@pytest.mark.parametrize("spec", ["0", "1"])
+def test_speculative_flip_ftran_parity(seed, spec, monkeypatch):
+    """The next iteration's bound-flip FTRAN (MakeBoxedVariableDualFeasible,
+    revised_simplex.cc:2391-2437) computed ahead: L and the etas after the
+    ratio test, the pivot's MPF update applied inside the direction's FTRAN,
+    the U solve on its own stream (engine/lu.cc SpecFlipBegin/Launch/Take).
+    Used or dropped, the results and the deterministic time are the
+    oracle's bit for bit; with it on, the next iterations use most of them."""
+    monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
+    monkeypatch.setenv("MILP_DEVICE_DUAL", "force")
+    monkeypatch.setenv("MILP_SPEC_FLIP", spec)
+    lp = lp_gen.sparse_c5_lp(600, 6000, 6, seed)
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1500)
+    before = _spec_flip_stats()
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+    after = _spec_flip_stats()
+    started, used = after[0] - before[0], after[1] - before[1]
+    if spec == "1":
+        assert started > 0 and used > 0, (started, used, after[2] - before[2])
+    else:
+        assert started == 0
+
+
 @pytest.mark.parametrize("builder", kat_lps.ALL, ids=lambda f: f.__name__)
 @pytest.mark.parametrize("dual", [0, 1])
 def test_device_u_solve_known_answers(builder, dual, monkeypatch):
