@@ -1200,6 +1200,7 @@ void BasisFactorization::SyncForUnitRow() const {
 void BasisFactorization::Clear() {
   DropAsync();
   SpecFlipDrop();
+  spec_mpf_.valid = false;
   num_updates_ = 0;
   tau_computation_can_be_optimized_ = false;
   lu_factorization_.Clear();
@@ -1290,9 +1291,19 @@ Status BasisFactorization::MiddleProductFormUpdate(int entering_col,
     return ForceRefactorization();
   }
   int u_index = 0;
-  const Fractional scalar_product =
-      MpfColumn(right_index, leaving_variable_row, left_index, &scratchpad_,
-                &scratchpad_non_zeros_, &storage_, &u_index);
+  Fractional scalar_product = 0.0;
+  const SpecMpf& sm = spec_mpf_;
+  if (sm.valid && sm.entering == entering_col && sm.leaving == leaving_variable_row &&
+      sm.right == right_index && sm.left == left_index &&
+      sm.factorizations == num_factorizations_ && sm.updates + 1 == num_updates_) {
+    // Built by the speculative flip FTRAN from the same columns (SpecFlipLaunch).
+    u_index = sm.u_index;
+    scalar_product = sm.dot;
+  } else {
+    scalar_product = MpfColumn(right_index, leaving_variable_row, left_index, &scratchpad_,
+                               &scratchpad_non_zeros_, &storage_, &u_index);
+  }
+  spec_mpf_.valid = false;
   RankOneUpdateElementaryMatrix m(&storage_, u_index, left_index, scalar_product);
   if (m.IsSingular()) {
     return Status(Status::ERROR_LU, "Degenerate rank-one update.");
@@ -1353,11 +1364,21 @@ void BasisFactorization::SpecFlipLaunch() const {
     SpecFlipDrop();
     return;
   }
-  spec_storage_.Reset(compact_matrix_.num_rows());
+  // u goes straight into storage_ (where MiddleProductFormUpdate would put
+  // it) unless a worker may be reading storage_ now; an unused column there
+  // is never referenced and goes with the next refactorization's Clear.
+  const bool into_storage =
+      async_kind_ == AsyncKind::kNone || async_kind_ == AsyncKind::kTauDeferred;
+  CompactSparseMatrix* out = into_storage ? &storage_ : &spec_storage_;
+  if (!into_storage) spec_storage_.Reset(compact_matrix_.num_rows());
   int u_index = 0;
   const Fractional dot = MpfColumn(right_index, spec_leaving_, left_index, &spec_scratch_,
-                                   &spec_scratch_nz_, &spec_storage_, &u_index);
-  const RankOneUpdateElementaryMatrix next(&storage_, u_index, left_index, dot, &spec_storage_);
+                                   &spec_scratch_nz_, out, &u_index);
+  if (into_storage) {
+    spec_mpf_ = SpecMpf{true, spec_entering_, spec_leaving_, right_index, left_index,
+                        num_updates_, u_index, num_factorizations_, dot};
+  }
+  const RankOneUpdateElementaryMatrix next(&storage_, u_index, left_index, dot, out);
   if (next.IsSingular()) {
     SpecFlipDrop();
     return;

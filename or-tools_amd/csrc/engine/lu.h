@@ -1381,6 +1381,16 @@ class BasisFactorization {
   mutable int spec_updates_ = 0;
   mutable int64_t spec_factorizations_ = 0;
   mutable CompactSparseMatrix spec_storage_;
+  // The u column SpecFlipLaunch built, when it went straight into storage_
+  // (no worker reading storage_ then): MiddleProductFormUpdate of the same
+  // pivot on the same factorization takes it instead of rebuilding it.
+  struct SpecMpf {
+    bool valid = false;
+    int entering = -1, leaving = -1, right = -1, left = -1, updates = 0, u_index = -1;
+    int64_t factorizations = 0;
+    Fractional dot = 0.0;
+  };
+  mutable SpecMpf spec_mpf_;
   mutable std::vector<Fractional> spec_scratch_;
   mutable std::vector<int> spec_scratch_nz_;
 
