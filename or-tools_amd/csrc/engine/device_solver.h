@@ -35,14 +35,12 @@ constexpr int kNumTriKinds = 6;
 // overwrites; the device solve has copied it by then.)
 struct OverlapWork {
   std::function<void()> f;
-  void Run() {
-    if (!f) return;
-    std::function<void()> g = std::move(f);
-    f = nullptr;
-    g();
-  }
+  void Run();
 };
 extern thread_local OverlapWork g_overlap;
+// Set while overlap work runs inside a device solve: that work's own dense
+// loops stay on the host (the solving thread's device context is busy).
+extern thread_local bool g_in_overlap;
 
 class DeviceSolver {
  public:

@@ -596,7 +596,7 @@ Fractional LuFactorization::DualEdgeSquaredNorm(int row) const {
 // The dense L loop of every FTRAN: on the device (same bits: outputs below
 // `start` receive nothing in the host loop either), else on the host.
 void LuFactorization::DenseLowerSolve(int start, std::vector<Fractional>* x) const {
-  if (device_solver_ == nullptr ||
+  if (device_solver_ == nullptr || g_in_overlap ||
       !device_solver_->LowerSolve(lower_, factorization_key_, x)) {
     lower_.LowerSolveStartingAt(start, x);
   }
@@ -606,7 +606,8 @@ void LuFactorization::DenseLowerSolve(int start, std::vector<Fractional>* x) con
 // (same bits, device_solver.h), else the host loop.
 void LuFactorization::DenseSolve(TriKind kind, const TriangularMatrix& t, int start,
                                  std::vector<Fractional>* x) const {
-  if (device_solver_ != nullptr && device_solver_->Solve(kind, t, factorization_key_, start, x)) {
+  if (device_solver_ != nullptr && !g_in_overlap &&
+      device_solver_->Solve(kind, t, factorization_key_, start, x)) {
     return;
   }
   switch (kind) {
@@ -1338,9 +1339,6 @@ bool BasisFactorization::SpecFlipBegin(ScatteredVector* f, int entering_col,
   SpecFlipDrop();
   if (!use_middle_product_form_update_) return false;
   std::swap(spec_vec_, *f);  // *f gets the idle (all-zero) vector
-  // RightSolve (basis_representation.cc:358-372) up to the etas it has now.
-  lu_factorization_.RightSolveLWithNonZeros(&spec_vec_);
-  rank_one_factorization_.RightSolveBegin(&spec_vec_, &spec_split_);
   spec_entering_ = entering_col;
   spec_leaving_ = leaving_row;
   spec_updates_ = num_updates_;
@@ -1364,6 +1362,11 @@ void BasisFactorization::SpecFlipLaunch() const {
     SpecFlipDrop();
     return;
   }
+  // RightSolve (basis_representation.cc:358-372): L and the etas it has now
+  // (none changed since the ratio test), while the device solves the
+  // direction's U; their dense loops stay on the host (g_in_overlap).
+  lu_factorization_.RightSolveLWithNonZeros(&spec_vec_);
+  rank_one_factorization_.RightSolveBegin(&spec_vec_, &spec_split_);
   // u goes straight into storage_ (where MiddleProductFormUpdate would put
   // it) unless a worker may be reading storage_ now; an unused column there
   // is never referenced and goes with the next refactorization's Clear.
@@ -1462,6 +1465,17 @@ void BasisFactorization::LeftSolve(ScatteredVector* y) const {
 }
 
 thread_local OverlapWork g_overlap;
+thread_local bool g_in_overlap = false;
+void OverlapWork::Run() {
+  if (!f) return;
+  std::function<void()> g = std::move(f);
+  f = nullptr;
+  struct Flag {
+    Flag() { g_in_overlap = true; }
+    ~Flag() { g_in_overlap = false; }
+  } flag;
+  g();
+}
 
 bool TriangularMatrix::ParallelTransposeSolve(bool forward, std::vector<Fractional>* rhs) const {
   // Opt-in (MILP_HOST_TRI_PAR=1): on the MI355X box the gain on config 2's

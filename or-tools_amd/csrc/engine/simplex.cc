@@ -113,14 +113,17 @@ enum SubPhase {
   kSubBtranY, kSubPricingCall, kSubCandidatesFull, kSubGetMaximum, kSubBtranW,
   kSubUpdateRowCall, kSubNormLoop, kSubQueue, kSubLuUpdate, kSubRefactorize,
   kSubBoxedScan, kSubFlipFtran, kSubRecomputeValues, kSubDualPrices, kSubFtranDirection,
-  kSubTau, kSubFlipScatter, kSubFlipSolve, kSubFlipPrices, kNumSubPhases
+  kSubTau, kSubFlipScatter, kSubFlipSolve, kSubFlipPrices, kSubRatioPrep, kSubRatioDevice,
+  kSubRatioReplay, kSubSpecBegin, kNumSubPhases
 };
 const char* const kSubPhaseNames[kNumSubPhases] = {
     "btran y (c_B B^-1)", "pricing device call", "prices full rebuild", "GetMaximum",
     "btran w (B^-T d)",   "update-row device",   "norm update loop",    "price queue/replay",
     "basis update (MPF)", "refactorize (LU)", "boxed dual-feas scan", "flip update (FTRAN)",
     "recompute x_B",      "dual prices",       "ftran direction",   "tau ftran",
-    "  flip: column scatter", "  flip: RightSolve", "  flip: x_B + prices"};
+    "  flip: column scatter", "  flip: RightSolve", "  flip: x_B + prices",
+    "  ratio: prepare (row, bits)", "  ratio: device call", "  ratio: host replay",
+    "  ratio: speculative flips"};
 double g_sub_ms[kNumSubPhases] = {};
 double g_dual_candidates = 0.0;  // device ratio test: candidates returned
 double g_dual_list = 0.0;        // update-row positions they were filtered from
@@ -2332,8 +2335,11 @@ Status EnteringVariable::DualChooseEnteringColumnDevice(bool nothing_to_recomput
       params_.harris_tolerance_ratio * reduced_costs_->GetDualFeasibilityTolerance();
   const Fractional minimum_delta =
       params_.degenerate_ministep_factor * reduced_costs_->GetDualFeasibilityTolerance();
+  SubTimer device_timer(kSubRatioDevice);
   dev->DualRatioCandidates(cost_variation > 0.0 ? 1.0 : -1.0, threshold, harris_tolerance,
                            minimum_delta, variation_magnitude, &candidates_);
+  device_timer.Stop();
+  SubTimer replay_timer(kSubRatioReplay);
   const DeviceLp::DualCandidates& cand = candidates_;
   num_operations_ += 10 * static_cast<int64_t>(cand.list_count);
   if (g_sub_on) {
@@ -5401,9 +5407,11 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
           &entering_col));
     } else if (dual_device_mode_) {
       const bool nothing_to_recompute = reduced_costs_.AreReducedCostsPrecise();
+      SubTimer prep_timer(kSubRatioPrep);
       update_row_.MaterializeOnDevice();
       reduced_costs_.PrepareForDeviceUse();  // GetReducedCosts() side effects
       FlushColumnBits();
+      prep_timer.Stop();
       Fractional coeff = 0.0;
       Fractional rc = 0.0;
       MILP_RETURN_IF_ERROR(entering_variable_.DualChooseEnteringColumnDevice(
@@ -5413,6 +5421,7 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
         update_row_.SetKnownCoefficient(entering_col, coeff);
         reduced_costs_.SetKnownReducedCost(entering_col, rc);
         if (spec_flip && !bound_flip_candidates_.empty()) {
+          SubTimer spec_timer(kSubSpecBegin);
           SpeculateFlips(entering_col, leaving_row, coeff, rc);
         }
       }
