@@ -9,7 +9,6 @@ exec_steps=(
   "tests@780=python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider"
   "smoke@120=python -u -c 'import __graft_entry__ as g; g.smoke()'"
   "bench@330=python -u bench.py"
-  "panel@60=./scripts/probes/pricing_panel 10000 50000"
   "c3s1@100=MILP_SMALL_BATCH_STREAMS=1 $B3"
 )
 bash scripts/gpu_run.sh "$out" "${exec_steps[@]}"

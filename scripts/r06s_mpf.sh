@@ -1,6 +1,6 @@
 #!/bin/bash
 # The speculative u column reused by the MPF update: parity, then config 5.
-out=${1:-gpurun_out/r07_d}
+out=${1:-gpurun_out/r06s_d}
 T="python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider"
 bash scripts/gpu_run.sh "$out" \
   "spec@300=$T tests/test_device_solve_gpu.py" \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Speculative flip FTRAN: its parity tests, the device-dual parity files,
 # then config 5 with it on (with the oracle check) and off.
-out=${1:-gpurun_out/r07_a}
+out=${1:-gpurun_out/r06s_a}
 T="python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider"
 bash scripts/gpu_run.sh "$out" \
   "spec@300=$T tests/test_device_solve_gpu.py -k 'speculative or async_tau'" \
