@@ -136,6 +136,13 @@ class DeviceLp : public DeviceSolver {
   // boxed column. flags[i] = 1 if (cols ? cols[i] : i) flips.
   void DualBoxedFlips(const std::vector<int>* cols, double threshold,
                       std::vector<uint8_t>* flags);
+  // The listed DualBoxedFlips of the next loop top, launched early (engine:
+  // right after this iteration's reduced-cost update, on the same stream, so
+  // that the loop top reads the flags instead of a launch and a wait). The
+  // next DualBoxedFlips takes them when it asks for the same columns and
+  // threshold, no reduced cost was written since and none of those columns'
+  // bits changed; otherwise it decides as usual. MILP_EARLY_FLIPS=0: off.
+  void DualBoxedFlipsEarly(const std::vector<int>& cols, double threshold);
 
   // --- dense triangular solves of the LU (device_solve.hip) -------------
   struct TriBuffer {  // a device buffer of the triangular-solve state
@@ -573,6 +580,19 @@ class DeviceLp : public DeviceSolver {
   uint8_t* m_flip_flags_ = nullptr;
   int32_t* h_flip_cols_ = nullptr;
   uint8_t* h_flip_flags_ = nullptr;
+  // DualBoxedFlipsEarly's launch (its columns and flags in h_flip_*).
+  struct EarlyFlips {
+    bool pending = false;
+    int n = 0;
+    double threshold = 0.0;
+    uint64_t rc_epoch = 0;
+    std::vector<int32_t> cols_changed;  // column bits written since the launch
+  };
+  EarlyFlips early_flips_;
+  bool early_flips_on_ = true;
+  uint64_t rc_epoch_ = 0;  // counts the writes of d_rc_
+  void* ev_flips_ = nullptr;
+  void WaitEarlyFlips();
   int last_candidates_ = 0;
   int dual_list_count_ = 0;  // update-row length seen by the last ratio test
   // Above this many breakpoints under the first bound, the dual ratio test

@@ -3,6 +3,7 @@
 #include "fibers.h"
 #include "host_pool.h"
 
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -83,6 +84,7 @@ DeviceLp::~DeviceLp() {
                   static_cast<void*>(h_flip_cols_), static_cast<void*>(h_flip_flags_)}) {
     if (p) (void)hipHostFree(p);
   }
+  if (ev_flips_ != nullptr) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev_flips_));
   for (void* e : ev_cb_) {
     if (e) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e));
   }
@@ -166,6 +168,7 @@ void DeviceLp::Init(int device) {
   if (const char* v = std::getenv("MILP_TRI_BTRAN")) tri_btran_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_PAIR")) tri_pair_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_SPEC_FLIP")) spec_flip_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MILP_EARLY_FLIPS")) early_flips_on_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_TRI_PAD")) tri_pad_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MILP_DENSE_TAIL")) dense_tail_mode_ = std::atoi(v);
   if (const char* v = std::getenv("MILP_DENSE_TAIL_MIN_ENTRIES")) {
@@ -1689,6 +1692,11 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
     MappedResize(&h_cb_bits_, &m_cb_bits_, 2 * size_t(n_total_));
     MappedResize(&h_flip_cols_, &m_flip_cols_, n_total_);
     MappedResize(&h_flip_flags_, &m_flip_flags_, n_total_);
+    if (ev_flips_ == nullptr) {
+      hipEvent_t e;
+      Check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+      ev_flips_ = e;
+    }
     for (void*& ev : ev_cb_) {
       if (ev == nullptr) {
         hipEvent_t e;
@@ -1703,6 +1711,8 @@ void DeviceLp::DualBegin(const std::vector<double>& rc, const std::vector<uint8_
       static_cast<int>(bound_diff.size()) != n_total_) {
     throw DeviceError("dual device mode: size mismatch");
   }
+  WaitEarlyFlips();
+  ++rc_epoch_;
   Upload(d_rc_, rc.data(), n_total_ * sizeof(double));
   Upload(d_colbits_, colbits.data(), n_total_);
   Upload(d_bound_diff_, bound_diff.data(), n_total_ * sizeof(double));
@@ -1715,6 +1725,9 @@ void DeviceLp::DualSetColBits(const std::vector<int32_t>& cols,
   const int n = static_cast<int>(cols.size());
   if (n == 0) return;
   if (n > n_total_) throw DeviceError("dual device mode: too many column changes");
+  if (early_flips_.pending) {
+    early_flips_.cols_changed.insert(early_flips_.cols_changed.end(), cols.begin(), cols.end());
+  }
   // Two alternating slots of mapped memory: the host fills one while the
   // kernel of the previous call may still read the other.
   const int slot = cb_slot_;
@@ -1731,6 +1744,7 @@ void DeviceLp::DualSetColBits(const std::vector<int32_t>& cols,
 
 void DeviceLp::DualTakePricedReducedCosts() {
   if (!shards_.empty()) return ShardedDualTakePricedReducedCosts();
+  ++rc_epoch_;
   Check(hipMemcpyAsync(d_rc_, d_out_n_, n_total_ * sizeof(double), hipMemcpyDeviceToDevice,
                        S(stream_)),
         "D2D");
@@ -1746,6 +1760,7 @@ void DeviceLp::DualDownloadReducedCosts(std::vector<double>* rc) {
 
 void DeviceLp::DualSetReducedCost(int col, double value) {
   if (!shards_.empty()) return ShardedDualSetReducedCost(col, value);
+  ++rc_epoch_;
   Check(milp_launch::set_double(d_rc_ + col, value, S(stream_)), "set rc");
 }
 
@@ -1886,6 +1901,7 @@ void DeviceLp::DualUpdateReducedCosts(double mult, int leaving_col, double leavi
     return ShardedDualUpdateReducedCosts(mult, leaving_col, leaving_value, entering_col);
   }
   CallTimer timer(&stats_, MI_K_RC_UPDATE);
+  ++rc_epoch_;
   BeginKernel(MI_K_RC_UPDATE);
   Check(milp_launch::update_reduced_costs(d_list_, d_out_list_, d_count_, n_total_, mult,
                                           leaving_col, leaving_value, entering_col, d_rc_,
@@ -1901,6 +1917,20 @@ void DeviceLp::DualBoxedFlips(const std::vector<int>* cols, double threshold,
   CallTimer timer(&stats_, MI_K_DUAL_RATIO);
   const int n = cols != nullptr ? static_cast<int>(cols->size()) : n_total_;
   flags->assign(n, 0);
+  if (early_flips_.pending) {
+    const EarlyFlips& e = early_flips_;
+    bool same = cols != nullptr && n == e.n && threshold == e.threshold &&
+                rc_epoch_ == e.rc_epoch &&
+                std::memcmp(cols->data(), h_flip_cols_, size_t(n) * sizeof(int32_t)) == 0;
+    for (size_t i = 0; same && i < e.cols_changed.size(); ++i) {
+      same = std::find(cols->begin(), cols->end(), e.cols_changed[i]) == cols->end();
+    }
+    WaitEarlyFlips();  // its buffers are reused below either way
+    if (same) {
+      std::memcpy(flags->data(), h_flip_flags_, n);
+      return;
+    }
+  }
   if (n == 0) return;
   if (cols != nullptr) {
     // A list (the candidates of one ratio test): columns in and flags out
@@ -1919,6 +1949,29 @@ void DeviceLp::DualBoxedFlips(const std::vector<int>* cols, double threshold,
         "boxed flips");
   Download(h_flip_flags_, d_slot_flags_, n);
   std::memcpy(flags->data(), h_flip_flags_, n);
+}
+
+void DeviceLp::DualBoxedFlipsEarly(const std::vector<int>& cols, double threshold) {
+  if (!early_flips_on_ || !shards_.empty() || !dual_ready_) return;
+  const int n = static_cast<int>(cols.size());
+  if (n == 0 || n > n_total_) return;
+  WaitEarlyFlips();
+  std::memcpy(h_flip_cols_, cols.data(), size_t(n) * sizeof(int32_t));
+  Check(milp_launch::boxed_flips(m_flip_cols_, n, d_rc_, d_colbits_, threshold, m_flip_flags_,
+                                 S(stream_)),
+        "boxed flips (early)");
+  Check(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_flips_), S(stream_)), "flips event");
+  early_flips_.pending = true;
+  early_flips_.n = n;
+  early_flips_.threshold = threshold;
+  early_flips_.rc_epoch = rc_epoch_;
+  early_flips_.cols_changed.clear();
+}
+
+void DeviceLp::WaitEarlyFlips() {
+  if (!early_flips_.pending) return;
+  early_flips_.pending = false;
+  Check(hipEventSynchronize(reinterpret_cast<hipEvent_t>(ev_flips_)), "flips event");
 }
 
 }  // namespace milp

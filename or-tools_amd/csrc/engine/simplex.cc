@@ -5475,6 +5475,12 @@ Status RevisedSimplex::DualMinimize(bool feasibility_phase, TimeLimit* time_limi
     reduced_costs_.ShiftCostIfNeeded(increasing_rc_is_needed, entering_col);
     reduced_costs_.UpdateBeforeBasisPivot(entering_col, leaving_row, direction_,
                                           &update_row_);
+    if (dual_device_mode_ && !bound_flip_candidates_.empty()) {
+      // The next loop top's MakeBoxedVariableDualFeasible decisions, from the
+      // reduced costs just updated (taken there if nothing changed them).
+      device_.DualBoxedFlipsEarly(bound_flip_candidates_,
+                                  reduced_costs_.GetDualFeasibilityTolerance());
+    }
     clock.Mark(6);
     dual_edge_norms_.UpdateBeforeBasisPivot(entering_col, leaving_row, direction_,
                                             update_row_.GetUnitRowLeftInverse());

@@ -122,6 +122,22 @@ def _spec_flip_stats():
     return list(out)
 
 
+@pytest.mark.parametrize("seed", [78, 81])
+@pytest.mark.parametrize("early", ["0", "1"])
+def test_early_boxed_flips_parity(seed, early, monkeypatch):
+    """The next loop top's boxed-flip decisions launched right after the
+    reduced-cost update (DeviceLp::DualBoxedFlipsEarly) and taken only when
+    nothing changed the reduced costs or those columns' bits since: the
+    oracle's results either way."""
+    monkeypatch.setenv("MILP_DEVICE_SOLVE", "force")
+    monkeypatch.setenv("MILP_DEVICE_DUAL", "force")
+    monkeypatch.setenv("MILP_EARLY_FLIPS", early)
+    lp = lp_gen.sparse_c5_lp(500, 5000, 6, seed)
+    p = abi.default_params(use_dual_simplex=1, max_number_of_iterations=1500)
+    o, ro, g, rg = parity_util.solve_both(lp, p, _handle)
+    parity_util.compare(o, ro, g, rg, lp)
+
+
 @pytest.mark.parametrize("seed", [78, 79, 80])
 @pytest.mark.parametrize("spec", ["0", "1"])
 def test_speculative_flip_ftran_parity(seed, spec, monkeypatch):
